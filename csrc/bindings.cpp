@@ -1,0 +1,250 @@
+// pybind11 module `igloo_amd._native`: SQL parser + gfx950 kernel launchers +
+// device runtime. Pointer arguments are passed as integers (torch
+// tensor.data_ptr()); shape/dtype validation happens in igloo_amd/ops before
+// any launch, so this layer is a thin, allocation-free trampoline.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <vector>
+
+#include "kernels/kernels.h"
+#include "runtime/runtime.h"
+#include "sql/ast.h"
+#include "sql/ast_py.h"
+
+namespace py = pybind11;
+using namespace igloo;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::list parse(const std::string& text) {
+  py::list out;
+  try {
+    for (auto& st : sql::parse_sql(text)) out.append(sql::to_python(st));
+  } catch (const sql::ParseError& e) {
+    PyErr_SetString(PyExc_SyntaxError, e.what());
+    throw py::error_already_set();
+  }
+  return out;
+}
+
+py::list tokenize(const std::string& text) {
+  py::list out;
+  static const char* names[] = {"ident", "quoted_ident", "keyword", "number", "string", "op", "end"};
+  try {
+    for (auto& t : sql::tokenize(text)) out.append(py::make_tuple(names[t.kind], t.text, t.pos));
+  } catch (const sql::ParseError& e) {
+    PyErr_SetString(PyExc_SyntaxError, e.what());
+    throw py::error_already_set();
+  }
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "igloo MI355X native core: SQL frontend, gfx950 kernels, device runtime";
+  m.attr("ARCH") = "gfx950";
+  m.attr("MAX_AGGS") = kern::kMaxAggs;
+  m.attr("MAX_GATHER_COLS") = kern::kMaxGatherCols;
+  m.attr("MAX_PARTS") = kern::kMaxParts;
+
+  // ------------------------------------------------------------------ SQL
+  m.def("parse_sql", &parse, "Parse SQL text into a list of statement ASTs (dicts)");
+  m.def("tokenize", &tokenize);
+
+  // -------------------------------------------------------------- runtime
+  m.def("device_count", &rt::device_count);
+  m.def("device_info", [](int dev) {
+    auto d = rt::device_info(dev);
+    py::dict r;
+    r["device"] = d.device;
+    r["name"] = d.name;
+    r["arch"] = d.arch;
+    r["total_mem"] = d.total_mem;
+    r["free_mem"] = d.free_mem;
+    r["cu_count"] = d.cu_count;
+    r["wave_size"] = d.wave_size;
+    r["lds_per_block"] = d.lds_per_block;
+    r["l2_bytes"] = d.l2_bytes;
+    r["clock_khz"] = d.clock_khz;
+    return r;
+  });
+  py::class_<rt::PinnedPool>(m, "PinnedPool")
+      .def(py::init<size_t>())
+      .def("acquire",
+           [](rt::PinnedPool& p, size_t bytes) {
+             size_t got = 0;
+             void* ptr = p.acquire(bytes, &got);
+             return py::make_tuple((uintptr_t)ptr, got);
+           })
+      .def("release", [](rt::PinnedPool& p, uintptr_t ptr, size_t bytes) { p.release((void*)ptr, bytes); })
+      .def_property_readonly("cached_bytes", &rt::PinnedPool::cached_bytes);
+
+  // ------------------------------------------------------- select / scan
+  m.def("select_num_tiles", &kern::select_num_tiles);
+  m.def("select_count", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t total, uintptr_t s) {
+    kern::select_count(P<const uint8_t>(mask), n, P<int64_t>(tiles), P<int64_t>(total), S(s));
+  });
+  m.def("select_write", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t out, bool idx64, uintptr_t s) {
+    kern::select_write(P<const uint8_t>(mask), n, P<const int64_t>(tiles), P<void>(out), idx64, S(s));
+  });
+  m.def("scan_workspace_tiles", &kern::scan_workspace_tiles);
+  m.def("exclusive_scan", [](uintptr_t in, bool in64, int64_t n, uintptr_t out, uintptr_t ws, uintptr_t total, uintptr_t s) {
+    kern::exclusive_scan(P<const void>(in), in64, n, P<int64_t>(out), P<int64_t>(ws), P<int64_t>(total), S(s));
+  });
+
+  // ------------------------------------------------------------ hash tables
+  m.def("join_build", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t tkeys, uintptr_t thead,
+                         uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t dups, uintptr_t s) {
+    kern::join_build(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<int64_t>(tkeys), P<int32_t>(thead),
+                     P<int32_t>(next), cap, kmin, direct, P<unsigned long long>(dups), S(s));
+  });
+  m.def("join_probe", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
+                         uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t counts, uintptr_t first,
+                         uintptr_t matched, uintptr_t s) {
+    kern::join_probe(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
+                     P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<int32_t>(counts),
+                     P<int32_t>(first), P<uint8_t>(matched), S(s));
+  });
+  m.def("join_expand", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
+                          uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t offsets, uintptr_t out_probe,
+                          uintptr_t out_build, uintptr_t s) {
+    kern::join_expand(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
+                      P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<const int64_t>(offsets),
+                      P<int32_t>(out_probe), P<int32_t>(out_build), S(s));
+  });
+  m.def("groupby_build", [](uintptr_t keys, bool key64, int64_t n, uintptr_t tkeys, uintptr_t trow, int64_t cap,
+                            int64_t kmin, bool direct, uintptr_t s) {
+    kern::groupby_build(P<const void>(keys), key64, n, P<int64_t>(tkeys), P<int32_t>(trow), cap, kmin, direct, S(s));
+  });
+  m.def("groupby_occupied", [](uintptr_t trow, int64_t cap, uintptr_t occ, uintptr_t s) {
+    kern::groupby_occupied(P<const int32_t>(trow), cap, P<uint8_t>(occ), S(s));
+  });
+  m.def("groupby_assign", [](uintptr_t slots, bool slots64, int64_t g, uintptr_t trow, uintptr_t gid_of_slot,
+                             uintptr_t rep_row, uintptr_t s) {
+    kern::groupby_assign(P<const void>(slots), slots64, g, P<const int32_t>(trow), P<int32_t>(gid_of_slot),
+                         P<int32_t>(rep_row), S(s));
+  });
+  m.def("groupby_lookup", [](uintptr_t keys, bool key64, int64_t n, uintptr_t tkeys, uintptr_t gid_of_slot,
+                             int64_t cap, int64_t kmin, bool direct, uintptr_t gid, uintptr_t s) {
+    kern::groupby_lookup(P<const void>(keys), key64, n, P<const int64_t>(tkeys), P<const int32_t>(gid_of_slot), cap,
+                         kmin, direct, P<int32_t>(gid), S(s));
+  });
+
+  // ------------------------------------------------------------ aggregation
+  m.def("agg_lds_max_groups", &kern::agg_lds_max_groups);
+  // descs: list of (op, src64, src, valid, dst, dst2)
+  m.def("agg_update", [](uintptr_t gid, int64_t n, int ngroups, const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t>>& descs, uintptr_t s) {
+    std::vector<kern::AggDesc> d;
+    for (auto& t : descs)
+      d.push_back({std::get<0>(t), std::get<1>(t), P<const void>(std::get<2>(t)), P<const uint8_t>(std::get<3>(t)),
+                   P<void>(std::get<4>(t)), P<void>(std::get<5>(t))});
+    kern::agg_update(P<const int32_t>(gid), n, ngroups, d.data(), (int)d.size(), S(s));
+  });
+
+  // ----------------------------------------------------------------- gather
+  // descs: list of (src, dst, elem_bytes, src_valid, dst_valid)
+  m.def("gather_multi", [](uintptr_t idx, bool idx64, int64_t n, const std::vector<std::tuple<uintptr_t, uintptr_t, int, uintptr_t, uintptr_t>>& descs, uintptr_t s) {
+    std::vector<kern::GatherDesc> d;
+    for (auto& t : descs)
+      d.push_back({P<const void>(std::get<0>(t)), P<void>(std::get<1>(t)), std::get<2>(t),
+                   P<const uint8_t>(std::get<3>(t)), P<uint8_t>(std::get<4>(t))});
+    kern::gather_multi(P<const void>(idx), idx64, n, d.data(), (int)d.size(), S(s));
+  });
+  m.def("str_gather_lengths", [](uintptr_t off, uintptr_t idx, bool idx64, int64_t n, uintptr_t len, uintptr_t s) {
+    kern::str_gather_lengths(P<const int64_t>(off), P<const void>(idx), idx64, n, P<int64_t>(len), S(s));
+  });
+  m.def("str_gather_copy", [](uintptr_t off, uintptr_t chars, uintptr_t idx, bool idx64, int64_t n, uintptr_t new_off,
+                              uintptr_t out, uintptr_t s) {
+    kern::str_gather_copy(P<const int64_t>(off), P<const uint8_t>(chars), P<const void>(idx), idx64, n,
+                          P<const int64_t>(new_off), P<uint8_t>(out), S(s));
+  });
+
+  // ---------------------------------------------------------------- strings
+  m.def("str_like", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t pat, uintptr_t kind, int mlen, bool ci,
+                       bool neg, uintptr_t out, uintptr_t s) {
+    kern::str_like(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(pat), P<const uint8_t>(kind),
+                   mlen, ci, neg, P<uint8_t>(out), S(s));
+  });
+  m.def("str_case", [](uintptr_t in, int64_t nbytes, bool up, uintptr_t out, uintptr_t flag, uintptr_t s) {
+    kern::str_case(P<const uint8_t>(in), nbytes, up, P<uint8_t>(out), P<int>(flag), S(s));
+  });
+  m.def("str_substr_lengths", [](uintptr_t off, uintptr_t chars, int64_t n, int64_t start, int64_t len, bool has_len,
+                                 uintptr_t out, uintptr_t s) {
+    kern::str_substr_lengths(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len, P<int64_t>(out), S(s));
+  });
+  m.def("str_substr_copy", [](uintptr_t off, uintptr_t chars, int64_t n, int64_t start, int64_t len, bool has_len,
+                              uintptr_t new_off, uintptr_t out, uintptr_t s) {
+    kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
+                          P<const int64_t>(new_off), P<uint8_t>(out), S(s));
+  });
+  m.def("str_hash64", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t valid, uintptr_t out, uintptr_t s) {
+    kern::str_hash64(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(valid), P<int64_t>(out), S(s));
+  });
+  m.def("str_eq_rows", [](uintptr_t aoff, uintptr_t achars, uintptr_t ai, uintptr_t boff, uintptr_t bchars, uintptr_t bi,
+                          bool idx64, int64_t n, uintptr_t mism, uintptr_t s) {
+    kern::str_eq_rows(P<const int64_t>(aoff), P<const uint8_t>(achars), P<const void>(ai), P<const int64_t>(boff),
+                      P<const uint8_t>(bchars), P<const void>(bi), idx64, n, P<int>(mism), S(s));
+  });
+  m.def("str_cmp_const", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t c, int64_t cn, int op, uintptr_t out,
+                            uintptr_t s) {
+    kern::str_cmp_const(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(c), cn, op,
+                        P<uint8_t>(out), S(s));
+  });
+  m.def("str_prefix_key", [](uintptr_t off, uintptr_t chars, int64_t n, int64_t skip, uintptr_t out, uintptr_t s) {
+    kern::str_prefix_key(P<const int64_t>(off), P<const uint8_t>(chars), n, skip, P<int64_t>(out), S(s));
+  });
+
+  // -------------------------------------------------------------- partition
+  m.def("partition_run_blocks", &kern::partition_run_blocks);
+  m.def("partition_run", [](uintptr_t keys, bool key64, int64_t n, int nparts, uintptr_t ws, uintptr_t total,
+                            uintptr_t perm, bool perm64, uintptr_t s) {
+    kern::partition_run(P<const void>(keys), key64, n, nparts, P<int64_t>(ws), P<int64_t>(total), P<void>(perm),
+                        perm64, S(s));
+  });
+  m.def("partition_ids", [](uintptr_t keys, bool key64, int64_t n, int nparts, uintptr_t out, uintptr_t s) {
+    kern::partition_ids(P<const void>(keys), key64, n, nparts, P<int32_t>(out), S(s));
+  });
+  m.def("date_part", [](uintptr_t days, int64_t n, int field, uintptr_t out, uintptr_t s) {
+    kern::date_part(P<const int32_t>(days), n, field, P<int32_t>(out), S(s));
+  });
+
+  // ---------------------------------------------------------------- datagen
+  // params: (kind, seed, row_base, min_len, max_len, vocab, vocab_off, vocab_n,
+  //          inject, inject_len, inject_every, suffix_char, aux, row_ids)
+  auto mkparams = [](const py::tuple& t) {
+    kern::TextGenParams p;
+    p.kind = t[0].cast<int>();
+    p.seed = t[1].cast<uint64_t>();
+    p.row_base = t[2].cast<int64_t>();
+    p.min_len = t[3].cast<int>();
+    p.max_len = t[4].cast<int>();
+    p.vocab = P<const uint8_t>(t[5].cast<uintptr_t>());
+    p.vocab_off = P<const int32_t>(t[6].cast<uintptr_t>());
+    p.vocab_n = t[7].cast<int>();
+    p.inject = P<const uint8_t>(t[8].cast<uintptr_t>());
+    p.inject_len = t[9].cast<int>();
+    p.inject_every = t[10].cast<int>();
+    p.suffix_char = t[11].cast<int>();
+    p.aux = P<const int32_t>(t[12].cast<uintptr_t>());
+    p.row_ids = t.size() > 13 ? P<const int64_t>(t[13].cast<uintptr_t>()) : nullptr;
+    return p;
+  };
+  m.def("textgen_lengths", [mkparams](const py::tuple& t, int64_t n, uintptr_t lens, bool device, uintptr_t s) {
+    auto p = mkparams(t);
+    py::gil_scoped_release rel;
+    kern::textgen_lengths(p, n, P<int64_t>(lens), device, S(s));
+  });
+  m.def("textgen_write", [mkparams](const py::tuple& t, int64_t n, uintptr_t off, uintptr_t chars, bool device, uintptr_t s) {
+    auto p = mkparams(t);
+    py::gil_scoped_release rel;
+    kern::textgen_write(p, n, P<const int64_t>(off), P<uint8_t>(chars), device, S(s));
+  });
+}

@@ -1,0 +1,294 @@
+// GPU hash tables for equi-joins and GROUP BY.
+//
+// Replaces the reference's HashJoinExec build/probe, which keys a
+// HashMap<Vec<u8>, Vec<RecordBatch>> on Debug-formatted key bytes and probes
+// row by row (reference crates/engine/src/operators/hash_join.rs:101-128,
+// :141-203), and DataFusion's AggregateExec group table.
+//
+// Layout (struct-of-arrays, one HBM line per probe in the common case):
+//   hashed mode: tkeys[cap] int64 (kEmptyKey = empty) + thead[cap] int32,
+//                open addressing with linear probing, cap = pow2 >= 2n;
+//   direct mode: when the key domain [kmin, kmin+cap) is dense enough the
+//                key itself is the slot (a perfect hash): no key array, no
+//                probing, one random read per probe row. TPC-H keys are
+//                dense integers, so most joins take this path.
+// Duplicate build keys are chained through next[row] (atomicExch on the
+// slot head), so the same table serves unique (PK) and multi-match joins.
+#include "common.h"
+#include "kernels.h"
+
+namespace igloo {
+namespace kern {
+
+namespace {
+
+constexpr int kMaxGrid = 256 * 8 * 16;  // 32768 blocks: every CU gets many waves of random loads
+
+template <typename K>
+__device__ inline bool load_key(const K* keys, const uint8_t* valid, int64_t i, int64_t* out) {
+  if (valid && !valid[i]) return false;
+  *out = (int64_t)keys[i];
+  return true;
+}
+
+// Find the slot holding `k` (hashed mode); -1 when absent.
+__device__ inline int64_t find_slot(const int64_t* __restrict__ tkeys, int64_t mask, int64_t k) {
+  int64_t slot = (int64_t)(mix64((uint64_t)k) & (uint64_t)mask);
+  for (;;) {
+    int64_t tk = tkeys[slot];
+    if (tk == k) return slot;
+    if (tk == kEmptyKey) return -1;
+    slot = (slot + 1) & mask;
+  }
+}
+
+// Insert-or-find `k` (hashed mode); returns the slot and whether the key
+// already existed.
+__device__ inline int64_t insert_slot(int64_t* __restrict__ tkeys, int64_t mask, int64_t k, bool* existed) {
+  int64_t slot = (int64_t)(mix64((uint64_t)k) & (uint64_t)mask);
+  for (;;) {
+    unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[slot], (unsigned long long)kEmptyKey,
+                                        (unsigned long long)k);
+    if ((int64_t)prev == kEmptyKey) { *existed = false; return slot; }
+    if ((int64_t)prev == k) { *existed = true; return slot; }
+    slot = (slot + 1) & mask;
+  }
+}
+
+template <typename K, bool DIRECT>
+__global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
+                                                           int64_t n, int64_t* __restrict__ tkeys,
+                                                           int32_t* __restrict__ thead, int32_t* __restrict__ next,
+                                                           int64_t cap, int64_t kmin, unsigned long long* dups) {
+  const int64_t mask = cap - 1;
+  unsigned long long local_dups = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k;
+    if (!load_key(keys, valid, i, &k)) { next[i] = -1; continue; }
+    int64_t slot;
+    if (DIRECT) {
+      slot = k - kmin;
+    } else {
+      bool existed;
+      slot = insert_slot(tkeys, mask, k, &existed);
+    }
+    int32_t old = atomicExch(&thead[slot], (int32_t)i);
+    next[i] = old;
+    local_dups += old != -1;
+  }
+  // one atomic per wave for the duplicate counter
+  for (int off = kWave / 2; off > 0; off >>= 1) local_dups += __shfl_xor(local_dups, off, kWave);
+  if (lane_id() == 0 && local_dups) atomicAdd(dups, local_dups);
+}
+
+template <typename K, bool DIRECT>
+__device__ inline int32_t probe_head(const K* keys, const uint8_t* valid, int64_t j, const int64_t* tkeys,
+                                     const int32_t* thead, int64_t cap, int64_t kmin) {
+  int64_t k;
+  if (!load_key(keys, valid, j, &k)) return -1;
+  if (DIRECT) {
+    int64_t s = k - kmin;
+    if (s < 0 || s >= cap) return -1;
+    return thead[s];
+  }
+  int64_t s = find_slot(tkeys, cap - 1, k);
+  return s < 0 ? -1 : thead[s];
+}
+
+// counts[j] = number of build matches of probe row j; first[j] = one match or -1.
+template <typename K, bool DIRECT>
+__global__ __launch_bounds__(kBlock) void join_probe_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
+                                                           int64_t m, const int64_t* __restrict__ tkeys,
+                                                           const int32_t* __restrict__ thead,
+                                                           const int32_t* __restrict__ next, int64_t cap, int64_t kmin,
+                                                           int32_t* __restrict__ counts, int32_t* __restrict__ first,
+                                                           uint8_t* __restrict__ build_matched) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin);
+    if (first) first[j] = h;
+    if (counts) {
+      int32_t c = 0;
+      for (int32_t r = h; r != -1; r = next[r]) {
+        ++c;
+        if (build_matched) build_matched[r] = 1;
+      }
+      counts[j] = c;
+    } else if (build_matched) {
+      for (int32_t r = h; r != -1; r = next[r]) build_matched[r] = 1;
+    }
+  }
+}
+
+template <typename K, bool DIRECT>
+__global__ __launch_bounds__(kBlock) void join_expand_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
+                                                            int64_t m, const int64_t* __restrict__ tkeys,
+                                                            const int32_t* __restrict__ thead,
+                                                            const int32_t* __restrict__ next, int64_t cap, int64_t kmin,
+                                                            const int64_t* __restrict__ offsets,
+                                                            int32_t* __restrict__ out_probe,
+                                                            int32_t* __restrict__ out_build) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin);
+    int64_t o = offsets[j];
+    for (int32_t r = h; r != -1; r = next[r]) {
+      out_probe[o] = (int32_t)j;
+      out_build[o] = r;
+      ++o;
+    }
+  }
+}
+
+template <typename K, bool DIRECT>
+__global__ __launch_bounds__(kBlock) void groupby_build_kernel(const K* __restrict__ keys, int64_t n,
+                                                              int64_t* __restrict__ tkeys, int32_t* __restrict__ trow,
+                                                              int64_t cap, int64_t kmin) {
+  const int64_t mask = cap - 1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k = (int64_t)keys[i];
+    int64_t slot;
+    if (DIRECT) {
+      slot = k - kmin;
+    } else {
+      bool existed;
+      slot = insert_slot(tkeys, mask, k, &existed);
+    }
+    // first occurrence row: plain read first avoids most atomics on hot groups
+    if (trow[slot] > (int32_t)i) atomicMin(&trow[slot], (int32_t)i);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void occupied_kernel(const int32_t* __restrict__ trow, int64_t cap,
+                                                         uint8_t* __restrict__ occ) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
+    occ[i] = trow[i] != INT32_MAX;
+}
+
+// gid_of_slot[slots[g]] = g ; rep_row[g] = trow[slots[g]]
+template <typename S>
+__global__ __launch_bounds__(kBlock) void assign_gid_kernel(const S* __restrict__ slots, int64_t g,
+                                                           const int32_t* __restrict__ trow,
+                                                           int32_t* __restrict__ gid_of_slot,
+                                                           int32_t* __restrict__ rep_row) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < g; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s = (int64_t)slots[i];
+    gid_of_slot[s] = (int32_t)i;
+    rep_row[i] = trow[s];
+  }
+}
+
+template <typename K, bool DIRECT>
+__global__ __launch_bounds__(kBlock) void groupby_lookup_kernel(const K* __restrict__ keys, int64_t n,
+                                                               const int64_t* __restrict__ tkeys,
+                                                               const int32_t* __restrict__ gid_of_slot, int64_t cap,
+                                                               int64_t kmin, int32_t* __restrict__ gid) {
+  const int64_t mask = cap - 1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k = (int64_t)keys[i];
+    int64_t slot = DIRECT ? k - kmin : find_slot(tkeys, mask, k);
+    gid[i] = gid_of_slot[slot];
+  }
+}
+
+#define DISPATCH_KEY(key64, direct, KERNEL, ...)                                      \
+  do {                                                                                \
+    if (key64) {                                                                      \
+      if (direct) hipLaunchKernelGGL((KERNEL<int64_t, true>), __VA_ARGS__);           \
+      else hipLaunchKernelGGL((KERNEL<int64_t, false>), __VA_ARGS__);                 \
+    } else {                                                                          \
+      if (direct) hipLaunchKernelGGL((KERNEL<int32_t, true>), __VA_ARGS__);           \
+      else hipLaunchKernelGGL((KERNEL<int32_t, false>), __VA_ARGS__);                 \
+    }                                                                                 \
+  } while (0)
+
+}  // namespace
+
+void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
+                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, hipStream_t stream) {
+  if (n == 0) return;
+  dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
+  if (key64) {
+    if (direct) hipLaunchKernelGGL((join_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
+    else hipLaunchKernelGGL((join_build_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
+  } else {
+    if (direct) hipLaunchKernelGGL((join_build_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
+    else hipLaunchKernelGGL((join_build_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
+  }
+  check_launch("join_build", stream);
+}
+
+void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
+                int32_t* first, uint8_t* build_matched, hipStream_t stream) {
+  if (m == 0) return;
+  dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
+  if (key64) {
+    if (direct) hipLaunchKernelGGL((join_probe_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
+    else hipLaunchKernelGGL((join_probe_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
+  } else {
+    if (direct) hipLaunchKernelGGL((join_probe_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
+    else hipLaunchKernelGGL((join_probe_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
+  }
+  check_launch("join_probe", stream);
+}
+
+void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
+                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, hipStream_t stream) {
+  if (m == 0) return;
+  dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
+  if (key64) {
+    if (direct) hipLaunchKernelGGL((join_expand_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
+    else hipLaunchKernelGGL((join_expand_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
+  } else {
+    if (direct) hipLaunchKernelGGL((join_expand_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
+    else hipLaunchKernelGGL((join_expand_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
+  }
+  check_launch("join_expand", stream);
+}
+
+void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,
+                   bool direct, hipStream_t stream) {
+  if (n == 0) return;
+  dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
+  if (key64) {
+    if (direct) hipLaunchKernelGGL((groupby_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, trow, cap, kmin);
+    else hipLaunchKernelGGL((groupby_build_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, trow, cap, kmin);
+  } else {
+    if (direct) hipLaunchKernelGGL((groupby_build_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, n, tkeys, trow, cap, kmin);
+    else hipLaunchKernelGGL((groupby_build_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, n, tkeys, trow, cap, kmin);
+  }
+  check_launch("groupby_build", stream);
+}
+
+void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, hipStream_t stream) {
+  hipLaunchKernelGGL(occupied_kernel, dim3(grid_for(cap, kBlock, kMaxGrid)), dim3(kBlock), 0, stream, trow, cap, occ);
+  check_launch("groupby_occupied", stream);
+}
+
+void groupby_assign(const void* slots, bool slots64, int64_t g, const int32_t* trow, int32_t* gid_of_slot,
+                    int32_t* rep_row, hipStream_t stream) {
+  if (g == 0) return;
+  dim3 gr(grid_for(g, kBlock, kMaxGrid)), b(kBlock);
+  if (slots64)
+    hipLaunchKernelGGL(assign_gid_kernel<int64_t>, gr, b, 0, stream, (const int64_t*)slots, g, trow, gid_of_slot, rep_row);
+  else
+    hipLaunchKernelGGL(assign_gid_kernel<int32_t>, gr, b, 0, stream, (const int32_t*)slots, g, trow, gid_of_slot, rep_row);
+  check_launch("groupby_assign", stream);
+}
+
+void groupby_lookup(const void* keys, bool key64, int64_t n, const int64_t* tkeys, const int32_t* gid_of_slot,
+                    int64_t cap, int64_t kmin, bool direct, int32_t* gid, hipStream_t stream) {
+  if (n == 0) return;
+  dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
+  if (key64) {
+    if (direct) hipLaunchKernelGGL((groupby_lookup_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, gid_of_slot, cap, kmin, gid);
+    else hipLaunchKernelGGL((groupby_lookup_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, gid_of_slot, cap, kmin, gid);
+  } else {
+    if (direct) hipLaunchKernelGGL((groupby_lookup_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, n, tkeys, gid_of_slot, cap, kmin, gid);
+    else hipLaunchKernelGGL((groupby_lookup_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, n, tkeys, gid_of_slot, cap, kmin, gid);
+  }
+  check_launch("groupby_lookup", stream);
+}
+
+}  // namespace kern
+}  // namespace igloo

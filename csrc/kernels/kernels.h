@@ -1,0 +1,135 @@
+// Host-side API of the igloo gfx950 kernel library. Every entry point takes
+// raw device pointers plus the HIP stream to launch on (the caller's current
+// torch stream), never allocates, and never synchronises — so a caller may
+// capture sequences of them into a hipGraph (cdna_hip_programming.md G9).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace igloo {
+namespace kern {
+
+constexpr int kMaxAggs = 8;
+constexpr int kMaxGatherCols = 16;
+constexpr int kMaxParts = 64;
+
+// ---- select.hip / scan.hip ---------------------------------------------------
+int64_t select_num_tiles(int64_t n);
+void select_count(const uint8_t* mask, int64_t n, int64_t* tile_counts, int64_t* total, hipStream_t stream);
+void select_write(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, void* out, bool idx64,
+                  hipStream_t stream);
+void scan_counts(int64_t* counts, int64_t n, int64_t* total, hipStream_t stream);
+int64_t scan_workspace_tiles(int64_t n);
+void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
+                    hipStream_t stream);
+
+// ---- hashtable.hip -----------------------------------------------------------
+void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
+                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, hipStream_t stream);
+void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
+                int32_t* first, uint8_t* build_matched, hipStream_t stream);
+void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
+                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, hipStream_t stream);
+void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,
+                   bool direct, hipStream_t stream);
+void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, hipStream_t stream);
+void groupby_assign(const void* slots, bool slots64, int64_t g, const int32_t* trow, int32_t* gid_of_slot,
+                    int32_t* rep_row, hipStream_t stream);
+void groupby_lookup(const void* keys, bool key64, int64_t n, const int64_t* tkeys, const int32_t* gid_of_slot,
+                    int64_t cap, int64_t kmin, bool direct, int32_t* gid, hipStream_t stream);
+
+// ---- agg.hip -------------------------------------------------------------------
+enum AggOp : int {
+  AGG_SUM_INT = 0,  // exact: dst = lo (u64), dst2 = hi (i64)
+  AGG_SUM_F64 = 1,
+  AGG_COUNT = 2,
+  AGG_MIN_INT = 3,
+  AGG_MAX_INT = 4,
+  AGG_MIN_F64 = 5,  // state is the order-preserving int64 image of the double
+  AGG_MAX_F64 = 6,
+};
+
+struct AggDesc {
+  int op;
+  int src64;             // integer sources: 1 = int64, 0 = int32
+  const void* src;       // null for COUNT(*)
+  const uint8_t* valid;  // null = all rows valid
+  void* dst;             // [ngroups] 8-byte states
+  void* dst2;            // [ngroups] high words for AGG_SUM_INT
+};
+
+int agg_lds_max_groups(int nagg);
+void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream);
+
+// ---- gather.hip ----------------------------------------------------------------
+struct GatherDesc {
+  const void* src;
+  void* dst;
+  int elem_bytes;  // 1, 2, 4, 8, 16
+  const uint8_t* src_valid;
+  uint8_t* dst_valid;  // null = do not produce validity
+};
+void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* descs, int ncols, hipStream_t stream);
+void str_gather_lengths(const int64_t* off, const void* idx, bool idx64, int64_t n, int64_t* len, hipStream_t stream);
+void str_gather_copy(const int64_t* off, const uint8_t* chars, const void* idx, bool idx64, int64_t n,
+                     const int64_t* new_off, uint8_t* out, hipStream_t stream);
+
+// ---- strings.hip ---------------------------------------------------------------
+void str_like(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* pat, const uint8_t* kind, int m,
+              bool case_insensitive, bool negate, uint8_t* out, hipStream_t stream);
+void str_case(const uint8_t* in, int64_t nbytes, bool to_upper, uint8_t* out, int* non_ascii, hipStream_t stream);
+void str_substr_lengths(const int64_t* off, const uint8_t* chars, int64_t n, int64_t start, int64_t len, bool has_len,
+                        int64_t* out_len, hipStream_t stream);
+void str_substr_copy(const int64_t* off, const uint8_t* chars, int64_t n, int64_t start, int64_t len, bool has_len,
+                     const int64_t* new_off, uint8_t* out, hipStream_t stream);
+void str_hash64(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* valid, int64_t* out,
+                hipStream_t stream);
+void str_eq_rows(const int64_t* aoff, const uint8_t* achars, const void* ai, const int64_t* boff, const uint8_t* bchars,
+                 const void* bi, bool idx64, int64_t n, int* mismatches, hipStream_t stream);
+void str_cmp_const(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* c, int64_t cn, int op,
+                   uint8_t* out, hipStream_t stream);
+void str_prefix_key(const int64_t* off, const uint8_t* chars, int64_t n, int64_t skip, int64_t* out,
+                    hipStream_t stream);
+
+// ---- partition.hip -------------------------------------------------------------
+int64_t partition_run_blocks(int64_t n);
+void partition_run(const void* keys, bool key64, int64_t n, int nparts, int64_t* counts_ws, int64_t* total,
+                   void* perm, bool perm64, hipStream_t stream);
+void partition_ids(const void* keys, bool key64, int64_t n, int nparts, int32_t* out, hipStream_t stream);
+void date_part(const int32_t* days, int64_t n, int field, int32_t* out, hipStream_t stream);
+
+// ---- datagen.hip ---------------------------------------------------------------
+enum TextKind : int {
+  TEXT_WORDS = 0,
+  TEXT_DISTINCT_WORDS = 1,
+  TEXT_ALNUM = 2,
+  TEXT_PREFIX_INT = 3,
+  TEXT_PREFIX_RANDINT = 4,
+  TEXT_PHONE = 5,
+};
+
+struct TextGenParams {
+  int kind;
+  uint64_t seed;
+  int64_t row_base;  // global row id of local row 0
+  int min_len, max_len;
+  const uint8_t* vocab;
+  const int32_t* vocab_off;
+  int vocab_n;
+  const uint8_t* inject;  // injected phrase (WORDS) or prefix (PREFIX_*)
+  int inject_len;
+  int inject_every;
+  int suffix_char;
+  const int32_t* aux;  // per-row int input (PHONE: nation key)
+  const int64_t* row_ids;  // optional per-row global ids (partitioned generation)
+};
+void textgen_lengths(const TextGenParams& p, int64_t n, int64_t* lens, bool device, hipStream_t stream);
+void textgen_write(const TextGenParams& p, int64_t n, const int64_t* off, uint8_t* chars, bool device,
+                   hipStream_t stream);
+
+}  // namespace kern
+}  // namespace igloo

@@ -1,0 +1,89 @@
+// Device-wide exclusive prefix sum (int32/int64 -> int64), used for join
+// output offsets, string offset construction and partition offsets.
+// Three-phase tile scan: tile reduce -> scan of tile sums -> tile rescan.
+// Tiles are 256 lanes x 8 items so a 600M-row input still launches ~290k
+// workgroups, and each phase streams the input once.
+#include "common.h"
+#include "kernels.h"
+
+namespace igloo {
+namespace kern {
+
+namespace {
+
+constexpr int kItems = 8;
+constexpr int kTile = kBlock * kItems;
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void tile_sum_kernel(const T* __restrict__ in, int64_t n,
+                                                         int64_t* __restrict__ sums) {
+  __shared__ int64_t red[kWavesPerBlock];
+  int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x;
+  int64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    if (i < n) s += (int64_t)in[i];
+  }
+  s = wave_reduce_sum(s);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void tile_scan_kernel(const T* __restrict__ in, int64_t n,
+                                                          const int64_t* __restrict__ tile_off,
+                                                          int64_t* __restrict__ out) {
+  __shared__ int64_t scratch[kWavesPerBlock + 1];
+  // each lane owns kItems consecutive rows
+  int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+  int64_t v[kItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    v[j] = base + j < n ? (int64_t)in[base + j] : 0;
+    s += v[j];
+  }
+  int64_t total;
+  int64_t run = tile_off[blockIdx.x] + block_exclusive_scan(s, scratch, &total);
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += v[j];
+  }
+}
+
+template <typename T>
+void exclusive_scan_impl(const T* in, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
+                         hipStream_t stream) {
+  int64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles == 0) {
+    IGLOO_HIP_CHECK(hipMemsetAsync(total, 0, sizeof(int64_t), stream));
+    return;
+  }
+  hipLaunchKernelGGL(tile_sum_kernel<T>, dim3((unsigned)tiles), dim3(kBlock), 0, stream, in, n, tile_ws);
+  check_launch("scan.tile_sum", stream);
+  scan_counts(tile_ws, tiles, total, stream);
+  hipLaunchKernelGGL(tile_scan_kernel<T>, dim3((unsigned)tiles), dim3(kBlock), 0, stream, in, n, tile_ws, out);
+  check_launch("scan.tile_scan", stream);
+}
+
+}  // namespace
+
+int64_t scan_workspace_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
+
+void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
+                    hipStream_t stream) {
+  if (in64)
+    exclusive_scan_impl((const int64_t*)in, n, out, tile_ws, total, stream);
+  else
+    exclusive_scan_impl((const int32_t*)in, n, out, tile_ws, total, stream);
+}
+
+}  // namespace kern
+}  // namespace igloo

@@ -1,0 +1,293 @@
+"""QueryEngine: the user-facing SQL entry point.
+
+Parity: reference crates/engine/src/lib.rs:27-62 — ``QueryEngine::new`` (registers
+the ``capitalize`` UDF), ``register_table``, ``execute(sql) -> Vec<RecordBatch>``
+(panics on error, :55-56), ``session_context``. Here ``execute`` runs the native
+parser -> binder -> optimizer -> GPU operators and returns ``pyarrow.RecordBatch``es;
+errors raise typed ``IglooError``s instead of panicking.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Any, Callable, Dict, List, Optional, Sequence, Union
+
+import pyarrow as pa
+import torch
+
+from . import types as T
+from .catalog import Catalog, Field, MemoryTable, TableSource
+from .columnar import Batch, Column
+from .exec.operators import ExecContext
+from .exec.planner import create_physical_plan
+from .sql import parse
+from .sql.binder import Binder, IdGen
+from .sql.logical import ColInfo, Plan
+from .sql.optimizer import optimize
+from .utils.errors import IglooError, NotSupported, PlanError
+from .utils.log import get_logger
+
+log = get_logger("engine")
+
+
+def default_device() -> str:
+    try:
+        if torch.cuda.is_available():
+            return "cuda"
+    except Exception:  # pragma: no cover
+        pass
+    return "cpu"
+
+
+class QueryResult:
+    """Materialised query output (host Arrow) + execution metrics."""
+
+    def __init__(self, table: pa.Table, elapsed_ms: float, plan_text: str = ""):
+        self.table = table
+        self.elapsed_ms = elapsed_ms
+        self.plan_text = plan_text
+
+    @property
+    def num_rows(self) -> int:
+        return self.table.num_rows
+
+    def to_arrow(self) -> pa.Table:
+        return self.table
+
+    def to_pandas(self):
+        return self.table.to_pandas()
+
+    def to_pylist(self):
+        return self.table.to_pylist()
+
+    def batches(self) -> List[pa.RecordBatch]:
+        return self.table.to_batches() or [pa.RecordBatch.from_pylist([], schema=self.table.schema)]
+
+    def __repr__(self):
+        return pretty_format(self.table)
+
+
+class QueryEngine:
+    def __init__(self, device: Optional[str] = None, catalog: Optional[Catalog] = None, comm=None,
+                 config: Optional[dict] = None):
+        self.device = torch.device(device or default_device())
+        self.catalog = catalog or Catalog()
+        self.comm = comm
+        self.session: Dict[str, Any] = dict(config or {})
+        self._ids = IdGen()
+        self._lock = threading.RLock()
+        self.last_metrics: Dict[str, Any] = {}
+        if self.device.type == "cuda":
+            from .ops._lib import native
+            native()  # fail loudly on a GPU box without the native extension
+
+    # -------------------------------------------------------------- catalog
+    def register_table(self, name: str, table: Union[TableSource, pa.Table, Batch, Dict[str, Column]], **kw):
+        if isinstance(table, pa.Table):
+            table = MemoryTable.from_arrow(table, device=self.device, **kw)
+        elif isinstance(table, pa.RecordBatch):
+            table = MemoryTable.from_arrow(pa.Table.from_batches([table]), device=self.device, **kw)
+        elif isinstance(table, Batch):
+            table = MemoryTable(table.columns, table.num_rows, **kw)
+        elif isinstance(table, dict):
+            table = MemoryTable(table, **kw)
+        self.catalog.register_table(name, table)
+        return table
+
+    def deregister_table(self, name: str):
+        return self.catalog.deregister_table(name)
+
+    def register_parquet(self, name: str, path: str, **kw):
+        from .connectors.parquet import ParquetTable
+        return self.register_table(name, ParquetTable(path, **kw))
+
+    def register_csv(self, name: str, path: str, schema=None, has_header: bool = True, delimiter: str = ",", **kw):
+        from .connectors.csv import CsvTable
+        return self.register_table(name, CsvTable(path, schema=schema, has_header=has_header, delimiter=delimiter, **kw))
+
+    def register_iceberg(self, name: str, path: str, **kw):
+        from .connectors.iceberg import IcebergTable
+        return self.register_table(name, IcebergTable(path, **kw))
+
+    def session_context(self) -> "QueryEngine":
+        return self
+
+    # -------------------------------------------------------------- planning
+    def logical_plan(self, sql: str, optimized: bool = True):
+        stmts = parse(sql)
+        if len(stmts) != 1:
+            raise PlanError("expected exactly one statement")
+        st = stmts[0]
+        if st["k"] == "explain":
+            st = st["c"][0]
+        if st["k"] != "query":
+            raise PlanError("not a query")
+        b = Binder(self.catalog, self._ids, self.session)
+        bq = b.bind_query(st)
+        plan = optimize(bq.plan) if optimized else bq.plan
+        return plan, bq.names
+
+    def explain(self, sql: str, analyze: bool = False) -> str:
+        r = self.sql(("EXPLAIN ANALYZE " if analyze else "EXPLAIN ") + sql)
+        return "\n".join(r.table.column("plan").to_pylist())
+
+    # -------------------------------------------------------------- execution
+    def execute(self, sql: str) -> List[pa.RecordBatch]:
+        """Run SQL; returns Arrow record batches (reference API shape)."""
+        return self.sql(sql).batches()
+
+    def query(self, sql: str) -> pa.Table:
+        return self.sql(sql).table
+
+    def sql(self, sql: str) -> QueryResult:
+        stmts = parse(sql)
+        if not stmts:
+            raise PlanError("empty SQL statement")
+        res = None
+        for st in stmts:
+            res = self._run_statement(st)
+        return res
+
+    def _run_statement(self, st: dict) -> QueryResult:
+        k = st["k"]
+        t0 = time.perf_counter()
+        if k == "query":
+            return self._run_query(st, t0)
+        if k == "explain":
+            return self._explain(st["c"][0], bool(st.get("analyze")))
+        if k == "set":
+            from .sql.binder import Binder as _B
+            v = Binder(self.catalog, self._ids).bind_expr(st["c"][0], __import__("igloo_amd.sql.binder", fromlist=["Scope"]).Scope([]))
+            self.session[st["s"]] = getattr(v, "value", None)
+            return QueryResult(pa.table({}), 0.0)
+        if k == "show":
+            if st["s"] != "tables":
+                raise NotSupported(f"SHOW {st['s']}")
+            names = self.catalog.table_names()
+            return QueryResult(pa.table({"table_name": pa.array(names, pa.string())}), 0.0)
+        if k == "drop_table":
+            if self.catalog.deregister_table(st["s"]) is None and not st.get("if_exists"):
+                raise PlanError(f"table '{st['s']}' does not exist")
+            return QueryResult(pa.table({}), 0.0)
+        if k == "create_view":
+            raise NotSupported("CREATE VIEW (use the Python API register_view)")
+        if k == "create_external_table":
+            return self._create_external(st)
+        if k == "create_table":
+            if st.get("query"):
+                b = Binder(self.catalog, self._ids, self.session)
+                bq = b.bind_query(st["query"])
+                batch = self._execute_plan(optimize(bq.plan))
+                cols = {n: batch.columns[c.cid] for n, c in zip(bq.names, bq.plan.schema)}
+                self.register_table(st["s"], MemoryTable(cols, batch.num_rows))
+                return QueryResult(pa.table({"count": [batch.num_rows]}), 0.0)
+            raise NotSupported("CREATE TABLE without AS SELECT")
+        raise NotSupported(f"statement {k}")
+
+    def _create_external(self, st) -> QueryResult:
+        name = st["s"]
+        fmt = st.get("stored_as", "PARQUET").upper()
+        loc = st.get("location")
+        if not loc:
+            raise PlanError("CREATE EXTERNAL TABLE requires LOCATION")
+        cols = st.get("columns", {}).get("c", []) if st.get("columns") else []
+        schema = [Field(c["s"], T.parse_type_name(c["type"]), not c.get("not_null")) for c in cols] or None
+        if fmt == "PARQUET":
+            self.register_parquet(name, loc)
+        elif fmt == "CSV":
+            self.register_csv(name, loc, schema=schema, has_header=bool(st.get("header")),
+                              delimiter=st.get("delimiter", ","))
+        elif fmt == "ICEBERG":
+            self.register_iceberg(name, loc)
+        else:
+            raise NotSupported(f"STORED AS {fmt}")
+        return QueryResult(pa.table({}), 0.0)
+
+    def _run_query(self, st: dict, t0: float) -> QueryResult:
+        b = Binder(self.catalog, self._ids, self.session)
+        bq = b.bind_query(st)
+        plan = optimize(bq.plan)
+        batch = self._execute_plan(plan)
+        table = self._to_arrow(batch, plan.schema, bq.names)
+        ms = (time.perf_counter() - t0) * 1e3
+        self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows}
+        return QueryResult(table, ms)
+
+    def make_context(self, analyze: bool = False) -> ExecContext:
+        return ExecContext(self, self.device, self.comm, analyze)
+
+    def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:
+        ctx = ctx or self.make_context()
+        node = create_physical_plan(plan)
+        out = node.execute(ctx)
+        if self.comm is not None and self.comm.world_size > 1:
+            from .parallel.exchange import gather_all
+            out = gather_all(out, ctx)
+        return out
+
+    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str]) -> pa.Table:
+        arrays, fields = [], []
+        for ci, nm in zip(schema, names):
+            col = batch.columns[ci.cid]
+            arr = col.to_arrow()
+            want = ci.dtype.to_arrow() if ci.dtype.kind != "null" else pa.null()
+            if arr.type != want:
+                try:
+                    arr = arr.cast(want)
+                except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                    pass
+            nullable = ci.nullable or arr.null_count > 0
+            arrays.append(arr)
+            fields.append(pa.field(nm, arr.type, nullable))
+        return pa.Table.from_arrays(arrays, schema=pa.schema(fields))
+
+    def _explain(self, st: dict, analyze: bool) -> QueryResult:
+        b = Binder(self.catalog, self._ids, self.session)
+        bq = b.bind_query(st)
+        logical = optimize(bq.plan)
+        node = create_physical_plan(logical)
+        rows_t, rows_p = ["logical_plan", "physical_plan"], [logical.explain(), node.explain()]
+        if analyze:
+            ctx = self.make_context(analyze=True)
+            t0 = time.perf_counter()
+            node.execute(ctx)
+            ms = (time.perf_counter() - t0) * 1e3
+            rows_t = ["physical_plan_with_metrics"]
+            txt = node.explain(ctx) + f"\ntotal: {ms:.3f} ms"
+            for n in _walk_exec(node):
+                if getattr(n, "order_log", None):
+                    txt += "\njoin order: " + " ; ".join(n.order_log)
+            rows_p = [txt]
+        return QueryResult(pa.table({"plan_type": rows_t, "plan": rows_p}), 0.0)
+
+
+def _walk_exec(n):
+    yield n
+    for c in n.children:
+        yield from _walk_exec(c)
+
+
+def pretty_format(table: pa.Table, max_rows: int = 50) -> str:
+    """ASCII table like arrow's print_batches (reference crates/igloo/src/main.rs:92)."""
+    names = table.column_names
+    rows = table.slice(0, max_rows).to_pylist()
+    cells = [[("" if r[n] is None else str(r[n])) for n in names] for r in rows]
+    widths = [max([len(n)] + [len(c[i]) for c in cells]) for i, n in enumerate(names)]
+    sep = "+" + "+".join("-" * (w + 2) for w in widths) + "+"
+    out = [sep, "|" + "|".join(f" {n:<{w}} " for n, w in zip(names, widths)) + "|", sep]
+    for c in cells:
+        out.append("|" + "|".join(f" {v:<{w}} " for v, w in zip(c, widths)) + "|")
+    out.append(sep)
+    if table.num_rows > max_rows:
+        out.append(f"... {table.num_rows - max_rows} more rows")
+    return "\n".join(out)
+
+
+def print_batches(batches) -> None:
+    if isinstance(batches, QueryResult):
+        t = batches.table
+    elif isinstance(batches, pa.Table):
+        t = batches
+    else:
+        t = pa.Table.from_batches(list(batches)) if batches else pa.table({})
+    print(pretty_format(t))

@@ -1,0 +1,135 @@
+"""Grouped aggregation (csrc/kernels/agg.hip).
+
+``grouped_aggregate`` updates up to 8 aggregate states per launch from one
+pass over the group ids. Integer SUMs are exact 128-bit; the result comes
+back as int64 when every group fits, else as an [g, 2] (lo, hi) tensor.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ._lib import is_gpu, launch, native, ptr, stream
+
+OPS = {"sum_int": 0, "sum_f64": 1, "count": 2, "min_int": 3, "max_int": 4, "min_f64": 5, "max_f64": 6}
+I64_MAX = 2**63 - 1
+I64_MIN = -(2**63)
+
+Spec = Tuple[str, Optional[torch.Tensor], Optional[torch.Tensor]]  # (op, values, valid)
+
+
+def _ordered_to_f64(x: torch.Tensor) -> torch.Tensor:
+    mask = (x >> 63) & 0x7FFFFFFFFFFFFFFF
+    return (x ^ mask).view(torch.float64)
+
+
+def _wide_to_result(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
+    fits = hi == (lo >> 63)
+    if bool(fits.all().item()):
+        return lo
+    return torch.stack([lo, hi], dim=1)
+
+
+def grouped_aggregate(gid: Optional[torch.Tensor], ngroups: int, specs: Sequence[Spec], n: int,
+                      device) -> List[torch.Tensor]:
+    device = torch.device(device)
+    if device.type != "cpu":
+        return _gpu(gid, ngroups, specs, n, device)
+    return _cpu(gid, ngroups, specs, n)
+
+
+def _gpu(gid, ngroups, specs, n, device) -> List[torch.Tensor]:
+    N = native()
+    g = max(ngroups, 1)
+    outs, descs, posts = [], [], []
+    for op, vals, valid in specs:
+        code = OPS[op]
+        dst2 = None
+        if op in ("sum_int", "sum_f64", "count"):
+            dst = torch.zeros(g, dtype=torch.float64 if op == "sum_f64" else torch.int64, device=device)
+            if op == "sum_int":
+                dst2 = torch.zeros(g, dtype=torch.int64, device=device)
+        elif op.startswith("min"):
+            dst = torch.full((g,), I64_MAX, dtype=torch.int64, device=device)
+        else:
+            dst = torch.full((g,), I64_MIN, dtype=torch.int64, device=device)
+        src64 = 1
+        if vals is not None:
+            assert vals.numel() == n and vals.is_contiguous()
+            if op in ("sum_int", "min_int", "max_int"):
+                assert vals.dtype in (torch.int32, torch.int64), vals.dtype
+                src64 = 1 if vals.dtype == torch.int64 else 0
+            else:
+                assert vals.dtype == torch.float64 or op == "count"
+        descs.append((code, src64, ptr(vals), ptr(valid), ptr(dst), ptr(dst2)))
+        posts.append((op, dst, dst2))
+    if n > 0:
+        s = stream(gid if gid is not None else posts[0][1])
+        for i in range(0, len(descs), 8):
+            launch("agg_update")
+            N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s)
+    for op, dst, dst2 in posts:
+        if op == "sum_int":
+            outs.append(_wide_to_result(dst, dst2))
+        elif op in ("min_f64", "max_f64"):
+            outs.append(_ordered_to_f64(dst))
+        else:
+            outs.append(dst)
+    return outs
+
+
+def _cpu(gid, ngroups, specs, n) -> List[torch.Tensor]:
+    g = max(ngroups, 1)
+    if gid is None:
+        gi = torch.zeros(n, dtype=torch.int64)
+    else:
+        gi = gid.to(torch.int64)
+    outs = []
+    for op, vals, valid in specs:
+        idx = gi
+        v = vals
+        if valid is not None:
+            sel = valid
+            idx = gi[sel]
+            v = vals[sel] if vals is not None else None
+        if op == "count":
+            outs.append(torch.bincount(idx, minlength=g)[:g].to(torch.int64) if idx.numel() else torch.zeros(g, dtype=torch.int64))
+        elif op == "sum_f64":
+            outs.append(torch.zeros(g, dtype=torch.float64).index_add_(0, idx, v.to(torch.float64)))
+        elif op == "sum_int":
+            v64 = v.to(torch.int64)
+            hi32 = v64 >> 32
+            lo32 = v64 & 0xFFFFFFFF
+            hs = torch.zeros(g, dtype=torch.int64).index_add_(0, idx, hi32)
+            ls = torch.zeros(g, dtype=torch.int64).index_add_(0, idx, lo32)
+            approx = hs.to(torch.float64) * 4294967296.0 + ls.to(torch.float64)
+            if bool((approx.abs() < 2.0**62).all().item()):
+                outs.append((hs << 32) + ls)
+            else:
+                tot = [int(h) * 4294967296 + int(l) for h, l in zip(hs.tolist(), ls.tolist())]
+                lo = torch.tensor([((t + 2**64) % 2**64) - (2**64 if ((t + 2**64) % 2**64) >= 2**63 else 0) for t in tot], dtype=torch.int64)
+                hi = torch.tensor([t >> 64 for t in tot], dtype=torch.int64)
+                outs.append(_wide_to_result(lo, hi))
+        elif op in ("min_int", "max_int"):
+            init = I64_MAX if op == "min_int" else I64_MIN
+            base = torch.full((g,), init, dtype=torch.int64)
+            outs.append(base.scatter_reduce(0, idx, v.to(torch.int64), reduce="amin" if op == "min_int" else "amax"))
+        elif op in ("min_f64", "max_f64"):
+            init = float("inf") if op == "min_f64" else float("-inf")
+            base = torch.full((g,), init, dtype=torch.float64)
+            outs.append(base.scatter_reduce(0, idx, v.to(torch.float64), reduce="amin" if op == "min_f64" else "amax"))
+        else:
+            raise ValueError(op)
+    return outs
+
+
+def wide_to_python(t: torch.Tensor) -> List[int]:
+    """[g] int64 or [g, 2] (lo, hi) -> Python ints."""
+    t = t.cpu()
+    if t.dim() == 1:
+        return [int(x) for x in t.tolist()]
+    out = []
+    for lo, hi in t.tolist():
+        out.append((hi << 64) + (lo & 0xFFFFFFFFFFFFFFFF))
+    return out

@@ -1,0 +1,107 @@
+"""Gathers by row index (csrc/kernels/gather.hip).
+
+``take_many`` gathers several columns with ONE launch for all fixed-width
+columns (plus validity), which is the late-materialisation step after a
+join/filter/sort. Negative indices produce NULL rows (outer-join padding).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+
+from ..columnar import Column
+from ._lib import is_gpu, launch, ptr, stream
+from .select import offsets_from_lengths
+
+
+def _cpu_take_tensor(t: torch.Tensor, idx: torch.Tensor, neg: bool) -> torch.Tensor:
+    if not neg:
+        return t.index_select(0, idx.long())
+    ii = idx.long()
+    safe = ii.clamp(min=0)
+    out = t.index_select(0, safe) if t.numel() else torch.zeros((ii.numel(),) + tuple(t.shape[1:]), dtype=t.dtype)
+    out[ii < 0] = 0
+    return out
+
+
+def _take_plain_strings(col: Column, idx: torch.Tensor, neg: bool) -> Column:
+    n = idx.numel()
+    if not is_gpu(idx):
+        ii = idx.long()
+        off = col.offsets
+        safe = ii.clamp(min=0)
+        starts = off.index_select(0, safe) if n else torch.zeros(0, dtype=torch.int64)
+        lens = (off.index_select(0, safe + 1) - starts) if n else torch.zeros(0, dtype=torch.int64)
+        if neg:
+            lens = torch.where(ii < 0, torch.zeros_like(lens), lens)
+        new_off, total = offsets_from_lengths(lens)
+        if total:
+            # byte positions: for each output byte, source = start[row] + (pos - new_off[row])
+            rows = torch.repeat_interleave(torch.arange(n), lens)
+            pos = torch.arange(total) - new_off[:-1].index_select(0, rows) + starts.index_select(0, rows)
+            chars = col.data.index_select(0, pos)
+        else:
+            chars = torch.zeros(0, dtype=torch.uint8)
+        return Column(col.dtype, chars, None, offsets=new_off)
+    N = launch("str_gather")
+    s = stream(idx)
+    idx64 = idx.dtype == torch.int64
+    lens = torch.empty(n, dtype=torch.int64, device=idx.device)
+    N.str_gather_lengths(ptr(col.offsets), ptr(idx), idx64, n, ptr(lens), s)
+    new_off, total = offsets_from_lengths(lens)
+    chars = torch.empty(max(total, 0), dtype=torch.uint8, device=idx.device)
+    if total:
+        N.str_gather_copy(ptr(col.offsets), ptr(col.data), ptr(idx), idx64, n, ptr(new_off), ptr(chars), s)
+    return Column(col.dtype, chars, None, offsets=new_off)
+
+
+def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> List[Column]:
+    """Gather rows ``idx`` of every column. ``neg=True``: idx may hold -1 (NULL row)."""
+    assert idx.dim() == 1 and idx.dtype in (torch.int32, torch.int64)
+    n = idx.numel()
+    gpu = is_gpu(idx)
+    out: List[Column] = []
+    descs = []      # GPU: (src, dst, elem_bytes, src_valid, dst_valid) -> one gather_multi launch
+    keepalive = []  # temporaries that must outlive the (stream-ordered) launch
+    for c in cols:
+        need_valid = neg or c.valid is not None
+        if c.is_plain_string:
+            nc = _take_plain_strings(c, idx, neg)
+            if need_valid:
+                if gpu:
+                    src = c.valid
+                    if src is None:
+                        src = torch.ones(len(c), dtype=torch.bool, device=idx.device)
+                        keepalive.append(src)
+                    v = torch.empty(n, dtype=torch.bool, device=idx.device)
+                    # validity gathered as a byte column; idx < 0 writes 0 = NULL
+                    descs.append((ptr(src), ptr(v), 1, 0, 0))
+                else:
+                    base = c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool)
+                    v = _cpu_take_tensor(base, idx, neg)
+                nc.valid = v
+            out.append(nc)
+            continue
+        if not gpu:
+            data = _cpu_take_tensor(c.data, idx, neg)
+            valid = None
+            if need_valid:
+                base = c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool)
+                valid = _cpu_take_tensor(base, idx, neg)
+            out.append(Column(c.dtype, data, valid, dictionary=c.dictionary))
+            continue
+        data = torch.empty((n,) + tuple(c.data.shape[1:]), dtype=c.data.dtype, device=idx.device)
+        esz = c.data.element_size() * (c.data.shape[1] if c.data.dim() == 2 else 1)
+        valid = torch.empty(n, dtype=torch.bool, device=idx.device) if need_valid else None
+        descs.append((ptr(c.data), ptr(data), esz, ptr(c.valid), ptr(valid)))
+        out.append(Column(c.dtype, data, valid, dictionary=c.dictionary))
+    if gpu and descs and n:
+        N = launch("gather_multi")
+        N.gather_multi(ptr(idx), idx.dtype == torch.int64, n, descs, stream(idx))
+    del keepalive
+    return out
+
+
+def take(col: Column, idx: torch.Tensor, neg: bool = False) -> Column:
+    return take_many([col], idx, neg)[0]

@@ -1,0 +1,232 @@
+"""Hash-join tables and GROUP BY encoding (csrc/kernels/hashtable.hip).
+
+``JoinTable`` builds once on the (smaller) build side and supports the probe
+shapes the join operator needs: full pair expansion (inner / outer), first
+match (unique build keys, semi/anti), and build-side "matched" flags (right /
+full outer). ``group_ids`` maps int64 group keys to dense group ids.
+
+CPU tensors use a sort + searchsorted reference implementation.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ._lib import is_gpu, launch, ptr, stream
+from .select import exclusive_scan, mask_to_indices
+
+EMPTY_KEY = -(2**63)
+INT32_MAX = 2**31 - 1
+
+
+def _next_pow2(x: int) -> int:
+    p = 1
+    while p < x:
+        p <<= 1
+    return p
+
+
+def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optional[Tuple[int, int]]:
+    if valid is not None:
+        keys = keys[valid]
+    if keys.numel() == 0:
+        return None
+    mn, mx = torch.aminmax(keys)
+    return int(mn.item()), int(mx.item())
+
+
+def _keys_ok(k: torch.Tensor) -> torch.Tensor:
+    assert k.dim() == 1 and k.dtype in (torch.int32, torch.int64), f"join keys must be int32/int64, got {k.dtype}"
+    return k.contiguous()
+
+
+class JoinTable:
+    """Hash table over build-side keys (int32/int64; NULL keys never match)."""
+
+    def __init__(self, keys: torch.Tensor, valid: Optional[torch.Tensor] = None):
+        keys = _keys_ok(keys)
+        self.n = n = keys.numel()
+        self.device = keys.device
+        self.gpu = is_gpu(keys)
+        self.valid = valid
+        rng = key_range(keys, valid)
+        self.empty = rng is None
+        if self.empty:
+            self.unique = True
+            return
+        self.kmin, kmax = rng
+        span = kmax - self.kmin + 1
+        self.direct = span <= 4 * n + 4096 and span < 2**31 - 1
+        if not self.gpu:
+            k = keys if valid is None else torch.where(valid, keys, torch.full_like(keys, kmax + 1) if kmax < 2**62 else keys)
+            sk, order = torch.sort(k.to(torch.int64), stable=True)
+            if valid is not None:
+                nv = int(valid.sum().item())
+                sk, order = sk[:nv], order[:nv]
+            self.sorted_keys, self.order = sk, order
+            self.unique = bool((sk[1:] != sk[:-1]).all().item()) if sk.numel() > 1 else True
+            return
+        N = launch("join_build")
+        self.cap = span if self.direct else _next_pow2(2 * n)
+        self.thead = torch.full((self.cap,), -1, dtype=torch.int32, device=self.device)
+        self.tkeys = (torch.empty(1, dtype=torch.int64, device=self.device) if self.direct
+                      else torch.full((self.cap,), EMPTY_KEY, dtype=torch.int64, device=self.device))
+        self.next = torch.empty(n, dtype=torch.int32, device=self.device)
+        dups = torch.zeros(1, dtype=torch.int64, device=self.device)
+        N.join_build(ptr(keys), keys.dtype == torch.int64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead),
+                     ptr(self.next), self.cap, self.kmin, self.direct, ptr(dups), stream(keys))
+        self.unique = int(dups.item()) == 0
+
+    # ----------------------------------------------------------------- probes
+    def probe_first(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
+                    build_matched: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One matching build row per probe row (-1 if none). Exact for unique builds;
+        with duplicates it returns an arbitrary match (enough for semi/anti joins)."""
+        pkeys = _keys_ok(pkeys)
+        m = pkeys.numel()
+        if self.empty or m == 0:
+            return torch.full((m,), -1, dtype=torch.int32, device=pkeys.device)
+        if not self.gpu:
+            cnt, lo = self._cpu_ranges(pkeys, pvalid)
+            first = torch.where(cnt > 0, self.order.index_select(0, lo.clamp(max=max(self.order.numel() - 1, 0))),
+                                torch.full_like(lo, -1)).to(torch.int32)
+            if build_matched is not None:
+                self._cpu_mark(cnt, lo, build_matched)
+            return first
+        first = torch.empty(m, dtype=torch.int32, device=pkeys.device)
+        N = launch("join_probe")
+        N.join_probe(ptr(pkeys), pkeys.dtype == torch.int64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead),
+                     ptr(self.next), self.cap, self.kmin, self.direct, 0, ptr(first), ptr(build_matched), stream(pkeys))
+        return first
+
+    def probe_pairs(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
+                    build_matched: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """All (probe_row, build_row) matches, grouped by probe row.
+        Returns (probe_idx int32, build_idx int32, counts int32 per probe row)."""
+        pkeys = _keys_ok(pkeys)
+        m = pkeys.numel()
+        dev = pkeys.device
+        if self.empty or m == 0:
+            z = torch.zeros(0, dtype=torch.int32, device=dev)
+            return z, z, torch.zeros(m, dtype=torch.int32, device=dev)
+        if not self.gpu:
+            cnt, lo = self._cpu_ranges(pkeys, pvalid)
+            if build_matched is not None:
+                self._cpu_mark(cnt, lo, build_matched)
+            total = int(cnt.sum().item())
+            pidx = torch.repeat_interleave(torch.arange(m), cnt)
+            starts = torch.cumsum(cnt, 0) - cnt
+            within = torch.arange(total) - starts.index_select(0, pidx)
+            bpos = lo.index_select(0, pidx) + within
+            bidx = self.order.index_select(0, bpos)
+            return pidx.to(torch.int32), bidx.to(torch.int32), cnt.to(torch.int32)
+        N = launch("join_probe")
+        s = stream(pkeys)
+        counts = torch.empty(m, dtype=torch.int32, device=dev)
+        k64 = pkeys.dtype == torch.int64
+        N.join_probe(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.next), self.cap,
+                     self.kmin, self.direct, ptr(counts), 0, ptr(build_matched), s)
+        offsets, total = exclusive_scan(counts)
+        pidx = torch.empty(total, dtype=torch.int32, device=dev)
+        bidx = torch.empty(total, dtype=torch.int32, device=dev)
+        if total:
+            launch("join_expand")
+            N.join_expand(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.next), self.cap,
+                          self.kmin, self.direct, ptr(offsets), ptr(pidx), ptr(bidx), s)
+        return pidx, bidx, counts
+
+    # ------------------------------------------------------------ cpu helpers
+    def _cpu_ranges(self, pkeys, pvalid):
+        pk = pkeys.to(torch.int64)
+        lo = torch.searchsorted(self.sorted_keys, pk, right=False)
+        hi = torch.searchsorted(self.sorted_keys, pk, right=True)
+        cnt = hi - lo
+        if pvalid is not None:
+            cnt = torch.where(pvalid, cnt, torch.zeros_like(cnt))
+        return cnt, lo
+
+    def _cpu_mark(self, cnt, lo, build_matched):
+        total = int(cnt.sum().item())
+        if total == 0:
+            return
+        pidx = torch.repeat_interleave(torch.arange(cnt.numel()), cnt)
+        starts = torch.cumsum(cnt, 0) - cnt
+        bpos = lo.index_select(0, pidx) + torch.arange(total) - starts.index_select(0, pidx)
+        build_matched[self.order.index_select(0, bpos)] = True
+
+
+def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
+    """Dense group ids for int keys (no NULLs: callers map NULL to a reserved key).
+
+    Returns (gid int32 [n], number of groups, representative row per group int32)."""
+    keys = _keys_ok(keys)
+    n = keys.numel()
+    dev = keys.device
+    if n == 0:
+        z = torch.zeros(0, dtype=torch.int32, device=dev)
+        return z, 0, z
+    if not is_gpu(keys):
+        uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
+        g = uniq.numel()
+        rep = torch.full((g,), n, dtype=torch.int64).scatter_reduce(0, inv, torch.arange(n), reduce="amin")
+        return inv.to(torch.int32), g, rep.to(torch.int32)
+    kmin, kmax = key_range(keys)
+    span = kmax - kmin + 1
+    direct = span <= 2 * n + 65536 and span < 2**31 - 1
+    cap = span if direct else _next_pow2(2 * n)
+    N = launch("groupby")
+    s = stream(keys)
+    k64 = keys.dtype == torch.int64
+    trow = torch.full((cap,), INT32_MAX, dtype=torch.int32, device=dev)
+    tkeys = (torch.empty(1, dtype=torch.int64, device=dev) if direct
+             else torch.full((cap,), EMPTY_KEY, dtype=torch.int64, device=dev))
+    N.groupby_build(ptr(keys), k64, n, ptr(tkeys), ptr(trow), cap, kmin, direct, s)
+    occ = torch.empty(cap, dtype=torch.bool, device=dev)
+    N.groupby_occupied(ptr(trow), cap, ptr(occ), s)
+    slots = mask_to_indices(occ)
+    g = slots.numel()
+    gid_of_slot = torch.empty(cap, dtype=torch.int32, device=dev)
+    rep = torch.empty(g, dtype=torch.int32, device=dev)
+    N.groupby_assign(ptr(slots), slots.dtype == torch.int64, g, ptr(trow), ptr(gid_of_slot), ptr(rep), s)
+    gid = torch.empty(n, dtype=torch.int32, device=dev)
+    N.groupby_lookup(ptr(keys), k64, n, ptr(tkeys), ptr(gid_of_slot), cap, kmin, direct, ptr(gid), s)
+    return gid, g, rep
+
+
+def pack_keys(cols: Sequence[torch.Tensor]) -> torch.Tensor:
+    """Combine several integer key columns into ONE int64 key per row that is
+    equal iff all inputs are equal. Bit-packs when the value ranges fit in 63
+    bits, otherwise re-encodes pairwise through ``group_ids``."""
+    assert cols
+    if len(cols) == 1:
+        c = cols[0]
+        return c if c.dtype in (torch.int32, torch.int64) else c.to(torch.int64)
+    ranges = []
+    for c in cols:
+        r = key_range(c) if c.numel() else (0, 0)
+        ranges.append(r)
+    bits = [max(1, int(hi - lo).bit_length()) for lo, hi in ranges]
+    if sum(bits) <= 62:
+        out = None
+        for c, (lo, _), b in zip(cols, ranges, bits):
+            v = c.to(torch.int64) - lo
+            out = v if out is None else (out << b) | v
+        return out
+    # pairwise dense re-encoding keeps every intermediate code < n
+    acc = cols[0].to(torch.int64)
+    for c in cols[1:]:
+        g1, n1, _ = group_ids(acc)
+        g2, n2, _ = group_ids(c.to(torch.int64) if c.dtype != torch.int64 else c)
+        acc = g1.to(torch.int64) * max(n2, 1) + g2.to(torch.int64)
+    return acc
+
+
+def pack_keys_pair(left: Sequence[torch.Tensor], right: Sequence[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Pack multi-column join keys of both sides with ONE shared encoding."""
+    if len(left) == 1:
+        return left[0], right[0]
+    nl = left[0].numel()
+    both = [torch.cat([a.to(torch.int64), b.to(torch.int64)]) for a, b in zip(left, right)]
+    packed = pack_keys(both)
+    return packed[:nl], packed[nl:]

@@ -1,0 +1,55 @@
+"""Stream compaction and prefix sums (csrc/kernels/select.hip, scan.hip)."""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from ._lib import idx_dtype, is_gpu, launch, ptr, stream
+
+
+def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
+    """Ordered indices of the True entries of a bool mask (int32 when they fit)."""
+    assert mask.dtype == torch.bool and mask.dim() == 1
+    n = mask.numel()
+    it = idx_dtype(n)
+    if not is_gpu(mask):
+        return torch.nonzero(mask).flatten().to(it)
+    mask = mask.contiguous()
+    N = launch("select")
+    tiles = N.select_num_tiles(n)
+    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
+    s = stream(mask)
+    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
+    total = int(ws[tiles].item())
+    out = torch.empty(total, dtype=it, device=mask.device)
+    if total:
+        N.select_write(ptr(mask), n, ptr(ws), ptr(out), it == torch.int64, s)
+    return out
+
+
+def exclusive_scan(counts: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """int32/int64 counts -> (int64 exclusive offsets, total)."""
+    assert counts.dim() == 1 and counts.dtype in (torch.int32, torch.int64)
+    n = counts.numel()
+    if not is_gpu(counts):
+        c = counts.to(torch.int64)
+        inc = torch.cumsum(c, 0)
+        total = int(inc[-1].item()) if n else 0
+        return inc - c, total
+    counts = counts.contiguous()
+    N = launch("exclusive_scan")
+    tiles = N.scan_workspace_tiles(n)
+    ws = torch.empty(tiles + 1, dtype=torch.int64, device=counts.device)
+    out = torch.empty(n, dtype=torch.int64, device=counts.device)
+    N.exclusive_scan(ptr(counts), counts.dtype == torch.int64, n, ptr(out), ptr(ws), ptr(ws) + 8 * tiles, stream(counts))
+    return out, int(ws[tiles].item())
+
+
+def offsets_from_lengths(lengths: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """Arrow offsets [n+1] from per-row lengths."""
+    ex, total = exclusive_scan(lengths)
+    off = torch.empty(lengths.numel() + 1, dtype=torch.int64, device=lengths.device)
+    off[:-1] = ex
+    off[-1] = total
+    return off, total

@@ -1,0 +1,283 @@
+"""String operators (csrc/kernels/strings.hip).
+
+Dictionary-encoded columns (low cardinality, e.g. p_type, l_shipmode) are
+evaluated once per distinct value on the host dictionary and mapped to rows
+through a code lookup table; plain columns (comments, names) run per-row HIP
+kernels on the GPU and pyarrow.compute on the CPU.
+"""
+from __future__ import annotations
+
+import re
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import torch
+
+from .. import types as T
+from ..columnar import Column
+from ._lib import is_gpu, launch, ptr, stream
+from .gather import take
+from .hashing import group_ids
+from .select import offsets_from_lengths
+
+CMP_OPS = {"=": 0, "<>": 1, "<": 2, "<=": 3, ">": 4, ">=": 5}
+
+
+# --------------------------------------------------------------------- helpers
+def tokenize_like(pattern: str, escape: Optional[str] = "\\") -> Tuple[bytes, bytes]:
+    """LIKE pattern -> (bytes, kinds) with kinds 0=literal byte, 1='_', 2='%'."""
+    out, kinds = bytearray(), bytearray()
+    i = 0
+    while i < len(pattern):
+        ch = pattern[i]
+        if escape and ch == escape and i + 1 < len(pattern):
+            for b in pattern[i + 1].encode("utf-8"):
+                out.append(b)
+                kinds.append(0)
+            i += 2
+            continue
+        if ch == "%":
+            if not (kinds and kinds[-1] == 2):  # collapse %%
+                out.append(0)
+                kinds.append(2)
+        elif ch == "_":
+            out.append(0)
+            kinds.append(1)
+        else:
+            for b in ch.encode("utf-8"):
+                out.append(b)
+                kinds.append(0)
+        i += 1
+    return bytes(out), bytes(kinds)
+
+
+def like_regex(pattern: str, ci: bool = False, escape: Optional[str] = "\\") -> "re.Pattern":
+    parts = []
+    i = 0
+    while i < len(pattern):
+        ch = pattern[i]
+        if escape and ch == escape and i + 1 < len(pattern):
+            parts.append(re.escape(pattern[i + 1]))
+            i += 2
+            continue
+        parts.append(".*" if ch == "%" else "." if ch == "_" else re.escape(ch))
+        i += 1
+    return re.compile("".join(parts), re.DOTALL | (re.IGNORECASE if ci else 0))
+
+
+def _lut_apply(col: Column, lut_vals: Sequence) -> torch.Tensor:
+    """Map dictionary codes through a per-dictionary-entry lookup table."""
+    lut = torch.tensor(list(lut_vals), device=col.device)
+    if lut.numel() == 0:
+        return torch.zeros(len(col), dtype=lut.dtype, device=col.device)
+    return lut.index_select(0, col.data.long())
+
+
+def _with_valid(values: torch.Tensor, col: Column) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    return values, col.valid
+
+
+# ------------------------------------------------------------------------ LIKE
+def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, escape: Optional[str] = "\\") -> torch.Tensor:
+    """Bool tensor (NULL rows are False; callers combine ``col.valid``)."""
+    if col.is_dict:
+        rx = like_regex(pattern, ci, escape)
+        lut = [(v is not None and rx.fullmatch(v) is not None) != negate for v in col.dict_values()]
+        return _lut_apply(col, lut).to(torch.bool)
+    n = len(col)
+    if not is_gpu(col.data):
+        arr = col.to_arrow()
+        r = pc.match_like(arr, pattern, ignore_case=ci)
+        if negate:
+            r = pc.invert(r)
+        return torch.from_numpy(r.fill_null(False).to_numpy(zero_copy_only=False).astype(np.bool_))
+    pat, kinds = tokenize_like(pattern, escape)
+    dev = col.device
+    pt = torch.tensor(list(pat) or [0], dtype=torch.uint8).to(dev)
+    kt = torch.tensor(list(kinds) or [0], dtype=torch.uint8).to(dev)
+    out = torch.empty(n, dtype=torch.bool, device=dev)
+    launch("str_like").str_like(ptr(col.offsets), ptr(col.data), n, ptr(pt), ptr(kt), len(pat), ci, negate, ptr(out),
+                                stream(out))
+    return out
+
+
+# --------------------------------------------------------------- comparisons
+def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
+    if col.is_dict:
+        import operator as o
+        f = {"=": o.eq, "<>": o.ne, "<": o.lt, "<=": o.le, ">": o.gt, ">=": o.ge}[op]
+        vb = value.encode("utf-8")
+        lut = [(v is not None and f(v.encode("utf-8"), vb)) for v in col.dict_values()]
+        return _lut_apply(col, lut).to(torch.bool)
+    n = len(col)
+    if not is_gpu(col.data):
+        arr = col.to_arrow()
+        fn = {"=": pc.equal, "<>": pc.not_equal, "<": pc.less, "<=": pc.less_equal, ">": pc.greater,
+              ">=": pc.greater_equal}[op]
+        r = fn(arr, pa.scalar(value, pa.large_string()))
+        return torch.from_numpy(r.fill_null(False).to_numpy(zero_copy_only=False).astype(np.bool_))
+    vb = value.encode("utf-8")
+    ct = torch.tensor(list(vb) or [0], dtype=torch.uint8).to(col.device)
+    out = torch.empty(n, dtype=torch.bool, device=col.device)
+    launch("str_cmp_const").str_cmp_const(ptr(col.offsets), ptr(col.data), n, ptr(ct), len(vb), CMP_OPS[op], ptr(out),
+                                          stream(out))
+    return out
+
+
+def in_list(col: Column, values: Sequence[str]) -> torch.Tensor:
+    if col.is_dict:
+        s = set(values)
+        return _lut_apply(col, [v in s for v in col.dict_values()]).to(torch.bool)
+    out = None
+    for v in values:
+        m = compare_const(col, "=", v)
+        out = m if out is None else (out | m)
+    return out if out is not None else torch.zeros(len(col), dtype=torch.bool, device=col.device)
+
+
+# ------------------------------------------------------------ transformations
+def _dict_transform(col: Column, fn) -> Column:
+    vals = [None if v is None else fn(v) for v in col.dict_values()]
+    uniq, remap = {}, []
+    for v in vals:
+        if v not in uniq:
+            uniq[v] = len(uniq)
+        remap.append(uniq[v])
+    new_dict = Column.from_arrow(pa.array(list(uniq.keys()), pa.large_string()), device=col.device, dict_encode=False)
+    codes = _lut_apply(col, remap).to(torch.int32) if remap else col.data
+    return Column(T.UTF8, codes, col.valid, dictionary=new_dict)
+
+
+def _host_roundtrip(col: Column, fn_arrow) -> Column:
+    arr = fn_arrow(col.to_arrow())
+    c = Column.from_arrow(arr, device=col.device, dict_encode=False)
+    return c
+
+
+def upper(col: Column) -> Column:
+    return _case(col, True)
+
+
+def lower(col: Column) -> Column:
+    return _case(col, False)
+
+
+def _case(col: Column, up: bool) -> Column:
+    if col.is_dict:
+        return _dict_transform(col, str.upper if up else str.lower)
+    if not is_gpu(col.data):
+        return _host_roundtrip(col, pc.utf8_upper if up else pc.utf8_lower)
+    out = torch.empty_like(col.data)
+    flag = torch.zeros(1, dtype=torch.int32, device=col.device)
+    launch("str_case").str_case(ptr(col.data), col.data.numel(), up, ptr(out), ptr(flag), stream(out))
+    if int(flag.item()):
+        # non-ASCII bytes present: full Unicode case mapping can change byte
+        # lengths ('ß' -> 'SS'), so take the exact host path.
+        return _host_roundtrip(col, pc.utf8_upper if up else pc.utf8_lower)
+    return Column(T.UTF8, out, col.valid, offsets=col.offsets)
+
+
+def _py_substr(s: str, start: int, length: Optional[int]) -> str:
+    first = max(start, 1)
+    last = None if length is None else start + length
+    if last is not None and last <= first:
+        return ""
+    return s[first - 1: None if last is None else last - 1]
+
+
+def substr(col: Column, start: int, length: Optional[int]) -> Column:
+    if col.is_dict:
+        return _dict_transform(col, lambda s: _py_substr(s, start, length))
+    n = len(col)
+    if not is_gpu(col.data):
+        vals = [None if v is None else _py_substr(v, start, length) for v in col.to_pylist()]
+        c = Column.from_arrow(pa.array(vals, pa.large_string()), device=col.device, dict_encode=False)
+        c.valid = col.valid
+        return c
+    N = launch("str_substr")
+    s = stream(col.data)
+    has_len = length is not None
+    lens = torch.empty(n, dtype=torch.int64, device=col.device)
+    N.str_substr_lengths(ptr(col.offsets), ptr(col.data), n, start, length or 0, has_len, ptr(lens), s)
+    off, total = offsets_from_lengths(lens)
+    chars = torch.empty(total, dtype=torch.uint8, device=col.device)
+    if total:
+        N.str_substr_copy(ptr(col.offsets), ptr(col.data), n, start, length or 0, has_len, ptr(off), ptr(chars), s)
+    return Column(T.UTF8, chars, col.valid, offsets=off)
+
+
+def char_length(col: Column) -> torch.Tensor:
+    if col.is_dict:
+        return _lut_apply(col, [0 if v is None else len(v) for v in col.dict_values()]).to(torch.int32)
+    arr = col.to_arrow()
+    r = pc.utf8_length(arr).fill_null(0).to_numpy(zero_copy_only=False)
+    return torch.from_numpy(r.astype(np.int32)).to(col.device)
+
+
+def concat(a: Column, b: Column) -> Column:
+    arr = pc.binary_join_element_wise(a.to_arrow(), b.to_arrow(), "")
+    return Column.from_arrow(arr, device=a.device)
+
+
+# ------------------------------------------------------------------ encoding
+def hash64(col: Column) -> torch.Tensor:
+    n = len(col)
+    if not is_gpu(col.data):
+        import xxhash
+        vals = col.to_pylist()
+        return torch.tensor([(xxhash.xxh64_intdigest(v.encode()) - 2**63) if v is not None else 0 for v in vals],
+                            dtype=torch.int64)
+    out = torch.empty(n, dtype=torch.int64, device=col.device)
+    launch("str_hash64").str_hash64(ptr(col.offsets), ptr(col.data), n, ptr(col.valid), ptr(out), stream(out))
+    return out
+
+
+def decode(col: Column) -> Column:
+    """Dictionary column -> plain column."""
+    if not col.is_dict:
+        return col
+    c = take(col.dictionary, col.data)
+    c.valid = col.valid
+    return c
+
+
+def dict_encode(col: Column) -> Column:
+    """Plain column -> dictionary column (exact: hash collisions are verified)."""
+    if col.is_dict:
+        return col
+    n = len(col)
+    if not is_gpu(col.data):
+        return Column.from_arrow(pc.dictionary_encode(col.to_arrow()), device=col.device)
+    h = hash64(col)
+    gid, g, rep = group_ids(h)
+    # verify every row equals its group's representative (no 64-bit collision)
+    mism = torch.zeros(1, dtype=torch.int32, device=col.device)
+    rep_of_row = rep.index_select(0, gid.long())
+    ri = rep_of_row.to(torch.int32)
+    ai = torch.arange(n, dtype=torch.int32, device=col.device)
+    launch("str_eq_rows").str_eq_rows(ptr(col.offsets), ptr(col.data), ptr(ai), ptr(col.offsets), ptr(col.data),
+                                      ptr(ri), False, n, ptr(mism), stream(mism))
+    if int(mism.item()):
+        return Column.from_arrow(pc.dictionary_encode(col.to_arrow()), device=col.device)
+    dictionary = take(col, rep)
+    dictionary.valid = None
+    return Column(T.UTF8, gid, col.valid, dictionary=dictionary)
+
+
+def sort_ranks(col: Column) -> torch.Tensor:
+    """Order-preserving int64 rank per row (byte-wise UTF-8 order)."""
+    c = dict_encode(col) if not col.is_dict else col
+    vals = c.dict_values()
+    order = sorted(range(len(vals)), key=lambda i: (vals[i] is None, (vals[i] or "").encode("utf-8")))
+    rank = [0] * len(vals)
+    for r, i in enumerate(order):
+        rank[i] = r
+    return _lut_apply(c, rank).to(torch.int64)
+
+
+def group_codes(col: Column) -> Tuple[torch.Tensor, Column]:
+    """(int32 codes, dictionary-encoded column) for GROUP BY / join on strings."""
+    c = dict_encode(col)
+    return c.data, c

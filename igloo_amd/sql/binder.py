@@ -1,0 +1,1061 @@
+"""Binder: native AST -> typed logical plan.
+
+Resolves names against the catalog and enclosing scopes (correlated
+subqueries), types and coerces expressions (DataFusion-compatible rules for
+the TPC-H surface: exact decimals, DATE/INTERVAL arithmetic, string/date
+literal coercion), and analyses aggregation (GROUP BY / HAVING / ORDER BY on
+aggregates, DISTINCT). Parity: this is the SqlToRel stage the reference gets
+from DataFusion via ``ctx.sql()`` (reference crates/engine/src/lib.rs:55).
+"""
+from __future__ import annotations
+
+import datetime
+import itertools
+from decimal import Decimal
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from .. import types as T
+from ..types import BOOL, DATE32, FLOAT64, INT32, INT64, UTF8, DataType
+from ..utils.errors import NotSupported, PlanError, TableNotFound
+from .expr import (AGG_FUNCS, AggCall, BinOp, Case, Cast, ColRef, Expr, Func, InList, IsNull, Like, Lit, Neg,
+                   Not, SubqueryExpr, and_all, col_refs, transform, walk)
+from .logical import (Aggregate, ColInfo, Filter, Join, Limit, Plan, Project, Scan, Sort, Union, Values)
+
+EPOCH = datetime.date(1970, 1, 1)
+INTERVAL = DataType("interval")
+
+
+def date_to_days(s: str) -> int:
+    try:
+        return (datetime.date.fromisoformat(s.strip()[:10]) - EPOCH).days
+    except ValueError as e:
+        raise PlanError(f"invalid date literal '{s}'") from e
+
+
+def days_to_date(d: int) -> datetime.date:
+    return EPOCH + datetime.timedelta(days=int(d))
+
+
+def add_months(days: int, months: int) -> int:
+    d = days_to_date(days)
+    y, m = divmod(d.month - 1 + months, 12)
+    y += d.year
+    m += 1
+    import calendar
+    day = min(d.day, calendar.monthrange(y, m)[1])
+    return (datetime.date(y, m, day) - EPOCH).days
+
+
+class IdGen:
+    def __init__(self, start: int = 1):
+        self._it = itertools.count(start)
+
+    def __call__(self) -> int:
+        return next(self._it)
+
+
+# ------------------------------------------------------------------------ scopes
+class Relation:
+    def __init__(self, qualifier: Optional[str], cols: List[ColInfo]):
+        self.qualifier = qualifier
+        self.cols = cols
+
+
+class Scope:
+    def __init__(self, rels: List[Relation], parent: Optional["Scope"] = None):
+        self.rels = rels
+        self.parent = parent
+        self.aliases: Dict[str, ColRef] = {}  # select-list aliases visible to ORDER BY / HAVING
+        self.outer_refs: set = set()          # cids of outer columns referenced from this scope
+
+    def lookup_local(self, parts: List[str]) -> List[ColInfo]:
+        name = parts[-1]
+        qual = ".".join(parts[:-1]) if len(parts) > 1 else None
+        found = []
+        for r in self.rels:
+            if qual is not None:
+                rq = r.qualifier or ""
+                if rq != qual and rq.split(".")[-1] != qual.split(".")[-1]:
+                    continue
+            for c in r.cols:
+                if c.name == name:
+                    found.append(c)
+        return found
+
+    def resolve(self, parts: List[str]) -> Tuple[ColInfo, int]:
+        scope, depth = self, 0
+        while scope is not None:
+            found = scope.lookup_local(parts)
+            if len(found) > 1:
+                # same cid visible twice (USING / NATURAL joins) is fine
+                if len({c.cid for c in found}) > 1:
+                    raise PlanError(f"ambiguous column reference '{'.'.join(parts)}'")
+            if found:
+                return found[0], depth
+            scope, depth = scope.parent, depth + 1
+        raise PlanError(f"column '{'.'.join(parts)}' not found")
+
+
+# ------------------------------------------------------------------- statements
+class BoundQuery:
+    def __init__(self, plan: Plan, names: List[str]):
+        self.plan = plan
+        self.names = names
+
+
+def _lst(node) -> list:
+    return node["c"] if node else []
+
+
+class Binder:
+    def __init__(self, catalog, ids: Optional[IdGen] = None, session: Optional[dict] = None):
+        self.catalog = catalog
+        self.ids = ids or IdGen()
+        self.session = session or {}
+
+    # =================================================================== query
+    def bind_query(self, q: dict, outer: Optional[Scope] = None, ctes: Optional[dict] = None) -> BoundQuery:
+        ctes = dict(ctes or {})
+        for c in _lst(q.get("with")):
+            ctes[c["s"]] = (c, dict(ctes))
+        prev = getattr(self, "_ctes", None)
+        self._ctes = ctes
+        try:
+            return self._bind_query_inner(q, outer, ctes)
+        finally:
+            self._ctes = prev
+
+    def _bind_query_inner(self, q: dict, outer: Optional[Scope], ctes: dict) -> BoundQuery:
+        order = _lst(q.get("order"))
+        limit = self._const_int(q.get("limit")) if q.get("limit") else None
+        offset = self._const_int(q.get("offset")) if q.get("offset") else 0
+        body = q["body"]
+        if body["k"] == "select":
+            bq = self._bind_select(body, outer, ctes, order)
+        else:
+            bq = self._bind_setop(body, outer, ctes)
+            if order:
+                bq = self._order_over_output(bq, order)
+        plan = bq.plan
+        if limit is not None or offset:
+            if isinstance(plan, Sort) and limit is not None:
+                plan = Sort(plan.input, plan.keys, fetch=limit + offset)
+            elif isinstance(plan, Project) and isinstance(plan.input, Sort) and limit is not None:
+                s = plan.input
+                plan = Project(Sort(s.input, s.keys, fetch=limit + offset), plan.exprs)
+            plan = Limit(plan, limit, offset)
+        return BoundQuery(plan, bq.names)
+
+    def _const_int(self, node) -> int:
+        e = self.bind_expr(node, Scope([]))
+        if not isinstance(e, Lit) or not isinstance(e.value, int):
+            raise PlanError("LIMIT/OFFSET must be an integer literal")
+        return int(e.value)
+
+    def _bind_setop(self, node, outer, ctes) -> BoundQuery:
+        k = node["k"]
+        if k == "select":
+            return self._bind_select(node, outer, ctes, [])
+        if k == "subquery_body":
+            return self.bind_query(node["query"], outer, ctes)
+        if k == "values":
+            return self._bind_values(node, outer)
+        if k != "setop":
+            raise NotSupported(f"set operand {k}")
+        op = node["s"]
+        a = self._bind_setop(node["c"][0], outer, ctes)
+        b = self._bind_setop(node["c"][1], outer, ctes)
+        if len(a.names) != len(b.names):
+            raise PlanError("UNION inputs have different numbers of columns")
+        if op.startswith("union"):
+            schema, kids = [], []
+            cast_a, cast_b = [], []
+            for ca, cb in zip(a.plan.schema, b.plan.schema):
+                t = T.common_numeric(ca.dtype, cb.dtype) if ca.dtype != cb.dtype else ca.dtype
+                schema.append(ColInfo(self.ids(), ca.name, t, ca.nullable or cb.nullable))
+            pa_ = Project(a.plan, [(ColInfo(s.cid, s.name, s.dtype, s.nullable), self._coerce(c.ref(), s.dtype))
+                                    for s, c in zip(schema, a.plan.schema)])
+            schema_b = [ColInfo(self.ids(), s.name, s.dtype, s.nullable) for s in schema]
+            pb_ = Project(b.plan, [(sb, self._coerce(c.ref(), sb.dtype)) for sb, c in zip(schema_b, b.plan.schema)])
+            # union output reuses the first input's cids
+            plan: Plan = Union([pa_, _rename(pb_, schema)], schema)
+            if op == "union":
+                plan = self._distinct(plan)
+            return BoundQuery(plan, a.names)
+        if op.startswith("intersect") or op.startswith("except"):
+            on = [(ca.ref(), cb.ref()) for ca, cb in zip(a.plan.schema, b.plan.schema)]
+            kind = "semi" if op.startswith("intersect") else "anti"
+            plan = Join(self._distinct(a.plan), b.plan, kind, on)
+            return BoundQuery(plan, a.names)
+        raise NotSupported(op)
+
+    def _distinct(self, plan: Plan) -> Plan:
+        groups = [(ColInfo(self.ids(), c.name, c.dtype, c.nullable), c.ref()) for c in plan.schema]
+        return Aggregate(plan, groups, [])
+
+    def _bind_values(self, node, outer) -> BoundQuery:
+        rows = [[self.bind_expr(e, Scope([], outer)) for e in r["c"]] for r in node["c"]]
+        width = len(rows[0])
+        schema = []
+        for j in range(width):
+            t = rows[0][j].dtype
+            for r in rows[1:]:
+                t = T.common_numeric(t, r[j].dtype) if t != r[j].dtype else t
+            schema.append(ColInfo(self.ids(), f"column{j + 1}", t, any(r[j].nullable for r in rows)))
+        rows = [[self._coerce(e, s.dtype) for e, s in zip(r, schema)] for r in rows]
+        return BoundQuery(Values(rows, schema), [s.name for s in schema])
+
+    def _order_over_output(self, bq: BoundQuery, order) -> BoundQuery:
+        scope = Scope([Relation(None, [ColInfo(c.cid, n, c.dtype, c.nullable) for c, n in zip(bq.plan.schema, bq.names)])])
+        keys = []
+        for o in order:
+            e = o["c"][0]
+            if e["k"] == "lit" and e.get("type") == "int":
+                idx = int(e["s"]) - 1
+                c = bq.plan.schema[idx]
+                bound: Expr = c.ref()
+            else:
+                bound = self.bind_expr(e, scope)
+            asc = not o.get("desc")
+            nf = o.get("nulls", "last" if asc else "first") == "first"
+            keys.append((bound, asc, nf))
+        return BoundQuery(Sort(bq.plan, keys), bq.names)
+
+    # ================================================================== select
+    def _bind_select(self, s: dict, outer: Optional[Scope], ctes: dict, order: list) -> BoundQuery:
+        # ---- FROM
+        if s.get("from"):
+            plan, rels = None, []
+            for item in _lst(s["from"]):
+                p, r = self._bind_from(item, outer, ctes)
+                plan = p if plan is None else Join(plan, p, "cross")
+                rels += r
+        else:
+            plan, rels = Values([[]], []), []
+        scope = Scope(rels, outer)
+        # ---- WHERE
+        if s.get("where"):
+            pred = self.bind_expr(s["where"], scope)
+            self._require_bool(pred, "WHERE")
+            plan = Filter(plan, pred)
+        # ---- SELECT list (stars expanded)
+        items: List[Tuple[Expr, str]] = []
+        for it in _lst(s["items"]):
+            if it["k"] == "star":
+                qual = it["s"] or None
+                for r in rels:
+                    if qual is None or r.qualifier == qual or (r.qualifier or "").split(".")[-1] == qual:
+                        for c in r.cols:
+                            items.append((c.ref(), c.name))
+                if qual and not any(r.qualifier == qual or (r.qualifier or "").split(".")[-1] == qual for r in rels):
+                    raise PlanError(f"unknown table '{qual}' in {qual}.*")
+                continue
+            e = self.bind_expr(it["c"][0], scope, allow_agg=True)
+            items.append((e, it.get("alias") or self._display_name(it["c"][0], e)))
+        # ---- GROUP BY
+        group_exprs: List[Expr] = []
+        for g in _lst(s.get("group")):
+            if g["k"] == "lit" and g.get("type") == "int":
+                idx = int(g["s"]) - 1
+                if not 0 <= idx < len(items):
+                    raise PlanError(f"GROUP BY position {idx + 1} out of range")
+                group_exprs.append(items[idx][0])
+                continue
+            if g["k"] == "col" and len(g["c"]) == 1:
+                # a select alias may be used in GROUP BY (when it is not also an input column)
+                nm = g["s"]
+                try:
+                    scope.resolve([nm])
+                except PlanError:
+                    hit = [e for e, a in items if a == nm]
+                    if hit:
+                        group_exprs.append(hit[0])
+                        continue
+            group_exprs.append(self.bind_expr(g, scope))
+        having = self.bind_expr(s["having"], scope, allow_agg=True) if s.get("having") else None
+        # ORDER BY expressions bound against input scope + aliases (resolved later)
+        aliases = {a: e for e, a in items}
+        order_bound = []
+        for o in order:
+            e = o["c"][0]
+            asc = not o.get("desc")
+            nf = o.get("nulls", "last" if asc else "first") == "first"
+            if e["k"] == "lit" and e.get("type") == "int":
+                idx = int(e["s"]) - 1
+                if not 0 <= idx < len(items):
+                    raise PlanError(f"ORDER BY position {idx + 1} out of range")
+                order_bound.append(("item", idx, asc, nf))
+                continue
+            if e["k"] == "col" and len(e["c"]) == 1 and e["s"] in aliases:
+                idx = [a for _, a in items].index(e["s"])
+                order_bound.append(("item", idx, asc, nf))
+                continue
+            bound = self.bind_expr(e, scope, allow_agg=True)
+            # an ORDER BY expression identical to a select item uses that item
+            hit = [i for i, (ie, _) in enumerate(items) if ie.sql() == bound.sql()]
+            if hit:
+                order_bound.append(("item", hit[0], asc, nf))
+            else:
+                order_bound.append(("expr", bound, asc, nf))
+        # ---- aggregation
+        has_aggs = any(_contains_agg(e) for e, _ in items) or (having is not None and _contains_agg(having)) or \
+            any(k == "expr" and _contains_agg(x) for k, x, _, _ in order_bound)
+        if group_exprs or has_aggs:
+            plan, rewrite = self._aggregate(plan, group_exprs, [e for e, _ in items] + ([having] if having is not None else [])
+                                            + [x for k, x, _, _ in order_bound if k == "expr"])
+            items = [(rewrite(e), a) for e, a in items]
+            if having is not None:
+                having = rewrite(having)
+            order_bound = [(k, rewrite(x) if k == "expr" else x, a, nf) for k, x, a, nf in order_bound]
+        if having is not None:
+            self._require_bool(having, "HAVING")
+            plan = Filter(plan, having)
+        # ---- projection (+ hidden ORDER BY columns)
+        proj = [(ColInfo(self.ids(), a, e.dtype, e.nullable), e) for e, a in items]
+        hidden = []
+        sort_keys = []
+        for k, x, asc, nf in order_bound:
+            if k == "item":
+                sort_keys.append((proj[x][0].ref(), asc, nf))
+            else:
+                ci = ColInfo(self.ids(), f"__order{len(hidden)}", x.dtype, x.nullable)
+                hidden.append((ci, x))
+                sort_keys.append((ci.ref(), asc, nf))
+        distinct = bool(s.get("distinct"))
+        if distinct and hidden:
+            raise PlanError("for SELECT DISTINCT, ORDER BY expressions must appear in select list")
+        plan = Project(plan, proj + hidden)
+        if distinct:
+            plan = self._distinct_keep(plan)
+        if sort_keys:
+            plan = Sort(plan, sort_keys)
+            if hidden:
+                plan = Project(plan, [(c, c.ref()) for c, _ in proj])
+        names = [c.name for c, _ in proj]
+        return BoundQuery(plan, names)
+
+    def _distinct_keep(self, plan: Project) -> Plan:
+        # DISTINCT keeps the projected cids so ORDER BY references stay valid
+        groups = [(c, c.ref()) for c in plan.schema]
+        return Aggregate(plan, [(ColInfo(c.cid, c.name, c.dtype, c.nullable), _Passthrough(c)) for c, _ in groups], [])
+
+    def _aggregate(self, plan: Plan, group_exprs: List[Expr], exprs: List[Expr]):
+        groups: List[Tuple[ColInfo, Expr]] = []
+        gmap: Dict[str, ColRef] = {}
+        for g in group_exprs:
+            key = g.sql()
+            if key in gmap:
+                continue
+            name = g.name if isinstance(g, ColRef) else key
+            ci = ColInfo(self.ids(), name, g.dtype, g.nullable)
+            groups.append((ci, g))
+            gmap[key] = ci.ref()
+        aggs: List[Tuple[ColInfo, AggCall]] = []
+        amap: Dict[str, ColRef] = {}
+        for e in exprs:
+            for x in walk(e):
+                if isinstance(x, AggCall):
+                    key = x.sql() + (f" FILTER {x.filter.sql()}" if x.filter is not None else "")
+                    if key not in amap:
+                        if x.arg is not None and _contains_agg(x.arg):
+                            raise PlanError("aggregate function calls cannot be nested")
+                        ci = ColInfo(self.ids(), x.sql(), x.dtype, x.func not in ("count",))
+                        aggs.append((ci, x))
+                        amap[key] = ci.ref()
+        agg = Aggregate(plan, groups, aggs)
+        group_cids = {ci.cid for ci, _ in groups}
+
+        def rewrite(e: Expr) -> Expr:
+            def fn(x):
+                k = x.sql()
+                if isinstance(x, AggCall):
+                    return amap[k + (f" FILTER {x.filter.sql()}" if x.filter is not None else "")]
+                if k in gmap:
+                    return gmap[k]
+                return None
+            out = _transform_top_down(e, fn)
+            for x in walk(out):
+                if isinstance(x, ColRef) and x.cid not in group_cids and x.cid not in {c.cid for c, _ in aggs}:
+                    if isinstance(x, ColRef) and not getattr(x, "_outer", False):
+                        raise PlanError(f"column '{x.name}' must appear in the GROUP BY clause or be used in an aggregate function")
+            return out
+        return agg, rewrite
+
+    # =================================================================== FROM
+    def _bind_from(self, item: dict, outer, ctes) -> Tuple[Plan, List[Relation]]:
+        k = item["k"]
+        if k == "table":
+            name = item["s"]
+            alias = item.get("alias")
+            if name in ctes:
+                cnode, cenv = ctes[name]
+                bq = self.bind_query(cnode["query"], outer, cenv)
+                cols = [c["s"] for c in _lst(cnode.get("columns"))] or bq.names
+                return self._derived(bq, alias or name, cols, item)
+            view = self.catalog.get_view(name) if hasattr(self.catalog, "get_view") else None
+            if view is not None:
+                from ..sql import parse
+                bq = self.bind_query(parse(view)[0], outer, {})
+                return self._derived(bq, alias or name, bq.names, item)
+            src = self.catalog.get_table(name)
+            if src is None:
+                raise TableNotFound(f"table '{name}' not found")
+            schema = [ColInfo(self.ids(), f.name, f.dtype, f.nullable, alias or name) for f in src.schema()]
+            qual = alias or name
+            rel = Relation(qual, schema)
+            if item.get("columns"):
+                new = [c["s"] for c in _lst(item["columns"])]
+                rel = Relation(qual, [ColInfo(c.cid, n, c.dtype, c.nullable, qual) for c, n in zip(schema, new)] + schema[len(new):])
+            return Scan(name, src, schema), [rel]
+        if k == "subquery":
+            bq = self.bind_query(item["query"], outer, ctes)
+            cols = [c["s"] for c in _lst(item.get("columns"))] or bq.names
+            return self._derived(bq, item.get("alias"), cols, item)
+        if k == "join":
+            lp, lr = self._bind_from(item["c"][0], outer, ctes)
+            rp, rr = self._bind_from(item["c"][1], outer, ctes)
+            kind = item["s"]
+            kind = {"left_semi": "semi", "left_anti": "anti"}.get(kind, kind)
+            if kind in ("right_semi", "right_anti"):
+                lp, rp, lr, rr = rp, lp, rr, lr
+                kind = kind.split("_")[1]
+            scope = Scope(lr + rr, outer)
+            residual = None
+            if item.get("on"):
+                residual = self.bind_expr(item["on"], scope)
+            names = None
+            if item.get("using"):
+                names = [c["s"] for c in _lst(item["using"])]
+            elif item.get("natural"):
+                ln = {c.name for r in lr for c in r.cols}
+                names = [c.name for r in rr for c in r.cols if c.name in ln]
+            if names:
+                conds = []
+                for n in names:
+                    a = Scope(lr).resolve([n])[0]
+                    b = Scope(rr).resolve([n])[0]
+                    conds.append(self._cmp("=", a.ref(), b.ref()))
+                residual = and_all(conds + ([residual] if residual is not None else []))
+                # the USING column is visible once (from the left input)
+                rr = [Relation(r.qualifier, [c for c in r.cols if c.name not in names]) for r in rr]
+            if kind == "cross":
+                return Join(lp, rp, "cross"), lr + rr
+            return Join(lp, rp, kind, [], residual), (lr + rr if kind not in ("semi", "anti") else lr)
+        raise NotSupported(f"FROM item {k}")
+
+    def _derived(self, bq: BoundQuery, alias, names, item) -> Tuple[Plan, List[Relation]]:
+        cols = [ColInfo(c.cid, n, c.dtype, c.nullable, alias) for c, n in zip(bq.plan.schema, names)]
+        return bq.plan, [Relation(alias, cols)]
+
+    # ============================================================ expressions
+    def bind_expr(self, node: dict, scope: Scope, allow_agg: bool = False) -> Expr:
+        k = node["k"]
+        if k == "paren":
+            return self.bind_expr(node["c"][0], scope, allow_agg)
+        if k == "col":
+            parts = [p["s"] for p in node["c"]]
+            if len(parts) == 1 and parts[0] in scope.aliases:
+                return scope.aliases[parts[0]]
+            ci, depth = scope.resolve(parts)
+            r = ci.ref()
+            if depth > 0:
+                r._outer = True  # type: ignore[attr-defined]
+                s = scope
+                for _ in range(depth):
+                    s.outer_refs.add(ci.cid)
+                    s = s.parent
+            return r
+        if k == "lit":
+            return self._literal(node)
+        if k == "bin":
+            op = node["s"]
+            l = self.bind_expr(node["c"][0], scope, allow_agg)
+            r = self.bind_expr(node["c"][1], scope, allow_agg)
+            if op in ("and", "or"):
+                self._require_bool(l, op.upper())
+                self._require_bool(r, op.upper())
+                return _fold(BinOp(op, l, r, BOOL))
+            if op in ("=", "<>", "<", "<=", ">", ">=", "is_distinct_from", "is_not_distinct_from"):
+                return self._cmp(op, l, r)
+            if op == "||":
+                return Func("concat", [self._coerce(l, UTF8), self._coerce(r, UTF8)], UTF8)
+            return self._arith(op, l, r)
+        if k == "un":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            if node["s"] == "not":
+                self._require_bool(x, "NOT")
+                if isinstance(x, Lit):
+                    return Lit(None if x.value is None else (not x.value), BOOL)
+                return Not(x)
+            if isinstance(x, Lit) and x.value is not None:
+                return Lit(-x.value, x.dtype)
+            return Neg(x, x.dtype)
+        if k == "between":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            lo = self.bind_expr(node["c"][1], scope, allow_agg)
+            hi = self.bind_expr(node["c"][2], scope, allow_agg)
+            e = BinOp("and", self._cmp(">=", x, lo), self._cmp("<=", x, hi), BOOL)
+            return Not(e) if node.get("neg") else e
+        if k == "inlist":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            vals = [self.bind_expr(v, scope, allow_agg) for v in node["c"][1:]]
+            if not all(isinstance(v, Lit) for v in vals):
+                ors = [self._cmp("=", x, v) for v in vals]
+                e = ors[0]
+                for o in ors[1:]:
+                    e = BinOp("or", e, o, BOOL)
+                return Not(e) if node.get("neg") else e
+            t = x.dtype
+            vals = [self._coerce_lit(v, t) for v in vals]
+            return InList(x, vals, bool(node.get("neg")))
+        if k == "like":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            p = self.bind_expr(node["c"][1], scope, allow_agg)
+            if not isinstance(p, Lit) or not isinstance(p.value, str):
+                raise NotSupported("LIKE pattern must be a string literal")
+            esc = "\\"
+            if node.get("escape"):
+                esc = self.bind_expr(node["escape"], scope).value
+            return Like(self._coerce(x, UTF8), p.value, bool(node.get("neg")), bool(node.get("ilike")), esc)
+        if k == "isnull":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            return IsNull(x, bool(node.get("neg")))
+        if k == "istruth":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            want = node["s"] == "true"
+            e = BinOp("and", IsNull(x, True), x if want else Not(x), BOOL)
+            return Not(e) if node.get("neg") else e
+        if k == "cast":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            t = T.parse_type_name(node["type"])
+            return self._cast(x, t)
+        if k == "case":
+            return self._case(node, scope, allow_agg)
+        if k == "extract":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            field = node["s"].lower()
+            field = {"years": "year", "months": "month", "days": "day", "dayofweek": "dow", "dayofyear": "doy"}.get(field, field)
+            if field not in ("year", "month", "day", "quarter", "dow", "doy"):
+                raise NotSupported(f"EXTRACT({field})")
+            x = self._coerce(x, DATE32)
+            if isinstance(x, Lit):
+                return Lit(_date_part_py(x.value, field), INT32)
+            return Func("date_part", [x], INT32, (field,))
+        if k == "func":
+            return self._func(node, scope, allow_agg)
+        if k in ("subq", "exists", "insub"):
+            sub_scope = Scope([], scope)
+            bq = self.bind_query(node["query"], sub_scope, getattr(self, "_ctes", None))
+            outer = set(sub_scope.outer_refs)
+            if k == "exists":
+                return SubqueryExpr("exists", bq.plan, None, bool(node.get("neg")), BOOL, outer)
+            if k == "subq":
+                if len(bq.plan.schema) != 1:
+                    raise PlanError("scalar subquery must return exactly one column")
+                c = bq.plan.schema[0]
+                return SubqueryExpr("scalar", bq.plan, None, False, c.dtype, outer)
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            if len(bq.plan.schema) != 1:
+                raise PlanError("IN subquery must return exactly one column")
+            return SubqueryExpr("in", bq.plan, x, bool(node.get("neg")), BOOL, outer)
+        if k == "row":
+            raise NotSupported("row constructors")
+        raise NotSupported(f"expression kind {k}")
+
+    # ------------------------------------------------------------ literals
+    def _literal(self, node) -> Lit:
+        t = node["type"]
+        s = node["s"]
+        if t == "int":
+            v = int(s)
+            return Lit(v, INT64)
+        if t == "dec":
+            d = Decimal(s)
+            sign, digits, exp = d.as_tuple()
+            scale = max(-exp, 0)
+            unscaled = int(d.scaleb(scale))
+            prec = max(len(str(abs(unscaled))), scale + 1)
+            return Lit(unscaled, T.DECIMAL(prec, scale))
+        if t == "float":
+            return Lit(float(s), FLOAT64)
+        if t == "str":
+            return Lit(s, UTF8)
+        if t == "bool":
+            return Lit(s == "true", BOOL)
+        if t == "null":
+            return Lit(None, T.NULL)
+        if t == "date":
+            return Lit(date_to_days(s), DATE32)
+        if t == "timestamp":
+            dt = datetime.datetime.fromisoformat(s)
+            return Lit(int((dt - datetime.datetime(1970, 1, 1)).total_seconds() * 1_000_000), T.TIMESTAMP)
+        if t == "interval":
+            return Lit(_parse_interval(s, node.get("unit")), INTERVAL)
+        raise NotSupported(f"literal type {t}")
+
+    # ------------------------------------------------------------ typing
+    @staticmethod
+    def _require_bool(e: Expr, where: str):
+        if e.dtype not in (BOOL, T.NULL):
+            raise PlanError(f"{where} requires a boolean expression, got {e.dtype}")
+
+    def _cast(self, x: Expr, t: DataType) -> Expr:
+        if x.dtype == t:
+            return x
+        if isinstance(x, Lit):
+            return _fold_cast(x, t)
+        return Cast(x, t)
+
+    def _coerce_lit(self, v: Lit, t: DataType) -> Lit:
+        if v.dtype == t or v.value is None:
+            return Lit(v.value, t) if v.value is None else v
+        if t.is_string:
+            return v if v.dtype.is_string else _fold_cast(v, UTF8)
+        if t.kind == "date32" and v.dtype.is_string:
+            return Lit(date_to_days(v.value), DATE32)
+        if t.is_numeric and v.dtype.is_numeric:
+            ct = T.common_numeric(t, v.dtype)
+            return _fold_cast(v, ct)
+        return _fold_cast(v, t)
+
+    def _coerce(self, e: Expr, t: DataType) -> Expr:
+        if e.dtype == t:
+            return e
+        if isinstance(e, Lit):
+            return self._coerce_lit(e, t) if e.value is not None else Lit(None, t)
+        return Cast(e, t)
+
+    def _cmp(self, op: str, l: Expr, r: Expr) -> Expr:
+        lt, rt = l.dtype, r.dtype
+        # literal coercion towards the column type
+        if lt != rt:
+            if isinstance(r, Lit) and not isinstance(l, Lit):
+                if lt.kind == "date32" and rt.is_string:
+                    r = Lit(date_to_days(r.value), DATE32)
+                elif lt.is_string and not rt.is_string and r.value is not None:
+                    r = _fold_cast(r, UTF8)
+            elif isinstance(l, Lit) and not isinstance(r, Lit):
+                if rt.kind == "date32" and lt.is_string:
+                    l = Lit(date_to_days(l.value), DATE32)
+                elif rt.is_string and not lt.is_string and l.value is not None:
+                    l = _fold_cast(l, UTF8)
+            lt, rt = l.dtype, r.dtype
+        if lt != rt:
+            ct = T.common_numeric(lt, rt)
+            l, r = self._coerce(l, ct), self._coerce(r, ct)
+        return _fold(BinOp(op, l, r, BOOL))
+
+    def _arith(self, op: str, l: Expr, r: Expr) -> Expr:
+        lt, rt = l.dtype, r.dtype
+        # ---- DATE / INTERVAL arithmetic
+        if lt == INTERVAL or rt == INTERVAL:
+            if rt == INTERVAL and op in ("+", "-") and lt.kind == "date32":
+                months, days = r.value
+                if op == "-":
+                    months, days = -months, -days
+                if isinstance(l, Lit):
+                    return Lit(add_months(l.value, months) + days if l.value is not None else None, DATE32)
+                if months:
+                    return Func("add_months", [l], DATE32, (months, days))
+                return BinOp("+", l, Lit(days, INT32), DATE32)
+            if lt == INTERVAL and op == "+" and rt.kind == "date32":
+                return self._arith("+", r, l)
+            raise NotSupported(f"interval arithmetic {lt} {op} {rt}")
+        if lt.kind == "date32" or rt.kind == "date32":
+            if op == "-" and lt.kind == "date32" and rt.kind == "date32":
+                return _fold(BinOp("-", l, r, INT64))
+            if op in ("+", "-") and lt.kind == "date32" and rt.is_integer:
+                return _fold(BinOp(op, l, r, DATE32))
+            if op == "+" and rt.kind == "date32" and lt.is_integer:
+                return _fold(BinOp(op, r, l, DATE32))
+            raise PlanError(f"cannot apply {op} to {lt} and {rt}")
+        if lt.is_string or rt.is_string:
+            raise PlanError(f"cannot apply {op} to {lt} and {rt}")
+        if lt.kind == "null" or rt.kind == "null":
+            t = rt if lt.kind == "null" else lt
+            return Lit(None, t if t.kind != "null" else INT64)
+        if lt.kind == "bool" or rt.kind == "bool":
+            raise PlanError(f"cannot apply {op} to boolean")
+        # ---- numeric
+        if lt.is_float or rt.is_float:
+            t = FLOAT64
+            return _fold(BinOp(op, self._coerce(l, t), self._coerce(r, t), t))
+        if lt.is_decimal or rt.is_decimal:
+            dl = lt if lt.is_decimal else _int_as_decimal(l)
+            dr = rt if rt.is_decimal else _int_as_decimal(r)
+            if op in ("+", "-"):
+                s = max(dl.scale, dr.scale)
+                p = min(38, max(dl.precision - dl.scale, dr.precision - dr.scale) + s + 1)
+                t = T.DECIMAL(p, s)
+                return _fold(BinOp(op, self._coerce(l, T.DECIMAL(dl.precision + s - dl.scale, s)),
+                                   self._coerce(r, T.DECIMAL(dr.precision + s - dr.scale, s)), t))
+            if op == "*":
+                t = T.DECIMAL(min(38, dl.precision + dr.precision + 1), dl.scale + dr.scale)
+                return _fold(BinOp("*", self._coerce(l, dl), self._coerce(r, dr), t))
+            if op == "/":
+                return _fold(BinOp("/", self._coerce(l, FLOAT64), self._coerce(r, FLOAT64), FLOAT64))
+            if op == "%":
+                s = max(dl.scale, dr.scale)
+                t = T.DECIMAL(max(dl.precision, dr.precision), s)
+                return _fold(BinOp("%", self._coerce(l, T.DECIMAL(dl.precision, s)), self._coerce(r, T.DECIMAL(dr.precision, s)), t))
+        if lt.is_integer and rt.is_integer:
+            return _fold(BinOp(op, self._coerce(l, INT64), self._coerce(r, INT64), INT64))
+        raise PlanError(f"cannot apply {op} to {lt} and {rt}")
+
+    def _case(self, node, scope, allow_agg) -> Expr:
+        operand = self.bind_expr(node["operand"], scope, allow_agg) if node.get("operand") else None
+        kids = node["c"]
+        whens = []
+        for i in range(0, len(kids), 2):
+            c = self.bind_expr(kids[i], scope, allow_agg)
+            v = self.bind_expr(kids[i + 1], scope, allow_agg)
+            if operand is not None:
+                c = self._cmp("=", operand, c)
+            whens.append((c, v))
+        els = self.bind_expr(node["else"], scope, allow_agg) if node.get("else") else None
+        t = None
+        for _, v in whens + ([(None, els)] if els is not None else []):
+            if v.dtype.kind == "null":
+                continue
+            t = v.dtype if t is None else (t if t == v.dtype else T.common_numeric(t, v.dtype))
+        t = t or T.NULL
+        whens = [(c, self._coerce(v, t)) for c, v in whens]
+        els = self._coerce(els, t) if els is not None else None
+        return Case(whens, els, t)
+
+    def _func(self, node, scope, allow_agg) -> Expr:
+        name = node["s"].lower()
+        if name in AGG_FUNCS or name in ("stddev_samp", "stddev_pop", "var_samp", "var_pop"):
+            if not allow_agg:
+                raise PlanError(f"aggregate function {name} not allowed here")
+            distinct = bool(node.get("distinct"))
+            if node.get("star"):
+                arg = None
+            else:
+                args = [self.bind_expr(a, scope) for a in node["c"]]
+                if len(args) != 1:
+                    raise NotSupported(f"{name} with {len(args)} arguments")
+                arg = args[0]
+            flt = self.bind_expr(node["filter"], scope) if node.get("filter") else None
+            return _make_agg(name, arg, distinct, flt)
+        args = [self.bind_expr(a, scope, allow_agg) for a in node["c"]]
+        if name in ("upper", "lower", "capitalize"):
+            _nargs(name, args, 1)
+            a = self._coerce(args[0], UTF8)
+            fn = "upper" if name == "capitalize" else name
+            if isinstance(a, Lit):
+                return Lit(None if a.value is None else (a.value.upper() if fn == "upper" else a.value.lower()), UTF8)
+            return Func(fn, [a], UTF8)
+        if name in ("substr", "substring"):
+            if len(args) not in (2, 3):
+                raise PlanError("substr takes 2 or 3 arguments")
+            a = self._coerce(args[0], UTF8)
+            if not all(isinstance(x, Lit) for x in args[1:]):
+                raise NotSupported("substr with non-literal positions")
+            start = int(args[1].value)
+            ln = int(args[2].value) if len(args) == 3 else None
+            if isinstance(a, Lit):
+                from ..ops.strings import _py_substr
+                return Lit(None if a.value is None else _py_substr(a.value, start, ln), UTF8)
+            return Func("substr", [a], UTF8, (start, ln))
+        if name in ("length", "char_length", "character_length"):
+            _nargs(name, args, 1)
+            return Func("char_length", [self._coerce(args[0], UTF8)], INT32)
+        if name == "abs":
+            _nargs(name, args, 1)
+            return Func("abs", args, args[0].dtype)
+        if name == "round":
+            d = int(args[1].value) if len(args) > 1 else 0
+            t = args[0].dtype
+            if t.is_decimal:
+                return Func("round", [args[0]], T.DECIMAL(t.precision, min(t.scale, max(d, 0))), (d,))
+            return Func("round", [self._coerce(args[0], FLOAT64) if not t.is_integer else args[0]],
+                        FLOAT64 if not t.is_integer else t, (d,))
+        if name in ("coalesce", "ifnull", "nvl"):
+            t = None
+            for a in args:
+                if a.dtype.kind != "null":
+                    t = a.dtype if t is None else (t if t == a.dtype else T.common_numeric(t, a.dtype))
+            t = t or T.NULL
+            return Func("coalesce", [self._coerce(a, t) for a in args], t)
+        if name == "nullif":
+            _nargs(name, args, 2)
+            return Case([(self._cmp("=", args[0], args[1]), Lit(None, args[0].dtype))], args[0], args[0].dtype)
+        if name in ("date_part", "datepart"):
+            field = args[0].value.lower()
+            return Func("date_part", [self._coerce(args[1], DATE32)], INT32, (field,))
+        if name == "year":
+            return Func("date_part", [self._coerce(args[0], DATE32)], INT32, ("year",))
+        if name in ("concat",):
+            out = args[0]
+            for a in args[1:]:
+                out = Func("concat", [self._coerce(out, UTF8), self._coerce(a, UTF8)], UTF8)
+            return out
+        if name in ("sqrt", "ln", "log10", "exp", "floor", "ceil", "ceiling"):
+            _nargs(name, args, 1)
+            return Func(name.replace("ceiling", "ceil"), [self._coerce(args[0], FLOAT64)], FLOAT64)
+        if name in ("power", "pow"):
+            return Func("power", [self._coerce(a, FLOAT64) for a in args], FLOAT64)
+        if name in ("to_date",):
+            return self._coerce(args[0], DATE32)
+        raise NotSupported(f"function {name}()")
+
+    def _display_name(self, ast: dict, e: Expr) -> str:
+        if isinstance(e, ColRef) and ast["k"] == "col":
+            return e.name
+        return _ast_text(ast)
+
+
+class _Passthrough(ColRef):
+    """Group key that is the projected column itself (DISTINCT)."""
+
+    def __init__(self, c: ColInfo):
+        super().__init__(c.cid, c.name, c.dtype, c.nullable)
+
+
+# ---------------------------------------------------------------------- helpers
+def _rename(p: Project, schema: List[ColInfo]) -> Project:
+    return Project(p.input, [(s, e) for s, (_, e) in zip(schema, p.exprs)])
+
+
+def _contains_agg(e: Expr) -> bool:
+    for x in walk(e):
+        if isinstance(x, AggCall):
+            return True
+    return False
+
+
+def _transform_top_down(e: Expr, fn) -> Expr:
+    r = fn(e)
+    if r is not None:
+        return r
+    kids = e.children()
+    if not kids:
+        return e
+    new = [_transform_top_down(k, fn) for k in kids]
+    if any(a is not b for a, b in zip(new, kids)):
+        # SubqueryExpr keeps its plan; other nodes rebuild from children
+        return e.with_children(new)
+    return e
+
+
+def _nargs(name, args, n):
+    if len(args) != n:
+        raise PlanError(f"{name}() takes {n} argument(s)")
+
+
+def _int_as_decimal(e: Expr) -> DataType:
+    if isinstance(e, Lit) and isinstance(e.value, int):
+        return T.DECIMAL(max(len(str(abs(e.value))), 1), 0)
+    return T.DECIMAL(19 if e.dtype.kind == "int64" else 10, 0)
+
+
+def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt) -> AggCall:
+    if name == "mean":
+        name = "avg"
+    if name == "count":
+        return AggCall("count", arg, distinct, INT64, flt)
+    if arg is None:
+        raise PlanError(f"{name}(*) is not valid")
+    t = arg.dtype
+    if name == "sum":
+        if t.is_integer or t.kind == "bool":
+            rt = INT64
+        elif t.is_decimal:
+            rt = T.DECIMAL(min(38, t.precision + 10), t.scale)
+        elif t.is_float:
+            rt = FLOAT64
+        else:
+            raise PlanError(f"sum({t}) is not supported")
+        return AggCall("sum", arg, distinct, rt, flt)
+    if name == "avg":
+        if t.is_decimal:
+            rt = T.DECIMAL(min(38, t.precision + 4), min(38, t.scale + 4))
+        elif t.is_numeric:
+            rt = FLOAT64
+        else:
+            raise PlanError(f"avg({t}) is not supported")
+        return AggCall("avg", arg, distinct, rt, flt)
+    if name in ("min", "max", "first_value"):
+        return AggCall(name if name != "first_value" else "min", arg, distinct, t, flt)
+    if name in ("stddev", "stddev_samp", "stddev_pop", "var", "var_samp", "var_pop"):
+        return AggCall(name, arg, distinct, FLOAT64, flt)
+    if name in ("bool_and", "bool_or"):
+        return AggCall(name, arg, distinct, BOOL, flt)
+    raise NotSupported(f"aggregate {name}")
+
+
+def _parse_interval(s: str, unit: Optional[str]) -> Tuple[int, int]:
+    """'3' month / '1 year' / '90 days' -> (months, days)."""
+    txt = s.strip().lower()
+    parts = txt.split()
+    if unit is None:
+        if len(parts) == 2:
+            txt, unit = parts
+        else:
+            unit = "day"
+    n = int(Decimal(txt.split()[0]))
+    unit = unit.rstrip("s")
+    if unit == "year":
+        return (12 * n, 0)
+    if unit == "month":
+        return (n, 0)
+    if unit == "week":
+        return (0, 7 * n)
+    if unit == "day":
+        return (0, n)
+    raise NotSupported(f"interval unit {unit}")
+
+
+def _date_part_py(days: int, field: str) -> int:
+    d = days_to_date(days)
+    return {"year": d.year, "month": d.month, "day": d.day, "quarter": (d.month - 1) // 3 + 1,
+            "dow": (d.weekday() + 1) % 7, "doy": d.timetuple().tm_yday}[field]
+
+
+def _fold_cast(v: Lit, t: DataType) -> Lit:
+    x = v.value
+    if x is None:
+        return Lit(None, t)
+    src = v.dtype
+    try:
+        if t.is_decimal:
+            if src.is_decimal:
+                ds = t.scale - src.scale
+                return Lit(x * 10**ds if ds >= 0 else _round_div(x, 10**(-ds)), t)
+            if src.is_integer:
+                return Lit(int(x) * 10**t.scale, t)
+            if src.is_float or src.is_string:
+                return Lit(int((Decimal(str(x)) * (10**t.scale)).to_integral_value()), t)
+        if t.is_integer:
+            if src.is_decimal:
+                return Lit(int(Decimal(x) / (10**src.scale)), t)
+            return Lit(int(float(x)) if src.is_string else int(x), t)
+        if t.is_float:
+            if src.is_decimal:
+                return Lit(x / 10**src.scale, t)
+            return Lit(float(x), t)
+        if t.is_string:
+            if src.is_decimal:
+                return Lit(Lit(x, src).sql(), t)
+            if src.kind == "date32":
+                return Lit(str(days_to_date(x)), t)
+            if src.kind == "bool":
+                return Lit("true" if x else "false", t)
+            return Lit(str(x), t)
+        if t.kind == "date32":
+            if src.is_string:
+                return Lit(date_to_days(x), t)
+            return Lit(int(x), t)
+        if t.kind == "bool":
+            if src.is_string:
+                return Lit(x.lower() in ("true", "t", "1", "yes"), t)
+            return Lit(bool(x), t)
+    except (ValueError, ArithmeticError) as e:
+        raise PlanError(f"cannot cast {v.sql()} to {t}") from e
+    return Lit(x, t)
+
+
+def _round_div(a: int, b: int) -> int:
+    q, r = divmod(abs(a), b)
+    if 2 * r >= b:
+        q += 1
+    return q if a >= 0 else -q
+
+
+def _fold(e: Expr) -> Expr:
+    """Constant-fold binary operations on literals."""
+    if not isinstance(e, BinOp) or not isinstance(e.left, Lit) or not isinstance(e.right, Lit):
+        return e
+    a, b = e.left.value, e.right.value
+    op = e.op
+    if op in ("and", "or"):
+        if op == "and":
+            if a is False or b is False:
+                return Lit(False, BOOL)
+            if a is None or b is None:
+                return Lit(None, BOOL)
+            return Lit(True, BOOL)
+        if a is True or b is True:
+            return Lit(True, BOOL)
+        if a is None or b is None:
+            return Lit(None, BOOL)
+        return Lit(False, BOOL)
+    if a is None or b is None:
+        return Lit(None, e.dtype)
+    lt, rt = e.left.dtype, e.right.dtype
+    try:
+        if op in ("=", "<>", "<", "<=", ">", ">="):
+            import operator as o
+            f = {"=": o.eq, "<>": o.ne, "<": o.lt, "<=": o.le, ">": o.gt, ">=": o.ge}[op]
+            return Lit(bool(f(a, b)), BOOL)
+        t = e.dtype
+        if t.is_decimal:
+            if op in ("+", "-"):
+                return Lit(a + b if op == "+" else a - b, t)
+            if op == "*":
+                return Lit(a * b, t)
+            if op == "%":
+                return Lit(int(__import__("math").fmod(a, b)), t)
+        if t.is_float:
+            fa = a / 10**lt.scale if lt.is_decimal else float(a)
+            fb = b / 10**rt.scale if rt.is_decimal else float(b)
+            if op == "+":
+                return Lit(fa + fb, t)
+            if op == "-":
+                return Lit(fa - fb, t)
+            if op == "*":
+                return Lit(fa * fb, t)
+            if op == "/":
+                return Lit(fa / fb if fb != 0 else None, t)
+        if t.is_integer or t.kind == "date32":
+            if op == "+":
+                return Lit(a + b, t)
+            if op == "-":
+                return Lit(a - b, t)
+            if op == "*":
+                return Lit(a * b, t)
+            if op == "/":
+                return Lit(int(a / b) if b != 0 else None, t)
+            if op == "%":
+                return Lit(int(__import__("math").fmod(a, b)) if b != 0 else None, t)
+    except (TypeError, ZeroDivisionError):
+        return e
+    return e
+
+
+_OPS_TXT = {"and": "AND", "or": "OR"}
+
+
+def _ast_text(n: dict) -> str:
+    """Readable column name for an unaliased select expression (DataFusion-like)."""
+    k = n["k"]
+    if k == "col":
+        return ".".join(p["s"] for p in n["c"])
+    if k == "lit":
+        t = n.get("type")
+        if t == "str":
+            return "Utf8(\"" + n["s"] + "\")"
+        if t == "int":
+            return f"Int64({n['s']})"
+        if t == "date":
+            return f"Date32(\"{n['s']}\")"
+        return n["s"]
+    if k == "bin":
+        return f"{_ast_text(n['c'][0])} {_OPS_TXT.get(n['s'], n['s'])} {_ast_text(n['c'][1])}"
+    if k == "paren":
+        return _ast_text(n["c"][0])
+    if k == "func":
+        if n.get("star"):
+            return f"{n['s']}(*)"
+        d = "DISTINCT " if n.get("distinct") else ""
+        return f"{n['s']}({d}{', '.join(_ast_text(c) for c in n['c'])})"
+    if k == "un":
+        return ("NOT " if n["s"] == "not" else "-") + _ast_text(n["c"][0])
+    if k == "cast":
+        return f"CAST({_ast_text(n['c'][0])} AS {n['type']})"
+    if k == "case":
+        return "CASE ... END"
+    if k == "extract":
+        return f"date_part(Utf8(\"{n['s']}\"),{_ast_text(n['c'][0])})"
+    return k

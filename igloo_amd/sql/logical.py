@@ -1,0 +1,292 @@
+"""Logical plan IR.
+
+The reference removed its own logical plan (reference
+crates/engine/src/logical_plan.rs:1 is one comment) and relies on DataFusion's
+``LogicalPlan``; its physical planner only understands TableScan, Projection,
+Filter and Join (reference crates/engine/src/physical_planner.rs:28-138).
+This IR covers the full SELECT surface: scans with pushed filters, projection,
+filter, n-ary inner join groups (ordered adaptively at run time), outer /
+semi / anti joins, hash aggregation, sort, limit, union, values.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from ..types import DataType
+from .expr import AggCall, ColRef, Expr
+
+
+@dataclass
+class ColInfo:
+    cid: int
+    name: str
+    dtype: DataType
+    nullable: bool = True
+    qualifier: Optional[str] = None
+
+    def ref(self) -> ColRef:
+        return ColRef(self.cid, self.name, self.dtype, self.nullable)
+
+
+class Plan:
+    schema: List[ColInfo]
+
+    @property
+    def inputs(self) -> List["Plan"]:
+        return []
+
+    def with_inputs(self, inputs: List["Plan"]) -> "Plan":
+        return self
+
+    def cids(self) -> List[int]:
+        return [c.cid for c in self.schema]
+
+    def col(self, cid: int) -> ColInfo:
+        for c in self.schema:
+            if c.cid == cid:
+                return c
+        raise KeyError(cid)
+
+    def label(self) -> str:
+        return type(self).__name__
+
+    def explain(self, indent: int = 0) -> str:
+        lines = ["  " * indent + self.label()]
+        for i in self.inputs:
+            lines.append(i.explain(indent + 1))
+        return "\n".join(lines)
+
+
+@dataclass(eq=False)
+class Scan(Plan):
+    table: str
+    source: Any                 # catalog TableSource
+    schema: List[ColInfo]       # projected columns (cid, name = source column name)
+    filters: List[Expr] = field(default_factory=list)
+
+    def label(self):
+        f = f" filters=[{', '.join(x.sql() for x in self.filters)}]" if self.filters else ""
+        return f"Scan: {self.table} projection=[{', '.join(c.name for c in self.schema)}]{f}"
+
+
+@dataclass(eq=False)
+class Values(Plan):
+    rows: List[List[Expr]]
+    schema: List[ColInfo]
+
+    def label(self):
+        return f"Values: {len(self.rows)} rows"
+
+
+@dataclass(eq=False)
+class Filter(Plan):
+    input: Plan
+    pred: Expr
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return self.input.schema
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Filter(inputs[0], self.pred)
+
+    def label(self):
+        return f"Filter: {self.pred.sql()}"
+
+
+@dataclass(eq=False)
+class Project(Plan):
+    input: Plan
+    exprs: List[Tuple[ColInfo, Expr]]
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return [c for c, _ in self.exprs]
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Project(inputs[0], self.exprs)
+
+    def label(self):
+        return "Projection: " + ", ".join(
+            e.sql() if isinstance(e, ColRef) and e.cid == c.cid else f"{e.sql()} AS {c.name}#{c.cid}"
+            for c, e in self.exprs)
+
+
+JOIN_KINDS = ("inner", "left", "right", "full", "semi", "anti", "cross")
+
+
+@dataclass(eq=False)
+class Join(Plan):
+    left: Plan
+    right: Plan
+    kind: str
+    on: List[Tuple[Expr, Expr]] = field(default_factory=list)   # equi keys (left expr, right expr)
+    residual: Optional[Expr] = None                              # extra ON condition
+    null_aware: bool = False                                     # NOT IN semantics for anti joins
+
+    @property
+    def schema(self):  # type: ignore[override]
+        if self.kind in ("semi", "anti"):
+            return self.left.schema
+        ls = self.left.schema
+        rs = self.right.schema
+        if self.kind in ("right", "full"):
+            ls = [ColInfo(c.cid, c.name, c.dtype, True, c.qualifier) for c in ls]
+        if self.kind in ("left", "full"):
+            rs = [ColInfo(c.cid, c.name, c.dtype, True, c.qualifier) for c in rs]
+        return ls + rs
+
+    @property
+    def inputs(self):
+        return [self.left, self.right]
+
+    def with_inputs(self, inputs):
+        return Join(inputs[0], inputs[1], self.kind, self.on, self.residual, self.null_aware)
+
+    def label(self):
+        on = ", ".join(f"{a.sql()} = {b.sql()}" for a, b in self.on)
+        r = f" filter={self.residual.sql()}" if self.residual is not None else ""
+        return f"Join({self.kind}): on=[{on}]{r}"
+
+
+@dataclass(eq=False)
+class MultiJoin(Plan):
+    """N-ary inner join; the executor picks the join order from actual sizes."""
+    children: List[Plan]
+    conds: List[Expr]  # conjuncts: equi predicates a = b across inputs + residuals
+
+    @property
+    def schema(self):  # type: ignore[override]
+        out = []
+        for c in self.children:
+            out += c.schema
+        return out
+
+    @property
+    def inputs(self):
+        return list(self.children)
+
+    def with_inputs(self, inputs):
+        return MultiJoin(list(inputs), self.conds)
+
+    def label(self):
+        return f"MultiJoin: {len(self.children)} inputs, conds=[{', '.join(c.sql() for c in self.conds)}]"
+
+
+@dataclass(eq=False)
+class Aggregate(Plan):
+    input: Plan
+    groups: List[Tuple[ColInfo, Expr]]
+    aggs: List[Tuple[ColInfo, AggCall]]
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return [c for c, _ in self.groups] + [c for c, _ in self.aggs]
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Aggregate(inputs[0], self.groups, self.aggs)
+
+    def label(self):
+        g = ", ".join(e.sql() for _, e in self.groups)
+        a = ", ".join(f"{e.sql()} AS {c.name}#{c.cid}" for c, e in self.aggs)
+        return f"Aggregate: groupBy=[{g}], aggr=[{a}]"
+
+
+@dataclass(eq=False)
+class Sort(Plan):
+    input: Plan
+    keys: List[Tuple[Expr, bool, bool]]  # (expr, ascending, nulls_first)
+    fetch: Optional[int] = None          # top-k when a LIMIT sits above
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return self.input.schema
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Sort(inputs[0], self.keys, self.fetch)
+
+    def label(self):
+        k = ", ".join(f"{e.sql()} {'ASC' if a else 'DESC'} NULLS {'FIRST' if nf else 'LAST'}" for e, a, nf in self.keys)
+        f = f", fetch={self.fetch}" if self.fetch is not None else ""
+        return f"Sort: {k}{f}"
+
+
+@dataclass(eq=False)
+class Limit(Plan):
+    input: Plan
+    limit: Optional[int]
+    offset: int = 0
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return self.input.schema
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Limit(inputs[0], self.limit, self.offset)
+
+    def label(self):
+        return f"Limit: skip={self.offset}, fetch={self.limit}"
+
+
+@dataclass(eq=False)
+class Union(Plan):
+    children: List[Plan]
+    schema: List[ColInfo]
+
+    @property
+    def inputs(self):
+        return list(self.children)
+
+    def with_inputs(self, inputs):
+        return Union(list(inputs), self.schema)
+
+    def label(self):
+        return "Union"
+
+
+def transform_plan(p: Plan, fn) -> Plan:
+    """Bottom-up plan rewrite."""
+    ins = p.inputs
+    if ins:
+        new = [transform_plan(i, fn) for i in ins]
+        if any(a is not b for a, b in zip(new, ins)):
+            p = p.with_inputs(new)
+    r = fn(p)
+    return p if r is None else r
+
+
+def walk_plan(p: Plan):
+    yield p
+    for i in p.inputs:
+        yield from walk_plan(i)
+
+
+def produced_cids(p: Plan) -> set:
+    """All column ids defined anywhere inside ``p`` (for correlation analysis)."""
+    out = set()
+    for n in walk_plan(p):
+        out.update(c.cid for c in n.schema)
+        if isinstance(n, Project):
+            out.update(c.cid for c, _ in n.exprs)
+    return out
