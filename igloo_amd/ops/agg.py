@@ -73,7 +73,10 @@ def _gpu(gid, ngroups, specs, n, device) -> List[torch.Tensor]:
         if op == "sum_int":
             outs.append(_wide_to_result(dst, dst2))
         elif op in ("min_f64", "max_f64"):
-            outs.append(_ordered_to_f64(dst))
+            # empty groups keep the int64 sentinel: report +/-inf like the CPU path
+            sentinel = I64_MAX if op == "min_f64" else I64_MIN
+            inf = float("inf") if op == "min_f64" else float("-inf")
+            outs.append(torch.where(dst == sentinel, torch.full_like(dst, 0).double() + inf, _ordered_to_f64(dst)))
         else:
             outs.append(dst)
     return outs

@@ -151,9 +151,15 @@ def _dict_transform(col: Column, fn) -> Column:
 
 
 def _host_roundtrip(col: Column, fn_arrow) -> Column:
-    arr = fn_arrow(col.to_arrow())
-    c = Column.from_arrow(arr, device=col.device, dict_encode=False)
-    return c
+    arr = col.to_arrow()
+    if fn_arrow in (pc.utf8_upper, pc.utf8_lower) and not pc.all(pc.string_is_ascii(arr)).as_py():
+        # full Unicode case mapping with Rust/Python semantics ('ß' -> 'SS'),
+        # which is what the reference's String::to_uppercase produces
+        f = str.upper if fn_arrow is pc.utf8_upper else str.lower
+        arr = pa.array([None if v is None else f(v) for v in arr.to_pylist()], pa.large_string())
+    else:
+        arr = fn_arrow(arr)
+    return Column.from_arrow(arr, device=col.device, dict_encode=False)
 
 
 def upper(col: Column) -> Column:

@@ -1,0 +1,187 @@
+"""Numerics of every gfx950 kernel vs the CPU reference implementation of the
+same op (torch / pyarrow on the host). Runs on a real MI355X."""
+import numpy as np
+import pyarrow as pa
+import pytest
+import torch
+
+from igloo_amd import types as T
+from igloo_amd.columnar import Column
+from igloo_amd.ops import agg as A
+from igloo_amd.ops import hashing as H
+from igloo_amd.ops import misc as M
+from igloo_amd.ops import strings as S
+from igloo_amd.ops.gather import take_many
+from igloo_amd.ops.select import exclusive_scan, mask_to_indices
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rng(seed=0):
+    return np.random.default_rng(seed)
+
+
+@pytest.mark.parametrize("n", [0, 1, 17, 4096, 4097, 1_000_003])
+def test_select(gpu_device, n):
+    m = torch.from_numpy(_rng(n).random(n) < 0.3)
+    ref = mask_to_indices(m)
+    got = mask_to_indices(m.to(DEV)).cpu()
+    assert got.dtype == ref.dtype and torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("n,dt", [(0, torch.int32), (5, torch.int32), (100_001, torch.int64), (3_000_000, torch.int32)])
+def test_exclusive_scan(gpu_device, n, dt):
+    c = torch.from_numpy(_rng(1).integers(0, 9, n)).to(dt)
+    ref, rt = exclusive_scan(c)
+    got, gt = exclusive_scan(c.to(DEV))
+    assert rt == gt and torch.equal(got.cpu(), ref)
+
+
+def test_take_many_fixed_strings_nulls(gpu_device):
+    r = _rng(2)
+    n = 50_000
+    vals = r.integers(-10**12, 10**12, n)
+    strs = pa.array([None if i % 7 == 0 else "s" * (i % 13) + str(i) for i in range(n)], pa.large_string())
+    cols = [Column(T.INT64, torch.from_numpy(vals)), Column.from_arrow(strs, dict_encode=False),
+            Column(T.DATE32, torch.from_numpy(r.integers(0, 20000, n).astype(np.int32)),
+                   torch.from_numpy(r.random(n) < 0.9))]
+    idx = torch.from_numpy(r.integers(-1, n, 123_457).astype(np.int32))
+    ref = take_many(cols, idx, neg=True)
+    got = take_many([c.to(DEV) for c in cols], idx.to(DEV), neg=True)
+    for a, b in zip(ref, got):
+        assert a.to_arrow().equals(b.to_arrow())
+
+
+@pytest.mark.parametrize("dense", [True, False])
+@pytest.mark.parametrize("dups", [False, True])
+def test_join_table(gpu_device, dense, dups):
+    r = _rng(3)
+    nb = 200_000
+    span = nb if dense else 10**15
+    bk = torch.from_numpy(r.choice(span, nb, replace=dups).astype(np.int64))
+    pk = torch.cat([bk[: nb // 2], torch.from_numpy(r.integers(0, span, 300_000))])
+    bvalid = torch.from_numpy(r.random(nb) < 0.95)
+    cpu = H.JoinTable(bk, bvalid)
+    gpu = H.JoinTable(bk.to(DEV), bvalid.to(DEV))
+    assert cpu.unique == gpu.unique
+    assert gpu.direct == dense
+    rp, rb, rc = cpu.probe_pairs(pk)
+    gp, gb, gc = gpu.probe_pairs(pk.to(DEV))
+    assert torch.equal(rc, gc.cpu())
+    a = sorted(zip(rp.tolist(), rb.tolist()))
+    b = sorted(zip(gp.cpu().tolist(), gb.cpu().tolist()))
+    assert a == b
+    fm = gpu.probe_first(pk.to(DEV)).cpu()
+    assert torch.equal(fm >= 0, rc > 0)
+    ok = fm >= 0
+    assert torch.equal(bk[fm[ok].long()], pk[ok])
+
+
+@pytest.mark.parametrize("card", [1, 6, 1000, 3_000_000])
+def test_group_ids(gpu_device, card):
+    r = _rng(4)
+    n = 2_000_000
+    keys = torch.from_numpy(r.integers(0, card, n) * (1 if card < 10**4 else 7919))
+    g, ng, rep = H.group_ids(keys.to(DEV))
+    rg, rng_, rrep = H.group_ids(keys)
+    assert ng == rng_
+    g, rep = g.cpu().long(), rep.cpu().long()
+    # same partition of rows: group of each row's key identical up to relabeling
+    assert torch.equal(keys[rep][g], keys)
+    assert torch.unique(keys[rep]).numel() == ng
+    # representative is the first occurrence
+    first = torch.full((ng,), n, dtype=torch.int64).scatter_reduce(0, g, torch.arange(n), reduce="amin")
+    assert torch.equal(first, rep)
+
+
+@pytest.mark.parametrize("ngroups", [1, 4, 300, 100_000])
+def test_grouped_aggregate(gpu_device, ngroups):
+    r = _rng(5)
+    n = 1_000_000
+    gid = torch.from_numpy(r.integers(0, ngroups, n).astype(np.int32))
+    iv = torch.from_numpy(r.integers(-(2**40), 2**40, n))
+    i32 = torch.from_numpy(r.integers(-1000, 1000, n).astype(np.int32))
+    fv = torch.from_numpy(r.standard_normal(n))
+    valid = torch.from_numpy(r.random(n) < 0.8)
+    specs = [("sum_int", iv, None), ("sum_int", i32, valid), ("count", None, None), ("count", None, valid),
+             ("min_int", iv, valid), ("max_int", i32, None), ("min_f64", fv, None), ("max_f64", fv, valid)]
+    ref = A.grouped_aggregate(gid, ngroups, specs, n, "cpu")
+    got = A.grouped_aggregate(gid.to(DEV), ngroups, [(o, None if v is None else v.to(DEV), None if m is None else m.to(DEV))
+                                                    for o, v, m in specs], n, DEV)
+    for (op, _, _), a, b in zip(specs, ref, got):
+        assert torch.equal(a, b.cpu()), op
+    # sum_f64 with tolerance (atomic order differs)
+    fs = A.grouped_aggregate(gid.to(DEV), ngroups, [("sum_f64", fv.to(DEV), None)], n, DEV)[0].cpu()
+    fr = A.grouped_aggregate(gid, ngroups, [("sum_f64", fv, None)], n, "cpu")[0]
+    assert torch.allclose(fs, fr, rtol=1e-9, atol=1e-6)
+
+
+def test_sum_int128_overflow(gpu_device):
+    n = 100_000
+    v = torch.full((n,), 2**62, dtype=torch.int64)
+    gid = torch.zeros(n, dtype=torch.int32)
+    got = A.grouped_aggregate(gid.to(DEV), 3, [("sum_int", v.to(DEV), None)], n, DEV)[0]
+    assert A.wide_to_python(got)[0] == n * 2**62
+
+
+def _str_col(vals, dict_encode=False):
+    return Column.from_arrow(pa.array(vals, pa.large_string()), dict_encode=dict_encode)
+
+
+WORDS = ["special", "requests", "forest green", "PROMO BRUSHED", "Customer xx Complaints", "", "a_b%c", "ünïcode"]
+
+
+def _words(n, seed=6):
+    r = _rng(seed)
+    return [" ".join(r.choice(WORDS, r.integers(0, 5))) for _ in range(n)]
+
+
+@pytest.mark.parametrize("pat", ["%special%requests%", "forest%", "%BRASS", "%", "", "_", "a\\_b\\%c%", "%n_c%",
+                                 "%Customer%Complaints%"])
+def test_like(gpu_device, pat):
+    vals = _words(20_000)
+    c = _str_col(vals)
+    ref = S.like(c, pat)
+    got = S.like(c.to(DEV), pat).cpu()
+    assert torch.equal(ref, got)
+
+
+def test_string_transforms(gpu_device):
+    vals = [w.replace("ü", "u").replace("ï", "i") for w in _words(30_000, 7)]
+    c = _str_col(vals)
+    g = c.to(DEV)
+    assert S.upper(g).to_arrow().equals(S.upper(c).to_arrow())
+    for start, ln in [(1, 2), (3, None), (0, 3), (5, 0), (-2, 4)]:
+        assert S.substr(g, start, ln).to_pylist() == S.substr(c, start, ln).to_pylist()
+    for op in ["=", "<>", "<", ">="]:
+        assert torch.equal(S.compare_const(g, op, "requests").cpu(), S.compare_const(c, op, "requests"))
+
+
+def test_upper_unicode_falls_back_exactly(gpu_device):
+    c = _str_col(["straße", "abc", None, "ÄÖü"])
+    assert S.upper(c.to(DEV)).to_pylist() == ["STRASSE", "ABC", None, "ÄÖÜ"]
+
+
+def test_dict_encode(gpu_device):
+    vals = _words(50_000, 8)
+    c = _str_col(vals).to(DEV)
+    d = S.dict_encode(c)
+    assert d.is_dict
+    assert d.to_pylist() == vals
+    assert len(d.dictionary) == len(set(vals))
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_hash_partition(gpu_device, nparts):
+    keys = torch.from_numpy(_rng(9).integers(0, 10**9, 777_777))
+    perm, counts = M.hash_partition(keys.to(DEV), nparts)
+    rperm, rcounts = M.hash_partition(keys, nparts)
+    assert counts == rcounts
+    assert torch.equal(perm.cpu().long(), rperm.long())
+
+
+def test_date_part(gpu_device):
+    d = torch.from_numpy(_rng(10).integers(-30000, 40000, 100_000).astype(np.int32))
+    for f in ["year", "month", "day", "quarter", "dow", "doy"]:
+        assert torch.equal(M.date_part(d.to(DEV), f).cpu(), M.date_part(d, f)), f

@@ -1,0 +1,41 @@
+"""TPC-H on the GPU (gfx950 kernels) vs the CPU engine and the sqlite oracle."""
+import pytest
+
+from igloo_amd.models.tpch import oracle, queries
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tpch_gpu(gpu_device):
+    import igloo_amd as ig
+    from igloo_amd.models.tpch import datagen
+    e = ig.QueryEngine(device=gpu_device)
+    tabs = datagen.register(e, 0.01)
+    return e, tabs
+
+
+def test_gpu_datagen_matches_cpu(tpch_gpu, tpch_cpu):
+    _, gt = tpch_gpu
+    _, ct, _ = tpch_cpu
+    for name in ct:
+        for col in ct[name].columns:
+            a = ct[name].columns[col].to_arrow()
+            b = gt[name].columns[col].to_arrow()
+            assert a.equals(b), f"{name}.{col} differs between CPU and GPU generation"
+
+
+@pytest.mark.parametrize("q", list(range(1, 23)))
+def test_tpch_gpu_query(tpch_gpu, tpch_cpu, q):
+    e, _ = tpch_gpu
+    _, _, con = tpch_cpu
+    got = [tuple(r.values()) for r in e.sql(queries.QUERIES[q]).table.to_pylist()]
+    exp = oracle.run_sqlite(con, q)
+    diff = oracle.rows_match(got, exp)
+    assert not diff, f"Q{q}: {diff}"
+
+
+def test_native_kernels_were_used(tpch_gpu):
+    from igloo_amd.ops._lib import KERNEL_CALLS
+    for k in ("select", "join_build", "join_probe", "groupby", "agg_update", "gather_multi"):
+        assert KERNEL_CALLS[k] > 0, f"{k} never launched: {dict(KERNEL_CALLS)}"
