@@ -260,9 +260,11 @@ def _decimal_to_int64(arr: pa.Array) -> np.ndarray:
 class Batch:
     """An ordered set of equally long columns keyed by column id (or name)."""
 
-    __slots__ = ("columns", "num_rows")
+    __slots__ = ("columns", "num_rows", "dist", "out_dist")
 
-    def __init__(self, columns: Dict[Any, Column], num_rows: Optional[int] = None):
+    def __init__(self, columns: Dict[Any, Column], num_rows: Optional[int] = None, dist=None):
+        self.dist = dist          # ("hash", cid) | ("replicated",) | None  (SPMD row placement)
+        self.out_dist = None
         self.columns = dict(columns)
         if num_rows is None:
             num_rows = len(next(iter(self.columns.values()))) if self.columns else 0

@@ -144,14 +144,21 @@ class ScanExec(ExecNode):
         names = [by_cid[cid].name for cid in sorted(need)]
         raw = s.source.scan(names, ctx)
         cols = {cid: raw.columns[by_cid[cid].name] for cid in sorted(need)}
+        dist = None
+        if ctx.world > 1:
+            if getattr(s.source, "replicated", False):
+                dist = ("replicated",)
+            elif getattr(s.source, "partitioned_by", None):
+                pc = [c.cid for c in table_cols if c.name == s.source.partitioned_by]
+                dist = ("hash", pc[0]) if pc else None
         b = Batch(cols, raw.num_rows)
         if s.filters:
             m = ctx.evaluator.mask(and_all(s.filters), b)
             idx = mask_to_indices(m)
             out_cids = [c.cid for c in s.schema]
             taken = take_many([b.columns[c] for c in out_cids], idx)
-            return Batch(dict(zip(out_cids, taken)), idx.numel())
-        return Batch({c.cid: cols[c.cid] for c in s.schema}, raw.num_rows)
+            return Batch(dict(zip(out_cids, taken)), idx.numel(), dist)
+        return Batch({c.cid: cols[c.cid] for c in s.schema}, raw.num_rows, dist)
 
 
 class ValuesExec(ExecNode):
@@ -169,7 +176,7 @@ class ValuesExec(ExecNode):
                 e = ctx.evaluator.eval(r[j], Batch({}, 1))
                 vals.append(e.value if isinstance(e, Scalar) else e.to_pylist()[0])
             cols[ci.cid] = _column_from_values(vals, ci.dtype, ctx.device)
-        return Batch(cols, n)
+        return Batch(cols, n, ("replicated",) if ctx.world > 1 else None)
 
 
 def _column_from_values(vals, dtype, device) -> Column:
@@ -208,7 +215,7 @@ def filter_batch(b: Batch, pred: Expr, ctx) -> Batch:
         return b
     keys = list(b.columns)
     taken = take_many([b.columns[k] for k in keys], idx)
-    return Batch(dict(zip(keys, taken)), idx.numel())
+    return Batch(dict(zip(keys, taken)), idx.numel(), b.dist)
 
 
 class ProjectExec(ExecNode):
@@ -223,9 +230,12 @@ class ProjectExec(ExecNode):
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
         cols = {}
+        dist = b.dist if (b.dist is None or b.dist[0] == "replicated") else None
         for ci, e in self.logical.exprs:
             cols[ci.cid] = ctx.evaluator.column(e, b)
-        return Batch(cols, b.num_rows)
+            if b.dist and b.dist[0] == "hash" and isinstance(e, ColRef) and e.cid == b.dist[1]:
+                dist = ("hash", ci.cid)
+        return Batch(cols, b.num_rows, dist)
 
 
 # ====================================================================== join keys
@@ -311,6 +321,9 @@ class HashJoinExec(ExecNode):
         if ctx.world > 1:
             from ..parallel.exchange import prepare_join
             lb, rb = prepare_join(lb, rb, j, ctx)
+            out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
+            out.dist = lb.out_dist
+            return out
         return hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
 
 
@@ -531,14 +544,17 @@ class MultiJoinExec(ExecNode):
             conds = [c for c in conds if c not in resid and (not keys or c not in [kk[2] for kk in keys])]
             on = [(kk[0], kk[1]) for kk in keys]
             la, lb_ = a["batch"], b["batch"]
+            out_dist = None
             if ctx.world > 1:
                 from ..parallel.exchange import prepare_join
                 fake = L.Join(None, None, "inner", on)  # type: ignore[arg-type]
                 la, lb_ = prepare_join(la, lb_, fake, ctx)
+                out_dist = la.out_dist
             if on:
                 out = hash_join(la, lb_, "inner", on, and_all(resid), ctx)
             else:
                 out = _nested_loop(la, lb_, "inner", and_all(resid), ctx)
+            out.dist = out_dist
             self.order_log.append(f"{a['name']} ⋈ {b['name']} -> {out.num_rows}")
             merged = {"batch": out, "cids": cids, "ndv": {}, "name": f"({a['name']}⋈{b['name']})"}
             rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
@@ -558,15 +574,15 @@ class MultiJoinExec(ExecNode):
         key = e.sql()
         if key not in rel["ndv"]:
             b = rel["batch"]
-            if b.num_rows == 0:
-                rel["ndv"][key] = 1
-            else:
+            g = 0
+            if b.num_rows:
                 c = ctx.evaluator.column(e, b)
                 k, _ = group_key_tensor(c)
                 _, g, _ = H.group_ids(k)
-                if ctx.world > 1:
-                    g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
-                rel["ndv"][key] = g
+            if ctx.world > 1:
+                # every rank takes part, even with an empty slice (collective order must match)
+                g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
+            rel["ndv"][key] = max(g, 1)
         return rel["ndv"][key]
 
 
@@ -809,7 +825,9 @@ class SortExec(ExecNode):
         if ctx.world > 1:
             from ..parallel.exchange import gather_all
             b = gather_all(b, ctx)
-        return sort_batch(b, self.logical.keys, self.logical.fetch, ctx)
+        out = sort_batch(b, self.logical.keys, self.logical.fetch, ctx)
+        out.dist = b.dist
+        return out
 
 
 def sort_batch(b: Batch, keys, fetch, ctx) -> Batch:
@@ -851,7 +869,9 @@ class LimitExec(ExecNode):
         if lo == 0 and hi == b.num_rows:
             return b
         idx = torch.arange(lo, hi, dtype=torch.int64, device=ctx.device)
-        return _take_batch(b, idx)
+        out = _take_batch(b, idx)
+        out.dist = b.dist
+        return out
 
 
 class UnionExec(ExecNode):
@@ -863,5 +883,16 @@ class UnionExec(ExecNode):
         outs = []
         for ch, p in zip(self.children, self.logical.children):
             b = ch.execute(ctx)
-            outs.append(Batch({s.cid: b.columns[c.cid] for s, c in zip(self.logical.schema, p.schema)}, b.num_rows))
+            outs.append(Batch({s.cid: b.columns[c.cid] for s, c in zip(self.logical.schema, p.schema)}, b.num_rows,
+                              b.dist))
+        if ctx.world > 1:
+            reps = [o.dist == ("replicated",) for o in outs]
+            if all(reps):
+                out = concat_batches(outs)
+                out.dist = ("replicated",)
+                return out
+            if any(reps) and ctx.comm.rank != 0:
+                # a replicated input contributes its rows once (from rank 0)
+                outs = [_take_batch(o, torch.zeros(0, dtype=torch.int32, device=ctx.device)) if r else o
+                        for o, r in zip(outs, reps)]
         return concat_batches(outs)

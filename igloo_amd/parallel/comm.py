@@ -1,0 +1,172 @@
+"""Communicator: one process per GPU, collectives over RCCL (xGMI) via
+``torch.distributed`` ("nccl" backend == RCCL on ROCm), gloo on CPU.
+
+The reference has no collective layer at all — every inter-process call is a
+gRPC/Flight RPC and the shuffle is declared but never implemented (reference
+crates/api/proto/coordinator.proto:50-58 "for shuffle", worker returns empty
+bytes at crates/worker/src/service.rs:26-32). SURVEY §2.5 M5/§5.8.
+
+xGMI is a full mesh of point-to-point links, so data exchanges use
+all-to-all-v (every peer sends directly on its own link) and all-gather-v,
+never ring-style reductions of large buffers; small control values (counts,
+sizes, NDVs) are batched into one tiny all-reduce / all-gather.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..utils.errors import CommError
+from ..utils.log import get_logger
+
+log = get_logger("comm")
+
+
+class Communicator:
+    def __init__(self, rank: int, world_size: int, device, group=None, backend: str = "nccl"):
+        self.rank = rank
+        self.world_size = world_size
+        self.device = torch.device(device)
+        self.group = group
+        self.backend = backend
+        self.bytes_sent = 0
+        self.calls = 0
+
+    # ------------------------------------------------------------- lifecycle
+    @staticmethod
+    def init(backend: Optional[str] = None, device=None, timeout_s: float = 600.0) -> "Communicator":
+        """Initialise from torchrun-style env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
+        rank = int(os.environ.get("RANK", "0"))
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        local = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if device is None:
+            device = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+        device = torch.device(device)
+        if backend is None:
+            backend = "nccl" if device.type == "cuda" else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not dist.is_initialized():
+            kw = {}
+            if device.type == "cuda":
+                torch.cuda.set_device(device)
+                kw["device_id"] = device
+            dist.init_process_group(backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        return Communicator(dist.get_rank(), dist.get_world_size(), device, None, backend)
+
+    def shutdown(self):
+        if dist.is_initialized():
+            try:
+                dist.barrier()
+            except Exception:  # pragma: no cover
+                pass
+            dist.destroy_process_group()
+
+    # ------------------------------------------------------------ primitives
+    def _t(self, x, dtype=torch.int64) -> torch.Tensor:
+        return torch.as_tensor(x, dtype=dtype, device=self.device)
+
+    def barrier(self):
+        if self.world_size > 1:
+            dist.barrier(group=self.group)
+
+    def allreduce_int(self, x: int) -> int:
+        if self.world_size == 1:
+            return int(x)
+        t = self._t([int(x)])
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def allreduce_ints(self, xs: Sequence[int]) -> List[int]:
+        if self.world_size == 1:
+            return [int(x) for x in xs]
+        t = self._t([int(x) for x in xs])
+        dist.all_reduce(t, group=self.group)
+        return [int(v) for v in t.tolist()]
+
+    def allreduce_max_float(self, x: float) -> float:
+        if self.world_size == 1:
+            return float(x)
+        t = self._t([float(x)], torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def allgather_ints(self, xs: Sequence[int]) -> List[List[int]]:
+        """Every rank contributes len(xs) ints; returns [rank][i]."""
+        k = len(xs)
+        if self.world_size == 1:
+            return [list(map(int, xs))]
+        t = self._t([int(x) for x in xs])
+        out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        v = out.tolist()
+        return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
+
+    def allgather_object(self, obj) -> list:
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def all_to_all_v(self, t: torch.Tensor, send_counts: Sequence[int],
+                     recv_counts: Optional[Sequence[int]] = None) -> Tuple[torch.Tensor, List[int]]:
+        """Rows of ``t`` grouped by destination (send_counts[r] rows to rank r)."""
+        W = self.world_size
+        if W == 1:
+            return t, [t.shape[0]]
+        if recv_counts is None:
+            m = self.all_to_all_counts(send_counts)
+            recv_counts = m
+        tail = tuple(t.shape[1:])
+        out = torch.empty((sum(recv_counts),) + tail, dtype=t.dtype, device=t.device)
+        row = 1
+        for d in tail:
+            row *= d
+        src = t.contiguous()
+        if src.dtype == torch.bool:
+            src = src.view(torch.uint8)
+            out = out.view(torch.uint8)
+        dist.all_to_all_single(out, src, list(map(int, recv_counts)), list(map(int, send_counts)), group=self.group)
+        self.calls += 1
+        self.bytes_sent += src.numel() * src.element_size()
+        if t.dtype == torch.bool:
+            out = out.view(torch.bool)
+        return out, list(recv_counts)
+
+    def all_to_all_counts(self, send_counts: Sequence[int]) -> List[int]:
+        W = self.world_size
+        s = self._t(list(send_counts))
+        r = torch.empty(W, dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(r, s, group=self.group)
+        return [int(x) for x in r.tolist()]
+
+    def all_gather_v(self, t: torch.Tensor, counts: Optional[List[int]] = None) -> Tuple[torch.Tensor, List[int]]:
+        """Concatenate every rank's ``t`` (variable row counts) on every rank."""
+        W = self.world_size
+        if W == 1:
+            return t, [t.shape[0]]
+        if counts is None:
+            counts = [c[0] for c in self.allgather_ints([t.shape[0]])]
+        # all-to-all with the same payload to every peer = all-gather-v on a
+        # point-to-point mesh (every peer pulls over its own xGMI link)
+        src = t.contiguous()
+        send = torch.cat([src] * W) if src.numel() else src.reshape((0,) + tuple(src.shape[1:]))
+        out, _ = self.all_to_all_v(send, [src.shape[0]] * W, counts)
+        return out, counts
+
+    def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world_size > 1:
+            dist.broadcast(t, src, group=self.group)
+        return t
+
+
+class LocalComm(Communicator):
+    """World of one (no process group): lets distributed code paths run unchanged."""
+
+    def __init__(self, device="cpu"):
+        super().__init__(0, 1, device, None, "local")

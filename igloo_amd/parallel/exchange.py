@@ -1,0 +1,374 @@
+"""Exchange operators for SPMD execution (one fragment slice per GPU).
+
+Every operator of a query runs on every rank over that rank's slice; rows
+move only at exchanges:
+
+* hash shuffle — stable hash-partition kernel (csrc/kernels/partition.hip)
+  + one RCCL all-to-all-v per column (co-locates join / group keys);
+* broadcast — all-gather-v of the (small) build side of a join (SURVEY §2.4
+  P6: hash-join build side replicated over xGMI);
+* two-phase aggregation — local partial aggregate, shuffle of the (small)
+  partial states by group key, final merge;
+* gather — final results / sort inputs collected on every rank.
+
+Distribution of a Batch is tracked in ``Batch.dist``: ``("hash", cid)`` (rows
+placed by mix64(key) % world), ``("replicated",)`` or ``None`` (arbitrary).
+Every decision is taken from globally reduced values, so all ranks issue the
+same collectives in the same order.
+
+Reference parity: FragmentType::Shuffle and GetDataForTask are declared but
+unimplemented (reference crates/coordinator/src/fragment.rs:12,
+crates/worker/src/service.rs:26-32); the DistributedPlanner places whole
+tables on workers and runs joins centrally (distributed_planner.rs:44-92).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+import torch
+
+from .. import types as T
+from ..columnar import Batch, Column
+from ..ops import misc as M
+from ..ops import strings as S
+from ..ops.gather import take_many
+from ..sql import logical as L
+from ..sql.expr import AggCall, ColRef, Expr
+from ..utils.errors import NotSupported
+from ..utils.log import get_logger
+
+log = get_logger("exchange")
+REPLICATED = ("replicated",)
+DEFAULT_BROADCAST_ROWS = 4_000_000
+
+
+def dist_of(b: Batch):
+    return getattr(b, "dist", None)
+
+
+def with_dist(b: Batch, d) -> Batch:
+    b.dist = d
+    return b
+
+
+# ------------------------------------------------------------------ key hashing
+def partition_keys(c: Column) -> torch.Tensor:
+    """Int64 per row whose mix64 decides the destination; identical for equal
+    SQL values whatever the column representation (plain / dictionary)."""
+    if c.dtype.is_string:
+        if c.is_dict:
+            dh = S.hash64(c.dictionary)
+            k = dh.index_select(0, c.data.long())
+        else:
+            k = S.hash64(c)
+        if c.valid is not None:
+            k = torch.where(c.valid, k, torch.zeros_like(k))
+        return k.contiguous()
+    x = c.data
+    if x.dtype in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+        x = torch.where(x == 0, torch.zeros_like(x), x).view(torch.int64)
+    elif x.dim() == 2:
+        x = x[:, 0]
+    elif x.dtype != torch.int64 and x.dtype != torch.int32:
+        x = x.to(torch.int64)
+    if c.valid is not None:
+        x = torch.where(c.valid, x, torch.zeros_like(x))
+    return x.contiguous()
+
+
+# -------------------------------------------------------------- dictionary sync
+_DICT_OK: Dict[int, object] = {}
+
+
+def unify_dictionary(c: Column, comm) -> Column:
+    """Make a dictionary column's codes meaningful on every rank."""
+    key = id(c.dictionary)
+    if _DICT_OK.get(key) is c.dictionary:
+        flag = 1
+    else:
+        flag = 0
+    flags = comm.allgather_ints([flag])
+    if all(f[0] == 1 for f in flags):
+        return c
+    vals = c.dict_values()
+    every = comm.allgather_object(vals)
+    if all(v == every[0] for v in every):
+        _DICT_OK[key] = c.dictionary
+        return c
+    union, index = [], {}
+    for vs in every:
+        for v in vs:
+            if v not in index:
+                index[v] = len(union)
+                union.append(v)
+    remap = torch.tensor([index[v] for v in vals] or [0], dtype=torch.int32, device=c.device)
+    codes = remap.index_select(0, c.data.long()) if len(vals) else c.data
+    d = Column.from_arrow(pa.array(union, pa.large_string()), device=c.device, dict_encode=False)
+    out = Column(T.UTF8, codes, c.valid, dictionary=d)
+    _DICT_OK[id(d)] = d
+    return out
+
+
+# ------------------------------------------------------ structural agreement
+def _sig(c: Column) -> tuple:
+    return (c.valid is not None, c.is_dict, c.is_plain_string, c.is_wide)
+
+
+def normalize_structure(b: Batch, comm) -> Batch:
+    """Make every rank's columns structurally identical (validity present,
+    dictionary vs plain strings, 64- vs 128-bit decimals) so the per-column
+    collectives that follow line up across ranks."""
+    keys = list(b.columns)
+    if not keys:
+        return b
+    bits = [sum(int(f) << i for i, f in enumerate(_sig(b.columns[k]))) for k in keys]
+    sigs = comm.allgather_ints(bits)  # one tiny all-gather for all columns
+    if all(s == sigs[0] for s in sigs):
+        return b
+    out = {}
+    for j, k in enumerate(keys):
+        c = b.columns[k]
+        any_valid = any(s[j] & 1 for s in sigs)
+        any_plain = any(s[j] & 4 for s in sigs)
+        any_wide = any(s[j] & 8 for s in sigs)
+        if any_plain and c.is_dict:
+            c = S.decode(c)
+        if any_wide and not c.is_wide and c.dtype.is_decimal:
+            c = Column(c.dtype, torch.stack([c.data, c.data >> 63], 1), c.valid)
+        if any_valid and c.valid is None:
+            c = Column(c.dtype, c.data, torch.ones(len(c), dtype=torch.bool, device=c.device), c.offsets, c.dictionary)
+        out[k] = c
+    return Batch(out, b.num_rows, b.dist)
+
+
+# --------------------------------------------------------------------- shuffle
+def _exchange_column(c: Column, send: List[int], recv: List[int], comm) -> Column:
+    valid = None
+    if c.valid is not None:
+        valid, _ = comm.all_to_all_v(c.valid, send, recv)
+    if c.is_plain_string:
+        lens = (c.offsets[1:] - c.offsets[:-1]).contiguous()
+        rlens, _ = comm.all_to_all_v(lens, send, recv)
+        # bytes per destination = sum of row lengths in each destination range
+        bounds = np.cumsum([0] + list(send))
+        offs = c.offsets.index_select(0, torch.as_tensor(bounds, device=c.device)).tolist()
+        bsend = [offs[i + 1] - offs[i] for i in range(len(send))]
+        chars, _ = comm.all_to_all_v(c.data, bsend)
+        off = torch.zeros(rlens.numel() + 1, dtype=torch.int64, device=c.device)
+        off[1:] = torch.cumsum(rlens, 0)
+        return Column(c.dtype, chars, valid, offsets=off)
+    if c.is_dict:
+        c = unify_dictionary(c, comm)
+        codes, _ = comm.all_to_all_v(c.data, send, recv)
+        return Column(c.dtype, codes, valid, dictionary=c.dictionary)
+    data, _ = comm.all_to_all_v(c.data, send, recv)
+    return Column(c.dtype, data, valid, dictionary=c.dictionary)
+
+
+def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
+    """Hash-repartition rows of ``b`` by ``key`` across all ranks."""
+    comm = ctx.comm
+    W = comm.world_size
+    b = normalize_structure(b, comm)
+    perm, send = M.hash_partition(key, W)
+    keys = list(b.columns)
+    cols = take_many([b.columns[k] for k in keys], perm) if keys else []
+    recv = comm.all_to_all_counts(send)
+    out = {k: _exchange_column(c, send, recv, comm) for k, c in zip(keys, cols)}
+    return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
+
+
+def _gather_column(c: Column, counts: List[int], comm) -> Column:
+    valid = None
+    if c.valid is not None:
+        valid, _ = comm.all_gather_v(c.valid, counts)
+    if c.is_plain_string:
+        lens = (c.offsets[1:] - c.offsets[:-1]).contiguous()
+        rl, _ = comm.all_gather_v(lens, counts)
+        chars, _ = comm.all_gather_v(c.data)
+        off = torch.zeros(rl.numel() + 1, dtype=torch.int64, device=c.device)
+        off[1:] = torch.cumsum(rl, 0)
+        return Column(c.dtype, chars, valid, offsets=off)
+    if c.is_dict:
+        c = unify_dictionary(c, comm)
+        codes, _ = comm.all_gather_v(c.data, counts)
+        return Column(c.dtype, codes, valid, dictionary=c.dictionary)
+    data, _ = comm.all_gather_v(c.data, counts)
+    return Column(c.dtype, data, valid, dictionary=c.dictionary)
+
+
+def gather_all(b: Batch, ctx) -> Batch:
+    """Every rank receives the concatenation of all ranks' rows."""
+    comm = ctx.comm
+    if comm is None or comm.world_size == 1 or dist_of(b) == REPLICATED:
+        return b
+    b = normalize_structure(b, comm)
+    counts = [c[0] for c in comm.allgather_ints([b.num_rows])]
+    keys = list(b.columns)
+    out = {k: _gather_column(b.columns[k], counts, comm) for k in keys}
+    return with_dist(Batch(out, sum(counts)), REPLICATED)
+
+
+# ----------------------------------------------------------------------- joins
+def _cid(e: Expr):
+    return e.cid if isinstance(e, ColRef) else None
+
+
+def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx):
+    """Move rows so the join can run rank-locally; returns (lb, rb) with the
+    output distribution stored in ``lb.out_dist``."""
+    from ..exec.operators import _pair_key
+    comm = ctx.comm
+    kind, on = join.kind, join.on
+    ld, rd = dist_of(lb), dist_of(rb)
+    rep_l, rep_r = ld == REPLICATED, rd == REPLICATED
+    nl, nr = comm.allreduce_ints([lb.num_rows if not rep_l else 0, rb.num_rows if not rep_r else 0])
+    if rep_l:
+        nl = lb.num_rows
+    if rep_r:
+        nr = rb.num_rows
+    limit = int(ctx.engine.session.get("broadcast_rows", DEFAULT_BROADCAST_ROWS)) if ctx.engine else DEFAULT_BROADCAST_ROWS
+
+    def done(l, r, d):
+        l.out_dist = d
+        return l, r
+
+    if rep_l and rep_r:
+        return done(lb, rb, REPLICATED)
+    if on:
+        for le, re_ in on:
+            lc, rc = _cid(le), _cid(re_)
+            if ld and rd and ld[0] == "hash" and rd[0] == "hash" and ld[1] == lc and rd[1] == rc and lc is not None:
+                return done(lb, rb, ld)
+    null_aware = getattr(join, "null_aware", False)
+    if kind in ("inner", "cross"):
+        if rep_r:
+            return done(lb, rb, ld)
+        if rep_l:
+            return done(lb, rb, rd)
+        if not on or min(nl, nr) <= limit:
+            if nr <= nl:
+                return done(lb, gather_all(rb, ctx), ld)
+            return done(gather_all(lb, ctx), rb, rd)
+    if kind in ("left", "semi", "anti"):
+        if rep_r and not rep_l:
+            return done(lb, rb, ld)
+        if (nr <= limit or null_aware or not on) and not rep_l:
+            return done(lb, gather_all(rb, ctx), ld)
+        if rep_l:
+            # preserved side replicated: bring everything together
+            return done(lb, gather_all(rb, ctx), REPLICATED)
+    if not on:
+        return done(gather_all(lb, ctx), gather_all(rb, ctx), REPLICATED)
+    # hash shuffle both sides on the first key pair
+    ev = ctx.evaluator
+    le, re_ = on[0]
+    lcol, rcol = ev.column(le, lb), ev.column(re_, rb)
+    if lcol.dtype.is_string or rcol.dtype.is_string:
+        lk, rk = partition_keys(lcol), partition_keys(rcol)
+    else:
+        lk, rk = _pair_key(lcol, rcol)
+        lk, rk = lk.to(torch.int64).contiguous(), rk.to(torch.int64).contiguous()
+    lc, rc = _cid(le), _cid(re_)
+    if not (ld and ld[0] == "hash" and ld[1] == lc and lc is not None and lcol.dtype == rcol.dtype):
+        lb = shuffle(lb, lk, ctx, lc)
+    if not (rd and rd[0] == "hash" and rd[1] == rc and rc is not None and lcol.dtype == rcol.dtype):
+        rb = shuffle(rb, rk, ctx, rc)
+    return done(lb, rb, ("hash", lc) if lc is not None else None)
+
+
+# ------------------------------------------------------------------ aggregation
+DECOMPOSABLE = {"sum", "count", "min", "max", "avg", "bool_and", "bool_or"}
+
+
+def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx) -> Batch:
+    from ..exec.operators import _avg, aggregate
+    groups, aggs = lg.groups, lg.aggs
+    d = dist_of(b)
+    if d == REPLICATED:
+        return with_dist(aggregate(groups, aggs, b, ctx), REPLICATED)
+    if d and d[0] == "hash":
+        for ci, e in groups:
+            if isinstance(e, ColRef) and e.cid == d[1]:
+                return with_dist(aggregate(groups, aggs, b, ctx), ("hash", ci.cid))
+    ev = ctx.evaluator
+    decomposable = all(a.func in DECOMPOSABLE and not a.distinct for _, a in aggs)
+    if not decomposable:
+        if groups:
+            k = partition_keys(ev.column(groups[0][1], b))
+            sb = shuffle(b, k, ctx)
+            return with_dist(aggregate(groups, aggs, sb, ctx), ("hash", groups[0][0].cid))
+        return with_dist(aggregate(groups, aggs, gather_all(b, ctx), ctx), REPLICATED)
+    # ---- phase 1: partial states
+    from ..sql.binder import IdGen
+    ids = _TmpIds()
+    partial, plan = [], []
+    for ci, a in aggs:
+        if a.func == "avg":
+            st = _sum_type(a.arg.dtype)
+            s_ci = L.ColInfo(ids(), "__ps", st)
+            c_ci = L.ColInfo(ids(), "__pc", T.INT64)
+            partial += [(s_ci, AggCall("sum", a.arg, False, st, a.filter)), (c_ci, AggCall("count", a.arg, False, T.INT64, a.filter))]
+            plan.append(("avg", ci, a, s_ci, c_ci))
+        else:
+            p_ci = L.ColInfo(ids(), "__p", a.dtype)
+            partial.append((p_ci, AggCall(a.func, a.arg, False, a.dtype, a.filter)))
+            plan.append((a.func, ci, a, p_ci, None))
+    pb = aggregate(groups, partial, b, ctx)
+    # ---- exchange partial states
+    if groups:
+        g0 = groups[0][0]
+        rb = shuffle(pb, partition_keys(pb.columns[g0.cid]), ctx, g0.cid)
+    else:
+        rb = gather_all(pb, ctx)
+    # ---- phase 2: merge
+    fgroups = [(ci, ColRef(ci.cid, ci.name, ci.dtype, ci.nullable)) for ci, _ in groups]
+    final, post = [], []
+    for func, ci, a, p1, p2 in plan:
+        if func == "avg":
+            fs = L.ColInfo(ids(), "__fs", p1.dtype)
+            fc = L.ColInfo(ids(), "__fc", T.INT64)
+            final += [(fs, AggCall("sum", p1.ref(), False, p1.dtype)), (fc, AggCall("sum", p2.ref(), False, T.INT64))]
+            post.append(("avg", ci, a, fs, fc))
+        elif func == "count":
+            final.append((ci, AggCall("sum", p1.ref(), False, T.INT64)))
+            post.append(("count", ci, a, None, None))
+        else:
+            merge = {"sum": "sum", "min": "min", "max": "max", "bool_and": "bool_and", "bool_or": "bool_or"}[func]
+            final.append((ci, AggCall(merge, p1.ref(), False, a.dtype)))
+            post.append((func, ci, a, None, None))
+    fb = aggregate(fgroups, final, rb, ctx)
+    out = {ci.cid: fb.columns[ci.cid] for ci, _ in groups}
+    for func, ci, a, fs, fc in post:
+        if func == "avg":
+            s, c = fb.columns[fs.cid], fb.columns[fc.cid]
+            cnt = c.data if c.valid is None else torch.where(c.valid, c.data, torch.zeros_like(c.data))
+            out[ci.cid] = Column(a.dtype, _avg(s.data, cnt, a.arg.dtype, a.dtype), cnt > 0)
+        elif func == "count":
+            c = fb.columns[ci.cid]
+            data = c.data if c.valid is None else torch.where(c.valid, c.data, torch.zeros_like(c.data))
+            out[ci.cid] = Column(T.INT64, data)
+        else:
+            out[ci.cid] = fb.columns[ci.cid]
+    res = Batch(out, fb.num_rows)
+    return with_dist(res, ("hash", groups[0][0].cid) if groups else REPLICATED)
+
+
+def _sum_type(t):
+    if t.is_decimal:
+        return T.DECIMAL(min(38, t.precision + 10), t.scale)
+    if t.is_float:
+        return T.FLOAT64
+    return T.INT64
+
+
+class _TmpIds:
+    """Temporary column ids for partial states (negative: never collide with binder ids)."""
+    _n = 0
+
+    def __call__(self) -> int:
+        _TmpIds._n -= 1
+        return _TmpIds._n
