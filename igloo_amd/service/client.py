@@ -1,0 +1,123 @@
+"""Flight client (reference crates/client is a println! placeholder).
+
+``IglooClient(uri).query(sql)`` plans with GetFlightInfo and streams the
+result with DoGet; ``flight_sql=True`` speaks Flight SQL
+(CommandStatementQuery); ``execute_raw`` sends the SQL as the ticket like the
+reference's do_get. Control-plane helpers wrap the DoAction messages.
+
+CLI: ``python -m igloo_amd.service.client --sql "..." [--uri grpc://host:50051]``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from typing import List, Optional
+
+import pyarrow as pa
+import pyarrow.flight as fl
+
+from . import protocol as P
+
+
+class _Bearer(fl.ClientMiddleware):
+    def __init__(self, token):
+        self.token = token
+
+    def sending_headers(self):
+        return {"authorization": f"Bearer {self.token}"}
+
+
+class _BearerFactory(fl.ClientMiddlewareFactory):
+    def __init__(self, token):
+        self.token = token
+
+    def start_call(self, info):
+        return _Bearer(self.token)
+
+
+class IglooClient:
+    def __init__(self, uri: str = "grpc://127.0.0.1:50051", token: Optional[str] = None, timeout: Optional[float] = None):
+        mw = [_BearerFactory(token)] if token else None
+        self.uri = uri
+        self.client = fl.connect(uri, middleware=mw)
+        self.options = fl.FlightCallOptions(timeout=timeout) if timeout else fl.FlightCallOptions()
+
+    def close(self):
+        self.client.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------- queries
+    def query(self, sql: str, flight_sql: bool = False) -> pa.Table:
+        cmd = P.command_statement_query(sql) if flight_sql else sql.encode()
+        info = self.client.get_flight_info(fl.FlightDescriptor.for_command(cmd), self.options)
+        tables = [self.client.do_get(ep.ticket, self.options).read_all() for ep in info.endpoints]
+        if not tables:
+            return info.schema.empty_table()
+        return pa.concat_tables(tables) if len(tables) > 1 else tables[0]
+
+    def schema(self, sql: str) -> pa.Schema:
+        return self.client.get_flight_info(fl.FlightDescriptor.for_command(sql.encode()), self.options).schema
+
+    def execute_raw(self, sql: str) -> pa.Table:
+        return self.client.do_get(fl.Ticket(sql.encode()), self.options).read_all()
+
+    def upload(self, name: str, table: pa.Table):
+        w, _ = self.client.do_put(fl.FlightDescriptor.for_path(name), table.schema, self.options)
+        w.write_table(table)
+        w.close()
+
+    def tables(self) -> List[str]:
+        return [f.descriptor.path[0].decode() for f in self.client.list_flights(options=self.options)]
+
+    # --------------------------------------------------------- control plane
+    def action(self, kind: str, body: bytes = b"") -> bytes:
+        res = list(self.client.do_action(fl.Action(kind, body), self.options))
+        return res[0].body.to_pybytes() if res else b""
+
+    def register_worker(self, info: P.WorkerInfo) -> P.RegistrationAck:
+        return P.RegistrationAck.from_json(self.action("register_worker", info.to_json()))
+
+    def heartbeat(self, hb: P.HeartbeatInfo) -> P.HeartbeatResponse:
+        return P.HeartbeatResponse.from_json(self.action("heartbeat", hb.to_json()))
+
+    def execute_task(self, td: P.TaskDefinition) -> P.TaskStatus:
+        return P.TaskStatus.from_json(self.action("execute_task", td.to_json()))
+
+    def get_data_for_task(self, task_id: str) -> pa.Table:
+        b = self.action("get_data_for_task", P.DataForTaskRequest(task_id).to_json())
+        return pa.ipc.open_stream(b).read_all()
+
+    def list_workers(self) -> list:
+        return json.loads(self.action("list_workers"))
+
+    def metrics(self) -> dict:
+        return json.loads(self.action("metrics"))
+
+    def explain(self, sql: str) -> str:
+        return self.action("explain", sql.encode()).decode()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="igloo-client")
+    ap.add_argument("--uri", default="grpc://127.0.0.1:50051")
+    ap.add_argument("--sql", "-s", required=False)
+    ap.add_argument("--flight-sql", action="store_true")
+    ap.add_argument("--token", default=None)
+    a = ap.parse_args(argv)
+    print("igloo-client starting up...")
+    if not a.sql:
+        return 0
+    from ..engine import print_batches
+    with IglooClient(a.uri, a.token) as c:
+        print_batches(c.query(a.sql, flight_sql=a.flight_sql))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,195 @@
+"""``igloo-worker``: one process per GPU; a node's processes form one SPMD group.
+
+Parity: reference crates/worker/src/main.rs:13-52 — random uuid id, fixed
+address 127.0.0.1:50052, coordinator URL as positional argv[1], RegisterWorker
+then a heartbeat every 5 s (errors printed, responses ignored), WorkerService
+whose ExecuteTask only prints and answers "SUBMITTED"
+(crates/worker/src/service.rs:10-33).
+
+Here (launched by torchrun, one rank per GPU):
+* every rank binds its GPU, joins the RCCL communicator and holds its hash
+  partition of the tables (from --tpch / --config);
+* rank 0 hosts the group's Flight endpoint, registers the group with the
+  coordinator (GPU inventory of all ranks), heartbeats, re-registers when the
+  coordinator forgets it, and for every query broadcasts the SQL to the other
+  ranks over a gloo control group, so all ranks execute the same SPMD plan;
+  exchanges between ranks go over RCCL/xGMI and rank 0 streams the result.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import sys
+import threading
+import time
+import uuid
+from datetime import timedelta
+from typing import Optional
+
+import pyarrow as pa
+import torch
+
+from ..utils.config import IglooConfig, load_config, register_config_tables
+from ..utils.log import get_logger
+from . import protocol as P
+
+log = get_logger("worker")
+
+
+class WorkerGroup:
+    def __init__(self, engine, comm=None, coordinator: Optional[str] = None, host: str = "127.0.0.1",
+                 port: int = 50052, token: Optional[str] = None, heartbeat_s: float = 5.0):
+        self.engine = engine
+        self.comm = comm
+        self.rank = comm.rank if comm else 0
+        self.world = comm.world_size if comm else 1
+        self.coordinator = coordinator
+        self.token = token
+        self.heartbeat_s = heartbeat_s
+        self.id = str(uuid.uuid4())
+        self.host, self.port = host, port
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self.server = None
+        self.ctrl = None
+        if self.world > 1:
+            import torch.distributed as dist
+            # control messages may wait for hours between queries: a CPU (gloo)
+            # group with a long timeout, separate from the RCCL data group
+            self.ctrl = dist.new_group(backend="gloo", timeout=timedelta(days=7))
+
+    # ---------------------------------------------------------------- SPMD
+    def _bcast(self, obj=None):
+        import torch.distributed as dist
+        box = [obj]
+        dist.broadcast_object_list(box, src=0, group=self.ctrl)
+        return box[0]
+
+    def run_spmd(self, sql: str) -> pa.Table:
+        with self._lock:
+            if self.world > 1:
+                self._bcast(("query", sql))
+            return self.engine.query(sql)
+
+    def follower_loop(self):
+        """Ranks > 0: execute whatever rank 0 broadcasts."""
+        while True:
+            cmd = self._bcast()
+            if cmd[0] == "shutdown":
+                return
+            if cmd[0] == "query":
+                try:
+                    self.engine.query(cmd[1])
+                except Exception as e:  # noqa: BLE001 - rank 0 reports the error to the client
+                    log.warning("rank %d: query failed: %s", self.rank, e)
+
+    # ------------------------------------------------------------- rank 0
+    def devices(self) -> list:
+        info = {"rank": self.rank, "device": str(self.engine.device)}
+        if self.engine.device.type == "cuda":
+            from ..ops._lib import native
+            try:
+                info.update(native().device_info(self.engine.device.index or 0))
+            except Exception:  # noqa: BLE001
+                pass
+        if self.world > 1:
+            return self.comm.allgather_object(info)
+        return [info]
+
+    def start_server(self):
+        from .flight_server import IglooFlightServer
+        self.server = IglooFlightServer(self.engine, f"grpc://{self.host}:{self.port}", runner=self.run_spmd,
+                                        auth_token=self.token)
+        self.port = self.server.port
+        self.address = f"grpc://{self.host}:{self.port}"
+        self.server.start_background(host=self.host)
+
+    def register(self) -> bool:
+        if not self.coordinator:
+            return False
+        from .client import IglooClient
+        try:
+            with IglooClient(self.coordinator, self.token, timeout=10) as c:
+                ack = c.register_worker(P.WorkerInfo(self.id, self.address, self._devices, self.world))
+            log.info("registered with %s: %s", self.coordinator, ack.message)
+            self.heartbeat_s = ack.heartbeat_interval_s or self.heartbeat_s
+            return True
+        except Exception as e:  # noqa: BLE001
+            print(f"failed to register with coordinator {self.coordinator}: {e}", file=sys.stderr)
+            return False
+
+    def heartbeat_loop(self):
+        from .client import IglooClient
+        while not self._stop.wait(self.heartbeat_s):
+            try:
+                with IglooClient(self.coordinator, self.token, timeout=5) as c:
+                    r = c.heartbeat(P.HeartbeatInfo(self.id))
+                if not r.ok:  # coordinator restarted or evicted us
+                    self.register()
+            except Exception as e:  # noqa: BLE001
+                print(f"heartbeat failed: {e}", file=sys.stderr)
+
+    def serve(self):
+        """Blocking: rank 0 serves + heartbeats; other ranks follow."""
+        devs = self.devices()  # collective: every rank
+        if self.rank != 0:
+            self.follower_loop()
+            return
+        self._devices = devs
+        self.start_server()
+        if self.register():
+            threading.Thread(target=self.heartbeat_loop, daemon=True, name="igloo-heartbeat").start()
+        print(f"igloo worker group {self.id} ({self.world} GPU rank(s)) serving on {self.address}", flush=True)
+        signal.signal(signal.SIGINT, lambda *_: self._stop.set())
+        signal.signal(signal.SIGTERM, lambda *_: self._stop.set())
+        self._stop.wait()
+        self.shutdown()
+
+    def shutdown(self):
+        self._stop.set()
+        if self.world > 1 and self.rank == 0:
+            with self._lock:
+                self._bcast(("shutdown",))
+        if self.server is not None:
+            self.server.shutdown()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="igloo-worker")
+    ap.add_argument("coordinator_pos", nargs="?", default=None, help="coordinator URL (reference: argv[1])")
+    ap.add_argument("--coordinator", default=None)
+    ap.add_argument("--host", default=None)
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("-c", "--config", default=None)
+    ap.add_argument("--tpch", type=float, default=None, help="generate this rank's TPC-H partition at SF")
+    ap.add_argument("--device", default=None)
+    a = ap.parse_args(argv)
+    cfg = load_config(a.config, {"worker_host": a.host, "worker_port": a.port, "device": a.device})
+    coord = a.coordinator or a.coordinator_pos or f"grpc://{cfg.coordinator_host}:{cfg.coordinator_port}"
+    coord = coord.replace("http://", "grpc://")
+    import igloo_amd as ig
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = cfg.device or (f"cuda:{local}" if torch.cuda.is_available() else "cpu")
+    comm = None
+    if world > 1:
+        from ..parallel.comm import Communicator
+        comm = Communicator.init(device=device, timeout_s=3600)
+    engine = ig.QueryEngine(device=device, comm=comm)
+    rank = comm.rank if comm else 0
+    if a.tpch:
+        from ..models.tpch import datagen
+        for name, t in datagen.generate(a.tpch, device, rank, world).items():
+            engine.register_table(name, t)
+    register_config_tables(engine, cfg)
+    wg = WorkerGroup(engine, comm, coord, cfg.worker_host, cfg.worker_port + (0 if rank == 0 else 0),
+                     cfg.auth_token, cfg.heartbeat_interval_s)
+    wg.serve()
+    if comm is not None:
+        comm.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
