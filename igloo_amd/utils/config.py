@@ -90,7 +90,8 @@ def register_config_tables(engine, cfg: IglooConfig):
             engine.register_iceberg(name, spec["path"])
         elif fmt == "postgres":
             from ..connectors.postgres import PostgresTable
-            engine.register_table(name, PostgresTable(spec["dsn"], spec.get("table", name), query=spec.get("query")))
+            engine.register_table(name, PostgresTable(spec["dsn"], spec.get("table", name), query=spec.get("query"),
+                                                      version_sql=spec.get("version_sql")))
         elif fmt == "mysql":
             from ..connectors.mysql import MySqlTable
             engine.register_table(name, MySqlTable(spec["dsn"], spec.get("table", name), query=spec.get("query")))
