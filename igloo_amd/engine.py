@@ -257,6 +257,8 @@ class QueryEngine:
             for n in _walk_exec(node):
                 if getattr(n, "order_log", None):
                     txt += "\njoin order: " + " ; ".join(n.order_log)
+            if ctx.spans:
+                txt += "\nphases (inclusive, synchronised):\n" + ctx.span_report()
             rows_p = [txt]
         return QueryResult(pa.table({"plan_type": rows_t, "plan": rows_p}), 0.0)
 

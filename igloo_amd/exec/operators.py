@@ -51,6 +51,15 @@ class ExecContext:
         self.metrics: Dict[int, dict] = {}
         self._subq: Dict[int, object] = {}
         self.evaluator = Evaluator(self)
+        self.spans: Dict[str, list] = {}  # phase -> [total ms, calls] (EXPLAIN ANALYZE only)
+
+    def span(self, name: str):
+        """Time a phase inside an operator (device-synchronised; no-op unless analyzing)."""
+        return _Span(self, name) if self.analyze else _NOSPAN
+
+    def span_report(self) -> str:
+        rows = sorted(self.spans.items(), key=lambda kv: -kv[1][0])
+        return "\n".join(f"  {k:<28} {v[0]:10.3f} ms  x{v[1]}" for k, v in rows)
 
     @property
     def world(self) -> int:
@@ -80,6 +89,35 @@ class ExecContext:
                     v = (v - datetime.date(1970, 1, 1)).days
                 self._subq[key] = v
         return self._subq[key]
+
+
+class _Span:
+    __slots__ = ("ctx", "name", "t0")
+
+    def __init__(self, ctx, name):
+        self.ctx, self.name = ctx, name
+
+    def __enter__(self):
+        _sync(self.ctx)
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        _sync(self.ctx)
+        v = self.ctx.spans.setdefault(self.name, [0.0, 0])
+        v[0] += (time.perf_counter() - self.t0) * 1e3
+        v[1] += 1
+        return False
+
+
+class _NoSpan:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NOSPAN = _NoSpan()
 
 
 def _sync(ctx):
@@ -142,7 +180,8 @@ class ScanExec(ExecNode):
         for f in s.filters:
             need |= col_refs(f)
         names = [by_cid[cid].name for cid in sorted(need)]
-        raw = s.source.scan(names, ctx)
+        with ctx.span("scan.source"):
+            raw = s.source.scan(names, ctx)
         cols = {cid: raw.columns[by_cid[cid].name] for cid in sorted(need)}
         dist = None
         if ctx.world > 1:
@@ -153,10 +192,12 @@ class ScanExec(ExecNode):
                 dist = ("hash", pc[0]) if pc else None
         b = Batch(cols, raw.num_rows)
         if s.filters:
-            m = ctx.evaluator.mask(and_all(s.filters), b)
-            idx = mask_to_indices(m)
+            with ctx.span("scan.filter_eval"):
+                m = ctx.evaluator.mask(and_all(s.filters), b)
+                idx = mask_to_indices(m)
             out_cids = [c.cid for c in s.schema]
-            taken = take_many([b.columns[c] for c in out_cids], idx)
+            with ctx.span("scan.filter_gather"):
+                taken = take_many([b.columns[c] for c in out_cids], idx)
             return Batch(dict(zip(out_cids, taken)), idx.numel(), dist)
         return Batch({c.cid: cols[c.cid] for c in s.schema}, raw.num_rows, dist)
 
@@ -209,12 +250,14 @@ class FilterExec(ExecNode):
 
 
 def filter_batch(b: Batch, pred: Expr, ctx) -> Batch:
-    m = ctx.evaluator.mask(pred, b)
-    idx = mask_to_indices(m)
+    with ctx.span("filter.eval"):
+        m = ctx.evaluator.mask(pred, b)
+        idx = mask_to_indices(m)
     if idx.numel() == b.num_rows:
         return b
     keys = list(b.columns)
-    taken = take_many([b.columns[k] for k in keys], idx)
+    with ctx.span("filter.gather"):
+        taken = take_many([b.columns[k] for k in keys], idx)
     return Batch(dict(zip(keys, taken)), idx.numel(), b.dist)
 
 
@@ -335,9 +378,10 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
         return out
     if kind == "cross" or not on:
         return _nested_loop(lb, rb, kind, residual, ctx)
-    lcols = [ev.column(a, lb) for a, _ in on]
-    rcols = [ev.column(b, rb) for _, b in on]
-    lk, rk, lvalid, rvalid = key_tensors(lcols, rcols)
+    with ctx.span("join.keys"):
+        lcols = [ev.column(a, lb) for a, _ in on]
+        rcols = [ev.column(b, rb) for _, b in on]
+        lk, rk, lvalid, rvalid = key_tensors(lcols, rcols)
     n_l, n_r = lb.num_rows, rb.num_rows
     dev = ctx.device
     # null-aware anti join (NOT IN): a NULL on the build side empties the result
@@ -354,24 +398,33 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
         # build on the smaller side
         out = hash_join(rb, lb, "inner", [(b, a) for a, b in on], None, ctx)
         return out
-    table = H.JoinTable(rk, rvalid)
+    with ctx.span("join.build"):
+        table = H.JoinTable(rk, rvalid)
     if kind in ("semi", "anti") and residual is None:
-        first = table.probe_first(lk, lvalid)
-        m = first >= 0 if kind == "semi" else first < 0
-        return _take_batch(lb, mask_to_indices(m))
+        with ctx.span("join.probe"):
+            first = table.probe_first(lk, lvalid)
+            m = first >= 0 if kind == "semi" else first < 0
+            sel = mask_to_indices(m)
+        with ctx.span("join.gather"):
+            return _take_batch(lb, sel)
     if residual is None and table.unique and kind in ("inner", "left"):
-        first = table.probe_first(lk, lvalid)
-        if kind == "inner":
-            pidx = mask_to_indices(first >= 0)
-            bidx = first.index_select(0, pidx.long())
-            return _combine(lb, rb, pidx, bidx, False)
-        lidx = torch.arange(n_l, dtype=torch.int32, device=dev)
-        return _combine(lb, rb, lidx, first, True)
+        with ctx.span("join.probe"):
+            first = table.probe_first(lk, lvalid)
+            if kind == "inner":
+                pidx = mask_to_indices(first >= 0)
+                bidx = first.index_select(0, pidx.long())
+        with ctx.span("join.gather"):
+            if kind == "inner":
+                return _combine(lb, rb, pidx, bidx, False)
+            lidx = torch.arange(n_l, dtype=torch.int32, device=dev)
+            return _combine(lb, rb, lidx, first, True)
     matched = torch.zeros(n_r, dtype=torch.bool, device=dev) if (kind == "full" and residual is None) else None
-    pidx, bidx, counts = table.probe_pairs(lk, lvalid, matched)
+    with ctx.span("join.probe_pairs"):
+        pidx, bidx, counts = table.probe_pairs(lk, lvalid, matched)
     if residual is not None:
-        pair = _combine(lb, rb, pidx, bidx, False)
-        keep = ev.mask(residual, pair)
+        with ctx.span("join.residual"):
+            pair = _combine(lb, rb, pidx, bidx, False)
+            keep = ev.mask(residual, pair)
         sel = mask_to_indices(keep)
         pidx = pidx.index_select(0, sel.long())
         bidx = bidx.index_select(0, sel.long())
@@ -389,7 +442,8 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
         else:
             return _combine(lb, rb, pidx, bidx, False)
     if kind == "inner":
-        return _combine(lb, rb, pidx, bidx, False)
+        with ctx.span("join.gather"):
+            return _combine(lb, rb, pidx, bidx, False)
     if kind in ("left", "full"):
         # unmatched probe rows get a NULL build side
         miss = mask_to_indices(counts == 0)
@@ -510,16 +564,43 @@ class MultiJoinExec(ExecNode):
         self.children = children
         self.order_log: List[str] = []
 
+    #: a semi join is applied to its input before the join when the subquery
+    #: side has at most this fraction of the input's rows
+    EAGER_SEMI_RATIO = 0.125
+
     def describe(self):
-        return f"{len(self.children)} inputs, conds=[{', '.join(c.sql() for c in self.logical.conds)}]"
+        lg = self.logical
+        extra = f", semi=[{'; '.join(s.sql() for s in lg.semis)}]" if lg.semis else ""
+        return f"{len(lg.children)} inputs, conds=[{', '.join(c.sql() for c in lg.conds)}]{extra}"
+
+    def _semi(self, lb: Batch, rb: Batch, sp, ctx) -> Batch:
+        if ctx.world > 1:
+            from ..parallel.exchange import prepare_join
+            j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
+            lb, rb = prepare_join(lb, rb, j, ctx)
+            out = hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
+            out.dist = lb.out_dist
+            return out
+        return hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
 
     def _run(self, ctx):
+        lg = self.logical
+        nch = len(lg.children)
         rels = []
-        for ch in self.children:
+        for ch in self.children[:nch]:
             b = ch.execute(ctx)
             rels.append({"batch": b, "cids": set(b.columns), "ndv": {}, "name": ch.describe()[:40]})
-        conds = list(self.logical.conds)
         self.order_log = []
+        deferred = []
+        for sp, rex in zip(lg.semis, self.children[nch:]):
+            rb = rex.execute(ctx)
+            tgt = rels[sp.child]
+            if sp.kind == "semi" and _global_rows(rb, ctx) <= self.EAGER_SEMI_RATIO * _global_rows(tgt["batch"], ctx):
+                tgt["batch"] = self._semi(tgt["batch"], rb, sp, ctx)
+                self.order_log.append(f"{sp.kind} pre-filter on {tgt['name']} -> {tgt['batch'].num_rows}")
+            else:
+                deferred.append((sp, rb))
+        conds = list(lg.conds)
         while len(rels) > 1:
             best = None
             for i in range(len(rels)):
@@ -561,6 +642,8 @@ class MultiJoinExec(ExecNode):
         b = rels[0]["batch"]
         if conds:
             b = filter_batch(b, and_all(conds), ctx)
+        for sp, rb in deferred:
+            b = self._semi(b, rb, sp, ctx)
         return b
 
     def _estimate(self, a, b, keys, ctx) -> float:
@@ -576,9 +659,10 @@ class MultiJoinExec(ExecNode):
             b = rel["batch"]
             g = 0
             if b.num_rows:
-                c = ctx.evaluator.column(e, b)
-                k, _ = group_key_tensor(c)
-                _, g, _ = H.group_ids(k)
+                with ctx.span("multijoin.ndv"):
+                    c = ctx.evaluator.column(e, b)
+                    k, _ = group_key_tensor(c)
+                    _, g, _ = H.group_ids(k)
             if ctx.world > 1:
                 # every rank takes part, even with an empty slice (collective order must match)
                 g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
@@ -628,31 +712,37 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
     ev = ctx.evaluator
     n = b.num_rows
     dev = ctx.device
-    gcols = [ev.column(e, b) for _, e in groups]
+    with ctx.span("agg.eval_keys"):
+        gcols = [ev.column(e, b) for _, e in groups]
     if groups:
-        keys, reps_src = [], []
-        for c in gcols:
-            k, src = group_key_tensor(c)
-            keys.append(k)
-            reps_src.append(src)
         if n == 0:
             return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
-        packed = H.pack_keys(keys)
-        gid, ng, rep = H.group_ids(packed)
+        with ctx.span("agg.encode_keys"):
+            keys, reps_src = [], []
+            for c in gcols:
+                k, src = group_key_tensor(c)
+                keys.append(k)
+                reps_src.append(src)
+        with ctx.span("agg.group_ids"):
+            packed = H.pack_keys(keys)
+            gid, ng, rep = H.group_ids(packed)
     else:
         gid, ng, rep = None, 1, None
     out: Dict[int, Column] = {}
     if groups:
-        taken = take_many(reps_src, rep)
+        with ctx.span("agg.take_keys"):
+            taken = take_many(reps_src, rep)
         for (ci, _), c in zip(groups, taken):
             out[ci.cid] = c
     specs, finals = [], []
-    for ci, a in aggs:
-        _plan_agg(ci, a, b, gid, ng, n, ctx, specs, finals)
-    results = A.grouped_aggregate(gid, ng, [s[:3] for s in specs], n, dev) if specs else []
-    for fin in finals:
-        ci, col = fin(results)
-        out[ci.cid] = col
+    with ctx.span("agg.eval_args"):
+        for ci, a in aggs:
+            _plan_agg(ci, a, b, gid, ng, n, ctx, specs, finals)
+    with ctx.span("agg.kernel"):
+        results = A.grouped_aggregate(gid, ng, [s[:3] for s in specs], n, dev) if specs else []
+        for fin in finals:
+            ci, col = fin(results)
+            out[ci.cid] = col
     return Batch(out, ng)
 
 

@@ -26,7 +26,7 @@ def create_physical_plan(p: L.Plan) -> ExecNode:
     if isinstance(p, L.Join):
         return HashJoinExec(p, create_physical_plan(p.left), create_physical_plan(p.right))
     if isinstance(p, L.MultiJoin):
-        return MultiJoinExec(p, [create_physical_plan(c) for c in p.children])
+        return MultiJoinExec(p, [create_physical_plan(c) for c in p.inputs])
     if isinstance(p, L.Aggregate):
         return HashAggExec(p, create_physical_plan(p.input))
     if isinstance(p, L.Sort):

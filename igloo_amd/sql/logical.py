@@ -159,10 +159,29 @@ class Join(Plan):
 
 
 @dataclass(eq=False)
+class SemiSpec:
+    """A semi/anti join whose probe keys all come from ONE MultiJoin input
+    (``child``): the executor may apply it to that input before joining (when
+    the subquery side is small) or to the joined result."""
+    child: int
+    right: Plan
+    kind: str
+    on: List[Tuple[Expr, Expr]]
+    residual: Optional[Expr] = None
+    null_aware: bool = False
+
+    def sql(self) -> str:
+        on = ", ".join(f"{a.sql()} = {b.sql()}" for a, b in self.on)
+        r = f" filter={self.residual.sql()}" if self.residual is not None else ""
+        return f"{self.kind}@{self.child} on=[{on}]{r}"
+
+
+@dataclass(eq=False)
 class MultiJoin(Plan):
     """N-ary inner join; the executor picks the join order from actual sizes."""
     children: List[Plan]
     conds: List[Expr]  # conjuncts: equi predicates a = b across inputs + residuals
+    semis: List[SemiSpec] = field(default_factory=list)
 
     @property
     def schema(self):  # type: ignore[override]
@@ -173,13 +192,16 @@ class MultiJoin(Plan):
 
     @property
     def inputs(self):
-        return list(self.children)
+        return list(self.children) + [s.right for s in self.semis]
 
     def with_inputs(self, inputs):
-        return MultiJoin(list(inputs), self.conds)
+        n = len(self.children)
+        semis = [SemiSpec(s.child, r, s.kind, s.on, s.residual, s.null_aware) for s, r in zip(self.semis, inputs[n:])]
+        return MultiJoin(list(inputs[:n]), self.conds, semis)
 
     def label(self):
-        return f"MultiJoin: {len(self.children)} inputs, conds=[{', '.join(c.sql() for c in self.conds)}]"
+        extra = f", semi=[{'; '.join(s.sql() for s in self.semis)}]" if self.semis else ""
+        return f"MultiJoin: {len(self.children)} inputs, conds=[{', '.join(c.sql() for c in self.conds)}]{extra}"
 
 
 @dataclass(eq=False)

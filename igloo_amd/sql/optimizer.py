@@ -23,14 +23,15 @@ from ..types import BOOL
 from ..utils.errors import NotSupported, PlanError
 from .expr import (AggCall, BinOp, ColRef, Expr, Not, SubqueryExpr, and_all, col_refs, conjuncts, has_subquery,
                    replace_cols, transform, walk)
-from .logical import (Aggregate, ColInfo, Filter, Join, Limit, MultiJoin, Plan, Project, Scan, Sort, Union,
-                      Values, produced_cids, transform_plan, walk_plan)
+from .logical import (Aggregate, ColInfo, Filter, Join, Limit, MultiJoin, Plan, Project, Scan, SemiSpec, Sort,
+                      Union, Values, produced_cids, transform_plan, walk_plan)
 
 
 def optimize(plan: Plan) -> Plan:
     plan = decorrelate(plan)
     plan = push_filters(plan, [])
     plan = transform_plan(plan, _extract_join_keys)
+    plan = transform_plan(plan, _attach_semi_joins)
     plan = prune(plan, set(plan.cids()))
     return plan
 
@@ -401,6 +402,26 @@ def _extract_join_keys(p: Plan):
     return Join(p.left, p.right, p.kind, keys, and_all(resid), p.null_aware)
 
 
+# ============================================================ semi-join placement
+def _attach_semi_joins(p: Plan):
+    """Semi/anti join over a MultiJoin whose probe side only needs one input:
+    record it on the MultiJoin so the executor can filter that input first
+    (e.g. TPC-H Q18: ``o_orderkey IN (<57 keys>)`` shrinks orders before the
+    600M-row lineitem join) or, when the subquery side is large, after the join."""
+    if not (isinstance(p, Join) and p.kind in ("semi", "anti") and isinstance(p.left, MultiJoin)):
+        return None
+    mj = p.left
+    rc = set(p.right.cids())
+    need = _refs([a for a, _ in p.on]) | (_refs([p.residual]) - rc)
+    if not need:
+        return None
+    for i, ch in enumerate(mj.children):
+        if need <= set(ch.cids()):
+            spec = SemiSpec(i, p.right, p.kind, list(p.on), p.residual, p.null_aware)
+            return MultiJoin(mj.children, mj.conds, mj.semis + [spec])
+    return None
+
+
 # ============================================================ column pruning
 def _refs(exprs) -> Set[int]:
     out: Set[int] = set()
@@ -429,7 +450,13 @@ def prune(p: Plan, required: Set[int]) -> Plan:
                     p.kind, p.on, p.residual, p.null_aware)
     if isinstance(p, MultiJoin):
         need = required | _refs(p.conds)
-        return MultiJoin([prune(ch, need & set(ch.cids())) for ch in p.children], p.conds)
+        semis = []
+        for sp in p.semis:
+            rc = set(sp.right.cids())
+            sneed = _refs([x for ab in sp.on for x in ab] + [sp.residual])
+            need |= sneed - rc
+            semis.append(SemiSpec(sp.child, prune(sp.right, sneed & rc), sp.kind, sp.on, sp.residual, sp.null_aware))
+        return MultiJoin([prune(ch, need & set(ch.cids())) for ch in p.children], p.conds, semis)
     if isinstance(p, Aggregate):
         aggs = [(c, a) for c, a in p.aggs if c.cid in required]
         need = _refs([e for _, e in p.groups]) | _refs(a for _, a in aggs)
