@@ -120,6 +120,13 @@ PYBIND11_MODULE(_native, m) {
                       P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<const int64_t>(offsets),
                       P<int32_t>(out_probe), P<int32_t>(out_build), S(s));
   });
+  m.attr("HLL_REGISTERS") = kern::kHllRegisters;
+  m.def("hll_blocks", [](int64_t n) { return kern::hll_blocks(n); });
+  m.def("hll_sketch", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t block_regs, uintptr_t regs,
+                         uintptr_t s) {
+    kern::hll_sketch(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<uint8_t>(block_regs),
+                     P<uint8_t>(regs), S(s));
+  });
   m.def("groupby_build", [](uintptr_t keys, bool key64, int64_t n, uintptr_t tkeys, uintptr_t trow, int64_t cap,
                             int64_t kmin, bool direct, uintptr_t s) {
     kern::groupby_build(P<const void>(keys), key64, n, P<int64_t>(tkeys), P<int32_t>(trow), cap, kmin, direct, S(s));

@@ -25,6 +25,15 @@ int64_t scan_workspace_tiles(int64_t n);
 void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
                     hipStream_t stream);
 
+// ---- sketch.hip --------------------------------------------------------------
+constexpr int kHllBits = 12;
+constexpr int kHllRegisters = 1 << kHllBits;
+constexpr int kHllMaxBlocks = 1024;
+int hll_blocks(int64_t n);
+// block_regs: [hll_blocks(n) x kHllRegisters] workspace; regs: [kHllRegisters] output
+void hll_sketch(const void* keys, bool key64, const uint8_t* valid, int64_t n, uint8_t* block_regs, uint8_t* regs,
+                hipStream_t stream);
+
 // ---- hashtable.hip -----------------------------------------------------------
 void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
                 int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, hipStream_t stream);

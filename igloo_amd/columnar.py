@@ -183,6 +183,11 @@ class Column:
                 validity = pa.array(v, pa.bool_()).buffers()[1]
         dt = self.dtype
         if dt.is_string:
+            if self.dictionary is not None and self.data.is_cuda and len(self.dictionary) > 2 * n + 1024:
+                # small slice of a big dictionary (e.g. top-k rows of a grouped
+                # result): decode on the device, ship only the referenced bytes
+                from .ops.strings import decode
+                return decode(self).to_arrow()
             if self.dictionary is not None:
                 codes = self.data.cpu().numpy().astype(np.int32)
                 dic = self.dictionary.to_arrow()

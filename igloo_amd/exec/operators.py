@@ -32,6 +32,7 @@ from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
+from ..ops._lib import launch, ptr, stream
 from ..ops.gather import take, take_many
 from ..ops.select import mask_to_indices
 from ..sql import logical as L
@@ -654,18 +655,32 @@ class MultiJoinExec(ExecNode):
         return na * nb / max(da, db, 1)
 
     def _ndv(self, rel, e: Expr, ctx) -> int:
+        """NDV of a join key: HyperLogLog sketch on the GPU (one streaming read;
+        rank sketches merge by max, so the distributed estimate is global),
+        exact distinct count on the CPU."""
         key = e.sql()
         if key not in rel["ndv"]:
             b = rel["batch"]
-            g = 0
-            if b.num_rows:
-                with ctx.span("multijoin.ndv"):
-                    c = ctx.evaluator.column(e, b)
-                    k, _ = group_key_tensor(c)
-                    _, g, _ = H.group_ids(k)
-            if ctx.world > 1:
-                # every rank takes part, even with an empty slice (collective order must match)
-                g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
+            with ctx.span("multijoin.ndv"):
+                if ctx.device.type == "cuda":
+                    if b.num_rows:
+                        c = ctx.evaluator.column(e, b)
+                        k, _ = group_key_tensor(c)
+                        regs = H.hll_sketch(k)
+                    else:
+                        regs = torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device)
+                    if ctx.world > 1:
+                        # every rank takes part, even with an empty slice (collective order must match)
+                        regs = ctx.comm.allreduce_max_tensor(regs)
+                    g = int(round(H.hll_estimate(regs)))
+                else:
+                    g = 0
+                    if b.num_rows:
+                        c = ctx.evaluator.column(e, b)
+                        k, _ = group_key_tensor(c)
+                        g = H.ndv(k)
+                    if ctx.world > 1:
+                        g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
             rel["ndv"][key] = max(g, 1)
         return rel["ndv"][key]
 
@@ -717,15 +732,8 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
     if groups:
         if n == 0:
             return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
-        with ctx.span("agg.encode_keys"):
-            keys, reps_src = [], []
-            for c in gcols:
-                k, src = group_key_tensor(c)
-                keys.append(k)
-                reps_src.append(src)
         with ctx.span("agg.group_ids"):
-            packed = H.pack_keys(keys)
-            gid, ng, rep = H.group_ids(packed)
+            gid, ng, rep, reps_src = _encode_groups(gcols, ctx)
     else:
         gid, ng, rep = None, 1, None
     out: Dict[int, Column] = {}
@@ -744,6 +752,56 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
             ci, col = fin(results)
             out[ci.cid] = col
     return Batch(out, ng)
+
+
+def _encode_groups(gcols: List[Column], ctx):
+    """Dense group ids for GROUP BY over ``gcols`` -> (gid, ng, rep_row, rep_source_cols).
+
+    Functional-dependency shortcut (GPU): when plain (non-dictionary) string
+    keys are present, group by the integer key with the widest domain first and
+    verify on the device that every other key is constant within those groups
+    (a row-vs-representative comparison, far cheaper than hashing and
+    dictionary-encoding strings). Keys that pass are dropped from the grouping
+    — the result is identical to grouping by all of them. TPC-H Q10 groups by
+    c_custkey plus six customer attributes: one direct-mapped integer group-by
+    replaces seven encodings."""
+    plain = [i for i, c in enumerate(gcols) if c.dtype.is_string and not c.is_dict]
+    others = [i for i in range(len(gcols)) if i not in plain]
+    keys: Dict[int, torch.Tensor] = {}
+    reps_src: List[Column] = list(gcols)
+    for i in others:
+        keys[i], reps_src[i] = group_key_tensor(gcols[i])
+    needed = list(range(len(gcols)))
+    if plain and others and ctx.device.type == "cuda":
+        spans = {i: H.key_range(keys[i]) for i in others}
+        lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
+        gid, ng, rep = H.group_ids(keys[lead])
+        rr = rep.index_select(0, gid.long())
+        bad = []
+        for i in range(len(gcols)):
+            if i == lead:
+                continue
+            c = gcols[i]
+            if i in plain:
+                m = torch.zeros(1, dtype=torch.int32, device=ctx.device)
+                launch("str_eq_rows").str_eq_rows(ptr(c.offsets), ptr(c.data), 0, ptr(c.offsets), ptr(c.data),
+                                                  ptr(rr), False, len(c), ptr(m), stream(m))
+                m = m.to(torch.int64)[0]
+            else:
+                m = (keys[i] != keys[i].index_select(0, rr)).sum()
+            if c.valid is not None:
+                m = m + (c.valid != c.valid.index_select(0, rr)).sum()
+            bad.append((i, m))
+        counts = torch.stack([m for _, m in bad]).tolist()
+        needed = [lead] + [i for (i, _), cnt in zip(bad, counts) if cnt]
+        if len(needed) == 1:
+            return gid, ng, rep, reps_src
+    for i in plain:
+        if i in needed:
+            keys[i], _ = group_key_tensor(gcols[i])
+    packed = H.pack_keys([keys[i] for i in needed])
+    gid, ng, rep = H.group_ids(packed)
+    return gid, ng, rep, reps_src
 
 
 def _empty_col(t, dev) -> Column:

@@ -244,7 +244,12 @@ def decode(col: Column) -> Column:
     """Dictionary column -> plain column."""
     if not col.is_dict:
         return col
-    c = take(col.dictionary, col.data)
+    if col.valid is not None:
+        # codes under NULL rows are unspecified: never dereference them
+        idx = torch.where(col.valid, col.data, torch.full_like(col.data, -1))
+        c = take(col.dictionary, idx, neg=True)
+    else:
+        c = take(col.dictionary, col.data)
     c.valid = col.valid
     return c
 

@@ -95,6 +95,14 @@ class Communicator:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
+    def allreduce_max_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        """Element-wise max over ranks (in a 32-bit copy: portable across backends)."""
+        if self.world_size == 1:
+            return t
+        w = t.to(torch.int32)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX, group=self.group)
+        return w.to(t.dtype)
+
     def allgather_ints(self, xs: Sequence[int]) -> List[List[int]]:
         """Every rank contributes len(xs) ints; returns [rank][i]."""
         k = len(xs)

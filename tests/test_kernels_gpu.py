@@ -185,3 +185,43 @@ def test_date_part(gpu_device):
     d = torch.from_numpy(_rng(10).integers(-30000, 40000, 100_000).astype(np.int32))
     for f in ["year", "month", "day", "quarter", "dow", "doy"]:
         assert torch.equal(M.date_part(d.to(DEV), f).cpu(), M.date_part(d, f)), f
+
+
+@pytest.mark.parametrize("card,n", [(1, 1000), (50, 100_000), (20_000, 1_000_000), (3_000_000, 6_000_000)])
+def test_hll_ndv(gpu_device, card, n):
+    g = _rng(11)
+    k = torch.from_numpy(g.integers(0, card, n).astype(np.int32)).to(gpu_device)
+    exact = torch.unique(k).numel()
+    est = H.ndv(k)
+    assert abs(est - exact) <= max(2, 0.05 * exact), (est, exact)
+    # int64 keys with NULLs: nulls are not counted
+    k64 = k.to(torch.int64) * 1_000_003
+    valid = k % 2 == 0
+    exact2 = torch.unique(k64[valid]).numel()
+    est2 = H.ndv(k64, valid)
+    assert abs(est2 - exact2) <= max(2, 0.05 * exact2), (est2, exact2)
+
+
+def test_group_by_functional_dependency(gpu_device):
+    """FD shortcut: a string key that is constant per int key is dropped from the
+    grouping; one that is not must still split the groups (and NULLs count)."""
+    import igloo_amd as ig
+    n = 200_000
+    g = _rng(12)
+    k = g.integers(0, 5000, n)
+    dep = np.array([f"name-{x:05d}" for x in k], dtype=object)
+    nodep = dep.copy()
+    nodep[::97] = "other"
+    nullable = dep.copy()
+    nullable[::101] = None
+    t = pa.table({"k": pa.array(k, pa.int64()), "dep": pa.array(dep, pa.large_string()),
+                  "nodep": pa.array(nodep, pa.large_string()), "nl": pa.array(nullable, pa.large_string()),
+                  "v": pa.array(np.ones(n, dtype=np.int64))})
+    res = {}
+    for dev in ("cpu", gpu_device):
+        e = ig.QueryEngine(device=dev)
+        e.register_table("t", t)
+        res[dev] = [e.query(f"SELECT k, {c}, sum(v) AS s FROM t GROUP BY k, {c} ORDER BY k, {c} NULLS FIRST")
+                    .to_pylist() for c in ("dep", "nodep", "nl")]
+    assert res["cpu"] == res[gpu_device]
+    assert len(res["cpu"][1]) > len(res["cpu"][0]) and len(res["cpu"][2]) > len(res["cpu"][0])
