@@ -58,6 +58,55 @@ __global__ __launch_bounds__(kBlock) void like_kernel(const int64_t* __restrict_
   }
 }
 
+// LDS-staged LIKE: a block takes 256 consecutive strings, copies their byte
+// range into LDS with 16-byte coalesced loads, then each lane matches its
+// string out of LDS. The per-lane byte-serial scan of the simple kernel above
+// touches a new 64-byte line every few bytes per lane; staging turns the HBM
+// traffic into one streaming read of the character buffer.
+constexpr int kLikeTileBytes = 24576;
+constexpr int kLikeMaxPattern = 256;
+
+__global__ __launch_bounds__(kBlock) void like_tile_kernel(const int64_t* __restrict__ off,
+                                                          const uint8_t* __restrict__ chars, int64_t n,
+                                                          const uint8_t* __restrict__ pat,
+                                                          const uint8_t* __restrict__ kind, int m, bool ci,
+                                                          bool negate, uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kLikeTileBytes];
+  __shared__ uint8_t spat[kLikeMaxPattern], skind[kLikeMaxPattern];
+  for (int i = threadIdx.x; i < m; i += kBlock) {
+    spat[i] = pat[i];
+    skind[i] = kind[i];
+  }
+  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t i0 = t * kBlock;
+    const int64_t i1 = i0 + kBlock < n ? i0 + kBlock : n;
+    const uintptr_t lo = (uintptr_t)(chars + off[i0]);
+    const uintptr_t hi = (uintptr_t)(chars + off[i1]);
+    const uintptr_t start = lo & ~(uintptr_t)15;       // never below the allocation (>= 256 B aligned)
+    const uintptr_t full_end = hi & ~(uintptr_t)15;    // vector loads stop here; the tail goes bytewise
+    const bool staged = hi - start <= (uintptr_t)kLikeTileBytes;
+    __syncthreads();  // previous tile finished reading buf; pattern visible on the first pass
+    if (staged) {
+      const int64_t nvec = (int64_t)(full_end - start) / 16;
+      for (int64_t v = threadIdx.x; v < nvec; v += kBlock)
+        *(uint4*)(buf + v * 16) = *(const uint4*)(start + v * 16);
+      for (uintptr_t a = full_end + threadIdx.x; a < hi; a += kBlock) buf[a - start] = *(const uint8_t*)a;
+    }
+    __syncthreads();
+    const int64_t i = i0 + threadIdx.x;
+    if (i < i1) {
+      const int64_t a = off[i], len = off[i + 1] - a;
+      bool r;
+      if (staged)
+        r = like_match(buf + ((uintptr_t)(chars + a) - start), len, spat, skind, m, ci);
+      else
+        r = like_match(chars + a, len, spat, skind, m, ci);
+      out[i] = r != negate;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void case_kernel(const uint8_t* __restrict__ in, int64_t nbytes, bool to_upper,
                                                      uint8_t* __restrict__ out, int* __restrict__ non_ascii) {
   int found = 0;
@@ -204,8 +253,12 @@ __global__ __launch_bounds__(kBlock) void prefix_key_kernel(const int64_t* __res
 void str_like(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* pat, const uint8_t* kind, int m,
               bool case_insensitive, bool negate, uint8_t* out, hipStream_t stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(like_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, off, chars, n, pat, kind, m,
-                     case_insensitive, negate, out);
+  if (m <= kLikeMaxPattern)
+    hipLaunchKernelGGL(like_tile_kernel, dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock), 0, stream, off, chars, n,
+                       pat, kind, m, case_insensitive, negate, out);
+  else
+    hipLaunchKernelGGL(like_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, off, chars, n, pat, kind,
+                       m, case_insensitive, negate, out);
   check_launch("str_like", stream);
 }
 

@@ -361,6 +361,8 @@ class HashJoinExec(ExecNode):
     def _run(self, ctx):
         j = self.logical
         lb = self.children[0].execute(ctx)
+        if j.kind in ("inner", "left", "semi") and j.on:
+            push_key_filter(self.children[1], j.on, lb, ctx)
         rb = self.children[1].execute(ctx)
         if ctx.world > 1:
             from ..parallel.exchange import prepare_join
@@ -369,6 +371,72 @@ class HashJoinExec(ExecNode):
             out.dist = lb.out_dist
             return out
         return hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
+
+
+#: largest (global) probe side whose keys are pushed into the build side's aggregate
+RUNTIME_FILTER_MAX_ROWS = 16_000_000
+
+
+def _agg_group_source(node: ExecNode, cid: int):
+    """Follow output column ``cid`` down through projections / filters to the
+    aggregate that produces it as a GROUP BY key: (HashAggExec, group expr)."""
+    while True:
+        if isinstance(node, ProjectExec):
+            src = [e for ci, e in node.logical.exprs if ci.cid == cid]
+            if not src or not isinstance(src[0], ColRef):
+                return None
+            cid = src[0].cid
+            node = node.children[0]
+        elif isinstance(node, FilterExec):
+            node = node.children[0]
+        elif isinstance(node, HashAggExec):
+            for ci, e in node.logical.groups:
+                if ci.cid == cid:
+                    return node, e
+            return None
+        else:
+            return None
+
+
+def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
+    """Sideways information passing: when the build side of an inner / left /
+    semi join is an aggregate grouped by the join key, only groups whose key
+    occurs on the (already materialised, small) probe side can ever match, so
+    the aggregate's INPUT is semi-joined with those keys before grouping.
+    TPC-H Q17/Q20/Q2: a correlated aggregate over all of lineitem/partsupp
+    shrinks to the handful of parts the outer query selected."""
+    if _global_rows(lb, ctx) > RUNTIME_FILTER_MAX_ROWS:
+        return
+    for a, b in on:
+        if not isinstance(b, ColRef):
+            continue
+        found = _agg_group_source(build, b.cid)
+        if found is None:
+            continue
+        agg, gexpr = found
+        if a.dtype.is_string or gexpr.dtype.is_string:
+            continue
+        lcol = ctx.evaluator.column(a, lb)
+        if ctx.world > 1 and lb.dist != ("replicated",):
+            from ..parallel.exchange import gather_all
+            lcol = gather_all(Batch({0: lcol}, lb.num_rows, lb.dist), ctx).columns[0]
+        agg.runtime_filters.append((gexpr, lcol))
+        return
+
+
+def apply_key_filters(b: Batch, filters, ctx) -> Batch:
+    for gexpr, lcol in filters:
+        with ctx.span("agg.runtime_filter"):
+            kcol = ctx.evaluator.column(gexpr, b)
+            pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
+            if b.num_rows == 0:
+                continue
+            first = H.JoinTable(bk, bvalid).probe_first(pk, pvalid)
+            sel = mask_to_indices(first >= 0)
+            if sel.numel() < b.num_rows:
+                keys = list(b.columns)
+                b = Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], sel))), sel.numel(), b.dist)
+    return b
 
 
 def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Batch:
@@ -395,6 +463,24 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             lk = lk.index_select(0, keep.long())
             lvalid = None
             n_l = lb.num_rows
+    if kind in ("semi", "anti") and not null_aware and n_l and n_r > 4 * n_l:
+        # EXISTS against a much larger relation (TPC-H Q21/Q4 shapes): build on
+        # the small probe side, stream the big side through it and flag the
+        # probe rows that found a (residual-qualified) partner
+        with ctx.span("join.build"):
+            table = H.JoinTable(lk, lvalid)
+        matched = torch.zeros(n_l, dtype=torch.bool, device=dev)
+        with ctx.span("join.probe"):
+            if residual is None:
+                table.probe_first(rk, rvalid, build_matched=matched)
+            else:
+                ridx, lidx, _ = table.probe_pairs(rk, rvalid)
+                pair = _combine(lb, rb, lidx, ridx, False)
+                keep = mask_to_indices(ev.mask(residual, pair))
+                matched[lidx.index_select(0, keep.long()).long()] = True
+            sel = mask_to_indices(matched if kind == "semi" else ~matched)
+        with ctx.span("join.gather"):
+            return _take_batch(lb, sel)
     if kind == "inner" and residual is None and n_l < n_r:
         # build on the smaller side
         out = hash_join(rb, lb, "inner", [(b, a) for a, b in on], None, ctx)
@@ -709,6 +795,7 @@ class HashAggExec(ExecNode):
     def __init__(self, logical: L.Aggregate, child: ExecNode):
         self.logical = logical
         self.children = [child]
+        self.runtime_filters: list = []  # (group expr, key column) set by a parent join
 
     def describe(self):
         a = self.logical
@@ -717,6 +804,9 @@ class HashAggExec(ExecNode):
 
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
+        if self.runtime_filters:
+            filters, self.runtime_filters = self.runtime_filters, []
+            b = apply_key_filters(b, filters, ctx)
         if ctx.world > 1:
             from ..parallel.exchange import distributed_aggregate
             return distributed_aggregate(self.logical, b, ctx)

@@ -147,6 +147,25 @@ def test_like(gpu_device, pat):
     assert torch.equal(ref, got)
 
 
+def test_like_long_strings_and_slices(gpu_device):
+    # tiles whose bytes overflow the LDS stage (unstaged path), mixed with short
+    # ones, and a sliced column whose character buffer starts mid-allocation
+    r = _rng(9)
+    vals = []
+    for i in range(5000):
+        w = " ".join(r.choice(WORDS, r.integers(0, 40 if i % 700 < 300 else 4)))
+        vals.append(w)
+    c = _str_col(vals)
+    for pat in ("%special%requests%", "%green", "Customer%", "%ü%"):
+        ref = S.like(c, pat)
+        assert torch.equal(ref, S.like(c.to(DEV), pat).cpu())
+    from igloo_amd.ops.gather import take
+    idx = torch.arange(3, 4999, 3, dtype=torch.int32)
+    sub_cpu = take(c, idx)
+    sub_gpu = take(c.to(DEV), idx.to(DEV))
+    assert torch.equal(S.like(sub_cpu, "%requests%"), S.like(sub_gpu, "%requests%").cpu())
+
+
 def test_string_transforms(gpu_device):
     vals = [w.replace("ü", "u").replace("ï", "i") for w in _words(30_000, 7)]
     c = _str_col(vals)
