@@ -5,6 +5,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <tuple>
+#include <vector>
+
 #include <vector>
 
 #include "kernels/kernels.h"
@@ -119,6 +122,74 @@ PYBIND11_MODULE(_native, m) {
     kern::join_expand(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
                       P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<const int64_t>(offsets),
                       P<int32_t>(out_probe), P<int32_t>(out_build), S(s));
+  });
+  // fused scan kernels. cols: [(ptr, width)], terms: [(col, kind, lo, hi, set)],
+  // keys: [(col, lo, mul)], aggs: [(op, checked, [(col, a, b)], dst, dst2)]
+  using FfCols = std::vector<std::pair<uintptr_t, int64_t>>;
+  using FfTerms = std::vector<std::tuple<int, int, int64_t, int64_t, uint64_t>>;
+  using FfKeys = std::vector<std::tuple<int, int64_t, int64_t>>;
+  using FfAggs = std::vector<std::tuple<int, int, std::vector<std::tuple<int64_t, int64_t, int64_t>>, uintptr_t,
+                                        uintptr_t>>;
+  auto make_ff = [](const FfCols& cols, const FfTerms& terms, uintptr_t mask) {
+    if (cols.size() > (size_t)kern::kFfMaxCols || terms.size() > (size_t)kern::kFfMaxTerms)
+      throw std::runtime_error("fused scan: too many columns / terms");
+    kern::FfSpec f{};
+    f.ncols = (int32_t)cols.size();
+    for (size_t i = 0; i < cols.size(); ++i) {
+      f.cols[i].ptr = reinterpret_cast<const void*>(cols[i].first);
+      f.cols[i].width = cols[i].second;
+      if (!(f.cols[i].width == 1 || f.cols[i].width == 2 || f.cols[i].width == 4 || f.cols[i].width == 8))
+        throw std::runtime_error("fused scan: bad column width");
+    }
+    f.nterms = (int32_t)terms.size();
+    for (size_t i = 0; i < terms.size(); ++i) {
+      auto [col, kind, lo, hi, set] = terms[i];
+      if (col < 0 || col >= f.ncols || kind < 0 || kind > 2) throw std::runtime_error("fused scan: bad term");
+      f.terms[i] = kern::FfTerm{col, kind, lo, hi, set};
+    }
+    f.mask = P<const uint8_t>(mask);
+    return f;
+  };
+  m.def("ff_mask", [make_ff](const FfCols& cols, const FfTerms& terms, uintptr_t mask, int64_t n, uintptr_t out,
+                             uintptr_t s) {
+    kern::FfSpec f = make_ff(cols, terms, mask);
+    kern::ff_mask(f, n, P<uint8_t>(out), S(s));
+  });
+  m.def("ff_aggregate", [make_ff](const FfCols& cols, const FfTerms& terms, uintptr_t mask, const FfKeys& keys,
+                                  int ngroups, const FfAggs& aggs, uintptr_t counts, uintptr_t overflow, int64_t n,
+                                  uintptr_t s) {
+    kern::FfSpec f = make_ff(cols, terms, mask);
+    if (keys.size() > 2 || ngroups < 1 || ngroups > kern::kFfMaxGroups || aggs.size() > (size_t)kern::kFfMaxAggs)
+      throw std::runtime_error("fused aggregate: shape out of range");
+    f.nkeys = (int32_t)keys.size();
+    for (size_t i = 0; i < keys.size(); ++i) {
+      auto [col, lo, mul] = keys[i];
+      if (col < 0 || col >= f.ncols) throw std::runtime_error("fused aggregate: bad key column");
+      f.key_col[i] = col;
+      f.key_lo[i] = lo;
+      f.key_mul[i] = mul;
+    }
+    f.ngroups = ngroups;
+    f.naggs = (int32_t)aggs.size();
+    for (size_t i = 0; i < aggs.size(); ++i) {
+      auto& [op, checked, facs, dst, dst2] = aggs[i];
+      if (op < 0 || op > 3 || facs.size() > (size_t)kern::kFfMaxFactors)
+        throw std::runtime_error("fused aggregate: bad aggregate");
+      kern::FfAgg& A = f.aggs[i];
+      A.op = op;
+      A.checked = checked;
+      A.nfac = (int32_t)facs.size();
+      for (size_t k = 0; k < facs.size(); ++k) {
+        auto [col, a, b] = facs[k];
+        if (col >= f.ncols) throw std::runtime_error("fused aggregate: bad factor column");
+        A.f[k] = kern::FfFactor{col, a, b};
+      }
+      A.dst = P<int64_t>(dst);
+      A.dst2 = P<int64_t>(dst2);
+    }
+    f.counts = P<int64_t>(counts);
+    f.overflow = P<int>(overflow);
+    kern::ff_aggregate(f, n, S(s));
   });
   m.attr("HLL_REGISTERS") = kern::kHllRegisters;
   m.def("hll_blocks", [](int64_t n) { return kern::hll_blocks(n); });

@@ -25,6 +25,49 @@ int64_t scan_workspace_tiles(int64_t n);
 void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
                     hipStream_t stream);
 
+// ---- fused.hip ----------------------------------------------------------------
+constexpr int kFfMaxCols = 8;
+constexpr int kFfMaxTerms = 8;
+constexpr int kFfMaxAggs = 8;
+constexpr int kFfMaxGroups = 16;
+constexpr int kFfMaxFactors = 3;
+struct FfColumn {
+  const void* ptr;
+  int64_t width;  // bytes: 1, 2, 4, 8 (signed except 1 = uint8/bool)
+};
+// kind 0: lo <= v <= hi; 1: NOT (lo <= v <= hi); 2: v in bitmask `set` (0 <= v < 64)
+struct FfTerm {
+  int32_t col, kind;
+  int64_t lo, hi;
+  uint64_t set;
+};
+// value factor: col < 0 -> a, else a + b * col
+struct FfFactor {
+  int64_t col, a, b;
+};
+// op: 0 sum (int128: dst = lo, dst2 = hi), 1 count, 2 min, 3 max (int64)
+struct FfAgg {
+  int32_t op, nfac;
+  int32_t checked, pad;
+  FfFactor f[kFfMaxFactors];
+  int64_t* dst;
+  int64_t* dst2;
+};
+struct FfSpec {
+  int32_t ncols, nterms, nkeys, naggs, ngroups, pad;
+  FfColumn cols[kFfMaxCols];
+  FfTerm terms[kFfMaxTerms];
+  int32_t key_col[2];
+  int64_t key_lo[2];
+  int64_t key_mul[2];
+  FfAgg aggs[kFfMaxAggs];
+  const uint8_t* mask;  // optional precomputed conjunct (nullptr = none)
+  int64_t* counts;      // [ngroups] rows per group (aggregate only)
+  int* overflow;        // set when a checked product overflows int64
+};
+void ff_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream);
+void ff_aggregate(const FfSpec& spec, int64_t n, hipStream_t stream);
+
 // ---- sketch.hip --------------------------------------------------------------
 constexpr int kHllBits = 12;
 constexpr int kHllRegisters = 1 << kHllBits;

@@ -1,0 +1,416 @@
+"""Planner for the fused scan kernels (csrc/kernels/fused.hip).
+
+Turns a scan predicate into AND-ed range / code-set terms over integer
+columns (decimals as scaled int64, dates as days, dictionary codes) and an
+aggregate over a scan into a small-domain GROUP BY of sums of products of
+affine terms — the shape of TPC-H's scan-heavy queries (Q1, Q6 and the
+``price * (1 - discount)`` revenue expression nearly every query sums).
+
+Semantics mirror ``expr_eval.Evaluator`` exactly: comparisons happen in the
+common numeric type (bounds are adjusted with exact integer ceil/floor instead
+of rescaling the column), products keep the scale sum, decimal products whose
+static precision exceeds 18 digits are overflow-checked. A conjunct that does
+not fit a term is evaluated node by node into a mask the kernel reads;
+aggregates that do not fit return None so the caller keeps its generic path.
+
+Role in the reference: DataFusion's FilterExec -> ProjectionExec ->
+AggregateExec chain run by ``QueryEngine::execute`` (reference
+crates/engine/src/lib.rs:55-56; operators/filter.rs:47).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .. import types as T
+from ..columnar import Batch, Column
+from ..sql.expr import BinOp, Cast, ColRef, Expr, InList, Lit, conjuncts
+from ..types import DataType
+from ..utils.errors import ExecutionError
+
+MAX_COLS, MAX_TERMS, MAX_AGGS, MAX_GROUPS, MAX_FACTORS = 8, 8, 8, 16, 3
+I64_MIN, I64_MAX = -(2**63), 2**63 - 1
+FLIP = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
+
+
+class Bail(Exception):
+    pass
+
+
+def _debug(what, why):
+    if os.environ.get("IGLOO_FUSED_DEBUG"):
+        print(f"[fused] {what}: fallback ({why})", flush=True)
+
+
+def _floordiv(a: int, b: int) -> int:
+    return a // b
+
+
+def _ceildiv(a: int, b: int) -> int:
+    return -((-a) // b)
+
+
+class Spec:
+    """Columns + filter terms (+ fallback mask) of one fused launch."""
+
+    def __init__(self, b: Batch, ev):
+        self.b = b
+        self.ev = ev
+        self.cols: List[torch.Tensor] = []
+        self._idx: Dict[int, int] = {}
+        self.terms: List[tuple] = []
+        self.mask: Optional[torch.Tensor] = None
+        self.always_false = False
+
+    def col(self, c: Column) -> int:
+        if c.valid is not None or c.is_wide or (c.dtype.is_string and not c.is_dict):
+            raise Bail("nullable / wide / plain-string column")
+        x = c.data
+        if x.dtype in (torch.bool, torch.uint8, torch.int8, torch.int16):
+            x = x.to(torch.int32)   # the kernels load 4- or 8-byte words
+        if x.dtype not in (torch.int32, torch.int64) or x.dim() != 1:
+            raise Bail(f"column dtype {x.dtype}")
+        if not x.is_contiguous():
+            x = x.contiguous()
+        key = id(c.data)
+        if key not in self._idx:
+            if len(self.cols) >= MAX_COLS:
+                raise Bail("too many columns")
+            self._idx[key] = len(self.cols)
+            self.cols.append(x)
+        return self._idx[key]
+
+    def colref(self, e: ColRef) -> Tuple[int, Column]:
+        c = self.b.columns.get(e.cid)
+        if c is None:
+            raise Bail("column not in batch")
+        return self.col(c), c
+
+    # ------------------------------------------------------------- filter
+    def add_predicate(self, pred: Expr) -> None:
+        for c in conjuncts(pred):
+            try:
+                self._term(c)
+            except Bail as why:
+                _debug("conjunct", why)
+                m = self.ev.mask(c, self.b)
+                self.mask = m if self.mask is None else (self.mask & m)
+
+    def _range(self, ci: int, op: str, v: int):
+        if len(self.terms) >= MAX_TERMS:
+            raise Bail("too many terms")
+        lo, hi, kind = I64_MIN, I64_MAX, 0
+        if op == "=":
+            lo = hi = v
+        elif op == "<>":
+            lo = hi = v
+            kind = 1
+        elif op == "<":
+            if v == I64_MIN:
+                self.always_false = True
+                return
+            hi = v - 1
+        elif op == "<=":
+            hi = v
+        elif op == ">":
+            if v == I64_MAX:
+                self.always_false = True
+                return
+            lo = v + 1
+        elif op == ">=":
+            lo = v
+        self.terms.append((ci, kind, lo, hi, 0))
+
+    def _term(self, c: Expr) -> None:
+        if isinstance(c, InList):
+            self._inlist(c)
+            return
+        if not (isinstance(c, BinOp) and c.op in FLIP):
+            raise Bail(f"conjunct {type(c).__name__}")
+        l, r, op = c.left, c.right, c.op
+        if isinstance(l, Lit) and not isinstance(r, Lit):
+            l, r, op = r, l, FLIP[op]
+        cast_t = None
+        # CAST(col AS wider decimal/int) only rescales exactly: compare the raw column
+        while isinstance(l, Cast) and (l.dtype.is_decimal or l.dtype.is_integer) and \
+                (l.x.dtype.is_decimal or l.x.dtype.is_integer) and \
+                (l.dtype.scale if l.dtype.is_decimal else 0) >= (l.x.dtype.scale if l.x.dtype.is_decimal else 0):
+            cast_t = cast_t or l.dtype
+            l = l.x
+        if not (isinstance(l, ColRef) and isinstance(r, Lit)) or r.value is None:
+            raise Bail("not column-vs-literal")
+        ci, col = self.colref(l)
+        if col.is_dict:
+            if op not in ("=", "<>"):
+                raise Bail("string range on a dictionary")
+            code = _dict_code(col, str(r.value))
+            if code is None:
+                if op == "=":
+                    self.always_false = True
+                return  # '<>' a value not in the dictionary: always true
+            self._range(ci, op, code)
+            return
+        lt, rt = (cast_t or col.dtype), r.dtype
+        if lt.is_float or rt.is_float or lt.is_string or rt.is_string:
+            raise Bail("float / string comparison")
+        if lt.kind in ("date32", "timestamp", "bool") or rt.kind in ("date32", "timestamp", "bool"):
+            self._range(ci, op, int(r.value))
+            return
+        t = lt if lt == rt else T.common_numeric(lt, rt)
+        cs = col.dtype.scale if col.dtype.is_decimal else 0
+        ls = rt.scale if rt.is_decimal else 0
+        ts = t.scale if t.is_decimal else 0
+        L = int(r.value) * 10 ** (ts - ls)       # literal in the common scale
+        f = 10 ** (ts - cs)                      # column multiplier into the common scale
+        if f == 1:
+            self._range(ci, op, L)
+            return
+        # col * f  OP  L   <=>   col OP' bound (exact integer bounds)
+        if op == "<":
+            self._range(ci, "<", _ceildiv(L, f))
+        elif op == "<=":
+            self._range(ci, "<=", _floordiv(L, f))
+        elif op == ">":
+            self._range(ci, ">", _floordiv(L, f))
+        elif op == ">=":
+            self._range(ci, ">=", _ceildiv(L, f))
+        elif op == "=":
+            if L % f:
+                self.always_false = True
+            else:
+                self._range(ci, "=", L // f)
+        else:  # '<>'
+            if L % f == 0:
+                self._range(ci, "<>", L // f)
+
+    def _inlist(self, c: InList) -> None:
+        if not isinstance(c.x, ColRef) or any(v.value is None for v in c.values):
+            raise Bail("IN over an expression / NULL")
+        ci, col = self.colref(c.x)
+        if not col.is_dict or len(col.dictionary) > 64:
+            raise Bail("IN on a non-dictionary column")
+        bits = 0
+        for v in c.values:
+            code = _dict_code(col, str(v.value))
+            if code is not None:
+                bits |= 1 << code
+        if len(self.terms) >= MAX_TERMS:
+            raise Bail("too many terms")
+        if c.negated:
+            bits = ~bits & ((1 << 64) - 1)
+        self.terms.append((ci, 2, 0, 0, bits))
+
+    def args(self):
+        return ([(t.data_ptr(), t.element_size()) for t in self.cols], self.terms,
+                self.mask.data_ptr() if self.mask is not None else 0)
+
+
+def _dict_code(col: Column, s: str) -> Optional[int]:
+    cache = getattr(col.dictionary, "_code_of", None)
+    if cache is None:
+        vals = col.dictionary.to_arrow().to_pylist()
+        cache = {v: i for i, v in enumerate(vals)}
+        try:
+            col.dictionary._code_of = cache
+        except AttributeError:
+            pass
+    return cache.get(s)
+
+
+# ------------------------------------------------------------------ masks
+def predicate_mask(pred: Expr, b: Batch, ev) -> Optional[torch.Tensor]:
+    """Scan predicate -> bool mask with one fused kernel, or None (no term applies)."""
+    from ..ops._lib import launch, stream
+    if b.num_rows == 0:
+        return None
+    spec = Spec(b, ev)
+    spec.add_predicate(pred)
+    n = b.num_rows
+    dev = ev.device(b)
+    if spec.always_false:
+        return torch.zeros(n, dtype=torch.bool, device=dev)
+    if not spec.terms:
+        return spec.mask  # every conjunct needed the generic evaluator
+    out = torch.empty(n, dtype=torch.bool, device=dev)
+    cols, terms, mask = spec.args()
+    launch("ff_mask").ff_mask(cols, terms, mask, n, out.data_ptr(), stream(out))
+    return out
+
+
+# -------------------------------------------------------------- aggregates
+def _factors(e: Expr, spec: Spec) -> Tuple[List[tuple], int, bool]:
+    """e == prod(a + b * col) -> (factors, scale, checked) in the Evaluator's
+    representation of e.dtype; raises Bail otherwise."""
+    t = e.dtype
+    if isinstance(e, ColRef):
+        ci, col = spec.colref(e)
+        if col.is_dict or col.dtype.is_float:
+            raise Bail("dictionary / float argument")
+        return [(ci, 0, 1)], (col.dtype.scale if col.dtype.is_decimal else 0), False
+    if isinstance(e, Lit):
+        if e.value is None or t.is_float or t.is_string:
+            raise Bail("literal argument")
+        return [(-1, int(e.value), 0)], (t.scale if t.is_decimal else 0), False
+    if isinstance(e, Cast) and t.is_decimal and (e.x.dtype.is_decimal or e.x.dtype.is_integer):
+        fs, s, chk = _factors(e.x, spec)
+        d = t.scale - s
+        if d < 0 or len(fs) != 1:
+            raise Bail("down-scaling cast")
+        ci, a, b_ = fs[0]
+        return [(ci, a * 10**d, b_ * 10**d)], t.scale, chk
+    if isinstance(e, BinOp) and e.op == "*" and (t.is_decimal or t.is_integer):
+        fl, sl, cl = _factors(e.left, spec)
+        fr, sr, cr = _factors(e.right, spec)
+        fs = fl + fr
+        consts = [f for f in fs if f[0] < 0]
+        var = [f for f in fs if f[0] >= 0]
+        k = 1
+        for f in consts:
+            k *= f[1]
+        fs = var + ([(-1, k, 0)] if k != 1 or not var else [])
+        if len(fs) > MAX_FACTORS:
+            raise Bail("too many factors")
+        return fs, sl + sr, cl or cr or (t.is_decimal and t.precision > 18)
+    if isinstance(e, BinOp) and e.op in ("+", "-") and (t.is_decimal or t.is_integer):
+        l, r = e.left, e.right
+        sign = 1 if e.op == "+" else -1
+        if isinstance(l, Lit) and not isinstance(r, Lit):
+            lit, x, lit_first = l, r, True
+        elif isinstance(r, Lit):
+            lit, x, lit_first = r, l, False
+        else:
+            raise Bail("sum of two columns")
+        if lit.value is None:
+            raise Bail("NULL literal")
+        fx, sx, chk = _factors(x, spec)
+        if len(fx) != 1 or fx[0][0] < 0:
+            raise Bail("affine over a product")
+        ts = t.scale if t.is_decimal else 0
+        ls = lit.dtype.scale if lit.dtype.is_decimal else 0
+        if ts < sx or ts < ls:
+            raise Bail("down-scaling add")
+        L = int(lit.value) * 10 ** (ts - ls)
+        ci, a, b_ = fx[0]
+        m = 10 ** (ts - sx)
+        if lit_first:   # L +/- (a + b col)
+            return [(ci, L + sign * a * m, sign * b_ * m)], ts, chk
+        return [(ci, a * m + sign * L, b_ * m)], ts, chk  # (a + b col) +/- L
+    raise Bail(f"argument {type(e).__name__}")
+
+
+def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> Optional[Batch]:
+    """GROUP BY (domain <= 16) over a scanned batch with the scan filter and the
+    argument arithmetic fused into one kernel, or None if the shape does not fit."""
+    from ..ops._lib import launch, stream
+    from .operators import _avg
+    dev = ctx.device
+    if dev.type != "cuda" or b.num_rows == 0:
+        return None
+    n = b.num_rows
+    try:
+        spec = Spec(b, ctx.evaluator)
+        keys, kinfo, G = [], [], 1
+        for ci, e in groups:
+            if not isinstance(e, ColRef):
+                raise Bail("computed group key")
+            k, col = spec.colref(e)
+            if col.is_dict:
+                lo, size = 0, len(col.dictionary)
+            elif col.dtype.is_integer or col.dtype.kind in ("date32", "bool"):
+                mn, mx = torch.aminmax(col.data)
+                lo, size = int(mn.item()), int(mx.item()) - int(mn.item()) + 1
+            else:
+                raise Bail("group key type")
+            kinfo.append((ci, col, k, lo, max(size, 1)))
+            G *= max(size, 1)
+            if G > MAX_GROUPS or len(kinfo) > 2:
+                raise Bail("group domain")
+        mul = 1
+        for ci, col, k, lo, size in reversed(kinfo):
+            keys.append((k, lo, mul))
+            mul *= size
+        plan = []
+        descs = []
+        for ci, a in aggs:
+            if a.distinct or a.filter is not None or a.func not in ("sum", "count", "avg", "min", "max"):
+                raise Bail(f"aggregate {a.func}")
+            if a.func == "count":
+                if a.arg is not None:
+                    c = ctx.evaluator.eval(a.arg, b) if not isinstance(a.arg, ColRef) else b.columns.get(a.arg.cid)
+                    if c is None or getattr(c, "valid", None) is not None:
+                        raise Bail("count over a nullable argument")
+                plan.append((ci, a, None))
+                continue
+            if a.arg.dtype.is_float or a.arg.dtype.is_string:
+                raise Bail("float / string argument")
+            fs, scale, chk = _factors(a.arg, spec)
+            want = a.arg.dtype.scale if a.arg.dtype.is_decimal else 0
+            if scale != want:
+                raise Bail(f"scale {scale} != {want}")
+            op = {"sum": 0, "avg": 0, "min": 2, "max": 3}[a.func]
+            plan.append((ci, a, len(descs)))
+            descs.append((op, int(chk), fs))
+        if len(descs) > MAX_AGGS:
+            raise Bail("too many aggregates")
+        if pred is not None:
+            spec.add_predicate(pred)
+    except Bail as why:
+        _debug("aggregate", why)
+        return None
+    counts = torch.zeros(G, dtype=torch.int64, device=dev)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    bufs, kaggs = [], []
+    for op, chk, fs in descs:
+        if op == 0:
+            d, d2 = torch.zeros(G, dtype=torch.int64, device=dev), torch.zeros(G, dtype=torch.int64, device=dev)
+        else:
+            d = torch.full((G,), I64_MAX if op == 2 else I64_MIN, dtype=torch.int64, device=dev)
+            d2 = None
+        bufs.append((d, d2))
+        kaggs.append((op, chk, [(int(c), int(a_), int(b_)) for c, a_, b_ in fs], d.data_ptr(),
+                      d2.data_ptr() if d2 is not None else 0))
+    if not spec.always_false:
+        cols, terms, mask = spec.args()
+        with ctx.span("agg.fused_scan"):
+            launch("ff_aggregate").ff_aggregate(cols, terms, mask, keys, G, kaggs, counts.data_ptr(), ovf.data_ptr(),
+                                                n, stream(counts))
+    if any(chk for _, chk, _ in descs) and int(ovf.item()):
+        raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
+    from ..ops.agg import _wide_to_result
+    res = [(_wide_to_result(d, d2) if d2 is not None else d) for d, d2 in bufs]
+    if groups:
+        keep = torch.nonzero(counts > 0).flatten()
+        ng = keep.numel()
+    else:
+        keep, ng = None, 1
+
+    def sel(x):
+        return x if keep is None else x.index_select(0, keep)
+    out: Dict[int, Column] = {}
+    if groups:
+        stride = 1
+        for ci, col, k, lo, size in reversed(kinfo):
+            code = (keep // stride) % size + lo
+            stride *= size
+            if col.is_dict:
+                out[ci.cid] = Column(col.dtype, code.to(torch.int32), None, dictionary=col.dictionary)
+            else:
+                out[ci.cid] = Column(col.dtype, code.to(col.data.dtype), None)
+    cnt = sel(counts)
+    for ci, a, i in plan:
+        t = a.dtype
+        if a.func == "count":
+            out[ci.cid] = Column(T.INT64, cnt)
+            continue
+        v = sel(res[i])
+        nonempty = cnt > 0
+        valid = None if groups else nonempty
+        if a.func == "avg":
+            out[ci.cid] = Column(t, _avg(v, cnt, a.arg.dtype, t), nonempty)
+        elif a.func == "sum":
+            out[ci.cid] = Column(t, v, valid)
+        else:
+            out[ci.cid] = Column(t, v.to(t.torch_dtype), valid)
+    return Batch(out, ng)

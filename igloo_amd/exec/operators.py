@@ -38,6 +38,7 @@ from ..ops.select import mask_to_indices
 from ..sql import logical as L
 from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
 from ..utils.errors import ExecutionError, NotSupported
+from . import fused
 from .expr_eval import Evaluator, Scalar, _convert_tensor
 
 
@@ -171,7 +172,8 @@ class ScanExec(ExecNode):
         f = f", filters=[{', '.join(x.sql() for x in s.filters)}]" if s.filters else ""
         return f"{s.table} projection=[{', '.join(c.name for c in s.schema)}]{f}"
 
-    def _run(self, ctx):
+    def scan_raw(self, ctx) -> Batch:
+        """Scanned columns (projection + filter inputs) before filtering, keyed by cid."""
         s = self.logical
         table_cols = getattr(s, "table_cols", s.schema)
         by_cid = {c.cid: c for c in table_cols}
@@ -191,16 +193,60 @@ class ScanExec(ExecNode):
             elif getattr(s.source, "partitioned_by", None):
                 pc = [c.cid for c in table_cols if c.name == s.source.partitioned_by]
                 dist = ("hash", pc[0]) if pc else None
-        b = Batch(cols, raw.num_rows)
+        return Batch(cols, raw.num_rows, dist)
+
+    @property
+    def predicate(self) -> Optional[Expr]:
+        return and_all(self.logical.filters) if self.logical.filters else None
+
+    def finish(self, b: Batch, ctx) -> Batch:
+        """Apply the fused scan filter and the projection to a ``scan_raw`` batch."""
+        s = self.logical
+        out_cids = [c.cid for c in s.schema]
         if s.filters:
             with ctx.span("scan.filter_eval"):
-                m = ctx.evaluator.mask(and_all(s.filters), b)
+                m = predicate_mask(self.predicate, b, ctx)
                 idx = mask_to_indices(m)
-            out_cids = [c.cid for c in s.schema]
             with ctx.span("scan.filter_gather"):
                 taken = take_many([b.columns[c] for c in out_cids], idx)
-            return Batch(dict(zip(out_cids, taken)), idx.numel(), dist)
-        return Batch({c.cid: cols[c.cid] for c in s.schema}, raw.num_rows, dist)
+            return Batch(dict(zip(out_cids, taken)), idx.numel(), b.dist)
+        return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
+
+    def _run(self, ctx):
+        return self.finish(self.scan_raw(ctx), ctx)
+
+
+def predicate_mask(pred: Expr, b: Batch, ctx) -> torch.Tensor:
+    """Filter mask: one fused VM kernel on the GPU when the predicate fits, else
+    node-by-node evaluation."""
+    if ctx.device.type == "cuda":
+        m = fused.predicate_mask(pred, b, ctx.evaluator)
+        if m is not None:
+            return m
+    return ctx.evaluator.mask(pred, b)
+
+
+class LazyBatch(Batch):
+    """A Batch materialised on first access (lets the aggregate fuse the scan
+    filter and skip building the filtered batch altogether)."""
+
+    def __init__(self, thunk, dist):  # noqa: D401 - no Batch.__init__: attributes are lazy
+        self._thunk = thunk
+        self._b = None
+        self.dist = dist
+
+    def _get(self) -> Batch:
+        if self._b is None:
+            self._b = self._thunk()
+        return self._b
+
+    @property
+    def columns(self):  # type: ignore[override]
+        return self._get().columns
+
+    @property
+    def num_rows(self):  # type: ignore[override]
+        return self._get().num_rows
 
 
 class ValuesExec(ExecNode):
@@ -252,7 +298,7 @@ class FilterExec(ExecNode):
 
 def filter_batch(b: Batch, pred: Expr, ctx) -> Batch:
     with ctx.span("filter.eval"):
-        m = ctx.evaluator.mask(pred, b)
+        m = predicate_mask(pred, b, ctx)
         idx = mask_to_indices(m)
     if idx.numel() == b.num_rows:
         return b
@@ -803,14 +849,30 @@ class HashAggExec(ExecNode):
                 f"aggr=[{', '.join(x.sql() for _, x in a.aggs)}]")
 
     def _run(self, ctx):
-        b = self.children[0].execute(ctx)
+        lg = self.logical
+        child = self.children[0]
+        local = None
+        if isinstance(child, ScanExec) and ctx.device.type == "cuda" and not self.runtime_filters:
+            # scan -> filter -> aggregate in one fused kernel when the shape allows
+            raw = child.scan_raw(ctx)
+            pred = child.predicate
+
+            def local(groups, aggs, raw=raw, pred=pred):
+                return fused.fused_scan_aggregate(groups, aggs, raw, pred, ctx)
+            if ctx.world == 1:
+                out = local(lg.groups, lg.aggs)
+                if out is not None:
+                    return out
+            b = LazyBatch(lambda: child.finish(raw, ctx), raw.dist)
+        else:
+            b = child.execute(ctx)
         if self.runtime_filters:
             filters, self.runtime_filters = self.runtime_filters, []
             b = apply_key_filters(b, filters, ctx)
         if ctx.world > 1:
             from ..parallel.exchange import distributed_aggregate
-            return distributed_aggregate(self.logical, b, ctx)
-        return aggregate(self.logical.groups, self.logical.aggs, b, ctx)
+            return distributed_aggregate(lg, b, ctx, local=local)
+        return aggregate(lg.groups, lg.aggs, b, ctx)
 
 
 def aggregate(groups, aggs, b: Batch, ctx) -> Batch:

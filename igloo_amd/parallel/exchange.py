@@ -284,7 +284,9 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx):
 DECOMPOSABLE = {"sum", "count", "min", "max", "avg", "bool_and", "bool_or"}
 
 
-def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx) -> Batch:
+def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
+    """``local(groups, partial_aggs) -> Batch | None`` may compute the phase-1
+    partial states directly from the scan (fused VM kernel)."""
     from ..exec.operators import _avg, aggregate
     groups, aggs = lg.groups, lg.aggs
     d = dist_of(b)
@@ -317,7 +319,9 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx) -> Batch:
             p_ci = L.ColInfo(ids(), "__p", a.dtype)
             partial.append((p_ci, AggCall(a.func, a.arg, False, a.dtype, a.filter)))
             plan.append((a.func, ci, a, p_ci, None))
-    pb = aggregate(groups, partial, b, ctx)
+    pb = local(groups, partial) if local is not None else None
+    if pb is None:
+        pb = aggregate(groups, partial, b, ctx)
     # ---- exchange partial states
     if groups:
         g0 = groups[0][0]
