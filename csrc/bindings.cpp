@@ -219,12 +219,15 @@ PYBIND11_MODULE(_native, m) {
   // ------------------------------------------------------------ aggregation
   m.def("agg_lds_max_groups", &kern::agg_lds_max_groups);
   // descs: list of (op, src64, src, valid, dst, dst2)
-  m.def("agg_update", [](uintptr_t gid, int64_t n, int ngroups, const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t>>& descs, uintptr_t s) {
+  m.def("agg_update", [](uintptr_t gid, int64_t n, int ngroups, const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t>>& descs, uintptr_t s, bool sorted_gids) {
     std::vector<kern::AggDesc> d;
     for (auto& t : descs)
       d.push_back({std::get<0>(t), std::get<1>(t), P<const void>(std::get<2>(t)), P<const uint8_t>(std::get<3>(t)),
                    P<void>(std::get<4>(t)), P<void>(std::get<5>(t))});
-    kern::agg_update(P<const int32_t>(gid), n, ngroups, d.data(), (int)d.size(), S(s));
+    kern::agg_update(P<const int32_t>(gid), n, ngroups, d.data(), (int)d.size(), S(s), sorted_gids);
+  }, py::arg("gid"), py::arg("n"), py::arg("ngroups"), py::arg("descs"), py::arg("s"), py::arg("sorted_gids") = false);
+  m.def("fill_runs", [](uintptr_t starts, bool starts64, int64_t nruns, int64_t n, uintptr_t gid, uintptr_t s) {
+    kern::fill_runs(P<const void>(starts), starts64, nruns, n, P<int32_t>(gid), S(s));
   });
 
   // ----------------------------------------------------------------- gather

@@ -200,7 +200,24 @@ __global__ __launch_bounds__(kBlock) void groupby_lookup_kernel(const K* __restr
     }                                                                                 \
   } while (0)
 
+template <typename I>
+__global__ __launch_bounds__(kBlock) void fill_runs_kernel(const I* __restrict__ starts, int64_t nruns, int64_t n,
+                                                          int32_t* __restrict__ gid) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nruns; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = starts[r], e = r + 1 < nruns ? (int64_t)starts[r + 1] : n;
+    for (int64_t i = b; i < e; ++i) gid[i] = (int32_t)r;
+  }
+}
+
 }  // namespace
+
+void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int32_t* gid, hipStream_t stream) {
+  if (nruns == 0) return;
+  dim3 g(grid_for(nruns, kBlock, kMaxGrid)), b(kBlock);
+  if (starts64) hipLaunchKernelGGL(fill_runs_kernel<int64_t>, g, b, 0, stream, (const int64_t*)starts, nruns, n, gid);
+  else hipLaunchKernelGGL(fill_runs_kernel<int32_t>, g, b, 0, stream, (const int32_t*)starts, nruns, n, gid);
+  check_launch("fill_runs", stream);
+}
 
 void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
                 int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, hipStream_t stream) {

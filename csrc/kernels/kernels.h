@@ -86,6 +86,8 @@ void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, c
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
                  const int64_t* offsets, int32_t* out_probe, int32_t* out_build, hipStream_t stream);
+// run ids of a non-decreasing key column: gid[i] = r for rows in [starts[r], starts[r+1])
+void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int32_t* gid, hipStream_t stream);
 void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,
                    bool direct, hipStream_t stream);
 void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, hipStream_t stream);
@@ -115,7 +117,8 @@ struct AggDesc {
 };
 
 int agg_lds_max_groups(int nagg);
-void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream);
+void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream,
+                bool sorted_gids = false);
 
 // ---- gather.hip ----------------------------------------------------------------
 struct GatherDesc {

@@ -885,6 +885,7 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
         if n == 0:
             return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
         with ctx.span("agg.group_ids"):
+            ctx.sorted_gids = False
             gid, ng, rep, reps_src = _encode_groups(gcols, ctx)
     else:
         gid, ng, rep = None, 1, None
@@ -899,7 +900,9 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
         for ci, a in aggs:
             _plan_agg(ci, a, b, gid, ng, n, ctx, specs, finals)
     with ctx.span("agg.kernel"):
-        results = A.grouped_aggregate(gid, ng, [s[:3] for s in specs], n, dev) if specs else []
+        results = A.grouped_aggregate(gid, ng, [s[:3] for s in specs], n, dev,
+                                      sorted_gids=gid is not None and getattr(ctx, "sorted_gids", False)) \
+            if specs else []
         for fin in finals:
             ci, col = fin(results)
             out[ci.cid] = col
@@ -927,7 +930,8 @@ def _encode_groups(gcols: List[Column], ctx):
     if plain and others and ctx.device.type == "cuda":
         spans = {i: H.key_range(keys[i]) for i in others}
         lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
-        gid, ng, rep = H.group_ids(keys[lead])
+        gid, ng, rep, srt = H.group_ids_ex(keys[lead])
+        ctx.sorted_gids = srt
         rr = rep.index_select(0, gid.long())
         bad = []
         for i in range(len(gcols)):
@@ -952,7 +956,8 @@ def _encode_groups(gcols: List[Column], ctx):
         if i in needed:
             keys[i], _ = group_key_tensor(gcols[i])
     packed = H.pack_keys([keys[i] for i in needed])
-    gid, ng, rep = H.group_ids(packed)
+    gid, ng, rep, srt = H.group_ids_ex(packed)
+    ctx.sorted_gids = srt
     return gid, ng, rep, reps_src
 
 

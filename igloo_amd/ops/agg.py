@@ -32,14 +32,16 @@ def _wide_to_result(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
 
 
 def grouped_aggregate(gid: Optional[torch.Tensor], ngroups: int, specs: Sequence[Spec], n: int,
-                      device) -> List[torch.Tensor]:
+                      device, sorted_gids: bool = False) -> List[torch.Tensor]:
+    """``sorted_gids``: group ids are non-decreasing (clustered keys) — the GPU
+    then folds runs in registers instead of issuing one atomic per row."""
     device = torch.device(device)
     if device.type != "cpu":
-        return _gpu(gid, ngroups, specs, n, device)
+        return _gpu(gid, ngroups, specs, n, device, sorted_gids)
     return _cpu(gid, ngroups, specs, n)
 
 
-def _gpu(gid, ngroups, specs, n, device) -> List[torch.Tensor]:
+def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor]:
     N = native()
     g = max(ngroups, 1)
     outs, descs, posts = [], [], []
@@ -68,7 +70,7 @@ def _gpu(gid, ngroups, specs, n, device) -> List[torch.Tensor]:
         s = stream(gid if gid is not None else posts[0][1])
         for i in range(0, len(descs), 8):
             launch("agg_update")
-            N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s)
+            N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s, bool(sorted_gids))
     for op, dst, dst2 in posts:
         if op == "sum_int":
             outs.append(_wide_to_result(dst, dst2))

@@ -244,3 +244,23 @@ def test_group_by_functional_dependency(gpu_device):
                     .to_pylist() for c in ("dep", "nodep", "nl")]
     assert res["cpu"] == res[gpu_device]
     assert len(res["cpu"][1]) > len(res["cpu"][0]) and len(res["cpu"][2]) > len(res["cpu"][0])
+
+
+@pytest.mark.parametrize("n", [3_000_000])
+def test_sorted_group_ids_and_aggregate(gpu_device, n):
+    """Clustered keys take the run-id + register-folding path; results must
+    equal the hash path (and the CPU reference)."""
+    g = _rng(13)
+    k = torch.from_numpy(np.sort(g.integers(0, n // 3, n)).astype(np.int64))
+    v = torch.from_numpy(g.integers(-10**12, 10**12, n).astype(np.int64))
+    kd, vd = k.to(gpu_device), v.to(gpu_device)
+    gid, ng, rep, srt = H.group_ids_ex(kd)
+    assert srt and ng == torch.unique(k).numel()
+    assert torch.equal(kd.index_select(0, rep.long()), torch.unique(k).to(gpu_device))
+    specs = [("sum_int", vd, None), ("count", None, None), ("min_int", vd, None), ("max_int", vd, None)]
+    fast = A.grouped_aggregate(gid, ng, specs, n, gpu_device, sorted_gids=True)
+    slow = A.grouped_aggregate(gid, ng, specs, n, gpu_device, sorted_gids=False)
+    for a_, b_ in zip(fast, slow):
+        assert torch.equal(a_.cpu(), b_.cpu())
+    # unsorted keys are detected as such
+    assert not H.group_ids_ex(kd.flip(0))[3]
