@@ -105,23 +105,24 @@ PYBIND11_MODULE(_native, m) {
 
   // ------------------------------------------------------------ hash tables
   m.def("join_build", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t tkeys, uintptr_t thead,
-                         uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t dups, uintptr_t s) {
+                         uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t dups, uintptr_t bits,
+                         uint64_t bmask, uintptr_t s) {
     kern::join_build(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<int64_t>(tkeys), P<int32_t>(thead),
-                     P<int32_t>(next), cap, kmin, direct, P<unsigned long long>(dups), S(s));
+                     P<int32_t>(next), cap, kmin, direct, P<unsigned long long>(dups), P<uint32_t>(bits), bmask, S(s));
   });
   m.def("join_probe", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
                          uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t counts, uintptr_t first,
-                         uintptr_t matched, uintptr_t s) {
+                         uintptr_t matched, uintptr_t bits, uint64_t bmask, uintptr_t s) {
     kern::join_probe(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
                      P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<int32_t>(counts),
-                     P<int32_t>(first), P<uint8_t>(matched), S(s));
+                     P<int32_t>(first), P<uint8_t>(matched), P<const uint32_t>(bits), bmask, S(s));
   });
   m.def("join_expand", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
                           uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t offsets, uintptr_t out_probe,
-                          uintptr_t out_build, uintptr_t s) {
+                          uintptr_t out_build, uintptr_t bits, uint64_t bmask, uintptr_t s) {
     kern::join_expand(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
                       P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<const int64_t>(offsets),
-                      P<int32_t>(out_probe), P<int32_t>(out_build), S(s));
+                      P<int32_t>(out_probe), P<int32_t>(out_build), P<const uint32_t>(bits), bmask, S(s));
   });
   // fused scan kernels. cols: [(ptr, width)], terms: [(col, kind, lo, hi, set)],
   // keys: [(col, lo, mul)], aggs: [(op, checked, [(col, a, b)], dst, dst2)]

@@ -55,11 +55,17 @@ __device__ inline int64_t insert_slot(int64_t* __restrict__ tkeys, int64_t mask,
   }
 }
 
+// Optional 1-hash Bloom filter over the build keys (<= 4 MB, so it stays in a
+// XCD's L2): a selective probe (most probe keys absent) answers from L2 and
+// never touches the HBM-sized table.
+__device__ inline uint64_t bloom_bit(int64_t k, uint64_t bmask) { return (mix64((uint64_t)k) >> 7) & bmask; }
+
 template <typename K, bool DIRECT>
 __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
                                                            int64_t n, int64_t* __restrict__ tkeys,
                                                            int32_t* __restrict__ thead, int32_t* __restrict__ next,
-                                                           int64_t cap, int64_t kmin, unsigned long long* dups) {
+                                                           int64_t cap, int64_t kmin, unsigned long long* dups,
+                                                           uint32_t* __restrict__ bits, uint64_t bmask) {
   const int64_t mask = cap - 1;
   unsigned long long local_dups = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -75,6 +81,10 @@ __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict_
     int32_t old = atomicExch(&thead[slot], (int32_t)i);
     next[i] = old;
     local_dups += old != -1;
+    if (bits) {
+      const uint64_t bb = bloom_bit(k, bmask);
+      atomicOr(&bits[bb >> 5], 1u << (bb & 31));
+    }
   }
   // one atomic per wave for the duplicate counter
   for (int off = kWave / 2; off > 0; off >>= 1) local_dups += __shfl_xor(local_dups, off, kWave);
@@ -83,9 +93,14 @@ __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict_
 
 template <typename K, bool DIRECT>
 __device__ inline int32_t probe_head(const K* keys, const uint8_t* valid, int64_t j, const int64_t* tkeys,
-                                     const int32_t* thead, int64_t cap, int64_t kmin) {
+                                     const int32_t* thead, int64_t cap, int64_t kmin, const uint32_t* bits,
+                                     uint64_t bmask) {
   int64_t k;
   if (!load_key(keys, valid, j, &k)) return -1;
+  if (bits) {
+    const uint64_t b = bloom_bit(k, bmask);
+    if (!((bits[b >> 5] >> (b & 31)) & 1u)) return -1;
+  }
   if (DIRECT) {
     int64_t s = k - kmin;
     if (s < 0 || s >= cap) return -1;
@@ -102,9 +117,10 @@ __global__ __launch_bounds__(kBlock) void join_probe_kernel(const K* __restrict_
                                                            const int32_t* __restrict__ thead,
                                                            const int32_t* __restrict__ next, int64_t cap, int64_t kmin,
                                                            int32_t* __restrict__ counts, int32_t* __restrict__ first,
-                                                           uint8_t* __restrict__ build_matched) {
+                                                           uint8_t* __restrict__ build_matched,
+                                                           const uint32_t* __restrict__ bits, uint64_t bmask) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
-    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin);
+    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin, bits, bmask);
     if (first) first[j] = h;
     if (counts) {
       int32_t c = 0;
@@ -126,9 +142,10 @@ __global__ __launch_bounds__(kBlock) void join_expand_kernel(const K* __restrict
                                                             const int32_t* __restrict__ next, int64_t cap, int64_t kmin,
                                                             const int64_t* __restrict__ offsets,
                                                             int32_t* __restrict__ out_probe,
-                                                            int32_t* __restrict__ out_build) {
+                                                            int32_t* __restrict__ out_build,
+                                                            const uint32_t* __restrict__ bits, uint64_t bmask) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
-    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin);
+    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin, bits, bmask);
     int64_t o = offsets[j];
     for (int32_t r = h; r != -1; r = next[r]) {
       out_probe[o] = (int32_t)j;
@@ -220,45 +237,47 @@ void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int3
 }
 
 void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
-                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, hipStream_t stream) {
+                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, uint32_t* bits,
+                uint64_t bmask, hipStream_t stream) {
   if (n == 0) return;
   dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
   if (key64) {
-    if (direct) hipLaunchKernelGGL((join_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
-    else hipLaunchKernelGGL((join_build_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
+    if (direct) hipLaunchKernelGGL((join_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
+    else hipLaunchKernelGGL((join_build_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
   } else {
-    if (direct) hipLaunchKernelGGL((join_build_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
-    else hipLaunchKernelGGL((join_build_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups);
+    if (direct) hipLaunchKernelGGL((join_build_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
+    else hipLaunchKernelGGL((join_build_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
   }
   check_launch("join_build", stream);
 }
 
 void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
-                int32_t* first, uint8_t* build_matched, hipStream_t stream) {
+                int32_t* first, uint8_t* build_matched, const uint32_t* bits, uint64_t bmask, hipStream_t stream) {
   if (m == 0) return;
   dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
   if (key64) {
-    if (direct) hipLaunchKernelGGL((join_probe_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
-    else hipLaunchKernelGGL((join_probe_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
+    if (direct) hipLaunchKernelGGL((join_probe_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
+    else hipLaunchKernelGGL((join_probe_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
   } else {
-    if (direct) hipLaunchKernelGGL((join_probe_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
-    else hipLaunchKernelGGL((join_probe_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched);
+    if (direct) hipLaunchKernelGGL((join_probe_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
+    else hipLaunchKernelGGL((join_probe_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
   }
   check_launch("join_probe", stream);
 }
 
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
-                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, hipStream_t stream) {
+                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, const uint32_t* bits, uint64_t bmask,
+                 hipStream_t stream) {
   if (m == 0) return;
   dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
   if (key64) {
-    if (direct) hipLaunchKernelGGL((join_expand_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
-    else hipLaunchKernelGGL((join_expand_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
+    if (direct) hipLaunchKernelGGL((join_expand_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
+    else hipLaunchKernelGGL((join_expand_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
   } else {
-    if (direct) hipLaunchKernelGGL((join_expand_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
-    else hipLaunchKernelGGL((join_expand_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build);
+    if (direct) hipLaunchKernelGGL((join_expand_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
+    else hipLaunchKernelGGL((join_expand_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
   }
   check_launch("join_expand", stream);
 }

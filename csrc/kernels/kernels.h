@@ -78,14 +78,18 @@ void hll_sketch(const void* keys, bool key64, const uint8_t* valid, int64_t n, u
                 hipStream_t stream);
 
 // ---- hashtable.hip -----------------------------------------------------------
+// bits/bmask: optional Bloom filter (bits: (bmask+1)/32 words, zeroed before
+// join_build; nullptr disables it on build or probe)
 void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
-                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, hipStream_t stream);
+                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, uint32_t* bits,
+                uint64_t bmask, hipStream_t stream);
 void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
-                int32_t* first, uint8_t* build_matched, hipStream_t stream);
+                int32_t* first, uint8_t* build_matched, const uint32_t* bits, uint64_t bmask, hipStream_t stream);
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
-                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, hipStream_t stream);
+                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, const uint32_t* bits, uint64_t bmask,
+                 hipStream_t stream);
 // run ids of a non-decreasing key column: gid[i] = r for rows in [starts[r], starts[r+1])
 void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int32_t* gid, hipStream_t stream);
 void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,

@@ -527,6 +527,25 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             sel = mask_to_indices(matched if kind == "semi" else ~matched)
         with ctx.span("join.gather"):
             return _take_batch(lb, sel)
+    if kind == "left" and residual is None and n_l and n_r > 4 * n_l:
+        # LEFT JOIN against a much larger relation (TPC-H Q13: customer ⟕ orders):
+        # build on the preserved side, stream the big side through it, then
+        # append the preserved rows nothing matched
+        with ctx.span("join.build"):
+            table = H.JoinTable(lk, lvalid)
+        matched = torch.zeros(n_l, dtype=torch.bool, device=dev)
+        with ctx.span("join.probe"):
+            if table.unique:
+                first = table.probe_first(rk, rvalid, build_matched=matched)
+                ridx = mask_to_indices(first >= 0)
+                lidx = first.index_select(0, ridx.long())
+            else:
+                ridx, lidx, _ = table.probe_pairs(rk, rvalid, build_matched=matched)
+            miss = mask_to_indices(~matched)
+        with ctx.span("join.gather"):
+            all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
+            all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
+            return _combine(lb, rb, all_l, all_r, True)
     if kind == "inner" and residual is None and n_l < n_r:
         # build on the smaller side
         out = hash_join(rb, lb, "inner", [(b, a) for a, b in on], None, ctx)

@@ -18,6 +18,8 @@ from .select import exclusive_scan, mask_to_indices
 
 EMPTY_KEY = -(2**63)
 INT32_MAX = 2**31 - 1
+BLOOM_MAX_KEYS = 4 << 20   # build sides up to this size get a Bloom filter
+BLOOM_MIN_RATIO = 4        # ... used when probe rows >= ratio x build rows
 
 
 def _next_pow2(x: int) -> int:
@@ -69,13 +71,20 @@ class JoinTable:
             return
         N = launch("join_build")
         self.cap = span if self.direct else _next_pow2(2 * n)
+        # Bloom filter for selective probes: ~8 bits per key, at most 4 MB (L2-resident)
+        self.bits, self.bmask = None, 0
+        if n <= BLOOM_MAX_KEYS:
+            nbits = min(max(_next_pow2(8 * n), 1 << 15), 1 << 25)
+            self.bits = torch.zeros(nbits // 32, dtype=torch.int32, device=self.device)
+            self.bmask = nbits - 1
         self.thead = torch.full((self.cap,), -1, dtype=torch.int32, device=self.device)
         self.tkeys = (torch.empty(1, dtype=torch.int64, device=self.device) if self.direct
                       else torch.full((self.cap,), EMPTY_KEY, dtype=torch.int64, device=self.device))
         self.next = torch.empty(n, dtype=torch.int32, device=self.device)
         dups = torch.zeros(1, dtype=torch.int64, device=self.device)
         N.join_build(ptr(keys), keys.dtype == torch.int64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead),
-                     ptr(self.next), self.cap, self.kmin, self.direct, ptr(dups), stream(keys))
+                     ptr(self.next), self.cap, self.kmin, self.direct, ptr(dups), ptr(self.bits), self.bmask,
+                     stream(keys))
         self.unique = int(dups.item()) == 0
 
     # ----------------------------------------------------------------- probes
@@ -96,8 +105,10 @@ class JoinTable:
             return first
         first = torch.empty(m, dtype=torch.int32, device=pkeys.device)
         N = launch("join_probe")
+        bits, bmask = self._bloom(m)
         N.join_probe(ptr(pkeys), pkeys.dtype == torch.int64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead),
-                     ptr(self.next), self.cap, self.kmin, self.direct, 0, ptr(first), ptr(build_matched), stream(pkeys))
+                     ptr(self.next), self.cap, self.kmin, self.direct, 0, ptr(first), ptr(build_matched), bits, bmask,
+                     stream(pkeys))
         return first
 
     def probe_pairs(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
@@ -125,16 +136,24 @@ class JoinTable:
         s = stream(pkeys)
         counts = torch.empty(m, dtype=torch.int32, device=dev)
         k64 = pkeys.dtype == torch.int64
+        bits, bmask = self._bloom(m)
         N.join_probe(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.next), self.cap,
-                     self.kmin, self.direct, ptr(counts), 0, ptr(build_matched), s)
+                     self.kmin, self.direct, ptr(counts), 0, ptr(build_matched), bits, bmask, s)
         offsets, total = exclusive_scan(counts)
         pidx = torch.empty(total, dtype=torch.int32, device=dev)
         bidx = torch.empty(total, dtype=torch.int32, device=dev)
         if total:
             launch("join_expand")
             N.join_expand(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.next), self.cap,
-                          self.kmin, self.direct, ptr(offsets), ptr(pidx), ptr(bidx), s)
+                          self.kmin, self.direct, ptr(offsets), ptr(pidx), ptr(bidx), bits, bmask, s)
         return pidx, bidx, counts
+
+    def _bloom(self, m: int) -> Tuple[int, int]:
+        """Use the Bloom filter only when the probe side is much larger than the
+        build side (then most probes are expected to miss)."""
+        if self.bits is not None and m >= BLOOM_MIN_RATIO * self.n:
+            return ptr(self.bits), self.bmask
+        return 0, 0
 
     # ------------------------------------------------------------ cpu helpers
     def _cpu_ranges(self, pkeys, pvalid):
