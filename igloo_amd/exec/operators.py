@@ -509,6 +509,10 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             lk = lk.index_select(0, keep.long())
             lvalid = None
             n_l = lb.num_rows
+    if dev.type == "cuda" and len(on) == 1 and kind in ("inner", "semi", "anti", "left") and not null_aware:
+        out = _sorted_join(lb, rb, lk, rk, lvalid, rvalid, kind, residual, ctx)
+        if out is not None:
+            return out
     if kind in ("semi", "anti") and not null_aware and n_l and n_r > 4 * n_l:
         # EXISTS against a much larger relation (TPC-H Q21/Q4 shapes): build on
         # the small probe side, stream the big side through it and flag the
@@ -613,6 +617,73 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
     if kind == "anti":
         return _take_batch(lb, mask_to_indices(counts == 0))
     raise NotSupported(f"join kind {kind}")
+
+
+#: big side of a join at least this large is checked for a sorted key column
+SORTED_JOIN_MIN_ROWS = 1 << 22
+
+
+def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residual, ctx) -> Optional[Batch]:
+    """Join against a big side whose key column is sorted (clustered tables:
+    lineitem by l_orderkey, orders by o_orderkey, and every filtered / joined
+    batch that preserved that order). The small side binary-searches its key
+    range in the big side instead of hashing and streaming the big side
+    (TPC-H Q21: 1.5M probes into 600M lineitem rows instead of 980M probes),
+    and the output stays in key order, which the GROUP BY then exploits.
+    Returns None when the shape does not apply."""
+    n_l, n_r = lb.num_rows, rb.num_rows
+    if n_l == 0 or n_r == 0:
+        return None
+    big_right = n_r >= n_l if kind == "inner" else True
+    big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
+    nb, ns = big.numel(), small.numel()
+    if nb < SORTED_JOIN_MIN_ROWS or 4 * ns > nb or bvalid is not None:
+        return None
+    with ctx.span("join.sorted_check"):
+        if not H.is_sorted(big):
+            return None
+    dev = ctx.device
+    with ctx.span("join.sorted_search"):
+        q = small.to(big.dtype)
+        lo = torch.searchsorted(big, q)
+        hi = torch.searchsorted(big, q, right=True)
+        cnt = hi - lo
+        if svalid is not None:
+            cnt = torch.where(svalid, cnt, torch.zeros_like(cnt))
+    if kind in ("semi", "anti") and residual is None:
+        with ctx.span("join.gather"):
+            m = cnt > 0
+            return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
+    with ctx.span("join.sorted_expand"):
+        total = int(cnt.sum().item())
+        it = torch.int32 if max(total, nb, ns) < 2**31 - 1 else torch.int64
+        sidx = torch.repeat_interleave(torch.arange(ns, device=dev, dtype=it), cnt, output_size=total)
+        starts = torch.cumsum(cnt, 0) - cnt
+        bidx = (lo.index_select(0, sidx.long()) - starts.index_select(0, sidx.long())
+                + torch.arange(total, device=dev, dtype=torch.int64)).to(it)
+        lidx, ridx = (sidx, bidx) if big_right else (bidx, sidx)
+    if residual is not None:
+        with ctx.span("join.residual"):
+            pair = _combine(lb, rb, lidx, ridx, False)
+            keep = mask_to_indices(ctx.evaluator.mask(residual, pair))
+            lidx = lidx.index_select(0, keep.long())
+            ridx = ridx.index_select(0, keep.long())
+            if kind == "inner":
+                return _take_batch(pair, keep)
+    if kind == "inner":
+        with ctx.span("join.gather"):
+            return _combine(lb, rb, lidx, ridx, False)
+    hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
+    hit[lidx.long()] = True
+    if kind == "semi":
+        return _take_batch(lb, mask_to_indices(hit))
+    if kind == "anti":
+        return _take_batch(lb, mask_to_indices(~hit))
+    # left join, big right side
+    miss = mask_to_indices(~hit)
+    all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
+    all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
+    return _combine(lb, rb, all_l, all_r, True)
 
 
 def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:

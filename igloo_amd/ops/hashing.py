@@ -178,6 +178,20 @@ class JoinTable:
 #: inputs at least this large are checked for sorted (clustered) keys first
 SORTED_CHECK_ROWS = 1 << 20
 
+def is_sorted(keys: torch.Tensor) -> bool:
+    """Non-decreasing check (one pass; remembered on the tensor object, so the
+    resident key columns of a table are checked once)."""
+    hit = getattr(keys, "_igloo_sorted", None)
+    if hit is not None:
+        return hit
+    n = keys.numel()
+    r = True if n < 2 else bool((keys[1:] >= keys[:-1]).all().item())
+    try:
+        keys._igloo_sorted = r
+    except (AttributeError, RuntimeError):
+        pass
+    return r
+
 
 def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, bool]:
     """``group_ids`` plus whether the ids are non-decreasing. Clustered keys
@@ -186,7 +200,7 @@ def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, b
     keys = _keys_ok(keys)
     n = keys.numel()
     if n >= SORTED_CHECK_ROWS and is_gpu(keys):
-        if bool((keys[1:] >= keys[:-1]).all().item()):
+        if is_sorted(keys):
             bound = torch.empty(n, dtype=torch.bool, device=keys.device)
             bound[0] = True
             torch.ne(keys[1:], keys[:-1], out=bound[1:])
