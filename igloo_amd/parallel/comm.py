@@ -33,6 +33,9 @@ class Communicator:
         self.device = torch.device(device)
         self.group = group
         self.backend = backend
+        # gloo moves host tensors only: device data is staged through the host
+        # (used to rehearse multi-rank GPU code paths on a single GPU)
+        self.wire = torch.device("cpu") if backend == "gloo" else self.device
         self.bytes_sent = 0
         self.calls = 0
 
@@ -47,13 +50,14 @@ class Communicator:
             device = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
         device = torch.device(device)
         if backend is None:
-            backend = "nccl" if device.type == "cuda" else "gloo"
+            backend = os.environ.get("IGLOO_COMM_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = {}
             if device.type == "cuda":
                 torch.cuda.set_device(device)
-                kw["device_id"] = device
+                if backend == "nccl":
+                    kw["device_id"] = device
             dist.init_process_group(backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         return Communicator(dist.get_rank(), dist.get_world_size(), device, None, backend)
@@ -68,7 +72,7 @@ class Communicator:
 
     # ------------------------------------------------------------ primitives
     def _t(self, x, dtype=torch.int64) -> torch.Tensor:
-        return torch.as_tensor(x, dtype=dtype, device=self.device)
+        return torch.as_tensor(x, dtype=dtype, device=self.wire)
 
     def barrier(self):
         if self.world_size > 1:
@@ -99,9 +103,9 @@ class Communicator:
         """Element-wise max over ranks (in a 32-bit copy: portable across backends)."""
         if self.world_size == 1:
             return t
-        w = t.to(torch.int32)
+        w = t.to(device=self.wire, dtype=torch.int32)
         dist.all_reduce(w, op=dist.ReduceOp.MAX, group=self.group)
-        return w.to(t.dtype)
+        return w.to(device=t.device, dtype=t.dtype)
 
     def allgather_ints(self, xs: Sequence[int]) -> List[List[int]]:
         """Every rank contributes len(xs) ints; returns [rank][i]."""
@@ -109,7 +113,7 @@ class Communicator:
         if self.world_size == 1:
             return [list(map(int, xs))]
         t = self._t([int(x) for x in xs])
-        out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.device)
+        out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.wire)
         dist.all_gather_into_tensor(out, t, group=self.group)
         v = out.tolist()
         return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
@@ -131,11 +135,8 @@ class Communicator:
             m = self.all_to_all_counts(send_counts)
             recv_counts = m
         tail = tuple(t.shape[1:])
-        out = torch.empty((sum(recv_counts),) + tail, dtype=t.dtype, device=t.device)
-        row = 1
-        for d in tail:
-            row *= d
-        src = t.contiguous()
+        out = torch.empty((sum(recv_counts),) + tail, dtype=t.dtype, device=self.wire)
+        src = t.contiguous().to(self.wire)
         if src.dtype == torch.bool:
             src = src.view(torch.uint8)
             out = out.view(torch.uint8)
@@ -144,12 +145,12 @@ class Communicator:
         self.bytes_sent += src.numel() * src.element_size()
         if t.dtype == torch.bool:
             out = out.view(torch.bool)
-        return out, list(recv_counts)
+        return out.to(t.device), list(recv_counts)
 
     def all_to_all_counts(self, send_counts: Sequence[int]) -> List[int]:
         W = self.world_size
         s = self._t(list(send_counts))
-        r = torch.empty(W, dtype=torch.int64, device=self.device)
+        r = torch.empty(W, dtype=torch.int64, device=self.wire)
         dist.all_to_all_single(r, s, group=self.group)
         return [int(x) for x in r.tolist()]
 
@@ -169,7 +170,10 @@ class Communicator:
 
     def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:
-            dist.broadcast(t, src, group=self.group)
+            w = t.to(self.wire)
+            dist.broadcast(w, src, group=self.group)
+            if w is not t:
+                t.copy_(w)
         return t
 
 

@@ -19,16 +19,23 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path, sf, queries):
+def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_thresholds=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import igloo_amd as ig
     from igloo_amd.models.tpch import datagen
     from igloo_amd.models.tpch import queries as Q
     from igloo_amd.parallel.comm import Communicator
-    comm = Communicator.init(backend="gloo", device="cpu", timeout_s=90)
-    e = ig.QueryEngine(device="cpu", comm=comm)
-    for name, t in datagen.generate(sf, "cpu", rank, world).items():
+    if low_thresholds:
+        # small data must still take the large-data paths (sorted joins, run ids, Bloom probes)
+        from igloo_amd.exec import operators as O
+        from igloo_amd.ops import hashing as H
+        O.SORTED_JOIN_MIN_ROWS = 1000
+        H.SORTED_CHECK_ROWS = 1000
+        H.BLOOM_MIN_RATIO = 2
+    comm = Communicator.init(backend="gloo", device=device, timeout_s=120)
+    e = ig.QueryEngine(device=device, comm=comm)
+    for name, t in datagen.generate(sf, device, rank, world).items():
         e.register_table(name, t)
     res = {}
     for q in queries:
@@ -44,16 +51,27 @@ def _worker(rank, world, port, out_path, sf, queries):
     comm.shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_tpch_distributed_gloo(world, tpch_cpu):
+def run_distributed(world, con, device="cpu", low_thresholds=False):
+    """Run TPC-H 1-22 on ``world`` ranks (gloo) and compare rank 0 with sqlite."""
     from igloo_amd.models.tpch import oracle
-    _, _, con = tpch_cpu
     qs = list(range(1, 23))
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.json")
-        mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs), nprocs=world, join=True,
-                           start_method="spawn")
+        mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs, device, low_thresholds), nprocs=world,
+                           join=True, start_method="spawn")
         res = json.load(open(out))
+    return check(res, qs, con)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tpch_distributed_gloo(world, tpch_cpu):
+    _, _, con = tpch_cpu
+    bad = run_distributed(world, con)
+    assert not bad, "\n".join(bad)
+
+
+def check(res, qs, con):
+    from igloo_amd.models.tpch import oracle
     bad = []
     for q in qs:
         r = res[str(q)]
@@ -65,7 +83,7 @@ def test_tpch_distributed_gloo(world, tpch_cpu):
         d = oracle.rows_match(got, exp)
         if d:
             bad.append(f"Q{q}: {d}")
-    assert not bad, "\n".join(bad)
+    return bad
 
 
 def _num(x):

@@ -39,3 +39,14 @@ def test_native_kernels_were_used(tpch_gpu):
     from igloo_amd.ops._lib import KERNEL_CALLS
     for k in ("select", "join_build", "join_probe", "groupby", "agg_update", "gather_multi"):
         assert KERNEL_CALLS[k] > 0, f"{k} never launched: {dict(KERNEL_CALLS)}"
+
+
+def test_tpch_distributed_gpu_ranks(tpch_cpu):
+    """Two SPMD ranks sharing the one GPU (gloo, collectives staged through the
+    host): exercises every GPU-only operator path (fused scans, sorted joins,
+    run-id group-by, HLL NDV merges, runtime filters) under hash partitioning,
+    shuffles and two-phase aggregation — the code the 8-GPU RCCL run takes."""
+    import test_distributed_cpu as D
+    _, _, con = tpch_cpu
+    bad = D.run_distributed(2, con, device="cuda:0", low_thresholds=True)
+    assert not bad, "\n".join(bad)
