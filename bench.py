@@ -57,13 +57,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    device = "cpu" if a.cpu else f"cuda:{local}"
+    # IGLOO_BENCH_SHARE_GPU=1: every rank on cuda:0 with host-staged gloo
+    # collectives — a rehearsal of the multi-rank path on a one-GPU box
+    shared = os.environ.get("IGLOO_BENCH_SHARE_GPU") == "1"
+    device = "cpu" if a.cpu else ("cuda:0" if shared else f"cuda:{local}")
     if not a.cpu:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(torch.device(device))
     comm = None
     if world > 1:
         from igloo_amd.parallel.comm import Communicator
-        comm = Communicator.init(backend="gloo" if a.cpu else "nccl", device=device)
+        comm = Communicator.init(backend="gloo" if (a.cpu or shared) else "nccl", device=device)
 
     def barrier():
         if comm is not None:
