@@ -213,6 +213,18 @@ class QueryEngine:
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows}
         return QueryResult(table, ms)
 
+    def explain_fragments(self, sql: str, workers=("all-ranks",)) -> str:
+        """Stage DAG of ``sql`` (fragments, placement, exchanges)."""
+        from .parallel.fragments import DistributedPlanner, explain_fragments
+        plan, _ = self.logical_plan(sql)
+        return explain_fragments(DistributedPlanner(workers).plan(plan))
+
+    def execute_logical(self, plan: Plan, names: Optional[List[str]] = None) -> pa.Table:
+        """Run an (optimized) logical plan — e.g. one deserialized from a fragment
+        request — and return its Arrow result."""
+        names = names or [c.name for c in plan.schema]
+        return self._to_arrow(self._execute_plan(plan), plan.schema, names)
+
     def make_context(self, analyze: bool = False) -> ExecContext:
         return ExecContext(self, self.device, self.comm, analyze)
 

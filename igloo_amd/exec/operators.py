@@ -249,6 +249,20 @@ class LazyBatch(Batch):
         return self._get().num_rows
 
 
+class FragmentInputExec(ExecNode):
+    """Output of another query fragment, materialized by the fragment scheduler."""
+
+    def __init__(self, logical: L.FragmentRef):
+        self.logical = logical
+        self.children = []
+
+    def _run(self, ctx):
+        inputs = getattr(ctx, "fragment_inputs", None) or {}
+        if self.logical.fragment_id not in inputs:
+            raise ExecutionError(f"input of fragment {self.logical.fragment_id} is not available")
+        return inputs[self.logical.fragment_id]
+
+
 class ValuesExec(ExecNode):
     def __init__(self, logical: L.Values):
         self.logical = logical

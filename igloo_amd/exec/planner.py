@@ -10,8 +10,8 @@ from __future__ import annotations
 from ..columnar import Batch
 from ..sql import logical as L
 from ..utils.errors import NotSupported
-from .operators import (ExecContext, ExecNode, FilterExec, HashAggExec, HashJoinExec, LimitExec, MultiJoinExec,
-                        ProjectExec, ScanExec, SortExec, UnionExec, ValuesExec)
+from .operators import (ExecContext, ExecNode, FilterExec, FragmentInputExec, HashAggExec, HashJoinExec, LimitExec,
+                        MultiJoinExec, ProjectExec, ScanExec, SortExec, UnionExec, ValuesExec)
 
 
 def create_physical_plan(p: L.Plan) -> ExecNode:
@@ -35,6 +35,8 @@ def create_physical_plan(p: L.Plan) -> ExecNode:
         return LimitExec(p, create_physical_plan(p.input))
     if isinstance(p, L.Union):
         return UnionExec(p, [create_physical_plan(c) for c in p.children])
+    if isinstance(p, L.FragmentRef):
+        return FragmentInputExec(p)
     raise NotSupported(f"no physical operator for {type(p).__name__}")
 
 

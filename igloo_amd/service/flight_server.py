@@ -53,13 +53,15 @@ class IglooFlightServer(fl.FlightServerBase):
 
     def __init__(self, engine, location: str = "grpc://127.0.0.1:50051", registry=None,
                  runner: Optional[Callable[[str], pa.Table]] = None, auth_token: Optional[str] = None,
-                 task_handler: Optional[Callable[[P.TaskDefinition], P.TaskStatus]] = None, **kw):
+                 task_handler: Optional[Callable[[P.TaskDefinition], P.TaskStatus]] = None,
+                 fragment_runner: Optional[Callable[[bytes], pa.Table]] = None, **kw):
         mw = {"auth": _TokenMiddlewareFactory(auth_token)} if auth_token else None
         super().__init__(location, middleware=mw, **kw)
         self.engine = engine
         self.registry = registry
         self.runner = runner
         self.task_handler = task_handler
+        self.fragment_runner = fragment_runner
         self._pending: Dict[str, Tuple[str, float]] = {}
         self._results: Dict[str, pa.Table] = {}
         self._lock = threading.Lock()
@@ -186,7 +188,7 @@ class IglooFlightServer(fl.FlightServerBase):
         return [("register_worker", "WorkerInfo -> RegistrationAck"), ("heartbeat", "HeartbeatInfo -> HeartbeatResponse"),
                 ("execute_task", "TaskDefinition -> TaskStatus"), ("get_data_for_task", "DataForTaskRequest -> IPC"),
                 ("list_workers", "-> workers JSON"), ("metrics", "-> metrics JSON"), ("explain", "SQL -> plan text"),
-                ("health", "-> ok")]
+                ("execute_fragment", "serialized fragment + input IPC -> IPC"), ("health", "-> ok")]
 
     def do_action(self, context, action):
         kind, body = action.type, action.body.to_pybytes() if action.body is not None else b""
@@ -230,6 +232,17 @@ class IglooFlightServer(fl.FlightServerBase):
             yield fl.Result(json.dumps(m, default=str).encode())
         elif kind == "explain":
             yield fl.Result(self.engine.explain(body.decode()).encode())
+        elif kind == "execute_fragment":
+            if self.fragment_runner is not None:
+                t = self.fragment_runner(body)
+            else:
+                from ..parallel.fragments import run_encoded_fragment
+                t = run_encoded_fragment(self.engine, body)
+            self.metrics["fragments"] = self.metrics.get("fragments", 0) + 1
+            sink = pa.BufferOutputStream()
+            with pa.ipc.new_stream(sink, t.schema) as w:
+                w.write_table(t)
+            yield fl.Result(sink.getvalue())
         elif kind == "health":
             yield fl.Result(b"ok")
         else:

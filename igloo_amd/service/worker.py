@@ -72,17 +72,27 @@ class WorkerGroup:
                 self._bcast(("query", sql))
             return self.engine.query(sql)
 
+    def run_spmd_fragment(self, payload: bytes) -> pa.Table:
+        from ..parallel.fragments import run_encoded_fragment
+        with self._lock:
+            if self.world > 1:
+                self._bcast(("fragment", payload))
+            return run_encoded_fragment(self.engine, payload)
+
     def follower_loop(self):
         """Ranks > 0: execute whatever rank 0 broadcasts."""
+        from ..parallel.fragments import run_encoded_fragment
         while True:
             cmd = self._bcast()
             if cmd[0] == "shutdown":
                 return
-            if cmd[0] == "query":
-                try:
+            try:
+                if cmd[0] == "query":
                     self.engine.query(cmd[1])
-                except Exception as e:  # noqa: BLE001 - rank 0 reports the error to the client
-                    log.warning("rank %d: query failed: %s", self.rank, e)
+                elif cmd[0] == "fragment":
+                    run_encoded_fragment(self.engine, cmd[1])
+            except Exception as e:  # noqa: BLE001 - rank 0 reports the error to the client
+                log.warning("rank %d: %s failed: %s", self.rank, cmd[0], e)
 
     # ------------------------------------------------------------- rank 0
     def devices(self) -> list:
@@ -100,7 +110,7 @@ class WorkerGroup:
     def start_server(self):
         from .flight_server import IglooFlightServer
         self.server = IglooFlightServer(self.engine, f"grpc://{self.host}:{self.port}", runner=self.run_spmd,
-                                        auth_token=self.token)
+                                        auth_token=self.token, fragment_runner=self.run_spmd_fragment)
         self.port = self.server.port
         self.address = f"grpc://{self.host}:{self.port}"
         self.server.start_background(host=self.host)

@@ -205,6 +205,17 @@ class MultiJoin(Plan):
 
 
 @dataclass(eq=False)
+class FragmentRef(Plan):
+    """Leaf standing for the materialized output of another query fragment
+    (igloo_amd.parallel.fragments)."""
+    fragment_id: str
+    schema: List[ColInfo]
+
+    def label(self):
+        return f"FragmentRef: {self.fragment_id[:8]}"
+
+
+@dataclass(eq=False)
 class Aggregate(Plan):
     input: Plan
     groups: List[Tuple[ColInfo, Expr]]
