@@ -107,6 +107,8 @@ def main():
             print(f"[bench] warmup {w}: {time.perf_counter() - tw:.3f}s", file=sys.stderr, flush=True)
     per_q = {} if a.per_query else None
     barrier()
+    if os.environ.get("IGLOO_PROF_GAP"):
+        time.sleep(1.0)   # idle gap that scripts/kernel_summary.py uses to isolate the timed steps in a trace
     t1 = time.perf_counter()
     for s in range(a.steps):
         suite(per_q)

@@ -270,6 +270,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("str_hash64", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t valid, uintptr_t out, uintptr_t s) {
     kern::str_hash64(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(valid), P<int64_t>(out), S(s));
   });
+  m.def("str_like_segments", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t seg, uintptr_t seg_off, int nseg,
+                                 bool anchor_start, bool anchor_end, bool negate, uintptr_t out, uintptr_t s) {
+    kern::str_like_segments(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(seg),
+                            P<const int32_t>(seg_off), nseg, anchor_start, anchor_end, negate, P<uint8_t>(out), S(s));
+  });
   m.def("str_eq_rows", [](uintptr_t aoff, uintptr_t achars, uintptr_t ai, uintptr_t boff, uintptr_t bchars, uintptr_t bi,
                           bool idx64, int64_t n, uintptr_t mism, uintptr_t s) {
     kern::str_eq_rows(P<const int64_t>(aoff), P<const uint8_t>(achars), P<const void>(ai), P<const int64_t>(boff),

@@ -145,6 +145,10 @@ void str_substr_lengths(const int64_t* off, const uint8_t* chars, int64_t n, int
                         int64_t* out_len, hipStream_t stream);
 void str_substr_copy(const int64_t* off, const uint8_t* chars, int64_t n, int64_t start, int64_t len, bool has_len,
                      const int64_t* new_off, uint8_t* out, hipStream_t stream);
+// LIKE made of '%'-separated literals (no '_'): segments concatenated in `seg`
+// with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%'
+void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
+                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, hipStream_t stream);
 void str_hash64(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* valid, int64_t* out,
                 hipStream_t stream);
 void str_eq_rows(const int64_t* aoff, const uint8_t* achars, const void* ai, const int64_t* boff, const uint8_t* bchars,

@@ -107,6 +107,160 @@ __global__ __launch_bounds__(kBlock) void like_tile_kernel(const int64_t* __rest
   }
 }
 
+// LIKE over '%'-separated literal segments (no '_', case-sensitive) — the
+// shape of nearly every analytic LIKE: 'PROMO%', '%BRASS', '%green%',
+// '%special%requests%'. Per tile of 256 strings staged in LDS:
+//   1. every lane takes 16-byte chunks of the tile and marks, for every
+//      segment, the positions where it starts: 4-byte windows built with
+//      v_alignbyte from five dwords are compared against the segment prefix in
+//      registers, the rare candidates are verified byte-wise, and the 16-bit
+//      mask goes to an LDS bitmap (one LDS read per 16 positions);
+//   2. each lane then walks its string greedily: the earliest hit of segment 0
+//      at/after the cursor, then segment 1 after that, ... using bit scans.
+constexpr int kSegMax = 4;
+constexpr int kSegBits = kLikeTileBytes / 64;  // 64-bit words per segment bitmap
+
+__device__ inline int next_hit(const uint64_t* bits, int from, int last) {
+  // smallest p in [from, last] with bit p set, or -1
+  if (from > last) return -1;
+  int w = from >> 6;
+  uint64_t word = bits[w] & (~0ULL << (from & 63));
+  const int lw = last >> 6;
+  while (true) {
+    if (word) {
+      const int p = (w << 6) + __builtin_ctzll(word);
+      return p <= last ? p : -1;
+    }
+    if (++w > lw) return -1;
+    word = bits[w];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void like_seg_kernel(const int64_t* __restrict__ off,
+                                                         const uint8_t* __restrict__ chars, int64_t n,
+                                                         const uint8_t* __restrict__ seg, const int32_t* seg_off,
+                                                         int nseg, bool anchor_start, bool anchor_end, bool negate,
+                                                         uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kLikeTileBytes + 64];
+  __shared__ uint64_t bits[kSegMax][kSegBits];
+  __shared__ uint8_t sseg[kLikeMaxPattern];
+  __shared__ int32_t soff[kSegMax + 1];
+  const int total = seg_off[nseg];
+  for (int i = threadIdx.x; i < total; i += kBlock) sseg[i] = seg[i];
+  if (threadIdx.x <= nseg) soff[threadIdx.x] = seg_off[threadIdx.x];
+  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t i0 = t * kBlock;
+    const int64_t i1 = i0 + kBlock < n ? i0 + kBlock : n;
+    const uintptr_t lo = (uintptr_t)(chars + off[i0]);
+    const uintptr_t hi = (uintptr_t)(chars + off[i1]);
+    const uintptr_t start = lo & ~(uintptr_t)15;
+    const uintptr_t full_end = hi & ~(uintptr_t)15;
+    const int len = (int)(hi - start);
+    const bool staged = hi - start <= (uintptr_t)kLikeTileBytes;
+    __syncthreads();  // previous tile done; pattern visible on the first pass
+    if (staged) {
+      const int64_t nvec = (int64_t)(full_end - start) / 16;
+      for (int64_t v = threadIdx.x; v < nvec; v += kBlock) *(uint4*)(buf + v * 16) = *(const uint4*)(start + v * 16);
+      for (uintptr_t a = full_end + threadIdx.x; a < hi; a += kBlock) buf[a - start] = *(const uint8_t*)a;
+      if (threadIdx.x < 64) buf[len + threadIdx.x] = 0;  // pad: comparisons may read past the tile end
+      __syncthreads();
+      // each lane tests the 16 positions of one 16-byte chunk against every
+      // segment's 4-byte prefix in registers (v_alignbyte windows), verifies
+      // the rare candidates byte-wise, and stores a 16-bit hit mask
+      const int nchunks = ((len + 63) >> 6) * 4;
+      for (int j = threadIdx.x; j < nchunks; j += kBlock) {
+        const uint4 v = *(const uint4*)(buf + j * 16);
+        const uint32_t d[5] = {v.x, v.y, v.z, v.w, *(const uint32_t*)(buf + j * 16 + 16)};
+        for (int sg = 0; sg < nseg; ++sg) {
+          const int s0 = soff[sg], sl = soff[sg + 1] - s0;
+          const int pl = sl < 4 ? sl : 4;
+          uint32_t pref = 0;
+          for (int k = 0; k < pl; ++k) pref |= (uint32_t)sseg[s0 + k] << (8 * k);
+          const uint32_t pmask = pl == 4 ? 0xffffffffu : ((1u << (8 * pl)) - 1);
+          uint32_t m = 0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3);
+            m |= (uint32_t)((w & pmask) == pref) << q;
+          }
+          const int base = j * 16;
+          const int room = len - sl - base + 1;  // positions base+q with q < room fit in the tile
+          m &= room >= 16 ? 0xffffu : room <= 0 ? 0u : ((1u << room) - 1);
+          if (sl > 4) {
+            for (uint32_t c = m; c; c &= c - 1) {
+              const int q = __builtin_ctz(c);
+              for (int k = 4; k < sl; ++k)
+                if (buf[base + q + k] != sseg[s0 + k]) {
+                  m &= ~(1u << q);
+                  break;
+                }
+            }
+          }
+          ((uint16_t*)bits[sg])[j] = (uint16_t)m;
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t i = i0 + threadIdx.x;
+    if (i < i1) {
+      const int64_t a = off[i], e = off[i + 1];
+      bool r;
+      if (staged) {
+        const int b0 = (int)((uintptr_t)(chars + a) - start), b1 = (int)((uintptr_t)(chars + e) - start);
+        int cur = b0;
+        r = true;
+        for (int sg = 0; sg < nseg && r; ++sg) {
+          const int sl = soff[sg + 1] - soff[sg];
+          const bool last = sg == nseg - 1;
+          if (sg == 0 && anchor_start) {
+            r = cur + sl <= b1 && ((bits[0][cur >> 6] >> (cur & 63)) & 1ULL);
+            cur += sl;
+          } else if (last && anchor_end) {
+            const int p = b1 - sl;
+            r = p >= cur && ((bits[sg][p >> 6] >> (p & 63)) & 1ULL);
+            cur = b1;
+          } else {
+            const int p = next_hit(bits[sg], cur, b1 - sl);
+            r = p >= 0;
+            cur = p + sl;
+          }
+        }
+        if (r && anchor_end && (nseg == 0 || (nseg == 1 && anchor_start))) r = cur == b1;
+      } else {
+        // oversized tile: literal-by-literal search in global memory
+        const uint8_t* s = chars + a;
+        const int64_t L = e - a;
+        int64_t cur = 0;
+        r = true;
+        for (int sg = 0; sg < nseg && r; ++sg) {
+          const int s0 = soff[sg], sl = soff[sg + 1] - s0;
+          const bool last = sg == nseg - 1;
+          auto eq = [&](int64_t p) {
+            for (int k = 0; k < sl; ++k)
+              if (s[p + k] != sseg[s0 + k]) return false;
+            return true;
+          };
+          if (sg == 0 && anchor_start) {
+            r = cur + sl <= L && eq(cur);
+            cur += sl;
+          } else if (last && anchor_end) {
+            r = L - sl >= cur && eq(L - sl);
+            cur = L;
+          } else {
+            int64_t p = cur;
+            while (p + sl <= L && !eq(p)) ++p;
+            r = p + sl <= L;
+            cur = p + sl;
+          }
+        }
+        if (r && anchor_end && (nseg == 0 || (nseg == 1 && anchor_start))) r = cur == L;
+      }
+      out[i] = r != negate;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void case_kernel(const uint8_t* __restrict__ in, int64_t nbytes, bool to_upper,
                                                      uint8_t* __restrict__ out, int* __restrict__ non_ascii) {
   int found = 0;
@@ -260,6 +414,15 @@ void str_like(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t
     hipLaunchKernelGGL(like_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, off, chars, n, pat, kind,
                        m, case_insensitive, negate, out);
   check_launch("str_like", stream);
+}
+
+void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
+                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, hipStream_t stream) {
+  if (n == 0) return;
+  if (nseg > kSegMax) throw std::runtime_error("str_like_segments: too many segments");
+  hipLaunchKernelGGL(like_seg_kernel, dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock), 0, stream, off, chars, n,
+                     seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  check_launch("str_like_segments", stream);
 }
 
 void str_case(const uint8_t* in, int64_t nbytes, bool to_upper, uint8_t* out, int* non_ascii, hipStream_t stream) {

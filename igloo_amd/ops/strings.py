@@ -53,6 +53,32 @@ def tokenize_like(pattern: str, escape: Optional[str] = "\\") -> Tuple[bytes, by
     return bytes(out), bytes(kinds)
 
 
+def _like_segments(pat: bytes, kinds: bytes):
+    """'%'-separated literal segments of a tokenized LIKE pattern, or None when
+    the pattern has '_' wildcards / too many or too long segments.
+    Returns (concatenated bytes, offsets, anchored_start, anchored_end)."""
+    if 1 in kinds:
+        return None
+    segs, cur = [], bytearray()
+    for b, k in zip(pat, kinds):
+        if k == 2:
+            if cur:
+                segs.append(bytes(cur))
+                cur = bytearray()
+        else:
+            cur.append(b)
+    if cur:
+        segs.append(bytes(cur))
+    a0 = not kinds or kinds[0] != 2
+    a1 = not kinds or kinds[-1] != 2
+    if len(segs) > 4 or sum(map(len, segs)) > 256 or (not segs and (a0 or a1)):
+        return None   # empty pattern '' (matches only empty strings) keeps the generic matcher
+    off = [0]
+    for sg in segs:
+        off.append(off[-1] + len(sg))
+    return b"".join(segs), off, a0, a1
+
+
 def like_regex(pattern: str, ci: bool = False, escape: Optional[str] = "\\") -> "re.Pattern":
     parts = []
     i = 0
@@ -95,6 +121,15 @@ def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, esca
         return torch.from_numpy(r.fill_null(False).to_numpy(zero_copy_only=False).astype(np.bool_))
     pat, kinds = tokenize_like(pattern, escape)
     dev = col.device
+    segs = None if ci else _like_segments(pat, kinds)
+    if segs is not None:
+        seg_bytes, seg_off, a0, a1 = segs
+        sb = torch.tensor(list(seg_bytes) or [0], dtype=torch.uint8).to(dev)
+        so = torch.tensor(seg_off, dtype=torch.int32).to(dev)
+        out = torch.empty(n, dtype=torch.bool, device=dev)
+        launch("str_like_segments").str_like_segments(ptr(col.offsets), ptr(col.data), n, ptr(sb), ptr(so),
+                                                      len(seg_off) - 1, a0, a1, negate, ptr(out), stream(out))
+        return out
     pt = torch.tensor(list(pat) or [0], dtype=torch.uint8).to(dev)
     kt = torch.tensor(list(kinds) or [0], dtype=torch.uint8).to(dev)
     out = torch.empty(n, dtype=torch.bool, device=dev)

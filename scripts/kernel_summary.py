@@ -1,0 +1,49 @@
+"""Per-kernel time of the timed steps from a rocprofv3 kernel trace.
+
+bench.py (with IGLOO_PROF_GAP=1) idles for 1 s between warmup and the timed
+steps; everything before the last gap > 0.5 s (data generation, warmup) is
+dropped, the rest is grouped by kernel name and divided by --steps.
+
+usage: python scripts/kernel_summary.py <run_kernel_trace.csv> [--steps N] [--top 30]
+"""
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    name = re.sub(r"^void ", "", name)
+    return name[:100]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--gap-ms", type=float, default=500.0)
+    a = ap.parse_args()
+    rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                   for r in csv.DictReader(open(a.trace))), key=lambda x: x[0])
+    cut = 0
+    for i in range(1, len(rows)):
+        if rows[i][0] - rows[i - 1][1] > a.gap_ms * 1e6:
+            cut = i
+    rows = rows[cut:]
+    tot, cnt = defaultdict(int), defaultdict(int)
+    for s, e, n in rows:
+        tot[short(n)] += e - s
+        cnt[short(n)] += 1
+    busy = sum(tot.values())
+    span = rows[-1][1] - rows[0][0] if rows else 0
+    print(f"kernels={len(rows)} busy={busy / 1e6 / a.steps:.2f} ms/step span={span / 1e6 / a.steps:.2f} ms/step "
+          f"(busy/span={busy / max(span, 1):.2f})")
+    print(f"{'ms/step':>9} {'calls':>6} {'us/call':>9}  kernel")
+    for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
+        print(f"{t / 1e6 / a.steps:9.3f} {cnt[n] // a.steps:6d} {t / 1e3 / cnt[n]:9.1f}  {n}")
+
+
+if __name__ == "__main__":
+    main()

@@ -138,13 +138,16 @@ def _words(n, seed=6):
 
 
 @pytest.mark.parametrize("pat", ["%special%requests%", "forest%", "%BRASS", "%", "", "_", "a\\_b\\%c%", "%n_c%",
-                                 "%Customer%Complaints%"])
+                                 "%Customer%Complaints%", "special", "spec%cial", "special%special", "%al%al%",
+                                 "%%", "%s", "f%n", "%e%e%e%e%", "%e%e%e%e%e%", "PROMO%", "%requests"])
 def test_like(gpu_device, pat):
+    # segment-bitmap kernel for '_'-free patterns, generic matcher otherwise
     vals = _words(20_000)
     c = _str_col(vals)
     ref = S.like(c, pat)
     got = S.like(c.to(DEV), pat).cpu()
     assert torch.equal(ref, got)
+    assert torch.equal(S.like(c, pat, negate=True), S.like(c.to(DEV), pat, negate=True).cpu())
 
 
 def test_like_long_strings_and_slices(gpu_device):
@@ -156,7 +159,7 @@ def test_like_long_strings_and_slices(gpu_device):
         w = " ".join(r.choice(WORDS, r.integers(0, 40 if i % 700 < 300 else 4)))
         vals.append(w)
     c = _str_col(vals)
-    for pat in ("%special%requests%", "%green", "Customer%", "%ü%"):
+    for pat in ("%special%requests%", "%green", "Customer%", "%ü%", "special%requests", "%s%s%", "%n_c%"):
         ref = S.like(c, pat)
         assert torch.equal(ref, S.like(c.to(DEV), pat).cpu())
     from igloo_amd.ops.gather import take
