@@ -125,12 +125,12 @@ PYBIND11_MODULE(_native, m) {
                       P<int32_t>(out_probe), P<int32_t>(out_build), P<const uint32_t>(bits), bmask, S(s));
   });
   // fused scan kernels. cols: [(ptr, width)], terms: [(col, kind, lo, hi, set)],
-  // keys: [(col, lo, mul)], aggs: [(op, checked, [(col, a, b)], dst, dst2)]
+  // keys: [(col, lo, mul)], aggs: [(op, checked, [(col, a, b)], dst, dst2, shared)]
   using FfCols = std::vector<std::pair<uintptr_t, int64_t>>;
   using FfTerms = std::vector<std::tuple<int, int, int64_t, int64_t, uint64_t>>;
   using FfKeys = std::vector<std::tuple<int, int64_t, int64_t>>;
   using FfAggs = std::vector<std::tuple<int, int, std::vector<std::tuple<int64_t, int64_t, int64_t>>, uintptr_t,
-                                        uintptr_t>>;
+                                        uintptr_t, int>>;
   auto make_ff = [](const FfCols& cols, const FfTerms& terms, uintptr_t mask) {
     if (cols.size() > (size_t)kern::kFfMaxCols || terms.size() > (size_t)kern::kFfMaxTerms)
       throw std::runtime_error("fused scan: too many columns / terms");
@@ -139,7 +139,7 @@ PYBIND11_MODULE(_native, m) {
     for (size_t i = 0; i < cols.size(); ++i) {
       f.cols[i].ptr = reinterpret_cast<const void*>(cols[i].first);
       f.cols[i].width = cols[i].second;
-      if (!(f.cols[i].width == 1 || f.cols[i].width == 2 || f.cols[i].width == 4 || f.cols[i].width == 8))
+      if (!(f.cols[i].width == 4 || f.cols[i].width == 8))  // the kernels load 4- or 8-byte words
         throw std::runtime_error("fused scan: bad column width");
     }
     f.nterms = (int32_t)terms.size();
@@ -173,12 +173,15 @@ PYBIND11_MODULE(_native, m) {
     f.ngroups = ngroups;
     f.naggs = (int32_t)aggs.size();
     for (size_t i = 0; i < aggs.size(); ++i) {
-      auto& [op, checked, facs, dst, dst2] = aggs[i];
+      auto& [op, checked, facs, dst, dst2, shared] = aggs[i];
       if (op < 0 || op > 3 || facs.size() > (size_t)kern::kFfMaxFactors)
         throw std::runtime_error("fused aggregate: bad aggregate");
+      if (shared < 0 || shared > (int)facs.size() || (shared > 0 && (i == 0 || f.aggs[i - 1].nfac != shared)))
+        throw std::runtime_error("fused aggregate: bad shared prefix");
       kern::FfAgg& A = f.aggs[i];
       A.op = op;
       A.checked = checked;
+      A.shared = shared;
       A.nfac = (int32_t)facs.size();
       for (size_t k = 0; k < facs.size(); ++k) {
         auto [col, a, b] = facs[k];

@@ -14,13 +14,22 @@
 //     gid = sum((k_i - lo_i) * mul_i) < 16;
 //   * aggregate = SUM / MIN / MAX of prod_{f<=3} (a_f + b_f * col_f) in exact
 //     int64 fixed point (optionally overflow-checked), or COUNT.
-// Every descriptor loop has a wave-uniform trip count, so the per-row code is
-// straight-line loads + compares + multiply-adds.
 //
-// Aggregation: each lane pre-reduces its kFfRows rows, the wave reduces each
-// (group, aggregate) with cross-lane shuffles (int128 sums exact through
-// 32-bit halves), lane 0 accumulates into wave-private LDS slots, and the
-// block merges its slots into global memory with one atomic per slot.
+// Code shape (what made these kernels VALU/SALU-bound before, and the fix):
+//   * descriptor loops are OUTER and the lane's kFfRows rows INNER (unrolled),
+//     so each term / factor / aggregate descriptor is fetched and branched on
+//     once per 4 rows instead of once per row;
+//   * a lane's rows live in one 8 x int64 register vector per row and a column
+//     is picked with a VGPR-indexed move (uniform index), not a select chain;
+//   * column addresses are a wave-uniform 64-bit base (SGPR) plus a 32-bit lane
+//     offset, so loads use the saddr form with no 64-bit multiply per load.
+//
+// Aggregation: every (aggregate, group) cell owns int64 slots in LDS indexed by
+// lane (shared by the block's waves; ds_add/ds_min/ds_max atomics), so a row
+// costs two LDS adds per SUM and no cross-lane traffic. SUMs stay exact: the
+// unsigned low and signed high 32-bit halves of each value go to separate slots
+// and the block merge recombines them in int128. Cells x lanes are sized to
+// the LDS budget (lanes share slots when there are many cells).
 #include "common.h"
 #include "kernels.h"
 
@@ -30,239 +39,231 @@ namespace kern {
 namespace {
 
 constexpr int kFfRows = 4;  // rows per lane per iteration (coalesced: base + j*64 + lane)
+static_assert(kFfMaxCols == 8 && kFfRows == 4, "row vectors are written for 8 columns x 4 rows");
+// row vector of VW >= NC int64 lanes (power of two, so a column index is masked, never out of range)
+template <int NC>
+constexpr int ff_vw() { return NC <= 1 ? 1 : NC <= 2 ? 2 : NC <= 4 ? 4 : 8; }
+template <int VW>
+using ff_vec = long long __attribute__((ext_vector_type(VW)));
 
 // Branch-free column load (int32 / int64 columns): two dword loads at
-// p + row*w and p + row*w + (w-4) (the same dword twice for int32 columns).
-// Keeping every load unconditional lets all of a row's loads be in flight at
-// once (a width switch per load made the compiler wait after each one).
-__device__ __forceinline__ int64_t ff_load(const FfColumn& c, int64_t row) {
-  const char* p = (const char*)c.ptr + row * c.width;
-  const uint32_t lo = *(const uint32_t*)p;
-  const uint32_t hi = *(const uint32_t*)(p + (c.width - 4));
+// p + idx*w and p + idx*w + (w-4) (the same dword twice for int32 columns);
+// p is the wave-uniform address of the iteration's first row. Keeping every
+// load unconditional lets all of a row's loads be in flight at once (a width
+// switch per load made the compiler wait after each one).
+__device__ __forceinline__ int64_t ff_load(const FfColumn& c, int64_t base, uint32_t idx) {
+  const int64_t w = c.width;
+  const char* p = (const char*)c.ptr + base * w;
+  const uint32_t off = idx << (w == 8 ? 3 : 2);
+  const uint32_t lo = *(const uint32_t*)(p + off);
+  const uint32_t hi = *(const uint32_t*)(p + (off + (uint32_t)(w - 4)));
   // both dwords are always consumed (a select let the compiler sink the second
   // load into a branch and wait on it): int32 columns sign-extend via shifts
   const int64_t v = (int64_t)(((uint64_t)hi << 32) | lo);
-  const int sh = c.width == 8 ? 0 : 32;
+  const int sh = w == 8 ? 0 : 32;
   return (int64_t)((uint64_t)v << sh) >> sh;
 }
 
-// Column values of one lane's rows as 32 named scalars (no array at all:
-// any dynamically indexed local array ended up in scratch). The wave-uniform
-// column number is resolved by a select chain over the static slots.
-#define FF_COLS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
-static_assert(kFfMaxCols == 8 && kFfRows == 4, "FfRowVals is written for 8 columns x 4 rows");
-struct FfRowVals {
-#define FF_DECL(c) int64_t c##_0, c##_1, c##_2, c##_3;
-#define FF_DECL2(c) FF_DECL(v##c)
-  FF_COLS(FF_DECL2)
-#undef FF_DECL2
-#undef FF_DECL
+// The row vectors are kernel locals (r0..r3) handed to helpers BY VALUE: an
+// element read through a reference/struct lvalue is canonicalised into a
+// dynamic GEP, which pins the vectors in scratch. NC (the number of input
+// columns) is a compile-time bound, so the load block has no branches and
+// every column's loads are issued before the first wait.
+#define FF_LOAD_ROWS(NC, S, base, idx)                              \
+  ff_vec<ff_vw<NC>()> r0 = {}, r1 = r0, r2 = r0, r3 = r0;          \
+  _Pragma("unroll") for (int c_ = 0; c_ < NC; ++c_) {             \
+    r0[c_] = ff_load(S.cols[c_], base, idx[0]);                    \
+    r1[c_] = ff_load(S.cols[c_], base, idx[1]);                    \
+    r2[c_] = ff_load(S.cols[c_], base, idx[2]);                    \
+    r3[c_] = ff_load(S.cols[c_], base, idx[3]);                    \
+  }
+#define FF_ROW(j) ((j) == 0 ? r0 : (j) == 1 ? r1 : (j) == 2 ? r2 : r3)
+
+template <int VW>
+__device__ __forceinline__ int64_t col_of(const ff_vec<VW> rv, int c) {
+  return rv[c & (VW - 1)];
+}
+
+// Iteration setup: wave-uniform first row, per-lane row offsets (clamped into
+// range for the tail; `live` marks real rows).
+struct FfIter {
+  int64_t base;
+  uint32_t idx[kFfRows];
+  bool live[kFfRows];
 };
-
-// NC (the number of input columns) is a template parameter: the load block
-// has no branches, so every column's loads are issued before the first wait.
-template <int NC>
-__device__ __forceinline__ void ff_load_rows(const FfSpec& S, const int64_t* rows, FfRowVals& R) {
-#define FF_LD(c)                                   \
-  if constexpr (c < NC) {                         \
-    R.v##c##_0 = ff_load(S.cols[c], rows[0]);     \
-    R.v##c##_1 = ff_load(S.cols[c], rows[1]);     \
-    R.v##c##_2 = ff_load(S.cols[c], rows[2]);     \
-    R.v##c##_3 = ff_load(S.cols[c], rows[3]);     \
-  }
-  FF_COLS(FF_LD)
-#undef FF_LD
-}
-
-template <int NC>
-__device__ __forceinline__ int64_t col_of(const FfRowVals& R, int c, int j) {
-  c = __builtin_amdgcn_readfirstlane(c);
-  int64_t out = 0;
-#define FF_SEL(k)                                                                                      \
-  if constexpr (k < NC)                                                                               \
-    out = (c == k) ? (j == 0 ? R.v##k##_0 : j == 1 ? R.v##k##_1 : j == 2 ? R.v##k##_2 : R.v##k##_3) : out;
-  FF_COLS(FF_SEL)
-#undef FF_SEL
-  return out;
-}
-
-template <int NC>
-__device__ __forceinline__ bool ff_pass(const FfSpec& S, const FfRowVals& R, int j, int64_t row) {
-  bool ok = true;
-  for (int t = 0; t < S.nterms; ++t) {
-    const FfTerm& T = S.terms[t];
-    const int64_t v = col_of<NC>(R, T.col, j);
-    const bool in_range = v >= T.lo && v <= T.hi;
-    const bool in_set = v >= 0 && v < 64 && ((T.set >> (v & 63)) & 1ULL);
-    const bool hit = T.kind == 2 ? in_set : in_range;
-    ok &= (T.kind == 1) ? !hit : hit;
-  }
-  if (S.mask) ok &= S.mask[row] != 0;
-  return ok;
-}
-
-template <int NC>
-__device__ __forceinline__ int64_t ff_value(const FfAgg& A, const FfRowVals& R, int j, int* ovf) {
-  int64_t acc = 1;
-  for (int f = 0; f < A.nfac; ++f) {
-    const FfFactor& F = A.f[f];
-    const int64_t term =
-        F.col < 0 ? F.a : (int64_t)((uint64_t)F.a + (uint64_t)F.b * (uint64_t)col_of<NC>(R, (int)F.col, j));
-    if (A.checked) {
-      int64_t r;
-      if (__builtin_mul_overflow(acc, term, &r)) *ovf = 1;
-      acc = r;
-    } else {
-      acc = (int64_t)((uint64_t)acc * (uint64_t)term);
-    }
-  }
-  return acc;
-}
-
-__device__ __forceinline__ void ff_rows(int64_t base, int lane, int64_t n, int64_t* rows, bool* live) {
+__device__ __forceinline__ FfIter ff_iter(int64_t base, int lane, int64_t n) {
+  FfIter it;
+  it.base = base;
+  const int64_t rem = n - base;  // > 0
 #pragma unroll
   for (int j = 0; j < kFfRows; ++j) {
-    const int64_t r = base + j * kWave + lane;
-    live[j] = r < n;
-    rows[j] = r < n ? r : n - 1;
+    const int64_t r = j * kWave + lane;
+    it.live[j] = r < rem;
+    it.idx[j] = (uint32_t)(r < rem ? r : rem - 1);
+  }
+  return it;
+}
+
+// filter: all terms, descriptor-outer
+template <int VW>
+__device__ __forceinline__ void ff_pass4(const FfSpec& S, const ff_vec<VW> r0, const ff_vec<VW> r1,
+                                         const ff_vec<VW> r2, const ff_vec<VW> r3, const FfIter& it, bool* pass) {
+#pragma unroll
+  for (int j = 0; j < kFfRows; ++j) pass[j] = it.live[j];
+  for (int t = 0; t < S.nterms; ++t) {
+    const FfTerm& T = S.terms[t];
+    const int c = __builtin_amdgcn_readfirstlane(T.col);
+    const int kind = T.kind;
+    const int64_t lo = T.lo, hi = T.hi;
+    const uint64_t set = T.set;
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) {
+      const int64_t v = col_of<VW>(FF_ROW(j), c);
+      bool hit;
+      if (kind == 2) hit = v >= 0 && v < 64 && ((set >> (v & 63)) & 1ULL);
+      else hit = v >= lo && v <= hi;
+      pass[j] &= (kind == 1) ? !hit : hit;
+    }
+  }
+  if (S.mask) {
+    const uint8_t* m = S.mask + it.base;
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) pass[j] &= m[it.idx[j]] != 0;
   }
 }
+
+// group ids: keys descriptor-outer
+template <int VW>
+__device__ __forceinline__ void ff_gid4(const FfSpec& S, const ff_vec<VW> r0, const ff_vec<VW> r1,
+                                        const ff_vec<VW> r2, const ff_vec<VW> r3, int* gid) {
+#pragma unroll
+  for (int j = 0; j < kFfRows; ++j) gid[j] = 0;
+  for (int k = 0; k < S.nkeys; ++k) {
+    const int c = __builtin_amdgcn_readfirstlane(S.key_col[k]);
+    const int lo = (int)S.key_lo[k], mul = (int)S.key_mul[k];  // small domains: codes and offsets fit in 32 bits
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) gid[j] += ((int)col_of<VW>(FF_ROW(j), c) - lo) * mul;
+  }
+}
+
+// aggregate argument: product of affine factors, factor-outer. `val` holds
+// the previous aggregate's values on entry (reused when A.shared > 0).
+// Checked products take a 32 x 32 -> 64-bit multiply when both operands fit in
+// 32 bits (the common case: fixed-point prices times small factors) and the
+// overflow-checked 64-bit path otherwise.
+template <int VW>
+__device__ __forceinline__ void ff_value4(const FfAgg& A, const ff_vec<VW> r0, const ff_vec<VW> r1,
+                                          const ff_vec<VW> r2, const ff_vec<VW> r3, int64_t* val, int* ovf) {
+  const int shared = A.shared;
+  if (shared == 0) {
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) val[j] = 1;
+  }
+  const bool checked = A.checked;
+  for (int f = shared; f < A.nfac; ++f) {
+    const FfFactor& F = A.f[f];
+    const int c = __builtin_amdgcn_readfirstlane((int)F.col);
+    const int64_t a = F.a, b = F.b;
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) {
+      int64_t term;
+      if (c < 0) term = a;
+      else if (b == 1) term = (int64_t)((uint64_t)a + (uint64_t)col_of<VW>(FF_ROW(j), c));
+      else if (b == -1) term = (int64_t)((uint64_t)a - (uint64_t)col_of<VW>(FF_ROW(j), c));
+      else term = (int64_t)((uint64_t)a + (uint64_t)b * (uint64_t)col_of<VW>(FF_ROW(j), c));
+      const int64_t x = val[j];
+      if ((int64_t)(int32_t)x == x && (int64_t)(int32_t)term == term) {
+        val[j] = (int64_t)(int32_t)x * (int64_t)(int32_t)term;
+      } else if (checked) {
+        int64_t r;
+        if (__builtin_mul_overflow(x, term, &r)) *ovf = 1;
+        val[j] = r;
+      } else {
+        val[j] = (int64_t)((uint64_t)x * (uint64_t)term);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int ff_wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 template <int NC>
 __global__ __launch_bounds__(kBlock) void ff_mask_kernel(const FfSpec S, int64_t n, uint8_t* __restrict__ out) {
-  const int wave = threadIdx.x / kWave, lane = lane_id();
+  const int wave = ff_wave_uniform(threadIdx.x / kWave), lane = lane_id();
   const int64_t per_iter = (int64_t)kWave * kFfRows;
   const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * per_iter;
   for (int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * per_iter; base < n; base += stride) {
-    int64_t rows[kFfRows];
-    bool live[kFfRows];
-    ff_rows(base, lane, n, rows, live);
-    FfRowVals R;
-    ff_load_rows<NC>(S, rows, R);
+    const FfIter it = ff_iter(base, lane, n);
+    FF_LOAD_ROWS(NC, S, base, it.idx)
+    bool pass[kFfRows];
+    ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
+    uint8_t* o = out + base;
 #pragma unroll
     for (int j = 0; j < kFfRows; ++j)
-      if (live[j]) out[rows[j]] = ff_pass<NC>(S, R, j, rows[j]);
+      if (it.live[j]) o[it.idx[j]] = pass[j];
   }
 }
 
-__device__ inline int64_t wsum(int64_t v) {
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
-}
-__device__ inline int64_t wmin(int64_t v) {
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    const int64_t o = __shfl_xor(v, off, kWave);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-__device__ inline int64_t wmax(int64_t v) {
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    const int64_t o = __shfl_xor(v, off, kWave);
-    v = o > v ? o : v;
-  }
-  return v;
+// LDS slot of (cell, half, lane): lanes fold onto `lanes` slots (a power of
+// two <= 64 chosen on the host so cells * 2 * lanes int64 fit the LDS budget)
+__device__ __forceinline__ int ff_slot(int cell, int half, int lane, int lanes) {
+  return (cell * 2 + half) * lanes + (lane & (lanes - 1));
 }
 
+// LDS layout: cell = a * G + g for aggregates, NA * G + g for the row counts.
 template <int NC>
-__global__ __launch_bounds__(kBlock) void ff_agg_kernel(const FfSpec S, int64_t n) {
-  // [wave][group][agg or count][lo, hi]
-  __shared__ int64_t slots[kWavesPerBlock][kFfMaxGroups][kFfMaxAggs + 1][2];
-  const int wave = threadIdx.x / kWave, lane = lane_id();
+__global__ __launch_bounds__(kBlock) void ff_agg_kernel(const FfSpec S, int64_t n, int lanes) {
+  extern __shared__ int64_t acc[];
+  const int wave = ff_wave_uniform(threadIdx.x / kWave), lane = lane_id();
   const int G = S.ngroups, NA = S.naggs;
-  for (int s = threadIdx.x; s < kWavesPerBlock * kFfMaxGroups * (kFfMaxAggs + 1); s += kBlock) {
-    const int w = s / (kFfMaxGroups * (kFfMaxAggs + 1));
-    const int rem = s % (kFfMaxGroups * (kFfMaxAggs + 1));
-    const int g = rem / (kFfMaxAggs + 1), a = rem % (kFfMaxAggs + 1);
+  const int cells = (NA + 1) * G;
+  for (int s = threadIdx.x; s < cells * 2 * lanes; s += kBlock) {
+    const int cell = s / (2 * lanes), a = cell / G;
     int64_t init = 0;
     if (a < NA && S.aggs[a].op == 2) init = INT64_MAX;
     if (a < NA && S.aggs[a].op == 3) init = INT64_MIN;
-    slots[w][g][a][0] = init;
-    slots[w][g][a][1] = 0;
+    acc[s] = init;
   }
   __syncthreads();
   int ovf = 0;
   const int64_t per_iter = (int64_t)kWave * kFfRows;
   const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * per_iter;
   for (int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * per_iter; base < n; base += stride) {
-    int64_t rows[kFfRows];
-    bool live[kFfRows];
-    ff_rows(base, lane, n, rows, live);
-    FfRowVals R;
-    ff_load_rows<NC>(S, rows, R);
+    const FfIter it = ff_iter(base, lane, n);
+    FF_LOAD_ROWS(NC, S, base, it.idx)
     bool pass[kFfRows];
+    ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
     int gid[kFfRows];
-    bool any = false;
+    ff_gid4<ff_vw<NC>()>(S, r0, r1, r2, r3, gid);
+    // per-row slot base (group g, this lane); aggregate a adds a * G cells
+    int64_t* rowslot[kFfRows];
 #pragma unroll
-    for (int j = 0; j < kFfRows; ++j) {
-      pass[j] = live[j] && ff_pass<NC>(S, R, j, rows[j]);
-      int g = 0;
-      for (int k = 0; k < S.nkeys; ++k) g += (int)((col_of<NC>(R, S.key_col[k], j) - S.key_lo[k]) * S.key_mul[k]);
-      gid[j] = g;
-      any |= pass[j];
-    }
-    if (!__ballot(any)) continue;
-    // row counts per group
-    for (int g = 0; g < G; ++g) {
-      int cnt = 0;
+    for (int j = 0; j < kFfRows; ++j) rowslot[j] = acc + ff_slot(gid[j], 0, lane, lanes);
+    const int cell_stride = 2 * lanes;  // int64 per cell
 #pragma unroll
-      for (int j = 0; j < kFfRows; ++j) cnt += pass[j] && gid[j] == g;
-      if (!__ballot(cnt != 0)) continue;
-      const int64_t wc = wsum(cnt);
-      if (lane == 0) slots[wave][g][kFfMaxAggs][0] += wc;
-    }
-    // aggregates: argument values once per row, then one reduction per group
-#pragma unroll
-    for (int a = 0; a < kFfMaxAggs; ++a) {
-      if (a >= NA) continue;
+    for (int j = 0; j < kFfRows; ++j)
+      if (pass[j])
+        __hip_atomic_fetch_add(rowslot[j] + NA * G * cell_stride, (int64_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    int64_t val[kFfRows];
+    for (int a = 0; a < NA; ++a) {
       const FfAgg& A = S.aggs[a];
-      int64_t val[kFfRows];
+      const int op = A.op;
+      if (op == 1) continue;  // COUNT: the group row count (never a chain link: it has no factors)
+      ff_value4<ff_vw<NC>()>(A, r0, r1, r2, r3, val, &ovf);
+      const int aoff = a * G * cell_stride;
 #pragma unroll
-      for (int j = 0; j < kFfRows; ++j) val[j] = (pass[j] && A.op != 1) ? ff_value<NC>(A, R, j, &ovf) : 0;
-      for (int g = 0; g < G; ++g) {
-        bool m[kFfRows];
-        int cnt = 0;
-#pragma unroll
-        for (int j = 0; j < kFfRows; ++j) {
-          m[j] = pass[j] && gid[j] == g;
-          cnt += m[j];
-        }
-        if (!__ballot(cnt != 0)) continue;
-        if (A.op == 0) {  // exact sum: per-lane partial in 32-bit halves
-          int64_t lo = 0, hi = 0;
-#pragma unroll
-          for (int j = 0; j < kFfRows; ++j)
-            if (m[j]) {
-              lo += (int64_t)(uint32_t)(uint64_t)val[j];
-              hi += val[j] >> 32;
-            }
-          const int64_t slo = wsum(lo), shi = wsum(hi);
-          if (lane == 0) {
-            __int128 acc = ((__int128)slots[wave][g][a][1] << 64) | (unsigned __int128)(uint64_t)slots[wave][g][a][0];
-            acc += ((__int128)shi << 32) + (__int128)slo;
-            slots[wave][g][a][0] = (int64_t)(uint64_t)acc;
-            slots[wave][g][a][1] = (int64_t)(acc >> 64);
-          }
-        } else if (A.op == 1) {
-          const int64_t wc = wsum(cnt);
-          if (lane == 0) slots[wave][g][a][0] += wc;
-        } else if (A.op == 2) {
-          int64_t r = INT64_MAX;
-#pragma unroll
-          for (int j = 0; j < kFfRows; ++j)
-            if (m[j]) r = val[j] < r ? val[j] : r;
-          r = wmin(r);
-          if (lane == 0 && r < slots[wave][g][a][0]) slots[wave][g][a][0] = r;
+      for (int j = 0; j < kFfRows; ++j) {
+        if (!pass[j]) continue;
+        int64_t* slot = rowslot[j] + aoff;
+        if (op == 0) {
+          __hip_atomic_fetch_add(slot, (int64_t)(uint32_t)(uint64_t)val[j], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(slot + lanes, val[j] >> 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (op == 2) {
+          __hip_atomic_fetch_min(slot, val[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
-          int64_t r = INT64_MIN;
-#pragma unroll
-          for (int j = 0; j < kFfRows; ++j)
-            if (m[j]) r = val[j] > r ? val[j] : r;
-          r = wmax(r);
-          if (lane == 0 && r > slots[wave][g][a][0]) slots[wave][g][a][0] = r;
+          __hip_atomic_fetch_max(slot, val[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
     }
@@ -270,31 +271,35 @@ __global__ __launch_bounds__(kBlock) void ff_agg_kernel(const FfSpec S, int64_t 
   __syncthreads();
   for (int s = threadIdx.x; s < G * (NA + 1); s += kBlock) {
     const int g = s / (NA + 1), a = s % (NA + 1);
-    if (a == NA) {
+    const int ccell = NA * G + g;
+    if (a == NA || S.aggs[a].op == 1) {
       int64_t c = 0;
-      for (int w = 0; w < kWavesPerBlock; ++w) c += slots[w][g][kFfMaxAggs][0];
-      if (c) atomicAdd((unsigned long long*)&S.counts[g], (unsigned long long)c);
+      for (int l = 0; l < lanes; ++l) c += acc[ff_slot(ccell, 0, l, lanes)];
+      if (c) atomicAdd((unsigned long long*)(a == NA ? &S.counts[g] : &S.aggs[a].dst[g]), (unsigned long long)c);
       continue;
     }
     const FfAgg& A = S.aggs[a];
+    const int cell = a * G + g;
     if (A.op == 0) {
-      __int128 acc = 0;
-      for (int w = 0; w < kWavesPerBlock; ++w)
-        acc += ((__int128)slots[w][g][a][1] << 64) | (unsigned __int128)(uint64_t)slots[w][g][a][0];
-      if (acc != 0)
-        atomic_add_i128_parts((unsigned long long*)&A.dst[g], (long long*)&A.dst2[g], (unsigned long long)(uint64_t)acc,
-                              (long long)(int64_t)(acc >> 64));
-    } else if (A.op == 1) {
-      int64_t c = 0;
-      for (int w = 0; w < kWavesPerBlock; ++w) c += slots[w][g][a][0];
-      if (c) atomicAdd((unsigned long long*)&A.dst[g], (unsigned long long)c);
+      __int128 t = 0;
+      for (int l = 0; l < lanes; ++l)
+        t += ((__int128)acc[ff_slot(cell, 1, l, lanes)] << 32) + (__int128)(uint64_t)acc[ff_slot(cell, 0, l, lanes)];
+      if (t != 0)
+        atomic_add_i128_parts((unsigned long long*)&A.dst[g], (long long*)&A.dst2[g], (unsigned long long)(uint64_t)t,
+                              (long long)(int64_t)(t >> 64));
     } else if (A.op == 2) {
       int64_t r = INT64_MAX;
-      for (int w = 0; w < kWavesPerBlock; ++w) r = slots[w][g][a][0] < r ? slots[w][g][a][0] : r;
+      for (int l = 0; l < lanes; ++l) {
+        const int64_t x = acc[ff_slot(cell, 0, l, lanes)];
+        r = x < r ? x : r;
+      }
       atomicMin((long long*)&A.dst[g], (long long)r);
     } else {
       int64_t r = INT64_MIN;
-      for (int w = 0; w < kWavesPerBlock; ++w) r = slots[w][g][a][0] > r ? slots[w][g][a][0] : r;
+      for (int l = 0; l < lanes; ++l) {
+        const int64_t x = acc[ff_slot(cell, 0, l, lanes)];
+        r = x > r ? x : r;
+      }
       atomicMax((long long*)&A.dst[g], (long long)r);
     }
   }
@@ -309,10 +314,20 @@ void launch_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream
                      spec, n, out);
 }
 
+constexpr int kFfLdsMax = 64 * 1024;
+
 template <int NC>
 void launch_agg(const FfSpec& spec, int64_t n, hipStream_t stream) {
-  hipLaunchKernelGGL(ff_agg_kernel<NC>, dim3(grid_for(n, kBlock * kFfRows * 4, 256 * 8)), dim3(kBlock), 0, stream, spec,
-                     n);
+  // per-lane slots while they fit the LDS budget, fewer (shared) lanes beyond
+  const size_t cells = (size_t)(spec.naggs + 1) * spec.ngroups;
+  int lanes = kWave;
+  while (lanes > 1 && cells * 2 * lanes * sizeof(int64_t) > (size_t)kFfLdsMax) lanes >>= 1;
+  const size_t lds = cells * 2 * lanes * sizeof(int64_t);
+  // persistent-style grid: about as many blocks as stay resident (LDS-limited),
+  // each streaming many rows, so the per-block init/merge is amortised
+  const int per_cu = lds <= 20 * 1024 ? 8 : lds <= 32 * 1024 ? 4 : 2;
+  hipLaunchKernelGGL(ff_agg_kernel<NC>, dim3(grid_for(n, kBlock * kFfRows * 4, 256 * per_cu)), dim3(kBlock), lds,
+                     stream, spec, n, lanes);
 }
 
 void ff_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream) {

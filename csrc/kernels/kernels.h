@@ -46,9 +46,11 @@ struct FfFactor {
   int64_t col, a, b;
 };
 // op: 0 sum (int128: dst = lo, dst2 = hi), 1 count, 2 min, 3 max (int64)
+// shared > 0: the first `shared` factors equal the previous aggregate's whole
+// product (its value is reused; the host orders aggregates to form such chains)
 struct FfAgg {
   int32_t op, nfac;
-  int32_t checked, pad;
+  int32_t checked, shared;
   FfFactor f[kFfMaxFactors];
   int64_t* dst;
   int64_t* dst2;

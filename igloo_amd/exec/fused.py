@@ -350,8 +350,15 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
             if scale != want:
                 raise Bail(f"scale {scale} != {want}")
             op = {"sum": 0, "avg": 0, "min": 2, "max": 3}[a.func]
-            plan.append((ci, a, len(descs)))
-            descs.append((op, int(chk), fs))
+            d = (op, int(chk), tuple(fs))
+            if d not in descs:   # avg(x) next to sum(x): one accumulator
+                descs.append(d)
+            plan.append((ci, a, d))
+        # lexicographic factor order puts a product right after its prefix, so
+        # the kernel extends the previous value instead of recomputing it
+        descs.sort(key=lambda d: (d[2], d[0], d[1]))
+        pos = {d: i for i, d in enumerate(descs)}
+        plan = [(ci, a, None if d is None else pos[d]) for ci, a, d in plan]
         if len(descs) > MAX_AGGS:
             raise Bail("too many aggregates")
         if pred is not None:
@@ -362,6 +369,7 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
     counts = torch.zeros(G, dtype=torch.int64, device=dev)
     ovf = torch.zeros(1, dtype=torch.int32, device=dev)
     bufs, kaggs = [], []
+    prev = None
     for op, chk, fs in descs:
         if op == 0:
             d, d2 = torch.zeros(G, dtype=torch.int64, device=dev), torch.zeros(G, dtype=torch.int64, device=dev)
@@ -369,8 +377,15 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
             d = torch.full((G,), I64_MAX if op == 2 else I64_MIN, dtype=torch.int64, device=dev)
             d2 = None
         bufs.append((d, d2))
+        # reuse the previous product when it is a prefix of this one (an
+        # unchecked predecessor may have wrapped, so a checked one needs a checked prefix)
+        shared = 0
+        if prev is not None and prev[2] and len(prev[2]) < len(fs) and fs[:len(prev[2])] == prev[2] \
+                and (prev[1] or not chk):
+            shared = len(prev[2])
+        prev = (op, chk, fs)
         kaggs.append((op, chk, [(int(c), int(a_), int(b_)) for c, a_, b_ in fs], d.data_ptr(),
-                      d2.data_ptr() if d2 is not None else 0))
+                      d2.data_ptr() if d2 is not None else 0, shared))
     if not spec.always_false:
         cols, terms, mask = spec.args()
         with ctx.span("agg.fused_scan"):

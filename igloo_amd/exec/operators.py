@@ -999,7 +999,10 @@ class MultiJoinExec(ExecNode):
                     out = _nested_loop(la, lb_, "inner", and_all(resid), ctx)
             out.dist = out_dist
             self.order_log.append(f"{a['name']} ⋈ {b['name']} -> {out.num_rows}")
-            merged = {"batch": out, "cids": cids, "ndv": {}, "name": f"({a['name']}⋈{b['name']})"}
+            # key NDVs carry over (capped by the output size) instead of re-sketching intermediates
+            cap = _global_rows(out, ctx)   # global: every rank must derive the same estimates / join order
+            ndv = {k: max(1, min(v, cap)) for d in (a["ndv"], b["ndv"]) for k, v in d.items()}
+            merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})"}
             rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
         b = rels[0]["batch"]
         if isinstance(b, LateBatch):

@@ -258,6 +258,11 @@ HLL_M = 1 << HLL_BITS
 def hll_sketch(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """HyperLogLog registers (uint8 [4096]) of the key column (GPU only; None on CPU).
     Sketches of several ranks merge by element-wise max."""
+    src = keys
+    if valid is None:
+        hit = getattr(src, "_igloo_hll", None)
+        if hit is not None:   # resident table columns are sketched once (like is_sorted)
+            return hit
     keys = _keys_ok(keys)
     n = keys.numel()
     if not is_gpu(keys):
@@ -268,6 +273,11 @@ def hll_sketch(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Opti
     N = launch("hll_sketch")
     ws = torch.empty(N.hll_blocks(n) * HLL_M, dtype=torch.uint8, device=keys.device)
     N.hll_sketch(ptr(keys), keys.dtype == torch.int64, ptr(valid), n, ptr(ws), ptr(regs), stream(keys))
+    if valid is None:
+        try:
+            src._igloo_hll = regs
+        except (AttributeError, RuntimeError):
+            pass
     return regs
 
 

@@ -54,6 +54,11 @@ QUERIES = [
     """SELECT k, min(f) AS mn, max(f) AS mx, sum(f * 2.5) AS s, min(price) AS mp, max(d) AS md,
               sum(CASE WHEN flag = 'R' THEN price ELSE 0 END) AS cr, count(*) AS c
        FROM t WHERE k IN (-5, -1, 0, 3, 5) OR f > 150 GROUP BY k ORDER BY k""",
+    # product chains (a prefix reused by the next aggregate) mixed with min/max
+    # and duplicate arguments; price * price * disc leaves the 32-bit fast path
+    """SELECT status, min(price * (1 - disc)) AS a, sum(price * (1 - disc)) AS b, max(price * (1 - disc) * (1 + tax)) AS c,
+              sum(price * (1 - disc) * (1 + tax)) AS e, sum(price * price * disc) AS pp, avg(price) AS ap, sum(price) AS sp
+       FROM t GROUP BY status ORDER BY status""",
     # empty filter result: global aggregates are NULL / 0
     "SELECT sum(price) AS s, count(*) AS c, min(f) AS m, avg(qty) AS a FROM t WHERE qty < 0",
     # plain filter through the VM mask kernel (no aggregate)
