@@ -8,8 +8,7 @@
 #include <tuple>
 #include <vector>
 
-#include <vector>
-
+#include "io/parquet_meta.h"
 #include "kernels/kernels.h"
 #include "runtime/runtime.h"
 #include "sql/ast.h"
@@ -47,6 +46,81 @@ py::list tokenize(const std::string& text) {
     throw py::error_already_set();
   }
   return out;
+}
+
+py::dict leaf_dict(const io::PqLeaf& l) {
+  py::dict d;
+  d["name"] = l.name;
+  d["type"] = l.type;
+  d["type_length"] = l.type_length;
+  d["max_def"] = l.max_def;
+  d["max_rep"] = l.max_rep;
+  d["converted_type"] = l.converted_type;
+  d["logical"] = l.logical;
+  d["scale"] = l.scale;
+  d["precision"] = l.precision;
+  return d;
+}
+
+py::dict chunk_dict(const io::PqChunk& c) {
+  py::dict d;
+  d["type"] = c.type;
+  d["codec"] = c.codec;
+  d["num_values"] = c.num_values;
+  d["start"] = c.start();
+  d["length"] = c.total_compressed;
+  d["uncompressed"] = c.total_uncompressed;
+  d["data_page_offset"] = c.data_page_offset;
+  d["dictionary_page_offset"] = c.dictionary_page_offset;
+  d["encodings"] = c.encodings;
+  d["external"] = c.external;
+  d["null_count"] = c.stats.has_nulls ? py::object(py::int_(c.stats.null_count)) : py::object(py::none());
+  d["min"] = c.stats.has_min ? py::object(py::bytes(c.stats.min)) : py::object(py::none());
+  d["max"] = c.stats.has_max ? py::object(py::bytes(c.stats.max)) : py::object(py::none());
+  return d;
+}
+
+py::dict page_header_dict(const io::PqPageHeader& h) {
+  py::dict d;
+  d["type"] = h.type;
+  d["header_len"] = h.header_len;
+  d["compressed"] = h.compressed;
+  d["uncompressed"] = h.uncompressed;
+  d["num_values"] = h.num_values;
+  d["encoding"] = h.encoding;
+  d["def_encoding"] = h.def_encoding;
+  d["num_nulls"] = h.num_nulls;
+  d["num_rows"] = h.num_rows;
+  d["def_len"] = h.def_len;
+  d["rep_len"] = h.rep_len;
+  d["is_compressed"] = h.is_compressed;
+  return d;
+}
+
+kern::PqDecodeSpec decode_spec(const py::dict& d, bool need_output = true) {
+  kern::PqDecodeSpec s{};
+  s.phys = d["phys"].cast<int>();
+  s.type_len = d["type_len"].cast<int>();
+  s.out_width = d["out_width"].cast<int>();
+  s.conv = d["conv"].cast<int>();
+  s.conv_k = d["conv_k"].cast<int64_t>();
+  s.max_def = d["max_def"].cast<int>();
+  s.out = P<void>(d["out"].cast<uintptr_t>());
+  s.valid = P<uint8_t>(d["valid"].cast<uintptr_t>());
+  s.scratch = P<uint32_t>(d["scratch"].cast<uintptr_t>());
+  s.str_len = P<int64_t>(d["str_len"].cast<uintptr_t>());
+  s.str_pos = P<int64_t>(d["str_pos"].cast<uintptr_t>());
+  s.codes = P<int32_t>(d["codes"].cast<uintptr_t>());
+  s.dict_len = P<int64_t>(d["dict_len"].cast<uintptr_t>());
+  s.dict_pos = P<int64_t>(d["dict_pos"].cast<uintptr_t>());
+  s.raw = P<const uint8_t>(d["raw"].cast<uintptr_t>());
+  s.dec = P<const uint8_t>(d["dec"].cast<uintptr_t>());
+  s.error = P<int>(d["error"].cast<uintptr_t>());
+  if (s.max_def < 0 || s.max_def > 1 || s.phys < 0 || s.phys > kern::PQ_PHYS_FLBA || !s.raw || !s.error)
+    throw std::runtime_error("pq_decode: bad spec");
+  if (need_output && (s.phys == kern::PQ_PHYS_BYTE_ARRAY ? !(s.codes || (s.str_len && s.str_pos)) : !s.out))
+    throw std::runtime_error("pq_decode: missing output buffer");
+  return s;
 }
 
 }  // namespace
@@ -304,6 +378,85 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("date_part", [](uintptr_t days, int64_t n, int field, uintptr_t out, uintptr_t s) {
     kern::date_part(P<const int32_t>(days), n, field, P<int32_t>(out), S(s));
+  });
+
+  // ---------------------------------------------------------------- parquet
+  m.def("pq_file_meta", [](const std::string& path) {
+    io::PqFileMeta meta;
+    {
+      py::gil_scoped_release rel;
+      meta = io::read_file_meta(path);
+    }
+    py::dict d;
+    d["version"] = meta.version;
+    d["num_rows"] = meta.num_rows;
+    d["created_by"] = meta.created_by;
+    py::list leaves, groups;
+    for (auto& l : meta.leaves) leaves.append(leaf_dict(l));
+    for (auto& g : meta.row_groups) {
+      py::dict gd;
+      gd["num_rows"] = g.num_rows;
+      py::list cs;
+      for (auto& c : g.chunks) cs.append(chunk_dict(c));
+      gd["chunks"] = cs;
+      groups.append(gd);
+    }
+    d["leaves"] = leaves;
+    d["row_groups"] = groups;
+    return d;
+  }, "Parse a Parquet footer (native Thrift compact decoder)");
+  m.def("pq_page_headers", [](uintptr_t host, int64_t n) {
+    py::list out;
+    for (auto& h : io::parse_chunk_pages(P<const uint8_t>(host), (size_t)n)) out.append(page_header_dict(h));
+    return out;
+  });
+  m.def("pq_pread", [](const std::string& path, const std::vector<std::tuple<int64_t, int64_t, uintptr_t>>& ranges,
+                       int threads) {
+    std::vector<io::ReadRange> rs;
+    for (auto& [off, len, dst] : ranges) {
+      if (off < 0 || len < 0 || !dst) throw std::runtime_error("pq_pread: bad range");
+      rs.push_back({off, len, P<uint8_t>(dst)});
+    }
+    py::gil_scoped_release rel;
+    io::pread_ranges(path, rs, threads);
+  });
+  m.def("pq_plan", [](uintptr_t host, const std::vector<std::tuple<int64_t, int64_t, int, int64_t, int64_t>>& chunks,
+                      int phys, int max_def, int max_rep) {
+    std::vector<io::PqChunkIn> cs;
+    for (auto& [off, len, codec, first, rows] : chunks) cs.push_back({off, len, codec, first, rows});
+    io::PqPlan plan;
+    {
+      py::gil_scoped_release rel;
+      plan = io::plan_column(P<const uint8_t>(host), cs, phys, max_def, max_rep);
+    }
+    py::dict d;
+    d["pages"] = py::bytes((const char*)plan.pages.data(), plan.pages.size());
+    d["jobs"] = py::bytes((const char*)plan.jobs.data(), plan.jobs.size());
+    d["num_pages"] = plan.num_pages;
+    d["num_jobs"] = plan.num_jobs;
+    d["num_dict_pages"] = plan.num_dict_pages;
+    d["dec_bytes"] = plan.dec_bytes;
+    d["dict_entries"] = plan.dict_entries;
+    d["plain_pages"] = plan.plain_pages;
+    d["max_page_values"] = plan.max_page_values;
+    d["unsupported"] = plan.unsupported;
+    return d;
+  }, "Plan GPU decode descriptors for one column's chunks staged at `host`");
+  m.def("pq_snappy", [](uintptr_t jobs, int64_t njobs, uintptr_t raw, uintptr_t dec, uintptr_t err, uintptr_t s) {
+    if (njobs > 0 && (!jobs || !raw || !dec || !err)) throw std::runtime_error("pq_snappy: null buffer");
+    kern::pq_snappy(P<const kern::PqSnappyJob>(jobs), njobs, P<const uint8_t>(raw), P<uint8_t>(dec), P<int>(err), S(s));
+  });
+  m.def("pq_dict_strings", [](uintptr_t pages, int64_t npages, const py::dict& spec, uintptr_t s) {
+    kern::PqDecodeSpec sp = decode_spec(spec, false);
+    if (!sp.dict_len || !sp.dict_pos) throw std::runtime_error("pq_dict_strings: missing dictionary tables");
+    kern::pq_dict_strings(P<const kern::PqPage>(pages), npages, sp, S(s));
+  });
+  m.def("pq_decode", [](uintptr_t pages, int64_t npages, const py::dict& spec, uintptr_t s) {
+    kern::PqDecodeSpec sp = decode_spec(spec);
+    kern::pq_decode(P<const kern::PqPage>(pages), npages, sp, S(s));
+  });
+  m.def("pq_str_copy", [](uintptr_t pos, uintptr_t off, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::pq_str_copy(P<const int64_t>(pos), P<const int64_t>(off), n, P<uint8_t>(out), S(s));
   });
 
   // ---------------------------------------------------------------- datagen

@@ -196,5 +196,61 @@ void textgen_lengths(const TextGenParams& p, int64_t n, int64_t* lens, bool devi
 void textgen_write(const TextGenParams& p, int64_t n, const int64_t* off, uint8_t* chars, bool device,
                    hipStream_t stream);
 
+// ---- parquet.hip ---------------------------------------------------------------
+enum PqPhys : int { PQ_PHYS_BOOLEAN = 0, PQ_PHYS_INT32 = 1, PQ_PHYS_INT64 = 2, PQ_PHYS_INT96 = 3, PQ_PHYS_FLOAT = 4,
+                    PQ_PHYS_DOUBLE = 5, PQ_PHYS_BYTE_ARRAY = 6, PQ_PHYS_FLBA = 7 };
+enum PqPageKind : int { PQ_PAGE_DATA_V1 = 0, PQ_PAGE_DATA_V2 = 1, PQ_PAGE_DICT = 2 };
+enum PqPageFlags : int { PQ_DATA_IN_DEC = 1, PQ_DICT_IN_DEC = 2 };
+enum PqConv : int { PQ_CONV_COPY = 0, PQ_CONV_NARROW = 1, PQ_CONV_SEXT = 2, PQ_CONV_ZEXT = 3, PQ_CONV_F2D = 4,
+                    PQ_CONV_FLBA = 5, PQ_CONV_MUL = 6, PQ_CONV_DIV = 7, PQ_CONV_BOOL = 8 };
+
+// One page of a column, planned on the host (csrc/io/parquet_meta.cpp).
+// Offsets are into the staged raw buffer, or the decompression buffer when
+// the matching PQ_*_IN_DEC flag is set.
+struct PqPage {
+  int64_t data_off;    // payload (values; v1 pages start with the level streams)
+  int64_t levels_off;  // v2: definition levels (raw buffer); -1 otherwise
+  int64_t dict_off;    // the chunk's dictionary payload; -1 if none
+  int64_t out_row;     // first output row
+  int32_t size;        // payload bytes at data_off
+  int32_t num_values;  // rows of the page (flat columns)
+  int32_t levels_len;  // v2 definition-level bytes
+  int32_t encoding;    // parquet Encoding of the values
+  int32_t kind;        // PqPageKind
+  int32_t flags;       // PqPageFlags
+  int32_t dict_base;   // first global dictionary slot of the chunk
+  int32_t dict_count;  // dictionary entries of the chunk
+};
+static_assert(sizeof(PqPage) == 64, "PqPage layout is shared with the host planner");
+
+struct PqSnappyJob {
+  int64_t src_off;  // raw buffer
+  int64_t dst_off;  // decompression buffer
+  int32_t src_len, dst_len;
+};
+
+struct PqDecodeSpec {
+  int32_t phys, type_len, out_width, conv;
+  int64_t conv_k;   // PQ_CONV_MUL / PQ_CONV_DIV factor
+  int32_t max_def, pad;
+  void* out;        // fixed width values [rows]
+  uint8_t* valid;   // [rows] or null (then the column must have no NULLs)
+  uint32_t* scratch;  // [rows] compact value index -> dictionary index / byte offset
+  int64_t* str_len;   // strings, plain output: per-row length
+  int64_t* str_pos;   // ... and address of the bytes
+  int32_t* codes;     // strings, dictionary output: global dictionary slot per row
+  int64_t* dict_len;  // [dictionary entries] (BYTE_ARRAY dictionaries)
+  int64_t* dict_pos;
+  const uint8_t* raw;
+  const uint8_t* dec;
+  int* error;         // first error code (0 = ok)
+};
+
+void pq_snappy(const PqSnappyJob* jobs, int64_t njobs, const uint8_t* raw, uint8_t* dec, int* error,
+               hipStream_t stream);
+void pq_dict_strings(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream);
+void pq_decode(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream);
+void pq_str_copy(const int64_t* pos, const int64_t* off, int64_t n, uint8_t* out, hipStream_t stream);
+
 }  // namespace kern
 }  // namespace igloo

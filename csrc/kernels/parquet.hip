@@ -1,0 +1,648 @@
+// GPU Parquet page decoding for gfx950.
+//
+// Replaces the reference's host-side parquet-rs reader (crates/engine/src/
+// operators/parquet_scan.rs:47-58: 1024-row record batches on a blocking
+// thread) with device decoding of whole column chunks that were staged into
+// HBM with one H2D copy (host side: csrc/io/parquet_meta.cpp plans the pages).
+//
+// Kernels (one launch per column, one workgroup per page):
+//   pq_snappy_kernel       raw snappy -> dec buffer. One wave per compressed
+//                          page; every lane parses the same tag from an LDS
+//                          input window (broadcast reads), copies are spread
+//                          over the 64 lanes, back-references are served from
+//                          a 64 KiB LDS history ring (snappy offsets < 64 KiB).
+//   pq_dict_strings_kernel BYTE_ARRAY dictionary pages -> (position, length)
+//                          of every dictionary entry.
+//   pq_decode_kernel       data pages: RLE/bit-packed definition levels ->
+//                          validity; PLAIN / dictionary values -> typed output
+//                          (conversion fused: decimal widening, FLBA big-endian
+//                          decimals, timestamp units, booleans); strings ->
+//                          per-row (position, length) or global dictionary code.
+//   pq_str_copy_kernel     string bytes into the Arrow chars buffer once the
+//                          offsets are known (exclusive scan of the lengths).
+//
+// RLE / bit-packed hybrid streams are decoded block-cooperatively: lane 0 of
+// the workgroup parses up to kRunCap run headers into LDS, then all 256 lanes
+// decode values by binary search over the run starts.
+#include "common.h"
+#include "kernels.h"
+
+namespace igloo {
+namespace kern {
+
+namespace {
+
+constexpr int kRunCap = 512;
+constexpr int kWalkWin = 8192;
+constexpr int kItems = 4;  // rows per lane per mapping step
+constexpr int kSnapRing = 65536;
+constexpr int kSnapIn = 4096;
+
+enum : int {
+  PQ_ERR_RLE = 1,
+  PQ_ERR_DICT_INDEX = 2,
+  PQ_ERR_BYTE_ARRAY = 3,
+  PQ_ERR_SNAPPY = 4,
+  PQ_ERR_SNAPPY_SIZE = 5,
+  PQ_ERR_DECIMAL = 6,
+  PQ_ERR_ENCODING = 7,
+  PQ_ERR_NULLS = 8,
+  PQ_ERR_TRUNCATED = 9,
+};
+
+__device__ inline void set_error(int* err, int code) { atomicCAS(err, 0, code); }
+
+__device__ inline uint32_t ld_u32(const uint8_t* p) {
+  if ((((uintptr_t)p) & 3) == 0) return *reinterpret_cast<const uint32_t*>(p);
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ inline uint64_t ld_u64(const uint8_t* p) {
+  if ((((uintptr_t)p) & 7) == 0) return *reinterpret_cast<const uint64_t*>(p);
+  return (uint64_t)ld_u32(p) | ((uint64_t)ld_u32(p + 4) << 32);
+}
+
+struct RleTable {
+  int32_t start[kRunCap + 1];
+  uint32_t val[kRunCap];
+  int64_t ptr[kRunCap];  // bit-packed run: data address; RLE run: 0
+  int64_t cur;
+  int32_t done;
+  int32_t nruns;
+  int32_t err;
+};
+
+// Decode `count` values of an RLE / bit-packed hybrid stream [p, end) with bit
+// width bw (0..32). sink(i, v) runs once per value index i in [0, count), on
+// some lane of the block. Must be called by every lane; ends synchronised.
+template <typename Sink>
+__device__ bool rle_decode(const uint8_t* p, const uint8_t* end, int bw, int count, RleTable& t, Sink sink) {
+  const int nbytes = (bw + 7) >> 3;
+  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1u);
+  if (threadIdx.x == 0) {
+    t.cur = (int64_t)p;
+    t.done = 0;
+    t.err = 0;
+  }
+  __syncthreads();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint8_t* q = (const uint8_t*)t.cur;
+      int done = t.done, nr = 0;
+      while (nr < kRunCap && done < count) {
+        uint32_t h = 0;
+        int sh = 0;
+        bool ok = false;
+        while (q < end && sh <= 28) {
+          const uint8_t b = *q++;
+          h |= (uint32_t)(b & 0x7f) << sh;
+          if (!(b & 0x80)) {
+            ok = true;
+            break;
+          }
+          sh += 7;
+        }
+        if (!ok) {
+          t.err = 1;
+          break;
+        }
+        const int64_t left = count - done;
+        int64_t n;
+        t.start[nr] = done;
+        if (h & 1) {
+          const int64_t groups = h >> 1;
+          n = groups * 8;
+          const int64_t bytes = groups * bw;
+          const int64_t need = left < n ? left : n;
+          if (bw > 0 && (int64_t)(end - q) * 8 < need * bw) {  // truncated run
+            t.err = 1;
+            break;
+          }
+          t.ptr[nr] = bw > 0 ? (int64_t)q : 0;
+          t.val[nr] = 0;
+          q += bytes < (int64_t)(end - q) ? bytes : (int64_t)(end - q);
+        } else {
+          n = h >> 1;
+          if (n == 0 || q + nbytes > end) {
+            t.err = 1;
+            break;
+          }
+          uint32_t v = 0;
+          for (int b = 0; b < nbytes; ++b) v |= (uint32_t)q[b] << (8 * b);
+          q += nbytes;
+          t.ptr[nr] = 0;
+          t.val[nr] = v & mask;
+        }
+        done += (int)(left < n ? left : n);
+        ++nr;
+      }
+      t.start[nr] = done;
+      t.nruns = nr;
+      t.cur = (int64_t)q;
+      t.done = done;
+    }
+    __syncthreads();
+    const int nr = t.nruns;
+    const int lo = t.start[0], hi = t.start[nr];
+    if (t.err) return false;
+    for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) {
+      int a = 0, b = nr - 1;
+      while (a < b) {
+        const int m = (a + b + 1) >> 1;
+        if (t.start[m] <= i) a = m;
+        else b = m - 1;
+      }
+      uint32_t v;
+      if (t.ptr[a] == 0) {
+        v = t.val[a];
+      } else {
+        const int64_t bit = (int64_t)(i - t.start[a]) * bw;
+        const uint8_t* q = (const uint8_t*)t.ptr[a] + (bit >> 3);
+        const int sh = (int)(bit & 7);
+        const int nb = (sh + bw + 7) >> 3;
+        uint64_t w = 0;
+        for (int k = 0; k < nb; ++k) w |= (uint64_t)q[k] << (8 * k);
+        v = (uint32_t)(w >> sh) & mask;
+      }
+      sink(i, v);
+    }
+    const bool fin = hi >= count || nr == 0;
+    __syncthreads();
+    if (fin) return true;
+  }
+}
+
+struct WalkState {
+  int64_t pos;
+  int32_t j;
+  int32_t err;
+};
+
+// Positions of `count` PLAIN BYTE_ARRAY values (4-byte little-endian length +
+// bytes) in [p, end). The stream is walked by lane 0 over 8 KiB LDS windows
+// the whole block stages. sink(j, offset_of_bytes, length) runs on lane 0.
+template <typename Sink>
+__device__ bool walk_byte_array(const uint8_t* p, const uint8_t* end, int count, uint8_t* win, WalkState& w,
+                                Sink sink) {
+  const int64_t size = end - p;
+  if (threadIdx.x == 0) {
+    w.pos = 0;
+    w.j = 0;
+    w.err = 0;
+  }
+  __syncthreads();
+  for (;;) {
+    const int64_t wbeg = w.pos;
+    const int j0 = w.j;
+    if (w.err || j0 >= count) break;
+    if (wbeg + 4 > size) {
+      __syncthreads();
+      return false;
+    }
+    const int64_t wlen = size - wbeg < kWalkWin ? size - wbeg : kWalkWin;
+    for (int64_t k = threadIdx.x; k < wlen; k += blockDim.x) win[k] = p[wbeg + k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t pos = wbeg;
+      int j = j0;
+      while (j < count && pos + 4 <= wbeg + wlen) {
+        const uint8_t* q = win + (pos - wbeg);
+        const uint32_t len =
+            (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        if ((int64_t)len > size - pos - 4) {
+          w.err = 1;
+          break;
+        }
+        sink(j, (uint32_t)(pos + 4), len);
+        pos += 4 + (int64_t)len;
+        ++j;
+      }
+      w.pos = pos;
+      w.j = j;
+    }
+    __syncthreads();
+  }
+  const bool ok = w.err == 0;
+  __syncthreads();
+  return ok;
+}
+
+__device__ inline int block_sum_int(int v, int* red) {
+  v = (int)wave_reduce_sum((int64_t)v);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = v;
+  __syncthreads();
+  int t = 0;
+  for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+__device__ inline const uint8_t* data_ptr(const PqPage& pg, const PqDecodeSpec& s) {
+  return ((pg.flags & PQ_DATA_IN_DEC) ? s.dec : s.raw) + pg.data_off;
+}
+__device__ inline const uint8_t* dict_ptr(const PqPage& pg, const PqDecodeSpec& s) {
+  return ((pg.flags & PQ_DICT_IN_DEC) ? s.dec : s.raw) + pg.dict_off;
+}
+
+// big-endian two's complement (FIXED_LEN_BYTE_ARRAY decimal) -> int64
+__device__ inline int64_t flba_to_i64(const uint8_t* p, int len, bool* ovf) {
+  if (len <= 8) {
+    uint64_t u = 0;
+    for (int k = 0; k < len; ++k) u = (u << 8) | p[k];
+    const int sh = 64 - 8 * len;
+    return sh >= 64 ? 0 : (int64_t)(u << sh) >> sh;
+  }
+  uint64_t u = 0;
+  for (int k = len - 8; k < len; ++k) u = (u << 8) | p[k];
+  const int64_t v = (int64_t)u;
+  const uint8_t sign = v < 0 ? 0xff : 0;
+  for (int k = 0; k < len - 8; ++k)
+    if (p[k] != sign) *ovf = true;
+  return v;
+}
+
+// One output row of a fixed-width column from its source bytes.
+__device__ inline void store_fixed(const PqDecodeSpec& s, int64_t row, const uint8_t* src, int* err) {
+  switch (s.conv) {
+    case PQ_CONV_COPY:
+      if (s.out_width == 4) reinterpret_cast<uint32_t*>(s.out)[row] = ld_u32(src);
+      else reinterpret_cast<uint64_t*>(s.out)[row] = ld_u64(src);
+      break;
+    case PQ_CONV_NARROW: {
+      const uint32_t v = ld_u32(src);
+      if (s.out_width == 1) reinterpret_cast<uint8_t*>(s.out)[row] = (uint8_t)v;
+      else reinterpret_cast<uint16_t*>(s.out)[row] = (uint16_t)v;
+      break;
+    }
+    case PQ_CONV_SEXT:
+      reinterpret_cast<int64_t*>(s.out)[row] = (int64_t)(int32_t)ld_u32(src);
+      break;
+    case PQ_CONV_ZEXT:
+      reinterpret_cast<int64_t*>(s.out)[row] = (int64_t)ld_u32(src);
+      break;
+    case PQ_CONV_F2D: {
+      const uint32_t b = ld_u32(src);
+      float f;
+      __builtin_memcpy(&f, &b, 4);
+      reinterpret_cast<double*>(s.out)[row] = (double)f;
+      break;
+    }
+    case PQ_CONV_FLBA: {
+      bool ovf = false;
+      const int64_t v = flba_to_i64(src, s.type_len, &ovf);
+      if (ovf) set_error(err, PQ_ERR_DECIMAL);
+      reinterpret_cast<int64_t*>(s.out)[row] = v;
+      break;
+    }
+    case PQ_CONV_MUL:
+      reinterpret_cast<int64_t*>(s.out)[row] = (int64_t)ld_u64(src) * s.conv_k;
+      break;
+    case PQ_CONV_DIV:
+      reinterpret_cast<int64_t*>(s.out)[row] = (int64_t)ld_u64(src) / s.conv_k;
+      break;
+    default:
+      set_error(err, PQ_ERR_ENCODING);
+  }
+}
+
+__device__ inline void store_zero(const PqDecodeSpec& s, int64_t row) {
+  if (s.phys == PQ_PHYS_BYTE_ARRAY) {
+    if (s.codes) {
+      s.codes[row] = 0;
+    } else {
+      s.str_len[row] = 0;
+      s.str_pos[row] = 0;
+    }
+    return;
+  }
+  switch (s.out_width) {
+    case 1: reinterpret_cast<uint8_t*>(s.out)[row] = 0; break;
+    case 2: reinterpret_cast<uint16_t*>(s.out)[row] = 0; break;
+    case 4: reinterpret_cast<uint32_t*>(s.out)[row] = 0; break;
+    default: reinterpret_cast<uint64_t*>(s.out)[row] = 0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restrict__ pages, PqDecodeSpec s) {
+  __shared__ RleTable rt;
+  __shared__ WalkState ws;
+  __shared__ uint8_t win[kWalkWin];
+  __shared__ int64_t scan_ws[kWavesPerBlock + 1];
+  __shared__ int red[kWavesPerBlock];
+
+  const PqPage pg = pages[blockIdx.x];
+  if (pg.kind == PQ_PAGE_DICT) return;
+  const int n = pg.num_values;
+  const int64_t row0 = pg.out_row;
+  const uint8_t* p = data_ptr(pg, s);
+  const uint8_t* end = p + pg.size;
+
+  // ---- definition levels -> validity
+  int nnz = n;
+  if (s.max_def > 0) {
+    const uint8_t* lv;
+    const uint8_t* lend;
+    if (pg.kind == PQ_PAGE_DATA_V2) {
+      lv = s.raw + pg.levels_off;
+      lend = lv + pg.levels_len;
+    } else {
+      if (p + 4 > end) {
+        if (threadIdx.x == 0) set_error(s.error, PQ_ERR_TRUNCATED);
+        return;
+      }
+      const uint32_t len = ld_u32(p);
+      lv = p + 4;
+      lend = lv + len;
+      if (lend > end) {
+        if (threadIdx.x == 0) set_error(s.error, PQ_ERR_TRUNCATED);
+        return;
+      }
+      p = lend;
+    }
+    const int bw = 32 - __clz(s.max_def);
+    int local = 0;
+    uint8_t* valid = s.valid ? s.valid + row0 : nullptr;
+    const uint32_t md = (uint32_t)s.max_def;
+    const bool ok = rle_decode(lv, lend, bw, n, rt, [&](int i, uint32_t v) {
+      const uint8_t f = v == md;
+      if (valid) valid[i] = f;
+      local += f;
+    });
+    if (!ok) {
+      if (threadIdx.x == 0) set_error(s.error, PQ_ERR_RLE);
+      return;
+    }
+    nnz = block_sum_int(local, red);
+    if (!s.valid && nnz != n) {
+      if (threadIdx.x == 0) set_error(s.error, PQ_ERR_NULLS);
+      return;
+    }
+  }
+  const bool has_nulls = nnz != n;
+
+  // ---- values -> compact index j (dictionary index / bool / byte-array offset)
+  const int enc = pg.encoding;
+  const bool dict = enc == 2 || enc == 8;
+  const bool bool_rle = s.phys == PQ_PHYS_BOOLEAN && enc == 3;
+  const bool str_plain = s.phys == PQ_PHYS_BYTE_ARRAY && !dict;
+  uint32_t* idx = s.scratch + row0;
+  if (nnz > 0) {
+    bool ok = true;
+    if (dict) {
+      if (p >= end) {
+        ok = false;
+      } else {
+        const int bw = *p;
+        ok = bw <= 32 && rle_decode(p + 1, end, bw, nnz, rt, [&](int j, uint32_t v) { idx[j] = v; });
+      }
+    } else if (bool_rle) {
+      if (p + 4 > end) {
+        ok = false;
+      } else {
+        const uint32_t len = ld_u32(p);
+        ok = p + 4 + len <= end &&
+             rle_decode(p + 4, p + 4 + len, 1, nnz, rt, [&](int j, uint32_t v) { idx[j] = v; });
+      }
+    } else if (enc != 0) {
+      if (threadIdx.x == 0) set_error(s.error, PQ_ERR_ENCODING);
+      return;
+    } else if (str_plain) {
+      if (!walk_byte_array(p, end, nnz, win, ws, [&](int j, uint32_t off, uint32_t) { idx[j] = off; })) {
+        if (threadIdx.x == 0) set_error(s.error, PQ_ERR_BYTE_ARRAY);
+        return;
+      }
+    }
+    if (!ok) {
+      if (threadIdx.x == 0) set_error(s.error, PQ_ERR_RLE);
+      return;
+    }
+  }
+  __syncthreads();
+
+  // ---- rows: compact value index j = number of valid rows before row i
+  const int w_in = (s.phys == PQ_PHYS_INT32 || s.phys == PQ_PHYS_FLOAT) ? 4
+                   : s.phys == PQ_PHYS_FLBA                             ? s.type_len
+                                                                        : 8;
+  const uint8_t* dp = dict ? dict_ptr(pg, s) : nullptr;
+  const uint32_t dcount = (uint32_t)pg.dict_count;
+  int64_t carry = 0;
+  for (int base = 0; base < n; base += kBlock * kItems) {
+    const int i0 = base + (int)threadIdx.x * kItems;
+    int f[kItems];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int i = i0 + k;
+      f[k] = i < n ? (has_nulls ? (int)s.valid[row0 + i] : 1) : 0;
+      cnt += f[k];
+    }
+    int64_t j;
+    if (has_nulls) {
+      int64_t tot;
+      j = carry + block_exclusive_scan(cnt, scan_ws, &tot);
+      carry += tot;
+    } else {
+      j = i0;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int i = i0 + k;
+      if (i >= n) break;
+      const int64_t row = row0 + i;
+      if (!f[k]) {
+        store_zero(s, row);
+        continue;
+      }
+      if (s.phys == PQ_PHYS_BYTE_ARRAY) {
+        if (dict) {
+          const uint32_t d = idx[j];
+          if (d >= dcount) {
+            set_error(s.error, PQ_ERR_DICT_INDEX);
+            store_zero(s, row);
+          } else if (s.codes) {
+            s.codes[row] = pg.dict_base + (int32_t)d;
+          } else {
+            s.str_len[row] = s.dict_len[pg.dict_base + d];
+            s.str_pos[row] = s.dict_pos[pg.dict_base + d];
+          }
+        } else {
+          const uint32_t off = idx[j];
+          s.str_len[row] = (int64_t)ld_u32(p + off - 4);
+          s.str_pos[row] = (int64_t)(p + off);
+        }
+      } else if (s.phys == PQ_PHYS_BOOLEAN) {
+        uint8_t v;
+        if (bool_rle) v = (uint8_t)(idx[j] & 1);
+        else v = (p + (j >> 3) < end) ? (uint8_t)((p[j >> 3] >> (j & 7)) & 1) : 0;
+        reinterpret_cast<uint8_t*>(s.out)[row] = v;
+      } else if (dict) {
+        const uint32_t d = idx[j];
+        if (d >= dcount) {
+          set_error(s.error, PQ_ERR_DICT_INDEX);
+          store_zero(s, row);
+        } else {
+          store_fixed(s, row, dp + (int64_t)d * w_in, s.error);
+        }
+      } else {
+        const uint8_t* src = p + j * w_in;
+        if (src + w_in > end) {
+          set_error(s.error, PQ_ERR_TRUNCATED);
+          store_zero(s, row);
+        } else {
+          store_fixed(s, row, src, s.error);
+        }
+      }
+      ++j;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void pq_dict_strings_kernel(const PqPage* __restrict__ pages, PqDecodeSpec s) {
+  __shared__ WalkState ws;
+  __shared__ uint8_t win[kWalkWin];
+  const PqPage pg = pages[blockIdx.x];
+  if (pg.kind != PQ_PAGE_DICT) return;
+  const uint8_t* p = data_ptr(pg, s);
+  const uint8_t* end = p + pg.size;
+  int64_t* dl = s.dict_len + pg.dict_base;
+  int64_t* dpos = s.dict_pos + pg.dict_base;
+  const bool ok = walk_byte_array(p, end, pg.num_values, win, ws, [&](int j, uint32_t off, uint32_t len) {
+    dl[j] = len;
+    dpos[j] = (int64_t)(p + off);
+  });
+  if (!ok && threadIdx.x == 0) set_error(s.error, PQ_ERR_BYTE_ARRAY);
+}
+
+__global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __restrict__ jobs,
+                                                       const uint8_t* __restrict__ raw, uint8_t* __restrict__ dec,
+                                                       int* __restrict__ err) {
+  __shared__ uint8_t ring[kSnapRing];
+  __shared__ uint8_t inw[kSnapIn];
+  const PqSnappyJob jb = jobs[blockIdx.x];
+  const uint8_t* src = raw + jb.src_off;
+  const int64_t slen = jb.src_len;
+  uint8_t* dst = dec + jb.dst_off;
+  const int64_t dlen = jb.dst_len;
+  const int lane = threadIdx.x;
+  int64_t wbeg = 0, wend = 0;
+
+  auto refill = [&](int64_t at) {
+    __syncthreads();
+    wbeg = at;
+    wend = slen < at + kSnapIn ? slen : at + kSnapIn;
+    for (int64_t k = lane; k < wend - wbeg; k += 64) inw[k] = src[wbeg + k];
+    __syncthreads();
+  };
+  auto fail = [&](int code) {
+    if (lane == 0) set_error(err, code);
+  };
+  refill(0);
+  int64_t ip = 0;
+  uint64_t ulen = 0;
+  for (int sh = 0;; sh += 7) {
+    if (ip >= wend || sh > 35) return fail(PQ_ERR_SNAPPY);
+    const uint32_t b = inw[ip++ - wbeg];
+    ulen |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) break;
+  }
+  if ((int64_t)ulen != dlen) return fail(PQ_ERR_SNAPPY_SIZE);
+  int64_t op = 0;
+  while (ip < slen) {
+    if (ip + 5 > wend && wend < slen) refill(ip);
+    const uint32_t tag = inw[ip - wbeg];
+    int64_t len, off;
+    if ((tag & 3) == 0) {
+      len = (tag >> 2) + 1;
+      ip += 1;
+      if (len > 60) {
+        const int nb = (int)len - 60;
+        if (ip + nb > wend) return fail(PQ_ERR_SNAPPY);
+        len = 0;
+        for (int b = 0; b < nb; ++b) len |= (int64_t)inw[ip + b - wbeg] << (8 * b);
+        len += 1;
+        ip += nb;
+      }
+      if (ip + len > slen || op + len > dlen) return fail(PQ_ERR_SNAPPY);
+      for (int64_t k = lane; k < len; k += 64) {
+        const uint8_t v = src[ip + k];
+        dst[op + k] = v;
+        ring[(op + k) & (kSnapRing - 1)] = v;
+      }
+      ip += len;
+      op += len;
+      continue;
+    }
+    const int kind = tag & 3;
+    const int hdr = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+    if (ip + hdr > wend) return fail(PQ_ERR_SNAPPY);
+    const uint8_t* q = inw + (ip - wbeg);
+    if (kind == 1) {
+      len = ((tag >> 2) & 7) + 4;
+      off = ((int64_t)(tag >> 5) << 8) | q[1];
+    } else if (kind == 2) {
+      len = (tag >> 2) + 1;
+      off = (int64_t)q[1] | ((int64_t)q[2] << 8);
+    } else {
+      len = (tag >> 2) + 1;
+      off = (int64_t)q[1] | ((int64_t)q[2] << 8) | ((int64_t)q[3] << 16) | ((int64_t)q[4] << 24);
+    }
+    ip += hdr;
+    if (off <= 0 || off > op || off >= kSnapRing || op + len > dlen) return fail(PQ_ERR_SNAPPY);
+    // len <= 64: one pass of the wave; an overlapping copy repeats the last `off` bytes
+    uint8_t v = 0;
+    if (lane < len) v = ring[(op - off + (lane % off)) & (kSnapRing - 1)];
+    if (lane < len) {
+      dst[op + lane] = v;
+      ring[(op + lane) & (kSnapRing - 1)] = v;
+    }
+    op += len;
+  }
+  if (op != dlen) fail(PQ_ERR_SNAPPY_SIZE);
+}
+
+__global__ __launch_bounds__(kBlock) void pq_str_copy_kernel(const int64_t* __restrict__ pos,
+                                                             const int64_t* __restrict__ off, int64_t n,
+                                                             uint8_t* __restrict__ out) {
+  // one wave copies 64 consecutive strings, its lanes striding over each string's bytes
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t r0 = wave * kWave; r0 < n; r0 += nwaves * kWave) {
+    const int64_t r1 = r0 + kWave < n ? r0 + kWave : n;
+    for (int64_t r = r0; r < r1; ++r) {
+      const uint8_t* sp = reinterpret_cast<const uint8_t*>(pos[r]);
+      const int64_t o = off[r], len = off[r + 1] - o;
+      for (int64_t k = lane; k < len; k += kWave) out[o + k] = sp[k];
+    }
+  }
+}
+
+}  // namespace
+
+void pq_snappy(const PqSnappyJob* jobs, int64_t njobs, const uint8_t* raw, uint8_t* dec, int* error,
+               hipStream_t stream) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(pq_snappy_kernel, dim3((unsigned)njobs), dim3(64), 0, stream, jobs, raw, dec, error);
+  check_launch("pq_snappy", stream);
+}
+
+void pq_dict_strings(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream) {
+  if (npages <= 0) return;
+  hipLaunchKernelGGL(pq_dict_strings_kernel, dim3((unsigned)npages), dim3(kBlock), 0, stream, pages, spec);
+  check_launch("pq_dict_strings", stream);
+}
+
+void pq_decode(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream) {
+  if (npages <= 0) return;
+  hipLaunchKernelGGL(pq_decode_kernel, dim3((unsigned)npages), dim3(kBlock), 0, stream, pages, spec);
+  check_launch("pq_decode", stream);
+}
+
+void pq_str_copy(const int64_t* pos, const int64_t* off, int64_t n, uint8_t* out, hipStream_t stream) {
+  if (n <= 0) return;
+  const unsigned grid = grid_for(n, kBlock, 8192);
+  hipLaunchKernelGGL(pq_str_copy_kernel, dim3(grid), dim3(kBlock), 0, stream, pos, off, n, out);
+  check_launch("pq_str_copy", stream);
+}
+
+}  // namespace kern
+}  // namespace igloo
