@@ -421,13 +421,13 @@ PYBIND11_MODULE(_native, m) {
     io::pread_ranges(path, rs, threads);
   });
   m.def("pq_plan", [](uintptr_t host, const std::vector<std::tuple<int64_t, int64_t, int, int64_t, int64_t>>& chunks,
-                      int phys, int max_def, int max_rep) {
+                      int phys, int max_def, int max_rep, int64_t dec_base) {
     std::vector<io::PqChunkIn> cs;
     for (auto& [off, len, codec, first, rows] : chunks) cs.push_back({off, len, codec, first, rows});
     io::PqPlan plan;
     {
       py::gil_scoped_release rel;
-      plan = io::plan_column(P<const uint8_t>(host), cs, phys, max_def, max_rep);
+      plan = io::plan_column(P<const uint8_t>(host), cs, phys, max_def, max_rep, dec_base);
     }
     py::dict d;
     d["pages"] = py::bytes((const char*)plan.pages.data(), plan.pages.size());
@@ -441,19 +441,27 @@ PYBIND11_MODULE(_native, m) {
     d["max_page_values"] = plan.max_page_values;
     d["unsupported"] = plan.unsupported;
     return d;
-  }, "Plan GPU decode descriptors for one column's chunks staged at `host`");
+  }, "Plan GPU decode descriptors for one column's chunks staged at `host`",
+     py::arg("host"), py::arg("chunks"), py::arg("phys"), py::arg("max_def"), py::arg("max_rep"),
+     py::arg("dec_base") = 0);
+  m.def("pq_pack_spec", [](const py::dict& spec, bool need_output) {
+    kern::PqDecodeSpec sp = decode_spec(spec, need_output);
+    return py::bytes(reinterpret_cast<const char*>(&sp), sizeof(sp));
+  }, "Validated binary PqDecodeSpec (concatenate one per column and upload)");
+  m.attr("PQ_SPEC_BYTES") = (int)sizeof(kern::PqDecodeSpec);
   m.def("pq_snappy", [](uintptr_t jobs, int64_t njobs, uintptr_t raw, uintptr_t dec, uintptr_t err, uintptr_t s) {
     if (njobs > 0 && (!jobs || !raw || !dec || !err)) throw std::runtime_error("pq_snappy: null buffer");
     kern::pq_snappy(P<const kern::PqSnappyJob>(jobs), njobs, P<const uint8_t>(raw), P<uint8_t>(dec), P<int>(err), S(s));
   });
-  m.def("pq_dict_strings", [](uintptr_t pages, int64_t npages, const py::dict& spec, uintptr_t s) {
-    kern::PqDecodeSpec sp = decode_spec(spec, false);
-    if (!sp.dict_len || !sp.dict_pos) throw std::runtime_error("pq_dict_strings: missing dictionary tables");
-    kern::pq_dict_strings(P<const kern::PqPage>(pages), npages, sp, S(s));
+  m.def("pq_dict_strings", [](uintptr_t pages, int64_t npages, uintptr_t page_col, uintptr_t specs, uintptr_t s) {
+    if (npages > 0 && (!pages || !page_col || !specs)) throw std::runtime_error("pq_dict_strings: null buffer");
+    kern::pq_dict_strings(P<const kern::PqPage>(pages), npages, P<const int32_t>(page_col),
+                          P<const kern::PqDecodeSpec>(specs), S(s));
   });
-  m.def("pq_decode", [](uintptr_t pages, int64_t npages, const py::dict& spec, uintptr_t s) {
-    kern::PqDecodeSpec sp = decode_spec(spec);
-    kern::pq_decode(P<const kern::PqPage>(pages), npages, sp, S(s));
+  m.def("pq_decode", [](uintptr_t pages, int64_t npages, uintptr_t page_col, uintptr_t specs, uintptr_t s) {
+    if (npages > 0 && (!pages || !page_col || !specs)) throw std::runtime_error("pq_decode: null buffer");
+    kern::pq_decode(P<const kern::PqPage>(pages), npages, P<const int32_t>(page_col),
+                    P<const kern::PqDecodeSpec>(specs), S(s));
   });
   m.def("pq_str_copy", [](uintptr_t pos, uintptr_t off, int64_t n, uintptr_t out, uintptr_t s) {
     kern::pq_str_copy(P<const int64_t>(pos), P<const int64_t>(off), n, P<uint8_t>(out), S(s));

@@ -527,8 +527,10 @@ void pread_ranges(const std::string& path, const std::vector<ReadRange>& ranges,
   if (!err.empty()) throw ParquetError(err);
 }
 
-PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, int phys, int max_def, int max_rep) {
+PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, int phys, int max_def, int max_rep,
+                   int64_t dec_base) {
   PqPlan plan;
+  plan.dec_bytes = align_up(dec_base, 16);
   if (max_rep > 0) {
     plan.unsupported = "repeated (nested) column";
     return plan;

@@ -129,8 +129,10 @@ struct PqPlan {
   std::string unsupported;   // non-empty: this column needs the host decoder
 };
 
+// dec_base: first free byte of the (shared) decompression buffer; plan.dec_bytes
+// is returned as the end of this column's slots (dec_base included).
 PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, int phys_type, int max_def,
-                   int max_rep);
+                   int max_rep, int64_t dec_base = 0);
 
 }  // namespace io
 }  // namespace igloo

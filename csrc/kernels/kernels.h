@@ -248,8 +248,11 @@ struct PqDecodeSpec {
 
 void pq_snappy(const PqSnappyJob* jobs, int64_t njobs, const uint8_t* raw, uint8_t* dec, int* error,
                hipStream_t stream);
-void pq_dict_strings(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream);
-void pq_decode(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream);
+// pages of several columns in one launch: page_col[i] indexes specs[] (device arrays)
+void pq_dict_strings(const PqPage* pages, int64_t npages, const int32_t* page_col, const PqDecodeSpec* specs,
+                     hipStream_t stream);
+void pq_decode(const PqPage* pages, int64_t npages, const int32_t* page_col, const PqDecodeSpec* specs,
+               hipStream_t stream);
 void pq_str_copy(const int64_t* pos, const int64_t* off, int64_t n, uint8_t* out, hipStream_t stream);
 
 }  // namespace kern

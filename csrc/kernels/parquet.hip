@@ -5,7 +5,8 @@
 // thread) with device decoding of whole column chunks that were staged into
 // HBM with one H2D copy (host side: csrc/io/parquet_meta.cpp plans the pages).
 //
-// Kernels (one launch per column, one workgroup per page):
+// Kernels (one launch for every page of every column of a scan, one workgroup
+// per page; page_col[] selects the page's column spec):
 //   pq_snappy_kernel       raw snappy -> dec buffer. One wave per compressed
 //                          page; every lane parses the same tag from an LDS
 //                          input window (broadcast reads), copies are spread
@@ -322,7 +323,9 @@ __device__ inline void store_zero(const PqDecodeSpec& s, int64_t row) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restrict__ pages, PqDecodeSpec s) {
+__global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restrict__ pages,
+                                                           const int32_t* __restrict__ page_col,
+                                                           const PqDecodeSpec* __restrict__ specs) {
   __shared__ RleTable rt;
   __shared__ WalkState ws;
   __shared__ uint8_t win[kWalkWin];
@@ -331,6 +334,7 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
 
   const PqPage pg = pages[blockIdx.x];
   if (pg.kind == PQ_PAGE_DICT) return;
+  const PqDecodeSpec s = specs[page_col[blockIdx.x]];
   const int n = pg.num_values;
   const int64_t row0 = pg.out_row;
   const uint8_t* p = data_ptr(pg, s);
@@ -496,11 +500,15 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
   }
 }
 
-__global__ __launch_bounds__(kBlock) void pq_dict_strings_kernel(const PqPage* __restrict__ pages, PqDecodeSpec s) {
+__global__ __launch_bounds__(kBlock) void pq_dict_strings_kernel(const PqPage* __restrict__ pages,
+                                                                 const int32_t* __restrict__ page_col,
+                                                                 const PqDecodeSpec* __restrict__ specs) {
   __shared__ WalkState ws;
   __shared__ uint8_t win[kWalkWin];
   const PqPage pg = pages[blockIdx.x];
   if (pg.kind != PQ_PAGE_DICT) return;
+  const PqDecodeSpec s = specs[page_col[blockIdx.x]];
+  if (s.phys != PQ_PHYS_BYTE_ARRAY || !s.dict_len) return;
   const uint8_t* p = data_ptr(pg, s);
   const uint8_t* end = p + pg.size;
   int64_t* dl = s.dict_len + pg.dict_base;
@@ -625,15 +633,17 @@ void pq_snappy(const PqSnappyJob* jobs, int64_t njobs, const uint8_t* raw, uint8
   check_launch("pq_snappy", stream);
 }
 
-void pq_dict_strings(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream) {
+void pq_dict_strings(const PqPage* pages, int64_t npages, const int32_t* page_col, const PqDecodeSpec* specs,
+                     hipStream_t stream) {
   if (npages <= 0) return;
-  hipLaunchKernelGGL(pq_dict_strings_kernel, dim3((unsigned)npages), dim3(kBlock), 0, stream, pages, spec);
+  hipLaunchKernelGGL(pq_dict_strings_kernel, dim3((unsigned)npages), dim3(kBlock), 0, stream, pages, page_col, specs);
   check_launch("pq_dict_strings", stream);
 }
 
-void pq_decode(const PqPage* pages, int64_t npages, const PqDecodeSpec& spec, hipStream_t stream) {
+void pq_decode(const PqPage* pages, int64_t npages, const int32_t* page_col, const PqDecodeSpec* specs,
+               hipStream_t stream) {
   if (npages <= 0) return;
-  hipLaunchKernelGGL(pq_decode_kernel, dim3((unsigned)npages), dim3(kBlock), 0, stream, pages, spec);
+  hipLaunchKernelGGL(pq_decode_kernel, dim3((unsigned)npages), dim3(kBlock), 0, stream, pages, page_col, specs);
   check_launch("pq_decode", stream);
 }
 

@@ -10,10 +10,12 @@ Pipeline per scan:
      csrc/io/parquet_meta.cpp) — schema leaves, row groups, chunk offsets;
   2. staging: the projected column chunks of this rank's row groups are read
      with multithreaded ``pread`` straight into one pinned host buffer per
-     column, then copied to HBM in one non-blocking H2D transfer (the next
-     column's reads overlap the previous column's copy and decode);
+     batch of columns (<= 4 GiB), then copied to HBM in one non-blocking H2D
+     transfer (the next batch's reads overlap the previous batch's decode);
   3. planning: the C++ planner walks the page headers in the pinned buffer and
-     emits device page descriptors + snappy jobs;
+     emits device page descriptors + snappy jobs; the pages of every column
+     of a batch go to ONE launch of each kernel (page -> column spec table),
+     so small columns do not leave the GPU idle;
   4. device: ``pq_snappy`` (one wave per compressed page, LDS history ring),
      ``pq_dict_strings`` (dictionary entry positions), ``pq_decode`` (levels ->
      validity, PLAIN / RLE_DICTIONARY values -> typed columns with the type
@@ -48,6 +50,8 @@ ERRORS = {1: "malformed RLE/bit-packed stream", 2: "dictionary index out of rang
           7: "unsupported page encoding", 8: "NULL in a column whose statistics say it has none",
           9: "truncated page"}
 READ_THREADS = int(os.environ.get("IGLOO_PARQUET_READ_THREADS", "8"))
+#: staged bytes per decode batch (pinned host buffer + one set of launches)
+BATCH_BYTES = int(os.environ.get("IGLOO_PARQUET_BATCH_BYTES", str(4 << 30)))
 
 
 class FileMeta:
@@ -142,26 +146,43 @@ class GpuParquetReader:
     def read(self, columns: Sequence[Tuple[str, T.DataType]], groups: Sequence[Tuple[int, int]],
              device) -> Tuple[Dict[str, Column], Dict[str, str]]:
         """Decode ``columns`` over row groups ``groups`` ([(file index, rg)]).
-        Returns (decoded columns, {column: reason} for those left to the host)."""
+        Returns (decoded columns, {column: reason} for those left to the host).
+
+        Columns are staged in batches of at most BATCH_BYTES; every batch is one
+        pinned buffer, one H2D copy, one snappy launch and one decode launch
+        over the pages of all its columns (the next batch's reads overlap the
+        previous batch's device work)."""
         device = torch.device(device)
         N = native()
         out: Dict[str, Column] = {}
         rejected: Dict[str, str] = {}
         err = torch.zeros(1, dtype=torch.int32, device=device)
         keep = []  # pinned staging buffers must outlive their async H2D copies
-        st = {"read_s": 0.0, "plan_s": 0.0, "bytes": 0, "pages": 0}
+        st = {"read_s": 0.0, "plan_s": 0.0, "bytes": 0, "pages": 0, "batches": 0}
         t0 = time.perf_counter()
         nrows = sum(self.metas[fi].row_groups[rg]["num_rows"] for fi, rg in groups)
+        todo = []
         for name, dt in columns:
             why = self.supports(name, dt)
             if why is not None:
                 rejected[name] = why
-                continue
-            col = self._read_column(N, name, dt, groups, nrows, device, err, keep, st)
-            if isinstance(col, str):
-                rejected[name] = col
+            elif not groups:
+                out[name] = _empty_column(dt, device)
             else:
-                out[name] = col
+                lay = self._layout(name, dt, groups)
+                if isinstance(lay, str):
+                    rejected[name] = lay
+                else:
+                    todo.append(lay)
+        batch, size = [], 0
+        for lay in todo:
+            if batch and size + lay["bytes"] > BATCH_BYTES:
+                self._read_batch(N, batch, nrows, device, err, keep, st, out, rejected)
+                batch, size = [], 0
+            batch.append(lay)
+            size += lay["bytes"]
+        if batch:
+            self._read_batch(N, batch, nrows, device, err, keep, st, out, rejected)
         if out:
             code = int(err.item())  # one sync for every column of the scan
             if code:
@@ -171,88 +192,129 @@ class GpuParquetReader:
         return out, rejected
 
     # --------------------------------------------------------------- internals
-    def _read_column(self, N, name, dt, groups, nrows, device, err, keep, st):
-        if not groups:
-            return _empty_column(dt, device)
+    def _layout(self, name, dt, groups):
+        """Chunk byte ranges of one column over ``groups`` (or a reason string)."""
         m0 = self.metas[groups[0][0]]
         leaf0 = m0.leaves[m0.leaf_index[name]]
-        conv, out_w, factor = conversion(leaf0, dt)
-        chunks, per_file, total, first_row, may_null = [], {}, 0, 0, False
+        conv = conversion(leaf0, dt)
+        ranges, total, first_row, may_null = [], 0, 0, False
         for fi, rg in groups:
             m = self.metas[fi]
-            li = m.leaf_index[name]
-            leaf = m.leaves[li]
-            if leaf["type"] != leaf0["type"] or conversion(leaf, dt) != (conv, out_w, factor) \
-                    or leaf["max_def"] != leaf0["max_def"]:
+            leaf = m.leaves[m.leaf_index[name]]
+            if leaf["type"] != leaf0["type"] or conversion(leaf, dt) != conv or leaf["max_def"] != leaf0["max_def"]:
                 return "files disagree on the column's physical layout"
             g = m.row_groups[rg]
-            c = g["chunks"][li]
-            per_file.setdefault(fi, []).append((c["start"], c["length"], total))
-            chunks.append((total, c["length"], c["codec"], first_row, g["num_rows"]))
+            c = g["chunks"][m.leaf_index[name]]
+            ranges.append((fi, c["start"], c["length"], total, c["codec"], first_row, g["num_rows"]))
             if leaf["max_def"] > 0 and (c["null_count"] is None or c["null_count"] > 0):
                 may_null = True
             first_row += g["num_rows"]
             total += (c["length"] + 63) // 64 * 64
+        return {"name": name, "dt": dt, "leaf": leaf0, "conv": conv, "ranges": ranges, "bytes": total,
+                "may_null": may_null}
+
+    def _read_batch(self, N, batch, n, device, err, keep, st, out, rejected):
+        # ---- stage every column of the batch into one pinned buffer
+        base = 0
+        for lay in batch:
+            lay["base"] = base
+            base += lay["bytes"]
         t0 = time.perf_counter()
-        host = torch.empty(total + 64, dtype=torch.uint8, pin_memory=True)
+        host = torch.empty(base + 64, dtype=torch.uint8, pin_memory=True)
         hp = host.data_ptr()
+        per_file: Dict[int, list] = {}
+        for lay in batch:
+            for fi, start, length, off, *_ in lay["ranges"]:
+                per_file.setdefault(fi, []).append((start, length, hp + lay["base"] + off))
         for fi, rs in per_file.items():
-            N.pq_pread(self.files[fi], [(s, n, hp + off) for s, n, off in rs], READ_THREADS)
+            N.pq_pread(self.files[fi], rs, READ_THREADS)
         st["read_s"] += time.perf_counter() - t0
-        st["bytes"] += total
-        raw = torch.empty(total + 64, dtype=torch.uint8, device=device)
+        st["bytes"] += base
+        st["batches"] += 1
+        raw = torch.empty(base + 64, dtype=torch.uint8, device=device)
         raw.copy_(host, non_blocking=True)
         keep.append(host)
+        # ---- plan pages of every column (shared raw / dec buffers)
         t1 = time.perf_counter()
-        try:
-            plan = N.pq_plan(hp, chunks, leaf0["type"], leaf0["max_def"], leaf0["max_rep"])
-        except RuntimeError as e:
-            raise IoError(f"corrupt parquet column {name}: {e}") from e
+        plans, dec_end = [], 0
+        for lay in batch:
+            chunks = [(lay["base"] + off, length, codec, first, rows)
+                      for _fi, _s, length, off, codec, first, rows in lay["ranges"]]
+            leaf = lay["leaf"]
+            try:
+                plan = N.pq_plan(hp, chunks, leaf["type"], leaf["max_def"], leaf["max_rep"], dec_end)
+            except RuntimeError as e:
+                raise IoError(f"corrupt parquet column {lay['name']}: {e}") from e
+            if plan["unsupported"]:
+                rejected[lay["name"]] = plan["unsupported"]
+                continue
+            dec_end = plan["dec_bytes"]
+            plans.append((lay, plan))
         st["plan_s"] += time.perf_counter() - t1
-        if plan["unsupported"]:
-            return plan["unsupported"]
-        st["pages"] += plan["num_pages"]
-        pages = _upload(plan["pages"], device)
-        dec = torch.empty(plan["dec_bytes"] + 64, dtype=torch.uint8, device=device) if plan["dec_bytes"] else None
+        if not plans:
+            return
         s = stream(raw)
-        if plan["num_jobs"]:
-            jobs = _upload(plan["jobs"], device)
-            launch("pq_snappy").pq_snappy(ptr(jobs), plan["num_jobs"], ptr(raw), ptr(dec), ptr(err), s)
-        n = nrows
-        valid = torch.empty(n, dtype=torch.bool, device=device) if (leaf0["max_def"] > 0 and may_null) else None
-        scratch = torch.empty(max(n, 1), dtype=torch.int32, device=device)
-        spec = dict(phys=leaf0["type"], type_len=leaf0["type_length"], out_width=out_w, conv=CONV[conv],
-                    conv_k=factor, max_def=leaf0["max_def"], out=0, valid=ptr(valid), scratch=ptr(scratch),
-                    str_len=0, str_pos=0, codes=0, dict_len=0, dict_pos=0, raw=ptr(raw), dec=ptr(dec),
-                    error=ptr(err))
-        if dt.kind != "utf8":
-            tdt = torch.bool if dt.kind == "bool" else dt.torch_dtype
-            data = torch.empty(n, dtype=tdt, device=device)
-            spec["out"] = ptr(data)
-            launch("pq_decode").pq_decode(ptr(pages), plan["num_pages"], spec, s)
-            return Column(dt, data, valid)
-        # ---- strings
-        E = plan["dict_entries"]
-        dlen = dpos = None
-        if E:
-            dlen = torch.empty(E, dtype=torch.int64, device=device)
-            dpos = torch.empty(E, dtype=torch.int64, device=device)
-            spec.update(dict_len=ptr(dlen), dict_pos=ptr(dpos))
-            launch("pq_dict_strings").pq_dict_strings(ptr(pages), plan["num_pages"], spec, s)
-        if E and plan["plain_pages"] == 0:
-            codes = torch.empty(max(n, 1), dtype=torch.int32, device=device)
-            spec["codes"] = ptr(codes)
-            launch("pq_decode").pq_decode(ptr(pages), plan["num_pages"], spec, s)
-            dictionary = _gather_strings(dpos, dlen, device, s)
-            from ..ops.strings import dict_encode
-            enc = dict_encode(dictionary)  # entries repeated across chunk dictionaries -> one code
-            codes = enc.data.index_select(0, codes[:n].long()).to(torch.int32)
-            return Column(T.UTF8, codes, valid, dictionary=enc.dictionary)
-        slen = torch.empty(max(n, 1), dtype=torch.int64, device=device)
-        spos = torch.empty(max(n, 1), dtype=torch.int64, device=device)
-        spec.update(str_len=ptr(slen), str_pos=ptr(spos))
-        launch("pq_decode").pq_decode(ptr(pages), plan["num_pages"], spec, s)
-        return _gather_strings(spos[:n], slen[:n], device, s, valid)
+        dec = torch.empty(dec_end + 64, dtype=torch.uint8, device=device) if dec_end else None
+        jobs = b"".join(p["jobs"] for _, p in plans)
+        njobs = sum(p["num_jobs"] for _, p in plans)
+        if njobs:
+            jt = _upload(jobs, device)
+            launch("pq_snappy").pq_snappy(ptr(jt), njobs, ptr(raw), ptr(dec), ptr(err), s)
+        # ---- outputs + one spec per column
+        specs, page_col, pages, posts = [], [], [], []
+        scratch = torch.empty(max(n, 1) * len(plans), dtype=torch.int32, device=device)
+        for ci, (lay, plan) in enumerate(plans):
+            leaf, dt = lay["leaf"], lay["dt"]
+            conv, out_w, factor = lay["conv"]
+            valid = torch.empty(n, dtype=torch.bool, device=device) if (leaf["max_def"] > 0 and lay["may_null"]) else None
+            spec = dict(phys=leaf["type"], type_len=leaf["type_length"], out_width=out_w, conv=CONV[conv],
+                        conv_k=factor, max_def=leaf["max_def"], out=0, valid=ptr(valid),
+                        scratch=ptr(scratch) + 4 * ci * max(n, 1), str_len=0, str_pos=0, codes=0, dict_len=0,
+                        dict_pos=0, raw=ptr(raw), dec=ptr(dec), error=ptr(err))
+            post = {"lay": lay, "valid": valid}
+            if dt.kind != "utf8":
+                data = torch.empty(n, dtype=torch.bool if dt.kind == "bool" else dt.torch_dtype, device=device)
+                spec["out"] = ptr(data)
+                post["data"] = data
+            else:
+                E = plan["dict_entries"]
+                if E:
+                    post["dlen"] = torch.empty(E, dtype=torch.int64, device=device)
+                    post["dpos"] = torch.empty(E, dtype=torch.int64, device=device)
+                    spec.update(dict_len=ptr(post["dlen"]), dict_pos=ptr(post["dpos"]))
+                if E and plan["plain_pages"] == 0:
+                    post["codes"] = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+                    spec["codes"] = ptr(post["codes"])
+                else:
+                    post["slen"] = torch.empty(max(n, 1), dtype=torch.int64, device=device)
+                    post["spos"] = torch.empty(max(n, 1), dtype=torch.int64, device=device)
+                    spec.update(str_len=ptr(post["slen"]), str_pos=ptr(post["spos"]))
+            specs.append(N.pq_pack_spec(spec, True))
+            pages.append(plan["pages"])
+            page_col += [ci] * plan["num_pages"]
+            posts.append(post)
+            st["pages"] += plan["num_pages"]
+        npages = len(page_col)
+        pt = _upload(b"".join(pages), device)
+        pc = torch.tensor(page_col, dtype=torch.int32).to(device)
+        sp = _upload(b"".join(specs), device)
+        if any("dlen" in p for p in posts):
+            launch("pq_dict_strings").pq_dict_strings(ptr(pt), npages, ptr(pc), ptr(sp), s)
+        launch("pq_decode").pq_decode(ptr(pt), npages, ptr(pc), ptr(sp), s)
+        # ---- strings: dictionaries / offsets + bytes
+        for post in posts:
+            lay = post["lay"]
+            name, dt, valid = lay["name"], lay["dt"], post["valid"]
+            if "data" in post:
+                out[name] = Column(dt, post["data"], valid)
+            elif "codes" in post:
+                dictionary = _gather_strings(post["dpos"], post["dlen"], device, s)
+                from ..ops.strings import dict_encode
+                enc = dict_encode(dictionary)  # entries repeated across chunk dictionaries -> one code
+                codes = enc.data.index_select(0, post["codes"][:n].long()).to(torch.int32)
+                out[name] = Column(T.UTF8, codes, valid, dictionary=enc.dictionary)
+            else:
+                out[name] = _gather_strings(post["spos"][:n], post["slen"][:n], device, s, valid)
 
 
 def _upload(b: bytes, device) -> torch.Tensor:
