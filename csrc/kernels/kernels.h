@@ -196,6 +196,14 @@ void textgen_lengths(const TextGenParams& p, int64_t n, int64_t* lens, bool devi
 void textgen_write(const TextGenParams& p, int64_t n, const int64_t* off, uint8_t* chars, bool device,
                    hipStream_t stream);
 
+// ---- ranges.hip ----------------------------------------------------------------
+// big: non-decreasing int32/int64 keys; per probe key q[i]: big[lo[i] .. lo[i]+cnt[i]) == q[i]
+void sorted_ranges(const void* big, bool key64, int64_t nb, const void* q, const uint8_t* qvalid, int64_t nq,
+                   int64_t* lo, int64_t* cnt, hipStream_t stream);
+// off: exclusive offsets [ns] of the range lengths (total = sum); pairs (s, lo[s] + k) for k < len(s)
+void expand_ranges(const int64_t* off, const int64_t* lo, int64_t ns, int64_t total, void* sidx, void* bidx,
+                   bool out64, hipStream_t stream);
+
 // ---- parquet.hip ---------------------------------------------------------------
 enum PqPhys : int { PQ_PHYS_BOOLEAN = 0, PQ_PHYS_INT32 = 1, PQ_PHYS_INT64 = 2, PQ_PHYS_INT96 = 3, PQ_PHYS_FLOAT = 4,
                     PQ_PHYS_DOUBLE = 5, PQ_PHYS_BYTE_ARRAY = 6, PQ_PHYS_FLBA = 7 };

@@ -1,0 +1,146 @@
+// Sorted-key join primitives for clustered inputs (lineitem by l_orderkey,
+// orders by o_orderkey, and every join output that preserved that order).
+//
+//   sorted_ranges: for each probe key, the range [lo, lo+cnt) of equal keys in
+//     a non-decreasing build column — one lower-bound binary search, then a
+//     short forward scan (TPC-H keys repeat <= 7 times) that falls back to a
+//     second binary search for long runs. Replaces two torch.searchsorted
+//     passes.
+//   expand_ranges: the (probe row, build row) pairs of those ranges, output
+//     parallel and load balanced: a workgroup owns 2048 consecutive outputs,
+//     finds the probe rows overlapping them with two binary searches over the
+//     exclusive offsets, stages those offsets in LDS and lets every lane
+//     binary-search its outputs there; stores are coalesced. Replaces
+//     torch.repeat_interleave + cumsum + index_select (one thread per probe
+//     row writing its run: 17 ms for one 60M-pair expansion at SF100).
+#include "common.h"
+#include "kernels.h"
+
+namespace igloo {
+namespace kern {
+
+namespace {
+
+constexpr int kExpItems = 8;
+constexpr int kExpTile = kBlock * kExpItems;
+constexpr int kScanRun = 16;
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void sorted_ranges_kernel(const K* __restrict__ big, int64_t nb,
+                                                              const K* __restrict__ q,
+                                                              const uint8_t* __restrict__ qvalid, int64_t nq,
+                                                              int64_t* __restrict__ lo_out,
+                                                              int64_t* __restrict__ cnt_out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+    if (qvalid && !qvalid[i]) {
+      lo_out[i] = 0;
+      cnt_out[i] = 0;
+      continue;
+    }
+    const K key = q[i];
+    int64_t a = 0, b = nb;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (big[m] < key) a = m + 1;
+      else b = m;
+    }
+    int64_t e = a;
+    int k = 0;
+    while (e < nb && k < kScanRun && big[e] == key) {
+      ++e;
+      ++k;
+    }
+    if (k == kScanRun && e < nb && big[e] == key) {
+      int64_t a2 = e, b2 = nb;
+      while (a2 < b2) {
+        const int64_t m = (a2 + b2) >> 1;
+        if (big[m] <= key) a2 = m + 1;
+        else b2 = m;
+      }
+      e = a2;
+    }
+    lo_out[i] = a;
+    cnt_out[i] = e - a;
+  }
+}
+
+// largest r in [0, n) with off[r] <= t (off non-decreasing, off[0] <= t)
+__device__ inline int64_t row_of(const int64_t* off, int64_t n, int64_t t) {
+  int64_t a = 0, b = n - 1;
+  while (a < b) {
+    const int64_t m = (a + b + 1) >> 1;
+    if (off[m] <= t) a = m;
+    else b = m - 1;
+  }
+  return a;
+}
+
+template <typename O>
+__global__ __launch_bounds__(kBlock) void expand_ranges_kernel(const int64_t* __restrict__ off,
+                                                              const int64_t* __restrict__ lo, int64_t ns,
+                                                              int64_t total, O* __restrict__ sidx,
+                                                              O* __restrict__ bidx) {
+  __shared__ int64_t soff[kExpTile + 1];
+  __shared__ int64_t rr[2];
+  const int64_t t0 = (int64_t)blockIdx.x * kExpTile;
+  if (t0 >= total) return;
+  const int64_t t1 = t0 + kExpTile < total ? t0 + kExpTile : total;
+  if (threadIdx.x == 0) {
+    rr[0] = row_of(off, ns, t0);
+    rr[1] = row_of(off, ns, t1 - 1);
+  }
+  __syncthreads();
+  const int64_t r0 = rr[0], nr = rr[1] - rr[0] + 1;
+  if (nr <= kExpTile) {
+    for (int64_t k = threadIdx.x; k < nr; k += blockDim.x) soff[k] = off[r0 + k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kExpItems; ++k) {
+      const int64_t t = t0 + threadIdx.x + (int64_t)k * kBlock;
+      if (t >= t1) break;
+      const int64_t j = row_of(soff, nr, t);
+      const int64_t r = r0 + j;
+      sidx[t] = (O)r;
+      bidx[t] = (O)(lo[r] + (t - soff[j]));
+    }
+  } else {  // many empty ranges inside the tile: search the global offsets
+    for (int k = 0; k < kExpItems; ++k) {
+      const int64_t t = t0 + threadIdx.x + (int64_t)k * kBlock;
+      if (t >= t1) break;
+      const int64_t r = row_of(off, ns, t);
+      sidx[t] = (O)r;
+      bidx[t] = (O)(lo[r] + (t - off[r]));
+    }
+  }
+}
+
+}  // namespace
+
+void sorted_ranges(const void* big, bool key64, int64_t nb, const void* q, const uint8_t* qvalid, int64_t nq,
+                   int64_t* lo, int64_t* cnt, hipStream_t stream) {
+  if (nq <= 0) return;
+  const unsigned grid = grid_for(nq, kBlock, 1 << 16);
+  if (key64)
+    hipLaunchKernelGGL(sorted_ranges_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<const int64_t*>(big), nb, static_cast<const int64_t*>(q), qvalid, nq, lo, cnt);
+  else
+    hipLaunchKernelGGL(sorted_ranges_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<const int32_t*>(big), nb, static_cast<const int32_t*>(q), qvalid, nq, lo, cnt);
+  check_launch("sorted_ranges", stream);
+}
+
+void expand_ranges(const int64_t* off, const int64_t* lo, int64_t ns, int64_t total, void* sidx, void* bidx,
+                   bool out64, hipStream_t stream) {
+  if (total <= 0 || ns <= 0) return;
+  const unsigned grid = (unsigned)((total + kExpTile - 1) / kExpTile);
+  if (out64)
+    hipLaunchKernelGGL(expand_ranges_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, stream, off, lo, ns, total,
+                       static_cast<int64_t*>(sidx), static_cast<int64_t*>(bidx));
+  else
+    hipLaunchKernelGGL(expand_ranges_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, stream, off, lo, ns, total,
+                       static_cast<int32_t*>(sidx), static_cast<int32_t*>(bidx));
+  check_launch("expand_ranges", stream);
+}
+
+}  // namespace kern
+}  // namespace igloo

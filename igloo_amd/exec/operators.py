@@ -658,23 +658,13 @@ def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residu
             return None
     dev = ctx.device
     with ctx.span("join.sorted_search"):
-        q = small.to(big.dtype)
-        lo = torch.searchsorted(big, q)
-        hi = torch.searchsorted(big, q, right=True)
-        cnt = hi - lo
-        if svalid is not None:
-            cnt = torch.where(svalid, cnt, torch.zeros_like(cnt))
+        lo, cnt = H.sorted_ranges(big, small, svalid)
     if kind in ("semi", "anti") and residual is None:
         with ctx.span("join.gather"):
             m = cnt > 0
             return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
     with ctx.span("join.sorted_expand"):
-        total = int(cnt.sum().item())
-        it = torch.int32 if max(total, nb, ns) < 2**31 - 1 else torch.int64
-        sidx = torch.repeat_interleave(torch.arange(ns, device=dev, dtype=it), cnt, output_size=total)
-        starts = torch.cumsum(cnt, 0) - cnt
-        bidx = (lo.index_select(0, sidx.long()) - starts.index_select(0, sidx.long())
-                + torch.arange(total, device=dev, dtype=torch.int64)).to(it)
+        sidx, bidx = H.expand_ranges(lo, cnt, nb)
         lidx, ridx = (sidx, bidx) if big_right else (bidx, sidx)
     if residual is not None:
         with ctx.span("join.residual"):
@@ -804,18 +794,9 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
     if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS and 4 * small.numel() <= big.numel() \
             and bvalid is None and H.is_sorted(big):
         with ctx.span("join.sorted_search"):
-            q = small.to(big.dtype)
-            lo = torch.searchsorted(big, q)
-            cnt = torch.searchsorted(big, q, right=True) - lo
-            if svalid is not None:
-                cnt = torch.where(svalid, cnt, torch.zeros_like(cnt))
+            lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
-            total = int(cnt.sum().item())
-            it = torch.int32 if max(total, big.numel()) < 2**31 - 1 else torch.int64
-            sidx = torch.repeat_interleave(torch.arange(small.numel(), device=dev, dtype=it), cnt, output_size=total)
-            starts = torch.cumsum(cnt, 0) - cnt
-            bidx = (lo.index_select(0, sidx.long()) - starts.index_select(0, sidx.long())
-                    + torch.arange(total, device=dev, dtype=torch.int64)).to(it)
+            sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     # hash: build on the smaller side, probe with the bigger
     with ctx.span("join.build"):
@@ -1100,9 +1081,66 @@ class HashAggExec(ExecNode):
         return (f"gby=[{', '.join(e.sql() for _, e in a.groups)}], "
                 f"aggr=[{', '.join(x.sql() for _, x in a.aggs)}]")
 
+    def _eager_count(self, ctx) -> Optional[Batch]:
+        """GROUP BY <left join key>, COUNT(<right column>)... over a LEFT JOIN on
+        that key (TPC-H Q13: customer LEFT JOIN orders, count per customer):
+        count the right side per key first, then look the counts up per left row
+        and sum them per group — a group-by over the right input plus a probe of
+        the left keys, instead of materialising and re-grouping the join
+        (150M-row join output at SF100). Exact: a left row with k partners
+        contributes k to COUNT(x) exactly when x is non-NULL on each partner."""
+        lg, child = self.logical, self.children[0]
+        if ctx.world > 1 or not isinstance(child, HashJoinExec) or len(lg.groups) != 1 or not lg.aggs:
+            return None
+        j = child.logical
+        if j.kind != "left" or j.residual is not None or len(j.on) != 1:
+            return None
+        lkey, rkey = j.on[0]
+        gci, gexpr = lg.groups[0]
+        if not (isinstance(gexpr, ColRef) and isinstance(lkey, ColRef) and gexpr.cid == lkey.cid):
+            return None
+        right_cids = {c.cid for c in j.right.schema}
+        for _, a in lg.aggs:
+            if not (a.func == "count" and not a.distinct and a.filter is None and isinstance(a.arg, ColRef)
+                    and a.arg.cid in right_cids):
+                return None
+        ev = ctx.evaluator
+        lb = child.children[0].execute(ctx)
+        rb = child.children[1].execute(ctx)
+        with ctx.span("agg.eager_count"):
+            lk, rk, lvalid, rvalid = key_tensors([ev.column(lkey, lb)], [ev.column(rkey, rb)])
+            if rvalid is not None:  # NULL keys never match
+                keep = mask_to_indices(rvalid)
+                rk = rk.index_select(0, keep.long())
+                rb = _take_batch(rb, keep)
+            cnt_cols = {}
+            if rk.numel():
+                gid, ng, rep, srt = H.group_ids_ex(rk)
+                specs = [("count", None, ev.column(a.arg, rb).valid) for _, a in lg.aggs]
+                counts = A.grouped_aggregate(gid, ng, specs, rk.numel(), ctx.device, sorted_gids=srt)
+                first = H.JoinTable(rk.index_select(0, rep.long())).probe_first(lk, lvalid)
+                hit = first >= 0
+                safe = torch.where(hit, first, torch.zeros_like(first)).long()
+                for k, c in enumerate(counts):
+                    cnt_cols[-(k + 1)] = torch.where(hit, c.index_select(0, safe), torch.zeros_like(safe))
+            else:
+                for k in range(len(lg.aggs)):
+                    cnt_cols[-(k + 1)] = torch.zeros(lb.num_rows, dtype=torch.int64, device=ctx.device)
+        cols = dict(lb.columns)
+        aggs = []
+        for k, (ci, _) in enumerate(lg.aggs):
+            tmp = -(10**9) - k  # temporary column ids (binder ids are positive)
+            cols[tmp] = Column(T.INT64, cnt_cols[-(k + 1)].contiguous())
+            aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
+        return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
+
     def _run(self, ctx):
         lg = self.logical
         child = self.children[0]
+        if ctx.device.type == "cuda" and not self.runtime_filters:
+            out = self._eager_count(ctx)
+            if out is not None:
+                return out
         local = None
         if isinstance(child, ScanExec) and ctx.device.type == "cuda" and not self.runtime_filters:
             # scan -> filter -> aggregate in one fused kernel when the shape allows
@@ -1387,10 +1425,34 @@ class SortExec(ExecNode):
         return out
 
 
+#: ORDER BY ... LIMIT k over more than this many rows (and > 4k) first keeps the
+#: rows that can still make the top k on the leading key
+TOPK_PREFILTER_ROWS = 4096
+
+
+def _topk_candidates(b: Batch, keys, fetch, ctx) -> Optional[torch.Tensor]:
+    """Rows whose leading sort key ranks within the first ``fetch`` (ties kept):
+    the only rows an ORDER BY ... LIMIT can return. Lets string tie-breakers be
+    ranked over a handful of rows instead of the whole input (TPC-H Q2, Q21)."""
+    e, asc, _nf = keys[0]
+    c = ctx.evaluator.column(e, b)
+    if c.dtype.is_string or c.is_wide or c.valid is not None or c.data.dim() != 1:
+        return None
+    v = c.data
+    if v.dtype == torch.bool:
+        v = v.to(torch.int8)
+    kth = torch.topk(v, fetch, largest=not asc, sorted=True).values[-1]
+    return mask_to_indices(v <= kth if asc else v >= kth)
+
+
 def sort_batch(b: Batch, keys, fetch, ctx) -> Batch:
     n = b.num_rows
     if n <= 1:
         return b
+    if fetch is not None and 0 < fetch and n > max(TOPK_PREFILTER_ROWS, 4 * fetch):
+        cand = _topk_candidates(b, keys, fetch, ctx)
+        if cand is not None and cand.numel() < n:
+            return sort_batch(_take_batch(b, cand), keys, fetch, ctx)
     ev = ctx.evaluator
     ks = []
     for e, asc, nf in keys:

@@ -193,6 +193,46 @@ def is_sorted(keys: torch.Tensor) -> bool:
     return r
 
 
+def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Tensor] = None
+                  ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """For each probe key q[i]: (lo, cnt) with big[lo : lo+cnt] == q[i] (big non-decreasing).
+    GPU: one fused search kernel (csrc/kernels/ranges.hip)."""
+    big = _keys_ok(big)
+    q = q.to(big.dtype).contiguous()
+    nq = q.numel()
+    if not is_gpu(big):
+        lo = torch.searchsorted(big, q)
+        cnt = torch.searchsorted(big, q, right=True) - lo
+        if qvalid is not None:
+            cnt = torch.where(qvalid, cnt, torch.zeros_like(cnt))
+        return lo, cnt
+    lo = torch.empty(nq, dtype=torch.int64, device=big.device)
+    cnt = torch.empty(nq, dtype=torch.int64, device=big.device)
+    launch("sorted_ranges").sorted_ranges(ptr(big), big.dtype == torch.int64, big.numel(), ptr(q),
+                                          ptr(qvalid.contiguous() if qvalid is not None else None), nq, ptr(lo),
+                                          ptr(cnt), stream(big))
+    return lo, cnt
+
+
+def expand_ranges(lo: torch.Tensor, cnt: torch.Tensor, big_n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All pairs (s, lo[s] + k), k < cnt[s], grouped by s (int32 when they fit)."""
+    ns = lo.numel()
+    dev = lo.device
+    off, total = exclusive_scan(cnt)
+    it = torch.int32 if max(total, big_n, ns) < INT32_MAX else torch.int64
+    if not is_gpu(lo):
+        sidx = torch.repeat_interleave(torch.arange(ns, dtype=it), cnt, output_size=total)
+        bidx = (lo.index_select(0, sidx.long()) - off.index_select(0, sidx.long())
+                + torch.arange(total, dtype=torch.int64)).to(it)
+        return sidx, bidx
+    sidx = torch.empty(total, dtype=it, device=dev)
+    bidx = torch.empty(total, dtype=it, device=dev)
+    if total:
+        launch("expand_ranges").expand_ranges(ptr(off), ptr(lo.contiguous()), ns, total, ptr(sidx), ptr(bidx),
+                                              it == torch.int64, stream(lo))
+    return sidx, bidx
+
+
 def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, bool]:
     """``group_ids`` plus whether the ids are non-decreasing. Clustered keys
     (lineitem by l_orderkey, any output that follows a sorted probe side) get

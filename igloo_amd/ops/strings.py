@@ -315,12 +315,15 @@ def dict_encode(col: Column) -> Column:
 def sort_ranks(col: Column) -> torch.Tensor:
     """Order-preserving int64 rank per row (byte-wise UTF-8 order)."""
     c = dict_encode(col) if not col.is_dict else col
-    vals = c.dict_values()
-    order = sorted(range(len(vals)), key=lambda i: (vals[i] is None, (vals[i] or "").encode("utf-8")))
-    rank = [0] * len(vals)
-    for r, i in enumerate(order):
-        rank[i] = r
-    return _lut_apply(c, rank).to(torch.int64)
+    d = c.dictionary.to_arrow()
+    if len(d) == 0:
+        return torch.zeros(len(c), dtype=torch.int64, device=c.device)
+    # Arrow orders strings byte-wise (UTF-8 code point order), NULL entries last
+    order = pc.array_sort_indices(d, null_placement="at_end").to_numpy()
+    rank = np.empty(len(order), dtype=np.int64)
+    rank[order] = np.arange(len(order), dtype=np.int64)
+    lut = torch.from_numpy(rank).to(c.device)
+    return lut.index_select(0, c.data.long())
 
 
 def group_codes(col: Column) -> Tuple[torch.Tensor, Column]:

@@ -267,3 +267,25 @@ def test_sorted_group_ids_and_aggregate(gpu_device, n):
         assert torch.equal(a_.cpu(), b_.cpu())
     # unsorted keys are detected as such
     assert not H.group_ids_ex(kd.flip(0))[3]
+
+
+def test_sorted_ranges_and_expand_vs_torch(gpu_device):
+    """ranges.hip: fused lower/upper bound search + load-balanced range expansion
+    against torch.searchsorted / repeat_interleave (fp32-free integer oracle)."""
+    from igloo_amd.ops import hashing as H
+    g = torch.Generator().manual_seed(7)
+    for dtype in (torch.int32, torch.int64):
+        # runs of 0..40 equal keys (long runs exercise the binary-search upper bound)
+        reps = torch.randint(0, 41, (5000,), generator=g)
+        big = torch.repeat_interleave(torch.arange(5000, dtype=dtype) * 3, reps)
+        q = torch.randint(-5, 15010, (20000,), generator=g).to(dtype)
+        qvalid = torch.rand(20000, generator=g) > 0.1
+        lo_ref = torch.searchsorted(big, q)
+        cnt_ref = torch.where(qvalid, torch.searchsorted(big, q, right=True) - lo_ref, torch.zeros_like(lo_ref))
+        lo, cnt = H.sorted_ranges(big.to(gpu_device), q.to(gpu_device), qvalid.to(gpu_device))
+        assert torch.equal(cnt.cpu(), cnt_ref)
+        assert torch.equal(lo.cpu()[cnt_ref > 0], lo_ref[cnt_ref > 0])
+        s, b = H.expand_ranges(lo, cnt, big.numel())
+        s_ref, b_ref = H.expand_ranges(lo_ref, cnt_ref, big.numel())
+        assert torch.equal(s.cpu().long(), s_ref.long()) and torch.equal(b.cpu().long(), b_ref.long())
+        assert torch.equal(big[b.cpu().long()], q[s.cpu().long()])
