@@ -366,6 +366,43 @@ PYBIND11_MODULE(_native, m) {
     kern::str_prefix_key(P<const int64_t>(off), P<const uint8_t>(chars), n, skip, P<int64_t>(out), S(s));
   });
 
+  // -------------------------------------------------------------------- csv
+  m.attr("CSV_TILE") = kern::kCsvTile;
+  m.attr("CSV_COLUMN_BYTES") = (int)sizeof(kern::CsvColumn);
+  m.def("csv_num_tiles", &kern::csv_num_tiles);
+  m.def("csv_quote_parity", [](uintptr_t buf, int64_t n, int quote, uintptr_t tile_par, uintptr_t s) {
+    kern::csv_quote_parity(P<const uint8_t>(buf), n, (uint8_t)quote, P<uint8_t>(tile_par), S(s));
+  });
+  m.def("csv_rows", [](uintptr_t buf, int64_t n, int64_t start, int quote, uintptr_t tile_state, uintptr_t tile_rows,
+                       uintptr_t tile_off, uintptr_t rows_end, uintptr_t s) {
+    kern::csv_rows(P<const uint8_t>(buf), n, start, (uint8_t)quote, P<const uint8_t>(tile_state),
+                   P<int64_t>(tile_rows), P<const int64_t>(tile_off), P<int64_t>(rows_end), S(s));
+  });
+  // cols: [(kind, scale, out, len, valid)] -> packed CsvColumn array (upload, then pass to csv_parse)
+  m.def("csv_pack_columns", [](const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t>>& cols) {
+    std::vector<kern::CsvColumn> v;
+    for (auto& [kind, scale, out, len, valid] : cols) {
+      if (kind < kern::CSV_SKIP || kind > kern::CSV_UTF8) throw std::runtime_error("csv: bad column kind");
+      if (kind != kern::CSV_SKIP && !out) throw std::runtime_error("csv: missing output buffer");
+      if (kind == kern::CSV_UTF8 && !len) throw std::runtime_error("csv: missing length buffer");
+      v.push_back({kind, scale, P<void>(out), P<int64_t>(len), P<uint8_t>(valid)});
+    }
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(kern::CsvColumn));
+  });
+  m.def("csv_parse", [](uintptr_t buf, int64_t start, uintptr_t rows_end, int64_t nrows, uintptr_t cols, int ncols,
+                        int delim, int quote, uintptr_t err, uintptr_t s) {
+    kern::csv_parse(P<const uint8_t>(buf), start, P<const int64_t>(rows_end), nrows,
+                    P<const kern::CsvColumn>(cols), ncols, (uint8_t)delim, (uint8_t)quote, P<int>(err), S(s));
+  });
+  m.def("csv_str_lengths", [](uintptr_t len_flag, int64_t n, uintptr_t len, uintptr_t s) {
+    kern::csv_str_lengths(P<const int64_t>(len_flag), n, P<int64_t>(len), S(s));
+  });
+  m.def("csv_str_copy", [](uintptr_t pos, uintptr_t len_flag, uintptr_t off, int64_t n, int quote, uintptr_t out,
+                           uintptr_t s) {
+    kern::csv_str_copy(P<const int64_t>(pos), P<const int64_t>(len_flag), P<const int64_t>(off), n, (uint8_t)quote,
+                       P<uint8_t>(out), S(s));
+  });
+
   // ----------------------------------------------------------- sorted joins
   m.def("sorted_ranges", [](uintptr_t big, bool key64, int64_t nb, uintptr_t q, uintptr_t qvalid, int64_t nq,
                             uintptr_t lo, uintptr_t cnt, uintptr_t s) {

@@ -196,6 +196,27 @@ void textgen_lengths(const TextGenParams& p, int64_t n, int64_t* lens, bool devi
 void textgen_write(const TextGenParams& p, int64_t n, const int64_t* off, uint8_t* chars, bool device,
                    hipStream_t stream);
 
+// ---- csv.hip -------------------------------------------------------------------
+constexpr int64_t kCsvTile = 16 * 1024;  // bytes per wave in the row-splitting passes
+enum CsvKind : int { CSV_SKIP = 0, CSV_INT32 = 1, CSV_INT64 = 2, CSV_DECIMAL = 3, CSV_FLOAT64 = 4, CSV_DATE = 5,
+                     CSV_BOOL = 6, CSV_UTF8 = 7 };
+struct CsvColumn {
+  int32_t kind, scale;  // scale: CSV_DECIMAL fractional digits
+  void* out;            // values [rows]; CSV_UTF8: int64 address of the field bytes
+  int64_t* len;         // CSV_UTF8: byte length (bit 62 set: quoted field with "" escapes)
+  uint8_t* valid;       // [rows] or null (then an empty numeric field is an error)
+};
+int64_t csv_num_tiles(int64_t n);
+void csv_quote_parity(const uint8_t* buf, int64_t n, uint8_t quote, uint8_t* tile_par, hipStream_t stream);
+// rows_end == null: count terminators per tile into tile_rows; else write them at tile_off[tile]
+void csv_rows(const uint8_t* buf, int64_t n, int64_t start, uint8_t quote, const uint8_t* tile_state,
+              int64_t* tile_rows, const int64_t* tile_off, int64_t* rows_end, hipStream_t stream);
+void csv_parse(const uint8_t* buf, int64_t start, const int64_t* rows_end, int64_t nrows, const CsvColumn* cols,
+               int ncols, uint8_t delim, uint8_t quote, int* err, hipStream_t stream);
+void csv_str_lengths(const int64_t* len_flag, int64_t n, int64_t* len, hipStream_t stream);
+void csv_str_copy(const int64_t* pos, const int64_t* len_flag, const int64_t* off, int64_t n, uint8_t quote,
+                  uint8_t* out, hipStream_t stream);
+
 // ---- ranges.hip ----------------------------------------------------------------
 // big: non-decreasing int32/int64 keys; per probe key q[i]: big[lo[i] .. lo[i]+cnt[i]) == q[i]
 void sorted_ranges(const void* big, bool key64, int64_t nb, const void* q, const uint8_t* qvalid, int64_t nq,

@@ -7,8 +7,11 @@ mapped to ``Error::Unknown`` (:18-46); and the coordinator's DataFusion
 ListingTable CSV with an explicit schema (reference crates/coordinator/src/main.rs:26-44).
 
 Both shapes are provided: ``scan_rows()`` returns the reference's rows of
-strings; ``scan()`` (TableSource) returns typed device columns, parsed with
-Arrow's multithreaded CSV reader and uploaded to HBM once.
+strings; ``scan()`` (TableSource) returns typed device columns. On a GPU the
+file is staged in HBM and parsed by gfx950 kernels (igloo_amd/connectors/
+gpu_csv.py: quote-aware row splitting + typed field parsing); on CPU, or when
+a value does not parse as the declared type, Arrow's multithreaded CSV reader
+is used. ``IGLOO_CSV_GPU=0`` forces the host reader.
 """
 from __future__ import annotations
 
@@ -26,6 +29,10 @@ from ..columnar import Batch, Column
 from ..utils.errors import IoError
 
 Row = List[str]
+GPU_PARSE = os.environ.get("IGLOO_CSV_GPU", "1") != "0"
+#: files up to this size infer their schema from the whole file, larger ones
+#: from the first block (the GPU parse then checks every value)
+FULL_INFER_BYTES = 64 << 20
 
 
 class CsvTable(TableSource):
@@ -37,6 +44,8 @@ class CsvTable(TableSource):
         self._schema = schema
         self._table: Optional[pa.Table] = None
         self._resident = {}
+        self._gpu_rows: Optional[int] = None
+        self.last_scan = ""   # "gpu" | "host" (| "host: <reason>")
 
     # -------------------------------------------------------- reference API
     @staticmethod
@@ -83,27 +92,73 @@ class CsvTable(TableSource):
     def schema(self) -> List[Field]:
         if self._schema:
             return self._schema
-        t = self._load()
-        self._schema = [Field(f.name, T.from_arrow_type(f.type), True) for f in t.schema]
+        if os.path.exists(self.path) and os.path.getsize(self.path) > FULL_INFER_BYTES:
+            sch = self._infer_first_block()
+        else:
+            sch = self._load().schema
+        self._schema = [Field(f.name, T.from_arrow_type(f.type), True) for f in sch]
         return self._schema
 
+    def _infer_first_block(self) -> pa.Schema:
+        ro = pacsv.ReadOptions(autogenerate_column_names=not self.has_header, block_size=4 << 20)
+        try:
+            with pacsv.open_csv(self.path, read_options=ro,
+                                parse_options=pacsv.ParseOptions(delimiter=self.delimiter)) as r:
+                return r.schema
+        except (pa.ArrowInvalid, OSError) as e:
+            raise IoError(f"csv error in {self.path}: {e}") from e
+
     def num_rows(self) -> int:
+        if self._gpu_rows is not None:
+            return self._gpu_rows
         return self._load().num_rows
+
+    def _scan_gpu(self, columns: Sequence[str], device):
+        from .gpu_csv import CsvParseError, read_csv_gpu
+        fields = self.schema()
+        try:
+            cols = read_csv_gpu(self.path, fields, columns, device, has_header=self.has_header,
+                                delimiter=self.delimiter)
+        except CsvParseError as e:
+            self.last_scan = f"host: {e}"
+            return None
+        self.last_scan = "gpu"
+        if cols:
+            self._gpu_rows = len(next(iter(cols.values())))
+        return cols
 
     def scan(self, columns: Sequence[str], ctx) -> Batch:
         device = ctx.device if ctx is not None else torch.device("cpu")
-        t = self._load()
         rank, world = 0, 1
         if ctx is not None and ctx.comm is not None:
             rank, world = ctx.comm.rank, ctx.comm.world_size
-        if world > 1:  # contiguous row ranges per rank
-            per = (t.num_rows + world - 1) // world
-            t = t.slice(rank * per, per)
-        out = {}
-        types = {f.name: f.dtype for f in self.schema()}
-        for c in columns:
-            key = (c, str(device), rank, world)
-            if key not in self._resident:
-                self._resident[key] = Column.from_arrow(t.column(c), device=device, dtype=types[c])
-            out[c] = self._resident[key]
-        return Batch(out, t.num_rows)
+        missing = [c for c in columns if (c, str(device), rank, world) not in self._resident]
+        if missing and device.type == "cuda" and GPU_PARSE:
+            cols = self._scan_gpu(missing, device)
+            if cols is not None:
+                n = len(next(iter(cols.values()))) if cols else 0
+                lo, hi = 0, n
+                if world > 1:  # contiguous row ranges per rank
+                    per = (n + world - 1) // world
+                    lo, hi = min(rank * per, n), min((rank + 1) * per, n)
+                for c in missing:
+                    col = cols[c]
+                    if world > 1:
+                        from ..ops.gather import take
+                        col = take(col, torch.arange(lo, hi, dtype=torch.int64, device=device))
+                    self._resident[(c, str(device), rank, world)] = col
+                missing = []
+        if missing:
+            t = self._load()
+            if world > 1:  # contiguous row ranges per rank
+                per = (t.num_rows + world - 1) // world
+                t = t.slice(rank * per, per)
+            types = {f.name: f.dtype for f in self.schema()}
+            for c in missing:
+                self._resident[(c, str(device), rank, world)] = Column.from_arrow(t.column(c), device=device,
+                                                                                 dtype=types[c])
+            if not self.last_scan.startswith("host"):
+                self.last_scan = "host"
+        out = {c: self._resident[(c, str(device), rank, world)] for c in columns}
+        n = len(next(iter(out.values()))) if out else self.num_rows()
+        return Batch(out, n)
