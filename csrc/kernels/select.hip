@@ -2,12 +2,14 @@
 //
 // Replaces arrow's filter_record_batch / DataFusion FilterExec compaction
 // (reference crates/engine/src/operators/filter.rs:57). Three launches:
-//   1. per-tile popcount of the mask (16 bytes per lane, one uint4 load),
+//   1. per-tile popcount of the mask (32 bytes per lane, two uint4 loads),
 //   2. exclusive scan of the tile counts (one workgroup),
-//   3. per-tile rewrite: each lane expands its 16 flags at its block-scan
-//      offset, so output order equals input order (stable).
-// A tile is kBlock*16 = 4096 rows, so SF100 lineitem (600M rows) launches
-// ~146k workgroups: far more than 256 CUs x occupancy, as the HBM stream wants.
+//   3. per-tile rewrite: each lane expands its 32 flags at its block-scan
+//      offset into an LDS staging buffer, then the workgroup streams the
+//      tile's indices out with contiguous (coalesced) stores; output order
+//      equals input order (stable).
+// A tile is kBlock*32 = 8192 rows, so SF100 lineitem (600M rows) launches
+// ~73k workgroups: far more than 256 CUs x occupancy, as the HBM stream wants.
 #include "common.h"
 #include "kernels.h"
 
@@ -16,19 +18,37 @@ namespace kern {
 
 namespace {
 
-constexpr int kItems = 16;
+constexpr int kItems = 32;
 constexpr int kTile = kBlock * kItems;
 
-__device__ inline int count16(const uint8_t* mask, int64_t base, int64_t n) {
-  int c = 0;
+// flags of rows [base, base + kItems) as 0/1 bytes (bool bytes are 0/1)
+__device__ inline void load_flags(const uint8_t* mask, int64_t base, int64_t n, uint32_t (&w)[kItems / 4]) {
   if (base + kItems <= n && (((uintptr_t)(mask + base)) & 15) == 0) {
-    uint4 v = *reinterpret_cast<const uint4*>(mask + base);
-    // bool bytes are 0/1, so popcount of each word counts set rows
-    c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+#pragma unroll
+    for (int q = 0; q < kItems / 16; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(mask + base)[q];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
   } else {
-    for (int j = 0; j < kItems; ++j)
-      if (base + j < n) c += mask[base + j] != 0;
+#pragma unroll
+    for (int q = 0; q < kItems / 4; ++q) {
+      uint32_t x = 0;
+      for (int b = 0; b < 4; ++b)
+        if (base + 4 * q + b < n && mask[base + 4 * q + b]) x |= 1u << (8 * b);
+      w[q] = x;
+    }
   }
+}
+
+__device__ inline int count_flags(const uint8_t* mask, int64_t base, int64_t n) {
+  uint32_t w[kItems / 4];
+  load_flags(mask, base, n, w);
+  int c = 0;
+#pragma unroll
+  for (int q = 0; q < kItems / 4; ++q) c += __popc(w[q]);
   return c;
 }
 
@@ -36,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void tile_count_kernel(const uint8_t* __res
                                                            int64_t* __restrict__ counts) {
   __shared__ int64_t red[kWavesPerBlock];
   int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
-  int64_t c = count16(mask, base, n);
+  int64_t c = count_flags(mask, base, n);
   c = wave_reduce_sum(c);
   if (lane_id() == 0) red[threadIdx.x / kWave] = c;
   __syncthreads();
@@ -89,25 +109,24 @@ __global__ __launch_bounds__(kBlock) void tile_write_kernel(const uint8_t* __res
                                                            const int64_t* __restrict__ offsets,
                                                            IdxT* __restrict__ out) {
   __shared__ int64_t scratch[kWavesPerBlock + 1];
-  int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
-  uint8_t flags[kItems];
-  if (base + kItems <= n && (((uintptr_t)(mask + base)) & 15) == 0) {
-    uint4 v = *reinterpret_cast<const uint4*>(mask + base);
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) flags[j] = (w[j >> 2] >> ((j & 3) * 8)) & 0xff;
-  } else {
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) flags[j] = base + j < n ? mask[base + j] : 0;
-  }
+  __shared__ uint16_t stage[kTile];  // row offsets inside the tile, in output order
+  const int64_t tile_base = (int64_t)blockIdx.x * kTile;
+  const int first = threadIdx.x * kItems;
+  uint32_t w[kItems / 4];
+  load_flags(mask, tile_base + first, n, w);
   int64_t c = 0;
 #pragma unroll
-  for (int j = 0; j < kItems; ++j) c += flags[j] != 0;
+  for (int q = 0; q < kItems / 4; ++q) c += __popc(w[q]);
   int64_t total;
-  int64_t pos = offsets[blockIdx.x] + block_exclusive_scan(c, scratch, &total);
+  int pos = (int)block_exclusive_scan(c, scratch, &total);
 #pragma unroll
-  for (int j = 0; j < kItems; ++j)
-    if (flags[j]) out[pos++] = (IdxT)(base + j);
+  for (int q = 0; q < kItems / 4; ++q)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((w[q] >> (8 * b)) & 1u) stage[pos++] = (uint16_t)(first + 4 * q + b);
+  __syncthreads();
+  IdxT* dst = out + offsets[blockIdx.x];
+  for (int k = threadIdx.x; k < (int)total; k += kBlock) dst[k] = (IdxT)(tile_base + stage[k]);
 }
 
 }  // namespace

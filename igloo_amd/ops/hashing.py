@@ -20,6 +20,10 @@ EMPTY_KEY = -(2**63)
 INT32_MAX = 2**31 - 1
 BLOOM_MAX_KEYS = 4 << 20   # build sides up to this size get a Bloom filter
 BLOOM_MIN_RATIO = 4        # ... used when probe rows >= ratio x build rows
+#: join build keys whose [min, max] span is at most this use the direct-mapped
+#: table (one random read per probe) whatever the build size: 2^26 slots is a
+#: 256 MB head array, small next to 288 GB of HBM
+DIRECT_JOIN_MAX_SPAN = 1 << 26
 
 
 def _next_pow2(x: int) -> int:
@@ -59,7 +63,7 @@ class JoinTable:
             return
         self.kmin, kmax = rng
         span = kmax - self.kmin + 1
-        self.direct = span <= 4 * n + 4096 and span < 2**31 - 1
+        self.direct = span < 2**31 - 1 and (span <= 4 * n + 4096 or span <= DIRECT_JOIN_MAX_SPAN)
         if not self.gpu:
             k = keys if valid is None else torch.where(valid, keys, torch.full_like(keys, kmax + 1) if kmax < 2**62 else keys)
             sk, order = torch.sort(k.to(torch.int64), stable=True)
