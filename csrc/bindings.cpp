@@ -219,7 +219,8 @@ PYBIND11_MODULE(_native, m) {
     f.nterms = (int32_t)terms.size();
     for (size_t i = 0; i < terms.size(); ++i) {
       auto [col, kind, lo, hi, set] = terms[i];
-      if (col < 0 || col >= f.ncols || kind < 0 || kind > 2) throw std::runtime_error("fused scan: bad term");
+      if (col < 0 || col >= f.ncols || kind < 0 || kind > 3 || (kind == 3 && (int64_t)set >= f.ncols))
+        throw std::runtime_error("fused scan: bad term");
       f.terms[i] = kern::FfTerm{col, kind, lo, hi, set};
     }
     f.mask = P<const uint8_t>(mask);

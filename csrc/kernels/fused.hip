@@ -116,12 +116,18 @@ __device__ __forceinline__ void ff_pass4(const FfSpec& S, const ff_vec<VW> r0, c
     const int kind = T.kind;
     const int64_t lo = T.lo, hi = T.hi;
     const uint64_t set = T.set;
+    const int c2 = __builtin_amdgcn_readfirstlane((int)(set & 0xff));  // kind 3: second column
 #pragma unroll
     for (int j = 0; j < kFfRows; ++j) {
       const int64_t v = col_of<VW>(FF_ROW(j), c);
       bool hit;
       if (kind == 2) hit = v >= 0 && v < 64 && ((set >> (v & 63)) & 1ULL);
-      else hit = v >= lo && v <= hi;
+      else if (kind == 3) {
+        const int64_t d = v - col_of<VW>(FF_ROW(j), c2);
+        hit = d >= lo && d <= hi;
+      } else {
+        hit = v >= lo && v <= hi;
+      }
       pass[j] &= (kind == 1) ? !hit : hit;
     }
   }

@@ -5,6 +5,8 @@
 // :242-280 combine_with_nulls) with one launch that reads the index vector
 // once and gathers up to kMaxGatherCols fixed-width columns. A negative index
 // produces a NULL row (outer-join padding).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -18,25 +20,53 @@ struct GatherParams {
   GatherDesc d[kMaxGatherCols];
 };
 
-template <typename I>
+constexpr int kGatherRows = 4;  // rows per lane: independent random loads in flight per column
+
+template <typename T, int kGatherRows>
+__device__ inline void gather_col(const void* src_, void* dst_, const int64_t (&s)[kGatherRows],
+                                  const int64_t (&i)[kGatherRows], int64_t n) {
+  const T* __restrict__ src = static_cast<const T*>(src_);
+  T* __restrict__ dst = static_cast<T*>(dst_);
+  T v[kGatherRows];
+#pragma unroll
+  for (int r = 0; r < kGatherRows; ++r) v[r] = s[r] >= 0 ? src[s[r]] : T{};
+#pragma unroll
+  for (int r = 0; r < kGatherRows; ++r)
+    if (i[r] < n) dst[i[r]] = v[r];
+}
+
+// Rows base + r * blockDim (r < kGatherRows) per lane: every store of a column
+// follows all of that column's loads, so a lane keeps kGatherRows random
+// reads in flight instead of one load->store round trip per value.
+template <typename I, int kGatherRows>
 __global__ __launch_bounds__(kBlock) void gather_multi_kernel(const I* __restrict__ idx, int64_t n, GatherParams p) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t s = (int64_t)idx[i];
-    bool ok = s >= 0;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherRows;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x * kGatherRows + threadIdx.x; base < n; base += step) {
+    int64_t i[kGatherRows], s[kGatherRows];
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r) {
+      i[r] = base + (int64_t)r * blockDim.x;
+      s[r] = i[r] < n ? (int64_t)idx[i[r]] : -1;
+    }
     for (int c = 0; c < p.ncols; ++c) {
       const GatherDesc& d = p.d[c];
       switch (d.elem_bytes) {
-        case 1: ((uint8_t*)d.dst)[i] = ok ? ((const uint8_t*)d.src)[s] : 0; break;
-        case 2: ((uint16_t*)d.dst)[i] = ok ? ((const uint16_t*)d.src)[s] : 0; break;
-        case 4: ((uint32_t*)d.dst)[i] = ok ? ((const uint32_t*)d.src)[s] : 0; break;
-        case 8: ((uint64_t*)d.dst)[i] = ok ? ((const uint64_t*)d.src)[s] : 0; break;
-        case 16: {
-          uint4 z = {0, 0, 0, 0};
-          ((uint4*)d.dst)[i] = ok ? ((const uint4*)d.src)[s] : z;
-          break;
-        }
+        case 1: gather_col<uint8_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 2: gather_col<uint16_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 4: gather_col<uint32_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 8: gather_col<uint64_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 16: gather_col<uint4, kGatherRows>(d.src, d.dst, s, i, n); break;
       }
-      if (d.dst_valid) d.dst_valid[i] = ok && (!d.src_valid || d.src_valid[s]);
+      if (d.dst_valid) {
+        const uint8_t* __restrict__ sv = d.src_valid;
+        uint8_t* __restrict__ dv = d.dst_valid;
+        uint8_t v[kGatherRows];
+#pragma unroll
+        for (int r = 0; r < kGatherRows; ++r) v[r] = s[r] >= 0 && (!sv || sv[s[r]]);
+#pragma unroll
+        for (int r = 0; r < kGatherRows; ++r)
+          if (i[r] < n) dv[i[r]] = v[r];
+      }
     }
   }
 }
@@ -73,11 +103,19 @@ void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* desc
     GatherParams p;
     p.ncols = ncols - base < kMaxGatherCols ? ncols - base : kMaxGatherCols;
     for (int c = 0; c < p.ncols; ++c) p.d[c] = descs[base + c];
-    dim3 g(grid_for(n, kBlock, 65536)), b(kBlock);
-    if (idx64)
-      hipLaunchKernelGGL(gather_multi_kernel<int64_t>, g, b, 0, stream, (const int64_t*)idx, n, p);
-    else
-      hipLaunchKernelGGL(gather_multi_kernel<int32_t>, g, b, 0, stream, (const int32_t*)idx, n, p);
+    static const int rows = getenv("IGLOO_GATHER_ROWS") ? atoi(getenv("IGLOO_GATHER_ROWS")) : kGatherRows;
+    const int R = rows == 1 ? 1 : kGatherRows;
+    dim3 g(grid_for(n, kBlock * R, 65536)), b(kBlock);
+    if (R == 1) {
+      if (idx64)
+        hipLaunchKernelGGL((gather_multi_kernel<int64_t, 1>), g, b, 0, stream, (const int64_t*)idx, n, p);
+      else
+        hipLaunchKernelGGL((gather_multi_kernel<int32_t, 1>), g, b, 0, stream, (const int32_t*)idx, n, p);
+    } else if (idx64) {
+      hipLaunchKernelGGL((gather_multi_kernel<int64_t, kGatherRows>), g, b, 0, stream, (const int64_t*)idx, n, p);
+    } else {
+      hipLaunchKernelGGL((gather_multi_kernel<int32_t, kGatherRows>), g, b, 0, stream, (const int32_t*)idx, n, p);
+    }
     check_launch("gather_multi", stream);
   }
 }

@@ -35,7 +35,8 @@ struct FfColumn {
   const void* ptr;
   int64_t width;  // bytes: 1, 2, 4, 8 (signed except 1 = uint8/bool)
 };
-// kind 0: lo <= v <= hi; 1: NOT (lo <= v <= hi); 2: v in bitmask `set` (0 <= v < 64)
+// kind 0: lo <= v <= hi; 1: NOT (lo <= v <= hi); 2: v in bitmask `set` (0 <= v < 64);
+// 3: lo <= v - col[set] <= hi (column-vs-column comparison, e.g. l_commitdate < l_receiptdate)
 struct FfTerm {
   int32_t col, kind;
   int64_t lo, hi;

@@ -31,6 +31,7 @@ from ..types import DataType
 from ..utils.errors import ExecutionError
 
 MAX_COLS, MAX_TERMS, MAX_AGGS, MAX_GROUPS, MAX_FACTORS = 8, 8, 8, 16, 3
+COL_COL = os.environ.get("IGLOO_FF_COLCOL", "0") == "1"  # column-vs-column range terms (A/B: no gain measured)
 I64_MIN, I64_MAX = -(2**63), 2**63 - 1
 FLIP = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
 
@@ -139,6 +140,9 @@ class Spec:
                 (l.dtype.scale if l.dtype.is_decimal else 0) >= (l.x.dtype.scale if l.x.dtype.is_decimal else 0):
             cast_t = cast_t or l.dtype
             l = l.x
+        if isinstance(l, ColRef) and isinstance(r, ColRef) and cast_t is None and COL_COL:
+            self._col_col(l, r, op)
+            return
         if not (isinstance(l, ColRef) and isinstance(r, Lit)) or r.value is None:
             raise Bail("not column-vs-literal")
         ci, col = self.colref(l)
@@ -184,6 +188,21 @@ class Spec:
         else:  # '<>'
             if L % f == 0:
                 self._range(ci, "<>", L // f)
+
+    def _col_col(self, l: ColRef, r: ColRef, op: str) -> None:
+        """l OP r on two 4-byte integer-like columns of one type (dates, int32):
+        a range term on l - r (kind 3), which cannot overflow in int64."""
+        if op == "<>" or l.dtype != r.dtype or l.dtype.kind not in ("date32", "int32", "int16", "int8"):
+            raise Bail("column-vs-column comparison")
+        if len(self.terms) >= MAX_TERMS:
+            raise Bail("too many terms")
+        cl, coll = self.colref(l)
+        cr, colr = self.colref(r)
+        if coll.is_dict or colr.is_dict:
+            raise Bail("dictionary column comparison")
+        lo, hi = {"<": (I64_MIN, -1), "<=": (I64_MIN, 0), ">": (1, I64_MAX), ">=": (0, I64_MAX),
+                  "=": (0, 0)}[op]
+        self.terms.append((cl, 3, lo, hi, cr))
 
     def _inlist(self, c: InList) -> None:
         if not isinstance(c.x, ColRef) or any(v.value is None for v in c.values):

@@ -433,6 +433,9 @@ class HashJoinExec(ExecNode):
         return hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
 
 
+#: eager COUNT under LEFT JOIN: right-key spans up to this count with one histogram
+EAGER_COUNT_DIRECT_SPAN = 1 << 27
+
 #: largest (global) probe side whose keys are pushed into the build side's aggregate
 RUNTIME_FILTER_MAX_ROWS = 16_000_000
 
@@ -1114,7 +1117,24 @@ class HashAggExec(ExecNode):
                 rk = rk.index_select(0, keep.long())
                 rb = _take_batch(rb, keep)
             cnt_cols = {}
-            if rk.numel():
+            rng = H.key_range(rk) if rk.numel() else None
+            span = rng[1] - rng[0] + 1 if rng else 0
+            if rng and span <= EAGER_COUNT_DIRECT_SPAN:
+                # dense key domain: one histogram pass over the right keys, then a
+                # direct lookup per left key (no hash table, no group ids)
+                kmin = rng[0]
+                li = lk.to(torch.int64) - kmin
+                inr = (li >= 0) & (li < span)
+                if lvalid is not None:
+                    inr &= lvalid
+                li = torch.where(inr, li, torch.zeros_like(li))
+                rbase = (rk.to(torch.int64) - kmin)
+                for k, (_, a) in enumerate(lg.aggs):
+                    av = ev.column(a.arg, rb).valid
+                    keys = rbase if av is None else torch.where(av, rbase, torch.full_like(rbase, span))
+                    hist = torch.bincount(keys, minlength=span + 1)[:span]
+                    cnt_cols[-(k + 1)] = torch.where(inr, hist.index_select(0, li), torch.zeros_like(li))
+            elif rk.numel():
                 gid, ng, rep, srt = H.group_ids_ex(rk)
                 specs = [("count", None, ev.column(a.arg, rb).valid) for _, a in lg.aggs]
                 counts = A.grouped_aggregate(gid, ng, specs, rk.numel(), ctx.device, sorted_gids=srt)
