@@ -19,6 +19,7 @@ reference's ExecutionPlan implementations and DataFusion's inherited ones
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -892,6 +893,11 @@ class LateBatch(Batch):
         return Batch(out, self._n, self.dist)
 
 
+#: a multi-way join returns its LateBatch (row indices into the inputs) to the
+#: parent instead of materialising every input column
+LAZY_JOIN_OUTPUT = os.environ.get("IGLOO_LAZY_JOIN", "1") != "0"
+
+
 class MultiJoinExec(ExecNode):
     """N-ary inner join. Inputs are materialised first, then joined greedily:
     each step joins the connected pair with the smallest estimated result
@@ -989,6 +995,10 @@ class MultiJoinExec(ExecNode):
             merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})"}
             rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
         b = rels[0]["batch"]
+        if isinstance(b, LateBatch) and not conds and not deferred and LAZY_JOIN_OUTPUT:
+            # hand the index form up: the parent gathers only the columns it
+            # reads (join keys and unused payload are never materialised)
+            return b
         if isinstance(b, LateBatch):
             with ctx.span("join.gather"):
                 b = b.materialize()
