@@ -416,6 +416,15 @@ PYBIND11_MODULE(_native, m) {
                         S(s));
   });
 
+  m.def("sorted_match", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
+                           uintptr_t counts, uintptr_t offsets, uintptr_t sidx, uintptr_t bidx, bool out64,
+                           uintptr_t s) {
+    if (ns > 0 && (!big2 || !small2 || !lo || !cnt || (!offsets && !counts) || (offsets && (!sidx || !bidx))))
+      throw std::runtime_error("sorted_match: null buffer");
+    kern::sorted_match(P<const void>(big2), P<const void>(small2), key64, P<const int64_t>(lo), P<const int64_t>(cnt),
+                       ns, P<int32_t>(counts), P<const int64_t>(offsets), P<void>(sidx), P<void>(bidx), out64, S(s));
+  });
+
   // -------------------------------------------------------------- partition
   m.def("partition_run_blocks", &kern::partition_run_blocks);
   m.def("partition_run", [](uintptr_t keys, bool key64, int64_t n, int nparts, uintptr_t ws, uintptr_t total,

@@ -225,6 +225,11 @@ void sorted_ranges(const void* big, bool key64, int64_t nb, const void* q, const
 // off: exclusive offsets [ns] of the range lengths (total = sum); pairs (s, lo[s] + k) for k < len(s)
 void expand_ranges(const int64_t* off, const int64_t* lo, int64_t ns, int64_t total, void* sidx, void* bidx,
                    bool out64, hipStream_t stream);
+// second equality key inside the first key's ranges: offsets == null -> counts[ns] of matches,
+// else pairs written at offsets (exclusive scan of those counts)
+void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
+                  int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
+                  hipStream_t stream);
 
 // ---- parquet.hip ---------------------------------------------------------------
 enum PqPhys : int { PQ_PHYS_BOOLEAN = 0, PQ_PHYS_INT32 = 1, PQ_PHYS_INT64 = 2, PQ_PHYS_INT96 = 3, PQ_PHYS_FLOAT = 4,

@@ -144,3 +144,73 @@ void expand_ranges(const int64_t* off, const int64_t* lo, int64_t ns, int64_t to
 
 }  // namespace kern
 }  // namespace igloo
+
+// ---- sorted ranges + a second equality key ---------------------------------
+// Two-column equi-join whose big side is sorted on the first key (partsupp by
+// ps_partkey joined on (partkey, suppkey): TPC-H Q9): after sorted_ranges on
+// the first key, each probe row scans its (short) range for the second key.
+// Pass 0 counts matches per probe row; pass 1 writes the (probe, build) pairs
+// at the exclusive offsets of those counts.
+namespace igloo {
+namespace kern {
+namespace {
+
+template <typename K2, typename O, bool WRITE>
+__global__ __launch_bounds__(kBlock) void sorted_match_kernel(const K2* __restrict__ big2,
+                                                             const K2* __restrict__ small2,
+                                                             const int64_t* __restrict__ lo,
+                                                             const int64_t* __restrict__ cnt, int64_t ns,
+                                                             int32_t* __restrict__ counts,
+                                                             const int64_t* __restrict__ offsets,
+                                                             O* __restrict__ sidx, O* __restrict__ bidx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = lo[i], c = cnt[i];
+    const K2 key = small2[i];
+    int64_t o = WRITE ? offsets[i] : 0;
+    int32_t m = 0;
+    for (int64_t k = 0; k < c; ++k) {
+      if (big2[l + k] == key) {
+        if (WRITE) {
+          sidx[o] = (O)i;
+          bidx[o] = (O)(l + k);
+          ++o;
+        }
+        ++m;
+      }
+    }
+    if (!WRITE) counts[i] = m;
+  }
+}
+
+template <typename K2>
+void launch_match(const void* big2, const void* small2, const int64_t* lo, const int64_t* cnt, int64_t ns,
+                  int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64, hipStream_t stream) {
+  const dim3 g(grid_for(ns, kBlock, 1 << 16)), b(kBlock);
+  const K2* B = static_cast<const K2*>(big2);
+  const K2* S = static_cast<const K2*>(small2);
+  if (!offsets)
+    hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, false>), g, b, 0, stream, B, S, lo, cnt, ns, counts, nullptr,
+                       nullptr, nullptr);
+  else if (out64)
+    hipLaunchKernelGGL((sorted_match_kernel<K2, int64_t, true>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
+                       offsets, static_cast<int64_t*>(sidx), static_cast<int64_t*>(bidx));
+  else
+    hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, true>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
+                       offsets, static_cast<int32_t*>(sidx), static_cast<int32_t*>(bidx));
+}
+
+}  // namespace
+
+void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
+                  int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
+                  hipStream_t stream) {
+  if (ns <= 0) return;
+  if (key64)
+    launch_match<int64_t>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, stream);
+  else
+    launch_match<int32_t>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, stream);
+  check_launch("sorted_match", stream);
+}
+
+}  // namespace kern
+}  // namespace igloo

@@ -815,6 +815,43 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
     return (ssel, bsel) if big_right else (bsel, ssel)
 
 
+_INT_KEYS = ("int32", "int64")
+TWO_KEY_SORTED = os.environ.get("IGLOO_TWO_KEY_SORTED", "1") == "1"
+
+
+def _two_key_sorted_pairs(A, B, on, ctx) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """Two-column inner equi-join whose bigger side is sorted on one of the two
+    key columns (partsupp on ps_partkey in Q9's (partkey, suppkey) join): a
+    binary search finds each probe row's range of the sorted key and the other
+    key is compared inside that range on the device (ops.hashing
+    .sorted_match_pairs) — no key packing, no hash table. None when the shape
+    does not apply (nulls, non-integer keys, unsorted big side)."""
+    if A.num_rows == 0 or B.num_rows == 0:
+        return None
+    ev = ctx.evaluator
+    big_right = B.num_rows >= A.num_rows
+    big_rel, small_rel = (B, A) if big_right else (A, B)
+    pair_cols = []
+    for x, y in on:
+        bx, sx = (y, x) if big_right else (x, y)
+        bc, sc = ev.column(bx, big_rel), ev.column(sx, small_rel)
+        if bc.dtype.kind not in _INT_KEYS or sc.dtype.kind not in _INT_KEYS or bc.valid is not None \
+                or sc.valid is not None:
+            return None
+        pair_cols.append((bc.data, sc.data))
+    for first in (0, 1):
+        b1, s1 = pair_cols[first]
+        b2, s2 = pair_cols[1 - first]
+        if b1.numel() < SORTED_JOIN_MIN_ROWS or not H.is_sorted(b1):
+            continue
+        dt = torch.int64 if torch.int64 in (b1.dtype, s1.dtype) else torch.int32
+        k2 = torch.int64 if torch.int64 in (b2.dtype, s2.dtype) else torch.int32
+        with ctx.span("join.sorted_match"):
+            sidx, bidx = H.sorted_match_pairs(b1.to(dt), b2.to(k2), s1.to(dt), s2.to(k2))
+        return (sidx, bidx) if big_right else (bidx, sidx)
+    return None
+
+
 class _LazyColumns:
     """Mapping view of a LateBatch: gathers a column the first time it is read."""
 
@@ -1013,9 +1050,15 @@ class MultiJoinExec(ExecNode):
         A = la if isinstance(la, LateBatch) else LateBatch([(la, None)], la.num_rows)
         B = lb if isinstance(lb, LateBatch) else LateBatch([(lb, None)], lb.num_rows)
         ev = ctx.evaluator
-        with ctx.span("join.keys"):
-            lk, rk, lvalid, rvalid = key_tensors([ev.column(x, A) for x, _ in on], [ev.column(y, B) for _, y in on])
-        lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx)
+        pairs = _two_key_sorted_pairs(A, B, on, ctx) \
+            if TWO_KEY_SORTED and len(on) == 2 and ctx.device.type == "cuda" else None
+        if pairs is not None:
+            lidx, ridx = pairs
+        else:
+            with ctx.span("join.keys"):
+                lk, rk, lvalid, rvalid = key_tensors([ev.column(x, A) for x, _ in on],
+                                                     [ev.column(y, B) for _, y in on])
+            lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx)
         if residual is not None:
             with ctx.span("join.residual"):
                 P = LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())

@@ -237,6 +237,34 @@ def expand_ranges(lo: torch.Tensor, cnt: torch.Tensor, big_n: int) -> Tuple[torc
     return sidx, bidx
 
 
+def sorted_match_pairs(big1: torch.Tensor, big2: torch.Tensor, small1: torch.Tensor, small2: torch.Tensor
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(small row, big row) pairs with big1 == small1 and big2 == small2, big1
+    non-decreasing (ranges on the first key, then the second key checked inside
+    each range on the device). Grouped by small row."""
+    lo, cnt = sorted_ranges(big1, small1)
+    ns = small1.numel()
+    big2 = _keys_ok(big2)
+    small2 = small2.to(big2.dtype).contiguous()
+    if not is_gpu(big1):
+        s, b = expand_ranges(lo, cnt, big1.numel())
+        keep = big2.index_select(0, b.long()) == small2.index_select(0, s.long())
+        return s[keep], b[keep]
+    N = launch("sorted_match")
+    st = stream(big1)
+    counts = torch.empty(max(ns, 1), dtype=torch.int32, device=big1.device)
+    k64 = big2.dtype == torch.int64
+    N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, ptr(counts), 0, 0, 0, False, st)
+    off, total = exclusive_scan(counts[:ns])
+    it = torch.int32 if max(total, big1.numel(), ns) < INT32_MAX else torch.int64
+    sidx = torch.empty(total, dtype=it, device=big1.device)
+    bidx = torch.empty(total, dtype=it, device=big1.device)
+    if total:
+        N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, 0, ptr(off), ptr(sidx), ptr(bidx),
+                       it == torch.int64, st)
+    return sidx, bidx
+
+
 def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, bool]:
     """``group_ids`` plus whether the ids are non-decreasing. Clustered keys
     (lineitem by l_orderkey, any output that follows a sorted probe side) get

@@ -289,3 +289,25 @@ def test_sorted_ranges_and_expand_vs_torch(gpu_device):
         s_ref, b_ref = H.expand_ranges(lo_ref, cnt_ref, big.numel())
         assert torch.equal(s.cpu().long(), s_ref.long()) and torch.equal(b.cpu().long(), b_ref.long())
         assert torch.equal(big[b.cpu().long()], q[s.cpu().long()])
+
+
+def test_sorted_match_pairs_vs_torch(gpu_device):
+    """ranges.hip sorted_match: two-key join (first key sorted on the big side,
+    second key compared inside each range) against a brute-force CPU oracle."""
+    from igloo_amd.ops import hashing as H
+    g = torch.Generator().manual_seed(11)
+    for dtype in (torch.int32, torch.int64):
+        reps = torch.randint(0, 9, (4000,), generator=g)
+        big1 = torch.repeat_interleave(torch.arange(4000, dtype=dtype), reps)
+        big2 = torch.randint(0, 6, (big1.numel(),), generator=g).to(dtype)
+        s1 = torch.randint(-2, 4005, (30000,), generator=g).to(dtype)
+        s2 = torch.randint(0, 6, (30000,), generator=g).to(dtype)
+        s, b = H.sorted_match_pairs(big1.to(gpu_device), big2.to(gpu_device), s1.to(gpu_device), s2.to(gpu_device))
+        s_ref, b_ref = H.sorted_match_pairs(big1, big2, s1, s2)  # CPU path: expand + compare
+        assert torch.equal(s.cpu().long(), s_ref.long()) and torch.equal(b.cpu().long(), b_ref.long())
+        assert torch.equal(big1[b.cpu().long()], s1[s.cpu().long()])
+        assert torch.equal(big2[b.cpu().long()], s2[s.cpu().long()])
+        # every true match is found
+        want = sum(int(((big1 == s1[i]) & (big2 == s2[i])).sum()) for i in range(0, 30000, 997))
+        got = sum(int((s.cpu().long() == i).sum()) for i in range(0, 30000, 997))
+        assert got == want
