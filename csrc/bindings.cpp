@@ -416,6 +416,18 @@ PYBIND11_MODULE(_native, m) {
                         S(s));
   });
 
+  m.def("dense_index_build", [](uintptr_t big, bool key64, int64_t nb, int64_t kmin, int64_t kmax, uintptr_t first,
+                                bool first64, uintptr_t long_gap, uintptr_t s) {
+    if (nb <= 0 || kmax < kmin || !big || !first) throw std::runtime_error("dense_index_build: bad arguments");
+    kern::dense_index_build(P<const void>(big), key64, nb, kmin, kmax, P<void>(first), first64, P<int32_t>(long_gap),
+                            S(s));
+  });
+  m.def("dense_ranges", [](uintptr_t first, bool first64, int64_t kmin, int64_t kmax, uintptr_t q, bool key64,
+                           uintptr_t qvalid, int64_t nq, uintptr_t lo, uintptr_t cnt, uintptr_t s) {
+    if (nq > 0 && (!first || !q || !lo || !cnt)) throw std::runtime_error("dense_ranges: null buffer");
+    kern::dense_ranges(P<const void>(first), first64, kmin, kmax, P<const void>(q), key64, P<const uint8_t>(qvalid), nq,
+                       P<int64_t>(lo), P<int64_t>(cnt), S(s));
+  });
   m.def("sorted_match", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
                            uintptr_t counts, uintptr_t offsets, uintptr_t sidx, uintptr_t bidx, bool out64,
                            uintptr_t s) {

@@ -227,6 +227,11 @@ void expand_ranges(const int64_t* off, const int64_t* lo, int64_t ns, int64_t to
                    bool out64, hipStream_t stream);
 // second equality key inside the first key's ranges: offsets == null -> counts[ns] of matches,
 // else pairs written at offsets (exclusive scan of those counts)
+// lower-bound table first[k-kmin] (kmax-kmin+2 entries) of a sorted key column, and range lookups in it
+void dense_index_build(const void* big, bool key64, int64_t nb, int64_t kmin, int64_t kmax, void* first, bool first64,
+                       int32_t* long_gap, hipStream_t stream);
+void dense_ranges(const void* first, bool first64, int64_t kmin, int64_t kmax, const void* q, bool key64,
+                  const uint8_t* qvalid, int64_t nq, int64_t* lo, int64_t* cnt, hipStream_t stream);
 void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
                   int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
                   hipStream_t stream);

@@ -214,3 +214,131 @@ void sorted_match(const void* big2, const void* small2, bool key64, const int64_
 
 }  // namespace kern
 }  // namespace igloo
+
+// ---- dense range index over a sorted key column -----------------------------
+// For a non-decreasing key column whose value span is close to its length
+// (partsupp.ps_partkey: 4 rows per key; orders.o_orderkey: 1 of 4 values used)
+// a lower-bound table first[k - kmin] = first row with key >= k turns each
+// range lookup into two adjacent loads instead of a ~27-step binary search
+// whose probes miss the cache when the queries arrive in random key order
+// (Q9 probes partsupp in lineitem order: 11 ms searching vs ~1 ms indexed).
+// Row i fills the entries between the previous row's key and its own.
+namespace igloo {
+namespace kern {
+namespace {
+
+// Gaps longer than kGapFill are not filled (one lane would serialise them):
+// the key's own entry is still written and *long_gap is set, so the caller
+// pre-fills the table with -1, rebuilds, and runs the fix-up pass
+// (long_gap == null) that searches the entries left at -1.
+constexpr int64_t kGapFill = 64;
+
+template <typename K, typename I>
+__global__ __launch_bounds__(kBlock) void dense_index_kernel(const K* __restrict__ big, int64_t nb, int64_t kmin,
+                                                            int64_t kmax, I* __restrict__ first,
+                                                            int32_t* __restrict__ long_gap) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= nb; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t prev = i == 0 ? kmin - 1 : (int64_t)big[i - 1];
+    const int64_t cur = i == nb ? kmax + 1 : (int64_t)big[i];
+    if (cur == prev) continue;
+    int64_t k = cur - prev > kGapFill ? cur : prev + 1;
+    if (k != prev + 1) *long_gap = 1;
+    for (; k <= cur; ++k) first[k - kmin] = (I)i;
+  }
+}
+
+// long-gap fix-up: entries still holding the sentinel get a lower-bound search
+// (neighbouring lanes search neighbouring keys, so the probes share cache lines)
+template <typename K, typename I>
+__global__ __launch_bounds__(kBlock) void dense_fill_kernel(const K* __restrict__ big, int64_t nb, int64_t kmin,
+                                                           int64_t span, I sentinel, I* __restrict__ first) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k <= span; k += (int64_t)gridDim.x * blockDim.x) {
+    if (first[k] != sentinel) continue;
+    const int64_t key = kmin + k;
+    int64_t a = 0, b = nb;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if ((int64_t)big[m] < key) a = m + 1;
+      else b = m;
+    }
+    first[k] = (I)a;
+  }
+}
+
+template <typename K, typename I>
+__global__ __launch_bounds__(kBlock) void dense_ranges_kernel(const I* __restrict__ first, int64_t kmin, int64_t kmax,
+                                                             const K* __restrict__ q,
+                                                             const uint8_t* __restrict__ qvalid, int64_t nq,
+                                                             int64_t* __restrict__ lo_out,
+                                                             int64_t* __restrict__ cnt_out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = (int64_t)q[i];
+    int64_t lo = 0, c = 0;
+    if ((!qvalid || qvalid[i]) && k >= kmin && k <= kmax) {
+      lo = (int64_t)first[k - kmin];
+      c = (int64_t)first[k - kmin + 1] - lo;
+    }
+    lo_out[i] = lo;
+    cnt_out[i] = c;
+  }
+}
+
+template <typename K>
+void dense_launch(bool build, const void* big, int64_t nb, int64_t kmin, int64_t kmax, void* first, bool first64,
+                  int32_t* long_gap, const void* q, const uint8_t* qvalid, int64_t nq, int64_t* lo, int64_t* cnt, hipStream_t stream) {
+  const dim3 b(kBlock);
+  if (build && !long_gap) {  // fix-up pass
+    const int64_t span = kmax - kmin + 1;
+    const dim3 g(grid_for(span + 1, kBlock, 1 << 16));
+    if (first64)
+      hipLaunchKernelGGL((dense_fill_kernel<K, int64_t>), g, b, 0, stream, static_cast<const K*>(big), nb, kmin, span,
+                         (int64_t)-1, static_cast<int64_t*>(first));
+    else
+      hipLaunchKernelGGL((dense_fill_kernel<K, int32_t>), g, b, 0, stream, static_cast<const K*>(big), nb, kmin, span,
+                         (int32_t)-1, static_cast<int32_t*>(first));
+  } else if (build) {
+    const dim3 g(grid_for(nb + 1, kBlock, 1 << 16));
+    if (first64)
+      hipLaunchKernelGGL((dense_index_kernel<K, int64_t>), g, b, 0, stream, static_cast<const K*>(big), nb, kmin, kmax,
+                         static_cast<int64_t*>(first), long_gap);
+    else
+      hipLaunchKernelGGL((dense_index_kernel<K, int32_t>), g, b, 0, stream, static_cast<const K*>(big), nb, kmin, kmax,
+                         static_cast<int32_t*>(first), long_gap);
+  } else {
+    const dim3 g(grid_for(nq, kBlock, 1 << 16));
+    if (first64)
+      hipLaunchKernelGGL((dense_ranges_kernel<K, int64_t>), g, b, 0, stream, static_cast<const int64_t*>(first), kmin,
+                         kmax, static_cast<const K*>(q), qvalid, nq, lo, cnt);
+    else
+      hipLaunchKernelGGL((dense_ranges_kernel<K, int32_t>), g, b, 0, stream, static_cast<const int32_t*>(first), kmin,
+                         kmax, static_cast<const K*>(q), qvalid, nq, lo, cnt);
+  }
+}
+
+}  // namespace
+
+void dense_index_build(const void* big, bool key64, int64_t nb, int64_t kmin, int64_t kmax, void* first, bool first64,
+                       int32_t* long_gap, hipStream_t stream) {
+  if (key64)
+    dense_launch<int64_t>(true, big, nb, kmin, kmax, first, first64, long_gap, nullptr, nullptr, 0, nullptr, nullptr,
+                          stream);
+  else
+    dense_launch<int32_t>(true, big, nb, kmin, kmax, first, first64, long_gap, nullptr, nullptr, 0, nullptr, nullptr,
+                          stream);
+  check_launch("dense_index_build", stream);
+}
+
+void dense_ranges(const void* first, bool first64, int64_t kmin, int64_t kmax, const void* q, bool key64,
+                  const uint8_t* qvalid, int64_t nq, int64_t* lo, int64_t* cnt, hipStream_t stream) {
+  if (nq <= 0) return;
+  if (key64)
+    dense_launch<int64_t>(false, nullptr, 0, kmin, kmax, const_cast<void*>(first), first64, nullptr, q, qvalid, nq, lo,
+                          cnt, stream);
+  else
+    dense_launch<int32_t>(false, nullptr, 0, kmin, kmax, const_cast<void*>(first), first64, nullptr, q, qvalid, nq, lo,
+                          cnt, stream);
+  check_launch("dense_ranges", stream);
+}
+
+}  // namespace kern
+}  // namespace igloo

@@ -9,6 +9,7 @@ CPU tensors use a sort + searchsorted reference implementation.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -197,6 +198,57 @@ def is_sorted(keys: torch.Tensor) -> bool:
     return r
 
 
+DENSE_INDEX = os.environ.get("IGLOO_DENSE_INDEX", "1") == "1"
+DENSE_INDEX_MIN_QUERIES = 1 << 20   # below this a binary search per query is cheaper than building
+DENSE_INDEX_MAX_SPAN_RATIO = 4      # table entries per indexed row (orders: 1 of 4 key values used)
+
+
+def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = None):
+    """Lower-bound table of a sorted key column (csrc/kernels/ranges.hip):
+    ``(kmin, kmax, first)`` with first[k - kmin] = first row whose key >= k,
+    or None when the key span is too sparse. Remembered on the tensor object
+    (resident table columns build it once)."""
+    hit = getattr(big, "_igloo_dense", None)
+    if hit or not build or (hit is False and queries is None):
+        return hit or None
+    nb = big.numel()
+    idx = False
+    if nb:
+        rng = getattr(big, "_igloo_range", None)
+        if rng is None:
+            mm = torch.stack([big[0].to(torch.int64), big[-1].to(torch.int64)]).cpu()
+            rng = (int(mm[0]), int(mm[1]))
+            try:
+                big._igloo_range = rng
+            except (AttributeError, RuntimeError):
+                pass
+        kmin, kmax = rng
+        span = kmax - kmin + 1
+        # the table must be small next to both the indexed rows and the lookups it serves
+        limit = DENSE_INDEX_MAX_SPAN_RATIO * min(nb, queries if queries is not None else nb) + 4096
+        if span <= limit:
+            it = torch.int64 if nb >= INT32_MAX else torch.int32
+            first = torch.empty(span + 1, dtype=it, device=big.device)
+            gap = torch.zeros(1, dtype=torch.int32, device=big.device)
+            N = launch("dense_index_build")
+            st = stream(big)
+            N.dense_index_build(ptr(big), big.dtype == torch.int64, nb, kmin, kmax, ptr(first),
+                                it == torch.int64, ptr(gap), st)
+            if int(gap.item()):
+                # long key gaps: rebuild over a -1 fill, then search the entries left at -1
+                first.fill_(-1)
+                N.dense_index_build(ptr(big), big.dtype == torch.int64, nb, kmin, kmax, ptr(first),
+                                    it == torch.int64, ptr(gap), st)
+                N.dense_index_build(ptr(big), big.dtype == torch.int64, nb, kmin, kmax, ptr(first),
+                                    it == torch.int64, 0, st)
+            idx = (kmin, kmax, first)
+    try:
+        big._igloo_dense = idx
+    except (AttributeError, RuntimeError):
+        pass
+    return idx or None
+
+
 def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Tensor] = None
                   ) -> Tuple[torch.Tensor, torch.Tensor]:
     """For each probe key q[i]: (lo, cnt) with big[lo : lo+cnt] == q[i] (big non-decreasing).
@@ -212,6 +264,14 @@ def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Ten
         return lo, cnt
     lo = torch.empty(nq, dtype=torch.int64, device=big.device)
     cnt = torch.empty(nq, dtype=torch.int64, device=big.device)
+    idx = dense_index(big, build=nq >= DENSE_INDEX_MIN_QUERIES, queries=nq) if DENSE_INDEX else None
+    if idx:
+        kmin, kmax, first = idx
+        launch("dense_ranges").dense_ranges(ptr(first), first.dtype == torch.int64, kmin, kmax, ptr(q),
+                                            q.dtype == torch.int64,
+                                            ptr(qvalid.contiguous() if qvalid is not None else None), nq, ptr(lo),
+                                            ptr(cnt), stream(big))
+        return lo, cnt
     launch("sorted_ranges").sorted_ranges(ptr(big), big.dtype == torch.int64, big.numel(), ptr(q),
                                           ptr(qvalid.contiguous() if qvalid is not None else None), nq, ptr(lo),
                                           ptr(cnt), stream(big))

@@ -311,3 +311,27 @@ def test_sorted_match_pairs_vs_torch(gpu_device):
         want = sum(int(((big1 == s1[i]) & (big2 == s2[i])).sum()) for i in range(0, 30000, 997))
         got = sum(int((s.cpu().long() == i).sum()) for i in range(0, 30000, 997))
         assert got == want
+
+
+def test_dense_range_index_vs_searchsorted(gpu_device, monkeypatch):
+    """ranges.hip dense_index_build/dense_ranges: lower-bound table lookups equal
+    torch.searchsorted ranges, including keys outside [min, max], NULL probes and
+    long key gaps (suffix-min fix-up path)."""
+    from igloo_amd.ops import hashing as H
+    monkeypatch.setattr(H, "DENSE_INDEX_MIN_QUERIES", 0)
+    g = torch.Generator().manual_seed(5)
+    for dtype in (torch.int32, torch.int64):
+        for jump in (0, 5000):   # a 5000-key hole > kGapFill: long-gap path
+            keys = torch.arange(20000, dtype=dtype) * 2 + 7
+            keys[10000:] += jump
+            reps = torch.randint(0, 5, (20000,), generator=g)
+            big = torch.repeat_interleave(keys, reps)
+            q = torch.randint(0, 40000 + jump + 20, (50000,), generator=g).to(dtype)
+            qvalid = torch.rand(50000, generator=g) > 0.05
+            lo_ref = torch.searchsorted(big, q)
+            cnt_ref = torch.where(qvalid, torch.searchsorted(big, q, right=True) - lo_ref, torch.zeros_like(lo_ref))
+            bd = big.to(gpu_device)
+            lo, cnt = H.sorted_ranges(bd, q.to(gpu_device), qvalid.to(gpu_device))
+            assert H.dense_index(bd, build=False) is not None
+            assert torch.equal(cnt.cpu(), cnt_ref)
+            assert torch.equal(lo.cpu()[cnt_ref > 0], lo_ref[cnt_ref > 0])
