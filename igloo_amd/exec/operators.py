@@ -20,6 +20,7 @@ reference's ExecutionPlan implementations and DataFusion's inherited ones
 from __future__ import annotations
 
 import os
+import re
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -55,6 +56,7 @@ class ExecContext:
         self._subq: Dict[int, object] = {}
         self.evaluator = Evaluator(self)
         self.spans: Dict[str, list] = {}  # phase -> [total ms, calls] (EXPLAIN ANALYZE only)
+        self.scan_cache: Dict[tuple, tuple] = {}  # (source, filters) -> (row ids, gathered columns by name)
 
     def span(self, name: str):
         """Time a phase inside an operator (device-synchronised; no-op unless analyzing)."""
@@ -163,6 +165,9 @@ class ExecNode:
 
 
 # ============================================================================ scan
+_CID = re.compile(r"#\d+")
+
+
 class ScanExec(ExecNode):
     def __init__(self, logical: L.Scan):
         self.logical = logical
@@ -205,12 +210,25 @@ class ScanExec(ExecNode):
         s = self.logical
         out_cids = [c.cid for c in s.schema]
         if s.filters:
-            with ctx.span("scan.filter_eval"):
-                m = predicate_mask(self.predicate, b, ctx)
-                idx = mask_to_indices(m)
-            with ctx.span("scan.filter_gather"):
-                taken = take_many([b.columns[c] for c in out_cids], idx)
-            return Batch(dict(zip(out_cids, taken)), idx.numel(), b.dist)
+            # one query scanning a table twice under the same filter (Q21's l1 and
+            # l3, Q11/Q15 view repeats) evaluates it and gathers each column once
+            name = {c.cid: c.name for c in getattr(s, "table_cols", s.schema)}
+            name.update({c.cid: c.name for c in s.schema})
+            fsql = tuple(sorted(_CID.sub("", f.sql()) for f in s.filters))
+            key = (id(s.source), b.num_rows, fsql)
+            hit = None if any("random" in x.lower() for x in fsql) else ctx.scan_cache.get(key)
+            if hit is None:
+                with ctx.span("scan.filter_eval"):
+                    m = predicate_mask(self.predicate, b, ctx)
+                    idx = mask_to_indices(m)
+                hit = ctx.scan_cache[key] = (idx, {})
+            idx, taken_by_name = hit
+            todo = [c for c in out_cids if name[c] not in taken_by_name]
+            if todo:
+                with ctx.span("scan.filter_gather"):
+                    for c, col in zip(todo, take_many([b.columns[c] for c in todo], idx)):
+                        taken_by_name[name[c]] = col
+            return Batch({c: taken_by_name[name[c]] for c in out_cids}, idx.numel(), b.dist)
         return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
 
     def _run(self, ctx):
@@ -1083,7 +1101,14 @@ class MultiJoinExec(ExecNode):
         if key not in rel["ndv"]:
             b = rel["batch"]
             with ctx.span("multijoin.ndv"):
-                if ctx.device.type == "cuda":
+                cached = None
+                if ctx.world == 1 and b.num_rows:
+                    c = ctx.evaluator.column(e, b)
+                    # resident table columns: the sketch of the same tensor is reused across queries
+                    cached = getattr(c.data, "_igloo_ndv", None) if c.valid is None else None
+                if cached is not None:
+                    g = cached
+                elif ctx.device.type == "cuda":
                     if b.num_rows:
                         c = ctx.evaluator.column(e, b)
                         k, _ = group_key_tensor(c)
@@ -1102,6 +1127,11 @@ class MultiJoinExec(ExecNode):
                         g = H.ndv(k)
                     if ctx.world > 1:
                         g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
+                if cached is None and ctx.world == 1 and b.num_rows and c.valid is None and not c.is_dict:
+                    try:
+                        c.data._igloo_ndv = g
+                    except (AttributeError, RuntimeError):
+                        pass
             rel["ndv"][key] = max(g, 1)
         return rel["ndv"][key]
 
