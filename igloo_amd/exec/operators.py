@@ -1272,20 +1272,28 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
     ev = ctx.evaluator
     n = b.num_rows
     dev = ctx.device
-    with ctx.span("agg.eval_keys"):
-        gcols = [ev.column(e, b) for _, e in groups]
-    if groups:
-        if n == 0:
-            return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
-        with ctx.span("agg.group_ids"):
-            ctx.sorted_gids = False
-            gid, ng, rep, reps_src = _encode_groups(gcols, ctx)
+    late = None
+    if groups and n and isinstance(b, LateBatch) and dev.type == "cuda":
+        with ctx.span("agg.late_keys"):
+            late = _late_group_keys(groups, b, ctx)
+    if late is not None:
+        gid, ng, rep, taken = late
     else:
-        gid, ng, rep = None, 1, None
+        with ctx.span("agg.eval_keys"):
+            gcols = [ev.column(e, b) for _, e in groups]
+        if groups:
+            if n == 0:
+                return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
+            with ctx.span("agg.group_ids"):
+                ctx.sorted_gids = False
+                gid, ng, rep, reps_src = _encode_groups(gcols, ctx)
+        else:
+            gid, ng, rep = None, 1, None
+        if groups:
+            with ctx.span("agg.take_keys"):
+                taken = take_many(reps_src, rep)
     out: Dict[int, Column] = {}
     if groups:
-        with ctx.span("agg.take_keys"):
-            taken = take_many(reps_src, rep)
         for (ci, _), c in zip(groups, taken):
             out[ci.cid] = c
     specs, finals = [], []
@@ -1300,6 +1308,52 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
             ci, col = fin(results)
             out[ci.cid] = col
     return Batch(out, ng)
+
+
+def _late_group_keys(groups, b: "LateBatch", ctx):
+    """GROUP BY over a join result still in index form, with plain string keys
+    (TPC-H Q10: c_custkey plus six customer/nation attributes over 11M joined
+    rows). Group by the widest integer key, then check per join input that its
+    row index is constant within every group: a key whose source row is fixed
+    by the group is functionally dependent on it, so it is dropped from the
+    grouping and gathered only for the ng representative rows — the strings
+    are never materialised for all joined rows. Returns (gid, ng, rep, taken)
+    or None (shape does not apply or a dependency fails: the caller groups
+    normally)."""
+    cids = [e.cid if isinstance(e, ColRef) else None for _, e in groups]
+    if any(c is None or c not in b.owner for c in cids):
+        return None
+    base = [b.parts[b.owner[c]][0].columns[c] for c in cids]
+    plain = [i for i, c in enumerate(base) if c.dtype.is_string and not c.is_dict]
+    others = [i for i in range(len(cids)) if i not in plain]
+    if not plain or not others:
+        return None
+    keys = {i: group_key_tensor(b.gather(cids[i]))[0] for i in others}
+    spans = {i: H.key_range(keys[i]) for i in others}
+    lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
+    gid, ng, rep, srt = H.group_ids_ex(keys[lead])
+    rr = rep.index_select(0, gid.long())
+    checks, parts = [], set()
+    for i in range(len(cids)):
+        k = b.owner[cids[i]]
+        if i == lead or k in parts:
+            continue
+        idx = b.parts[k][1]
+        if idx is None:
+            return None
+        parts.add(k)
+        checks.append((idx != idx.index_select(0, rr)).sum())
+    if checks and int(torch.stack(checks).sum().item()):
+        return None
+    ctx.sorted_gids = srt
+    taken = []
+    for i, c in enumerate(cids):
+        if i == lead:
+            taken.append(take(b.gather(c), rep))
+        else:
+            bb, idx = b.parts[b.owner[c]]
+            taken.append(take(bb.columns[c], idx.index_select(0, rep.long())))
+    return gid, ng, rep, taken
 
 
 def _encode_groups(gcols: List[Column], ctx):
