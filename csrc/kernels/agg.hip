@@ -14,6 +14,8 @@
 //   * non-decreasing group ids (clustered keys): run-by-run register folding,
 //     atomics only at chunk edges;
 //   * otherwise: direct global atomics (high-cardinality GROUP BY).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -250,6 +252,175 @@ __global__ __launch_bounds__(kBlock) void agg_sorted_kernel(const int32_t* __res
   }
 }
 
+// Non-decreasing group ids, chunked: each lane folds kSortedRows consecutive
+// rows in registers first (segments closed inside the chunk are stored
+// directly), so the cross-lane segmented scan runs once per kSortedRows rows
+// instead of once per row. Per lane: head = first segment of the chunk (gid
+// gH, may continue from earlier lanes), tail = last segment (gid gT, may
+// continue into later lanes); a one-segment chunk only has a tail. The scan
+// chains tails with equal gids (non-decreasing gids: equal => contiguous).
+// A segment that may cross the wave's tile (its chain starts at a one-segment
+// lane 0, or it is lane 0's head, or lane 63's tail) merges atomically.
+constexpr int kSortedRows = 8;
+
+// A lane's 8 consecutive rows in as few loads as possible (full, aligned
+// chunks: 2x16 B of gids, 4x16 B of int64/f64 values, one 8 B validity word).
+// With one scalar load per row, 16 resident waves' 6 KB tiles overflow the
+// 32 KB vector L1 and every line is refetched up to 8 times.
+__device__ inline void load_gids8(const int32_t* gid, int64_t r0, int64_t n, int g[kSortedRows]) {
+  if (r0 + kSortedRows <= n && ((uintptr_t)(gid + r0) & 15) == 0) {
+    const int4 a = *(const int4*)(gid + r0), b = *(const int4*)(gid + r0 + 4);
+    g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w;
+    g[4] = b.x; g[5] = b.y; g[6] = b.z; g[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) g[j] = r0 + j < n ? gid[r0 + j] : -1;
+  }
+}
+
+// raw 64-bit row payloads (int sign-extended / f64 bits / 1 for COUNT) and validity bits
+__device__ inline unsigned load_vals8(const AggDesc& a, int64_t r0, int64_t n, unsigned long long v[kSortedRows]) {
+  const bool full = r0 + kSortedRows <= n;
+  unsigned ok = 0;
+  if (a.valid) {
+    if (full && ((uintptr_t)(a.valid + r0) & 7) == 0) {
+      const unsigned long long w = *(const unsigned long long*)(a.valid + r0);
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) ok |= ((w >> (8 * j)) & 0xff) ? (1u << j) : 0u;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) ok |= (r0 + j < n && a.valid[r0 + j]) ? (1u << j) : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) ok |= r0 + j < n ? (1u << j) : 0u;
+  }
+  if (a.op == AGG_COUNT) {
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) v[j] = 1;
+    return ok;
+  }
+  const bool wide = a.op == AGG_SUM_F64 || a.op == AGG_MIN_F64 || a.op == AGG_MAX_F64 || a.src64;
+  if (wide) {
+    const unsigned long long* src = (const unsigned long long*)a.src + r0;
+    if (full && ((uintptr_t)src & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; j += 2) {
+        const ulonglong2 x = *(const ulonglong2*)(src + j);
+        v[j] = x.x;
+        v[j + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) v[j] = r0 + j < n ? src[j] : 0;
+    }
+    if (a.op == AGG_MIN_F64 || a.op == AGG_MAX_F64) {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) {
+        double d;
+        __builtin_memcpy(&d, &v[j], 8);
+        v[j] = (unsigned long long)f64_to_ordered(d);
+      }
+    }
+  } else {
+    const int32_t* src = (const int32_t*)a.src + r0;
+    if (full && ((uintptr_t)src & 15) == 0) {
+      const int4 x = *(const int4*)src, y = *(const int4*)(src + 4);
+      v[0] = (long long)x.x; v[1] = (long long)x.y; v[2] = (long long)x.z; v[3] = (long long)x.w;
+      v[4] = (long long)y.x; v[5] = (long long)y.y; v[6] = (long long)y.z; v[7] = (long long)y.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) v[j] = r0 + j < n ? (unsigned long long)(long long)src[j] : 0;
+    }
+  }
+  return ok;
+}
+
+__global__ __launch_bounds__(kBlock) void agg_sorted_chunk_kernel(const int32_t* __restrict__ gid, int64_t n,
+                                                                 AggParams p) {
+  const int lane = lane_id();
+  const int64_t wave_id = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  constexpr int64_t kTileRows = (int64_t)kWave * kSortedRows;
+  for (int64_t base = wave_id * kTileRows; base < n; base += nwaves * kTileRows) {
+    const int64_t r0 = base + (int64_t)lane * kSortedRows;
+    int g[kSortedRows];
+    load_gids8(gid, r0, n, g);
+    const bool valid = g[0] >= 0;
+    int gT = g[0];
+    bool multi = false;
+#pragma unroll
+    for (int j = 1; j < kSortedRows; ++j) {
+      if (g[j] >= 0) {
+        multi |= g[j] != gT;
+        gT = g[j];
+      }
+    }
+    const int gH = g[0];
+    // chain start lane over equal tails
+    int og[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) og[s] = __shfl_up(gT, 1 << s, kWave);
+    int start = lane;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int o = __shfl_up(start, 1 << s, kWave);
+      if (lane >= (1 << s) && og[s] == gT && o < start) start = o;
+    }
+    const bool multi0 = __shfl(multi ? 1 : 0, 0, kWave) != 0;
+    const int prev_gT = og[0];
+    const int prev_start = __shfl_up(start, 1, kWave);
+    const int next_gH = __shfl_down(gH, 1, kWave);
+    const bool has_carry = lane > 0 && prev_gT == gH;
+    const bool head_atomic = lane == 0 || (has_carry && prev_start == 0 && !multi0);
+    const bool tail_end = valid && (lane == kWave - 1 || next_gH != gT);
+    const bool tail_atomic = lane == kWave - 1 || (start == 0 && !multi0);
+    for (int k = 0; k < p.nagg; ++k) {
+      const AggDesc& a = p.d[k];
+      unsigned long long lo, hlo = 0;
+      long long hi, hhi = 0;
+      init_state(a.op, &lo, &hi);
+      unsigned long long v[kSortedRows];
+      const unsigned ok = load_vals8(a, r0, n, v);
+      bool in_head = true;
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) {
+        if (g[j] < 0) break;
+        if (j > 0 && g[j] != g[j - 1]) {
+          if (in_head) {
+            hlo = lo;
+            hhi = hi;
+            in_head = false;
+          } else {
+            store_exclusive(a, g[j - 1], lo, hi);
+          }
+          init_state(a.op, &lo, &hi);
+        }
+        if (ok & (1u << j))
+          seg_combine(a.op, &lo, &hi, v[j], a.op == AGG_SUM_INT && (long long)v[j] < 0 ? -1LL : 0LL);
+      }
+      // segmented inclusive scan of the tails across lanes
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const unsigned long long olo = __shfl_up(lo, 1 << s, kWave);
+        const long long ohi = __shfl_up(hi, 1 << s, kWave);
+        if (lane >= (1 << s) && og[s] == gT) seg_combine(a.op, &lo, &hi, olo, ohi);
+      }
+      const unsigned long long clo = __shfl_up(lo, 1, kWave);
+      const long long chi = __shfl_up(hi, 1, kWave);
+      if (valid && multi) {
+        if (has_carry) seg_combine(a.op, &hlo, &hhi, clo, chi);
+        if (head_atomic) merge_global(a, gH, hlo, hhi);
+        else store_exclusive(a, gH, hlo, hhi);
+      }
+      if (tail_end) {
+        if (tail_atomic) merge_global(a, gT, lo, hi);
+        else store_exclusive(a, gT, lo, hi);
+      }
+    }
+  }
+}
+
 // Single group: registers -> wave reduction -> one global atomic per wave.
 __device__ inline void wave_merge(const AggDesc& a, unsigned long long lo, long long hi) {
   for (int off = kWave / 2; off > 0; off >>= 1) {
@@ -346,6 +517,15 @@ __global__ __launch_bounds__(kBlock) void agg_single_kernel(int64_t n, AggParams
 
 }  // namespace
 
+// IGLOO_AGG_SORTED_ROWS=1 selects the one-row-per-lane sorted kernel (A/B)
+static bool sorted_per_row() {
+  static const bool v = [] {
+    const char* e = std::getenv("IGLOO_AGG_SORTED_ROWS");
+    return e && e[0] == '1' && e[1] == 0;
+  }();
+  return v;
+}
+
 int agg_lds_max_groups(int nagg) {
   // keep the LDS state at <= 64 KiB so several workgroups stay resident per CU
   const int bytes = 64 * 1024;
@@ -368,6 +548,10 @@ void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs
     int64_t maxg = ngroups <= 64 ? 8192 : 2048;
     hipLaunchKernelGGL(agg_lds_kernel, dim3(grid_for(n, kBlock * 8, maxg)), dim3(kBlock), lds, stream, gid, n, ngroups, p);
     check_launch("agg_lds", stream);
+  } else if (sorted_gids && !sorted_per_row()) {
+    hipLaunchKernelGGL(agg_sorted_chunk_kernel, dim3(grid_for(n, kBlock * kSortedRows, 32768)), dim3(kBlock), 0, stream,
+                       gid, n, p);
+    check_launch("agg_sorted_chunk", stream);
   } else if (sorted_gids) {
     hipLaunchKernelGGL(agg_sorted_kernel, dim3(grid_for(n, kBlock, 32768)), dim3(kBlock), 0, stream, gid, n, p);
     check_launch("agg_sorted", stream);

@@ -269,6 +269,37 @@ def test_sorted_group_ids_and_aggregate(gpu_device, n):
     assert not H.group_ids_ex(kd.flip(0))[3]
 
 
+@pytest.mark.parametrize("runs", ["ones", "mixed", "long"])
+def test_sorted_aggregate_chunked_vs_cpu(gpu_device, runs):
+    """agg_sorted_chunk_kernel (8 rows per lane, cross-lane tail chains, atomics
+    only at tile edges) against the CPU reference: runs of 1 row, mixed runs,
+    and runs longer than a 512-row wave tile; NULLs; n not a tile multiple."""
+    g = _rng(17)
+    n = 1_000_003
+    if runs == "ones":
+        k = np.arange(n)
+    elif runs == "mixed":
+        k = np.sort(g.integers(0, n // 4, n))
+    else:
+        k = np.repeat(np.arange(n // 1500 + 1), 1500)[:n]
+    gid = torch.from_numpy(np.unique(k, return_inverse=True)[1].astype(np.int32))
+    ng = int(gid.max()) + 1
+    v = torch.from_numpy(g.integers(-10**12, 10**12, n).astype(np.int64))
+    f = torch.from_numpy(g.standard_normal(n))
+    valid = torch.from_numpy(g.random(n) > 0.2)
+    specs = [("sum_int", v, None), ("count", None, valid), ("min_int", v, valid), ("max_int", v, None),
+             ("sum_f64", f, valid)]
+    ref = A.grouped_aggregate(gid, ng, specs, n, "cpu")
+    dspecs = [(op, x.to(gpu_device) if x is not None else None, m.to(gpu_device) if m is not None else None)
+              for op, x, m in specs]
+    got = A.grouped_aggregate(gid.to(gpu_device), ng, dspecs, n, gpu_device, sorted_gids=True)
+    for (op, _, _), r, o in zip(specs, ref, got):
+        if op == "sum_f64":
+            assert torch.allclose(o.cpu(), r, rtol=1e-9, atol=1e-9)
+        else:
+            assert torch.equal(o.cpu(), r), op
+
+
 def test_sorted_ranges_and_expand_vs_torch(gpu_device):
     """ranges.hip: fused lower/upper bound search + load-balanced range expansion
     against torch.searchsorted / repeat_interleave (fp32-free integer oracle)."""
