@@ -219,7 +219,9 @@ PYBIND11_MODULE(_native, m) {
     f.nterms = (int32_t)terms.size();
     for (size_t i = 0; i < terms.size(); ++i) {
       auto [col, kind, lo, hi, set] = terms[i];
-      if (col < 0 || col >= f.ncols || kind < 0 || kind > 3 || (kind == 3 && (int64_t)set >= f.ncols))
+      // kind = base kind (0 range, 1 not-range, 2 code set, 3 col-col range) | OR-group << 8 (0: top level)
+      const int base = kind & 0xff, grp = kind >> 8;
+      if (col < 0 || col >= f.ncols || kind < 0 || base > 3 || grp > 31 || (base == 3 && (int64_t)set >= f.ncols))
         throw std::runtime_error("fused scan: bad term");
       f.terms[i] = kern::FfTerm{col, kind, lo, hi, set};
     }

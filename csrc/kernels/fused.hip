@@ -108,12 +108,20 @@ __device__ __forceinline__ FfIter ff_iter(int64_t base, int lane, int64_t n) {
 template <int VW>
 __device__ __forceinline__ void ff_pass4(const FfSpec& S, const ff_vec<VW> r0, const ff_vec<VW> r1,
                                          const ff_vec<VW> r2, const ff_vec<VW> r3, const FfIter& it, bool* pass) {
+  // terms with an OR-group (kind >> 8 = g > 0) form one disjunction: the row
+  // passes it when every term of at least one group holds (gok bit g)
+  uint32_t gok[kFfRows];
+  uint32_t used = 0;
 #pragma unroll
-  for (int j = 0; j < kFfRows; ++j) pass[j] = it.live[j];
+  for (int j = 0; j < kFfRows; ++j) {
+    pass[j] = it.live[j];
+    gok[j] = 0xffffffffu;
+  }
   for (int t = 0; t < S.nterms; ++t) {
     const FfTerm& T = S.terms[t];
     const int c = __builtin_amdgcn_readfirstlane(T.col);
-    const int kind = T.kind;
+    const int kind = T.kind & 0xff;
+    const int grp = T.kind >> 8;
     const int64_t lo = T.lo, hi = T.hi;
     const uint64_t set = T.set;
     const int c2 = __builtin_amdgcn_readfirstlane((int)(set & 0xff));  // kind 3: second column
@@ -128,8 +136,15 @@ __device__ __forceinline__ void ff_pass4(const FfSpec& S, const ff_vec<VW> r0, c
       } else {
         hit = v >= lo && v <= hi;
       }
-      pass[j] &= (kind == 1) ? !hit : hit;
+      const bool ok = (kind == 1) ? !hit : hit;
+      if (grp == 0) pass[j] &= ok;
+      else if (!ok) gok[j] &= ~(1u << grp);
     }
+    if (grp) used |= 1u << grp;
+  }
+  if (used) {
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) pass[j] &= (gok[j] & used) != 0;
   }
   if (S.mask) {
     const uint8_t* m = S.mask + it.base;

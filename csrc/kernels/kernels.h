@@ -27,7 +27,7 @@ void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t*
 
 // ---- fused.hip ----------------------------------------------------------------
 constexpr int kFfMaxCols = 8;
-constexpr int kFfMaxTerms = 8;
+constexpr int kFfMaxTerms = 16;
 constexpr int kFfMaxAggs = 8;
 constexpr int kFfMaxGroups = 16;
 constexpr int kFfMaxFactors = 3;

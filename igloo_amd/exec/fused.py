@@ -30,7 +30,8 @@ from ..sql.expr import BinOp, Cast, ColRef, Expr, InList, Lit, conjuncts
 from ..types import DataType
 from ..utils.errors import ExecutionError
 
-MAX_COLS, MAX_TERMS, MAX_AGGS, MAX_GROUPS, MAX_FACTORS = 8, 8, 8, 16, 3
+MAX_COLS, MAX_TERMS, MAX_AGGS, MAX_GROUPS, MAX_FACTORS = 8, 16, 8, 16, 3
+MAX_OR_GROUPS = 31  # disjuncts of the one OR conjunct a launch can hold
 COL_COL = os.environ.get("IGLOO_FF_COLCOL", "0") == "1"  # column-vs-column range terms (A/B: no gain measured)
 I64_MIN, I64_MAX = -(2**63), 2**63 - 1
 FLIP = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
@@ -64,6 +65,9 @@ class Spec:
         self.terms: List[tuple] = []
         self.mask: Optional[torch.Tensor] = None
         self.always_false = False
+        self._group = 0            # OR-group of the terms being added (0: top-level conjunct)
+        self._group_false = False  # the current disjunct can never hold
+        self._has_or = False
 
     def col(self, c: Column) -> int:
         if c.valid is not None or c.is_wide or (c.dtype.is_string and not c.is_dict):
@@ -93,15 +97,58 @@ class Spec:
     def add_predicate(self, pred: Expr) -> None:
         for c in conjuncts(pred):
             try:
-                self._term(c)
+                if isinstance(c, BinOp) and c.op == "or":
+                    self._disjunction(c)
+                else:
+                    self._term(c)
             except Bail as why:
                 _debug("conjunct", why)
                 m = self.ev.mask(c, self.b)
                 self.mask = m if self.mask is None else (self.mask & m)
 
+    def _false(self) -> None:
+        if self._group:
+            self._group_false = True
+        else:
+            self.always_false = True
+
+    def _disjunction(self, c: Expr) -> None:
+        """OR of conjunctions (TPC-H Q19's three brand/container/quantity
+        branches): every disjunct's terms carry its OR-group id; the kernel
+        passes a row when all terms of some group hold. One OR per launch."""
+        ds = _disjuncts(c)
+        if self._has_or or len(ds) > MAX_OR_GROUPS:
+            raise Bail("second OR / too many disjuncts")
+        saved = list(self.terms)
+        g, always_true = 0, False
+        try:
+            for d in ds:
+                self._group, self._group_false = g + 1, False
+                start = len(self.terms)
+                for x in conjuncts(d):
+                    if isinstance(x, BinOp) and x.op == "or":
+                        raise Bail("nested OR")
+                    self._term(x)
+                if self._group_false:
+                    del self.terms[start:]   # this disjunct never holds
+                    continue
+                if len(self.terms) == start:
+                    always_true = True       # this disjunct always holds
+                g += 1
+        except Bail:
+            self.terms = saved
+            raise
+        finally:
+            self._group, self._group_false = 0, False
+        if always_true:
+            self.terms = saved
+        elif g == 0:
+            self.terms = saved
+            self.always_false = True
+        else:
+            self._has_or = True
+
     def _range(self, ci: int, op: str, v: int):
-        if len(self.terms) >= MAX_TERMS:
-            raise Bail("too many terms")
         lo, hi, kind = I64_MIN, I64_MAX, 0
         if op == "=":
             lo = hi = v
@@ -110,18 +157,30 @@ class Spec:
             kind = 1
         elif op == "<":
             if v == I64_MIN:
-                self.always_false = True
+                self._false()
                 return
             hi = v - 1
         elif op == "<=":
             hi = v
         elif op == ">":
             if v == I64_MAX:
-                self.always_false = True
+                self._false()
                 return
             lo = v + 1
         elif op == ">=":
             lo = v
+        kind |= self._group << 8
+        if kind == self._group << 8:
+            # merge with a range on the same column and group (BETWEEN = two terms)
+            for i, (c0, k0, lo0, hi0, s0) in enumerate(self.terms):
+                if c0 == ci and k0 == kind:
+                    lo, hi = max(lo, lo0), min(hi, hi0)
+                    if lo > hi:
+                        self._false()
+                    self.terms[i] = (ci, kind, lo, hi, 0)
+                    return
+        if len(self.terms) >= MAX_TERMS:
+            raise Bail("too many terms")
         self.terms.append((ci, kind, lo, hi, 0))
 
     def _term(self, c: Expr) -> None:
@@ -152,7 +211,7 @@ class Spec:
             code = _dict_code(col, str(r.value))
             if code is None:
                 if op == "=":
-                    self.always_false = True
+                    self._false()
                 return  # '<>' a value not in the dictionary: always true
             self._range(ci, op, code)
             return
@@ -182,7 +241,7 @@ class Spec:
             self._range(ci, ">=", _ceildiv(L, f))
         elif op == "=":
             if L % f:
-                self.always_false = True
+                self._false()
             else:
                 self._range(ci, "=", L // f)
         else:  # '<>'
@@ -202,7 +261,7 @@ class Spec:
             raise Bail("dictionary column comparison")
         lo, hi = {"<": (I64_MIN, -1), "<=": (I64_MIN, 0), ">": (1, I64_MAX), ">=": (0, I64_MAX),
                   "=": (0, 0)}[op]
-        self.terms.append((cl, 3, lo, hi, cr))
+        self.terms.append((cl, 3 | self._group << 8, lo, hi, cr))
 
     def _inlist(self, c: InList) -> None:
         if not isinstance(c.x, ColRef) or any(v.value is None for v in c.values):
@@ -219,11 +278,20 @@ class Spec:
             raise Bail("too many terms")
         if c.negated:
             bits = ~bits & ((1 << 64) - 1)
-        self.terms.append((ci, 2, 0, 0, bits))
+        if bits == 0:
+            self._false()
+            return
+        self.terms.append((ci, 2 | self._group << 8, 0, 0, bits))
 
     def args(self):
         return ([(t.data_ptr(), t.element_size()) for t in self.cols], self.terms,
                 self.mask.data_ptr() if self.mask is not None else 0)
+
+
+def _disjuncts(e: Expr) -> List[Expr]:
+    if isinstance(e, BinOp) and e.op == "or":
+        return _disjuncts(e.left) + _disjuncts(e.right)
+    return [e]
 
 
 def _dict_code(col: Column, s: str) -> Optional[int]:

@@ -562,7 +562,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             else:
                 ridx, lidx, _ = table.probe_pairs(rk, rvalid)
                 pair = _combine(lb, rb, lidx, ridx, False)
-                keep = mask_to_indices(ev.mask(residual, pair))
+                keep = mask_to_indices(predicate_mask(residual, pair, ctx))
                 matched[lidx.index_select(0, keep.long()).long()] = True
             sel = mask_to_indices(matched if kind == "semi" else ~matched)
         with ctx.span("join.gather"):
@@ -616,7 +616,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
     if residual is not None:
         with ctx.span("join.residual"):
             pair = _combine(lb, rb, pidx, bidx, False)
-            keep = ev.mask(residual, pair)
+            keep = predicate_mask(residual, pair, ctx)
         sel = mask_to_indices(keep)
         pidx = pidx.index_select(0, sel.long())
         bidx = bidx.index_select(0, sel.long())
@@ -691,7 +691,7 @@ def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residu
     if residual is not None:
         with ctx.span("join.residual"):
             pair = _combine(lb, rb, lidx, ridx, False)
-            keep = mask_to_indices(ctx.evaluator.mask(residual, pair))
+            keep = mask_to_indices(predicate_mask(residual, pair, ctx))
             lidx = lidx.index_select(0, keep.long())
             ridx = ridx.index_select(0, keep.long())
             if kind == "inner":
@@ -721,7 +721,7 @@ def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:
     ri = torch.arange(n_r, device=dev, dtype=torch.int64).repeat(n_l)
     pair = _combine(lb, rb, li, ri, False)
     if residual is not None:
-        keep = mask_to_indices(ctx.evaluator.mask(residual, pair))
+        keep = mask_to_indices(predicate_mask(residual, pair, ctx))
         li, ri = li.index_select(0, keep.long()), ri.index_select(0, keep.long())
         pair = _take_batch(pair, keep) if kind in ("inner", "cross") else pair
     if kind in ("inner", "cross"):
@@ -1080,7 +1080,7 @@ class MultiJoinExec(ExecNode):
         if residual is not None:
             with ctx.span("join.residual"):
                 P = LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
-                keep = mask_to_indices(ev.mask(residual, P))
+                keep = mask_to_indices(predicate_mask(residual, P, ctx))
                 lidx = lidx.index_select(0, keep.long())
                 ridx = ridx.index_select(0, keep.long())
         with ctx.span("join.compose"):

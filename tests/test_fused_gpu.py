@@ -67,6 +67,15 @@ QUERIES = [
     # decimal column vs literal of another scale / int literal; IN on a dictionary
     "SELECT count(*) AS c, sum(qty) AS s FROM t WHERE qty < 24 AND price > 1000.005 AND status IN ('F', 'X')",
     "SELECT count(*) AS c FROM t WHERE disc = 0.055",
+    # OR of conjunctions (Q19 shape): OR-group terms, BETWEEN merged per group
+    "SELECT count(*) AS c, sum(price * (1 - disc)) AS r FROM t WHERE status = 'F' AND "
+    "((flag = 'A' AND qty BETWEEN 1 AND 11 AND k <= 2) OR (flag = 'R' AND status IN ('F') AND qty BETWEEN 10 AND 20) "
+    "OR (qty >= 20 AND qty <= 30 AND d < DATE '1995-01-01'))",
+    # a disjunct that never holds (value not in the dictionary) / one that always holds
+    "SELECT count(*) AS c FROM t WHERE (flag = 'Z' AND k = 1) OR (k = 2 AND disc > 0.05)",
+    "SELECT count(*) AS c FROM t WHERE (k = 1 AND disc < 0.02) OR flag <> 'Z'",
+    # a disjunct the kernel cannot take (float): whole OR evaluated node by node
+    "SELECT count(*) AS c, sum(qty) AS s FROM t WHERE (f > 10 AND k = 1) OR (k = 3 AND qty < 10)",
 ]
 
 
