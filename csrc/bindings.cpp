@@ -430,6 +430,11 @@ PYBIND11_MODULE(_native, m) {
     kern::dense_ranges(P<const void>(first), first64, kmin, kmax, P<const void>(q), key64, P<const uint8_t>(qvalid), nq,
                        P<int64_t>(lo), P<int64_t>(cnt), S(s));
   });
+  m.def("key_histogram", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, int64_t kmin, int64_t span,
+                            uintptr_t counts, uintptr_t s) {
+    if (n > 0 && (!keys || !counts || span <= 0)) throw std::runtime_error("key_histogram: bad arguments");
+    kern::key_histogram(P<const void>(keys), key64, P<const uint8_t>(valid), n, kmin, span, P<int32_t>(counts), S(s));
+  });
   m.def("sorted_match", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
                            uintptr_t counts, uintptr_t offsets, uintptr_t sidx, uintptr_t bidx, bool out64,
                            uintptr_t s) {

@@ -174,6 +174,31 @@ __global__ __launch_bounds__(kBlock) void groupby_build_kernel(const K* __restri
   }
 }
 
+// Direct-mapped GROUP BY over a small key span (Q5's 5 nations, Q7/Q9's
+// (nation, year) pairs over millions of rows): the first-row table lives in
+// LDS per workgroup, so the atomics that would serialise on a handful of
+// global words stay on-chip; one global atomicMin per touched slot per
+// workgroup at the end.
+constexpr int64_t kGroupLdsSlots = 16384;
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void groupby_build_lds_kernel(const K* __restrict__ keys, int64_t n,
+                                                                  int32_t* __restrict__ trow, int64_t cap,
+                                                                  int64_t kmin) {
+  __shared__ int32_t srow[kGroupLdsSlots];
+  for (int64_t s = threadIdx.x; s < cap; s += blockDim.x) srow[s] = INT32_MAX;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = (int64_t)keys[i] - kmin;
+    if (srow[slot] > (int32_t)i) atomicMin(&srow[slot], (int32_t)i);
+  }
+  __syncthreads();
+  for (int64_t s = threadIdx.x; s < cap; s += blockDim.x) {
+    const int32_t r = srow[s];
+    if (r != INT32_MAX && trow[s] > r) atomicMin(&trow[s], r);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void occupied_kernel(const int32_t* __restrict__ trow, int64_t cap,
                                                          uint8_t* __restrict__ occ) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
@@ -285,6 +310,16 @@ void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, 
 void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,
                    bool direct, hipStream_t stream) {
   if (n == 0) return;
+  if (direct && cap <= kGroupLdsSlots) {
+    // a few hundred workgroups: enough to fill the CUs, few end-of-block merges
+    const dim3 g(grid_for(n, kBlock * 16, 1024)), b(kBlock);
+    if (key64)
+      hipLaunchKernelGGL(groupby_build_lds_kernel<int64_t>, g, b, 0, stream, (const int64_t*)keys, n, trow, cap, kmin);
+    else
+      hipLaunchKernelGGL(groupby_build_lds_kernel<int32_t>, g, b, 0, stream, (const int32_t*)keys, n, trow, cap, kmin);
+    check_launch("groupby_build_lds", stream);
+    return;
+  }
   dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
   if (key64) {
     if (direct) hipLaunchKernelGGL((groupby_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, trow, cap, kmin);

@@ -124,6 +124,9 @@ struct AggDesc {
 };
 
 int agg_lds_max_groups(int nagg);
+// counts[k - kmin] += 1 per valid key in [kmin, kmin + span) (int32 counters, zeroed by the caller)
+void key_histogram(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t span,
+                   int32_t* counts, hipStream_t stream);
 void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream,
                 bool sorted_gids = false);
 

@@ -1211,11 +1211,8 @@ class HashAggExec(ExecNode):
                 if lvalid is not None:
                     inr &= lvalid
                 li = torch.where(inr, li, torch.zeros_like(li))
-                rbase = (rk.to(torch.int64) - kmin)
                 for k, (_, a) in enumerate(lg.aggs):
-                    av = ev.column(a.arg, rb).valid
-                    keys = rbase if av is None else torch.where(av, rbase, torch.full_like(rbase, span))
-                    hist = torch.bincount(keys, minlength=span + 1)[:span]
+                    hist = A.key_histogram(rk, kmin, span, ev.column(a.arg, rb).valid)
                     cnt_cols[-(k + 1)] = torch.where(inr, hist.index_select(0, li), torch.zeros_like(li))
             elif rk.numel():
                 gid, ng, rep, srt = H.group_ids_ex(rk)

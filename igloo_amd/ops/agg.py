@@ -138,3 +138,21 @@ def wide_to_python(t: torch.Tensor) -> List[int]:
     for lo, hi in t.tolist():
         out.append((hi << 64) + (lo & 0xFFFFFFFFFFFFFFFF))
     return out
+
+
+def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int64 counts[span]: rows per key value kmin + i (NULL / out-of-domain keys skipped).
+    GPU: 32-bit atomics straight from the key column (csrc/kernels/agg.hip)."""
+    if keys.device.type == "cpu" or keys.numel() >= 2**31:   # (int32 counters)
+        k = keys.to(torch.int64) - kmin
+        ok = (k >= 0) & (k < span)
+        if valid is not None:
+            ok &= valid
+        return torch.bincount(k[ok], minlength=span)[:span]
+    assert keys.dtype in (torch.int32, torch.int64) and span < 2**31
+    keys = keys.contiguous()
+    counts = torch.zeros(span, dtype=torch.int32, device=keys.device)
+    launch("key_histogram").key_histogram(ptr(keys), keys.dtype == torch.int64,
+                                          ptr(valid.contiguous() if valid is not None else None), keys.numel(), kmin,
+                                          span, ptr(counts), stream(keys))
+    return counts.to(torch.int64)

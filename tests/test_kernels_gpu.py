@@ -366,3 +366,28 @@ def test_dense_range_index_vs_searchsorted(gpu_device, monkeypatch):
             assert H.dense_index(bd, build=False) is not None
             assert torch.equal(cnt.cpu(), cnt_ref)
             assert torch.equal(lo.cpu()[cnt_ref > 0], lo_ref[cnt_ref > 0])
+
+
+def test_key_histogram_and_small_span_group_ids(gpu_device):
+    """agg.hip key_histogram (32-bit atomics) vs torch.bincount, and the
+    LDS-privatised direct GROUP BY build (span <= 16384) vs the CPU path."""
+    g = _rng(23)
+    n = 2_000_000
+    keys = torch.from_numpy(g.integers(-50, 5000, n).astype(np.int32))
+    valid = torch.from_numpy(g.random(n) > 0.3)
+    ref = A.key_histogram(keys, 0, 4000, valid)
+    got = A.key_histogram(keys.to(gpu_device), 0, 4000, valid.to(gpu_device))
+    assert torch.equal(got.cpu(), ref)
+    for span in (5, 700, 16000):
+        k = torch.from_numpy(g.integers(100, 100 + span, n).astype(np.int64))
+        gid, ng, rep = H.group_ids(k.to(gpu_device))
+        assert ng == torch.unique(k).numel()
+        kd = k.to(gpu_device)
+        # rep is each group's FIRST row and gid maps rows back to it
+        assert torch.equal(kd.index_select(0, rep.long()).index_select(0, gid.long()), kd)
+        first = {}
+        for i, v in enumerate(k[:50000].tolist()):
+            first.setdefault(v, i)
+        reps = dict(zip(kd.index_select(0, rep.long()).cpu().tolist(), rep.cpu().tolist()))
+        for v, i in first.items():
+            assert reps[v] == i
