@@ -213,8 +213,9 @@ PYBIND11_MODULE(_native, m) {
     for (size_t i = 0; i < cols.size(); ++i) {
       f.cols[i].ptr = reinterpret_cast<const void*>(cols[i].first);
       f.cols[i].width = cols[i].second;
-      if (!(f.cols[i].width == 4 || f.cols[i].width == 8))  // the kernels load 4- or 8-byte words
-        throw std::runtime_error("fused scan: bad column width");
+      const int64_t w = f.cols[i].width;  // signed 1/2/4/8-byte integer columns
+      if (!(w == 1 || w == 2 || w == 4 || w == 8) || (cols[i].first % w) != 0)
+        throw std::runtime_error("fused scan: bad column width / alignment");
     }
     f.nterms = (int32_t)terms.size();
     for (size_t i = 0; i < terms.size(); ++i) {

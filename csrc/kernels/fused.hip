@@ -30,6 +30,8 @@
 // unsigned low and signed high 32-bit halves of each value go to separate slots
 // and the block merge recombines them in int128. Cells x lanes are sized to
 // the LDS budget (lanes share slots when there are many cells).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -46,22 +48,28 @@ constexpr int ff_vw() { return NC <= 1 ? 1 : NC <= 2 ? 2 : NC <= 4 ? 4 : 8; }
 template <int VW>
 using ff_vec = long long __attribute__((ext_vector_type(VW)));
 
-// Branch-free column load (int32 / int64 columns): two dword loads at
-// p + idx*w and p + idx*w + (w-4) (the same dword twice for int32 columns);
-// p is the wave-uniform address of the iteration's first row. Keeping every
-// load unconditional lets all of a row's loads be in flight at once (a width
-// switch per load made the compiler wait after each one).
+// Branch-free column load (1/2/4/8-byte integer columns): two dword loads at
+// the aligned dword holding the value and the next one for 8-byte columns (the
+// same dword twice otherwise); p is the wave-uniform address of the
+// iteration's first row. Keeping every load unconditional lets all of a row's
+// loads be in flight at once (a width switch per load made the compiler wait
+// after each one). Narrow columns (resident decimals whose values fit 8/16/32
+// bits: l_discount, l_quantity, ...) cut the bytes a scan streams; a sub-dword
+// value is shifted down and sign-extended. The aligned dword never leaves the
+// allocation (PyTorch blocks are 512-byte multiples).
 __device__ __forceinline__ int64_t ff_load(const FfColumn& c, int64_t base, uint32_t idx) {
   const int64_t w = c.width;
   const char* p = (const char*)c.ptr + base * w;
-  const uint32_t off = idx << (w == 8 ? 3 : 2);
-  const uint32_t lo = *(const uint32_t*)(p + off);
-  const uint32_t hi = *(const uint32_t*)(p + (off + (uint32_t)(w - 4)));
+  const uint32_t off = idx * (uint32_t)w;
+  const uint32_t mis = ((uint32_t)(uintptr_t)(p + off)) & 3u;
+  const uint32_t a = off - mis;
+  const uint32_t lo = *(const uint32_t*)(p + a);
+  const uint32_t hi = *(const uint32_t*)(p + (a + (w == 8 ? 4u : 0u)));
   // both dwords are always consumed (a select let the compiler sink the second
-  // load into a branch and wait on it): int32 columns sign-extend via shifts
-  const int64_t v = (int64_t)(((uint64_t)hi << 32) | lo);
-  const int sh = w == 8 ? 0 : 32;
-  return (int64_t)((uint64_t)v << sh) >> sh;
+  // load into a branch and wait on it)
+  const uint64_t v = (((uint64_t)hi << 32) | lo) >> (mis * 8);
+  const int sh = 64 - 8 * (int)w;
+  return (int64_t)(v << sh) >> sh;
 }
 
 // The row vectors are kernel locals (r0..r3) handed to helpers BY VALUE: an
@@ -232,13 +240,21 @@ __device__ __forceinline__ int ff_slot(int cell, int half, int lane, int lanes) 
 }
 
 // LDS layout: cell = a * G + g for aggregates, NA * G + g for the row counts.
+// 512-thread blocks (A/B at SF100: 256 -> 9.7 ms, 512 -> 9.2 ms, 1024 ->
+// 10.5 ms for Q1): the LDS table is per block, so larger blocks put more
+// waves behind the same LDS bytes (Q1: 54 cells x 2 halves x
+// 64 lanes = 55 KB; at 256 threads only 2 blocks = 8 waves fit a CU and the
+// streaming loads are latency-bound).
+constexpr int kFfAggBlock = 512;
+
 template <int NC>
-__global__ __launch_bounds__(kBlock) void ff_agg_kernel(const FfSpec S, int64_t n, int lanes) {
+__global__ __launch_bounds__(1024) void ff_agg_kernel(const FfSpec S, int64_t n, int lanes) {
   extern __shared__ int64_t acc[];
   const int wave = ff_wave_uniform(threadIdx.x / kWave), lane = lane_id();
+  const int waves = blockDim.x / kWave;
   const int G = S.ngroups, NA = S.naggs;
   const int cells = (NA + 1) * G;
-  for (int s = threadIdx.x; s < cells * 2 * lanes; s += kBlock) {
+  for (int s = threadIdx.x; s < cells * 2 * lanes; s += blockDim.x) {
     const int cell = s / (2 * lanes), a = cell / G;
     int64_t init = 0;
     if (a < NA && S.aggs[a].op == 2) init = INT64_MAX;
@@ -248,8 +264,8 @@ __global__ __launch_bounds__(kBlock) void ff_agg_kernel(const FfSpec S, int64_t 
   __syncthreads();
   int ovf = 0;
   const int64_t per_iter = (int64_t)kWave * kFfRows;
-  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * per_iter;
-  for (int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * per_iter; base < n; base += stride) {
+  const int64_t stride = (int64_t)gridDim.x * waves * per_iter;
+  for (int64_t base = ((int64_t)blockIdx.x * waves + wave) * per_iter; base < n; base += stride) {
     const FfIter it = ff_iter(base, lane, n);
     FF_LOAD_ROWS(NC, S, base, it.idx)
     bool pass[kFfRows];
@@ -290,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void ff_agg_kernel(const FfSpec S, int64_t 
     }
   }
   __syncthreads();
-  for (int s = threadIdx.x; s < G * (NA + 1); s += kBlock) {
+  for (int s = threadIdx.x; s < G * (NA + 1); s += blockDim.x) {
     const int g = s / (NA + 1), a = s % (NA + 1);
     const int ccell = NA * G + g;
     if (a == NA || S.aggs[a].op == 1) {
@@ -344,10 +360,18 @@ void launch_agg(const FfSpec& spec, int64_t n, hipStream_t stream) {
   int lanes = kWave;
   while (lanes > 1 && cells * 2 * lanes * sizeof(int64_t) > (size_t)kFfLdsMax) lanes >>= 1;
   const size_t lds = cells * 2 * lanes * sizeof(int64_t);
-  // persistent-style grid: about as many blocks as stay resident (LDS-limited),
-  // each streaming many rows, so the per-block init/merge is amortised
-  const int per_cu = lds <= 20 * 1024 ? 8 : lds <= 32 * 1024 ? 4 : 2;
-  hipLaunchKernelGGL(ff_agg_kernel<NC>, dim3(grid_for(n, kBlock * kFfRows * 4, 256 * per_cu)), dim3(kBlock), lds,
+  static const int block = [] {
+    const char* e = std::getenv("IGLOO_FF_AGG_BLOCK");
+    const int v = e ? std::atoi(e) : kFfAggBlock;
+    return (v == 256 || v == 512 || v == 1024) ? v : kFfAggBlock;
+  }();
+  // persistent-style grid: about as many blocks as stay resident (LDS-limited,
+  // 160 KB per CU; at most 2048 threads), each streaming many rows, so the
+  // per-block init/merge is amortised
+  int per_cu = (int)((160 * 1024) / (lds ? lds : 1));
+  per_cu = per_cu < 1 ? 1 : per_cu;
+  per_cu = per_cu > 2048 / block ? 2048 / block : per_cu;
+  hipLaunchKernelGGL(ff_agg_kernel<NC>, dim3(grid_for(n, block * kFfRows * 4, 256 * per_cu)), dim3(block), lds,
                      stream, spec, n, lanes);
 }
 

@@ -56,6 +56,15 @@ class TableSource:
         return pa.schema([pa.field(f.name, f.dtype.to_arrow(), f.nullable) for f in self.schema()])
 
 
+def _mark_resident(c: Column) -> None:
+    """Flag a table column's data tensor as long-lived, so per-tensor derived
+    structures (narrow copies for the fused scans) are worth building."""
+    try:
+        c.data._igloo_resident = True
+    except (AttributeError, RuntimeError):
+        pass
+
+
 class MemoryTable(TableSource):
     """Device-resident table (the HBM tier): columns stay in GPU memory and a
     scan hands out the resident columns without copying."""
@@ -64,6 +73,8 @@ class MemoryTable(TableSource):
                  partitioned_by: Optional[str] = None, replicated: bool = False,
                  fields: Optional[List[Field]] = None):
         self.columns = dict(columns)
+        for c in self.columns.values():
+            _mark_resident(c)
         self._n = num_rows if num_rows is not None else (len(next(iter(columns.values()))) if columns else 0)
         self.partitioned_by = partitioned_by
         self.replicated = replicated

@@ -118,3 +118,25 @@ def test_fused_decimal_overflow_detected(gpu_device):
     e.register_table("t", big)
     with pytest.raises(Exception, match="overflow"):
         e.query("SELECT sum(a * b) FROM t")
+
+
+def test_fused_narrow_columns_match_cpu(gpu_device, monkeypatch):
+    """Resident int64/int32 columns narrowed to int8/int16/int32 shadows (the
+    1/2-byte loads of ff_load) give the same answers as the CPU evaluator."""
+    from igloo_amd.exec import fused
+    monkeypatch.setattr(fused, "NARROW_MIN_ROWS", 0)
+    t = _table(100_000, seed=9)
+    eg = ig.QueryEngine(device=gpu_device)
+    eg.register_table("t", t)
+    ec = ig.QueryEngine(device="cpu")
+    ec.register_table("t", t)
+    for sql in QUERIES:
+        a, b = ec.query(sql).to_pylist(), eg.query(sql).to_pylist()
+        assert len(a) == len(b)
+        for rc, rg in zip(a, b):
+            for k in rc:
+                assert _close(rc[k], rg[k]), (sql, k, rc[k], rg[k])
+    import torch
+    src = eg.catalog.get_table("t")
+    widths = {getattr(c.data, "_igloo_narrow", c.data).dtype for c in src.columns.values()}
+    assert torch.int8 in widths and torch.int16 in widths
