@@ -685,6 +685,13 @@ def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residu
         with ctx.span("join.gather"):
             m = cnt > 0
             return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
+    if kind in ("semi", "anti") and dev.type == "cuda":
+        cmp = _col_compare(residual, lb, rb)
+        if cmp is not None:
+            with ctx.span("join.sorted_exists"):
+                lcol, rcol, op = cmp   # residual: lcol OP rcol; the big side is the right
+                m = H.sorted_exists(rcol, lcol, lo, cnt, FLIP_OP[op])
+                return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
     with ctx.span("join.sorted_expand"):
         sidx, bidx = H.expand_ranges(lo, cnt, nb)
         lidx, ridx = (sidx, bidx) if big_right else (bidx, sidx)
@@ -710,6 +717,28 @@ def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residu
     all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
     all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
     return _combine(lb, rb, all_l, all_r, True)
+
+
+FLIP_OP = {"=": "=", "<>": "<>", "<": ">", "<=": ">=", ">": "<", ">=": "<="}
+_CMP_KINDS = ("int8", "int16", "int32", "int64", "date32")
+
+
+def _col_compare(residual, lb: Batch, rb: Batch):
+    """(left data, right data, op) when the residual is ``left_col OP right_col``
+    over non-null integer-like columns of one type; else None."""
+    if not (isinstance(residual, BinOp) and residual.op in FLIP_OP and isinstance(residual.left, ColRef)
+            and isinstance(residual.right, ColRef)):
+        return None
+    l, r, op = residual.left, residual.right, residual.op
+    if l.cid in rb.columns and r.cid in lb.columns:
+        l, r, op = r, l, FLIP_OP[op]
+    if l.cid not in lb.columns or r.cid not in rb.columns:
+        return None
+    a, b = lb.columns[l.cid], rb.columns[r.cid]
+    if a.valid is not None or b.valid is not None or a.dtype != b.dtype or a.dtype.kind not in _CMP_KINDS \
+            or a.is_dict or b.is_dict:
+        return None
+    return a.data, b.data, op
 
 
 def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:

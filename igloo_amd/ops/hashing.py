@@ -325,6 +325,28 @@ def sorted_match_pairs(big1: torch.Tensor, big2: torch.Tensor, small1: torch.Ten
     return sidx, bidx
 
 
+EXISTS_OPS = {"=": 0, "<>": 1, "<": 2, "<=": 3, ">": 4, ">=": 5}
+
+
+def sorted_exists(big2: torch.Tensor, small2: torch.Tensor, lo: torch.Tensor, cnt: torch.Tensor, op: str
+                  ) -> torch.Tensor:
+    """bool[ns]: some row k of small row i's range (lo, cnt) has big2[k] OP small2[i]."""
+    dt = torch.int64 if torch.int64 in (big2.dtype, small2.dtype) else torch.int32
+    big2, small2 = big2.to(dt).contiguous(), small2.to(dt).contiguous()
+    ns = small2.numel()
+    if not is_gpu(big2):
+        s, b = expand_ranges(lo, cnt, big2.numel())
+        bv, sv = big2.index_select(0, b.long()), small2.index_select(0, s.long())
+        ok = {"=": bv == sv, "<>": bv != sv, "<": bv < sv, "<=": bv <= sv, ">": bv > sv, ">=": bv >= sv}[op]
+        hit = torch.zeros(ns, dtype=torch.bool)
+        hit[s.long()[ok]] = True
+        return hit
+    hit = torch.empty(ns, dtype=torch.bool, device=big2.device)
+    launch("sorted_exists").sorted_exists(ptr(big2), ptr(small2), dt == torch.int64, ptr(lo), ptr(cnt), ns,
+                                          EXISTS_OPS[op], ptr(hit), stream(big2))
+    return hit
+
+
 def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, bool]:
     """``group_ids`` plus whether the ids are non-decreasing. Clustered keys
     (lineitem by l_orderkey, any output that follows a sorted probe side) get

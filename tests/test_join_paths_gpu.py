@@ -36,6 +36,8 @@ QUERIES = [
     "SELECT sk FROM small WHERE EXISTS (SELECT 1 FROM big WHERE bk = sk)",
     "SELECT sk FROM small WHERE EXISTS (SELECT 1 FROM big WHERE bk = sk AND bs <> ss)",
     "SELECT sk FROM small WHERE NOT EXISTS (SELECT 1 FROM big WHERE bk = sk AND bs <> ss)",
+    "SELECT sk FROM small WHERE EXISTS (SELECT 1 FROM big WHERE bk = sk AND bs < ss)",
+    "SELECT sk FROM small WHERE NOT EXISTS (SELECT 1 FROM big WHERE bk = sk AND ss >= bs)",
     "SELECT sn, count(bv) AS c FROM small LEFT JOIN big ON sn = bk GROUP BY sn",
     "SELECT sk, count(*) AS c FROM small JOIN big ON sk = bk GROUP BY sk",
 ]
