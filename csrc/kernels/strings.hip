@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kBlock) void like_kernel(const int64_t* __restrict_
 // string out of LDS. The per-lane byte-serial scan of the simple kernel above
 // touches a new 64-byte line every few bytes per lane; staging turns the HBM
 // traffic into one streaming read of the character buffer.
-constexpr int kLikeTileBytes = 24576;
+constexpr int kLikeTileBytes = 16384;  // 256 rows of ~50-byte comments; 24.6 KB LDS per block -> 6 blocks per CU
 constexpr int kLikeMaxPattern = 256;
 
 __global__ __launch_bounds__(kBlock) void like_tile_kernel(const int64_t* __restrict__ off,

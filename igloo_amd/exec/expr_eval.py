@@ -571,9 +571,12 @@ def _convert_tensor(c: Column, t: DataType) -> torch.Tensor:
 def _overflow_guard(a, c):
     """Decimal product whose static precision exceeds 18 digits: verify at run time
     that the int64 product cannot overflow (raises otherwise)."""
+    ts = [v for v in (a, c) if isinstance(v, torch.Tensor) and v.numel()]
+    dev_max = iter(torch.stack([v.abs().max().to(torch.int64) for v in ts]).tolist() if ts else [])  # one sync
+
     def mx(v):
         if isinstance(v, torch.Tensor):
-            return int(v.abs().max().item()) if v.numel() else 0
+            return int(next(dev_max)) if v.numel() else 0
         return abs(int(v))
     if mx(a) * mx(c) >= 2**63:
         raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")

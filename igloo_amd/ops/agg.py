@@ -71,9 +71,13 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
         for i in range(0, len(descs), 8):
             launch("agg_update")
             N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s, bool(sorted_gids))
+    # one host sync for every integer SUM's "fits in int64" check
+    wide = [(dst, dst2) for op, dst, dst2 in posts if op == "sum_int"]
+    fits = torch.stack([(h == (l >> 63)).all() for l, h in wide]).tolist() if wide else []
+    fit_iter = iter(fits)
     for op, dst, dst2 in posts:
         if op == "sum_int":
-            outs.append(_wide_to_result(dst, dst2))
+            outs.append(dst if next(fit_iter) else torch.stack([dst, dst2], dim=1))
         elif op in ("min_f64", "max_f64"):
             # empty groups keep the int64 sentinel: report +/-inf like the CPU path
             sentinel = I64_MAX if op == "min_f64" else I64_MIN

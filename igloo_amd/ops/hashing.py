@@ -40,7 +40,8 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
     if keys.numel() == 0:
         return None
     mn, mx = torch.aminmax(keys)
-    return int(mn.item()), int(mx.item())
+    lo, hi = torch.stack([mn.to(torch.int64), mx.to(torch.int64)]).tolist()   # one host sync
+    return int(lo), int(hi)
 
 
 def _keys_ok(k: torch.Tensor) -> torch.Tensor:

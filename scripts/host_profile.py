@@ -41,6 +41,10 @@ def main():
     torch.cuda.synchronize()
     pr.disable()
     print(f"suite {time.perf_counter() - t0:.3f}s (profiled)")
+    s = io.StringIO()
+    st = pstats.Stats(pr, stream=s)
+    st.sort_stats("tottime").print_callers(r"method 'item'|method 'cpu'|method 'tolist'")
+    print(s.getvalue())
     for key in ("tottime", "cumulative"):
         s = io.StringIO()
         pstats.Stats(pr, stream=s).sort_stats(key).print_stats(a.top)
