@@ -26,6 +26,7 @@ import torch
 
 from .. import types as T
 from ..columnar import Batch, Column
+from ..ops._lib import to_host_ints
 from ..sql.expr import BinOp, Cast, ColRef, Expr, InList, Lit, conjuncts
 from ..types import DataType
 from ..utils.errors import ExecutionError
@@ -438,7 +439,8 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
                 lo, size = 0, len(col.dictionary)
             elif col.dtype.is_integer or col.dtype.kind in ("date32", "bool"):
                 mn, mx = torch.aminmax(col.data)
-                lo, size = int(mn.item()), int(mx.item()) - int(mn.item()) + 1
+                lo, hi = to_host_ints(torch.stack([mn.to(torch.int64), mx.to(torch.int64)]))
+                size = hi - lo + 1
             else:
                 raise Bail("group key type")
             kinfo.append((ci, col, k, lo, max(size, 1)))
@@ -509,7 +511,7 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
         with ctx.span("agg.fused_scan"):
             launch("ff_aggregate").ff_aggregate(cols, terms, mask, keys, G, kaggs, counts.data_ptr(), ovf.data_ptr(),
                                                 n, stream(counts))
-    if any(chk for _, chk, _ in descs) and int(ovf.item()):
+    if any(chk for _, chk, _ in descs) and to_host_ints(ovf)[0]:
         raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
     from ..ops.agg import _wide_to_result
     res = [(_wide_to_result(d, d2) if d2 is not None else d) for d, d2 in bufs]

@@ -10,7 +10,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import is_gpu, launch, native, ptr, stream
+from ._lib import is_gpu, launch, native, ptr, stream, to_host_ints
 
 OPS = {"sum_int": 0, "sum_f64": 1, "count": 2, "min_int": 3, "max_int": 4, "min_f64": 5, "max_f64": 6}
 I64_MAX = 2**63 - 1
@@ -73,7 +73,7 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
             N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s, bool(sorted_gids))
     # one host sync for every integer SUM's "fits in int64" check
     wide = [(dst, dst2) for op, dst, dst2 in posts if op == "sum_int"]
-    fits = torch.stack([(h == (l >> 63)).all() for l, h in wide]).tolist() if wide else []
+    fits = to_host_ints(torch.stack([(h == (l >> 63)).all() for l, h in wide])) if wide else []
     fit_iter = iter(fits)
     for op, dst, dst2 in posts:
         if op == "sum_int":

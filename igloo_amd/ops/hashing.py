@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import is_gpu, launch, ptr, stream
+from ._lib import is_gpu, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints
 from .select import exclusive_scan, mask_to_indices
 
 EMPTY_KEY = -(2**63)
@@ -40,7 +40,7 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
     if keys.numel() == 0:
         return None
     mn, mx = torch.aminmax(keys)
-    lo, hi = torch.stack([mn.to(torch.int64), mx.to(torch.int64)]).tolist()   # one host sync
+    lo, hi = to_host_ints(torch.stack([mn.to(torch.int64), mx.to(torch.int64)]))   # one host sync
     return int(lo), int(hi)
 
 
@@ -91,7 +91,7 @@ class JoinTable:
         N.join_build(ptr(keys), keys.dtype == torch.int64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead),
                      ptr(self.next), self.cap, self.kmin, self.direct, ptr(dups), ptr(self.bits), self.bmask,
                      stream(keys))
-        self.unique = int(dups.item()) == 0
+        self.unique = to_host_int(dups) == 0
 
     # ----------------------------------------------------------------- probes
     def probe_first(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
@@ -191,7 +191,7 @@ def is_sorted(keys: torch.Tensor) -> bool:
     if hit is not None:
         return hit
     n = keys.numel()
-    r = True if n < 2 else bool((keys[1:] >= keys[:-1]).all().item())
+    r = True if n < 2 else bool(to_host_int((keys[1:] >= keys[:-1]).all()))
     try:
         keys._igloo_sorted = r
     except (AttributeError, RuntimeError):
@@ -235,7 +235,7 @@ def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = 
             st = stream(big)
             N.dense_index_build(ptr(big), big.dtype == torch.int64, nb, kmin, kmax, ptr(first),
                                 it == torch.int64, ptr(gap), st)
-            if int(gap.item()):
+            if to_host_int(gap):
                 # long key gaps: rebuild over a -1 fill, then search the entries left at -1
                 first.fill_(-1)
                 N.dense_index_build(ptr(big), big.dtype == torch.int64, nb, kmin, kmax, ptr(first),
@@ -441,7 +441,7 @@ def hll_estimate(regs: torch.Tensor) -> float:
     for small cardinalities). Relative error ~1.04/sqrt(4096) = 1.6%."""
     r = regs.to(torch.float64)
     m = float(HLL_M)
-    z, zeros = torch.stack([torch.pow(2.0, -r).sum(), (regs == 0).sum().to(torch.float64)]).tolist()
+    z, zeros = to_host_f64s(torch.stack([torch.pow(2.0, -r).sum(), (regs == 0).sum().to(torch.float64)]))
     zeros = int(zeros)
     alpha = 0.7213 / (1.0 + 1.079 / m)
     e = alpha * m * m / z

@@ -5,7 +5,7 @@ from typing import Tuple
 
 import torch
 
-from ._lib import idx_dtype, is_gpu, launch, ptr, stream
+from ._lib import idx_dtype, is_gpu, launch, ptr, stream, to_host_int
 
 
 def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
@@ -21,7 +21,7 @@ def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
     ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
     s = stream(mask)
     N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
-    total = int(ws[tiles].item())
+    total = to_host_int(ws[tiles:])
     out = torch.empty(total, dtype=it, device=mask.device)
     if total:
         N.select_write(ptr(mask), n, ptr(ws), ptr(out), it == torch.int64, s)
@@ -43,7 +43,7 @@ def exclusive_scan(counts: torch.Tensor) -> Tuple[torch.Tensor, int]:
     ws = torch.empty(tiles + 1, dtype=torch.int64, device=counts.device)
     out = torch.empty(n, dtype=torch.int64, device=counts.device)
     N.exclusive_scan(ptr(counts), counts.dtype == torch.int64, n, ptr(out), ptr(ws), ptr(ws) + 8 * tiles, stream(counts))
-    return out, int(ws[tiles].item())
+    return out, to_host_int(ws[tiles:])
 
 
 def offsets_from_lengths(lengths: torch.Tensor) -> Tuple[torch.Tensor, int]:
