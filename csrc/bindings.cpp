@@ -191,6 +191,25 @@ PYBIND11_MODULE(_native, m) {
                      P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<int32_t>(counts),
                      P<int32_t>(first), P<uint8_t>(matched), P<const uint32_t>(bits), bmask, S(s));
   });
+  m.def("probe_hit_tiles", [](int64_t m_) { return kern::probe_hit_tiles(m_); });
+  m.def("probe_hits", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
+                         int64_t cap, int64_t kmin, bool direct, uintptr_t bits, uint64_t bmask, bool negate,
+                         uintptr_t words, uintptr_t tile_counts, uintptr_t s) {
+    if (m_ > 0 && (!keys || !thead || !words || !tile_counts || (!direct && !tkeys)))
+      throw std::runtime_error("probe_hits: null buffer");
+    kern::probe_hits(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
+                     P<const int32_t>(thead), cap, kmin, direct, P<const uint32_t>(bits), bmask, negate,
+                     P<unsigned long long>(words), P<int64_t>(tile_counts), S(s));
+  });
+  m.def("probe_write", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
+                          int64_t cap, int64_t kmin, bool direct, uintptr_t words, uintptr_t tile_off,
+                          uintptr_t out_probe, bool out64, uintptr_t out_build, uintptr_t s) {
+    if (m_ > 0 && (!keys || !thead || !words || !tile_off || !out_probe || (!direct && !tkeys)))
+      throw std::runtime_error("probe_write: null buffer");
+    kern::probe_write(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
+                      P<const int32_t>(thead), cap, kmin, direct, P<const unsigned long long>(words),
+                      P<const int64_t>(tile_off), P<void>(out_probe), out64, P<int32_t>(out_build), S(s));
+  });
   m.def("join_expand", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
                           uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t offsets, uintptr_t out_probe,
                           uintptr_t out_build, uintptr_t bits, uint64_t bmask, uintptr_t s) {

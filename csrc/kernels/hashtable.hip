@@ -416,3 +416,134 @@ void groupby_lookup(const void* keys, bool key64, int64_t n, const int64_t* tkey
 
 }  // namespace kern
 }  // namespace igloo
+
+// ---- probe + compaction in two passes --------------------------------------
+// First-match probes whose result is a row selection (inner join on a unique
+// build side, semi / anti joins): instead of writing first[] for every probe
+// row and compacting it (first: 4 B/row written, compared, flag-compacted:
+// ~15 B of traffic per probe row for a 600M-row lineitem probe), pass 1
+// writes one hit bit per row and a count per 8192-row tile; pass 2 (after an
+// exclusive scan of the tile counts) re-probes only the hit rows and writes
+// (probe row, build row) at their final positions, in row order.
+namespace igloo {
+namespace kern {
+namespace {
+constexpr int kHitTile = 8192;                 // rows per tile
+constexpr int kHitWords = kHitTile / kWave;    // 64-bit hit words per tile (128)
+
+template <typename K, bool DIRECT>
+__global__ __launch_bounds__(kBlock) void probe_hits_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
+                                                           int64_t m, const int64_t* __restrict__ tkeys,
+                                                           const int32_t* __restrict__ thead, int64_t cap,
+                                                           int64_t kmin, const uint32_t* __restrict__ bits,
+                                                           uint64_t bmask, bool negate,
+                                                           unsigned long long* __restrict__ words,
+                                                           int64_t* __restrict__ tile_counts) {
+  __shared__ int64_t red[kWavesPerBlock];
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  const int64_t tiles = (m + kHitTile - 1) / kHitTile;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    int64_t cnt = 0;
+#pragma unroll 4
+    for (int it = 0; it < kHitTile / kBlock; ++it) {
+      const int64_t row = t * kHitTile + (int64_t)it * kBlock + threadIdx.x;
+      bool hit = false;
+      if (row < m) {
+        const int32_t h = probe_head<K, DIRECT>(keys, valid, row, tkeys, thead, cap, kmin, bits, bmask);
+        hit = (h >= 0) != negate;
+      }
+      const unsigned long long b = __ballot(hit);
+      if (lane == 0 && t * kHitTile + (int64_t)it * kBlock + wave * kWave < m)
+        words[t * kHitWords + it * kWavesPerBlock + wave] = b;
+      cnt += __popcll(b);
+    }
+    if (lane == 0) red[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t s = 0;
+      for (int w = 0; w < kWavesPerBlock; ++w) s += red[w];
+      tile_counts[t] = s;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename K, bool DIRECT, typename O>
+__global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
+                                                            int64_t m, const int64_t* __restrict__ tkeys,
+                                                            const int32_t* __restrict__ thead, int64_t cap,
+                                                            int64_t kmin, const unsigned long long* __restrict__ words,
+                                                            const int64_t* __restrict__ tile_off,
+                                                            O* __restrict__ out_probe, int32_t* __restrict__ out_build) {
+  __shared__ int64_t woff[kHitWords];
+  __shared__ int64_t scratch[kWavesPerBlock + 1];
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  const int64_t tiles = (m + kHitTile - 1) / kHitTile;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t nrows = m - t * kHitTile < kHitTile ? m - t * kHitTile : kHitTile;
+    const int nwords = (int)((nrows + kWave - 1) / kWave);
+    const unsigned long long w0 = threadIdx.x < nwords ? words[t * kHitWords + threadIdx.x] : 0ULL;
+    int64_t total;
+    const int64_t ex = block_exclusive_scan((int64_t)__popcll(w0), scratch, &total);
+    if (threadIdx.x < kHitWords) woff[threadIdx.x] = ex;
+    __syncthreads();
+    if (total) {
+      const int64_t base = tile_off[t];
+      for (int w = wave; w < nwords; w += kWavesPerBlock) {
+        const unsigned long long b = words[t * kHitWords + w];
+        if (!((b >> lane) & 1ULL)) continue;
+        const int64_t row = t * kHitTile + (int64_t)w * kWave + lane;
+        const int64_t pos = base + woff[w] + __popcll(b & ((1ULL << lane) - 1ULL));
+        out_probe[pos] = (O)row;
+        if (out_build) out_build[pos] = probe_head<K, DIRECT>(keys, valid, row, tkeys, thead, cap, kmin, nullptr, 0);
+      }
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+int64_t probe_hit_tiles(int64_t m) { return (m + kHitTile - 1) / kHitTile; }
+
+void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits, uint64_t bmask,
+                bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream) {
+  if (m == 0) return;
+  const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
+#define IG_PH(KT, D)                                                                                              \
+  hipLaunchKernelGGL((probe_hits_kernel<KT, D>), g, b, 0, stream, (const KT*)keys, valid, m, tkeys, thead, cap, kmin, \
+                     bits, bmask, negate, words, tile_counts)
+  if (key64) {
+    if (direct) IG_PH(int64_t, true);
+    else IG_PH(int64_t, false);
+  } else {
+    if (direct) IG_PH(int32_t, true);
+    else IG_PH(int32_t, false);
+  }
+#undef IG_PH
+  check_launch("probe_hits", stream);
+}
+
+void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                 const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
+                 const int64_t* tile_off, void* out_probe, bool out64, int32_t* out_build, hipStream_t stream) {
+  if (m == 0) return;
+  const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
+#define IG_PW(KT, D, OT)                                                                                           \
+  hipLaunchKernelGGL((probe_write_kernel<KT, D, OT>), g, b, 0, stream, (const KT*)keys, valid, m, tkeys, thead, cap, \
+                     kmin, words, tile_off, (OT*)out_probe, out_build)
+#define IG_PW2(KT, D) \
+  if (out64) IG_PW(KT, D, int64_t); else IG_PW(KT, D, int32_t)
+  if (key64) {
+    if (direct) { IG_PW2(int64_t, true); }
+    else { IG_PW2(int64_t, false); }
+  } else {
+    if (direct) { IG_PW2(int32_t, true); }
+    else { IG_PW2(int32_t, false); }
+  }
+#undef IG_PW2
+#undef IG_PW
+  check_launch("probe_write", stream);
+}
+}  // namespace kern
+}  // namespace igloo

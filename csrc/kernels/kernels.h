@@ -89,6 +89,15 @@ void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, i
 void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
                 int32_t* first, uint8_t* build_matched, const uint32_t* bits, uint64_t bmask, hipStream_t stream);
+// first-match probe as a row selection: pass 1 hit bits (words[tiles*128]) + per-tile counts, pass 2
+// (tile_off = exclusive scan of the counts) writes hit rows (+ their build rows) in row order
+int64_t probe_hit_tiles(int64_t m);
+void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits, uint64_t bmask,
+                bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream);
+void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                 const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
+                 const int64_t* tile_off, void* out_probe, bool out64, int32_t* out_build, hipStream_t stream);
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
                  const int64_t* offsets, int32_t* out_probe, int32_t* out_build, const uint32_t* bits, uint64_t bmask,

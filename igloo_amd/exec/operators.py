@@ -513,8 +513,7 @@ def apply_key_filters(b: Batch, filters, ctx) -> Batch:
             pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
             if b.num_rows == 0:
                 continue
-            first = H.JoinTable(bk, bvalid).probe_first(pk, pvalid)
-            sel = mask_to_indices(first >= 0)
+            sel, _ = H.JoinTable(bk, bvalid).probe_select(pk, pvalid, want_build=False)
             if sel.numel() < b.num_rows:
                 keys = list(b.columns)
                 b = Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], sel))), sel.numel(), b.dist)
@@ -594,17 +593,15 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
         table = H.JoinTable(rk, rvalid)
     if kind in ("semi", "anti") and residual is None:
         with ctx.span("join.probe"):
-            first = table.probe_first(lk, lvalid)
-            m = first >= 0 if kind == "semi" else first < 0
-            sel = mask_to_indices(m)
+            sel, _ = table.probe_select(lk, lvalid, negate=kind != "semi", want_build=False)
         with ctx.span("join.gather"):
             return _take_batch(lb, sel)
     if residual is None and table.unique and kind in ("inner", "left"):
         with ctx.span("join.probe"):
-            first = table.probe_first(lk, lvalid)
             if kind == "inner":
-                pidx = mask_to_indices(first >= 0)
-                bidx = first.index_select(0, pidx.long())
+                pidx, bidx = table.probe_select(lk, lvalid)
+            else:
+                first = table.probe_first(lk, lvalid)
         with ctx.span("join.gather"):
             if kind == "inner":
                 return _combine(lb, rb, pidx, bidx, False)
@@ -854,9 +851,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         table = H.JoinTable(small, svalid)
     with ctx.span("join.probe"):
         if table.unique:
-            first = table.probe_first(big, bvalid)
-            bsel = mask_to_indices(first >= 0)
-            ssel = first.index_select(0, bsel.long())
+            bsel, ssel = table.probe_select(big, bvalid)
         else:
             bsel, ssel, _ = table.probe_pairs(big, bvalid)
     return (ssel, bsel) if big_right else (bsel, ssel)

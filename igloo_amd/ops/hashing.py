@@ -25,6 +25,8 @@ BLOOM_MIN_RATIO = 4        # ... used when probe rows >= ratio x build rows
 #: table (one random read per probe) whatever the build size: 2^26 slots is a
 #: 256 MB head array, small next to 288 GB of HBM
 DIRECT_JOIN_MAX_SPAN = 1 << 26
+#: first-match probes that only select rows use the two-pass hit-bit kernels
+PROBE_SELECT = os.environ.get("IGLOO_PROBE_SELECT", "1") == "1"
 
 
 def _next_pow2(x: int) -> int:
@@ -116,6 +118,36 @@ class JoinTable:
                      ptr(self.next), self.cap, self.kmin, self.direct, 0, ptr(first), ptr(build_matched), bits, bmask,
                      stream(pkeys))
         return first
+
+    def probe_select(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None, negate: bool = False,
+                     want_build: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """Probe rows with a match (``negate``: without one), in row order, and
+        for matches their (first) build row — what ``probe_first`` + compaction
+        give, in two passes that never write a per-row result (GPU)."""
+        pkeys = _keys_ok(pkeys)
+        m = pkeys.numel()
+        dev = pkeys.device
+        if not self.gpu or self.empty or m == 0 or not PROBE_SELECT:
+            first = self.probe_first(pkeys, pvalid)
+            sel = mask_to_indices(first < 0 if negate else first >= 0)
+            return sel, (first.index_select(0, sel.long()) if want_build and not negate else None)
+        N = launch("probe_hits")
+        st = stream(pkeys)
+        k64 = pkeys.dtype == torch.int64
+        tiles = N.probe_hit_tiles(m)
+        words = torch.empty(tiles * 128, dtype=torch.int64, device=dev)
+        tcount = torch.empty(tiles, dtype=torch.int64, device=dev)
+        bits, bmask = self._bloom(m)
+        N.probe_hits(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.cap, self.kmin,
+                     self.direct, bits, bmask, negate, ptr(words), ptr(tcount), st)
+        toff, total = exclusive_scan(tcount)
+        it = torch.int32 if m < INT32_MAX else torch.int64
+        pidx = torch.empty(total, dtype=it, device=dev)
+        bidx = torch.empty(total, dtype=torch.int32, device=dev) if want_build and not negate else None
+        if total:
+            N.probe_write(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.cap, self.kmin,
+                          self.direct, ptr(words), ptr(toff), ptr(pidx), it == torch.int64, ptr(bidx), st)
+        return pidx, bidx
 
     def probe_pairs(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
                     build_matched: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

@@ -11,6 +11,7 @@ from igloo_amd.ops import agg as A
 from igloo_amd.ops import hashing as H
 from igloo_amd.ops import misc as M
 from igloo_amd.ops import strings as S
+from igloo_amd.ops.select import mask_to_indices
 from igloo_amd.ops.gather import take_many
 from igloo_amd.ops.select import exclusive_scan, mask_to_indices
 
@@ -391,3 +392,29 @@ def test_key_histogram_and_small_span_group_ids(gpu_device):
         reps = dict(zip(kd.index_select(0, rep.long()).cpu().tolist(), rep.cpu().tolist()))
         for v, i in first.items():
             assert reps[v] == i
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_probe_select_vs_probe_first(gpu_device, direct):
+    """hashtable.hip probe_hits/probe_write (hit bits per 8192-row tile, then
+    ordered writes of hit rows) == probe_first + compaction, for matches and
+    misses (anti), with NULL probe keys and a partial last tile."""
+    g = _rng(31)
+    span = 50_000 if direct else 10**12
+    build = torch.from_numpy(np.unique(g.integers(0, span, 20_000)).astype(np.int64)).to(gpu_device)
+    m = 1_000_003
+    probe = torch.from_numpy(g.integers(0, span if direct else 10**12, m).astype(np.int64))
+    probe[::7] = build.cpu()[torch.randint(0, build.numel(), (len(probe[::7]),), generator=torch.Generator().manual_seed(1))]
+    pd = probe.to(gpu_device)
+    pvalid = torch.from_numpy(g.random(m) > 0.1).to(gpu_device)
+    t = H.JoinTable(build)
+    assert t.direct == direct and t.unique
+    first = t.probe_first(pd, pvalid)
+    for negate in (False, True):
+        want = mask_to_indices(first < 0 if negate else first >= 0)
+        pidx, bidx = t.probe_select(pd, pvalid, negate=negate)
+        assert torch.equal(pidx.cpu().long(), want.cpu().long())
+        if negate:
+            assert bidx is None
+        else:
+            assert torch.equal(bidx.cpu().long(), first.index_select(0, want.long()).cpu().long())
