@@ -233,7 +233,7 @@ PYBIND11_MODULE(_native, m) {
       f.cols[i].ptr = reinterpret_cast<const void*>(cols[i].first);
       f.cols[i].width = cols[i].second;
       const int64_t w = f.cols[i].width;  // signed 1/2/4/8-byte integer columns
-      if (!(w == 1 || w == 2 || w == 4 || w == 8) || (cols[i].first % w) != 0)
+      if (!(w == 1 || w == 2 || w == 4 || w == 8) || (cols[i].first % (w < 4 ? 4 : w)) != 0)
         throw std::runtime_error("fused scan: bad column width / alignment");
     }
     f.nterms = (int32_t)terms.size();

@@ -78,8 +78,8 @@ class Spec:
             x = x.to(torch.int16)   # the kernels sign-extend 1/2/4/8-byte words
         if x.dtype not in (torch.int8, torch.int16, torch.int32, torch.int64) or x.dim() != 1:
             raise Bail(f"column dtype {x.dtype}")
-        if not x.is_contiguous():
-            x = x.contiguous()
+        if not x.is_contiguous() or (x.element_size() < 4 and x.data_ptr() % 4):
+            x = x.clone(memory_format=torch.contiguous_format)   # sub-dword columns start 4-byte aligned (ff_load)
         key = id(c.data)
         if key not in self._idx:
             if len(self.cols) >= MAX_COLS:
