@@ -455,6 +455,18 @@ PYBIND11_MODULE(_native, m) {
     if (n > 0 && (!keys || !counts || span <= 0)) throw std::runtime_error("key_histogram: bad arguments");
     kern::key_histogram(P<const void>(keys), key64, P<const uint8_t>(valid), n, kmin, span, P<int32_t>(counts), S(s));
   });
+  m.def("key_histogram_buckets", [](int64_t span) { return kern::key_histogram_buckets(span); });
+  m.def("key_histogram_blocks", []() { return kern::key_histogram_blocks(); });
+  m.def("key_histogram_partitioned", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, int64_t kmin,
+                                        int64_t span, int phase, uintptr_t cnt, uintptr_t off, int64_t total,
+                                        uintptr_t part, uintptr_t counts, uintptr_t s) {
+    if (span <= 0 || span > (int64_t(1) << 27) || n >= (int64_t(1) << 31) || phase < 0 || phase > 2 || !keys ||
+        (phase == 0 && !cnt) || (phase >= 1 && (!off || !part)) || (phase == 2 && !counts))
+      throw std::runtime_error("key_histogram_partitioned: bad arguments");
+    kern::key_histogram_partitioned(P<const void>(keys), key64, P<const uint8_t>(valid), n, kmin, span, phase,
+                                    P<int32_t>(cnt), P<const int64_t>(off), total, P<uint16_t>(part),
+                                    P<int32_t>(counts), S(s));
+  });
   m.def("sorted_exists", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
                             int op, uintptr_t hit, uintptr_t s) {
     if (op < 0 || op > 5 || (ns > 0 && (!big2 || !small2 || !lo || !cnt || !hit)))

@@ -136,6 +136,14 @@ int agg_lds_max_groups(int nagg);
 // counts[k - kmin] += 1 per valid key in [kmin, kmin + span) (int32 counters, zeroed by the caller)
 void key_histogram(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t span,
                    int32_t* counts, hipStream_t stream);
+// radix-partitioned variant for large domains (span <= 2^27, n < 2^31): phase 0 per-(bucket, block)
+// counts -> cnt[buckets * blocks]; caller scans them into off; phase 1 scatters 16-bit low keys into
+// part[total]; phase 2 counts each bucket in LDS into counts[span]
+int key_histogram_buckets(int64_t span);
+int key_histogram_blocks();
+void key_histogram_partitioned(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin,
+                               int64_t span, int phase, int32_t* cnt, const int64_t* off, int64_t total,
+                               uint16_t* part, int32_t* counts, hipStream_t stream);
 void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream,
                 bool sorted_gids = false);
 

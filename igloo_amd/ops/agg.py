@@ -6,6 +6,7 @@ back as int64 when every group fits, else as an [g, 2] (lo, hi) tensor.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -155,8 +156,35 @@ def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torc
         return torch.bincount(k[ok], minlength=span)[:span]
     assert keys.dtype in (torch.int32, torch.int64) and span < 2**31
     keys = keys.contiguous()
+    n = keys.numel()
+    if HIST_PARTITIONED and n >= (1 << 22) and (1 << 16) <= span <= (1 << 27):
+        return _key_histogram_partitioned(keys, kmin, span, valid)
     counts = torch.zeros(span, dtype=torch.int32, device=keys.device)
     launch("key_histogram").key_histogram(ptr(keys), keys.dtype == torch.int64,
                                           ptr(valid.contiguous() if valid is not None else None), keys.numel(), kmin,
                                           span, ptr(counts), stream(keys))
+    return counts.to(torch.int64)
+
+
+HIST_PARTITIONED = os.environ.get("IGLOO_HIST_PARTITIONED", "1") == "1"
+
+
+def _key_histogram_partitioned(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torch.Tensor]):
+    """Radix-partitioned COUNT per key (csrc/kernels/agg.hip): bucket counts,
+    scan, 16-bit scatter, one LDS histogram per 8192-key bucket."""
+    from .select import exclusive_scan
+    N = launch("key_histogram_partitioned")
+    st = stream(keys)
+    dev = keys.device
+    n = keys.numel()
+    k64 = keys.dtype == torch.int64
+    vp = ptr(valid.contiguous() if valid is not None else None)
+    nbk, nblk = N.key_histogram_buckets(span), N.key_histogram_blocks()
+    cnt = torch.empty(nbk * nblk, dtype=torch.int32, device=dev)
+    N.key_histogram_partitioned(ptr(keys), k64, vp, n, kmin, span, 0, ptr(cnt), 0, 0, 0, 0, st)
+    off, total = exclusive_scan(cnt)
+    part = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
+    counts = torch.empty(span, dtype=torch.int32, device=dev)
+    N.key_histogram_partitioned(ptr(keys), k64, vp, n, kmin, span, 1, 0, ptr(off), total, ptr(part), 0, st)
+    N.key_histogram_partitioned(ptr(keys), k64, vp, n, kmin, span, 2, 0, ptr(off), total, ptr(part), ptr(counts), st)
     return counts.to(torch.int64)

@@ -379,6 +379,16 @@ def test_key_histogram_and_small_span_group_ids(gpu_device):
     ref = A.key_histogram(keys, 0, 4000, valid)
     got = A.key_histogram(keys.to(gpu_device), 0, 4000, valid.to(gpu_device))
     assert torch.equal(got.cpu(), ref)
+    # radix-partitioned path (n >= 2^22, span >= 2^16; span not a bucket multiple)
+    n2 = 5_000_000
+    for dt, span in ((np.int32, 300_001), (np.int64, 1_500_000)):
+        keys2 = torch.from_numpy(g.integers(-1000, span + 1000, n2).astype(dt))
+        valid2 = torch.from_numpy(g.random(n2) > 0.1)
+        ref2 = A.key_histogram(keys2, 7, span, valid2)
+        got2 = A.key_histogram(keys2.to(gpu_device), 7, span, valid2.to(gpu_device))
+        assert torch.equal(got2.cpu(), ref2)
+        got3 = A.key_histogram(keys2.to(gpu_device), 7, span, None)
+        assert torch.equal(got3.cpu(), A.key_histogram(keys2, 7, span, None))
     for span in (5, 700, 16000):
         k = torch.from_numpy(g.integers(100, 100 + span, n).astype(np.int64))
         gid, ng, rep = H.group_ids(k.to(gpu_device))
