@@ -14,6 +14,7 @@ import threading
 
 import torch
 
+from ..utils import faults as _faults
 from ..utils.errors import DeviceError
 
 _native = None
@@ -59,6 +60,8 @@ def ptr(t) -> int:
 def launch(name: str):
     """Record a native launch (cheap counter) and return the native module."""
     KERNEL_CALLS[name] += 1
+    if _faults.ACTIVE:
+        _faults.check("kernel_error", name)
     return native()
 
 

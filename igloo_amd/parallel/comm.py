@@ -20,6 +20,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..utils import faults
 from ..utils.errors import CommError
 from ..utils.log import get_logger
 
@@ -75,10 +76,14 @@ class Communicator:
         return torch.as_tensor(x, dtype=dtype, device=self.wire)
 
     def barrier(self):
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "barrier")
         if self.world_size > 1:
             dist.barrier(group=self.group)
 
     def allreduce_int(self, x: int) -> int:
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allreduce_int")
         if self.world_size == 1:
             return int(x)
         t = self._t([int(x)])
@@ -86,6 +91,8 @@ class Communicator:
         return int(t.item())
 
     def allreduce_ints(self, xs: Sequence[int]) -> List[int]:
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allreduce_ints")
         if self.world_size == 1:
             return [int(x) for x in xs]
         t = self._t([int(x) for x in xs])
@@ -93,6 +100,8 @@ class Communicator:
         return [int(v) for v in t.tolist()]
 
     def allreduce_max_float(self, x: float) -> float:
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allreduce_max_float")
         if self.world_size == 1:
             return float(x)
         t = self._t([float(x)], torch.float64)
@@ -101,6 +110,8 @@ class Communicator:
 
     def allreduce_max_tensor(self, t: torch.Tensor) -> torch.Tensor:
         """Element-wise max over ranks (in a 32-bit copy: portable across backends)."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allreduce_max_tensor")
         if self.world_size == 1:
             return t
         w = t.to(device=self.wire, dtype=torch.int32)
@@ -109,6 +120,8 @@ class Communicator:
 
     def allgather_ints(self, xs: Sequence[int]) -> List[List[int]]:
         """Every rank contributes len(xs) ints; returns [rank][i]."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allgather_ints")
         k = len(xs)
         if self.world_size == 1:
             return [list(map(int, xs))]
@@ -119,6 +132,8 @@ class Communicator:
         return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
 
     def allgather_object(self, obj) -> list:
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allgather_object")
         if self.world_size == 1:
             return [obj]
         out = [None] * self.world_size
@@ -128,6 +143,8 @@ class Communicator:
     def all_to_all_v(self, t: torch.Tensor, send_counts: Sequence[int],
                      recv_counts: Optional[Sequence[int]] = None) -> Tuple[torch.Tensor, List[int]]:
         """Rows of ``t`` grouped by destination (send_counts[r] rows to rank r)."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "all_to_all_v")
         W = self.world_size
         if W == 1:
             return t, [t.shape[0]]
@@ -148,6 +165,8 @@ class Communicator:
         return out.to(t.device), list(recv_counts)
 
     def all_to_all_counts(self, send_counts: Sequence[int]) -> List[int]:
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "all_to_all_counts")
         W = self.world_size
         s = self._t(list(send_counts))
         r = torch.empty(W, dtype=torch.int64, device=self.wire)
@@ -156,6 +175,8 @@ class Communicator:
 
     def all_gather_v(self, t: torch.Tensor, counts: Optional[List[int]] = None) -> Tuple[torch.Tensor, List[int]]:
         """Concatenate every rank's ``t`` (variable row counts) on every rank."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "all_gather_v")
         W = self.world_size
         if W == 1:
             return t, [t.shape[0]]
@@ -169,6 +190,8 @@ class Communicator:
         return out, counts
 
     def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "broadcast_tensor")
         if self.world_size > 1:
             w = t.to(self.wire)
             dist.broadcast(w, src, group=self.group)

@@ -28,7 +28,7 @@ from typing import Callable, Dict, Optional, Tuple
 import pyarrow as pa
 import pyarrow.flight as fl
 
-from ..utils.errors import IglooError, PlanError, SqlParseError, TableNotFound
+from ..utils.errors import CommError, DeviceError, IglooError, PlanError, SqlParseError, TableNotFound
 from ..utils.log import get_logger
 from . import protocol as P
 
@@ -111,6 +111,10 @@ class IglooFlightServer(fl.FlightServerBase):
         except (SqlParseError, PlanError, TableNotFound) as e:
             self.metrics["errors"] += 1
             raise ValueError(f"{type(e).__name__}: {e}") from None
+        except (DeviceError, CommError) as e:
+            # the worker group (GPU / collective), not the query, failed: retryable elsewhere
+            self.metrics["errors"] += 1
+            raise fl.FlightUnavailableError(f"{type(e).__name__}: {e}") from None
         except IglooError as e:
             self.metrics["errors"] += 1
             raise fl.FlightServerError(f"{type(e).__name__}: {e}") from None

@@ -30,6 +30,7 @@ from typing import Optional
 import pyarrow as pa
 import torch
 
+from ..utils import faults
 from ..utils.config import IglooConfig, load_config, register_config_tables
 from ..utils.log import get_logger
 from . import protocol as P
@@ -67,6 +68,9 @@ class WorkerGroup:
         return box[0]
 
     def run_spmd(self, sql: str) -> pa.Table:
+        if faults.ACTIVE:
+            faults.check("kill_worker")
+            faults.check("fail_query", sql)
         with self._lock:
             if self.world > 1:
                 self._bcast(("query", sql))
@@ -132,6 +136,8 @@ class WorkerGroup:
     def heartbeat_loop(self):
         from .client import IglooClient
         while not self._stop.wait(self.heartbeat_s):
+            if faults.fire("drop_heartbeat", self.id):
+                continue
             try:
                 with IglooClient(self.coordinator, self.token, timeout=5) as c:
                     r = c.heartbeat(P.HeartbeatInfo(self.id))
@@ -176,6 +182,8 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default=None)
     a = ap.parse_args(argv)
     cfg = load_config(a.config, {"worker_host": a.host, "worker_port": a.port, "device": a.device})
+    if cfg.fault:
+        faults.configure(cfg.fault)
     coord = a.coordinator or a.coordinator_pos or f"grpc://{cfg.coordinator_host}:{cfg.coordinator_port}"
     coord = coord.replace("http://", "grpc://")
     import igloo_amd as ig

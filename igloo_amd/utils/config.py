@@ -35,6 +35,7 @@ class IglooConfig:
     tables: Dict[str, Dict[str, Any]] = field(default_factory=dict)
     auth_token: Optional[str] = None
     log_level: str = "warning"
+    fault: Optional[str] = None   # fault-injection spec (utils/faults.py), e.g. "drop_heartbeat"
 
     def to_dict(self) -> dict:
         return asdict(self)

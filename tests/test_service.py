@@ -94,8 +94,10 @@ def test_protocol_any_roundtrip():
     assert P.unpack_any(b"SELECT 1") is None
 
 
-def _spawn_worker(coord, tag):
+def _spawn_worker(coord, tag, fault=None):
     env = dict(os.environ, PYTHONPATH=ROOT, IGLOO_HEARTBEAT_INTERVAL_S="0.3")
+    if fault:
+        env["IGLOO_FAULT"] = fault
     return subprocess.Popen([sys.executable, "-m", "igloo_amd.service.worker", "--coordinator", coord, "--port", "0",
                              "--tpch", "0.01", "--device", "cpu"], env=env, cwd=ROOT,
                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
@@ -126,6 +128,60 @@ def test_coordinator_routes_and_fails_over():
             time.sleep(2.5)  # heartbeat timeout -> eviction
             assert c.query(sql).to_pylist()[0]["n"] == n
             assert len(co.registry.alive()) <= 1
+    finally:
+        for p in ws:
+            p.kill()
+        co.shutdown()
+
+
+def test_fault_spec_and_local_hooks():
+    from igloo_amd.ops import _lib
+    from igloo_amd.parallel.comm import LocalComm
+    from igloo_amd.utils import faults
+    from igloo_amd.utils.errors import CommError, DeviceError
+    fs = faults.parse("drop_heartbeat; kernel_error@join_probe:1, comm_timeout@all_to_all_v:2")
+    assert [(f.kind, f.target, f.remaining) for f in fs] == [
+        ("drop_heartbeat", None, None), ("kernel_error", "join_probe", 1), ("comm_timeout", "all_to_all_v", 2)]
+    with pytest.raises(ValueError):
+        faults.parse("explode@x")
+    import torch
+    with faults.inject("kernel_error@join_probe:1;comm_timeout@all_to_all_v:2"):
+        with pytest.raises(DeviceError):
+            _lib.launch("join_probe")
+        assert faults.active()[0].remaining == 0   # count consumed: fires once
+        c = LocalComm("cpu")
+        t = torch.arange(4)
+        for _ in range(2):
+            with pytest.raises(CommError):
+                c.all_to_all_v(t, [4])
+        assert torch.equal(c.all_to_all_v(t, [4])[0], t)
+        c.all_gather_v(t)   # other collectives unaffected
+    assert not faults.ACTIVE
+
+
+def test_injected_faults_drive_eviction_and_retry():
+    """drop_heartbeat -> the reaper evicts a live worker; fail_query -> the
+    coordinator marks the failing group dead and reruns the query elsewhere."""
+    co = Coordinator(IglooConfig(coordinator_port=0, heartbeat_interval_s=0.3, heartbeat_timeout_s=1.5,
+                                 device="cpu")).start()
+    from igloo_amd.models.tpch import datagen
+    datagen.register(co.engine, 0.01)  # the coordinator plans schemas locally
+    ws = [_spawn_worker(co.address, 0, fault="fail_query@lineitem"), _spawn_worker(co.address, 1),
+          _spawn_worker(co.address, 2, fault="drop_heartbeat")]
+    try:
+        t0 = time.time()
+        while len(co.registry.snapshot()) < 3 and time.time() - t0 < 120:
+            time.sleep(0.2)
+        assert len(co.registry.snapshot()) == 3, [w.stdout.read1(4096) for w in ws if w.poll() is not None]
+        time.sleep(2.5)   # the heartbeat-dropping worker is evicted although its process lives
+        assert ws[2].poll() is None and len(co.registry.alive()) == 2
+        sql = "SELECT count(*) AS n FROM lineitem"
+        with IglooClient(co.address) as c:
+            for _ in range(2):   # least-loaded routing reaches the faulty group by the second query
+                assert c.query(sql).to_pylist()[0]["n"] == 59875
+        outcomes = [o for (_, _, _, o) in co.executor.log]
+        assert any(o.startswith("retry") for o in outcomes), co.executor.log
+        assert co.executor.log[-1][1] != "local" and len(co.registry.alive()) == 1
     finally:
         for p in ws:
             p.kill()
