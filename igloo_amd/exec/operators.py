@@ -227,6 +227,11 @@ class ScanExec(ExecNode):
             if todo:
                 with ctx.span("scan.filter_gather"):
                     for c, col in zip(todo, take_many([b.columns[c] for c in todo], idx)):
+                        if NDV_DERIVED and col.valid is None and not col.is_dict:
+                            try:   # filtered subset of a source column: its NDV derives from the source's
+                                col.data._igloo_base = (b.columns[c], b.num_rows)
+                            except (AttributeError, RuntimeError):
+                                pass
                         taken_by_name[name[c]] = col
             return Batch({c: taken_by_name[name[c]] for c in out_cids}, idx.numel(), b.dist)
         return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
@@ -1130,8 +1135,12 @@ class MultiJoinExec(ExecNode):
                     c = ctx.evaluator.column(e, b)
                     # resident table columns: the sketch of the same tensor is reused across queries
                     cached = getattr(c.data, "_igloo_ndv", None) if c.valid is None else None
+                base = getattr(c.data, "_igloo_base", None) if cached is None and ctx.world == 1 and \
+                    b.num_rows and c.valid is None else None
                 if cached is not None:
                     g = cached
+                elif base is not None:
+                    g = _derived_ndv(base, b.num_rows)
                 elif ctx.device.type == "cuda":
                     if b.num_rows:
                         c = ctx.evaluator.column(e, b)
@@ -1158,6 +1167,27 @@ class MultiJoinExec(ExecNode):
                         pass
             rel["ndv"][key] = max(g, 1)
         return rel["ndv"][key]
+
+
+NDV_DERIVED = os.environ.get("IGLOO_NDV_DERIVED", "1") == "1"
+
+
+def _derived_ndv(base, n: int) -> int:
+    """NDV of an n-row filtered subset of a source column with N rows and D
+    distinct values, by Cardenas' formula D * (1 - (1 - n/N)^(N/D)) (rows
+    selected independently of the key) — no pass over the subset. D comes
+    from one sketch of the source column, remembered on its tensor."""
+    col, N = base
+    D = getattr(col.data, "_igloo_ndv", None)
+    if D is None:
+        k, _ = group_key_tensor(col)
+        D = max(int(round(H.hll_estimate(H.hll_sketch(k)))) if k.is_cuda else H.ndv(k), 1)
+        try:
+            col.data._igloo_ndv = D
+        except (AttributeError, RuntimeError):
+            pass
+    sel = min(n / max(N, 1), 1.0)
+    return max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / D))))))
 
 
 def _global_rows(b: Batch, ctx) -> int:
