@@ -168,7 +168,19 @@ class ExecNode:
 _CID = re.compile(r"#\d+")
 
 
+def _tag_base(col: Column, src: Column, n_src: int):
+    if NDV_DERIVED and col.valid is None and not col.is_dict:
+        try:   # filtered subset of a source column: its NDV derives from the source's
+            col.data._igloo_base = (src, n_src)
+        except (AttributeError, RuntimeError):
+            pass
+
+
 class ScanExec(ExecNode):
+    #: set by a parent multi-way join: a filtered scan may hand over its rows
+    #: as indices into the source (LateBatch) instead of gathered columns
+    late_ok = False
+
     def __init__(self, logical: L.Scan):
         self.logical = logical
         self.children = []
@@ -223,15 +235,16 @@ class ScanExec(ExecNode):
                     idx = mask_to_indices(m)
                 hit = ctx.scan_cache[key] = (idx, {})
             idx, taken_by_name = hit
+            if self.late_ok and LATE_SCAN and ctx.world == 1 and ctx.device.type == "cuda":
+                # index form: the join gathers its key columns now and payload
+                # columns only for the rows that survive it
+                src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
+                return _LazyScanBatch(src, idx, name, taken_by_name, ctx)
             todo = [c for c in out_cids if name[c] not in taken_by_name]
             if todo:
                 with ctx.span("scan.filter_gather"):
                     for c, col in zip(todo, take_many([b.columns[c] for c in todo], idx)):
-                        if NDV_DERIVED and col.valid is None and not col.is_dict:
-                            try:   # filtered subset of a source column: its NDV derives from the source's
-                                col.data._igloo_base = (b.columns[c], b.num_rows)
-                            except (AttributeError, RuntimeError):
-                                pass
+                        _tag_base(col, b.columns[c], b.num_rows)
                         taken_by_name[name[c]] = col
             return Batch({c: taken_by_name[name[c]] for c in out_cids}, idx.numel(), b.dist)
         return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
@@ -955,7 +968,12 @@ class LateBatch(Batch):
         c = self._cache.get(cid)
         if c is None:
             bb, idx = self.parts[self.owner[cid]]
-            c = bb.columns[cid] if idx is None else take(bb.columns[cid], idx)
+            if idx is None:
+                c = bb.columns[cid]
+            elif isinstance(bb, _LazyScanBatch):
+                c = bb.take_rows([cid], idx)[0]
+            else:
+                c = take(bb.columns[cid], idx)
             self._cache[cid] = c
         return c
 
@@ -973,8 +991,85 @@ class LateBatch(Batch):
             else:
                 pending = [k for k in keys if k not in self._cache]
                 out.update({k: self._cache[k] for k in keys if k in self._cache})
-                out.update(zip(pending, take_many([bb.columns[k] for k in pending], idx)))
+                if isinstance(bb, _LazyScanBatch):
+                    out.update(zip(pending, bb.take_rows(pending, idx)))
+                else:
+                    out.update(zip(pending, take_many([bb.columns[k] for k in pending], idx)))
         return Batch(out, self._n, self.dist)
+
+
+LATE_SCAN = os.environ.get("IGLOO_LATE_SCAN", "1") == "1"
+
+
+class _ScanColumns:
+    """Mapping view of a _LazyScanBatch: gathers a column on first read."""
+
+    def __init__(self, b: "_LazyScanBatch"):
+        self._b = b
+
+    def __getitem__(self, cid):
+        return self._b.gather(cid)
+
+    def get(self, cid, default=None):
+        return self._b.gather(cid) if cid in self._b.src.columns else default
+
+    def __contains__(self, cid):
+        return cid in self._b.src.columns
+
+    def __iter__(self):
+        return iter(self._b.src.columns)
+
+    def __len__(self):
+        return len(self._b.src.columns)
+
+    def keys(self):
+        return list(self._b.src.columns)
+
+    def values(self):
+        return [self._b.gather(c) for c in self._b.src.columns]
+
+    def items(self):
+        return [(c, self._b.gather(c)) for c in self._b.src.columns]
+
+
+class _LazyScanBatch(Batch):
+    """A filtered scan whose columns are gathered on first read (shared with
+    other scans of the same table under the same filter in the query). A
+    LateBatch over it gathers never-read payload columns straight from the
+    source through the composed row index — only for rows that survive the
+    join — while its own row indices stay those of the filtered scan."""
+
+    def __init__(self, src: Batch, idx: torch.Tensor, names: dict, shared: dict, ctx):  # noqa: D401
+        self.src, self.idx, self._names, self._shared, self._ctx = src, idx, names, shared, ctx
+        self.num_rows = idx.numel()
+        self.dist = src.dist
+        self.out_dist = None
+        self.columns = _ScanColumns(self)
+
+    def has(self, cid) -> bool:
+        return self._names[cid] in self._shared
+
+    def gather(self, cid) -> Column:
+        c = self._shared.get(self._names[cid])
+        if c is None:
+            with self._ctx.span("scan.filter_gather"):
+                c = take(self.src.columns[cid], self.idx)
+            _tag_base(c, self.src.columns[cid], self.src.num_rows)
+            self._shared[self._names[cid]] = c
+        return c
+
+    def take_rows(self, cids, rows: torch.Tensor) -> List[Column]:
+        """Columns at filtered-scan rows ``rows``; unread ones via the source."""
+        out, pend = {}, []
+        for c in cids:
+            if self.has(c):
+                out[c] = take(self._shared[self._names[c]], rows)
+            else:
+                pend.append(c)
+        if pend:
+            comp = self.idx.index_select(0, rows.long())
+            out.update(zip(pend, take_many([self.src.columns[c] for c in pend], comp)))
+        return [out[c] for c in cids]
 
 
 #: a multi-way join returns its LateBatch (row indices into the inputs) to the
@@ -991,6 +1086,9 @@ class MultiJoinExec(ExecNode):
     def __init__(self, logical: L.MultiJoin, children: List[ExecNode]):
         self.logical = logical
         self.children = children
+        for ch in children[:len(logical.children)]:
+            if isinstance(ch, ScanExec):
+                ch.late_ok = True
         self.order_log: List[str] = []
 
     #: a semi join is applied to its input before the join when the subquery
@@ -1003,6 +1101,10 @@ class MultiJoinExec(ExecNode):
         return f"{len(lg.children)} inputs, conds=[{', '.join(c.sql() for c in lg.conds)}]{extra}"
 
     def _semi(self, lb: Batch, rb: Batch, sp, ctx) -> Batch:
+        if isinstance(lb, LateBatch):
+            lb = lb.materialize()
+        elif isinstance(lb, _LazyScanBatch):
+            lb = Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
         if ctx.world > 1:
             from ..parallel.exchange import prepare_join
             j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
