@@ -999,6 +999,7 @@ class LateBatch(Batch):
 
 
 LATE_SCAN = os.environ.get("IGLOO_LATE_SCAN", "1") == "1"
+PRUNE_PARTS = os.environ.get("IGLOO_PRUNE_PARTS", "1") == "1"
 
 
 class _ScanColumns:
@@ -1086,6 +1087,7 @@ class MultiJoinExec(ExecNode):
     def __init__(self, logical: L.MultiJoin, children: List[ExecNode]):
         self.logical = logical
         self.children = children
+        self.required = None   # column ids the parent reads (set by the planner when known)
         for ch in children[:len(logical.children)]:
             if isinstance(ch, ScanExec):
                 ch.late_ok = True
@@ -1174,6 +1176,8 @@ class MultiJoinExec(ExecNode):
                 else:
                     out = _nested_loop(la, lb_, "inner", and_all(resid), ctx)
             out.dist = out_dist
+            if self.required is not None and isinstance(out, LateBatch) and PRUNE_PARTS:
+                out = self._prune(out, conds, deferred)
             self.order_log.append(f"{a['name']} ⋈ {b['name']} -> {out.num_rows}")
             # key NDVs carry over (capped by the output size) instead of re-sketching intermediates
             cap = _global_rows(out, ctx)   # global: every rank must derive the same estimates / join order
@@ -1193,6 +1197,25 @@ class MultiJoinExec(ExecNode):
         for sp, rb in deferred:
             b = self._semi(b, rb, sp, ctx)
         return b
+
+    def _prune(self, out: "LateBatch", conds, deferred) -> "LateBatch":
+        """Drop index parts none of whose columns is read any more (by the
+        parent, a remaining join condition or a deferred semi join): later
+        steps then compose fewer row-index vectors."""
+        need = set(self.required)
+        for c in conds:
+            need |= col_refs(c)
+        for sp, _ in deferred:
+            for x, _y in sp.on:
+                need |= col_refs(x)
+            if sp.residual is not None:
+                need |= col_refs(sp.residual)
+        keep = [(bb, idx) for bb, idx in out.parts if any(c in need for c in bb.columns)] or out.parts[:1]
+        if len(keep) == len(out.parts):
+            return out
+        pruned = LateBatch(keep, out.num_rows, out.dist)
+        pruned._cache = {k: v for k, v in out._cache.items() if k in pruned.owner}
+        return pruned
 
     def _late_join(self, la: Batch, lb: Batch, on, residual, ctx) -> "LateBatch":
         """Inner join producing index pairs over the inputs' rows (no payload gather)."""

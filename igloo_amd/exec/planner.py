@@ -9,9 +9,17 @@ from __future__ import annotations
 
 from ..columnar import Batch
 from ..sql import logical as L
+from ..sql.expr import col_refs, has_subquery
 from ..utils.errors import NotSupported
 from .operators import (ExecContext, ExecNode, FilterExec, FragmentInputExec, HashAggExec, HashJoinExec, LimitExec,
                         MultiJoinExec, ProjectExec, ScanExec, SortExec, UnionExec, ValuesExec)
+
+
+def _require(child: ExecNode, exprs) -> None:
+    """Tell a multi-way join which of its columns the parent reads, so index
+    parts no remaining condition or output needs stop being carried."""
+    if isinstance(child, MultiJoinExec) and not any(has_subquery(e) for e in exprs):
+        child.required = set().union(*[col_refs(e) for e in exprs]) if exprs else set()
 
 
 def create_physical_plan(p: L.Plan) -> ExecNode:
@@ -22,13 +30,17 @@ def create_physical_plan(p: L.Plan) -> ExecNode:
     if isinstance(p, L.Filter):
         return FilterExec(p, create_physical_plan(p.input))
     if isinstance(p, L.Project):
-        return ProjectExec(p, create_physical_plan(p.input))
+        node = ProjectExec(p, create_physical_plan(p.input))
+        _require(node.children[0], [e for _, e in p.exprs])
+        return node
     if isinstance(p, L.Join):
         return HashJoinExec(p, create_physical_plan(p.left), create_physical_plan(p.right))
     if isinstance(p, L.MultiJoin):
         return MultiJoinExec(p, [create_physical_plan(c) for c in p.inputs])
     if isinstance(p, L.Aggregate):
-        return HashAggExec(p, create_physical_plan(p.input))
+        node = HashAggExec(p, create_physical_plan(p.input))
+        _require(node.children[0], [e for _, e in p.groups] + [a for _, a in p.aggs])
+        return node
     if isinstance(p, L.Sort):
         return SortExec(p, create_physical_plan(p.input))
     if isinstance(p, L.Limit):
