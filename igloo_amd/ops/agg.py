@@ -171,7 +171,7 @@ HIST_PARTITIONED = os.environ.get("IGLOO_HIST_PARTITIONED", "1") == "1"
 
 def _key_histogram_partitioned(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torch.Tensor]):
     """Radix-partitioned COUNT per key (csrc/kernels/agg.hip): bucket counts,
-    scan, 16-bit scatter, one LDS histogram per 8192-key bucket."""
+    scan, 16-bit scatter, one LDS histogram per 16384-key bucket."""
     from .select import exclusive_scan
     N = launch("key_histogram_partitioned")
     st = stream(keys)
