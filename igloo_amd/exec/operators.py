@@ -34,7 +34,7 @@ from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
-from ..ops._lib import launch, ptr, stream
+from ..ops._lib import launch, ptr, stream, to_host_int
 from ..ops.gather import take, take_many
 from ..ops.select import mask_to_indices
 from ..sql import logical as L
@@ -846,6 +846,18 @@ def concat_columns(cols: List[Column]) -> Column:
 
 
 # ====================================================================== multi join
+def _resident_ndv(t: torch.Tensor) -> int:
+    """NDV of a resident key column (HyperLogLog, remembered on the tensor)."""
+    d = getattr(t, "_igloo_ndv", None)
+    if d is None:
+        d = max(1, int(round(H.hll_estimate(H.hll_sketch(t)))))
+        try:
+            t._igloo_ndv = d
+        except (AttributeError, RuntimeError):
+            pass
+    return d
+
+
 def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor]:
     """(left row, right row) index pairs of an inner equi-join on packed keys:
     binary search into a sorted big side, else hash build on the smaller side
@@ -864,6 +876,26 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         with ctx.span("join.sorted_expand"):
             sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
+    if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
+            and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
+            and small.numel() * (big.numel() / _resident_ndv(big)) * PERM_INDEX_MAX_FRAC <= big.numel():
+        # unsorted resident column, much smaller other side: search its
+        # secondary index and touch only the matching rows
+        skeys, perm = H.perm_index(big)
+        with ctx.span("join.index_search"):
+            lo, cnt = H.sorted_ranges(skeys, small, svalid)
+            total = to_host_int(cnt.sum())
+        # the index hands out rows grouped by key, i.e. in random row order:
+        # for a large result the ordered hash probe output gathers (and
+        # probes later sorted joins) far more cheaply, so the index only
+        # serves results below 1/PERM_INDEX_MAX_FRAC of the column
+        if total * PERM_INDEX_MAX_FRAC <= big.numel():
+            with ctx.span("join.index_expand"):
+                sidx, pos = H.expand_ranges(lo, cnt, big.numel())
+                bidx = perm.index_select(0, pos.long())
+                if bidx.dtype != sidx.dtype:
+                    bidx = bidx.to(sidx.dtype)
+            return (sidx, bidx) if big_right else (bidx, sidx)
     # hash: build on the smaller side, probe with the bigger
     with ctx.span("join.build"):
         table = H.JoinTable(small, svalid)
@@ -874,6 +906,12 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
             bsel, ssel, _ = table.probe_pairs(big, bvalid)
     return (ssel, bsel) if big_right else (bsel, ssel)
 
+
+#: join a resident unsorted key column through its secondary index when the
+#: other side has at most 1/PERM_INDEX_RATIO of its rows
+PERM_INDEX = os.environ.get("IGLOO_PERM_INDEX", "1") == "1"
+PERM_INDEX_RATIO = int(os.environ.get("IGLOO_PERM_INDEX_RATIO", "32"))
+PERM_INDEX_MAX_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_MAX_FRAC", "20"))
 
 _INT_KEYS = ("int32", "int64")
 TWO_KEY_SORTED = os.environ.get("IGLOO_TWO_KEY_SORTED", "1") == "1"

@@ -311,6 +311,26 @@ def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Ten
     return lo, cnt
 
 
+def perm_index(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Secondary index of an unsorted resident key column: (keys in sorted
+    order, int32 row permutation), built once per column tensor (a stable
+    device radix sort) and kept with it like the other derived structures —
+    a join with a much smaller side then reads only the matching ranges
+    instead of probing every row of the column."""
+    hit = getattr(keys, "_igloo_perm", None)
+    if hit is not None:
+        return hit
+    sk, perm = torch.sort(keys, stable=True)
+    out = (sk, perm.to(torch.int32) if keys.numel() < INT32_MAX else perm)
+    del perm
+    try:
+        sk._igloo_sorted = True
+        keys._igloo_perm = out
+    except (AttributeError, RuntimeError):
+        pass
+    return out
+
+
 def expand_ranges(lo: torch.Tensor, cnt: torch.Tensor, big_n: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """All pairs (s, lo[s] + k), k < cnt[s], grouped by s (int32 when they fit)."""
     ns = lo.numel()

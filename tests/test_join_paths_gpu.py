@@ -47,9 +47,13 @@ def _norm(t):
     return sorted((tuple((k, v) for k, v in sorted(r.items())) for r in t.to_pylist()), key=repr)
 
 
-@pytest.mark.parametrize("sorted_big", [True, False])
+@pytest.mark.parametrize("sorted_big,perm", [(True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("qi", range(len(QUERIES)))
-def test_join_paths_match_cpu(gpu_device, monkeypatch, sorted_big, qi):
+def test_join_paths_match_cpu(gpu_device, monkeypatch, sorted_big, perm, qi):
+    """perm: the unsorted resident big side is joined through its secondary
+    (sorted permutation) index instead of a hash probe."""
+    monkeypatch.setattr(O, "PERM_INDEX", perm)
+    monkeypatch.setattr(O, "PERM_INDEX_MAX_FRAC", 1)
     monkeypatch.setattr(O, "SORTED_JOIN_MIN_ROWS", 1000)
     monkeypatch.setattr(H, "SORTED_CHECK_ROWS", 1000)
     monkeypatch.setattr(H, "BLOOM_MIN_RATIO", 2)
