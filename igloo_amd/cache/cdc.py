@@ -20,7 +20,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
-from ..catalog import TableSource
+from ..catalog import TableSource, _mark_resident
 from ..columnar import Batch
 from ..utils.log import get_logger
 from .tiered import TieredCache
@@ -43,6 +43,7 @@ class CdcManager:
         self._lock = threading.RLock()
         self._versions: Dict[str, Any] = {}
         self._probes: Dict[str, Callable[[], Any]] = {}
+        self._last_poll: Dict[str, float] = {}
         self._subs: List[Callable[[ChangeEvent], None]] = []
         self.events: List[ChangeEvent] = []
         self._stop = threading.Event()
@@ -50,10 +51,17 @@ class CdcManager:
 
     # ---------------------------------------------------------- registration
     def track(self, table: str, probe: Optional[Callable[[], Any]] = None, version: Any = 0):
+        """Start tracking ``table`` (re-registering a name resets it and drops
+        its cache entries)."""
         with self._lock:
+            known = table in self._versions
             self._versions[table] = probe() if probe is not None else version
+            self._probes.pop(table, None)
             if probe is not None:
                 self._probes[table] = probe
+                self._last_poll[table] = time.monotonic()
+        if known:
+            self._invalidate(table)
 
     def version(self, table: str) -> Any:
         with self._lock:
@@ -72,6 +80,27 @@ class CdcManager:
         self._invalidate(ev.table)
         for s in self._subs:
             s(ev)
+
+    def maybe_poll(self, table: str, min_interval_s: float = 1.0) -> bool:
+        """Poll one table's version probe unless it ran within ``min_interval_s``;
+        True when the version changed (its cache entries are then invalid)."""
+        probe = self._probes.get(table)
+        if probe is None:
+            return False
+        now = time.monotonic()
+        with self._lock:
+            if now - self._last_poll.get(table, -1e18) < min_interval_s:
+                return False
+            self._last_poll[table] = now
+        try:
+            v = probe()
+        except Exception as e:  # noqa: BLE001 - a failing probe keeps the cached data
+            log.warning("cdc probe for %s failed: %s", table, e)
+            return False
+        if v != self._versions.get(table):
+            self.apply_event(ChangeEvent(table, "snapshot", v))
+            return True
+        return False
 
     def poll(self) -> List[str]:
         """Re-run every version probe; returns tables whose version changed."""
@@ -110,18 +139,44 @@ class CdcManager:
 
 
 class CachedTable(TableSource):
-    """Serve scans of ``source`` from the HBM cache tier, keyed by the CDC version."""
+    """Serve scans of ``source`` from the cache tier, keyed by the CDC version.
 
-    def __init__(self, name: str, source: TableSource, cache: TieredCache, cdc: Optional[CdcManager] = None):
+    Every external source the engine registers (Parquet, Iceberg, CSV,
+    Postgres, MySQL) is wrapped in one: the first scan of a column reads it
+    from the source (GPU Parquet / CSV decode, wire protocols) into HBM and
+    later scans hand out the resident column. The column's version comes from
+    the table's CDC probe (file set + mtimes, Iceberg snapshot id, Postgres
+    ``version_sql``), polled at most every ``poll_interval_s``; a new version
+    invalidates the table's entries. HBM / host / disk byte budgets are the
+    TieredCache's (config ``cache_hbm_gb`` / ``cache_host_gb`` / ``cache_dir``).
+    """
+
+    #: cached scans hand out whole resident columns (no statistics pruning)
+    prunes = False
+    cacheable = False
+
+    def __init__(self, name: str, source: TableSource, cache: TieredCache, cdc: Optional[CdcManager] = None,
+                 poll_interval_s: Optional[float] = None):
         self.name = name
         self.source = source
         self.cache = cache
         self.cdc = cdc
+        # bounded staleness: file-system probes (stat of every file) run at most
+        # once a second; database probes (``version_sql``) on every scan
+        self.poll_interval_s = poll_interval_s if poll_interval_s is not None else \
+            getattr(source, "cdc_poll_s", 1.0)
         self.partitioned_by = getattr(source, "partitioned_by", None)
         self.replicated = getattr(source, "replicated", False)
-        if cdc is not None and cdc.version(name) is None:
-            probe = (lambda s=source: getattr(s, "version", None)) if hasattr(source, "version") else None
+        self.hits = self.misses = 0
+        if cdc is not None:
+            probe = (lambda s=source: getattr(s, "version", None)) if hasattr(type(source), "version") else None
             cdc.track(name, probe)
+
+    def __getattr__(self, item):
+        # connector-specific attributes (last_gpu_stats, files, ...) of the wrapped source
+        if item == "source":
+            raise AttributeError(item)
+        return getattr(self.source, item)
 
     def schema(self):
         return self.source.schema()
@@ -129,21 +184,39 @@ class CachedTable(TableSource):
     def num_rows(self):
         return self.source.num_rows()
 
+    def _key(self, c: str, ctx) -> str:
+        rank, world = 0, 1
+        if ctx is not None and ctx.comm is not None:
+            rank, world = ctx.comm.rank, ctx.comm.world_size
+        dev = str(ctx.device) if ctx is not None else "cpu"
+        return f"{self.name}/{rank}of{world}/{dev}/{c}"
+
     def scan(self, columns: Sequence[str], ctx) -> Batch:
-        ver = self.cdc.version(self.name) if self.cdc is not None else None
-        rank = ctx.comm.rank if ctx is not None and ctx.comm is not None else 0
+        ver = None
+        if self.cdc is not None:
+            self.cdc.maybe_poll(self.name, self.poll_interval_s)
+            ver = self.cdc.version(self.name)
         out, n, missing = {}, None, []
         for c in columns:
-            hit = self.cache.get(f"{self.name}/{rank}/{c}", ver)
+            hit = self.cache.get(self._key(c, ctx), ver)
             if hit is None:
                 missing.append(c)
             else:
                 out[c] = hit.columns[c]
                 n = hit.num_rows
         if missing:
+            self.misses += len(missing)
             b = self.source.scan(missing, ctx)
             for c in missing:
-                self.cache.put(f"{self.name}/{rank}/{c}", Batch({c: b.columns[c]}, b.num_rows), ver)
-                out[c] = b.columns[c]
+                col = b.columns[c]
+                _mark_resident(col)
+                self.cache.put(self._key(c, ctx), Batch({c: col}, b.num_rows), ver)
+                out[c] = col
             n = b.num_rows
-        return Batch({c: out[c] for c in columns}, n if n is not None else 0)
+        self.hits += len(columns) - len(missing)
+        if n is None:
+            n = self.source.num_rows() or 0
+        return Batch({c: out[c] for c in columns}, n)
+
+    def evict(self) -> int:
+        return self.cache.invalidate(f"{self.name}/")

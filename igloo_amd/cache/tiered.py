@@ -29,6 +29,7 @@ import torch
 from ..columnar import Batch, Column
 from ..utils.errors import IglooError
 from ..utils.log import get_logger
+from ..utils.memory import batch_nbytes
 
 log = get_logger("cache")
 GiB = 1 << 30
@@ -49,7 +50,9 @@ Value = Union[List[pa.RecordBatch], pa.Table, Batch]
 
 def _nbytes(v) -> int:
     if isinstance(v, Batch):
-        return v.nbytes
+        # device columns are charged with their derived structures (narrow
+        # copies, secondary / range indexes) — utils/memory.py
+        return batch_nbytes(v.columns.values())
     if isinstance(v, pa.Table):
         return v.nbytes
     if isinstance(v, list):
@@ -82,7 +85,16 @@ class TieredCache:
 
     # ---------------------------------------------------------------- sizes
     def _used(self, tier) -> int:
+        if tier is self._hbm:
+            # derived structures attach to resident columns after ``put``:
+            # re-measure device entries every time
+            return sum(_nbytes(e[0]) for e in tier.values())
         return sum(e[2] for e in tier.values())
+
+    def enforce(self) -> None:
+        """Re-apply the byte budgets (after queries grew derived structures)."""
+        with self._lock:
+            self._enforce()
 
     @property
     def hbm_used(self) -> int:
@@ -174,8 +186,10 @@ class TieredCache:
         cfg = self.config
         while self._hbm and self._used(self._hbm) > cfg.hbm_bytes:
             k, (v, ver, nb) = self._hbm.popitem(last=False)
-            self._host[k] = (v.to_arrow(), ver, nb, "batch")
+            t = v.to_arrow()
+            self._host[k] = (t, ver, t.nbytes, "batch")
             self.stats["evictions"] += 1
+            log.info("cache: demoted %s from HBM to host (%d bytes)", k, nb)
         while self._host and self._used(self._host) > cfg.host_bytes:
             k, (t, ver, nb, kind) = self._host.popitem(last=False)
             if self._dir:

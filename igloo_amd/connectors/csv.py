@@ -36,6 +36,8 @@ FULL_INFER_BYTES = 64 << 20
 
 
 class CsvTable(TableSource):
+    cacheable = True   # resident copies live in the engine's cache tier
+
     def __init__(self, path: str, schema: Optional[List[Field]] = None, has_header: bool = True,
                  delimiter: str = ","):
         self.path = path
@@ -43,7 +45,6 @@ class CsvTable(TableSource):
         self.delimiter = delimiter
         self._schema = schema
         self._table: Optional[pa.Table] = None
-        self._resident = {}
         self._gpu_rows: Optional[int] = None
         self.last_scan = ""   # "gpu" | "host" (| "host: <reason>")
 
@@ -127,12 +128,25 @@ class CsvTable(TableSource):
             self._gpu_rows = len(next(iter(cols.values())))
         return cols
 
+    @property
+    def version(self):
+        """CDC probe: the file's mtime and size (a rewrite drops cached columns)."""
+        try:
+            st = os.stat(self.path)
+        except OSError:
+            return None
+        if self._table is not None and getattr(self, "_ver", None) not in (None, (st.st_mtime_ns, st.st_size)):
+            self._table = None   # host copy of the old contents
+        self._ver = (st.st_mtime_ns, st.st_size)
+        return self._ver
+
     def scan(self, columns: Sequence[str], ctx) -> Batch:
         device = ctx.device if ctx is not None else torch.device("cpu")
         rank, world = 0, 1
         if ctx is not None and ctx.comm is not None:
             rank, world = ctx.comm.rank, ctx.comm.world_size
-        missing = [c for c in columns if (c, str(device), rank, world) not in self._resident]
+        out = {}
+        missing = list(columns)
         if missing and device.type == "cuda" and GPU_PARSE:
             cols = self._scan_gpu(missing, device)
             if cols is not None:
@@ -146,7 +160,7 @@ class CsvTable(TableSource):
                     if world > 1:
                         from ..ops.gather import take
                         col = take(col, torch.arange(lo, hi, dtype=torch.int64, device=device))
-                    self._resident[(c, str(device), rank, world)] = col
+                    out[c] = col
                 missing = []
         if missing:
             t = self._load()
@@ -155,10 +169,8 @@ class CsvTable(TableSource):
                 t = t.slice(rank * per, per)
             types = {f.name: f.dtype for f in self.schema()}
             for c in missing:
-                self._resident[(c, str(device), rank, world)] = Column.from_arrow(t.column(c), device=device,
-                                                                                 dtype=types[c])
+                out[c] = Column.from_arrow(t.column(c), device=device, dtype=types[c])
             if not self.last_scan.startswith("host"):
                 self.last_scan = "host"
-        out = {c: self._resident[(c, str(device), rank, world)] for c in columns}
         n = len(next(iter(out.values()))) if out else self.num_rows()
-        return Batch(out, n)
+        return Batch({c: out[c] for c in columns}, n)

@@ -92,8 +92,15 @@ def snapshot_files(table_path: str, meta: dict, snapshot_id: Optional[int] = Non
 
 
 class IcebergTable(TableSource):
+    cacheable = True   # resident copies live in the engine's cache tier, keyed by the snapshot id
+
     def __init__(self, path: str, snapshot_id: Optional[int] = None):
         self.path = path
+        self._pinned = snapshot_id
+        self._load(snapshot_id)
+
+    def _load(self, snapshot_id: Optional[int]):
+        path = self.path
         self.metadata = None
         files = None
         try:
@@ -119,14 +126,28 @@ class IcebergTable(TableSource):
     def num_rows(self) -> int:
         return self._inner.num_rows() if self._inner else 0
 
-    def scan(self, columns: Sequence[str], ctx) -> Batch:
+    prunes = True
+
+    def scan(self, columns: Sequence[str], ctx, filters=None) -> Batch:
         if self._inner is None:
             raise IoError(f"Iceberg table {self.path} has no data files")
-        return self._inner.scan(columns, ctx)
+        return self._inner.scan(columns, ctx, filters=filters)
 
     @property
     def version(self):
-        return self.snapshot_id
+        """CDC probe: the current snapshot id (re-read from the metadata, so a
+        commit — new vN.metadata.json + version hint — is seen); without
+        metadata the data files' mtimes."""
+        if self._pinned is None:
+            try:
+                cur = read_metadata(self.path).get("current-snapshot-id")
+            except (OSError, ValueError, json.JSONDecodeError):
+                cur = None
+            if cur is not None and cur != self.snapshot_id:
+                self._load(None)
+        if self.snapshot_id is not None:
+            return self.snapshot_id
+        return self._inner.version if self._inner is not None else None
 
 
 # ----------------------------------------------------------------- writing

@@ -243,14 +243,24 @@ def _convert(vals: List[Optional[bytes]], t: T.DataType) -> pa.Array:
 
 class MySqlTable(TableSource):
     replicated = True  # see PostgresTable
+    cacheable = True   # resident copies live in the engine's cache tier
+    cdc_poll_s = 0.0   # the version query runs before every scan
 
-    def __init__(self, dsn: str, table: str, query: Optional[str] = None):
+    def __init__(self, dsn: str, table: str, query: Optional[str] = None, version_sql: Optional[str] = None):
         self.dsn = dsn
         self.table = table
         self.base = query or f"SELECT * FROM {table}"
+        self.version_sql = version_sql
         self._conn = None
         self._fields = None
-        self._resident: Dict[tuple, Column] = {}
+
+    @property
+    def version(self):
+        """CDC probe (e.g. ``SELECT max(updated_at) FROM t``); None = never changes."""
+        if not self.version_sql:
+            return None
+        _, rows = self.conn().query(self.version_sql)
+        return rows[0][0] if rows else None
 
     def conn(self) -> MySqlConnection:
         if self._conn is None:
@@ -277,12 +287,11 @@ class MySqlTable(TableSource):
     def scan(self, columns: Sequence[str], ctx) -> Batch:
         import torch
         device = ctx.device if ctx is not None else torch.device("cpu")
-        missing = [c for c in columns if (c, str(device)) not in self._resident]
-        if missing:
-            t = self.read(missing)
+        out = {}
+        if columns:
+            t = self.read(columns)
             types = {f.name: f.dtype for f in self.schema()}
-            for c in missing:
-                self._resident[(c, str(device))] = Column.from_arrow(t.column(c), device=device, dtype=types[c])
-        out = {c: self._resident[(c, str(device))] for c in columns}
+            for c in columns:
+                out[c] = Column.from_arrow(t.column(c), device=device, dtype=types[c])
         n = len(next(iter(out.values()))) if out else self.num_rows()
         return Batch(out, n)

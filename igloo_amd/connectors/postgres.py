@@ -257,6 +257,9 @@ class PostgresTable(TableSource):
     # every SPMD rank reads the whole (small, dimension-like) table: the planner
     # treats it as replicated, so joins against partitioned facts need no shuffle
     replicated = True
+    # resident copies live in the engine's cache tier (cache/cdc.py), keyed by ``version``
+    cacheable = True
+    cdc_poll_s = 0.0   # the version query runs before every scan
 
     def __init__(self, dsn: str, table: str, query: Optional[str] = None, version_sql: Optional[str] = None):
         self.dsn = dsn
@@ -265,8 +268,6 @@ class PostgresTable(TableSource):
         self.version_sql = version_sql
         self._conn: Optional[PgConnection] = None
         self._fields: Optional[List[Field]] = None
-        self._resident: Dict[tuple, Column] = {}
-        self._ver = None
 
     def conn(self) -> PgConnection:
         if self._conn is None:
@@ -300,16 +301,11 @@ class PostgresTable(TableSource):
     def scan(self, columns: Sequence[str], ctx) -> Batch:
         import torch
         device = ctx.device if ctx is not None else torch.device("cpu")
-        ver = self.version
-        if ver != self._ver:
-            self._resident.clear()
-            self._ver = ver
-        missing = [c for c in columns if (c, str(device)) not in self._resident]
-        if missing:
-            t = self.read(missing)
+        out = {}
+        if columns:
+            t = self.read(columns)
             types = {f.name: f.dtype for f in self.schema()}
-            for c in missing:
-                self._resident[(c, str(device))] = Column.from_arrow(t.column(c), device=device, dtype=types[c])
-        out = {c: self._resident[(c, str(device))] for c in columns}
+            for c in columns:
+                out[c] = Column.from_arrow(t.column(c), device=device, dtype=types[c])
         n = len(next(iter(out.values()))) if out else (self.num_rows() or 0)
         return Batch(out, n)

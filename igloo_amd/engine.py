@@ -69,7 +69,11 @@ class QueryResult:
 
 class QueryEngine:
     def __init__(self, device: Optional[str] = None, catalog: Optional[Catalog] = None, comm=None,
-                 config: Optional[dict] = None):
+                 config: Optional[dict] = None, cache_hbm_gb: Optional[float] = None,
+                 cache_host_gb: Optional[float] = None, cache_dir: Optional[str] = None):
+        from .cache.cdc import CdcManager
+        from .cache.tiered import CacheConfig, TieredCache
+        from .utils.memory import device_capacity
         self.device = torch.device(device or default_device())
         self.catalog = catalog or Catalog()
         self.comm = comm
@@ -80,9 +84,26 @@ class QueryEngine:
         if self.device.type == "cuda":
             from .ops._lib import native
             native()  # fail loudly on a GPU box without the native extension
+        # cache tier for external sources (reference crates/cache/src/lib.rs:12-56,
+        # README "automatic cache invalidation via CDC"): resident decoded
+        # columns in HBM, demoted to host memory / Arrow IPC files past the
+        # budgets; the default HBM budget leaves a quarter of the device for
+        # query working memory (288 GB MI355X -> 216 GB of cached columns)
+        cap = device_capacity(self.device)
+        hbm = cache_hbm_gb * 2**30 if cache_hbm_gb is not None else (0.75 * cap if cap else 32 * 2**30)
+        host = cache_host_gb * 2**30 if cache_host_gb is not None else 32 * 2**30
+        self.cache = TieredCache(CacheConfig(hbm_bytes=int(hbm), host_bytes=int(host), disk_path=cache_dir,
+                                             device=str(self.device)))
+        self.cdc = CdcManager(self.cache)
 
     # -------------------------------------------------------------- catalog
-    def register_table(self, name: str, table: Union[TableSource, pa.Table, Batch, Dict[str, Column]], **kw):
+    def register_table(self, name: str, table: Union[TableSource, pa.Table, Batch, Dict[str, Column]],
+                       cache: Optional[bool] = None, **kw):
+        """Register a table. External sources (``cacheable`` connectors) are
+        served through the cache tier unless ``cache=False``."""
+        if isinstance(table, TableSource) and (cache if cache is not None else getattr(table, "cacheable", False)):
+            from .cache.cdc import CachedTable
+            table = CachedTable(name, table, self.cache, self.cdc)
         if isinstance(table, pa.Table):
             table = MemoryTable.from_arrow(table, device=self.device, **kw)
         elif isinstance(table, pa.RecordBatch):
@@ -95,19 +116,22 @@ class QueryEngine:
         return table
 
     def deregister_table(self, name: str):
+        self.cache.invalidate(f"{name}/")
         return self.catalog.deregister_table(name)
 
-    def register_parquet(self, name: str, path: str, **kw):
+    def register_parquet(self, name: str, path: str, cache: Optional[bool] = None, **kw):
         from .connectors.parquet import ParquetTable
-        return self.register_table(name, ParquetTable(path, **kw))
+        return self.register_table(name, ParquetTable(path, **kw), cache=cache)
 
-    def register_csv(self, name: str, path: str, schema=None, has_header: bool = True, delimiter: str = ",", **kw):
+    def register_csv(self, name: str, path: str, schema=None, has_header: bool = True, delimiter: str = ",",
+                     cache: Optional[bool] = None, **kw):
         from .connectors.csv import CsvTable
-        return self.register_table(name, CsvTable(path, schema=schema, has_header=has_header, delimiter=delimiter, **kw))
+        return self.register_table(name, CsvTable(path, schema=schema, has_header=has_header, delimiter=delimiter,
+                                                  **kw), cache=cache)
 
-    def register_iceberg(self, name: str, path: str, **kw):
+    def register_iceberg(self, name: str, path: str, cache: Optional[bool] = None, **kw):
         from .connectors.iceberg import IcebergTable
-        return self.register_table(name, IcebergTable(path, **kw))
+        return self.register_table(name, IcebergTable(path, **kw), cache=cache)
 
     def session_context(self) -> "QueryEngine":
         return self
@@ -207,10 +231,12 @@ class QueryEngine:
         b = Binder(self.catalog, self._ids, self.session)
         bq = b.bind_query(st)
         plan = optimize(bq.plan)
-        batch = self._execute_plan(plan)
+        ctx = self.make_context()
+        batch = self._execute_plan(plan, ctx)
         table = self._to_arrow(batch, plan.schema, bq.names)
+        self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
-        self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows}
+        self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned}
         return QueryResult(table, ms)
 
     def explain_fragments(self, sql: str, workers=("all-ranks",)) -> str:

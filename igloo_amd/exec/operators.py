@@ -57,6 +57,20 @@ class ExecContext:
         self.evaluator = Evaluator(self)
         self.spans: Dict[str, list] = {}  # phase -> [total ms, calls] (EXPLAIN ANALYZE only)
         self.scan_cache: Dict[tuple, tuple] = {}  # (source, filters) -> (row ids, gathered columns by name)
+        # rows of base tables this query read (each table once; index / range
+        # searches into a resident column subtract the rows they skipped)
+        self.rows_scanned = 0
+        self._scanned_sources: set = set()
+
+    def note_scan(self, source, rows: int) -> None:
+        if id(source) not in self._scanned_sources:
+            self._scanned_sources.add(id(source))
+            self.rows_scanned += rows
+
+    def note_partial_read(self, t: torch.Tensor, rows_read: int) -> None:
+        """A join searched resident column ``t`` and touched only ``rows_read`` rows."""
+        if getattr(t, "_igloo_resident", False):
+            self.rows_scanned -= max(0, t.numel() - rows_read)
 
     def span(self, name: str):
         """Time a phase inside an operator (device-synchronised; no-op unless analyzing)."""
@@ -202,7 +216,14 @@ class ScanExec(ExecNode):
             need |= col_refs(f)
         names = [by_cid[cid].name for cid in sorted(need)]
         with ctx.span("scan.source"):
-            raw = s.source.scan(names, ctx)
+            if s.filters and getattr(s.source, "prunes", False):
+                # row-group statistics pruning (the filter is still applied below)
+                from ..connectors.parquet import pushable_filters
+                pf = pushable_filters(s.filters, {cid: by_cid[cid].name for cid in need})
+                raw = s.source.scan(names, ctx, filters=pf)
+            else:
+                raw = s.source.scan(names, ctx)
+        ctx.note_scan(s.source, raw.num_rows)
         cols = {cid: raw.columns[by_cid[cid].name] for cid in sorted(need)}
         dist = None
         if ctx.world > 1:
@@ -875,6 +896,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
             lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
             sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
+        ctx.note_partial_read(big, sidx.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
             and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
@@ -890,6 +912,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         # probes later sorted joins) far more cheaply, so the index only
         # serves results below 1/PERM_INDEX_MAX_FRAC of the column
         if total * PERM_INDEX_MAX_FRAC <= big.numel():
+            ctx.note_partial_read(big, total)
             with ctx.span("join.index_expand"):
                 sidx, pos = H.expand_ranges(lo, cnt, big.numel())
                 bidx = perm.index_select(0, pos.long())

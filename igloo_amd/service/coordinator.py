@@ -68,7 +68,7 @@ class DistributedExecutor:
             except RETRYABLE as e:
                 w.failures += 1
                 self.log.append((sql, w.info.id, (time.perf_counter() - t0) * 1e3, f"retry: {type(e).__name__}"))
-                self.registry.mark_dead(w.info.id, f"(query failed: {type(e).__name__})")
+                self.registry.mark_dead(w.info.id, f"(query failed: {type(e).__name__})", quarantine=True)
             except pa.ArrowKeyError:
                 # NotFound = empty result from the worker
                 return self.engine.logical_schema_table(sql) if hasattr(self.engine, "logical_schema_table") else \

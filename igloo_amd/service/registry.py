@@ -30,12 +30,18 @@ class WorkerState:
     alive: bool = True
     tasks_done: int = 0
     failures: int = 0
+    quarantine_until: float = 0.0
 
 
 class WorkerRegistry:
-    def __init__(self, heartbeat_interval_s: float = 5.0, timeout_s: Optional[float] = None):
+    def __init__(self, heartbeat_interval_s: float = 5.0, timeout_s: Optional[float] = None,
+                 quarantine_s: Optional[float] = None):
         self.heartbeat_interval_s = heartbeat_interval_s
         self.timeout_s = timeout_s if timeout_s is not None else 3 * heartbeat_interval_s
+        #: a group that failed a query stays out of routing this long even if
+        #: it keeps heartbeating / re-registering (its process may be alive
+        #: while its GPUs or communicator are not)
+        self.quarantine_s = quarantine_s if quarantine_s is not None else 20 * heartbeat_interval_s
         self._lock = threading.RLock()
         self.workers: Dict[str, WorkerState] = {}
         self._listeners: List[Callable[[str], None]] = []
@@ -44,7 +50,14 @@ class WorkerRegistry:
 
     def register(self, info: WorkerInfo) -> RegistrationAck:
         with self._lock:
-            self.workers[info.id] = WorkerState(info)
+            old = self.workers.get(info.id)
+            if old is not None and old.quarantine_until > time.time():
+                old.info = info
+                return RegistrationAck("Quarantined", self.heartbeat_interval_s)
+            st = WorkerState(info)
+            if old is not None:
+                st.failures, st.tasks_done = old.failures, old.tasks_done
+            self.workers[info.id] = st
         log.info("registered worker %s at %s (%d GPUs)", info.id, info.address, info.world_size)
         return RegistrationAck("Registered", self.heartbeat_interval_s)
 
@@ -60,12 +73,14 @@ class WorkerRegistry:
         with self._lock:
             return [w for w in self.workers.values() if w.alive]
 
-    def mark_dead(self, worker_id: str, reason: str = ""):
+    def mark_dead(self, worker_id: str, reason: str = "", quarantine: bool = False):
         with self._lock:
             st = self.workers.get(worker_id)
             if st is None or not st.alive:
                 return
             st.alive = False
+            if quarantine:
+                st.quarantine_until = time.time() + self.quarantine_s
         log.warning("worker %s marked dead %s", worker_id, reason)
         for fn in self._listeners:
             fn(worker_id)

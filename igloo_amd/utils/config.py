@@ -95,6 +95,7 @@ def register_config_tables(engine, cfg: IglooConfig):
                                                       version_sql=spec.get("version_sql")))
         elif fmt == "mysql":
             from ..connectors.mysql import MySqlTable
-            engine.register_table(name, MySqlTable(spec["dsn"], spec.get("table", name), query=spec.get("query")))
+            engine.register_table(name, MySqlTable(spec["dsn"], spec.get("table", name), query=spec.get("query"),
+                                                   version_sql=spec.get("version_sql")))
         else:
             raise ValueError(f"unknown table format {fmt}")
