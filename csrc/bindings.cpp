@@ -166,6 +166,74 @@ PYBIND11_MODULE(_native, m) {
 
   // ------------------------------------------------------- select / scan
   m.def("select_num_tiles", &kern::select_num_tiles);
+  // ---- pack.hip
+  auto pack_spec = [](const std::vector<std::tuple<uintptr_t, uintptr_t, int, int>>& cols, int row_bytes) {
+    if (cols.size() > (size_t)kern::kMaxPackCols) throw std::runtime_error("pack: too many columns");
+    kern::PackSpec spec{};
+    spec.ncols = (int32_t)cols.size();
+    spec.row_bytes = row_bytes;
+    for (size_t i = 0; i < cols.size(); ++i) {
+      spec.cols[i].src = P<const void>(std::get<0>(cols[i]));
+      spec.cols[i].dst = P<void>(std::get<1>(cols[i]));
+      spec.cols[i].width = std::get<2>(cols[i]);
+      spec.cols[i].offset = std::get<3>(cols[i]);
+      if (spec.cols[i].offset + spec.cols[i].width > row_bytes) throw std::runtime_error("pack: field outside row");
+    }
+    return spec;
+  };
+  m.def("pack_rows", [pack_spec](std::vector<std::tuple<uintptr_t, uintptr_t, int, int>> cols, int row_bytes,
+                                 uintptr_t perm, bool perm64, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::pack_rows(pack_spec(cols, row_bytes), P<const void>(perm), perm64, n, P<uint8_t>(out), S(s));
+  });
+  m.def("unpack_rows", [pack_spec](std::vector<std::tuple<uintptr_t, uintptr_t, int, int>> cols, int row_bytes,
+                                   uintptr_t in, int64_t n, uintptr_t s) {
+    kern::unpack_rows(pack_spec(cols, row_bytes), P<const uint8_t>(in), n, S(s));
+  });
+  // ---- util.hip
+  m.def("column_stats", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::column_stats(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<long long>(out), S(s));
+  });
+  m.def("run_bounds", [](uintptr_t keys, bool key64, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::run_bounds(P<const void>(keys), key64, n, P<uint8_t>(out), S(s));
+  });
+  // ---- sort.hip
+  m.def("radix_sort_ws_bytes", &kern::radix_sort_ws_bytes);
+  m.def("radix_sort_pairs", [](uintptr_t k0, uintptr_t k1, bool key64, uintptr_t v0, uintptr_t v1, bool val64,
+                               int64_t n, int begin_bit, int end_bit, uintptr_t ws, uintptr_t s) {
+    return kern::radix_sort_pairs(P<void>(k0), P<void>(k1), key64, P<void>(v0), P<void>(v1), val64, n, begin_bit,
+                                  end_bit, P<void>(ws), S(s));
+  });
+  m.def("sort_key_pack", [](std::vector<std::tuple<uintptr_t, uintptr_t, uint64_t, uint64_t, int, int, int, int, int>> cols,
+                            uintptr_t perm, bool perm64, int64_t n, uintptr_t out, bool out32, uintptr_t s) {
+    if (cols.empty() || cols.size() > (size_t)kern::kMaxSortCols) throw std::runtime_error("sort_key_pack: bad column count");
+    kern::SortKeySpec spec{};
+    spec.ncols = (int32_t)cols.size();
+    int total = 0;
+    for (size_t i = 0; i < cols.size(); ++i) {
+      auto& c = spec.cols[i];
+      const auto& t = cols[i];
+      c.ptr = P<const void>(std::get<0>(t));
+      c.valid = P<const uint8_t>(std::get<1>(t));
+      c.lo = std::get<2>(t);
+      c.span = std::get<3>(t);
+      c.kind = std::get<4>(t);
+      c.width = std::get<5>(t);
+      c.bits = std::get<6>(t);
+      c.desc = std::get<7>(t);
+      c.nulls_first = std::get<8>(t);
+      if (c.bits < 0 || c.bits > 64) throw std::runtime_error("sort_key_pack: bad field width");
+      total += c.bits + (c.valid ? 1 : 0);
+    }
+    if (total > (out32 ? 32 : 64)) throw std::runtime_error("sort_key_pack: key fields exceed the key width");
+    kern::sort_key_pack(spec, P<const void>(perm), perm64, n, P<void>(out), out32, S(s));
+  });
+  m.def("radix_digit_hist", [](uintptr_t keys, bool key64, int64_t n, int shift, uint64_t prefix, int pshift,
+                               uintptr_t hist, uintptr_t s) {
+    kern::radix_digit_hist(P<const void>(keys), key64, n, shift, prefix, pshift, P<unsigned long long>(hist), S(s));
+  });
+  m.def("radix_le_mask", [](uintptr_t keys, bool key64, int64_t n, uint64_t bound, uintptr_t mask, uintptr_t s) {
+    kern::radix_le_mask(P<const void>(keys), key64, n, bound, P<uint8_t>(mask), S(s));
+  });
   m.def("select_count", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t total, uintptr_t s) {
     kern::select_count(P<const uint8_t>(mask), n, P<int64_t>(tiles), P<int64_t>(total), S(s));
   });

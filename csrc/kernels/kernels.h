@@ -25,6 +25,51 @@ int64_t scan_workspace_tiles(int64_t n);
 void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
                     hipStream_t stream);
 
+// ---- sort.hip -------------------------------------------------------------------
+constexpr int kMaxSortCols = 8;
+// kind: 0 signed int (width 1/2/4/8), 1 float64, 2 uint8/bool, 3 float32.
+// Field = ordered(value) - lo (DESC: span - that), `bits` wide; a nullable
+// column adds a NULL flag bit above the field.
+struct SortKeyCol {
+  const void* ptr;
+  const uint8_t* valid;
+  uint64_t lo, span;
+  int32_t kind, width, bits, desc, nulls_first, pad;
+};
+struct SortKeySpec {
+  int32_t ncols, pad;
+  SortKeyCol cols[kMaxSortCols];
+};
+int64_t radix_sort_ws_bytes(int64_t n);
+// Stable LSD sort of (key, value) pairs on key bits [begin_bit, end_bit).
+// Returns 0 when the result is in (k0, v0), 1 when in (k1, v1).
+int radix_sort_pairs(void* k0, void* k1, bool key64, void* v0, void* v1, bool val64, int64_t n, int begin_bit,
+                     int end_bit, void* ws, hipStream_t stream);
+// out: uint32 keys when out32 (total field width <= 32), else uint64
+void sort_key_pack(const SortKeySpec& spec, const void* perm, bool perm64, int64_t n, void* out, bool out32,
+                   hipStream_t stream);
+void radix_digit_hist(const void* keys, bool key64, int64_t n, int shift, uint64_t prefix, int pshift,
+                      unsigned long long* hist, hipStream_t stream);
+void radix_le_mask(const void* keys, bool key64, int64_t n, uint64_t bound, uint8_t* mask, hipStream_t stream);
+
+// ---- pack.hip -------------------------------------------------------------------
+constexpr int kMaxPackCols = 48;
+struct PackCol {
+  const void* src;  // pack: source column (row stride = width)
+  void* dst;        // unpack: destination column
+  int32_t width, offset;
+};
+struct PackSpec {
+  int32_t ncols, row_bytes;
+  PackCol cols[kMaxPackCols];
+};
+void pack_rows(const PackSpec& spec, const void* perm, bool perm64, int64_t n, uint8_t* out, hipStream_t stream);
+void unpack_rows(const PackSpec& spec, const uint8_t* in, int64_t n, hipStream_t stream);
+
+// ---- util.hip -------------------------------------------------------------------
+void column_stats(const void* keys, bool key64, const uint8_t* valid, int64_t n, long long* out, hipStream_t stream);
+void run_bounds(const void* keys, bool key64, int64_t n, uint8_t* out, hipStream_t stream);
+
 // ---- fused.hip ----------------------------------------------------------------
 constexpr int kFfMaxCols = 8;
 constexpr int kFfMaxTerms = 16;

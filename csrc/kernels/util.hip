@@ -1,0 +1,139 @@
+// Whole-column checks the planner asks for before choosing a join / group-by
+// strategy, as single-pass bandwidth kernels (they replaced ATen compare +
+// reduce pairs that each read the column twice and launched 2-3 kernels):
+//
+//   column_stats  -> {min, max, sorted flag} of an int32/int64 key column
+//                    (NULL rows skipped) in ONE read: every lane checks its
+//                    run of 8 rows plus the row before it; block min/max via
+//                    wave shuffles, one atomic per block;
+//   run_bounds    -> bound[i] = (i == 0 || k[i] != k[i-1]) for run-id group-by
+//                    over clustered keys.
+#include "common.h"
+#include "kernels.h"
+
+namespace igloo {
+namespace kern {
+
+namespace {
+
+constexpr int kPer = 8;  // rows per lane
+
+__device__ inline int64_t wave_min(int64_t v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    int64_t o = __shfl_xor(v, off, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ inline int64_t wave_max(int64_t v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    int64_t o = __shfl_xor(v, off, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void column_stats_kernel(const T* __restrict__ k, const uint8_t* __restrict__ valid,
+                                                              int64_t n, long long* __restrict__ out) {
+  __shared__ int64_t smin[kWavesPerBlock], smax[kWavesPerBlock];
+  __shared__ int sbad;
+  if (threadIdx.x == 0) sbad = 0;
+  __syncthreads();
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  bool bad = false;
+  const int64_t stride = (int64_t)gridDim.x * kBlock * kPer;
+  for (int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kPer; base < n; base += stride) {
+    T v[kPer];
+    if (base + kPer <= n && sizeof(T) * kPer % 16 == 0 && (((uintptr_t)(k + base)) & 15) == 0) {
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(T) * kPer / 16); ++q) {
+        const uint4 w = reinterpret_cast<const uint4*>(k + base)[q];
+        __builtin_memcpy(&v[q * 16 / sizeof(T)], &w, 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) v[j] = base + j < n ? k[base + j] : T(0);
+    }
+    T prev = base > 0 ? k[base - 1] : v[0];
+    bool prev_ok = base > 0 && (valid == nullptr || valid[base - 1]);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (base + j >= n) break;
+      const bool ok = valid == nullptr || valid[base + j];
+      if (ok) {
+        const int64_t x = (int64_t)v[j];
+        mn = x < mn ? x : mn;
+        mx = x > mx ? x : mx;
+        if (prev_ok && v[j] < prev) bad = true;
+        prev = v[j];
+        prev_ok = true;
+      }
+    }
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const uint64_t anybad = __ballot(bad);
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    smin[w] = mn;
+    smax[w] = mx;
+    if (anybad) sbad = 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t a = smin[0], b = smax[0];
+    for (int i = 1; i < kWavesPerBlock; ++i) {
+      a = smin[i] < a ? smin[i] : a;
+      b = smax[i] > b ? smax[i] : b;
+    }
+    if (a != INT64_MAX) atomicMin(&out[0], (long long)a);
+    if (b != INT64_MIN) atomicMax(&out[1], (long long)b);
+    if (sbad) atomicMax(&out[2], 1LL);
+  }
+}
+
+__global__ void stats_init_kernel(long long* out) {
+  out[0] = INT64_MAX;
+  out[1] = INT64_MIN;
+  out[2] = 0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void run_bounds_kernel(const T* __restrict__ k, int64_t n, uint8_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    out[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
+}
+
+}  // namespace
+
+void column_stats(const void* keys, bool key64, const uint8_t* valid, int64_t n, long long* out, hipStream_t stream) {
+  // out[0] = min, out[1] = max over non-NULL rows; out[2] = 1 if some row is
+  // below its predecessor (only meaningful without NULLs)
+  hipLaunchKernelGGL(stats_init_kernel, dim3(1), dim3(1), 0, stream, out);
+  if (n <= 0) return;
+  const unsigned g = grid_for(n, kBlock * kPer, 4096);
+  if (key64)
+    hipLaunchKernelGGL(column_stats_kernel<int64_t>, dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys, valid, n,
+                       out);
+  else
+    hipLaunchKernelGGL(column_stats_kernel<int32_t>, dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys, valid, n,
+                       out);
+  check_launch("util.column_stats", stream);
+}
+
+void run_bounds(const void* keys, bool key64, int64_t n, uint8_t* out, hipStream_t stream) {
+  if (n <= 0) return;
+  const unsigned g = grid_for(n, kBlock * 4, 8192);
+  if (key64)
+    hipLaunchKernelGGL(run_bounds_kernel<int64_t>, dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys, n, out);
+  else
+    hipLaunchKernelGGL(run_bounds_kernel<int32_t>, dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys, n, out);
+  check_launch("util.run_bounds", stream);
+}
+
+}  // namespace kern
+}  // namespace igloo

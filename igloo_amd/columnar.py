@@ -30,7 +30,7 @@ class Column:
     ``valid`` is an optional bool tensor (True = not null).
     """
 
-    __slots__ = ("dtype", "data", "valid", "offsets", "dictionary", "_host_dict", "_sorted_dict")
+    __slots__ = ("dtype", "data", "valid", "offsets", "dictionary", "_host_dict", "_sorted_dict", "_unified")
 
     def __init__(self, dtype: DataType, data: torch.Tensor, valid: Optional[torch.Tensor] = None,
                  offsets: Optional[torch.Tensor] = None, dictionary: Optional["Column"] = None):
@@ -41,6 +41,7 @@ class Column:
         self.dictionary = dictionary
         self._host_dict = None
         self._sorted_dict = None
+        self._unified = None      # content digest when used as a dictionary (parallel/exchange.py)
 
     # ------------------------------------------------------------------ shape
     def __len__(self) -> int:
@@ -265,11 +266,12 @@ def _decimal_to_int64(arr: pa.Array) -> np.ndarray:
 class Batch:
     """An ordered set of equally long columns keyed by column id (or name)."""
 
-    __slots__ = ("columns", "num_rows", "dist", "out_dist")
+    __slots__ = ("columns", "num_rows", "dist", "out_dist", "preamble")
 
     def __init__(self, columns: Dict[Any, Column], num_rows: Optional[int] = None, dist=None):
         self.dist = dist          # ("hash", cid) | ("replicated",) | None  (SPMD row placement)
         self.out_dist = None
+        self.preamble = None      # per-rank ints of the last exchange preamble (parallel/exchange.py)
         self.columns = dict(columns)
         if num_rows is None:
             num_rows = len(next(iter(self.columns.values()))) if self.columns else 0

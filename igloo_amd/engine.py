@@ -232,11 +232,14 @@ class QueryEngine:
         bq = b.bind_query(st)
         plan = optimize(bq.plan)
         ctx = self.make_context()
+        c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
         batch = self._execute_plan(plan, ctx)
         table = self._to_arrow(batch, plan.schema, bq.names)
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned}
+        if self.comm is not None:
+            self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
         return QueryResult(table, ms)
 
     def explain_fragments(self, sql: str, workers=("all-ranks",)) -> str:
@@ -287,6 +290,7 @@ class QueryEngine:
         rows_t, rows_p = ["logical_plan", "physical_plan"], [logical.explain(), node.explain()]
         if analyze:
             ctx = self.make_context(analyze=True)
+            c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
             t0 = time.perf_counter()
             node.execute(ctx)
             ms = (time.perf_counter() - t0) * 1e3
@@ -295,6 +299,9 @@ class QueryEngine:
             for n in _walk_exec(node):
                 if getattr(n, "order_log", None):
                     txt += "\njoin order: " + " ; ".join(n.order_log)
+            if self.comm is not None and self.comm.world_size > 1:
+                txt += (f"\nexchange: {self.comm.calls - c0[0]} collectives, "
+                        f"{self.comm.bytes_sent - c0[1]} bytes sent by this rank")
             if ctx.spans:
                 txt += "\nphases (inclusive, synchronised):\n" + ctx.span_report()
             rows_p = [txt]

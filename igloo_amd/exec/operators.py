@@ -35,8 +35,8 @@ from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
 from ..ops._lib import launch, ptr, stream, to_host_int
-from ..ops.gather import take, take_many
-from ..ops.select import mask_to_indices
+from ..ops.gather import gather_tensor, take, take_many
+from ..ops.select import exclusive_scan, mask_to_indices
 from ..sql import logical as L
 from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
 from ..utils.errors import ExecutionError, NotSupported
@@ -580,7 +580,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
         if n_r and lvalid is not None:
             keep = mask_to_indices(lvalid)
             lb = _take_batch(lb, keep)
-            lk = lk.index_select(0, keep.long())
+            lk = gather_tensor(lk, keep)
             lvalid = None
             n_l = lb.num_rows
     if dev.type == "cuda" and len(on) == 1 and kind in ("inner", "semi", "anti", "left") and not null_aware:
@@ -601,7 +601,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
                 ridx, lidx, _ = table.probe_pairs(rk, rvalid)
                 pair = _combine(lb, rb, lidx, ridx, False)
                 keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-                matched[lidx.index_select(0, keep.long()).long()] = True
+                matched[gather_tensor(lidx, keep).long()] = True
             sel = mask_to_indices(matched if kind == "semi" else ~matched)
         with ctx.span("join.gather"):
             return _take_batch(lb, sel)
@@ -616,7 +616,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             if table.unique:
                 first = table.probe_first(rk, rvalid, build_matched=matched)
                 ridx = mask_to_indices(first >= 0)
-                lidx = first.index_select(0, ridx.long())
+                lidx = gather_tensor(first, ridx)
             else:
                 ridx, lidx, _ = table.probe_pairs(rk, rvalid, build_matched=matched)
             miss = mask_to_indices(~matched)
@@ -654,8 +654,8 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             pair = _combine(lb, rb, pidx, bidx, False)
             keep = predicate_mask(residual, pair, ctx)
         sel = mask_to_indices(keep)
-        pidx = pidx.index_select(0, sel.long())
-        bidx = bidx.index_select(0, sel.long())
+        pidx = gather_tensor(pidx, sel)
+        bidx = gather_tensor(bidx, sel)
         if kind in ("semi", "anti", "left", "full"):
             hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
             hit[pidx.long()] = True
@@ -735,8 +735,8 @@ def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residu
         with ctx.span("join.residual"):
             pair = _combine(lb, rb, lidx, ridx, False)
             keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-            lidx = lidx.index_select(0, keep.long())
-            ridx = ridx.index_select(0, keep.long())
+            lidx = gather_tensor(lidx, keep)
+            ridx = gather_tensor(ridx, keep)
             if kind == "inner":
                 return _take_batch(pair, keep)
     if kind == "inner":
@@ -787,7 +787,7 @@ def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:
     pair = _combine(lb, rb, li, ri, False)
     if residual is not None:
         keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-        li, ri = li.index_select(0, keep.long()), ri.index_select(0, keep.long())
+        li, ri = gather_tensor(li, keep), gather_tensor(ri, keep)
         pair = _take_batch(pair, keep) if kind in ("inner", "cross") else pair
     if kind in ("inner", "cross"):
         return pair
@@ -906,7 +906,8 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         skeys, perm = H.perm_index(big)
         with ctx.span("join.index_search"):
             lo, cnt = H.sorted_ranges(skeys, small, svalid)
-            total = to_host_int(cnt.sum())
+            scanned = exclusive_scan(cnt)     # one sync: size check + expansion offsets
+            total = scanned[1]
         # the index hands out rows grouped by key, i.e. in random row order:
         # for a large result the ordered hash probe output gathers (and
         # probes later sorted joins) far more cheaply, so the index only
@@ -914,8 +915,8 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         if total * PERM_INDEX_MAX_FRAC <= big.numel():
             ctx.note_partial_read(big, total)
             with ctx.span("join.index_expand"):
-                sidx, pos = H.expand_ranges(lo, cnt, big.numel())
-                bidx = perm.index_select(0, pos.long())
+                sidx, pos = H.expand_ranges(lo, cnt, big.numel(), scanned)
+                bidx = gather_tensor(perm, pos)
                 if bidx.dtype != sidx.dtype:
                     bidx = bidx.to(sidx.dtype)
             return (sidx, bidx) if big_right else (bidx, sidx)
@@ -1039,7 +1040,7 @@ class LateBatch(Batch):
         return c
 
     def compose(self, sel: torch.Tensor):
-        return [(bb, sel if idx is None else idx.index_select(0, sel.long()).to(sel.dtype if sel.dtype == torch.int64
+        return [(bb, sel if idx is None else gather_tensor(idx, sel).to(sel.dtype if sel.dtype == torch.int64
                                                                                else idx.dtype))
                 for bb, idx in self.parts]
 
@@ -1129,7 +1130,7 @@ class _LazyScanBatch(Batch):
             else:
                 pend.append(c)
         if pend:
-            comp = self.idx.index_select(0, rows.long())
+            comp = gather_tensor(self.idx, rows)
             out.update(zip(pend, take_many([self.src.columns[c] for c in pend], comp)))
         return [out[c] for c in cids]
 
@@ -1186,16 +1187,24 @@ class MultiJoinExec(ExecNode):
             rels.append({"batch": b, "cids": set(b.columns), "ndv": {}, "name": ch.describe()[:40]})
         self.order_log = []
         deferred = []
-        for sp, rex in zip(lg.semis, self.children[nch:]):
-            rb = rex.execute(ctx)
+        semis = [(sp, rex.execute(ctx)) for sp, rex in zip(lg.semis, self.children[nch:])]
+        # global row counts of every input in ONE all-reduce (SPMD: every rank
+        # must derive the same join order)
+        g = _global_rows_many([r["batch"] for r in rels] + [rb for _, rb in semis], ctx)
+        for r, n in zip(rels, g):
+            r["grows"] = n
+        for (sp, rb), nrb in zip(semis, g[len(rels):]):
             tgt = rels[sp.child]
-            if sp.kind == "semi" and _global_rows(rb, ctx) <= self.EAGER_SEMI_RATIO * _global_rows(tgt["batch"], ctx):
+            if sp.kind == "semi" and nrb <= self.EAGER_SEMI_RATIO * tgt["grows"]:
                 tgt["batch"] = self._semi(tgt["batch"], rb, sp, ctx)
+                tgt["grows"] = _global_rows(tgt["batch"], ctx)
                 self.order_log.append(f"{sp.kind} pre-filter on {tgt['name']} -> {tgt['batch'].num_rows}")
             else:
                 deferred.append((sp, rb))
         conds = list(lg.conds)
         while len(rels) > 1:
+            if ctx.world > 1:
+                self._prefetch_ndv(rels, conds, ctx)
             best = None
             for i in range(len(rels)):
                 for k in range(i + 1, len(rels)):
@@ -1207,7 +1216,7 @@ class MultiJoinExec(ExecNode):
                         best = (est, i, k, keys)
             if best is None:
                 # no join edge: cross join the two smallest inputs
-                order = sorted(range(len(rels)), key=lambda x: _global_rows(rels[x]["batch"], ctx))
+                order = sorted(range(len(rels)), key=lambda x: rels[x]["grows"])
                 i, k = sorted(order[:2])
                 keys = []
             else:
@@ -1223,7 +1232,7 @@ class MultiJoinExec(ExecNode):
             if ctx.world > 1:
                 from ..parallel.exchange import prepare_join
                 fake = L.Join(None, None, "inner", on)  # type: ignore[arg-type]
-                la, lb_ = prepare_join(la, lb_, fake, ctx)
+                la, lb_ = prepare_join(la, lb_, fake, ctx, rows=(a["grows"], b["grows"]))
                 out_dist = la.out_dist
             if on and ctx.world == 1:
                 out = self._late_join(la, lb_, on, and_all(resid), ctx)
@@ -1243,7 +1252,7 @@ class MultiJoinExec(ExecNode):
             # key NDVs carry over (capped by the output size) instead of re-sketching intermediates
             cap = _global_rows(out, ctx)   # global: every rank must derive the same estimates / join order
             ndv = {k: max(1, min(v, cap)) for d in (a["ndv"], b["ndv"]) for k, v in d.items()}
-            merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})"}
+            merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})", "grows": cap}
             rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
         b = rels[0]["batch"]
         if isinstance(b, LateBatch) and not conds and not deferred and LAZY_JOIN_OUTPUT:
@@ -1296,13 +1305,47 @@ class MultiJoinExec(ExecNode):
             with ctx.span("join.residual"):
                 P = LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
                 keep = mask_to_indices(predicate_mask(residual, P, ctx))
-                lidx = lidx.index_select(0, keep.long())
-                ridx = ridx.index_select(0, keep.long())
+                lidx = gather_tensor(lidx, keep)
+                ridx = gather_tensor(ridx, keep)
         with ctx.span("join.compose"):
             return LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
 
+    def _prefetch_ndv(self, rels, conds, ctx) -> None:
+        """SPMD: sketch every join key the next ordering step will ask for and
+        merge all rank sketches with ONE all-reduce (instead of one per key)."""
+        need = []
+        for i in range(len(rels)):
+            for k in range(i + 1, len(rels)):
+                keys = _edges(conds, rels[i]["cids"], rels[k]["cids"])
+                if keys:
+                    for rel, e in ((rels[i], keys[0][0]), (rels[k], keys[0][1])):
+                        if e.sql() not in rel["ndv"] and all(e.sql() != x.sql() or rel is not r for r, x in need):
+                            need.append((rel, e))
+        if not need:
+            return
+        if ctx.device.type != "cuda":
+            # CPU ranks: exact local distinct counts, summed (an upper bound) in one all-reduce
+            local = []
+            for rel, e in need:
+                b = rel["batch"]
+                local.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if b.num_rows else 0)
+            for (rel, e), g in zip(need, ctx.comm.allreduce_ints(local)):
+                rel["ndv"][e.sql()] = max(g, 1)
+            return
+        regs = []
+        for rel, e in need:
+            b = rel["batch"]
+            if b.num_rows:
+                k, _ = group_key_tensor(ctx.evaluator.column(e, b))
+                regs.append(H.hll_sketch(k))
+            else:
+                regs.append(torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
+        merged = ctx.comm.allreduce_max_tensor(torch.stack(regs))
+        for (rel, e), r in zip(need, merged):
+            rel["ndv"][e.sql()] = max(int(round(H.hll_estimate(r))), 1)
+
     def _estimate(self, a, b, keys, ctx) -> float:
-        na, nb = _global_rows(a["batch"], ctx), _global_rows(b["batch"], ctx)
+        na, nb = a["grows"], b["grows"]
         ka, kb = keys[0][0], keys[0][1]
         da = self._ndv(a, ka, ctx)
         db = self._ndv(b, kb, ctx)
@@ -1382,6 +1425,12 @@ def _global_rows(b: Batch, ctx) -> int:
     return b.num_rows
 
 
+def _global_rows_many(bs: Sequence[Batch], ctx) -> List[int]:
+    if ctx.world > 1 and bs:
+        return ctx.comm.allreduce_ints([b.num_rows for b in bs])
+    return [b.num_rows for b in bs]
+
+
 def _edges(conds, ca: set, cb: set):
     """Equi-join edges between two inputs: list of (expr_a, expr_b, cond)."""
     out = []
@@ -1437,7 +1486,7 @@ class HashAggExec(ExecNode):
             lk, rk, lvalid, rvalid = key_tensors([ev.column(lkey, lb)], [ev.column(rkey, rb)])
             if rvalid is not None:  # NULL keys never match
                 keep = mask_to_indices(rvalid)
-                rk = rk.index_select(0, keep.long())
+                rk = gather_tensor(rk, keep)
                 rb = _take_batch(rb, keep)
             cnt_cols = {}
             rng = H.key_range(rk) if rk.numel() else None
@@ -1458,7 +1507,7 @@ class HashAggExec(ExecNode):
                 gid, ng, rep, srt = H.group_ids_ex(rk)
                 specs = [("count", None, ev.column(a.arg, rb).valid) for _, a in lg.aggs]
                 counts = A.grouped_aggregate(gid, ng, specs, rk.numel(), ctx.device, sorted_gids=srt)
-                first = H.JoinTable(rk.index_select(0, rep.long())).probe_first(lk, lvalid)
+                first = H.JoinTable(gather_tensor(rk, rep)).probe_first(lk, lvalid)
                 hit = first >= 0
                 safe = torch.where(hit, first, torch.zeros_like(first)).long()
                 for k, c in enumerate(counts):
@@ -1569,7 +1618,7 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
     spans = {i: H.key_range(keys[i]) for i in others}
     lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
     gid, ng, rep, srt = H.group_ids_ex(keys[lead])
-    rr = rep.index_select(0, gid.long())
+    rr = gather_tensor(rep, gid)
     checks, parts = [], set()
     for i in range(len(cids)):
         k = b.owner[cids[i]]
@@ -1589,7 +1638,7 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
             taken.append(take(b.gather(c), rep))
         else:
             bb, idx = b.parts[b.owner[c]]
-            taken.append(take(bb.columns[c], idx.index_select(0, rep.long())))
+            taken.append(take(bb.columns[c], gather_tensor(idx, rep)))
     return gid, ng, rep, taken
 
 
@@ -1616,7 +1665,7 @@ def _encode_groups(gcols: List[Column], ctx):
         lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
         gid, ng, rep, srt = H.group_ids_ex(keys[lead])
         ctx.sorted_gids = srt
-        rr = rep.index_select(0, gid.long())
+        rr = gather_tensor(rep, gid)
         bad = []
         for i in range(len(gcols)):
             if i == lead:
@@ -1721,13 +1770,16 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
             vals = d.dictionary
             i = add("min_int" if func == "min" else "max_int", ranks.contiguous(), valid)
             # map winning rank back to a dictionary code
-            order = torch.argsort(S.sort_ranks(Column(T.UTF8, torch.arange(len(vals), dtype=torch.int32, device=dev), None, dictionary=vals)))
+            from ..ops.sort import argsort as _argsort
+            dranks = S.sort_ranks(Column(T.UTF8, torch.arange(len(vals), dtype=torch.int32, device=dev), None,
+                                         dictionary=vals))
+            order = _argsort([(dranks, False, False, None)], dranks.numel(), dev)
 
             def fin(r, i=i, order=order, d=d):
                 rk = r[i]
                 vv = null_if_empty(r, rk)
                 safe = rk.clamp(0, max(len(order) - 1, 0))
-                codes = order.index_select(0, safe.long()).to(torch.int32) if len(order) else safe.to(torch.int32)
+                codes = gather_tensor(order, safe).to(torch.int32) if len(order) else safe.to(torch.int32)
                 return ci, Column(T.UTF8, codes, vv, dictionary=d.dictionary)
             finals.append(fin)
             return
@@ -1811,43 +1863,43 @@ class SortExec(ExecNode):
 
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
-        if ctx.world > 1:
+        fetch = self.logical.fetch
+        if ctx.world > 1 and b.dist != ("replicated",):
             from ..parallel.exchange import gather_all
+            if fetch is not None:
+                # distributed ORDER BY ... LIMIT k: local top-k first, then only
+                # k rows per rank cross the fabric
+                dist = b.dist
+                b = sort_batch(b, self.logical.keys, fetch, ctx)
+                b.dist = dist
             b = gather_all(b, ctx)
-        out = sort_batch(b, self.logical.keys, self.logical.fetch, ctx)
+        out = sort_batch(b, self.logical.keys, fetch, ctx)
         out.dist = b.dist
         return out
 
 
-#: ORDER BY ... LIMIT k over more than this many rows (and > 4k) first keeps the
-#: rows that can still make the top k on the leading key
-TOPK_PREFILTER_ROWS = 4096
-
-
-def _topk_candidates(b: Batch, keys, fetch, ctx) -> Optional[torch.Tensor]:
-    """Rows whose leading sort key ranks within the first ``fetch`` (ties kept):
-    the only rows an ORDER BY ... LIMIT can return. Lets string tie-breakers be
-    ranked over a handful of rows instead of the whole input (TPC-H Q2, Q21)."""
-    e, asc, _nf = keys[0]
-    c = ctx.evaluator.column(e, b)
-    if c.dtype.is_string or c.is_wide or c.valid is not None or c.data.dim() != 1:
-        return None
-    v = c.data
-    if v.dtype == torch.bool:
-        v = v.to(torch.int8)
-    kth = torch.topk(v, fetch, largest=not asc, sorted=True).values[-1]
-    return mask_to_indices(v <= kth if asc else v >= kth)
-
-
 def sort_batch(b: Batch, keys, fetch, ctx) -> Batch:
+    """ORDER BY [LIMIT fetch]: packed keys + radix sort, or radix select +
+    candidate sort for a LIMIT (ops/sort.py)."""
+    from ..ops import sort as SO
     n = b.num_rows
     if n <= 1:
         return b
-    if fetch is not None and 0 < fetch and n > max(TOPK_PREFILTER_ROWS, 4 * fetch):
-        cand = _topk_candidates(b, keys, fetch, ctx)
-        if cand is not None and cand.numel() < n:
-            return sort_batch(_take_batch(b, cand), keys, fetch, ctx)
     ev = ctx.evaluator
+    if fetch is not None and len(keys) > 1 and ctx.device.type == "cuda":
+        # keep the rows the leading numeric keys can still admit to the top
+        # `fetch` before ranking string tie-breakers (TPC-H Q2, Q21)
+        lead = []
+        for e, asc, nf in keys:
+            c = ev.column(e, b)
+            if c.dtype.is_string or c.is_wide or c.data.dim() != 1:
+                break
+            lead.append((c.data, not asc, nf, c.valid))
+        if lead and len(lead) < len(keys):
+            cand = SO.topk_candidates(lead, n, fetch)
+            if cand is not None and cand.numel() < n:
+                b = _take_batch(b, cand)
+                n = b.num_rows
     ks = []
     for e, asc, nf in keys:
         c = ev.column(e, b)
@@ -1858,9 +1910,10 @@ def sort_batch(b: Batch, keys, fetch, ctx) -> Batch:
         else:
             v = c.data
         ks.append((v, not asc, nf, c.valid))
-    perm = M.argsort_keys(ks, n, ctx.device)
-    if fetch is not None:
-        perm = perm[:fetch]
+    if fetch is not None and fetch < n:
+        perm = SO.topk(ks, n, fetch, ctx.device)
+    else:
+        perm = SO.argsort(ks, n, ctx.device)
     return _take_batch(b, perm)
 
 
@@ -1874,8 +1927,15 @@ class LimitExec(ExecNode):
 
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
-        if ctx.world > 1:
+        if ctx.world > 1 and b.dist != ("replicated",):
             from ..parallel.exchange import gather_all
+            if self.logical.limit is not None:
+                # any offset+limit rows of each rank can make the answer
+                keep = min(b.num_rows, self.logical.offset + self.logical.limit)
+                if keep < b.num_rows:
+                    dist = b.dist
+                    b = _take_batch(b, torch.arange(keep, dtype=torch.int64, device=ctx.device))
+                    b.dist = dist
             b = gather_all(b, ctx)
         lo = min(self.logical.offset, b.num_rows)
         hi = b.num_rows if self.logical.limit is None else min(b.num_rows, lo + self.logical.limit)

@@ -157,7 +157,8 @@ def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torc
     assert keys.dtype in (torch.int32, torch.int64) and span < 2**31
     keys = keys.contiguous()
     n = keys.numel()
-    if HIST_PARTITIONED and n >= (1 << 22) and (1 << 16) <= span <= (1 << 27):
+    # (int32 scatter positions: n < 2^31 is guaranteed by the bincount branch above)
+    if HIST_PARTITIONED and (1 << 22) <= n < 2**31 - 1 and (1 << 16) <= span <= (1 << 27):
         return _key_histogram_partitioned(keys, kmin, span, valid)
     counts = torch.zeros(span, dtype=torch.int32, device=keys.device)
     launch("key_histogram").key_histogram(ptr(keys), keys.dtype == torch.int64,

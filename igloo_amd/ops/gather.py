@@ -103,5 +103,20 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
     return out
 
 
+def gather_tensor(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """``t[idx]`` along dim 0 (idx int32/int64, no negatives). GPU: the
+    gather_multi kernel (int32 indices used as is, no int64 conversion pass)."""
+    if not is_gpu(idx):
+        return t.index_select(0, idx.long())
+    t = t.contiguous()
+    n = idx.numel()
+    out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=idx.device)
+    if n:
+        esz = t.element_size() * (t.shape[1] if t.dim() == 2 else 1)
+        launch("gather_multi").gather_multi(ptr(idx), idx.dtype == torch.int64, n, [(ptr(t), ptr(out), esz, 0, 0)],
+                                            stream(idx))
+    return out
+
+
 def take(col: Column, idx: torch.Tensor, neg: bool = False) -> Column:
     return take_many([col], idx, neg)[0]

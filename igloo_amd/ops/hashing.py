@@ -36,14 +36,39 @@ def _next_pow2(x: int) -> int:
     return p
 
 
+def column_stats(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Tuple[Optional[Tuple[int, int]], bool]:
+    """((min, max) of the non-NULL keys or None, non-decreasing?) — one pass of
+    csrc/kernels/util.hip and one host sync on the GPU. Remembered on resident
+    key columns (no validity)."""
+    if valid is None:
+        hit = getattr(keys, "_igloo_stats", None)
+        if hit is not None:
+            return hit
+    n = keys.numel()
+    if not is_gpu(keys) or keys.dtype not in (torch.int32, torch.int64):
+        k = keys if valid is None else keys[valid]
+        if k.numel() == 0:
+            return None, True
+        mn, mx = torch.aminmax(k)
+        srt = True if k.numel() < 2 else bool((k[1:] >= k[:-1]).all().item())
+        return (int(mn.item()), int(mx.item())), srt
+    out = torch.empty(3, dtype=torch.int64, device=keys.device)
+    launch("column_stats").column_stats(ptr(keys.contiguous()), keys.dtype == torch.int64,
+                                         ptr(valid.contiguous() if valid is not None else None), n, ptr(out),
+                                         stream(keys))
+    mn, mx, bad = to_host_ints(out)
+    res = ((mn, mx) if mn <= mx else None), (bad == 0 and valid is None)
+    if valid is None and getattr(keys, "_igloo_resident", False):
+        try:
+            keys._igloo_stats = res
+            keys._igloo_sorted = res[1]
+        except (AttributeError, RuntimeError):
+            pass
+    return res
+
+
 def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optional[Tuple[int, int]]:
-    if valid is not None:
-        keys = keys[valid]
-    if keys.numel() == 0:
-        return None
-    mn, mx = torch.aminmax(keys)
-    lo, hi = to_host_ints(torch.stack([mn.to(torch.int64), mx.to(torch.int64)]))   # one host sync
-    return int(lo), int(hi)
+    return column_stats(keys, valid)[0]
 
 
 def _keys_ok(k: torch.Tensor) -> torch.Tensor:
@@ -223,7 +248,7 @@ def is_sorted(keys: torch.Tensor) -> bool:
     if hit is not None:
         return hit
     n = keys.numel()
-    r = True if n < 2 else bool(to_host_int((keys[1:] >= keys[:-1]).all()))
+    r = True if n < 2 else column_stats(keys)[1]
     try:
         keys._igloo_sorted = r
     except (AttributeError, RuntimeError):
@@ -313,29 +338,30 @@ def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Ten
 
 def perm_index(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """Secondary index of an unsorted resident key column: (keys in sorted
-    order, int32 row permutation), built once per column tensor (a stable
-    device radix sort) and kept with it like the other derived structures —
+    order, int32 row permutation), built once per column tensor (the stable
+    radix sort of ops/sort.py) and kept with it like the other derived
+    structures (charged to the column in the HBM cache budget) —
     a join with a much smaller side then reads only the matching ranges
     instead of probing every row of the column."""
     hit = getattr(keys, "_igloo_perm", None)
     if hit is not None:
         return hit
-    sk, perm = torch.sort(keys, stable=True)
-    out = (sk, perm.to(torch.int32) if keys.numel() < INT32_MAX else perm)
-    del perm
+    from .sort import perm_sort_int
+    out = perm_sort_int(keys)
     try:
-        sk._igloo_sorted = True
+        out[0]._igloo_sorted = True
         keys._igloo_perm = out
     except (AttributeError, RuntimeError):
         pass
     return out
 
 
-def expand_ranges(lo: torch.Tensor, cnt: torch.Tensor, big_n: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """All pairs (s, lo[s] + k), k < cnt[s], grouped by s (int32 when they fit)."""
+def expand_ranges(lo: torch.Tensor, cnt: torch.Tensor, big_n: int, scanned=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All pairs (s, lo[s] + k), k < cnt[s], grouped by s (int32 when they fit).
+    ``scanned``: the caller's ``exclusive_scan(cnt)`` result, reused."""
     ns = lo.numel()
     dev = lo.device
-    off, total = exclusive_scan(cnt)
+    off, total = scanned if scanned is not None else exclusive_scan(cnt)
     it = torch.int32 if max(total, big_n, ns) < INT32_MAX else torch.int64
     if not is_gpu(lo):
         sidx = torch.repeat_interleave(torch.arange(ns, dtype=it), cnt, output_size=total)
@@ -409,8 +435,7 @@ def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, b
     if n >= SORTED_CHECK_ROWS and is_gpu(keys):
         if is_sorted(keys):
             bound = torch.empty(n, dtype=torch.bool, device=keys.device)
-            bound[0] = True
-            torch.ne(keys[1:], keys[:-1], out=bound[1:])
+            launch("run_bounds").run_bounds(ptr(keys), keys.dtype == torch.int64, n, ptr(bound), stream(keys))
             starts = mask_to_indices(bound)
             g = starts.numel()
             gid = torch.empty(n, dtype=torch.int32, device=keys.device)

@@ -86,23 +86,7 @@ def date_part(days: torch.Tensor, field: str) -> torch.Tensor:
 def argsort_keys(keys: Sequence[Tuple[torch.Tensor, bool, bool, Optional[torch.Tensor]]], n: int,
                  device) -> torch.Tensor:
     """Lexicographic stable argsort. keys: (values, descending, nulls_first, valid).
-
-    LSD order: stable-sort by the least significant key first. Values must be
-    numeric (strings are turned into order-preserving ranks by the caller)."""
-    perm = torch.arange(n, dtype=torch.int64, device=device)
-    for vals, desc, nulls_first, valid in reversed(list(keys)):
-        v = vals.index_select(0, perm)
-        if v.dtype == torch.bool:
-            v = v.to(torch.int8)
-        if valid is not None:
-            vv = valid.index_select(0, perm)
-            # put NULLs at the requested end by sorting on a two-part key
-            o = torch.sort(v, stable=True, descending=desc).indices
-            perm = perm.index_select(0, o)
-            vv = vv.index_select(0, o)
-            o2 = torch.sort(vv.to(torch.int8), stable=True, descending=not nulls_first).indices
-            perm = perm.index_select(0, o2)
-        else:
-            o = torch.sort(v, stable=True, descending=desc).indices
-            perm = perm.index_select(0, o)
-    return perm
+    GPU: packed keys + the radix sort of ops/sort.py; values must be numeric
+    (strings are turned into order-preserving ranks by the caller)."""
+    from .sort import argsort
+    return argsort(keys, n, device)

@@ -17,6 +17,7 @@ import torch
 
 from .. import types as T
 from ..columnar import Column
+from .gather import gather_tensor
 from ._lib import is_gpu, launch, ptr, stream
 from .gather import take
 from .hashing import group_ids
@@ -98,7 +99,7 @@ def _lut_apply(col: Column, lut_vals: Sequence) -> torch.Tensor:
     lut = torch.tensor(list(lut_vals), device=col.device)
     if lut.numel() == 0:
         return torch.zeros(len(col), dtype=lut.dtype, device=col.device)
-    return lut.index_select(0, col.data.long())
+    return gather_tensor(lut, col.data)
 
 
 def _with_valid(values: torch.Tensor, col: Column) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -300,7 +301,7 @@ def dict_encode(col: Column) -> Column:
     gid, g, rep = group_ids(h)
     # verify every row equals its group's representative (no 64-bit collision)
     mism = torch.zeros(1, dtype=torch.int32, device=col.device)
-    rep_of_row = rep.index_select(0, gid.long())
+    rep_of_row = gather_tensor(rep, gid)
     ri = rep_of_row.to(torch.int32)
     ai = torch.arange(n, dtype=torch.int32, device=col.device)
     launch("str_eq_rows").str_eq_rows(ptr(col.offsets), ptr(col.data), ptr(ai), ptr(col.offsets), ptr(col.data),
@@ -323,7 +324,7 @@ def sort_ranks(col: Column) -> torch.Tensor:
     rank = np.empty(len(order), dtype=np.int64)
     rank[order] = np.arange(len(order), dtype=np.int64)
     lut = torch.from_numpy(rank).to(c.device)
-    return lut.index_select(0, c.data.long())
+    return gather_tensor(lut, c.data)
 
 
 def group_codes(col: Column) -> Tuple[torch.Tensor, Column]:

@@ -66,6 +66,7 @@ class Communicator:
     def shutdown(self):
         if dist.is_initialized():
             try:
+                self.calls += 1
                 dist.barrier()
             except Exception:  # pragma: no cover
                 pass
@@ -79,6 +80,7 @@ class Communicator:
         if faults.ACTIVE:
             faults.check("comm_timeout", "barrier")
         if self.world_size > 1:
+            self.calls += 1
             dist.barrier(group=self.group)
 
     def allreduce_int(self, x: int) -> int:
@@ -87,6 +89,7 @@ class Communicator:
         if self.world_size == 1:
             return int(x)
         t = self._t([int(x)])
+        self.calls += 1
         dist.all_reduce(t, group=self.group)
         return int(t.item())
 
@@ -96,6 +99,7 @@ class Communicator:
         if self.world_size == 1:
             return [int(x) for x in xs]
         t = self._t([int(x) for x in xs])
+        self.calls += 1
         dist.all_reduce(t, group=self.group)
         return [int(v) for v in t.tolist()]
 
@@ -105,6 +109,7 @@ class Communicator:
         if self.world_size == 1:
             return float(x)
         t = self._t([float(x)], torch.float64)
+        self.calls += 1
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
@@ -115,8 +120,24 @@ class Communicator:
         if self.world_size == 1:
             return t
         w = t.to(device=self.wire, dtype=torch.int32)
+        self.calls += 1
         dist.all_reduce(w, op=dist.ReduceOp.MAX, group=self.group)
         return w.to(device=t.device, dtype=t.dtype)
+
+    def allreduce_tensor(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """Element-wise SUM / MIN / MAX over ranks of an int64 / float64 tensor."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allreduce_tensor")
+        if self.world_size == 1:
+            return t
+        w = t.contiguous().to(self.wire)
+        if w is t:
+            w = w.clone()
+        self.calls += 1
+        dist.all_reduce(w, op={"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op],
+                        group=self.group)
+        self.bytes_sent += w.numel() * w.element_size()
+        return w.to(t.device)
 
     def allgather_ints(self, xs: Sequence[int]) -> List[List[int]]:
         """Every rank contributes len(xs) ints; returns [rank][i]."""
@@ -127,6 +148,7 @@ class Communicator:
             return [list(map(int, xs))]
         t = self._t([int(x) for x in xs])
         out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.wire)
+        self.calls += 1
         dist.all_gather_into_tensor(out, t, group=self.group)
         v = out.tolist()
         return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
@@ -137,6 +159,7 @@ class Communicator:
         if self.world_size == 1:
             return [obj]
         out = [None] * self.world_size
+        self.calls += 1
         dist.all_gather_object(out, obj, group=self.group)
         return out
 
@@ -157,8 +180,8 @@ class Communicator:
         if src.dtype == torch.bool:
             src = src.view(torch.uint8)
             out = out.view(torch.uint8)
-        dist.all_to_all_single(out, src, list(map(int, recv_counts)), list(map(int, send_counts)), group=self.group)
         self.calls += 1
+        dist.all_to_all_single(out, src, list(map(int, recv_counts)), list(map(int, send_counts)), group=self.group)
         self.bytes_sent += src.numel() * src.element_size()
         if t.dtype == torch.bool:
             out = out.view(torch.bool)
@@ -170,11 +193,31 @@ class Communicator:
         W = self.world_size
         s = self._t(list(send_counts))
         r = torch.empty(W, dtype=torch.int64, device=self.wire)
+        self.calls += 1
         dist.all_to_all_single(r, s, group=self.group)
         return [int(x) for x in r.tolist()]
 
+    def all_to_all_matrix(self, rows: Sequence[Sequence[int]]) -> List[List[int]]:
+        """rows[r] = k ints for peer r; returns [r][k] received from every peer
+        (row counts and string byte counts of a shuffle in ONE exchange)."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "all_to_all_counts")
+        W = self.world_size
+        k = len(rows[0]) if rows else 0
+        if W == 1:
+            return [list(map(int, r)) for r in rows]
+        s = self._t([int(x) for r in rows for x in r])
+        r = torch.empty(W * k, dtype=torch.int64, device=self.wire)
+        self.calls += 1
+        dist.all_to_all_single(r, s, group=self.group)
+        v = r.tolist()
+        return [v[i * k:(i + 1) * k] for i in range(W)]
+
     def all_gather_v(self, t: torch.Tensor, counts: Optional[List[int]] = None) -> Tuple[torch.Tensor, List[int]]:
-        """Concatenate every rank's ``t`` (variable row counts) on every rank."""
+        """Concatenate every rank's ``t`` (variable row counts) on every rank.
+        Equal counts: one native all-gather. Otherwise grouped point-to-point
+        sends of the SAME source buffer to every peer (one ncclSend per xGMI
+        link, no W-fold staging copy), received straight into the output."""
         if faults.ACTIVE:
             faults.check("comm_timeout", "all_gather_v")
         W = self.world_size
@@ -182,18 +225,50 @@ class Communicator:
             return t, [t.shape[0]]
         if counts is None:
             counts = [c[0] for c in self.allgather_ints([t.shape[0]])]
-        # all-to-all with the same payload to every peer = all-gather-v on a
-        # point-to-point mesh (every peer pulls over its own xGMI link)
-        src = t.contiguous()
-        send = torch.cat([src] * W) if src.numel() else src.reshape((0,) + tuple(src.shape[1:]))
-        out, _ = self.all_to_all_v(send, [src.shape[0]] * W, counts)
-        return out, counts
+        tail = tuple(t.shape[1:])
+        src = t.contiguous().to(self.wire)
+        if src.dtype == torch.bool:
+            src = src.view(torch.uint8)
+        out = torch.empty((sum(counts),) + tail, dtype=src.dtype, device=self.wire)
+        self.bytes_sent += src.numel() * src.element_size() * (W - 1)
+        if all(c == counts[0] for c in counts):
+            if counts[0]:
+                self.calls += 1
+                dist.all_gather_into_tensor(out, src, group=self.group)
+        else:
+            offs = [0]
+            for c in counts:
+                offs.append(offs[-1] + c)
+            ops = []
+            for r in range(W):
+                if r == self.rank:
+                    if counts[r]:
+                        out[offs[r]:offs[r + 1]].copy_(src)
+                    continue
+                if src.shape[0]:
+                    ops.append(dist.P2POp(dist.isend, src, self._peer(r), group=self.group))
+                if counts[r]:
+                    ops.append(dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], self._peer(r), group=self.group))
+            if ops:
+                self.calls += 1
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+        if t.dtype == torch.bool:
+            out = out.view(torch.bool)
+        return out.to(t.device), counts
+
+    def _peer(self, r: int) -> int:
+        """Global rank of group member ``r`` (P2P ops address global ranks)."""
+        if self.group is None:
+            return r
+        return dist.get_global_rank(self.group, r)
 
     def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if faults.ACTIVE:
             faults.check("comm_timeout", "broadcast_tensor")
         if self.world_size > 1:
             w = t.to(self.wire)
+            self.calls += 1
             dist.broadcast(w, src, group=self.group)
             if w is not t:
                 t.copy_(w)

@@ -31,6 +31,7 @@ import torch
 
 from .. import types as T
 from ..columnar import Batch, Column
+from ..ops.gather import gather_tensor
 from ..ops import misc as M
 from ..ops import strings as S
 from ..ops.gather import take_many
@@ -60,7 +61,7 @@ def partition_keys(c: Column) -> torch.Tensor:
     if c.dtype.is_string:
         if c.is_dict:
             dh = S.hash64(c.dictionary)
-            k = dh.index_select(0, c.data.long())
+            k = gather_tensor(dh, c.data)
         else:
             k = S.hash64(c)
         if c.valid is not None:
@@ -80,36 +81,52 @@ def partition_keys(c: Column) -> torch.Tensor:
 
 
 # -------------------------------------------------------------- dictionary sync
-_DICT_OK: Dict[int, object] = {}
+def _dict_digest(d: Column) -> int:
+    """Order-sensitive 63-bit digest of a dictionary's values (cached on it)."""
+    h = d._unified
+    if h is None:
+        import hashlib
+        hh = hashlib.blake2b(digest_size=8)
+        for v in d.to_arrow().to_pylist():
+            hh.update(b"\x00" if v is None else (v.encode() + b"\x01"))
+        h = int.from_bytes(hh.digest(), "little") >> 1
+        d._unified = h
+    return h
+
+
+def unify_dictionaries(cols: List[Column], comm, digests=None) -> List[Column]:
+    """Make the codes of every dictionary column meaningful on every rank.
+    One tiny all-gather of content digests for ALL dictionary columns (or the
+    caller's, ``digests[rank][j]`` for the j-th dictionary column); only a
+    column whose dictionaries differ between ranks gathers them (as a plain
+    string column: offsets + bytes over the device collectives, no pickling)
+    and re-codes through the union built on the device."""
+    idx = [i for i, c in enumerate(cols) if c.is_dict]
+    if not idx:
+        return cols
+    if digests is None:
+        digests = comm.allgather_ints([_dict_digest(cols[i].dictionary) for i in idx])
+    out = list(cols)
+    for j, i in enumerate(idx):
+        if all(d[j] == digests[0][j] for d in digests):
+            continue
+        c = cols[i]
+        d = c.dictionary
+        # same structure on every rank for the packed gather: plain, no validity
+        mine = Column(T.UTF8, d.data, None, offsets=d.offsets) if d.is_plain_string else \
+            Column(T.UTF8, S.decode(d).data, None, offsets=S.decode(d).offsets)
+        counts = [x[0] for x in comm.allgather_ints([len(mine)])]
+        every = _gather_column(mine, counts, comm)      # concatenation of all ranks' dictionaries
+        enc = S.dict_encode(every)                      # union: codes into a deduplicated dictionary
+        start = sum(counts[:comm.rank])
+        remap = enc.data[start:start + len(mine)].to(torch.int32)
+        codes = gather_tensor(remap, c.data) if len(mine) else c.data
+        out[i] = Column(T.UTF8, codes, c.valid, dictionary=enc.dictionary)
+    return out
 
 
 def unify_dictionary(c: Column, comm) -> Column:
-    """Make a dictionary column's codes meaningful on every rank."""
-    key = id(c.dictionary)
-    if _DICT_OK.get(key) is c.dictionary:
-        flag = 1
-    else:
-        flag = 0
-    flags = comm.allgather_ints([flag])
-    if all(f[0] == 1 for f in flags):
-        return c
-    vals = c.dict_values()
-    every = comm.allgather_object(vals)
-    if all(v == every[0] for v in every):
-        _DICT_OK[key] = c.dictionary
-        return c
-    union, index = [], {}
-    for vs in every:
-        for v in vs:
-            if v not in index:
-                index[v] = len(union)
-                union.append(v)
-    remap = torch.tensor([index[v] for v in vals] or [0], dtype=torch.int32, device=c.device)
-    codes = remap.index_select(0, c.data.long()) if len(vals) else c.data
-    d = Column.from_arrow(pa.array(union, pa.large_string()), device=c.device, dict_encode=False)
-    out = Column(T.UTF8, codes, c.valid, dictionary=d)
-    _DICT_OK[id(d)] = d
-    return out
+    return unify_dictionaries([c], comm)[0]
 
 
 # ------------------------------------------------------ structural agreement
@@ -117,98 +134,183 @@ def _sig(c: Column) -> tuple:
     return (c.valid is not None, c.is_dict, c.is_plain_string, c.is_wide)
 
 
-def normalize_structure(b: Batch, comm) -> Batch:
+def normalize_structure(b: Batch, comm, extra: Sequence[int] = ()) -> Batch:
     """Make every rank's columns structurally identical (validity present,
-    dictionary vs plain strings, 64- vs 128-bit decimals) so the per-column
-    collectives that follow line up across ranks."""
+    dictionary vs plain strings, 64- vs 128-bit decimals) so the packed
+    collectives that follow line up across ranks, and give dictionary columns
+    one shared code space. ONE all-gather carries every column's structure
+    bits, every dictionary's content digest and the caller's ``extra`` ints
+    (e.g. row counts); they come back as ``b.preamble[rank]``."""
     keys = list(b.columns)
-    if not keys:
-        return b
-    bits = [sum(int(f) << i for i, f in enumerate(_sig(b.columns[k]))) for k in keys]
-    sigs = comm.allgather_ints(bits)  # one tiny all-gather for all columns
-    if all(s == sigs[0] for s in sigs):
-        return b
+    cols = [b.columns[k] for k in keys]
+    bits = [sum(int(f) << i for i, f in enumerate(_sig(c))) for c in cols]
+    digs = [_dict_digest(c.dictionary) if c.is_dict else 0 for c in cols]
+    rows = comm.allgather_ints(list(extra) + bits + digs)
+    ne, nk = len(extra), len(keys)
+    sigs = [r[ne:ne + nk] for r in rows]
     out = {}
     for j, k in enumerate(keys):
-        c = b.columns[k]
-        any_valid = any(s[j] & 1 for s in sigs)
-        any_plain = any(s[j] & 4 for s in sigs)
-        any_wide = any(s[j] & 8 for s in sigs)
-        if any_plain and c.is_dict:
-            c = S.decode(c)
-        if any_wide and not c.is_wide and c.dtype.is_decimal:
-            c = Column(c.dtype, torch.stack([c.data, c.data >> 63], 1), c.valid)
-        if any_valid and c.valid is None:
-            c = Column(c.dtype, c.data, torch.ones(len(c), dtype=torch.bool, device=c.device), c.offsets, c.dictionary)
+        c = cols[j]
+        if any(s[j] != sigs[0][j] for s in sigs):
+            any_valid = any(s[j] & 1 for s in sigs)
+            any_plain = any(s[j] & 4 for s in sigs)
+            any_wide = any(s[j] & 8 for s in sigs)
+            if any_plain and c.is_dict:
+                c = S.decode(c)
+            if any_wide and not c.is_wide and c.dtype.is_decimal:
+                c = Column(c.dtype, torch.stack([c.data, c.data >> 63], 1), c.valid)
+            if any_valid and c.valid is None:
+                c = Column(c.dtype, c.data, torch.ones(len(c), dtype=torch.bool, device=c.device), c.offsets,
+                           c.dictionary)
         out[k] = c
-    return Batch(out, b.num_rows, b.dist)
+    # dictionary columns that stayed dictionary-coded everywhere
+    dict_js = [j for j in range(nk) if out[keys[j]].is_dict]
+    if dict_js:
+        digests = [[r[ne + nk + j] for j in dict_js] for r in rows]
+        unified = unify_dictionaries([out[keys[j]] for j in dict_js], comm, digests)
+        for j, c in zip(dict_js, unified):
+            out[keys[j]] = c
+    nb = Batch(out, b.num_rows, b.dist)
+    nb.preamble = [r[:ne] for r in rows]
+    return nb
 
 
 # --------------------------------------------------------------------- shuffle
-def _exchange_column(c: Column, send: List[int], recv: List[int], comm) -> Column:
-    valid = None
-    if c.valid is not None:
-        valid, _ = comm.all_to_all_v(c.valid, send, recv)
-    if c.is_plain_string:
-        lens = (c.offsets[1:] - c.offsets[:-1]).contiguous()
-        rlens, _ = comm.all_to_all_v(lens, send, recv)
-        # bytes per destination = sum of row lengths in each destination range
-        bounds = np.cumsum([0] + list(send))
-        offs = c.offsets.index_select(0, torch.as_tensor(bounds, device=c.device)).tolist()
-        bsend = [offs[i + 1] - offs[i] for i in range(len(send))]
-        chars, _ = comm.all_to_all_v(c.data, bsend)
-        off = torch.zeros(rlens.numel() + 1, dtype=torch.int64, device=c.device)
-        off[1:] = torch.cumsum(rlens, 0)
-        return Column(c.dtype, chars, valid, offsets=off)
-    if c.is_dict:
-        c = unify_dictionary(c, comm)
-        codes, _ = comm.all_to_all_v(c.data, send, recv)
-        return Column(c.dtype, codes, valid, dictionary=c.dictionary)
-    data, _ = comm.all_to_all_v(c.data, send, recv)
-    return Column(c.dtype, data, valid, dictionary=c.dictionary)
+def _fixed_parts(cols: List[Column]):
+    """Per column the tensors that travel packed in one row matrix:
+    validity bytes, dictionary codes / values, plain-string row lengths."""
+    tensors, spec = [], []
+    for c in cols:
+        vi = None
+        if c.valid is not None:
+            vi = len(tensors)
+            tensors.append(c.valid)
+        di = len(tensors)
+        if c.is_plain_string:
+            tensors.append((c.offsets[1:] - c.offsets[:-1]).contiguous())
+        else:
+            tensors.append(c.data)
+        spec.append((di, vi))
+    return tensors, spec
+
+
+def _rebuild(cols: List[Column], spec, parts: List[torch.Tensor], chars: Dict[int, torch.Tensor]) -> List[Column]:
+    out = []
+    for j, (c, (di, vi)) in enumerate(zip(cols, spec)):
+        valid = parts[vi] if vi is not None else None
+        if c.is_plain_string:
+            lens = parts[di]
+            off = torch.zeros(lens.numel() + 1, dtype=torch.int64, device=lens.device)
+            if lens.numel():
+                from ..ops.select import exclusive_scan
+                ex, total = exclusive_scan(lens)
+                off[:-1] = ex
+                off[-1] = total
+            out.append(Column(c.dtype, chars[j], valid, offsets=off))
+        else:
+            out.append(Column(c.dtype, parts[di], valid, dictionary=c.dictionary))
+    return out
 
 
 def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
-    """Hash-repartition rows of ``b`` by ``key`` across all ranks."""
+    """Hash-repartition rows of ``b`` by ``key`` across all ranks.
+
+    Collectives: one all-to-all of the [rank x (rows, string bytes...)] count
+    matrix, ONE all-to-all-v of every fixed-width column packed row-wise
+    (gathered into destination order by the pack kernel itself), and one
+    all-to-all-v of bytes per plain-string column."""
+    from ..ops.gather import take
+    from ..ops.pack import pack_rows, unpack_rows
     comm = ctx.comm
     W = comm.world_size
     b = normalize_structure(b, comm)
     perm, send = M.hash_partition(key, W)
     keys = list(b.columns)
-    cols = take_many([b.columns[k] for k in keys], perm) if keys else []
-    recv = comm.all_to_all_counts(send)
-    out = {k: _exchange_column(c, send, recv, comm) for k, c in zip(keys, cols)}
+    cols = [b.columns[k] for k in keys]
+    tensors, spec = _fixed_parts(cols)
+    # string bytes per destination (strings gathered into destination order)
+    bounds = np.cumsum([0] + list(send)).tolist()
+    sgath, sbytes = {}, []
+    for j, c in enumerate(cols):
+        if c.is_plain_string:
+            g = take(c, perm)
+            sgath[j] = g
+            offs = g.offsets.index_select(0, torch.as_tensor(bounds, device=g.offsets.device)).tolist()
+            sbytes.append([offs[r + 1] - offs[r] for r in range(W)])
+    mat = [[send[r]] + [sb[r] for sb in sbytes] for r in range(W)]
+    rmat = comm.all_to_all_matrix(mat)
+    recv = [r[0] for r in rmat]
+    parts: List[torch.Tensor] = []
+    if tensors:
+        packed, lay = pack_rows(tensors, perm, b.num_rows)
+        rpacked, _ = comm.all_to_all_v(packed, send, recv)
+        parts = unpack_rows(rpacked, lay, tensors)
+    chars = {}
+    for k, (j, g) in enumerate(sgath.items()):
+        chars[j], _ = comm.all_to_all_v(g.data, sbytes[k], [r[1 + k] for r in rmat])
+    out = dict(zip(keys, _rebuild(cols, spec, parts, chars)))
     return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
 
 
 def _gather_column(c: Column, counts: List[int], comm) -> Column:
-    valid = None
-    if c.valid is not None:
-        valid, _ = comm.all_gather_v(c.valid, counts)
-    if c.is_plain_string:
-        lens = (c.offsets[1:] - c.offsets[:-1]).contiguous()
-        rl, _ = comm.all_gather_v(lens, counts)
-        chars, _ = comm.all_gather_v(c.data)
-        off = torch.zeros(rl.numel() + 1, dtype=torch.int64, device=c.device)
-        off[1:] = torch.cumsum(rl, 0)
-        return Column(c.dtype, chars, valid, offsets=off)
-    if c.is_dict:
-        c = unify_dictionary(c, comm)
-        codes, _ = comm.all_gather_v(c.data, counts)
-        return Column(c.dtype, codes, valid, dictionary=c.dictionary)
-    data, _ = comm.all_gather_v(c.data, counts)
-    return Column(c.dtype, data, valid, dictionary=c.dictionary)
+    """All-gather of one column (dictionaries must already agree)."""
+    return _gather_columns([c], counts, comm)[0]
+
+
+def _str_bytes(c: Column) -> int:
+    return int(c.data.numel())
+
+
+def _gather_columns(cols: List[Column], counts: List[int], comm,
+                    str_bytes: Optional[List[List[int]]] = None) -> List[Column]:
+    """All-gather of columns with agreeing structure: one packed all-gather-v
+    of the fixed-width parts and ONE all-gather-v of every plain-string
+    column's bytes concatenated (``str_bytes[rank][k]``: byte count of the
+    k-th string column per rank, exchanged here when not given)."""
+    from ..ops.pack import pack_rows, unpack_rows
+    n = len(cols[0]) if cols else 0
+    tensors, spec = _fixed_parts(cols)
+    parts: List[torch.Tensor] = []
+    if tensors:
+        packed, lay = pack_rows(tensors, None, n)
+        rpacked, _ = comm.all_gather_v(packed, counts)
+        parts = unpack_rows(rpacked, lay, tensors)
+    sj = [j for j, c in enumerate(cols) if c.is_plain_string]
+    chars = {}
+    if sj:
+        if str_bytes is None:
+            str_bytes = comm.allgather_ints([_str_bytes(cols[j]) for j in sj])
+        local = cols[sj[0]].data if len(sj) == 1 else torch.cat([cols[j].data for j in sj])
+        allb, _ = comm.all_gather_v(local, [sum(r) for r in str_bytes])
+        pieces = {j: [] for j in sj}
+        pos = 0
+        for r in range(len(str_bytes)):
+            for k, j in enumerate(sj):
+                pieces[j].append(allb[pos:pos + str_bytes[r][k]])
+                pos += str_bytes[r][k]
+        for j in sj:
+            chars[j] = pieces[j][0] if len(pieces[j]) == 1 else torch.cat(pieces[j])
+    return _rebuild(cols, spec, parts, chars)
 
 
 def gather_all(b: Batch, ctx) -> Batch:
-    """Every rank receives the concatenation of all ranks' rows."""
+    """Every rank receives the concatenation of all ranks' rows (one packed
+    all-gather-v for the fixed-width columns)."""
     comm = ctx.comm
     if comm is None or comm.world_size == 1 or dist_of(b) == REPLICATED:
         return b
-    b = normalize_structure(b, comm)
-    counts = [c[0] for c in comm.allgather_ints([b.num_rows])]
     keys = list(b.columns)
-    out = {k: _gather_column(b.columns[k], counts, comm) for k in keys}
+    # string byte counts ride along in the preamble (-1: not a plain string
+    # here; same length on every rank)
+    pre = [b.num_rows] + [_str_bytes(b.columns[k]) if b.columns[k].is_plain_string else -1 for k in keys]
+    b = normalize_structure(b, comm, pre)
+    counts = [p[0] for p in b.preamble]
+    cols = [b.columns[k] for k in keys]
+    sj = [j for j, c in enumerate(cols) if c.is_plain_string]
+    sb = [[p[1 + j] for j in sj] for p in b.preamble]
+    if any(x < 0 for r in sb for x in r):
+        sb = None   # a dictionary column was decoded by normalisation: exchange its byte counts
+    out = dict(zip(keys, _gather_columns(cols, counts, comm, sb))) if keys else {}
     return with_dist(Batch(out, sum(counts)), REPLICATED)
 
 
@@ -217,15 +319,19 @@ def _cid(e: Expr):
     return e.cid if isinstance(e, ColRef) else None
 
 
-def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx):
+def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[int, int]] = None):
     """Move rows so the join can run rank-locally; returns (lb, rb) with the
-    output distribution stored in ``lb.out_dist``."""
+    output distribution stored in ``lb.out_dist``. ``rows``: the inputs'
+    global row counts when the caller already reduced them."""
     from ..exec.operators import _pair_key
     comm = ctx.comm
     kind, on = join.kind, join.on
     ld, rd = dist_of(lb), dist_of(rb)
     rep_l, rep_r = ld == REPLICATED, rd == REPLICATED
-    nl, nr = comm.allreduce_ints([lb.num_rows if not rep_l else 0, rb.num_rows if not rep_r else 0])
+    if rows is not None:
+        nl, nr = rows
+    else:
+        nl, nr = comm.allreduce_ints([lb.num_rows if not rep_l else 0, rb.num_rows if not rep_r else 0])
     if rep_l:
         nl = lb.num_rows
     if rep_r:
@@ -322,12 +428,16 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     pb = local(groups, partial) if local is not None else None
     if pb is None:
         pb = aggregate(groups, partial, b, ctx)
-    # ---- exchange partial states
-    if groups:
+    # ---- exchange partial states: all-reduce over a small dense key domain
+    # (global aggregates, dictionary-coded group keys) else hash shuffle
+    rb = _dense_allreduce(groups, partial, pb, ctx)
+    out_dist = REPLICATED if rb is not None else None
+    if rb is None and groups:
         g0 = groups[0][0]
         rb = shuffle(pb, partition_keys(pb.columns[g0.cid]), ctx, g0.cid)
-    else:
+    elif rb is None:
         rb = gather_all(pb, ctx)
+        out_dist = REPLICATED
     # ---- phase 2: merge
     fgroups = [(ci, ColRef(ci.cid, ci.name, ci.dtype, ci.nullable)) for ci, _ in groups]
     final, post = [], []
@@ -358,7 +468,112 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
         else:
             out[ci.cid] = fb.columns[ci.cid]
     res = Batch(out, fb.num_rows)
-    return with_dist(res, ("hash", groups[0][0].cid) if groups else REPLICATED)
+    return with_dist(res, out_dist if out_dist is not None else ("hash", groups[0][0].cid))
+
+
+#: largest dense group-key domain whose partial states are all-reduced
+DENSE_ALLREDUCE_MAX = 4096
+_I64_MAX, _I64_MIN = 2**63 - 1, -2**63
+
+
+def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
+    """Two-phase aggregation over a small dense key domain (no GROUP BY, or
+    dictionary-coded / boolean group keys whose dictionary sizes multiply to
+    at most DENSE_ALLREDUCE_MAX, e.g. TPC-H Q1's returnflag x linestatus):
+    every rank scatters its partial states into dense per-key arrays and ONE
+    all-reduce per reduction op (SUM / MIN / MAX) merges them — no shuffle,
+    and the result is replicated on every rank (so a following ORDER BY needs
+    no gather). Returns the merged partial-state batch or None when the shape
+    does not apply (128-bit sums, strings, large domains)."""
+    comm = ctx.comm
+    dev = ctx.device
+    cols = [pb.columns[ci.cid] for ci, _ in partial]
+    for (ci, a), c in zip(partial, cols):
+        if a.func not in ("sum", "count", "min", "max", "bool_and", "bool_or") or c.is_wide or c.dtype.is_string \
+                or c.data.dim() != 1:
+            return None
+    # group keys -> dense index (structure agreement first: every rank decides alike)
+    keys = [pb.columns[ci.cid] for ci, _ in groups]
+    if any(not (k.is_dict or k.dtype.kind == "bool") for k in keys):
+        return None
+    sig = comm.allgather_ints([int(k.valid is not None) for k in keys] + [int(pb.num_rows)])
+    nullable = [any(r[j] for r in sig) for j in range(len(keys))]
+    keys = unify_dictionaries(keys, comm) if keys else keys
+    sizes = [(len(k.dictionary) if k.is_dict else 2) + (1 if nullable[j] else 0) for j, k in enumerate(keys)]
+    domain = 1
+    for z in sizes:
+        domain *= max(z, 1)
+    if domain > DENSE_ALLREDUCE_MAX:
+        return None
+    n = pb.num_rows
+    idx = torch.zeros(n, dtype=torch.int64, device=dev)
+    for j, k in enumerate(keys):
+        code = k.data.to(torch.int64)
+        if nullable[j] and k.valid is not None:
+            code = torch.where(k.valid, code, torch.full_like(code, sizes[j] - 1))
+        idx = idx * sizes[j] + code
+    isum, fsum, imin, imax, fmin, fmax = [], [], [], [], [], []
+
+    def dense(vals, fill, dtype):
+        d = torch.full((domain,), fill, dtype=dtype, device=dev)
+        if n:
+            d.index_put_((idx,), vals.to(dtype), accumulate=False)
+        return d
+
+    presence = dense(torch.ones(n, dtype=torch.int64, device=dev), 0, torch.int64)
+    isum.append(presence)
+    slots = []
+    for (ci, a), c in zip(partial, cols):
+        isf = c.data.dtype in (torch.float32, torch.float64)
+        valid = c.valid if c.valid is not None else torch.ones(n, dtype=torch.bool, device=dev)
+        vcount = dense(valid.to(torch.int64), 0, torch.int64)
+        isum.append(vcount)
+        if a.func in ("sum", "count"):
+            v = torch.where(valid, c.data, torch.zeros_like(c.data))
+            lst = fsum if isf else isum
+            lst.append(dense(v, 0, torch.float64 if isf else torch.int64))
+        else:
+            is_min = a.func in ("min", "bool_and")
+            fill = (float("inf") if is_min else float("-inf")) if isf else (_I64_MAX if is_min else _I64_MIN)
+            v = torch.where(valid, c.data.to(torch.float64 if isf else torch.int64),
+                            torch.full((n,), fill, dtype=torch.float64 if isf else torch.int64, device=dev))
+            lst = (fmin if is_min else fmax) if isf else (imin if is_min else imax)
+            lst.append(dense(v, fill, torch.float64 if isf else torch.int64))
+        slots.append((lst, len(lst) - 1, len(isum) - 1))
+    red = {}
+    for name, lst, op in (("isum", isum, "sum"), ("fsum", fsum, "sum"), ("imin", imin, "min"), ("imax", imax, "max"),
+                          ("fmin", fmin, "min"), ("fmax", fmax, "max")):
+        if lst:
+            red[id(lst)] = comm.allreduce_tensor(torch.stack(lst), op)
+    present = mask_idx = None
+    tot = red[id(isum)]
+    from ..ops.select import mask_to_indices
+    mask_idx = mask_to_indices(tot[0] > 0)
+    m = mask_idx.numel()
+    out = {}
+    rest = mask_idx.to(torch.int64)
+    for j in range(len(keys) - 1, -1, -1):
+        code = rest % sizes[j]
+        rest = rest // sizes[j]
+        k = keys[j]
+        valid = None
+        if nullable[j]:
+            valid = code != sizes[j] - 1
+            code = torch.where(valid, code, torch.zeros_like(code))
+        ci = groups[j][0]
+        if k.is_dict:
+            out[ci.cid] = Column(k.dtype, code.to(torch.int32), valid, dictionary=k.dictionary)
+        else:
+            out[ci.cid] = Column(k.dtype, code.to(torch.bool), valid)
+    for ((ci, a), c), (lst, li, vi) in zip(zip(partial, cols), slots):
+        vals = gather_tensor(red[id(lst)][li], mask_idx)
+        has = gather_tensor(tot[vi], mask_idx) > 0
+        if a.func == "count":
+            out[ci.cid] = Column(c.dtype, vals.to(torch.int64))
+        else:
+            data = vals.to(c.data.dtype) if c.dtype.kind != "bool" else vals != 0
+            out[ci.cid] = Column(c.dtype, torch.where(has, data, torch.zeros_like(data)), has)
+    return Batch(out, m)
 
 
 def _sum_type(t):

@@ -42,7 +42,8 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
         try:
             from igloo_amd.models.tpch.oracle import normalize
             rows = [[normalize(v) for v in r.values()] for r in e.sql(Q.QUERIES[q]).table.to_pylist()]
-            res[q] = {"rows": rows}
+            res[q] = {"rows": rows, "collectives": e.last_metrics.get("collectives"),
+                      "bytes": e.last_metrics.get("exchange_bytes")}
         except Exception as ex:  # noqa: BLE001
             res[q] = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0:
@@ -60,6 +61,7 @@ def run_distributed(world, con, device="cpu", low_thresholds=False):
         mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs, device, low_thresholds), nprocs=world,
                            join=True, start_method="spawn")
         res = json.load(open(out))
+    run_distributed.last = res
     return check(res, qs, con)
 
 
@@ -68,6 +70,12 @@ def test_tpch_distributed_gloo(world, tpch_cpu):
     _, _, con = tpch_cpu
     bad = run_distributed(world, con)
     assert not bad, "\n".join(bad)
+    calls = {int(q): r["collectives"] for q, r in run_distributed.last.items()}
+    print("collectives per query:", calls)
+    # packed exchanges + dense all-reduce aggregation: Q1 (4 groups) merges its
+    # partial states with one all-reduce per op, Q6 (global sum) likewise
+    assert calls[1] <= 6 and calls[6] <= 4, calls
+    assert sum(calls.values()) <= 22 * 20, calls
 
 
 def check(res, qs, con):
