@@ -63,6 +63,19 @@ class Communicator:
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         return Communicator(dist.get_rank(), dist.get_world_size(), device, None, backend)
 
+    def abort(self):
+        """Tear the data communicator down without a collective (a peer died):
+        RCCL ops blocked on the dead rank return an error instead of waiting
+        for the collective timeout."""
+        if not dist.is_initialized():
+            return
+        try:
+            from torch.distributed import distributed_c10d as c10d
+            if hasattr(c10d, "_abort_process_group"):
+                c10d._abort_process_group(self.group or c10d.GroupMember.WORLD)
+        except Exception as e:  # noqa: BLE001 - gloo groups have no abort: TCP resets end their ops
+            log.warning("communicator abort: %s", e)
+
     def shutdown(self):
         if dist.is_initialized():
             try:

@@ -38,9 +38,18 @@ from . import protocol as P
 log = get_logger("worker")
 
 
+class GroupBroken(Exception):
+    """A rank of the SPMD group died or its communicator failed."""
+
+
 class WorkerGroup:
+    #: a follower whose in-group heartbeat is older than this is presumed dead
+    RANK_TIMEOUT_S = 3.0
+    RANK_HEARTBEAT_S = 0.5
+
     def __init__(self, engine, comm=None, coordinator: Optional[str] = None, host: str = "127.0.0.1",
-                 port: int = 50052, token: Optional[str] = None, heartbeat_s: float = 5.0):
+                 port: int = 50052, token: Optional[str] = None, heartbeat_s: float = 5.0,
+                 collective_timeout_s: float = 60.0):
         self.engine = engine
         self.comm = comm
         self.rank = comm.rank if comm else 0
@@ -54,11 +63,71 @@ class WorkerGroup:
         self._stop = threading.Event()
         self.server = None
         self.ctrl = None
+        self.status = None
+        self.broken: Optional[str] = None
+        self.exit_code = 0
         if self.world > 1:
             import torch.distributed as dist
             # control messages may wait for hours between queries: a CPU (gloo)
             # group with a long timeout, separate from the RCCL data group
             self.ctrl = dist.new_group(backend="gloo", timeout=timedelta(days=7))
+            # per-query status agreement: every rank reports success / its error
+            # after each SPMD query, bounded by the collective timeout
+            self.status = dist.new_group(backend="gloo", timeout=timedelta(seconds=collective_timeout_s))
+            self.store = dist.distributed_c10d._get_default_store()
+            threading.Thread(target=self._rank_heartbeat, daemon=True, name="igloo-rank-hb").start()
+            if self.rank == 0:
+                threading.Thread(target=self._watchdog, daemon=True, name="igloo-watchdog").start()
+
+    # ------------------------------------------------------- group liveness
+    def _rank_heartbeat(self):
+        """Every rank stamps its liveness into the group's rendezvous store."""
+        while not self._stop.is_set():
+            try:
+                self.store.set(f"igloo/hb/{self.rank}", repr(time.time()))
+            except Exception:  # noqa: BLE001 - rank 0 (the store host) is gone
+                if self.rank != 0:
+                    log.warning("rank %d: group store unreachable, exiting", self.rank)
+                    os._exit(3)
+                return
+            self._stop.wait(self.RANK_HEARTBEAT_S)
+
+    def _watchdog(self):
+        """Rank 0: a follower that stopped stamping is dead. The group is then
+        marked broken: its communicator is aborted (a collective blocked on the
+        dead rank errors out instead of hanging until the collective timeout),
+        the coordinator is no longer heartbeated (it evicts the group and
+        retries queries elsewhere) and the process exits non-zero once the
+        in-flight query has been answered with a retryable error."""
+        start = time.time()
+        while not self._stop.wait(self.RANK_HEARTBEAT_S):
+            now = time.time()
+            for r in range(1, self.world):
+                try:
+                    ts = float(self.store.get(f"igloo/hb/{r}").decode())
+                except Exception:  # noqa: BLE001 - not stamped yet
+                    ts = start
+                if now - ts > self.RANK_TIMEOUT_S:
+                    self._break(f"rank {r} stopped heartbeating ({now - ts:.1f}s)")
+                    return
+
+    def _break(self, why: str):
+        if self.broken:
+            return
+        self.broken = why
+        self.exit_code = 3
+        log.warning("worker group %s broken: %s", self.id, why)
+        if self.comm is not None:
+            self.comm.abort()
+        # answer the in-flight query first, then leave (no re-exec: a fresh process restarts us)
+        threading.Timer(2.0, self._stop.set).start()
+
+    def _agree(self, ok: bool, err: str):
+        """All ranks exchange (ok, error) after a query; returns the failures."""
+        import torch.distributed as dist
+        box = [None] * self.world
+        dist.all_gather_object(box, (self.rank, ok, err), group=self.status)
+        return [(r, e) for r, o, e in box if not o]
 
     # ---------------------------------------------------------------- SPMD
     def _bcast(self, obj=None):
@@ -71,32 +140,78 @@ class WorkerGroup:
         if faults.ACTIVE:
             faults.check("kill_worker")
             faults.check("fail_query", sql)
-        with self._lock:
-            if self.world > 1:
-                self._bcast(("query", sql))
-            return self.engine.query(sql)
+        return self._spmd(("query", sql), lambda: self.engine.query(sql))
 
     def run_spmd_fragment(self, payload: bytes) -> pa.Table:
         from ..parallel.fragments import run_encoded_fragment
+        return self._spmd(("fragment", payload), lambda: run_encoded_fragment(self.engine, payload))
+
+    def _spmd(self, cmd, fn) -> pa.Table:
+        """Rank 0: broadcast the command, run it, then agree with every rank on
+        the outcome. A rank-local failure (device fault on one GPU) or a broken
+        group surfaces as a retryable CommError / DeviceError; an error every
+        rank hit (bad SQL) is re-raised as is."""
+        from ..utils.errors import CommError, DeviceError, IglooError
         with self._lock:
-            if self.world > 1:
-                self._bcast(("fragment", payload))
-            return run_encoded_fragment(self.engine, payload)
+            if self.broken:
+                raise CommError(f"worker group broken: {self.broken}")
+            if self.world == 1:
+                return fn()
+            try:
+                self._bcast(cmd)
+            except Exception as e:  # noqa: BLE001
+                self._break(f"control broadcast failed: {e}")
+                raise CommError(f"worker group broken: {self.broken}") from None
+            res, err, exc = None, "", None
+            try:
+                res = fn()
+            except Exception as e:  # noqa: BLE001
+                exc, err = e, f"{type(e).__name__}: {e}"
+            if self.broken:
+                raise CommError(f"worker group broken: {self.broken}")
+            try:
+                failed = self._agree(exc is None, err)
+            except Exception as e:  # noqa: BLE001 - a rank died before reporting
+                self._break(f"status exchange failed: {e}")
+                raise CommError(f"worker group broken: {self.broken}") from None
+            if not failed:
+                return res
+            if exc is not None and len(failed) == self.world and isinstance(exc, IglooError) \
+                    and not isinstance(exc, (CommError, DeviceError)):
+                raise exc   # the query itself is wrong on every rank
+            raise DeviceError("query failed on rank(s) " + "; ".join(f"{r}: {e}" for r, e in failed))
 
     def follower_loop(self):
-        """Ranks > 0: execute whatever rank 0 broadcasts."""
+        """Ranks > 0: execute whatever rank 0 broadcasts, then report the outcome."""
         from ..parallel.fragments import run_encoded_fragment
         while True:
-            cmd = self._bcast()
+            try:
+                cmd = self._bcast()
+            except Exception as e:  # noqa: BLE001 - rank 0 is gone
+                log.warning("rank %d: control channel lost (%s), exiting", self.rank, e)
+                self.exit_code = 3
+                return
             if cmd[0] == "shutdown":
                 return
+            if faults.ACTIVE:
+                faults.check("kill_worker", f"rank{self.rank}")
+            ok, err = True, ""
             try:
                 if cmd[0] == "query":
+                    if faults.ACTIVE:
+                        faults.check("fail_query", f"rank{self.rank}:{cmd[1]}")
                     self.engine.query(cmd[1])
                 elif cmd[0] == "fragment":
                     run_encoded_fragment(self.engine, cmd[1])
-            except Exception as e:  # noqa: BLE001 - rank 0 reports the error to the client
-                log.warning("rank %d: %s failed: %s", self.rank, cmd[0], e)
+            except Exception as e:  # noqa: BLE001 - reported to rank 0 below
+                ok, err = False, f"{type(e).__name__}: {e}"
+                log.warning("rank %d: %s failed: %s", self.rank, cmd[0], err)
+            try:
+                self._agree(ok, err)
+            except Exception as e:  # noqa: BLE001
+                log.warning("rank %d: status exchange failed (%s), exiting", self.rank, e)
+                self.exit_code = 3
+                return
 
     # ------------------------------------------------------------- rank 0
     def devices(self) -> list:
@@ -136,7 +251,7 @@ class WorkerGroup:
     def heartbeat_loop(self):
         from .client import IglooClient
         while not self._stop.wait(self.heartbeat_s):
-            if faults.fire("drop_heartbeat", self.id):
+            if self.broken or faults.fire("drop_heartbeat", self.id):
                 continue
             try:
                 with IglooClient(self.coordinator, self.token, timeout=5) as c:
@@ -164,9 +279,12 @@ class WorkerGroup:
 
     def shutdown(self):
         self._stop.set()
-        if self.world > 1 and self.rank == 0:
+        if self.world > 1 and self.rank == 0 and not self.broken:
             with self._lock:
-                self._bcast(("shutdown",))
+                try:
+                    self._bcast(("shutdown",))
+                except Exception:  # noqa: BLE001
+                    pass
         if self.server is not None:
             self.server.shutdown()
 
@@ -193,7 +311,7 @@ def main(argv=None) -> int:
     comm = None
     if world > 1:
         from ..parallel.comm import Communicator
-        comm = Communicator.init(device=device, timeout_s=3600)
+        comm = Communicator.init(device=device, timeout_s=cfg.collective_timeout_s)
     engine = ig.QueryEngine(device=device, comm=comm)
     rank = comm.rank if comm else 0
     if a.tpch:
@@ -202,8 +320,12 @@ def main(argv=None) -> int:
             engine.register_table(name, t)
     register_config_tables(engine, cfg)
     wg = WorkerGroup(engine, comm, coord, cfg.worker_host, cfg.worker_port + (0 if rank == 0 else 0),
-                     cfg.auth_token, cfg.heartbeat_interval_s)
+                     cfg.auth_token, cfg.heartbeat_interval_s, cfg.collective_timeout_s)
     wg.serve()
+    if wg.exit_code:
+        # broken group: leave without collective teardown (a peer is gone)
+        sys.stdout.flush()
+        os._exit(wg.exit_code)
     if comm is not None:
         comm.shutdown()
     return 0

@@ -23,6 +23,8 @@ class IglooConfig:
     # liveness (reference worker heartbeats every 5 s, coordinator never evicts)
     heartbeat_interval_s: float = 5.0
     heartbeat_timeout_s: float = 15.0
+    # upper bound of any data collective inside a worker group (then the group is broken)
+    collective_timeout_s: float = 60.0
     # execution
     device: Optional[str] = None
     gpus_per_node: int = 8

@@ -186,3 +186,57 @@ def test_injected_faults_drive_eviction_and_retry():
         for p in ws:
             p.kill()
         co.shutdown()
+
+
+def _spawn_group_rank(coord, rank, world, port, fault=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, IGLOO_HEARTBEAT_INTERVAL_S="0.3", RANK=str(rank), LOCAL_RANK=str(rank),
+               WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               IGLOO_COLLECTIVE_TIMEOUT_S="20")
+    if fault:
+        env["IGLOO_FAULT"] = fault
+    return subprocess.Popen([sys.executable, "-m", "igloo_amd.service.worker", "--coordinator", coord, "--port", "0",
+                             "--tpch", "0.01", "--device", "cpu"], env=env, cwd=ROOT,
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+
+
+def test_rank_death_inside_group_fails_over_within_30s():
+    """SPMD recovery: rank 1 of a 2-rank worker group dies
+    mid-query (IGLOO_FAULT=kill_worker@rank1). Rank 0's collective fails
+    promptly, the group agrees the query failed and marks itself broken, the
+    coordinator quarantines it and reruns the query on the healthy group, and
+    the broken group's rank 0 exits non-zero instead of hanging."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    co = Coordinator(IglooConfig(coordinator_port=0, heartbeat_interval_s=0.3, heartbeat_timeout_s=1.5,
+                                 device="cpu")).start()
+    from igloo_amd.models.tpch import datagen
+    datagen.register(co.engine, 0.01)
+    group = [_spawn_group_rank(co.address, r, 2, port, fault="kill_worker@rank1") for r in range(2)]
+    healthy = None
+    try:
+        t0 = time.time()
+        while len(co.registry.alive()) < 1 and time.time() - t0 < 120:
+            time.sleep(0.2)
+        assert len(co.registry.alive()) == 1, [p.stdout.read1(4096) for p in group if p.poll() is not None]
+        healthy = _spawn_worker(co.address, 9)
+        while len(co.registry.alive()) < 2 and time.time() - t0 < 180:
+            time.sleep(0.2)
+        assert len(co.registry.alive()) == 2
+        sql = "SELECT count(*) AS n FROM lineitem"
+        t1 = time.time()
+        with IglooClient(co.address) as c:
+            assert c.query(sql).to_pylist()[0]["n"] == 59875
+        took = time.time() - t1
+        assert took < 30, took
+        outcomes = [o for (_, _, _, o) in co.executor.log]
+        assert outcomes[0].startswith("retry") and outcomes[-1] == "ok", co.executor.log
+        assert co.executor.log[-1][1] != "local"
+        assert group[1].wait(timeout=10) == 17          # the injected death
+        assert group[0].wait(timeout=20) == 3           # broken group left instead of hanging
+    finally:
+        for p in group + ([healthy] if healthy else []):
+            p.kill()
+        co.shutdown()
