@@ -520,60 +520,95 @@ __global__ __launch_bounds__(kBlock) void pq_dict_strings_kernel(const PqPage* _
   if (!ok && threadIdx.x == 0) set_error(s.error, PQ_ERR_BYTE_ARRAY);
 }
 
+// One wave per compressed page. Every lane reads the same tag bytes from the
+// LDS input window; the parse state (input / output positions, lengths,
+// offsets) is made wave-uniform with readfirstlane, so tag decoding and all
+// loop control are scalar (SALU + scalar branches) and the vector units only
+// move bytes. Literal bytes are copied from the window (an LDS read, not a
+// global load on the element's critical path); matches read the LDS history
+// ring and, for distances beyond it, the already written output (same wave:
+// a wait orders the read after our stores). Positions are 32-bit (a page is
+// < 2 GiB). The 16 KiB ring lets several pages decode per CU at once.
+constexpr int kSnapRingS = 16384;
+constexpr int kSnapInS = 2048;
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 __global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __restrict__ jobs,
                                                        const uint8_t* __restrict__ raw, uint8_t* __restrict__ dec,
                                                        int* __restrict__ err) {
-  __shared__ uint8_t ring[kSnapRing];
-  __shared__ uint8_t inw[kSnapIn];
+  __shared__ uint8_t ring[kSnapRingS];
+  __shared__ uint8_t inw[kSnapInS];
   const PqSnappyJob jb = jobs[blockIdx.x];
   const uint8_t* src = raw + jb.src_off;
-  const int64_t slen = jb.src_len;
+  const int slen = uni(jb.src_len);
   uint8_t* dst = dec + jb.dst_off;
-  const int64_t dlen = jb.dst_len;
+  const int dlen = uni(jb.dst_len);
   const int lane = threadIdx.x;
-  int64_t wbeg = 0, wend = 0;
+  int wbeg = 0, wend = 0;
 
-  auto refill = [&](int64_t at) {
+  auto refill = [&](int at) {
     __syncthreads();
     wbeg = at;
-    wend = slen < at + kSnapIn ? slen : at + kSnapIn;
-    for (int64_t k = lane; k < wend - wbeg; k += 64) inw[k] = src[wbeg + k];
+    wend = slen < at + kSnapInS ? slen : at + kSnapInS;
+    const int cnt = wend - wbeg;
+    if (((((uintptr_t)(src + wbeg)) & 3) == 0)) {
+      for (int k = 4 * lane; k < cnt; k += 256) {
+        if (k + 4 <= cnt) {
+          *reinterpret_cast<uint32_t*>(inw + k) = *reinterpret_cast<const uint32_t*>(src + wbeg + k);
+        } else {
+          for (int t = k; t < cnt; ++t) inw[t] = src[wbeg + t];
+        }
+      }
+    } else {
+      for (int k = lane; k < cnt; k += 64) inw[k] = src[wbeg + k];
+    }
     __syncthreads();
   };
+  auto byte_at = [&](int pos) -> uint32_t { return (uint32_t)uni(inw[pos - wbeg]); };
   auto fail = [&](int code) {
     if (lane == 0) set_error(err, code);
   };
   refill(0);
-  int64_t ip = 0;
-  uint64_t ulen = 0;
+  int ip = 0;
+  uint32_t ulen = 0;
   for (int sh = 0;; sh += 7) {
-    if (ip >= wend || sh > 35) return fail(PQ_ERR_SNAPPY);
-    const uint32_t b = inw[ip++ - wbeg];
-    ulen |= (uint64_t)(b & 0x7f) << sh;
+    if (ip >= wend || sh > 28) return fail(PQ_ERR_SNAPPY);
+    const uint32_t b = byte_at(ip++);
+    ulen |= (b & 0x7f) << sh;
     if (!(b & 0x80)) break;
   }
-  if ((int64_t)ulen != dlen) return fail(PQ_ERR_SNAPPY_SIZE);
-  int64_t op = 0;
+  if ((int)ulen != dlen) return fail(PQ_ERR_SNAPPY_SIZE);
+  int op = 0;
   while (ip < slen) {
     if (ip + 5 > wend && wend < slen) refill(ip);
-    const uint32_t tag = inw[ip - wbeg];
-    int64_t len, off;
+    const uint32_t tag = byte_at(ip);
+    int len, off;
     if ((tag & 3) == 0) {
-      len = (tag >> 2) + 1;
+      len = (int)(tag >> 2) + 1;
       ip += 1;
       if (len > 60) {
-        const int nb = (int)len - 60;
+        const int nb = len - 60;
         if (ip + nb > wend) return fail(PQ_ERR_SNAPPY);
-        len = 0;
-        for (int b = 0; b < nb; ++b) len |= (int64_t)inw[ip + b - wbeg] << (8 * b);
-        len += 1;
+        uint32_t l = 0;
+        for (int b = 0; b < nb; ++b) l |= byte_at(ip + b) << (8 * b);
+        len = (int)l + 1;
         ip += nb;
       }
-      if (ip + len > slen || op + len > dlen) return fail(PQ_ERR_SNAPPY);
-      for (int64_t k = lane; k < len; k += 64) {
-        const uint8_t v = src[ip + k];
-        dst[op + k] = v;
-        ring[(op + k) & (kSnapRing - 1)] = v;
+      len = uni(len);
+      if (len <= 0 || ip + len > slen || op + len > dlen) return fail(PQ_ERR_SNAPPY);
+      // copy the literal out of the input window, refilling for long ones
+      int done = 0;
+      while (done < len) {
+        if (ip + done >= wend) refill(ip + done);
+        const int avail = uni((wend - (ip + done)) < (len - done) ? (wend - (ip + done)) : (len - done));
+        const uint8_t* w = inw + (ip + done - wbeg);
+        for (int k = lane; k < avail; k += 64) {
+          const uint8_t v = w[k];
+          dst[op + done + k] = v;
+          ring[(op + done + k) & (kSnapRingS - 1)] = v;
+        }
+        done += avail;
       }
       ip += len;
       op += len;
@@ -582,25 +617,35 @@ __global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __rest
     const int kind = tag & 3;
     const int hdr = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
     if (ip + hdr > wend) return fail(PQ_ERR_SNAPPY);
-    const uint8_t* q = inw + (ip - wbeg);
     if (kind == 1) {
-      len = ((tag >> 2) & 7) + 4;
-      off = ((int64_t)(tag >> 5) << 8) | q[1];
+      len = (int)((tag >> 2) & 7) + 4;
+      off = (int)(((tag >> 5) << 8) | byte_at(ip + 1));
     } else if (kind == 2) {
-      len = (tag >> 2) + 1;
-      off = (int64_t)q[1] | ((int64_t)q[2] << 8);
+      len = (int)(tag >> 2) + 1;
+      off = (int)(byte_at(ip + 1) | (byte_at(ip + 2) << 8));
     } else {
-      len = (tag >> 2) + 1;
-      off = (int64_t)q[1] | ((int64_t)q[2] << 8) | ((int64_t)q[3] << 16) | ((int64_t)q[4] << 24);
+      len = (int)(tag >> 2) + 1;
+      const uint32_t o = byte_at(ip + 1) | (byte_at(ip + 2) << 8) | (byte_at(ip + 3) << 16) | (byte_at(ip + 4) << 24);
+      off = o > 0x7fffffffu ? 0 : (int)o;
     }
+    len = uni(len);
+    off = uni(off);
     ip += hdr;
-    if (off <= 0 || off > op || off >= kSnapRing || op + len > dlen) return fail(PQ_ERR_SNAPPY);
+    if (off <= 0 || off > op || op + len > dlen) return fail(PQ_ERR_SNAPPY);
     // len <= 64: one pass of the wave; an overlapping copy repeats the last `off` bytes
+    const int from = op - off + (off >= len ? lane : lane % off);
     uint8_t v = 0;
-    if (lane < len) v = ring[(op - off + (lane % off)) & (kSnapRing - 1)];
+    if (off + len <= kSnapRingS) {
+      if (lane < len) v = ring[from & (kSnapRingS - 1)];
+    } else {
+      // beyond the ring: our own earlier output (wait for this wave's stores)
+      __builtin_amdgcn_s_waitcnt(0);
+      __threadfence_block();
+      if (lane < len) v = __builtin_nontemporal_load(dst + from);
+    }
     if (lane < len) {
       dst[op + lane] = v;
-      ring[(op + lane) & (kSnapRing - 1)] = v;
+      ring[(op + lane) & (kSnapRingS - 1)] = v;
     }
     op += len;
   }

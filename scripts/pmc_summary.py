@@ -1,0 +1,78 @@
+"""Per-kernel counter / roofline table from scripts/pmc_passes.sh output.
+
+For every pass directory: counter_collection.csv (per dispatch counters) is
+joined with kernel_trace.csv (dispatch durations) on the dispatch id; per
+kernel name the counters are summed over dispatches. FETCH_SIZE / WRITE_SIZE
+(KB) over the summed kernel time give achieved HBM-side bandwidth, reported
+against the ~8 TB/s MI355X peak.
+
+usage: python scripts/pmc_summary.py gpurun_out/pmc [--top 15]
+"""
+import argparse
+import csv
+import glob
+import os
+import re
+from collections import defaultdict
+
+PEAK_GBS = 8000.0
+
+
+def short(n):
+    n = re.sub(r"\(anonymous namespace\)::", "", n)
+    n = re.sub(r"^void ", "", n)
+    return n.split("(")[0][:60]
+
+
+def load_pass(d):
+    cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not cc:
+        return {}, {}
+    dur = {}
+    for r in csv.DictReader(open(kt[0])) if kt else []:
+        dur[r.get("Dispatch_Id")] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    per = defaultdict(lambda: defaultdict(float))
+    seen = set()
+    time_ns = defaultdict(float)
+    for r in csv.DictReader(open(cc[0])):
+        k = short(r["Kernel_Name"])
+        per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        did = r.get("Dispatch_Id")
+        if did not in seen:
+            seen.add(did)
+            time_ns[k] += dur.get(did, 0)
+    return per, time_ns
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--top", type=int, default=15)
+    a = ap.parse_args()
+    counters = defaultdict(dict)
+    times = defaultdict(float)
+    for d in sorted(glob.glob(os.path.join(a.root, "p*"))):
+        if not os.path.isdir(d):
+            continue
+        per, tns = load_pass(d)
+        for k, cs in per.items():
+            counters[k].update(cs)
+            times[k] = max(times[k], tns.get(k, 0))
+    rows = sorted(times.items(), key=lambda kv: -kv[1])[:a.top]
+    print(f"{'kernel':60s} {'ms':>8s} {'fetch GB':>9s} {'write GB':>9s} {'GB/s':>8s} {'%peak':>6s} "
+          f"{'VALU/wave':>10s} {'LDS/wave':>9s} {'LDSconf':>8s} {'MFMA':>6s}")
+    for k, t in rows:
+        c = counters[k]
+        ms = t / 1e6
+        fetch = c.get("FETCH_SIZE", 0) / 1e6   # KB -> GB
+        write = c.get("WRITE_SIZE", 0) / 1e6
+        gbs = (fetch + write) / (ms / 1e3) if ms else 0
+        waves = max(c.get("SQ_WAVES", 1), 1)
+        print(f"{k:60s} {ms:8.2f} {fetch:9.3f} {write:9.3f} {gbs:8.0f} {100 * gbs / PEAK_GBS:6.1f} "
+              f"{c.get('SQ_INSTS_VALU', 0) / waves:10.0f} {c.get('SQ_INSTS_LDS', 0) / waves:9.0f} "
+              f"{c.get('SQ_LDS_BANK_CONFLICT', 0):8.0f} {c.get('SQ_INSTS_MFMA', 0):6.0f}")
+
+
+if __name__ == "__main__":
+    main()

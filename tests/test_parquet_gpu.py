@@ -136,3 +136,19 @@ def test_engine_query_over_gpu_parquet(tmp_path, gpu_device):
         b = mem.query(queries.QUERIES[q])
         assert a.to_pylist() == b.to_pylist(), q
     assert src.last_gpu_stats and not src.last_gpu_stats["host_columns"]
+
+
+def test_snappy_far_matches_beyond_lds_ring(tmp_path, gpu_device):
+    """Pages whose snappy stream copies from 16-60 KiB back (beyond the
+    kernel's LDS history ring): repeated 20-40 KB random blocks."""
+    rng = np.random.default_rng(7)
+    blocks = [bytes(rng.integers(97, 123, int(sz), dtype=np.uint8)) for sz in (20_000, 33_000, 41_000)]
+    vals = []
+    for i in range(60):
+        b = blocks[i % 3]
+        vals.append(b.decode() + f"-{i}")
+    t = pa.table({"s": pa.array(vals, pa.string()),
+                  "k": pa.array(np.tile(rng.integers(0, 2**40, 4096), 3), pa.int64())[:60]})
+    path = str(tmp_path / "far.parquet")
+    pq.write_table(t, path, compression="snappy", use_dictionary=False, data_page_size=1 << 20)
+    _check(path, t, gpu_device)
