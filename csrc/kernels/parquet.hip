@@ -520,17 +520,26 @@ __global__ __launch_bounds__(kBlock) void pq_dict_strings_kernel(const PqPage* _
   if (!ok && threadIdx.x == 0) set_error(s.error, PQ_ERR_BYTE_ARRAY);
 }
 
-// One wave per compressed page. Every lane reads the same tag bytes from the
-// LDS input window; the parse state (input / output positions, lengths,
-// offsets) is made wave-uniform with readfirstlane, so tag decoding and all
-// loop control are scalar (SALU + scalar branches) and the vector units only
-// move bytes. Literal bytes are copied from the window (an LDS read, not a
-// global load on the element's critical path); matches read the LDS history
-// ring and, for distances beyond it, the already written output (same wave:
-// a wait orders the read after our stores). Positions are 32-bit (a page is
-// < 2 GiB). The 16 KiB ring lets several pages decode per CU at once.
+// One wave per compressed page, decoding a BATCH of snappy elements per step:
+//   1. speculative parse: lane k assumes an element starts k bytes into the
+//      64-byte step window and computes its size, output length and offset
+//      from the LDS input window;
+//   2. scalar walk: starting at lane 0, the true element starts are chained
+//      with readlane (SALU), giving a 64-bit mask of element lanes;
+//   3. output offsets: wave prefix sum of the element lengths;
+//   4. copy: literals and matches whose source lies before the batch are
+//      independent -> every such lane copies its own element in parallel;
+//      matches that read output of this batch are then copied in order, each
+//      by the whole wave (64 bytes per step).
+// Back-references read a 16 KiB LDS history ring, or — beyond it — the
+// already written output (ordered after this wave's stores by a wait).
+// A literal too long for the window streams through it on its own. Page
+// sizes are < 2 GiB, so positions are 32-bit.
 constexpr int kSnapRingS = 16384;
-constexpr int kSnapInS = 2048;
+constexpr int kSnapInS = 4096;
+// a batch writes at most one window-sized literal plus 32 short matches:
+// independent ring reads closer than this never alias the batch's own writes
+constexpr int kSnapFarRing = kSnapRingS - kSnapInS - 2048 - 64;
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -538,13 +547,14 @@ __global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __rest
                                                        const uint8_t* __restrict__ raw, uint8_t* __restrict__ dec,
                                                        int* __restrict__ err) {
   __shared__ uint8_t ring[kSnapRingS];
-  __shared__ uint8_t inw[kSnapInS];
+  __shared__ uint8_t inw[kSnapInS + 8];
   const PqSnappyJob jb = jobs[blockIdx.x];
   const uint8_t* src = raw + jb.src_off;
   const int slen = uni(jb.src_len);
   uint8_t* dst = dec + jb.dst_off;
   const int dlen = uni(jb.dst_len);
   const int lane = threadIdx.x;
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   int wbeg = 0, wend = 0;
 
   auto refill = [&](int at) {
@@ -565,7 +575,6 @@ __global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __rest
     }
     __syncthreads();
   };
-  auto byte_at = [&](int pos) -> uint32_t { return (uint32_t)uni(inw[pos - wbeg]); };
   auto fail = [&](int code) {
     if (lane == 0) set_error(err, code);
   };
@@ -574,80 +583,147 @@ __global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __rest
   uint32_t ulen = 0;
   for (int sh = 0;; sh += 7) {
     if (ip >= wend || sh > 28) return fail(PQ_ERR_SNAPPY);
-    const uint32_t b = byte_at(ip++);
+    const uint32_t b = (uint32_t)uni(inw[ip++ - wbeg]);
     ulen |= (b & 0x7f) << sh;
     if (!(b & 0x80)) break;
   }
   if ((int)ulen != dlen) return fail(PQ_ERR_SNAPPY_SIZE);
   int op = 0;
   while (ip < slen) {
-    if (ip + 5 > wend && wend < slen) refill(ip);
-    const uint32_t tag = byte_at(ip);
-    int len, off;
-    if ((tag & 3) == 0) {
-      len = (int)(tag >> 2) + 1;
-      ip += 1;
-      if (len > 60) {
-        const int nb = len - 60;
-        if (ip + nb > wend) return fail(PQ_ERR_SNAPPY);
-        uint32_t l = 0;
-        for (int b = 0; b < nb; ++b) l |= byte_at(ip + b) << (8 * b);
-        len = (int)l + 1;
-        ip += nb;
+    if (ip + 128 > wend && wend < slen) refill(ip);
+    // ---- 1. speculative parse at ip + lane
+    const int P = ip + lane;                 // absolute input position of this lane's candidate
+    const int avail = wend - P;              // window bytes from P on
+    int sz = 1 << 30, olen = 0, off = 0, lsrc = 0;
+    bool lit = false;
+    if (avail > 0) {
+      const uint8_t* w = inw + (P - wbeg);
+      const uint32_t t = w[0];
+      const uint32_t b1 = avail > 1 ? w[1] : 0, b2 = avail > 2 ? w[2] : 0;
+      const uint32_t b3 = avail > 3 ? w[3] : 0, b4 = avail > 4 ? w[4] : 0;
+      const int kind = t & 3;
+      if (kind == 0) {
+        int L = (int)(t >> 2) + 1, hdr = 1;
+        if (L > 60) {
+          const int nb = L - 60;
+          uint32_t l = b1;
+          if (nb > 1) l |= b2 << 8;
+          if (nb > 2) l |= b3 << 16;
+          if (nb > 3) l |= b4 << 24;
+          L = (int)l + 1;
+          hdr = 1 + nb;
+        }
+        lit = true;
+        olen = L;
+        lsrc = P + hdr;
+        sz = (L > 0 && L < (1 << 29)) ? hdr + L : (1 << 30);
+      } else if (kind == 1) {
+        olen = (int)((t >> 2) & 7) + 4;
+        off = (int)(((t >> 5) << 8) | b1);
+        sz = 2;
+      } else if (kind == 2) {
+        olen = (int)(t >> 2) + 1;
+        off = (int)(b1 | (b2 << 8));
+        sz = 3;
+      } else {
+        olen = (int)(t >> 2) + 1;
+        const uint32_t o = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+        off = o > 0x7fffffffu ? 0 : (int)o;
+        sz = 5;
       }
-      len = uni(len);
-      if (len <= 0 || ip + len > slen || op + len > dlen) return fail(PQ_ERR_SNAPPY);
-      // copy the literal out of the input window, refilling for long ones
+      if (sz > avail) sz = 1 << 30;   // not entirely inside the window
+    }
+    // ---- 2. scalar walk over the true element starts
+    uint64_t starts = 0;
+    int pos = 0;
+    while (pos < 64) {
+      const int s = __builtin_amdgcn_readlane(sz, pos);
+      if (s >= (1 << 30) || ip + pos + s > slen) break;
+      starts |= 1ull << pos;
+      pos += s;
+    }
+    if (starts == 0) {
+      // the element at ip does not fit the window: a long literal, streamed
+      const uint32_t t = (uint32_t)uni(inw[ip - wbeg]);
+      if ((t & 3) != 0 || !uni((int)lit)) return fail(PQ_ERR_SNAPPY);
+      const int L = uni(olen), hdr = uni(lsrc) - ip;
+      if (L <= 0 || ip + hdr + L > slen || op + L > dlen) return fail(PQ_ERR_SNAPPY);
+      ip += hdr;
       int done = 0;
-      while (done < len) {
+      while (done < L) {
         if (ip + done >= wend) refill(ip + done);
-        const int avail = uni((wend - (ip + done)) < (len - done) ? (wend - (ip + done)) : (len - done));
+        const int av = uni((wend - (ip + done)) < (L - done) ? (wend - (ip + done)) : (L - done));
         const uint8_t* w = inw + (ip + done - wbeg);
-        for (int k = lane; k < avail; k += 64) {
+        for (int k = lane; k < av; k += 64) {
           const uint8_t v = w[k];
           dst[op + done + k] = v;
           ring[(op + done + k) & (kSnapRingS - 1)] = v;
         }
-        done += avail;
+        done += av;
       }
-      ip += len;
-      op += len;
+      ip += L;
+      op += L;
       continue;
     }
-    const int kind = tag & 3;
-    const int hdr = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
-    if (ip + hdr > wend) return fail(PQ_ERR_SNAPPY);
-    if (kind == 1) {
-      len = (int)((tag >> 2) & 7) + 4;
-      off = (int)(((tag >> 5) << 8) | byte_at(ip + 1));
-    } else if (kind == 2) {
-      len = (int)(tag >> 2) + 1;
-      off = (int)(byte_at(ip + 1) | (byte_at(ip + 2) << 8));
-    } else {
-      len = (int)(tag >> 2) + 1;
-      const uint32_t o = byte_at(ip + 1) | (byte_at(ip + 2) << 8) | (byte_at(ip + 3) << 16) | (byte_at(ip + 4) << 24);
-      off = o > 0x7fffffffu ? 0 : (int)o;
+    // ---- 3. output offsets of the element lanes
+    const bool is_el = (starts >> lane) & 1ull;
+    int mylen = is_el ? olen : 0;
+    int inc = mylen;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
     }
-    len = uni(len);
-    off = uni(off);
-    ip += hdr;
-    if (off <= 0 || off > op || op + len > dlen) return fail(PQ_ERR_SNAPPY);
-    // len <= 64: one pass of the wave; an overlapping copy repeats the last `off` bytes
-    const int from = op - off + (off >= len ? lane : lane % off);
-    uint8_t v = 0;
-    if (off + len <= kSnapRingS) {
-      if (lane < len) v = ring[from & (kSnapRingS - 1)];
-    } else {
-      // beyond the ring: our own earlier output (wait for this wave's stores)
+    const int total = __builtin_amdgcn_readlane(inc, 63);
+    const int o = op + inc - mylen;          // this element's output position
+    bool bad = is_el && (o + olen > dlen || (!lit && (off <= 0 || off > o)));
+    if (__ballot(bad)) return fail(PQ_ERR_SNAPPY);
+    // ---- 4a. independent elements, one lane each
+    const bool dep = is_el && !lit && (o - off + olen > op);
+    const bool far = is_el && !lit && !dep && off > kSnapFarRing;
+    if (__ballot(far)) {
       __builtin_amdgcn_s_waitcnt(0);
       __threadfence_block();
-      if (lane < len) v = __builtin_nontemporal_load(dst + from);
     }
-    if (lane < len) {
-      dst[op + lane] = v;
-      ring[(op + lane) & (kSnapRingS - 1)] = v;
+    if (is_el && !dep) {
+      if (lit) {
+        const uint8_t* w = inw + (lsrc - wbeg);
+        for (int b = 0; b < olen; ++b) {
+          const uint8_t v = w[b];
+          dst[o + b] = v;
+          ring[(o + b) & (kSnapRingS - 1)] = v;
+        }
+      } else if (!far) {
+        for (int b = 0; b < olen; ++b) {
+          const uint8_t v = ring[(o - off + b) & (kSnapRingS - 1)];
+          dst[o + b] = v;
+          ring[(o + b) & (kSnapRingS - 1)] = v;
+        }
+      } else {
+        for (int b = 0; b < olen; ++b) {
+          const uint8_t v = __builtin_nontemporal_load(dst + (o - off + b));
+          dst[o + b] = v;
+          ring[(o + b) & (kSnapRingS - 1)] = v;
+        }
+      }
     }
-    op += len;
+    // ---- 4b. elements that read this batch's output, in order, whole wave each
+    uint64_t deps = __ballot(dep);
+    while (deps) {
+      const int k = __builtin_ctzll(deps);
+      deps &= deps - 1;
+      const int eo = __builtin_amdgcn_readlane(o, k);
+      const int el = __builtin_amdgcn_readlane(olen, k);
+      const int eoff = __builtin_amdgcn_readlane(off, k);
+      if (lane < el) {
+        const int from = eo - eoff + (eoff >= el ? lane : lane % eoff);
+        const uint8_t v = ring[from & (kSnapRingS - 1)];
+        dst[eo + lane] = v;
+        ring[(eo + lane) & (kSnapRingS - 1)] = v;
+      }
+    }
+    ip += pos;
+    op += total;
   }
   if (op != dlen) fail(PQ_ERR_SNAPPY_SIZE);
 }

@@ -53,7 +53,7 @@ READ_THREADS = int(os.environ.get("IGLOO_PARQUET_READ_THREADS", str(min(16, os.c
 #: staged bytes per decode batch (pinned host buffer + one set of launches):
 #: small enough that the host reads batch i+1 while the GPU copies and
 #: decodes batch i, large enough that every launch fills the chip
-BATCH_BYTES = int(os.environ.get("IGLOO_PARQUET_BATCH_BYTES", str(1 << 30)))
+BATCH_BYTES = int(os.environ.get("IGLOO_PARQUET_BATCH_BYTES", str(256 << 20)))
 
 
 class FileMeta:
