@@ -291,7 +291,7 @@ PYBIND11_MODULE(_native, m) {
   using FfTerms = std::vector<std::tuple<int, int, int64_t, int64_t, uint64_t>>;
   using FfKeys = std::vector<std::tuple<int, int64_t, int64_t>>;
   using FfAggs = std::vector<std::tuple<int, int, std::vector<std::tuple<int64_t, int64_t, int64_t>>, uintptr_t,
-                                        uintptr_t, int>>;
+                                        uintptr_t, int, int>>;
   auto make_ff = [](const FfCols& cols, const FfTerms& terms, uintptr_t mask) {
     if (cols.size() > (size_t)kern::kFfMaxCols || terms.size() > (size_t)kern::kFfMaxTerms)
       throw std::runtime_error("fused scan: too many columns / terms");
@@ -338,7 +338,7 @@ PYBIND11_MODULE(_native, m) {
     f.ngroups = ngroups;
     f.naggs = (int32_t)aggs.size();
     for (size_t i = 0; i < aggs.size(); ++i) {
-      auto& [op, checked, facs, dst, dst2, shared] = aggs[i];
+      auto& [op, checked, facs, dst, dst2, shared, vbits] = aggs[i];
       if (op < 0 || op > 3 || facs.size() > (size_t)kern::kFfMaxFactors)
         throw std::runtime_error("fused aggregate: bad aggregate");
       if (shared < 0 || shared > (int)facs.size() || (shared > 0 && (i == 0 || f.aggs[i - 1].nfac != shared)))
@@ -355,11 +355,13 @@ PYBIND11_MODULE(_native, m) {
       }
       A.dst = P<int64_t>(dst);
       A.dst2 = P<int64_t>(dst2);
+      A.vbits = vbits > 0 && vbits < 64 ? vbits : 64;
     }
     f.counts = P<int64_t>(counts);
     f.overflow = P<int>(overflow);
     kern::ff_aggregate(f, n, S(s));
   });
+  m.def("ff_set_mfma", [](bool on) { return kern::ff_set_mfma(on); });
   m.attr("HLL_REGISTERS") = kern::kHllRegisters;
   m.def("hll_blocks", [](int64_t n) { return kern::hll_blocks(n); });
   m.def("hll_sketch", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t block_regs, uintptr_t regs,

@@ -345,6 +345,156 @@ __global__ __launch_bounds__(1024) void ff_agg_kernel(const FfSpec S, int64_t n,
   if (__any(ovf) && lane == 0 && S.overflow) atomicOr(S.overflow, 1);
 }
 
+// ---------------------------------------------------------------------------
+// One-hot MFMA aggregation (SUM / COUNT over <= 16 groups).
+//
+// A group-by SUM is a matrix product: D[g][c] += sum_k onehot[g][k] * x[k][c]
+// over rows k. Per 64 rows a wave builds
+//   A = one-hot of the rows' group ids (16 groups x 64 rows, int8 0/1) and
+//   B = the rows' aggregate values split into 7-bit limbs (64 rows x 16
+//       limb columns per tile, int8; the top limb of a value is signed),
+// and v_mfma_i32_16x16x64_i8 accumulates D (16 x 16 int32) — exact integer
+// sums with no atomics and no per-(row, aggregate) LDS traffic. A value of
+// w bits (bound from the factor column widths) takes ceil((w - 8) / 7) + 1
+// limbs; the row count is one more limb column of 1s.
+//
+// Fragment maps (gfx950, v_mfma_i32_16x16x64_i8): lane l holds
+// A[m = l & 15][k = 16 (l >> 4) + j] and B[k = 16 (l >> 4) + j][n = l & 15]
+// (j = 0..15, one byte each) and D[m = 4 (l >> 4) + i][n = l & 15] (i < 4).
+// Rows reach the fragments through LDS: lane r writes its gid byte and its
+// limb bytes column-major ([column][64 rows], 80-byte column stride against
+// bank conflicts), every lane then reads 16 consecutive bytes per operand.
+// int32 accumulators get at most 64 * 128 per step, so they are folded into
+// int64 every 2^14 steps; a block merges its waves and adds each (group,
+// aggregate) as int128 with two 64-bit atomics.
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int kMfmaCol = 80;                   // LDS bytes per limb column (64 rows + pad)
+constexpr int kMfmaMaxTiles = 4;               // <= 64 limb columns
+constexpr int kMfmaBlock = 256;
+
+struct FfMfmaLayout {
+  int32_t col0[kFfMaxAggs], nlimb[kFfMaxAggs];  // first limb column / limb count per aggregate (0 for COUNT)
+  int32_t count_col, ncols;
+};
+
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t g4) {
+  // 0x01 in each byte of x equal to the matching byte of g4, exactly
+  const uint32_t d = x ^ g4;
+  const uint32_t y = ~(((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d | 0x7f7f7f7fu);
+  return y >> 7;
+}
+
+template <int NC, int NT>
+__global__ __launch_bounds__(kMfmaBlock) void ff_mfma_agg_kernel(const FfSpec S, const FfMfmaLayout Lay, int64_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kMfmaBlock / kWave][NT * 16 * kMfmaCol + kMfmaCol];
+  __shared__ long long red[kMfmaBlock / kWave][NT * 16][16];
+  const int wave = ff_wave_uniform(threadIdx.x / kWave), lane = lane_id();
+  const int waves = kMfmaBlock / kWave;
+  uint8_t* T = tile[wave];
+  uint8_t* gidb = T + NT * 16 * kMfmaCol;
+  for (int i = lane; i < NT * 16 * kMfmaCol; i += kWave) T[i] = 0;   // unused limb columns stay 0
+  v4i acc[NT];
+  long long acc64[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    acc[t] = v4i{0, 0, 0, 0};
+    for (int i = 0; i < 4; ++i) acc64[t][i] = 0;
+  }
+  int ovf = 0, steps = 0;
+  const int NA = S.naggs;
+  const uint32_t g4 = (uint32_t)(lane & 15) * 0x01010101u;
+  const int q16 = 16 * (lane >> 4);
+  const int64_t per_iter = (int64_t)kWave * kFfRows;
+  const int64_t stride = (int64_t)gridDim.x * waves * per_iter;
+  for (int64_t base = ((int64_t)blockIdx.x * waves + wave) * per_iter; base < n; base += stride) {
+    const FfIter it = ff_iter(base, lane, n);
+    FF_LOAD_ROWS(NC, S, base, it.idx)
+    bool pass[kFfRows];
+    ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
+    int gid[kFfRows];
+    ff_gid4<ff_vw<NC>()>(S, r0, r1, r2, r3, gid);
+    // every aggregate's value for this lane's 4 rows (product chains reuse
+    // the previous aggregate's value, as in ff_agg_kernel)
+    int64_t vals[kFfMaxAggs][kFfRows];
+    int64_t val[kFfRows];
+#pragma unroll
+    for (int a = 0; a < kFfMaxAggs; ++a) {
+      if (a < NA && S.aggs[a].op != 1) {
+        ff_value4<ff_vw<NC>()>(S.aggs[a], r0, r1, r2, r3, val, &ovf);
+#pragma unroll
+        for (int j = 0; j < kFfRows; ++j) vals[a][j] = val[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) {
+      const bool on = it.live[j] && pass[j];
+      gidb[lane] = on ? (uint8_t)gid[j] : (uint8_t)0xff;
+#pragma unroll
+      for (int a = 0; a < kFfMaxAggs; ++a) {
+        if (a < NA && S.aggs[a].op != 1) {
+          const int64_t v = on ? vals[a][j] : 0;
+          const int c0 = Lay.col0[a], nl = Lay.nlimb[a];
+          for (int l = 0; l < nl; ++l) {
+            const int64_t limb = (l == nl - 1) ? (v >> (7 * l)) : ((v >> (7 * l)) & 127);
+            T[(c0 + l) * kMfmaCol + lane] = (uint8_t)(int8_t)limb;
+          }
+        }
+      }
+      T[Lay.count_col * kMfmaCol + lane] = (it.live[j] && pass[j]) ? 1 : 0;
+      __builtin_amdgcn_wave_barrier();
+      const uint4 gw = *reinterpret_cast<const uint4*>(gidb + q16);
+      v4i af;
+      af[0] = (int)bytes_eq(gw.x, g4);
+      af[1] = (int)bytes_eq(gw.y, g4);
+      af[2] = (int)bytes_eq(gw.z, g4);
+      af[3] = (int)bytes_eq(gw.w, g4);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const uint4 bw = *reinterpret_cast<const uint4*>(T + (16 * t + (lane & 15)) * kMfmaCol + q16);
+        const v4i bf = v4i{(int)bw.x, (int)bw.y, (int)bw.z, (int)bw.w};
+        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, acc[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (++steps == (1 << 14)) {
+        steps = 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i];
+          acc[t] = v4i{0, 0, 0, 0};
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i];
+  // D[m = 4 (lane >> 4) + i][n = lane & 15] of tile t -> red[wave][16 t + n][m]
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    for (int i = 0; i < 4; ++i) red[wave][16 * t + (lane & 15)][4 * (lane >> 4) + i] = acc64[t][i];
+  __syncthreads();
+  const int G = S.ngroups;
+  for (int s = threadIdx.x; s < G * (NA + 1); s += kMfmaBlock) {
+    const int g = s / (NA + 1), a = s % (NA + 1);
+    auto limb_sum = [&](int col) {
+      long long x = 0;
+      for (int w = 0; w < waves; ++w) x += red[w][col][g];
+      return x;
+    };
+    if (a == NA || S.aggs[a].op == 1) {
+      const long long c = limb_sum(Lay.count_col);
+      if (c) atomicAdd((unsigned long long*)(a == NA ? &S.counts[g] : &S.aggs[a].dst[g]), (unsigned long long)c);
+      continue;
+    }
+    __int128 tot = 0;
+    for (int l = 0; l < Lay.nlimb[a]; ++l) tot += (__int128)limb_sum(Lay.col0[a] + l) << (7 * l);
+    if (tot != 0)
+      atomic_add_i128_parts((unsigned long long*)&S.aggs[a].dst[g], (long long*)&S.aggs[a].dst2[g],
+                            (unsigned long long)(uint64_t)tot, (long long)(int64_t)(tot >> 64));
+  }
+  if (__any(ovf) && lane == 0 && S.overflow) atomicOr(S.overflow, 1);
+}
+
 }  // namespace
 
 template <int NC>
@@ -392,8 +542,64 @@ void ff_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream) {
   check_launch("ff_mask", stream);
 }
 
+static bool g_ff_mfma = [] {
+  const char* e = std::getenv("IGLOO_FF_MFMA");
+  return e ? std::atoi(e) != 0 : true;
+}();
+
+bool ff_set_mfma(bool on) {
+  const bool prev = g_ff_mfma;
+  g_ff_mfma = on;
+  return prev;
+}
+
+template <int NC>
+static void launch_mfma(const FfSpec& spec, const FfMfmaLayout& lay, int nt, int64_t n, hipStream_t stream) {
+  const unsigned grid = grid_for(n, kMfmaBlock * kFfRows * 8, 256 * 3);
+  switch (nt) {
+    case 1: hipLaunchKernelGGL((ff_mfma_agg_kernel<NC, 1>), dim3(grid), dim3(kMfmaBlock), 0, stream, spec, lay, n); break;
+    case 2: hipLaunchKernelGGL((ff_mfma_agg_kernel<NC, 2>), dim3(grid), dim3(kMfmaBlock), 0, stream, spec, lay, n); break;
+    case 3: hipLaunchKernelGGL((ff_mfma_agg_kernel<NC, 3>), dim3(grid), dim3(kMfmaBlock), 0, stream, spec, lay, n); break;
+    default: hipLaunchKernelGGL((ff_mfma_agg_kernel<NC, 4>), dim3(grid), dim3(kMfmaBlock), 0, stream, spec, lay, n); break;
+  }
+}
+
+// SUM / COUNT only, <= 16 groups, <= 64 limb columns: the one-hot MFMA path
+static bool try_mfma(const FfSpec& spec, int64_t n, hipStream_t stream) {
+  if (!g_ff_mfma || spec.ngroups > 16) return false;
+  FfMfmaLayout lay{};
+  int col = 0;
+  for (int a = 0; a < spec.naggs; ++a) {
+    const FfAgg& A = spec.aggs[a];
+    if (A.op != 0 && A.op != 1) return false;
+    if (A.op == 1) continue;
+    const int w = A.vbits > 0 && A.vbits <= 64 ? A.vbits : 64;
+    const int nl = w <= 8 ? 1 : (w - 8 + 6) / 7 + 1;
+    lay.col0[a] = col;
+    lay.nlimb[a] = nl;
+    col += nl;
+  }
+  lay.count_col = col++;
+  lay.ncols = col;
+  const int nt = (col + 15) / 16;
+  if (nt > kMfmaMaxTiles) return false;
+  switch (spec.ncols) {
+    case 1: launch_mfma<1>(spec, lay, nt, n, stream); break;
+    case 2: launch_mfma<2>(spec, lay, nt, n, stream); break;
+    case 3: launch_mfma<3>(spec, lay, nt, n, stream); break;
+    case 4: launch_mfma<4>(spec, lay, nt, n, stream); break;
+    case 5: launch_mfma<5>(spec, lay, nt, n, stream); break;
+    case 6: launch_mfma<6>(spec, lay, nt, n, stream); break;
+    case 7: launch_mfma<7>(spec, lay, nt, n, stream); break;
+    default: launch_mfma<8>(spec, lay, nt, n, stream); break;
+  }
+  check_launch("ff_aggregate_mfma", stream);
+  return true;
+}
+
 void ff_aggregate(const FfSpec& spec, int64_t n, hipStream_t stream) {
   if (n == 0) return;
+  if (try_mfma(spec, n, stream)) return;
   switch (spec.ncols) {
     case 1: launch_agg<1>(spec, n, stream); break;
     case 2: launch_agg<2>(spec, n, stream); break;

@@ -100,6 +100,7 @@ struct FfAgg {
   FfFactor f[kFfMaxFactors];
   int64_t* dst;
   int64_t* dst2;
+  int32_t vbits, pad;   // bound on the value's two's-complement width (0 = 64)
 };
 struct FfSpec {
   int32_t ncols, nterms, nkeys, naggs, ngroups, pad;
@@ -115,6 +116,8 @@ struct FfSpec {
 };
 void ff_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream);
 void ff_aggregate(const FfSpec& spec, int64_t n, hipStream_t stream);
+// one-hot MFMA aggregation (SUM / COUNT, <= 16 groups) on / off; returns the previous setting
+bool ff_set_mfma(bool on);
 
 // ---- sketch.hip --------------------------------------------------------------
 constexpr int kHllBits = 12;

@@ -71,8 +71,11 @@ class MemoryTable(TableSource):
 
     def __init__(self, columns: Dict[str, Column], num_rows: Optional[int] = None,
                  partitioned_by: Optional[str] = None, replicated: bool = False,
-                 fields: Optional[List[Field]] = None):
+                 fields: Optional[List[Field]] = None, resident: bool = True):
         self.columns = dict(columns)
+        # resident=False: columns stay where they are (e.g. host memory under a
+        # small device budget) and each scan moves a transient copy
+        self.resident = resident
         for c in self.columns.values():
             _mark_resident(c)
         self._n = num_rows if num_rows is not None else (len(next(iter(columns.values()))) if columns else 0)
@@ -99,7 +102,8 @@ class MemoryTable(TableSource):
             col = self.columns[c]
             if dev is not None and col.device != dev:
                 col = col.to(dev)
-                self.columns[c] = col  # promote to the execution device once (cache tier)
+                if self.resident:
+                    self.columns[c] = col  # promote to the execution device once (cache tier)
             out[c] = col
         return Batch(out, self._n)
 

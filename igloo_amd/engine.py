@@ -237,7 +237,8 @@ class QueryEngine:
         table = self._to_arrow(batch, plan.schema, bq.names)
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
-        self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned}
+        self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
+                             "spill": dict(ctx.spill)}
         if self.comm is not None:
             self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
         return QueryResult(table, ms)
@@ -299,6 +300,9 @@ class QueryEngine:
             for n in _walk_exec(node):
                 if getattr(n, "order_log", None):
                     txt += "\njoin order: " + " ; ".join(n.order_log)
+            if ctx.spill["joins"]:
+                txt += (f"\nspill: {ctx.spill['joins']} partitioned join(s), {ctx.spill['partitions']} partitions, "
+                        f"{ctx.spill['bytes']} bytes staged in host memory (device budget {ctx.budget} bytes)")
             if self.comm is not None and self.comm.world_size > 1:
                 txt += (f"\nexchange: {self.comm.calls - c0[0]} collectives, "
                         f"{self.comm.bytes_sent - c0[1]} bytes sent by this rank")

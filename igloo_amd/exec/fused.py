@@ -419,6 +419,25 @@ def _factors(e: Expr, spec: Spec) -> Tuple[List[tuple], int, bool]:
     raise Bail(f"argument {type(e).__name__}")
 
 
+def _value_bits(fs, spec) -> int:
+    """Bound on the two's-complement width of prod(a + b * col) from the
+    (narrow) widths of the factor columns; the one-hot MFMA aggregation sizes
+    its 7-bit limb decomposition with it (0 = unknown / 64 bits)."""
+    widths = [w for _, w in spec.args()[0]]
+    bound = 1
+    for c, a, b in fs:
+        c = int(c)
+        if c < 0:
+            f = abs(int(a))
+        else:
+            w = widths[c] if c < len(widths) else 8
+            f = abs(int(a)) + abs(int(b)) * (1 << (8 * int(w) - 1))
+        bound *= max(f, 1)
+        if bound >= 1 << 63:
+            return 0
+    return bound.bit_length() + 1
+
+
 def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> Optional[Batch]:
     """GROUP BY (domain <= 16) over a scanned batch with the scan filter and the
     argument arithmetic fused into one kernel, or None if the shape does not fit."""
@@ -505,7 +524,7 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
             shared = len(prev[2])
         prev = (op, chk, fs)
         kaggs.append((op, chk, [(int(c), int(a_), int(b_)) for c, a_, b_ in fs], d.data_ptr(),
-                      d2.data_ptr() if d2 is not None else 0, shared))
+                      d2.data_ptr() if d2 is not None else 0, shared, _value_bits(fs, spec)))
     if not spec.always_false:
         cols, terms, mask = spec.args()
         with ctx.span("agg.fused_scan"):

@@ -57,6 +57,13 @@ class ExecContext:
         self.evaluator = Evaluator(self)
         self.spans: Dict[str, list] = {}  # phase -> [total ms, calls] (EXPLAIN ANALYZE only)
         self.scan_cache: Dict[tuple, tuple] = {}  # (source, filters) -> (row ids, gathered columns by name)
+        # device working-memory budget of the join operators (bytes, None =
+        # unbounded): a join whose inputs exceed it runs partitioned, spilling
+        # partitions to pinned host memory (``grace_join``)
+        sess = getattr(engine, "session", None) or {}
+        gb = sess.get("device_budget_gb", os.environ.get("IGLOO_DEVICE_BUDGET_GB"))
+        self.budget = int(float(gb) * 2**30) if gb not in (None, "", 0, "0") else None
+        self.spill = {"joins": 0, "partitions": 0, "bytes": 0}
         # rows of base tables this query read (each table once; index / range
         # searches into a resident column subtract the rows they skipped)
         self.rows_scanned = 0
@@ -559,7 +566,108 @@ def apply_key_filters(b: Batch, filters, ctx) -> Batch:
     return b
 
 
+def _batch_bytes(b: Batch) -> int:
+    try:
+        return sum(c.nbytes for c in b.columns.values())
+    except Exception:  # noqa: BLE001 - lazy batches
+        return 0
+
+
+#: a join's working memory is taken as this multiple of its input bytes
+#: (hash table, pair lists, gathered output)
+JOIN_MEM_FACTOR = 3
+
+
+def _to_host(b: Batch) -> Batch:
+    """Spill a batch to (pinned) host memory."""
+    out = {}
+    for k, c in b.columns.items():
+        def mv(t):
+            if t is None or not t.is_cuda:
+                return t
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            return h
+        d = c.dictionary
+        out[k] = Column(c.dtype, mv(c.data), mv(c.valid), mv(c.offsets), d)
+    if b.num_rows and any(c.data.is_cuda for c in b.columns.values()):
+        torch.cuda.synchronize()
+    return Batch(out, b.num_rows, b.dist)
+
+
+def _to_device(b: Batch, dev) -> Batch:
+    return Batch({k: Column(c.dtype, c.data.to(dev, non_blocking=True),
+                            None if c.valid is None else c.valid.to(dev, non_blocking=True),
+                            None if c.offsets is None else c.offsets.to(dev, non_blocking=True), c.dictionary)
+                  for k, c in b.columns.items()}, b.num_rows, b.dist)
+
+
+def grace_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Optional[Batch]:
+    """Partitioned (grace) hash join for inputs whose working memory exceeds
+    ``ctx.budget``: both sides are hash-partitioned on the join keys into P
+    partitions, every partition is moved to pinned host memory, then each
+    partition pair is brought back and joined on the device on its own and
+    its output spilled; the outputs are concatenated at the end. Rows with
+    equal keys share a partition, so inner / left / semi / anti joins
+    decompose exactly (NULL keys go to partition 0 on both sides; NOT IN's
+    "any NULL on the build side" rule is decided before partitioning).
+    Returns None when the inputs fit the budget."""
+    if ctx.budget is None or not on or kind not in ("inner", "left", "semi", "anti"):
+        return None
+    need = JOIN_MEM_FACTOR * (_batch_bytes(lb) + _batch_bytes(rb))
+    if need <= ctx.budget or lb.num_rows == 0 or rb.num_rows == 0:
+        return None
+    from ..parallel.exchange import partition_keys
+    ev = ctx.evaluator
+    if kind == "anti" and null_aware:
+        rcols = [ev.column(b, rb) for _, b in on]
+        if any(c.valid is not None and bool((~c.valid).any().item()) for c in rcols):
+            return _empty_like(lb)
+    P = 2
+    while need / P > ctx.budget / 2 and P < 1024:
+        P *= 2
+    dev = ctx.device
+
+    def parts(b: Batch, exprs) -> List[Batch]:
+        key = None
+        for e in exprs:
+            k = partition_keys(ev.column(e, b)).to(torch.int64)
+            key = k if key is None else (key * 1000003) ^ k
+        perm, counts = M.hash_partition(key.contiguous(), P)
+        out, start = [], 0
+        keys = list(b.columns)
+        for c in counts:
+            idx = perm[start:start + c]
+            start += c
+            cols = take_many([b.columns[k] for k in keys], idx) if keys else []
+            piece = Batch(dict(zip(keys, cols)), c)
+            ctx.spill["bytes"] += _batch_bytes(piece)
+            out.append(_to_host(piece) if dev.type == "cuda" else piece)
+        return out
+
+    with ctx.span("join.spill_partition"):
+        lparts = parts(lb, [a for a, _ in on])
+        rparts = parts(rb, [b for _, b in on])
+    ctx.spill["joins"] += 1
+    ctx.spill["partitions"] += P
+    outs = []
+    with ctx.span("join.spill_probe"):
+        saved, ctx.budget = ctx.budget, None      # each partition pair runs in memory
+        try:
+            for lp, rp in zip(lparts, rparts):
+                l_d, r_d = _to_device(lp, dev), _to_device(rp, dev)
+                o = hash_join(l_d, r_d, kind, on, residual, ctx, null_aware=null_aware)
+                outs.append(_to_host(o) if dev.type == "cuda" else o)
+        finally:
+            ctx.budget = saved
+    return concat_batches([_to_device(o, dev) for o in outs])
+
+
 def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Batch:
+    if ctx.budget is not None:
+        g = grace_join(lb, rb, kind, on, residual, ctx, null_aware)
+        if g is not None:
+            return g
     ev = ctx.evaluator
     if kind == "right":
         # mirror into a left join
@@ -1234,7 +1342,9 @@ class MultiJoinExec(ExecNode):
                 fake = L.Join(None, None, "inner", on)  # type: ignore[arg-type]
                 la, lb_ = prepare_join(la, lb_, fake, ctx, rows=(a["grows"], b["grows"]))
                 out_dist = la.out_dist
-            if on and ctx.world == 1:
+            over = ctx.budget is not None and \
+                JOIN_MEM_FACTOR * (_batch_bytes(la) + _batch_bytes(lb_)) > ctx.budget
+            if on and ctx.world == 1 and not over:
                 out = self._late_join(la, lb_, on, and_all(resid), ctx)
             else:
                 if isinstance(la, LateBatch):

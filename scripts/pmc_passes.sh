@@ -11,7 +11,7 @@ i=0
 while read -r SET; do
   [ -z "$SET" ] && continue
   i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $SET --output-format csv -d "$R/gpurun_out/pmc/p$i" -o run -- \
+  IGLOO_PROF_GAP=1 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $SET --output-format csv -d "$R/gpurun_out/pmc/p$i" -o run -- \
     python3 "$R/bench.py" --source hbm --sf ${SF:-100} --steps 1 --warmup 1 --queries ${QUERIES:-1-22} \
     > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($SET) rc=$rc"; [ $rc -eq 0 ] || exit $rc

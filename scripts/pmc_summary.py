@@ -24,18 +24,29 @@ def short(n):
     return n.split("(")[0][:60]
 
 
-def load_pass(d):
+def load_pass(d, gap_ns=500e6):
+    """Counters of the dispatches after the last idle gap > 0.5 s (bench.py
+    with IGLOO_PROF_GAP=1 idles 1 s before the timed steps)."""
     cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     if not cc:
         return {}, {}
-    dur = {}
+    dur, start = {}, {}
     for r in csv.DictReader(open(kt[0])) if kt else []:
         dur[r.get("Dispatch_Id")] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        start[r.get("Dispatch_Id")] = int(r["Start_Timestamp"])
+    cut = 0
+    ts = sorted(start.values())
+    for a, b in zip(ts, ts[1:]):
+        if b - a > gap_ns:
+            cut = b
+    keep = {k for k, v in start.items() if v >= cut}
     per = defaultdict(lambda: defaultdict(float))
     seen = set()
     time_ns = defaultdict(float)
     for r in csv.DictReader(open(cc[0])):
+        if keep and r.get("Dispatch_Id") not in keep:
+            continue
         k = short(r["Kernel_Name"])
         per[k][r["Counter_Name"]] += float(r["Counter_Value"])
         did = r.get("Dispatch_Id")
