@@ -18,7 +18,8 @@ QUERIES = [
        WHERE l_shipdate >= date '1994-01-01' AND l_shipdate < date '1995-01-01'
          AND l_discount BETWEEN 0.05 AND 0.07 AND l_quantity < 24""",
     # negative values + 15 groups (shipmode x linestatus <= 14)
-    """SELECT l_shipmode, l_linestatus, sum(l_discount - 0.06) AS s, sum(l_tax - l_discount) AS t, count(*) AS n
+    """SELECT l_shipmode, l_linestatus, sum(l_discount - 0.06) AS s, sum(l_quantity * (l_tax - 0.05)) AS t,
+              count(*) AS n
        FROM lineitem GROUP BY l_shipmode, l_linestatus ORDER BY l_shipmode, l_linestatus""",
 ]
 
