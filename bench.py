@@ -15,6 +15,9 @@ Data path (default ``--source parquet``):
      HBM cache tier + every derived structure the queries build (sortedness
      flags, range/secondary indexes, HLL sketches, narrow copies) + the
      queries themselves.
+     Scan shapes get query-specialised kernels (igloo_amd/ops/jit.py):
+     hiprtc compiles them on host threads during the cold suite, which runs
+     the interpreted kernels; remaining compile time is ``jit.wait_s``.
   3. ``--warmup`` untimed suites, then ``--steps`` timed suites over the
      cached columns (bracketed by barrier + device sync, max over ranks):
      ``value`` is seconds per warm suite.
@@ -182,6 +185,14 @@ def main():
         log("[bench] cold per query (ms): " + " ".join(f"Q{q}={cold_per_q[q] * 1e3:.1f}" for q in qs))
     ref = {q: digest(t) for q, t in cold_res.items()}
     del cold_res
+    # generated scan kernels (ops/jit.py) compile on host threads while the
+    # cold suite runs on the interpreted ones; whatever is still compiling is
+    # waited for here and reported (not hidden in the warm steps)
+    from igloo_amd.ops import jit as _jit
+    tj = time.perf_counter()
+    _jit.wait_all(timeout=120)
+    jit_wait_s = time.perf_counter() - tj
+    log(f"[bench] jit: {_jit.STATS} wait {jit_wait_s:.3f}s")
 
     for w in range(a.warmup):
         tw = time.perf_counter()
@@ -253,6 +264,8 @@ def main():
                        "sf": a.sf, "queries": qs},
             "warm_s": round(step_s, 4),
             "cold_s": round(cold_s, 4),
+            "jit": {"wait_s": round(jit_wait_s, 3), "kernels_compiled": _jit.STATS["compiled"],
+                    "disk_hits": _jit.STATS["disk_hits"], "failed": _jit.STATS["failed"]},
             "load": load,
             "verified": verified,
             "cpu_check": cpu_check,

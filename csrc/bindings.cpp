@@ -125,12 +125,17 @@ kern::PqDecodeSpec decode_spec(const py::dict& d, bool need_output = true) {
 
 }  // namespace
 
+namespace igloo {
+void register_jit(py::module_& m);  // runtime/jit.cpp
+}
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "igloo MI355X native core: SQL frontend, gfx950 kernels, device runtime";
   m.attr("ARCH") = "gfx950";
   m.attr("MAX_AGGS") = kern::kMaxAggs;
   m.attr("MAX_GATHER_COLS") = kern::kMaxGatherCols;
   m.attr("MAX_PARTS") = kern::kMaxParts;
+  igloo::register_jit(m);
 
   // ------------------------------------------------------------------ SQL
   m.def("parse_sql", &parse, "Parse SQL text into a list of statement ASTs (dicts)");

@@ -40,7 +40,7 @@ namespace kern {
 
 namespace {
 
-constexpr int kFfRows = 4;  // rows per lane per iteration (coalesced: base + j*64 + lane)
+constexpr int kFfRows = 4;  // rows per lane per iteration (consecutive: base + 4 lane + j)
 static_assert(kFfMaxCols == 8 && kFfRows == 4, "row vectors are written for 8 columns x 4 rows");
 // row vector of VW >= NC int64 lanes (power of two, so a column index is masked, never out of range)
 template <int NC>
@@ -74,18 +74,87 @@ __device__ __forceinline__ int64_t ff_load(const FfColumn& c, int64_t base, uint
   return (int64_t)(v << sh) >> sh;
 }
 
+// Four consecutive rows of one column for a lane (rows base + 4 lane + j):
+// one load of 4 w bytes per lane (dword / dwordx2 / dwordx4 / 2 x dwordx4, a
+// wave reads one contiguous 256 w-byte span) and one bit-field extract per
+// value — against two dword loads, a 64-bit funnel shift and a sign-extending
+// shift pair per value for the row-strided form (ff_load). The width branch is
+// wave-uniform (kernel argument). Full iterations only: the tail keeps ff_load.
+struct FfQuad {
+  int64_t v0, v1, v2, v3;
+};
+struct FfRaw {
+  uint4 a, b;
+};
+// Load phase, branch-free: one dwordx4 per column at the lane's first row
+// (a 1/2-byte column uses its first 4/8 bytes; the iteration is "full" only
+// when those 16 bytes stay inside the column), plus a second dwordx4 for
+// 8-byte columns. Loads in per-width branches made the compiler wait for each
+// at the branch join; here every column's loads are in flight before the
+// first wait and the values are extracted afterwards (ff_extract4).
+__device__ __forceinline__ FfRaw ff_fetch4(const FfColumn& c, int64_t base, int lane) {
+  const int64_t w = c.width;
+  const char* p = (const char*)c.ptr + base * w;
+  const uint32_t off = (uint32_t)lane * 4u * (uint32_t)w;
+  FfRaw r;
+  r.a = *(const uint4*)(p + off);
+  if (w == 8) r.b = *(const uint4*)(p + off + 16);
+  return r;
+}
+__device__ __forceinline__ FfQuad ff_extract4(const FfColumn& c, const FfRaw& r) {
+  const int64_t w = c.width;
+  FfQuad q;
+  if (w == 1) {
+    const int x = (int)r.a.x;
+    q.v0 = (int8_t)x;
+    q.v1 = (int8_t)(x >> 8);
+    q.v2 = (int8_t)(x >> 16);
+    q.v3 = x >> 24;
+  } else if (w == 2) {
+    q.v0 = (int16_t)r.a.x;
+    q.v1 = (int)r.a.x >> 16;
+    q.v2 = (int16_t)r.a.y;
+    q.v3 = (int)r.a.y >> 16;
+  } else if (w == 4) {
+    q.v0 = (int)r.a.x;
+    q.v1 = (int)r.a.y;
+    q.v2 = (int)r.a.z;
+    q.v3 = (int)r.a.w;
+  } else {
+    q.v0 = (int64_t)(((uint64_t)r.a.y << 32) | r.a.x);
+    q.v1 = (int64_t)(((uint64_t)r.a.w << 32) | r.a.z);
+    q.v2 = (int64_t)(((uint64_t)r.b.y << 32) | r.b.x);
+    q.v3 = (int64_t)(((uint64_t)r.b.w << 32) | r.b.z);
+  }
+  return q;
+}
+
 // The row vectors are kernel locals (r0..r3) handed to helpers BY VALUE: an
 // element read through a reference/struct lvalue is canonicalised into a
 // dynamic GEP, which pins the vectors in scratch. NC (the number of input
-// columns) is a compile-time bound, so the load block has no branches and
-// every column's loads are issued before the first wait.
-#define FF_LOAD_ROWS(NC, S, base, idx)                              \
-  ff_vec<ff_vw<NC>()> r0 = {}, r1 = r0, r2 = r0, r3 = r0;          \
-  _Pragma("unroll") for (int c_ = 0; c_ < NC; ++c_) {             \
-    r0[c_] = ff_load(S.cols[c_], base, idx[0]);                    \
-    r1[c_] = ff_load(S.cols[c_], base, idx[1]);                    \
-    r2[c_] = ff_load(S.cols[c_], base, idx[2]);                    \
-    r3[c_] = ff_load(S.cols[c_], base, idx[3]);                    \
+// columns) is a compile-time bound, so the load block has no per-lane
+// branches and every column's loads are issued before the first wait.
+// A lane owns rows base + 4 lane + j (j < 4).
+#define FF_LOAD_ROWS(NC, S, base, it)                                \
+  ff_vec<ff_vw<NC>()> r0 = {}, r1 = r0, r2 = r0, r3 = r0;            \
+  if ((it).full) {                                                   \
+    FfRaw raw_[NC];                                                  \
+    _Pragma("unroll") for (int c_ = 0; c_ < NC; ++c_)               \
+      raw_[c_] = ff_fetch4(S.cols[c_], base, lane);                  \
+    _Pragma("unroll") for (int c_ = 0; c_ < NC; ++c_) {             \
+      const FfQuad q_ = ff_extract4(S.cols[c_], raw_[c_]);           \
+      r0[c_] = q_.v0;                                                \
+      r1[c_] = q_.v1;                                                \
+      r2[c_] = q_.v2;                                                \
+      r3[c_] = q_.v3;                                                \
+    }                                                                \
+  } else {                                                           \
+    _Pragma("unroll") for (int c_ = 0; c_ < NC; ++c_) {             \
+      r0[c_] = ff_load(S.cols[c_], base, (it).idx[0]);               \
+      r1[c_] = ff_load(S.cols[c_], base, (it).idx[1]);               \
+      r2[c_] = ff_load(S.cols[c_], base, (it).idx[2]);               \
+      r3[c_] = ff_load(S.cols[c_], base, (it).idx[3]);               \
+    }                                                                \
   }
 #define FF_ROW(j) ((j) == 0 ? r0 : (j) == 1 ? r1 : (j) == 2 ? r2 : r3)
 
@@ -100,14 +169,16 @@ struct FfIter {
   int64_t base;
   uint32_t idx[kFfRows];
   bool live[kFfRows];
+  bool full;  // all kWave * kFfRows rows in range (wave-uniform)
 };
 __device__ __forceinline__ FfIter ff_iter(int64_t base, int lane, int64_t n) {
   FfIter it;
   it.base = base;
   const int64_t rem = n - base;  // > 0
+  it.full = rem >= (int64_t)kWave * kFfRows + 12;  // + 12: the last lane's 16-byte load of a 1-byte column
 #pragma unroll
   for (int j = 0; j < kFfRows; ++j) {
-    const int64_t r = j * kWave + lane;
+    const int64_t r = kFfRows * lane + j;
     it.live[j] = r < rem;
     it.idx[j] = (uint32_t)(r < rem ? r : rem - 1);
   }
@@ -158,8 +229,14 @@ __device__ __forceinline__ void ff_pass4(const FfSpec& S, const ff_vec<VW> r0, c
   }
   if (S.mask) {
     const uint8_t* m = S.mask + it.base;
+    if (it.full) {  // the lane's 4 mask bytes in one dword (mask buffers are 4-byte aligned)
+      const uint32_t mw = *(const uint32_t*)(m + it.idx[0]);  // idx[0] = 4 lane
 #pragma unroll
-    for (int j = 0; j < kFfRows; ++j) pass[j] &= m[it.idx[j]] != 0;
+      for (int j = 0; j < kFfRows; ++j) pass[j] &= ((mw >> (8 * j)) & 0xffu) != 0;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kFfRows; ++j) pass[j] &= m[it.idx[j]] != 0;
+    }
   }
 }
 
@@ -225,13 +302,20 @@ __global__ __launch_bounds__(kBlock) void ff_mask_kernel(const FfSpec S, int64_t
   const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * per_iter;
   for (int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * per_iter; base < n; base += stride) {
     const FfIter it = ff_iter(base, lane, n);
-    FF_LOAD_ROWS(NC, S, base, it.idx)
+    FF_LOAD_ROWS(NC, S, base, it)
     bool pass[kFfRows];
     ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
     uint8_t* o = out + base;
+    if (it.full) {
+      uint32_t w = 0;
 #pragma unroll
-    for (int j = 0; j < kFfRows; ++j)
-      if (it.live[j]) o[it.idx[j]] = pass[j];
+      for (int j = 0; j < kFfRows; ++j) w |= (uint32_t)pass[j] << (8 * j);
+      *(uint32_t*)(o + kFfRows * lane) = w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kFfRows; ++j)
+        if (it.live[j]) o[it.idx[j]] = pass[j];
+    }
   }
 }
 
@@ -250,7 +334,7 @@ __device__ __forceinline__ int ff_slot(int cell, int half, int lane, int lanes) 
 constexpr int kFfAggBlock = 512;
 
 template <int NC>
-__global__ __launch_bounds__(1024) void ff_agg_kernel(const FfSpec S, int64_t n, int lanes) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ff_agg_kernel(const FfSpec S, int64_t n, int lanes) {
   extern __shared__ int64_t acc[];
   const int wave = ff_wave_uniform(threadIdx.x / kWave), lane = lane_id();
   const int waves = blockDim.x / kWave;
@@ -269,7 +353,7 @@ __global__ __launch_bounds__(1024) void ff_agg_kernel(const FfSpec S, int64_t n,
   const int64_t stride = (int64_t)gridDim.x * waves * per_iter;
   for (int64_t base = ((int64_t)blockIdx.x * waves + wave) * per_iter; base < n; base += stride) {
     const FfIter it = ff_iter(base, lane, n);
-    FF_LOAD_ROWS(NC, S, base, it.idx)
+    FF_LOAD_ROWS(NC, S, base, it)
     bool pass[kFfRows];
     ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
     int gid[kFfRows];
@@ -349,26 +433,33 @@ __global__ __launch_bounds__(1024) void ff_agg_kernel(const FfSpec S, int64_t n,
 // One-hot MFMA aggregation (SUM / COUNT over <= 16 groups).
 //
 // A group-by SUM is a matrix product: D[g][c] += sum_k onehot[g][k] * x[k][c]
-// over rows k. Per 64 rows a wave builds
-//   A = one-hot of the rows' group ids (16 groups x 64 rows, int8 0/1) and
-//   B = the rows' aggregate values split into 7-bit limbs (64 rows x 16
-//       limb columns per tile, int8; the top limb of a value is signed),
-// and v_mfma_i32_16x16x64_i8 accumulates D (16 x 16 int32) — exact integer
-// sums with no atomics and no per-(row, aggregate) LDS traffic. A value of
-// w bits (bound from the factor column widths) takes ceil((w - 8) / 7) + 1
-// limbs; the row count is one more limb column of 1s.
+// over rows k. A wave takes 256 rows per iteration (4 per lane) and builds
+//   A = one-hot of the rows' group ids (16 groups x 64 rows per MFMA, int8), and
+//   B = the rows' aggregate values split into byte limbs (64 rows x 16 limb
+//       columns per tile, int8),
+// then v_mfma_i32_16x16x64_i8 accumulates D (16 x 16 int32) — exact integer
+// sums with no atomics and no per-(row, aggregate) LDS traffic.
 //
-// Fragment maps (gfx950, v_mfma_i32_16x16x64_i8): lane l holds
+// Limbs: a value of w bits (bound from the factor column widths) takes
+// ceil(w / 8) bytes of its two's-complement form. The top byte is signed; a
+// lower byte u in [0, 255] is stored as u - 128 (= u ^ 0x80 read as int8) and
+// the block merge adds back 128 x (rows of the group), taken from a column of
+// 1s (the COUNT column). Filtered-out rows get group byte 0xff, so their
+// one-hot row is zero and their limbs need no masking.
+//
+// LDS staging (per wave, column-major): column c holds 256 bytes, byte
+// 4 * lane + j = row j of that lane, so a lane packs its 4 rows' limb l into
+// ONE dword (two v_perm_b32 per limb) and a column is one conflict-free
+// ds_write_b32. Fragment maps (gfx950, v_mfma_i32_16x16x64_i8): lane l holds
 // A[m = l & 15][k = 16 (l >> 4) + j] and B[k = 16 (l >> 4) + j][n = l & 15]
-// (j = 0..15, one byte each) and D[m = 4 (l >> 4) + i][n = l & 15] (i < 4).
-// Rows reach the fragments through LDS: lane r writes its gid byte and its
-// limb bytes column-major ([column][64 rows], 80-byte column stride against
-// bank conflicts), every lane then reads 16 consecutive bytes per operand.
-// int32 accumulators get at most 64 * 128 per step, so they are folded into
-// int64 every 2^14 steps; a block merges its waves and adds each (group,
+// (j = 0..15, one byte each) and D[m = 4 (l >> 4) + i][n = l & 15] (i < 4);
+// K-step s covers column bytes [64 s, 64 s + 64). The 272-byte column stride
+// spreads the 16 columns one ds_read_b128 touches over all 64 banks.
+// int32 accumulators gain at most 64 * 128 per MFMA, so they are folded into
+// int64 every 2^12 iterations; a block merges its waves and adds each (group,
 // aggregate) as int128 with two 64-bit atomics.
 typedef int v4i __attribute__((ext_vector_type(4)));
-constexpr int kMfmaCol = 80;                   // LDS bytes per limb column (64 rows + pad)
+constexpr int kMfmaCol = 272;                  // LDS bytes per limb column (256 rows + pad)
 constexpr int kMfmaMaxTiles = 4;               // <= 64 limb columns
 constexpr int kMfmaBlock = 256;
 
@@ -384,15 +475,29 @@ __device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t g4) {
   return y >> 7;
 }
 
+// byte b (0..3) of each of x0..x3 packed into one dword: two pair-perms + one merge
+__device__ __forceinline__ uint32_t limb_dword(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t b) {
+  // v_perm_b32(s0, s1, sel): selector byte values 0..3 pick s1's bytes, 4..7 s0's
+  const uint32_t sel = b | ((b + 4) << 8);                      // (x_lo.b, x_hi.b) in bytes 0, 1
+  const uint32_t p01 = __builtin_amdgcn_perm(x1, x0, sel);
+  const uint32_t p23 = __builtin_amdgcn_perm(x3, x2, sel);
+  return __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+}
+
 template <int NC, int NT>
 __global__ __launch_bounds__(kMfmaBlock) void ff_mfma_agg_kernel(const FfSpec S, const FfMfmaLayout Lay, int64_t n) {
-  __shared__ __attribute__((aligned(16))) uint8_t tile[kMfmaBlock / kWave][NT * 16 * kMfmaCol + kMfmaCol];
-  __shared__ long long red[kMfmaBlock / kWave][NT * 16][16];
+  constexpr int kCols = NT * 16 + 1;   // limb columns + the group-id column
+  // the waves' staging tiles, reused for the block merge once every wave is done
+  static_assert(NT * 16 * 16 * sizeof(long long) <= kCols * kMfmaCol, "merge buffer fits the tiles");
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kMfmaBlock / kWave][kCols * kMfmaCol];
+  auto red = reinterpret_cast<long long (*)[NT * 16][16]>(&tile[0][0]);
   const int wave = ff_wave_uniform(threadIdx.x / kWave), lane = lane_id();
   const int waves = kMfmaBlock / kWave;
   uint8_t* T = tile[wave];
   uint8_t* gidb = T + NT * 16 * kMfmaCol;
-  for (int i = lane; i < NT * 16 * kMfmaCol; i += kWave) T[i] = 0;   // unused limb columns stay 0
+  // unused limb columns stay 0, the count column holds 1s
+  for (int c = 0; c < NT * 16; ++c)
+    *reinterpret_cast<uint32_t*>(T + c * kMfmaCol + 4 * lane) = c == Lay.count_col ? 0x01010101u : 0u;
   v4i acc[NT];
   long long acc64[NT][4];
 #pragma unroll
@@ -408,66 +513,62 @@ __global__ __launch_bounds__(kMfmaBlock) void ff_mfma_agg_kernel(const FfSpec S,
   const int64_t stride = (int64_t)gridDim.x * waves * per_iter;
   for (int64_t base = ((int64_t)blockIdx.x * waves + wave) * per_iter; base < n; base += stride) {
     const FfIter it = ff_iter(base, lane, n);
-    FF_LOAD_ROWS(NC, S, base, it.idx)
+    FF_LOAD_ROWS(NC, S, base, it)
     bool pass[kFfRows];
     ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
     int gid[kFfRows];
     ff_gid4<ff_vw<NC>()>(S, r0, r1, r2, r3, gid);
-    // every aggregate's value for this lane's 4 rows (product chains reuse
-    // the previous aggregate's value, as in ff_agg_kernel)
-    int64_t vals[kFfMaxAggs][kFfRows];
+    uint32_t gw = 0;
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) gw |= (uint32_t)(pass[j] ? gid[j] & 0xff : 0xff) << (8 * j);
+    *reinterpret_cast<uint32_t*>(gidb + 4 * lane) = gw;
+    // each aggregate's values for this lane's 4 rows, straight into limb
+    // columns (product chains reuse the previous aggregate's value)
     int64_t val[kFfRows];
-#pragma unroll
-    for (int a = 0; a < kFfMaxAggs; ++a) {
-      if (a < NA && S.aggs[a].op != 1) {
-        ff_value4<ff_vw<NC>()>(S.aggs[a], r0, r1, r2, r3, val, &ovf);
-#pragma unroll
-        for (int j = 0; j < kFfRows; ++j) vals[a][j] = val[j];
+    for (int a = 0; a < NA; ++a) {
+      const FfAgg& A = S.aggs[a];
+      if (A.op == 1) continue;
+      ff_value4<ff_vw<NC>()>(A, r0, r1, r2, r3, val, &ovf);
+      const int c0 = Lay.col0[a], nl = Lay.nlimb[a];
+      const uint32_t l0 = (uint32_t)val[0], l1 = (uint32_t)val[1], l2 = (uint32_t)val[2], l3 = (uint32_t)val[3];
+      const uint32_t h0 = (uint32_t)(val[0] >> 32), h1 = (uint32_t)(val[1] >> 32), h2 = (uint32_t)(val[2] >> 32),
+                     h3 = (uint32_t)(val[3] >> 32);
+      for (int l = 0; l < nl; ++l) {
+        uint32_t d = l < 4 ? limb_dword(l0, l1, l2, l3, l) : limb_dword(h0, h1, h2, h3, l - 4);
+        if (l != nl - 1) d ^= 0x80808080u;   // lower limbs: u - 128 as int8
+        *reinterpret_cast<uint32_t*>(T + (c0 + l) * kMfmaCol + 4 * lane) = d;
       }
     }
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int j = 0; j < kFfRows; ++j) {
-      const bool on = it.live[j] && pass[j];
-      gidb[lane] = on ? (uint8_t)gid[j] : (uint8_t)0xff;
-#pragma unroll
-      for (int a = 0; a < kFfMaxAggs; ++a) {
-        if (a < NA && S.aggs[a].op != 1) {
-          const int64_t v = on ? vals[a][j] : 0;
-          const int c0 = Lay.col0[a], nl = Lay.nlimb[a];
-          for (int l = 0; l < nl; ++l) {
-            const int64_t limb = (l == nl - 1) ? (v >> (7 * l)) : ((v >> (7 * l)) & 127);
-            T[(c0 + l) * kMfmaCol + lane] = (uint8_t)(int8_t)limb;
-          }
-        }
-      }
-      T[Lay.count_col * kMfmaCol + lane] = (it.live[j] && pass[j]) ? 1 : 0;
-      __builtin_amdgcn_wave_barrier();
-      const uint4 gw = *reinterpret_cast<const uint4*>(gidb + q16);
+    for (int s = 0; s < 4; ++s) {
+      const uint4 gv = *reinterpret_cast<const uint4*>(gidb + 64 * s + q16);
       v4i af;
-      af[0] = (int)bytes_eq(gw.x, g4);
-      af[1] = (int)bytes_eq(gw.y, g4);
-      af[2] = (int)bytes_eq(gw.z, g4);
-      af[3] = (int)bytes_eq(gw.w, g4);
+      af[0] = (int)bytes_eq(gv.x, g4);
+      af[1] = (int)bytes_eq(gv.y, g4);
+      af[2] = (int)bytes_eq(gv.z, g4);
+      af[3] = (int)bytes_eq(gv.w, g4);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const uint4 bw = *reinterpret_cast<const uint4*>(T + (16 * t + (lane & 15)) * kMfmaCol + q16);
+        const uint4 bw = *reinterpret_cast<const uint4*>(T + (16 * t + (lane & 15)) * kMfmaCol + 64 * s + q16);
         const v4i bf = v4i{(int)bw.x, (int)bw.y, (int)bw.z, (int)bw.w};
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, acc[t], 0, 0, 0);
       }
-      __builtin_amdgcn_wave_barrier();
-      if (++steps == (1 << 14)) {
-        steps = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (++steps == (1 << 12)) {
+      steps = 0;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i];
-          acc[t] = v4i{0, 0, 0, 0};
-        }
+      for (int t = 0; t < NT; ++t) {
+        for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i];
+        acc[t] = v4i{0, 0, 0, 0};
       }
     }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t)
     for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i];
+  __syncthreads();
   // D[m = 4 (lane >> 4) + i][n = lane & 15] of tile t -> red[wave][16 t + n][m]
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -481,13 +582,17 @@ __global__ __launch_bounds__(kMfmaBlock) void ff_mfma_agg_kernel(const FfSpec S,
       for (int w = 0; w < waves; ++w) x += red[w][col][g];
       return x;
     };
+    const long long cnt = limb_sum(Lay.count_col);
     if (a == NA || S.aggs[a].op == 1) {
-      const long long c = limb_sum(Lay.count_col);
-      if (c) atomicAdd((unsigned long long*)(a == NA ? &S.counts[g] : &S.aggs[a].dst[g]), (unsigned long long)c);
+      if (cnt) atomicAdd((unsigned long long*)(a == NA ? &S.counts[g] : &S.aggs[a].dst[g]), (unsigned long long)cnt);
       continue;
     }
+    const int nl = Lay.nlimb[a];
     __int128 tot = 0;
-    for (int l = 0; l < Lay.nlimb[a]; ++l) tot += (__int128)limb_sum(Lay.col0[a] + l) << (7 * l);
+    for (int l = 0; l < nl; ++l) {
+      const long long x = limb_sum(Lay.col0[a] + l) + (l == nl - 1 ? 0 : 128 * cnt);
+      tot += (__int128)x << (8 * l);
+    }
     if (tot != 0)
       atomic_add_i128_parts((unsigned long long*)&S.aggs[a].dst[g], (long long*)&S.aggs[a].dst2[g],
                             (unsigned long long)(uint64_t)tot, (long long)(int64_t)(tot >> 64));
@@ -515,7 +620,7 @@ void launch_agg(const FfSpec& spec, int64_t n, hipStream_t stream) {
   static const int block = [] {
     const char* e = std::getenv("IGLOO_FF_AGG_BLOCK");
     const int v = e ? std::atoi(e) : kFfAggBlock;
-    return (v == 256 || v == 512 || v == 1024) ? v : kFfAggBlock;
+    return (v == 256 || v == 512) ? v : kFfAggBlock;
   }();
   // persistent-style grid: about as many blocks as stay resident (LDS-limited,
   // 160 KB per CU; at most 2048 threads), each streaming many rows, so the
@@ -542,9 +647,14 @@ void ff_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream) {
   check_launch("ff_mask", stream);
 }
 
+// Off by default: kernel-level A/B at SF100 (scripts/ff_ab.sh, rocprofv3)
+// measured the interpreted one-hot MFMA path at 9.2 ms for Q1 against 6.6 ms
+// for the LDS-atomic kernel (the per-row value/limb interpretation dominates
+// either way); the generated scan kernels (exec/fused_jit.py) replace both
+// on warm queries.
 static bool g_ff_mfma = [] {
   const char* e = std::getenv("IGLOO_FF_MFMA");
-  return e ? std::atoi(e) != 0 : true;
+  return e ? std::atoi(e) != 0 : false;
 }();
 
 bool ff_set_mfma(bool on) {
@@ -555,7 +665,11 @@ bool ff_set_mfma(bool on) {
 
 template <int NC>
 static void launch_mfma(const FfSpec& spec, const FfMfmaLayout& lay, int nt, int64_t n, hipStream_t stream) {
-  const unsigned grid = grid_for(n, kMfmaBlock * kFfRows * 8, 256 * 3);
+  // persistent-style: about as many blocks as stay resident (LDS-limited)
+  const int lds = (kMfmaBlock / kWave) * (nt * 16 + 1) * kMfmaCol;
+  int per_cu = (160 * 1024) / lds;
+  per_cu = per_cu < 1 ? 1 : per_cu > 8 ? 8 : per_cu;
+  const unsigned grid = grid_for(n, kMfmaBlock * kFfRows * 8, 256 * per_cu);
   switch (nt) {
     case 1: hipLaunchKernelGGL((ff_mfma_agg_kernel<NC, 1>), dim3(grid), dim3(kMfmaBlock), 0, stream, spec, lay, n); break;
     case 2: hipLaunchKernelGGL((ff_mfma_agg_kernel<NC, 2>), dim3(grid), dim3(kMfmaBlock), 0, stream, spec, lay, n); break;
@@ -574,7 +688,7 @@ static bool try_mfma(const FfSpec& spec, int64_t n, hipStream_t stream) {
     if (A.op != 0 && A.op != 1) return false;
     if (A.op == 1) continue;
     const int w = A.vbits > 0 && A.vbits <= 64 ? A.vbits : 64;
-    const int nl = w <= 8 ? 1 : (w - 8 + 6) / 7 + 1;
+    const int nl = (w + 7) / 8;
     lay.col0[a] = col;
     lay.nlimb[a] = nl;
     col += nl;

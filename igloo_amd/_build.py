@@ -94,7 +94,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if out.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
         return out
     tmp = out.with_suffix(".tmp.so")
-    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)]
+    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
+           "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
     if os.environ.get("IGLOO_SANITIZE"):
         cmd += [f"-fsanitize={os.environ['IGLOO_SANITIZE']}"]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -353,6 +353,9 @@ def predicate_mask(pred: Expr, b: Batch, ev) -> Optional[torch.Tensor]:
     if not spec.terms:
         return spec.mask  # every conjunct needed the generic evaluator
     out = torch.empty(n, dtype=torch.bool, device=dev)
+    from .fused_jit import jit_mask
+    if jit_mask(spec, n, out, stream(out)):
+        return out
     cols, terms, mask = spec.args()
     launch("ff_mask").ff_mask(cols, terms, mask, n, out.data_ptr(), stream(out))
     return out
@@ -526,10 +529,12 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
         kaggs.append((op, chk, [(int(c), int(a_), int(b_)) for c, a_, b_ in fs], d.data_ptr(),
                       d2.data_ptr() if d2 is not None else 0, shared, _value_bits(fs, spec)))
     if not spec.always_false:
+        from .fused_jit import jit_aggregate
         cols, terms, mask = spec.args()
         with ctx.span("agg.fused_scan"):
-            launch("ff_aggregate").ff_aggregate(cols, terms, mask, keys, G, kaggs, counts.data_ptr(), ovf.data_ptr(),
-                                                n, stream(counts))
+            if not jit_aggregate(spec, keys, G, kaggs, counts, ovf, n, stream(counts)):
+                launch("ff_aggregate").ff_aggregate(cols, terms, mask, keys, G, kaggs, counts.data_ptr(),
+                                                    ovf.data_ptr(), n, stream(counts))
     if any(chk for _, chk, _ in descs) and to_host_ints(ovf)[0]:
         raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
     from ..ops.agg import _wide_to_result

@@ -60,6 +60,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--top", type=int, default=15)
+    ap.add_argument("--raw", action="store_true", help="also dump every counter (per wave where it is a count)")
     a = ap.parse_args()
     counters = defaultdict(dict)
     times = defaultdict(float)
@@ -83,6 +84,15 @@ def main():
         print(f"{k:60s} {ms:8.2f} {fetch:9.3f} {write:9.3f} {gbs:8.0f} {100 * gbs / PEAK_GBS:6.1f} "
               f"{c.get('SQ_INSTS_VALU', 0) / waves:10.0f} {c.get('SQ_INSTS_LDS', 0) / waves:9.0f} "
               f"{c.get('SQ_LDS_BANK_CONFLICT', 0):8.0f} {c.get('SQ_INSTS_MFMA', 0):6.0f}")
+    if a.raw:
+        for k, t in rows:
+            c = counters[k]
+            waves = max(c.get("SQ_WAVES", 1), 1)
+            print(f"\n{k} ({t / 1e6:.2f} ms, {waves:.0f} waves)")
+            for name in sorted(c):
+                v = c[name]
+                extra = f"  ({v / waves:.1f}/wave)" if name.startswith("SQ_INSTS") or name.startswith("SQ_WAIT") else ""
+                print(f"    {name:32s} {v:16.0f}{extra}")
 
 
 if __name__ == "__main__":

@@ -5,6 +5,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# generated kernels compile on first use (not in the background) so every GPU
+# test exercises the code path warm queries take (igloo_amd/ops/jit.py)
+os.environ.setdefault("IGLOO_JIT", "sync")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 

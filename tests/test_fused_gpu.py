@@ -17,6 +17,17 @@ from igloo_amd.ops._lib import KERNEL_CALLS
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["interp", "jit"])
+def scan_mode(request, monkeypatch):
+    """Every test runs on the interpreted kernels (fused.hip) and on the
+    generated ones (exec/fused_jit.py, compiled synchronously)."""
+    from igloo_amd.exec import fused_jit
+    from igloo_amd.ops import jit
+    monkeypatch.setattr(fused_jit, "ENABLED", request.param == "jit")
+    monkeypatch.setattr(jit, "MODE", "sync")
+    return request.param
+
+
 def _table(n=300_000, seed=3):
     r = np.random.default_rng(seed)
     price = r.integers(90_000, 10_500_000, n)            # decimal(15,2) scaled
@@ -101,14 +112,16 @@ def test_fused_matches_cpu(gpu_device, qi):
             assert _close(rc[k], rg[k]), (k, rc[k], rg[k])
 
 
-def test_fused_kernels_used(gpu_device):
+def test_fused_kernels_used(gpu_device, scan_mode):
     e = ig.QueryEngine(device=gpu_device)
     e.register_table("t", _table(50_000))
     before = dict(KERNEL_CALLS)
     e.query(QUERIES[0])
     e.query(QUERIES[4])
-    assert KERNEL_CALLS["ff_aggregate"] > before.get("ff_aggregate", 0)
-    assert KERNEL_CALLS["ff_mask"] > before.get("ff_mask", 0)
+    agg, mask = (("jit:igloo_jit_scan_agg", "jit:igloo_jit_scan_mask") if scan_mode == "jit"
+                 else ("ff_aggregate", "ff_mask"))
+    assert KERNEL_CALLS[agg] > before.get(agg, 0)
+    assert KERNEL_CALLS[mask] > before.get(mask, 0)
 
 
 def test_fused_decimal_overflow_detected(gpu_device):

@@ -39,8 +39,10 @@ def engines():
 
 
 @pytest.mark.parametrize("qi", range(len(QUERIES)))
-def test_mfma_aggregation_matches(engines, qi):
+def test_mfma_aggregation_matches(engines, qi, monkeypatch):
+    from igloo_amd.exec import fused_jit
     from igloo_amd.ops import _lib
+    monkeypatch.setattr(fused_jit, "ENABLED", False)   # the interpreted kernels under test
     g, c = engines
     sql = QUERIES[qi]
     N = _lib.native()
