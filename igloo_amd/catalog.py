@@ -119,11 +119,14 @@ class Catalog:
         self._lock = threading.RLock()
         self.tables: Dict[str, TableSource] = {}
         self.views: Dict[str, str] = {}
+        #: bumped by every DDL change (plan caches key on it)
+        self.version = 0
 
     def register_table(self, name: str, source: TableSource) -> Optional[TableSource]:
         with self._lock:
             old = self.tables.get(name)
             self.tables[name] = source
+            self.version += 1
             return old
 
     def get_table(self, name: str) -> Optional[TableSource]:
@@ -132,11 +135,13 @@ class Catalog:
 
     def deregister_table(self, name: str) -> Optional[TableSource]:
         with self._lock:
+            self.version += 1
             self.views.pop(name, None)
             return self.tables.pop(name, None)
 
     def register_view(self, name: str, sql: str):
         with self._lock:
+            self.version += 1
             self.views[name] = sql
 
     def get_view(self, name: str) -> Optional[str]:

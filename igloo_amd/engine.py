@@ -8,6 +8,8 @@ errors raise typed ``IglooError``s instead of panicking.
 """
 from __future__ import annotations
 
+import collections
+import os
 import threading
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence, Union
@@ -26,6 +28,12 @@ from .sql.logical import ColInfo, Plan
 from .sql.optimizer import optimize
 from .utils.errors import IglooError, NotSupported, PlanError
 from .utils.log import get_logger
+
+#: cache optimized logical plans per SQL text (parse + bind + optimize cost
+#: ~1 ms of Python per TPC-H query); keyed on the catalog version and the
+#: session settings, so any DDL or SET invalidates
+PLAN_CACHE = os.environ.get("IGLOO_PLAN_CACHE", "1") == "1"
+PLAN_CACHE_SIZE = 256
 
 log = get_logger("engine")
 
@@ -78,6 +86,8 @@ class QueryEngine:
         self.catalog = catalog or Catalog()
         self.comm = comm
         self.session: Dict[str, Any] = dict(config or {})
+        # optimized logical plans by (SQL text, catalog version, session settings)
+        self._plans: "collections.OrderedDict" = collections.OrderedDict()
         self._ids = IdGen()
         self._lock = threading.RLock()
         self.last_metrics: Dict[str, Any] = {}
@@ -164,7 +174,21 @@ class QueryEngine:
         return self.sql(sql).table
 
     def sql(self, sql: str) -> QueryResult:
+        key = None
+        if PLAN_CACHE:
+            key = (sql, self.catalog.version, tuple(sorted((k, repr(v)) for k, v in self.session.items())))
+            hit = self._plans.get(key)
+            if hit is not None:
+                self._plans.move_to_end(key)
+                return self._exec_query(hit[0], hit[1], time.perf_counter(), cached=True)
         stmts = parse(sql)
+        if key is not None and len(stmts) == 1 and stmts[0]["k"] == "query":
+            t0 = time.perf_counter()
+            plan, names = self._plan_query(stmts[0])
+            self._plans[key] = (plan, names)
+            while len(self._plans) > PLAN_CACHE_SIZE:
+                self._plans.popitem(last=False)
+            return self._exec_query(plan, names, t0)
         if not stmts:
             raise PlanError("empty SQL statement")
         res = None
@@ -227,18 +251,29 @@ class QueryEngine:
             raise NotSupported(f"STORED AS {fmt}")
         return QueryResult(pa.table({}), 0.0)
 
-    def _run_query(self, st: dict, t0: float) -> QueryResult:
+    def _plan_query(self, st: dict):
         b = Binder(self.catalog, self._ids, self.session)
         bq = b.bind_query(st)
-        plan = optimize(bq.plan)
+        return optimize(bq.plan), bq.names
+
+    def _run_query(self, st: dict, t0: float) -> QueryResult:
+        plan, names = self._plan_query(st)
+        return self._exec_query(plan, names, t0)
+
+    def _exec_query(self, plan, names, t0: float, cached: bool = False) -> QueryResult:
+        """Execute an optimized logical plan. A cached plan is only the
+        parse / bind / optimize output for the same SQL text, catalog version
+        and session settings: every execution builds fresh physical operators
+        and recomputes everything from the tables (scalar subqueries included)."""
+        bq_names = names
         ctx = self.make_context()
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
         batch = self._execute_plan(plan, ctx)
-        table = self._to_arrow(batch, plan.schema, bq.names)
+        table = self._to_arrow(batch, plan.schema, bq_names)
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
-                             "spill": dict(ctx.spill)}
+                             "spill": dict(ctx.spill), "plan_cached": cached}
         if self.comm is not None:
             self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
         return QueryResult(table, ms)
