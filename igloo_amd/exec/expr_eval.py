@@ -12,6 +12,7 @@ projection.rs:60-64).
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Optional, Tuple, Union
 
 import numpy as np
@@ -27,6 +28,12 @@ from ..sql.expr import (AggCall, BinOp, Case, Cast, ColRef, Expr, Func, InList, 
                         SubqueryExpr)
 from ..types import DataType
 from ..utils.errors import ExecutionError, NotSupported
+
+#: generated expression kernels (exec/expr_jit.py) for composite expressions
+#: over GPU batches of at least this many rows
+JIT_MIN_ROWS = int(os.environ.get("IGLOO_EXPR_JIT_MIN_ROWS", "1"))
+_JIT_ROOTS = {BinOp, Case, Cast, Func, Not, Neg, IsNull, InList}
+_JIT_ON_CPU = False   # tests: run the generator (source collection only) on CPU batches
 
 
 class Scalar:
@@ -56,7 +63,26 @@ class Evaluator:
         self.ctx = ctx
 
     # ------------------------------------------------------------------ entry
+    _jit_off = 0   # > 0 while a generated kernel's uncovered subtree is evaluated here
+
     def eval(self, e: Expr, b: Batch) -> Value:
+        if not self._jit_off and type(e) in _JIT_ROOTS and b.num_rows >= JIT_MIN_ROWS and b.columns \
+                and (next(iter(b.columns.values())).data.is_cuda or _JIT_ON_CPU):
+            from . import expr_jit
+            r = expr_jit.evaluate(e, b, self)
+            if isinstance(r, Column):
+                return r
+            if r is expr_jit.PENDING:
+                # compiling in the background: this run goes node by node without
+                # generating code for the subtrees as well
+                self._jit_off += 1
+                try:
+                    return self._eval_nodes(e, b)
+                finally:
+                    self._jit_off -= 1
+        return self._eval_nodes(e, b)
+
+    def _eval_nodes(self, e: Expr, b: Batch) -> Value:
         m = getattr(self, "_" + type(e).__name__, None)
         if m is None:
             if isinstance(e, ColRef):
@@ -243,8 +269,16 @@ class Evaluator:
             return Scalar(None, T.BOOL)
         t = lt if lt == rt else T.common_numeric(lt, rt)
         rep = T.INT64 if t.kind in ("date32", "timestamp", "bool") else t
-        a, va = self._num(l, rep) if t.kind != "bool" else (_bool_parts(l)[0].to(torch.int8), l.valid)
-        c, vc = self._num(r, rep) if t.kind != "bool" else (_bool_parts(r)[0].to(torch.int8), r.valid)
+        if t.kind == "bool":
+            def bpart(v):
+                if isinstance(v, Scalar):
+                    return int(bool(v.value)), None
+                return _bool_parts(v)[0].to(torch.int8), v.valid
+            a, va = bpart(l)
+            c, vc = bpart(r)
+        else:
+            a, va = self._num(l, rep)
+            c, vc = self._num(r, rep)
         fn = {"=": torch.eq, "<>": torch.ne, "<": torch.lt, "<=": torch.le, ">": torch.gt, ">=": torch.ge}[op]
         if not isinstance(a, torch.Tensor):
             # flip so the tensor is on the left
