@@ -18,6 +18,9 @@ Data path (default ``--source parquet``):
      Scan shapes get query-specialised kernels (igloo_amd/ops/jit.py):
      hiprtc compiles them on host threads during the cold suite, which runs
      the interpreted kernels; remaining compile time is ``jit.wait_s``.
+     Repeated queries over unchanged data replay their host readbacks
+     (sizes, ranges) and validate them on the device at the end of each query
+     (``speculation`` counts, engine.py); every kernel still runs every step.
   3. ``--warmup`` untimed suites, then ``--steps`` timed suites over the
      cached columns (bracketed by barrier + device sync, max over ranks):
      ``value`` is seconds per warm suite.
@@ -158,10 +161,14 @@ def main():
                 rows[k] = comm.allreduce_int(rows[k])
     log(f"[bench] sf={a.sf} world={world} source={a.source} load={load} rows={rows}")
 
+    spec_modes = {}
+
     def suite(record=None, results=None, scanned=None):
         for q in qs:
             tq = time.perf_counter()
             r = eng.sql(queries.QUERIES[q])
+            m = eng.last_metrics.get("speculation")
+            spec_modes[m] = spec_modes.get(m, 0) + 1
             if results is not None:
                 results[q] = r.table
             if scanned is not None:
@@ -204,6 +211,7 @@ def main():
     barrier()
     if os.environ.get("IGLOO_PROF_GAP"):
         time.sleep(1.0)   # idle gap that scripts/kernel_summary.py uses to isolate the timed steps in a trace
+    spec_modes.clear()
     t1 = time.perf_counter()
     for s in range(a.steps):
         res = {}
@@ -264,6 +272,9 @@ def main():
                        "sf": a.sf, "queries": qs},
             "warm_s": round(step_s, 4),
             "cold_s": round(cold_s, 4),
+            # timed-step queries whose host readbacks were replayed and validated
+            # on the device (engine.QueryEngine._execute_speculative)
+            "speculation": {str(k): v for k, v in spec_modes.items()},
             "jit": {"wait_s": round(jit_wait_s, 3), "kernels_compiled": _jit.STATS["compiled"],
                     "disk_hits": _jit.STATS["disk_hits"], "failed": _jit.STATS["failed"]},
             "load": load,

@@ -78,6 +78,9 @@ class TieredCache:
         self._host: "OrderedDict[str, Tuple[pa.Table, Any, int, str]]" = OrderedDict()  # kind: batch|batches|table
         self._disk: "OrderedDict[str, Tuple[str, Any, int, str]]" = OrderedDict()
         self.stats = {"hits": 0, "misses": 0, "evictions": 0, "spills": 0, "promotions": 0}
+        #: bumped whenever cached data may change identity (put / drop / evict /
+        #: re-materialise); engine.py keys replayed query cardinalities on it
+        self.generation = 0
         self._dir = None
         if self.config.disk_path:
             os.makedirs(self.config.disk_path, exist_ok=True)
@@ -113,6 +116,7 @@ class TieredCache:
     # ---------------------------------------------------------------- API
     def put(self, key: str, value: Value, version: Any = None) -> None:
         with self._lock:
+            self.generation += 1
             self._drop(key)
             nb = _nbytes(value)
             if isinstance(value, Batch):
@@ -152,6 +156,7 @@ class TieredCache:
     def _materialise(self, key, tier, e):
         if tier is self._hbm:
             return e[0]
+        self.generation += 1     # a fresh copy of the data (new device tensors)
         if tier is self._host:
             t, ver, nb, kind = e
         else:
@@ -173,6 +178,7 @@ class TieredCache:
         return t
 
     def _drop(self, key):
+        self.generation += 1
         self._hbm.pop(key, None)
         self._host.pop(key, None)
         e = self._disk.pop(key, None)

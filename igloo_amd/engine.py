@@ -34,6 +34,9 @@ from .utils.log import get_logger
 #: session settings, so any DDL or SET invalidates
 PLAN_CACHE = os.environ.get("IGLOO_PLAN_CACHE", "1") == "1"
 PLAN_CACHE_SIZE = 256
+#: replay the host readbacks of repeated queries over unchanged data (see
+#: QueryEngine._execute_speculative)
+SPECULATE = os.environ.get("IGLOO_SPECULATE", "1") == "1"
 
 log = get_logger("engine")
 
@@ -88,6 +91,7 @@ class QueryEngine:
         self.session: Dict[str, Any] = dict(config or {})
         # optimized logical plans by (SQL text, catalog version, session settings)
         self._plans: "collections.OrderedDict" = collections.OrderedDict()
+        self._spec: Dict[Any, dict] = {}   # replayable host readbacks per (plan, catalog, cache generation)
         self._ids = IdGen()
         self._lock = threading.RLock()
         self.last_metrics: Dict[str, Any] = {}
@@ -180,7 +184,7 @@ class QueryEngine:
             hit = self._plans.get(key)
             if hit is not None:
                 self._plans.move_to_end(key)
-                return self._exec_query(hit[0], hit[1], time.perf_counter(), cached=True)
+                return self._exec_query(hit[0], hit[1], time.perf_counter(), cached=True, key=key)
         stmts = parse(sql)
         if key is not None and len(stmts) == 1 and stmts[0]["k"] == "query":
             t0 = time.perf_counter()
@@ -188,7 +192,7 @@ class QueryEngine:
             self._plans[key] = (plan, names)
             while len(self._plans) > PLAN_CACHE_SIZE:
                 self._plans.popitem(last=False)
-            return self._exec_query(plan, names, t0)
+            return self._exec_query(plan, names, t0, key=key)
         if not stmts:
             raise PlanError("empty SQL statement")
         res = None
@@ -260,7 +264,7 @@ class QueryEngine:
         plan, names = self._plan_query(st)
         return self._exec_query(plan, names, t0)
 
-    def _exec_query(self, plan, names, t0: float, cached: bool = False) -> QueryResult:
+    def _exec_query(self, plan, names, t0: float, cached: bool = False, key=None) -> QueryResult:
         """Execute an optimized logical plan. A cached plan is only the
         parse / bind / optimize output for the same SQL text, catalog version
         and session settings: every execution builds fresh physical operators
@@ -268,12 +272,12 @@ class QueryEngine:
         bq_names = names
         ctx = self.make_context()
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
-        batch = self._execute_plan(plan, ctx)
+        batch, spec = self._execute_speculative(plan, ctx, key)
         table = self._to_arrow(batch, plan.schema, bq_names)
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
-                             "spill": dict(ctx.spill), "plan_cached": cached}
+                             "spill": dict(ctx.spill), "plan_cached": cached, "speculation": spec}
         if self.comm is not None:
             self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
         return QueryResult(table, ms)
@@ -292,6 +296,48 @@ class QueryEngine:
 
     def make_context(self, analyze: bool = False) -> ExecContext:
         return ExecContext(self, self.device, self.comm, analyze)
+
+    def _execute_speculative(self, plan: Plan, ctx: ExecContext, key):
+        """Run the plan; for a repeated query over unchanged data, replay the
+        host readbacks (sizes, ranges, strategy choices) of the previous
+        executions instead of waiting on the device for each (ops/_lib.py
+        Speculation): the host enqueues the whole query while the GPU runs it,
+        and one sync at the end checks every replayed value against the device.
+        A recording is replayed only after two consecutive executions produced
+        it identically; a failed check re-executes the query with real
+        readbacks (and after two failures the query is no longer replayed)."""
+        from .ops import _lib
+        if not (SPECULATE and key is not None and self.device.type == "cuda"
+                and (self.comm is None or self.comm.world_size == 1)):
+            return self._execute_plan(plan, ctx), None
+        skey = (key, self.catalog.version, self.cache.generation)
+        st = self._spec.get(skey)
+        if st is None:
+            if len(self._spec) >= PLAN_CACHE_SIZE:
+                self._spec.pop(next(iter(self._spec)))
+            st = self._spec[skey] = {"log": None, "stable": False, "fails": 0}
+        if st["stable"] and st["fails"] < 2:
+            sp = _lib.Speculation("replay", st["log"])
+            _lib.set_speculation(sp)
+            try:
+                batch = self._execute_plan(plan, ctx)
+            finally:
+                _lib.set_speculation(None)
+            if sp.validate():
+                return batch, "replayed"
+            st["fails"] += 1
+            st["stable"] = False
+            ctx = self.make_context()
+            log.info("speculative readbacks diverged (%s); re-executing", "site" if sp.diverged else "value")
+        sp = _lib.Speculation("record")
+        _lib.set_speculation(sp)
+        try:
+            batch = self._execute_plan(plan, ctx)
+        finally:
+            _lib.set_speculation(None)
+        st["stable"] = st["log"] is not None and st["log"] == sp.log
+        st["log"] = sp.log
+        return batch, "recorded"
 
     def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:
         ctx = ctx or self.make_context()

@@ -460,8 +460,12 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
             if col.is_dict:
                 lo, size = 0, len(col.dictionary)
             elif col.dtype.is_integer or col.dtype.kind in ("date32", "bool"):
-                mn, mx = torch.aminmax(col.data)
-                lo, hi = to_host_ints(torch.stack([mn.to(torch.int64), mx.to(torch.int64)]))
+                from ..ops.hashing import key_range
+                rng = key_range(col.data) if col.data.dtype in (torch.int32, torch.int64) else None
+                if rng is None:   # other widths / empty: one reduction
+                    mn, mx = torch.aminmax(col.data)
+                    rng = to_host_ints(torch.stack([mn.to(torch.int64), mx.to(torch.int64)]))
+                lo, hi = rng
                 size = hi - lo + 1
             else:
                 raise Bail("group key type")

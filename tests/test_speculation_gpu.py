@@ -1,0 +1,80 @@
+"""Replayed host readbacks (ops/_lib.py Speculation, engine._execute_speculative):
+a repeated query over unchanged data is enqueued without per-operator device
+syncs and validated with one check at the end; results stay identical, a
+diverging call sequence or value is detected and re-executed."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu_engine():
+    import torch
+    import igloo_amd as ig
+    from igloo_amd.models.tpch import datagen
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = ig.QueryEngine(device="cuda:0")
+    datagen.register(e, 0.1)
+    return e
+
+
+@pytest.mark.parametrize("q", [1, 3, 5, 9, 13, 18, 21, 22])
+def test_replayed_queries_match(gpu_engine, q):
+    from bench import digest
+    from igloo_amd.models.tpch import queries
+    e = gpu_engine
+    sql = queries.QUERIES[q]
+    first = digest(e.sql(sql).table)
+    modes = []
+    for _ in range(4):
+        assert digest(e.sql(sql).table) == first
+        modes.append(e.last_metrics["speculation"])
+    assert modes[-1] == "replayed", modes
+
+
+def test_reregistered_table_is_not_replayed(gpu_engine):
+    import pyarrow as pa
+    e = gpu_engine
+    e.register_table("spec_t", pa.table({"a": list(range(1000)), "b": [i % 7 for i in range(1000)]}))
+    sql = "SELECT b, count(*) AS n, sum(a) AS s FROM spec_t WHERE a % 3 = 1 GROUP BY b ORDER BY b"
+    for _ in range(3):
+        want = e.sql(sql).to_pylist()
+    assert e.last_metrics["speculation"] == "replayed"
+    e.register_table("spec_t", pa.table({"a": list(range(5000)), "b": [i % 5 for i in range(5000)]}))
+    got = e.sql(sql).to_pylist()
+    assert e.last_metrics["speculation"] == "recorded"
+    assert len(got) == 5 and got != want
+
+
+def test_diverging_site_fails_validation():
+    import torch
+    from igloo_amd.ops import _lib
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    x = torch.tensor([3, 4], device="cuda:0")
+
+    def a():
+        return _lib.to_host_ints(x)
+
+    def b():
+        return _lib.to_host_ints(x)
+    rec = _lib.Speculation("record")
+    _lib.set_speculation(rec)
+    a()
+    _lib.set_speculation(None)
+    ok = _lib.Speculation("replay", rec.log)
+    _lib.set_speculation(ok)
+    assert a() == [3, 4]
+    _lib.set_speculation(None)
+    assert ok.validate()
+    bad = _lib.Speculation("replay", rec.log)
+    _lib.set_speculation(bad)
+    assert b() == [3, 4]          # other call site: a real readback
+    _lib.set_speculation(None)
+    assert not bad.validate()
+    changed = _lib.Speculation("replay", [(rec.log[0][0], [3, 5])])
+    _lib.set_speculation(changed)
+    a()
+    _lib.set_speculation(None)
+    assert not changed.validate()
