@@ -206,7 +206,9 @@ class CachedTable(TableSource):
                 n = hit.num_rows
         if missing:
             self.misses += len(missing)
-            b = self.source.scan(missing, ctx)
+            from ..ops._lib import unlogged
+            with unlogged():     # a cache fill, not part of the query's repeatable readbacks
+                b = self.source.scan(missing, ctx)
             for c in missing:
                 col = b.columns[c]
                 _mark_resident(col)

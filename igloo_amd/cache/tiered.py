@@ -78,8 +78,9 @@ class TieredCache:
         self._host: "OrderedDict[str, Tuple[pa.Table, Any, int, str]]" = OrderedDict()  # kind: batch|batches|table
         self._disk: "OrderedDict[str, Tuple[str, Any, int, str]]" = OrderedDict()
         self.stats = {"hits": 0, "misses": 0, "evictions": 0, "spills": 0, "promotions": 0}
-        #: bumped whenever cached data may change identity (put / drop / evict /
-        #: re-materialise); engine.py keys replayed query cardinalities on it
+        #: bumped whenever cached data changes identity (replace / drop / evict /
+        #: re-materialise from a lower tier; adding a new key does not);
+        #: engine.py keys replayed query readbacks on it
         self.generation = 0
         self._dir = None
         if self.config.disk_path:
@@ -116,8 +117,8 @@ class TieredCache:
     # ---------------------------------------------------------------- API
     def put(self, key: str, value: Value, version: Any = None) -> None:
         with self._lock:
-            self.generation += 1
-            self._drop(key)
+            if key in self:
+                self._drop(key)   # replaced data: _drop bumps the generation
             nb = _nbytes(value)
             if isinstance(value, Batch):
                 self._hbm[key] = (value, version, nb)

@@ -78,6 +78,14 @@ class QueryResult:
         return pretty_format(self.table)
 
 
+def _confirm(prev, cur):
+    """Replayable log from two recordings of the same query, or None when their
+    call sequences differ. Sites whose values differ become volatile (None)."""
+    if prev is None or len(prev) != len(cur) or any(a[0] != b[0] for a, b in zip(prev, cur)):
+        return None
+    return [(a[0], a[1] if a[1] == b[1] else None) for a, b in zip(prev, cur)]
+
+
 class QueryEngine:
     def __init__(self, device: Optional[str] = None, catalog: Optional[Catalog] = None, comm=None,
                  config: Optional[dict] = None, cache_hbm_gb: Optional[float] = None,
@@ -303,9 +311,11 @@ class QueryEngine:
         executions instead of waiting on the device for each (ops/_lib.py
         Speculation): the host enqueues the whole query while the GPU runs it,
         and one sync at the end checks every replayed value against the device.
-        A recording is replayed only after two consecutive executions produced
-        it identically; a failed check re-executes the query with real
-        readbacks (and after two failures the query is no longer replayed)."""
+        A recording is replayed once two executions produced the same call
+        sequence (values that differed between them are read back for real
+        every time); a replay that leaves the recorded sequence continues with
+        real readbacks and needs re-confirming; a value mismatch re-executes the query with
+        real readbacks (after two, the query is no longer replayed)."""
         from .ops import _lib
         if not (SPECULATE and key is not None and self.device.type == "cuda"
                 and (self.comm is None or self.comm.world_size == 1)):
@@ -315,8 +325,8 @@ class QueryEngine:
         if st is None:
             if len(self._spec) >= PLAN_CACHE_SIZE:
                 self._spec.pop(next(iter(self._spec)))
-            st = self._spec[skey] = {"log": None, "stable": False, "fails": 0}
-        if st["stable"] and st["fails"] < 2:
+            st = self._spec[skey] = {"log": None, "candidate": None, "fails": 0}
+        if st["log"] is not None and st["fails"] < 2:
             sp = _lib.Speculation("replay", st["log"])
             _lib.set_speculation(sp)
             try:
@@ -324,19 +334,23 @@ class QueryEngine:
             finally:
                 _lib.set_speculation(None)
             if sp.validate():
-                return batch, "replayed"
+                if not sp.complete:
+                    # the call sequence changed: this run's own sequence must be
+                    # confirmed by the next execution before it is replayed
+                    st["log"], st["candidate"] = None, sp.fresh
+                return batch, "replayed" if sp.complete else "partial"
             st["fails"] += 1
-            st["stable"] = False
+            st["log"] = st["candidate"] = None
             ctx = self.make_context()
-            log.info("speculative readbacks diverged (%s); re-executing", "site" if sp.diverged else "value")
+            log.warning("speculative readbacks did not match the device; re-executing")
         sp = _lib.Speculation("record")
         _lib.set_speculation(sp)
         try:
             batch = self._execute_plan(plan, ctx)
         finally:
             _lib.set_speculation(None)
-        st["stable"] = st["log"] is not None and st["log"] == sp.log
-        st["log"] = sp.log
+        st["log"] = _confirm(st["candidate"], sp.log)
+        st["candidate"] = sp.log if st["log"] is None else None
         return batch, "recorded"
 
     def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:

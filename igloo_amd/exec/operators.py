@@ -34,7 +34,7 @@ from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
-from ..ops._lib import launch, ptr, stream, to_host_int
+from ..ops._lib import launch, ptr, stream, to_host_int, unlogged
 from ..ops.gather import gather_tensor, take, take_many
 from ..ops.select import exclusive_scan, mask_to_indices
 from ..sql import logical as L
@@ -979,7 +979,8 @@ def _resident_ndv(t: torch.Tensor) -> int:
     """NDV of a resident key column (HyperLogLog, remembered on the tensor)."""
     d = getattr(t, "_igloo_ndv", None)
     if d is None:
-        d = max(1, int(round(H.hll_estimate(H.hll_sketch(t)))))
+        with unlogged():      # remembered on the resident tensor: a one-time build
+            d = max(1, int(round(H.hll_estimate(H.hll_sketch(t)))))
         try:
             t._igloo_ndv = d
         except (AttributeError, RuntimeError):
@@ -1490,7 +1491,11 @@ class MultiJoinExec(ExecNode):
                     if ctx.world > 1:
                         # every rank takes part, even with an empty slice (collective order must match)
                         regs = ctx.comm.allreduce_max_tensor(regs)
-                    g = int(round(H.hll_estimate(regs)))
+                    if b.num_rows and c.valid is None and getattr(c.data, "_igloo_resident", False):
+                        with unlogged():     # remembered on the resident column below
+                            g = int(round(H.hll_estimate(regs)))
+                    else:
+                        g = int(round(H.hll_estimate(regs)))
                 else:
                     g = 0
                     if b.num_rows:
@@ -1520,7 +1525,8 @@ def _derived_ndv(base, n: int) -> int:
     D = getattr(col.data, "_igloo_ndv", None)
     if D is None:
         k, _ = group_key_tensor(col)
-        D = max(int(round(H.hll_estimate(H.hll_sketch(k)))) if k.is_cuda else H.ndv(k), 1)
+        with unlogged():
+            D = max(int(round(H.hll_estimate(H.hll_sketch(k)))) if k.is_cuda else H.ndv(k), 1)
         try:
             col.data._igloo_ndv = D
         except (AttributeError, RuntimeError):

@@ -104,12 +104,16 @@ class Speculation:
     device sync: the host keeps launching while the GPU works) and queues a
     device-side copy of the real value; ``validate`` compares all of them with
     one sync at the end of the query. A call-site mismatch ends speculation
-    for the rest of the query (real readbacks from there on) and the query is
-    re-executed; so is any value mismatch. engine.py only replays a recording
-    that two consecutive executions over unchanged data produced identically.
+    for the rest of the query (real readbacks from there on) and the query's
+    recording is
+    re-recorded; any value mismatch re-executes the query. engine.py keys
+    recordings on the plan, the catalog version and the cache generation, and
+    trusts one only after two executions produced the same call sequence;
+    values that differed between those two (non-deterministic intermediates,
+    e.g. hash-assigned ids) are marked volatile (``None``) and always read back.
     """
 
-    __slots__ = ("mode", "log", "pos", "actual", "expected", "diverged", "checked")
+    __slots__ = ("mode", "log", "pos", "actual", "expected", "diverged", "checked", "fresh")
 
     def __init__(self, mode: str, log: list = None):
         self.mode = mode
@@ -119,20 +123,38 @@ class Speculation:
         self.expected: list = []
         self.diverged = False
         self.checked = 0
+        self.fresh: list = []   # replay: this run's own (site, values) sequence
+    @property
+    def complete(self) -> bool:
+        """The replay followed the recorded call sequence to its end."""
+        return not self.diverged and self.pos == len(self.log)
 
     def validate(self) -> bool:
-        """True when every replayed value equals the device value (one sync)."""
+        """True when every replayed value equals the device value (one sync).
+        Values handed out before a divergence were replayed at matching call
+        sites; after it, readbacks were real - so a diverged run is still
+        correct when this holds (its recording just needs refreshing)."""
         if self.mode != "replay":
             return True
-        if self.diverged or self.pos != len(self.log):
-            return False
         if not self.actual:
             return True
         dev = self.actual[0].device
         act = torch.cat(self.actual)
         exp = torch.tensor(self.expected, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         self.checked = act.numel()
-        return bool((act == exp).all().item())
+        ok = bool((act == exp).all().item())
+        if not ok and os.environ.get("IGLOO_SPEC_DEBUG"):
+            a, pos = act.tolist(), 0
+            for (site, vals) in self.log[:self.pos]:
+                if vals is None:
+                    continue
+                got = a[pos:pos + len(vals)]
+                if got != list(vals):
+                    code, line = site[0]
+                    print(f"[speculation] {code.co_filename}:{line} ({code.co_name}) replayed {list(vals)[:8]} "
+                          f"device {got[:8]}", flush=True)
+                pos += len(vals)
+        return ok
 
 
 _spec = threading.local()
@@ -140,6 +162,25 @@ _spec = threading.local()
 
 def set_speculation(s: "Speculation | None") -> None:
     _spec.cur = s
+
+
+class unlogged:
+    """Readbacks inside are real and stay out of the speculation log: used
+    around the one-time builds of derived structures remembered on resident
+    columns (stats, sortedness, indexes, sketches, narrow copies), so the
+    first execution of a query records the same readback sequence as the
+    later ones that find those structures cached."""
+
+    __slots__ = ("prev",)
+
+    def __enter__(self):
+        self.prev = getattr(_spec, "cur", None)
+        _spec.cur = None
+        return self
+
+    def __exit__(self, *exc):
+        _spec.cur = self.prev
+        return False
 
 
 def _site() -> tuple:
@@ -161,11 +202,18 @@ def to_host_ints(t: torch.Tensor) -> list:
     if not sp.diverged and sp.pos < len(sp.log) and sp.log[sp.pos][0] == site:
         v = sp.log[sp.pos][1]
         sp.pos += 1
+        if v is None:                  # volatile site: differs between runs, always read for real
+            v = _to_host_ints(t)
+            sp.fresh.append((site, v))
+            return v
         sp.actual.append(t.reshape(-1).to(torch.int64, copy=True))
         sp.expected.extend(v)
+        sp.fresh.append((site, v))
         return list(v)
     sp.diverged = True
-    return _to_host_ints(t)
+    v = _to_host_ints(t)
+    sp.fresh.append((site, v))
+    return v
 
 
 def _to_host_ints(t: torch.Tensor) -> list:

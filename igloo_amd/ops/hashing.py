@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import is_gpu, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints
+from ._lib import is_gpu, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
 from .select import exclusive_scan, mask_to_indices
 
 EMPTY_KEY = -(2**63)
@@ -56,7 +56,11 @@ def column_stats(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Tu
     launch("column_stats").column_stats(ptr(keys.contiguous()), keys.dtype == torch.int64,
                                          ptr(valid.contiguous() if valid is not None else None), n, ptr(out),
                                          stream(keys))
-    mn, mx, bad = to_host_ints(out)
+    if valid is None and getattr(keys, "_igloo_resident", False):
+        with unlogged():      # remembered below: a one-time build (ops/_lib.py unlogged)
+            mn, mx, bad = to_host_ints(out)
+    else:
+        mn, mx, bad = to_host_ints(out)
     res = ((mn, mx) if mn <= mx else None), (bad == 0 and valid is None)
     if valid is None and getattr(keys, "_igloo_resident", False):
         try:
@@ -269,6 +273,11 @@ def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = 
     hit = getattr(big, "_igloo_dense", None)
     if hit or not build or (hit is False and queries is None):
         return hit or None
+    with unlogged():          # built once per column tensor
+        return _dense_index_build(big, queries)
+
+
+def _dense_index_build(big: torch.Tensor, queries: Optional[int]):
     nb = big.numel()
     idx = False
     if nb:
@@ -347,7 +356,8 @@ def perm_index(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     if hit is not None:
         return hit
     from .sort import perm_sort_int
-    out = perm_sort_int(keys)
+    with unlogged():
+        out = perm_sort_int(keys)
     try:
         out[0]._igloo_sorted = True
         keys._igloo_perm = out
