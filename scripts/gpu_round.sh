@@ -12,7 +12,7 @@ if [ -z "$NOSUITE" ]; then
   timeout -k 10 700 $T tests -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "suite rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -z "$NOBENCH" ]; then
-  timeout -k 10 600 python bench.py --sf ${SF:-100} --steps 5 --warmup 2 --per-query > gpurun_out/bench.log 2>&1; rc=$?
+  timeout -k 10 600 python bench.py --sf ${SF:-100} --steps ${STEPS:-5} --warmup ${WARM:-1} --per-query > gpurun_out/bench.log 2>&1; rc=$?
   echo "bench rc=$rc"; grep -E "cold suite|Q[0-9]" gpurun_out/bench.log | tr '\n' ' '; echo; tail -1 gpurun_out/bench.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "$PROF" ]; then
