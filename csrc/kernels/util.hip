@@ -4,10 +4,12 @@
 //
 //   column_stats  -> {min, max, sorted flag} of an int32/int64 key column
 //                    (NULL rows skipped) in ONE read: every lane checks its
-//                    run of 8 rows plus the row before it; block min/max via
+//                    run of 64 bytes plus the row before it; block min/max via
 //                    wave shuffles, one atomic per block;
 //   run_bounds    -> bound[i] = (i == 0 || k[i] != k[i-1]) for run-id group-by
 //                    over clustered keys.
+#include <limits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -16,7 +18,6 @@ namespace kern {
 
 namespace {
 
-constexpr int kPer = 8;  // rows per lane
 
 __device__ inline int64_t wave_min(int64_t v) {
 #pragma unroll
@@ -35,44 +36,60 @@ __device__ inline int64_t wave_max(int64_t v) {
   return v;
 }
 
-template <typename T>
+// 64 bytes per lane per iteration (4 x dwordx4), min/max in the column's own
+// type; the NULL-free path (HAS_VALID = false, the common case: resident key
+// columns and join outputs) has no per-row branches: the sortedness check
+// compares each row with its neighbour inside the run plus one load of the
+// row before it. (SF100 PMC: the previous 8-row, per-row-checked loop ran at
+// 1.7 TB/s over 77 calls per suite.)
+template <typename T, bool HAS_VALID>
 __global__ __launch_bounds__(kBlock) void column_stats_kernel(const T* __restrict__ k, const uint8_t* __restrict__ valid,
                                                               int64_t n, long long* __restrict__ out) {
+  constexpr int kRun = 64 / sizeof(T);
   __shared__ int64_t smin[kWavesPerBlock], smax[kWavesPerBlock];
   __shared__ int sbad;
   if (threadIdx.x == 0) sbad = 0;
   __syncthreads();
-  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  T tmn = std::numeric_limits<T>::max(), tmx = std::numeric_limits<T>::min();
+  bool any = false;
   bool bad = false;
-  const int64_t stride = (int64_t)gridDim.x * kBlock * kPer;
-  for (int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kPer; base < n; base += stride) {
-    T v[kPer];
-    if (base + kPer <= n && sizeof(T) * kPer % 16 == 0 && (((uintptr_t)(k + base)) & 15) == 0) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock * kRun;
+  const bool aligned = (((uintptr_t)k) & 15) == 0;
+  for (int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kRun; base < n; base += stride) {
+    T v[kRun];
+    if (!HAS_VALID && aligned && base + kRun <= n) {
 #pragma unroll
-      for (int q = 0; q < (int)(sizeof(T) * kPer / 16); ++q) {
+      for (int q = 0; q < 4; ++q) {
         const uint4 w = reinterpret_cast<const uint4*>(k + base)[q];
         __builtin_memcpy(&v[q * 16 / sizeof(T)], &w, 16);
       }
-    } else {
+      const T before = base > 0 ? k[base - 1] : v[0];
+      bad |= v[0] < before;
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) v[j] = base + j < n ? k[base + j] : T(0);
+      for (int j = 0; j < kRun; ++j) {
+        tmn = v[j] < tmn ? v[j] : tmn;
+        tmx = v[j] > tmx ? v[j] : tmx;
+        if (j) bad |= v[j] < v[j - 1];
+      }
+      any = true;
+      continue;
     }
-    T prev = base > 0 ? k[base - 1] : v[0];
-    bool prev_ok = base > 0 && (valid == nullptr || valid[base - 1]);
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      if (base + j >= n) break;
-      const bool ok = valid == nullptr || valid[base + j];
-      if (ok) {
-        const int64_t x = (int64_t)v[j];
-        mn = x < mn ? x : mn;
-        mx = x > mx ? x : mx;
-        if (prev_ok && v[j] < prev) bad = true;
-        prev = v[j];
+    // tail / NULL-aware path
+    T prev = base > 0 ? k[base - 1] : T(0);
+    bool prev_ok = base > 0 && (!HAS_VALID || valid[base - 1]);
+    for (int j = 0; j < kRun && base + j < n; ++j) {
+      const T x = k[base + j];
+      if (!HAS_VALID || valid[base + j]) {
+        tmn = x < tmn ? x : tmn;
+        tmx = x > tmx ? x : tmx;
+        any = true;
+        if (prev_ok && x < prev) bad = true;
+        prev = x;
         prev_ok = true;
       }
     }
   }
+  int64_t mn = any ? (int64_t)tmn : INT64_MAX, mx = any ? (int64_t)tmx : INT64_MIN;
   mn = wave_min(mn);
   mx = wave_max(mx);
   const uint64_t anybad = __ballot(bad);
@@ -115,13 +132,23 @@ void column_stats(const void* keys, bool key64, const uint8_t* valid, int64_t n,
   // below its predecessor (only meaningful without NULLs)
   hipLaunchKernelGGL(stats_init_kernel, dim3(1), dim3(1), 0, stream, out);
   if (n <= 0) return;
-  const unsigned g = grid_for(n, kBlock * kPer, 4096);
-  if (key64)
-    hipLaunchKernelGGL(column_stats_kernel<int64_t>, dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys, valid, n,
-                       out);
-  else
-    hipLaunchKernelGGL(column_stats_kernel<int32_t>, dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys, valid, n,
-                       out);
+  const int run = key64 ? 8 : 16;
+  const unsigned g = grid_for(n, kBlock * run, 4096);
+  if (key64) {
+    if (valid)
+      hipLaunchKernelGGL((column_stats_kernel<int64_t, true>), dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys,
+                         valid, n, out);
+    else
+      hipLaunchKernelGGL((column_stats_kernel<int64_t, false>), dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys,
+                         valid, n, out);
+  } else {
+    if (valid)
+      hipLaunchKernelGGL((column_stats_kernel<int32_t, true>), dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys,
+                         valid, n, out);
+    else
+      hipLaunchKernelGGL((column_stats_kernel<int32_t, false>), dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys,
+                         valid, n, out);
+  }
   check_launch("util.column_stats", stream);
 }
 

@@ -30,8 +30,11 @@ def main():
         qs += list(range(int(lo), int(hi or lo) + 1))
     e = ig.QueryEngine(device="cuda:0")
     datagen.register(e, a.sf)
-    for q in qs:
-        e.sql(queries.QUERIES[q])
+    from igloo_amd.ops import jit
+    for _ in range(3):      # JIT compiles settle, speculation recordings confirmed
+        for q in qs:
+            e.sql(queries.QUERIES[q])
+        jit.wait_all(120)
     torch.cuda.synchronize()
     pr = cProfile.Profile()
     t0 = time.perf_counter()

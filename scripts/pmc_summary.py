@@ -61,6 +61,7 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--raw", action="store_true", help="also dump every counter (per wave where it is a count)")
+    ap.add_argument("--exclude", default=r"textgen|datagen|gen_|_gen\b|rand", help="kernel-name regex to drop (data generation)")
     a = ap.parse_args()
     counters = defaultdict(dict)
     times = defaultdict(float)
@@ -71,7 +72,8 @@ def main():
         for k, cs in per.items():
             counters[k].update(cs)
             times[k] = max(times[k], tns.get(k, 0))
-    rows = sorted(times.items(), key=lambda kv: -kv[1])[:a.top]
+    rx = re.compile(a.exclude) if a.exclude else None
+    rows = sorted(((k, t) for k, t in times.items() if not (rx and rx.search(k))), key=lambda kv: -kv[1])[:a.top]
     print(f"{'kernel':60s} {'ms':>8s} {'fetch GB':>9s} {'write GB':>9s} {'GB/s':>8s} {'%peak':>6s} "
           f"{'VALU/wave':>10s} {'LDS/wave':>9s} {'LDSconf':>8s} {'MFMA':>6s}")
     for k, t in rows:

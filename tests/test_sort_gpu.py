@@ -160,6 +160,15 @@ def test_column_stats_and_run_bounds(gpu_device, n, dtype):
             assert srt == (n < 2 or bool((x[1:] >= x[:-1]).all()))
     s = torch.sort(x).values
     assert H.column_stats(s.to(DEV))[1] is True
+    if n > 40:
+        # one inversion exactly at a lane-run boundary (16 int32 / 8 int64 rows), and a
+        # misaligned start (vector loads need 16-byte alignment: scalar path)
+        run = 16 if dtype == torch.int32 else 8
+        t = s.clone()
+        t[run], t[run - 1] = s[run - 1] - 1, s[run - 1]
+        assert H.column_stats(t.to(DEV))[1] is False
+        sub = s.to(DEV)[1:]
+        assert H.column_stats(sub) == ((int(s[1:].min()), int(s[1:].max())), True)
     if n > 1:
         bound = torch.empty(n, dtype=torch.bool, device=DEV)
         _lib.native().run_bounds(s.to(DEV).data_ptr(), dtype == torch.int64, n, bound.data_ptr(),
