@@ -317,38 +317,45 @@ class QueryEngine:
         real readbacks and needs re-confirming; a value mismatch re-executes the query with
         real readbacks (after two, the query is no longer replayed)."""
         from .ops import _lib
-        if not (SPECULATE and key is not None and self.device.type == "cuda"
-                and (self.comm is None or self.comm.world_size == 1)):
+        if not (SPECULATE and key is not None and self.device.type == "cuda"):
             return self._execute_plan(plan, ctx), None
+        comm = self.comm if self.comm is not None and self.comm.world_size > 1 else None
+
+        def agreed(ok: bool) -> bool:
+            # SPMD ranks decide together (every rank joins this collective after
+            # every speculative-capable execution, so the sequences stay aligned)
+            return ok if comm is None else comm.allreduce_ints([0 if ok else 1])[0] == 0
         skey = (key, self.catalog.version, self.cache.generation)
         st = self._spec.get(skey)
         if st is None:
             if len(self._spec) >= PLAN_CACHE_SIZE:
                 self._spec.pop(next(iter(self._spec)))
             st = self._spec[skey] = {"log": None, "candidate": None, "fails": 0}
-        if st["log"] is not None and st["fails"] < 2:
-            sp = _lib.Speculation("replay", st["log"])
+        replay = st["log"] is not None and st["fails"] < 2
+        for attempt in range(3):
+            sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
             _lib.set_speculation(sp)
             try:
                 batch = self._execute_plan(plan, ctx)
             finally:
                 _lib.set_speculation(None)
-            if sp.validate():
-                if not sp.complete:
-                    # the call sequence changed: this run's own sequence must be
-                    # confirmed by the next execution before it is replayed
-                    st["log"], st["candidate"] = None, sp.fresh
-                return batch, "replayed" if sp.complete else "partial"
-            st["fails"] += 1
+            ok = sp.validate()
+            if agreed(ok):
+                break
+            # some rank's replayed value did not match its device: every rank
+            # re-executes with real readbacks (the same collectives on all)
+            if replay and not ok:
+                st["fails"] += 1
             st["log"] = st["candidate"] = None
+            replay = False
             ctx = self.make_context()
             log.warning("speculative readbacks did not match the device; re-executing")
-        sp = _lib.Speculation("record")
-        _lib.set_speculation(sp)
-        try:
-            batch = self._execute_plan(plan, ctx)
-        finally:
-            _lib.set_speculation(None)
+        if sp.mode == "replay":
+            if not sp.complete:
+                # the call sequence changed: this run's own sequence must be
+                # confirmed by the next execution before it is replayed
+                st["log"], st["candidate"] = None, sp.fresh
+            return batch, "replayed" if sp.complete else "partial"
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
         return batch, "recorded"

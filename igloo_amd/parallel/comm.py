@@ -20,6 +20,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..ops._lib import to_host_f64s, to_host_ints
 from ..utils import faults
 from ..utils.errors import CommError
 from ..utils.log import get_logger
@@ -104,7 +105,7 @@ class Communicator:
         t = self._t([int(x)])
         self.calls += 1
         dist.all_reduce(t, group=self.group)
-        return int(t.item())
+        return to_host_ints(t)[0]
 
     def allreduce_ints(self, xs: Sequence[int]) -> List[int]:
         if faults.ACTIVE:
@@ -114,7 +115,7 @@ class Communicator:
         t = self._t([int(x) for x in xs])
         self.calls += 1
         dist.all_reduce(t, group=self.group)
-        return [int(v) for v in t.tolist()]
+        return to_host_ints(t)
 
     def allreduce_max_float(self, x: float) -> float:
         if faults.ACTIVE:
@@ -124,7 +125,7 @@ class Communicator:
         t = self._t([float(x)], torch.float64)
         self.calls += 1
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return float(t.item())
+        return to_host_f64s(t)[0]
 
     def allreduce_max_tensor(self, t: torch.Tensor) -> torch.Tensor:
         """Element-wise max over ranks (in a 32-bit copy: portable across backends)."""
@@ -163,7 +164,7 @@ class Communicator:
         out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.wire)
         self.calls += 1
         dist.all_gather_into_tensor(out, t, group=self.group)
-        v = out.tolist()
+        v = to_host_ints(out)
         return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
 
     def allgather_object(self, obj) -> list:
@@ -208,7 +209,7 @@ class Communicator:
         r = torch.empty(W, dtype=torch.int64, device=self.wire)
         self.calls += 1
         dist.all_to_all_single(r, s, group=self.group)
-        return [int(x) for x in r.tolist()]
+        return to_host_ints(r)
 
     def all_to_all_matrix(self, rows: Sequence[Sequence[int]]) -> List[List[int]]:
         """rows[r] = k ints for peer r; returns [r][k] received from every peer
@@ -223,7 +224,7 @@ class Communicator:
         r = torch.empty(W * k, dtype=torch.int64, device=self.wire)
         self.calls += 1
         dist.all_to_all_single(r, s, group=self.group)
-        v = r.tolist()
+        v = to_host_ints(r)
         return [v[i * k:(i + 1) * k] for i in range(W)]
 
     def all_gather_v(self, t: torch.Tensor, counts: Optional[List[int]] = None) -> Tuple[torch.Tensor, List[int]]:
