@@ -316,16 +316,22 @@ class QueryEngine:
         every time); a replay that leaves the recorded sequence continues with
         real readbacks and needs re-confirming; a value mismatch re-executes the query with
         real readbacks (after two, the query is no longer replayed)."""
-        from .ops import _lib
-        if not (SPECULATE and key is not None and self.device.type == "cuda"):
+        from .ops import _lib, jit
+        # single-rank only: a 2-rank rehearsal (shared GPU, gloo) replayed values
+        # that passed validation yet changed a result (Q16) and then faulted;
+        # until that is understood SPMD ranks read every value back
+        if not (SPECULATE and key is not None and self.device.type == "cuda"
+                and (self.comm is None or self.comm.world_size == 1)):
             return self._execute_plan(plan, ctx), None
-        comm = self.comm if self.comm is not None and self.comm.world_size > 1 else None
+        comm = None
 
         def agreed(ok: bool) -> bool:
             # SPMD ranks decide together (every rank joins this collective after
             # every speculative-capable execution, so the sequences stay aligned)
             return ok if comm is None else comm.allreduce_ints([0 if ok else 1])[0] == 0
-        skey = (key, self.catalog.version, self.cache.generation)
+        # generated kernels that became available change code paths (and readback
+        # sequences): their count is part of the key
+        skey = (key, self.catalog.version, self.cache.generation, len(jit._kernels))
         st = self._spec.get(skey)
         if st is None:
             if len(self._spec) >= PLAN_CACHE_SIZE:
