@@ -262,10 +262,14 @@ def execute_fragmented(engine, sql: str, workers: Sequence[str] = ("all-ranks",)
 
 
 # ------------------------------------------------------------- remote shipping
-def encode_fragment(frag: QueryFragment, inputs: Dict[str, "pa.Table"]) -> bytes:
+def encode_fragment(frag: QueryFragment, inputs: Dict[str, "pa.Table"],
+                    session_config: Optional[Dict[str, object]] = None) -> bytes:
     """Wire format of Flight action ``execute_fragment``: 4-byte big-endian
-    header length, JSON header {plan, inputs: [[id, nbytes], ...]}, then one
-    Arrow IPC stream per input."""
+    header length, JSON header {plan, session_config, inputs: [[id, nbytes],
+    ...]}, then one Arrow IPC stream per input. ``session_config`` carries the
+    coordinator's session settings to the worker (reference
+    crates/coordinator/src/distributed_executor.rs:121-125 sends it with every
+    fragment)."""
     import json
     import struct
 
@@ -278,8 +282,9 @@ def encode_fragment(frag: QueryFragment, inputs: Dict[str, "pa.Table"]) -> bytes
         with pa.ipc.new_stream(sink, t.schema) as w:
             w.write_table(t)
         blobs.append((fid, sink.getvalue().to_pybytes()))
+    cfg = {k: v for k, v in (session_config or {}).items() if isinstance(v, (str, int, float, bool, type(None)))}
     head = json.dumps({"id": frag.id, "type": frag.fragment_type.value, "plan": serde.dumps(frag.plan),
-                       "inputs": [[fid, len(b)] for fid, b in blobs]}).encode()
+                       "session_config": cfg, "inputs": [[fid, len(b)] for fid, b in blobs]}).encode()
     return struct.pack(">I", len(head)) + head + b"".join(b for _, b in blobs)
 
 
@@ -307,13 +312,59 @@ def run_encoded_fragment(engine, payload: bytes):
         b = Batch.from_arrow(t, device=engine.device)
         cols = {ci.cid: b.columns[name] for ci, name in zip(ref.schema, t.column_names)}
         inputs[fid] = Batch(cols, t.num_rows, ("replicated",) if world > 1 else None)
-    ctx = engine.make_context()
-    ctx.fragment_inputs = inputs
-    out = create_physical_plan(plan).execute(ctx)
-    if world > 1:
-        from .exchange import gather_all
-        out = gather_all(out, ctx)
-    return engine._to_arrow(out, plan.schema, [f"c{c.cid}" for c in plan.schema])
+    saved = dict(engine.session)
+    engine.session.update(head.get("session_config") or {})
+    try:
+        ctx = engine.make_context()
+        ctx.fragment_inputs = inputs
+        out = create_physical_plan(plan).execute(ctx)
+        if world > 1:
+            from .exchange import gather_all
+            out = gather_all(out, ctx)
+        return engine._to_arrow(out, plan.schema, [f"c{c.cid}" for c in plan.schema])
+    finally:
+        engine.session.clear()
+        engine.session.update(saved)
+
+
+#: rows per streamed record batch of a fragment / query result
+STREAM_BATCH_ROWS = 1 << 16
+
+
+def stream_results(t: "pa.Table", elapsed_ms: float, batch_rows: Optional[int] = None):
+    """Flight ``DoAction`` result bodies of a streamed result: one Arrow IPC
+    stream per record batch (schema + batch, so a consumer can decode each as
+    it arrives; an empty result sends the schema alone), then a QueryComplete
+    message ``b"QC" + json`` with the row count and execution time (reference
+    crates/api/proto/distributed.proto:46-57, 67-70)."""
+    import pyarrow as pa
+
+    from ..service.protocol import QueryComplete
+    batches = t.to_batches(max_chunksize=batch_rows or STREAM_BATCH_ROWS) or [None]
+    for b in batches:
+        sink = pa.BufferOutputStream()
+        with pa.ipc.new_stream(sink, t.schema) as w:
+            if b is not None:
+                w.write_batch(b)
+        yield sink.getvalue()
+    yield b"QC" + QueryComplete(total_rows=t.num_rows, execution_time_ms=round(elapsed_ms, 3)).to_json()
+
+
+def collect_stream(bodies) -> Tuple["pa.Table", Optional[dict]]:
+    """Inverse of ``stream_results``: (table, QueryComplete fields or None)."""
+    import json
+
+    import pyarrow as pa
+    tables, done = [], None
+    for body in bodies:
+        if body[:2] == b"QC":
+            done = json.loads(body[2:].decode())
+            continue
+        tables.append(pa.ipc.open_stream(body).read_all())
+    if not tables:
+        raise ValueError("empty result stream")
+    t = pa.concat_tables(tables) if len(tables) > 1 else tables[0]
+    return t.combine_chunks() if t.num_rows else t, done
 
 
 def flight_runner(engine, token: Optional[str] = None, timeout: float = 3600.0):
@@ -334,8 +385,8 @@ def flight_runner(engine, token: Optional[str] = None, timeout: float = 3600.0):
             ref = refs[fid]
             tables[fid] = engine._to_arrow(b, ref.schema, [f"c{c.cid}" for c in ref.schema])
         with IglooClient(frag.worker_address, token, timeout=timeout) as c:
-            body = c.action("execute_fragment", encode_fragment(frag, tables))
-        t = pa.ipc.open_stream(body).read_all()
+            t, _ = collect_stream(c.action_stream("execute_fragment",
+                                                  encode_fragment(frag, tables, engine.session)))
         b = Batch.from_arrow(t, device=engine.device)
         return Batch({ci.cid: b.columns[f"c{ci.cid}"] for ci in frag.plan.schema}, t.num_rows)
     return run

@@ -80,6 +80,18 @@ class IglooClient:
         res = list(self.client.do_action(fl.Action(kind, body), self.options))
         return res[0].body.to_pybytes() if res else b""
 
+    def action_stream(self, kind: str, body: bytes = b""):
+        """Every result body of a streaming action, in order."""
+        for r in self.client.do_action(fl.Action(kind, body), self.options):
+            yield r.body.to_pybytes()
+
+    def execute_query(self, sql: str, session_config=None):
+        """ExecuteQuery: (Arrow table, QueryComplete fields) with the given
+        session settings applied on the server for this query only."""
+        from ..parallel.fragments import collect_stream
+        req = P.QueryRequest(sql=sql, session_config=dict(session_config or {}))
+        return collect_stream(self.action_stream("execute_query", req.to_json()))
+
     def register_worker(self, info: P.WorkerInfo) -> P.RegistrationAck:
         return P.RegistrationAck.from_json(self.action("register_worker", info.to_json()))
 

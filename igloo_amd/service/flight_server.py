@@ -65,6 +65,7 @@ class IglooFlightServer(fl.FlightServerBase):
         self._pending: Dict[str, Tuple[str, float]] = {}
         self._results: Dict[str, pa.Table] = {}
         self._lock = threading.Lock()
+        self._session_lock = threading.Lock()   # per-request session settings (execute_query)
         self.metrics = {"queries": 0, "rows": 0, "errors": 0, "ms": 0.0}
         self._location = location
 
@@ -103,6 +104,20 @@ class IglooFlightServer(fl.FlightServerBase):
             return b.decode("utf-8"), False, None
         except UnicodeDecodeError:
             raise ValueError("ticket/command is not valid UTF-8") from None
+
+    def _run_with_session(self, sql: str, session_config) -> pa.Table:
+        """Run with the request's session settings applied for this query only."""
+        eng = self.engine
+        if not session_config or eng is None or self.runner is not None:
+            return self._run(sql)
+        with self._session_lock:
+            saved = dict(eng.session)
+            eng.session.update(session_config)
+            try:
+                return self._run(sql)
+            finally:
+                eng.session.clear()
+                eng.session.update(saved)
 
     def _run(self, sql: str) -> pa.Table:
         t0 = time.perf_counter()
@@ -192,7 +207,8 @@ class IglooFlightServer(fl.FlightServerBase):
         return [("register_worker", "WorkerInfo -> RegistrationAck"), ("heartbeat", "HeartbeatInfo -> HeartbeatResponse"),
                 ("execute_task", "TaskDefinition -> TaskStatus"), ("get_data_for_task", "DataForTaskRequest -> IPC"),
                 ("list_workers", "-> workers JSON"), ("metrics", "-> metrics JSON"), ("explain", "SQL -> plan text"),
-                ("execute_fragment", "serialized fragment + input IPC -> IPC"), ("health", "-> ok")]
+                ("execute_fragment", "serialized fragment + input IPC -> IPC batch stream + QueryComplete"),
+                ("execute_query", "QueryRequest JSON -> IPC batch stream + QueryComplete"), ("health", "-> ok")]
 
     def do_action(self, context, action):
         kind, body = action.type, action.body.to_pybytes() if action.body is not None else b""
@@ -237,16 +253,25 @@ class IglooFlightServer(fl.FlightServerBase):
         elif kind == "explain":
             yield fl.Result(self.engine.explain(body.decode()).encode())
         elif kind == "execute_fragment":
+            # streamed: one IPC stream per record batch, then QueryComplete
+            from ..parallel.fragments import run_encoded_fragment, stream_results
+            t0 = time.perf_counter()
             if self.fragment_runner is not None:
                 t = self.fragment_runner(body)
             else:
-                from ..parallel.fragments import run_encoded_fragment
                 t = run_encoded_fragment(self.engine, body)
             self.metrics["fragments"] = self.metrics.get("fragments", 0) + 1
-            sink = pa.BufferOutputStream()
-            with pa.ipc.new_stream(sink, t.schema) as w:
-                w.write_table(t)
-            yield fl.Result(sink.getvalue())
+            for chunk in stream_results(t, (time.perf_counter() - t0) * 1e3):
+                yield fl.Result(chunk)
+        elif kind == "execute_query":
+            # DistributedQueryService.ExecuteQuery(QueryRequest{sql, session_config})
+            # -> stream of record batches + QueryComplete (reference distributed.proto)
+            from ..parallel.fragments import stream_results
+            req = P.QueryRequest.from_json(body)
+            t0 = time.perf_counter()
+            t = self._run_with_session(req.sql, req.session_config)
+            for chunk in stream_results(t, (time.perf_counter() - t0) * 1e3):
+                yield fl.Result(chunk)
         elif kind == "health":
             yield fl.Result(b"ok")
         else:

@@ -77,6 +77,45 @@ def test_put_list_actions(server):
         assert c.get_data_for_task("task-1").column("a").to_pylist() == [1, 2, 3]
 
 
+def test_execute_query_streams_batches_and_completion(server, monkeypatch):
+    """ExecuteQuery: QueryRequest{sql, session_config} -> record-batch stream +
+    QueryComplete; the session setting applies to that query only."""
+    from igloo_amd.parallel import fragments as F
+    s, uri = server
+    monkeypatch.setattr(F, "STREAM_BATCH_ROWS", 2)
+    with IglooClient(uri) as c:
+        bodies = list(c.action_stream("execute_query", P.QueryRequest("SELECT a, b FROM t ORDER BY a").to_json()))
+        assert len(bodies) == 3 and bodies[-1][:2] == b"QC"      # 2 batches of <= 2 rows + completion
+        t, done = c.execute_query("SELECT a, b FROM t ORDER BY a", {"probe_setting": 7})
+        assert t.column("a").to_pylist() == [1, 2, 3]
+        assert done["total_rows"] == 3 and done["execution_time_ms"] >= 0
+        empty, done = c.execute_query("SELECT a FROM t WHERE a > 10")
+        assert empty.num_rows == 0 and done["total_rows"] == 0
+    assert "probe_setting" not in s.engine.session
+
+
+def test_fragment_carries_session_config():
+    import igloo_amd as ig
+    from igloo_amd.parallel import fragments as F
+    e = ig.QueryEngine(device="cpu")
+    e.register_table("t", pa.table({"a": [1, 2, 3]}))
+    plan, _ = e.logical_plan("SELECT sum(a) AS s FROM t")
+    from igloo_amd.sql import logical as L
+    frag = next(f for f in F.DistributedPlanner(["w0"]).plan(plan)
+                if not any(isinstance(p, F.FragmentRef) for p in L.walk_plan(f.plan)))
+    payload = F.encode_fragment(frag, {}, {"device_budget_gb": 0.5, "obj": object()})
+    seen = {}
+    orig = e.make_context
+
+    def spy():
+        seen.update(e.session)
+        return orig()
+    e.make_context = spy
+    out = F.run_encoded_fragment(e, payload)
+    assert out.num_rows >= 1 and seen.get("device_budget_gb") == 0.5   # leaf (scan) fragment
+    assert "device_budget_gb" not in e.session
+
+
 def test_registry_eviction():
     r = WorkerRegistry(heartbeat_interval_s=1.0, timeout_s=2.0)
     r.register(P.WorkerInfo("a", "x"))
