@@ -27,6 +27,7 @@ from .sql.binder import Binder, IdGen
 from .sql.logical import ColInfo, Plan
 from .sql.optimizer import optimize
 from .utils.errors import IglooError, NotSupported, PlanError
+from .utils import trace as _trace
 from .utils.log import get_logger
 
 #: cache optimized logical plans per SQL text (parse + bind + optimize cost
@@ -280,7 +281,8 @@ class QueryEngine:
         bq_names = names
         ctx = self.make_context()
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
-        batch, spec = self._execute_speculative(plan, ctx, key)
+        with _trace.Range("query"):
+            batch, spec = self._execute_speculative(plan, ctx, key)
         table = self._to_arrow(batch, plan.schema, bq_names)
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3

@@ -35,6 +35,7 @@ from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
 from ..ops._lib import launch, ptr, stream, to_host_int, unlogged
+from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
 from ..ops.select import exclusive_scan, mask_to_indices
 from ..sql import logical as L
@@ -80,8 +81,11 @@ class ExecContext:
             self.rows_scanned -= max(0, t.numel() - rows_read)
 
     def span(self, name: str):
-        """Time a phase inside an operator (device-synchronised; no-op unless analyzing)."""
-        return _Span(self, name) if self.analyze else _NOSPAN
+        """Time a phase inside an operator (device-synchronised; no-op unless
+        analyzing); a roctx range when IGLOO_ROCTX=1 (utils/trace.py)."""
+        if self.analyze:
+            return _Span(self, name)
+        return _trace.Range(name) if _trace.ENABLED else _NOSPAN
 
     def span_report(self) -> str:
         rows = sorted(self.spans.items(), key=lambda kv: -kv[1][0])
@@ -156,6 +160,15 @@ class ExecNode:
     logical: L.Plan
 
     def execute(self, ctx: ExecContext) -> Batch:
+        if _trace.ENABLED:
+            _trace.push(type(self).__name__)
+            try:
+                return self._execute(ctx)
+            finally:
+                _trace.pop()
+        return self._execute(ctx)
+
+    def _execute(self, ctx: ExecContext) -> Batch:
         if ctx.analyze:
             _sync(ctx)
             t0 = time.perf_counter()

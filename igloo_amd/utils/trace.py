@@ -1,0 +1,66 @@
+"""roctx ranges for rocprofv3 timelines (``IGLOO_ROCTX=1``).
+
+Every physical operator's execution, every EXPLAIN-ANALYZE phase span and
+every query become named ranges in the marker trace
+(``rocprofv3 --marker-trace --kernel-trace``), so kernels line up with the
+operator that launched them. Loaded through ctypes from ROCm's libroctx64;
+with the variable unset (the default) the hooks are a constant-False check.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+ENABLED = os.environ.get("IGLOO_ROCTX", "0") == "1"
+_lib = None
+
+
+def _load():
+    global _lib, ENABLED
+    if _lib is None:
+        for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so", "librocprofiler-sdk-roctx.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.restype = ctypes.c_int
+                lib.roctxRangePop.restype = ctypes.c_int
+                lib.roctxMarkA.argtypes = [ctypes.c_char_p]
+                _lib = lib
+                break
+            except (OSError, AttributeError):
+                continue
+        if _lib is None:
+            ENABLED = False
+    return _lib
+
+
+def push(name: str) -> None:
+    if ENABLED and _load() is not None:
+        _lib.roctxRangePushA(name.encode()[:200])
+
+
+def pop() -> None:
+    if ENABLED and _lib is not None:
+        _lib.roctxRangePop()
+
+
+def mark(name: str) -> None:
+    if ENABLED and _load() is not None:
+        _lib.roctxMarkA(name.encode()[:200])
+
+
+class Range:
+    """``with trace.Range("query Q1"): ...``"""
+
+    __slots__ = ("name",)
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        pop()
+        return False

@@ -1,0 +1,19 @@
+"""roctx ranges (utils/trace.py): operator / query ranges are pushed and popped
+in balance when IGLOO_ROCTX=1 (libroctx64 works without a GPU)."""
+import pyarrow as pa
+
+
+def test_roctx_ranges_balance(monkeypatch):
+    import igloo_amd as ig
+    from igloo_amd.utils import trace
+    calls = []
+    monkeypatch.setattr(trace, "ENABLED", True)
+    real_push, real_pop = trace.push, trace.pop
+    monkeypatch.setattr(trace, "push", lambda n: (calls.append(("push", n)), real_push(n)))
+    monkeypatch.setattr(trace, "pop", lambda: (calls.append(("pop", None)), real_pop()))
+    e = ig.QueryEngine(device="cpu")
+    e.register_table("t", pa.table({"a": [1, 2, 3], "b": [1, 1, 2]}))
+    assert e.sql("SELECT b, sum(a) AS s FROM t GROUP BY b ORDER BY b").to_pylist() == [{"b": 1, "s": 3}, {"b": 2, "s": 3}]
+    pushes = [n for k, n in calls if k == "push"]
+    assert len(pushes) == sum(1 for k, _ in calls if k == "pop") >= 3
+    assert any("Sort" in n or "Aggregate" in n for n in pushes)
