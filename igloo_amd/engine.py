@@ -79,6 +79,32 @@ class QueryResult:
         return pretty_format(self.table)
 
 
+def _host_columns(cols: List[Column]) -> List[Column]:
+    """Result columns moved to the host with ONE synchronisation: every device
+    buffer (values, validity, offsets, small dictionaries) is copied with a
+    non-blocking D2H copy, then the stream is synchronised once (instead of a
+    blocking copy per buffer inside ``Column.to_arrow``). A string column that
+    references a large device dictionary keeps its device path (it decodes
+    only the referenced strings on the GPU)."""
+    if not any(c.data.is_cuda for c in cols):
+        return cols
+
+    def cpu(t):
+        return None if t is None else t.to("cpu", non_blocking=True)
+
+    def move(c: Column) -> Column:
+        if not c.data.is_cuda:
+            return c
+        d = c.dictionary
+        if d is not None and len(d) > 2 * len(c) + 1024:
+            return c
+        return Column(c.dtype, cpu(c.data), cpu(c.valid), offsets=cpu(c.offsets),
+                      dictionary=move(d) if d is not None else None)
+    out = [move(c) for c in cols]
+    torch.cuda.current_stream(next(c.data.device for c in cols if c.data.is_cuda)).synchronize()
+    return out
+
+
 def _confirm(prev, cur):
     """Replayable log from two recordings of the same query, or None when their
     call sequences differ. Sites whose values differ become volatile (None)."""
@@ -379,8 +405,8 @@ class QueryEngine:
 
     def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str]) -> pa.Table:
         arrays, fields = [], []
-        for ci, nm in zip(schema, names):
-            col = batch.columns[ci.cid]
+        host = _host_columns([batch.columns[ci.cid] for ci in schema])
+        for ci, nm, col in zip(schema, names, host):
             arr = col.to_arrow()
             want = ci.dtype.to_arrow() if ci.dtype.kind != "null" else pa.null()
             if arr.type != want:

@@ -1,0 +1,30 @@
+#!/bin/bash
+# rocprofv3 marker + kernel trace of a few warm SF10 queries with roctx ranges
+# per query / operator / phase (IGLOO_ROCTX=1); summarised per range name.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+R="$(pwd)"
+rm -rf "$R/gpurun_out/roctx"
+IGLOO_ROCTX=1 IGLOO_PROF_GAP=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv \
+  -d "$R/gpurun_out/roctx" -o run -- python3 "$R/bench.py" --sf ${SF:-10} --source hbm --queries ${QS:-3,5,9} \
+  --steps 1 --warmup 2 > "$R/gpurun_out/roctx.log" 2>&1 || exit 1
+python3 - "$R/gpurun_out/roctx" <<'PY'
+import csv, glob, sys
+from collections import defaultdict
+f = (glob.glob(sys.argv[1] + "/**/*marker_api_trace.csv", recursive=True) or [None])[0]
+if f is None:
+    print("no marker trace"); sys.exit(0)
+rows = list(csv.DictReader(open(f)))
+print("columns:", list(rows[0].keys()) if rows else [])
+agg = defaultdict(lambda: [0.0, 0])
+for r in rows:
+    name = r.get("Message") or r.get("Function") or "?"
+    try:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    except (KeyError, ValueError):
+        continue
+    agg[name][0] += d
+    agg[name][1] += 1
+for k, (ms, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:30]:
+    print(f"{ms:10.3f} ms {n:6d}  {k}")
+PY
