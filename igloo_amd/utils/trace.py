@@ -18,7 +18,8 @@ _lib = None
 def _load():
     global _lib, ENABLED
     if _lib is None:
-        for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so", "librocprofiler-sdk-roctx.so"):
+        # the rocprofiler-sdk roctx first: rocprofv3 --marker-trace records its ranges
+        for name in ("/opt/rocm/lib/librocprofiler-sdk-roctx.so", "librocprofiler-sdk-roctx.so", "libroctx64.so"):
             try:
                 lib = ctypes.CDLL(name)
                 lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
