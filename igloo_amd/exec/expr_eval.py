@@ -23,6 +23,7 @@ import torch
 from .. import types as T
 from ..columnar import Batch, Column
 from ..ops import misc as M
+from ..ops._lib import to_host_ints
 from ..ops import strings as S
 from ..sql.expr import (AggCall, BinOp, Case, Cast, ColRef, Expr, Func, InList, IsNull, Like, Lit, Neg, Not,
                         SubqueryExpr)
@@ -191,7 +192,7 @@ class Evaluator:
             if t.is_float:
                 out = a / c
                 zero = (c == 0) if isinstance(c, torch.Tensor) else None
-                if zero is not None and bool(zero.any()):
+                if zero is not None and _any(zero):
                     valid = _and_valid(valid, ~zero)
                 elif not isinstance(c, torch.Tensor) and c == 0:
                     return Scalar(None, t)
@@ -200,7 +201,7 @@ class Evaluator:
                     zero = c == 0
                     safe = torch.where(zero, torch.ones_like(c), c)
                     out = torch.div(a, safe, rounding_mode="trunc")
-                    if bool(zero.any()):
+                    if _any(zero):
                         valid = _and_valid(valid, ~zero)
                 else:
                     if c == 0:
@@ -606,7 +607,7 @@ def _overflow_guard(a, c):
     """Decimal product whose static precision exceeds 18 digits: verify at run time
     that the int64 product cannot overflow (raises otherwise)."""
     ts = [v for v in (a, c) if isinstance(v, torch.Tensor) and v.numel()]
-    dev_max = iter(torch.stack([v.abs().max().to(torch.int64) for v in ts]).tolist() if ts else [])  # one sync
+    dev_max = iter(to_host_ints(torch.stack([v.abs().max().to(torch.int64) for v in ts])) if ts else [])  # one sync
 
     def mx(v):
         if isinstance(v, torch.Tensor):
@@ -615,6 +616,10 @@ def _overflow_guard(a, c):
     if mx(a) * mx(c) >= 2**63:
         raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
     return a, c
+
+
+def _any(m: torch.Tensor) -> bool:
+    return bool(to_host_ints(m.any().to(torch.int64))[0]) if m.is_cuda else bool(m.any())
 
 
 def _bool_parts(v: Column):

@@ -34,7 +34,7 @@ from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
-from ..ops._lib import launch, ptr, stream, to_host_int, unlogged
+from ..ops._lib import launch, ptr, stream, to_host_int, to_host_ints, unlogged
 from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
 from ..ops.select import exclusive_scan, mask_to_indices
@@ -477,7 +477,7 @@ def group_key_tensor(c: Column) -> Tuple[torch.Tensor, Column]:
     k = _num_key(c)
     if c.valid is not None:
         if k.numel():
-            mx = int(k.max().item())
+            mx = to_host_int(k.max().to(torch.int64))
             k = torch.where(c.valid, k.to(torch.int64), torch.full((k.numel(),), mx + 1, dtype=torch.int64, device=k.device))
     return k, c
 
@@ -634,7 +634,7 @@ def grace_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fa
     ev = ctx.evaluator
     if kind == "anti" and null_aware:
         rcols = [ev.column(b, rb) for _, b in on]
-        if any(c.valid is not None and bool((~c.valid).any().item()) for c in rcols):
+        if any(c.valid is not None and to_host_int((~c.valid).any().to(torch.int64)) for c in rcols):
             return _empty_like(lb)
     P = 2
     while need / P > ctx.budget / 2 and P < 1024:
@@ -696,7 +696,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
     dev = ctx.device
     # null-aware anti join (NOT IN): a NULL on the build side empties the result
     if kind == "anti" and null_aware:
-        if rvalid is not None and n_r and bool((~rvalid).any().item()):
+        if rvalid is not None and n_r and to_host_int((~rvalid).any().to(torch.int64)):
             return _empty_like(lb)
         if n_r and lvalid is not None:
             keep = mask_to_indices(lvalid)
@@ -980,7 +980,7 @@ def concat_columns(cols: List[Column]) -> Column:
         for i, p in enumerate(plains):
             o = p.offsets if i == 0 else p.offsets[1:]
             offs.append(o + base)
-            base += int(p.offsets[-1].item())
+            base += to_host_int(p.offsets[-1:])
         return Column(T.UTF8, torch.cat([p.data for p in plains]), valid, offsets=torch.cat(offs))
     if any(c.is_wide for c in cols) and not all(c.is_wide for c in cols):
         cols = [c if c.is_wide else Column(c.dtype, torch.stack([c.data, c.data >> 63], 1), c.valid) for c in cols]
@@ -1758,7 +1758,7 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
             return None
         parts.add(k)
         checks.append((idx != idx.index_select(0, rr)).sum())
-    if checks and int(torch.stack(checks).sum().item()):
+    if checks and to_host_int(torch.stack(checks).sum().to(torch.int64)):
         return None
     ctx.sorted_gids = srt
     taken = []
@@ -1810,7 +1810,7 @@ def _encode_groups(gcols: List[Column], ctx):
             if c.valid is not None:
                 m = m + (c.valid != c.valid.index_select(0, rr)).sum()
             bad.append((i, m))
-        counts = torch.stack([m for _, m in bad]).tolist()
+        counts = to_host_ints(torch.stack([m for _, m in bad]).to(torch.int64))
         needed = [lead] + [i for (i, _), cnt in zip(bad, counts) if cnt]
         if len(needed) == 1:
             return gid, ng, rep, reps_src
@@ -1954,7 +1954,7 @@ def _avg(s: torch.Tensor, c: torch.Tensor, src, t) -> torch.Tensor:
         up = 10 ** (t.scale - (src.scale if src.is_decimal else 0))
         if s.dim() == 1:
             lim = (2**63 - 1) // up
-            if bool((s.abs() < lim).all().item()):
+            if to_host_int((s.abs() < lim).all().to(torch.int64)):
                 num = s * up
                 q = torch.div(num.abs() + cc // 2, cc, rounding_mode="floor") * torch.sign(num)
                 return q

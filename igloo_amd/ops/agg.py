@@ -27,7 +27,7 @@ def _ordered_to_f64(x: torch.Tensor) -> torch.Tensor:
 
 def _wide_to_result(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
     fits = hi == (lo >> 63)
-    if bool(fits.all().item()):
+    if (to_host_ints(fits.all().to(torch.int64))[0] if fits.is_cuda else bool(fits.all().item())):
         return lo
     return torch.stack([lo, hi], dim=1)
 

@@ -6,7 +6,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import idx_dtype, is_gpu, launch, ptr, stream
+from ._lib import idx_dtype, is_gpu, launch, ptr, stream, to_host_ints
 
 DATE_FIELDS = {"year": 0, "month": 1, "day": 2, "quarter": 3, "dow": 4, "doy": 5}
 
@@ -52,7 +52,7 @@ def hash_partition(keys: torch.Tensor, nparts: int) -> Tuple[torch.Tensor, List[
     perm = torch.empty(n, dtype=it, device=keys.device)
     N.partition_run(ptr(keys), keys.dtype == torch.int64, n, nparts, ptr(ws), ptr(ws) + 8 * nparts * blocks,
                     ptr(perm), it == torch.int64, stream(keys))
-    starts = ws[: nparts * blocks].view(nparts, blocks)[:, 0].tolist()
+    starts = to_host_ints(ws[: nparts * blocks].view(nparts, blocks)[:, 0])
     counts = [(starts[p + 1] if p + 1 < nparts else n) - starts[p] for p in range(nparts)]
     return perm, counts
 

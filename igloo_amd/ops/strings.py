@@ -18,7 +18,7 @@ import torch
 from .. import types as T
 from ..columnar import Column
 from .gather import gather_tensor
-from ._lib import is_gpu, launch, ptr, stream
+from ._lib import is_gpu, launch, ptr, stream, to_host_int
 from .gather import take
 from .hashing import group_ids
 from .select import offsets_from_lengths
@@ -214,7 +214,7 @@ def _case(col: Column, up: bool) -> Column:
     out = torch.empty_like(col.data)
     flag = torch.zeros(1, dtype=torch.int32, device=col.device)
     launch("str_case").str_case(ptr(col.data), col.data.numel(), up, ptr(out), ptr(flag), stream(out))
-    if int(flag.item()):
+    if to_host_int(flag):
         # non-ASCII bytes present: full Unicode case mapping can change byte
         # lengths ('ß' -> 'SS'), so take the exact host path.
         return _host_roundtrip(col, pc.utf8_upper if up else pc.utf8_lower)
@@ -306,7 +306,7 @@ def dict_encode(col: Column) -> Column:
     ai = torch.arange(n, dtype=torch.int32, device=col.device)
     launch("str_eq_rows").str_eq_rows(ptr(col.offsets), ptr(col.data), ptr(ai), ptr(col.offsets), ptr(col.data),
                                       ptr(ri), False, n, ptr(mism), stream(mism))
-    if int(mism.item()):
+    if to_host_int(mism):
         return Column.from_arrow(pc.dictionary_encode(col.to_arrow()), device=col.device)
     dictionary = take(col, rep)
     dictionary.valid = None
