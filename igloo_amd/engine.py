@@ -344,7 +344,7 @@ class QueryEngine:
         every time); a replay that leaves the recorded sequence continues with
         real readbacks and needs re-confirming; a value mismatch re-executes the query with
         real readbacks (after two, the query is no longer replayed)."""
-        from .ops import _lib, jit
+        from .ops import _lib
         # single-rank only: a 2-rank rehearsal (shared GPU, gloo) replayed values
         # that passed validation yet changed a result (Q16) and then faulted;
         # until that is understood SPMD ranks read every value back
@@ -357,9 +357,10 @@ class QueryEngine:
             # SPMD ranks decide together (every rank joins this collective after
             # every speculative-capable execution, so the sequences stay aligned)
             return ok if comm is None else comm.allreduce_ints([0 if ok else 1])[0] == 0
-        # generated kernels that became available change code paths (and readback
-        # sequences): their count is part of the key
-        skey = (key, self.catalog.version, self.cache.generation, len(jit._kernels))
+        # (a generated kernel that becomes available changes the code path and
+        # so the readback call sites: the replay diverges, stays correct, and the
+        # new sequence is confirmed by the next execution)
+        skey = (key, self.catalog.version, self.cache.generation)
         st = self._spec.get(skey)
         if st is None:
             if len(self._spec) >= PLAN_CACHE_SIZE:

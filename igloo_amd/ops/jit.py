@@ -39,6 +39,7 @@ _lock = threading.Lock()
 _kernels: Dict[str, "JitKernel"] = {}
 _pending: Dict[str, cf.Future] = {}
 _failed: Dict[str, str] = {}
+_names: Dict[str, str] = {}
 _pool: Optional[cf.ThreadPoolExecutor] = None
 STATS = {"compiled": 0, "disk_hits": 0, "launches": 0, "fallbacks": 0, "failed": 0}
 
@@ -128,6 +129,7 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
                 _pool = cf.ThreadPoolExecutor(max_workers=int(os.environ.get("IGLOO_JIT_THREADS", "2")),
                                               thread_name_prefix="igloo-jit")
             _pending[key] = _pool.submit(_compile, src, name, key)
+            _names[key] = name
             STATS["fallbacks"] += 1
             return None
         if not fut.done():
@@ -146,10 +148,25 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
 
 
 def wait_all(timeout: Optional[float] = None) -> None:
-    """Block until every submitted compile finished (bench warmup, tests)."""
+    """Block until every submitted compile finished, then load them all (so
+    the set of generated kernels changes at one point, not query by query)."""
     with _lock:
         futs = list(_pending.values())
     cf.wait(futs, timeout=timeout)
+    with _lock:
+        for key, fut in list(_pending.items()):
+            if not fut.done():
+                continue
+            del _pending[key]
+            try:
+                code = fut.result()
+            except Exception as e:   # noqa: BLE001 - recorded, the interpreted kernels stay
+                _failed[key] = str(e)
+                STATS["failed"] += 1
+                continue
+            name = _names.get(key, "")
+            if name:
+                _load(code, name, key)
 
 
 def failures() -> List[str]:
