@@ -418,6 +418,140 @@ def agg_source(sh: _Shape, terms, has_mask: bool, keys, G: int, aggs, split: Seq
     return "\n".join(L)
 
 
+MFMA = os.environ.get("IGLOO_FF_JIT_MFMA", "1") == "1"
+MFMA_COL = 272   # LDS bytes per limb column: 256 rows + 16 (spreads a ds_read_b128 over all banks)
+
+MFMA_PRELUDE = r"""
+typedef int v4i __attribute__((ext_vector_type(4)));
+// byte b of each of x0..x3 packed into one dword (v_perm_b32 pairs + merge)
+__device__ __forceinline__ u32 limb_dword(u32 x0, u32 x1, u32 x2, u32 x3, u32 b) {
+  const u32 sel = b | ((b + 4) << 8);
+  const u32 p01 = __builtin_amdgcn_perm(x1, x0, sel);
+  const u32 p23 = __builtin_amdgcn_perm(x3, x2, sel);
+  return __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+}
+// 0x01 in each byte of x equal to the matching byte of g4
+__device__ __forceinline__ u32 bytes_eq(u32 x, u32 g4) {
+  const u32 d = x ^ g4;
+  const u32 y = ~(((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d | 0x7f7f7f7fu);
+  return y >> 7;
+}
+"""
+
+
+def mfma_agg_source(sh: _Shape, terms, has_mask: bool, keys, G: int, aggs) -> Tuple[str, int]:
+    """SUM / COUNT over 2..16 groups as one-hot x byte-limb products on the
+    matrix cores (v_mfma_i32_16x16x64_i8), the generated-kernel form of
+    csrc/kernels/fused.hip ff_mfma_agg_kernel (see its comment for the
+    fragment maps and the biased lower limbs). Limb counts come from the
+    static value bounds. Returns (source, LDS bytes per block)."""
+    assert ROWS == 4 and 1 < G <= 16
+    NA = len(aggs)
+    lines: List[str] = []
+    vals_per_row = []
+    for j in range(ROWS):
+        V = _Values(sh, j)
+        vals_per_row.append([V.value(tuple(fs), bool(chk)) for _, chk, fs in aggs])
+        lines.append(V.lines)
+    col0, nlimb, col = [], [], 0
+    for i in range(NA):
+        bnd = max(v[i][1] for v in vals_per_row)
+        nbits = min(64, max(1, int(bnd).bit_length()) + 1)
+        nl = (nbits + 7) // 8
+        col0.append(col)
+        nlimb.append(nl)
+        col += nl
+    cnt_col = col
+    ncols = col + 1
+    NT = (ncols + 15) // 16
+    if NT > 4:
+        raise ValueError("too many limb columns")
+    NC = NT * 16
+    tile_bytes = (NC + 1) * MFMA_COL
+    L = [f"#define ROWS {ROWS}", PRELUDE, MFMA_PRELUDE,
+         f"extern \"C\" __global__ __launch_bounds__({BLOCK}) void igloo_jit_scan_agg_mfma("]
+    ps = _params(sh, has_mask) + ["i64* __restrict__ counts"]
+    for i in range(NA):
+        ps += [f"i64* __restrict__ d{i}", f"i64* __restrict__ e{i}"]
+    ps += ["int* __restrict__ ovf", "i64 n"]
+    L.append("    " + ", ".join(ps) + ") {")
+    L.append(f"  __shared__ __attribute__((aligned(16))) u8 tile[{BLOCK // 64}][{tile_bytes}];")
+    L.append("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;")
+    L.append("  u8* T = tile[wave];")
+    L.append(f"  u8* gidb = T + {NC * MFMA_COL};")
+    L.append(f"  for (int c = 0; c < {NC}; ++c) *(u32*)(T + c * {MFMA_COL} + 4 * lane) = c == {cnt_col} ? 0x01010101u : 0u;")
+    L.append(f"  v4i acc[{NT}];")
+    L.append(f"  i64 acc64[{NT}][4];")
+    L.append(f"  for (int t = 0; t < {NT}; ++t) {{ acc[t] = v4i{{0, 0, 0, 0}}; for (int i = 0; i < 4; ++i) acc64[t][i] = 0; }}")
+    L.append("  int of = 0, steps = 0;")
+    L.append("  const u32 g4 = (u32)(lane & 15) * 0x01010101u;")
+    L.append("  const int q16 = 16 * (lane >> 4);")
+    L.append(f"  const i64 step = (i64)gridDim.x * {BLOCK * ROWS};")
+    # wave-uniform loop: every lane of a wave runs every MFMA
+    L.append(f"  for (i64 wbase = (i64)blockIdx.x * {BLOCK * ROWS} + (i64)wave * {64 * ROWS}; wbase < n; wbase += step) {{")
+    L.append("    const i64 r = wbase + 4 * lane;")
+    L += ["    " + x for x in _loads(sh, has_mask)]
+    for j in range(ROWS):
+        p = f"lv{j} && " + _terms_expr(sh, terms, j) + (f" && mk{j}" if has_mask else "")
+        g = " + ".join(f"(i32)(x{k}_{j} - {_lit(lo)}) * {mul}" if lo else f"(i32)x{k}_{j} * {mul}"
+                       for k, lo, mul in keys) or "0"
+        L.append(f"    const bool p{j} = {p};")
+        L.append(f"    const u32 g{j} = p{j} ? (u32)({g}) & 0xffu : 0xffu;")
+        L += ["    " + x for x in lines[j]]
+    L.append(f"    *(u32*)(gidb + 4 * lane) = g0 | (g1 << 8) | (g2 << 16) | (g3 << 24);")
+    for i in range(NA):
+        v = [vals_per_row[j][i][0] for j in range(ROWS)]
+        L.append(f"    {{ const i64 a0 = (i64){v[0]}, a1 = (i64){v[1]}, a2 = (i64){v[2]}, a3 = (i64){v[3]};")
+        for l in range(nlimb[i]):
+            half = "" if l < 4 else " >> 32"
+            xs = ", ".join(f"(u32)((u64)a{j}{half})" for j in range(ROWS))
+            flip = " ^ 0x80808080u" if l != nlimb[i] - 1 else ""
+            L.append(f"      *(u32*)(T + {(col0[i] + l) * MFMA_COL} + 4 * lane) = limb_dword({xs}, {l % 4}u){flip};")
+        L.append("    }")
+    L.append("    __builtin_amdgcn_wave_barrier();")
+    L.append("#pragma unroll")
+    L.append("    for (int s = 0; s < 4; ++s) {")
+    L.append("      const uint4 gv = *(const uint4*)(gidb + 64 * s + q16);")
+    L.append("      v4i af;")
+    L.append("      af[0] = (int)bytes_eq(gv.x, g4); af[1] = (int)bytes_eq(gv.y, g4);")
+    L.append("      af[2] = (int)bytes_eq(gv.z, g4); af[3] = (int)bytes_eq(gv.w, g4);")
+    L.append("#pragma unroll")
+    L.append(f"      for (int t = 0; t < {NT}; ++t) {{")
+    L.append(f"        const uint4 bw = *(const uint4*)(T + (16 * t + (lane & 15)) * {MFMA_COL} + 64 * s + q16);")
+    L.append("        const v4i bf = v4i{(int)bw.x, (int)bw.y, (int)bw.z, (int)bw.w};")
+    L.append("        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf, acc[t], 0, 0, 0);")
+    L.append("      }")
+    L.append("    }")
+    L.append("    __builtin_amdgcn_wave_barrier();")
+    L.append("    if (++steps == 4096) {")
+    L.append(f"      steps = 0;")
+    L.append(f"      for (int t = 0; t < {NT}; ++t) {{ for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i]; acc[t] = v4i{{0, 0, 0, 0}}; }}")
+    L.append("    }")
+    L.append("  }")
+    L.append(f"  for (int t = 0; t < {NT}; ++t) for (int i = 0; i < 4; ++i) acc64[t][i] += acc[t][i];")
+    L.append("  __syncthreads();")
+    L.append(f"  long long (*red)[{NC}][16] = reinterpret_cast<long long (*)[{NC}][16]>(&tile[0][0]);")
+    L.append(f"  for (int t = 0; t < {NT}; ++t) for (int i = 0; i < 4; ++i) red[wave][16 * t + (lane & 15)][4 * (lane >> 4) + i] = acc64[t][i];")
+    L.append("  __syncthreads();")
+    L.append(f"  for (int s = threadIdx.x; s < {G * (NA + 1)}; s += {BLOCK}) {{")
+    L.append(f"    const int g = s / {NA + 1}, o = s % {NA + 1};")
+    L.append(f"    i64 cnt = 0; for (int w = 0; w < {BLOCK // 64}; ++w) cnt += red[w][{cnt_col}][g];")
+    L.append(f"    if (o == {NA}) {{ if (cnt) atomicAdd((unsigned long long*)&counts[g], (unsigned long long)cnt); continue; }}")
+    for i in range(NA):
+        L.append(f"    if (o == {i}) {{")
+        L.append("      __int128 tot = 0;")
+        for l in range(nlimb[i]):
+            bias = " + 128 * cnt" if l != nlimb[i] - 1 else ""
+            L.append(f"      {{ i64 x = 0; for (int w = 0; w < {BLOCK // 64}; ++w) x += red[w][{col0[i] + l}][g];"
+                     f" tot += (__int128)(x{bias}) << {8 * l}; }}")
+        L.append(f"      add128(&d{i}[g], &e{i}[g], tot);")
+        L.append("    }")
+    L.append("  }")
+    L.append("  if (of) atomicOr(ovf, 1);")
+    L.append("}")
+    return "\n".join(L), (BLOCK // 64) * tile_bytes
+
+
 def jit_aggregate(spec, keys, G: int, kaggs, counts: torch.Tensor, ovf: torch.Tensor, n: int, stream: int) -> bool:
     """kaggs: the interpreted kernel's aggregate tuples
     (op, checked, factors, dst, dst2, shared, vbits)."""
@@ -448,8 +582,18 @@ def jit_aggregate(spec, keys, G: int, kaggs, counts: torch.Tensor, ovf: torch.Te
     for op, chk, fs, d, d2, shared, vbits in kaggs:
         vb = vbits if 0 < vbits <= 64 else 64
         split.append(op == 0 and vb + lg + 1 > 63)
-    src = agg_source(sh, spec.terms, has_mask, keys, G, aggs, split, lanes)
-    k = jit.get(src, "igloo_jit_scan_agg")
+    name = "igloo_jit_scan_agg"
+    if MFMA and 1 < G <= 16 and all(op == 0 for op, *_ in aggs) and ROWS == 4:
+        try:
+            src, lds = mfma_agg_source(sh, spec.terms, has_mask, keys, G, aggs)
+            name = "igloo_jit_scan_agg_mfma"
+            per_cu = max(1, min(4, (160 * 1024) // lds))
+            grid = max(1, min(-(-n // (BLOCK * ROWS)), 256 * per_cu))
+        except ValueError:
+            src = agg_source(sh, spec.terms, has_mask, keys, G, aggs, split, lanes)
+    else:
+        src = agg_source(sh, spec.terms, has_mask, keys, G, aggs, split, lanes)
+    k = jit.get(src, name)
     if k is None:
         return False
     args = [t.data_ptr() for t in spec.cols] + ([spec.mask.data_ptr()] if has_mask else []) + [counts.data_ptr()]

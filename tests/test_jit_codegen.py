@@ -60,3 +60,14 @@ def test_or_groups_and_checked_overflow():
     src = FJ.agg_source(sh, terms, True, [], 1, aggs, [True, True], 64)
     assert "__builtin_mul_overflow" in src and "||" in src
     _compile(src, "igloo_jit_scan_agg")
+
+
+def test_q1_shape_mfma_compiles():
+    sh = cols(2, 1, 1, 2, 4, 1, 1)
+    terms = [(0, 0, -(2**63), 10471, 0)]
+    keys = [(1, 0, 2), (2, 0, 1)]
+    aggs = [(0, 0, ((3, 0, 1),)), (0, 0, ((4, 0, 1),)), (0, 0, ((4, 0, 1), (5, 100, -1))),
+            (0, 1, ((4, 0, 1), (5, 100, -1), (6, 100, 1))), (0, 0, ((5, 0, 1),))]
+    src, lds = FJ.mfma_agg_source(sh, terms, False, keys, 6, aggs)
+    assert "__builtin_amdgcn_mfma_i32_16x16x64_i8" in src and lds <= 160 * 1024
+    _compile(src, "igloo_jit_scan_agg_mfma")
