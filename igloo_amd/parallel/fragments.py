@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import enum
 import uuid
-from concurrent.futures import FIRST_EXCEPTION, ThreadPoolExecutor, wait
+from concurrent.futures import FIRST_COMPLETED, FIRST_EXCEPTION, ThreadPoolExecutor, wait
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple
 
@@ -216,12 +216,7 @@ class FragmentScheduler:
                         results[f.id] = self.runner(f, {d: results[d] for d in f.dependencies})
                         self.log.append((wave, f.id))
                 else:
-                    futs = {pool.submit(self.runner, f, {d: results[d] for d in f.dependencies}): f for f in ready}
-                    finished, _ = wait(futs, return_when=FIRST_EXCEPTION)
-                    for fut in futs:
-                        f = futs[fut]
-                        results[f.id] = fut.result()  # re-raises the first failure
-                        self.log.append((wave, f.id))
+                    return self._run_dataflow(fragments, pending, root_id, pool)
                 for f in ready:
                     done.add(f.id)
                     del pending[f.id]
@@ -234,6 +229,45 @@ class FragmentScheduler:
         finally:
             if pool is not None:
                 pool.shutdown(wait=False, cancel_futures=True)
+        return results[root_id]
+
+
+    def _run_dataflow(self, fragments, pending, root_id, pool):
+        """Concurrent schedule: a fragment starts as soon as ITS inputs are
+        done (not when the whole wave is), so a slow fragment only delays its
+        own consumers; the log records the order of starts (the "wave" field
+        is the start index)."""
+        results: Dict[str, object] = {}
+        done: Set[str] = set()
+        running: Dict[object, QueryFragment] = {}
+        started = 0
+        consumers: Dict[str, int] = {}
+        for f in fragments:
+            for d in f.dependencies:
+                consumers[d] = consumers.get(d, 0) + 1
+
+        def launch_ready():
+            nonlocal started
+            for f in fragments:
+                if f.id in pending and f.is_ready(done) and all(f is not g for g in running.values()):
+                    running[pool.submit(self.runner, f, {d: results[d] for d in f.dependencies})] = f
+                    self.log.append((started, f.id))
+                    started += 1
+        launch_ready()
+        while running:
+            finished, _ = wait(list(running), return_when=FIRST_COMPLETED)
+            for fut in finished:
+                f = running.pop(fut)
+                results[f.id] = fut.result()    # re-raises the first failure
+                done.add(f.id)
+                del pending[f.id]
+                for d in f.dependencies:       # inputs nobody else still needs
+                    consumers[d] -= 1
+                    if consumers[d] == 0 and d != root_id:
+                        results.pop(d, None)
+            launch_ready()
+        if pending:
+            raise ExecutionError("Circular dependency detected in query fragments")
         return results[root_id]
 
 

@@ -84,6 +84,25 @@ def test_scheduler_propagates_errors_and_runs_waves_concurrently():
         F.FragmentScheduler(run, max_concurrency=2).execute([mk("bad", []), mk("d", ["bad"])])
 
 
+def test_dataflow_schedule_starts_consumers_before_slow_siblings_finish():
+    """Concurrent schedule: c (needs only a) runs while b is still running."""
+    import threading
+    mk = lambda i, deps: F.QueryFragment(i, F.FragmentType.SCAN, L.Values([], []), dependencies=deps)  # noqa: E731
+    b_release, c_done = threading.Event(), threading.Event()
+
+    def run(f, inputs):
+        if f.id == "b":
+            assert b_release.wait(10), "c never ran while b was running"
+            return 10
+        if f.id == "c":
+            c_done.set()
+            b_release.set()
+        return sum(inputs.values()) + 1
+    frs = [mk("a", []), mk("b", []), mk("c", ["a"]), mk("d", ["b", "c"])]
+    assert F.FragmentScheduler(run, max_concurrency=3).execute(frs) == 10 + 2 + 1
+    assert c_done.is_set()
+
+
 def test_remote_fragments_over_flight(eng):
     """Fragments placed on a Flight worker run there; results equal local execution."""
     from igloo_amd.service.flight_server import IglooFlightServer
