@@ -418,7 +418,11 @@ def agg_source(sh: _Shape, terms, has_mask: bool, keys, G: int, aggs, split: Seq
     return "\n".join(L)
 
 
-MFMA = os.environ.get("IGLOO_FF_JIT_MFMA", "1") == "1"
+# Off by default: SF100 kernel A/B (profiles/r2_ab_jit_mfma{0,1}_q1q6.txt) measured
+# the generated MFMA aggregation at 1.45 ms for Q1 against 1.23 ms for the
+# generated LDS-atomic kernel - the scan is bound by loads / filter / value
+# arithmetic, not by the per-row accumulation the matrix cores take over.
+MFMA = os.environ.get("IGLOO_FF_JIT_MFMA", "0") == "1"
 MFMA_COL = 272   # LDS bytes per limb column: 256 rows + 16 (spreads a ds_read_b128 over all banks)
 
 MFMA_PRELUDE = r"""

@@ -17,13 +17,15 @@ from igloo_amd.ops._lib import KERNEL_CALLS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["interp", "jit"])
+@pytest.fixture(autouse=True, params=["interp", "jit", "jit-mfma"])
 def scan_mode(request, monkeypatch):
-    """Every test runs on the interpreted kernels (fused.hip) and on the
-    generated ones (exec/fused_jit.py, compiled synchronously)."""
+    """Every test runs on the interpreted kernels (fused.hip), on the generated
+    ones (exec/fused_jit.py, compiled synchronously) and on the generated
+    one-hot MFMA aggregation."""
     from igloo_amd.exec import fused_jit
     from igloo_amd.ops import jit
-    monkeypatch.setattr(fused_jit, "ENABLED", request.param == "jit")
+    monkeypatch.setattr(fused_jit, "ENABLED", request.param != "interp")
+    monkeypatch.setattr(fused_jit, "MFMA", request.param == "jit-mfma")
     monkeypatch.setattr(jit, "MODE", "sync")
     return request.param
 
@@ -118,7 +120,7 @@ def test_fused_kernels_used(gpu_device, scan_mode):
     before = dict(KERNEL_CALLS)
     e.query(QUERIES[0])
     e.query(QUERIES[4])
-    if scan_mode == "jit":
+    if scan_mode != "interp":
         aggs, mask = ("jit:igloo_jit_scan_agg", "jit:igloo_jit_scan_agg_mfma"), "jit:igloo_jit_scan_mask"
     else:
         aggs, mask = ("ff_aggregate",), "ff_mask"
