@@ -39,8 +39,6 @@ N GPUs:      python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
 from __future__ import annotations
 
 import argparse
-import decimal
-import hashlib
 import json
 import os
 import sys
@@ -63,29 +61,6 @@ def parse_queries(s: str):
     return out
 
 
-def digest(table) -> str:
-    """Order-independent digest of a query result: row count, exact sums of
-    integer / decimal columns, rounded float sums, hashed multiset of the
-    other values."""
-    import pyarrow as pa
-    import pyarrow.compute as pc
-    parts = [str(table.num_rows)]
-    for name in table.column_names:
-        col = table.column(name)
-        t = col.type
-        parts.append(f"{name}:{col.null_count}")
-        if pa.types.is_integer(t) or pa.types.is_decimal(t):
-            s = pc.sum(col).as_py() if table.num_rows else 0
-            parts.append(str(decimal.Decimal(s or 0).normalize()))
-        elif pa.types.is_floating(t):
-            s = pc.sum(col).as_py() if table.num_rows else 0.0
-            parts.append(f"{(s or 0.0):.9g}")
-        else:
-            vals = sorted(str(v) for v in col.to_pylist())
-            parts.append(hashlib.sha1("\x1f".join(vals).encode()).hexdigest()[:16])
-    return "|".join(parts)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,6 +80,7 @@ def main():
     import torch
     import igloo_amd as ig
     from igloo_amd.models.tpch import datagen, parquet_gen, queries
+    from igloo_amd.utils.digest import digest
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

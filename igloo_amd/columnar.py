@@ -30,7 +30,8 @@ class Column:
     ``valid`` is an optional bool tensor (True = not null).
     """
 
-    __slots__ = ("dtype", "data", "valid", "offsets", "dictionary", "_host_dict", "_sorted_dict", "_unified")
+    __slots__ = ("dtype", "data", "valid", "offsets", "dictionary", "_host_dict", "_sorted_dict", "_unified",
+                 "_cache")
 
     def __init__(self, dtype: DataType, data: torch.Tensor, valid: Optional[torch.Tensor] = None,
                  offsets: Optional[torch.Tensor] = None, dictionary: Optional["Column"] = None):
@@ -40,6 +41,7 @@ class Column:
         self.offsets = offsets
         self.dictionary = dictionary
         self._host_dict = None
+        self._cache = None
         self._sorted_dict = None
         self._unified = None      # content digest when used as a dictionary (parallel/exchange.py)
 
@@ -83,11 +85,21 @@ class Column:
 
     # ------------------------------------------------------------ host helpers
     def dict_values(self) -> List[Optional[str]]:
-        """Host copy of a dictionary column's values (cached; dictionaries are small)."""
+        """Host copy of a dictionary column's values, cached on the dictionary
+        itself: a resident table's dictionary is shared by every column built
+        from it, so repeated queries convert it once."""
         assert self.dictionary is not None
-        if self._host_dict is None:
-            self._host_dict = self.dictionary.to_arrow().to_pylist()
-        return self._host_dict
+        d = self.dictionary
+        if d._host_dict is None:
+            d._host_dict = d.to_arrow().to_pylist()
+        return d._host_dict
+
+    def derived(self) -> dict:
+        """Per-column cache of small structures derived from its values (used on
+        dictionaries: lookup tables per predicate, sort ranks, code maps)."""
+        if self._cache is None:
+            self._cache = {}
+        return self._cache
 
     def to(self, device) -> "Column":
         device = torch.device(device)

@@ -27,7 +27,10 @@ from .sql.binder import Binder, IdGen
 from .sql.logical import ColInfo, Plan
 from .sql.optimizer import optimize
 from .utils.errors import IglooError, NotSupported, PlanError
+from .exec import graphs as _graphs
+from .ops import jit as _jit
 from .utils import trace as _trace
+from .utils.digest import digest
 from .utils.log import get_logger
 
 #: cache optimized logical plans per SQL text (parse + bind + optimize cost
@@ -126,6 +129,8 @@ class QueryEngine:
         self.session: Dict[str, Any] = dict(config or {})
         # optimized logical plans by (SQL text, catalog version, session settings)
         self._plans: "collections.OrderedDict" = collections.OrderedDict()
+        self._graph_pool = None
+        self.graphs_disabled = False    # set after a capture the runtime refused (exec/graphs.py)
         self._spec: Dict[Any, dict] = {}   # replayable host readbacks per (plan, catalog, cache generation)
         self._ids = IdGen()
         self._lock = threading.RLock()
@@ -308,8 +313,10 @@ class QueryEngine:
         ctx = self.make_context()
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
         with _trace.Range("query"):
-            batch, spec = self._execute_speculative(plan, ctx, key)
+            batch, spec, st = self._execute_speculative(plan, ctx, key)
         table = self._to_arrow(batch, plan.schema, bq_names)
+        if st is not None:
+            table = self._check_graph(st, spec, table, plan, bq_names, ctx)
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
@@ -350,7 +357,7 @@ class QueryEngine:
         # until that is understood SPMD ranks read every value back
         if not (SPECULATE and key is not None and self.device.type == "cuda"
                 and (self.comm is None or self.comm.world_size == 1)):
-            return self._execute_plan(plan, ctx), None
+            return self._execute_plan(plan, ctx), None, None
         comm = None
 
         def agreed(ok: bool) -> bool:
@@ -365,8 +372,32 @@ class QueryEngine:
         if st is None:
             if len(self._spec) >= PLAN_CACHE_SIZE:
                 self._spec.pop(next(iter(self._spec)))
-            st = self._spec[skey] = {"log": None, "candidate": None, "fails": 0}
+            st = self._spec[skey] = {"log": None, "candidate": None, "fails": 0, "graph": None,
+                                     "capture_next": False, "digest": None, "graph_aborts": 0}
         replay = st["log"] is not None and st["fails"] < 2
+        if _graphs.GRAPHS and not self.graphs_disabled and replay and st["fails"] == 0 and st["graph_aborts"] < 2:
+            g = st["graph"]
+            if g is not None and not g.current():
+                # the generated-kernel set changed: the recording diverges from
+                # here, and a new graph is captured once a replay completes again
+                st["graph"] = g = None
+            if g is None and st["capture_next"] and st["digest"] is not None \
+                    and _jit.generation() is not None:
+                st["capture_next"] = False
+                with _trace.Range("graph.capture"):
+                    g = st["graph"] = _graphs.capture(self, plan, st["log"], self.make_context)
+                if g is None:
+                    st["graph_aborts"] += 1
+            if g is not None:
+                if g.replay(ctx):
+                    return g.batch, "graph", st
+                # a replayed value no longer matches the device: eager, real readbacks
+                st["graph"] = None
+                st["fails"] += 1
+                st["log"] = st["candidate"] = None
+                replay = False
+                ctx = self.make_context()
+                log.warning("query graph: replayed values did not match the device; re-executing")
         for attempt in range(3):
             sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
             _lib.set_speculation(sp)
@@ -390,10 +421,38 @@ class QueryEngine:
                 # the call sequence changed: this run's own sequence must be
                 # confirmed by the next execution before it is replayed
                 st["log"], st["candidate"] = None, sp.fresh
-            return batch, "replayed" if sp.complete else "partial"
+            elif _graphs.GRAPHS and st["fails"] == 0 and st["graph"] is None and st["graph_aborts"] < 2:
+                st["capture_next"] = True    # _check_graph keeps this result's digest
+            return batch, "replayed" if sp.complete else "partial", st
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
-        return batch, "recorded"
+        return batch, "recorded", st
+
+    def _check_graph(self, st: dict, spec, table: pa.Table, plan: Plan, names, ctx) -> pa.Table:
+        """Digest bookkeeping around query graphs (exec/graphs.py): the eager
+        result before a capture is digested; the graph's first result must
+        match it, otherwise the query is never captured again and this result
+        is recomputed eagerly."""
+        if spec == "replayed" and st["capture_next"]:
+            st["digest"] = digest(table)
+        elif spec == "graph":
+            g = st["graph"]
+            if not g.checked:
+                if digest(table) != st["digest"]:
+                    log.warning("query graph result differs from the eager execution; graph dropped")
+                    _graphs.STATS["failed"] += 1
+                    st["graph"] = None
+                    st["graph_aborts"] = 2
+                    ctx.__init__(self, self.device, self.comm, ctx.analyze)
+                    return self._to_arrow(self._execute_plan(plan, ctx), plan.schema, names)
+                g.checked = True
+        return table
+
+    def graph_pool(self):
+        """The private memory pool every query graph of this engine captures into."""
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        return self._graph_pool
 
     def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:
         ctx = ctx or self.make_context()

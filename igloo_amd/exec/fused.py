@@ -26,7 +26,7 @@ import torch
 
 from .. import types as T
 from ..columnar import Batch, Column
-from ..ops._lib import to_host_ints
+from ..ops._lib import check_not_capturing, to_host_ints
 from ..sql.expr import BinOp, Cast, ColRef, Expr, InList, Lit, conjuncts
 from ..types import DataType
 from ..utils.errors import ExecutionError
@@ -307,6 +307,7 @@ def narrow(x: torch.Tensor) -> torch.Tensor:
         return x
     hit = getattr(x, "_igloo_narrow", None)
     if hit is None:
+        check_not_capturing("narrow copy of a resident column")
         mn, mx = (int(v) for v in torch.aminmax(x))
         hit = x
         for t in _NARROW_TYPES:
@@ -329,14 +330,10 @@ def _disjuncts(e: Expr) -> List[Expr]:
 
 
 def _dict_code(col: Column, s: str) -> Optional[int]:
-    cache = getattr(col.dictionary, "_code_of", None)
+    dc = col.dictionary.derived()
+    cache = dc.get("code_of")
     if cache is None:
-        vals = col.dictionary.to_arrow().to_pylist()
-        cache = {v: i for i, v in enumerate(vals)}
-        try:
-            col.dictionary._code_of = cache
-        except AttributeError:
-            pass
+        cache = dc["code_of"] = {v: i for i, v in enumerate(col.dict_values())}
     return cache.get(s)
 
 
@@ -546,7 +543,8 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
     from ..ops.agg import _wide_to_result
     res = [(_wide_to_result(d, d2) if d2 is not None else d) for d, d2 in bufs]
     if groups:
-        keep = torch.nonzero(counts > 0).flatten()
+        from ..ops.select import mask_to_indices
+        keep = mask_to_indices(counts > 0)     # replayable size readback (no hidden nonzero sync)
         ng = keep.numel()
     else:
         keep, ng = None, 1

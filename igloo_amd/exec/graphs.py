@@ -1,0 +1,172 @@
+"""Query graphs: a repeated query over unchanged data runs as one HIP graph.
+
+Once a query's host readbacks replay completely from a trusted recording
+(engine.py ``_execute_speculative``, ops/_lib.py ``Speculation``), its host
+control flow no longer depends on the device: every kernel, memset and copy it
+enqueues is fixed by the plan and the data. The next execution then runs the
+operators once more under stream capture instead of eagerly. The HIP graph it
+records is the whole query (scans, joins, aggregation, sort, and the device-side
+check of every replayed value), and every later execution is one
+``hipGraphLaunch`` plus one stream sync. That removes the Python operator
+dispatch (2-6 ms per query at SF100, ``profiles/r2_roctx_per_query_idle_sf100.txt``)
+and the per-launch overhead from the critical path.
+
+Every replay still runs every kernel over the resident columns. Nothing is cached
+but the launch sequence. What keeps a graph valid:
+
+* the key. Graphs live in the speculation state, which is keyed on the SQL text,
+  the catalog version and the cache generation (a table change, eviction or
+  refill drops them), and each graph also records the generated-kernel set it
+  was captured with (ops/jit.py ``generation``). A kernel that finishes
+  compiling makes the next execution re-capture.
+* the device check. The replayed sizes and ranges are compared with the device
+  values inside the graph (one int64 mismatch count read after each replay). On
+  a mismatch the graph is dropped and the query re-executes eagerly with real
+  readbacks.
+* the first replay. Right after capture, the graph's result digest
+  (utils/digest.py) must equal the previous eager execution's. Otherwise the
+  query is marked never to be captured again.
+* capture refusal. Anything a graph cannot replay raises
+  ``CaptureAbort`` before any HIP call (ops/_lib.py): a real readback, a
+  one-time derived-structure build, a generated-kernel load, a host spill. The
+  query then stays eager.
+
+Memory: all graphs of an engine share one private pool (``torch.cuda.graph_pool_handle``).
+Graphs replay one at a time on one stream, and each writes its intermediates before
+reading them, so a later capture may reuse blocks an earlier one freed. The pool holds
+about the largest query's working set plus every graph's result columns.
+
+The reference has no GPU execution and so nothing comparable; its engine
+rebuilds DataFusion physical plans per query (reference
+crates/engine/src/lib.rs:112-140). This is the HIP-graph half of SURVEY §5.7's
+"HIP streams and graphs instead of a tracing compiler".
+"""
+from __future__ import annotations
+
+import logging
+import os
+import traceback
+from typing import Optional
+
+import torch
+
+from ..ops import _lib
+from ..ops import jit as _jit
+
+log = logging.getLogger("igloo.graphs")
+
+GRAPHS = os.environ.get("IGLOO_GRAPHS", "1") == "1"
+
+_streams: dict = {}
+STATS = {"captured": 0, "replays": 0, "aborted": 0, "failed": 0, "mismatch": 0}
+LAST_ERROR: list = []    # why the last captures did not produce a graph (debugging, tests)
+
+
+def _note(msg: str) -> None:
+    LAST_ERROR.append(msg)
+    del LAST_ERROR[:-8]
+
+
+def _capture_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _streams.get(dev.index)
+    if s is None:
+        s = _streams[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+class QueryGraph:
+    """One captured query: the graph, its static result batch and the device
+    mismatch counter of its replayed values."""
+
+    __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays")
+
+    def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill):
+        self.graph = graph
+        self.batch = batch
+        self.bad = bad
+        self.expected = expected       # kept alive: read by the graph's compare kernel
+        self.jit_gen = jit_gen
+        self.rows_scanned = rows_scanned
+        self.spill = spill
+        self.checked = False           # first replay compared with the eager result
+        self.replays = 0
+
+    def current(self) -> bool:
+        """Still built from the generated kernels that are loaded now."""
+        return self.jit_gen == _jit.generation()
+
+    def replay(self, ctx) -> bool:
+        """Launch the graph on the current stream; True when every replayed
+        value matched the device (one sync)."""
+        self.graph.replay()
+        self.replays += 1
+        STATS["replays"] += 1
+        ctx.rows_scanned = self.rows_scanned
+        ctx.spill = dict(self.spill)
+        ok = int(self.bad.item()) == 0
+        if not ok:
+            STATS["mismatch"] += 1
+        return ok
+
+
+def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
+    """Capture ``plan`` executed under a replay of the recording ``log_``.
+    Returns None (query stays eager) when the capture is refused or fails."""
+    dev = engine.device
+    gen = _jit.generation()
+    if gen is None:
+        return None
+    sp = _lib.Speculation("replay", log_)
+    exp = sp.expected_values()
+    expected = torch.tensor(exp or [0], dtype=torch.int64).to(dev)[:len(exp)]
+    ctx = make_ctx()
+    cur = torch.cuda.current_stream(dev)
+    s = _capture_stream(dev)
+    s.wait_stream(cur)
+    g = torch.cuda.CUDAGraph()
+    batch = bad = None
+    _lib.set_speculation(sp)
+    _lib.set_capturing(True)
+    # torch raises before any synchronizing call (blocking copy, .item(),
+    # nonzero) reaches HIP: such a site ends the capture cleanly instead of
+    # invalidating it inside the runtime
+    sync_mode = torch.cuda.get_sync_debug_mode()
+    torch.cuda.set_sync_debug_mode(2)
+    try:
+        with torch.cuda.stream(s):
+            g.capture_begin(pool=engine.graph_pool(), capture_error_mode="thread_local")
+            try:
+                batch = engine._execute_plan(plan, ctx)
+                if not sp.complete:
+                    raise _lib.CaptureAbort("call sequence left the recording")
+                bad = sp.device_mismatches(expected)
+            finally:
+                g.capture_end()
+    except _lib.CaptureAbort as e:
+        engine._graph_pool = None
+        STATS["aborted"] += 1
+        _note(f"aborted: {e}")
+        log.debug("query graph not captured: %s", e)
+        return None
+    except RuntimeError as e:
+        engine._graph_pool = None
+        if "synchronizing" in str(e):      # raised by torch before the call: a clean abort
+            STATS["aborted"] += 1
+            _note("aborted (sync): " + traceback.format_exc(limit=-4))
+            return None
+        # a HIP call the capture refused: the runtime invalidated the capture.
+        # This engine stops capturing (a failed capture's allocator state is
+        # not something to build on); the query stays eager.
+        engine.graphs_disabled = True
+        STATS["failed"] += 1
+        _note("failed: " + traceback.format_exc(limit=-5))
+        log.warning("query graph capture failed, graphs disabled for this engine: %s", e)
+        torch.cuda.synchronize(dev)
+        return None
+    finally:
+        torch.cuda.set_sync_debug_mode(sync_mode)
+        _lib.set_capturing(False)
+        _lib.set_speculation(None)
+        cur.wait_stream(s)
+    STATS["captured"] += 1
+    return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill)

@@ -34,7 +34,7 @@ from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
-from ..ops._lib import launch, ptr, stream, to_host_int, to_host_ints, unlogged
+from ..ops._lib import check_not_capturing, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
 from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
 from ..ops.select import exclusive_scan, mask_to_indices
@@ -109,8 +109,12 @@ class ExecContext:
                 self._subq[key] = None
             else:
                 col = b.columns[e.plan.schema[0].cid]
-                v = col.to_arrow()[0].as_py()
                 t = e.plan.schema[0].dtype
+                dv = _device_scalar(col, t)
+                if dv is not _NO_SCALAR:
+                    self._subq[key] = dv
+                    return dv
+                v = col.to_arrow()[0].as_py()
                 if t.is_decimal and v is not None:
                     from decimal import Decimal
                     v = int(Decimal(v).scaleb(t.scale))
@@ -119,6 +123,30 @@ class ExecContext:
                     v = (v - datetime.date(1970, 1, 1)).days
                 self._subq[key] = v
         return self._subq[key]
+
+
+_NO_SCALAR = object()
+
+
+def _device_scalar(col: Column, t):
+    """First value of a device column through the replayable readback path
+    (ops/_lib.py to_host_ints): integers, dates (days) and decimals (scaled
+    integers) as int, floats bit-exact, NULL as None. Other types return
+    ``_NO_SCALAR`` (host conversion)."""
+    d = col.data
+    if not d.is_cuda or col.offsets is not None or col.dictionary is not None or t.kind in ("null", "timestamp") \
+            or t.is_string:
+        return _NO_SCALAR
+    if col.valid is not None and not to_host_int(col.valid[:1]):
+        return None
+    if d.dim() == 2:
+        lo, hi = to_host_ints(d[:1].reshape(-1))
+        return (hi << 64) | (lo & 0xFFFFFFFFFFFFFFFF)
+    if d.dtype.is_floating_point:
+        return to_host_f64s(d[:1])[0]
+    if d.dtype == torch.bool:
+        return bool(to_host_int(d[:1]))
+    return to_host_int(d[:1])
 
 
 class _Span:
@@ -593,6 +621,7 @@ JOIN_MEM_FACTOR = 3
 
 def _to_host(b: Batch) -> Batch:
     """Spill a batch to (pinned) host memory."""
+    check_not_capturing("spill to host memory")
     out = {}
     for k, c in b.columns.items():
         def mv(t):

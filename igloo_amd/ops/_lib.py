@@ -94,6 +94,31 @@ def _distributed() -> bool:
     return d.is_available() and d.is_initialized()
 
 
+class CaptureAbort(RuntimeError):
+    """Raised while a query is being captured into a HIP graph
+    (exec/graphs.py) at anything a graph cannot replay: a real host readback,
+    a one-time build of a derived structure, a generated-kernel load, a spill
+    to host memory. Raised before any HIP call, so the capture ends cleanly
+    and the query runs eagerly."""
+
+
+_capture = threading.local()
+
+
+def capturing() -> bool:
+    """This thread is capturing a query graph."""
+    return getattr(_capture, "on", False)
+
+
+def set_capturing(on: bool) -> None:
+    _capture.on = on
+
+
+def check_not_capturing(what: str) -> None:
+    if getattr(_capture, "on", False):
+        raise CaptureAbort(what)
+
+
 class Speculation:
     """Host readbacks of one query execution, recorded or replayed.
 
@@ -128,6 +153,25 @@ class Speculation:
     def complete(self) -> bool:
         """The replay followed the recorded call sequence to its end."""
         return not self.diverged and self.pos == len(self.log)
+
+    def expected_values(self) -> list:
+        """Every non-volatile value of the recorded log, in call order: what a
+        complete replay hands out (and what the device must confirm)."""
+        out = []
+        for _site, vals in self.log:
+            if vals is not None:
+                out.extend(vals)
+        return out
+
+    def device_mismatches(self, expected_dev: torch.Tensor) -> torch.Tensor:
+        """Device int64 scalar: how many replayed values differ from the device
+        (stream-ordered, no sync; used inside a graph capture)."""
+        if not self.actual:
+            return torch.zeros((), dtype=torch.int64, device=expected_dev.device)
+        act = torch.cat(self.actual)
+        if act.numel() != expected_dev.numel():
+            raise CaptureAbort("replayed value count differs from the recording")
+        return (act != expected_dev).sum()
 
     def validate(self) -> bool:
         """True when every replayed value equals the device value (one sync).
@@ -174,6 +218,7 @@ class unlogged:
     __slots__ = ("prev",)
 
     def __enter__(self):
+        check_not_capturing("one-time build of a derived structure")
         self.prev = getattr(_spec, "cur", None)
         _spec.cur = None
         return self
@@ -222,6 +267,8 @@ def _to_host_ints(t: torch.Tensor) -> list:
     (a blocking D2H copy + stream synchronize: ~66 us per call on MI355X vs
     ~18 us polled; a query issues ~25 data-dependent sizes). Values are exact:
     the poll ends on a changed sentinel or an idle stream, whichever first."""
+    if t.is_cuda:
+        check_not_capturing("host readback")
     # single-process only: a 2-rank run sharing one GPU hung in its first query
     # with polled readbacks (cause not isolated), so SPMD ranks keep .tolist()
     if not t.is_cuda or not FAST_READBACK or _distributed():

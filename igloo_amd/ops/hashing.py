@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import is_gpu, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
+from ._lib import check_not_capturing, is_gpu, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
 from .select import exclusive_scan, mask_to_indices
 
 EMPTY_KEY = -(2**63)
@@ -505,6 +505,8 @@ def hll_sketch(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Opti
         hit = getattr(src, "_igloo_hll", None)
         if hit is not None:   # resident table columns are sketched once (like is_sorted)
             return hit
+    if valid is None and getattr(src, "_igloo_resident", False):
+        check_not_capturing("sketch of a resident column")   # kept on the column: a one-time build
     keys = _keys_ok(keys)
     n = keys.numel()
     if not is_gpu(keys):

@@ -28,7 +28,7 @@ import threading
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence
 
-from ._lib import KERNEL_CALLS, native
+from ._lib import KERNEL_CALLS, check_not_capturing, native
 
 MODE = os.environ.get("IGLOO_JIT", "async").lower()
 ARCH = "gfx950"
@@ -86,6 +86,7 @@ def _compile(src: str, name: str, key: str) -> bytes:
 
 
 def _load(code: bytes, name: str, key: str) -> JitKernel:
+    check_not_capturing("generated-kernel load")   # module loads are not graph operations
     k = JitKernel(name, native().jit_load(code, name), key)
     _kernels[key] = k
     return k
@@ -171,3 +172,14 @@ def wait_all(timeout: Optional[float] = None) -> None:
 
 def failures() -> List[str]:
     return list(_failed.values())
+
+
+def generation() -> Optional[int]:
+    """Identifies the set of generated kernels a query can use: the number
+    loaded plus the number failed, or None while compiles are in flight (the
+    set is about to change). A query graph (exec/graphs.py) captured under
+    one generation is re-captured under the next."""
+    with _lock:
+        if _pending:
+            return None
+        return len(_kernels) + len(_failed)

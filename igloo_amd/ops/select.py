@@ -51,5 +51,5 @@ def offsets_from_lengths(lengths: torch.Tensor) -> Tuple[torch.Tensor, int]:
     ex, total = exclusive_scan(lengths)
     off = torch.empty(lengths.numel() + 1, dtype=torch.int64, device=lengths.device)
     off[:-1] = ex
-    off[-1] = total
+    off[-1:].fill_(total)     # a device fill (item assignment would upload a host scalar)
     return off, total

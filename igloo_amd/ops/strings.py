@@ -18,7 +18,7 @@ import torch
 from .. import types as T
 from ..columnar import Column
 from .gather import gather_tensor
-from ._lib import is_gpu, launch, ptr, stream, to_host_int
+from ._lib import check_not_capturing, is_gpu, launch, ptr, stream, to_host_int
 from .gather import take
 from .hashing import group_ids
 from .select import offsets_from_lengths
@@ -94,12 +94,36 @@ def like_regex(pattern: str, ci: bool = False, escape: Optional[str] = "\\") -> 
     return re.compile("".join(parts), re.DOTALL | (re.IGNORECASE if ci else 0))
 
 
-def _lut_apply(col: Column, lut_vals: Sequence) -> torch.Tensor:
-    """Map dictionary codes through a per-dictionary-entry lookup table."""
-    lut = torch.tensor(list(lut_vals), device=col.device)
+def _lut_apply(col: Column, lut_vals, key=None) -> torch.Tensor:
+    """Map dictionary codes through a per-dictionary-entry lookup table.
+    ``lut_vals``: the table, or (with ``key``) a callable building it; keyed
+    tables are kept on the dictionary, so a repeated predicate reuses its
+    device table instead of rebuilding and uploading it every query."""
+    cache = col.dictionary.derived() if key is not None else None
+    lut = cache.get(key) if cache is not None else None
+    if lut is None:
+        check_not_capturing("dictionary lookup-table upload")
+        lut = torch.tensor(list(lut_vals() if callable(lut_vals) else lut_vals), device=col.device)
+        if cache is not None:
+            cache[key] = lut
     if lut.numel() == 0:
         return torch.zeros(len(col), dtype=lut.dtype, device=col.device)
     return gather_tensor(lut, col.data)
+
+
+_CONSTS: dict = {}
+
+
+def _consts(key, build):
+    """Device copies of small per-pattern constants (LIKE segments, comparison
+    bytes), uploaded once per pattern and device."""
+    v = _CONSTS.get(key)
+    if v is None:
+        check_not_capturing("pattern constant upload")
+        if len(_CONSTS) > 4096:
+            _CONSTS.clear()
+        v = _CONSTS[key] = build()
+    return v
 
 
 def _with_valid(values: torch.Tensor, col: Column) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -110,9 +134,10 @@ def _with_valid(values: torch.Tensor, col: Column) -> Tuple[torch.Tensor, Option
 def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, escape: Optional[str] = "\\") -> torch.Tensor:
     """Bool tensor (NULL rows are False; callers combine ``col.valid``)."""
     if col.is_dict:
-        rx = like_regex(pattern, ci, escape)
-        lut = [(v is not None and rx.fullmatch(v) is not None) != negate for v in col.dict_values()]
-        return _lut_apply(col, lut).to(torch.bool)
+        def build():
+            rx = like_regex(pattern, ci, escape)
+            return [(v is not None and rx.fullmatch(v) is not None) != negate for v in col.dict_values()]
+        return _lut_apply(col, build, ("like", pattern, ci, negate, escape)).to(torch.bool)
     n = len(col)
     if not is_gpu(col.data):
         arr = col.to_arrow()
@@ -125,14 +150,16 @@ def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, esca
     segs = None if ci else _like_segments(pat, kinds)
     if segs is not None:
         seg_bytes, seg_off, a0, a1 = segs
-        sb = torch.tensor(list(seg_bytes) or [0], dtype=torch.uint8).to(dev)
-        so = torch.tensor(seg_off, dtype=torch.int32).to(dev)
+        sb, so = _consts(("seg", pattern, escape, dev), lambda: (
+            torch.tensor(list(seg_bytes) or [0], dtype=torch.uint8).to(dev),
+            torch.tensor(seg_off, dtype=torch.int32).to(dev)))
         out = torch.empty(n, dtype=torch.bool, device=dev)
         launch("str_like_segments").str_like_segments(ptr(col.offsets), ptr(col.data), n, ptr(sb), ptr(so),
                                                       len(seg_off) - 1, a0, a1, negate, ptr(out), stream(out))
         return out
-    pt = torch.tensor(list(pat) or [0], dtype=torch.uint8).to(dev)
-    kt = torch.tensor(list(kinds) or [0], dtype=torch.uint8).to(dev)
+    pt, kt = _consts(("pat", pattern, escape, dev), lambda: (
+        torch.tensor(list(pat) or [0], dtype=torch.uint8).to(dev),
+        torch.tensor(list(kinds) or [0], dtype=torch.uint8).to(dev)))
     out = torch.empty(n, dtype=torch.bool, device=dev)
     launch("str_like").str_like(ptr(col.offsets), ptr(col.data), n, ptr(pt), ptr(kt), len(pat), ci, negate, ptr(out),
                                 stream(out))
@@ -145,8 +172,8 @@ def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
         import operator as o
         f = {"=": o.eq, "<>": o.ne, "<": o.lt, "<=": o.le, ">": o.gt, ">=": o.ge}[op]
         vb = value.encode("utf-8")
-        lut = [(v is not None and f(v.encode("utf-8"), vb)) for v in col.dict_values()]
-        return _lut_apply(col, lut).to(torch.bool)
+        return _lut_apply(col, lambda: [(v is not None and f(v.encode("utf-8"), vb)) for v in col.dict_values()],
+                          ("cmp", op, value)).to(torch.bool)
     n = len(col)
     if not is_gpu(col.data):
         arr = col.to_arrow()
@@ -155,7 +182,7 @@ def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
         r = fn(arr, pa.scalar(value, pa.large_string()))
         return torch.from_numpy(r.fill_null(False).to_numpy(zero_copy_only=False).astype(np.bool_))
     vb = value.encode("utf-8")
-    ct = torch.tensor(list(vb) or [0], dtype=torch.uint8).to(col.device)
+    ct = _consts(("bytes", value, col.device), lambda: torch.tensor(list(vb) or [0], dtype=torch.uint8).to(col.device))
     out = torch.empty(n, dtype=torch.bool, device=col.device)
     launch("str_cmp_const").str_cmp_const(ptr(col.offsets), ptr(col.data), n, ptr(ct), len(vb), CMP_OPS[op], ptr(out),
                                           stream(out))
@@ -165,7 +192,7 @@ def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
 def in_list(col: Column, values: Sequence[str]) -> torch.Tensor:
     if col.is_dict:
         s = set(values)
-        return _lut_apply(col, [v in s for v in col.dict_values()]).to(torch.bool)
+        return _lut_apply(col, lambda: [v in s for v in col.dict_values()], ("in", tuple(values))).to(torch.bool)
     out = None
     for v in values:
         m = compare_const(col, "=", v)
@@ -252,7 +279,8 @@ def substr(col: Column, start: int, length: Optional[int]) -> Column:
 
 def char_length(col: Column) -> torch.Tensor:
     if col.is_dict:
-        return _lut_apply(col, [0 if v is None else len(v) for v in col.dict_values()]).to(torch.int32)
+        return _lut_apply(col, lambda: [0 if v is None else len(v) for v in col.dict_values()],
+                          ("char_length",)).to(torch.int32)
     arr = col.to_arrow()
     r = pc.utf8_length(arr).fill_null(0).to_numpy(zero_copy_only=False)
     return torch.from_numpy(r.astype(np.int32)).to(col.device)
@@ -316,14 +344,18 @@ def dict_encode(col: Column) -> Column:
 def sort_ranks(col: Column) -> torch.Tensor:
     """Order-preserving int64 rank per row (byte-wise UTF-8 order)."""
     c = dict_encode(col) if not col.is_dict else col
-    d = c.dictionary.to_arrow()
-    if len(d) == 0:
-        return torch.zeros(len(c), dtype=torch.int64, device=c.device)
-    # Arrow orders strings byte-wise (UTF-8 code point order), NULL entries last
-    order = pc.array_sort_indices(d, null_placement="at_end").to_numpy()
-    rank = np.empty(len(order), dtype=np.int64)
-    rank[order] = np.arange(len(order), dtype=np.int64)
-    lut = torch.from_numpy(rank).to(c.device)
+    cache = c.dictionary.derived()
+    lut = cache.get("rank")
+    if lut is None:
+        check_not_capturing("dictionary rank upload")
+        d = c.dictionary.to_arrow()
+        if len(d) == 0:
+            return torch.zeros(len(c), dtype=torch.int64, device=c.device)
+        # Arrow orders strings byte-wise (UTF-8 code point order), NULL entries last
+        order = pc.array_sort_indices(d, null_placement="at_end").to_numpy()
+        rank = np.empty(len(order), dtype=np.int64)
+        rank[order] = np.arange(len(order), dtype=np.int64)
+        lut = cache["rank"] = torch.from_numpy(rank).to(c.device)
     return gather_tensor(lut, c.data)
 
 

@@ -20,7 +20,7 @@ def main():
     a = ap.parse_args()
     import torch
     import igloo_amd as ig
-    from bench import digest
+    from igloo_amd.utils.digest import digest
     from igloo_amd.catalog import MemoryTable
     from igloo_amd.models.tpch import datagen, queries
     cpu = ig.QueryEngine(device="cpu")

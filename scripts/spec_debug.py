@@ -2,7 +2,7 @@
 import sys; sys.path.insert(0, '.')
 import igloo_amd as ig
 from igloo_amd.models.tpch import datagen, queries
-from bench import digest
+from igloo_amd.utils.digest import digest
 e = ig.QueryEngine(device="cuda:0"); datagen.register(e, 1.0)
 for q in range(1, 23):
     modes = []; ds = set()

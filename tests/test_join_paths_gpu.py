@@ -65,3 +65,42 @@ def test_join_paths_match_cpu(gpu_device, monkeypatch, sorted_big, perm, qi):
         e.register_table("small", small)
         res[dev] = _norm(e.query(QUERIES[qi]))
     assert res["cpu"] == res[gpu_device]
+
+
+def _phases(e, sql):
+    txt = e.sql("EXPLAIN ANALYZE " + sql).table.column("plan").to_pylist()[0]
+    return txt[txt.find("phases"):]
+
+
+@pytest.mark.parametrize("skewed", [False, True])
+def test_perm_index_default_gating(gpu_device, skewed):
+    """Default thresholds (no monkeypatching): an unsorted resident 4.2M-row
+    key column joined with 1000 keys goes through its secondary index when the
+    matching ranges are small, and falls back to the hash join after the index
+    search when a hot key makes the result too large. The chosen
+    path is read from EXPLAIN ANALYZE's phase spans; answers match the CPU."""
+    n = (1 << 22) + 100_000
+    r = np.random.default_rng(11)
+    k = r.permutation(n).astype(np.int64)
+    if skewed:
+        k[: n // 2] = 0                  # one hot key: half the column
+        r.shuffle(k)
+    big = pa.table({"bk": pa.array(k), "bv": pa.array(r.integers(0, 1000, n), pa.int64())})
+    sk = r.choice(n, 1000, replace=False).astype(np.int64)
+    sk[0] = 0
+    small = pa.table({"sk": pa.array(sk)})
+    sql = "SELECT count(*) AS c, sum(bv) AS s FROM small JOIN big ON sk = bk"
+    res = {}
+    for dev in ("cpu", gpu_device):
+        e = ig.QueryEngine(device=dev)
+        e.register_table("big", big)
+        e.register_table("small", small)
+        res[dev] = e.query(sql).to_pylist()
+        if dev != "cpu":
+            ph = _phases(e, sql)
+            assert "join.index_search" in ph, ph
+            if skewed:
+                assert "join.index_expand" not in ph and "join.probe" in ph, ph
+            else:
+                assert "join.index_expand" in ph and "join.probe" not in ph, ph
+    assert res["cpu"] == res[gpu_device]

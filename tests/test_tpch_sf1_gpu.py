@@ -44,7 +44,7 @@ def engines(tmp_path_factory):
 
 @pytest.mark.parametrize("q", range(1, 23))
 def test_sf1_gpu_equals_cpu(engines, q):
-    from bench import digest
+    from igloo_amd.utils.digest import digest
     from igloo_amd.models.tpch import queries
     from igloo_amd.ops import _lib
     gpu, cpu, pq = engines
