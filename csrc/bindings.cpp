@@ -242,8 +242,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("select_count", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t total, uintptr_t s) {
     kern::select_count(P<const uint8_t>(mask), n, P<int64_t>(tiles), P<int64_t>(total), S(s));
   });
-  m.def("select_write", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t out, bool idx64, uintptr_t s) {
-    kern::select_write(P<const uint8_t>(mask), n, P<const int64_t>(tiles), P<void>(out), idx64, S(s));
+  m.def("select_write", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t out, bool idx64, int64_t cap,
+                           uintptr_t s) {
+    kern::select_write(P<const uint8_t>(mask), n, P<const int64_t>(tiles), P<void>(out), idx64, cap, S(s));
   });
   m.def("scan_workspace_tiles", &kern::scan_workspace_tiles);
   m.def("exclusive_scan", [](uintptr_t in, bool in64, int64_t n, uintptr_t out, uintptr_t ws, uintptr_t total, uintptr_t s) {
@@ -378,8 +379,8 @@ PYBIND11_MODULE(_native, m) {
                             int64_t kmin, bool direct, uintptr_t s) {
     kern::groupby_build(P<const void>(keys), key64, n, P<int64_t>(tkeys), P<int32_t>(trow), cap, kmin, direct, S(s));
   });
-  m.def("groupby_occupied", [](uintptr_t trow, int64_t cap, uintptr_t occ, uintptr_t s) {
-    kern::groupby_occupied(P<const int32_t>(trow), cap, P<uint8_t>(occ), S(s));
+  m.def("groupby_occupied", [](uintptr_t trow, int64_t cap, uintptr_t occ, uintptr_t gid_of_slot, uintptr_t s) {
+    kern::groupby_occupied(P<const int32_t>(trow), cap, P<uint8_t>(occ), P<int32_t>(gid_of_slot), S(s));
   });
   m.def("groupby_assign", [](uintptr_t slots, bool slots64, int64_t g, uintptr_t trow, uintptr_t gid_of_slot,
                              uintptr_t rep_row, uintptr_t s) {
@@ -441,6 +442,9 @@ PYBIND11_MODULE(_native, m) {
                               uintptr_t new_off, uintptr_t out, uintptr_t s) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
+  });
+  m.def("str_prefix_keys", [](uintptr_t off, uintptr_t chars, int64_t n, int chunks, uintptr_t out, uintptr_t s) {
+    kern::str_prefix_keys(P<const int64_t>(off), P<const uint8_t>(chars), n, chunks, P<int64_t>(out), S(s));
   });
   m.def("str_hash64", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t valid, uintptr_t out, uintptr_t s) {
     kern::str_hash64(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(valid), P<int64_t>(out), S(s));

@@ -74,6 +74,9 @@ __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict_
     int64_t slot;
     if (DIRECT) {
       slot = k - kmin;
+      // a key outside the span only occurs under a replayed key range that the
+      // end-of-query check will reject (ops/_lib.py Speculation): stay in bounds
+      if ((uint64_t)slot >= (uint64_t)cap) continue;
     } else {
       bool existed;
       slot = insert_slot(tkeys, mask, k, &existed);
@@ -207,6 +210,9 @@ __global__ __launch_bounds__(kBlock) void groupby_build_kernel(const K* __restri
     int64_t slot;
     if (DIRECT) {
       slot = k - kmin;
+      // a key outside the span only occurs under a replayed key range that the
+      // end-of-query check will reject (ops/_lib.py Speculation): stay in bounds
+      if ((uint64_t)slot >= (uint64_t)cap) continue;
     } else {
       bool existed;
       slot = insert_slot(tkeys, mask, k, &existed);
@@ -232,6 +238,7 @@ __global__ __launch_bounds__(kBlock) void groupby_build_lds_kernel(const K* __re
   __syncthreads();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t slot = (int64_t)keys[i] - kmin;
+    if ((uint64_t)slot >= (uint64_t)cap) continue;   // see groupby_build_kernel
     if (srow[slot] > (int32_t)i) atomicMin(&srow[slot], (int32_t)i);
   }
   __syncthreads();
@@ -241,10 +248,14 @@ __global__ __launch_bounds__(kBlock) void groupby_build_lds_kernel(const K* __re
   }
 }
 
+// also zeroes gid_of_slot: a slot the (replayed) group count leaves unassigned
+// then maps to group 0 instead of an uninitialised id (see groupby_build_kernel)
 __global__ __launch_bounds__(kBlock) void occupied_kernel(const int32_t* __restrict__ trow, int64_t cap,
-                                                         uint8_t* __restrict__ occ) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
+                                                         uint8_t* __restrict__ occ, int32_t* __restrict__ gid_of_slot) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
     occ[i] = trow[i] != INT32_MAX;
+    gid_of_slot[i] = 0;
+  }
 }
 
 // gid_of_slot[slots[g]] = g ; rep_row[g] = trow[slots[g]]
@@ -269,6 +280,7 @@ __global__ __launch_bounds__(kBlock) void groupby_lookup_kernel(const K* __restr
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t k = (int64_t)keys[i];
     int64_t slot = DIRECT ? k - kmin : find_slot(tkeys, mask, k);
+    if (DIRECT && (uint64_t)slot >= (uint64_t)cap) slot = 0;   // see groupby_build_kernel
     gid[i] = gid_of_slot[slot];
   }
 }
@@ -384,8 +396,8 @@ void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int3
   check_launch("groupby_build", stream);
 }
 
-void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, hipStream_t stream) {
-  hipLaunchKernelGGL(occupied_kernel, dim3(grid_for(cap, kBlock, kMaxGrid)), dim3(kBlock), 0, stream, trow, cap, occ);
+void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, int32_t* gid_of_slot, hipStream_t stream) {
+  hipLaunchKernelGGL(occupied_kernel, dim3(grid_for(cap, kBlock, kMaxGrid)), dim3(kBlock), 0, stream, trow, cap, occ, gid_of_slot);
   check_launch("groupby_occupied", stream);
 }
 

@@ -18,7 +18,7 @@ constexpr int kMaxParts = 64;
 // ---- select.hip / scan.hip ---------------------------------------------------
 int64_t select_num_tiles(int64_t n);
 void select_count(const uint8_t* mask, int64_t n, int64_t* tile_counts, int64_t* total, hipStream_t stream);
-void select_write(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, void* out, bool idx64,
+void select_write(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, void* out, bool idx64, int64_t cap,
                   hipStream_t stream);
 void scan_counts(int64_t* counts, int64_t n, int64_t* total, hipStream_t stream);
 int64_t scan_workspace_tiles(int64_t n);
@@ -154,7 +154,7 @@ void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, 
 void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int32_t* gid, hipStream_t stream);
 void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,
                    bool direct, hipStream_t stream);
-void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, hipStream_t stream);
+void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, int32_t* gid_of_slot, hipStream_t stream);
 void groupby_assign(const void* slots, bool slots64, int64_t g, const int32_t* trow, int32_t* gid_of_slot,
                     int32_t* rep_row, hipStream_t stream);
 void groupby_lookup(const void* keys, bool key64, int64_t n, const int64_t* tkeys, const int32_t* gid_of_slot,
@@ -220,6 +220,8 @@ void str_substr_copy(const int64_t* off, const uint8_t* chars, int64_t n, int64_
 // with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%'
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
                        int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, hipStream_t stream);
+void str_prefix_keys(const int64_t* off, const uint8_t* chars, int64_t n, int chunks, int64_t* out,
+                     hipStream_t stream);
 void str_hash64(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* valid, int64_t* out,
                 hipStream_t stream);
 void str_eq_rows(const int64_t* aoff, const uint8_t* achars, const void* ai, const int64_t* boff, const uint8_t* bchars,

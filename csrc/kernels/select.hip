@@ -107,7 +107,7 @@ namespace {
 template <typename IdxT>
 __global__ __launch_bounds__(kBlock) void tile_write_kernel(const uint8_t* __restrict__ mask, int64_t n,
                                                            const int64_t* __restrict__ offsets,
-                                                           IdxT* __restrict__ out) {
+                                                           IdxT* __restrict__ out, int64_t cap) {
   __shared__ int64_t scratch[kWavesPerBlock + 1];
   __shared__ uint16_t stage[kTile];  // row offsets inside the tile, in output order
   const int64_t tile_base = (int64_t)blockIdx.x * kTile;
@@ -125,8 +125,15 @@ __global__ __launch_bounds__(kBlock) void tile_write_kernel(const uint8_t* __res
     for (int b = 0; b < 4; ++b)
       if ((w[q] >> (8 * b)) & 1u) stage[pos++] = (uint16_t)(first + 4 * q + b);
   __syncthreads();
-  IdxT* dst = out + offsets[blockIdx.x];
-  for (int k = threadIdx.x; k < (int)total; k += kBlock) dst[k] = (IdxT)(tile_base + stage[k]);
+  // writes stay inside the caller's buffer of ``cap`` entries, and the last
+  // tile zero-fills [total, cap): a size the host replayed instead of reading
+  // (ops/_lib.py Speculation) can then never make this kernel or a consumer of
+  // the indices touch memory out of bounds before the replay is validated
+  const int64_t o = offsets[blockIdx.x];
+  for (int k = threadIdx.x; k < (int)total; k += kBlock)
+    if (o + k < cap) out[o + k] = (IdxT)(tile_base + stage[k]);
+  if (blockIdx.x == gridDim.x - 1)
+    for (int64_t p = offsets[gridDim.x] + threadIdx.x; p < cap; p += kBlock) out[p] = (IdxT)0;
 }
 
 }  // namespace
@@ -147,16 +154,16 @@ void select_count(const uint8_t* mask, int64_t n, int64_t* tile_counts, int64_t*
   check_launch("select.scan", stream);
 }
 
-void select_write(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, void* out, bool idx64,
+void select_write(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, void* out, bool idx64, int64_t cap,
                   hipStream_t stream) {
   int64_t tiles = select_num_tiles(n);
   if (tiles == 0) return;
   if (idx64)
     hipLaunchKernelGGL(tile_write_kernel<int64_t>, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
-                       mask, n, tile_offsets, (int64_t*)out);
+                       mask, n, tile_offsets, (int64_t*)out, cap);
   else
     hipLaunchKernelGGL(tile_write_kernel<int32_t>, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
-                       mask, n, tile_offsets, (int32_t*)out);
+                       mask, n, tile_offsets, (int32_t*)out, cap);
   check_launch("select.tile_write", stream);
 }
 

@@ -448,6 +448,36 @@ void str_substr_copy(const int64_t* off, const uint8_t* chars, int64_t n, int64_
   check_launch("str_substr_copy", stream);
 }
 
+// Order-preserving 8-byte chunks of each string: out[k * n + i] holds bytes
+// [8k, 8k + 8) of string i big-endian, zero padded (a shorter string sorts
+// first on a common prefix, as in byte-wise UTF-8 order), sign bit flipped so
+// signed int64 order equals unsigned byte order. An LSD sort over the chunks
+// (last chunk first) orders the strings: ops/strings.py sort_ranks.
+__global__ __launch_bounds__(kBlock) void prefix_keys_kernel(const int64_t* __restrict__ off,
+                                                             const uint8_t* __restrict__ chars, int64_t n,
+                                                             int chunks, int64_t* __restrict__ out) {
+  const int64_t total = n * chunks;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = t / n, i = t - k * n;
+    const int64_t a = off[i], len = off[i + 1] - a, b0 = 8 * k;
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t p = b0 + j;
+      v = (v << 8) | (p < len ? (uint64_t)chars[a + p] : 0u);
+    }
+    out[t] = (int64_t)(v ^ 0x8000000000000000ull);
+  }
+}
+
+void str_prefix_keys(const int64_t* off, const uint8_t* chars, int64_t n, int chunks, int64_t* out,
+                     hipStream_t stream) {
+  if (n == 0 || chunks <= 0) return;
+  hipLaunchKernelGGL(prefix_keys_kernel, dim3(grid_for(n * chunks, kBlock, 65536)), dim3(kBlock), 0, stream, off,
+                     chars, n, chunks, out);
+  check_launch("str_prefix_keys", stream);
+}
+
 void str_hash64(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* valid, int64_t* out,
                 hipStream_t stream) {
   if (n == 0) return;

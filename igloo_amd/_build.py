@@ -45,7 +45,8 @@ def _includes() -> list[str]:
 
 def _sources() -> list[Path]:
     srcs = sorted(CSRC.rglob("*.cpp")) + sorted(CSRC.rglob("*.hip"))
-    return srcs
+    # csrc/tools/: standalone host programs (sanitizer driver), not extension units
+    return [p for p in srcs if "tools" not in p.relative_to(CSRC).parts]
 
 
 def _headers_digest() -> str:

@@ -132,6 +132,9 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     # invalidating it inside the runtime
     sync_mode = torch.cuda.get_sync_debug_mode()
     torch.cuda.set_sync_debug_mode(2)
+    dump = os.environ.get("IGLOO_GRAPH_DUMP")     # debugging: DOT dump of every captured graph
+    if dump:
+        g.enable_debug_mode()
     try:
         with torch.cuda.stream(s):
             g.capture_begin(pool=engine.graph_pool(), capture_error_mode="thread_local")
@@ -168,5 +171,8 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         _lib.set_capturing(False)
         _lib.set_speculation(None)
         cur.wait_stream(s)
+    if dump:
+        os.makedirs(dump, exist_ok=True)
+        g.debug_dump(os.path.join(dump, f"graph_{STATS['captured']}.dot"))
     STATS["captured"] += 1
     return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill)

@@ -751,7 +751,7 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
                 ridx, lidx, _ = table.probe_pairs(rk, rvalid)
                 pair = _combine(lb, rb, lidx, ridx, False)
                 keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-                matched[gather_tensor(lidx, keep).long()] = True
+                matched.index_fill_(0, gather_tensor(lidx, keep).long(), True)
             sel = mask_to_indices(matched if kind == "semi" else ~matched)
         with ctx.span("join.gather"):
             return _take_batch(lb, sel)
@@ -808,14 +808,14 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
         bidx = gather_tensor(bidx, sel)
         if kind in ("semi", "anti", "left", "full"):
             hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
-            hit[pidx.long()] = True
+            hit.index_fill_(0, pidx.long(), True)
             if kind == "semi":
                 return _take_batch(lb, mask_to_indices(hit))
             if kind == "anti":
                 return _take_batch(lb, mask_to_indices(~hit))
             if kind == "full":
                 matched = torch.zeros(n_r, dtype=torch.bool, device=dev)
-                matched[bidx.long()] = True
+                matched.index_fill_(0, bidx.long(), True)
             counts = hit.to(torch.int32)
         else:
             return _combine(lb, rb, pidx, bidx, False)
@@ -893,7 +893,7 @@ def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residu
         with ctx.span("join.gather"):
             return _combine(lb, rb, lidx, ridx, False)
     hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
-    hit[lidx.long()] = True
+    hit.index_fill_(0, lidx.long(), True)
     if kind == "semi":
         return _take_batch(lb, mask_to_indices(hit))
     if kind == "anti":
@@ -942,7 +942,7 @@ def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:
     if kind in ("inner", "cross"):
         return pair
     hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
-    hit[li] = True
+    hit.index_fill_(0, li.long(), True)
     if kind == "semi":
         return _take_batch(lb, mask_to_indices(hit))
     if kind == "anti":
@@ -952,7 +952,7 @@ def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:
         out = _combine(lb, rb, torch.cat([li, miss]), torch.cat([ri, torch.full_like(miss, -1)]), True)
         if kind == "full":
             rh = torch.zeros(n_r, dtype=torch.bool, device=dev)
-            rh[ri] = True
+            rh.index_fill_(0, ri.long(), True)
             um = mask_to_indices(~rh).to(torch.int64)
             out = concat_batches([out, _combine(lb, rb, torch.full_like(um, -1), um, True, left_null=True)])
         return out
@@ -1876,7 +1876,7 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
         if n:
             _, _, rep = H.group_ids(pair)
             first = torch.zeros(n, dtype=torch.bool, device=dev)
-            first[rep.long()] = True
+            first.index_fill_(0, rep.long(), True)
             keep_rows = keep_rows & first
         valid = keep_rows
     base = len(specs)

@@ -239,7 +239,7 @@ class JoinTable:
         pidx = torch.repeat_interleave(torch.arange(cnt.numel()), cnt)
         starts = torch.cumsum(cnt, 0) - cnt
         bpos = lo.index_select(0, pidx) + torch.arange(total) - starts.index_select(0, pidx)
-        build_matched[self.order.index_select(0, bpos)] = True
+        build_matched.index_fill_(0, self.order.index_select(0, bpos).long(), True)
 
 
 #: inputs at least this large are checked for sorted (clustered) keys first
@@ -428,7 +428,7 @@ def sorted_exists(big2: torch.Tensor, small2: torch.Tensor, lo: torch.Tensor, cn
         bv, sv = big2.index_select(0, b.long()), small2.index_select(0, s.long())
         ok = {"=": bv == sv, "<>": bv != sv, "<": bv < sv, "<=": bv <= sv, ">": bv > sv, ">=": bv >= sv}[op]
         hit = torch.zeros(ns, dtype=torch.bool)
-        hit[s.long()[ok]] = True
+        hit.index_fill_(0, s.long()[ok], True)
         return hit
     hit = torch.empty(ns, dtype=torch.bool, device=big2.device)
     launch("sorted_exists").sorted_exists(ptr(big2), ptr(small2), dt == torch.int64, ptr(lo), ptr(cnt), ns,
@@ -482,14 +482,31 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
              else torch.full((cap,), EMPTY_KEY, dtype=torch.int64, device=dev))
     N.groupby_build(ptr(keys), k64, n, ptr(tkeys), ptr(trow), cap, kmin, direct, s)
     occ = torch.empty(cap, dtype=torch.bool, device=dev)
-    N.groupby_occupied(ptr(trow), cap, ptr(occ), s)
+    gid_of_slot = torch.empty(cap, dtype=torch.int32, device=dev)
+    N.groupby_occupied(ptr(trow), cap, ptr(occ), ptr(gid_of_slot), s)
     slots = mask_to_indices(occ)
     g = slots.numel()
-    gid_of_slot = torch.empty(cap, dtype=torch.int32, device=dev)
     rep = torch.empty(g, dtype=torch.int32, device=dev)
     N.groupby_assign(ptr(slots), slots.dtype == torch.int64, g, ptr(trow), ptr(gid_of_slot), ptr(rep), s)
     gid = torch.empty(n, dtype=torch.int32, device=dev)
     N.groupby_lookup(ptr(keys), k64, n, ptr(tkeys), ptr(gid_of_slot), cap, kmin, direct, ptr(gid), s)
+    if not direct and g > 1:
+        # hashed slots depend on the order in which threads inserted colliding
+        # keys, so slot-order ids differ between runs; renumber the groups by
+        # their first row (the direct path is already in key order). Stable ids
+        # keep every later readback that depends on them (packed-key ranges,
+        # group order) identical across executions, which replayed readbacks
+        # and query graphs rely on.
+        from .gather import gather_tensor
+        first = rep.clamp(max=n - 1).long()        # in bounds even under a mismatched replay
+        mark = torch.zeros(n, dtype=torch.bool, device=dev)
+        mark.index_fill_(0, first, True)
+        order = mask_to_indices(mark)
+        newpos = torch.zeros(n, dtype=torch.int32, device=dev)
+        newpos.index_copy_(0, order.long(), torch.arange(order.numel(), dtype=torch.int32, device=dev))
+        remap = newpos.index_select(0, first)
+        gid = gather_tensor(remap, gid)
+        rep = order.to(torch.int32)
     return gid, g, rep
 
 

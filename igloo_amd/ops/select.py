@@ -24,7 +24,7 @@ def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
     total = to_host_int(ws[tiles:])
     out = torch.empty(total, dtype=it, device=mask.device)
     if total:
-        N.select_write(ptr(mask), n, ptr(ws), ptr(out), it == torch.int64, s)
+        N.select_write(ptr(mask), n, ptr(ws), ptr(out), it == torch.int64, total, s)
     return out
 
 

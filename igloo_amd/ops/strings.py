@@ -18,7 +18,7 @@ import torch
 from .. import types as T
 from ..columnar import Column
 from .gather import gather_tensor
-from ._lib import check_not_capturing, is_gpu, launch, ptr, stream, to_host_int
+from ._lib import capturing, check_not_capturing, is_gpu, launch, ptr, stream, to_host_int
 from .gather import take
 from .hashing import group_ids
 from .select import offsets_from_lengths
@@ -346,6 +346,11 @@ def sort_ranks(col: Column) -> torch.Tensor:
     c = dict_encode(col) if not col.is_dict else col
     cache = c.dictionary.derived()
     lut = cache.get("rank")
+    dd = c.dictionary
+    if lut is None and is_gpu(dd.data) and dd.valid is None and dd.offsets is not None:
+        lut = _device_ranks(dd)
+        if not capturing():     # a rank computed inside a graph lives in its pool: never cache it
+            cache["rank"] = lut
     if lut is None:
         check_not_capturing("dictionary rank upload")
         d = c.dictionary.to_arrow()
@@ -357,6 +362,26 @@ def sort_ranks(col: Column) -> torch.Tensor:
         rank[order] = np.arange(len(order), dtype=np.int64)
         lut = cache["rank"] = torch.from_numpy(rank).to(c.device)
     return gather_tensor(lut, c.data)
+
+
+def _device_ranks(d: Column) -> torch.Tensor:
+    """Byte-wise UTF-8 order rank of every entry of a plain-string dictionary,
+    on the device: an LSD radix argsort over 8-byte big-endian chunks
+    (``str_prefix_keys``, last chunk first; ops/sort.py). The only host value is
+    the longest entry's length (a replayable readback)."""
+    from .sort import argsort
+    n = len(d)
+    dev = d.data.device
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    lens = d.offsets[1:] - d.offsets[:-1]
+    chunks = max(1, (to_host_int(lens.max()) + 7) // 8)
+    keys = torch.empty(chunks * n, dtype=torch.int64, device=dev)
+    launch("str_prefix_keys").str_prefix_keys(ptr(d.offsets), ptr(d.data), n, chunks, ptr(keys), stream(keys))
+    perm = argsort([(keys[k * n:(k + 1) * n], False, False, None) for k in range(chunks)], n, dev)
+    rank = torch.empty(n, dtype=torch.int64, device=dev)
+    rank.index_copy_(0, perm.long(), torch.arange(n, dtype=torch.int64, device=dev))
+    return rank
 
 
 def group_codes(col: Column) -> Tuple[torch.Tensor, Column]:

@@ -49,6 +49,12 @@ for q in qs:
         print(f"Q{q} run {i}: {e.last_metrics['speculation']} {1e3 * (time.perf_counter() - t):.2f} ms rows={r.table.num_rows}",
               flush=True)
     print(graphs.STATS, flush=True)
+    if e.last_metrics["speculation"] != "graph":
+        for st in e._spec.values():
+            for site, vals in (st.get("log") or []):
+                if vals is None:
+                    code, line = site[0]
+                    print(f"  volatile readback: {code.co_filename.split('repo/')[-1]}:{line} ({code.co_name})", flush=True)
     for m in graphs.LAST_ERROR:
         print(m, flush=True)
     graphs.LAST_ERROR.clear()

@@ -176,3 +176,31 @@ def test_column_stats_and_run_bounds(gpu_device, n, dtype):
         ref = torch.ones(n, dtype=torch.bool)
         ref[1:] = s[1:] != s[:-1]
         assert torch.equal(bound.cpu(), ref)
+
+
+def test_device_string_ranks_match_arrow_order():
+    """ops/strings.py _device_ranks (8-byte big-endian chunks + LSD radix
+    argsort) orders a plain-string dictionary exactly like Arrow's byte-wise
+    UTF-8 sort: shared prefixes, empty strings, prefixes of each other,
+    multi-byte characters, lengths across several chunks."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import torch
+    from igloo_amd.columnar import Column
+    from igloo_amd.ops import strings as S
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = np.random.default_rng(3)
+    alphabet = list("abcAB z09") + ["é", "ß", "日"]
+    vals = {"", "a", "ab", "abcdefgh", "abcdefghi", "abcdefgh\x01", "Customer#000000001", "Customer#000000010"}
+    while len(vals) < 3000:
+        vals.add("".join(r.choice(alphabet, size=int(r.integers(0, 30)))))
+    vals = list(vals)
+    r.shuffle(vals)
+    d = Column.from_arrow(pa.array(vals, pa.large_string()), device="cuda:0", dict_encode=False)
+    got = S._device_ranks(d).cpu().numpy()
+    order = pc.array_sort_indices(pa.array(vals, pa.large_string())).to_numpy()
+    want = np.empty(len(vals), dtype=np.int64)
+    want[order] = np.arange(len(vals))
+    assert (got == want).all()
