@@ -61,6 +61,9 @@ def parse_queries(s: str):
     return out
 
 
+_MODE_TAG = {"recorded": "R", "replayed": "P", "graph": "G", "partial": "x"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -140,11 +143,13 @@ def main():
     spec_modes = {}
 
     def suite(record=None, results=None, scanned=None):
+        modes = []
         for q in qs:
             tq = time.perf_counter()
             r = eng.sql(queries.QUERIES[q])
             m = eng.last_metrics.get("speculation")
             spec_modes[m] = spec_modes.get(m, 0) + 1
+            modes.append(f"{q}:{_MODE_TAG.get(m, '-')}")
             if results is not None:
                 results[q] = r.table
             if scanned is not None:
@@ -152,6 +157,8 @@ def main():
             if record is not None:
                 barrier()
                 record[q] = record.get(q, 0.0) + (time.perf_counter() - tq)
+        if a.per_query:
+            log("[bench] modes " + " ".join(modes))
 
     # ---- cold: first touch of every column (Parquet read + GPU decode) and structure
     barrier()
@@ -222,6 +229,11 @@ def main():
     if comm is not None:
         scanned = comm.allreduce_int(int(scanned))
     if rank == 0:
+        if a.per_query:
+            from igloo_amd.exec import graphs as _graphs
+            log(f"[bench] graphs: {_graphs.STATS}")
+            for msg in _graphs.LAST_ERROR:
+                log("[bench] graph not captured: " + msg.strip().replace("\n", " | ")[-600:])
         if per_q:
             for q in qs:
                 print(f"[bench] Q{q:02d} {per_q[q] / a.steps * 1e3:9.2f} ms", file=sys.stderr)

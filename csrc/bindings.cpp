@@ -443,6 +443,9 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("avg_wide", [](uintptr_t sums, bool wide, uintptr_t cnt, int64_t n, int64_t up, uintptr_t out, uintptr_t s) {
+    kern::avg_wide(P<const int64_t>(sums), wide, P<const int64_t>(cnt), n, up, P<int64_t>(out), S(s));
+  });
   m.def("str_prefix_keys", [](uintptr_t off, uintptr_t chars, int64_t n, int chunks, uintptr_t out, uintptr_t s) {
     kern::str_prefix_keys(P<const int64_t>(off), P<const uint8_t>(chars), n, chunks, P<int64_t>(out), S(s));
   });

@@ -162,5 +162,51 @@ void run_bounds(const void* keys, bool key64, int64_t n, uint8_t* out, hipStream
   check_launch("util.run_bounds", stream);
 }
 
+namespace {
+
+// Exact decimal AVG finaliser: out[i] = round_half_away(sum[i] * up / max(cnt[i], 1))
+// for 128-bit sums stored as (lo, hi) int64 pairs (or plain int64 when hi is
+// null). Keeps the whole aggregation on the device (no host round trip for
+// the int128 division), so AVG over wide sums can live inside a query graph.
+__global__ __launch_bounds__(kBlock) void avg_wide_kernel(const int64_t* __restrict__ sums, bool wide,
+                                                          const int64_t* __restrict__ cnt, int64_t n, int64_t up,
+                                                          int64_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    __int128 v = wide ? (((__int128)sums[2 * i + 1]) << 64) | (unsigned __int128)(uint64_t)sums[2 * i]
+                      : (__int128)sums[i];
+    const bool neg = v < 0;
+    unsigned __int128 num = (unsigned __int128)(neg ? -v : v) * (unsigned __int128)up;
+    const uint64_t k = (uint64_t)(cnt[i] > 0 ? cnt[i] : 1);
+    // schoolbook 128 / 64 division (the divisor fits 64 bits): two 64-bit steps
+    const uint64_t hi = (uint64_t)(num >> 64), lo = (uint64_t)num;
+    const uint64_t qh = hi / k, rh = hi % k;
+    unsigned __int128 rest = ((unsigned __int128)rh << 64) | lo;
+    // rest < k * 2^64: long division bit by bit over the low word
+    uint64_t ql = 0;
+    unsigned __int128 r = 0;
+    for (int b = 127; b >= 0; --b) {
+      r = (r << 1) | (uint64_t)((rest >> b) & 1);
+      if (r >= k) {
+        r -= k;
+        if (b < 64) ql |= (uint64_t)1 << b;
+      }
+    }
+    unsigned __int128 q = ((unsigned __int128)qh << 64) | ql;
+    if (2 * r >= (unsigned __int128)k) q += 1;   // half away from zero
+    const int64_t res = (int64_t)(uint64_t)q;
+    out[i] = neg ? -res : res;
+  }
+}
+
+}  // namespace
+
+void avg_wide(const int64_t* sums, bool wide, const int64_t* cnt, int64_t n, int64_t up, int64_t* out,
+              hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(avg_wide_kernel, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, stream, sums, wide, cnt, n,
+                     up, out);
+  check_launch("util.avg_wide", stream);
+}
+
 }  // namespace kern
 }  // namespace igloo

@@ -426,6 +426,11 @@ class QueryEngine:
             return batch, "replayed" if sp.complete else "partial", st
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
+        if st["log"] is not None and _graphs.GRAPHS and st["fails"] == 0 and st["graph"] is None \
+                and st["graph_aborts"] < 2:
+            # a confirmed recording: the next execution captures it straight
+            # away (its graph is checked against this run's result digest)
+            st["capture_next"] = True
         return batch, "recorded", st
 
     def _check_graph(self, st: dict, spec, table: pa.Table, plan: Plan, names, ctx) -> pa.Table:
@@ -433,7 +438,7 @@ class QueryEngine:
         result before a capture is digested; the graph's first result must
         match it, otherwise the query is never captured again and this result
         is recomputed eagerly."""
-        if spec == "replayed" and st["capture_next"]:
+        if spec in ("replayed", "recorded") and st["capture_next"]:
             st["digest"] = digest(table)
         elif spec == "graph":
             g = st["graph"]

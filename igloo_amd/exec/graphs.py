@@ -64,7 +64,7 @@ LAST_ERROR: list = []    # why the last captures did not produce a graph (debugg
 
 def _note(msg: str) -> None:
     LAST_ERROR.append(msg)
-    del LAST_ERROR[:-8]
+    del LAST_ERROR[:-24]
 
 
 def _capture_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -148,7 +148,8 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     except _lib.CaptureAbort as e:
         engine._graph_pool = None
         STATS["aborted"] += 1
-        _note(f"aborted: {e}")
+        _note(f"aborted: {e} :: " + " <- ".join(
+            f"{f.filename.split('igloo_amd/')[-1]}:{f.lineno}" for f in traceback.extract_tb(e.__traceback__)[-4:][::-1]))
         log.debug("query graph not captured: %s", e)
         return None
     except RuntimeError as e:

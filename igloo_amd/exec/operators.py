@@ -1981,6 +1981,12 @@ def _avg(s: torch.Tensor, c: torch.Tensor, src, t) -> torch.Tensor:
     cc = c.clamp(min=1)
     if t.is_decimal:
         up = 10 ** (t.scale - (src.scale if src.is_decimal else 0))
+        if s.is_cuda:
+            # exact rounded division of the (int64 or 128-bit) sums on the device
+            out = torch.empty(s.shape[0], dtype=torch.int64, device=s.device)
+            launch("avg_wide").avg_wide(ptr(s.contiguous()), s.dim() == 2, ptr(c.to(torch.int64).contiguous()),
+                                        s.shape[0], up, ptr(out), stream(s))
+            return out
         if s.dim() == 1:
             lim = (2**63 - 1) // up
             if to_host_int((s.abs() < lim).all().to(torch.int64)):

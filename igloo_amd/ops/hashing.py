@@ -273,8 +273,17 @@ def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = 
     hit = getattr(big, "_igloo_dense", None)
     if hit or not build or (hit is False and queries is None):
         return hit or None
+    rng = getattr(big, "_igloo_range", None)
+    if hit is False and rng is not None and rng[1] - rng[0] + 1 > _dense_limit(big.numel(), queries):
+        return None           # still too sparse for this many lookups: nothing to build
     with unlogged():          # built once per column tensor
         return _dense_index_build(big, queries)
+
+
+def _dense_limit(nb: int, queries: Optional[int]) -> int:
+    """Largest key span worth a table: small next to both the indexed rows and
+    the lookups it serves."""
+    return DENSE_INDEX_MAX_SPAN_RATIO * min(nb, queries if queries is not None else nb) + 4096
 
 
 def _dense_index_build(big: torch.Tensor, queries: Optional[int]):
@@ -291,9 +300,7 @@ def _dense_index_build(big: torch.Tensor, queries: Optional[int]):
                 pass
         kmin, kmax = rng
         span = kmax - kmin + 1
-        # the table must be small next to both the indexed rows and the lookups it serves
-        limit = DENSE_INDEX_MAX_SPAN_RATIO * min(nb, queries if queries is not None else nb) + 4096
-        if span <= limit:
+        if span <= _dense_limit(nb, queries):
             it = torch.int64 if nb >= INT32_MAX else torch.int32
             first = torch.empty(span + 1, dtype=it, device=big.device)
             gap = torch.zeros(1, dtype=torch.int32, device=big.device)

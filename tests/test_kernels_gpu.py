@@ -428,3 +428,34 @@ def test_probe_select_vs_probe_first(gpu_device, direct):
             assert bidx is None
         else:
             assert torch.equal(bidx.cpu().long(), first.index_select(0, want.long()).cpu().long())
+
+
+def test_avg_wide_exact_rounding():
+    """util.hip avg_wide: exact decimal AVG of 128-bit (lo, hi) and int64 sums,
+    rounded half away from zero, vs Python integers."""
+    import random
+    import torch
+    from igloo_amd.exec.operators import _avg
+    from igloo_amd import types as T
+    rnd = random.Random(7)
+    vals = [0, 1, -1, 5, -5, 2**63 - 1, -(2**63), 2**90 + 12345, -(2**95) - 7, 10**30 + 3]
+    vals += [rnd.randrange(-(2**100), 2**100) for _ in range(500)]
+    cnts = [rnd.randrange(1, 10**9) for _ in vals]
+    cnts[0] = 0
+    lo = [((v + 2**128) % 2**64) - (2**64 if ((v + 2**128) % 2**64) >= 2**63 else 0) for v in vals]
+    hi = [v >> 64 for v in vals]
+    s = torch.tensor(list(zip(lo, hi)), dtype=torch.int64, device="cuda:0")
+    c = torch.tensor(cnts, dtype=torch.int64, device="cuda:0")
+    src, t = T.DECIMAL(15, 2), T.DECIMAL(19, 6)
+    got = _avg(s, c, src, t).cpu().tolist()
+    up = 10 ** 4
+    for v, k, g in zip(vals, cnts, got):
+        k = max(k, 1)
+        num = v * up
+        q = (abs(num) + k // 2) // k
+        want = q if num >= 0 else -q
+        if -(2**63) <= want < 2**63:
+            assert g == want, (v, k, g, want)
+    small = torch.tensor([7, -7, 100, -101], dtype=torch.int64, device="cuda:0")
+    cs = torch.tensor([2, 2, 3, 3], dtype=torch.int64, device="cuda:0")
+    assert _avg(small, cs, src, t).cpu().tolist() == [35000, -35000, 333333, -336667]
