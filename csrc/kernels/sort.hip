@@ -319,6 +319,14 @@ __global__ __launch_bounds__(kBlock) void sort_key_pack_kernel(SortKeySpec spec,
   }
 }
 
+// Zeroes the digit histogram. A kernel rather than hipMemsetAsync: inside a
+// captured query graph (igloo_amd/exec/graphs.py) the memset node did not
+// reliably clear the buffer before the histogram kernel ran on replay (the
+// replayed counts came back offset by the buffer's previous contents).
+__global__ void rs_zero_hist_kernel(unsigned long long* __restrict__ hist, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) hist[i] = 0ull;
+}
+
 template <typename K>
 __global__ __launch_bounds__(kBlock) void rs_digit_hist_kernel(const K* __restrict__ keys, int64_t n, int shift,
                                                                uint64_t prefix, int pshift,
@@ -381,7 +389,7 @@ void sort_key_pack(const SortKeySpec& spec, const void* perm, bool perm64, int64
 
 void radix_digit_hist(const void* keys, bool key64, int64_t n, int shift, uint64_t prefix, int pshift,
                       unsigned long long* hist, hipStream_t stream) {
-  IGLOO_HIP_CHECK(hipMemsetAsync(hist, 0, kRadix * sizeof(unsigned long long), stream));
+  hipLaunchKernelGGL(rs_zero_hist_kernel, dim3(1), dim3(kRadix), 0, stream, hist, kRadix);
   if (n <= 0) return;
   const unsigned g = grid_for(n, kBlock * 8, 2048);
   if (key64)

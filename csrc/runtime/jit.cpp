@@ -21,6 +21,7 @@
 #include <pybind11/stl.h>
 
 #include <cstdint>
+#include <deque>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -98,6 +99,13 @@ int64_t load(const std::string& code, const std::string& name) {
   return (int64_t)g_loaded.size() - 1;
 }
 
+struct KernArgs {
+  std::vector<uint64_t> buf;
+  size_t size;
+};
+// kernarg buffers of captured launches (stable addresses: deque push_back)
+static std::deque<KernArgs> g_captured_args;
+
 // args: the kernel's parameters in order, each one 8-byte slot (pointers and
 // 64-bit integers: the generator declares nothing narrower)
 void launch(int64_t h, uint32_t grid, uint32_t block, uint32_t shmem, uintptr_t stream,
@@ -109,9 +117,21 @@ void launch(int64_t h, uint32_t grid, uint32_t block, uint32_t shmem, uintptr_t 
     f = g_loaded[h].fn;
   }
   if (grid == 0 || block == 0 || block > 1024) throw std::runtime_error("jit launch: bad geometry");
-  std::vector<uint64_t> buf(args);
-  size_t size = buf.size() * sizeof(uint64_t);
-  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+  // Under stream capture (query graphs, igloo_amd/exec/graphs.py) the kernel
+  // node may keep referring to the kernarg buffer passed through `extra`
+  // rather than copying it, so a captured launch gets a buffer that lives as
+  // long as the process (a few hundred bytes per captured launch); graph
+  // replays read garbage arguments otherwise. Eager launches use the stack.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing((hipStream_t)stream, &cap);
+  KernArgs local{args, args.size() * sizeof(uint64_t)};
+  KernArgs* ka = &local;
+  if (cap != hipStreamCaptureStatusNone) {
+    std::lock_guard<std::mutex> g(g_mu);
+    g_captured_args.push_back(local);
+    ka = &g_captured_args.back();
+  }
+  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, ka->buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &ka->size,
                    HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, shmem, (hipStream_t)stream, nullptr, extra),
         "hipModuleLaunchKernel");

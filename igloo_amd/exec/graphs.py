@@ -56,6 +56,8 @@ from ..ops import jit as _jit
 log = logging.getLogger("igloo.graphs")
 
 GRAPHS = os.environ.get("IGLOO_GRAPHS", "1") == "1"
+#: one memory pool for all graphs of an engine (0: a private pool per graph)
+SHARED_POOL = os.environ.get("IGLOO_GRAPH_SHARED_POOL", "0") == "1"
 
 _streams: dict = {}
 STATS = {"captured": 0, "replays": 0, "aborted": 0, "failed": 0, "mismatch": 0}
@@ -78,9 +80,10 @@ class QueryGraph:
     """One captured query: the graph, its static result batch and the device
     mismatch counter of its replayed values."""
 
-    __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays")
+    __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp")
 
-    def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill):
+    def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None):
+        self.sp = sp                   # the capture's speculation (sites + device values, for reports)
         self.graph = graph
         self.batch = batch
         self.bad = bad
@@ -106,6 +109,11 @@ class QueryGraph:
         ok = int(self.bad.item()) == 0
         if not ok:
             STATS["mismatch"] += 1
+            try:
+                act = self.sp.actual[0].tolist() if self.sp is not None and self.sp.actual else []
+                _note(f"mismatch: {self.sp.mismatch_sites(act)[:4]}")
+            except Exception:   # noqa: BLE001 - diagnostics only
+                pass
         return ok
 
 
@@ -137,7 +145,7 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         g.enable_debug_mode()
     try:
         with torch.cuda.stream(s):
-            g.capture_begin(pool=engine.graph_pool(), capture_error_mode="thread_local")
+            g.capture_begin(pool=engine.graph_pool() if SHARED_POOL else None, capture_error_mode="thread_local")
             try:
                 batch = engine._execute_plan(plan, ctx)
                 if not sp.complete:
@@ -176,4 +184,4 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         os.makedirs(dump, exist_ok=True)
         g.debug_dump(os.path.join(dump, f"graph_{STATS['captured']}.dot"))
     STATS["captured"] += 1
-    return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill)
+    return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp)

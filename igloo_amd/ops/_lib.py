@@ -171,7 +171,21 @@ class Speculation:
         act = torch.cat(self.actual)
         if act.numel() != expected_dev.numel():
             raise CaptureAbort("replayed value count differs from the recording")
+        self.actual = [act]      # kept: a mismatch report reads the device values back
         return (act != expected_dev).sum()
+
+    def mismatch_sites(self, act: list) -> list:
+        """(file:line, replayed, device) of every replayed value that differs."""
+        out, pos = [], 0
+        for site, vals in self.log:
+            if vals is None:
+                continue
+            got = act[pos:pos + len(vals)]
+            if got != list(vals):
+                code, line = site[0]
+                out.append((f"{code.co_filename.split('igloo_amd/')[-1]}:{line}", list(vals)[:4], got[:4]))
+            pos += len(vals)
+        return out
 
     def validate(self) -> bool:
         """True when every replayed value equals the device value (one sync).

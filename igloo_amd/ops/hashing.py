@@ -276,7 +276,9 @@ def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = 
     rng = getattr(big, "_igloo_range", None)
     if hit is False and rng is not None and rng[1] - rng[0] + 1 > _dense_limit(big.numel(), queries):
         return None           # still too sparse for this many lookups: nothing to build
-    with unlogged():          # built once per column tensor
+    if not getattr(big, "_igloo_resident", False):
+        return _dense_index_build(big, queries)    # an intermediate: built (and read back) every execution
+    with unlogged():          # built once per resident column tensor
         return _dense_index_build(big, queries)
 
 
@@ -292,8 +294,7 @@ def _dense_index_build(big: torch.Tensor, queries: Optional[int]):
     if nb:
         rng = getattr(big, "_igloo_range", None)
         if rng is None:
-            mm = torch.stack([big[0].to(torch.int64), big[-1].to(torch.int64)]).cpu()
-            rng = (int(mm[0]), int(mm[1]))
+            rng = tuple(to_host_ints(torch.stack([big[0].to(torch.int64), big[-1].to(torch.int64)])))
             try:
                 big._igloo_range = rng
             except (AttributeError, RuntimeError):
