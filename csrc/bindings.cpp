@@ -443,6 +443,9 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("wide_fits", [](uintptr_t lo, uintptr_t hi, int64_t n, uintptr_t flag, uintptr_t s) {
+    kern::wide_fits(P<const int64_t>(lo), P<const int64_t>(hi), n, P<int>(flag), S(s));
+  });
   m.def("avg_wide", [](uintptr_t sums, bool wide, uintptr_t cnt, int64_t n, int64_t up, uintptr_t out, uintptr_t s) {
     kern::avg_wide(P<const int64_t>(sums), wide, P<const int64_t>(cnt), n, up, P<int64_t>(out), S(s));
   });

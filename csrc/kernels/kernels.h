@@ -220,6 +220,7 @@ void str_substr_copy(const int64_t* off, const uint8_t* chars, int64_t n, int64_
 // with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%'
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
                        int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, hipStream_t stream);
+void wide_fits(const int64_t* lo, const int64_t* hi, int64_t n, int* flag, hipStream_t stream);
 void avg_wide(const int64_t* sums, bool wide, const int64_t* cnt, int64_t n, int64_t up, int64_t* out,
               hipStream_t stream);
 void str_prefix_keys(const int64_t* off, const uint8_t* chars, int64_t n, int chunks, int64_t* out,

@@ -198,7 +198,30 @@ __global__ __launch_bounds__(kBlock) void avg_wide_kernel(const int64_t* __restr
   }
 }
 
+__global__ void zero_flag_kernel(int* __restrict__ flag) { *flag = 0; }
+
+__global__ __launch_bounds__(kBlock) void wide_fits_kernel(const int64_t* __restrict__ lo,
+                                                           const int64_t* __restrict__ hi, int64_t n,
+                                                           int* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= hi[i] != (lo[i] >> 63);
+  if (__any(bad) && lane_id() == 0) atomicOr(flag, 1);
+}
+
 }  // namespace
+
+// flag = 1 when some 128-bit (lo, hi) sum does not fit int64 (hi is not the
+// sign extension of lo). Replaces a torch `.all()` over the groups: a torch
+// multi-block reduction zeroes its semaphores with a memset, and inside a
+// captured query graph that memset was not reliably ordered.
+void wide_fits(const int64_t* lo, const int64_t* hi, int64_t n, int* flag, hipStream_t stream) {
+  hipLaunchKernelGGL(zero_flag_kernel, dim3(1), dim3(1), 0, stream, flag);
+  if (n > 0)
+    hipLaunchKernelGGL(wide_fits_kernel, dim3(grid_for(n, kBlock * 4, 8192)), dim3(kBlock), 0, stream, lo, hi, n,
+                       flag);
+  check_launch("util.wide_fits", stream);
+}
 
 void avg_wide(const int64_t* sums, bool wide, const int64_t* cnt, int64_t n, int64_t up, int64_t* out,
               hipStream_t stream) {

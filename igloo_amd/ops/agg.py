@@ -25,9 +25,24 @@ def _ordered_to_f64(x: torch.Tensor) -> torch.Tensor:
     return (x ^ mask).view(torch.float64)
 
 
+def _wide_flags(pairs) -> torch.Tensor:
+    """int32 [len(pairs)]: 1 where some (lo, hi) sum of the pair does not fit
+    int64 (one hand-written pass per pair, no torch reduction)."""
+    dev = pairs[0][0].device
+    flags = torch.empty(len(pairs), dtype=torch.int32, device=dev)
+    N = launch("wide_fits")
+    for i, (lo, hi) in enumerate(pairs):
+        lo, hi = lo.contiguous(), hi.contiguous()
+        N.wide_fits(ptr(lo), ptr(hi), lo.numel(), ptr(flags) + 4 * i, stream(lo))
+    return flags
+
+
 def _wide_to_result(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
-    fits = hi == (lo >> 63)
-    if (to_host_ints(fits.all().to(torch.int64))[0] if fits.is_cuda else bool(fits.all().item())):
+    if lo.is_cuda:
+        fits = not to_host_ints(_wide_flags([(lo, hi)]))[0]
+    else:
+        fits = bool((hi == (lo >> 63)).all().item())
+    if fits:
         return lo
     return torch.stack([lo, hi], dim=1)
 
@@ -74,7 +89,7 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
             N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s, bool(sorted_gids))
     # one host sync for every integer SUM's "fits in int64" check
     wide = [(dst, dst2) for op, dst, dst2 in posts if op == "sum_int"]
-    fits = to_host_ints(torch.stack([(h == (l >> 63)).all() for l, h in wide])) if wide else []
+    fits = [1 - f for f in to_host_ints(_wide_flags(wide))] if wide else []
     fit_iter = iter(fits)
     for op, dst, dst2 in posts:
         if op == "sum_int":
