@@ -251,6 +251,12 @@ def is_sorted(keys: torch.Tensor) -> bool:
     hit = getattr(keys, "_igloo_sorted", None)
     if hit is not None:
         return hit
+    base = getattr(keys, "_igloo_base", None)
+    if base is not None and base[0].data.dtype == keys.dtype and is_sorted(base[0].data):
+        # a filtered scan's rows of a sorted source column, in row order
+        # (exec/operators.py _tag_base): sorted without another pass (the
+        # source's flag is computed once and remembered on it)
+        return True
     n = keys.numel()
     r = True if n < 2 else column_stats(keys)[1]
     try:
