@@ -265,7 +265,12 @@ def to_host_ints(t: torch.Tensor) -> list:
             v = _to_host_ints(t)
             sp.fresh.append((site, v))
             return v
-        sp.actual.append(t.reshape(-1).to(torch.int64, copy=True))
+        # a reference, not a copy: the tensor stays alive (its memory is not
+        # reused) and readback sources are not written again after being read
+        # (a copy per value was ~700 D2D copy launches per SF100 suite); a
+        # source that were overwritten would fail validation, never pass it
+        a = t.reshape(-1)
+        sp.actual.append(a if a.dtype == torch.int64 else a.to(torch.int64))
         sp.expected.extend(v)
         sp.fresh.append((site, v))
         return list(v)

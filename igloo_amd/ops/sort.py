@@ -208,13 +208,13 @@ def _select_candidates(keys: torch.Tensor, bits: int, k: int) -> Optional[torch.
         return None
     N = launch("radix_select")
     k64 = keys.dtype == torch.int64
-    hist = torch.empty(256, dtype=torch.int64, device=keys.device)
     st = stream(keys)
     limit = max(8 * k, 1 << 16)
     pshift, prefix = bits, 0        # rows in play: (key >> pshift) == prefix (all rows: keys < 2^bits)
     shift = max(bits - 8, 0)
     below = 0                       # rows known to rank before the bucket in play
     while True:
+        hist = torch.empty(256, dtype=torch.int64, device=keys.device)   # fresh per pass: its readback may be replayed
         N.radix_digit_hist(ptr(keys), k64, n, shift, prefix, pshift, ptr(hist), st)
         counts = to_host_ints(hist)
         run, digit = below, 255

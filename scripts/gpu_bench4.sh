@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_graphs_gpu.py tests/test_kernels_gpu.py tests/test_fused_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_part.log 2>&1 && \
+timeout -k 10 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_join_paths_gpu.py tests/test_tpch_gpu.py tests/test_tpch_sf1_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_part.log 2>&1 && \
 timeout -k 10 600 python -u bench.py --steps 8 --warmup 5 --per-query > gpurun_out/bench_sf100.log 2>&1
 rc=$?
 echo "exit $rc"
