@@ -104,9 +104,14 @@ void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* desc
     p.ncols = ncols - base < kMaxGatherCols ? ncols - base : kMaxGatherCols;
     for (int c = 0; c < p.ncols; ++c) p.d[c] = descs[base + c];
     static const int rows = getenv("IGLOO_GATHER_ROWS") ? atoi(getenv("IGLOO_GATHER_ROWS")) : kGatherRows;
-    const int R = rows == 1 ? 1 : kGatherRows;
+    const int R = rows == 1 ? 1 : (rows == 8 ? 8 : kGatherRows);
     dim3 g(grid_for(n, kBlock * R, 65536)), b(kBlock);
-    if (R == 1) {
+    if (R == 8) {
+      if (idx64)
+        hipLaunchKernelGGL((gather_multi_kernel<int64_t, 8>), g, b, 0, stream, (const int64_t*)idx, n, p);
+      else
+        hipLaunchKernelGGL((gather_multi_kernel<int32_t, 8>), g, b, 0, stream, (const int32_t*)idx, n, p);
+    } else if (R == 1) {
       if (idx64)
         hipLaunchKernelGGL((gather_multi_kernel<int64_t, 1>), g, b, 0, stream, (const int64_t*)idx, n, p);
       else
