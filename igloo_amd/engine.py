@@ -41,6 +41,7 @@ PLAN_CACHE_SIZE = 256
 #: replay the host readbacks of repeated queries over unchanged data (see
 #: QueryEngine._execute_speculative)
 SPECULATE = os.environ.get("IGLOO_SPECULATE", "1") == "1"
+SPMD_SPECULATE = os.environ.get("IGLOO_SPMD_SPECULATE", "0") == "1"
 
 log = get_logger("engine")
 
@@ -352,13 +353,14 @@ class QueryEngine:
         real readbacks and needs re-confirming; a value mismatch re-executes the query with
         real readbacks (after two, the query is no longer replayed)."""
         from .ops import _lib
-        # single-rank only: a 2-rank rehearsal (shared GPU, gloo) replayed values
-        # that passed validation yet changed a result (Q16) and then faulted;
-        # until that is understood SPMD ranks read every value back
-        if not (SPECULATE and key is not None and self.device.type == "cuda"
-                and (self.comm is None or self.comm.world_size == 1)):
+        # SPMD ranks replay only with IGLOO_SPMD_SPECULATE=1: a 2-rank rehearsal
+        # (shared GPU, gloo) once replayed values that passed validation yet
+        # changed a result (Q16, whose hash-slot group ids were then
+        # non-deterministic; fixed since, ops/hashing.py group_ids) and faulted
+        spmd = self.comm is not None and self.comm.world_size > 1
+        if not (SPECULATE and key is not None and self.device.type == "cuda" and (not spmd or SPMD_SPECULATE)):
             return self._execute_plan(plan, ctx), None, None
-        comm = None
+        comm = self.comm if spmd else None
 
         def agreed(ok: bool) -> bool:
             # SPMD ranks decide together (every rank joins this collective after
@@ -375,7 +377,8 @@ class QueryEngine:
             st = self._spec[skey] = {"log": None, "candidate": None, "fails": 0, "graph": None,
                                      "capture_next": False, "digest": None, "graph_aborts": 0}
         replay = st["log"] is not None and st["fails"] < 2
-        if _graphs.GRAPHS and not self.graphs_disabled and replay and st["fails"] == 0 and st["graph_aborts"] < 2:
+        if _graphs.GRAPHS and comm is None and not self.graphs_disabled and replay and st["fails"] == 0 \
+                and st["graph_aborts"] < 2:
             g = st["graph"]
             if g is not None and not g.current():
                 # the generated-kernel set changed: the recording diverges from
@@ -421,12 +424,13 @@ class QueryEngine:
                 # the call sequence changed: this run's own sequence must be
                 # confirmed by the next execution before it is replayed
                 st["log"], st["candidate"] = None, sp.fresh
-            elif _graphs.GRAPHS and st["fails"] == 0 and st["graph"] is None and st["graph_aborts"] < 2:
+            elif _graphs.GRAPHS and comm is None and st["fails"] == 0 and st["graph"] is None \
+                    and st["graph_aborts"] < 2:
                 st["capture_next"] = True    # _check_graph keeps this result's digest
             return batch, "replayed" if sp.complete else "partial", st
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
-        if st["log"] is not None and _graphs.GRAPHS and st["fails"] == 0 and st["graph"] is None \
+        if st["log"] is not None and _graphs.GRAPHS and comm is None and st["fails"] == 0 and st["graph"] is None \
                 and st["graph_aborts"] < 2:
             # a confirmed recording: the next execution captures it straight
             # away (its graph is checked against this run's result digest)
