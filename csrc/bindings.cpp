@@ -513,10 +513,11 @@ PYBIND11_MODULE(_native, m) {
 
   // ----------------------------------------------------------- sorted joins
   m.def("sorted_ranges", [](uintptr_t big, bool key64, int64_t nb, uintptr_t q, uintptr_t qvalid, int64_t nq,
-                            uintptr_t lo, uintptr_t cnt, uintptr_t s) {
+                            uintptr_t lo, uintptr_t cnt, uintptr_t fence, int64_t nf, uintptr_t s) {
     kern::sorted_ranges(P<const void>(big), key64, nb, P<const void>(q), P<const uint8_t>(qvalid), nq, P<int64_t>(lo),
-                        P<int64_t>(cnt), S(s));
+                        P<int64_t>(cnt), P<const void>(fence), nf, S(s));
   });
+  m.attr("SEARCH_FENCE") = kern::kFence;
   m.def("expand_ranges", [](uintptr_t off, uintptr_t lo, int64_t ns, int64_t total, uintptr_t sidx, uintptr_t bidx,
                             bool out64, uintptr_t s) {
     kern::expand_ranges(P<const int64_t>(off), P<const int64_t>(lo), ns, total, P<void>(sidx), P<void>(bidx), out64,

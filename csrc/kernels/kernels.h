@@ -293,8 +293,10 @@ void csv_str_copy(const int64_t* pos, const int64_t* len_flag, const int64_t* of
 
 // ---- ranges.hip ----------------------------------------------------------------
 // big: non-decreasing int32/int64 keys; per probe key q[i]: big[lo[i] .. lo[i]+cnt[i]) == q[i]
+// fence (optional): big[j * kFence] for j < nf (ops/hashing.py search_fence)
+constexpr int64_t kFence = 256;
 void sorted_ranges(const void* big, bool key64, int64_t nb, const void* q, const uint8_t* qvalid, int64_t nq,
-                   int64_t* lo, int64_t* cnt, hipStream_t stream);
+                   int64_t* lo, int64_t* cnt, const void* fence, int64_t nf, hipStream_t stream);
 // off: exclusive offsets [ns] of the range lengths (total = sum); pairs (s, lo[s] + k) for k < len(s)
 void expand_ranges(const int64_t* off, const int64_t* lo, int64_t ns, int64_t total, void* sidx, void* bidx,
                    bool out64, hipStream_t stream);

@@ -30,7 +30,8 @@ __global__ __launch_bounds__(kBlock) void sorted_ranges_kernel(const K* __restri
                                                               const K* __restrict__ q,
                                                               const uint8_t* __restrict__ qvalid, int64_t nq,
                                                               int64_t* __restrict__ lo_out,
-                                                              int64_t* __restrict__ cnt_out) {
+                                                              int64_t* __restrict__ cnt_out,
+                                                              const K* __restrict__ fence, int64_t nf) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
     if (qvalid && !qvalid[i]) {
       lo_out[i] = 0;
@@ -39,6 +40,19 @@ __global__ __launch_bounds__(kBlock) void sorted_ranges_kernel(const K* __restri
     }
     const K key = q[i];
     int64_t a = 0, b = nb;
+    if (fence) {
+      // fence[j] = big[j * kFence] (a 1/kFence sample small enough to stay in
+      // L2 / MALL): its lower bound j brackets the answer to one kFence-row
+      // window, so the search touches ~3 HBM lines instead of ~20
+      int64_t fa = 0, fb = nf;
+      while (fa < fb) {
+        const int64_t m = (fa + fb) >> 1;
+        if (fence[m] < key) fa = m + 1;
+        else fb = m;
+      }
+      a = fa > 0 ? (fa - 1) * kFence : 0;
+      b = fa * kFence < nb ? fa * kFence : nb;
+    }
     while (a < b) {
       const int64_t m = (a + b) >> 1;
       if (big[m] < key) a = m + 1;
@@ -117,15 +131,17 @@ __global__ __launch_bounds__(kBlock) void expand_ranges_kernel(const int64_t* __
 }  // namespace
 
 void sorted_ranges(const void* big, bool key64, int64_t nb, const void* q, const uint8_t* qvalid, int64_t nq,
-                   int64_t* lo, int64_t* cnt, hipStream_t stream) {
+                   int64_t* lo, int64_t* cnt, const void* fence, int64_t nf, hipStream_t stream) {
   if (nq <= 0) return;
   const unsigned grid = grid_for(nq, kBlock, 1 << 16);
   if (key64)
     hipLaunchKernelGGL(sorted_ranges_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, stream,
-                       static_cast<const int64_t*>(big), nb, static_cast<const int64_t*>(q), qvalid, nq, lo, cnt);
+                       static_cast<const int64_t*>(big), nb, static_cast<const int64_t*>(q), qvalid, nq, lo, cnt,
+                       static_cast<const int64_t*>(fence), nf);
   else
     hipLaunchKernelGGL(sorted_ranges_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, stream,
-                       static_cast<const int32_t*>(big), nb, static_cast<const int32_t*>(q), qvalid, nq, lo, cnt);
+                       static_cast<const int32_t*>(big), nb, static_cast<const int32_t*>(q), qvalid, nq, lo, cnt,
+                       static_cast<const int32_t*>(fence), nf);
   check_launch("sorted_ranges", stream);
 }
 

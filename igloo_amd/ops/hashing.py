@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import check_not_capturing, is_gpu, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
+from ._lib import check_not_capturing, is_gpu, launch, native, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
 from .select import exclusive_scan, mask_to_indices
 
 EMPTY_KEY = -(2**63)
@@ -353,10 +353,33 @@ def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Ten
                                             ptr(qvalid.contiguous() if qvalid is not None else None), nq, ptr(lo),
                                             ptr(cnt), stream(big))
         return lo, cnt
+    fence = search_fence(big) if SEARCH_FENCE else None
     launch("sorted_ranges").sorted_ranges(ptr(big), big.dtype == torch.int64, big.numel(), ptr(q),
                                           ptr(qvalid.contiguous() if qvalid is not None else None), nq, ptr(lo),
-                                          ptr(cnt), stream(big))
+                                          ptr(cnt), ptr(fence), 0 if fence is None else fence.numel(), stream(big))
     return lo, cnt
+
+
+SEARCH_FENCE = os.environ.get("IGLOO_SEARCH_FENCE", "1") == "1"
+SEARCH_FENCE_MIN_ROWS = 1 << 22
+
+
+def search_fence(big: torch.Tensor) -> Optional[torch.Tensor]:
+    """Every 256th key of a large sorted RESIDENT key column (1/256 of its
+    bytes, kept with it like the other derived structures): binary searches
+    first narrow to one 256-row window through it (L2/MALL-resident), then
+    touch only that window of the column (csrc/kernels/ranges.hip)."""
+    if big.numel() < SEARCH_FENCE_MIN_ROWS or not getattr(big, "_igloo_resident", False):
+        return None
+    hit = getattr(big, "_igloo_fence", None)
+    if hit is None:
+        check_not_capturing("search fence of a resident column")
+        hit = big[::native().SEARCH_FENCE].contiguous()
+        try:
+            big._igloo_fence = hit
+        except (AttributeError, RuntimeError):
+            return None
+    return hit
 
 
 def perm_index(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -6,7 +6,8 @@ with the column tensor like an index (attributes set by the operators):
 * ``_igloo_narrow``  narrow integer copy read by the fused scans (exec/fused.py);
 * ``_igloo_perm``    secondary index: sorted keys + row permutation (ops/hashing.py);
 * ``_igloo_dense``   dense lower-bound range index of a sorted key column;
-* ``_igloo_hll``     HyperLogLog registers (4 KB).
+* ``_igloo_hll``     HyperLogLog registers (4 KB);
+* ``_igloo_fence``   every 256th key of a sorted column (binary-search fence).
 
 The cache tier (cache/tiered.py) charges them to the column that owns them,
 so the HBM budget covers what the table really holds, and evicting a column
@@ -18,7 +19,7 @@ from typing import Iterable
 
 import torch
 
-DERIVED_ATTRS = ("_igloo_narrow", "_igloo_perm", "_igloo_dense", "_igloo_hll")
+DERIVED_ATTRS = ("_igloo_narrow", "_igloo_perm", "_igloo_dense", "_igloo_hll", "_igloo_fence")
 
 
 def _tensor_bytes(x) -> int:

@@ -459,3 +459,28 @@ def test_avg_wide_exact_rounding():
     small = torch.tensor([7, -7, 100, -101], dtype=torch.int64, device="cuda:0")
     cs = torch.tensor([2, 2, 3, 3], dtype=torch.int64, device="cuda:0")
     assert _avg(small, cs, src, t).cpu().tolist() == [35000, -35000, 333333, -336667]
+
+
+def test_sorted_ranges_with_search_fence():
+    """ops/hashing.py search_fence + ranges.hip: binary searches over a large
+    sorted resident column narrowed through every 256th key give the same
+    (lo, cnt) as numpy searchsorted (duplicates, gaps, keys outside the range,
+    runs longer than a fence window)."""
+    import numpy as np
+    import torch
+    from igloo_amd.ops import hashing as H
+    r = np.random.default_rng(5)
+    n = 5_000_000
+    k = np.sort(np.concatenate([r.integers(0, 2_000_000, n - 3000), np.full(3000, 777_777)])).astype(np.int32)
+    big = torch.from_numpy(k).to("cuda:0")
+    big._igloo_resident = True
+    q = np.concatenate([r.integers(-10, 2_000_010, 200_000), [777_777, k[0], k[-1], -5, 3_000_000]]).astype(np.int32)
+    lo, cnt = H.sorted_ranges(big, torch.from_numpy(q).to("cuda:0"))
+    assert getattr(big, "_igloo_fence", None) is not None
+    want_lo = np.searchsorted(k, q, side="left")
+    want_cnt = np.searchsorted(k, q, side="right") - want_lo
+    got_cnt = cnt.cpu().numpy()
+    got_lo = lo.cpu().numpy()
+    assert (got_cnt == want_cnt).all()
+    hit = want_cnt > 0
+    assert (got_lo[hit] == want_lo[hit]).all()
