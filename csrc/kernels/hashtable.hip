@@ -58,7 +58,14 @@ __device__ inline int64_t insert_slot(int64_t* __restrict__ tkeys, int64_t mask,
 // Optional 1-hash Bloom filter over the build keys (<= 4 MB, so it stays in a
 // XCD's L2): a selective probe (most probe keys absent) answers from L2 and
 // never touches the HBM-sized table.
-__device__ inline uint64_t bloom_bit(int64_t k, uint64_t bmask) { return (mix64((uint64_t)k) >> 7) & bmask; }
+// Bloom bit of key k. With kExactBits set in bmask (direct-mapped tables whose
+// key span fits the bitmap, ops/hashing.py JoinTable) the "filter" is an exact
+// membership bitmap indexed by k - kmin: no false positives, so a probe reads
+// the table only for keys that are present. Callers range-check k first.
+constexpr uint64_t kExactBits = 1ull << 63;
+__device__ inline uint64_t bloom_bit(int64_t k, uint64_t bmask, int64_t kmin) {
+  return (bmask & kExactBits) ? (uint64_t)(k - kmin) : ((mix64((uint64_t)k) >> 7) & bmask);
+}
 
 template <typename K, bool DIRECT>
 __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
@@ -85,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict_
     next[i] = old;
     local_dups += old != -1;
     if (bits) {
-      const uint64_t bb = bloom_bit(k, bmask);
+      const uint64_t bb = bloom_bit(k, bmask, kmin);
       atomicOr(&bits[bb >> 5], 1u << (bb & 31));
     }
   }
@@ -100,15 +107,12 @@ __device__ inline int32_t probe_head(const K* keys, const uint8_t* valid, int64_
                                      uint64_t bmask) {
   int64_t k;
   if (!load_key(keys, valid, j, &k)) return -1;
+  if (DIRECT && (k - kmin < 0 || k - kmin >= cap)) return -1;
   if (bits) {
-    const uint64_t b = bloom_bit(k, bmask);
+    const uint64_t b = bloom_bit(k, bmask, kmin);
     if (!((bits[b >> 5] >> (b & 31)) & 1u)) return -1;
   }
-  if (DIRECT) {
-    int64_t s = k - kmin;
-    if (s < 0 || s >= cap) return -1;
-    return thead[s];
-  }
+  if (DIRECT) return thead[k - kmin];
   int64_t s = find_slot(tkeys, cap - 1, k);
   return s < 0 ? -1 : thead[s];
 }
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void join_probe_first_direct_kernel(
       uint32_t w[kProbeRows];
 #pragma unroll
       for (int r = 0; r < kProbeRows; ++r) {
-        const uint64_t b = ok[r] ? bloom_bit(s[r] + kmin, bmask) : 0;
+        const uint64_t b = ok[r] ? bloom_bit(s[r] + kmin, bmask, kmin) : 0;
         w[r] = ok[r] ? (bits[b >> 5] >> (b & 31)) & 1u : 0u;
       }
 #pragma unroll

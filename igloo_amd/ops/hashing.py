@@ -21,6 +21,8 @@ EMPTY_KEY = -(2**63)
 INT32_MAX = 2**31 - 1
 BLOOM_MAX_KEYS = 4 << 20   # build sides up to this size get a Bloom filter
 BLOOM_MIN_RATIO = 4        # ... used when probe rows >= ratio x build rows
+EXACT_BITMAP = os.environ.get("IGLOO_EXACT_BITMAP", "1") == "1"
+EXACT_BITMAP_MAX_SPAN = 1 << 25   # direct tables up to this key span use an exact bitmap instead
 #: join build keys whose [min, max] span is at most this use the direct-mapped
 #: table (one random read per probe) whatever the build size: 2^26 slots is a
 #: 256 MB head array, small next to 288 GB of HBM
@@ -110,7 +112,12 @@ class JoinTable:
         self.cap = span if self.direct else _next_pow2(2 * n)
         # Bloom filter for selective probes: ~8 bits per key, at most 4 MB (L2-resident)
         self.bits, self.bmask = None, 0
-        if n <= BLOOM_MAX_KEYS:
+        if self.direct and EXACT_BITMAP and span <= EXACT_BITMAP_MAX_SPAN:
+            # exact membership bitmap over the key span (<= 4 MB, L2-resident):
+            # no false positives (csrc/kernels/hashtable.hip kExactBits)
+            self.bits = torch.zeros((span + 31) // 32, dtype=torch.int32, device=self.device)
+            self.bmask = 1 << 63
+        elif n <= BLOOM_MAX_KEYS:
             nbits = min(max(_next_pow2(8 * n), 1 << 15), 1 << 25)
             self.bits = torch.zeros(nbits // 32, dtype=torch.int32, device=self.device)
             self.bmask = nbits - 1
