@@ -191,13 +191,28 @@ class CachedTable(TableSource):
         dev = str(ctx.device) if ctx is not None else "cpu"
         return f"{self.name}/{rank}of{world}/{dev}/{c}"
 
+    def poll(self) -> bool:
+        """Run this table's CDC probe (rate-limited by ``poll_interval_s``);
+        True when the source changed (its cache entries are then dropped and
+        the cache generation moves). engine.py calls it before replaying a
+        query graph, which never reaches ``scan``."""
+        if self.cdc is None:
+            return False
+        return self.cdc.maybe_poll(self.name, self.poll_interval_s)
+
+    def cdc_version(self):
+        return self.cdc.version(self.name) if self.cdc is not None else None
+
     def scan(self, columns: Sequence[str], ctx) -> Batch:
         ver = None
         if self.cdc is not None:
             self.cdc.maybe_poll(self.name, self.poll_interval_s)
             ver = self.cdc.version(self.name)
         out, n, missing = {}, None, []
+        keys = getattr(ctx, "cache_keys", None)
         for c in columns:
+            if keys is not None:
+                keys.append(self._key(c, ctx))
             hit = self.cache.get(self._key(c, ctx), ver)
             if hit is None:
                 missing.append(c)

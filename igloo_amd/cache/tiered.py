@@ -143,6 +143,14 @@ class TieredCache:
             log.info("cache miss %s", key)
             return None
 
+    def touch(self, keys) -> None:
+        """Mark HBM entries as just used (a query graph replay reads them
+        without going through ``get``)."""
+        with self._lock:
+            for k in keys:
+                if k in self._hbm:
+                    self._hbm.move_to_end(k)
+
     def invalidate(self, prefix: str = "") -> int:
         with self._lock:
             keys = [k for k in list(self._hbm) + list(self._host) + list(self._disk) if k.startswith(prefix)]

@@ -41,7 +41,9 @@ PLAN_CACHE_SIZE = 256
 #: replay the host readbacks of repeated queries over unchanged data (see
 #: QueryEngine._execute_speculative)
 SPECULATE = os.environ.get("IGLOO_SPECULATE", "1") == "1"
-SPMD_SPECULATE = os.environ.get("IGLOO_SPMD_SPECULATE", "0") == "1"
+SPMD_SPECULATE = os.environ.get("IGLOO_SPMD_SPECULATE", "1") == "1"
+#: SPMD query graphs (collectives captured with the kernels; RCCL only)
+SPMD_GRAPHS = os.environ.get("IGLOO_SPMD_GRAPHS", "1") == "1"
 
 log = get_logger("engine")
 
@@ -150,6 +152,17 @@ class QueryEngine:
         self.cache = TieredCache(CacheConfig(hbm_bytes=int(hbm), host_bytes=int(host), disk_path=cache_dir,
                                              device=str(self.device)))
         self.cdc = CdcManager(self.cache)
+        # device bytes the cache tier's resident columns and the query graphs'
+        # private memory pools may hold together (exec/graphs.py); past it the
+        # least recently replayed graphs are dropped (their pools return to
+        # the allocator). The rest of HBM is query working memory.
+        gb = (config or {}).get("hbm_budget_gb", os.environ.get("IGLOO_HBM_BUDGET_GB"))
+        self.hbm_budget = int(float(gb) * 2**30) if gb not in (None, "") else (int(0.9 * cap) if cap else None)
+        self._graphs: "collections.OrderedDict[int, dict]" = collections.OrderedDict()   # LRU of states with graphs
+        self.graph_bytes = 0
+        self.graph_stats = {"evicted": 0, "dropped_stale": 0}
+        self._spec_current: Dict[Any, Any] = {}     # plan key -> its live speculation key
+        self._query_sources: Dict[Any, list] = {}   # plan key -> cached table sources it reads
 
     # -------------------------------------------------------------- catalog
     def register_table(self, name: str, table: Union[TableSource, pa.Table, Batch, Dict[str, Column]],
@@ -351,56 +364,104 @@ class QueryEngine:
         sequence (values that differed between them are read back for real
         every time); a replay that leaves the recorded sequence continues with
         real readbacks and needs re-confirming; a value mismatch re-executes the query with
-        real readbacks (after two, the query is no longer replayed)."""
+        real readbacks (after two, the query is no longer replayed).
+
+        SPMD ranks (one per GPU) speculate too: replaying a readback changes
+        only when the host waits, never which collectives a rank issues, so
+        ranks in different modes stay aligned. Every rank joins one tiny
+        all-reduce after each execution (validation agreement) and, when
+        graphs are possible, one before it (all ranks replay graphs, or none).
+        Graphs with collectives inside need a device transport (RCCL): a gloo
+        (host-staged) group never captures."""
         from .ops import _lib
-        # SPMD ranks replay only with IGLOO_SPMD_SPECULATE=1: a 2-rank rehearsal
-        # (shared GPU, gloo) once replayed values that passed validation yet
-        # changed a result (Q16, whose hash-slot group ids were then
-        # non-deterministic; fixed since, ops/hashing.py group_ids) and faulted
-        spmd = self.comm is not None and self.comm.world_size > 1
+        spmd = self.comm is not None and self.comm.spmd
         if not (SPECULATE and key is not None and self.device.type == "cuda" and (not spmd or SPMD_SPECULATE)):
             return self._execute_plan(plan, ctx), None, None
         comm = self.comm if spmd else None
+        graphs_on = _graphs.GRAPHS and (comm is None or (comm.backend == "nccl" and SPMD_GRAPHS))
 
         def agreed(ok: bool) -> bool:
             # SPMD ranks decide together (every rank joins this collective after
             # every speculative-capable execution, so the sequences stay aligned)
             return ok if comm is None else comm.allreduce_ints([0 if ok else 1])[0] == 0
+        # CDC: a graph replay never reaches CachedTable.scan (where scans poll
+        # their source), so the probes of the tables this query read last time
+        # run here, rate-limited the same way; a changed source invalidates its
+        # cache entries and moves the cache generation, i.e. the key below
+        srcs = self._query_sources.get(key, ())
+        for s in srcs:
+            try:
+                s.poll()
+            except Exception as e:  # noqa: BLE001 - a failing probe keeps the cached data
+                log.warning("cdc poll of %s failed: %s", getattr(s, "name", s), e)
         # (a generated kernel that becomes available changes the code path and
         # so the readback call sites: the replay diverges, stays correct, and the
         # new sequence is confirmed by the next execution)
-        skey = (key, self.catalog.version, self.cache.generation)
+        skey = (key, self.catalog.version, self.cache.generation, tuple(s.cdc_version() for s in srcs))
         st = self._spec.get(skey)
         if st is None:
+            old = self._spec_current.pop(key, None)
+            if old is not None:
+                # the data this query's recording (and graph) was built on changed
+                ost = self._spec.pop(old, None)
+                if ost is not None and ost.get("graph") is not None:
+                    self.graph_stats["dropped_stale"] += 1
+                    self._set_graph(ost, None)
             if len(self._spec) >= PLAN_CACHE_SIZE:
-                self._spec.pop(next(iter(self._spec)))
+                self._set_graph(self._spec.pop(next(iter(self._spec))), None)
             st = self._spec[skey] = {"log": None, "candidate": None, "fails": 0, "graph": None,
-                                     "capture_next": False, "digest": None, "graph_aborts": 0}
+                                     "capture_next": False, "digest": None, "graph_aborts": 0,
+                                     "cache_keys": ()}
+            self._spec_current[key] = skey
         replay = st["log"] is not None and st["fails"] < 2
-        if _graphs.GRAPHS and comm is None and not self.graphs_disabled and replay and st["fails"] == 0 \
-                and st["graph_aborts"] < 2:
+        mode = "eager"
+        if graphs_on and not self.graphs_disabled and replay and st["fails"] == 0 and st["graph_aborts"] < 2:
             g = st["graph"]
             if g is not None and not g.current():
                 # the generated-kernel set changed: the recording diverges from
                 # here, and a new graph is captured once a replay completes again
-                st["graph"] = g = None
-            if g is None and st["capture_next"] and st["digest"] is not None \
-                    and _jit.generation() is not None:
-                st["capture_next"] = False
-                with _trace.Range("graph.capture"):
-                    g = st["graph"] = _graphs.capture(self, plan, st["log"], self.make_context)
-                if g is None:
-                    st["graph_aborts"] += 1
+                self._set_graph(st, None)
+                g = None
             if g is not None:
-                if g.replay(ctx):
-                    return g.batch, "graph", st
-                # a replayed value no longer matches the device: eager, real readbacks
-                st["graph"] = None
-                st["fails"] += 1
-                st["log"] = st["candidate"] = None
-                replay = False
-                ctx = self.make_context()
-                log.warning("query graph: replayed values did not match the device; re-executing")
+                mode = "graph"
+            elif st["capture_next"] and st["digest"] is not None and _jit.generation() is not None:
+                mode = "capture"
+        if comm is not None and graphs_on:
+            # all ranks run graphs or none: [ranks staying eager, ranks capturing]
+            n_eager, n_cap = comm.allreduce_ints([int(mode == "eager"), int(mode == "capture")])
+            if n_eager:
+                mode = "eager"
+            elif n_cap:
+                ok = True
+                if mode == "capture":
+                    ok = self._capture(st, plan)
+                if not agreed(ok):
+                    self._set_graph(st, None)
+                    mode = "eager"
+                else:
+                    # some rank replays a fresh graph for the first time: every
+                    # rank joins the digest agreement in _check_graph
+                    mode = "graph"
+                    st["check_all"] = True
+        elif mode == "capture":
+            mode = "graph" if self._capture(st, plan) else "eager"
+        if mode == "graph":
+            g = st["graph"]
+            ok = g.replay(ctx)
+            if comm is not None:
+                comm.calls += g.comm_calls
+                comm.bytes_sent += g.comm_bytes
+            if agreed(ok):
+                self._touch_graph(st)
+                return g.batch, "graph", st
+            # a replayed value no longer matches the device (on some rank):
+            # eager, real readbacks
+            self._set_graph(st, None)
+            st["fails"] += 1
+            st["log"] = st["candidate"] = None
+            replay = False
+            ctx = self.make_context()
+            log.warning("query graph: replayed values did not match the device; re-executing")
         for attempt in range(3):
             sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
             _lib.set_speculation(sp)
@@ -419,38 +480,104 @@ class QueryEngine:
             replay = False
             ctx = self.make_context()
             log.warning("speculative readbacks did not match the device; re-executing")
+        self._query_sources[key] = [s for s in ctx.sources if hasattr(s, "poll")]
+        st["cache_keys"] = tuple(dict.fromkeys(ctx.cache_keys))
+        can_graph = graphs_on and st["fails"] == 0 and st["graph"] is None and st["graph_aborts"] < 2
         if sp.mode == "replay":
             if not sp.complete:
                 # the call sequence changed: this run's own sequence must be
                 # confirmed by the next execution before it is replayed
                 st["log"], st["candidate"] = None, sp.fresh
-            elif _graphs.GRAPHS and comm is None and st["fails"] == 0 and st["graph"] is None \
-                    and st["graph_aborts"] < 2:
+            elif can_graph:
                 st["capture_next"] = True    # _check_graph keeps this result's digest
             return batch, "replayed" if sp.complete else "partial", st
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
-        if st["log"] is not None and _graphs.GRAPHS and comm is None and st["fails"] == 0 and st["graph"] is None \
-                and st["graph_aborts"] < 2:
+        if st["log"] is not None and can_graph:
             # a confirmed recording: the next execution captures it straight
             # away (its graph is checked against this run's result digest)
             st["capture_next"] = True
         return batch, "recorded", st
 
+    def _capture(self, st: dict, plan: Plan) -> bool:
+        """Capture ``plan`` under a replay of ``st``'s recording into a query graph."""
+        st["capture_next"] = False
+        c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
+        with _trace.Range("graph.capture"):
+            g = _graphs.capture(self, plan, st["log"], self.make_context)
+        if g is None:
+            st["graph_aborts"] += 1
+            return False
+        if self.comm is not None:
+            # collectives recorded into the graph (counted again on every replay)
+            g.comm_calls, g.comm_bytes = self.comm.calls - c0[0], self.comm.bytes_sent - c0[1]
+            self.comm.calls, self.comm.bytes_sent = c0
+        self._set_graph(st, g)
+        return True
+
+    # ------------------------------------------------------- graph memory
+    def _set_graph(self, st: dict, g) -> None:
+        """Attach (or drop, ``g=None``) ``st``'s query graph, keeping the
+        graphs' pool bytes accounted against ``hbm_budget``."""
+        old = st.get("graph")
+        if old is not None:
+            self._graphs.pop(id(st), None)
+            self.graph_bytes -= old.nbytes
+        st["graph"] = g
+        if g is not None:
+            self._graphs[id(st)] = st
+            self.graph_bytes += g.nbytes
+            self.enforce_graph_budget(keep=st)
+
+    def _touch_graph(self, st: dict) -> None:
+        if id(st) in self._graphs:
+            self._graphs.move_to_end(id(st))
+        if st["cache_keys"]:
+            self.cache.touch(st["cache_keys"])   # the replay read these resident columns
+
+    def enforce_graph_budget(self, keep: Optional[dict] = None) -> int:
+        """Drop least recently replayed graphs while the cache tier's resident
+        bytes plus the graphs' pool bytes exceed ``hbm_budget``; returns how
+        many were dropped. A dropped graph's query runs eagerly (replayed
+        readbacks) and may be captured again later."""
+        if self.hbm_budget is None or not self._graphs:
+            return 0
+        n = 0
+        used = self.cache.hbm_used
+        while self._graphs and used + self.graph_bytes > self.hbm_budget:
+            sid = next(iter(self._graphs))
+            st = self._graphs[sid]
+            if st is keep:
+                if len(self._graphs) == 1:
+                    break
+                self._graphs.move_to_end(sid)
+                continue
+            self._set_graph(st, None)
+            self.graph_stats["evicted"] += 1
+            n += 1
+        if n and self.device.type == "cuda":
+            torch.cuda.empty_cache()      # the dropped graphs' private pools
+        return n
+
     def _check_graph(self, st: dict, spec, table: pa.Table, plan: Plan, names, ctx) -> pa.Table:
         """Digest bookkeeping around query graphs (exec/graphs.py): the eager
         result before a capture is digested; the graph's first result must
         match it, otherwise the query is never captured again and this result
-        is recomputed eagerly."""
+        is recomputed eagerly (SPMD ranks agree on it: their results are
+        replicated, and all of them are on their first replay together)."""
         if spec in ("replayed", "recorded") and st["capture_next"]:
             st["digest"] = digest(table)
         elif spec == "graph":
             g = st["graph"]
-            if not g.checked:
-                if digest(table) != st["digest"]:
+            check_all = st.pop("check_all", False)
+            if not g.checked or check_all:
+                ok = g.checked or digest(table) == st["digest"]
+                if check_all:
+                    ok = self.comm.allreduce_ints([0 if ok else 1])[0] == 0
+                if not ok:
                     log.warning("query graph result differs from the eager execution; graph dropped")
                     _graphs.STATS["failed"] += 1
-                    st["graph"] = None
+                    self._set_graph(st, None)
                     st["graph_aborts"] = 2
                     ctx.__init__(self, self.device, self.comm, ctx.analyze)
                     return self._to_arrow(self._execute_plan(plan, ctx), plan.schema, names)
@@ -467,7 +594,7 @@ class QueryEngine:
         ctx = ctx or self.make_context()
         node = create_physical_plan(plan)
         out = node.execute(ctx)
-        if self.comm is not None and self.comm.world_size > 1:
+        if self.comm is not None and self.comm.spmd:
             from .parallel.exchange import gather_all
             out = gather_all(out, ctx)
         return out
@@ -508,7 +635,7 @@ class QueryEngine:
             if ctx.spill["joins"]:
                 txt += (f"\nspill: {ctx.spill['joins']} partitioned join(s), {ctx.spill['partitions']} partitions, "
                         f"{ctx.spill['bytes']} bytes staged in host memory (device budget {ctx.budget} bytes)")
-            if self.comm is not None and self.comm.world_size > 1:
+            if self.comm is not None and self.comm.spmd:
                 txt += (f"\nexchange: {self.comm.calls - c0[0]} collectives, "
                         f"{self.comm.bytes_sent - c0[1]} bytes sent by this rank")
             if ctx.spans:

@@ -31,10 +31,17 @@ but the launch sequence. What keeps a graph valid:
   one-time derived-structure build, a generated-kernel load, a host spill. The
   query then stays eager.
 
-Memory: all graphs of an engine share one private pool (``torch.cuda.graph_pool_handle``).
-Graphs replay one at a time on one stream, and each writes its intermediates before
-reading them, so a later capture may reuse blocks an earlier one freed. The pool holds
-about the largest query's working set plus every graph's result columns.
+Memory: each graph owns a private pool (its whole working set stays reserved
+between replays). The capture measures the pool's bytes and the engine charges
+them, together with the cache tier's resident columns, against its HBM budget
+(engine.py ``enforce_graph_budget``): past it, the least recently replayed
+graphs are dropped and their pools freed. ``IGLOO_GRAPH_SHARED_POOL=1`` shares
+one pool between all graphs of an engine instead.
+
+CDC: a replay never reaches ``CachedTable.scan``, so the engine polls the CDC
+probes of the query's tables before every replay (same rate limit); a changed
+source moves the cache generation and so the key, and the stale graph is
+dropped.
 
 The reference has no GPU execution and so nothing comparable; its engine
 rebuilds DataFusion physical plans per query (reference
@@ -80,10 +87,14 @@ class QueryGraph:
     """One captured query: the graph, its static result batch and the device
     mismatch counter of its replayed values."""
 
-    __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp")
+    __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp",
+                 "nbytes", "comm_calls", "comm_bytes")
 
-    def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None):
+    def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None, nbytes=0):
         self.sp = sp                   # the capture's speculation (sites + device values, for reports)
+        self.nbytes = nbytes           # device bytes of the graph's private memory pool
+        self.comm_calls = 0            # collectives inside the graph (SPMD)
+        self.comm_bytes = 0
         self.graph = graph
         self.batch = batch
         self.bad = bad
@@ -133,6 +144,9 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     s.wait_stream(cur)
     g = torch.cuda.CUDAGraph()
     batch = bad = None
+    # the graph's private pool is what capture adds to the reserved bytes
+    # (engine.py charges it against the HBM budget)
+    reserved0 = torch.cuda.memory_reserved(dev)
     _lib.set_speculation(sp)
     _lib.set_capturing(True)
     # torch raises before any synchronizing call (blocking copy, .item(),
@@ -184,4 +198,5 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         os.makedirs(dump, exist_ok=True)
         g.debug_dump(os.path.join(dump, f"graph_{STATS['captured']}.dot"))
     STATS["captured"] += 1
-    return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp)
+    nbytes = max(0, torch.cuda.memory_reserved(dev) - reserved0)
+    return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp, nbytes)

@@ -69,10 +69,16 @@ class ExecContext:
         # searches into a resident column subtract the rows they skipped)
         self.rows_scanned = 0
         self._scanned_sources: set = set()
+        # table sources this query read (engine.py polls their CDC probes before
+        # replaying the query's graph) and the cache-tier keys it was served
+        # from (a graph replay refreshes their LRU position)
+        self.sources: list = []
+        self.cache_keys: list = []
 
     def note_scan(self, source, rows: int) -> None:
         if id(source) not in self._scanned_sources:
             self._scanned_sources.add(id(source))
+            self.sources.append(source)
             self.rows_scanned += rows
 
     def note_partial_read(self, t: torch.Tensor, rows_read: int) -> None:
@@ -95,12 +101,18 @@ class ExecContext:
     def world(self) -> int:
         return self.comm.world_size if self.comm is not None else 1
 
+    @property
+    def spmd(self) -> bool:
+        """Rows are spread over ranks: exchanges run (also a forced world of
+        one, parallel/comm.py ``force_spmd``, which runs every collective)."""
+        return self.comm is not None and self.comm.spmd
+
     def scalar_subquery(self, e) -> object:
         key = id(e.plan)
         if key not in self._subq:
             from .planner import execute_plan
             b = execute_plan(e.plan, self)
-            if self.world > 1:
+            if self.spmd:
                 from ..parallel.exchange import gather_all
                 b = gather_all(b, self)
             if b.num_rows > 1:
@@ -274,7 +286,7 @@ class ScanExec(ExecNode):
         ctx.note_scan(s.source, raw.num_rows)
         cols = {cid: raw.columns[by_cid[cid].name] for cid in sorted(need)}
         dist = None
-        if ctx.world > 1:
+        if ctx.spmd:
             if getattr(s.source, "replicated", False):
                 dist = ("replicated",)
             elif getattr(s.source, "partitioned_by", None):
@@ -304,7 +316,7 @@ class ScanExec(ExecNode):
                     idx = mask_to_indices(m)
                 hit = ctx.scan_cache[key] = (idx, {})
             idx, taken_by_name = hit
-            if self.late_ok and LATE_SCAN and ctx.world == 1 and ctx.device.type == "cuda":
+            if self.late_ok and LATE_SCAN and not ctx.spmd and ctx.device.type == "cuda":
                 # index form: the join gathers its key columns now and payload
                 # columns only for the rows that survive it
                 src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
@@ -384,7 +396,7 @@ class ValuesExec(ExecNode):
                 e = ctx.evaluator.eval(r[j], Batch({}, 1))
                 vals.append(e.value if isinstance(e, Scalar) else e.to_pylist()[0])
             cols[ci.cid] = _column_from_values(vals, ci.dtype, ctx.device)
-        return Batch(cols, n, ("replicated",) if ctx.world > 1 else None)
+        return Batch(cols, n, ("replicated",) if ctx.spmd else None)
 
 
 def _column_from_values(vals, dtype, device) -> Column:
@@ -530,7 +542,7 @@ class HashJoinExec(ExecNode):
         if j.kind in ("inner", "left", "semi") and j.on:
             push_key_filter(self.children[1], j.on, lb, ctx)
         rb = self.children[1].execute(ctx)
-        if ctx.world > 1:
+        if ctx.spmd:
             from ..parallel.exchange import prepare_join
             lb, rb = prepare_join(lb, rb, j, ctx)
             out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
@@ -586,7 +598,7 @@ def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
         if a.dtype.is_string or gexpr.dtype.is_string:
             continue
         lcol = ctx.evaluator.column(a, lb)
-        if ctx.world > 1 and lb.dist != ("replicated",):
+        if ctx.spmd and lb.dist != ("replicated",):
             from ..parallel.exchange import gather_all
             lcol = gather_all(Batch({0: lcol}, lb.num_rows, lb.dist), ctx).columns[0]
         agg.runtime_filters.append((gexpr, lcol))
@@ -1320,7 +1332,7 @@ class MultiJoinExec(ExecNode):
             lb = lb.materialize()
         elif isinstance(lb, _LazyScanBatch):
             lb = Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
-        if ctx.world > 1:
+        if ctx.spmd:
             from ..parallel.exchange import prepare_join
             j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
             lb, rb = prepare_join(lb, rb, j, ctx)
@@ -1354,7 +1366,7 @@ class MultiJoinExec(ExecNode):
                 deferred.append((sp, rb))
         conds = list(lg.conds)
         while len(rels) > 1:
-            if ctx.world > 1:
+            if ctx.spmd:
                 self._prefetch_ndv(rels, conds, ctx)
             best = None
             for i in range(len(rels)):
@@ -1380,14 +1392,14 @@ class MultiJoinExec(ExecNode):
             on = [(kk[0], kk[1]) for kk in keys]
             la, lb_ = a["batch"], b["batch"]
             out_dist = None
-            if ctx.world > 1:
+            if ctx.spmd:
                 from ..parallel.exchange import prepare_join
                 fake = L.Join(None, None, "inner", on)  # type: ignore[arg-type]
                 la, lb_ = prepare_join(la, lb_, fake, ctx, rows=(a["grows"], b["grows"]))
                 out_dist = la.out_dist
             over = ctx.budget is not None and \
                 JOIN_MEM_FACTOR * (_batch_bytes(la) + _batch_bytes(lb_)) > ctx.budget
-            if on and ctx.world == 1 and not over:
+            if on and not ctx.spmd and not over:
                 out = self._late_join(la, lb_, on, and_all(resid), ctx)
             else:
                 if isinstance(la, LateBatch):
@@ -1513,11 +1525,11 @@ class MultiJoinExec(ExecNode):
             b = rel["batch"]
             with ctx.span("multijoin.ndv"):
                 cached = None
-                if ctx.world == 1 and b.num_rows:
+                if not ctx.spmd and b.num_rows:
                     c = ctx.evaluator.column(e, b)
                     # resident table columns: the sketch of the same tensor is reused across queries
                     cached = getattr(c.data, "_igloo_ndv", None) if c.valid is None else None
-                base = getattr(c.data, "_igloo_base", None) if cached is None and ctx.world == 1 and \
+                base = getattr(c.data, "_igloo_base", None) if cached is None and not ctx.spmd and \
                     b.num_rows and c.valid is None else None
                 if cached is not None:
                     g = cached
@@ -1530,7 +1542,7 @@ class MultiJoinExec(ExecNode):
                         regs = H.hll_sketch(k)
                     else:
                         regs = torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device)
-                    if ctx.world > 1:
+                    if ctx.spmd:
                         # every rank takes part, even with an empty slice (collective order must match)
                         regs = ctx.comm.allreduce_max_tensor(regs)
                     if b.num_rows and c.valid is None and getattr(c.data, "_igloo_resident", False):
@@ -1544,9 +1556,9 @@ class MultiJoinExec(ExecNode):
                         c = ctx.evaluator.column(e, b)
                         k, _ = group_key_tensor(c)
                         g = H.ndv(k)
-                    if ctx.world > 1:
+                    if ctx.spmd:
                         g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
-                if cached is None and ctx.world == 1 and b.num_rows and c.valid is None and not c.is_dict:
+                if cached is None and not ctx.spmd and b.num_rows and c.valid is None and not c.is_dict:
                     try:
                         c.data._igloo_ndv = g
                     except (AttributeError, RuntimeError):
@@ -1578,13 +1590,13 @@ def _derived_ndv(base, n: int) -> int:
 
 
 def _global_rows(b: Batch, ctx) -> int:
-    if ctx.world > 1:
+    if ctx.spmd:
         return ctx.comm.allreduce_int(b.num_rows)
     return b.num_rows
 
 
 def _global_rows_many(bs: Sequence[Batch], ctx) -> List[int]:
-    if ctx.world > 1 and bs:
+    if ctx.spmd and bs:
         return ctx.comm.allreduce_ints([b.num_rows for b in bs])
     return [b.num_rows for b in bs]
 
@@ -1623,7 +1635,7 @@ class HashAggExec(ExecNode):
         (150M-row join output at SF100). Exact: a left row with k partners
         contributes k to COUNT(x) exactly when x is non-NULL on each partner."""
         lg, child = self.logical, self.children[0]
-        if ctx.world > 1 or not isinstance(child, HashJoinExec) or len(lg.groups) != 1 or not lg.aggs:
+        if ctx.spmd or not isinstance(child, HashJoinExec) or len(lg.groups) != 1 or not lg.aggs:
             return None
         j = child.logical
         if j.kind != "left" or j.residual is not None or len(j.on) != 1:
@@ -1696,7 +1708,7 @@ class HashAggExec(ExecNode):
 
             def local(groups, aggs, raw=raw, pred=pred):
                 return fused.fused_scan_aggregate(groups, aggs, raw, pred, ctx)
-            if ctx.world == 1:
+            if not ctx.spmd:
                 out = local(lg.groups, lg.aggs)
                 if out is not None:
                     return out
@@ -1706,7 +1718,7 @@ class HashAggExec(ExecNode):
         if self.runtime_filters:
             filters, self.runtime_filters = self.runtime_filters, []
             b = apply_key_filters(b, filters, ctx)
-        if ctx.world > 1:
+        if ctx.spmd:
             from ..parallel.exchange import distributed_aggregate
             return distributed_aggregate(lg, b, ctx, local=local)
         return aggregate(lg.groups, lg.aggs, b, ctx)
@@ -2028,7 +2040,7 @@ class SortExec(ExecNode):
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
         fetch = self.logical.fetch
-        if ctx.world > 1 and b.dist != ("replicated",):
+        if ctx.spmd and b.dist != ("replicated",):
             from ..parallel.exchange import gather_all
             if fetch is not None:
                 # distributed ORDER BY ... LIMIT k: local top-k first, then only
@@ -2091,7 +2103,7 @@ class LimitExec(ExecNode):
 
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
-        if ctx.world > 1 and b.dist != ("replicated",):
+        if ctx.spmd and b.dist != ("replicated",):
             from ..parallel.exchange import gather_all
             if self.logical.limit is not None:
                 # any offset+limit rows of each rank can make the answer
@@ -2122,7 +2134,7 @@ class UnionExec(ExecNode):
             b = ch.execute(ctx)
             outs.append(Batch({s.cid: b.columns[c.cid] for s, c in zip(self.logical.schema, p.schema)}, b.num_rows,
                               b.dist))
-        if ctx.world > 1:
+        if ctx.spmd:
             reps = [o.dist == ("replicated",) for o in outs]
             if all(reps):
                 out = concat_batches(outs)

@@ -29,9 +29,15 @@ log = get_logger("comm")
 
 
 class Communicator:
-    def __init__(self, rank: int, world_size: int, device, group=None, backend: str = "nccl"):
+    def __init__(self, rank: int, world_size: int, device, group=None, backend: str = "nccl",
+                 force_spmd: bool = False):
         self.rank = rank
         self.world_size = world_size
+        #: rows are spread over ranks and exchanges run. ``force_spmd`` keeps it
+        #: on for a world of one: every exchange and collective then really runs
+        #: (RCCL / gloo with one rank) — the single-GPU rehearsal of the
+        #: multi-GPU code path, including collectives inside query graphs
+        self.spmd = world_size > 1 or force_spmd
         self.device = torch.device(device)
         self.group = group
         self.backend = backend
@@ -43,8 +49,11 @@ class Communicator:
 
     # ------------------------------------------------------------- lifecycle
     @staticmethod
-    def init(backend: Optional[str] = None, device=None, timeout_s: float = 600.0) -> "Communicator":
-        """Initialise from torchrun-style env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
+    def init(backend: Optional[str] = None, device=None, timeout_s: float = 600.0,
+             force_spmd: Optional[bool] = None) -> "Communicator":
+        """Initialise from torchrun-style env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT).
+        ``force_spmd`` (default: env IGLOO_FORCE_SPMD=1) runs the SPMD path
+        even for a world of one."""
         rank = int(os.environ.get("RANK", "0"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -62,7 +71,9 @@ class Communicator:
                     kw["device_id"] = device
             dist.init_process_group(backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
-        return Communicator(dist.get_rank(), dist.get_world_size(), device, None, backend)
+        if force_spmd is None:
+            force_spmd = os.environ.get("IGLOO_FORCE_SPMD") == "1"
+        return Communicator(dist.get_rank(), dist.get_world_size(), device, None, backend, force_spmd)
 
     def abort(self):
         """Tear the data communicator down without a collective (a peer died):
@@ -93,14 +104,14 @@ class Communicator:
     def barrier(self):
         if faults.ACTIVE:
             faults.check("comm_timeout", "barrier")
-        if self.world_size > 1:
+        if self.spmd:
             self.calls += 1
             dist.barrier(group=self.group)
 
     def allreduce_int(self, x: int) -> int:
         if faults.ACTIVE:
             faults.check("comm_timeout", "allreduce_int")
-        if self.world_size == 1:
+        if not self.spmd:
             return int(x)
         t = self._t([int(x)])
         self.calls += 1
@@ -110,7 +121,7 @@ class Communicator:
     def allreduce_ints(self, xs: Sequence[int]) -> List[int]:
         if faults.ACTIVE:
             faults.check("comm_timeout", "allreduce_ints")
-        if self.world_size == 1:
+        if not self.spmd:
             return [int(x) for x in xs]
         t = self._t([int(x) for x in xs])
         self.calls += 1
@@ -120,7 +131,7 @@ class Communicator:
     def allreduce_max_float(self, x: float) -> float:
         if faults.ACTIVE:
             faults.check("comm_timeout", "allreduce_max_float")
-        if self.world_size == 1:
+        if not self.spmd:
             return float(x)
         t = self._t([float(x)], torch.float64)
         self.calls += 1
@@ -131,7 +142,7 @@ class Communicator:
         """Element-wise max over ranks (in a 32-bit copy: portable across backends)."""
         if faults.ACTIVE:
             faults.check("comm_timeout", "allreduce_max_tensor")
-        if self.world_size == 1:
+        if not self.spmd:
             return t
         w = t.to(device=self.wire, dtype=torch.int32)
         self.calls += 1
@@ -142,7 +153,7 @@ class Communicator:
         """Element-wise SUM / MIN / MAX over ranks of an int64 / float64 tensor."""
         if faults.ACTIVE:
             faults.check("comm_timeout", "allreduce_tensor")
-        if self.world_size == 1:
+        if not self.spmd:
             return t
         w = t.contiguous().to(self.wire)
         if w is t:
@@ -158,7 +169,7 @@ class Communicator:
         if faults.ACTIVE:
             faults.check("comm_timeout", "allgather_ints")
         k = len(xs)
-        if self.world_size == 1:
+        if not self.spmd:
             return [list(map(int, xs))]
         t = self._t([int(x) for x in xs])
         out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.wire)
@@ -170,7 +181,7 @@ class Communicator:
     def allgather_object(self, obj) -> list:
         if faults.ACTIVE:
             faults.check("comm_timeout", "allgather_object")
-        if self.world_size == 1:
+        if not self.spmd:
             return [obj]
         out = [None] * self.world_size
         self.calls += 1
@@ -183,7 +194,7 @@ class Communicator:
         if faults.ACTIVE:
             faults.check("comm_timeout", "all_to_all_v")
         W = self.world_size
-        if W == 1:
+        if not self.spmd:
             return t, [t.shape[0]]
         if recv_counts is None:
             m = self.all_to_all_counts(send_counts)
@@ -218,7 +229,7 @@ class Communicator:
             faults.check("comm_timeout", "all_to_all_counts")
         W = self.world_size
         k = len(rows[0]) if rows else 0
-        if W == 1:
+        if not self.spmd:
             return [list(map(int, r)) for r in rows]
         s = self._t([int(x) for r in rows for x in r])
         r = torch.empty(W * k, dtype=torch.int64, device=self.wire)
@@ -235,7 +246,7 @@ class Communicator:
         if faults.ACTIVE:
             faults.check("comm_timeout", "all_gather_v")
         W = self.world_size
-        if W == 1:
+        if not self.spmd:
             return t, [t.shape[0]]
         if counts is None:
             counts = [c[0] for c in self.allgather_ints([t.shape[0]])]
@@ -280,7 +291,7 @@ class Communicator:
     def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if faults.ACTIVE:
             faults.check("comm_timeout", "broadcast_tensor")
-        if self.world_size > 1:
+        if self.spmd:
             w = t.to(self.wire)
             self.calls += 1
             dist.broadcast(w, src, group=self.group)

@@ -297,7 +297,7 @@ def gather_all(b: Batch, ctx) -> Batch:
     """Every rank receives the concatenation of all ranks' rows (one packed
     all-gather-v for the fixed-width columns)."""
     comm = ctx.comm
-    if comm is None or comm.world_size == 1 or dist_of(b) == REPLICATED:
+    if comm is None or not comm.spmd or dist_of(b) == REPLICATED:
         return b
     keys = list(b.columns)
     # string byte counts ride along in the preamble (-1: not a plain string

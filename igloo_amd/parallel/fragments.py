@@ -289,7 +289,7 @@ def execute_fragmented(engine, sql: str, workers: Sequence[str] = ("all-ranks",)
     plan, names = engine.logical_plan(sql)
     frags = DistributedPlanner(workers).plan(plan)
     batch = FragmentScheduler(local_runner(engine)).execute(frags)
-    if engine.comm is not None and engine.comm.world_size > 1:
+    if engine.comm is not None and engine.comm.spmd:
         from .exchange import gather_all
         batch = gather_all(batch, engine.make_context())
     return engine._to_arrow(batch, plan.schema, names), frags
@@ -338,21 +338,21 @@ def run_encoded_fragment(engine, payload: bytes):
     refs = {p.fragment_id: p for p in L.walk_plan(plan) if isinstance(p, FragmentRef)}
     off = 4 + hlen
     inputs = {}
-    world = engine.comm.world_size if engine.comm is not None else 1
+    spmd = engine.comm is not None and engine.comm.spmd
     for fid, n in head["inputs"]:
         t = pa.ipc.open_stream(payload[off:off + n]).read_all()
         off += n
         ref = refs[fid]
         b = Batch.from_arrow(t, device=engine.device)
         cols = {ci.cid: b.columns[name] for ci, name in zip(ref.schema, t.column_names)}
-        inputs[fid] = Batch(cols, t.num_rows, ("replicated",) if world > 1 else None)
+        inputs[fid] = Batch(cols, t.num_rows, ("replicated",) if spmd else None)
     saved = dict(engine.session)
     engine.session.update(head.get("session_config") or {})
     try:
         ctx = engine.make_context()
         ctx.fragment_inputs = inputs
         out = create_physical_plan(plan).execute(ctx)
-        if world > 1:
+        if spmd:
             from .exchange import gather_all
             out = gather_all(out, ctx)
         return engine._to_arrow(out, plan.schema, [f"c{c.cid}" for c in plan.schema])

@@ -1,0 +1,92 @@
+"""Single-GPU rehearsal of the multi-GPU (SPMD) path: a world of ONE rank with
+``force_spmd`` runs every exchange and every collective for real — RCCL on a
+GPU (``--backend nccl``), gloo on the CPU — so the code the 2/4/8-GPU runs take
+(shuffles, broadcasts, two-phase aggregation, speculation agreement, query
+graphs with collectives inside) executes on one device.
+
+Reports per query: collectives issued, execution mode (R/P/G = recorded /
+replayed / graph) and time; checks every result against a plain single-rank
+engine over the same data.
+
+    python scripts/spmd_world1.py --sf 0.1 --device cuda:0 --backend nccl --runs 6
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf", type=float, default=0.01)
+    ap.add_argument("--device", default="cpu")
+    ap.add_argument("--backend", default=None)
+    ap.add_argument("--runs", type=int, default=4)
+    ap.add_argument("--queries", default="1-22")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    import torch
+    import igloo_amd as ig
+    from igloo_amd.models.tpch import datagen, queries
+    from igloo_amd.parallel.comm import Communicator
+    from igloo_amd.utils.digest import digest
+    qs = []
+    for part in a.queries.split(","):
+        lo, _, hi = part.partition("-")
+        qs += list(range(int(lo), int(hi or lo) + 1))
+    backend = a.backend or ("nccl" if a.device.startswith("cuda") else "gloo")
+    comm = Communicator.init(backend=backend, device=a.device, force_spmd=True, timeout_s=300)
+    e = ig.QueryEngine(device=a.device, comm=comm)
+    ref = ig.QueryEngine(device=a.device)
+    tabs = datagen.generate(a.sf, a.device, 0, 1)
+    for n, t in tabs.items():
+        e.register_table(n, t)
+        ref.register_table(n, t)
+    want = {q: digest(ref.sql(queries.QUERIES[q]).table) for q in qs}
+    del ref
+    out = {"backend": backend, "sf": a.sf, "queries": {}}
+    bad = []
+    for q in qs:
+        rec = []
+        for i in range(a.runs):
+            t0 = time.perf_counter()
+            r = e.sql(queries.QUERIES[q])
+            if a.device.startswith("cuda"):
+                torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            m = e.last_metrics
+            ok = digest(r.table) == want[q]
+            if not ok:
+                bad.append((q, i))
+            rec.append({"ms": round(ms, 3), "collectives": m.get("collectives"), "mode": m.get("speculation"),
+                        "ok": ok})
+        out["queries"][q] = rec
+        print(f"Q{q:02d} " + " ".join(f"{x['mode'] or '-'}:{x['collectives']}c:{x['ms']:.1f}ms{'' if x['ok'] else '!BAD'}"
+                                       for x in rec), flush=True)
+    last = [out["queries"][q][-1] for q in qs]
+    out["suite_ms_last"] = round(sum(x["ms"] for x in last), 2)
+    out["collectives_last"] = {q: out["queries"][q][-1]["collectives"] for q in qs}
+    out["mismatches"] = bad
+    from igloo_amd.exec import graphs
+    out["graphs"] = dict(graphs.STATS)
+    out["graph_errors"] = list(graphs.LAST_ERROR)[-6:]
+    print(json.dumps({k: v for k, v in out.items() if k != "queries"}), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    comm.shutdown()
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -83,3 +83,71 @@ def test_graph_recaptured_after_jit_generation_change(gpu_engine, monkeypatch):
     after = _run(e, sql, 5)
     assert {d for d, _ in after} == {runs[-1][0]}
     assert after[0][1] != "graph"
+
+
+def _until_graph(e, sql, n=8):
+    from igloo_amd.utils.digest import digest
+    seen = []
+    for _ in range(n):
+        d = digest(e.sql(sql).table)
+        seen.append((d, e.last_metrics["speculation"]))
+        if seen[-1][1] == "graph":
+            break
+    return seen
+
+
+def test_graph_replay_sees_parquet_rewrite(tmp_path):
+    """CDC under graphs: a query that has become a graph must notice a
+    rewritten source file (the replay itself never reaches the scan)."""
+    import os
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    import igloo_amd as ig
+    from igloo_amd.ops import jit
+    d = tmp_path / "t"
+    d.mkdir()
+    n = 20_000
+
+    def write(mult):
+        pq.write_table(pa.table({"k": pa.array(range(n), pa.int64()),
+                                 "v": pa.array([i * mult for i in range(n)], pa.int64())}), str(d / "a.parquet"))
+    write(1)
+    e = ig.QueryEngine(device="cuda:0")
+    e.register_parquet("t", str(d))
+    sql = "SELECT count(*) AS n, sum(v) AS s FROM t WHERE k < 5000"
+    jit.wait_all(timeout=120)
+    runs = _until_graph(e, sql)
+    assert runs[-1][1] == "graph", runs
+    assert e.query(sql).to_pylist() == [{"n": 5000, "s": sum(range(5000))}]
+    write(3)
+    st = os.stat(d / "a.parquet")
+    os.utime(d / "a.parquet", ns=(st.st_atime_ns, st.st_mtime_ns + 5_000_000_000))
+    e.cdc._last_poll.clear()          # skip the 1 s poll interval
+    assert e.query(sql).to_pylist() == [{"n": 5000, "s": 3 * sum(range(5000))}]
+    assert e.last_metrics["speculation"] != "graph"
+    assert e.graph_stats["dropped_stale"] >= 1
+    runs = _until_graph(e, sql)
+    assert runs[-1][1] == "graph", runs
+    assert e.query(sql).to_pylist() == [{"n": 5000, "s": 3 * sum(range(5000))}]
+
+
+def test_graph_pools_bounded_by_hbm_budget():
+    """Graph pools count against the engine's HBM budget: past it the least
+    recently replayed graphs are dropped, answers unchanged."""
+    import igloo_amd as ig
+    from igloo_amd.models.tpch import datagen, queries
+    from igloo_amd.ops import jit
+    from igloo_amd.utils.digest import digest
+    e = ig.QueryEngine(device="cuda:0")
+    datagen.register(e, 0.02)
+    jit.wait_all(timeout=120)
+    want = {q: digest(ig.QueryEngine(device="cuda:0", catalog=e.catalog).sql(queries.QUERIES[q]).table)
+            for q in (1, 3, 6)}
+    e.hbm_budget = 1      # every graph beyond the newest one is over budget
+    for q in (1, 3, 6, 1):
+        runs = _until_graph(e, queries.QUERIES[q])
+        assert {x for x, _ in runs} == {want[q]}, q
+        assert runs[-1][1] == "graph", (q, runs)
+        assert len(e._graphs) == 1 and e.graph_bytes == e._graphs[next(iter(e._graphs))]["graph"].nbytes
+    assert e.graph_stats["evicted"] >= 3, e.graph_stats
+    e.hbm_budget = None
