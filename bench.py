@@ -97,9 +97,18 @@ def main():
     if not a.cpu:
         torch.cuda.set_device(torch.device(device))
     comm = None
-    if world > 1:
+    # IGLOO_FORCE_SPMD=1 on one GPU: the multi-GPU code path with a world of
+    # one (every exchange and collective runs, RCCL; parallel/comm.py)
+    force_spmd = os.environ.get("IGLOO_FORCE_SPMD") == "1"
+    if world > 1 or force_spmd:
         from igloo_amd.parallel.comm import Communicator
-        comm = Communicator.init(backend="gloo" if (a.cpu or shared) else "nccl", device=device)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        comm = Communicator.init(backend="gloo" if (a.cpu or shared) else "nccl", device=device,
+                                 force_spmd=force_spmd)
+    spmd = comm is not None
 
     def barrier():
         if comm is not None:
@@ -124,10 +133,10 @@ def main():
                     files=man["files"], dataset_reused=man["reused"], compression=man["compression"])
         rows = dict(man["rows"])
         eng = ig.QueryEngine(device=device, comm=comm)
-        parquet_gen.register_dataset(eng, a.data_dir, a.sf, rank, world, lean=a.lean)
+        parquet_gen.register_dataset(eng, a.data_dir, a.sf, rank, world, lean=a.lean, spmd=spmd)
     else:
         eng = ig.QueryEngine(device=device, comm=comm)
-        tabs = datagen.generate(a.sf, device, rank, world, lean=a.lean)
+        tabs = datagen.generate(a.sf, device, rank, world, lean=a.lean, spmd=spmd)
         for name, t in tabs.items():
             eng.register_table(name, t)
         barrier()
@@ -135,6 +144,7 @@ def main():
         rows = {k: v.num_rows() for k, v in tabs.items()}
         del tabs
     if comm is not None:
+        # fact tables are partitioned over ranks; dimension tables replicated
         for k in rows:
             if parquet_gen.PARTITION_KEY[k] is not None:
                 rows[k] = comm.allreduce_int(rows[k])
@@ -257,7 +267,10 @@ def main():
             "dtype": "exact decimal(15,2) int64 fixed-point / int32 keys",
             "data": src_txt,
             "config": {"model": f"TPC-H SF{a.sf:g} queries {a.queries}", "global_batch": sum(rows.values()),
-                       "seq_len": None, "parallelism": f"dp{world}" if world > 1 else "single-gpu",
+                       "seq_len": None,
+                       "parallelism": (f"dp{world}" if world > 1 else ("spmd-world1-rehearsal" if spmd else "single-gpu")),
+                       "layout": ("fact tables (lineitem, orders) hash-partitioned by order key, dimension tables "
+                                  "replicated" if spmd else "single rank"),
                        "sf": a.sf, "queries": qs},
             "warm_s": round(step_s, 4),
             "cold_s": round(cold_s, 4),

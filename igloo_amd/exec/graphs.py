@@ -88,13 +88,14 @@ class QueryGraph:
     mismatch counter of its replayed values."""
 
     __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp",
-                 "nbytes", "comm_calls", "comm_bytes")
+                 "nbytes", "comm_calls", "comm_bytes", "keep")
 
     def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None, nbytes=0):
         self.sp = sp                   # the capture's speculation (sites + device values, for reports)
         self.nbytes = nbytes           # device bytes of the graph's private memory pool
         self.comm_calls = 0            # collectives inside the graph (SPMD)
         self.comm_bytes = 0
+        self.keep = []
         self.graph = graph
         self.batch = batch
         self.bad = bad
@@ -191,6 +192,8 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         return None
     finally:
         torch.cuda.set_sync_debug_mode(sync_mode)
+        if batch is None or bad is None:
+            _lib.capture_keepalive()       # a failed capture keeps nothing
         _lib.set_capturing(False)
         _lib.set_speculation(None)
         cur.wait_stream(s)
@@ -199,4 +202,6 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         g.debug_dump(os.path.join(dump, f"graph_{STATS['captured']}.dot"))
     STATS["captured"] += 1
     nbytes = max(0, torch.cuda.memory_reserved(dev) - reserved0)
-    return QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp, nbytes)
+    qg = QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp, nbytes)
+    qg.keep = _lib.capture_keepalive()     # pinned host buffers its copy nodes read
+    return qg

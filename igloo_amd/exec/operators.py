@@ -34,7 +34,8 @@ from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
 from ..ops import strings as S
-from ..ops._lib import check_not_capturing, launch, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
+from ..ops._lib import (check_not_capturing, device_ints, launch, ptr, stream, to_host_f64s, to_host_int,
+                       to_host_ints, unlogged)
 from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
 from ..ops.select import exclusive_scan, mask_to_indices
@@ -453,10 +454,13 @@ class ProjectExec(ExecNode):
         b = self.children[0].execute(ctx)
         cols = {}
         dist = b.dist if (b.dist is None or b.dist[0] == "replicated") else None
+        hashed = []
         for ci, e in self.logical.exprs:
             cols[ci.cid] = ctx.evaluator.column(e, b)
-            if b.dist and b.dist[0] == "hash" and isinstance(e, ColRef) and e.cid == b.dist[1]:
-                dist = ("hash", ci.cid)
+            if b.dist and b.dist[0] == "hash" and isinstance(e, ColRef) and e.cid in b.dist[1:]:
+                hashed.append(ci.cid)
+        if hashed:
+            dist = ("hash",) + tuple(hashed)
         return Batch(cols, b.num_rows, dist)
 
 
@@ -1351,20 +1355,31 @@ class MultiJoinExec(ExecNode):
         self.order_log = []
         deferred = []
         semis = [(sp, rex.execute(ctx)) for sp, rex in zip(lg.semis, self.children[nch:])]
-        # global row counts of every input in ONE all-reduce (SPMD: every rank
-        # must derive the same join order)
-        g = _global_rows_many([r["batch"] for r in rels] + [rb for _, rb in semis], ctx)
+        conds = list(lg.conds)
+        # global row counts of every input (SPMD: every rank must derive the
+        # same join order) — together with the merged NDV sketches of every
+        # join key the ordering will ask for, in ONE collective
+        if ctx.spmd:
+            g = self._spmd_stats([r["batch"] for r in rels] + [rb for _, rb in semis],
+                                 self._ndv_needs(rels, conds), ctx)
+        else:
+            g = _global_rows_many([r["batch"] for r in rels] + [rb for _, rb in semis], ctx)
         for r, n in zip(rels, g):
             r["grows"] = n
         for (sp, rb), nrb in zip(semis, g[len(rels):]):
             tgt = rels[sp.child]
             if sp.kind == "semi" and nrb <= self.EAGER_SEMI_RATIO * tgt["grows"]:
                 tgt["batch"] = self._semi(tgt["batch"], rb, sp, ctx)
-                tgt["grows"] = _global_rows(tgt["batch"], ctx)
+                if ctx.spmd:
+                    # estimated (no collective): a semi join keeps at most the
+                    # subquery side's rows; key NDVs are capped alike
+                    tgt["grows"] = max(1, min(tgt["grows"], nrb))
+                    tgt["ndv"] = {k: max(1, min(v, tgt["grows"])) for k, v in tgt["ndv"].items()}
+                else:
+                    tgt["grows"] = _global_rows(tgt["batch"], ctx)
                 self.order_log.append(f"{sp.kind} pre-filter on {tgt['name']} -> {tgt['batch'].num_rows}")
             else:
                 deferred.append((sp, rb))
-        conds = list(lg.conds)
         while len(rels) > 1:
             if ctx.spmd:
                 self._prefetch_ndv(rels, conds, ctx)
@@ -1414,8 +1429,14 @@ class MultiJoinExec(ExecNode):
             if self.required is not None and isinstance(out, LateBatch) and PRUNE_PARTS:
                 out = self._prune(out, conds, deferred)
             self.order_log.append(f"{a['name']} ⋈ {b['name']} -> {out.num_rows}")
-            # key NDVs carry over (capped by the output size) instead of re-sketching intermediates
-            cap = _global_rows(out, ctx)   # global: every rank must derive the same estimates / join order
+            # key NDVs carry over (capped by the output size) instead of re-sketching intermediates.
+            # SPMD ranks take the estimate as the output's global size (every rank
+            # derives the same value with no collective; the estimate is from
+            # global counts and merged sketches) instead of counting it
+            if ctx.spmd:
+                cap = max(1, int(min(best[0], 2**62))) if best is not None else max(1, a["grows"] * b["grows"])
+            else:
+                cap = _global_rows(out, ctx)
             ndv = {k: max(1, min(v, cap)) for d in (a["ndv"], b["ndv"]) for k, v in d.items()}
             merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})", "grows": cap}
             rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
@@ -1475,17 +1496,71 @@ class MultiJoinExec(ExecNode):
         with ctx.span("join.compose"):
             return LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
 
-    def _prefetch_ndv(self, rels, conds, ctx) -> None:
-        """SPMD: sketch every join key the next ordering step will ask for and
-        merge all rank sketches with ONE all-reduce (instead of one per key)."""
+    @staticmethod
+    def _ndv_needs(rels, conds, only=None) -> list:
+        """(relation, key expression) of every join key the next ordering step
+        asks an NDV for and that is not known yet."""
         need = []
         for i in range(len(rels)):
             for k in range(i + 1, len(rels)):
                 keys = _edges(conds, rels[i]["cids"], rels[k]["cids"])
                 if keys:
                     for rel, e in ((rels[i], keys[0][0]), (rels[k], keys[0][1])):
+                        if only is not None and rel is not only:
+                            continue
                         if e.sql() not in rel["ndv"] and all(e.sql() != x.sql() or rel is not r for r, x in need):
                             need.append((rel, e))
+        return need
+
+    def _spmd_stats(self, batches, need, ctx) -> List[int]:
+        """SPMD: global row counts of ``batches`` (a replicated batch counts
+        once) and the global NDV of every ``need`` key, in ONE collective: an
+        all-gather of [counts | HLL registers] (counts summed, registers
+        max-merged locally) on the GPU, one all-reduce of [counts | exact local
+        distinct counts] on the CPU. Sets ``rel["ndv"]``; returns the counts."""
+        comm = ctx.comm
+        local = [0 if _replicated(b) else b.num_rows for b in batches]
+        if ctx.device.type != "cuda":
+            nd = []
+            for rel, e in need:
+                b = rel["batch"]
+                mine = b.num_rows and (not _replicated(b) or comm.rank == 0)   # a replicated input counts once
+                nd.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
+            g = comm.allreduce_ints(local + nd)
+            for (rel, e), v in zip(need, g[len(local):]):
+                rel["ndv"][e.sql()] = max(v, 1)
+            g = g[:len(local)]
+        else:
+            regs = []
+            for rel, e in need:
+                b = rel["batch"]
+                if b.num_rows:
+                    k, _ = group_key_tensor(ctx.evaluator.column(e, b))
+                    regs.append(H.hll_sketch(k))
+                else:
+                    regs.append(torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
+            parts = [device_ints(local, ctx.device)]
+            if regs:
+                parts.append(torch.stack(regs).view(torch.int64).reshape(-1))
+            allg = comm.allgather_tensor(torch.cat(parts)).view(comm.world_size, -1)
+            nb = len(local)
+            # counts and NDV estimates reach the host in one readback
+            vals = [allg[:, :nb].sum(0)]
+            if regs:
+                merged = allg[:, nb:].contiguous().view(torch.uint8).view(comm.world_size, len(regs), H.HLL_M) \
+                    .amax(0)
+                vals.append(H.hll_terms(merged).view(torch.int64).reshape(-1))
+            host = to_host_ints(torch.cat(vals))
+            g = host[:nb]
+            for j, (rel, e) in enumerate(need):
+                z, zeros = np.array(host[nb + 2 * j:nb + 2 * j + 2], dtype=np.int64).view(np.float64)
+                rel["ndv"][e.sql()] = max(int(round(H.hll_from_terms(float(z), int(zeros)))), 1)
+        return [b.num_rows if _replicated(b) else n for b, n in zip(batches, g)]
+
+    def _prefetch_ndv(self, rels, conds, ctx) -> None:
+        """SPMD: sketch every join key the next ordering step will ask for and
+        merge all rank sketches with ONE all-reduce (instead of one per key)."""
+        need = self._ndv_needs(rels, conds)
         if not need:
             return
         if ctx.device.type != "cuda":
@@ -1493,7 +1568,8 @@ class MultiJoinExec(ExecNode):
             local = []
             for rel, e in need:
                 b = rel["batch"]
-                local.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if b.num_rows else 0)
+                mine = b.num_rows and (not _replicated(b) or ctx.comm.rank == 0)   # a replicated input counts once
+                local.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
             for (rel, e), g in zip(need, ctx.comm.allreduce_ints(local)):
                 rel["ndv"][e.sql()] = max(g, 1)
             return
@@ -1589,15 +1665,22 @@ def _derived_ndv(base, n: int) -> int:
     return max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / D))))))
 
 
+def _replicated(b) -> bool:
+    return getattr(b, "dist", None) == ("replicated",)
+
+
 def _global_rows(b: Batch, ctx) -> int:
-    if ctx.spmd:
+    if ctx.spmd and not _replicated(b):
         return ctx.comm.allreduce_int(b.num_rows)
     return b.num_rows
 
 
 def _global_rows_many(bs: Sequence[Batch], ctx) -> List[int]:
-    if ctx.spmd and bs:
-        return ctx.comm.allreduce_ints([b.num_rows for b in bs])
+    """Global row counts (a replicated batch's rows count once) in at most
+    one all-reduce."""
+    if ctx.spmd and any(not _replicated(b) for b in bs):
+        g = ctx.comm.allreduce_ints([0 if _replicated(b) else b.num_rows for b in bs])
+        return [b.num_rows if _replicated(b) else n for b, n in zip(bs, g)]
     return [b.num_rows for b in bs]
 
 

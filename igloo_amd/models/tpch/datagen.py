@@ -320,12 +320,47 @@ def gen_orders_lineitem(sf, device, rank=0, world=1, lean=False):
     return orders, lineitem
 
 
+#: multi-rank layout: the fact tables are hash-partitioned by order key
+#: (co-located, so lineitem-orders joins and per-order aggregation are
+#: rank-local) and every dimension table is replicated on every rank (at SF100
+#: they are ~125M rows, ~8 GB decoded, against 288 GB of HBM per GPU), so a
+#: fact-dimension join needs no exchange at all: only aggregate merges and
+#: final results cross xGMI. ``replicate_dims=False`` hash-partitions every
+#: table by its primary key instead (exercises the shuffle paths).
+PARTITIONED = ("orders", "lineitem")
+#: primary-key partitioning of every table (``replicate_dims=False``)
+PARTITION_KEY = {"region": None, "nation": None, "supplier": "s_suppkey", "customer": "c_custkey",
+                 "part": "p_partkey", "partsupp": "ps_partkey", "orders": "o_orderkey", "lineitem": "l_orderkey"}
+REPLICATED = ("region", "nation", "supplier", "customer", "part", "partsupp")
+
+
 def generate(sf: float, device="cpu", rank: int = 0, world: int = 1, lean: bool = False,
-             tables: Optional[List[str]] = None) -> Dict[str, MemoryTable]:
-    """All 8 TPC-H tables (this rank's partition) as device-resident MemoryTables."""
+             tables: Optional[List[str]] = None, replicate_dims: bool = True,
+             spmd: Optional[bool] = None) -> Dict[str, MemoryTable]:
+    """All 8 TPC-H tables (this rank's partition) as device-resident MemoryTables.
+    ``spmd`` (default: world > 1) tags the tables with the multi-rank layout
+    (also for a forced world of one, parallel/comm.py ``force_spmd``)."""
     device = torch.device(device)
     want = set(tables or S.TABLES)
     out: Dict[str, MemoryTable] = {}
+    spmd = world > 1 if spmd is None else spmd
+    if spmd and world == 1:
+        out = generate(sf, device, 0, 1, lean, tables, spmd=False)
+        for t, tab in out.items():
+            if replicate_dims and t in REPLICATED:
+                tab.replicated, tab.partitioned_by = True, None
+            elif t != "region" and t != "nation":
+                tab.partitioned_by = PARTITION_KEY[t]
+        return out
+    if world > 1 and replicate_dims:
+        dims = [t for t in REPLICATED if t in want]
+        if dims:
+            out.update(generate(sf, device, 0, 1, lean, dims, spmd=False))
+            for t in dims:
+                out[t].replicated, out[t].partitioned_by = True, None
+        want -= set(REPLICATED)
+        if not want:
+            return out
     if "region" in want:
         out["region"] = gen_region(device)
     if "nation" in want:
@@ -347,8 +382,9 @@ def generate(sf: float, device="cpu", rank: int = 0, world: int = 1, lean: bool 
     return out
 
 
-def register(engine, sf: float, rank: int = 0, world: int = 1, lean: bool = False) -> Dict[str, MemoryTable]:
-    tabs = generate(sf, engine.device, rank, world, lean)
+def register(engine, sf: float, rank: int = 0, world: int = 1, lean: bool = False,
+             replicate_dims: bool = True, spmd: Optional[bool] = None) -> Dict[str, MemoryTable]:
+    tabs = generate(sf, engine.device, rank, world, lean, replicate_dims=replicate_dims, spmd=spmd)
     for name, t in tabs.items():
         engine.register_table(name, t)
     return tabs

@@ -38,10 +38,11 @@ from ...columnar import Column
 from . import datagen
 from . import schema as S
 
-#: per-table partitioning column of the multi-rank layout (None = replicated)
-PARTITION_KEY = {"region": None, "nation": None, "supplier": "s_suppkey", "customer": "c_custkey",
-                 "part": "p_partkey", "partsupp": "ps_partkey", "orders": "o_orderkey", "lineitem": "l_orderkey"}
-FORMAT_VERSION = 2
+#: multi-rank layout (models/tpch/datagen.py): fact tables partitioned by
+#: order key in per-rank directories, dimension tables written once to a shared
+#: directory that every rank reads whole (replicated); None = replicated
+PARTITION_KEY = {t: (datagen.PARTITION_KEY[t] if t in datagen.PARTITIONED else None) for t in datagen.PARTITION_KEY}
+FORMAT_VERSION = 3
 
 
 def column_slice(c: Column, a: int, b: int) -> Column:
@@ -77,19 +78,27 @@ def _write_chunk(path: str, cols: Dict[str, Column], a: int, b: int, row_group: 
 
 
 def dataset_dir(root: str, sf: float, rank: int = 0, world: int = 1, lean: bool = False) -> str:
+    """This rank's partition of the fact tables."""
     tag = f"sf{sf:g}{'_lean' if lean else ''}"
     return os.path.join(root, tag, f"r{rank}of{world}")
 
 
-def write_dataset(sf: float, root: str, device="cuda", rank: int = 0, world: int = 1, lean: bool = False,
-                  rows_per_file: int = 8 << 20, row_group: int = 1 << 20, compression: str = "snappy",
-                  threads: Optional[int] = None, log=None) -> dict:
-    """Generate this rank's TPC-H partition and write it as Parquet under
-    ``dataset_dir(root, ...)``; returns the manifest (reused when complete)."""
-    out = dataset_dir(root, sf, rank, world, lean)
+def shared_dir(root: str, sf: float, lean: bool = False) -> str:
+    """The replicated dimension tables (identical for every world size, so the
+    1/2/4/8-GPU runs of one node write them once)."""
+    tag = f"sf{sf:g}{'_lean' if lean else ''}"
+    return os.path.join(root, tag, "shared")
+
+
+def _table_dir(root, sf, name, rank, world, lean) -> str:
+    if PARTITION_KEY[name] is None:
+        return os.path.join(shared_dir(root, sf, lean), name)
+    return os.path.join(dataset_dir(root, sf, rank, world, lean), name)
+
+
+def _write_tables(out: str, want: dict, tables, gen, rows_per_file: int, row_group: int, compression: str,
+                  threads: int) -> dict:
     man_path = os.path.join(out, "_manifest.json")
-    want = {"format": FORMAT_VERSION, "sf": sf, "rank": rank, "world": world, "lean": lean,
-            "rows_per_file": rows_per_file, "row_group": row_group, "compression": compression}
     if os.path.exists(man_path):
         with open(man_path) as f:
             man = json.load(f)
@@ -98,16 +107,15 @@ def write_dataset(sf: float, root: str, device="cuda", rank: int = 0, world: int
             return man
     shutil.rmtree(out, ignore_errors=True)
     os.makedirs(out)
-    threads = threads or min(16, os.cpu_count() or 4)
     t0 = time.perf_counter()
-    tabs = datagen.generate(sf, device, rank, world, lean=lean)
-    if torch.device(device).type == "cuda":
+    tabs = gen()
+    if any(c.data.is_cuda for t in tabs.values() for c in t.columns.values()):
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
     t1 = time.perf_counter()
     jobs = []
     with cf.ThreadPoolExecutor(max_workers=threads) as ex:
-        for name in S.TABLES:
+        for name in tables:
             t = tabs[name]
             os.makedirs(os.path.join(out, name))
             n = t.num_rows()
@@ -124,19 +132,64 @@ def write_dataset(sf: float, root: str, device="cuda", rank: int = 0, world: int
     with open(man_path + ".tmp", "w") as f:
         json.dump(man, f)
     os.replace(man_path + ".tmp", man_path)
+    return man
+
+
+def write_dataset(sf: float, root: str, device="cuda", rank: int = 0, world: int = 1, lean: bool = False,
+                  rows_per_file: int = 8 << 20, row_group: int = 1 << 20, compression: str = "snappy",
+                  threads: Optional[int] = None, log=None, wait_s: float = 3600.0) -> dict:
+    """Generate and write this rank's partition of the fact tables and (rank 0)
+    the shared dimension tables; other ranks wait for the shared manifest.
+    Returns the combined manifest (complete datasets are reused)."""
+    threads = threads or min(16, os.cpu_count() or 4)
+    base = {"sf": sf, "lean": lean, "rows_per_file": rows_per_file, "row_group": row_group,
+            "compression": compression}
+    facts = [t for t in S.TABLES if PARTITION_KEY[t] is not None]
+    dims = [t for t in S.TABLES if PARTITION_KEY[t] is None]
+    m1 = _write_tables(dataset_dir(root, sf, rank, world, lean),
+                       dict(base, format=FORMAT_VERSION, rank=rank, world=world), facts,
+                       lambda: datagen.generate(sf, device, rank, world, lean=lean, tables=facts),
+                       rows_per_file, row_group, compression, threads)
+    sd = shared_dir(root, sf, lean)
+    want2 = dict(base, format=FORMAT_VERSION, shared=True)
+    if rank == 0:
+        m2 = _write_tables(sd, want2, dims, lambda: datagen.generate(sf, device, 0, 1, lean=lean, tables=dims),
+                           rows_per_file, row_group, compression, threads)
+    else:
+        t0 = time.perf_counter()
+        mp_ = os.path.join(sd, "_manifest.json")
+        while True:
+            if os.path.exists(mp_):
+                with open(mp_) as f:
+                    m2 = json.load(f)
+                if all(m2.get(k) == v for k, v in want2.items()):
+                    m2["reused"] = True
+                    break
+            if time.perf_counter() - t0 > wait_s:
+                raise TimeoutError(f"shared dimension tables not written to {sd}")
+            time.sleep(0.5)
+    man = {"format": FORMAT_VERSION, "sf": sf, "rank": rank, "world": world, "lean": lean,
+           "rows": dict(m1["rows"], **m2["rows"]), "bytes": m1["bytes"] + (m2["bytes"] if rank == 0 else 0),
+           "files": m1["files"] + (m2["files"] if rank == 0 else 0),
+           "gen_s": round(m1["gen_s"] + (m2["gen_s"] if rank == 0 and not m2["reused"] else 0), 3),
+           "write_s": round(m1["write_s"] + (m2["write_s"] if rank == 0 and not m2["reused"] else 0), 3),
+           "reused": m1["reused"] and m2["reused"], "compression": compression}
     if log:
-        log(f"[parquet] wrote {len(jobs)} files, {nbytes / 1e9:.2f} GB in {write_s:.1f}s (gen {gen_s:.1f}s) -> {out}")
+        log(f"[parquet] {man['files']} files, {man['bytes'] / 1e9:.2f} GB written in {man['write_s']:.1f}s "
+            f"(gen {man['gen_s']:.1f}s, reused {man['reused']}) -> {dataset_dir(root, sf, rank, world, lean)} + {sd}")
     return man
 
 
 def register_dataset(engine, root: str, sf: float, rank: int = 0, world: int = 1, lean: bool = False,
-                     tables: Optional[List[str]] = None, **kw) -> Dict[str, object]:
-    """Register every table of a written dataset (this rank's partition)."""
-    out = dataset_dir(root, sf, rank, world, lean)
+                     tables: Optional[List[str]] = None, spmd: Optional[bool] = None, **kw) -> Dict[str, object]:
+    """Register every table of a written dataset (this rank's partition of
+    the fact tables, the shared dimension tables whole). ``spmd`` (default
+    world > 1) tags them with the multi-rank layout."""
+    spmd = world > 1 if spmd is None else spmd
     srcs = {}
     for name in tables or S.TABLES:
         key = PARTITION_KEY[name]
         srcs[name] = engine.register_parquet(
-            name, os.path.join(out, name), local=True, replicated=(key is None and world > 1),
-            partitioned_by=key if world > 1 else None, **kw)
+            name, _table_dir(root, sf, name, rank, world, lean), local=True, replicated=(key is None and spmd),
+            partitioned_by=key if spmd else None, **kw)
     return srcs

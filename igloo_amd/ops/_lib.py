@@ -114,6 +114,27 @@ def set_capturing(on: bool) -> None:
     _capture.on = on
 
 
+def device_ints(values, device, dtype=torch.int64) -> torch.Tensor:
+    """Host ints -> a device tensor without a synchronizing copy: staged in
+    pinned memory and copied stream-ordered. Under graph capture the copy is a
+    graph node that reads the pinned buffer at every replay, so the buffer is
+    kept alive with the capture (``capture_keepalive``)."""
+    h = torch.tensor(values, dtype=dtype).pin_memory()
+    if getattr(_capture, "on", False):
+        keep = getattr(_capture, "keep", None)
+        if keep is None:
+            keep = _capture.keep = []
+        keep.append(h)
+    return h.to(device, non_blocking=True)
+
+
+def capture_keepalive() -> list:
+    """Host buffers the current capture's graph reads (cleared per capture)."""
+    keep = getattr(_capture, "keep", None) or []
+    _capture.keep = []
+    return keep
+
+
 def check_not_capturing(what: str) -> None:
     if getattr(_capture, "on", False):
         raise CaptureAbort(what)

@@ -586,13 +586,22 @@ def hll_sketch(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Opti
     return regs
 
 
+def hll_terms(regs: torch.Tensor) -> torch.Tensor:
+    """Per sketch (rows of ``regs``) the float64 pair (sum 2^-r, zero
+    registers) the estimate is computed from, on the device."""
+    r = regs.to(torch.float64)
+    return torch.stack([torch.pow(2.0, -r).sum(-1), (regs == 0).sum(-1).to(torch.float64)], -1)
+
+
 def hll_estimate(regs: torch.Tensor) -> float:
     """Cardinality estimate from HLL registers (bias-corrected; linear counting
     for small cardinalities). Relative error ~1.04/sqrt(4096) = 1.6%."""
-    r = regs.to(torch.float64)
+    z, zeros = to_host_f64s(hll_terms(regs))
+    return hll_from_terms(z, int(zeros))
+
+
+def hll_from_terms(z: float, zeros: int) -> float:
     m = float(HLL_M)
-    z, zeros = to_host_f64s(torch.stack([torch.pow(2.0, -r).sum(), (regs == 0).sum().to(torch.float64)]))
-    zeros = int(zeros)
     alpha = 0.7213 / (1.0 + 1.079 / m)
     e = alpha * m * m / z
     if e <= 2.5 * m and zeros > 0:

@@ -20,7 +20,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from ..ops._lib import to_host_f64s, to_host_ints
+from ..ops._lib import device_ints, to_host_f64s, to_host_ints
 from ..utils import faults
 from ..utils.errors import CommError
 from ..utils.log import get_logger
@@ -99,6 +99,8 @@ class Communicator:
 
     # ------------------------------------------------------------ primitives
     def _t(self, x, dtype=torch.int64) -> torch.Tensor:
+        if self.wire.type == "cuda":
+            return device_ints(x, self.wire, dtype)     # no sync; capture-safe
         return torch.as_tensor(x, dtype=dtype, device=self.wire)
 
     def barrier(self):
@@ -177,6 +179,20 @@ class Communicator:
         dist.all_gather_into_tensor(out, t, group=self.group)
         v = to_host_ints(out)
         return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
+
+    def allgather_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        """Every rank's equally sized ``t`` concatenated (rank order), on the
+        data device; one all-gather (staged through the host under gloo)."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "allgather_tensor")
+        if not self.spmd:
+            return t
+        src = t.contiguous().to(self.wire)
+        out = torch.empty((self.world_size * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=self.wire)
+        self.calls += 1
+        dist.all_gather_into_tensor(out, src, group=self.group)
+        self.bytes_sent += src.numel() * src.element_size() * (self.world_size - 1)
+        return out.to(t.device)
 
     def allgather_object(self, obj) -> list:
         if faults.ACTIVE:

@@ -11,8 +11,10 @@ move only at exchanges:
   partial states by group key, final merge (SURVEY §2.4 P7);
 * gather — final results / sort inputs collected on every rank.
 
-Distribution of a Batch is tracked in ``Batch.dist``: ``("hash", cid)`` (rows
-placed by mix64(key) % world), ``("replicated",)`` or ``None`` (arbitrary).
+Distribution of a Batch is tracked in ``Batch.dist``: ``("hash", cid, ...)``
+(rows placed by mix64(key) % world; after a co-partitioned equi-join every
+column equal to the key is listed), ``("replicated",)`` or ``None``
+(arbitrary).
 Every decision is taken from globally reduced values, so all ranks issue the
 same collectives in the same order.
 
@@ -47,6 +49,11 @@ DEFAULT_BROADCAST_ROWS = 4_000_000
 
 def dist_of(b: Batch):
     return getattr(b, "dist", None)
+
+
+def hashed_on(d, cid) -> bool:
+    """Rows placed by the hash of column ``cid`` (or a column equal to it)."""
+    return cid is not None and bool(d) and d[0] == "hash" and cid in d[1:]
 
 
 def with_dist(b: Batch, d) -> Batch:
@@ -252,6 +259,23 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
     return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
 
 
+def local_slice(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
+    """This rank's hash partition of a REPLICATED batch, with no
+    communication: every rank holds all rows, so each keeps those whose
+    ``mix64(key) % world`` is its rank (the partition function of ``shuffle``).
+    The result is co-partitioned with any batch shuffled on the same key."""
+    from ..ops.gather import take_many as _take_many
+    from ..ops.select import mask_to_indices
+    comm = ctx.comm
+    d = ("hash", key_cid) if key_cid is not None else None
+    if comm.world_size == 1:
+        return Batch(dict(b.columns), b.num_rows, d)
+    idx = mask_to_indices(M.partition_ids(key, comm.world_size) == comm.rank)
+    keys = list(b.columns)
+    cols = _take_many([b.columns[k] for k in keys], idx)
+    return Batch(dict(zip(keys, cols)), idx.numel(), d)
+
+
 def _gather_column(c: Column, counts: List[int], comm) -> Column:
     """All-gather of one column (dictionaries must already agree)."""
     return _gather_columns([c], counts, comm)[0]
@@ -328,14 +352,6 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
     kind, on = join.kind, join.on
     ld, rd = dist_of(lb), dist_of(rb)
     rep_l, rep_r = ld == REPLICATED, rd == REPLICATED
-    if rows is not None:
-        nl, nr = rows
-    else:
-        nl, nr = comm.allreduce_ints([lb.num_rows if not rep_l else 0, rb.num_rows if not rep_r else 0])
-    if rep_l:
-        nl = lb.num_rows
-    if rep_r:
-        nr = rb.num_rows
     limit = int(ctx.engine.session.get("broadcast_rows", DEFAULT_BROADCAST_ROWS)) if ctx.engine else DEFAULT_BROADCAST_ROWS
 
     def done(l, r, d):
@@ -347,8 +363,22 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
     if on:
         for le, re_ in on:
             lc, rc = _cid(le), _cid(re_)
-            if ld and rd and ld[0] == "hash" and rd[0] == "hash" and ld[1] == lc and rd[1] == rc and lc is not None:
-                return done(lb, rb, ld)
+            if hashed_on(ld, lc) and hashed_on(rd, rc):
+                # co-partitioned: rank-local; the output is placed by both keys
+                return done(lb, rb, ld + tuple(c for c in rd[1:] if c not in ld))
+    if kind in ("inner", "cross") and (rep_l or rep_r):
+        return done(lb, rb, rd if rep_l else ld)
+    if kind in ("left", "semi", "anti") and rep_r:
+        return done(lb, rb, ld)
+    # global sizes decide broadcast vs shuffle (a replicated side counts once)
+    if rows is not None:
+        nl, nr = rows
+    else:
+        nl, nr = comm.allreduce_ints([lb.num_rows if not rep_l else 0, rb.num_rows if not rep_r else 0])
+    if rep_l:
+        nl = lb.num_rows
+    if rep_r:
+        nr = rb.num_rows
     null_aware = getattr(join, "null_aware", False)
     if kind in ("inner", "cross"):
         if rep_r:
@@ -364,12 +394,16 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
             return done(lb, rb, ld)
         if (nr <= limit or null_aware or not on) and not rep_l:
             return done(lb, gather_all(rb, ctx), ld)
-        if rep_l:
-            # preserved side replicated: bring everything together
+        if rep_l and (nr <= limit or null_aware or not on):
+            # preserved side replicated, small other side: bring everything together
             return done(lb, gather_all(rb, ctx), REPLICATED)
+        # preserved side replicated, large other side (TPC-H Q13 / Q22:
+        # customer against orders): each rank keeps its hash slice of the
+        # replicated side (no exchange) and the other side is shuffled below
     if not on:
         return done(gather_all(lb, ctx), gather_all(rb, ctx), REPLICATED)
-    # hash shuffle both sides on the first key pair
+    # hash shuffle both sides on the first key pair (a replicated side is
+    # sliced locally instead: shuffling it would multiply its rows)
     ev = ctx.evaluator
     le, re_ = on[0]
     lcol, rcol = ev.column(le, lb), ev.column(re_, rb)
@@ -379,11 +413,15 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
         lk, rk = _pair_key(lcol, rcol)
         lk, rk = lk.to(torch.int64).contiguous(), rk.to(torch.int64).contiguous()
     lc, rc = _cid(le), _cid(re_)
-    if not (ld and ld[0] == "hash" and ld[1] == lc and lc is not None and lcol.dtype == rcol.dtype):
+    if rep_l:
+        lb = local_slice(lb, lk, ctx, lc)
+    elif not (hashed_on(ld, lc) and lcol.dtype == rcol.dtype):
         lb = shuffle(lb, lk, ctx, lc)
-    if not (rd and rd[0] == "hash" and rd[1] == rc and rc is not None and lcol.dtype == rcol.dtype):
+    if rep_r:
+        rb = local_slice(rb, rk, ctx, rc)
+    elif not (hashed_on(rd, rc) and lcol.dtype == rcol.dtype):
         rb = shuffle(rb, rk, ctx, rc)
-    return done(lb, rb, ("hash", lc) if lc is not None else None)
+    return done(lb, rb, ("hash",) + tuple(c for c in (lc, rc) if c is not None) if lc is not None else None)
 
 
 # ------------------------------------------------------------------ aggregation
@@ -400,7 +438,7 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
         return with_dist(aggregate(groups, aggs, b, ctx), REPLICATED)
     if d and d[0] == "hash":
         for ci, e in groups:
-            if isinstance(e, ColRef) and e.cid == d[1]:
+            if isinstance(e, ColRef) and hashed_on(d, e.cid):
                 return with_dist(aggregate(groups, aggs, b, ctx), ("hash", ci.cid))
     ev = ctx.evaluator
     decomposable = all(a.func in DECOMPOSABLE and not a.distinct for _, a in aggs)

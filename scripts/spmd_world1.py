@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--runs", type=int, default=4)
     ap.add_argument("--queries", default="1-22")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--partitioned-dims", action="store_true", help="hash-partition every table (no replication)")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
@@ -48,10 +49,14 @@ def main():
     comm = Communicator.init(backend=backend, device=a.device, force_spmd=True, timeout_s=300)
     e = ig.QueryEngine(device=a.device, comm=comm)
     ref = ig.QueryEngine(device=a.device)
-    tabs = datagen.generate(a.sf, a.device, 0, 1)
+    # the multi-rank table layout (replicated dimensions, fact tables
+    # partitioned by order key) on one rank; the reference engine reads the
+    # same tensors as plain tables
+    import igloo_amd.catalog as C
+    tabs = datagen.generate(a.sf, a.device, 0, 1, replicate_dims=not a.partitioned_dims, spmd=True)
     for n, t in tabs.items():
         e.register_table(n, t)
-        ref.register_table(n, t)
+        ref.register_table(n, C.MemoryTable(t.columns, t.num_rows()))
     want = {q: digest(ref.sql(queries.QUERIES[q]).table) for q in qs}
     del ref
     out = {"backend": backend, "sf": a.sf, "queries": {}}

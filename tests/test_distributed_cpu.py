@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_thresholds=False):
+def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_thresholds=False, replicate_dims=True):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import igloo_amd as ig
@@ -35,7 +35,7 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
         H.BLOOM_MIN_RATIO = 2
     comm = Communicator.init(backend="gloo", device=device, timeout_s=120)
     e = ig.QueryEngine(device=device, comm=comm)
-    for name, t in datagen.generate(sf, device, rank, world).items():
+    for name, t in datagen.generate(sf, device, rank, world, replicate_dims=replicate_dims).items():
         e.register_table(name, t)
     res = {}
     for q in queries:
@@ -52,23 +52,27 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
     comm.shutdown()
 
 
-def run_distributed(world, con, device="cpu", low_thresholds=False):
+def run_distributed(world, con, device="cpu", low_thresholds=False, replicate_dims=True):
     """Run TPC-H 1-22 on ``world`` ranks (gloo) and compare rank 0 with sqlite."""
     from igloo_amd.models.tpch import oracle
     qs = list(range(1, 23))
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.json")
-        mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs, device, low_thresholds), nprocs=world,
+        mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs, device, low_thresholds, replicate_dims),
+                           nprocs=world,
                            join=True, start_method="spawn")
         res = json.load(open(out))
     run_distributed.last = res
     return check(res, qs, con)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_tpch_distributed_gloo(world, tpch_cpu):
+@pytest.mark.parametrize("world,replicate_dims", [(2, True), (3, True), (2, False), (3, False)])
+def test_tpch_distributed_gloo(world, replicate_dims, tpch_cpu):
+    """Both multi-rank layouts: replicated dimension tables with fact tables
+    co-partitioned by order key (the bench layout), and every table
+    hash-partitioned by its primary key (every shuffle / broadcast path)."""
     _, _, con = tpch_cpu
-    bad = run_distributed(world, con)
+    bad = run_distributed(world, con, replicate_dims=replicate_dims)
     assert not bad, "\n".join(bad)
     calls = {int(q): r["collectives"] for q, r in run_distributed.last.items()}
     print("collectives per query:", calls)
@@ -76,6 +80,10 @@ def test_tpch_distributed_gloo(world, tpch_cpu):
     # partial states with one all-reduce per op, Q6 (global sum) likewise
     assert calls[1] <= 6 and calls[6] <= 4, calls
     assert sum(calls.values()) <= 22 * 20, calls
+    if replicate_dims:
+        # fact-dimension joins are rank-local: the headline queries exchange
+        # only aggregate merges and results
+        assert all(calls[q] <= 6 for q in (1, 3, 5, 9, 18)), calls
 
 
 def check(res, qs, con):
