@@ -78,6 +78,10 @@ def main():
                     help="check result digests against the CPU engine (auto: sf <= 1)")
     ap.add_argument("--per-query", action="store_true", help="print per-query times to stderr")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (debug)")
+    ap.add_argument("--eager-steps", type=int, default=2,
+                    help="suites timed with query graphs off (warm_eager_s), after the headline steps")
+    ap.add_argument("--vary-params", type=int, default=2, metavar="STREAMS",
+                    help="suites with fresh TPC-H substitution parameters per query (adhoc_s; 0 = skip)")
     a = ap.parse_args()
 
     import torch
@@ -218,6 +222,43 @@ def main():
         elapsed = comm.allreduce_max_float(elapsed)
     step_s = elapsed / max(a.steps, 1)
 
+    # ---- secondary measurements (after the headline steps, not part of ``value``):
+    # warm_eager_s — the same SQL with query graphs off (replayed readbacks,
+    # Python operator dispatch); adhoc_s — every statement new SQL text
+    # (TPC-H substitution parameters, models/tpch/params.py): nothing keyed
+    # on the SQL text (plans, readbacks, graphs) applies
+    from igloo_amd.exec import graphs as _graphs_mod
+    from igloo_amd.models.tpch import params as _params
+    eager_s = adhoc_s = None
+    if a.eager_steps > 0:
+        saved = _graphs_mod.GRAPHS
+        _graphs_mod.GRAPHS = False
+        try:
+            suite()          # first eager pass re-records readbacks without graphs
+            barrier()
+            te = time.perf_counter()
+            for _ in range(a.eager_steps):
+                suite()
+            barrier()
+            eager_s = (time.perf_counter() - te) / a.eager_steps
+        finally:
+            _graphs_mod.GRAPHS = saved
+        if comm is not None:
+            eager_s = comm.allreduce_max_float(eager_s)
+        log(f"[bench] warm eager (graphs off): {eager_s:.4f}s per suite")
+    if a.vary_params > 0:
+        streams = [_params.stream(qs, 1000 + k, a.sf) for k in range(a.vary_params)]
+        barrier()
+        ta = time.perf_counter()
+        for st_sql in streams:
+            for q in qs:
+                eng.sql(st_sql[q])
+        barrier()
+        adhoc_s = (time.perf_counter() - ta) / a.vary_params
+        if comm is not None:
+            adhoc_s = comm.allreduce_max_float(adhoc_s)
+        log(f"[bench] ad-hoc (fresh substitution parameters): {adhoc_s:.4f}s per suite")
+
     # ---- verification (outside the timed region)
     mismatches = [(i, q) for i, res in enumerate(step_results) for q, t in res.items() if digest(t) != ref[q]]
     del step_results
@@ -273,6 +314,9 @@ def main():
                                   "replicated" if spmd else "single rank"),
                        "sf": a.sf, "queries": qs},
             "warm_s": round(step_s, 4),
+            "warm_graph_s": round(step_s, 4),
+            "warm_eager_s": round(eager_s, 4) if eager_s is not None else None,
+            "adhoc_s": round(adhoc_s, 4) if adhoc_s is not None else None,
             "cold_s": round(cold_s, 4),
             # timed-step queries whose host readbacks were replayed and validated
             # on the device (engine.QueryEngine._execute_speculative)

@@ -1,0 +1,72 @@
+"""RCCL probe for a world of one rank (tests/test_rccl_gpu.py): every
+collective parallel/comm.py uses, then the same collectives captured in a HIP
+graph. Prints a progress line after each step so a hang names its step.
+
+    MASTER_PORT=29555 python scripts/rccl_probe.py
+"""
+
+import os, sys, torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ.get("ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("PORT", "29555"), RANK="0", WORLD_SIZE="1")
+from igloo_amd.parallel.comm import Communicator
+dev = torch.device("cuda:0")
+c = Communicator.init(backend="nccl", device=dev, force_spmd=True, timeout_s=120)
+print("step 1", flush=True)
+assert c.backend == "nccl" and c.spmd and c.world_size == 1
+print("step 2", flush=True)
+x = torch.arange(1000, dtype=torch.int64, device=dev)
+y, rc = c.all_to_all_v(x, [1000])                      # all_to_all_single
+assert rc == [1000] and torch.equal(y, x)
+print("step 3", flush=True)
+assert c.all_to_all_counts([7]) == [7]
+print("step 4", flush=True)
+g, cnt = c.all_gather_v(x[:300], [300])                 # all_gather_into_tensor
+assert cnt == [300] and torch.equal(g, x[:300])
+print("step 5", flush=True)
+assert c.allgather_ints([3, 4]) == [[3, 4]]
+print("step 6", flush=True)
+assert c.allreduce_ints([5, 6]) == [5, 6]               # all_reduce
+print("step 7", flush=True)
+t = c.allreduce_tensor(torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev), "max")
+assert t.tolist() == [1.5, 2.5]
+print("step 8", flush=True)
+b = c.broadcast_tensor(torch.full((4,), 9, dtype=torch.int32, device=dev))   # broadcast
+assert b.tolist() == [9] * 4
+print("step 9", flush=True)
+# point-to-point (the uneven all-gather-v path): send to / receive from self
+r = torch.empty(200, dtype=torch.int64, device=dev)
+for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, x[:200], 0), dist.P2POp(dist.irecv, r, 0)]):
+    q.wait()
+    print("step 10", flush=True)
+assert torch.equal(r, x[:200])
+print("step 11", flush=True)
+# collectives inside a captured HIP graph, replayed with new inputs
+src = torch.zeros(512, dtype=torch.int64, device=dev)
+dst = torch.empty_like(src)
+red = torch.zeros(8, dtype=torch.int64, device=dev)
+s = torch.cuda.Stream(dev)
+s.wait_stream(torch.cuda.current_stream(dev))
+with torch.cuda.stream(s):
+    dist.all_to_all_single(dst, src * 2, [512], [512]); dist.all_reduce(red)   # warm the communicator
+torch.cuda.current_stream(dev).wait_stream(s)
+torch.cuda.synchronize()
+print("step 12", flush=True)
+gr = torch.cuda.CUDAGraph()
+print("step 13", flush=True)
+with torch.cuda.graph(gr):
+    tmp = src * 2
+    dist.all_to_all_single(dst, tmp, [512], [512])
+    dist.all_reduce(red)
+    ag = torch.empty(512, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(ag, dst)
+for k in (1, 5):
+    src.copy_(torch.arange(512, device=dev) + k)
+    red.fill_(k)
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(dst, (torch.arange(512, device=dev) + k) * 2), k
+    assert torch.equal(ag, dst) and red.tolist() == [k] * 8, k
+    print("step 14", flush=True)
+c.shutdown()
+print("RCCL_API_OK")
