@@ -39,21 +39,41 @@ RETRYABLE = (fl.FlightUnavailableError, fl.FlightTimedOutError, fl.FlightCancell
              TimeoutError)
 
 
+def _supervised(w) -> bool:
+    return any(isinstance(d, dict) and d.get("supervisor") for d in (w.info.devices or []))
+
+
 class DistributedExecutor:
     def __init__(self, registry: WorkerRegistry, engine, token: Optional[str] = None, max_attempts: int = 3,
-                 timeout_s: float = 3600.0):
+                 timeout_s: float = 3600.0, recovery_wait_s: float = 30.0):
         self.registry = registry
         self.engine = engine
         self.token = token
         self.max_attempts = max_attempts
         self.timeout_s = timeout_s
+        #: after a supervised group failed a query, how long to wait for its
+        #: node supervisor's replacement group (the surviving GPUs) before
+        #: falling back to local execution (service/supervisor.py)
+        self.recovery_wait_s = recovery_wait_s
         self.log = []  # (sql, worker id | "local", ms, outcome)
+
+    def _await_replacement(self, tried: set) -> list:
+        deadline = time.time() + self.recovery_wait_s
+        while time.time() < deadline:
+            cands = [w for w in self.registry.alive() if w.info.id not in tried]
+            if cands:
+                return cands
+            time.sleep(0.05)
+        return []
 
     def run(self, sql: str) -> pa.Table:
         from .client import IglooClient
         tried = set()
+        failed_supervised = False
         for _ in range(self.max_attempts):
             cands = [w for w in self.registry.alive() if w.info.id not in tried]
+            if not cands and failed_supervised:
+                cands = self._await_replacement(tried)
             if not cands:
                 break
             w = min(cands, key=lambda s: s.tasks_done)
@@ -67,6 +87,7 @@ class DistributedExecutor:
                 return t
             except RETRYABLE as e:
                 w.failures += 1
+                failed_supervised = failed_supervised or _supervised(w)
                 self.log.append((sql, w.info.id, (time.perf_counter() - t0) * 1e3, f"retry: {type(e).__name__}"))
                 self.registry.mark_dead(w.info.id, f"(query failed: {type(e).__name__})", quarantine=True)
             except pa.ArrowKeyError:
@@ -89,7 +110,8 @@ class Coordinator:
         self.cfg = cfg or IglooConfig()
         self.engine = engine or ig.QueryEngine(device=self.cfg.device)
         self.registry = WorkerRegistry(self.cfg.heartbeat_interval_s, self.cfg.heartbeat_timeout_s)
-        self.executor = DistributedExecutor(self.registry, self.engine, self.cfg.auth_token)
+        self.executor = DistributedExecutor(self.registry, self.engine, self.cfg.auth_token,
+                                            recovery_wait_s=getattr(self.cfg, "recovery_wait_s", 30.0))
         p = self.cfg.coordinator_port if port is None else port
         self.location = f"grpc://{self.cfg.coordinator_host}:{p}"
         self.server = IglooFlightServer(self.engine, self.location, self.registry, runner=self.executor.run,

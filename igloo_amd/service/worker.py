@@ -216,6 +216,11 @@ class WorkerGroup:
     # ------------------------------------------------------------- rank 0
     def devices(self) -> list:
         info = {"rank": self.rank, "device": str(self.engine.device)}
+        if os.environ.get("IGLOO_SUPERVISOR_ID"):
+            # started by a node supervisor (service/supervisor.py): a replacement
+            # group follows if this one breaks, the coordinator waits for it
+            info.update(supervisor=os.environ["IGLOO_SUPERVISOR_ID"],
+                        generation=int(os.environ.get("IGLOO_GENERATION", "0")))
         if self.engine.device.type == "cuda":
             from ..ops._lib import native
             try:

@@ -25,6 +25,9 @@ class IglooConfig:
     heartbeat_timeout_s: float = 15.0
     # upper bound of any data collective inside a worker group (then the group is broken)
     collective_timeout_s: float = 60.0
+    # after a supervised worker group fails, wait this long for the node
+    # supervisor's replacement group on the surviving GPUs (service/supervisor.py)
+    recovery_wait_s: float = 30.0
     # execution
     device: Optional[str] = None
     gpus_per_node: int = 8

@@ -2,6 +2,7 @@
 import os
 import subprocess
 import sys
+import threading
 import time
 
 import pyarrow as pa
@@ -278,4 +279,47 @@ def test_rank_death_inside_group_fails_over_within_30s():
     finally:
         for p in group + ([healthy] if healthy else []):
             p.kill()
+        co.shutdown()
+
+
+def test_rank_death_recovers_on_surviving_ranks_of_the_node():
+    """SURVEY §5.3 retry on N-1: a node supervisor runs a 3-rank SPMD worker
+    group (gloo, CPU). Rank 2 dies mid-query (kill_worker@rank2); there is NO
+    other worker group. The supervisor starts a fresh 2-rank group on the
+    surviving devices (new process group, partitions re-derived for world 2),
+    the coordinator waits for it and retries, and the answer is correct —
+    within 30 s of submitting the query."""
+    from igloo_amd.models.tpch import datagen, queries
+    from igloo_amd.service.supervisor import NodeSupervisor
+    co = Coordinator(IglooConfig(coordinator_port=0, heartbeat_interval_s=0.3, heartbeat_timeout_s=1.5,
+                                 device="cpu", recovery_wait_s=40.0)).start()
+    datagen.register(co.engine, 0.01)
+    want = co.engine.query(queries.QUERIES[5]).to_pylist()
+    env = dict(os.environ, PYTHONPATH=ROOT, IGLOO_HEARTBEAT_INTERVAL_S="0.3", IGLOO_COLLECTIVE_TIMEOUT_S="20")
+    sup = NodeSupervisor(["cpu", "cpu", "cpu"], co.address, ["--tpch", "0.01"], env=env,
+                         first_generation_env={"IGLOO_FAULT": "kill_worker@rank2"}, grace_s=2.0)
+    t = threading.Thread(target=sup.run, daemon=True)
+    t.start()
+    try:
+        t0 = time.time()
+        while len(co.registry.alive()) < 1 and time.time() - t0 < 120:
+            time.sleep(0.2)
+        assert len(co.registry.alive()) == 1
+        first = co.registry.alive()[0]
+        assert first.info.world_size == 3
+        t1 = time.time()
+        with IglooClient(co.address) as c:
+            got = c.query(queries.QUERIES[5]).to_pylist()
+        took = time.time() - t1
+        assert got == want
+        assert took < 30, took
+        outcomes = [(w, o) for (_, w, _, o) in co.executor.log]
+        assert outcomes[0][0] == first.info.id and outcomes[0][1].startswith("retry"), co.executor.log
+        assert outcomes[-1][1] == "ok" and outcomes[-1][0] not in ("local", first.info.id), co.executor.log
+        ran = [w for w in co.registry.snapshot() if w["id"] == outcomes[-1][0]][0]
+        assert ran["world_size"] == 2
+        h = sup.history[0]
+        assert h["exit_codes"][2] == 17 and h["dead"] == ["cpu"] and sup.generation == 1
+    finally:
+        sup.shutdown()
         co.shutdown()
