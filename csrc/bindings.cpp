@@ -443,6 +443,30 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("str_char_length", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::str_char_length(P<const int64_t>(off), P<const uint8_t>(chars), n, P<int32_t>(out), S(s));
+  });
+  m.def("str_concat2_lengths", [](uintptr_t oa, bool ba, uintptr_t ob, bool bb, int64_t n, uintptr_t len, uintptr_t s) {
+    kern::str_concat2_lengths(P<const int64_t>(oa), ba, P<const int64_t>(ob), bb, n, P<int64_t>(len), S(s));
+  });
+  m.def("str_concat2_copy", [](uintptr_t oa, uintptr_t ca, bool ba, uintptr_t ob, uintptr_t cb, bool bb, int64_t n,
+                               uintptr_t off, uintptr_t out, uintptr_t s) {
+    kern::str_concat2_copy(P<const int64_t>(oa), P<const uint8_t>(ca), ba, P<const int64_t>(ob), P<const uint8_t>(cb),
+                           bb, n, P<const int64_t>(off), P<uint8_t>(out), S(s));
+  });
+  m.def("fmt_lengths", [](uintptr_t vals, int kind, int64_t n, int scale, uintptr_t valid, uintptr_t len, uintptr_t s) {
+    kern::fmt_lengths(P<const void>(vals), kind, n, scale, P<const uint8_t>(valid), P<int64_t>(len), S(s));
+  });
+  m.def("fmt_write", [](uintptr_t vals, int kind, int64_t n, int scale, uintptr_t valid, uintptr_t off, uintptr_t out,
+                        uintptr_t s) {
+    kern::fmt_write(P<const void>(vals), kind, n, scale, P<const uint8_t>(valid), P<const int64_t>(off), P<uint8_t>(out),
+                    S(s));
+  });
+  m.def("str_parse", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t valid, int kind, int scale, uintptr_t out,
+                        uintptr_t err, uintptr_t s) {
+    kern::str_parse(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(valid), kind, scale,
+                    P<void>(out), P<int>(err), S(s));
+  });
   m.def("wide_fits", [](uintptr_t lo, uintptr_t hi, int64_t n, uintptr_t flag, uintptr_t s) {
     kern::wide_fits(P<const int64_t>(lo), P<const int64_t>(hi), n, P<int>(flag), S(s));
   });

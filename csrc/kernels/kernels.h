@@ -216,6 +216,18 @@ void str_substr_lengths(const int64_t* off, const uint8_t* chars, int64_t n, int
                         int64_t* out_len, hipStream_t stream);
 void str_substr_copy(const int64_t* off, const uint8_t* chars, int64_t n, int64_t start, int64_t len, bool has_len,
                      const int64_t* new_off, uint8_t* out, hipStream_t stream);
+// string expressions (strexpr.hip)
+void str_char_length(const int64_t* off, const uint8_t* chars, int64_t n, int32_t* out, hipStream_t stream);
+void str_concat2_lengths(const int64_t* oa, bool ba, const int64_t* ob, bool bb, int64_t n, int64_t* len,
+                         hipStream_t stream);
+void str_concat2_copy(const int64_t* oa, const uint8_t* ca, bool ba, const int64_t* ob, const uint8_t* cb, bool bb,
+                      int64_t n, const int64_t* off, uint8_t* out, hipStream_t stream);
+void fmt_lengths(const void* vals, int kind, int64_t n, int scale, const uint8_t* valid, int64_t* len,
+                 hipStream_t stream);
+void fmt_write(const void* vals, int kind, int64_t n, int scale, const uint8_t* valid, const int64_t* off,
+               uint8_t* out, hipStream_t stream);
+void str_parse(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* valid, int kind, int scale,
+               void* out, int* err, hipStream_t stream);
 // LIKE made of '%'-separated literals (no '_'): segments concatenated in `seg`
 // with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%'
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,

@@ -326,6 +326,8 @@ class QueryEngine:
         bq_names = names
         ctx = self.make_context()
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
+        from .ops._lib import HOST_STEPS
+        h0 = sum(HOST_STEPS.values())
         with _trace.Range("query"):
             batch, spec, st = self._execute_speculative(plan, ctx, key)
         table = self._to_arrow(batch, plan.schema, bq_names)
@@ -334,7 +336,9 @@ class QueryEngine:
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
-                             "spill": dict(ctx.spill), "plan_cached": cached, "speculation": spec}
+                             "spill": dict(ctx.spill), "plan_cached": cached, "speculation": spec,
+                             # work that left the GPU (ops/_lib.py note_host_step)
+                             "host_steps": sum(HOST_STEPS.values()) - h0}
         if self.comm is not None:
             self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
         return QueryResult(table, ms)
@@ -622,8 +626,10 @@ class QueryEngine:
         node = create_physical_plan(logical)
         rows_t, rows_p = ["logical_plan", "physical_plan"], [logical.explain(), node.explain()]
         if analyze:
+            from .ops._lib import HOST_STEPS
             ctx = self.make_context(analyze=True)
             c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
+            h0 = dict(HOST_STEPS)
             t0 = time.perf_counter()
             node.execute(ctx)
             ms = (time.perf_counter() - t0) * 1e3
@@ -638,6 +644,9 @@ class QueryEngine:
             if self.comm is not None and self.comm.spmd:
                 txt += (f"\nexchange: {self.comm.calls - c0[0]} collectives, "
                         f"{self.comm.bytes_sent - c0[1]} bytes sent by this rank")
+            host = {k: v - h0.get(k, 0) for k, v in HOST_STEPS.items() if v - h0.get(k, 0)}
+            if self.device.type == "cuda":
+                txt += "\nhost steps: " + (", ".join(f"{k} x{v}" for k, v in host.items()) if host else "none")
             if ctx.spans:
                 txt += "\nphases (inclusive, synchronised):\n" + ctx.span_report()
             rows_p = [txt]

@@ -344,12 +344,10 @@ class Evaluator:
         if t.is_string:
             if src.is_string:
                 return v
-            arr = v.to_arrow()
             if src.is_decimal or src.kind in ("date32",) or src.is_numeric or src.kind == "bool":
-                return Column.from_arrow(pc.cast(arr, pa.large_string()), device=v.device, dict_encode=False)
+                return S.to_string(v)       # GPU text formatting (strexpr.hip)
         if src.is_string:
-            arr = S.decode(v).to_arrow()
-            return Column.from_arrow(pc.cast(arr, t.to_arrow()), device=v.device, dtype=t)
+            return S.parse(v, t)            # GPU parse (strexpr.hip); malformed -> error
         if t.kind == "bool":
             return Column(t, v.data != 0, v.valid)
         if src.kind == "null":
@@ -395,14 +393,23 @@ class Evaluator:
                                         valid if valid is not None else torch.ones(n, dtype=torch.bool, device=dev))
             dic = Column.from_arrow(pa.array(lits or [""], pa.large_string()), device=dev, dict_encode=False)
             return Column(T.UTF8, codes, valid, dictionary=dic)
-        # general case: host assembly (rare)
-        masks = [m.cpu().numpy() for m, _ in vals]
-        arrays = [(pa.array([v.value] * n, pa.large_string()) if isinstance(v, Scalar) else S.decode(v).to_arrow())
-                  for v in branches]
-        out = arrays[-1]
-        for m, arr in reversed(list(zip(masks, arrays[:-1]))):
-            out = pc.if_else(pa.array(m), arr, out)
-        return Column.from_arrow(out, device=dev)
+        # general case: the first matching WHEN picks its branch (else the
+        # ELSE branch); one device string gather assembles the rows
+        choice = torch.full((n,), len(vals), dtype=torch.int64, device=dev)
+        for k in range(len(vals) - 1, -1, -1):
+            choice = torch.where(vals[k][0], torch.full_like(choice, k), choice)
+        return S.select_rows([self._str_col(v, dev) for v in branches], choice, n)
+
+    @staticmethod
+    def _str_col(v, dev) -> Column:
+        """A string operand as a column (a scalar becomes a one-row constant;
+        NULL a one-row NULL)."""
+        if isinstance(v, Scalar):
+            if v.value is None:
+                c = S.const_column("", dev)
+                return Column(T.UTF8, c.data, torch.zeros(1, dtype=torch.bool, device=dev), offsets=c.offsets)
+            return S.const_column(str(v.value), dev)
+        return v
 
     def _InList(self, e: InList, b: Batch) -> Value:
         v = self.eval(e.x, b)
@@ -451,12 +458,7 @@ class Evaluator:
         if name == "add_months":
             months, days = e.options
             c = args[0]
-            d = c.data.cpu().numpy().astype("int64").astype("datetime64[D]")
-            mon = d.astype("datetime64[M]") + np.timedelta64(months, "M")
-            day = (d - d.astype("datetime64[M]")).astype(np.int64)
-            nxt = (mon + np.timedelta64(1, "M")).astype("datetime64[D]")
-            res = np.minimum(mon.astype("datetime64[D]") + day, nxt - np.timedelta64(1, "D")) + np.timedelta64(days, "D")
-            return Column(T.DATE32, torch.from_numpy(res.astype(np.int64).astype(np.int32)).to(c.device), c.valid)
+            return Column(T.DATE32, add_months(c.data, months, days), c.valid)
         if name == "abs":
             c = args[0]
             return Column(c.dtype, c.data.abs(), c.valid)
@@ -478,8 +480,9 @@ class Evaluator:
         if name == "coalesce":
             return self._coalesce(e, args, b)
         if name == "concat":
-            l, r = [a if isinstance(a, Column) else Column.full(a.value, T.UTF8, b.num_rows, self.device(b)) for a in args]
-            return S.concat(S.decode(l), S.decode(r))
+            dev = self.device(b)
+            l, r = [self._str_col(a, dev) if isinstance(a, Scalar) else a for a in args]
+            return S.concat(l, r, b.num_rows)
         if name in ("sqrt", "ln", "log10", "exp", "floor", "ceil"):
             c = args[0]
             x = _convert_tensor(c, T.FLOAT64)
@@ -531,9 +534,17 @@ class Evaluator:
         dev = self.device(b)
         t = e.dtype
         if t.is_string:
-            arrs = [(pa.array([a.value] * n, pa.large_string()) if isinstance(a, Scalar) else S.decode(a).to_arrow())
-                    for a in args]
-            return Column.from_arrow(pc.coalesce(*arrs), device=dev)
+            # first non-NULL argument per row, assembled by one device gather
+            choice = torch.full((n,), len(args) - 1, dtype=torch.int64, device=dev)
+            for k in range(len(args) - 2, -1, -1):
+                a = args[k]
+                if isinstance(a, Scalar):
+                    if a.value is not None:
+                        choice = torch.full_like(choice, k)
+                    continue
+                ok = a.valid if a.valid is not None else torch.ones(n, dtype=torch.bool, device=dev)
+                choice = torch.where(ok, torch.full_like(choice, k), choice)
+            return S.select_rows([self._str_col(a, dev) for a in args], choice, n)
         out, valid = _full_of(args[-1], t, n, dev)
         for a in reversed(args[:-1]):
             x, xv = _full_of(a, t, n, dev)
@@ -543,6 +554,37 @@ class Evaluator:
             out = torch.where(xv, x, out)
             valid = xv | valid if valid is not None else None
         return Column(t, out, valid)
+
+
+def add_months(days: torch.Tensor, months: int, extra_days: int = 0) -> torch.Tensor:
+    """date32 + INTERVAL 'n' MONTH (+ days) on the device: civil date from
+    days (Hinnant), month arithmetic, day clamped to the target month's
+    length (Jan 31 + 1 month = Feb 28/29), back to days — integer tensor ops,
+    no host round trip."""
+    z = days.to(torch.int64) + 719468
+    era = torch.div(z, 146097, rounding_mode="floor")      # floor division: no negative-year adjustment
+    doe = z - era * 146097
+    yoe = torch.div(doe - torch.div(doe, 1460, rounding_mode="floor") + torch.div(doe, 36524, rounding_mode="floor")
+                    - torch.div(doe, 146096, rounding_mode="floor"), 365, rounding_mode="floor")
+    doy = doe - (365 * yoe + torch.div(yoe, 4, rounding_mode="floor") - torch.div(yoe, 100, rounding_mode="floor"))
+    mp = torch.div(5 * doy + 2, 153, rounding_mode="floor")
+    d = doy - torch.div(153 * mp + 2, 5, rounding_mode="floor") + 1
+    m = torch.where(mp < 10, mp + 3, mp - 9)
+    y = yoe + era * 400 + (m <= 2).to(torch.int64)
+    k = y * 12 + (m - 1) + months
+    y2 = torch.div(k, 12, rounding_mode="floor")
+    m2 = k - y2 * 12 + 1
+    leap = ((y2 % 4 == 0) & (y2 % 100 != 0)) | (y2 % 400 == 0)
+    mdays = torch.tensor([31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31], dtype=torch.int64,
+                         device=days.device).index_select(0, m2 - 1) + (leap & (m2 == 2)).to(torch.int64)
+    d2 = torch.minimum(d, mdays)
+    # days_from_civil
+    yy = y2 - (m2 <= 2).to(torch.int64)
+    era2 = torch.div(yy, 400, rounding_mode="floor")
+    yoe2 = yy - era2 * 400
+    doy2 = torch.div(153 * torch.where(m2 > 2, m2 - 3, m2 + 9) + 2, 5, rounding_mode="floor") + d2 - 1
+    doe2 = yoe2 * 365 + torch.div(yoe2, 4, rounding_mode="floor") - torch.div(yoe2, 100, rounding_mode="floor") + doy2
+    return (era2 * 146097 + doe2 - 719468 + extra_days).to(torch.int32)
 
 
 # =============================================================== conversions

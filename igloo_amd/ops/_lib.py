@@ -114,11 +114,23 @@ def set_capturing(on: bool) -> None:
     _capture.on = on
 
 
+#: host steps a GPU query took (name -> count): work that left the device
+#: (exec/expr_eval.py, ops/strings.py); EXPLAIN ANALYZE lists them and the GPU
+#: tests assert the TPC-H / reference-compat queries take none
+HOST_STEPS: "collections.Counter[str]" = collections.Counter()
+
+
+def note_host_step(what: str) -> None:
+    HOST_STEPS[what] += 1
+
+
 def device_ints(values, device, dtype=torch.int64) -> torch.Tensor:
     """Host ints -> a device tensor without a synchronizing copy: staged in
     pinned memory and copied stream-ordered. Under graph capture the copy is a
     graph node that reads the pinned buffer at every replay, so the buffer is
     kept alive with the capture (``capture_keepalive``)."""
+    if torch.device(device).type != "cuda":
+        return torch.tensor(values, dtype=dtype, device=device)
     h = torch.tensor(values, dtype=dtype).pin_memory()
     if getattr(_capture, "on", False):
         keep = getattr(_capture, "keep", None)

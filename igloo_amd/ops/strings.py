@@ -1,9 +1,12 @@
-"""String operators (csrc/kernels/strings.hip).
+"""String operators (csrc/kernels/strings.hip, strexpr.hip).
 
 Dictionary-encoded columns (low cardinality, e.g. p_type, l_shipmode) are
-evaluated once per distinct value on the host dictionary and mapped to rows
-through a code lookup table; plain columns (comments, names) run per-row HIP
-kernels on the GPU and pyarrow.compute on the CPU.
+evaluated once per distinct value — on the GPU by running the plain-string
+kernel over the dictionary's own device column — and mapped to rows through a
+code lookup table; plain columns (comments, names) run per-row HIP kernels on
+the GPU and pyarrow.compute on the CPU (the CPU engine's reference path).
+What still leaves the GPU (non-ASCII case mapping, float text formatting) is
+counted by ``note_host_step`` and reported by EXPLAIN ANALYZE.
 """
 from __future__ import annotations
 
@@ -18,7 +21,7 @@ import torch
 from .. import types as T
 from ..columnar import Column
 from .gather import gather_tensor
-from ._lib import capturing, check_not_capturing, is_gpu, launch, ptr, stream, to_host_int
+from ._lib import capturing, check_not_capturing, device_ints, is_gpu, launch, note_host_step, ptr, stream, to_host_int
 from .gather import take
 from .hashing import group_ids
 from .select import offsets_from_lengths
@@ -111,6 +114,28 @@ def _lut_apply(col: Column, lut_vals, key=None) -> torch.Tensor:
     return gather_tensor(lut, col.data)
 
 
+def _dict_lut_dev(col: Column, key, plain_fn) -> torch.Tensor:
+    """Per-code result of ``plain_fn`` evaluated over the dictionary's own
+    (plain, device) string column — the dictionary never leaves the GPU —
+    then gathered by the codes. The table is kept on the dictionary (not
+    while a graph is being captured: its contents would only exist inside
+    that graph's replays)."""
+    from ._lib import capturing
+    d = col.dictionary
+    cache = d.derived()
+    lut = cache.get(key)
+    if lut is None:
+        dp = decode(d) if d.is_dict else d
+        lut = plain_fn(dp)
+        if dp.valid is not None:
+            lut = lut & dp.valid if lut.dtype == torch.bool else torch.where(dp.valid, lut, torch.zeros_like(lut))
+        if not capturing():
+            cache[key] = lut
+    if lut.numel() == 0:
+        return torch.zeros(len(col), dtype=lut.dtype, device=col.device)
+    return gather_tensor(lut, col.data)
+
+
 _CONSTS: dict = {}
 
 
@@ -134,6 +159,9 @@ def _with_valid(values: torch.Tensor, col: Column) -> Tuple[torch.Tensor, Option
 def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, escape: Optional[str] = "\\") -> torch.Tensor:
     """Bool tensor (NULL rows are False; callers combine ``col.valid``)."""
     if col.is_dict:
+        if is_gpu(col.data):
+            return _dict_lut_dev(col, ("like", pattern, ci, negate, escape),
+                                 lambda d: like(d, pattern, ci, negate, escape))
         def build():
             rx = like_regex(pattern, ci, escape)
             return [(v is not None and rx.fullmatch(v) is not None) != negate for v in col.dict_values()]
@@ -169,6 +197,8 @@ def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, esca
 # --------------------------------------------------------------- comparisons
 def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
     if col.is_dict:
+        if is_gpu(col.data):
+            return _dict_lut_dev(col, ("cmp", op, value), lambda d: compare_const(d, op, value))
         import operator as o
         f = {"=": o.eq, "<>": o.ne, "<": o.lt, "<=": o.le, ">": o.gt, ">=": o.ge}[op]
         vb = value.encode("utf-8")
@@ -191,6 +221,8 @@ def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
 
 def in_list(col: Column, values: Sequence[str]) -> torch.Tensor:
     if col.is_dict:
+        if is_gpu(col.data):
+            return _dict_lut_dev(col, ("in", tuple(values)), lambda d: in_list(d, values))
         s = set(values)
         return _lut_apply(col, lambda: [v in s for v in col.dict_values()], ("in", tuple(values))).to(torch.bool)
     out = None
@@ -201,7 +233,18 @@ def in_list(col: Column, values: Sequence[str]) -> torch.Tensor:
 
 
 # ------------------------------------------------------------ transformations
-def _dict_transform(col: Column, fn) -> Column:
+def _dict_transform(col: Column, fn, plain_fn=None) -> Column:
+    """A string -> string function over a dictionary column: applied to the
+    dictionary's values only. On the GPU (``plain_fn`` = the same function
+    over a plain device column) the transformed values are re-encoded on the
+    device (equal results share one code) and the codes remapped by a gather."""
+    if plain_fn is not None and is_gpu(col.data):
+        d = col.dictionary
+        dp = decode(d) if d.is_dict else d
+        enc = dict_encode(plain_fn(dp))
+        remap = enc.data.to(torch.int32)
+        codes = gather_tensor(remap, col.data) if len(dp) else col.data
+        return Column(T.UTF8, codes, col.valid, dictionary=enc.dictionary)
     vals = [None if v is None else fn(v) for v in col.dict_values()]
     uniq, remap = {}, []
     for v in vals:
@@ -235,7 +278,7 @@ def lower(col: Column) -> Column:
 
 def _case(col: Column, up: bool) -> Column:
     if col.is_dict:
-        return _dict_transform(col, str.upper if up else str.lower)
+        return _dict_transform(col, str.upper if up else str.lower, lambda d: _case(d, up))
     if not is_gpu(col.data):
         return _host_roundtrip(col, pc.utf8_upper if up else pc.utf8_lower)
     out = torch.empty_like(col.data)
@@ -244,6 +287,7 @@ def _case(col: Column, up: bool) -> Column:
     if to_host_int(flag):
         # non-ASCII bytes present: full Unicode case mapping can change byte
         # lengths ('ß' -> 'SS'), so take the exact host path.
+        note_host_step("upper/lower of non-ASCII text")
         return _host_roundtrip(col, pc.utf8_upper if up else pc.utf8_lower)
     return Column(T.UTF8, out, col.valid, offsets=col.offsets)
 
@@ -258,7 +302,7 @@ def _py_substr(s: str, start: int, length: Optional[int]) -> str:
 
 def substr(col: Column, start: int, length: Optional[int]) -> Column:
     if col.is_dict:
-        return _dict_transform(col, lambda s: _py_substr(s, start, length))
+        return _dict_transform(col, lambda s: _py_substr(s, start, length), lambda d: substr(d, start, length))
     n = len(col)
     if not is_gpu(col.data):
         vals = [None if v is None else _py_substr(v, start, length) for v in col.to_pylist()]
@@ -278,17 +322,160 @@ def substr(col: Column, start: int, length: Optional[int]) -> Column:
 
 
 def char_length(col: Column) -> torch.Tensor:
+    """Characters (UTF-8 code points) per row, int32 (NULL rows: 0)."""
     if col.is_dict:
+        if is_gpu(col.data):
+            return _dict_lut_dev(col, ("char_length",), char_length).to(torch.int32)
         return _lut_apply(col, lambda: [0 if v is None else len(v) for v in col.dict_values()],
                           ("char_length",)).to(torch.int32)
-    arr = col.to_arrow()
-    r = pc.utf8_length(arr).fill_null(0).to_numpy(zero_copy_only=False)
-    return torch.from_numpy(r.astype(np.int32)).to(col.device)
+    if not is_gpu(col.data):
+        arr = col.to_arrow()
+        r = pc.utf8_length(arr).fill_null(0).to_numpy(zero_copy_only=False)
+        return torch.from_numpy(r.astype(np.int32)).to(col.device)
+    n = len(col)
+    out = torch.empty(n, dtype=torch.int32, device=col.device)
+    launch("str_char_length").str_char_length(ptr(col.offsets), ptr(col.data), n, ptr(out), stream(out))
+    return out
 
 
-def concat(a: Column, b: Column) -> Column:
-    arr = pc.binary_join_element_wise(a.to_arrow(), b.to_arrow(), "")
-    return Column.from_arrow(arr, device=a.device)
+def const_column(value: str, device) -> Column:
+    """One-row plain string column (a constant operand broadcast by the kernels)."""
+    b = value.encode("utf-8")
+    key = ("const_col", value, str(device))
+    def build():
+        return (torch.tensor(list(b) or [0], dtype=torch.uint8).to(device)[:len(b)],
+                torch.tensor([0, len(b)], dtype=torch.int64).to(device))
+    chars, off = _consts(key, build)
+    return Column(T.UTF8, chars, None, offsets=off)
+
+
+def concat(a: Column, b: Column, n: Optional[int] = None) -> Column:
+    """a || b (NULL when either side is NULL). Either side may be a one-row
+    constant column broadcast over ``n`` rows."""
+    n = n if n is not None else max(len(a), len(b))
+    if not is_gpu(a.data if len(a) else b.data):
+        aa, bb = a.to_arrow().cast(pa.large_string()), b.to_arrow().cast(pa.large_string())
+        if len(aa) == 1 and n != 1:
+            aa = pa.array([aa[0].as_py()] * n, pa.large_string())
+        if len(bb) == 1 and n != 1:
+            bb = pa.array([bb[0].as_py()] * n, pa.large_string())
+        return Column.from_arrow(pc.binary_join_element_wise(aa, bb, pa.scalar("", pa.large_string())), device=a.device)
+    a, b = decode(a), decode(b)
+    ba, bb_ = len(a) == 1 and n != 1, len(b) == 1 and n != 1
+    N = launch("str_concat")
+    s = stream(a.offsets)
+    lens = torch.empty(n, dtype=torch.int64, device=a.device)
+    N.str_concat2_lengths(ptr(a.offsets), ba, ptr(b.offsets), bb_, n, ptr(lens), s)
+    off, total = offsets_from_lengths(lens)
+    chars = torch.empty(total, dtype=torch.uint8, device=a.device)
+    if total:
+        N.str_concat2_copy(ptr(a.offsets), ptr(a.data), ba, ptr(b.offsets), ptr(b.data), bb_, n, ptr(off), ptr(chars), s)
+    va = None if a.valid is None else (a.valid.expand(n) if ba else a.valid)
+    vb = None if b.valid is None else (b.valid.expand(n) if bb_ else b.valid)
+    valid = va if vb is None else (vb if va is None else va & vb)
+    return Column(T.UTF8, chars, valid.contiguous() if valid is not None else None, offsets=off)
+
+
+#: fmt / parse kinds of the strexpr kernels
+_FMT_FIXED, _FMT_I32, _FMT_DATE, _FMT_BOOL = 0, 1, 2, 3
+
+
+def to_string(col: Column) -> Column:
+    """CAST(x AS VARCHAR) on the GPU for integers, decimals (text at the
+    type's scale), dates (ISO) and booleans. Floats keep the host formatter
+    (shortest round-trip text), reported as a host step."""
+    t = col.dtype
+    n = len(col)
+    x = col.data
+    if t.is_decimal and col.is_wide:
+        kind = None
+    elif t.is_decimal or t.kind in ("int64",) or (t.is_integer and x.dtype == torch.int64):
+        kind, scale, x = _FMT_FIXED, (t.scale if t.is_decimal else 0), x.to(torch.int64).contiguous()
+    elif t.is_integer:
+        kind, scale, x = _FMT_I32, 0, x.to(torch.int32).contiguous()
+    elif t.kind == "date32":
+        kind, scale, x = _FMT_DATE, 0, x.to(torch.int32).contiguous()
+    elif t.kind == "bool":
+        kind, scale, x = _FMT_BOOL, 0, x.to(torch.uint8).contiguous()
+    else:
+        kind = None
+    if kind is None or not is_gpu(x):
+        if is_gpu(x):
+            note_host_step(f"CAST({t} AS VARCHAR)")
+        return Column.from_arrow(pc.cast(col.to_arrow(), pa.large_string()), device=col.device, dict_encode=False)
+    N = launch("fmt")
+    s = stream(x)
+    valid = col.valid.to(torch.uint8).contiguous() if col.valid is not None else None
+    lens = torch.empty(n, dtype=torch.int64, device=x.device)
+    N.fmt_lengths(ptr(x), kind, n, scale, ptr(valid), ptr(lens), s)
+    off, total = offsets_from_lengths(lens)
+    chars = torch.empty(total, dtype=torch.uint8, device=x.device)
+    if total:
+        N.fmt_write(ptr(x), kind, n, scale, ptr(valid), ptr(off), ptr(chars), s)
+    return Column(T.UTF8, chars, col.valid, offsets=off)
+
+
+def parse(col: Column, t) -> Column:
+    """CAST(varchar AS t) on the GPU: integers, decimals (exact at t's scale),
+    dates, doubles and booleans; a malformed value raises ExecutionError."""
+    from ..utils.errors import ExecutionError
+    c = decode(col)
+    n = len(c)
+    if not is_gpu(c.data):
+        return Column.from_arrow(pc.cast(c.to_arrow(), t.to_arrow()), device=c.device, dtype=t)
+    if t.is_decimal:
+        kind, scale, dt = 2, t.scale, torch.int64
+    elif t.kind == "date32":
+        kind, scale, dt = 3, 0, torch.int32
+    elif t.is_float:
+        kind, scale, dt = 4, 0, torch.float64
+    elif t.kind == "bool":
+        kind, scale, dt = 5, 0, torch.uint8
+    elif t.is_integer:
+        kind, scale, dt = (0, 0, torch.int64) if t.torch_dtype == torch.int64 else (1, 0, torch.int32)
+    else:
+        note_host_step(f"CAST(VARCHAR AS {t})")
+        return Column.from_arrow(pc.cast(c.to_arrow(), t.to_arrow()), device=c.device, dtype=t)
+    out = torch.empty(n, dtype=dt, device=c.device)
+    err = torch.zeros(1, dtype=torch.int32, device=c.device)
+    valid = c.valid.to(torch.uint8).contiguous() if c.valid is not None else None
+    launch("str_parse").str_parse(ptr(c.offsets), ptr(c.data), n, ptr(valid), kind, scale, ptr(out), ptr(err),
+                                  stream(out))
+    if to_host_int(err):
+        raise ExecutionError(f"cannot cast string value to {t}")
+    if dt == torch.uint8:
+        out = out.to(torch.bool)
+    elif t.torch_dtype != dt and t.kind != "date32":
+        out = out.to(t.torch_dtype)
+    return Column(t, out, c.valid)
+
+
+def select_rows(branches: Sequence[Column], choice: torch.Tensor, n: int) -> Column:
+    """Row i takes row i of ``branches[choice[i]]`` (a one-row branch is a
+    constant). Every branch is appended into one plain column and a single
+    device string gather picks the rows: CASE / COALESCE over strings."""
+    parts, base = [], []
+    pos = 0
+    for br in branches:
+        p = decode(br)
+        if p.valid is None:
+            p = Column(T.UTF8, p.data, torch.ones(len(p), dtype=torch.bool, device=p.device), offsets=p.offsets)
+        parts.append(p)
+        base.append(pos)
+        pos += len(p)
+    offs = [parts[0].offsets]
+    shift = parts[0].offsets[-1:]
+    for p in parts[1:]:
+        offs.append(p.offsets[1:] + shift)
+        shift = shift + p.offsets[-1:]
+    allc = Column(T.UTF8, torch.cat([p.data for p in parts]), torch.cat([p.valid for p in parts]),
+                  offsets=torch.cat(offs))
+    rows = torch.arange(n, dtype=torch.int64, device=choice.device)
+    starts = device_ints(base, choice.device)
+    single = device_ints([int(len(p) == 1 and n != 1) for p in parts], choice.device).bool()
+    ch = choice.to(torch.int64)
+    idx = starts.index_select(0, ch) + torch.where(single.index_select(0, ch), torch.zeros_like(rows), rows)
+    return take(allc, idx)
 
 
 # ------------------------------------------------------------------ encoding
