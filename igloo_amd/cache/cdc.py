@@ -138,6 +138,19 @@ class CdcManager:
             log.info("cdc: %s changed, invalidated %d cache entries", table, n)
 
 
+def _slice(c, a: int, b: int):
+    """Rows [a, b) of a resident column as views (string bytes re-based; the
+    byte bounds come through the replayable readback path)."""
+    from ..columnar import Column
+    from ..ops._lib import to_host_ints
+    valid = None if c.valid is None else c.valid[a:b]
+    if c.offsets is not None:
+        off = c.offsets[a:b + 1]
+        lo, hi = to_host_ints(off[[0, -1]]) if b > a else (0, 0)
+        return Column(c.dtype, c.data[lo:hi], valid, offsets=off - lo)
+    return Column(c.dtype, c.data[a:b], valid, dictionary=c.dictionary)
+
+
 class CachedTable(TableSource):
     """Serve scans of ``source`` from the cache tier, keyed by the CDC version.
 
@@ -151,8 +164,6 @@ class CachedTable(TableSource):
     TieredCache's (config ``cache_hbm_gb`` / ``cache_host_gb`` / ``cache_dir``).
     """
 
-    #: cached scans hand out whole resident columns (no statistics pruning)
-    prunes = False
     cacheable = False
 
     def __init__(self, name: str, source: TableSource, cache: TieredCache, cdc: Optional[CdcManager] = None,
@@ -168,6 +179,10 @@ class CachedTable(TableSource):
         self.partitioned_by = getattr(source, "partitioned_by", None)
         self.replicated = getattr(source, "replicated", False)
         self.hits = self.misses = 0
+        #: row-group statistics pruning on the cached path (see ``_prune_rows``)
+        self.last_prune_stats: dict = {}
+        self._ranges_cache: dict = {}
+        self._prune_memo: dict = {}
         if cdc is not None:
             probe = (lambda s=source: getattr(s, "version", None)) if hasattr(type(source), "version") else None
             cdc.track(name, probe)
@@ -177,6 +192,11 @@ class CachedTable(TableSource):
         if item == "source":
             raise AttributeError(item)
         return getattr(self.source, item)
+
+    @property
+    def prunes(self) -> bool:
+        """Scans take pushed filters when the source keeps row-group statistics."""
+        return bool(getattr(self.source, "prunes", False)) and hasattr(self.source, "prune")
 
     def schema(self):
         return self.source.schema()
@@ -203,7 +223,74 @@ class CachedTable(TableSource):
     def cdc_version(self):
         return self.cdc.version(self.name) if self.cdc is not None else None
 
-    def scan(self, columns: Sequence[str], ctx) -> Batch:
+    def _prune_rows(self, ctx, filters):
+        """Rows of the resident columns that the source's row-group statistics
+        cannot rule out: None (all rows), a (start, stop) slice, or a device
+        index vector. Resident columns concatenate this rank's row groups in
+        ``my_row_groups`` order, so a kept row group is a row range of them."""
+        src = self.source
+        groups = src.my_row_groups(ctx)
+        # the statistics walk is host work over every row group's footer
+        # entries: memoised per filter set and source version
+        mkey = (repr(filters), getattr(src, "_stat_version", None), len(groups),
+                ctx.comm.rank if ctx is not None and ctx.comm is not None else 0)
+        keep = self._prune_memo.get(mkey)
+        if keep is None:
+            keep = src.prune(groups, filters)
+            if len(self._prune_memo) > 256:
+                self._prune_memo.clear()
+            self._prune_memo[mkey] = keep
+        self.last_prune_stats = {"row_groups": len(groups), "row_groups_read": len(keep),
+                                 "row_groups_pruned": len(groups) - len(keep)}
+        if len(keep) == len(groups):
+            return None
+        kept = set(keep)
+        ranges, pos = [], 0
+        for fi, rg in groups:
+            n = src._meta[fi].row_group(rg).num_rows
+            if (fi, rg) in kept:
+                if ranges and ranges[-1][1] == pos:
+                    ranges[-1] = (ranges[-1][0], pos + n)
+                else:
+                    ranges.append((pos, pos + n))
+            pos += n
+        if not ranges:
+            return (0, 0)
+        if len(ranges) == 1:
+            return ranges[0]
+        key = (tuple(ranges), str(ctx.device) if ctx is not None else "cpu")
+        idx = self._ranges_cache.get(key)
+        if idx is None:
+            import torch
+            from ..ops._lib import device_ints
+            lens = [b - a for a, b in ranges]
+            starts = device_ints([a for a, _ in ranges], ctx.device)
+            rep = torch.repeat_interleave(starts, device_ints(lens, ctx.device), output_size=sum(lens))
+            first = device_ints([0] + list(__import__("itertools").accumulate(lens))[:-1], ctx.device)
+            pos_in = torch.arange(sum(lens), device=ctx.device) - torch.repeat_interleave(
+                first, device_ints(lens, ctx.device), output_size=sum(lens))
+            idx = rep + pos_in
+            if len(self._ranges_cache) > 64:
+                self._ranges_cache.clear()
+            self._ranges_cache[key] = idx
+        return idx
+
+    def scan(self, columns: Sequence[str], ctx, filters=None) -> Batch:
+        b = self._scan_all(columns, ctx)
+        if not filters or not self.prunes:
+            self.last_prune_stats = {}
+            return b
+        rows = self._prune_rows(ctx, filters)
+        if rows is None:
+            return b
+        if isinstance(rows, tuple):
+            a, z = rows
+            return Batch({c: _slice(col, a, z) for c, col in b.columns.items()}, z - a)
+        from ..ops.gather import take_many
+        keys = list(b.columns)
+        return Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], rows))), int(rows.numel()))
+
+    def _scan_all(self, columns: Sequence[str], ctx) -> Batch:
         ver = None
         if self.cdc is not None:
             self.cdc.maybe_poll(self.name, self.poll_interval_s)

@@ -126,3 +126,30 @@ def test_tpch_parquet_dataset_roundtrip(tmp_path):
         assert a.to_pylist() == b.to_pylist(), q
     li = os.path.join(parquet_gen.dataset_dir(str(tmp_path), 0.01), "lineitem")
     assert sorted(os.listdir(li))[0] == "part-00000.parquet"
+
+
+def test_row_group_pruning_on_the_cached_path(tmp_path):
+    """Statistics pruning also applies to scans served from the cache tier:
+    the resident column is complete (the fill reads every row group) and a
+    filtered scan hands out only the row ranges of the row groups the
+    statistics cannot rule out."""
+    n = 10_000
+    t = pa.table({"k": pa.array(range(n), pa.int64()),
+                  "d": pa.array([i % 97 for i in range(n)], pa.int32()),
+                  "s": pa.array([f"s{i // 1000}" for i in range(n)])})
+    pq.write_table(t, str(tmp_path / "t.parquet"), row_group_size=1000)
+    e = ig.QueryEngine(device="cpu")
+    src = e.register_parquet("t", str(tmp_path / "t.parquet"))      # cached (the default)
+    assert type(src).__name__ == "CachedTable" and src.prunes
+    for _ in range(2):   # miss (fill), then hit
+        r = e.query("SELECT count(*) AS n, sum(d) AS sd FROM t WHERE k >= 2500 AND k < 4000").to_pylist()
+        assert r == [{"n": 1500, "sd": sum(i % 97 for i in range(2500, 4000))}]
+        assert src.last_prune_stats == {"row_groups": 10, "row_groups_read": 2, "row_groups_pruned": 8}
+    assert src.hits >= 2
+    # two separate ranges (an index gather), strings included
+    r = e.query("SELECT count(*) AS n, min(s) AS lo, max(s) AS hi FROM t WHERE k IN (5, 9999)").to_pylist()
+    assert r == [{"n": 2, "lo": "s0", "hi": "s9"}] and src.last_prune_stats["row_groups_read"] == 2
+    r = e.query("SELECT count(*) AS n FROM t WHERE s = 's7'").to_pylist()
+    assert r == [{"n": 1000}] and src.last_prune_stats["row_groups_read"] == 1
+    e.query("SELECT count(*) AS n FROM t WHERE d = 3")
+    assert src.last_prune_stats.get("row_groups_pruned", 0) == 0
