@@ -330,6 +330,7 @@ def main():
             "rows_read_per_suite": int(scanned),
         }
         print(json.dumps(out), flush=True)
+    eng.close()              # query graphs hold RCCL resources (Communicator.shutdown)
     if comm is not None:
         comm.shutdown()
 

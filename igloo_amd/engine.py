@@ -329,10 +329,11 @@ class QueryEngine:
         from .ops._lib import HOST_STEPS
         h0 = sum(HOST_STEPS.values())
         with _trace.Range("query"):
-            batch, spec, st = self._execute_speculative(plan, ctx, key)
-        table = self._to_arrow(batch, plan.schema, bq_names)
-        if st is not None:
-            table = self._check_graph(st, spec, table, plan, bq_names, ctx)
+            batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
+        if table is None:
+            table = self._to_arrow(batch, plan.schema, bq_names)
+        if st is not None and spec in ("replayed", "recorded") and st["capture_next"]:
+            st["digest"] = digest(table)      # the next execution's graph must reproduce it
         self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
@@ -358,7 +359,7 @@ class QueryEngine:
     def make_context(self, analyze: bool = False) -> ExecContext:
         return ExecContext(self, self.device, self.comm, analyze)
 
-    def _execute_speculative(self, plan: Plan, ctx: ExecContext, key):
+    def _execute_speculative(self, plan: Plan, ctx: ExecContext, key, names=None):
         """Run the plan; for a repeated query over unchanged data, replay the
         host readbacks (sizes, ranges, strategy choices) of the previous
         executions instead of waiting on the device for each (ops/_lib.py
@@ -372,22 +373,27 @@ class QueryEngine:
 
         SPMD ranks (one per GPU) speculate too: replaying a readback changes
         only when the host waits, never which collectives a rank issues, so
-        ranks in different modes stay aligned. Every rank joins one tiny
-        all-reduce after each execution (validation agreement) and, when
-        graphs are possible, one before it (all ranks replay graphs, or none).
-        Graphs with collectives inside need a device transport (RCCL): a gloo
+        ranks in different modes stay aligned. Every rank joins ONE tiny
+        all-reduce after each execution: it agrees on the validation (and on
+        a fresh graph's first-result digest) and on whether every rank is
+        ready to capture, so ranks capture their query graphs together; a rank
+        that cannot runs eagerly, which issues the same collectives. Graphs
+        with collectives inside need a device transport (RCCL): a gloo
         (host-staged) group never captures."""
         from .ops import _lib
         spmd = self.comm is not None and self.comm.spmd
         if not (SPECULATE and key is not None and self.device.type == "cuda" and (not spmd or SPMD_SPECULATE)):
-            return self._execute_plan(plan, ctx), None, None
+            return self._execute_plan(plan, ctx), None, None, None
         comm = self.comm if spmd else None
         graphs_on = _graphs.GRAPHS and (comm is None or (comm.backend == "nccl" and SPMD_GRAPHS))
 
-        def agreed(ok: bool) -> bool:
-            # SPMD ranks decide together (every rank joins this collective after
-            # every speculative-capable execution, so the sequences stay aligned)
-            return ok if comm is None else comm.allreduce_ints([0 if ok else 1])[0] == 0
+        def agree(*flags: bool) -> List[bool]:
+            # SPMD ranks decide together: every rank joins this ONE tiny
+            # all-reduce after every speculative-capable execution, so their
+            # collective sequences stay aligned; a flag is set when any rank set it
+            if comm is None:
+                return [bool(f) for f in flags]
+            return [v > 0 for v in comm.allreduce_ints([int(bool(f)) for f in flags])]
         # CDC: a graph replay never reaches CachedTable.scan (where scans poll
         # their source), so the probes of the tables this query read last time
         # run here, rate-limited the same way; a changed source invalidates its
@@ -418,48 +424,42 @@ class QueryEngine:
                                      "cache_keys": ()}
             self._spec_current[key] = skey
         replay = st["log"] is not None and st["fails"] < 2
-        mode = "eager"
-        if graphs_on and not self.graphs_disabled and replay and st["fails"] == 0 and st["graph_aborts"] < 2:
+        g = st["graph"]
+        if g is not None and not g.current():
+            # the generated-kernel set changed: the recording diverges from
+            # here, and a new graph is captured once a replay completes again
+            self._set_graph(st, None)
+            g = None
+        if g is None and st["capture_next"] and graphs_on and replay and st["fails"] == 0 \
+                and st["graph_aborts"] < 2:
+            # capture_next was agreed by every rank, so ranks normally capture
+            # together; a rank whose capture is refused simply runs eagerly
+            # (a graph and an eager execution issue the same collectives)
+            st["capture_next"] = False
+            if self.graphs_disabled or not self._capture(st, plan):
+                st["graph_aborts"] += 1
             g = st["graph"]
-            if g is not None and not g.current():
-                # the generated-kernel set changed: the recording diverges from
-                # here, and a new graph is captured once a replay completes again
-                self._set_graph(st, None)
-                g = None
-            if g is not None:
-                mode = "graph"
-            elif st["capture_next"] and st["digest"] is not None and _jit.generation() is not None:
-                mode = "capture"
-        if comm is not None and graphs_on:
-            # all ranks run graphs or none: [ranks staying eager, ranks capturing]
-            n_eager, n_cap = comm.allreduce_ints([int(mode == "eager"), int(mode == "capture")])
-            if n_eager:
-                mode = "eager"
-            elif n_cap:
-                ok = True
-                if mode == "capture":
-                    ok = self._capture(st, plan)
-                if not agreed(ok):
-                    self._set_graph(st, None)
-                    mode = "eager"
-                else:
-                    # some rank replays a fresh graph for the first time: every
-                    # rank joins the digest agreement in _check_graph
-                    mode = "graph"
-                    st["check_all"] = True
-        elif mode == "capture":
-            mode = "graph" if self._capture(st, plan) else "eager"
-        if mode == "graph":
-            g = st["graph"]
+        if g is not None:
             ok = g.replay(ctx)
+            table = None
+            if ok and not g.checked:
+                # first replay: its result must equal the eager execution's
+                table = self._to_arrow(g.batch, plan.schema, names)
+                ok = digest(table) == st["digest"]
+                if not ok:
+                    log.warning("query graph result differs from the eager execution; graph dropped")
+                    _graphs.STATS["failed"] += 1
+                    st["graph_aborts"] = 2
             if comm is not None:
                 comm.calls += g.comm_calls
                 comm.bytes_sent += g.comm_bytes
-            if agreed(ok):
+            if not agree(not ok, True)[0]:
+                g.checked = True
                 self._touch_graph(st)
-                return g.batch, "graph", st
-            # a replayed value no longer matches the device (on some rank):
-            # eager, real readbacks
+                return g.batch, "graph", st, table
+            # a replayed value (or the first result) did not match on some
+            # rank: every rank drops its graph and re-executes eagerly with
+            # real readbacks (the same collectives on all)
             self._set_graph(st, None)
             st["fails"] += 1
             st["log"] = st["candidate"] = None
@@ -474,11 +474,18 @@ class QueryEngine:
             finally:
                 _lib.set_speculation(None)
             ok = sp.validate()
-            if agreed(ok):
+            # would this rank capture next time (a complete replay, or a
+            # recording confirmed by this run)? Agreed with the validation:
+            # ranks capture only together
+            ready = graphs_on and ok and st["fails"] == 0 and st["graph"] is None and st["graph_aborts"] < 2 \
+                and not self.graphs_disabled and _jit.generation() is not None and (
+                    sp.complete if sp.mode == "replay" else _confirm(st["candidate"], sp.log) is not None)
+            bad, not_ready = agree(not ok, not ready)
+            if not bad:
                 break
             # some rank's replayed value did not match its device: every rank
             # re-executes with real readbacks (the same collectives on all)
-            if replay and not ok:
+            if replay:
                 st["fails"] += 1
             st["log"] = st["candidate"] = None
             replay = False
@@ -486,31 +493,26 @@ class QueryEngine:
             log.warning("speculative readbacks did not match the device; re-executing")
         self._query_sources[key] = [s for s in ctx.sources if hasattr(s, "poll")]
         st["cache_keys"] = tuple(dict.fromkeys(ctx.cache_keys))
-        can_graph = graphs_on and st["fails"] == 0 and st["graph"] is None and st["graph_aborts"] < 2
+        if not bad and not not_ready:
+            st["capture_next"] = True       # _exec_query keeps this result's digest
         if sp.mode == "replay":
             if not sp.complete:
                 # the call sequence changed: this run's own sequence must be
                 # confirmed by the next execution before it is replayed
                 st["log"], st["candidate"] = None, sp.fresh
-            elif can_graph:
-                st["capture_next"] = True    # _check_graph keeps this result's digest
-            return batch, "replayed" if sp.complete else "partial", st
+            return batch, "replayed" if sp.complete else "partial", st, None
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
-        if st["log"] is not None and can_graph:
-            # a confirmed recording: the next execution captures it straight
-            # away (its graph is checked against this run's result digest)
-            st["capture_next"] = True
-        return batch, "recorded", st
+        return batch, "recorded", st, None
 
     def _capture(self, st: dict, plan: Plan) -> bool:
         """Capture ``plan`` under a replay of ``st``'s recording into a query graph."""
-        st["capture_next"] = False
+        if st["digest"] is None:
+            return False
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
         with _trace.Range("graph.capture"):
             g = _graphs.capture(self, plan, st["log"], self.make_context)
         if g is None:
-            st["graph_aborts"] += 1
             return False
         if self.comm is not None:
             # collectives recorded into the graph (counted again on every replay)
@@ -563,30 +565,19 @@ class QueryEngine:
             torch.cuda.empty_cache()      # the dropped graphs' private pools
         return n
 
-    def _check_graph(self, st: dict, spec, table: pa.Table, plan: Plan, names, ctx) -> pa.Table:
-        """Digest bookkeeping around query graphs (exec/graphs.py): the eager
-        result before a capture is digested; the graph's first result must
-        match it, otherwise the query is never captured again and this result
-        is recomputed eagerly (SPMD ranks agree on it: their results are
-        replicated, and all of them are on their first replay together)."""
-        if spec in ("replayed", "recorded") and st["capture_next"]:
-            st["digest"] = digest(table)
-        elif spec == "graph":
-            g = st["graph"]
-            check_all = st.pop("check_all", False)
-            if not g.checked or check_all:
-                ok = g.checked or digest(table) == st["digest"]
-                if check_all:
-                    ok = self.comm.allreduce_ints([0 if ok else 1])[0] == 0
-                if not ok:
-                    log.warning("query graph result differs from the eager execution; graph dropped")
-                    _graphs.STATS["failed"] += 1
-                    self._set_graph(st, None)
-                    st["graph_aborts"] = 2
-                    ctx.__init__(self, self.device, self.comm, ctx.analyze)
-                    return self._to_arrow(self._execute_plan(plan, ctx), plan.schema, names)
-                g.checked = True
-        return table
+    def close(self) -> None:
+        """Drop every query graph (and its memory pool). Call before tearing
+        down an RCCL process group: a live graph that captured collectives
+        keeps ``destroy_process_group`` from returning (scripts/rccl_probe.py)."""
+        for st in list(self._graphs.values()):
+            self._set_graph(st, None)
+        for st in self._spec.values():
+            st["graph"] = None
+        if self.device.type == "cuda":
+            import gc
+            gc.collect()
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
 
     def graph_pool(self):
         """The private memory pool every query graph of this engine captures into."""

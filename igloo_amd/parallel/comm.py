@@ -89,12 +89,19 @@ class Communicator:
             log.warning("communicator abort: %s", e)
 
     def shutdown(self):
+        """Barrier, then destroy the process group. Query graphs that captured
+        RCCL collectives must be released first (QueryEngine.close): while one
+        lives, destroy_process_group does not return."""
         if dist.is_initialized():
             try:
                 self.calls += 1
                 dist.barrier()
             except Exception:  # pragma: no cover
                 pass
+            if self.device.type == "cuda":
+                import gc
+                gc.collect()
+                torch.cuda.synchronize(self.device)
             dist.destroy_process_group()
 
     # ------------------------------------------------------------ primitives

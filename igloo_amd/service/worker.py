@@ -331,6 +331,7 @@ def main(argv=None) -> int:
         # broken group: leave without collective teardown (a peer is gone)
         sys.stdout.flush()
         os._exit(wg.exit_code)
+    engine.close()      # release query graphs (RCCL teardown waits on graph-held collectives)
     if comm is not None:
         comm.shutdown()
     return 0

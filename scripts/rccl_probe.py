@@ -42,31 +42,48 @@ for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, x[:200], 0), dist.P2POp(
 assert torch.equal(r, x[:200])
 print("step 11", flush=True)
 # collectives inside a captured HIP graph, replayed with new inputs
-src = torch.zeros(512, dtype=torch.int64, device=dev)
-dst = torch.empty_like(src)
-red = torch.zeros(8, dtype=torch.int64, device=dev)
-s = torch.cuda.Stream(dev)
-s.wait_stream(torch.cuda.current_stream(dev))
-with torch.cuda.stream(s):
-    dist.all_to_all_single(dst, src * 2, [512], [512]); dist.all_reduce(red)   # warm the communicator
-torch.cuda.current_stream(dev).wait_stream(s)
-torch.cuda.synchronize()
-print("step 12", flush=True)
-gr = torch.cuda.CUDAGraph()
-print("step 13", flush=True)
-with torch.cuda.graph(gr):
-    tmp = src * 2
-    dist.all_to_all_single(dst, tmp, [512], [512])
-    dist.all_reduce(red)
-    ag = torch.empty(512, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(ag, dst)
-for k in (1, 5):
-    src.copy_(torch.arange(512, device=dev) + k)
-    red.fill_(k)
-    gr.replay()
+if os.environ.get("PROBE_GRAPH", "1") == "1":
+    src = torch.zeros(512, dtype=torch.int64, device=dev)
+    dst = torch.empty_like(src)
+    red = torch.zeros(8, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        dist.all_to_all_single(dst, src * 2, [512], [512]); dist.all_reduce(red)   # warm the communicator
+    torch.cuda.current_stream(dev).wait_stream(s)
     torch.cuda.synchronize()
-    assert torch.equal(dst, (torch.arange(512, device=dev) + k) * 2), k
-    assert torch.equal(ag, dst) and red.tolist() == [k] * 8, k
-    print("step 14", flush=True)
-c.shutdown()
-print("RCCL_API_OK")
+    print("step 12", flush=True)
+    gr = torch.cuda.CUDAGraph()
+    print("step 13", flush=True)
+    with torch.cuda.graph(gr):
+        tmp = src * 2
+        dist.all_to_all_single(dst, tmp, [512], [512])
+        dist.all_reduce(red)
+        ag = torch.empty(512, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(ag, dst)
+    for k in (1, 5):
+        src.copy_(torch.arange(512, device=dev) + k)
+        red.fill_(k)
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(dst, (torch.arange(512, device=dev) + k) * 2), k
+        assert torch.equal(ag, dst) and red.tolist() == [k] * 8, k
+        print("step 14", flush=True)
+mode = os.environ.get("PROBE_SHUTDOWN", "comm")
+print("shutdown:", mode, flush=True)
+if mode == "comm":
+    c.shutdown()
+elif mode == "destroy":
+    dist.destroy_process_group()
+elif mode == "del_destroy":
+    import gc
+    gr = None
+    gc.collect()
+    torch.cuda.synchronize()
+    print("graph released", flush=True)
+    dist.destroy_process_group()
+elif mode == "barrier":
+    dist.barrier()
+    print("barrier done", flush=True)
+    dist.destroy_process_group()
+print("RCCL_API_OK", flush=True)
