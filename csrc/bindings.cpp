@@ -443,6 +443,10 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("const_ints", [](uintptr_t out, std::vector<int64_t> vals, uintptr_t s) {
+    kern::const_ints(P<int64_t>(out), vals.data(), (int64_t)vals.size(), S(s));
+  });
+  m.def("end_capture", [](uintptr_t s) { kern::end_capture(S(s)); });
   m.def("str_char_length", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t out, uintptr_t s) {
     kern::str_char_length(P<const int64_t>(off), P<const uint8_t>(chars), n, P<int32_t>(out), S(s));
   });

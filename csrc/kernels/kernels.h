@@ -67,6 +67,8 @@ void pack_rows(const PackSpec& spec, const void* perm, bool perm64, int64_t n, u
 void unpack_rows(const PackSpec& spec, const uint8_t* in, int64_t n, hipStream_t stream);
 
 // ---- util.hip -------------------------------------------------------------------
+void const_ints(int64_t* out, const int64_t* vals, int64_t n, hipStream_t stream);
+void end_capture(hipStream_t stream);
 void column_stats(const void* keys, bool key64, const uint8_t* valid, int64_t n, long long* out, hipStream_t stream);
 void run_bounds(const void* keys, bool key64, int64_t n, uint8_t* out, hipStream_t stream);
 

@@ -231,5 +231,40 @@ void avg_wide(const int64_t* sums, bool wide, const int64_t* cnt, int64_t n, int
   check_launch("util.avg_wide", stream);
 }
 
+// Small host constants written by a kernel whose arguments carry the values:
+// a graph-capturable "upload" (a host-to-device copy inside a captured HIP
+// graph is refused by the runtime, and would read host memory at replay).
+constexpr int kConstInts = 64;
+struct ConstInts {
+  int64_t v[kConstInts];
+};
+
+__global__ void const_ints_kernel(int64_t* __restrict__ out, int n, ConstInts vals) {
+  const int i = threadIdx.x;
+  if (i < n) out[i] = vals.v[i];
+}
+
+void const_ints(int64_t* out, const int64_t* vals, int64_t n, hipStream_t stream) {
+  for (int64_t base = 0; base < n; base += kConstInts) {
+    ConstInts c{};
+    const int k = (int)(n - base < kConstInts ? n - base : kConstInts);
+    for (int i = 0; i < k; ++i) c.v[i] = vals[base + i];
+    hipLaunchKernelGGL(const_ints_kernel, dim3(1), dim3(kConstInts), 0, stream, out + base, k, c);
+  }
+  check_launch("const_ints", stream);
+}
+
+// End a stream capture the runtime invalidated (the failed capture's graph
+// is discarded), so the thread can launch again.
+void end_capture(hipStream_t stream) {
+  hipStreamCaptureStatus st;
+  if (hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  (void)hipGetLastError();
+}
+
 }  // namespace kern
 }  // namespace igloo

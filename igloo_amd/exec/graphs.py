@@ -182,8 +182,14 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
             _note("aborted (sync): " + traceback.format_exc(limit=-4))
             return None
         # a HIP call the capture refused: the runtime invalidated the capture.
-        # This engine stops capturing (a failed capture's allocator state is
+        # End it for good (an invalidated capture can leave the stream in
+        # capture mode, and every later launch of this thread would fail);
+        # this engine stops capturing (a failed capture's allocator state is
         # not something to build on); the query stays eager.
+        try:
+            _lib.native().end_capture(s.cuda_stream)
+        except Exception:  # noqa: BLE001 - best effort
+            pass
         engine.graphs_disabled = True
         STATS["failed"] += 1
         _note("failed: " + traceback.format_exc(limit=-5))

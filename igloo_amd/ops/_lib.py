@@ -126,17 +126,19 @@ def note_host_step(what: str) -> None:
 
 def device_ints(values, device, dtype=torch.int64) -> torch.Tensor:
     """Host ints -> a device tensor without a synchronizing copy: staged in
-    pinned memory and copied stream-ordered. Under graph capture the copy is a
-    graph node that reads the pinned buffer at every replay, so the buffer is
-    kept alive with the capture (``capture_keepalive``)."""
+    pinned memory and copied stream-ordered; under graph capture (where the
+    runtime refuses host-to-device copies) written by a kernel whose
+    arguments carry the values."""
     if torch.device(device).type != "cuda":
         return torch.tensor(values, dtype=dtype, device=device)
-    h = torch.tensor(values, dtype=dtype).pin_memory()
     if getattr(_capture, "on", False):
-        keep = getattr(_capture, "keep", None)
-        if keep is None:
-            keep = _capture.keep = []
-        keep.append(h)
+        # inside a graph capture: the values travel as kernel arguments
+        vals = [int(v) for v in values]
+        out = torch.empty(len(vals), dtype=torch.int64, device=device)
+        if vals:
+            launch("const_ints").const_ints(out.data_ptr(), vals, torch.cuda.current_stream(out.device).cuda_stream)
+        return out if dtype == torch.int64 else out.to(dtype)
+    h = torch.tensor(values, dtype=dtype).pin_memory()
     return h.to(device, non_blocking=True)
 
 
