@@ -37,6 +37,7 @@ from ..ops.gather import gather_tensor
 from ..ops import misc as M
 from ..ops import strings as S
 from ..ops.gather import take_many
+from ..ops._lib import device_ints, to_host_ints
 from ..sql import logical as L
 from ..sql.expr import AggCall, ColRef, Expr
 from ..utils.errors import NotSupported
@@ -207,12 +208,11 @@ def _rebuild(cols: List[Column], spec, parts: List[torch.Tensor], chars: Dict[in
         valid = parts[vi] if vi is not None else None
         if c.is_plain_string:
             lens = parts[di]
-            off = torch.zeros(lens.numel() + 1, dtype=torch.int64, device=lens.device)
             if lens.numel():
-                from ..ops.select import exclusive_scan
-                ex, total = exclusive_scan(lens)
-                off[:-1] = ex
-                off[-1] = total
+                from ..ops.select import offsets_from_lengths
+                off, _ = offsets_from_lengths(lens)
+            else:
+                off = torch.zeros(1, dtype=torch.int64, device=lens.device)
             out.append(Column(c.dtype, chars[j], valid, offsets=off))
         else:
             out.append(Column(c.dtype, parts[di], valid, dictionary=c.dictionary))
@@ -242,7 +242,7 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
         if c.is_plain_string:
             g = take(c, perm)
             sgath[j] = g
-            offs = g.offsets.index_select(0, torch.as_tensor(bounds, device=g.offsets.device)).tolist()
+            offs = to_host_ints(g.offsets.index_select(0, device_ints(bounds, g.offsets.device)))
             sbytes.append([offs[r + 1] - offs[r] for r in range(W)])
     mat = [[send[r]] + [sb[r] for sb in sbytes] for r in range(W)]
     rmat = comm.all_to_all_matrix(mat)

@@ -72,6 +72,9 @@ if os.environ.get("PROBE_GRAPH", "1") == "1":
 mode = os.environ.get("PROBE_SHUTDOWN", "comm")
 print("shutdown:", mode, flush=True)
 if mode == "comm":
+    # a live graph that captured collectives keeps destroy_process_group from
+    # returning (PROBE_SHUTDOWN=destroy shows it): release it first
+    gr = None
     c.shutdown()
 elif mode == "destroy":
     dist.destroy_process_group()
