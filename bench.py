@@ -218,6 +218,7 @@ def main():
             print(f"[bench] step {s}: {time.perf_counter() - t1:.3f}s cumulative", file=sys.stderr, flush=True)
     barrier()
     elapsed = time.perf_counter() - t1
+    timed_modes = dict(spec_modes)
     if comm is not None:
         elapsed = comm.allreduce_max_float(elapsed)
     step_s = elapsed / max(a.steps, 1)
@@ -320,7 +321,7 @@ def main():
             "cold_s": round(cold_s, 4),
             # timed-step queries whose host readbacks were replayed and validated
             # on the device (engine.QueryEngine._execute_speculative)
-            "speculation": {str(k): v for k, v in spec_modes.items()},
+            "speculation": {str(k): v for k, v in timed_modes.items()},
             "jit": {"wait_s": round(jit_wait_s, 3), "kernels_compiled": _jit.STATS["compiled"],
                     "disk_hits": _jit.STATS["disk_hits"], "failed": _jit.STATS["failed"]},
             "load": load,

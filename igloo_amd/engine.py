@@ -424,7 +424,7 @@ class QueryEngine:
                                      "cache_keys": ()}
             self._spec_current[key] = skey
         replay = st["log"] is not None and st["fails"] < 2
-        g = st["graph"]
+        g = st["graph"] if graphs_on else None
         if g is not None and not g.current():
             # the generated-kernel set changed: the recording diverges from
             # here, and a new graph is captured once a replay completes again

@@ -317,7 +317,7 @@ class ScanExec(ExecNode):
                     idx = mask_to_indices(m)
                 hit = ctx.scan_cache[key] = (idx, {})
             idx, taken_by_name = hit
-            if self.late_ok and LATE_SCAN and not ctx.spmd and ctx.device.type == "cuda":
+            if self.late_ok and LATE_SCAN and ctx.device.type == "cuda":
                 # index form: the join gathers its key columns now and payload
                 # columns only for the rows that survive it
                 src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
@@ -1414,7 +1414,9 @@ class MultiJoinExec(ExecNode):
                 out_dist = la.out_dist
             over = ctx.budget is not None and \
                 JOIN_MEM_FACTOR * (_batch_bytes(la) + _batch_bytes(lb_)) > ctx.budget
-            if on and not ctx.spmd and not over:
+            # rank-local after prepare_join in SPMD too: index pairs over the
+            # (possibly exchanged) inputs, payload gathered once at the end
+            if on and not over:
                 out = self._late_join(la, lb_, on, and_all(resid), ctx)
             else:
                 if isinstance(la, LateBatch):

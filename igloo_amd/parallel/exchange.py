@@ -52,6 +52,17 @@ def dist_of(b: Batch):
     return getattr(b, "dist", None)
 
 
+def materialized(b: Batch) -> Batch:
+    """A plain Batch for an exchange: late-materialised join results and lazy
+    filtered scans (exec/operators.py LateBatch / _LazyScanBatch) gather their
+    columns first."""
+    if hasattr(b, "materialize"):
+        return b.materialize()
+    if type(b).__name__ == "_LazyScanBatch":
+        return Batch(dict(b.columns.items()), b.num_rows, b.dist)
+    return b
+
+
 def hashed_on(d, cid) -> bool:
     """Rows placed by the hash of column ``cid`` (or a column equal to it)."""
     return cid is not None and bool(d) and d[0] == "hash" and cid in d[1:]
@@ -230,7 +241,7 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
     from ..ops.pack import pack_rows, unpack_rows
     comm = ctx.comm
     W = comm.world_size
-    b = normalize_structure(b, comm)
+    b = normalize_structure(materialized(b), comm)
     perm, send = M.hash_partition(key, W)
     keys = list(b.columns)
     cols = [b.columns[k] for k in keys]
@@ -267,6 +278,7 @@ def local_slice(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
     from ..ops.gather import take_many as _take_many
     from ..ops.select import mask_to_indices
     comm = ctx.comm
+    b = materialized(b)
     d = ("hash", key_cid) if key_cid is not None else None
     if comm.world_size == 1:
         return Batch(dict(b.columns), b.num_rows, d)
@@ -323,6 +335,7 @@ def gather_all(b: Batch, ctx) -> Batch:
     comm = ctx.comm
     if comm is None or not comm.spmd or dist_of(b) == REPLICATED:
         return b
+    b = materialized(b)
     keys = list(b.columns)
     # string byte counts ride along in the preamble (-1: not a plain string
     # here; same length on every rank)
