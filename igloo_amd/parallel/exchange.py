@@ -491,6 +491,10 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
         out_dist = REPLICATED
     # ---- phase 2: merge
     fgroups = [(ci, ColRef(ci.cid, ci.name, ci.dtype, ci.nullable)) for ci, _ in groups]
+    # 128-bit partial sums (wide decimals: SF100 charges) merge as three
+    # int64 sums — high word, and the low word's two 32-bit halves — that
+    # cannot overflow, recombined into 128 bits after the merge
+    rb, wide_parts = _split_wide_partials(rb, plan, ids)
     final, post = [], []
     for func, ci, a, p1, p2 in plan:
         if func == "avg":
@@ -505,7 +509,9 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
             merge = {"sum": "sum", "min": "min", "max": "max", "bool_and": "bool_and", "bool_or": "bool_or"}[func]
             final.append((ci, AggCall(merge, p1.ref(), False, a.dtype)))
             post.append((func, ci, a, None, None))
+    final, recombine = _wide_finals(final, wide_parts, ids)
     fb = aggregate(fgroups, final, rb, ctx)
+    fb = _join_wide_finals(fb, recombine)
     out = {ci.cid: fb.columns[ci.cid] for ci, _ in groups}
     for func, ci, a, fs, fc in post:
         if func == "avg":
@@ -625,6 +631,63 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
             data = vals.to(c.data.dtype) if c.dtype.kind != "bool" else vals != 0
             out[ci.cid] = Column(c.dtype, torch.where(has, data, torch.zeros_like(data)), has)
     return Batch(out, m)
+
+
+def _split_wide_partials(rb: Batch, plan, ids):
+    """Replace every 128-bit partial-sum column of ``rb`` by three int64
+    columns (hi, lo >> 32, lo & 0xFFFFFFFF as unsigned halves); returns
+    (batch, {partial cid: (hi, mid, low) ColInfos})."""
+    wide = {}
+    cols = None
+    for func, ci, a, p1, p2 in plan:
+        c = rb.columns.get(p1.cid)
+        if c is None or not c.is_wide:
+            continue
+        if cols is None:
+            cols = dict(rb.columns)
+        lo, hi = c.data[:, 0], c.data[:, 1]
+        parts = (L.ColInfo(ids(), "__whi", T.INT64), L.ColInfo(ids(), "__wmid", T.INT64),
+                 L.ColInfo(ids(), "__wlow", T.INT64))
+        for pc, t in zip(parts, (hi, (lo >> 32) & 0xFFFFFFFF, lo & 0xFFFFFFFF)):
+            cols[pc.cid] = Column(T.INT64, t.contiguous(), c.valid)
+        wide[p1.cid] = parts
+    if cols is None:
+        return rb, wide
+    return Batch(cols, rb.num_rows, rb.dist), wide
+
+
+def _wide_finals(final, wide, ids):
+    """Merge aggregates with every SUM over a wide partial replaced by the
+    three int64 SUMs of its parts; returns (aggregates, recombination list)."""
+    if not wide:
+        return final, []
+    out, rec = [], []
+    for ci, call in final:
+        arg = call.arg
+        if call.func == "sum" and isinstance(arg, ColRef) and arg.cid in wide:
+            fs = [L.ColInfo(ids(), n, T.INT64) for n in ("__mhi", "__mmid", "__mlow")]
+            out += [(f, AggCall("sum", p.ref(), False, T.INT64)) for f, p in zip(fs, wide[arg.cid])]
+            rec.append((ci, fs))
+        else:
+            out.append((ci, call))
+    return out, rec
+
+
+def _join_wide_finals(fb: Batch, rec) -> Batch:
+    """hi * 2^64 + mid * 2^32 + low -> one 128-bit (lo, hi) column per merged
+    wide sum (mid, low >= 0 and < 2^63: sums of fewer than 2^31 32-bit halves)."""
+    if not rec:
+        return fb
+    cols = dict(fb.columns)
+    sign = -(2**63)
+    for ci, (fh, fm, fl) in rec:
+        hc = cols.pop(fh.cid)
+        mid, low = cols.pop(fm.cid).data, cols.pop(fl.cid).data
+        hi = hc.data
+        lo = low + ((mid & 0xFFFFFFFF) << 32)                     # wraps as uint64
+        carry = ((lo ^ sign) < (low ^ sign)).to(torch.int64)      # unsigned overflow of that add
+        cols[ci.cid] = Column(ci.dtype, torch.stack([lo, hi + (mid >> 32) + carry], 1).contiguous(), hc.valid)
+    return Batch(cols, fb.num_rows, fb.dist)
 
 
 def _sum_type(t):

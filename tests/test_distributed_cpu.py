@@ -109,3 +109,47 @@ def _num(x):
         except ValueError:
             return x
     return x
+
+
+def _wide_worker(rank, world, port, out_path):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from decimal import Decimal
+    import pyarrow as pa
+    import igloo_amd as ig
+    from igloo_amd.catalog import MemoryTable
+    from igloo_amd.parallel.comm import Communicator
+    comm = Communicator.init(backend="gloo", device="cpu", timeout_s=120)
+    n = 4000
+    big = 9 * 10**16
+    rows = range(rank, n, world)          # this rank's slice
+    t = pa.table({"g": pa.array([i % 7 for i in rows], pa.int64()),
+                  "v": pa.array([Decimal(big + i).scaleb(-2) * (1 if i % 3 else -1) for i in rows],
+                                pa.decimal128(18, 2))})
+    e = ig.QueryEngine(device="cpu", comm=comm)
+    e.register_table("t", MemoryTable.from_arrow(t))
+    r = e.query("SELECT g, sum(v) AS s, count(*) AS n FROM t GROUP BY g ORDER BY g").to_pylist()
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump([{k: str(v) for k, v in x.items()} for x in r], f)
+    comm.shutdown()
+
+
+def test_distributed_aggregate_merges_128bit_partial_sums():
+    """Per-rank partial SUMs past 64 bits (wide decimals, e.g. SF100 charge
+    sums) merge exactly across ranks."""
+    from decimal import Decimal
+    big = 9 * 10**16
+    want = {}
+    for i in range(4000):
+        v = Decimal(big + i).scaleb(-2) * (1 if i % 3 else -1)
+        s, c = want.get(i % 7, (Decimal(0), 0))
+        want[i % 7] = (s + v, c + 1)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.json")
+        mp.start_processes(_wide_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+        got = json.load(open(out))
+    assert [int(r["g"]) for r in got] == list(range(7))
+    for r in got:
+        s, c = want[int(r["g"])]
+        assert Decimal(r["s"]) == s and int(r["n"]) == c, r
