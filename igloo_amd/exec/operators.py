@@ -1720,7 +1720,7 @@ class HashAggExec(ExecNode):
         (150M-row join output at SF100). Exact: a left row with k partners
         contributes k to COUNT(x) exactly when x is non-NULL on each partner."""
         lg, child = self.logical, self.children[0]
-        if ctx.spmd or not isinstance(child, HashJoinExec) or len(lg.groups) != 1 or not lg.aggs:
+        if not isinstance(child, HashJoinExec) or len(lg.groups) != 1 or not lg.aggs:
             return None
         j = child.logical
         if j.kind != "left" or j.residual is not None or len(j.on) != 1:
@@ -1745,7 +1745,18 @@ class HashAggExec(ExecNode):
                 rb = _take_batch(rb, keep)
             cnt_cols = {}
             rng = H.key_range(rk) if rk.numel() else None
+            if ctx.spmd:
+                # SPMD: the right side is spread over ranks; one global key
+                # range, per-rank histograms summed by one all-reduce (a dense
+                # 8-byte count per key, ~120 MB at SF100, instead of shuffling
+                # the 150M-row right side by key); every left row then reads
+                # its global count, so the output keeps the left side's placement
+                lo_hi = ctx.comm.allgather_ints([rng[0], rng[1]] if rng else [2**62, -2**62])
+                g0, g1 = min(r[0] for r in lo_hi), max(r[1] for r in lo_hi)
+                rng = (g0, g1) if g0 <= g1 else None
             span = rng[1] - rng[0] + 1 if rng else 0
+            if ctx.spmd and (not rng or span > EAGER_COUNT_DIRECT_SPAN):
+                return self._spmd_join_aggregate(lb, rb, ctx)
             if rng and span <= EAGER_COUNT_DIRECT_SPAN:
                 # dense key domain: one histogram pass over the right keys, then a
                 # direct lookup per left key (no hash table, no group ids)
@@ -1756,7 +1767,10 @@ class HashAggExec(ExecNode):
                     inr &= lvalid
                 li = torch.where(inr, li, torch.zeros_like(li))
                 for k, (_, a) in enumerate(lg.aggs):
-                    hist = A.key_histogram(rk, kmin, span, ev.column(a.arg, rb).valid)
+                    hist = A.key_histogram(rk, kmin, span, ev.column(a.arg, rb).valid) if rk.numel() else \
+                        torch.zeros(span, dtype=torch.int64, device=ctx.device)
+                    if ctx.spmd:
+                        hist = ctx.comm.allreduce_tensor(hist, "sum")
                     cnt_cols[-(k + 1)] = torch.where(inr, hist.index_select(0, li), torch.zeros_like(li))
             elif rk.numel():
                 gid, ng, rep, srt = H.group_ids_ex(rk)
@@ -1776,7 +1790,22 @@ class HashAggExec(ExecNode):
             tmp = -(10**9) - k  # temporary column ids (binder ids are positive)
             cols[tmp] = Column(T.INT64, cnt_cols[-(k + 1)].contiguous())
             aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
+        if ctx.spmd:
+            # the left side's placement carries over (a replicated left side
+            # gives a replicated result; a partitioned one is merged by key)
+            from ..parallel.exchange import distributed_aggregate
+            return distributed_aggregate(L.Aggregate(None, lg.groups, aggs), Batch(cols, lb.num_rows, lb.dist), ctx)
         return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
+
+    def _spmd_join_aggregate(self, lb: Batch, rb: Batch, ctx) -> Batch:
+        """SPMD fallback after the inputs were computed: the plain exchange +
+        join + distributed aggregation."""
+        from ..parallel.exchange import distributed_aggregate, prepare_join
+        j = self.children[0].logical
+        lb, rb = prepare_join(lb, rb, j, ctx)
+        out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
+        out.dist = lb.out_dist
+        return distributed_aggregate(self.logical, out, ctx)
 
     def _run(self, ctx):
         lg = self.logical
