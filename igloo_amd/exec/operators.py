@@ -547,7 +547,10 @@ class HashJoinExec(ExecNode):
             push_key_filter(self.children[1], j.on, lb, ctx)
         rb = self.children[1].execute(ctx)
         if ctx.spmd:
-            from ..parallel.exchange import prepare_join
+            from ..parallel.exchange import prepare_join, semi_by_key_set
+            out = semi_by_key_set(lb, rb, j, ctx)
+            if out is not None:
+                return out
             lb, rb = prepare_join(lb, rb, j, ctx)
             out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
             out.dist = lb.out_dist
@@ -1337,8 +1340,11 @@ class MultiJoinExec(ExecNode):
         elif isinstance(lb, _LazyScanBatch):
             lb = Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
         if ctx.spmd:
-            from ..parallel.exchange import prepare_join
+            from ..parallel.exchange import prepare_join, semi_by_key_set
             j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
+            out = semi_by_key_set(lb, rb, j, ctx)
+            if out is not None:
+                return out
             lb, rb = prepare_join(lb, rb, j, ctx)
             out = hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
             out.dist = lb.out_dist

@@ -437,6 +437,61 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
     return done(lb, rb, ("hash",) + tuple(c for c in (lc, rc) if c is not None) if lc is not None else None)
 
 
+#: largest global key span a semi / anti join filters through a dense
+#: key-presence table (bytes, all-reduced)
+KEYSET_MAX_SPAN = 1 << 27
+
+
+def semi_by_key_set(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
+    """SEMI / ANTI join of a REPLICATED left side against a partitioned right
+    side (TPC-H Q22: customer NOT EXISTS orders) with no row movement: every
+    rank marks the keys of its right rows in a dense presence table over the
+    global key range, ONE all-reduce (max) makes it the global key set, and
+    each rank filters its replicated left rows locally — the result stays
+    replicated. Two collectives (key range, presence table) instead of
+    slicing the left side and shuffling the right side. None when the shape
+    does not apply."""
+    from ..exec.operators import _pair_key
+    from ..ops.select import mask_to_indices
+    comm = ctx.comm
+    if join.kind not in ("semi", "anti") or len(join.on or []) != 1 or join.residual is not None \
+            or getattr(join, "null_aware", False):
+        return None
+    if dist_of(lb) != REPLICATED or dist_of(rb) == REPLICATED:
+        return None
+    ev = ctx.evaluator
+    le, re_ = join.on[0]
+    lcol, rcol = ev.column(le, lb), ev.column(re_, rb)
+    if lcol.dtype.is_string or rcol.dtype.is_string or lcol.data.dim() != 1 or rcol.data.dim() != 1 \
+            or not (lcol.dtype.is_integer or lcol.dtype.kind == "date32") \
+            or not (rcol.dtype.is_integer or rcol.dtype.kind == "date32"):
+        return None
+    lk, rk = _pair_key(lcol, rcol)
+    lk, rk = lk.to(torch.int64), rk.to(torch.int64)
+    if rcol.valid is not None:
+        rk = gather_tensor(rk, mask_to_indices(rcol.valid))
+    from ..ops import hashing as H
+    rng = H.key_range(rk) if rk.numel() else None
+    lo_hi = comm.allgather_ints([rng[0], rng[1]] if rng else [2**62, -2**62])
+    g0, g1 = min(r[0] for r in lo_hi), max(r[1] for r in lo_hi)
+    span = g1 - g0 + 1 if g0 <= g1 else 0
+    if span > KEYSET_MAX_SPAN:
+        return None     # every rank decides alike (global range)
+    present = torch.zeros(max(span, 1), dtype=torch.uint8, device=ctx.device)
+    if rk.numel():
+        present.index_fill_(0, rk - g0, 1)
+    present = comm.allreduce_tensor(present, "max")
+    li = lk - g0
+    inr = (li >= 0) & (li < span)
+    hit = inr & (present.index_select(0, torch.where(inr, li, torch.zeros_like(li))) > 0)
+    if lcol.valid is not None:
+        hit &= lcol.valid
+    keep = mask_to_indices(hit if join.kind == "semi" else ~hit)
+    keys = list(lb.columns)
+    out = Batch(dict(zip(keys, take_many([lb.columns[k] for k in keys], keep))), int(keep.numel()), REPLICATED)
+    return out
+
+
 # ------------------------------------------------------------------ aggregation
 DECOMPOSABLE = {"sum", "count", "min", "max", "avg", "bool_and", "bool_or"}
 
