@@ -263,9 +263,10 @@ class Communicator:
 
     def all_gather_v(self, t: torch.Tensor, counts: Optional[List[int]] = None) -> Tuple[torch.Tensor, List[int]]:
         """Concatenate every rank's ``t`` (variable row counts) on every rank.
-        Equal counts: one native all-gather. Otherwise grouped point-to-point
-        sends of the SAME source buffer to every peer (one ncclSend per xGMI
-        link, no W-fold staging copy), received straight into the output."""
+        One all-gather of equal-sized blocks: each rank's rows padded to the
+        largest count (no point-to-point ops, so the same single collective
+        serves eager execution and RCCL query graphs), then the padding is
+        dropped by one device gather when the counts differ."""
         if faults.ACTIVE:
             faults.check("comm_timeout", "all_gather_v")
         W = self.world_size
@@ -277,30 +278,30 @@ class Communicator:
         src = t.contiguous().to(self.wire)
         if src.dtype == torch.bool:
             src = src.view(torch.uint8)
-        out = torch.empty((sum(counts),) + tail, dtype=src.dtype, device=self.wire)
-        self.bytes_sent += src.numel() * src.element_size() * (W - 1)
-        if all(c == counts[0] for c in counts):
-            if counts[0]:
-                self.calls += 1
-                dist.all_gather_into_tensor(out, src, group=self.group)
+        mx = max(counts) if counts else 0
+        total = sum(counts)
+        if mx == 0:
+            out = torch.empty((0,) + tail, dtype=src.dtype, device=self.wire)
         else:
-            offs = [0]
-            for c in counts:
-                offs.append(offs[-1] + c)
-            ops = []
-            for r in range(W):
-                if r == self.rank:
-                    if counts[r]:
-                        out[offs[r]:offs[r + 1]].copy_(src)
-                    continue
-                if src.shape[0]:
-                    ops.append(dist.P2POp(dist.isend, src, self._peer(r), group=self.group))
-                if counts[r]:
-                    ops.append(dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], self._peer(r), group=self.group))
-            if ops:
-                self.calls += 1
-                for req in dist.batch_isend_irecv(ops):
-                    req.wait()
+            if src.shape[0] < mx:
+                pad = torch.zeros((mx - src.shape[0],) + tail, dtype=src.dtype, device=self.wire)
+                src = torch.cat([src, pad]) if src.shape[0] else pad
+            blocks = torch.empty((W * mx,) + tail, dtype=src.dtype, device=self.wire)
+            self.calls += 1
+            dist.all_gather_into_tensor(blocks, src, group=self.group)
+            self.bytes_sent += src.numel() * src.element_size() * (W - 1)
+            if all(c == mx for c in counts):
+                out = blocks
+            else:
+                # rows [r * mx, r * mx + counts[r]) of every rank r
+                starts = [r * mx for r in range(W)]
+                dev = self.wire
+                cnt = device_ints(counts, dev) if dev.type == "cuda" else torch.tensor(counts, dtype=torch.int64)
+                st = device_ints(starts, dev) if dev.type == "cuda" else torch.tensor(starts, dtype=torch.int64)
+                first = torch.cumsum(cnt, 0) - cnt
+                idx = torch.repeat_interleave(st - first, cnt, output_size=total) + \
+                    torch.arange(total, dtype=torch.int64, device=dev)
+                out = blocks.index_select(0, idx)
         if t.dtype == torch.bool:
             out = out.view(torch.bool)
         return out.to(t.device), counts
