@@ -1,0 +1,67 @@
+#!/bin/bash
+# One GPU session on the gpurun box, by mode (several may be given, run in
+# order). Every GPU step has its own time limit and the script stops at the
+# first failing step; logs and summaries land in gpurun_out/.
+#
+#   tests   pytest -m gpu (the driver's round-end GPU tier)
+#   bench   bench.py at the driver's SF100 configuration (--steps 20 --warmup 5)
+#   spmd    multi-GPU code path on one GPU: scripts/spmd_world1.py (SF0.5, RCCL,
+#           every collective real) + bench.py with IGLOO_FORCE_SPMD=1 at SF100
+#   prof    rocprofv3 kernel trace of the warm SF100 suite (query graphs);
+#           per-kernel summary of the timed steps (scripts/kernel_summary.py)
+#   pmc     rocprofv3 counter passes (FETCH_SIZE / WRITE_SIZE / instruction
+#           mix; one pass per counter set, --kernel-trace only) over the warm
+#           graphed suite; per-kernel bandwidth table (scripts/pmc_summary.py)
+#
+#   gpurun -- 'bash scripts/gpu_run.sh tests bench'
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R" && mkdir -p gpurun_out
+export TMPDIR=/tmp
+for mode in "$@"; do
+  case "$mode" in
+    tests)
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/pytest_gpu.log ;;
+    bench)
+      timeout -k 10 1000 python -u bench.py --steps 20 --warmup 5 --per-query > gpurun_out/bench_sf100.log 2>&1
+      rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_sf100.log | cut -c1-400 ;;
+    spmd)
+      timeout -k 10 300 python -u scripts/spmd_world1.py --sf 0.5 --device cuda:0 --backend nccl --runs 6 \
+        --json gpurun_out/spmd_sf05.json > gpurun_out/spmd_sf05.log 2>&1
+      rc=$?; echo "spmd_world1 rc=$rc"; tail -1 gpurun_out/spmd_sf05.log | cut -c1-300
+      [ $rc -eq 0 ] || exit $rc
+      IGLOO_FORCE_SPMD=1 timeout -k 10 900 python -u bench.py --steps 10 --warmup 5 --per-query \
+        > gpurun_out/bench_sf100_spmd1.log 2>&1
+      rc=$?; echo "spmd bench rc=$rc"; tail -1 gpurun_out/bench_sf100_spmd1.log | cut -c1-400 ;;
+    prof)
+      IGLOO_PROF_GAP=1 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 3 --warmup 5 --eager-steps 0 \
+        --vary-params 0 > gpurun_out/prof.log 2>&1
+      rc=$?; echo "prof rc=$rc"
+      if [ $rc -eq 0 ]; then
+        T=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
+        python3 scripts/kernel_summary.py "$T" --steps 3 --top 40 > gpurun_out/kernel_summary.txt
+        python3 scripts/aten_share.py "$T" --steps 3 > gpurun_out/aten_share.txt
+        head -12 gpurun_out/kernel_summary.txt; rm -f "$T"
+      fi ;;
+    pmc)
+      i=0
+      while read -r SET; do
+        [ -z "$SET" ] && continue
+        i=$((i+1))
+        IGLOO_PROF_GAP=1 timeout -s KILL 600 rocprofv3 --kernel-trace --pmc $SET --output-format csv \
+          -d "$R/gpurun_out/pmc/p$i" -o run -- python3 "$R/bench.py" --source hbm --sf ${SF:-100} --steps 1 \
+          --warmup 5 --eager-steps 0 --vary-params 0 > gpurun_out/pmc_p$i.log 2>&1
+        rc=$?; echo "pmc pass $i ($SET) rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done <<SETS
+${PMC_SETS:-FETCH_SIZE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES
+WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_MFMA}
+SETS
+      python3 scripts/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt 2>&1
+      rc=$?; head -30 gpurun_out/pmc_summary.txt ;;
+    *) echo "unknown mode $mode"; exit 2 ;;
+  esac
+  [ $rc -eq 0 ] || exit $rc
+done
