@@ -283,7 +283,9 @@ def main():
     if rank == 0:
         if a.per_query:
             from igloo_amd.exec import graphs as _graphs
-            log(f"[bench] graphs: {_graphs.STATS}; HBM reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB, "
+            log(f"[bench] graphs: {_graphs.STATS}; engine graphs {len(eng._graphs)} holding "
+                f"{eng.graph_bytes / 2**30:.1f} GiB, {eng.graph_stats}; cache tier {eng.cache.hbm_used / 2**30:.1f} GiB; "
+                f"HBM reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB, "
                 f"peak allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
             for msg in _graphs.LAST_ERROR:
                 log("[bench] graph not captured: " + msg.strip().replace("\n", " | ")[-600:])
