@@ -163,6 +163,9 @@ class QueryEngine:
         self.graph_stats = {"evicted": 0, "dropped_stale": 0}
         self._spec_current: Dict[Any, Any] = {}     # plan key -> its live speculation key
         self._query_sources: Dict[Any, list] = {}   # plan key -> cached table sources it reads
+        #: SPMD: global NDV and global rows of base-table join keys
+        #: ((catalog version, cache generation), table, column) -> (ndv, rows)
+        self._gndv: Dict[Any, tuple] = {}
 
     # -------------------------------------------------------------- catalog
     def register_table(self, name: str, table: Union[TableSource, pa.Table, Batch, Dict[str, Column]],

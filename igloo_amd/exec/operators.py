@@ -1357,7 +1357,8 @@ class MultiJoinExec(ExecNode):
         rels = []
         for ch in self.children[:nch]:
             b = ch.execute(ctx)
-            rels.append({"batch": b, "cids": set(b.columns), "ndv": {}, "name": ch.describe()[:40]})
+            rels.append({"batch": b, "cids": set(b.columns), "ndv": {}, "name": ch.describe()[:40],
+                         "scan": _scan_info(ch)})
         self.order_log = []
         deferred = []
         semis = [(sp, rex.execute(ctx)) for sp, rex in zip(lg.semis, self.children[nch:])]
@@ -1367,7 +1368,7 @@ class MultiJoinExec(ExecNode):
         # join key the ordering will ask for, in ONE collective
         if ctx.spmd:
             g = self._spmd_stats([r["batch"] for r in rels] + [rb for _, rb in semis],
-                                 self._ndv_needs(rels, conds), ctx)
+                                 self._ndv_needs(rels, conds), ctx, rels)
         else:
             g = _global_rows_many([r["batch"] for r in rels] + [rb for _, rb in semis], ctx)
         for r, n in zip(rels, g):
@@ -1520,27 +1521,52 @@ class MultiJoinExec(ExecNode):
                             need.append((rel, e))
         return need
 
-    def _spmd_stats(self, batches, need, ctx) -> List[int]:
+    def _spmd_stats(self, batches, need, ctx, rels=()) -> List[int]:
         """SPMD: global row counts of ``batches`` (a replicated batch counts
         once) and the global NDV of every ``need`` key, in ONE collective: an
         all-gather of [counts | HLL registers] (counts summed, registers
         max-merged locally) on the GPU, one all-reduce of [counts | exact local
-        distinct counts] on the CPU. Sets ``rel["ndv"]``; returns the counts."""
+        distinct counts] on the CPU. Sets ``rel["ndv"]``; returns the counts.
+
+        Base-table key columns are sketched once: their global NDV (and the
+        table's global rows) is kept per engine, keyed by (table, column,
+        catalog version, cache generation); a later query reads it, and a
+        filtered scan of that column derives its NDV from it (Cardenas) with
+        its global row count — no sketch pass. Which keys are sketched follows
+        from the plan and that cache alone, so every rank sketches the same
+        ones (the all-gather's shape matches on every rank)."""
         comm = ctx.comm
         local = [0 if _replicated(b) else b.num_rows for b in batches]
+        eng = ctx.engine
+        cache = getattr(eng, "_gndv", None) if eng is not None else None
+        ver = (eng.catalog.version, eng.cache.generation) if cache is not None else None
+        plan = []      # per need: (kind, cache key, rel index)
+        for rel, e in need:
+            ri = next((i for i, r in enumerate(rels) if r is rel), None)
+            info = rel.get("scan")
+            kind, key = "sketch", None
+            if cache is not None and info is not None and isinstance(e, ColRef) and e.cid in info[1]:
+                key = (ver, info[0], info[1][e.cid])
+                if key in cache:
+                    kind = "derived" if info[2] else "cached"
+                elif not info[2]:
+                    kind = "sketch_base"
+            plan.append((kind, key, ri))
+        sk = [j for j, (kind, _, _) in enumerate(plan) if kind.startswith("sketch")]
         if ctx.device.type != "cuda":
             nd = []
-            for rel, e in need:
+            for j in sk:
+                rel, e = need[j]
                 b = rel["batch"]
                 mine = b.num_rows and (not _replicated(b) or comm.rank == 0)   # a replicated input counts once
                 nd.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
             g = comm.allreduce_ints(local + nd)
-            for (rel, e), v in zip(need, g[len(local):]):
-                rel["ndv"][e.sql()] = max(v, 1)
+            est = dict(zip(sk, g[len(local):]))
             g = g[:len(local)]
         else:
             regs = []
-            for rel, e in need:
+            for j in sk:
+                rel, e = need[j]
                 b = rel["batch"]
                 if b.num_rows:
                     k, _ = group_key_tensor(ctx.evaluator.column(e, b))
@@ -1560,10 +1586,27 @@ class MultiJoinExec(ExecNode):
                 vals.append(H.hll_terms(merged).view(torch.int64).reshape(-1))
             host = to_host_ints(torch.cat(vals))
             g = host[:nb]
-            for j, (rel, e) in enumerate(need):
-                z, zeros = np.array(host[nb + 2 * j:nb + 2 * j + 2], dtype=np.int64).view(np.float64)
-                rel["ndv"][e.sql()] = max(int(round(H.hll_from_terms(float(z), int(zeros)))), 1)
-        return [b.num_rows if _replicated(b) else n for b, n in zip(batches, g)]
+            est = {}
+            for t, j in enumerate(sk):
+                z, zeros = np.array(host[nb + 2 * t:nb + 2 * t + 2], dtype=np.int64).view(np.float64)
+                est[j] = int(round(H.hll_from_terms(float(z), int(zeros))))
+        counts = [b.num_rows if _replicated(b) else n for b, n in zip(batches, g)]
+        for j, ((rel, e), (kind, key, ri)) in enumerate(zip(need, plan)):
+            if kind == "cached":
+                v = cache[key][0]
+            elif kind == "derived":
+                D, N = cache[key]
+                n = counts[ri] if ri is not None else rel["batch"].num_rows
+                sel = min(n / max(N, 1), 1.0)
+                v = max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / max(D, 1)))))))
+            else:
+                v = est[j]
+                if kind == "sketch_base" and ri is not None:
+                    if len(cache) > 4096:
+                        cache.clear()
+                    cache[key] = (max(v, 1), counts[ri])
+            rel["ndv"][e.sql()] = max(v, 1)
+        return counts
 
     def _prefetch_ndv(self, rels, conds, ctx) -> None:
         """SPMD: sketch every join key the next ordering step will ask for and
@@ -1671,6 +1714,17 @@ def _derived_ndv(base, n: int) -> int:
             pass
     sel = min(n / max(N, 1), 1.0)
     return max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / D))))))
+
+
+def _scan_info(node):
+    """(table, {cid: column name}, filtered) of a plain table-scan input of a
+    multi-way join, else None (SPMD NDV cache, MultiJoinExec._spmd_stats)."""
+    if not isinstance(node, ScanExec):
+        return None
+    s = node.logical
+    names = {c.cid: c.name for c in getattr(s, "table_cols", s.schema)}
+    names.update({c.cid: c.name for c in s.schema})
+    return (s.table, names, bool(s.filters))
 
 
 def _replicated(b) -> bool:
