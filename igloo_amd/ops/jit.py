@@ -34,6 +34,13 @@ MODE = os.environ.get("IGLOO_JIT", "async").lower()
 ARCH = "gfx950"
 _VERSION = "1"  # bump when the compile options or the kernarg convention change
 CACHE_DIR = Path(os.environ.get("IGLOO_JIT_CACHE", os.path.join(os.environ.get("TMPDIR", "/tmp"), "igloo_jit")))
+#: ahead-of-time code objects shipped with the build (read-only, searched
+#: first): the query-specialised kernels of the TPC-H suite at the benchmark
+#: scale, compiled by ``scripts/gpu_run.sh jitcache`` so a fresh process does
+#: not pay for hiprtc in its first (cold) queries. A source not found here or
+#: in CACHE_DIR compiles on demand as usual.
+AOT_DIR = Path(os.environ.get("IGLOO_JIT_AOT", os.path.join(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__))), "_jit_cache")))
 
 _lock = threading.Lock()
 _kernels: Dict[str, "JitKernel"] = {}
@@ -111,13 +118,16 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
             return None
         fut = _pending.get(key)
         if fut is None:
-            p = _disk_path(key)
+            p = AOT_DIR / f"{key}.co"
+            if not p.exists():
+                p = _disk_path(key)
             if p.exists():
                 try:
                     STATS["disk_hits"] += 1
                     return _load(p.read_bytes(), name, key)
                 except Exception:   # stale / truncated cache entry: recompile
-                    p.unlink(missing_ok=True)
+                    if p.parent != AOT_DIR:
+                        p.unlink(missing_ok=True)
             if mode == "sync":
                 try:
                     return _load(_compile(src, name, key), name, key)

@@ -9,6 +9,8 @@
 #           every collective real) + bench.py with IGLOO_FORCE_SPMD=1 at SF100
 #   prof    rocprofv3 kernel trace of the warm SF100 suite (query graphs);
 #           per-kernel summary of the timed steps (scripts/kernel_summary.py)
+#   jitcache  compile the suite's generated kernels at SF100 (validation and
+#           substitution parameters) into gpurun_out/jit_cache
 #   pmc     rocprofv3 counter passes (FETCH_SIZE / WRITE_SIZE / instruction
 #           mix; one pass per counter set, --kernel-trace only) over the warm
 #           graphed suite; per-kernel bandwidth table (scripts/pmc_summary.py)
@@ -61,6 +63,12 @@ WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_A
 SETS
       python3 scripts/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt 2>&1
       rc=$?; head -30 gpurun_out/pmc_summary.txt ;;
+    jitcache)
+      # compile the suite's query-specialised kernels at the benchmark scale
+      # into gpurun_out/jit_cache (copied into igloo_amd/_jit_cache/ afterwards)
+      IGLOO_JIT_CACHE="$R/gpurun_out/jit_cache" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
+        --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 > gpurun_out/jitcache.log 2>&1
+      rc=$?; echo "jitcache rc=$rc"; ls gpurun_out/jit_cache | wc -l ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac
   [ $rc -eq 0 ] || exit $rc
