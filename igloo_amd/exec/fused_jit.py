@@ -106,36 +106,59 @@ class _Shape:
 
 def _terms_expr(sh: _Shape, terms, j: int) -> str:
     """Boolean expression of every filter term for row j (AND of top-level
-    terms, AND of the OR over conjunction groups)."""
+    terms, AND of the OR over conjunction groups). The terms' constants are
+    kernel arguments (``_term_args``), not literals: the source depends only
+    on the predicate's shape, so a query with other parameter values (a TPC-H
+    substitution, an ad-hoc date range) reuses the compiled kernel."""
     top: List[str] = []
     groups: dict = {}
-    for col, kindg, lo, hi, bits in terms:
+    for t, (col, kindg, lo, hi, bits) in enumerate(terms):
         kind, grp = kindg & 0xFF, kindg >> 8
         x = f"x{col}_{j}"
         mn, mx = sh.rng(col)
         if kind in (0, 1):
             parts = []
-            if lo > mn:
-                parts.append(f"{x} >= {_lit(lo)}")
-            if hi < mx:
-                parts.append(f"{x} <= {_lit(hi)}")
+            if lo > mn or lo > hi:
+                parts.append(f"{x} >= f{t}lo")
+            if hi < mx or lo > hi:
+                parts.append(f"{x} <= f{t}hi")
             e = "(" + " && ".join(parts) + ")" if parts else "true"
-            if lo > hi:
-                e = "false"
             if kind == 1:
                 e = f"!{e}"
         elif kind == 2:
-            e = f"((u64){x} < 64ull && ((0x{bits & 0xFFFFFFFFFFFFFFFF:x}ull >> (u32){x}) & 1ull))"
+            e = f"((u64){x} < 64ull && ((f{t}bits >> (u32){x}) & 1ull))"
         elif kind == 3:
             c2 = bits & 0xFF
             d = f"((i64){x} - (i64)x{c2}_{j})"
-            e = f"({d} >= {_lit(lo)} && {d} <= {_lit(hi)})"
+            e = f"({d} >= f{t}lo && {d} <= f{t}hi)"
         else:
             raise ValueError(f"term kind {kind}")
         (groups.setdefault(grp, []) if grp else top).append(e)
     if groups:
         top.append("(" + " || ".join("(" + " && ".join(g) + ")" for _, g in sorted(groups.items())) + ")")
     return " && ".join(top) if top else "true"
+
+
+def _term_params(terms) -> List[str]:
+    """Kernel parameters carrying the filter terms' constants (appended
+    after every other parameter)."""
+    ps = []
+    for t, (col, kindg, lo, hi, bits) in enumerate(terms):
+        if kindg & 0xFF == 2:
+            ps.append(f"u64 f{t}bits")
+        else:
+            ps += [f"i64 f{t}lo", f"i64 f{t}hi"]
+    return ps
+
+
+def _term_args(terms) -> List[int]:
+    out = []
+    for col, kindg, lo, hi, bits in terms:
+        if kindg & 0xFF == 2:
+            out.append(int(bits) & 0xFFFFFFFFFFFFFFFF)
+        else:
+            out += [int(lo), int(hi)]
+    return out
 
 
 class _Values:
@@ -244,7 +267,8 @@ def _aligned(cols: Sequence[torch.Tensor]) -> bool:
 # ------------------------------------------------------------------ mask
 def mask_source(sh: _Shape, terms, has_mask: bool) -> str:
     L = [f"#define ROWS {ROWS}", PRELUDE, f"extern \"C\" __global__ __launch_bounds__({BLOCK}) void igloo_jit_scan_mask("]
-    L.append("    " + ", ".join(_params(sh, has_mask) + ["u8* __restrict__ out", "i64 n"]) + ") {")
+    L.append("    " + ", ".join(_params(sh, has_mask) + ["u8* __restrict__ out", "i64 n"] + _term_params(terms))
+             + ") {")
     L.append(f"  const i64 step = (i64)gridDim.x * {BLOCK * ROWS};")
     L.append(f"  for (i64 r = ((i64)blockIdx.x * {BLOCK} + threadIdx.x) * {ROWS}; r < n; r += step) {{")
     L += ["    " + s for s in _loads(sh, has_mask)]
@@ -270,7 +294,7 @@ def jit_mask(spec, n: int, out: torch.Tensor, stream: int) -> bool:
         return False
     grid = max(1, min(-(-n // (BLOCK * ROWS)), 256 * 16))
     args = [t.data_ptr() for t in spec.cols] + ([spec.mask.data_ptr()] if has_mask else []) + [out.data_ptr(), n]
-    k.launch(grid, BLOCK, 0, stream, args)
+    k.launch(grid, BLOCK, 0, stream, args + _term_args(spec.terms))
     return True
 
 
@@ -291,7 +315,7 @@ def agg_source(sh: _Shape, terms, has_mask: bool, keys, G: int, aggs, split: Seq
     ps = _params(sh, has_mask) + ["i64* __restrict__ counts"]
     for i in range(NA):
         ps += [f"i64* __restrict__ d{i}", f"i64* __restrict__ e{i}"]
-    ps += ["int* __restrict__ ovf", "i64 n"]
+    ps += ["int* __restrict__ ovf", "i64 n"] + _term_params(terms)
     L.append("    " + ", ".join(ps) + ") {")
     L.append("  int of = 0;")
     if G == 1:
@@ -477,7 +501,7 @@ def mfma_agg_source(sh: _Shape, terms, has_mask: bool, keys, G: int, aggs) -> Tu
     ps = _params(sh, has_mask) + ["i64* __restrict__ counts"]
     for i in range(NA):
         ps += [f"i64* __restrict__ d{i}", f"i64* __restrict__ e{i}"]
-    ps += ["int* __restrict__ ovf", "i64 n"]
+    ps += ["int* __restrict__ ovf", "i64 n"] + _term_params(terms)
     L.append("    " + ", ".join(ps) + ") {")
     L.append(f"  __shared__ __attribute__((aligned(16))) u8 tile[{BLOCK // 64}][{tile_bytes}];")
     L.append("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;")
@@ -604,5 +628,5 @@ def jit_aggregate(spec, keys, G: int, kaggs, counts: torch.Tensor, ovf: torch.Te
     for op, chk, fs, d, d2, shared, vbits in kaggs:
         args += [d, d2 or d]
     args += [ovf.data_ptr(), n]
-    k.launch(grid, BLOCK, 0, stream, args)
+    k.launch(grid, BLOCK, 0, stream, args + _term_args(spec.terms))
     return True
