@@ -9,6 +9,7 @@
 #           every collective real) + bench.py with IGLOO_FORCE_SPMD=1 at SF100
 #   prof    rocprofv3 kernel trace of the warm SF100 suite (query graphs);
 #           per-kernel summary of the timed steps (scripts/kernel_summary.py)
+#   profq   per-query kernel summaries (QS="9 10 13" query sets, HBM tables)
 #   jitcache  compile the suite's generated kernels at SF100 (validation and
 #           substitution parameters) into gpurun_out/jit_cache
 #   pmc     rocprofv3 counter passes (FETCH_SIZE / WRITE_SIZE / instruction
@@ -63,6 +64,18 @@ WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_A
 SETS
       python3 scripts/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt 2>&1
       rc=$?; head -30 gpurun_out/pmc_summary.txt ;;
+    profq)
+      # per-query kernel summaries (tables generated in HBM), one rocprofv3 run
+      # per query set in QS (space separated, e.g. QS="9 10 13 21")
+      for q in ${QS:-9 10 13 21 5 18}; do
+        IGLOO_PROF_GAP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$R/gpurun_out/profq_$q" -o run -- python3 "$R/bench.py" --source hbm --queries $q --steps 3 --warmup 5 \
+          --eager-steps 0 --vary-params 0 > gpurun_out/profq_$q.log 2>&1
+        rc=$?; echo "profq $q rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        T=$(find gpurun_out/profq_$q -name "*kernel_trace.csv" | head -1)
+        python3 scripts/kernel_summary.py "$T" --steps 3 --top 25 > gpurun_out/profq_${q}_summary.txt
+        rm -rf gpurun_out/profq_$q; head -8 gpurun_out/profq_${q}_summary.txt
+      done ;;
     jitcache)
       # compile the suite's query-specialised kernels at the benchmark scale
       # into gpurun_out/jit_cache (copied into igloo_amd/_jit_cache/ afterwards)
