@@ -10,8 +10,9 @@
 #   prof    rocprofv3 kernel trace of the warm SF100 suite (query graphs);
 #           per-kernel summary of the timed steps (scripts/kernel_summary.py)
 #   profq   per-query kernel summaries (QS="9 10 13" query sets, HBM tables)
-#   jitcache  compile the suite's generated kernels at SF100 (validation and
-#           substitution parameters) into gpurun_out/jit_cache
+#   jitcache  compile the suite's generated kernels at SF100 (validation
+#           parameters only: ad-hoc runs must not find theirs precompiled) into
+#           gpurun_out/jit_cache
 #   pmc     rocprofv3 counter passes (FETCH_SIZE / WRITE_SIZE / instruction
 #           mix; one pass per counter set, --kernel-trace only) over the warm
 #           graphed suite; per-kernel bandwidth table (scripts/pmc_summary.py)
@@ -80,7 +81,7 @@ SETS
       # compile the suite's query-specialised kernels at the benchmark scale
       # into gpurun_out/jit_cache (copied into igloo_amd/_jit_cache/ afterwards)
       IGLOO_JIT_CACHE="$R/gpurun_out/jit_cache" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
-        --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 > gpurun_out/jitcache.log 2>&1
+        --steps 1 --warmup 1 --eager-steps 0 --vary-params 0 > gpurun_out/jitcache.log 2>&1
       rc=$?; echo "jitcache rc=$rc"; ls gpurun_out/jit_cache | wc -l ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac
