@@ -337,7 +337,8 @@ class QueryEngine:
             table = self._to_arrow(batch, plan.schema, bq_names)
         if st is not None and spec in ("replayed", "recorded") and st["capture_next"]:
             st["digest"] = digest(table)      # the next execution's graph must reproduce it
-        self.cache.enforce()   # derived structures built by this query count against the budget
+        if spec != "graph":
+            self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
                              "spill": dict(ctx.spill), "plan_cached": cached, "speculation": spec,
