@@ -64,7 +64,8 @@ ${PMC_SETS:-FETCH_SIZE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY
 WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_MFMA}
 SETS
       python3 scripts/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt 2>&1
-      rc=$?; head -30 gpurun_out/pmc_summary.txt ;;
+      rc=$?; head -30 gpurun_out/pmc_summary.txt
+      rm -rf gpurun_out/pmc ;;      # raw traces exceed what gpurun copies back
     profq)
       # per-query kernel summaries (tables generated in HBM), one rocprofv3 run
       # per query set in QS (space separated, e.g. QS="9 10 13 21")
