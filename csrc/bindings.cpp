@@ -253,43 +253,65 @@ PYBIND11_MODULE(_native, m) {
 
   // ------------------------------------------------------------ hash tables
   m.def("join_build", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t tkeys, uintptr_t thead,
-                         uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t dups, uintptr_t bits,
+                         bool rid64, int64_t cap, int64_t kmin, bool direct, uintptr_t dups, uintptr_t bits,
                          uint64_t bmask, uintptr_t s) {
-    kern::join_build(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<int64_t>(tkeys), P<int32_t>(thead),
-                     P<int32_t>(next), cap, kmin, direct, P<unsigned long long>(dups), P<uint32_t>(bits), bmask, S(s));
+    if (n > 0 && (!keys || !thead || !dups || (!direct && !tkeys))) throw std::runtime_error("join_build: null buffer");
+    kern::join_build(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<int64_t>(tkeys), P<void>(thead), rid64,
+                     cap, kmin, direct, P<unsigned long long>(dups), P<uint32_t>(bits), bmask, S(s));
+  });
+  m.def("join_csr_count", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t tkeys, uintptr_t cnt,
+                             bool rid64, int64_t cap, int64_t kmin, bool direct, uintptr_t s) {
+    if (n > 0 && (!keys || !cnt || (!direct && !tkeys))) throw std::runtime_error("join_csr_count: null buffer");
+    kern::join_csr_count(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<const int64_t>(tkeys),
+                         P<void>(cnt), rid64, cap, kmin, direct, S(s));
+  });
+  m.def("join_csr_scatter", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, uintptr_t tkeys, uintptr_t cnt,
+                               uintptr_t cstart, uintptr_t crows, bool rid64, int64_t cap, int64_t kmin, bool direct,
+                               uintptr_t s) {
+    if (n > 0 && (!keys || !cnt || !cstart || !crows || (!direct && !tkeys)))
+      throw std::runtime_error("join_csr_scatter: null buffer");
+    kern::join_csr_scatter(P<const void>(keys), key64, P<const uint8_t>(valid), n, P<const int64_t>(tkeys),
+                           P<void>(cnt), P<const void>(cstart), P<void>(crows), rid64, cap, kmin, direct, S(s));
   });
   m.def("join_probe", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
-                         uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t counts, uintptr_t first,
-                         uintptr_t matched, uintptr_t bits, uint64_t bmask, uintptr_t s) {
+                         uintptr_t cstart, uintptr_t crows, bool rid64, int64_t cap, int64_t kmin, bool direct,
+                         uintptr_t counts, uintptr_t first, uintptr_t matched, uintptr_t bits, uint64_t bmask,
+                         uintptr_t s) {
+    if (m_ > 0 && (!keys || !thead || (!direct && !tkeys) || (!cstart != !crows)))
+      throw std::runtime_error("join_probe: null buffer");
     kern::join_probe(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
-                     P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<int32_t>(counts),
-                     P<int32_t>(first), P<uint8_t>(matched), P<const uint32_t>(bits), bmask, S(s));
+                     P<const void>(thead), P<const void>(cstart), P<const void>(crows), rid64, cap, kmin, direct,
+                     P<int32_t>(counts), P<void>(first), P<uint8_t>(matched), P<const uint32_t>(bits), bmask, S(s));
   });
   m.def("probe_hit_tiles", [](int64_t m_) { return kern::probe_hit_tiles(m_); });
   m.def("probe_hits", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
-                         int64_t cap, int64_t kmin, bool direct, uintptr_t bits, uint64_t bmask, bool negate,
-                         uintptr_t words, uintptr_t tile_counts, uintptr_t s) {
+                         bool rid64, int64_t cap, int64_t kmin, bool direct, uintptr_t bits, uint64_t bmask,
+                         bool negate, uintptr_t words, uintptr_t tile_counts, uintptr_t s) {
     if (m_ > 0 && (!keys || !thead || !words || !tile_counts || (!direct && !tkeys)))
       throw std::runtime_error("probe_hits: null buffer");
     kern::probe_hits(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
-                     P<const int32_t>(thead), cap, kmin, direct, P<const uint32_t>(bits), bmask, negate,
+                     P<const void>(thead), rid64, cap, kmin, direct, P<const uint32_t>(bits), bmask, negate,
                      P<unsigned long long>(words), P<int64_t>(tile_counts), S(s));
   });
   m.def("probe_write", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
-                          int64_t cap, int64_t kmin, bool direct, uintptr_t words, uintptr_t tile_off,
+                          bool rid64, int64_t cap, int64_t kmin, bool direct, uintptr_t words, uintptr_t tile_off,
                           uintptr_t out_probe, bool out64, uintptr_t out_build, uintptr_t s) {
     if (m_ > 0 && (!keys || !thead || !words || !tile_off || !out_probe || (!direct && !tkeys)))
       throw std::runtime_error("probe_write: null buffer");
     kern::probe_write(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
-                      P<const int32_t>(thead), cap, kmin, direct, P<const unsigned long long>(words),
-                      P<const int64_t>(tile_off), P<void>(out_probe), out64, P<int32_t>(out_build), S(s));
+                      P<const void>(thead), rid64, cap, kmin, direct, P<const unsigned long long>(words),
+                      P<const int64_t>(tile_off), P<void>(out_probe), out64, P<void>(out_build), S(s));
   });
   m.def("join_expand", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
-                          uintptr_t next, int64_t cap, int64_t kmin, bool direct, uintptr_t offsets, uintptr_t out_probe,
-                          uintptr_t out_build, uintptr_t bits, uint64_t bmask, uintptr_t s) {
+                          uintptr_t cstart, uintptr_t crows, bool rid64, int64_t cap, int64_t kmin, bool direct,
+                          uintptr_t offsets, uintptr_t out_probe, uintptr_t out_build, uintptr_t bits, uint64_t bmask,
+                          uintptr_t s) {
+    if (m_ > 0 && (!keys || !thead || !offsets || !out_probe || !out_build || (!direct && !tkeys)))
+      throw std::runtime_error("join_expand: null buffer");
     kern::join_expand(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
-                      P<const int32_t>(thead), P<const int32_t>(next), cap, kmin, direct, P<const int64_t>(offsets),
-                      P<int32_t>(out_probe), P<int32_t>(out_build), P<const uint32_t>(bits), bmask, S(s));
+                      P<const void>(thead), P<const void>(cstart), P<const void>(crows), rid64, cap, kmin, direct,
+                      P<const int64_t>(offsets), P<int32_t>(out_probe), P<void>(out_build), P<const uint32_t>(bits),
+                      bmask, S(s));
   });
   // fused scan kernels. cols: [(ptr, width)], terms: [(col, kind, lo, hi, set)],
   // keys: [(col, lo, mul)], aggs: [(op, checked, [(col, a, b)], dst, dst2, shared)]

@@ -12,8 +12,12 @@
 //                key itself is the slot (a perfect hash): no key array, no
 //                probing, one random read per probe row. TPC-H keys are
 //                dense integers, so most joins take this path.
-// Duplicate build keys are chained through next[row] (atomicExch on the
-// slot head), so the same table serves unique (PK) and multi-match joins.
+// Every slot's head row (thead, one atomicExch per build row) serves unique
+// (PK) builds. A build with duplicate keys adds a CSR layout: per-slot counts,
+// an exclusive scan into cstart[cap+1] and a scatter of the row ids into
+// crows[n], so a multi-match probe reads one contiguous run instead of
+// pointer-chasing a next[] chain through HBM. Row ids (thead, crows, cstart,
+// probe outputs) are int32 below 2^31 build rows and int64 above (R).
 #include "common.h"
 #include "kernels.h"
 
@@ -67,17 +71,26 @@ __device__ inline uint64_t bloom_bit(int64_t k, uint64_t bmask, int64_t kmin) {
   return (bmask & kExactBits) ? (uint64_t)(k - kmin) : ((mix64((uint64_t)k) >> 7) & bmask);
 }
 
-template <typename K, bool DIRECT>
+__device__ inline int32_t atomic_add(int32_t* p, int32_t v) { return atomicAdd(p, v); }
+__device__ inline int64_t atomic_add(int64_t* p, int64_t v) {
+  return (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
+}
+__device__ inline int32_t atomic_exch(int32_t* p, int32_t v) { return atomicExch(p, v); }
+__device__ inline int64_t atomic_exch(int64_t* p, int64_t v) {
+  return (int64_t)atomicExch(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
+}
+
+template <typename K, bool DIRECT, typename R>
 __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
                                                            int64_t n, int64_t* __restrict__ tkeys,
-                                                           int32_t* __restrict__ thead, int32_t* __restrict__ next,
-                                                           int64_t cap, int64_t kmin, unsigned long long* dups,
-                                                           uint32_t* __restrict__ bits, uint64_t bmask) {
+                                                           R* __restrict__ thead, int64_t cap, int64_t kmin,
+                                                           unsigned long long* dups, uint32_t* __restrict__ bits,
+                                                           uint64_t bmask) {
   const int64_t mask = cap - 1;
   unsigned long long local_dups = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t k;
-    if (!load_key(keys, valid, i, &k)) { next[i] = -1; continue; }
+    if (!load_key(keys, valid, i, &k)) continue;
     int64_t slot;
     if (DIRECT) {
       slot = k - kmin;
@@ -88,9 +101,8 @@ __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict_
       bool existed;
       slot = insert_slot(tkeys, mask, k, &existed);
     }
-    int32_t old = atomicExch(&thead[slot], (int32_t)i);
-    next[i] = old;
-    local_dups += old != -1;
+    const R old = atomic_exch(&thead[slot], (R)i);
+    local_dups += old != (R)-1;
     if (bits) {
       const uint64_t bb = bloom_bit(k, bmask, kmin);
       atomicOr(&bits[bb >> 5], 1u << (bb & 31));
@@ -101,10 +113,52 @@ __global__ __launch_bounds__(kBlock) void join_build_kernel(const K* __restrict_
   if (lane_id() == 0 && local_dups) atomicAdd(dups, local_dups);
 }
 
+// slot of build row i (its key is in the table), -1 for a NULL key
 template <typename K, bool DIRECT>
-__device__ inline int32_t probe_head(const K* keys, const uint8_t* valid, int64_t j, const int64_t* tkeys,
-                                     const int32_t* thead, int64_t cap, int64_t kmin, const uint32_t* bits,
-                                     uint64_t bmask) {
+__device__ inline int64_t build_slot(const K* keys, const uint8_t* valid, int64_t i, const int64_t* tkeys,
+                                     int64_t cap, int64_t kmin) {
+  int64_t k;
+  if (!load_key(keys, valid, i, &k)) return -1;
+  if (DIRECT) {
+    const int64_t s = k - kmin;
+    return (uint64_t)s < (uint64_t)cap ? s : -1;
+  }
+  return find_slot(tkeys, cap - 1, k);
+}
+
+// CSR pass 1: rows per slot (cnt zeroed by the caller)
+template <typename K, bool DIRECT, typename R>
+__global__ __launch_bounds__(kBlock) void join_csr_count_kernel(const K* __restrict__ keys,
+                                                               const uint8_t* __restrict__ valid, int64_t n,
+                                                               const int64_t* __restrict__ tkeys, R* __restrict__ cnt,
+                                                               int64_t cap, int64_t kmin) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = build_slot<K, DIRECT>(keys, valid, i, tkeys, cap, kmin);
+    if (s >= 0) atomic_add(&cnt[s], (R)1);
+  }
+}
+
+// CSR pass 2 (cstart = exclusive scan of cnt): every row claims a position of
+// its slot's run by counting cnt back down
+template <typename K, bool DIRECT, typename R>
+__global__ __launch_bounds__(kBlock) void join_csr_scatter_kernel(const K* __restrict__ keys,
+                                                                 const uint8_t* __restrict__ valid, int64_t n,
+                                                                 const int64_t* __restrict__ tkeys,
+                                                                 R* __restrict__ cnt, const R* __restrict__ cstart,
+                                                                 R* __restrict__ crows, int64_t cap, int64_t kmin) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = build_slot<K, DIRECT>(keys, valid, i, tkeys, cap, kmin);
+    if (s < 0) continue;
+    const R pos = atomic_add(&cnt[s], (R)-1) - 1;
+    crows[(int64_t)cstart[s] + pos] = (R)i;
+  }
+}
+
+// slot holding probe row j's key, -1 when the key is NULL, outside the span,
+// filtered out by the bitmap or (hashed) absent; a direct slot may be empty
+template <typename K, bool DIRECT>
+__device__ inline int64_t probe_slot(const K* keys, const uint8_t* valid, int64_t j, const int64_t* tkeys,
+                                     int64_t cap, int64_t kmin, const uint32_t* bits, uint64_t bmask) {
   int64_t k;
   if (!load_key(keys, valid, j, &k)) return -1;
   if (DIRECT && (k - kmin < 0 || k - kmin >= cap)) return -1;
@@ -112,32 +166,43 @@ __device__ inline int32_t probe_head(const K* keys, const uint8_t* valid, int64_
     const uint64_t b = bloom_bit(k, bmask, kmin);
     if (!((bits[b >> 5] >> (b & 31)) & 1u)) return -1;
   }
-  if (DIRECT) return thead[k - kmin];
-  int64_t s = find_slot(tkeys, cap - 1, k);
-  return s < 0 ? -1 : thead[s];
+  if (DIRECT) return k - kmin;
+  return find_slot(tkeys, cap - 1, k);
 }
 
-// counts[j] = number of build matches of probe row j; first[j] = one match or -1.
-template <typename K, bool DIRECT>
+// counts[j] = number of build matches of probe row j; first[j] = one match or
+// -1; build_matched[r] = 1 for every matched build row. cstart/crows: the CSR
+// runs of a duplicate-key build (null: unique build, thead only).
+template <typename K, bool DIRECT, typename R>
 __global__ __launch_bounds__(kBlock) void join_probe_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
                                                            int64_t m, const int64_t* __restrict__ tkeys,
-                                                           const int32_t* __restrict__ thead,
-                                                           const int32_t* __restrict__ next, int64_t cap, int64_t kmin,
-                                                           int32_t* __restrict__ counts, int32_t* __restrict__ first,
+                                                           const R* __restrict__ thead, const R* __restrict__ cstart,
+                                                           const R* __restrict__ crows, int64_t cap, int64_t kmin,
+                                                           int32_t* __restrict__ counts, R* __restrict__ first,
                                                            uint8_t* __restrict__ build_matched,
                                                            const uint32_t* __restrict__ bits, uint64_t bmask) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
-    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin, bits, bmask);
-    if (first) first[j] = h;
-    if (counts) {
-      int32_t c = 0;
-      for (int32_t r = h; r != -1; r = next[r]) {
-        ++c;
-        if (build_matched) build_matched[r] = 1;
+    const int64_t s = probe_slot<K, DIRECT>(keys, valid, j, tkeys, cap, kmin, bits, bmask);
+    R h = (R)-1;
+    int64_t a = 0, e = 0;
+    if (s >= 0) {
+      if (cstart) {
+        a = cstart[s];
+        e = cstart[s + 1];
+        if (a < e) h = crows[a];
+      } else {
+        h = thead[s];
+        e = h >= 0;
       }
-      counts[j] = c;
-    } else if (build_matched) {
-      for (int32_t r = h; r != -1; r = next[r]) build_matched[r] = 1;
+    }
+    if (first) first[j] = h;
+    if (counts) counts[j] = (int32_t)(e - a);
+    if (build_matched) {
+      if (cstart) {
+        for (int64_t r = a; r < e; ++r) build_matched[crows[r]] = 1;
+      } else if (h >= 0) {
+        build_matched[h] = 1;
+      }
     }
   }
 }
@@ -148,58 +213,70 @@ __global__ __launch_bounds__(kBlock) void join_probe_kernel(const K* __restrict_
 // dependent chain (600M-row lineitem probes were latency-bound).
 constexpr int kProbeRows = 4;
 
-template <typename K>
+template <typename K, typename R>
 __global__ __launch_bounds__(kBlock) void join_probe_first_direct_kernel(
-    const K* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t m, const int32_t* __restrict__ thead,
-    int64_t cap, int64_t kmin, int32_t* __restrict__ first, const uint32_t* __restrict__ bits, uint64_t bmask) {
+    const K* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t m, const R* __restrict__ thead,
+    int64_t cap, int64_t kmin, R* __restrict__ first, const uint32_t* __restrict__ bits, uint64_t bmask) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j0 < m; j0 += stride * kProbeRows) {
+    // unconditional (clamped) loads, results selected afterwards: a load under
+    // a per-lane condition becomes a branch whose merge waits for it
     int64_t s[kProbeRows];
     bool ok[kProbeRows];
 #pragma unroll
     for (int r = 0; r < kProbeRows; ++r) {
       const int64_t j = j0 + r * stride;
-      ok[r] = j < m && (!valid || valid[j]);
-      s[r] = ok[r] ? (int64_t)keys[j] - kmin : -1;
-      ok[r] = ok[r] && s[r] >= 0 && s[r] < cap;
+      const int64_t jc = j < m ? j : m - 1;
+      const bool v = !valid || valid[jc];
+      s[r] = (int64_t)keys[jc] - kmin;
+      ok[r] = j < m && v && s[r] >= 0 && s[r] < cap;
     }
     if (bits) {
       uint32_t w[kProbeRows];
 #pragma unroll
       for (int r = 0; r < kProbeRows; ++r) {
-        const uint64_t b = ok[r] ? bloom_bit(s[r] + kmin, bmask, kmin) : 0;
-        w[r] = ok[r] ? (bits[b >> 5] >> (b & 31)) & 1u : 0u;
+        const uint64_t b = ok[r] || !(bmask & kExactBits) ? bloom_bit(s[r] + kmin, bmask, kmin) : 0;
+        w[r] = bits[b >> 5] >> (b & 31);
       }
 #pragma unroll
-      for (int r = 0; r < kProbeRows; ++r) ok[r] = ok[r] && w[r];
+      for (int r = 0; r < kProbeRows; ++r) ok[r] = ok[r] && (w[r] & 1u);
     }
-    int32_t h[kProbeRows];
+    R h[kProbeRows];
 #pragma unroll
-    for (int r = 0; r < kProbeRows; ++r) h[r] = ok[r] ? thead[s[r]] : -1;
+    for (int r = 0; r < kProbeRows; ++r) h[r] = thead[ok[r] ? s[r] : 0];
 #pragma unroll
     for (int r = 0; r < kProbeRows; ++r) {
       const int64_t j = j0 + r * stride;
-      if (j < m) first[j] = h[r];
+      if (j < m) first[j] = ok[r] ? h[r] : (R)-1;
     }
   }
 }
 
-template <typename K, bool DIRECT>
+// every (probe row, build row) match at offsets[j] (exclusive scan of counts)
+template <typename K, bool DIRECT, typename R>
 __global__ __launch_bounds__(kBlock) void join_expand_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
                                                             int64_t m, const int64_t* __restrict__ tkeys,
-                                                            const int32_t* __restrict__ thead,
-                                                            const int32_t* __restrict__ next, int64_t cap, int64_t kmin,
+                                                            const R* __restrict__ thead, const R* __restrict__ cstart,
+                                                            const R* __restrict__ crows, int64_t cap, int64_t kmin,
                                                             const int64_t* __restrict__ offsets,
-                                                            int32_t* __restrict__ out_probe,
-                                                            int32_t* __restrict__ out_build,
+                                                            int32_t* __restrict__ out_probe, R* __restrict__ out_build,
                                                             const uint32_t* __restrict__ bits, uint64_t bmask) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
-    int32_t h = probe_head<K, DIRECT>(keys, valid, j, tkeys, thead, cap, kmin, bits, bmask);
+    const int64_t s = probe_slot<K, DIRECT>(keys, valid, j, tkeys, cap, kmin, bits, bmask);
+    if (s < 0) continue;
     int64_t o = offsets[j];
-    for (int32_t r = h; r != -1; r = next[r]) {
-      out_probe[o] = (int32_t)j;
-      out_build[o] = r;
-      ++o;
+    if (cstart) {
+      const int64_t e = cstart[s + 1];
+      for (int64_t r = cstart[s]; r < e; ++r, ++o) {
+        out_probe[o] = (int32_t)j;
+        out_build[o] = crows[r];
+      }
+    } else {
+      const R h = thead[s];
+      if (h >= 0) {
+        out_probe[o] = (int32_t)j;
+        out_build[o] = h;
+      }
     }
   }
 }
@@ -289,16 +366,6 @@ __global__ __launch_bounds__(kBlock) void groupby_lookup_kernel(const K* __restr
   }
 }
 
-#define DISPATCH_KEY(key64, direct, KERNEL, ...)                                      \
-  do {                                                                                \
-    if (key64) {                                                                      \
-      if (direct) hipLaunchKernelGGL((KERNEL<int64_t, true>), __VA_ARGS__);           \
-      else hipLaunchKernelGGL((KERNEL<int64_t, false>), __VA_ARGS__);                 \
-    } else {                                                                          \
-      if (direct) hipLaunchKernelGGL((KERNEL<int32_t, true>), __VA_ARGS__);           \
-      else hipLaunchKernelGGL((KERNEL<int32_t, false>), __VA_ARGS__);                 \
-    }                                                                                 \
-  } while (0)
 
 template <typename I>
 __global__ __launch_bounds__(kBlock) void fill_runs_kernel(const I* __restrict__ starts, int64_t nruns, int64_t n,
@@ -319,60 +386,111 @@ void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int3
   check_launch("fill_runs", stream);
 }
 
-void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
-                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, uint32_t* bits,
-                uint64_t bmask, hipStream_t stream) {
+// launch KERNEL<K, DIRECT, R> with keys cast to the key type
+#define DISPATCH_KEY3(key64, direct, R, KERNEL, g, b, shm, st, keys, ...)                                  \
+  do {                                                                                                    \
+    if (key64) {                                                                                          \
+      if (direct) hipLaunchKernelGGL((KERNEL<int64_t, true, R>), g, b, shm, st, (const int64_t*)(keys), __VA_ARGS__); \
+      else hipLaunchKernelGGL((KERNEL<int64_t, false, R>), g, b, shm, st, (const int64_t*)(keys), __VA_ARGS__);       \
+    } else {                                                                                              \
+      if (direct) hipLaunchKernelGGL((KERNEL<int32_t, true, R>), g, b, shm, st, (const int32_t*)(keys), __VA_ARGS__); \
+      else hipLaunchKernelGGL((KERNEL<int32_t, false, R>), g, b, shm, st, (const int32_t*)(keys), __VA_ARGS__);       \
+    }                                                                                                     \
+  } while (0)
+
+void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, void* thead, bool rid64,
+                int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, uint32_t* bits, uint64_t bmask,
+                hipStream_t stream) {
   if (n == 0) return;
   dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
-  if (key64) {
-    if (direct) hipLaunchKernelGGL((join_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
-    else hipLaunchKernelGGL((join_build_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
-  } else {
-    if (direct) hipLaunchKernelGGL((join_build_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
-    else hipLaunchKernelGGL((join_build_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, n, tkeys, thead, next, cap, kmin, dups, bits, bmask);
-  }
+  if (rid64)
+    DISPATCH_KEY3(key64, direct, int64_t, join_build_kernel, g, b, 0, stream, keys, valid, n, tkeys, (int64_t*)thead,
+                  cap, kmin, dups, bits, bmask);
+  else
+    DISPATCH_KEY3(key64, direct, int32_t, join_build_kernel, g, b, 0, stream, keys, valid, n, tkeys, (int32_t*)thead,
+                  cap, kmin, dups, bits, bmask);
   check_launch("join_build", stream);
 }
 
-void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
-                int32_t* first, uint8_t* build_matched, const uint32_t* bits, uint64_t bmask, hipStream_t stream) {
-  if (m == 0) return;
-  dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
-  if (direct && first && !counts && !build_matched) {
+void join_csr_count(const void* keys, bool key64, const uint8_t* valid, int64_t n, const int64_t* tkeys, void* cnt,
+                    bool rid64, int64_t cap, int64_t kmin, bool direct, hipStream_t stream) {
+  if (n == 0) return;
+  dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
+  if (rid64)
+    DISPATCH_KEY3(key64, direct, int64_t, join_csr_count_kernel, g, b, 0, stream, keys, valid, n, tkeys, (int64_t*)cnt,
+                  cap, kmin);
+  else
+    DISPATCH_KEY3(key64, direct, int32_t, join_csr_count_kernel, g, b, 0, stream, keys, valid, n, tkeys, (int32_t*)cnt,
+                  cap, kmin);
+  check_launch("join_csr_count", stream);
+}
+
+void join_csr_scatter(const void* keys, bool key64, const uint8_t* valid, int64_t n, const int64_t* tkeys, void* cnt,
+                      const void* cstart, void* crows, bool rid64, int64_t cap, int64_t kmin, bool direct,
+                      hipStream_t stream) {
+  if (n == 0) return;
+  dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
+  if (rid64)
+    DISPATCH_KEY3(key64, direct, int64_t, join_csr_scatter_kernel, g, b, 0, stream, keys, valid, n, tkeys,
+                  (int64_t*)cnt, (const int64_t*)cstart, (int64_t*)crows, cap, kmin);
+  else
+    DISPATCH_KEY3(key64, direct, int32_t, join_csr_scatter_kernel, g, b, 0, stream, keys, valid, n, tkeys,
+                  (int32_t*)cnt, (const int32_t*)cstart, (int32_t*)crows, cap, kmin);
+  check_launch("join_csr_scatter", stream);
+}
+
+template <typename R>
+static void join_probe_t(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                         const R* thead, const R* cstart, const R* crows, int64_t cap, int64_t kmin, bool direct,
+                         int32_t* counts, R* first, uint8_t* build_matched, const uint32_t* bits, uint64_t bmask,
+                         hipStream_t stream) {
+  const dim3 b(kBlock);
+  if (direct && first && !counts && !build_matched && !cstart) {
     const dim3 g4(grid_for((m + kProbeRows - 1) / kProbeRows, kBlock, kMaxGrid));
     if (key64)
-      hipLaunchKernelGGL(join_probe_first_direct_kernel<int64_t>, g4, b, 0, stream, (const int64_t*)keys, valid, m,
-                         thead, cap, kmin, first, bits, bmask);
+      hipLaunchKernelGGL((join_probe_first_direct_kernel<int64_t, R>), g4, b, 0, stream, (const int64_t*)keys, valid,
+                         m, thead, cap, kmin, first, bits, bmask);
     else
-      hipLaunchKernelGGL(join_probe_first_direct_kernel<int32_t>, g4, b, 0, stream, (const int32_t*)keys, valid, m,
-                         thead, cap, kmin, first, bits, bmask);
+      hipLaunchKernelGGL((join_probe_first_direct_kernel<int32_t, R>), g4, b, 0, stream, (const int32_t*)keys, valid,
+                         m, thead, cap, kmin, first, bits, bmask);
     check_launch("join_probe_first_direct", stream);
     return;
   }
-  if (key64) {
-    if (direct) hipLaunchKernelGGL((join_probe_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
-    else hipLaunchKernelGGL((join_probe_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
-  } else {
-    if (direct) hipLaunchKernelGGL((join_probe_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
-    else hipLaunchKernelGGL((join_probe_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, counts, first, build_matched, bits, bmask);
-  }
+  const dim3 g(grid_for(m, kBlock, kMaxGrid));
+  DISPATCH_KEY3(key64, direct, R, join_probe_kernel, g, b, 0, stream, keys, valid, m, tkeys, thead, cstart, crows, cap,
+                kmin, counts, first, build_matched, bits, bmask);
   check_launch("join_probe", stream);
 }
 
+void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                const void* thead, const void* cstart, const void* crows, bool rid64, int64_t cap, int64_t kmin,
+                bool direct, int32_t* counts, void* first, uint8_t* build_matched, const uint32_t* bits,
+                uint64_t bmask, hipStream_t stream) {
+  if (m == 0) return;
+  if (rid64)
+    join_probe_t<int64_t>(keys, key64, valid, m, tkeys, (const int64_t*)thead, (const int64_t*)cstart,
+                          (const int64_t*)crows, cap, kmin, direct, counts, (int64_t*)first, build_matched, bits,
+                          bmask, stream);
+  else
+    join_probe_t<int32_t>(keys, key64, valid, m, tkeys, (const int32_t*)thead, (const int32_t*)cstart,
+                          (const int32_t*)crows, cap, kmin, direct, counts, (int32_t*)first, build_matched, bits,
+                          bmask, stream);
+}
+
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
-                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, const uint32_t* bits, uint64_t bmask,
-                 hipStream_t stream) {
+                 const void* thead, const void* cstart, const void* crows, bool rid64, int64_t cap, int64_t kmin,
+                 bool direct, const int64_t* offsets, int32_t* out_probe, void* out_build, const uint32_t* bits,
+                 uint64_t bmask, hipStream_t stream) {
   if (m == 0) return;
   dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
-  if (key64) {
-    if (direct) hipLaunchKernelGGL((join_expand_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
-    else hipLaunchKernelGGL((join_expand_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
-  } else {
-    if (direct) hipLaunchKernelGGL((join_expand_kernel<int32_t, true>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
-    else hipLaunchKernelGGL((join_expand_kernel<int32_t, false>), g, b, 0, stream, (const int32_t*)keys, valid, m, tkeys, thead, next, cap, kmin, offsets, out_probe, out_build, bits, bmask);
-  }
+  if (rid64)
+    DISPATCH_KEY3(key64, direct, int64_t, join_expand_kernel, g, b, 0, stream, keys, valid, m, tkeys,
+                  (const int64_t*)thead, (const int64_t*)cstart, (const int64_t*)crows, cap, kmin, offsets, out_probe,
+                  (int64_t*)out_build, bits, bmask);
+  else
+    DISPATCH_KEY3(key64, direct, int32_t, join_expand_kernel, g, b, 0, stream, keys, valid, m, tkeys,
+                  (const int32_t*)thead, (const int32_t*)cstart, (const int32_t*)crows, cap, kmin, offsets, out_probe,
+                  (int32_t*)out_build, bits, bmask);
   check_launch("join_expand", stream);
 }
 
@@ -447,10 +565,93 @@ namespace {
 constexpr int kHitTile = 8192;                 // rows per tile
 constexpr int kHitWords = kHitTile / kWave;    // 64-bit hit words per tile (128)
 
-template <typename K, bool DIRECT>
+// Batched head lookup of kHitBatch probe rows per lane: every key load, then
+// every filter-bit load, then every table load is issued before any result is
+// used, so a lane keeps kHitBatch misses in flight (a row-at-a-time dependent
+// chain left the 600M-row lineitem probes at ~10% of HBM bandwidth,
+// profiles/r3_sf100_pmc_roofline.txt). With an exact membership bitmap the bit
+// IS the answer and the table is not read at all (need_head false).
+constexpr int kHitBatch = 8;
+//
+// All loads are unconditional (indices clamped into range, results selected
+// afterwards): a load under a per-lane condition compiles to a branch whose
+// merge waits for it, which would serialise the batch again.
+template <typename K, bool DIRECT, typename R>
+__device__ inline void probe_heads(const K* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t m,
+                                   const int64_t (&row)[kHitBatch], const int64_t* __restrict__ tkeys,
+                                   const R* __restrict__ thead, int64_t cap, int64_t kmin,
+                                   const uint32_t* __restrict__ bits, uint64_t bmask, bool need_head,
+                                   int64_t (&h)[kHitBatch]) {
+  int64_t k[kHitBatch], rc[kHitBatch];
+  bool ok[kHitBatch];
+#pragma unroll
+  for (int r = 0; r < kHitBatch; ++r) {
+    rc[r] = row[r] < m ? row[r] : m - 1;
+    k[r] = (int64_t)keys[rc[r]];
+  }
+  uint8_t vb[kHitBatch];
+#pragma unroll
+  for (int r = 0; r < kHitBatch; ++r) vb[r] = 1;
+  if (valid) {
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) vb[r] = valid[rc[r]];
+  }
+#pragma unroll
+  for (int r = 0; r < kHitBatch; ++r) {
+    ok[r] = row[r] < m && vb[r];
+    if (DIRECT) ok[r] = ok[r] && k[r] - kmin >= 0 && k[r] - kmin < cap;
+  }
+  if (bits) {
+    uint32_t w[kHitBatch];
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) {
+      // exact bitmaps index by k - kmin: out-of-span keys (ok false) read bit 0
+      const uint64_t b = ok[r] || !(bmask & kExactBits) ? bloom_bit(k[r], bmask, kmin) : 0;
+      w[r] = bits[b >> 5] >> (b & 31);
+    }
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) ok[r] = ok[r] && (w[r] & 1u);
+  }
+  if (!need_head) {
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) h[r] = ok[r] ? 0 : -1;
+    return;
+  }
+  if (DIRECT) {
+    R x[kHitBatch];
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) x[r] = thead[ok[r] ? k[r] - kmin : 0];
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) h[r] = ok[r] ? x[r] : -1;
+  } else {
+    // first slot of every row in flight together; collisions walk on serially
+    const int64_t mask = cap - 1;
+    int64_t slot[kHitBatch], tk[kHitBatch];
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) {
+      slot[r] = (int64_t)(mix64((uint64_t)k[r]) & (uint64_t)mask);
+      tk[r] = tkeys[slot[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) {
+      while (ok[r] && tk[r] != k[r] && tk[r] != kEmptyKey) {
+        slot[r] = (slot[r] + 1) & mask;
+        tk[r] = tkeys[slot[r]];
+      }
+      ok[r] = ok[r] && tk[r] == k[r];
+    }
+    R x[kHitBatch];
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) x[r] = thead[ok[r] ? slot[r] : 0];
+#pragma unroll
+    for (int r = 0; r < kHitBatch; ++r) h[r] = ok[r] ? x[r] : -1;
+  }
+}
+
+template <typename K, bool DIRECT, typename R>
 __global__ __launch_bounds__(kBlock) void probe_hits_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
                                                            int64_t m, const int64_t* __restrict__ tkeys,
-                                                           const int32_t* __restrict__ thead, int64_t cap,
+                                                           const R* __restrict__ thead, int64_t cap,
                                                            int64_t kmin, const uint32_t* __restrict__ bits,
                                                            uint64_t bmask, bool negate,
                                                            unsigned long long* __restrict__ words,
@@ -458,20 +659,24 @@ __global__ __launch_bounds__(kBlock) void probe_hits_kernel(const K* __restrict_
   __shared__ int64_t red[kWavesPerBlock];
   const int lane = lane_id(), wave = threadIdx.x / kWave;
   const int64_t tiles = (m + kHitTile - 1) / kHitTile;
+  // a direct table with an exact bitmap: bit set <=> key present
+  const bool need_head = !(DIRECT && bits && (bmask & kExactBits));
   for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
     int64_t cnt = 0;
-#pragma unroll 4
-    for (int it = 0; it < kHitTile / kBlock; ++it) {
-      const int64_t row = t * kHitTile + (int64_t)it * kBlock + threadIdx.x;
-      bool hit = false;
-      if (row < m) {
-        const int32_t h = probe_head<K, DIRECT>(keys, valid, row, tkeys, thead, cap, kmin, bits, bmask);
-        hit = (h >= 0) != negate;
+    for (int it0 = 0; it0 < kHitTile / kBlock; it0 += kHitBatch) {
+      int64_t row[kHitBatch];
+      int64_t h[kHitBatch];
+#pragma unroll
+      for (int r = 0; r < kHitBatch; ++r) row[r] = t * kHitTile + (int64_t)(it0 + r) * kBlock + threadIdx.x;
+      probe_heads<K, DIRECT, R>(keys, valid, m, row, tkeys, thead, cap, kmin, bits, bmask, need_head, h);
+#pragma unroll
+      for (int r = 0; r < kHitBatch; ++r) {
+        const bool hit = row[r] < m && ((h[r] >= 0) != negate);
+        const unsigned long long b = __ballot(hit);
+        if (lane == 0 && t * kHitTile + (int64_t)(it0 + r) * kBlock + wave * kWave < m)
+          words[t * kHitWords + (it0 + r) * kWavesPerBlock + wave] = b;
+        cnt += __popcll(b);
       }
-      const unsigned long long b = __ballot(hit);
-      if (lane == 0 && t * kHitTile + (int64_t)it * kBlock + wave * kWave < m)
-        words[t * kHitWords + it * kWavesPerBlock + wave] = b;
-      cnt += __popcll(b);
     }
     if (lane == 0) red[wave] = cnt;
     __syncthreads();
@@ -484,13 +689,13 @@ __global__ __launch_bounds__(kBlock) void probe_hits_kernel(const K* __restrict_
   }
 }
 
-template <typename K, bool DIRECT, typename O>
+template <typename K, bool DIRECT, typename R, typename O>
 __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict__ keys, const uint8_t* __restrict__ valid,
                                                             int64_t m, const int64_t* __restrict__ tkeys,
-                                                            const int32_t* __restrict__ thead, int64_t cap,
+                                                            const R* __restrict__ thead, int64_t cap,
                                                             int64_t kmin, const unsigned long long* __restrict__ words,
                                                             const int64_t* __restrict__ tile_off,
-                                                            O* __restrict__ out_probe, int32_t* __restrict__ out_build) {
+                                                            O* __restrict__ out_probe, R* __restrict__ out_build) {
   __shared__ int64_t woff[kHitWords];
   __shared__ int64_t scratch[kWavesPerBlock + 1];
   const int lane = lane_id(), wave = threadIdx.x / kWave;
@@ -505,13 +710,27 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
     __syncthreads();
     if (total) {
       const int64_t base = tile_off[t];
-      for (int w = wave; w < nwords; w += kWavesPerBlock) {
-        const unsigned long long b = words[t * kHitWords + w];
-        if (!((b >> lane) & 1ULL)) continue;
-        const int64_t row = t * kHitTile + (int64_t)w * kWave + lane;
-        const int64_t pos = base + woff[w] + __popcll(b & ((1ULL << lane) - 1ULL));
-        out_probe[pos] = (O)row;
-        if (out_build) out_build[pos] = probe_head<K, DIRECT>(keys, valid, row, tkeys, thead, cap, kmin, nullptr, 0);
+      // kHitBatch hit words per wave at a time (waves own words wave, wave+4, ...)
+      for (int w0 = wave; w0 < nwords; w0 += kWavesPerBlock * kHitBatch) {
+        unsigned long long b[kHitBatch];
+        int64_t row[kHitBatch];
+#pragma unroll
+        for (int r = 0; r < kHitBatch; ++r) {
+          const int w = w0 + r * kWavesPerBlock;
+          b[r] = w < nwords ? words[t * kHitWords + w] : 0ULL;
+          // rows that are not hits are pushed past m: probe_heads skips them
+          row[r] = ((b[r] >> lane) & 1ULL) ? t * kHitTile + (int64_t)w * kWave + lane : m;
+        }
+        int64_t h[kHitBatch];
+        if (out_build) probe_heads<K, DIRECT, R>(keys, valid, m, row, tkeys, thead, cap, kmin, nullptr, 0, true, h);
+#pragma unroll
+        for (int r = 0; r < kHitBatch; ++r) {
+          if (row[r] >= m) continue;
+          const int w = w0 + r * kWavesPerBlock;
+          const int64_t pos = base + woff[w] + __popcll(b[r] & ((1ULL << lane) - 1ULL));
+          out_probe[pos] = (O)row[r];
+          if (out_build) out_build[pos] = (R)h[r];
+        }
       }
     }
     __syncthreads();
@@ -522,44 +741,61 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
 int64_t probe_hit_tiles(int64_t m) { return (m + kHitTile - 1) / kHitTile; }
 
 void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits, uint64_t bmask,
-                bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream) {
+                const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits,
+                uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream) {
   if (m == 0) return;
   const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
-#define IG_PH(KT, D)                                                                                              \
-  hipLaunchKernelGGL((probe_hits_kernel<KT, D>), g, b, 0, stream, (const KT*)keys, valid, m, tkeys, thead, cap, kmin, \
-                     bits, bmask, negate, words, tile_counts)
-  if (key64) {
-    if (direct) IG_PH(int64_t, true);
-    else IG_PH(int64_t, false);
-  } else {
-    if (direct) IG_PH(int32_t, true);
-    else IG_PH(int32_t, false);
-  }
-#undef IG_PH
+  if (rid64)
+    DISPATCH_KEY3(key64, direct, int64_t, probe_hits_kernel, g, b, 0, stream, keys, valid, m, tkeys,
+                  (const int64_t*)thead, cap, kmin, bits, bmask, negate, words, tile_counts);
+  else
+    DISPATCH_KEY3(key64, direct, int32_t, probe_hits_kernel, g, b, 0, stream, keys, valid, m, tkeys,
+                  (const int32_t*)thead, cap, kmin, bits, bmask, negate, words, tile_counts);
   check_launch("probe_hits", stream);
 }
 
-void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                 const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
-                 const int64_t* tile_off, void* out_probe, bool out64, int32_t* out_build, hipStream_t stream) {
-  if (m == 0) return;
+template <typename R, typename O>
+static void probe_write_t(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                          const R* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
+                          const int64_t* tile_off, O* out_probe, R* out_build, hipStream_t stream) {
   const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
-#define IG_PW(KT, D, OT)                                                                                           \
-  hipLaunchKernelGGL((probe_write_kernel<KT, D, OT>), g, b, 0, stream, (const KT*)keys, valid, m, tkeys, thead, cap, \
-                     kmin, words, tile_off, (OT*)out_probe, out_build)
-#define IG_PW2(KT, D) \
-  if (out64) IG_PW(KT, D, int64_t); else IG_PW(KT, D, int32_t)
   if (key64) {
-    if (direct) { IG_PW2(int64_t, true); }
-    else { IG_PW2(int64_t, false); }
+    if (direct)
+      hipLaunchKernelGGL((probe_write_kernel<int64_t, true, R, O>), g, b, 0, stream, (const int64_t*)keys, valid, m,
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
+    else
+      hipLaunchKernelGGL((probe_write_kernel<int64_t, false, R, O>), g, b, 0, stream, (const int64_t*)keys, valid, m,
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
   } else {
-    if (direct) { IG_PW2(int32_t, true); }
-    else { IG_PW2(int32_t, false); }
+    if (direct)
+      hipLaunchKernelGGL((probe_write_kernel<int32_t, true, R, O>), g, b, 0, stream, (const int32_t*)keys, valid, m,
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
+    else
+      hipLaunchKernelGGL((probe_write_kernel<int32_t, false, R, O>), g, b, 0, stream, (const int32_t*)keys, valid, m,
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
   }
-#undef IG_PW2
-#undef IG_PW
   check_launch("probe_write", stream);
+}
+
+void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
+                 const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
+                 const int64_t* tile_off, void* out_probe, bool out64, void* out_build, hipStream_t stream) {
+  if (m == 0) return;
+  if (rid64) {
+    if (out64)
+      probe_write_t<int64_t, int64_t>(keys, key64, valid, m, tkeys, (const int64_t*)thead, cap, kmin, direct, words,
+                                      tile_off, (int64_t*)out_probe, (int64_t*)out_build, stream);
+    else
+      probe_write_t<int64_t, int32_t>(keys, key64, valid, m, tkeys, (const int64_t*)thead, cap, kmin, direct, words,
+                                      tile_off, (int32_t*)out_probe, (int64_t*)out_build, stream);
+  } else {
+    if (out64)
+      probe_write_t<int32_t, int64_t>(keys, key64, valid, m, tkeys, (const int32_t*)thead, cap, kmin, direct, words,
+                                      tile_off, (int64_t*)out_probe, (int32_t*)out_build, stream);
+    else
+      probe_write_t<int32_t, int32_t>(keys, key64, valid, m, tkeys, (const int32_t*)thead, cap, kmin, direct, words,
+                                      tile_off, (int32_t*)out_probe, (int32_t*)out_build, stream);
+  }
 }
 }  // namespace kern
 }  // namespace igloo

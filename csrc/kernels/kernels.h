@@ -133,25 +133,37 @@ void hll_sketch(const void* keys, bool key64, const uint8_t* valid, int64_t n, u
 // ---- hashtable.hip -----------------------------------------------------------
 // bits/bmask: optional Bloom filter (bits: (bmask+1)/32 words, zeroed before
 // join_build; nullptr disables it on build or probe)
-void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, int32_t* thead,
-                int32_t* next, int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, uint32_t* bits,
-                uint64_t bmask, hipStream_t stream);
+// Row ids (thead, CSR cstart/crows, first / build-row outputs) are int32 when
+// rid64 is false (build side < 2^31 rows) and int64 otherwise.
+void join_build(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t* tkeys, void* thead, bool rid64,
+                int64_t cap, int64_t kmin, bool direct, unsigned long long* dups, uint32_t* bits, uint64_t bmask,
+                hipStream_t stream);
+// CSR runs of a duplicate-key build: cnt[cap+1] zeroed -> per-slot counts;
+// cstart = exclusive scan of cnt (cap+1 entries); scatter fills crows[n] and
+// consumes cnt
+void join_csr_count(const void* keys, bool key64, const uint8_t* valid, int64_t n, const int64_t* tkeys, void* cnt,
+                    bool rid64, int64_t cap, int64_t kmin, bool direct, hipStream_t stream);
+void join_csr_scatter(const void* keys, bool key64, const uint8_t* valid, int64_t n, const int64_t* tkeys, void* cnt,
+                      const void* cstart, void* crows, bool rid64, int64_t cap, int64_t kmin, bool direct,
+                      hipStream_t stream);
+// cstart/crows null: unique build (thead only)
 void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct, int32_t* counts,
-                int32_t* first, uint8_t* build_matched, const uint32_t* bits, uint64_t bmask, hipStream_t stream);
+                const void* thead, const void* cstart, const void* crows, bool rid64, int64_t cap, int64_t kmin,
+                bool direct, int32_t* counts, void* first, uint8_t* build_matched, const uint32_t* bits,
+                uint64_t bmask, hipStream_t stream);
 // first-match probe as a row selection: pass 1 hit bits (words[tiles*128]) + per-tile counts, pass 2
 // (tile_off = exclusive scan of the counts) writes hit rows (+ their build rows) in row order
 int64_t probe_hit_tiles(int64_t m);
 void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits, uint64_t bmask,
-                bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream);
+                const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits,
+                uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream);
 void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                 const int32_t* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
-                 const int64_t* tile_off, void* out_probe, bool out64, int32_t* out_build, hipStream_t stream);
+                 const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
+                 const int64_t* tile_off, void* out_probe, bool out64, void* out_build, hipStream_t stream);
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
-                 const int32_t* thead, const int32_t* next, int64_t cap, int64_t kmin, bool direct,
-                 const int64_t* offsets, int32_t* out_probe, int32_t* out_build, const uint32_t* bits, uint64_t bmask,
-                 hipStream_t stream);
+                 const void* thead, const void* cstart, const void* crows, bool rid64, int64_t cap, int64_t kmin,
+                 bool direct, const int64_t* offsets, int32_t* out_probe, void* out_build, const uint32_t* bits,
+                 uint64_t bmask, hipStream_t stream);
 // run ids of a non-decreasing key column: gid[i] = r for rows in [starts[r], starts[r+1])
 void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int32_t* gid, hipStream_t stream);
 void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,

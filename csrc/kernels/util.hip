@@ -63,8 +63,10 @@ __global__ __launch_bounds__(kBlock) void column_stats_kernel(const T* __restric
         const uint4 w = reinterpret_cast<const uint4*>(k + base)[q];
         __builtin_memcpy(&v[q * 16 / sizeof(T)], &w, 16);
       }
-      const T before = base > 0 ? k[base - 1] : v[0];
-      bad |= v[0] < before;
+      // unconditional (clamped) load: a conditional one would make the branch
+      // merge wait for the four vector loads above
+      const T before = k[base > 0 ? base - 1 : 0];
+      bad |= base > 0 && v[0] < before;
 #pragma unroll
       for (int j = 0; j < kRun; ++j) {
         tmn = v[j] < tmn ? v[j] : tmn;

@@ -290,6 +290,18 @@ class CachedTable(TableSource):
         keys = list(b.columns)
         return Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], rows))), int(rows.numel()))
 
+    def scan_morsels(self, columns: Sequence[str], ctx, filters=None, max_rows: int = 1 << 20):
+        """Morsels straight from the source (exec/morsel.py): a streamed scan
+        exists to keep the table out of device memory, so it bypasses the
+        cache tier."""
+        if self.cdc is not None:
+            self.cdc.maybe_poll(self.name, self.poll_interval_s)
+        yield from self.source.scan_morsels(columns, ctx, filters, max_rows)
+
+    @property
+    def can_stream(self) -> bool:
+        return bool(getattr(self.source, "can_stream", False))
+
     def _scan_all(self, columns: Sequence[str], ctx) -> Batch:
         ver = None
         if self.cdc is not None:

@@ -107,6 +107,23 @@ class MemoryTable(TableSource):
             out[c] = col
         return Batch(out, self._n)
 
+    #: ``scan_morsels`` available (exec/morsel.py)
+    can_stream = True
+
+    def scan_morsels(self, columns, ctx, filters=None, max_rows: int = 1 << 20):
+        """Row ranges of at most ``max_rows`` rows, each moved to the execution
+        device on its own (exec/morsel.py): a host-resident table streams
+        through a bounded device working set."""
+        from .cache.cdc import _slice
+        dev = ctx.device if ctx is not None else None
+        for a in range(0, self._n, max(1, max_rows)):
+            z = min(self._n, a + max_rows)
+            out = {}
+            for c in columns:
+                col = _slice(self.columns[c], a, z)
+                out[c] = col.to(dev) if dev is not None and col.device != dev else col
+            yield Batch(out, z - a)
+
     @property
     def nbytes(self) -> int:
         return sum(c.nbytes for c in self.columns.values())

@@ -73,6 +73,8 @@ class ParquetTable(TableSource):
     cacheable = True
     #: ``scan`` takes pushed filters for row-group statistics pruning
     prunes = True
+    #: ``scan_morsels`` available (exec/morsel.py)
+    can_stream = True
 
     def __init__(self, path: str, files: Optional[List[str]] = None, local: bool = False,
                  partitioned_by: Optional[str] = None, replicated: bool = False, cache: Optional[bool] = None):
@@ -148,9 +150,25 @@ class ParquetTable(TableSource):
         return keep
 
     # ------------------------------------------------------------- scan
-    def scan(self, columns: Sequence[str], ctx, filters=None) -> Batch:
+    def scan_morsels(self, columns: Sequence[str], ctx, filters=None, max_rows: int = 1 << 20):
+        """This rank's row groups (after statistics pruning) in runs of whole
+        row groups of about ``max_rows`` rows, each decoded on its own
+        (exec/morsel.py)."""
+        groups = self.prune(self.my_row_groups(ctx), filters)
+        run, rows = [], 0
+        for fi, rg in groups:
+            n = self._meta[fi].row_group(rg).num_rows
+            if run and rows + n > max_rows:
+                yield self.scan(columns, ctx, groups=run)
+                run, rows = [], 0
+            run.append((fi, rg))
+            rows += n
+        if run:
+            yield self.scan(columns, ctx, groups=run)
+
+    def scan(self, columns: Sequence[str], ctx, filters=None, groups=None) -> Batch:
         device = ctx.device if ctx is not None else torch.device("cpu")
-        all_groups = self.my_row_groups(ctx)
+        all_groups = self.my_row_groups(ctx) if groups is None else list(groups)
         groups = self.prune(all_groups, filters)
         stats = {"row_groups": len(all_groups), "row_groups_read": len(groups),
                  "row_groups_pruned": len(all_groups) - len(groups)}

@@ -341,7 +341,7 @@ class QueryEngine:
             self.cache.enforce()   # derived structures built by this query count against the budget
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
-                             "spill": dict(ctx.spill), "plan_cached": cached, "speculation": spec,
+                             "spill": dict(ctx.spill), "morsels": dict(ctx.morsels), "plan_cached": cached, "speculation": spec,
                              # work that left the GPU (ops/_lib.py note_host_step)
                              "host_steps": sum(HOST_STEPS.values()) - h0}
         if self.comm is not None:
@@ -633,8 +633,13 @@ class QueryEngine:
             for n in _walk_exec(node):
                 if getattr(n, "order_log", None):
                     txt += "\njoin order: " + " ; ".join(n.order_log)
-            if ctx.spill["joins"]:
+            if ctx.morsels["pipelines"]:
+                m = ctx.morsels
+                txt += (f"\nmorsels: {m['pipelines']} pipeline(s), {m['morsels']} morsels, {m['rows']} rows, "
+                        f"{m['bytes']} bytes streamed (device budget {ctx.budget} bytes)")
+            if ctx.spill["joins"] or ctx.spill.get("sorts"):
                 txt += (f"\nspill: {ctx.spill['joins']} partitioned join(s), {ctx.spill['partitions']} partitions, "
+                        f"{ctx.spill.get('sorts', 0)} external sort(s), {ctx.spill.get('sort_runs', 0)} sort runs, "
                         f"{ctx.spill['bytes']} bytes staged in host memory (device budget {ctx.budget} bytes)")
             if self.comm is not None and self.comm.spmd:
                 txt += (f"\nexchange: {self.comm.calls - c0[0]} collectives, "

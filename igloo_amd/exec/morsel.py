@@ -1,0 +1,264 @@
+"""Morsel-driven streaming and external sort under a device memory budget.
+
+The reference streams 1024-row record batches from its Parquet scan through
+bounded channels into the operators above it (reference
+crates/engine/src/operators/parquet_scan.rs:44-66; the hash join's probe
+channel, crates/engine/src/operators/hash_join.rs:136-138), so no operator
+holds a whole table. Here operators normally take whole device-resident
+columns (the HBM tier holds the tables: 288 GB per GPU). When a session sets a
+device budget (``device_budget_gb`` / IGLOO_DEVICE_BUDGET_GB) and a scan's
+columns exceed a fraction of it, the aggregation above that scan runs as a
+morsel pipeline instead:
+
+* the scan is read in morsels of whole row groups (Parquet) or row ranges
+  (host-resident memory tables), each sized to ``budget / MORSEL_FRACTION``
+  bytes, and moved to the device one at a time;
+* every morsel flows through the operators between the scan and the
+  aggregate (filters, projections, joins whose other side is built once and
+  memoised for the whole pipeline) and ends as PARTIAL aggregate states — the
+  same phase-1 states the SPMD exchange merges across ranks
+  (parallel/exchange.py ``partial_plan`` / ``merge_partials``);
+* the partial states of all morsels are concatenated and merged once.
+
+A scan can stream when every operator between it and the aggregate
+distributes over a union of row sets: filters, projections, inner joins (either
+side), the preserved side of left joins, the probe side of semi / anti joins,
+and inner multi-way joins. Anything else (a scan under another aggregate, a
+sort, a limit, the build side of an outer / semi join) runs whole, where the
+grace join (operators.py ``grace_join``) bounds its joins.
+
+``external_sort`` is the ORDER BY counterpart: an input over the budget is
+range-partitioned on its leading sort key by sampled splitters, the partitions
+are staged in pinned host memory, and each is brought back, sorted on the
+device and staged again; their concatenation is the sorted result.
+
+EXPLAIN ANALYZE reports both ("morsels: ..." and "spill: ...").
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+
+from ..columnar import Batch
+
+#: a morsel's scanned bytes are at most budget / MORSEL_FRACTION
+MORSEL_FRACTION = int(os.environ.get("IGLOO_MORSEL_FRACTION", "8"))
+#: stream a scan whose columns exceed budget / STREAM_FRACTION
+STREAM_FRACTION = int(os.environ.get("IGLOO_STREAM_FRACTION", "4"))
+MORSEL_MIN_ROWS = 1 << 14
+#: bytes per row assumed for a string column without statistics
+STRING_ROW_BYTES = 40
+
+
+# --------------------------------------------------------------- planning
+def _walk(node):
+    yield node
+    for c in node.children:
+        yield from _walk(c)
+
+
+def _contains(node, target) -> bool:
+    return any(n is target for n in _walk(node))
+
+
+def stream_path_ok(node, target) -> bool:
+    """Every operator on the path from ``node`` down to scan ``target``
+    distributes over a union of the scan's rows (see the module docstring)."""
+    from .operators import FilterExec, HashJoinExec, MultiJoinExec, ProjectExec
+    if node is target:
+        return True
+    if isinstance(node, (FilterExec, ProjectExec)):
+        return stream_path_ok(node.children[0], target)
+    if isinstance(node, HashJoinExec):
+        kind = node.logical.kind
+        left, right = node.children
+        if _contains(left, target):
+            return kind in ("inner", "left", "semi", "anti") and stream_path_ok(left, target)
+        if _contains(right, target):
+            return kind in ("inner", "right") and stream_path_ok(right, target)
+        return False
+    if isinstance(node, MultiJoinExec):
+        inside = [c for c in node.children if _contains(c, target)]
+        return len(inside) == 1 and stream_path_ok(inside[0], target)
+    return False
+
+
+def scan_bytes(scan) -> int:
+    """Bytes the scan's columns occupy (row count x column widths)."""
+    src = scan.logical.source
+    n = src.num_rows() if hasattr(src, "num_rows") else None
+    if not n:
+        return 0
+    names, _, _ = scan.column_names()
+    width = 0
+    for name in names:
+        try:
+            t = src.field(name).dtype
+        except Exception:  # noqa: BLE001 - sources without field lookup
+            width += 8
+            continue
+        if t.is_string:
+            width += STRING_ROW_BYTES
+        else:
+            width += max(1, getattr(t, "byte_width", None) or 8) + 1
+    return int(n) * width
+
+
+def pick_stream_scan(agg, ctx):
+    """The largest streamable scan below aggregate ``agg`` whose columns exceed
+    budget / STREAM_FRACTION, or None."""
+    from .operators import ScanExec
+    best, best_bytes = None, ctx.budget // STREAM_FRACTION
+    for n in _walk(agg.children[0]):
+        if not isinstance(n, ScanExec) or not getattr(n.logical.source, "can_stream", False):
+            continue
+        b = scan_bytes(n)
+        if b > best_bytes and stream_path_ok(agg.children[0], n):
+            best, best_bytes = n, b
+    return best
+
+
+# -------------------------------------------------------------- execution
+def streamed_aggregate(agg, ctx) -> Optional[Batch]:
+    """Run aggregate node ``agg`` as a morsel pipeline when the budget calls
+    for it; None when it does not (or the aggregates do not decompose)."""
+    from ..parallel.exchange import _TmpIds, decomposable, merge_partials, partial_plan
+    from .operators import ScanExec, aggregate, apply_key_filters, concat_batches
+    lg = agg.logical
+    if ctx.budget is None or ctx.spmd or not decomposable(lg.aggs):
+        return None
+    if any(getattr(a, "filter", None) is not None and _has_subquery(a.filter) for _, a in lg.aggs):
+        return None
+    scan = pick_stream_scan(agg, ctx)
+    if scan is None:
+        return None
+    child = agg.children[0]
+    names, _, _ = scan.column_names()
+    src = scan.logical.source
+    row_bytes = max(1, scan_bytes(scan) // max(1, src.num_rows() or 1))
+    max_rows = max(MORSEL_MIN_ROWS, ctx.budget // MORSEL_FRACTION // row_bytes)
+    ids = _TmpIds()
+    partial, plan = partial_plan(lg.aggs, ids)
+    # everything below the aggregate that does not read the streamed scan is
+    # computed once and reused by every morsel
+    on_path = {id(n) for n in _walk(child) if _contains(n, scan)}
+    saved = (ctx.memo, ctx.memo_ids, ctx.morsel)
+    ctx.memo, ctx.memo_ids = {}, {id(n) for n in _walk(child) if id(n) not in on_path}
+    ctx.morsel_depth += 1
+    parts: List[Batch] = []
+    stats = ctx.morsels
+    stats["pipelines"] += 1
+    try:
+        with ctx.span("morsel.pipeline"):
+            for k, raw in enumerate(src.scan_morsels(names, ctx, scan.pushable(), max_rows)):
+                ctx.morsel = (id(scan), raw, ("morsel", stats["pipelines"], k))
+                stats["morsels"] += 1
+                stats["rows"] += raw.num_rows
+                stats["bytes"] += raw.nbytes
+                ctx.rows_scanned += raw.num_rows
+                if isinstance(child, ScanExec):
+                    pb = None
+                    if ctx.device.type == "cuda" and not agg.runtime_filters:
+                        from . import fused
+                        pb = fused.fused_scan_aggregate(lg.groups, partial, scan.scan_raw(ctx), scan.predicate, ctx)
+                    b = child.execute(ctx) if pb is None else None
+                else:
+                    pb, b = None, child.execute(ctx)
+                if pb is None:
+                    if agg.runtime_filters:
+                        b = apply_key_filters(b, list(agg.runtime_filters), ctx)
+                    pb = aggregate(lg.groups, partial, b, ctx)
+                parts.append(pb)
+                ctx.scan_cache = {k2: v for k2, v in ctx.scan_cache.items() if k2[-1] != ctx.morsel[2]}
+                ctx.morsel = None
+    finally:
+        ctx.memo, ctx.memo_ids, ctx.morsel = saved
+        ctx.morsel_depth -= 1
+        agg.runtime_filters = []
+    if not parts:
+        return None
+    with ctx.span("morsel.merge"):
+        rb = concat_batches(parts)
+        return merge_partials(lg.groups, plan, rb, ids, ctx)
+
+
+def _has_subquery(e) -> bool:
+    from ..sql.expr import has_subquery
+    return has_subquery(e)
+
+
+# ------------------------------------------------------------ external sort
+#: rows sampled per partition when choosing range splitters
+SAMPLE_PER_PART = 64
+#: a sort's working memory is taken as this multiple of its input bytes
+SORT_MEM_FACTOR = 3
+
+
+def external_sort(b: Batch, keys, fetch, ctx) -> Optional[Batch]:
+    """ORDER BY over an input whose working memory exceeds the budget: range
+    partitions on the leading key (sampled splitters), staged in host memory,
+    each sorted on the device; None when the input fits (or the leading key
+    is not a plain fixed-width column)."""
+    from .operators import _batch_bytes, _take_batch, _to_device, _to_host, concat_batches, sort_batch
+    if ctx.budget is None or fetch is not None or b.num_rows < 2:
+        return None
+    need = SORT_MEM_FACTOR * _batch_bytes(b)
+    if need <= ctx.budget:
+        return None
+    e, asc, nulls_first = keys[0]
+    lead = ctx.evaluator.column(e, b)
+    if lead.dtype.is_string or lead.is_wide or lead.data.dim() != 1 or lead.dictionary is not None:
+        return None
+    P = 2
+    while need / P > ctx.budget / 2 and P < 4096:
+        P *= 2
+    n = b.num_rows
+    v = lead.data.to(torch.float64) if lead.data.dtype.is_floating_point else lead.data.to(torch.int64)
+    valid = lead.valid
+    # splitters: quantiles of a strided sample of the non-NULL leading keys
+    step = max(1, n // (P * SAMPLE_PER_PART))
+    samp = v[::step] if valid is None else v[::step][valid[::step]]
+    if samp.numel() == 0:
+        return None
+    samp, _ = torch.sort(samp)
+    q = torch.linspace(0, samp.numel() - 1, P + 1, device=samp.device)[1:-1].round().long()
+    split = torch.unique(samp.index_select(0, q))
+    # partition id: searchsorted on the splitters; descending order flips it;
+    # NULLs form their own partition at the requested end
+    pid = torch.searchsorted(split, v, right=True)
+    nparts = split.numel() + 1
+    if not asc:
+        pid = nparts - 1 - pid
+    if valid is not None:
+        pid = torch.where(valid, pid + (1 if nulls_first else 0),
+                          torch.full_like(pid, 0 if nulls_first else nparts))
+        nparts += 1
+    order = torch.argsort(pid, stable=True)
+    counts = torch.bincount(pid, minlength=nparts).tolist()
+    dev = ctx.device
+    outs, start = [], 0
+    ctx.spill["sorts"] = ctx.spill.get("sorts", 0) + 1
+    saved, ctx.budget = ctx.budget, None      # each partition sorts in memory
+    try:
+        with ctx.span("sort.spill_partitions"):
+            parts = []
+            for c in counts:
+                if c == 0:
+                    continue
+                piece = _take_batch(b, order[start:start + c])
+                start += c
+                ctx.spill["sort_runs"] = ctx.spill.get("sort_runs", 0) + 1
+                ctx.spill["bytes"] += _batch_bytes(piece)
+                parts.append(_to_host(piece) if dev.type == "cuda" else piece)
+            del order, pid
+        with ctx.span("sort.spill_runs"):
+            for p in parts:
+                d = _to_device(p, dev) if dev.type == "cuda" else p
+                s = sort_batch(d, keys, None, ctx)
+                outs.append(_to_host(s) if dev.type == "cuda" else s)
+    finally:
+        ctx.budget = saved
+    return concat_batches([_to_device(o, dev) if dev.type == "cuda" else o for o in outs])
+

@@ -75,6 +75,14 @@ class ExecContext:
         # from (a graph replay refreshes their LRU position)
         self.sources: list = []
         self.cache_keys: list = []
+        # morsel pipelines (exec/morsel.py): the streamed scan's current morsel
+        # (scan node id, raw batch, tag), results of the operators a pipeline
+        # computes once (node id -> Batch, for the node ids in memo_ids)
+        self.morsel = None
+        self.memo: Optional[dict] = None
+        self.memo_ids: set = set()
+        self.morsel_depth = 0
+        self.morsels = {"pipelines": 0, "morsels": 0, "rows": 0, "bytes": 0}
 
     def note_scan(self, source, rows: int) -> None:
         if id(source) not in self._scanned_sources:
@@ -201,6 +209,15 @@ class ExecNode:
     logical: L.Plan
 
     def execute(self, ctx: ExecContext) -> Batch:
+        if ctx.memo is not None and id(self) in ctx.memo_ids:
+            # computed once per morsel pipeline (exec/morsel.py)
+            hit = ctx.memo.get(id(self))
+            if hit is None:
+                hit = ctx.memo[id(self)] = self._execute_traced(ctx)
+            return hit
+        return self._execute_traced(ctx)
+
+    def _execute_traced(self, ctx: ExecContext) -> Batch:
         if _trace.ENABLED:
             _trace.push(type(self).__name__)
             try:
@@ -265,8 +282,9 @@ class ScanExec(ExecNode):
         f = f", filters=[{', '.join(x.sql() for x in s.filters)}]" if s.filters else ""
         return f"{s.table} projection=[{', '.join(c.name for c in s.schema)}]{f}"
 
-    def scan_raw(self, ctx) -> Batch:
-        """Scanned columns (projection + filter inputs) before filtering, keyed by cid."""
+    def column_names(self):
+        """(source column names to read, their cids, cid -> ColInfo): the
+        projection plus every filter input."""
         s = self.logical
         table_cols = getattr(s, "table_cols", s.schema)
         by_cid = {c.cid: c for c in table_cols}
@@ -275,16 +293,30 @@ class ScanExec(ExecNode):
         need = {c.cid for c in s.schema}
         for f in s.filters:
             need |= col_refs(f)
-        names = [by_cid[cid].name for cid in sorted(need)]
-        with ctx.span("scan.source"):
-            if s.filters and getattr(s.source, "prunes", False):
+        return [by_cid[cid].name for cid in sorted(need)], need, by_cid
+
+    def pushable(self):
+        """Filters the source can test against row-group statistics (or None)."""
+        s = self.logical
+        if not (s.filters and getattr(s.source, "prunes", False)):
+            return None
+        from ..connectors.parquet import pushable_filters
+        _, need, by_cid = self.column_names()
+        return pushable_filters(s.filters, {cid: by_cid[cid].name for cid in need})
+
+    def scan_raw(self, ctx) -> Batch:
+        """Scanned columns (projection + filter inputs) before filtering, keyed by cid."""
+        s = self.logical
+        table_cols = getattr(s, "table_cols", s.schema)
+        names, need, by_cid = self.column_names()
+        if ctx.morsel is not None and ctx.morsel[0] == id(self):
+            raw = ctx.morsel[1]          # the current morsel of a pipeline (exec/morsel.py)
+        else:
+            with ctx.span("scan.source"):
+                pf = self.pushable()
                 # row-group statistics pruning (the filter is still applied below)
-                from ..connectors.parquet import pushable_filters
-                pf = pushable_filters(s.filters, {cid: by_cid[cid].name for cid in need})
-                raw = s.source.scan(names, ctx, filters=pf)
-            else:
-                raw = s.source.scan(names, ctx)
-        ctx.note_scan(s.source, raw.num_rows)
+                raw = s.source.scan(names, ctx, filters=pf) if pf is not None else s.source.scan(names, ctx)
+            ctx.note_scan(s.source, raw.num_rows)
         cols = {cid: raw.columns[by_cid[cid].name] for cid in sorted(need)}
         dist = None
         if ctx.spmd:
@@ -309,7 +341,7 @@ class ScanExec(ExecNode):
             name = {c.cid: c.name for c in getattr(s, "table_cols", s.schema)}
             name.update({c.cid: c.name for c in s.schema})
             fsql = tuple(sorted(_CID.sub("", f.sql()) for f in s.filters))
-            key = (id(s.source), b.num_rows, fsql)
+            key = (id(s.source), b.num_rows, fsql, ctx.morsel[2] if ctx.morsel is not None else None)
             hit = None if any("random" in x.lower() for x in fsql) else ctx.scan_cache.get(key)
             if hit is None:
                 with ctx.span("scan.filter_eval"):
@@ -543,7 +575,9 @@ class HashJoinExec(ExecNode):
     def _run(self, ctx):
         j = self.logical
         lb = self.children[0].execute(ctx)
-        if j.kind in ("inner", "left", "semi") and j.on:
+        if j.kind in ("inner", "left", "semi") and j.on and ctx.memo is None:
+            # (not inside a morsel pipeline: the build side is computed once
+            # for all morsels, so it must not be narrowed to one morsel's keys)
             push_key_filter(self.children[1], j.on, lb, ctx)
         rb = self.children[1].execute(ctx)
         if ctx.spmd:
@@ -1870,6 +1904,11 @@ class HashAggExec(ExecNode):
     def _run(self, ctx):
         lg = self.logical
         child = self.children[0]
+        if ctx.budget is not None:
+            from .morsel import streamed_aggregate
+            out = streamed_aggregate(self, ctx)
+            if out is not None:
+                return out
         if ctx.device.type == "cuda" and not self.runtime_filters:
             out = self._eager_count(ctx)
             if out is not None:
@@ -2223,7 +2262,12 @@ class SortExec(ExecNode):
                 b = sort_batch(b, self.logical.keys, fetch, ctx)
                 b.dist = dist
             b = gather_all(b, ctx)
-        out = sort_batch(b, self.logical.keys, fetch, ctx)
+        out = None
+        if ctx.budget is not None:
+            from .morsel import external_sort
+            out = external_sort(b, self.logical.keys, fetch, ctx)
+        if out is None:
+            out = sort_batch(b, self.logical.keys, fetch, ctx)
         out.dist = b.dist
         return out
 

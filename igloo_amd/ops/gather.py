@@ -56,6 +56,13 @@ def _take_plain_strings(col: Column, idx: torch.Tensor, neg: bool) -> Column:
     return Column(col.dtype, chars, None, offsets=new_off)
 
 
+def _src_ptr(t) -> int:
+    """Source pointer for gather_multi: 0 for an empty (or absent) column, so
+    the kernel's unconditional loads of NULL rows read its zero page instead of
+    whatever lies at an empty tensor's address."""
+    return ptr(t) if t is not None and t.numel() else 0
+
+
 def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> List[Column]:
     """Gather rows ``idx`` of every column. ``neg=True``: idx may hold -1 (NULL row)."""
     assert idx.dim() == 1 and idx.dtype in (torch.int32, torch.int64)
@@ -76,7 +83,7 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
                         keepalive.append(src)
                     v = torch.empty(n, dtype=torch.bool, device=idx.device)
                     # validity gathered as a byte column; idx < 0 writes 0 = NULL
-                    descs.append((ptr(src), ptr(v), 1, 0, 0))
+                    descs.append((_src_ptr(src), ptr(v), 1, 0, 0))
                 else:
                     base = c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool)
                     v = _cpu_take_tensor(base, idx, neg)
@@ -94,7 +101,7 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
         data = torch.empty((n,) + tuple(c.data.shape[1:]), dtype=c.data.dtype, device=idx.device)
         esz = c.data.element_size() * (c.data.shape[1] if c.data.dim() == 2 else 1)
         valid = torch.empty(n, dtype=torch.bool, device=idx.device) if need_valid else None
-        descs.append((ptr(c.data), ptr(data), esz, ptr(c.valid), ptr(valid)))
+        descs.append((_src_ptr(c.data), ptr(data), esz, _src_ptr(c.valid), ptr(valid)))
         out.append(Column(c.dtype, data, valid, dictionary=c.dictionary))
     if gpu and descs and n:
         N = launch("gather_multi")

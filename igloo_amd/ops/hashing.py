@@ -121,15 +121,31 @@ class JoinTable:
             nbits = min(max(_next_pow2(8 * n), 1 << 15), 1 << 25)
             self.bits = torch.zeros(nbits // 32, dtype=torch.int32, device=self.device)
             self.bmask = nbits - 1
-        self.thead = torch.full((self.cap,), -1, dtype=torch.int32, device=self.device)
+        # row ids: int32 below 2^31 build rows, int64 above
+        self.rid = torch.int32 if n < INT32_MAX else torch.int64
+        self.rid64 = self.rid == torch.int64
+        self.thead = torch.full((self.cap,), -1, dtype=self.rid, device=self.device)
         self.tkeys = (torch.empty(1, dtype=torch.int64, device=self.device) if self.direct
                       else torch.full((self.cap,), EMPTY_KEY, dtype=torch.int64, device=self.device))
-        self.next = torch.empty(n, dtype=torch.int32, device=self.device)
         dups = torch.zeros(1, dtype=torch.int64, device=self.device)
-        N.join_build(ptr(keys), keys.dtype == torch.int64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead),
-                     ptr(self.next), self.cap, self.kmin, self.direct, ptr(dups), ptr(self.bits), self.bmask,
-                     stream(keys))
+        k64 = keys.dtype == torch.int64
+        st = stream(keys)
+        N.join_build(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
+                     self.kmin, self.direct, ptr(dups), ptr(self.bits), self.bmask, st)
         self.unique = to_host_int(dups) == 0
+        # duplicate keys: CSR runs (count -> exclusive scan -> scatter), so a
+        # multi-match probe reads one contiguous run of build rows
+        self.cstart = self.crows = None
+        if not self.unique:
+            cnt = torch.zeros(self.cap + 1, dtype=self.rid, device=self.device)
+            launch("join_csr_count").join_csr_count(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(cnt),
+                                                    self.rid64, self.cap, self.kmin, self.direct, st)
+            self.cstart = torch.zeros(self.cap + 1, dtype=self.rid, device=self.device)
+            torch.cumsum(cnt[:-1], 0, dtype=self.rid, out=self.cstart[1:])
+            self.crows = torch.empty(n, dtype=self.rid, device=self.device)
+            launch("join_csr_scatter").join_csr_scatter(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(cnt),
+                                                        ptr(self.cstart), ptr(self.crows), self.rid64, self.cap,
+                                                        self.kmin, self.direct, st)
 
     # ----------------------------------------------------------------- probes
     def probe_first(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
@@ -147,12 +163,12 @@ class JoinTable:
             if build_matched is not None:
                 self._cpu_mark(cnt, lo, build_matched)
             return first
-        first = torch.empty(m, dtype=torch.int32, device=pkeys.device)
+        first = torch.empty(m, dtype=self.rid, device=pkeys.device)
         N = launch("join_probe")
         bits, bmask = self._bloom(m)
         N.join_probe(ptr(pkeys), pkeys.dtype == torch.int64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead),
-                     ptr(self.next), self.cap, self.kmin, self.direct, 0, ptr(first), ptr(build_matched), bits, bmask,
-                     stream(pkeys))
+                     ptr(self.cstart), ptr(self.crows), self.rid64, self.cap, self.kmin, self.direct, 0, ptr(first),
+                     ptr(build_matched), bits, bmask, stream(pkeys))
         return first
 
     def probe_select(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None, negate: bool = False,
@@ -174,21 +190,22 @@ class JoinTable:
         words = torch.empty(tiles * 128, dtype=torch.int64, device=dev)
         tcount = torch.empty(tiles, dtype=torch.int64, device=dev)
         bits, bmask = self._bloom(m)
-        N.probe_hits(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.cap, self.kmin,
-                     self.direct, bits, bmask, negate, ptr(words), ptr(tcount), st)
+        N.probe_hits(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
+                     self.kmin, self.direct, bits, bmask, negate, ptr(words), ptr(tcount), st)
         toff, total = exclusive_scan(tcount)
         it = torch.int32 if m < INT32_MAX else torch.int64
         pidx = torch.empty(total, dtype=it, device=dev)
-        bidx = torch.empty(total, dtype=torch.int32, device=dev) if want_build and not negate else None
+        bidx = torch.empty(total, dtype=self.rid, device=dev) if want_build and not negate else None
         if total:
-            N.probe_write(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.cap, self.kmin,
-                          self.direct, ptr(words), ptr(toff), ptr(pidx), it == torch.int64, ptr(bidx), st)
+            N.probe_write(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
+                          self.kmin, self.direct, ptr(words), ptr(toff), ptr(pidx), it == torch.int64, ptr(bidx), st)
         return pidx, bidx
 
     def probe_pairs(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
                     build_matched: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """All (probe_row, build_row) matches, grouped by probe row.
-        Returns (probe_idx int32, build_idx int32, counts int32 per probe row)."""
+        Returns (probe_idx int32, build_idx (int32 below 2^31 build rows, else int64),
+        counts int32 per probe row)."""
         pkeys = _keys_ok(pkeys)
         m = pkeys.numel()
         dev = pkeys.device
@@ -206,20 +223,24 @@ class JoinTable:
             bpos = lo.index_select(0, pidx) + within
             bidx = self.order.index_select(0, bpos)
             return pidx.to(torch.int32), bidx.to(torch.int32), cnt.to(torch.int32)
+        if m >= INT32_MAX:
+            raise ValueError(f"probe_pairs: {m} probe rows exceed int32 probe ids; split the probe side")
         N = launch("join_probe")
         s = stream(pkeys)
         counts = torch.empty(m, dtype=torch.int32, device=dev)
         k64 = pkeys.dtype == torch.int64
         bits, bmask = self._bloom(m)
-        N.join_probe(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.next), self.cap,
-                     self.kmin, self.direct, ptr(counts), 0, ptr(build_matched), bits, bmask, s)
+        N.join_probe(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.cstart),
+                     ptr(self.crows), self.rid64, self.cap, self.kmin, self.direct, ptr(counts), 0,
+                     ptr(build_matched), bits, bmask, s)
         offsets, total = exclusive_scan(counts)
         pidx = torch.empty(total, dtype=torch.int32, device=dev)
-        bidx = torch.empty(total, dtype=torch.int32, device=dev)
+        bidx = torch.empty(total, dtype=self.rid, device=dev)
         if total:
             launch("join_expand")
-            N.join_expand(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.next), self.cap,
-                          self.kmin, self.direct, ptr(offsets), ptr(pidx), ptr(bidx), bits, bmask, s)
+            N.join_expand(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.cstart),
+                          ptr(self.crows), self.rid64, self.cap, self.kmin, self.direct, ptr(offsets), ptr(pidx),
+                          ptr(bidx), bits, bmask, s)
         return pidx, bidx, counts
 
     def _bloom(self, m: int) -> Tuple[int, int]:

@@ -499,7 +499,7 @@ DECOMPOSABLE = {"sum", "count", "min", "max", "avg", "bool_and", "bool_or"}
 def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     """``local(groups, partial_aggs) -> Batch | None`` may compute the phase-1
     partial states directly from the scan (fused VM kernel)."""
-    from ..exec.operators import _avg, aggregate
+    from ..exec.operators import aggregate
     groups, aggs = lg.groups, lg.aggs
     d = dist_of(b)
     if d == REPLICATED:
@@ -509,28 +509,15 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
             if isinstance(e, ColRef) and hashed_on(d, e.cid):
                 return with_dist(aggregate(groups, aggs, b, ctx), ("hash", ci.cid))
     ev = ctx.evaluator
-    decomposable = all(a.func in DECOMPOSABLE and not a.distinct for _, a in aggs)
-    if not decomposable:
+    if not decomposable(aggs):
         if groups:
             k = partition_keys(ev.column(groups[0][1], b))
             sb = shuffle(b, k, ctx)
             return with_dist(aggregate(groups, aggs, sb, ctx), ("hash", groups[0][0].cid))
         return with_dist(aggregate(groups, aggs, gather_all(b, ctx), ctx), REPLICATED)
     # ---- phase 1: partial states
-    from ..sql.binder import IdGen
     ids = _TmpIds()
-    partial, plan = [], []
-    for ci, a in aggs:
-        if a.func == "avg":
-            st = _sum_type(a.arg.dtype)
-            s_ci = L.ColInfo(ids(), "__ps", st)
-            c_ci = L.ColInfo(ids(), "__pc", T.INT64)
-            partial += [(s_ci, AggCall("sum", a.arg, False, st, a.filter)), (c_ci, AggCall("count", a.arg, False, T.INT64, a.filter))]
-            plan.append(("avg", ci, a, s_ci, c_ci))
-        else:
-            p_ci = L.ColInfo(ids(), "__p", a.dtype)
-            partial.append((p_ci, AggCall(a.func, a.arg, False, a.dtype, a.filter)))
-            plan.append((a.func, ci, a, p_ci, None))
+    partial, plan = partial_plan(aggs, ids)
     pb = local(groups, partial) if local is not None else None
     if pb is None:
         pb = aggregate(groups, partial, b, ctx)
@@ -545,6 +532,39 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
         rb = gather_all(pb, ctx)
         out_dist = REPLICATED
     # ---- phase 2: merge
+    res = merge_partials(groups, plan, rb, ids, ctx)
+    return with_dist(res, out_dist if out_dist is not None else ("hash", groups[0][0].cid))
+
+
+def decomposable(aggs) -> bool:
+    """Every aggregate merges from partial states (two-phase aggregation)."""
+    return all(a.func in DECOMPOSABLE and not a.distinct for _, a in aggs)
+
+
+def partial_plan(aggs, ids):
+    """Phase-1 aggregates whose states merge into ``aggs`` (AVG -> SUM + COUNT)
+    and the plan ``merge_partials`` follows. Shared by the SPMD exchange and the
+    morsel pipeline (exec/morsel.py), whose partial states come from ranks and
+    morsels respectively."""
+    partial, plan = [], []
+    for ci, a in aggs:
+        if a.func == "avg":
+            st = _sum_type(a.arg.dtype)
+            s_ci = L.ColInfo(ids(), "__ps", st)
+            c_ci = L.ColInfo(ids(), "__pc", T.INT64)
+            partial += [(s_ci, AggCall("sum", a.arg, False, st, a.filter)), (c_ci, AggCall("count", a.arg, False, T.INT64, a.filter))]
+            plan.append(("avg", ci, a, s_ci, c_ci))
+        else:
+            p_ci = L.ColInfo(ids(), "__p", a.dtype)
+            partial.append((p_ci, AggCall(a.func, a.arg, False, a.dtype, a.filter)))
+            plan.append((a.func, ci, a, p_ci, None))
+    return partial, plan
+
+
+def merge_partials(groups, plan, rb: Batch, ids, ctx) -> Batch:
+    """Phase 2: merge the partial states in ``rb`` (rows = partial groups) into
+    the final aggregates of ``plan`` (see ``partial_plan``)."""
+    from ..exec.operators import _avg, aggregate
     fgroups = [(ci, ColRef(ci.cid, ci.name, ci.dtype, ci.nullable)) for ci, _ in groups]
     # 128-bit partial sums (wide decimals: SF100 charges) merge as three
     # int64 sums — high word, and the low word's two 32-bit halves — that
@@ -579,8 +599,7 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
             out[ci.cid] = Column(T.INT64, data)
         else:
             out[ci.cid] = fb.columns[ci.cid]
-    res = Batch(out, fb.num_rows)
-    return with_dist(res, out_dist if out_dist is not None else ("hash", groups[0][0].cid))
+    return Batch(out, fb.num_rows)
 
 
 #: largest dense group-key domain whose partial states are all-reduced

@@ -1,12 +1,20 @@
 """Run the 22 TPC-H queries on the GPU with the device memory capped (the
 caching allocator's per-process fraction) and the engine's device budget set,
-and check every result digest against the CPU engine on the same data.
+over host-resident tables (every scan moves a transient copy; streamed scans
+move one morsel at a time), and check every result digest against a reference
+engine on the same data.
 
 usage: python scripts/budget_check.py [--sf 1] [--cap-gb 1] [--budget-gb 0.25]
+                                      [--ref cpu|gpu] [--json out.json]
+``--ref gpu``: the reference runs first on the GPU with device-resident
+tables and no cap (SF10 on the CPU engine takes too long), then everything it
+held is released before the cap is set.
 Exit status 0 when all match and peak reserved memory stayed under the cap."""
 import argparse
+import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -17,17 +25,41 @@ def main():
     ap.add_argument("--sf", type=float, default=1.0)
     ap.add_argument("--cap-gb", type=float, default=1.0)
     ap.add_argument("--budget-gb", type=float, default=0.25)
+    ap.add_argument("--ref", choices=["cpu", "gpu"], default="cpu")
+    ap.add_argument("--queries", default="1-22")
+    ap.add_argument("--json", default=None)
     a = ap.parse_args()
     import torch
     import igloo_amd as ig
     from igloo_amd.utils.digest import digest
     from igloo_amd.catalog import MemoryTable
     from igloo_amd.models.tpch import datagen, queries
-    cpu = ig.QueryEngine(device="cpu")
+    if "-" in a.queries:
+        lo, hi = a.queries.split("-")
+        qs = list(range(int(lo), int(hi) + 1))
+    else:
+        qs = [int(x) for x in a.queries.split(",")]
+    t0 = time.time()
     tabs = datagen.generate(a.sf, "cpu")
-    for name, t in tabs.items():
-        cpu.register_table(name, t)
-    want = {q: digest(cpu.sql(queries.QUERIES[q]).table) for q in range(1, 23)}
+    print(f"generated SF{a.sf} on the host in {time.time() - t0:.1f}s", flush=True)
+    if a.ref == "cpu":
+        ref = ig.QueryEngine(device="cpu")
+        for name, t in tabs.items():
+            ref.register_table(name, t)
+    else:
+        ref = ig.QueryEngine(device="cuda:0")
+        for name, t in tabs.items():
+            ref.register_table(name, MemoryTable({k: c.to("cuda:0") for k, c in t.columns.items()}, t.num_rows(),
+                                                 replicated=t.replicated))
+    want = {}
+    for q in qs:
+        want[q] = digest(ref.sql(queries.QUERIES[q]).table)
+    print(f"reference ({a.ref}) digests in {time.time() - t0:.1f}s", flush=True)
+    del ref
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     cap = int(a.cap_gb * 2**30)
     total = torch.cuda.get_device_properties(0).total_memory
     torch.cuda.set_per_process_memory_fraction(cap / total, 0)
@@ -37,20 +69,37 @@ def main():
     for name, t in tabs.items():
         # host-resident tables: every scan moves a transient copy to the device
         g.register_table(name, MemoryTable(t.columns, t.num_rows(), replicated=t.replicated, resident=False))
-    bad, spilled = [], 0
-    for q in range(1, 23):
-        got = digest(g.sql(queries.QUERIES[q]).table)
-        sp = g.last_metrics["spill"]
-        spilled += sp["joins"]
+    bad, failed, spilled, streamed, rows = [], [], 0, 0, []
+    for q in qs:
+        torch.cuda.reset_peak_memory_stats(0)
+        t1 = time.time()
+        try:
+            got = digest(g.sql(queries.QUERIES[q]).table)
+        except Exception as e:  # noqa: BLE001 - report and continue (an OOM under the cap)
+            print(f"Q{q}: FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)
+            failed.append(q)
+            torch.cuda.empty_cache()
+            continue
+        sp, mo = g.last_metrics["spill"], g.last_metrics["morsels"]
+        spilled += sp["joins"] + sp.get("sorts", 0)
+        streamed += mo["morsels"]
         peak = torch.cuda.max_memory_reserved(0)
-        print(f"Q{q}: {'ok' if got == want[q] else 'MISMATCH'} spill={sp} peak_reserved={peak / 2**20:.0f} MiB",
-              flush=True)
-        if got != want[q]:
+        ok = got == want[q]
+        rows.append({"q": q, "ok": ok, "s": round(time.time() - t1, 3), "peak_reserved_mib": peak // 2**20,
+                     "morsels": mo, "spill": sp})
+        print(f"Q{q}: {'ok' if ok else 'MISMATCH'} {time.time() - t1:.2f}s morsels={mo['morsels']} "
+              f"spill={sp} peak_reserved={peak / 2**20:.0f} MiB", flush=True)
+        if not ok:
             bad.append(q)
-    peak = torch.cuda.max_memory_reserved(0)
-    print(f"peak reserved {peak / 2**20:.0f} MiB (cap {cap / 2**20:.0f} MiB), partitioned joins {spilled}, "
-          f"mismatches {bad}", flush=True)
-    sys.exit(0 if not bad and peak <= cap and spilled > 0 else 1)
+    peak = max([r["peak_reserved_mib"] for r in rows] or [0])
+    print(f"SF{a.sf}: max peak reserved {peak} MiB (cap {cap / 2**20:.0f} MiB, engine budget {a.budget_gb} GB), "
+          f"morsels {streamed}, partitioned joins / external sorts {spilled}, mismatches {bad}, failed {failed}",
+          flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"sf": a.sf, "cap_gb": a.cap_gb, "budget_gb": a.budget_gb, "ref": a.ref, "queries": rows,
+                       "mismatches": bad, "failed": failed}, f, indent=1)
+    sys.exit(0 if not bad and not failed and peak * 2**20 <= cap and (spilled > 0 or streamed > 0) else 1)
 
 
 if __name__ == "__main__":

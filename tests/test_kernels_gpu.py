@@ -77,6 +77,16 @@ def test_join_table(gpu_device, dense, dups):
     assert torch.equal(fm >= 0, rc > 0)
     ok = fm >= 0
     assert torch.equal(bk[fm[ok].long()], pk[ok])
+    # duplicate keys take the CSR layout (contiguous runs of build rows)
+    assert (gpu.cstart is not None) == (not gpu.unique)
+    if gpu.cstart is not None:
+        assert int(gpu.cstart[-1]) == int(bvalid.sum())
+    # build-side match marks (right/full outer joins) through both layouts
+    mc = torch.zeros(nb, dtype=torch.bool)
+    mg = torch.zeros(nb, dtype=torch.bool, device=DEV)
+    cpu.probe_pairs(pk, build_matched=mc)
+    gpu.probe_pairs(pk.to(DEV), build_matched=mg)
+    assert torch.equal(mc, mg.cpu())
 
 
 @pytest.mark.parametrize("card", [1, 6, 1000, 3_000_000])
@@ -484,3 +494,40 @@ def test_sorted_ranges_with_search_fence():
     assert (got_cnt == want_cnt).all()
     hit = want_cnt > 0
     assert (got_lo[hit] == want_lo[hit]).all()
+
+
+def test_sorted_ranges_sorted_probe_keys(gpu_device, monkeypatch):
+    """ranges.hip sorted_ranges, wave-cooperative path: non-decreasing probe keys
+    (LDS-staged windows when 64 keys span <= 1024 build rows, windowed global
+    searches when they do not), mixed with unsorted and NULL-holding waves,
+    with and without the search fence, vs numpy searchsorted."""
+    from igloo_amd.ops import hashing as H
+    monkeypatch.setattr(H, "DENSE_INDEX", False)
+    r = np.random.default_rng(9)
+    for dt in (np.int32, np.int64):
+        for n, fenced in ((300_000, False), (3_000_000, True)):
+            k = np.sort(r.integers(0, n // 3, n)).astype(dt)
+            k[n // 2: n // 2 + 5000] = k[n // 2]          # one run longer than a window
+            big = torch.from_numpy(k).to(gpu_device)
+            if fenced:
+                big._igloo_resident = True
+            dense = np.sort(r.integers(-5, n // 3 + 5, 100_000))              # windows fit
+            sparse = np.sort(r.choice(n // 3 + 10, 20_000, replace=False))    # windows too wide
+            shuffled = r.integers(-5, n // 3 + 5, 10_000)
+            q = np.concatenate([dense, sparse, shuffled, [k[n // 2]] * 70]).astype(dt)
+            for with_valid in (False, True):
+                qv = None
+                if with_valid:
+                    v = np.ones(q.size, bool)
+                    v[100_000 + 20_000 + 10_000 - 640: 100_000 + 20_000 + 10_000 - 600] = False
+                    v[5000:5003] = False
+                    qv = torch.from_numpy(v).to(gpu_device)
+                lo, cnt = H.sorted_ranges(big, torch.from_numpy(q).to(gpu_device), qv)
+                want_lo = np.searchsorted(k, q, side="left")
+                want_cnt = np.searchsorted(k, q, side="right") - want_lo
+                if with_valid:
+                    want_cnt = np.where(v, want_cnt, 0)
+                got_cnt, got_lo = cnt.cpu().numpy(), lo.cpu().numpy()
+                assert (got_cnt == want_cnt).all(), (dt, n, with_valid)
+                hit = want_cnt > 0
+                assert (got_lo[hit] == want_lo[hit]).all(), (dt, n, with_valid)
