@@ -184,6 +184,107 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
         return merge_partials(lg.groups, plan, rb, ids, ctx)
 
 
+def big_streamable(node, ctx) -> bool:
+    """``node``'s output derives from a scan too big for the budget that
+    could stream (an aggregate over ``node`` would run as a morsel pipeline)."""
+    from .operators import ScanExec
+    lim = ctx.budget // STREAM_FRACTION
+    return any(isinstance(n, ScanExec) and getattr(n.logical.source, "can_stream", False) and scan_bytes(n) > lim
+               and stream_path_ok(node, n) for n in _walk(node))
+
+
+def semi_aggregate(kind, on, residual, null_aware, left_cids, right_plan, right_node, ctx, key):
+    """Build side of a SEMI / ANTI join that is too big for the budget,
+    replaced by an aggregate of it that streams in morsels:
+
+    * no residual: the build side's distinct keys (GROUP BY the keys);
+    * residual ``l.x <> r.y`` (TPC-H Q21's "another supplier of the same
+      order"): GROUP BY the keys with MIN(y), MAX(y) — some non-NULL y differs
+      from x exactly when MIN(y) <> x or MAX(y) <> x.
+
+    The aggregate holds one row per distinct key instead of the whole build
+    side, and is computed once per query (``key``: the join's identity; a
+    join inside a morsel pipeline runs once per morsel). Returns (aggregate
+    batch, spec for ``apply_semi_aggregate``) or None when the join does not
+    have this shape (NOT IN's NULL rules included) or its build side fits."""
+    from ..parallel.exchange import _TmpIds
+    from ..sql import logical as L
+    from ..sql.expr import AggCall, BinOp, ColRef
+    from .operators import HashAggExec
+    if ctx.budget is None or ctx.spmd or kind not in ("semi", "anti") or not on or null_aware:
+        return None
+    hit = ctx.semi_builds.get(key)
+    if hit is not None:
+        return hit
+    rcids = {c.cid for c in right_plan.schema}
+    ineq = None
+    if residual is not None:
+        r = residual
+        if not (isinstance(r, BinOp) and r.op == "<>" and isinstance(r.left, ColRef) and isinstance(r.right, ColRef)):
+            return None
+        x, y = (r.left, r.right) if r.left.cid in left_cids else (r.right, r.left)
+        if x.cid not in left_cids or y.cid not in rcids or x.dtype.is_string or y.dtype.is_string:
+            return None
+        ineq = (x, y)
+    if not big_streamable(right_node, ctx):
+        return None
+    ids = _TmpIds()
+    groups = [(L.ColInfo(ids(), f"__k{i}", rk.dtype, rk.nullable), rk) for i, (_, rk) in enumerate(on)]
+    aggs = []
+    if ineq is not None:
+        y = ineq[1]
+        aggs = [(L.ColInfo(ids(), "__mn", y.dtype), AggCall("min", y, False, y.dtype)),
+                (L.ColInfo(ids(), "__mx", y.dtype), AggCall("max", y, False, y.dtype))]
+    ab = HashAggExec(L.Aggregate(right_plan, groups, aggs), right_node).execute(ctx)
+    spec = {"kind": kind, "lkeys": [le for le, _ in on], "kcids": [ci.cid for ci, _ in groups],
+            "x": ineq[0] if ineq else None, "mn": aggs[0][0].cid if aggs else None,
+            "mx": aggs[1][0].cid if aggs else None}
+    ctx.semi_builds[key] = (ab, spec)
+    ctx.morsels["semi_aggregates"] = ctx.morsels.get("semi_aggregates", 0) + 1
+    return ab, spec
+
+
+def apply_semi_aggregate(lb: Batch, ab: Batch, spec, ctx) -> Batch:
+    """The rows of ``lb`` the SEMI (ANTI: not) join keeps, from the aggregated
+    build side of ``semi_aggregate``."""
+    from ..ops import hashing as H
+    from ..ops.select import mask_to_indices
+    from .operators import _take_batch, key_tensors
+    ev = ctx.evaluator
+    with ctx.span("join.aggregated_semi"):
+        if ab.num_rows == 0 or lb.num_rows == 0:
+            hit = torch.zeros(lb.num_rows, dtype=torch.bool, device=ctx.device)
+        else:
+            lk, rk, lvalid, rvalid = key_tensors([ev.column(le, lb) for le in spec["lkeys"]],
+                                                 [ab.columns[c] for c in spec["kcids"]])
+            first = H.JoinTable(rk, rvalid).probe_first(lk, lvalid)
+            hit = first >= 0
+            if spec["x"] is not None:
+                x = ev.column(spec["x"], lb)
+                safe = torch.where(hit, first, torch.zeros_like(first)).long()
+                mn, mx = ab.columns[spec["mn"]], ab.columns[spec["mx"]]
+                mnv, mxv = mn.data.index_select(0, safe), mx.data.index_select(0, safe)
+                xv = x.data.to(mnv.dtype)
+                cond = (mnv != xv) | (mxv != xv)
+                if mn.valid is not None:
+                    cond &= mn.valid.index_select(0, safe)
+                if x.valid is not None:
+                    cond &= x.valid
+                hit &= cond
+        keep = mask_to_indices(hit if spec["kind"] == "semi" else ~hit)
+    return _take_batch(lb, keep)
+
+
+def aggregated_semi_join(join, ctx) -> Optional[Batch]:
+    """HashJoinExec SEMI / ANTI through ``semi_aggregate`` (None: not applicable)."""
+    j = join.logical
+    r = semi_aggregate(j.kind, j.on, j.residual, j.null_aware, {c.cid for c in j.left.schema}, j.right,
+                       join.children[1], ctx, ("join", id(join)))
+    if r is None:
+        return None
+    return apply_semi_aggregate(join.children[0].execute(ctx), r[0], r[1], ctx)
+
+
 def _has_subquery(e) -> bool:
     from ..sql.expr import has_subquery
     return has_subquery(e)

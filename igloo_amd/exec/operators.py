@@ -83,6 +83,7 @@ class ExecContext:
         self.memo_ids: set = set()
         self.morsel_depth = 0
         self.morsels = {"pipelines": 0, "morsels": 0, "rows": 0, "bytes": 0}
+        self.semi_builds: dict = {}   # aggregated SEMI / ANTI build sides (exec/morsel.py)
 
     def note_scan(self, source, rows: int) -> None:
         if id(source) not in self._scanned_sources:
@@ -574,6 +575,11 @@ class HashJoinExec(ExecNode):
 
     def _run(self, ctx):
         j = self.logical
+        if ctx.budget is not None and j.kind in ("semi", "anti"):
+            from .morsel import aggregated_semi_join
+            out = aggregated_semi_join(self, ctx)
+            if out is not None:
+                return out
         lb = self.children[0].execute(ctx)
         if j.kind in ("inner", "left", "semi") and j.on and ctx.memo is None:
             # (not inside a morsel pipeline: the build side is computed once
@@ -1373,6 +1379,10 @@ class MultiJoinExec(ExecNode):
             lb = lb.materialize()
         elif isinstance(lb, _LazyScanBatch):
             lb = Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
+        agg = ctx.semi_builds.get(("multi", id(sp)))
+        if agg is not None and agg[0] is rb:
+            from .morsel import apply_semi_aggregate
+            return apply_semi_aggregate(lb, rb, agg[1], ctx)
         if ctx.spmd:
             from ..parallel.exchange import prepare_join, semi_by_key_set
             j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
@@ -1395,7 +1405,16 @@ class MultiJoinExec(ExecNode):
                          "scan": _scan_info(ch)})
         self.order_log = []
         deferred = []
-        semis = [(sp, rex.execute(ctx)) for sp, rex in zip(lg.semis, self.children[nch:])]
+        semis = []
+        for sp, rex in zip(lg.semis, self.children[nch:]):
+            agg = None
+            if ctx.budget is not None:
+                # a build side over the budget: its aggregate instead (exec/morsel.py)
+                from .morsel import semi_aggregate
+                lc = set().union(*[{c.cid for c in ch.schema} for ch in lg.children])
+                agg = semi_aggregate(sp.kind, sp.on, sp.residual, sp.null_aware, lc, sp.right, rex, ctx,
+                                     ("multi", id(sp)))
+            semis.append((sp, agg[0] if agg is not None else rex.execute(ctx)))
         conds = list(lg.conds)
         # global row counts of every input (SPMD: every rank must derive the
         # same join order) — together with the merged NDV sketches of every
@@ -1829,6 +1848,12 @@ class HashAggExec(ExecNode):
                     and a.arg.cid in right_cids):
                 return None
         ev = ctx.evaluator
+        if ctx.budget is not None and not ctx.spmd:
+            from .morsel import big_streamable
+            if big_streamable(child.children[1], ctx):
+                return self._eager_count_streamed(lkey, rkey, ctx)
+        if ctx.device.type != "cuda":
+            return None
         lb = child.children[0].execute(ctx)
         rb = child.children[1].execute(ctx)
         with ctx.span("agg.eager_count"):
@@ -1891,6 +1916,39 @@ class HashAggExec(ExecNode):
             return distributed_aggregate(L.Aggregate(None, lg.groups, aggs), Batch(cols, lb.num_rows, lb.dist), ctx)
         return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
 
+    def _eager_count_streamed(self, lkey, rkey, ctx) -> Batch:
+        """``_eager_count`` with a right side over the device budget: the
+        per-key counts come from an aggregate of the right side (GROUP BY the
+        join key, one COUNT per aggregate), which streams in morsels
+        (exec/morsel.py), instead of the materialised right side."""
+        from ..parallel.exchange import _TmpIds
+        lg, child = self.logical, self.children[0]
+        j = child.logical
+        ids = _TmpIds()
+        kci = L.ColInfo(ids(), "__k", rkey.dtype, rkey.nullable)
+        cnt = [(L.ColInfo(ids(), "__c", T.INT64, False), AggCall("count", a.arg, False, T.INT64)) for _, a in lg.aggs]
+        ab = HashAggExec(L.Aggregate(j.right, [(kci, rkey)], cnt), child.children[1]).execute(ctx)
+        lb = child.children[0].execute(ctx)
+        ev = ctx.evaluator
+        with ctx.span("agg.eager_count"):
+            lk, rk, lvalid, rvalid = key_tensors([ev.column(lkey, lb)], [ab.columns[kci.cid]])
+            cols = dict(lb.columns)
+            aggs = []
+            if ab.num_rows and lb.num_rows:
+                first = H.JoinTable(rk, rvalid).probe_first(lk, lvalid)
+                hit = first >= 0
+                safe = torch.where(hit, first, torch.zeros_like(first)).long()
+            for k, (ci, _) in enumerate(lg.aggs):
+                if ab.num_rows and lb.num_rows:
+                    c = ab.columns[cnt[k][0].cid].data
+                    v = torch.where(hit, c.index_select(0, safe), torch.zeros_like(safe))
+                else:
+                    v = torch.zeros(lb.num_rows, dtype=torch.int64, device=ctx.device)
+                tmp = -(10**9) - k
+                cols[tmp] = Column(T.INT64, v.contiguous())
+                aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
+        return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
+
     def _spmd_join_aggregate(self, lb: Batch, rb: Batch, ctx) -> Batch:
         """SPMD fallback after the inputs were computed: the plain exchange +
         join + distributed aggregation."""
@@ -1909,7 +1967,7 @@ class HashAggExec(ExecNode):
             out = streamed_aggregate(self, ctx)
             if out is not None:
                 return out
-        if ctx.device.type == "cuda" and not self.runtime_filters:
+        if (ctx.device.type == "cuda" or ctx.budget is not None) and not self.runtime_filters:
             out = self._eager_count(ctx)
             if out is not None:
                 return out
