@@ -27,22 +27,32 @@ struct GatherParams {
 __device__ __attribute__((aligned(16))) uint8_t g_gather_zero[64];
 
 constexpr int kGatherRows = 4;   // rows per lane
-constexpr int kGatherGroup = 4;  // columns whose loads are issued together
 
-// One launch gathers columns of ONE element type T (the launcher splits a
-// request by element size). Rows base + r * blockDim (r < kGatherRows) per
-// lane; columns in groups of kGatherGroup.
-//
-// Every load is unconditional: the index load clamps the row to n - 1 and a
-// source load clamps a negative index (NULL row) to 0, and the value is
-// selected afterwards. A load under a per-lane condition becomes a branch
-// whose merge waits for the load (s_waitcnt vmcnt(0) after every load: one
-// miss in flight per lane, ~38% of HBM bandwidth measured,
-// profiles/r3_sf100_pmc_roofline.txt); unconditional, a lane issues the
-// kGatherGroup x kGatherRows random reads of a group back to back and waits
-// once before the stores.
-template <typename I, typename T>
-__global__ __launch_bounds__(kBlock) void gather_multi_kernel(const I* __restrict__ idx, int64_t n, GatherParams p) {
+template <typename T, int kRows>
+__device__ inline void gather_col(const void* src_, void* dst_, const int64_t (&s)[kRows], const int64_t (&i)[kRows],
+                                  int64_t n) {
+  const T* __restrict__ src = static_cast<const T*>(src_);
+  T* __restrict__ dst = static_cast<T*>(dst_);
+  T v[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) v[r] = s[r] >= 0 ? src[s[r]] : T{};
+#pragma unroll
+  for (int r = 0; r < kRows; ++r)
+    if (i[r] < n) dst[i[r]] = v[r];
+}
+
+// Grouped variant (IGLOO_GATHER=grouped; within 1% of the per-column kernel over
+// the SF100 suite, profiles/r3_ab_gather_grouped.txt, where 3 of 4 gathers
+// move one column): one launch per element type T and
+// column count NC (<= 4, the launcher splits a request), rows base + r *
+// blockDim (r < kGatherRows) per lane. Every load is unconditional — the
+// index load clamps the row to n - 1, a source load clamps a NULL row's
+// negative index to 0, values are selected afterwards — so a lane issues its
+// NC x kGatherRows random reads back to back and waits once before the
+// stores (a load under a per-lane condition compiles to a branch whose merge
+// waits for it).
+template <typename I, typename T, int NC>
+__global__ __launch_bounds__(kBlock) void gather_grouped_kernel(const I* __restrict__ idx, int64_t n, GatherParams p) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherRows;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x * kGatherRows + threadIdx.x; base < n; base += step) {
     int64_t i[kGatherRows], s[kGatherRows], sc[kGatherRows];
@@ -52,26 +62,23 @@ __global__ __launch_bounds__(kBlock) void gather_multi_kernel(const I* __restric
       s[r] = (int64_t)idx[i[r] < n ? i[r] : n - 1];
       sc[r] = s[r] < 0 ? 0 : s[r];
     }
-    for (int c0 = 0; c0 < p.ncols; c0 += kGatherGroup) {
-      T v[kGatherGroup][kGatherRows];
+    T v[NC][kGatherRows];
 #pragma unroll
-      for (int cc = 0; cc < kGatherGroup; ++cc) {
-        const int c = c0 + cc < p.ncols ? c0 + cc : p.ncols - 1;  // past the end: reload the last column
-        const T* __restrict__ src = p.d[c].src ? static_cast<const T*>(p.d[c].src)
-                                               : reinterpret_cast<const T*>(g_gather_zero);
+    for (int c = 0; c < NC; ++c) {
+      const T* __restrict__ src = p.d[c].src ? static_cast<const T*>(p.d[c].src)
+                                             : reinterpret_cast<const T*>(g_gather_zero);
 #pragma unroll
-        for (int r = 0; r < kGatherRows; ++r) v[cc][r] = src[sc[r]];
-      }
-#pragma unroll
-      for (int cc = 0; cc < kGatherGroup; ++cc) {
-        if (c0 + cc >= p.ncols) break;
-        T* __restrict__ dst = static_cast<T*>(p.d[c0 + cc].dst);
-#pragma unroll
-        for (int r = 0; r < kGatherRows; ++r)
-          if (i[r] < n) dst[i[r]] = s[r] < 0 ? T{} : v[cc][r];
-      }
+      for (int r = 0; r < kGatherRows; ++r) v[c][r] = src[sc[r]];
     }
-    for (int c = 0; c < p.ncols; ++c) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      T* __restrict__ dst = static_cast<T*>(p.d[c].dst);
+#pragma unroll
+      for (int r = 0; r < kGatherRows; ++r)
+        if (i[r] < n) dst[i[r]] = s[r] < 0 ? T{} : v[c][r];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
       uint8_t* __restrict__ dv = p.d[c].dst_valid;
       if (!dv) continue;
       const uint8_t* __restrict__ sv = p.d[c].src_valid;
@@ -88,6 +95,43 @@ __global__ __launch_bounds__(kBlock) void gather_multi_kernel(const I* __restric
 #pragma unroll
       for (int r = 0; r < kGatherRows; ++r)
         if (i[r] < n) dv[i[r]] = vv[r];
+    }
+  }
+}
+
+// Per-column variant (IGLOO_GATHER=percol): rows base + r * blockDim (r <
+// kGatherRows) per lane, every column in one launch: every store of a column
+// follows all of that column's loads, so a lane keeps kGatherRows random
+// reads in flight instead of one load->store round trip per value.
+template <typename I, int kGatherRows>
+__global__ __launch_bounds__(kBlock) void gather_percol_kernel(const I* __restrict__ idx, int64_t n, GatherParams p) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherRows;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x * kGatherRows + threadIdx.x; base < n; base += step) {
+    int64_t i[kGatherRows], s[kGatherRows];
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r) {
+      i[r] = base + (int64_t)r * blockDim.x;
+      s[r] = i[r] < n ? (int64_t)idx[i[r]] : -1;
+    }
+    for (int c = 0; c < p.ncols; ++c) {
+      const GatherDesc& d = p.d[c];
+      switch (d.elem_bytes) {
+        case 1: gather_col<uint8_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 2: gather_col<uint16_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 4: gather_col<uint32_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 8: gather_col<uint64_t, kGatherRows>(d.src, d.dst, s, i, n); break;
+        case 16: gather_col<uint4, kGatherRows>(d.src, d.dst, s, i, n); break;
+      }
+      if (d.dst_valid) {
+        const uint8_t* __restrict__ sv = d.src_valid;
+        uint8_t* __restrict__ dv = d.dst_valid;
+        uint8_t v[kGatherRows];
+#pragma unroll
+        for (int r = 0; r < kGatherRows; ++r) v[r] = s[r] >= 0 && (!sv || sv[s[r]]);
+#pragma unroll
+        for (int r = 0; r < kGatherRows; ++r)
+          if (i[r] < n) dv[i[r]] = v[r];
+      }
     }
   }
 }
@@ -119,18 +163,35 @@ __global__ __launch_bounds__(kBlock) void str_copy_kernel(const int64_t* __restr
 }  // namespace
 
 namespace {
-template <typename T>
-void launch_gather(const void* idx, bool idx64, int64_t n, const GatherParams& p, hipStream_t stream) {
+template <typename T, int NC>
+void launch_grouped(const void* idx, bool idx64, int64_t n, const GatherParams& p, hipStream_t stream) {
   const dim3 g(grid_for(n, kBlock * kGatherRows, 65536)), b(kBlock);
   if (idx64)
-    hipLaunchKernelGGL((gather_multi_kernel<int64_t, T>), g, b, 0, stream, (const int64_t*)idx, n, p);
+    hipLaunchKernelGGL((gather_grouped_kernel<int64_t, T, NC>), g, b, 0, stream, (const int64_t*)idx, n, p);
   else
-    hipLaunchKernelGGL((gather_multi_kernel<int32_t, T>), g, b, 0, stream, (const int32_t*)idx, n, p);
+    hipLaunchKernelGGL((gather_grouped_kernel<int32_t, T, NC>), g, b, 0, stream, (const int32_t*)idx, n, p);
   check_launch("gather_multi", stream);
+}
+
+template <typename T>
+void launch_grouped_n(const void* idx, bool idx64, int64_t n, const GatherParams& p, hipStream_t stream) {
+  switch (p.ncols) {
+    case 1: launch_grouped<T, 1>(idx, idx64, n, p, stream); break;
+    case 2: launch_grouped<T, 2>(idx, idx64, n, p, stream); break;
+    case 3: launch_grouped<T, 3>(idx, idx64, n, p, stream); break;
+    default: launch_grouped<T, 4>(idx, idx64, n, p, stream); break;
+  }
+}
+
+bool grouped_gather() {
+  static const bool g = [] {
+    const char* e = getenv("IGLOO_GATHER");
+    return e && std::string(e) == "grouped";
+  }();
+  return g;
 }
 }  // namespace
 
-// One launch per element size present (up to kMaxGatherCols columns each).
 void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* descs, int ncols, hipStream_t stream) {
   if (n == 0 || ncols == 0) return;
   for (int c = 0; c < ncols; ++c) {
@@ -138,19 +199,35 @@ void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* desc
     if (eb != 1 && eb != 2 && eb != 4 && eb != 8 && eb != 16)
       throw std::runtime_error("gather_multi: unsupported element size " + std::to_string(eb));
   }
+  if (!grouped_gather()) {
+    // per-column kernel: every column of the request in one launch
+    for (int base = 0; base < ncols; base += kMaxGatherCols) {
+      GatherParams p;
+      p.ncols = ncols - base < kMaxGatherCols ? ncols - base : kMaxGatherCols;
+      for (int c = 0; c < p.ncols; ++c) p.d[c] = descs[base + c];
+      const dim3 g(grid_for(n, kBlock * kGatherRows, 65536)), b(kBlock);
+      if (idx64)
+        hipLaunchKernelGGL((gather_percol_kernel<int64_t, kGatherRows>), g, b, 0, stream, (const int64_t*)idx, n, p);
+      else
+        hipLaunchKernelGGL((gather_percol_kernel<int32_t, kGatherRows>), g, b, 0, stream, (const int32_t*)idx, n, p);
+      check_launch("gather_multi", stream);
+    }
+    return;
+  }
+  // grouped kernel: one launch per element size and group of <= 4 columns
   static const int sizes[5] = {1, 2, 4, 8, 16};
   for (int eb : sizes) {
     GatherParams p;
     p.ncols = 0;
     for (int c = 0; c <= ncols; ++c) {
-      const bool flush = c == ncols ? p.ncols > 0 : p.ncols == kMaxGatherCols;
+      const bool flush = c == ncols ? p.ncols > 0 : p.ncols == 4;
       if (flush) {
         switch (eb) {
-          case 1: launch_gather<uint8_t>(idx, idx64, n, p, stream); break;
-          case 2: launch_gather<uint16_t>(idx, idx64, n, p, stream); break;
-          case 4: launch_gather<uint32_t>(idx, idx64, n, p, stream); break;
-          case 8: launch_gather<uint64_t>(idx, idx64, n, p, stream); break;
-          default: launch_gather<uint4>(idx, idx64, n, p, stream); break;
+          case 1: launch_grouped_n<uint8_t>(idx, idx64, n, p, stream); break;
+          case 2: launch_grouped_n<uint16_t>(idx, idx64, n, p, stream); break;
+          case 4: launch_grouped_n<uint32_t>(idx, idx64, n, p, stream); break;
+          case 8: launch_grouped_n<uint64_t>(idx, idx64, n, p, stream); break;
+          default: launch_grouped_n<uint4>(idx, idx64, n, p, stream); break;
         }
         p.ncols = 0;
       }

@@ -2,11 +2,10 @@
 // orders by o_orderkey, and every join output that preserved that order).
 //
 //   sorted_ranges: for each probe key, the range [lo, lo+cnt) of equal keys in
-//     a non-decreasing build column. Sorted probe keys: a wave searches the
-//     window of its 64 keys once and the lanes search it in LDS; otherwise a
-//     lower-bound binary search per key, then a short forward scan (TPC-H keys
-//     repeat <= 7 times) that falls back to a second binary search for long
-//     runs. Replaces two torch.searchsorted passes.
+//     a non-decreasing build column — one lower-bound binary search, then a
+//     short forward scan (TPC-H keys repeat <= 7 times) that falls back to a
+//     second binary search for long runs. Replaces two torch.searchsorted
+//     passes.
 //   expand_ranges: the (probe row, build row) pairs of those ranges, output
 //     parallel and load balanced: a workgroup owns 2048 consecutive outputs,
 //     finds the probe rows overlapping them with two binary searches over the
@@ -26,50 +25,6 @@ constexpr int kExpItems = 8;
 constexpr int kExpTile = kBlock * kExpItems;
 constexpr int kScanRun = 16;
 
-// first index in [a, b) whose key is >= key (UPPER: > key), optionally
-// bracketed by the fence sample first
-template <typename K, bool UPPER>
-__device__ inline int64_t bound_search(const K* __restrict__ big, int64_t nb, K key, const K* __restrict__ fence,
-                                       int64_t nf) {
-  int64_t a = 0, b = nb;
-  if (fence) {
-    int64_t fa = 0, fb = nf;
-    while (fa < fb) {
-      const int64_t m = (fa + fb) >> 1;
-      if (UPPER ? fence[m] <= key : fence[m] < key) fa = m + 1;
-      else fb = m;
-    }
-    a = fa > 0 ? (fa - 1) * kFence : 0;
-    b = fa * kFence < nb ? fa * kFence : nb;
-  }
-  while (a < b) {
-    const int64_t m = (a + b) >> 1;
-    if (UPPER ? big[m] <= key : big[m] < key) a = m + 1;
-    else b = m;
-  }
-  return a;
-}
-
-template <typename K, bool UPPER>
-__device__ inline int lds_bound(const K* w, int n, K key) {
-  int a = 0, b = n;
-  while (a < b) {
-    const int m = (a + b) >> 1;
-    if (UPPER ? w[m] <= key : w[m] < key) a = m + 1;
-    else b = m;
-  }
-  return a;
-}
-
-// Probe keys are usually sorted too (a stable selection of a clustered
-// column). A wave then finds the build-side window of its 64 keys with two
-// searches (lower bound of its first key, upper bound of its last) run by two
-// lanes, stages the window in LDS when it fits and lets every lane search
-// there: two HBM search chains per 64 keys instead of 64. Waves whose keys are
-// not non-decreasing, or that hold a NULL, search per lane in global memory,
-// inside the window when there is one (its lines are then shared, L2-hot).
-constexpr int kRangeWin = 1024;  // staged build keys per wave
-
 template <typename K>
 __global__ __launch_bounds__(kBlock) void sorted_ranges_kernel(const K* __restrict__ big, int64_t nb,
                                                               const K* __restrict__ q,
@@ -77,57 +32,49 @@ __global__ __launch_bounds__(kBlock) void sorted_ranges_kernel(const K* __restri
                                                               int64_t* __restrict__ lo_out,
                                                               int64_t* __restrict__ cnt_out,
                                                               const K* __restrict__ fence, int64_t nf) {
-  __shared__ K win[kWavesPerBlock][kRangeWin];
-  const int lane = lane_id(), wave = threadIdx.x / kWave;
-  // block-uniform trip count: the barriers below are reached by every wave
-  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < nq; base += (int64_t)gridDim.x * kBlock) {
-    const int64_t c = base + wave * kWave;
-    const int64_t i = c + lane;
-    const bool inb = i < nq;
-    const K key = q[inb ? i : nq - 1];
-    const bool valid = inb && (!qvalid || qvalid[inb ? i : nq - 1]);
-    const K prev = __shfl_up(key, 1, kWave);
-    const bool bad = inb && (!valid || (lane > 0 && key < prev));
-    const bool mono = c < nq && __ballot(bad) == 0;
-    int64_t A = 0, B = nb;
-    if (mono) {
-      const int last = c + kWave <= nq ? kWave - 1 : (int)(nq - 1 - c);
-      const K kf = __shfl(key, 0, kWave), kl = __shfl(key, last, kWave);
-      int64_t r = 0;
-      if (lane == 0) r = bound_search<K, false>(big, nb, kf, fence, nf);
-      else if (lane == 1) r = bound_search<K, true>(big, nb, kl, fence, nf);
-      A = __shfl(r, 0, kWave);
-      B = __shfl(r, 1, kWave);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+    if (qvalid && !qvalid[i]) {
+      lo_out[i] = 0;
+      cnt_out[i] = 0;
+      continue;
     }
-    const bool staged = mono && B - A <= kRangeWin;
-    if (staged)
-      for (int64_t j = lane; j < B - A; j += kWave) win[wave][j] = big[A + j];
-    __syncthreads();
-    if (inb) {
-      int64_t a, e;
-      if (!valid) {
-        a = 0;
-        e = 0;
-      } else if (staged) {
-        a = A + lds_bound<K, false>(win[wave], (int)(B - A), key);
-        e = A + lds_bound<K, true>(win[wave], (int)(B - A), key);
-      } else if (mono) {
-        a = A + bound_search<K, false>(big + A, B - A, key, nullptr, 0);
-        e = A + bound_search<K, true>(big + A, B - A, key, nullptr, 0);
-      } else {
-        a = bound_search<K, false>(big, nb, key, fence, nf);
-        e = a;
-        int k = 0;
-        while (e < nb && k < kScanRun && big[e] == key) {
-          ++e;
-          ++k;
-        }
-        if (k == kScanRun && e < nb && big[e] == key) e = e + bound_search<K, true>(big + e, nb - e, key, nullptr, 0);
+    const K key = q[i];
+    int64_t a = 0, b = nb;
+    if (fence) {
+      // fence[j] = big[j * kFence] (a 1/kFence sample small enough to stay in
+      // L2 / MALL): its lower bound j brackets the answer to one kFence-row
+      // window, so the search touches ~3 HBM lines instead of ~20
+      int64_t fa = 0, fb = nf;
+      while (fa < fb) {
+        const int64_t m = (fa + fb) >> 1;
+        if (fence[m] < key) fa = m + 1;
+        else fb = m;
       }
-      lo_out[i] = a;
-      cnt_out[i] = e - a;
+      a = fa > 0 ? (fa - 1) * kFence : 0;
+      b = fa * kFence < nb ? fa * kFence : nb;
     }
-    __syncthreads();
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (big[m] < key) a = m + 1;
+      else b = m;
+    }
+    int64_t e = a;
+    int k = 0;
+    while (e < nb && k < kScanRun && big[e] == key) {
+      ++e;
+      ++k;
+    }
+    if (k == kScanRun && e < nb && big[e] == key) {
+      int64_t a2 = e, b2 = nb;
+      while (a2 < b2) {
+        const int64_t m = (a2 + b2) >> 1;
+        if (big[m] <= key) a2 = m + 1;
+        else b2 = m;
+      }
+      e = a2;
+    }
+    lo_out[i] = a;
+    cnt_out[i] = e - a;
   }
 }
 

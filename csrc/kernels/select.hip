@@ -4,9 +4,13 @@
 // (reference crates/engine/src/operators/filter.rs:57). Three launches:
 //   1. per-tile popcount of the mask (32 bytes per lane, two uint4 loads),
 //   2. exclusive scan of the tile counts (one workgroup),
-//   3. per-tile rewrite: each wave writes its rows' indices in rounds of
-//      256 rows, one contiguous output run per round (ballot prefix of the
-//      per-lane counts); output order equals input order (stable).
+//   3. per-tile rewrite: each lane expands its 32 flags at its block-scan
+//      offset into an LDS staging buffer, then the workgroup streams the
+//      tile's indices out with contiguous (coalesced) stores; output order
+//      equals input order (stable). (A variant without the LDS stage — one
+//      ballot-ranked output run per 256 rows, no bank conflicts — measured
+//      56 us/call against 35 us: its per-lane scattered stores cost more than
+//      the staging conflicts, profiles/r3_sf100_pmc_roofline.txt.)
 // A tile is kBlock*32 = 8192 rows, so SF100 lineitem (600M rows) launches
 // ~73k workgroups: far more than 256 CUs x occupancy, as the HBM stream wants.
 #include "common.h"
@@ -103,64 +107,34 @@ __global__ __launch_bounds__(1024) void scan_counts_kernel(int64_t* __restrict__
 
 namespace {
 
-// Each wave owns 2048 consecutive rows of the tile and reads them as 8 rounds
-// of one 4-flag word per lane (round q, lane l: rows q*256 + 4l .. +3), so
-// row order is (round, lane, byte). A lane's position inside the round is the
-// wave prefix of the per-lane counts (0..4), taken with three ballots of the
-// count's bits; every round then writes one contiguous run of output. No LDS
-// staging: the earlier per-lane scatter into a uint16 LDS buffer spent ~40%
-// of the kernel in bank conflicts (profiles/r3_sf100_pmc_roofline.txt).
-constexpr int kWaveRows = kTile / kWavesPerBlock;     // 2048
-constexpr int kRounds = kWaveRows / (4 * kWave);      // 8
-
 template <typename IdxT>
 __global__ __launch_bounds__(kBlock) void tile_write_kernel(const uint8_t* __restrict__ mask, int64_t n,
                                                            const int64_t* __restrict__ offsets,
                                                            IdxT* __restrict__ out, int64_t cap) {
-  __shared__ int64_t wcount[kWavesPerBlock];
-  const int lane = lane_id(), wave = threadIdx.x / kWave;
-  const int64_t wbase_row = (int64_t)blockIdx.x * kTile + (int64_t)wave * kWaveRows;
-  uint32_t w[kRounds];
-  if (wbase_row + kWaveRows <= n && (((uintptr_t)mask) & 3) == 0) {
-#pragma unroll
-    for (int q = 0; q < kRounds; ++q)
-      w[q] = *reinterpret_cast<const uint32_t*>(mask + wbase_row + q * 4 * kWave + 4 * lane);
-  } else {
-#pragma unroll
-    for (int q = 0; q < kRounds; ++q) {
-      uint32_t x = 0;
-      const int64_t r0 = wbase_row + q * 4 * kWave + 4 * lane;
-      for (int bb = 0; bb < 4; ++bb)
-        if (r0 + bb < n && mask[r0 + bb]) x |= 1u << (8 * bb);
-      w[q] = x;
-    }
-  }
+  __shared__ int64_t scratch[kWavesPerBlock + 1];
+  __shared__ uint16_t stage[kTile];  // row offsets inside the tile, in output order
+  const int64_t tile_base = (int64_t)blockIdx.x * kTile;
+  const int first = threadIdx.x * kItems;
+  uint32_t w[kItems / 4];
+  load_flags(mask, tile_base + first, n, w);
   int64_t c = 0;
 #pragma unroll
-  for (int q = 0; q < kRounds; ++q) c += __popc(w[q]);
-  c = wave_reduce_sum(c);
-  if (lane == 0) wcount[wave] = c;
+  for (int q = 0; q < kItems / 4; ++q) c += __popc(w[q]);
+  int64_t total;
+  int pos = (int)block_exclusive_scan(c, scratch, &total);
+#pragma unroll
+  for (int q = 0; q < kItems / 4; ++q)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((w[q] >> (8 * b)) & 1u) stage[pos++] = (uint16_t)(first + 4 * q + b);
   __syncthreads();
-  int64_t run = offsets[blockIdx.x];
-  for (int v = 0; v < wave; ++v) run += wcount[v];
   // writes stay inside the caller's buffer of ``cap`` entries, and the last
   // tile zero-fills [total, cap): a size the host replayed instead of reading
   // (ops/_lib.py Speculation) can then never make this kernel or a consumer of
   // the indices touch memory out of bounds before the replay is validated
-#pragma unroll
-  for (int q = 0; q < kRounds; ++q) {
-    const int cq = __popc(w[q]);
-    const uint64_t b1 = __ballot(cq & 1), b2 = __ballot(cq & 2), b4 = __ballot(cq & 4);
-    int64_t p = run + lane_prefix(b1) + 2 * lane_prefix(b2) + 4 * lane_prefix(b4);
-    const int64_t r0 = wbase_row + q * 4 * kWave + 4 * lane;
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb)
-      if ((w[q] >> (8 * bb)) & 1u) {
-        if (p < cap) out[p] = (IdxT)(r0 + bb);
-        ++p;
-      }
-    run += __popcll(b1) + 2 * __popcll(b2) + 4 * __popcll(b4);
-  }
+  const int64_t o = offsets[blockIdx.x];
+  for (int k = threadIdx.x; k < (int)total; k += kBlock)
+    if (o + k < cap) out[o + k] = (IdxT)(tile_base + stage[k]);
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t p = offsets[gridDim.x] + threadIdx.x; p < cap; p += kBlock) out[p] = (IdxT)0;
 }
