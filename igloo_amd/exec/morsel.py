@@ -184,6 +184,45 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
         return merge_partials(lg.groups, plan, rb, ids, ctx)
 
 
+def streamed_scan(scan, ctx) -> Optional[Batch]:
+    """A filtered scan over the budget, materialised morsel by morsel: each
+    morsel is filtered and projected on its own and only the surviving rows
+    are kept (concatenated at the end), so the device never holds the
+    unfiltered columns. None when the scan fits (or cannot stream)."""
+    from .operators import concat_batches
+    src = scan.logical.source
+    if not getattr(src, "can_stream", False):
+        return None
+    nbytes = scan_bytes(scan)
+    if nbytes <= ctx.budget // STREAM_FRACTION:
+        return None
+    names, _, _ = scan.column_names()
+    row_bytes = max(1, nbytes // max(1, src.num_rows() or 1))
+    max_rows = max(MORSEL_MIN_ROWS, ctx.budget // MORSEL_FRACTION // row_bytes)
+    stats = ctx.morsels
+    stats["pipelines"] += 1
+    saved = ctx.morsel
+    outs = []
+    late, scan.late_ok = scan.late_ok, False
+    try:
+        with ctx.span("morsel.scan"):
+            for k, raw in enumerate(src.scan_morsels(names, ctx, scan.pushable(), max_rows)):
+                ctx.morsel = (id(scan), raw, ("morsel", stats["pipelines"], k))
+                stats["morsels"] += 1
+                stats["rows"] += raw.num_rows
+                stats["bytes"] += raw.nbytes
+                ctx.rows_scanned += raw.num_rows
+                outs.append(scan.finish(scan.scan_raw(ctx), ctx))
+                ctx.scan_cache = {k2: v for k2, v in ctx.scan_cache.items() if k2[-1] != ctx.morsel[2]}
+    finally:
+        ctx.morsel = saved
+        scan.late_ok = late
+    if not outs:
+        return None
+    out = concat_batches(outs) if len(outs) > 1 else outs[0]
+    return out
+
+
 def big_streamable(node, ctx) -> bool:
     """``node``'s output derives from a scan too big for the budget that
     could stream (an aggregate over ``node`` would run as a morsel pipeline)."""

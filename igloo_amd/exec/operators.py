@@ -365,6 +365,12 @@ class ScanExec(ExecNode):
         return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
 
     def _run(self, ctx):
+        if ctx.budget is not None and self.logical.filters and not ctx.spmd \
+                and not (ctx.morsel is not None and ctx.morsel[0] == id(self)):
+            from .morsel import streamed_scan
+            out = streamed_scan(self, ctx)
+            if out is not None:
+                return out
         return self.finish(self.scan_raw(ctx), ctx)
 
 

@@ -11,6 +11,7 @@ tables and no cap (SF10 on the CPU engine takes too long), then everything it
 held is released before the cap is set.
 Exit status 0 when all match and peak reserved memory stayed under the cap."""
 import argparse
+import gc
 import json
 import os
 import sys
@@ -56,7 +57,6 @@ def main():
         want[q] = digest(ref.sql(queries.QUERIES[q]).table)
     print(f"reference ({a.ref}) digests in {time.time() - t0:.1f}s", flush=True)
     del ref
-    import gc
     gc.collect()
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -71,24 +71,27 @@ def main():
         g.register_table(name, MemoryTable(t.columns, t.num_rows(), replicated=t.replicated, resident=False))
     bad, failed, spilled, streamed, rows = [], [], 0, 0, []
     for q in qs:
+        gc.collect()
+        torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats(0)
         t1 = time.time()
         try:
             got = digest(g.sql(queries.QUERIES[q]).table)
         except Exception as e:  # noqa: BLE001 - report and continue (an OOM under the cap)
-            print(f"Q{q}: FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)
+            print(f"Q{q}: FAILED {type(e).__name__}: {str(e)[:300]}", flush=True)
             failed.append(q)
-            torch.cuda.empty_cache()
+            e = None
             continue
         sp, mo = g.last_metrics["spill"], g.last_metrics["morsels"]
         spilled += sp["joins"] + sp.get("sorts", 0)
         streamed += mo["morsels"]
         peak = torch.cuda.max_memory_reserved(0)
+        alloc = torch.cuda.max_memory_allocated(0)
         ok = got == want[q]
         rows.append({"q": q, "ok": ok, "s": round(time.time() - t1, 3), "peak_reserved_mib": peak // 2**20,
-                     "morsels": mo, "spill": sp})
+                     "peak_allocated_mib": alloc // 2**20, "morsels": mo, "spill": sp})
         print(f"Q{q}: {'ok' if ok else 'MISMATCH'} {time.time() - t1:.2f}s morsels={mo['morsels']} "
-              f"spill={sp} peak_reserved={peak / 2**20:.0f} MiB", flush=True)
+              f"spill={sp} peak allocated={alloc / 2**20:.0f} reserved={peak / 2**20:.0f} MiB", flush=True)
         if not ok:
             bad.append(q)
     peak = max([r["peak_reserved_mib"] for r in rows] or [0])

@@ -531,3 +531,16 @@ def test_sorted_ranges_sorted_probe_keys(gpu_device, monkeypatch):
                 assert (got_cnt == want_cnt).all(), (dt, n, with_valid)
                 hit = want_cnt > 0
                 assert (got_lo[hit] == want_lo[hit]).all(), (dt, n, with_valid)
+
+
+def test_like_many_tiles_per_workgroup(gpu_device):
+    """strings.hip like_seg: more tiles than workgroups (2.5M strings, 9766
+    tiles over at most 8192 workgroups), so workgroups run several tiles and
+    the next tile's register prefetch is exercised, staged and unstaged."""
+    base = _words(20_000, seed=12)
+    long_ = [" ".join(["special requests"] * 40)] * 3   # oversized tiles mixed in
+    vals = (base * 125)[:2_499_997] + long_
+    c = _str_col(vals)
+    g = c.to(DEV)
+    for pat in ("%special%requests%", "%green", "PROMO%", "%requests"):
+        assert torch.equal(S.like(c, pat), S.like(g, pat).cpu()), pat
