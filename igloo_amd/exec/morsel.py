@@ -80,7 +80,11 @@ def stream_path_ok(node, target) -> bool:
             return kind in ("inner", "right") and stream_path_ok(right, target)
         return False
     if isinstance(node, MultiJoinExec):
-        inside = [c for c in node.children if _contains(c, target)]
+        # the inner-join inputs only: the trailing children are SEMI / ANTI build sides
+        nin = len(node.logical.children)
+        if any(_contains(c, target) for c in node.children[nin:]):
+            return False
+        inside = [c for c in node.children[:nin] if _contains(c, target)]
         return len(inside) == 1 and stream_path_ok(inside[0], target)
     return False
 
@@ -124,8 +128,8 @@ def pick_stream_scan(agg, ctx):
 def streamed_aggregate(agg, ctx) -> Optional[Batch]:
     """Run aggregate node ``agg`` as a morsel pipeline when the budget calls
     for it; None when it does not (or the aggregates do not decompose)."""
-    from ..parallel.exchange import _TmpIds, decomposable, merge_partials, partial_plan
-    from .operators import ScanExec, aggregate, apply_key_filters, concat_batches
+    from ..parallel.exchange import _TmpIds, decomposable, partial_plan
+    from .operators import ScanExec, aggregate, apply_key_filters
     lg = agg.logical
     if ctx.budget is None or ctx.spmd or not decomposable(lg.aggs):
         return None
@@ -148,6 +152,7 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
     ctx.memo, ctx.memo_ids = {}, {id(n) for n in _walk(child) if id(n) not in on_path}
     ctx.morsel_depth += 1
     parts: List[Batch] = []
+    acc = _PartialStates(lg.groups, partial, plan, ids, ctx, max(1, (src.num_rows() or 1) // max_rows + 1))
     stats = ctx.morsels
     stats["pipelines"] += 1
     try:
@@ -170,18 +175,122 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
                     if agg.runtime_filters:
                         b = apply_key_filters(b, list(agg.runtime_filters), ctx)
                     pb = aggregate(lg.groups, partial, b, ctx)
-                parts.append(pb)
+                acc.add(pb)
                 ctx.scan_cache = {k2: v for k2, v in ctx.scan_cache.items() if k2[-1] != ctx.morsel[2]}
                 ctx.morsel = None
     finally:
         ctx.memo, ctx.memo_ids, ctx.morsel = saved
         ctx.morsel_depth -= 1
         agg.runtime_filters = []
-    if not parts:
-        return None
     with ctx.span("morsel.merge"):
-        rb = concat_batches(parts)
-        return merge_partials(lg.groups, plan, rb, ids, ctx)
+        return acc.finish()
+
+
+class _PartialStates:
+    """Partial aggregate states of a morsel pipeline, bounded in device memory:
+
+    * they accumulate on the device; past budget / 4 bytes they are compacted
+      (re-aggregated into one partial state per group: SUM of sums and
+      counts, MIN of mins, ...), which bounds them by the group count when
+      groups repeat across morsels (TPC-H Q17: parts over lineitem);
+    * when compaction cannot shrink them (groups aligned with the stream,
+      Q18's orders over lineitem), every later partial is hash-partitioned on
+      the group keys into pinned host memory, and the final merge runs one
+      partition at a time (a grace aggregation).
+    """
+
+    def __init__(self, groups, partial, plan, ids, ctx, morsels_expected: int):
+        self.groups, self.partial, self.plan, self.ids, self.ctx = groups, partial, plan, ids, ctx
+        self.parts: List[Batch] = []
+        self.bytes = 0
+        self.limit = ctx.budget // 4
+        self.spill = None          # P lists of host batches once partitioned
+        self.expected = morsels_expected
+        self.seen = 0
+
+    def add(self, pb: Batch) -> None:
+        from .operators import _batch_bytes, concat_batches
+        self.seen += 1
+        if self.spill is not None:
+            self._distribute(pb)
+            return
+        self.parts.append(pb)
+        self.bytes += _batch_bytes(pb)
+        if self.bytes <= self.limit or not self.groups or len(self.parts) < 2:
+            return
+        with self.ctx.span("morsel.compact"):
+            c = self._compact(concat_batches(self.parts))
+        cb = _batch_bytes(c)
+        self.ctx.morsels["compactions"] = self.ctx.morsels.get("compactions", 0) + 1
+        self.parts, self.bytes = [c], cb
+        if cb > self.limit // 2:
+            # groups do not repeat enough: partition everything to host memory
+            per = cb / max(1, self.seen)
+            total = per * max(self.expected, self.seen)
+            P = 2
+            while total / P > self.ctx.budget / 8 and P < 1024:
+                P *= 2
+            self.spill = [[] for _ in range(P)]
+            parts, self.parts, self.bytes = self.parts, [], 0
+            for b in parts:
+                self._distribute(b)
+        else:
+            self.limit = max(self.limit, 2 * cb)
+
+    def _compact(self, rb: Batch) -> Batch:
+        """Re-aggregate partial states into one partial row per group (same column ids)."""
+        from ..parallel.exchange import _join_wide_finals, _split_wide_partials, _wide_finals
+        from ..sql.expr import AggCall
+        from .operators import aggregate
+        fgroups = [(ci, ci.ref()) for ci, _ in self.groups]
+        rb, wide = _split_wide_partials(rb, self.plan, self.ids)
+        merge = {"sum": "sum", "count": "sum", "min": "min", "max": "max", "bool_and": "bool_and",
+                 "bool_or": "bool_or"}
+        final = [(pci, AggCall(merge[call.func], pci.ref(), False, pci.dtype)) for pci, call in self.partial]
+        final, rec = _wide_finals(final, wide, self.ids)
+        return _join_wide_finals(aggregate(fgroups, final, rb, self.ctx), rec)
+
+    def _distribute(self, b: Batch) -> None:
+        from ..ops import misc as M
+        from ..parallel.exchange import partition_keys
+        from .operators import _batch_bytes, _to_host, take_many
+        P = len(self.spill)
+        key = None
+        for ci, _ in self.groups:
+            k = partition_keys(b.columns[ci.cid]).to(torch.int64)
+            key = k if key is None else (key * 1000003) ^ k
+        perm, counts = M.hash_partition(key.contiguous(), P)
+        keys = list(b.columns)
+        start = 0
+        for p, c in enumerate(counts):
+            idx = perm[start:start + c]
+            start += c
+            if c == 0:
+                continue
+            piece = Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], idx))), c)
+            self.ctx.spill["bytes"] += _batch_bytes(piece)
+            self.spill[p].append(_to_host(piece) if self.ctx.device.type == "cuda" else piece)
+        self.ctx.spill["aggregate_partitions"] = P
+
+    def finish(self) -> Optional[Batch]:
+        from ..parallel.exchange import merge_partials
+        from .operators import _to_device, _to_host, concat_batches
+        if self.spill is None:
+            if not self.parts:
+                return None
+            return merge_partials(self.groups, self.plan, concat_batches(self.parts), self.ids, self.ctx)
+        dev = self.ctx.device
+        outs = []
+        for plist in self.spill:
+            if not plist:
+                continue
+            d = concat_batches([_to_device(b, dev) if dev.type == "cuda" else b for b in plist])
+            o = merge_partials(self.groups, self.plan, d, self.ids, self.ctx)
+            outs.append(_to_host(o) if dev.type == "cuda" else o)
+            del d
+        if not outs:
+            return None
+        return concat_batches([_to_device(o, dev) if dev.type == "cuda" else o for o in outs])
 
 
 def streamed_scan(scan, ctx) -> Optional[Batch]:

@@ -26,7 +26,7 @@ def engines():
 
 def test_tpch_22_under_budget_match(engines):
     full, small = engines
-    morsels, semi = {}, {}
+    morsels, semi, compact, parts = {}, {}, {}, {}
     for q in range(1, 23):
         want = digest(full.sql(queries.QUERIES[q]).table)
         got = digest(small.sql(queries.QUERIES[q]).table)
@@ -34,6 +34,12 @@ def test_tpch_22_under_budget_match(engines):
         m = small.last_metrics["morsels"]
         morsels[q] = m["morsels"]
         semi[q] = m.get("semi_aggregates", 0)
+        compact[q] = m.get("compactions", 0)
+        parts[q] = small.last_metrics["spill"].get("aggregate_partitions", 0)
+    # partial states re-aggregated when groups repeat across morsels (Q17:
+    # parts over lineitem) and hash-partitioned to host memory when they do
+    # not (Q18: one group per order)
+    assert compact[17] > 0 and parts[18] > 1, (compact, parts)
     # every query whose lineitem (Q13: orders) scan feeds an aggregate through
     # filters / joins, a SEMI / ANTI build side or Q13's per-key counts
     for q in (1, 3, 4, 5, 6, 7, 8, 9, 10, 12, 13, 14, 15, 17, 18, 19, 20, 21):
