@@ -10,7 +10,7 @@ from igloo_amd.catalog import MemoryTable
 from igloo_amd.models.tpch import datagen, queries
 from igloo_amd.utils.digest import digest
 
-BUDGET_GB = 1.5 / 1024        # 1.5 MB: lineitem at SF0.02 is ~5 MB of scanned columns
+BUDGET_GB = 1.25 / 1024       # 1.25 MB: lineitem at SF0.02 is ~5 MB of scanned columns
 
 
 @pytest.fixture(scope="module")
