@@ -275,6 +275,18 @@ def _decimal_to_int64(arr: pa.Array) -> np.ndarray:
     return out
 
 
+def batch_device(b) -> Optional[torch.device]:
+    """Device of a batch's columns without materialising any: lazy batches
+    (join results in index form, filtered scans) report theirs from their
+    row-index tensors; a plain batch from its first column."""
+    d = getattr(b, "device", None)
+    if isinstance(d, torch.device):
+        return d
+    for c in b.columns.values():
+        return c.device
+    return None
+
+
 class Batch:
     """An ordered set of equally long columns keyed by column id (or name)."""
 

@@ -21,7 +21,7 @@ import pyarrow.compute as pc
 import torch
 
 from .. import types as T
-from ..columnar import Batch, Column
+from ..columnar import Batch, Column, batch_device
 from ..ops import misc as M
 from ..ops._lib import to_host_ints
 from ..ops import strings as S
@@ -68,7 +68,7 @@ class Evaluator:
 
     def eval(self, e: Expr, b: Batch) -> Value:
         if not self._jit_off and type(e) in _JIT_ROOTS and b.num_rows >= JIT_MIN_ROWS and b.columns \
-                and (next(iter(b.columns.values())).data.is_cuda or _JIT_ON_CPU):
+                and (_JIT_ON_CPU or getattr(batch_device(b), "type", None) == "cuda"):
             from . import expr_jit
             r = expr_jit.evaluate(e, b, self)
             if isinstance(r, Column):
@@ -110,8 +110,9 @@ class Evaluator:
         return m
 
     def device(self, b: Batch) -> torch.device:
-        for c in b.columns.values():
-            return c.device
+        d = batch_device(b)
+        if d is not None:
+            return d
         return torch.device(self.ctx.device if self.ctx is not None else "cpu")
 
     # ------------------------------------------------------------ leaf nodes

@@ -29,7 +29,7 @@ import pyarrow as pa
 import torch
 
 from .. import types as T
-from ..columnar import Batch, Column
+from ..columnar import Batch, Column, batch_device
 from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
@@ -1215,10 +1215,11 @@ class _LazyColumns:
         return list(self._lb.owner)
 
     def values(self):
-        return [self._lb.gather(c) for c in self._lb.owner]
+        # lazy: a caller that only looks at the first column gathers one
+        return (self._lb.gather(c) for c in list(self._lb.owner))
 
     def items(self):
-        return [(c, self._lb.gather(c)) for c in self._lb.owner]
+        return ((c, self._lb.gather(c)) for c in list(self._lb.owner))
 
 
 class LateBatch(Batch):
@@ -1241,6 +1242,15 @@ class LateBatch(Batch):
     @property
     def columns(self):  # type: ignore[override]
         return _LazyColumns(self)
+
+    @property
+    def device(self):
+        """Device of the join result, from its index tensors (gathers nothing)."""
+        for bb, idx in self.parts:
+            d = idx.device if idx is not None else batch_device(bb)
+            if d is not None:
+                return d
+        return None
 
     def gather(self, cid) -> Column:
         c = self._cache.get(cid)
@@ -1305,10 +1315,10 @@ class _ScanColumns:
         return list(self._b.src.columns)
 
     def values(self):
-        return [self._b.gather(c) for c in self._b.src.columns]
+        return (self._b.gather(c) for c in list(self._b.src.columns))
 
     def items(self):
-        return [(c, self._b.gather(c)) for c in self._b.src.columns]
+        return ((c, self._b.gather(c)) for c in list(self._b.src.columns))
 
 
 class _LazyScanBatch(Batch):
@@ -1324,6 +1334,10 @@ class _LazyScanBatch(Batch):
         self.dist = src.dist
         self.out_dist = None
         self.columns = _ScanColumns(self)
+
+    @property
+    def device(self):
+        return self.idx.device
 
     def has(self, cid) -> bool:
         return self._names[cid] in self._shared

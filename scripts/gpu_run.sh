@@ -84,6 +84,25 @@ SETS
       IGLOO_JIT_CACHE="$R/gpurun_out/jit_cache" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
         --steps 1 --warmup 1 --eager-steps 0 --vary-params 0 > gpurun_out/jitcache.log 2>&1
       rc=$?; echo "jitcache rc=$rc"; ls gpurun_out/jit_cache | wc -l ;;
+    budget)
+      # all 22 queries at SF${SF:-10} with the device capped at 1 GB (morsels, spill, external sort)
+      timeout -k 10 900 python -u scripts/budget_check.py --sf ${SF:-10} --cap-gb 1 --budget-gb 0.25 --ref gpu \
+        --json gpurun_out/budget_sf${SF:-10}.json > gpurun_out/budget_sf${SF:-10}.log 2>&1
+      rc=$?; echo "budget rc=$rc"; tail -3 gpurun_out/budget_sf${SF:-10}.log ;;
+    share2)
+      # two ranks sharing the one GPU (gloo collectives, host staged) vs one rank, SF1
+      timeout -k 10 400 python -u bench.py --sf 1 --steps 10 --warmup 3 --per-query \
+        > gpurun_out/bench_sf1_1rank.log 2>&1
+      rc=$?; echo "sf1 1-rank rc=$rc"; tail -1 gpurun_out/bench_sf1_1rank.log | cut -c1-200
+      [ $rc -eq 0 ] || exit $rc
+      IGLOO_BENCH_SHARE_GPU=1 IGLOO_BENCH_DIR=/tmp/igloo_tpch_w2 timeout -k 10 600 python -u -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --sf 1 \
+        --steps 10 --warmup 3 --per-query > gpurun_out/bench_sf1_2rank_shared.log 2>&1
+      rc=$?; echo "sf1 2-rank shared rc=$rc"; tail -1 gpurun_out/bench_sf1_2rank_shared.log | cut -c1-200 ;;
+    gsites)
+      timeout -k 10 600 python -u scripts/gather_sites.py --sf ${SF:-100} --queries ${QS:-1-22} \
+        --out gpurun_out/gather_sites.txt > gpurun_out/gather_sites.log 2>&1
+      rc=$?; echo "gsites rc=$rc"; head -30 gpurun_out/gather_sites.txt ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac
   [ $rc -eq 0 ] || exit $rc
