@@ -286,7 +286,7 @@ def main():
             log(f"[bench] graphs: {_graphs.STATS}; engine graphs {len(eng._graphs)} holding "
                 f"{eng.graph_bytes / 2**30:.1f} GiB, {eng.graph_stats}; cache tier {eng.cache.hbm_used / 2**30:.1f} GiB; "
                 f"HBM reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB, "
-                f"peak allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+                f"peak allocated {eng.hbm_peak_bytes / 2**30:.1f} GiB (max per-query high-water mark)")
             for msg in _graphs.LAST_ERROR:
                 log("[bench] graph not captured: " + msg.strip().replace("\n", " | ")[-600:])
         if per_q:

@@ -506,9 +506,11 @@ PYBIND11_MODULE(_native, m) {
     kern::str_hash64(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(valid), P<int64_t>(out), S(s));
   });
   m.def("str_like_segments", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t seg, uintptr_t seg_off, int nseg,
-                                 bool anchor_start, bool anchor_end, bool negate, uintptr_t out, uintptr_t s) {
+                                 bool anchor_start, bool anchor_end, bool negate, uintptr_t out, int64_t nbytes,
+                                 uintptr_t s) {
     kern::str_like_segments(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(seg),
-                            P<const int32_t>(seg_off), nseg, anchor_start, anchor_end, negate, P<uint8_t>(out), S(s));
+                            P<const int32_t>(seg_off), nseg, anchor_start, anchor_end, negate, P<uint8_t>(out), nbytes,
+                            S(s));
   });
   m.def("str_eq_rows", [](uintptr_t aoff, uintptr_t achars, uintptr_t ai, uintptr_t boff, uintptr_t bchars, uintptr_t bi,
                           bool idx64, int64_t n, uintptr_t mism, uintptr_t s) {
@@ -568,6 +570,7 @@ PYBIND11_MODULE(_native, m) {
                         P<int64_t>(cnt), P<const void>(fence), nf, S(s));
   });
   m.attr("SEARCH_FENCE") = kern::kFence;
+  m.attr("STATS_SLOTS") = kern::kStatsSlots;
   m.def("expand_ranges", [](uintptr_t off, uintptr_t lo, int64_t ns, int64_t total, uintptr_t sidx, uintptr_t bidx,
                             bool out64, uintptr_t s) {
     kern::expand_ranges(P<const int64_t>(off), P<const int64_t>(lo), ns, total, P<void>(sidx), P<void>(bidx), out64,

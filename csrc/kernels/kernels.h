@@ -69,6 +69,9 @@ void unpack_rows(const PackSpec& spec, const uint8_t* in, int64_t n, hipStream_t
 // ---- util.hip -------------------------------------------------------------------
 void const_ints(int64_t* out, const int64_t* vals, int64_t n, hipStream_t stream);
 void end_capture(hipStream_t stream);
+// out: kStatsSlots int64 (min, max, unsorted flag, then per-block partials)
+constexpr int kStatsMaxBlocks = 4096;
+constexpr int kStatsSlots = 3 + 3 * kStatsMaxBlocks;
 void column_stats(const void* keys, bool key64, const uint8_t* valid, int64_t n, long long* out, hipStream_t stream);
 void run_bounds(const void* keys, bool key64, int64_t n, uint8_t* out, hipStream_t stream);
 
@@ -245,7 +248,7 @@ void str_parse(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_
 // LIKE made of '%'-separated literals (no '_'): segments concatenated in `seg`
 // with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%'
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
-                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, hipStream_t stream);
+                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, int64_t nbytes, hipStream_t stream);
 void wide_fits(const int64_t* lo, const int64_t* hi, int64_t n, int* flag, hipStream_t stream);
 void avg_wide(const int64_t* sums, bool wide, const int64_t* cnt, int64_t n, int64_t up, int64_t* out,
               hipStream_t stream);

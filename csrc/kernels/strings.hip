@@ -122,7 +122,6 @@ __global__ __launch_bounds__(kBlock) void like_tile_kernel(const int64_t* __rest
 // against this kernel's 5.0 ms for Q13 at SF100: the extra registers cost
 // more occupancy than the overlap gained.)
 constexpr int kSegMax = 4;
-constexpr int kSegBits = kLikeTileBytes / 64;  // 64-bit words per segment bitmap
 
 __device__ inline int next_hit(const uint64_t* bits, int from, int last) {
   // smallest p in [from, last] with bit p set, or -1
@@ -140,40 +139,46 @@ __device__ inline int next_hit(const uint64_t* bits, int from, int last) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void like_seg_kernel(const int64_t* __restrict__ off,
+// BLOCK threads take BLOCK consecutive strings per tile of at most TILE bytes.
+// BLOCK = 64 makes every wave its own workgroup: the three tile barriers are
+// single-wave barriers, and a wave waiting on its tile's loads never holds up
+// the three others' matching (the 256-thread shape syncs all four per tile).
+template <int BLOCK, int TILE>
+__global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restrict__ off,
                                                          const uint8_t* __restrict__ chars, int64_t n,
                                                          const uint8_t* __restrict__ seg, const int32_t* seg_off,
                                                          int nseg, bool anchor_start, bool anchor_end, bool negate,
                                                          uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kLikeTileBytes + 64];
+  constexpr int kSegBits = TILE / 64;  // 64-bit words per segment bitmap
+  __shared__ __attribute__((aligned(16))) uint8_t buf[TILE + 64];
   __shared__ uint64_t bits[kSegMax][kSegBits];
   __shared__ uint8_t sseg[kLikeMaxPattern];
   __shared__ int32_t soff[kSegMax + 1];
   const int total = seg_off[nseg];
-  for (int i = threadIdx.x; i < total; i += kBlock) sseg[i] = seg[i];
+  for (int i = threadIdx.x; i < total; i += BLOCK) sseg[i] = seg[i];
   if (threadIdx.x <= nseg) soff[threadIdx.x] = seg_off[threadIdx.x];
-  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  const int64_t tiles = (n + BLOCK - 1) / BLOCK;
   for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int64_t i0 = t * kBlock;
-    const int64_t i1 = i0 + kBlock < n ? i0 + kBlock : n;
+    const int64_t i0 = t * BLOCK;
+    const int64_t i1 = i0 + BLOCK < n ? i0 + BLOCK : n;
     const uintptr_t lo = (uintptr_t)(chars + off[i0]);
     const uintptr_t hi = (uintptr_t)(chars + off[i1]);
     const uintptr_t start = lo & ~(uintptr_t)15;
     const uintptr_t full_end = hi & ~(uintptr_t)15;
     const int len = (int)(hi - start);
-    const bool staged = hi - start <= (uintptr_t)kLikeTileBytes;
+    const bool staged = hi - start <= (uintptr_t)TILE;
     __syncthreads();  // previous tile done; pattern visible on the first pass
     if (staged) {
       const int64_t nvec = (int64_t)(full_end - start) / 16;
-      for (int64_t v = threadIdx.x; v < nvec; v += kBlock) *(uint4*)(buf + v * 16) = *(const uint4*)(start + v * 16);
-      for (uintptr_t a = full_end + threadIdx.x; a < hi; a += kBlock) buf[a - start] = *(const uint8_t*)a;
+      for (int64_t v = threadIdx.x; v < nvec; v += BLOCK) *(uint4*)(buf + v * 16) = *(const uint4*)(start + v * 16);
+      for (uintptr_t a = full_end + threadIdx.x; a < hi; a += BLOCK) buf[a - start] = *(const uint8_t*)a;
       if (threadIdx.x < 64) buf[len + threadIdx.x] = 0;  // pad: comparisons may read past the tile end
       __syncthreads();
       // each lane tests the 16 positions of one 16-byte chunk against every
       // segment's 4-byte prefix in registers (v_alignbyte windows), verifies
       // the rare candidates byte-wise, and stores a 16-bit hit mask
       const int nchunks = ((len + 63) >> 6) * 4;
-      for (int j = threadIdx.x; j < nchunks; j += kBlock) {
+      for (int j = threadIdx.x; j < nchunks; j += BLOCK) {
         const uint4 v = *(const uint4*)(buf + j * 16);
         const uint32_t d[5] = {v.x, v.y, v.z, v.w, *(const uint32_t*)(buf + j * 16 + 16)};
         for (int sg = 0; sg < nseg; ++sg) {
@@ -421,11 +426,29 @@ void str_like(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t
 }
 
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
-                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, hipStream_t stream) {
+                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, int64_t nbytes,
+                       hipStream_t stream) {
   if (n == 0) return;
   if (nseg > kSegMax) throw std::runtime_error("str_like_segments: too many segments");
-  hipLaunchKernelGGL(like_seg_kernel, dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock), 0, stream, off, chars, n,
-                     seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  // IGLOO_LIKE_WAVE=1: one-wave workgroups (A/B; measured slower for Q13 at
+  // SF100, 14.6 vs 11.7 ms per query, profiles/r3_ab_like_wave.txt)
+  static const bool wave = [] {
+    const char* e = getenv("IGLOO_LIKE_WAVE");
+    return e && e[0] == '1';
+  }();
+  // one wave per workgroup; tiles of 64 strings sized from the mean length
+  // (4 KB fits 64 TPC-H o_comment values, ~49 B, with room; longer strings
+  // take the 8 KB tile) so that nearly every tile is staged in LDS
+  const int64_t mean = nbytes / n;
+  if (wave && mean <= 48)
+    hipLaunchKernelGGL((like_seg_kernel<64, 4096>), dim3(grid_for(n, 64, 256 * 24 * 4)), dim3(64), 0, stream, off,
+                       chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  else if (wave && mean <= 100)
+    hipLaunchKernelGGL((like_seg_kernel<64, 8192>), dim3(grid_for(n, 64, 256 * 12 * 4)), dim3(64), 0, stream, off,
+                       chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  else
+    hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes>), dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock),
+                       0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
   check_launch("str_like_segments", stream);
 }
 

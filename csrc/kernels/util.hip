@@ -5,7 +5,10 @@
 //   column_stats  -> {min, max, sorted flag} of an int32/int64 key column
 //                    (NULL rows skipped) in ONE read: every lane checks its
 //                    run of 64 bytes plus the row before it; block min/max via
-//                    wave shuffles, one atomic per block;
+//                    wave shuffles into a per-block partial, reduced by a
+//                    one-block second kernel (same-address device atomics from
+//                    thousands of blocks serialise at the memory side: they
+//                    held the SF100 calls at ~1 TB/s);
 //   run_bounds    -> bound[i] = (i == 0 || k[i] != k[i-1]) for run-id group-by
 //                    over clustered keys.
 #include <limits>
@@ -44,7 +47,7 @@ __device__ inline int64_t wave_max(int64_t v) {
 // 1.7 TB/s over 77 calls per suite.)
 template <typename T, bool HAS_VALID>
 __global__ __launch_bounds__(kBlock) void column_stats_kernel(const T* __restrict__ k, const uint8_t* __restrict__ valid,
-                                                              int64_t n, long long* __restrict__ out) {
+                                                              int64_t n, long long* __restrict__ part) {
   constexpr int kRun = 64 / sizeof(T);
   __shared__ int64_t smin[kWavesPerBlock], smax[kWavesPerBlock];
   __shared__ int sbad;
@@ -108,16 +111,47 @@ __global__ __launch_bounds__(kBlock) void column_stats_kernel(const T* __restric
       a = smin[i] < a ? smin[i] : a;
       b = smax[i] > b ? smax[i] : b;
     }
-    if (a != INT64_MAX) atomicMin(&out[0], (long long)a);
-    if (b != INT64_MIN) atomicMax(&out[1], (long long)b);
-    if (sbad) atomicMax(&out[2], 1LL);
+    part[blockIdx.x * 3 + 0] = a;
+    part[blockIdx.x * 3 + 1] = b;
+    part[blockIdx.x * 3 + 2] = sbad;
   }
 }
 
-__global__ void stats_init_kernel(long long* out) {
-  out[0] = INT64_MAX;
-  out[1] = INT64_MIN;
-  out[2] = 0;
+// out[0..2] from the g per-block partials (one block)
+__global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const long long* __restrict__ part, int g,
+                                                              long long* __restrict__ out) {
+  __shared__ int64_t smin[kWavesPerBlock], smax[kWavesPerBlock];
+  __shared__ int sbad;
+  if (threadIdx.x == 0) sbad = 0;
+  __syncthreads();
+  int64_t mn = INT64_MAX, mx = INT64_MIN;
+  bool bad = false;
+  for (int i = threadIdx.x; i < g; i += kBlock) {
+    const int64_t a = part[i * 3], b = part[i * 3 + 1];
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+    bad |= part[i * 3 + 2] != 0;
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const uint64_t anybad = __ballot(bad);
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    smin[w] = mn;
+    smax[w] = mx;
+    if (anybad) sbad = 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t a = smin[0], b = smax[0];
+    for (int i = 1; i < kWavesPerBlock; ++i) {
+      a = smin[i] < a ? smin[i] : a;
+      b = smax[i] > b ? smax[i] : b;
+    }
+    out[0] = a;
+    out[1] = b;
+    out[2] = sbad;
+  }
 }
 
 template <typename T>
@@ -131,26 +165,32 @@ __global__ __launch_bounds__(kBlock) void run_bounds_kernel(const T* __restrict_
 
 void column_stats(const void* keys, bool key64, const uint8_t* valid, int64_t n, long long* out, hipStream_t stream) {
   // out[0] = min, out[1] = max over non-NULL rows; out[2] = 1 if some row is
-  // below its predecessor (only meaningful without NULLs)
-  hipLaunchKernelGGL(stats_init_kernel, dim3(1), dim3(1), 0, stream, out);
-  if (n <= 0) return;
+  // below its predecessor (only meaningful without NULLs). out holds
+  // kStatsSlots int64: out[3..] takes the per-block partials.
   const int run = key64 ? 8 : 16;
-  const unsigned g = grid_for(n, kBlock * run, 4096);
+  const unsigned g = n > 0 ? grid_for(n, kBlock * run, kStatsMaxBlocks) : 0;
+  long long* part = out + 3;
+  if (g == 0) {
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, part, 0, out);
+    check_launch("util.column_stats", stream);
+    return;
+  }
   if (key64) {
     if (valid)
       hipLaunchKernelGGL((column_stats_kernel<int64_t, true>), dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys,
-                         valid, n, out);
+                         valid, n, part);
     else
       hipLaunchKernelGGL((column_stats_kernel<int64_t, false>), dim3(g), dim3(kBlock), 0, stream, (const int64_t*)keys,
-                         valid, n, out);
+                         valid, n, part);
   } else {
     if (valid)
       hipLaunchKernelGGL((column_stats_kernel<int32_t, true>), dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys,
-                         valid, n, out);
+                         valid, n, part);
     else
       hipLaunchKernelGGL((column_stats_kernel<int32_t, false>), dim3(g), dim3(kBlock), 0, stream, (const int32_t*)keys,
-                         valid, n, out);
+                         valid, n, part);
   }
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, part, (int)g, out);
   check_launch("util.column_stats", stream);
 }
 

@@ -152,6 +152,7 @@ class QueryEngine:
         self.cache = TieredCache(CacheConfig(hbm_bytes=int(hbm), host_bytes=int(host), disk_path=cache_dir,
                                              device=str(self.device)))
         self.cdc = CdcManager(self.cache)
+        self.hbm_peak_bytes = 0     # highest per-query HBM high-water mark (last_metrics["hbm_peak_bytes"])
         # device bytes the cache tier's resident columns and the query graphs'
         # private memory pools may hold together (exec/graphs.py); past it the
         # least recently replayed graphs are dropped (their pools return to
@@ -331,10 +332,28 @@ class QueryEngine:
         c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
         from .ops._lib import HOST_STEPS
         h0 = sum(HOST_STEPS.values())
+        cs0 = (self.cache.stats["hits"], self.cache.stats["misses"])
+        gpu = self.device.type == "cuda"
+        if gpu:
+            # per-query HBM high-water mark and device time (one event pair;
+            # the result readback below already synchronises the stream)
+            torch.cuda.reset_peak_memory_stats(self.device)
+            mem0 = torch.cuda.memory_allocated(self.device)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         with _trace.Range("query"):
             batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
         if table is None:
             table = self._to_arrow(batch, plan.schema, bq_names)
+        dev_metrics = {}
+        if gpu:
+            ev1.record()
+            ev1.synchronize()
+            peak = torch.cuda.max_memory_allocated(self.device)
+            self.hbm_peak_bytes = max(self.hbm_peak_bytes, peak)
+            dev_metrics = {"device_ms": round(ev0.elapsed_time(ev1), 3), "hbm_peak_bytes": int(peak),
+                           "hbm_query_bytes": int(max(0, peak - mem0))}
+        hits, misses = self.cache.stats["hits"] - cs0[0], self.cache.stats["misses"] - cs0[1]
         if st is not None and spec in ("replayed", "recorded") and st["capture_next"]:
             st["digest"] = digest(table)      # the next execution's graph must reproduce it
         if spec != "graph":
@@ -343,7 +362,10 @@ class QueryEngine:
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
                              "spill": dict(ctx.spill), "morsels": dict(ctx.morsels), "plan_cached": cached, "speculation": spec,
                              # work that left the GPU (ops/_lib.py note_host_step)
-                             "host_steps": sum(HOST_STEPS.values()) - h0}
+                             "host_steps": sum(HOST_STEPS.values()) - h0,
+                             "cache": {"hits": hits, "misses": misses,
+                                       "hit_ratio": round(hits / (hits + misses), 4) if hits + misses else None},
+                             **dev_metrics}
         if self.comm is not None:
             self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
         return QueryResult(table, ms)

@@ -54,10 +54,11 @@ def column_stats(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Tu
         mn, mx = torch.aminmax(k)
         srt = True if k.numel() < 2 else bool((k[1:] >= k[:-1]).all().item())
         return (int(mn.item()), int(mx.item())), srt
-    out = torch.empty(3, dtype=torch.int64, device=keys.device)
-    launch("column_stats").column_stats(ptr(keys.contiguous()), keys.dtype == torch.int64,
-                                         ptr(valid.contiguous() if valid is not None else None), n, ptr(out),
-                                         stream(keys))
+    N = launch("column_stats")
+    buf = torch.empty(N.STATS_SLOTS, dtype=torch.int64, device=keys.device)   # result + per-block partials
+    N.column_stats(ptr(keys.contiguous()), keys.dtype == torch.int64,
+                   ptr(valid.contiguous() if valid is not None else None), n, ptr(buf), stream(keys))
+    out = buf[:3]
     if valid is None and getattr(keys, "_igloo_resident", False):
         with unlogged():      # remembered below: a one-time build (ops/_lib.py unlogged)
             mn, mx, bad = to_host_ints(out)

@@ -183,7 +183,8 @@ def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, esca
             torch.tensor(seg_off, dtype=torch.int32).to(dev)))
         out = torch.empty(n, dtype=torch.bool, device=dev)
         launch("str_like_segments").str_like_segments(ptr(col.offsets), ptr(col.data), n, ptr(sb), ptr(so),
-                                                      len(seg_off) - 1, a0, a1, negate, ptr(out), stream(out))
+                                                      len(seg_off) - 1, a0, a1, negate, ptr(out), col.data.numel(),
+                                                      stream(out))
         return out
     pt, kt = _consts(("pat", pattern, escape, dev), lambda: (
         torch.tensor(list(pat) or [0], dtype=torch.uint8).to(dev),

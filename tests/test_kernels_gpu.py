@@ -544,3 +544,18 @@ def test_like_many_tiles_per_workgroup(gpu_device):
     g = c.to(DEV)
     for pat in ("%special%requests%", "%green", "PROMO%", "%requests"):
         assert torch.equal(S.like(c, pat), S.like(g, pat).cpu()), pat
+
+
+@pytest.mark.parametrize("words", [(1, 4), (4, 9), (8, 20)])
+def test_like_tile_shapes(gpu_device, words):
+    """like_seg over short, medium and long strings against the CPU matcher
+    (the one-wave variant, IGLOO_LIKE_WAVE=1, picks its 4 KB / 8 KB tile from
+    the mean length; the default takes 16 KB four-wave tiles)."""
+    r = _rng(21)
+    lo, hi = words
+    vals = [" ".join(r.choice(WORDS, r.integers(lo, hi))) for _ in range(60_000)]
+    c = _str_col(vals)
+    g = c.to(DEV)
+    for pat in ("%special%requests%", "%Customer%Complaints%", "forest%", "%BRASS", "%e%e%e%"):
+        assert torch.equal(S.like(c, pat), S.like(g, pat).cpu()), pat
+        assert torch.equal(S.like(c, pat, negate=True), S.like(g, pat, negate=True).cpu()), pat

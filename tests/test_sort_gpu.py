@@ -142,7 +142,7 @@ def test_order_by_nulls_first_sql(gpu_device):
     assert r.column("k").to_pylist() == [5, 3, 2]
 
 
-@pytest.mark.parametrize("n", [0, 1, 9, 4096, 1_000_001])
+@pytest.mark.parametrize("n", [0, 1, 9, 4096, 1_000_001, 20_000_003])
 @pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
 def test_column_stats_and_run_bounds(gpu_device, n, dtype):
     from igloo_amd.ops import hashing as H
