@@ -246,8 +246,9 @@ class CachedTable(TableSource):
             return None
         kept = set(keep)
         ranges, pos = [], 0
+        nrows = src.group_rows() if hasattr(src, "group_rows") else None
         for fi, rg in groups:
-            n = src._meta[fi].row_group(rg).num_rows
+            n = nrows[(fi, rg)] if nrows is not None else src._meta[fi].row_group(rg).num_rows
             if (fi, rg) in kept:
                 if ranges and ranges[-1][1] == pos:
                     ranges[-1] = (ranges[-1][0], pos + n)
@@ -258,6 +259,13 @@ class CachedTable(TableSource):
             return (0, 0)
         if len(ranges) == 1:
             return ranges[0]
+        if 2 * sum(b - a for a, b in ranges) > pos:
+            # most rows survive in several runs: gathering every scanned column
+            # costs more than letting the filter kernel read them all (and the
+            # resident columns keep their derived structures: sortedness,
+            # indexes)
+            self.last_prune_stats["gathered"] = False
+            return None
         key = (tuple(ranges), str(ctx.device) if ctx is not None else "cpu")
         idx = self._ranges_cache.get(key)
         if idx is None:

@@ -103,6 +103,7 @@ class ParquetTable(TableSource):
         self._fields = [Field(f.name, T.from_arrow_type(f.type), f.nullable) for f in schema]
         self._stat_version = _file_version(self.files)
         self._gpu_reader = None
+        self._bounds: Dict[str, Dict[Tuple[int, int], object]] = {}   # column -> row group -> bounds
 
     def schema(self) -> List[Field]:
         return self._fields
@@ -141,13 +142,30 @@ class ParquetTable(TableSource):
         ``filters``: [(column name, op, [values])] with op in = < <= > >= in."""
         if not filters or not groups:
             return groups
-        keep = []
-        for fi, rg in groups:
-            m = self._meta[fi]
-            g = m.row_group(rg)
-            if not any(_refuted(g, m, f) for f in filters):
-                keep.append((fi, rg))
-        return keep
+        # decoded footer bounds per column, built once per metadata version:
+        # a filter set the engine has not seen (new substitution parameters)
+        # costs one comparison per row group, not a walk over footer objects
+        checks = [(self._column_bounds(name), op, values) for name, op, values in filters]
+        return [g for g in groups if not any(_bounds_refute(b.get(g), op, values) for b, op, values in checks)]
+
+    def group_rows(self) -> Dict[Tuple[int, int], int]:
+        """Row count of every (file, row group), kept per metadata version."""
+        r = self._bounds.get("\0rows")
+        if r is None:
+            r = self._bounds["\0rows"] = {(fi, rg): m.row_group(rg).num_rows
+                                          for fi, m in enumerate(self._meta) for rg in range(m.num_row_groups)}
+        return r
+
+    def _column_bounds(self, name: str) -> Dict[Tuple[int, int], object]:
+        b = self._bounds.get(name)
+        if b is None:
+            b = {}
+            for fi, m in enumerate(self._meta):
+                idx = _leaf_index(m, name)
+                for rg in range(m.num_row_groups):
+                    b[(fi, rg)] = _group_bounds(m, m.row_group(rg), idx)
+            self._bounds[name] = b
+        return b
 
     # ------------------------------------------------------------- scan
     def scan_morsels(self, columns: Sequence[str], ctx, filters=None, max_rows: int = 1 << 20):
@@ -238,27 +256,44 @@ def _stat_value(raw, phys: str, dec_scale: Optional[int]) -> Optional[object]:
     return v
 
 
-def _refuted(g, m, f) -> bool:
-    """True when row group ``g`` cannot hold a row satisfying ``f``."""
-    name, op, values = f
-    idx = _leaf_index(m, name)
+_ALL_NULL = "all-null"
+
+
+def _group_bounds(m, g, idx):
+    """Row group ``g``'s statistics for leaf column ``idx``: (min, max), the
+    marker _ALL_NULL, or None (no usable statistics)."""
     if idx is None:
-        return False
+        return None
     cm = g.column(idx)
     st = cm.statistics
     if st is None:
-        return False
+        return None
     if st.has_null_count and st.null_count == g.num_rows and g.num_rows > 0:
-        return True     # only NULLs: no comparison can be true
+        return _ALL_NULL
     if not st.has_min_max:
-        return False
+        return None
     sc = m.schema.column(idx)
     lt = sc.logical_type
     scale = sc.scale if lt is not None and lt.type == "DECIMAL" else None
     lo = _stat_value(st.min_raw, cm.physical_type, scale)
     hi = _stat_value(st.max_raw, cm.physical_type, scale)
     if lo is None or hi is None:
+        return None
+    return lo, hi
+
+
+def _refuted(g, m, f) -> bool:
+    """True when row group ``g`` cannot hold a row satisfying ``f``."""
+    name, op, values = f
+    return _bounds_refute(_group_bounds(m, g, _leaf_index(m, name)), op, values)
+
+
+def _bounds_refute(b, op, values) -> bool:
+    if b is None:
         return False
+    if b is _ALL_NULL:
+        return True     # only NULLs: no comparison can be true
+    lo, hi = b
     try:
         if op == "in":
             return all(v < lo or v > hi for v in values)

@@ -335,7 +335,7 @@ class QueryEngine:
         cs0 = (self.cache.stats["hits"], self.cache.stats["misses"])
         gpu = self.device.type == "cuda"
         if gpu:
-            # per-query HBM high-water mark and device time (one event pair;
+            # per-query HBM high-water mark and device-side span (one event pair;
             # the result readback below already synchronises the stream)
             torch.cuda.reset_peak_memory_stats(self.device)
             mem0 = torch.cuda.memory_allocated(self.device)
@@ -351,7 +351,7 @@ class QueryEngine:
             ev1.synchronize()
             peak = torch.cuda.max_memory_allocated(self.device)
             self.hbm_peak_bytes = max(self.hbm_peak_bytes, peak)
-            dev_metrics = {"device_ms": round(ev0.elapsed_time(ev1), 3), "hbm_peak_bytes": int(peak),
+            dev_metrics = {"device_span_ms": round(ev0.elapsed_time(ev1), 3), "hbm_peak_bytes": int(peak),
                            "hbm_query_bytes": int(max(0, peak - mem0))}
         hits, misses = self.cache.stats["hits"] - cs0[0], self.cache.stats["misses"] - cs0[1]
         if st is not None and spec in ("replayed", "recorded") and st["capture_next"]:
