@@ -306,24 +306,42 @@ def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = 
     or None when the key span is too sparse. Remembered on the tensor object
     (resident table columns build it once)."""
     hit = getattr(big, "_igloo_dense", None)
-    if hit or not build or (hit is False and queries is None):
+    resident = getattr(big, "_igloo_resident", False)
+    if hit or (hit is False and (queries is None or resident)):
         return hit or None
+    if resident:
+        # built once and kept with the resident column: every later lookup
+        # reuses it, so only its size matters, not this call's lookup count
+        # (lineitem.l_orderkey at SF100: 2.4 GB of int32 for 600M rows)
+        if queries is None or queries < DENSE_RESIDENT_MIN_QUERIES:
+            return None
+        with unlogged():
+            return _dense_index_build(big, None, resident=True)
+    if not build:
+        return None
     rng = getattr(big, "_igloo_range", None)
     if hit is False and rng is not None and rng[1] - rng[0] + 1 > _dense_limit(big.numel(), queries):
         return None           # still too sparse for this many lookups: nothing to build
-    if not getattr(big, "_igloo_resident", False):
-        return _dense_index_build(big, queries)    # an intermediate: built (and read back) every execution
-    with unlogged():          # built once per resident column tensor
-        return _dense_index_build(big, queries)
+    return _dense_index_build(big, queries)    # an intermediate: built (and read back) every execution
 
 
-def _dense_limit(nb: int, queries: Optional[int]) -> int:
+#: resident columns: lookups per call that justify building the table once,
+#: and the largest table (entries) worth its HBM when the keys are sparser
+#: than DENSE_INDEX_MAX_SPAN_RATIO (a hash-partitioned rank's slice of a fact
+#: table keeps the whole key span)
+DENSE_RESIDENT_MIN_QUERIES = 4096
+DENSE_RESIDENT_MAX_ENTRIES = 1 << 30
+
+
+def _dense_limit(nb: int, queries: Optional[int], resident: bool = False) -> int:
     """Largest key span worth a table: small next to both the indexed rows and
-    the lookups it serves."""
+    the lookups it serves (resident columns: next to the rows, or 4 GiB)."""
+    if resident:
+        return max(DENSE_INDEX_MAX_SPAN_RATIO * nb, DENSE_RESIDENT_MAX_ENTRIES) + 4096
     return DENSE_INDEX_MAX_SPAN_RATIO * min(nb, queries if queries is not None else nb) + 4096
 
 
-def _dense_index_build(big: torch.Tensor, queries: Optional[int]):
+def _dense_index_build(big: torch.Tensor, queries: Optional[int], resident: bool = False):
     nb = big.numel()
     idx = False
     if nb:
@@ -336,7 +354,7 @@ def _dense_index_build(big: torch.Tensor, queries: Optional[int]):
                 pass
         kmin, kmax = rng
         span = kmax - kmin + 1
-        if span <= _dense_limit(nb, queries):
+        if span <= _dense_limit(nb, queries, resident):
             it = torch.int64 if nb >= INT32_MAX else torch.int32
             first = torch.empty(span + 1, dtype=it, device=big.device)
             gap = torch.zeros(1, dtype=torch.int32, device=big.device)

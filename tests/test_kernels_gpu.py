@@ -484,11 +484,19 @@ def test_sorted_ranges_with_search_fence():
     k = np.sort(np.concatenate([r.integers(0, 2_000_000, n - 3000), np.full(3000, 777_777)])).astype(np.int32)
     big = torch.from_numpy(k).to("cuda:0")
     big._igloo_resident = True
+    big._igloo_dense = False        # no dense table: the fenced binary search
     q = np.concatenate([r.integers(-10, 2_000_010, 200_000), [777_777, k[0], k[-1], -5, 3_000_000]]).astype(np.int32)
     lo, cnt = H.sorted_ranges(big, torch.from_numpy(q).to("cuda:0"))
     assert getattr(big, "_igloo_fence", None) is not None
     want_lo = np.searchsorted(k, q, side="left")
     want_cnt = np.searchsorted(k, q, side="right") - want_lo
+    # a resident column without that memo builds its dense lower-bound table
+    big2 = torch.from_numpy(k).to("cuda:0")
+    big2._igloo_resident = True
+    lo2, cnt2 = H.sorted_ranges(big2, torch.from_numpy(q).to("cuda:0"))
+    assert getattr(big2, "_igloo_dense", None)
+    hit = want_cnt > 0
+    assert (cnt2.cpu().numpy() == want_cnt).all() and (lo2.cpu().numpy()[hit] == want_lo[hit]).all()
     got_cnt = cnt.cpu().numpy()
     got_lo = lo.cpu().numpy()
     assert (got_cnt == want_cnt).all()
