@@ -425,6 +425,17 @@ PYBIND11_MODULE(_native, m) {
                    P<void>(std::get<4>(t)), P<void>(std::get<5>(t))});
     kern::agg_update(P<const int32_t>(gid), n, ngroups, d.data(), (int)d.size(), S(s), sorted_gids);
   }, py::arg("gid"), py::arg("n"), py::arg("ngroups"), py::arg("descs"), py::arg("s"), py::arg("sorted_gids") = false);
+  m.def("sorted_having", [](uintptr_t keys, bool key64, int64_t n,
+                            const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t>>& descs,
+                            int hagg, int hop, long long hlo, long long hhi, double hf, uintptr_t rep, int64_t cap,
+                            uintptr_t counter, uintptr_t s) {
+    std::vector<kern::AggDesc> d;
+    for (auto& t : descs)
+      d.push_back({std::get<0>(t), std::get<1>(t), P<const void>(std::get<2>(t)), P<const uint8_t>(std::get<3>(t)),
+                   P<void>(std::get<4>(t)), P<void>(std::get<5>(t))});
+    kern::sorted_having(P<const void>(keys), key64, n, d.data(), (int)d.size(), hagg, hop, hlo, hhi, hf,
+                        P<int64_t>(rep), cap, P<unsigned long long>(counter), S(s));
+  });
   m.def("fill_runs", [](uintptr_t starts, bool starts64, int64_t nruns, int64_t n, uintptr_t gid, uintptr_t s) {
     kern::fill_runs(P<const void>(starts), starts64, nruns, n, P<int32_t>(gid), S(s));
   });

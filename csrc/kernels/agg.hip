@@ -515,6 +515,213 @@ __global__ __launch_bounds__(kBlock) void agg_single_kernel(int64_t n, AggParams
     if (k < p.nagg) wave_merge(p.d[k], lo[k], hi[k]);
 }
 
+
+// ---- sorted GROUP BY key HAVING <aggregate> <cmp> <constant>, fused --------
+// TPC-H Q18's "l_orderkey IN (SELECT l_orderkey FROM lineitem GROUP BY
+// l_orderkey HAVING sum(l_quantity) > 300)": lineitem is clustered by
+// l_orderkey, 600M rows form 150M runs of which ~6.5K pass. The general path
+// materialises run ids, 150M 128-bit partial states, and compacts them; here
+// each lane owns the runs that START among its 8 rows (vector loads), folds
+// them in registers, follows its last run past its chunk with cache-hot
+// scalar loads (at most kHavingMaxRun rows, else the overflow flag sends the
+// host to the general path), and only the passing runs are written: a lane
+// counts its passing runs, the wave takes one atomic for all of them, and a
+// second walk over the same registers writes them. Output order depends on
+// the atomics; the host sorts the (small) result by run start row.
+constexpr int kHavingMaxAggs = 4;
+constexpr int64_t kHavingMaxRun = 256;
+
+struct HavingParams {
+  int nagg;
+  AggDesc d[kHavingMaxAggs];
+  int hagg, hop;   // compared aggregate; 0 '=', 1 '<>', 2 '<', 3 '<=', 4 '>', 5 '>='
+  long long hlo, hhi;  // integer constant as int128 (units of the aggregate's state)
+  double hf;           // constant for f64 aggregates
+};
+
+__device__ inline bool having_ok(const HavingParams& p, unsigned long long lo, long long hi) {
+  const int op = p.d[p.hagg].op;
+  int c;
+  if (op == AGG_SUM_F64 || op == AGG_MIN_F64 || op == AGG_MAX_F64) {
+    double x;
+    if (op == AGG_SUM_F64) __builtin_memcpy(&x, &lo, 8);
+    else x = ordered_to_f64((long long)lo);
+    if (x != x) return false;   // NaN compares false
+    c = x < p.hf ? -1 : (x > p.hf ? 1 : 0);
+  } else {
+    const long long h = op == AGG_SUM_INT ? hi : ((long long)lo < 0 ? -1LL : 0LL);
+    if (h != p.hhi) c = h < p.hhi ? -1 : 1;
+    else c = lo < (unsigned long long)p.hlo ? -1 : (lo > (unsigned long long)p.hlo ? 1 : 0);
+  }
+  switch (p.hop) {
+    case 0: return c == 0;
+    case 1: return c != 0;
+    case 2: return c < 0;
+    case 3: return c <= 0;
+    case 4: return c > 0;
+    default: return c >= 0;
+  }
+}
+
+// one row of aggregate a from global memory (overhang rows)
+__device__ inline bool row_value(const AggDesc& a, int64_t i, unsigned long long* v) {
+  if (a.valid && !a.valid[i]) return false;
+  if (a.op == AGG_COUNT) {
+    *v = 1;
+  } else if (a.op == AGG_SUM_F64 || a.op == AGG_MIN_F64 || a.op == AGG_MAX_F64) {
+    const double d = ((const double*)a.src)[i];
+    if (a.op == AGG_SUM_F64) __builtin_memcpy(v, &d, 8);
+    else *v = (unsigned long long)f64_to_ordered(d);
+  } else {
+    *v = a.src64 ? (unsigned long long)((const int64_t*)a.src)[i]
+                 : (unsigned long long)(long long)((const int32_t*)a.src)[i];
+  }
+  return true;
+}
+
+__device__ inline void fold(int op, unsigned long long* lo, long long* hi, unsigned long long x) {
+  seg_combine(op, lo, hi, x, op == AGG_SUM_INT && (long long)x < 0 ? -1LL : 0LL);
+}
+
+// The runs starting among a lane's 8 rows, folded for ONE aggregate: emit(j,
+// lo, hi) for the run starting at row r0 + j. The last run is followed past
+// the chunk (4 rows per round trip) while the key repeats, for at most
+// kHavingMaxRun rows (*overflow set beyond).
+template <typename K, typename Emit>
+__device__ inline void fold_runs(const AggDesc& a, const K* __restrict__ keys, int64_t n, int64_t r0,
+                                 const K (&k)[kSortedRows], unsigned starts, bool* overflow, bool wave_converged,
+                                 Emit emit) {
+  unsigned long long v[kSortedRows];
+  const unsigned ok = load_vals8(a, r0, n, v);
+  // the next lane's rows (shuffled in while the whole wave is converged): a
+  // run that spills past this lane's chunk usually ends inside them
+  unsigned long long nv[kSortedRows];
+  unsigned nok = 0, nst = 0;
+  if (wave_converged) {
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) nv[j] = __shfl_down(v[j], 1, kWave);
+    nok = __shfl_down(ok, 1, kWave);
+    nst = __shfl_down(starts, 1, kWave);
+  }
+  unsigned long long lo = 0;
+  long long hi = 0;
+  int open = -1;
+#pragma unroll
+  for (int j = 0; j < kSortedRows; ++j) {
+    if ((starts >> j) & 1u) {
+      if (open >= 0) emit(open, lo, hi);
+      open = j;
+      init_state(a.op, &lo, &hi);
+    }
+    if (open >= 0 && ((ok >> j) & 1u)) fold(a.op, &lo, &hi, v[j]);
+  }
+  if (open < 0) return;
+  const K key = k[open];
+  int64_t r = r0 + kSortedRows;
+  bool more = r < n;
+  if (more && wave_converged && lane_id() < kWave - 1) {
+    // rows of the next lane up to its first run start
+    const int64_t live = n - r < kSortedRows ? n - r : kSortedRows;
+    const int c = nst ? __builtin_ctz(nst) : kSortedRows;
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j)
+      if (j < c && j < live && ((nok >> j) & 1u)) fold(a.op, &lo, &hi, nv[j]);
+    more = c == kSortedRows && live == kSortedRows;
+    r += kSortedRows;
+    more = more && r < n;
+  }
+  while (more) {
+    K kk[4];
+    unsigned long long x[4];
+    bool xv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool in = r + q < n;
+      kk[q] = in ? keys[r + q] : key;
+      xv[q] = in && row_value(a, r + q, &x[q]);
+      if (!in) kk[q] = (K)(key + 1);   // past the end: the run stops there
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!more) break;
+      if (kk[q] != key) {
+        more = false;
+        break;
+      }
+      if (xv[q]) fold(a.op, &lo, &hi, x[q]);
+    }
+    r += 4;
+    if (more && r - (r0 + open) >= kHavingMaxRun) {
+      *overflow = true;
+      more = false;
+    }
+  }
+  emit(open, lo, hi);
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void sorted_having_kernel(const K* __restrict__ keys, int64_t n, HavingParams p,
+                                                              int64_t* __restrict__ rep, int64_t cap,
+                                                              unsigned long long* __restrict__ counter) {
+  const int lane = lane_id();
+  const int64_t wave_id = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  constexpr int64_t kTileRows = (int64_t)kWave * kSortedRows;
+  bool overflow = false;
+  for (int64_t base = wave_id * kTileRows; base < n; base += nwaves * kTileRows) {
+    const int64_t r0 = base + (int64_t)lane * kSortedRows;
+    K k[kSortedRows];
+    if (r0 + kSortedRows <= n && sizeof(K) == 4 && ((uintptr_t)(keys + r0) & 15) == 0) {
+      const int4 a = *(const int4*)(keys + r0), b = *(const int4*)(keys + r0 + 4);
+      k[0] = (K)a.x; k[1] = (K)a.y; k[2] = (K)a.z; k[3] = (K)a.w;
+      k[4] = (K)b.x; k[5] = (K)b.y; k[6] = (K)b.z; k[7] = (K)b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) k[j] = r0 + j < n ? keys[r0 + j] : (K)0;
+    }
+    const K kprev = (r0 < n && r0 > 0) ? keys[r0 - 1] : (K)0;
+    unsigned starts = 0;
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) {
+      const bool st = r0 + j < n && (r0 + j == 0 || k[j] != (j ? k[j - 1] : kprev));
+      starts |= st ? (1u << j) : 0u;
+    }
+    // pass 0: the HAVING aggregate alone decides which runs pass
+    unsigned passmask = 0;
+    fold_runs(p.d[p.hagg], keys, n, r0, k, starts, &overflow, true, [&](int j, unsigned long long lo, long long hi) {
+      if (having_ok(p, lo, hi)) passmask |= 1u << j;
+    });
+    const int npass = __popc(passmask);
+    const int64_t inc = wave_inclusive_scan((int64_t)npass);
+    const int64_t total = __shfl(inc, kWave - 1, kWave);
+    if (total == 0) continue;
+    // one atomic per wave for its passing runs; pass 1 writes them
+    unsigned long long wbase = 0;
+    if (lane == kWave - 1) wbase = atomicAdd(&counter[0], (unsigned long long)total);
+    wbase = __shfl(wbase, kWave - 1, kWave);
+    const int64_t slot0 = (int64_t)wbase + inc - npass;
+    if (!passmask) continue;
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j)
+      if ((passmask >> j) & 1u) {
+        const int64_t o = slot0 + __popc(passmask & ((1u << j) - 1u));
+        if (o < cap) rep[o] = r0 + j;
+      }
+    for (int a = 0; a < p.nagg; ++a) {
+      const AggDesc& d = p.d[a];
+      bool ovf2 = false;
+      fold_runs(d, keys, n, r0, k, starts, &ovf2, false, [&](int j, unsigned long long lo, long long hi) {
+        if (!((passmask >> j) & 1u)) return;
+        const int64_t o = slot0 + __popc(passmask & ((1u << j) - 1u));
+        if (o < cap) {
+          ((unsigned long long*)d.dst)[o] = lo;
+          if (d.dst2) ((long long*)d.dst2)[o] = hi;
+        }
+      });
+    }
+  }
+  if (__any(overflow) && lane == 0) atomicOr(&counter[1], 1ULL);
+}
 }  // namespace
 
 // IGLOO_AGG_SORTED_ROWS=1 selects the one-row-per-lane sorted kernel (A/B)
@@ -530,6 +737,28 @@ int agg_lds_max_groups(int nagg) {
   // keep the LDS state at <= 64 KiB so several workgroups stay resident per CU
   const int bytes = 64 * 1024;
   return nagg > 0 ? bytes / (16 * nagg) : 0;
+}
+
+void sorted_having(const void* keys, bool key64, int64_t n, const AggDesc* descs, int nagg, int hagg, int hop,
+                   long long hlo, long long hhi, double hf, int64_t* rep, int64_t cap, unsigned long long* counter,
+                   hipStream_t stream) {
+  if (n <= 0) return;
+  if (nagg < 1 || nagg > kHavingMaxAggs || hagg < 0 || hagg >= nagg)
+    throw std::runtime_error("sorted_having: 1..4 aggregates, compared one among them");
+  HavingParams p{};
+  p.nagg = nagg;
+  for (int k = 0; k < nagg; ++k) p.d[k] = descs[k];
+  p.hagg = hagg;
+  p.hop = hop;
+  p.hlo = hlo;
+  p.hhi = hhi;
+  p.hf = hf;
+  const dim3 g(grid_for(n, kBlock * kSortedRows, 32768)), b(kBlock);
+  if (key64)
+    hipLaunchKernelGGL(sorted_having_kernel<int64_t>, g, b, 0, stream, (const int64_t*)keys, n, p, rep, cap, counter);
+  else
+    hipLaunchKernelGGL(sorted_having_kernel<int32_t>, g, b, 0, stream, (const int32_t*)keys, n, p, rep, cap, counter);
+  check_launch("sorted_having", stream);
 }
 
 void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream,

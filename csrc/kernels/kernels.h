@@ -198,6 +198,13 @@ struct AggDesc {
 };
 
 int agg_lds_max_groups(int nagg);
+// sorted keys: GROUP BY key HAVING descs[hagg] <hop> constant, fused (agg.hip):
+// passing runs -> rep[] (run start rows, unordered), descs[k].dst/dst2 [slot];
+// counter[0] = runs written (may exceed cap), counter[1] = 1 when a run was
+// longer than the kernel follows (caller falls back). hop: = <> < <= > >=
+void sorted_having(const void* keys, bool key64, int64_t n, const AggDesc* descs, int nagg, int hagg, int hop,
+                   long long hlo, long long hhi, double hf, int64_t* rep, int64_t cap, unsigned long long* counter,
+                   hipStream_t stream);
 // counts[k - kmin] += 1 per valid key in [kmin, kmin + span) (int32 counters, zeroed by the caller)
 void key_histogram(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t span,
                    int32_t* counts, hipStream_t stream);

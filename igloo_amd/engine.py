@@ -614,7 +614,12 @@ class QueryEngine:
     def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:
         ctx = ctx or self.make_context()
         node = create_physical_plan(plan)
-        out = node.execute(ctx)
+        from .ops import hashing as _H
+        tok = _H.TABLE_BYTES_LIMIT.set(ctx.budget // 4 if ctx.budget else None)
+        try:
+            out = node.execute(ctx)
+        finally:
+            _H.TABLE_BYTES_LIMIT.reset(tok)
         if self.comm is not None and self.comm.spmd:
             from .parallel.exchange import gather_all
             out = gather_all(out, ctx)

@@ -19,9 +19,11 @@ reference's ExecutionPlan implementations and DataFusion's inherited ones
 """
 from __future__ import annotations
 
+import math
 import os
 import re
 import time
+from fractions import Fraction
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -459,6 +461,8 @@ class FilterExec(ExecNode):
     def __init__(self, logical: L.Filter, child: ExecNode):
         self.logical = logical
         self.children = [child]
+        if isinstance(child, HashAggExec):
+            child.having = logical.pred     # HAVING: the aggregate may apply it while grouping
 
     def describe(self):
         return self.logical.pred.sql()
@@ -908,6 +912,9 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
 
 #: big side of a join at least this large is checked for a sorted key column
 SORTED_JOIN_MIN_ROWS = 1 << 22
+#: HashAggExec._sorted_having: fused sorted GROUP BY + HAVING (IGLOO_SORTED_HAVING=0 turns it off)
+SORTED_HAVING = os.environ.get("IGLOO_SORTED_HAVING", "1") != "0"
+SORTED_HAVING_MIN_ROWS = 1 << 16
 
 
 def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residual, ctx) -> Optional[Batch]:
@@ -1838,6 +1845,87 @@ class HashAggExec(ExecNode):
         self.logical = logical
         self.children = [child]
         self.runtime_filters: list = []  # (group expr, key column) set by a parent join
+        self.having = None               # predicate of a parent FilterExec (HAVING)
+
+    def _sorted_having(self, ctx) -> Optional[Batch]:
+        """GROUP BY a sorted key column HAVING <aggregate> <cmp> <constant> as
+        one fused pass (ops/agg.py sorted_having): only the passing groups are
+        materialised (TPC-H Q18: 6.5K of 150M l_orderkey groups at SF100). The
+        parent FilterExec still applies the predicate to them (NULL groups).
+        None when the shape does not apply (the general path runs)."""
+        lg, pred = self.logical, self.having
+        if (pred is None or ctx.device.type != "cuda" or ctx.spmd or ctx.budget is not None or self.runtime_filters
+                or not SORTED_HAVING or len(lg.groups) != 1 or not 1 <= len(lg.aggs) <= 4
+                or not isinstance(lg.groups[0][1], ColRef) or not isinstance(pred, BinOp)):
+            return None
+        if any(a.func not in ("sum", "count", "min", "max") or a.distinct or a.filter is not None for _, a in lg.aggs):
+            return None
+        flip = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
+        if pred.op not in flip:
+            return None
+        agg_cids = {ci.cid: i for i, (ci, _) in enumerate(lg.aggs)}
+        if isinstance(pred.left, ColRef) and pred.left.cid in agg_cids and isinstance(pred.right, Lit):
+            ref, lit, op = pred.left, pred.right, pred.op
+        elif isinstance(pred.right, ColRef) and pred.right.cid in agg_cids and isinstance(pred.left, Lit):
+            ref, lit, op = pred.right, pred.left, flip[pred.op]
+        else:
+            return None
+        if lit.value is None or not (lit.dtype.is_integer or lit.dtype.is_decimal or lit.dtype.is_float):
+            return None
+        if any(a.func in ("min", "max") and a.arg is not None and a.arg.dtype.is_string for _, a in lg.aggs):
+            return None
+        # an unfiltered scan whose group key column is sorted (decided before
+        # running anything, so every other aggregate path stays available)
+        child = self.children[0]
+        if not isinstance(child, ScanExec) or child.predicate is not None:
+            return None
+        gci, gexpr = lg.groups[0]
+        raw = child.scan_raw(ctx)
+        kc = raw.columns.get(gexpr.cid) if hasattr(raw, "columns") else None
+        if kc is None or kc.valid is not None or kc.data.dtype not in (torch.int32, torch.int64) \
+                or kc.data.dim() != 1 or kc.dtype.is_string or raw.num_rows < SORTED_HAVING_MIN_ROWS \
+                or not H.is_sorted(kc.data):
+            return None
+        b = child.finish(raw, ctx)
+        n = b.num_rows
+        kcol = ctx.evaluator.column(gexpr, b)
+        if kcol.data.data_ptr() != kc.data.data_ptr() or n != raw.num_rows:
+            return self._finish_general(b, ctx)
+        specs, finals, vidx = [], [], {}
+        for i, (ci, a) in enumerate(lg.aggs):
+            _plan_agg(ci, a, b, None, 1, n, ctx, specs, finals)
+            vidx[i] = len(specs) - 1          # the aggregate's value spec (sum/min/max/count)
+        if len(specs) > 4:
+            return self._finish_general(b, ctx)
+        hidx = vidx[agg_cids[ref.cid]]
+        hop_spec = specs[hidx][0]
+        a = lg.aggs[agg_cids[ref.cid]][1]
+        src = a.arg.dtype if a.arg is not None else T.INT64
+        lv = Fraction(lit.value, 10 ** lit.dtype.scale) if lit.dtype.is_decimal else Fraction(lit.value)
+        if hop_spec in ("sum_f64", "min_f64", "max_f64"):
+            const = float(lv)
+        else:
+            thr = lv * 10 ** (src.scale if (src.is_decimal and a.func != "count") else 0)
+            if thr.denominator != 1:
+                if op in ("=", "<>"):
+                    return self._finish_general(b, ctx)
+                # integral states: x > 2.5 <=> x > 2; x >= 2.5 <=> x >= 3; x < 2.5 <=> x < 3; x <= 2.5 <=> x <= 2
+                thr = math.floor(thr) if op in (">", "<=") else math.ceil(thr)
+            const = int(thr)
+        with ctx.span("agg.sorted_having"):
+            got = A.sorted_having(kcol.data, [sp[:3] for sp in specs], hidx, op, const)
+        if got is None:
+            return self._finish_general(b, ctx)
+        rep, results = got
+        out = {gci.cid: take(kcol, rep)}
+        for fin in finals:
+            ci, col = fin(results)
+            out[ci.cid] = col
+        return Batch(out, rep.numel())
+
+    def _finish_general(self, b, ctx) -> Batch:
+        lg = self.logical
+        return aggregate(lg.groups, lg.aggs, b, ctx)
 
     def describe(self):
         a = self.logical
@@ -1982,6 +2070,11 @@ class HashAggExec(ExecNode):
     def _run(self, ctx):
         lg = self.logical
         child = self.children[0]
+        if self.having is not None and not ctx.spmd and ctx.budget is None and ctx.device.type == "cuda" \
+                and not self.runtime_filters:
+            out = self._sorted_having(ctx)
+            if out is not None:
+                return out
         if ctx.budget is not None:
             from .morsel import streamed_aggregate
             out = streamed_aggregate(self, ctx)

@@ -204,3 +204,63 @@ def _key_histogram_partitioned(keys: torch.Tensor, kmin: int, span: int, valid: 
     N.key_histogram_partitioned(ptr(keys), k64, vp, n, kmin, span, 1, 0, ptr(off), total, ptr(part), 0, st)
     N.key_histogram_partitioned(ptr(keys), k64, vp, n, kmin, span, 2, 0, ptr(off), total, ptr(part), ptr(counts), st)
     return counts.to(torch.int64)
+
+
+HAVING_OPS = {"=": 0, "<>": 1, "<": 2, "<=": 3, ">": 4, ">=": 5}
+
+
+def sorted_having(keys: torch.Tensor, specs: Sequence[Spec], hidx: int, hop: str, hconst) -> Optional[Tuple[
+        torch.Tensor, List[torch.Tensor]]]:
+    """GROUP BY sorted ``keys`` HAVING specs[hidx] <hop> hconst in one pass
+    (csrc/kernels/agg.hip sorted_having): (run start rows of the passing
+    groups in row order, per-spec results for them), or None when a run is
+    longer than the kernel follows or too many groups pass (the caller takes
+    the general path). ``hconst``: int in the aggregate's raw units, or float
+    for f64 aggregates."""
+    from .sort import argsort
+    n = keys.numel()
+    dev = keys.device
+    cap = n // 64 + 4096
+    descs, posts = [], []
+    for op, vals, valid in specs:
+        dst = torch.empty(cap, dtype=torch.float64 if op == "sum_f64" else torch.int64, device=dev)
+        dst2 = torch.empty(cap, dtype=torch.int64, device=dev) if op == "sum_int" else None
+        src64 = 1
+        if vals is not None:
+            assert vals.numel() == n and vals.is_contiguous()
+            if op in ("sum_int", "min_int", "max_int"):
+                src64 = 1 if vals.dtype == torch.int64 else 0
+        descs.append((OPS[op], src64, ptr(vals), ptr(valid), ptr(dst), ptr(dst2)))
+        posts.append((op, dst, dst2))
+    c = int(hconst) if not isinstance(hconst, float) else 0
+    lo = ((c + 2**64) % 2**64) - (2**64 if ((c + 2**64) % 2**64) >= 2**63 else 0)
+    hi = c >> 64
+    if not (I64_MIN <= hi <= I64_MAX):
+        return None
+    rep = torch.empty(cap, dtype=torch.int64, device=dev)
+    counter = torch.zeros(2, dtype=torch.int64, device=dev)
+    launch("sorted_having").sorted_having(ptr(keys.contiguous()), keys.dtype == torch.int64, n, descs, hidx,
+                                          HAVING_OPS[hop], lo, hi, float(hconst), ptr(rep), cap, ptr(counter),
+                                          stream(keys))
+    m, overflow = to_host_ints(counter)
+    if overflow or m > cap:
+        return None
+    perm = argsort([(rep[:m], False, False, None)], m, dev) if m > 1 else torch.arange(m, device=dev)
+    rep = rep[:m].index_select(0, perm.long())
+    outs = []
+    wide = [(dst[:m].index_select(0, perm.long()), dst2[:m].index_select(0, perm.long()))
+            for op, dst, dst2 in posts if op == "sum_int"]
+    fits = iter([1 - f for f in to_host_ints(_wide_flags(wide))] if wide and m else [1] * len(wide))
+    witer = iter(wide)
+    for op, dst, dst2 in posts:
+        if op == "sum_int":
+            lo_, hi_ = next(witer)
+            outs.append(lo_ if next(fits) else torch.stack([lo_, hi_], dim=1))
+            continue
+        d = dst[:m].index_select(0, perm.long())
+        if op in ("min_f64", "max_f64"):
+            sentinel = I64_MAX if op == "min_f64" else I64_MIN
+            inf = float("inf") if op == "min_f64" else float("-inf")
+            d = torch.where(d == sentinel, torch.full_like(d, 0).double() + inf, _ordered_to_f64(d))
+        outs.append(d)
+    return rep, outs

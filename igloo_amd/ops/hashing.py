@@ -9,6 +9,7 @@ CPU tensors use a sort + searchsorted reference implementation.
 """
 from __future__ import annotations
 
+import contextvars
 import os
 from typing import List, Optional, Sequence, Tuple
 
@@ -27,6 +28,12 @@ EXACT_BITMAP_MAX_SPAN = 1 << 25   # direct tables up to this key span use an exa
 #: table (one random read per probe) whatever the build size: 2^26 slots is a
 #: 256 MB head array, small next to 288 GB of HBM
 DIRECT_JOIN_MAX_SPAN = 1 << 26
+
+#: bytes one join table may take under an engine device budget (set around a
+#: query's execution by engine.py); None = unbounded. A direct-mapped table is
+#: sized by the key span, not the build rows: a grace partition or a streamed
+#: semi-join build side keeps the whole span of its keys
+TABLE_BYTES_LIMIT: "contextvars.ContextVar[Optional[int]]" = contextvars.ContextVar("igloo_table_bytes", default=None)
 #: first-match probes that only select rows use the two-pass hit-bit kernels
 PROBE_SELECT = os.environ.get("IGLOO_PROBE_SELECT", "1") == "1"
 
@@ -99,7 +106,10 @@ class JoinTable:
             return
         self.kmin, kmax = rng
         span = kmax - self.kmin + 1
-        self.direct = span < 2**31 - 1 and (span <= 4 * n + 4096 or span <= DIRECT_JOIN_MAX_SPAN)
+        lim = TABLE_BYTES_LIMIT.get()
+        # (head + CSR start/count arrays: up to 3 int32 words per slot)
+        wide_ok = span <= DIRECT_JOIN_MAX_SPAN and (lim is None or 12 * span <= lim)
+        self.direct = span < 2**31 - 1 and (span <= 4 * n + 4096 or wide_ok)
         if not self.gpu:
             k = keys if valid is None else torch.where(valid, keys, torch.full_like(keys, kmax + 1) if kmax < 2**62 else keys)
             sk, order = torch.sort(k.to(torch.int64), stable=True)

@@ -78,7 +78,9 @@ def main():
         try:
             got = digest(g.sql(queries.QUERIES[q]).table)
         except Exception as e:  # noqa: BLE001 - report and continue (an OOM under the cap)
+            import traceback
             print(f"Q{q}: FAILED {type(e).__name__}: {str(e)[:300]}", flush=True)
+            print("".join(traceback.format_exc().splitlines(True)[-24:]), flush=True)
             failed.append(q)
             e = None
             continue
