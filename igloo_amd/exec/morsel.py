@@ -124,6 +124,76 @@ def pick_stream_scan(agg, ctx):
     return best
 
 
+#: morsels prepared ahead of the one being processed (IGLOO_MORSEL_PREFETCH=0: serial)
+PREFETCH_DEPTH = int(os.environ.get("IGLOO_MORSEL_PREFETCH", "1"))
+
+
+def prefetched(gen, ctx):
+    """The morsels of ``gen`` with the next ones produced ahead, on a helper
+    thread and a side HIP stream: the host slice / Parquet read, its H2D copy
+    and (Parquet) the page decode of morsel k+1 overlap the operators running
+    on morsel k on the compute stream. Each morsel is handed over behind an
+    event the compute stream waits on, and its tensors are recorded on the
+    compute stream so the caching allocator does not recycle them early.
+    At most PREFETCH_DEPTH morsels wait in the queue (device memory: the
+    current morsel, the queued ones and the one being produced)."""
+    from ..ops._lib import capturing
+    if PREFETCH_DEPTH <= 0 or ctx.device.type != "cuda" or capturing():
+        yield from gen
+        return
+    import queue
+    import threading
+    side = torch.cuda.Stream(device=ctx.device)
+    q: "queue.Queue" = queue.Queue(maxsize=PREFETCH_DEPTH)
+    stop = threading.Event()
+    end = object()
+
+    def work():
+        try:
+            with torch.cuda.device(ctx.device), torch.cuda.stream(side):
+                for b in gen:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    while not stop.is_set():
+                        try:
+                            q.put((b, ev), timeout=0.1)
+                            break
+                        except queue.Full:
+                            continue
+                    if stop.is_set():
+                        return
+        except BaseException as e:  # noqa: BLE001 - re-raised on the consumer side
+            q.put(e)
+        finally:
+            q.put(end)
+
+    t = threading.Thread(target=work, name="igloo-morsel-prefetch", daemon=True)
+    t.start()
+    cur = torch.cuda.current_stream(ctx.device)
+    try:
+        while True:
+            item = q.get()
+            if item is end:
+                break
+            if isinstance(item, BaseException):
+                raise item
+            b, ev = item
+            cur.wait_event(ev)
+            for c in b.columns.values():
+                for x in (c.data, c.valid, c.offsets):
+                    if x is not None and x.is_cuda:
+                        x.record_stream(cur)
+            yield b
+    finally:
+        stop.set()
+        while t.is_alive():
+            try:
+                q.get(timeout=0.1)
+            except queue.Empty:
+                pass
+        t.join()
+
+
 # -------------------------------------------------------------- execution
 def streamed_aggregate(agg, ctx) -> Optional[Batch]:
     """Run aggregate node ``agg`` as a morsel pipeline when the budget calls
@@ -157,7 +227,7 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
     stats["pipelines"] += 1
     try:
         with ctx.span("morsel.pipeline"):
-            for k, raw in enumerate(src.scan_morsels(names, ctx, scan.pushable(), max_rows)):
+            for k, raw in enumerate(prefetched(src.scan_morsels(names, ctx, scan.pushable(), max_rows), ctx)):
                 ctx.morsel = (id(scan), raw, ("morsel", stats["pipelines"], k))
                 stats["morsels"] += 1
                 stats["rows"] += raw.num_rows
@@ -315,7 +385,7 @@ def streamed_scan(scan, ctx) -> Optional[Batch]:
     late, scan.late_ok = scan.late_ok, False
     try:
         with ctx.span("morsel.scan"):
-            for k, raw in enumerate(src.scan_morsels(names, ctx, scan.pushable(), max_rows)):
+            for k, raw in enumerate(prefetched(src.scan_morsels(names, ctx, scan.pushable(), max_rows), ctx)):
                 ctx.morsel = (id(scan), raw, ("morsel", stats["pipelines"], k))
                 stats["morsels"] += 1
                 stats["rows"] += raw.num_rows
@@ -405,7 +475,12 @@ def apply_semi_aggregate(lb: Batch, ab: Batch, spec, ctx) -> Batch:
         else:
             lk, rk, lvalid, rvalid = key_tensors([ev.column(le, lb) for le in spec["lkeys"]],
                                                  [ab.columns[c] for c in spec["kcids"]])
-            first = H.JoinTable(rk, rvalid).probe_first(lk, lvalid)
+            lim = ctx.budget // 4 if ctx.budget else None
+            table_bytes = 12 * (1 << max(1, (2 * rk.numel() - 1).bit_length()))
+            if lim and table_bytes > lim:
+                first = _partitioned_probe_first(lk, lvalid, rk, rvalid, table_bytes, lim)
+            else:
+                first = H.JoinTable(rk, rvalid).probe_first(lk, lvalid)
             hit = first >= 0
             if spec["x"] is not None:
                 x = ev.column(spec["x"], lb)
@@ -421,6 +496,34 @@ def apply_semi_aggregate(lb: Batch, ab: Batch, spec, ctx) -> Batch:
                 hit &= cond
         keep = mask_to_indices(hit if spec["kind"] == "semi" else ~hit)
     return _take_batch(lb, keep)
+
+
+def _partitioned_probe_first(lk, lvalid, rk, rvalid, table_bytes: int, lim: int) -> torch.Tensor:
+    """``JoinTable(rk).probe_first(lk)`` with the table built one hash
+    partition of the keys at a time, each within ``lim`` bytes (a streamed
+    semi-join build side with millions of distinct keys, TPC-H Q21 under a
+    device budget). Returns int64 build-row indices, -1 where absent."""
+    from ..ops import hashing as H
+    from ..ops import misc as M
+    P = 2
+    while table_bytes / P > lim and P < 1024:
+        P *= 2
+    first = torch.full((lk.numel(),), -1, dtype=torch.int64, device=lk.device)
+    rperm, rcounts = M.hash_partition(rk.to(torch.int64).contiguous(), P)
+    lperm, lcounts = M.hash_partition(lk.to(torch.int64).contiguous(), P)
+    ra = la = 0
+    for p in range(P):
+        ri, li = rperm[ra:ra + rcounts[p]].long(), lperm[la:la + lcounts[p]].long()
+        ra += rcounts[p]
+        la += lcounts[p]
+        if ri.numel() == 0 or li.numel() == 0:
+            continue
+        t = H.JoinTable(rk.index_select(0, ri), None if rvalid is None else rvalid.index_select(0, ri))
+        f = t.probe_first(lk.index_select(0, li), None if lvalid is None else lvalid.index_select(0, li)).long()
+        ok = f >= 0
+        first.index_put_((li[ok],), ri.index_select(0, f[ok]))
+        del t
+    return first
 
 
 def aggregated_semi_join(join, ctx) -> Optional[Batch]:
