@@ -75,7 +75,7 @@ SETS
           --eager-steps 0 --vary-params 0 > gpurun_out/profq_$q.log 2>&1
         rc=$?; echo "profq $q rc=$rc"; [ $rc -eq 0 ] || exit $rc
         T=$(find gpurun_out/profq_$q -name "*kernel_trace.csv" | head -1)
-        python3 scripts/kernel_summary.py "$T" --steps 3 --top 25 > gpurun_out/profq_${q}_summary.txt
+        python3 scripts/kernel_summary.py "$T" --steps 3 --top 25 ${KD:+--dispatches "$KD"} > gpurun_out/profq_${q}_summary.txt
         rm -rf gpurun_out/profq_$q; head -8 gpurun_out/profq_${q}_summary.txt
       done ;;
     jitcache)

@@ -24,9 +24,16 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--gap-ms", type=float, default=500.0)
+    ap.add_argument("--dispatches", default=None, metavar="REGEX",
+                    help="also list every dispatch of the matching kernels in the timed steps (us, grid)")
     a = ap.parse_args()
-    rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
-                   for r in csv.DictReader(open(a.trace))), key=lambda x: x[0])
+    grid = {}
+    rows = []
+    for r in csv.DictReader(open(a.trace)):
+        t = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+        rows.append(t)
+        grid[t] = r.get("Grid_Size_X") or r.get("Grid_Size") or "?"
+    rows.sort(key=lambda x: x[0])
     cut = 0
     for i in range(1, len(rows)):
         if rows[i][0] - rows[i - 1][1] > a.gap_ms * 1e6:
@@ -43,6 +50,11 @@ def main():
     print(f"{'ms/step':>9} {'calls':>6} {'us/call':>9}  kernel")
     for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
         print(f"{t / 1e6 / a.steps:9.3f} {cnt[n] // a.steps:6d} {t / 1e3 / cnt[n]:9.1f}  {n}")
+    if a.dispatches:
+        print(f"\ndispatches matching {a.dispatches!r} (all timed steps, in order): us  grid  kernel")
+        for r in rows:
+            if re.search(a.dispatches, r[2]):
+                print(f"{(r[1] - r[0]) / 1e3:9.1f} {grid[r]:>10}  {short(r[2])[:70]}")
 
 
 if __name__ == "__main__":
