@@ -664,6 +664,35 @@ def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
         return
 
 
+def _index_key_filter(pk: torch.Tensor, bk: torch.Tensor, bvalid, ctx) -> Optional[torch.Tensor]:
+    """Rows of the resident unsorted key column ``pk`` whose key is in the
+    small set ``bk``, ascending, through the column's secondary index (the
+    same rule as inner_pairs): only the matching ranges are read instead of
+    probing every row (TPC-H Q17: 20K parts against 600M l_partkey, where the
+    probe fetches an L2 line per row for its bitmap bit). None when it does
+    not apply."""
+    n = pk.numel()
+    if not (ctx.device.type == "cuda" and PERM_INDEX and getattr(pk, "_igloo_resident", False)
+            and n >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * bk.numel() <= n
+            and bk.numel() * (n / _resident_ndv(pk)) * PERM_INDEX_SORT_FRAC <= n):
+        return None
+    keys = (bk if bvalid is None else gather_tensor(bk, mask_to_indices(bvalid))).to(pk.dtype)
+    _, _, rep = H.group_ids(keys)                       # a key set: each matching row once
+    keys = gather_tensor(keys, rep)
+    skeys, perm = H.perm_index(pk)
+    with ctx.span("agg.runtime_filter_index"):
+        lo, cnt = H.sorted_ranges(skeys, keys)
+        scanned = exclusive_scan(cnt)
+        if scanned[1] * PERM_INDEX_SORT_FRAC > n:
+            return None
+        _, pos = H.expand_ranges(lo, cnt, n, scanned)
+        rows = gather_tensor(perm, pos)
+        from ..ops.sort import sort_pairs
+        rows, _ = sort_pairs(rows, rows, max(1, (n - 1).bit_length()))
+    ctx.note_partial_read(pk, scanned[1])
+    return rows
+
+
 def apply_key_filters(b: Batch, filters, ctx) -> Batch:
     for gexpr, lcol in filters:
         with ctx.span("agg.runtime_filter"):
@@ -671,7 +700,9 @@ def apply_key_filters(b: Batch, filters, ctx) -> Batch:
             pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
             if b.num_rows == 0:
                 continue
-            sel, _ = H.JoinTable(bk, bvalid).probe_select(pk, pvalid, want_build=False)
+            sel = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
+            if sel is None:
+                sel, _ = H.JoinTable(bk, bvalid).probe_select(pk, pvalid, want_build=False)
             if sel.numel() < b.num_rows:
                 keys = list(b.columns)
                 b = Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], sel))), sel.numel(), b.dist)
@@ -1125,7 +1156,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
             and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
-            and small.numel() * (big.numel() / _resident_ndv(big)) * PERM_INDEX_MAX_FRAC <= big.numel():
+            and small.numel() * (big.numel() / _resident_ndv(big)) * PERM_INDEX_SORT_FRAC <= big.numel():
         # unsorted resident column, much smaller other side: search its
         # secondary index and touch only the matching rows
         skeys, perm = H.perm_index(big)
@@ -1137,13 +1168,22 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         # for a large result the ordered hash probe output gathers (and
         # probes later sorted joins) far more cheaply, so the index only
         # serves results below 1/PERM_INDEX_MAX_FRAC of the column
-        if total * PERM_INDEX_MAX_FRAC <= big.numel():
+        if total * PERM_INDEX_SORT_FRAC <= big.numel():
             ctx.note_partial_read(big, total)
             with ctx.span("join.index_expand"):
                 sidx, pos = H.expand_ranges(lo, cnt, big.numel(), scanned)
                 bidx = gather_tensor(perm, pos)
                 if bidx.dtype != sidx.dtype:
                     bidx = bidx.to(sidx.dtype)
+            if total * PERM_INDEX_MAX_FRAC > big.numel():
+                # a larger result (Q9: 32.6M of 600M lineitem rows for the
+                # green parts): back into row order with one radix sort of the
+                # pairs, so later gathers and sorted joins read ascending rows
+                # — cheaper than probing all 600M keys (an L2-line fetch per
+                # bitmap lookup)
+                from ..ops.sort import sort_pairs
+                with ctx.span("join.index_sort"):
+                    bidx, sidx = sort_pairs(bidx, sidx, max(1, (big.numel() - 1).bit_length()))
             return (sidx, bidx) if big_right else (bidx, sidx)
     # hash: build on the smaller side, probe with the bigger
     with ctx.span("join.build"):
@@ -1161,6 +1201,9 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
 PERM_INDEX = os.environ.get("IGLOO_PERM_INDEX", "1") == "1"
 PERM_INDEX_RATIO = int(os.environ.get("IGLOO_PERM_INDEX_RATIO", "32"))
 PERM_INDEX_MAX_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_MAX_FRAC", "20"))
+#: results up to 1/PERM_INDEX_SORT_FRAC of the column still take the index,
+#: sorted back into row order (above 1/PERM_INDEX_MAX_FRAC)
+PERM_INDEX_SORT_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_SORT_FRAC", "8"))
 
 _INT_KEYS = ("int32", "int64")
 TWO_KEY_SORTED = os.environ.get("IGLOO_TWO_KEY_SORTED", "1") == "1"
