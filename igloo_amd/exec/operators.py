@@ -679,14 +679,15 @@ def _index_key_filter(pk: torch.Tensor, bk: torch.Tensor, bvalid, ctx) -> Option
     keys = (bk if bvalid is None else gather_tensor(bk, mask_to_indices(bvalid))).to(pk.dtype)
     _, _, rep = H.group_ids(keys)                       # a key set: each matching row once
     keys = gather_tensor(keys, rep)
-    skeys, perm = H.perm_index(pk)
+    srt = H.is_sorted(pk)                              # sorted column: its own index (no permutation)
+    skeys, perm = (pk, None) if srt else H.perm_index(pk)
     with ctx.span("agg.runtime_filter_index"):
         lo, cnt = H.sorted_ranges(skeys, keys)
         scanned = exclusive_scan(cnt)
         if scanned[1] * PERM_INDEX_SORT_FRAC > n:
             return None
         _, pos = H.expand_ranges(lo, cnt, n, scanned)
-        rows = gather_tensor(perm, pos)
+        rows = pos if perm is None else gather_tensor(perm, pos)
         from ..ops.sort import sort_pairs
         rows, _ = sort_pairs(rows, rows, max(1, (n - 1).bit_length()))
     ctx.note_partial_read(pk, scanned[1])
@@ -1455,6 +1456,16 @@ class MultiJoinExec(ExecNode):
         if agg is not None and agg[0] is rb:
             from .morsel import apply_semi_aggregate
             return apply_semi_aggregate(lb, rb, agg[1], ctx)
+        if sp.kind == "semi" and sp.residual is None and not sp.null_aware and len(sp.on) == 1 and not ctx.spmd \
+                and lb.num_rows and rb.num_rows:
+            # a small key set against a big resident column (Q18's 6.5K qualifying
+            # orders against 150M o_orderkey): its index ranges, not a full probe
+            le, re_ = sp.on[0]
+            if isinstance(le, ColRef) and isinstance(re_, ColRef) and le.cid in lb.columns and re_.cid in rb.columns:
+                pk, bk, pvalid, bvalid = key_tensors([ctx.evaluator.column(le, lb)], [ctx.evaluator.column(re_, rb)])
+                rows = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
+                if rows is not None:
+                    return _take_batch(lb, rows)
         if ctx.spmd:
             from ..parallel.exchange import prepare_join, semi_by_key_set
             j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]

@@ -104,3 +104,45 @@ def test_perm_index_default_gating(gpu_device, skewed):
             else:
                 assert "join.index_expand" in ph and "join.probe" not in ph, ph
     assert res["cpu"] == res[gpu_device]
+
+
+def _index_tables(n=(1 << 22) + 50_000, n_small=40_000, seed=13):
+    """A 4.2M-row resident big side whose key column repeats every key 8 times
+    (unsorted: ``bk``; sorted copy: ``ok``) and a small key set."""
+    r = np.random.default_rng(seed)
+    k = r.permutation(np.repeat(np.arange(n // 8 + 1, dtype=np.int64), 8)[:n])
+    big = pa.table({"bk": pa.array(k), "ok": pa.array(np.sort(k)), "bv": pa.array(r.integers(0, 1000, n), pa.int64())})
+    small = pa.table({"sk": pa.array(r.choice(n // 8, n_small, replace=False).astype(np.int64)),
+                      "sw": pa.array(r.integers(1, 5, n_small), pa.int64())})
+    return big, small
+
+
+INDEX_QUERIES = [
+    # inner join, ~7.6 % of the big side: secondary index + sort back into row order
+    ("SELECT count(*) AS c, sum(bv) AS s, sum(bv * sw) AS t FROM small JOIN big ON sk = bk", "join.index_sort"),
+    # correlated aggregate (Q17 shape): the runtime key filter reads the index ranges
+    ("SELECT sum(bv) AS s FROM small, big WHERE bk = sk AND bv < (SELECT avg(b2.bv) FROM big b2 WHERE b2.bk = sk)",
+     None),
+    # semi join of the big side with a small key set (sorted and unsorted key columns)
+    ("SELECT count(*) AS c, sum(bv) AS s FROM big WHERE bk IN (SELECT sk FROM small WHERE sw = 1)", None),
+    ("SELECT count(*) AS c, sum(bv) AS s FROM big WHERE ok IN (SELECT sk FROM small WHERE sw = 1)", None),
+]
+
+
+@pytest.mark.parametrize("qi", range(len(INDEX_QUERIES)))
+def test_index_paths_default_thresholds(gpu_device, qi):
+    """Mid-size secondary-index joins, index-range runtime key filters and
+    semi joins (exec/operators.py inner_pairs, _index_key_filter) with the
+    default thresholds, against the CPU engine."""
+    big, small = _index_tables()
+    sql, phase = INDEX_QUERIES[qi]
+    res = {}
+    for dev in ("cpu", gpu_device):
+        e = ig.QueryEngine(device=dev)
+        e.register_table("big", big)
+        e.register_table("small", small)
+        res[dev] = e.query(sql).to_pylist()
+        if dev != "cpu" and phase:
+            ph = _phases(e, sql)
+            assert phase in ph, ph
+    assert res["cpu"] == res[gpu_device]
