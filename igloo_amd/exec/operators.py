@@ -1136,6 +1136,22 @@ def _resident_ndv(t: torch.Tensor) -> int:
     return d
 
 
+def _dense_lookup_ok(big: torch.Tensor, nq: int) -> bool:
+    """A sorted resident key column whose dense lower-bound table exists (or
+    is built now, once): a lookup is two reads whatever the probe count, so
+    the join needs no hash table even when the other side is not much
+    smaller (TPC-H customer.c_custkey against 5.7M-22.7M filtered orders)."""
+    if not (DENSE_JOIN and getattr(big, "_igloo_resident", False) and nq >= H.DENSE_RESIDENT_MIN_QUERIES):
+        return False
+    if not H.is_sorted(big):
+        return False
+    return bool(H.dense_index(big, build=True, queries=nq))
+
+
+#: inner_pairs: sorted resident key columns with a dense index take the range path at any size ratio
+DENSE_JOIN = os.environ.get("IGLOO_DENSE_JOIN", "1") == "1"
+
+
 def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor]:
     """(left row, right row) index pairs of an inner equi-join on packed keys:
     binary search into a sorted big side, else hash build on the smaller side
@@ -1147,8 +1163,8 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         return z, z
     big_right = n_r >= n_l
     big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
-    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS and 4 * small.numel() <= big.numel() \
-            and bvalid is None and H.is_sorted(big):
+    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS and bvalid is None \
+            and (4 * small.numel() <= big.numel() or _dense_lookup_ok(big, small.numel())) and H.is_sorted(big):
         with ctx.span("join.sorted_search"):
             lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
@@ -2252,6 +2268,22 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
     return Batch(out, ng)
 
 
+def _diff_bounds(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Device int64 [min, max] of a - b (both 0 <=> a == b everywhere) from
+    the two-stage column_stats kernel: an ATen ``(a != b).sum()`` is a
+    multi-block reduction whose semaphore memset does not replay inside a HIP
+    graph (the query would never graph)."""
+    d = (a.to(torch.int64) - b.to(torch.int64)).contiguous()
+    if not d.is_cuda:
+        return torch.stack([d.min(), d.max()]) if d.numel() else torch.zeros(2, dtype=torch.int64)
+    N = launch("column_stats")
+    buf = torch.empty(N.STATS_SLOTS, dtype=torch.int64, device=d.device)
+    if d.numel() == 0:
+        return torch.zeros(2, dtype=torch.int64, device=d.device)
+    N.column_stats(ptr(d), True, 0, d.numel(), ptr(buf), stream(d))
+    return buf[:2]
+
+
 def _late_group_keys(groups, b: "LateBatch", ctx):
     """GROUP BY over a join result still in index form, with plain string keys
     (TPC-H Q10: c_custkey plus six customer/nation attributes over 11M joined
@@ -2284,8 +2316,8 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
         if idx is None:
             return None
         parts.add(k)
-        checks.append((idx != idx.index_select(0, rr)).sum())
-    if checks and to_host_int(torch.stack(checks).sum().to(torch.int64)):
+        checks.append(_diff_bounds(idx, gather_tensor(idx, rr)))
+    if checks and any(to_host_ints(torch.cat(checks))):
         return None
     ctx.sorted_gids = srt
     taken = []

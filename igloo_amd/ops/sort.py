@@ -58,6 +58,12 @@ def _fields(keys: Sequence[SortKey]) -> List[tuple]:
             stats.append(torch.zeros(2, dtype=torch.int64, device=v.device))
             continue
         x = v.to(torch.uint8) if v.dtype == torch.bool else v
+        if is_gpu(x) and x.dtype in (torch.int32, torch.int64):
+            # bounds from the hand-written two-stage reduction (util.hip): the
+            # ATen aminmax zeroes its multi-block semaphores with a memset that
+            # does not replay inside a HIP graph, so the query never graphed
+            stats.append(_int_bounds(x))
+            continue
         mn, mx = torch.aminmax(x)
         if x.dtype in (torch.float64, torch.float32):
             stats.append(torch.stack([mn.to(torch.float64), mx.to(torch.float64)]).view(torch.int64))
@@ -86,6 +92,15 @@ def _fields(keys: Sequence[SortKey]) -> List[tuple]:
         out.append((t.contiguous(), None if valid is None else valid.contiguous(), lo & U64, span, kind, width,
                     bits, int(desc), int(nf)))
     return out
+
+
+def _int_bounds(x: torch.Tensor) -> torch.Tensor:
+    """int64 [min, max] of an int32/int64 device column (no host sync)."""
+    N = launch("column_stats")
+    buf = torch.empty(N.STATS_SLOTS, dtype=torch.int64, device=x.device)
+    x = x.contiguous()
+    N.column_stats(ptr(x), x.dtype == torch.int64, 0, x.numel(), ptr(buf), stream(x))
+    return buf[:2]
 
 
 def _groups(fields: List[tuple]) -> List[List[tuple]]:
