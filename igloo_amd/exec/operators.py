@@ -1150,6 +1150,8 @@ def _dense_lookup_ok(big: torch.Tensor, nq: int) -> bool:
 
 #: inner_pairs: sorted resident key columns with a dense index take the range path at any size ratio
 DENSE_JOIN = os.environ.get("IGLOO_DENSE_JOIN", "1") == "1"
+#: ... and the smaller side's sorted resident key column serves the bigger side's lookups
+DENSE_JOIN_SMALL = os.environ.get("IGLOO_DENSE_JOIN_SMALL", "1") == "1"
 
 
 def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -1170,6 +1172,15 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         with ctx.span("join.sorted_expand"):
             sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
         ctx.note_partial_read(big, sidx.numel())
+        return (sidx, bidx) if big_right else (bidx, sidx)
+    if dev.type == "cuda" and DENSE_JOIN_SMALL and svalid is None and small.numel() >= SORTED_JOIN_MIN_ROWS \
+            and _dense_lookup_ok(small, big.numel()):
+        # the smaller side is a sorted resident key column with a dense index
+        # (customer.c_custkey against 22.7M filtered orders in Q5): every row of
+        # the bigger side looks its key up (two reads) — no hash table is built
+        with ctx.span("join.dense_lookup"):
+            lo, cnt = H.sorted_ranges(small, big, bvalid)
+            bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
             and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
@@ -1912,6 +1923,23 @@ def _edges(conds, ca: set, cb: set):
 
 
 # ======================================================================= aggregate
+def having_constant(op: str, lit: Lit, src: T.DataType, func: str, float_state: bool):
+    """The HAVING literal in the units of the aggregate's raw state (fused
+    sorted GROUP BY + HAVING): a float for f64 states; else an int, where a
+    fractional threshold is rounded so that the integer comparison keeps its
+    meaning (x > 2.5 <=> x > 2, x >= 2.5 <=> x >= 3, x < 2.5 <=> x < 3,
+    x <= 2.5 <=> x <= 2). None for = / <> against a fractional value."""
+    lv = Fraction(lit.value, 10 ** lit.dtype.scale) if lit.dtype.is_decimal else Fraction(lit.value)
+    if float_state:
+        return float(lv)
+    thr = lv * 10 ** (src.scale if (src.is_decimal and func != "count") else 0)
+    if thr.denominator != 1:
+        if op in ("=", "<>"):
+            return None
+        thr = math.floor(thr) if op in (">", "<=") else math.ceil(thr)
+    return int(thr)
+
+
 class HashAggExec(ExecNode):
     def __init__(self, logical: L.Aggregate, child: ExecNode):
         self.logical = logical
@@ -1973,17 +2001,9 @@ class HashAggExec(ExecNode):
         hop_spec = specs[hidx][0]
         a = lg.aggs[agg_cids[ref.cid]][1]
         src = a.arg.dtype if a.arg is not None else T.INT64
-        lv = Fraction(lit.value, 10 ** lit.dtype.scale) if lit.dtype.is_decimal else Fraction(lit.value)
-        if hop_spec in ("sum_f64", "min_f64", "max_f64"):
-            const = float(lv)
-        else:
-            thr = lv * 10 ** (src.scale if (src.is_decimal and a.func != "count") else 0)
-            if thr.denominator != 1:
-                if op in ("=", "<>"):
-                    return self._finish_general(b, ctx)
-                # integral states: x > 2.5 <=> x > 2; x >= 2.5 <=> x >= 3; x < 2.5 <=> x < 3; x <= 2.5 <=> x <= 2
-                thr = math.floor(thr) if op in (">", "<=") else math.ceil(thr)
-            const = int(thr)
+        const = having_constant(op, lit, src, a.func, hop_spec in ("sum_f64", "min_f64", "max_f64"))
+        if const is None:
+            return self._finish_general(b, ctx)
         with ctx.span("agg.sorted_having"):
             got = A.sorted_having(kcol.data, [sp[:3] for sp in specs], hidx, op, const)
         if got is None:

@@ -30,3 +30,22 @@ def test_device_metrics_gpu(gpu_device):
     assert m["device_span_ms"] > 0 and m["hbm_peak_bytes"] > 0 and m["hbm_query_bytes"] >= 0
     assert e.hbm_peak_bytes >= m["hbm_peak_bytes"]
     assert m["device_span_ms"] <= m["elapsed_ms"] * 1.5 + 1.0
+
+
+def test_having_constant_units():
+    """exec/operators.py having_constant: the HAVING literal in the raw units
+    of the aggregate state, fractional thresholds rounded per comparison."""
+    from igloo_amd import types as T
+    from igloo_amd.exec.operators import having_constant
+    from igloo_amd.sql.expr import Lit
+    dec2 = T.DataType("decimal", 15, 2)
+    lit = Lit(30000, T.DataType("decimal", 5, 2))          # 300.00
+    assert having_constant(">", lit, dec2, "sum", False) == 30000
+    half = Lit(25, T.DataType("decimal", 2, 1))            # 2.5
+    assert having_constant(">", half, T.INT64, "count", False) == 2
+    assert having_constant(">=", half, T.INT64, "count", False) == 3
+    assert having_constant("<", half, T.INT64, "count", False) == 3
+    assert having_constant("<=", half, T.INT64, "count", False) == 2
+    assert having_constant("=", half, T.INT64, "count", False) is None
+    assert having_constant(">", Lit(3, T.INT64), dec2, "sum", False) == 300
+    assert having_constant("<", Lit(-25.5, T.FLOAT64), T.FLOAT64, "sum", True) == -25.5
