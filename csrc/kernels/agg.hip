@@ -85,7 +85,7 @@ __device__ inline void merge_global(const AggDesc& a, int64_t g, unsigned long l
   unsigned long long* dlo = (unsigned long long*)a.dst + g;
   switch (a.op) {
     case AGG_SUM_INT:
-      if (lo != 0 || hi != 0) atomic_add_i128_parts(dlo, (long long*)a.dst2 + g, lo, hi);
+      if (lo != 0 || hi != 0) atomic_add_i128_parts(dlo, a.dst2 ? (long long*)a.dst2 + g : nullptr, lo, hi);
       break;
     case AGG_SUM_F64: {
       double d;
@@ -207,7 +207,7 @@ __device__ inline void row_state(const AggDesc& a, int64_t i, bool live, unsigne
 
 __device__ inline void store_exclusive(const AggDesc& a, int64_t g, unsigned long long lo, long long hi) {
   ((unsigned long long*)a.dst)[g] = lo;
-  if (a.op == AGG_SUM_INT) ((long long*)a.dst2)[g] = hi;
+  if (a.op == AGG_SUM_INT && a.dst2) ((long long*)a.dst2)[g] = hi;
 }
 
 __global__ __launch_bounds__(kBlock) void agg_sorted_kernel(const int32_t* __restrict__ gid, int64_t n, AggParams p) {

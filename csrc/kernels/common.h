@@ -124,7 +124,13 @@ __host__ __device__ inline double ordered_to_f64(int64_t b) {
 // 128-bit atomic accumulate from two 64-bit atomics. The low word's returned
 // old value tells each adder whether IT produced a carry, so the final
 // (hi, lo) pair is exact regardless of interleaving.
+// hi == nullptr: a narrow (int64) sum whose exact total is known to fit
+// (ops/agg.py checks max|v| * rows): one modular 64-bit add, no carry word.
 __device__ inline void atomic_add_i128(unsigned long long* lo, long long* hi, int64_t v) {
+  if (hi == nullptr) {
+    atomicAdd(lo, (unsigned long long)v);
+    return;
+  }
   unsigned long long ulo = (unsigned long long)v;
   long long vhi = v < 0 ? -1 : 0;
   unsigned long long old = atomicAdd(lo, ulo);
@@ -136,6 +142,10 @@ __device__ inline void atomic_add_i128(unsigned long long* lo, long long* hi, in
 
 __device__ inline void atomic_add_i128_parts(unsigned long long* lo, long long* hi,
                                              unsigned long long ulo, long long vhi) {
+  if (hi == nullptr) {
+    atomicAdd(lo, ulo);
+    return;
+  }
   unsigned long long old = atomicAdd(lo, ulo);
   unsigned long long sum = old + ulo;
   long long carry = sum < old ? 1 : 0;
