@@ -591,6 +591,11 @@ class HashJoinExec(ExecNode):
             if out is not None:
                 return out
         lb = self.children[0].execute(ctx)
+        found = _semi_index_scan(self.children[1], j, ctx)
+        if found is not None:
+            out = _semi_index_then_filter(found, j, lb, ctx)
+            if out is not None:
+                return out
         if j.kind in ("inner", "left", "semi") and j.on and ctx.memo is None:
             # (not inside a morsel pipeline: the build side is computed once
             # for all morsels, so it must not be narrowed to one morsel's keys)
@@ -722,6 +727,89 @@ def _index_then_filter(scan: "ScanExec", raw: Batch, filters, ctx):
             cols = take_many([sub.columns[c] for c in out_cids], keep)
         return Batch(dict(zip(out_cids, cols)), keep.numel(), raw.dist), filters[:i] + filters[i + 1:]
     return None
+
+
+def _semi_index_scan(rnode, j, ctx):
+    """The filtered resident scan under a [NOT] EXISTS build side, for
+    ``_semi_index_then_filter``: (scan, raw batch, key column, output cid ->
+    scan cid) or None. Cheap: resident columns are not filtered here."""
+    if not (SEMI_INDEX and ctx.device.type == "cuda" and not ctx.spmd and ctx.budget is None and ctx.memo is None) \
+            or j.kind not in ("semi", "anti") or j.null_aware or len(j.on) != 1:
+        return None
+    le, re_ = j.on[0]
+    if not isinstance(le, ColRef) or not isinstance(re_, ColRef):
+        return None
+    chain = []
+    while isinstance(rnode, ProjectExec):               # column renames above the scan
+        chain.append(rnode)
+        rnode = rnode.children[0]
+    if not isinstance(rnode, ScanExec) or rnode.predicate is None:
+        return None
+
+    def resolve(cid):
+        for p in chain:
+            src = [e for ci, e in p.logical.exprs if ci.cid == cid]
+            if not src or not isinstance(src[0], ColRef):
+                return None
+            cid = src[0].cid
+        return cid
+    names = {c.cid: resolve(c.cid) for c in (chain[0].logical.schema if chain else rnode.logical.schema)}
+    raw = rnode.scan_raw(ctx)
+    rcol = raw.columns.get(names.get(re_.cid))
+    if rcol is None or rcol.valid is not None or rcol.dtype.is_string or raw.num_rows < SORTED_JOIN_MIN_ROWS \
+            or not getattr(rcol.data, "_igloo_resident", False) or not H.is_sorted(rcol.data):
+        return None
+    if j.residual is not None and any(c not in names or names[c] not in raw.columns
+                                      for c in col_refs(j.residual) if c in names):
+        return None
+    return rnode, raw, rcol, names
+
+
+def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
+    """[NOT] EXISTS against a FILTERED scan of a resident table sorted on
+    the join key, as an index nested loop: each left row's range of the
+    sorted key column (dense lower-bound table or binary search), the scan's
+    filter (and the join's residual) evaluated only on those candidate rows,
+    and a left row kept when some candidate passes (semi) or none does
+    (anti). TPC-H Q4: 5.7M orders against lineitem's commit < receipt filter
+    — 23M candidate rows checked instead of the filter over 600M rows, the
+    compaction and the gather of 385M keys; Q21's NOT EXISTS the same way
+    with its l_suppkey <> residual. None when the size does not apply."""
+    scan, raw, rcol, names = found
+    le = j.on[0][0]
+    n_r, n_l = raw.num_rows, lb.num_rows
+    if le.cid not in lb.columns or n_l == 0 or n_l * 2 > n_r:
+        return None
+    lcol = ctx.evaluator.column(le, lb)
+    if lcol.dtype.is_string:
+        return None
+    pl, pr, lvalid, _ = key_tensors([lcol], [rcol])
+    if pr is not rcol.data:
+        return None
+    with ctx.span("join.index_then_filter"):
+        _dense_lookup_ok(pr, n_l)           # the column's dense table, built once
+        lo, cnt = H.sorted_ranges(pr, pl, lvalid)
+        scanned = exclusive_scan(cnt)
+        if scanned[1] * PERM_INDEX_SORT_FRAC > n_r:
+            return None
+        lidx, pos = H.expand_ranges(lo, cnt, n_r, scanned)
+        keys = list(raw.columns)
+        sub = Batch(dict(zip(keys, take_many([raw.columns[k] for k in keys], pos))), pos.numel(), raw.dist)
+        ok = mask_to_indices(predicate_mask(scan.predicate, sub, ctx))
+        li = gather_tensor(lidx, ok)
+        if j.residual is not None and ok.numel():
+            refs = sorted(col_refs(j.residual))
+            lref = [c for c in refs if c in lb.columns]
+            rref = [c for c in refs if c not in lb.columns]
+            pair = dict(zip(lref, take_many([lb.columns[c] for c in lref], li)))
+            pair.update(zip(rref, take_many([sub.columns[names[c]] for c in rref], ok)))
+            li = gather_tensor(li, mask_to_indices(predicate_mask(j.residual, Batch(pair, ok.numel()), ctx)))
+        mark = torch.zeros(n_l, dtype=torch.bool, device=ctx.device)
+        if li.numel():
+            mark.index_fill_(0, li.long(), True)
+        keep = mask_to_indices(mark if j.kind == "semi" else ~mark)
+    ctx.note_partial_read(rcol.data, scanned[1])
+    return _take_batch(lb, keep)
 
 
 def apply_key_filters(b: Batch, filters, ctx) -> Batch:
@@ -1182,6 +1270,11 @@ def _dense_lookup_ok(big: torch.Tensor, nq: int) -> bool:
 DENSE_JOIN = os.environ.get("IGLOO_DENSE_JOIN", "1") == "1"
 #: HashAggExec: a runtime key filter over a filtered resident scan takes the key index first
 INDEX_THEN_FILTER = os.environ.get("IGLOO_INDEX_THEN_FILTER", "1") == "1"
+#: HashJoinExec: [NOT] EXISTS against a filtered scan sorted on the key runs as an index nested loop
+SEMI_INDEX = os.environ.get("IGLOO_SEMI_INDEX", "1") == "1"
+#: ... also for the semi joins deferred past a multi-way join (off: Q21 10.0 -> 10.8 ms, the residual's pair
+#: gathers cost more than the build-side filter they save; profiles/r3_ab_semi_index.txt)
+SEMI_INDEX_MULTI = os.environ.get("IGLOO_SEMI_INDEX_MULTI", "0") == "1"
 #: ... and the smaller side's sorted resident key column serves the bigger side's lookups
 DENSE_JOIN_SMALL = os.environ.get("IGLOO_DENSE_JOIN_SMALL", "1") == "1"
 
@@ -1482,6 +1575,21 @@ class _LazyScanBatch(Batch):
 LAZY_JOIN_OUTPUT = os.environ.get("IGLOO_LAZY_JOIN", "1") != "0"
 
 
+class _IndexSemi:
+    """A deferred semi / anti join build side taken by ``_semi_index_then_filter``."""
+
+    def __init__(self, node):
+        self.node = node
+
+
+def _plain(lb: Batch) -> Batch:
+    if isinstance(lb, LateBatch):
+        return lb.materialize()
+    if isinstance(lb, _LazyScanBatch):
+        return Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
+    return lb
+
+
 class MultiJoinExec(ExecNode):
     """N-ary inner join. Inputs are materialised first, then joined greedily:
     each step joins the connected pair with the smallest estimated result
@@ -1556,6 +1664,12 @@ class MultiJoinExec(ExecNode):
                 lc = set().union(*[{c.cid for c in ch.schema} for ch in lg.children])
                 agg = semi_aggregate(sp.kind, sp.on, sp.residual, sp.null_aware, lc, sp.right, rex, ctx,
                                      ("multi", id(sp)))
+            elif SEMI_INDEX_MULTI and (found := _semi_index_scan(rex, sp, ctx)) is not None \
+                    and found[1].num_rows > self.EAGER_SEMI_RATIO * rels[sp.child]["batch"].num_rows:
+                # applied after the joins as an index nested loop (the filtered
+                # build side is never materialised): deferred unconditionally
+                deferred.append((sp, _IndexSemi(rex)))
+                continue
             semis.append((sp, agg[0] if agg is not None else rex.execute(ctx)))
         conds = list(lg.conds)
         # global row counts of every input (SPMD: every rank must derive the
@@ -1655,6 +1769,13 @@ class MultiJoinExec(ExecNode):
         if conds:
             b = filter_batch(b, and_all(conds), ctx)
         for sp, rb in deferred:
+            if isinstance(rb, _IndexSemi):
+                found = _semi_index_scan(rb.node, sp, ctx)
+                out = _semi_index_then_filter(found, sp, _plain(b), ctx) if found is not None else None
+                if out is not None:
+                    b = out
+                    continue
+                rb = rb.node.execute(ctx)
             b = self._semi(b, rb, sp, ctx)
         return b
 

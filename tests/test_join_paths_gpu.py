@@ -126,14 +126,26 @@ INDEX_QUERIES = [
     # semi join of the big side with a small key set (sorted and unsorted key columns)
     ("SELECT count(*) AS c, sum(bv) AS s FROM big WHERE bk IN (SELECT sk FROM small WHERE sw = 1)", None),
     ("SELECT count(*) AS c, sum(bv) AS s FROM big WHERE ok IN (SELECT sk FROM small WHERE sw = 1)", None),
+    # [NOT] EXISTS against a filtered scan sorted on the key (Q4 shape): index
+    # nested loop, the scan filter evaluated on the candidate rows only
+    ("SELECT count(*) AS c, sum(sw) AS s FROM small WHERE EXISTS (SELECT * FROM big WHERE ok = sk AND bv < 100)",
+     "join.index_then_filter"),
+    ("SELECT count(*) AS c, sum(sw) AS s FROM small WHERE NOT EXISTS (SELECT * FROM big WHERE ok = sk AND bv < 20)",
+     "join.index_then_filter"),
+    # Q21 shape: both, deferred past a multi-way join, with residuals on the candidate pairs
+    ("SELECT count(*) AS c, sum(b1.bv) AS s FROM big b1, small WHERE b1.ok = sk AND sk < 50000 "
+     "AND EXISTS (SELECT * FROM big b2 WHERE b2.ok = b1.ok AND b2.bv <> b1.bv AND b2.bv < 500) "
+     "AND NOT EXISTS (SELECT * FROM big b3 WHERE b3.ok = b1.ok AND b3.bk <> b1.bk AND b3.bv < 30)",
+     "join.index_then_filter"),
 ]
 
 
 @pytest.mark.parametrize("qi", range(len(INDEX_QUERIES)))
-def test_index_paths_default_thresholds(gpu_device, qi):
+def test_index_paths_default_thresholds(gpu_device, qi, monkeypatch):
     """Mid-size secondary-index joins, index-range runtime key filters and
     semi joins (exec/operators.py inner_pairs, _index_key_filter) with the
     default thresholds, against the CPU engine."""
+    monkeypatch.setattr(O, "SEMI_INDEX_MULTI", True)      # opt-in path (Q21 shape) checked too
     big, small = _index_tables()
     sql, phase = INDEX_QUERIES[qi]
     res = {}
