@@ -793,7 +793,8 @@ def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
         if scanned[1] * PERM_INDEX_SORT_FRAC > n_r:
             return None
         lidx, pos = H.expand_ranges(lo, cnt, n_r, scanned)
-        keys = list(raw.columns)
+        # only the filter's inputs at every candidate; residual inputs at the survivors
+        keys = sorted(col_refs(scan.predicate))
         sub = Batch(dict(zip(keys, take_many([raw.columns[k] for k in keys], pos))), pos.numel(), raw.dist)
         ok = mask_to_indices(predicate_mask(scan.predicate, sub, ctx))
         li = gather_tensor(lidx, ok)
@@ -802,7 +803,7 @@ def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
             lref = [c for c in refs if c in lb.columns]
             rref = [c for c in refs if c not in lb.columns]
             pair = dict(zip(lref, take_many([lb.columns[c] for c in lref], li)))
-            pair.update(zip(rref, take_many([sub.columns[names[c]] for c in rref], ok)))
+            pair.update(zip(rref, take_many([raw.columns[names[c]] for c in rref], gather_tensor(pos, ok))))
             li = gather_tensor(li, mask_to_indices(predicate_mask(j.residual, Batch(pair, ok.numel()), ctx)))
         mark = torch.zeros(n_l, dtype=torch.bool, device=ctx.device)
         if li.numel():
