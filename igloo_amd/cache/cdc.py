@@ -178,6 +178,7 @@ class CachedTable(TableSource):
             getattr(source, "cdc_poll_s", 1.0)
         self.partitioned_by = getattr(source, "partitioned_by", None)
         self.replicated = getattr(source, "replicated", False)
+        self.cluster_key = getattr(source, "cluster_key", None)
         self.hits = self.misses = 0
         #: row-group statistics pruning on the cached path (see ``_prune_rows``)
         self.last_prune_stats: dict = {}

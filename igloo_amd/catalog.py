@@ -36,6 +36,9 @@ class TableSource:
     partitioned_by: Optional[str] = None
     #: every rank holds the full table
     replicated: bool = False
+    #: integer column the rows are stored in ascending order of (SPMD: a
+    #: replicated table splits by ranges of it, parallel/slicing.py)
+    cluster_key: Optional[str] = None
 
     def schema(self) -> List[Field]:
         raise NotImplementedError
@@ -71,7 +74,7 @@ class MemoryTable(TableSource):
 
     def __init__(self, columns: Dict[str, Column], num_rows: Optional[int] = None,
                  partitioned_by: Optional[str] = None, replicated: bool = False,
-                 fields: Optional[List[Field]] = None, resident: bool = True):
+                 fields: Optional[List[Field]] = None, resident: bool = True, cluster_key: Optional[str] = None):
         self.columns = dict(columns)
         # resident=False: columns stay where they are (e.g. host memory under a
         # small device budget) and each scan moves a transient copy
@@ -81,6 +84,7 @@ class MemoryTable(TableSource):
         self._n = num_rows if num_rows is not None else (len(next(iter(columns.values()))) if columns else 0)
         self.partitioned_by = partitioned_by
         self.replicated = replicated
+        self.cluster_key = cluster_key
         self._fields = fields or [Field(k, c.dtype, c.valid is not None) for k, c in self.columns.items()]
 
     @staticmethod

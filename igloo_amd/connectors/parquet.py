@@ -77,7 +77,8 @@ class ParquetTable(TableSource):
     can_stream = True
 
     def __init__(self, path: str, files: Optional[List[str]] = None, local: bool = False,
-                 partitioned_by: Optional[str] = None, replicated: bool = False, cache: Optional[bool] = None):
+                 partitioned_by: Optional[str] = None, replicated: bool = False, cache: Optional[bool] = None,
+                 cluster_key: Optional[str] = None):
         self.path = path
         self._fixed_files = files is not None
         self.files = files if files is not None else list_files(path)
@@ -86,6 +87,7 @@ class ParquetTable(TableSource):
         self.local = local
         self.partitioned_by = partitioned_by
         self.replicated = replicated
+        self.cluster_key = cluster_key
         if cache is not None:
             self.cacheable = cache
         self._lock = threading.Lock()

@@ -44,6 +44,8 @@ SPECULATE = os.environ.get("IGLOO_SPECULATE", "1") == "1"
 SPMD_SPECULATE = os.environ.get("IGLOO_SPMD_SPECULATE", "1") == "1"
 #: SPMD query graphs (collectives captured with the kernels; RCCL only)
 SPMD_GRAPHS = os.environ.get("IGLOO_SPMD_GRAPHS", "1") == "1"
+#: SPMD: a query over replicated tables only splits its largest table by key range
+SLICE_REPLICATED = os.environ.get("IGLOO_SLICE_REPLICATED", "1") == "1"
 
 log = get_logger("engine")
 
@@ -613,6 +615,7 @@ class QueryEngine:
 
     def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:
         ctx = ctx or self.make_context()
+        ctx.slices = self._slices_for(plan)
         node = create_physical_plan(plan)
         from .ops import hashing as _H
         tok = _H.TABLE_BYTES_LIMIT.set(ctx.budget // 4 if ctx.budget else None)
@@ -624,6 +627,14 @@ class QueryEngine:
             from .parallel.exchange import gather_all
             out = gather_all(out, ctx)
         return out
+
+    def _slices_for(self, plan: Plan) -> Dict[int, str]:
+        """SPMD: the replicated table a query over replicated tables only
+        splits by key range (parallel/slicing.py)."""
+        if self.comm is None or not self.comm.spmd or not SLICE_REPLICATED:
+            return {}
+        from .parallel.slicing import plan_slices
+        return plan_slices(plan, self.comm)
 
     def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str]) -> pa.Table:
         arrays, fields = [], []
@@ -650,6 +661,7 @@ class QueryEngine:
         if analyze:
             from .ops._lib import HOST_STEPS
             ctx = self.make_context(analyze=True)
+            ctx.slices = self._slices_for(logical)
             c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
             h0 = dict(HOST_STEPS)
             t0 = time.perf_counter()

@@ -443,6 +443,10 @@ def semi_aggregate(kind, on, residual, null_aware, left_cids, right_plan, right_
         x, y = (r.left, r.right) if r.left.cid in left_cids else (r.right, r.left)
         if x.cid not in left_cids or y.cid not in rcids or x.dtype.is_string or y.dtype.is_string:
             return None
+        if x.dtype != y.dtype or x.dtype.is_float:
+            # MIN/MAX(y) are compared with x as raw values: decimals of
+            # different scales (or int vs decimal) are in different units
+            return None
         ineq = (x, y)
     if not big_streamable(right_node, ctx):
         return None

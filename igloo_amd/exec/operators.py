@@ -86,6 +86,12 @@ class ExecContext:
         self.morsel_depth = 0
         self.morsels = {"pipelines": 0, "morsels": 0, "rows": 0, "bytes": 0}
         self.semi_builds: dict = {}   # aggregated SEMI / ANTI build sides (exec/morsel.py)
+        # raw scans a fast-path check already read (ScanExec.peek_raw): the
+        # general path that runs when the check fails reuses them
+        self.raw_peeks: Dict[int, Batch] = {}
+        # SPMD: {id(source): key column} of the replicated table this query
+        # splits by key range (parallel/slicing.py plan_slices)
+        self.slices: Dict[int, str] = {}
 
     def note_scan(self, source, rows: int) -> None:
         if id(source) not in self._scanned_sources:
@@ -309,11 +315,27 @@ class ScanExec(ExecNode):
 
     def scan_raw(self, ctx) -> Batch:
         """Scanned columns (projection + filter inputs) before filtering, keyed by cid."""
+        if ctx.morsel is None and id(self) in ctx.raw_peeks:
+            return ctx.raw_peeks.pop(id(self))
         s = self.logical
         table_cols = getattr(s, "table_cols", s.schema)
         names, need, by_cid = self.column_names()
+        slice_key = ctx.slices.get(id(s.source)) if ctx.morsel is None else None
         if ctx.morsel is not None and ctx.morsel[0] == id(self):
             raw = ctx.morsel[1]          # the current morsel of a pipeline (exec/morsel.py)
+        elif slice_key is not None:
+            # a query over replicated tables only: this rank's key-range
+            # slice of the largest one (parallel/slicing.py); read whole
+            # (no row-group pruning), so every scan of the table slices alike
+            from ..parallel.slicing import slice_columns
+            with ctx.span("scan.source"):
+                full = s.source.scan(names + ([slice_key] if slice_key not in names else []), ctx)
+                ctx.note_scan(s.source, full.num_rows)
+                scols, n, tag = slice_columns(full.columns, full.num_rows, slice_key, ctx.world, ctx.comm.rank)
+            cols = {cid: scols[by_cid[cid].name] for cid in sorted(need)}
+            kc = [cid for cid in sorted(need) if by_cid[cid].name == slice_key]
+            # (an unsorted key column splits by rows: partitioned, placed by no key)
+            return Batch(cols, n, (tag,) + tuple(kc) if tag is not None and kc else None)
         else:
             with ctx.span("scan.source"):
                 pf = self.pushable()
@@ -329,6 +351,15 @@ class ScanExec(ExecNode):
                 pc = [c.cid for c in table_cols if c.name == s.source.partitioned_by]
                 dist = ("hash", pc[0]) if pc else None
         return Batch(cols, raw.num_rows, dist)
+
+    def peek_raw(self, ctx) -> Batch:
+        """``scan_raw`` for a fast-path check that may still fall back to the
+        general path: the batch is kept so the scan is not read (decoded,
+        copied to the device) a second time when the check fails."""
+        raw = self.scan_raw(ctx)
+        if ctx.morsel is None:
+            ctx.raw_peeks[id(self)] = raw
+        return raw
 
     @property
     def predicate(self) -> Optional[Expr]:
@@ -495,15 +526,21 @@ class ProjectExec(ExecNode):
 
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
+        from ..parallel.exchange import keyed
         cols = {}
-        dist = b.dist if (b.dist is None or b.dist[0] == "replicated") else None
-        hashed = []
+        d = b.dist
+        # replicated / arbitrary carry over; a key placement keeps the
+        # output columns that are its key columns (renamed or not)
+        dist = d if d == ("replicated",) else None
+        placed = []
         for ci, e in self.logical.exprs:
             cols[ci.cid] = ctx.evaluator.column(e, b)
-            if b.dist and b.dist[0] == "hash" and isinstance(e, ColRef) and e.cid in b.dist[1:]:
-                hashed.append(ci.cid)
-        if hashed:
-            dist = ("hash",) + tuple(hashed)
+            if keyed(d) and isinstance(e, ColRef) and e.cid in d[1:]:
+                placed.append(ci.cid)
+        if placed:
+            dist = (d[0],) + tuple(placed)
+        elif keyed(d):
+            dist = None
         return Batch(cols, b.num_rows, dist)
 
 
@@ -650,8 +687,9 @@ def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
     the aggregate's INPUT is semi-joined with those keys before grouping.
     TPC-H Q17/Q20/Q2: a correlated aggregate over all of lineitem/partsupp
     shrinks to the handful of parts the outer query selected."""
-    if _global_rows(lb, ctx) > RUNTIME_FILTER_MAX_ROWS:
-        return
+    # (the candidate is found from the plan first: a build side that is no
+    # aggregate costs no collective, so SPMD ranks that reach this point by
+    # different rank-local fast-path decisions stay aligned)
     for a, b in on:
         if not isinstance(b, ColRef):
             continue
@@ -663,8 +701,15 @@ def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
             continue
         lcol = ctx.evaluator.column(a, lb)
         if ctx.spmd and lb.dist != ("replicated",):
+            # the global key set; the size check rides on the gather's own
+            # preamble (one collective fewer than counting first)
             from ..parallel.exchange import gather_all
-            lcol = gather_all(Batch({0: lcol}, lb.num_rows, lb.dist), ctx).columns[0]
+            g = gather_all(Batch({0: lcol}, lb.num_rows, lb.dist), ctx, max_rows=RUNTIME_FILTER_MAX_ROWS)
+            if g is None:
+                return
+            lcol = g.columns[0]
+        elif lb.num_rows > RUNTIME_FILTER_MAX_ROWS:
+            return
         agg.runtime_filters.append((gexpr, lcol))
         return
 
@@ -733,7 +778,7 @@ def _semi_index_scan(rnode, j, ctx):
     """The filtered resident scan under a [NOT] EXISTS build side, for
     ``_semi_index_then_filter``: (scan, raw batch, key column, output cid ->
     scan cid) or None. Cheap: resident columns are not filtered here."""
-    if not (SEMI_INDEX and ctx.device.type == "cuda" and not ctx.spmd and ctx.budget is None and ctx.memo is None) \
+    if not (SEMI_INDEX and ctx.device.type == "cuda" and ctx.budget is None and ctx.memo is None) \
             or j.kind not in ("semi", "anti") or j.null_aware or len(j.on) != 1:
         return None
     le, re_ = j.on[0]
@@ -754,7 +799,7 @@ def _semi_index_scan(rnode, j, ctx):
             cid = src[0].cid
         return cid
     names = {c.cid: resolve(c.cid) for c in (chain[0].logical.schema if chain else rnode.logical.schema)}
-    raw = rnode.scan_raw(ctx)
+    raw = rnode.peek_raw(ctx)
     rcol = raw.columns.get(names.get(re_.cid))
     if rcol is None or rcol.valid is not None or rcol.dtype.is_string or raw.num_rows < SORTED_JOIN_MIN_ROWS \
             or not getattr(rcol.data, "_igloo_resident", False) or not H.is_sorted(rcol.data):
@@ -776,8 +821,10 @@ def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
     compaction and the gather of 385M keys; Q21's NOT EXISTS the same way
     with its l_suppkey <> residual. None when the size does not apply."""
     scan, raw, rcol, names = found
-    le = j.on[0][0]
+    le, re_ = j.on[0]
     n_r, n_l = raw.num_rows, lb.num_rows
+    if ctx.spmd and not _rank_local_semi(lb, le, raw, names.get(re_.cid)):
+        return None
     if le.cid not in lb.columns or n_l == 0 or n_l * 2 > n_r:
         return None
     lcol = ctx.evaluator.column(le, lb)
@@ -810,7 +857,24 @@ def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
             mark.index_fill_(0, li.long(), True)
         keep = mask_to_indices(mark if j.kind == "semi" else ~mark)
     ctx.note_partial_read(rcol.data, scanned[1])
-    return _take_batch(lb, keep)
+    out = _take_batch(lb, keep)
+    out.dist = lb.dist
+    return out
+
+
+def _rank_local_semi(lb: Batch, lkey, rb: Batch, rcid) -> bool:
+    """SPMD: a SEMI / ANTI join of ``lb`` against ``rb`` on ``lkey`` = column
+    ``rcid`` can run on each rank's rows alone: the build side is replicated,
+    or both sides are placed by the join key with the same mapping (lineitem
+    and orders by order key). The rank-local fast paths check this from the
+    placements (plan + catalog, alike on every rank); whatever size check
+    they make on their own rows may differ between ranks, which is safe
+    because the general path they fall back to issues no collective for
+    such inputs either (parallel/exchange.py prepare_join, semi_by_key_set)."""
+    from ..parallel.exchange import REPLICATED, copartitioned
+    if rb.dist == REPLICATED:
+        return True
+    return isinstance(lkey, ColRef) and copartitioned(lb.dist, lkey.cid, rb.dist, rcid)
 
 
 def apply_key_filters(b: Batch, filters, ctx) -> Batch:
@@ -1624,16 +1688,19 @@ class MultiJoinExec(ExecNode):
         if agg is not None and agg[0] is rb:
             from .morsel import apply_semi_aggregate
             return apply_semi_aggregate(lb, rb, agg[1], ctx)
-        if sp.kind == "semi" and sp.residual is None and not sp.null_aware and len(sp.on) == 1 and not ctx.spmd \
+        if sp.kind == "semi" and sp.residual is None and not sp.null_aware and len(sp.on) == 1 \
                 and lb.num_rows and rb.num_rows:
             # a small key set against a big resident column (Q18's 6.5K qualifying
             # orders against 150M o_orderkey): its index ranges, not a full probe
             le, re_ = sp.on[0]
-            if isinstance(le, ColRef) and isinstance(re_, ColRef) and le.cid in lb.columns and re_.cid in rb.columns:
+            if isinstance(le, ColRef) and isinstance(re_, ColRef) and le.cid in lb.columns and re_.cid in rb.columns \
+                    and (not ctx.spmd or _rank_local_semi(lb, le, rb, re_.cid)):
                 pk, bk, pvalid, bvalid = key_tensors([ctx.evaluator.column(le, lb)], [ctx.evaluator.column(re_, rb)])
                 rows = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
                 if rows is not None:
-                    return _take_batch(lb, rows)
+                    out = _take_batch(lb, rows)
+                    out.dist = lb.dist
+                    return out
         if ctx.spmd:
             from ..parallel.exchange import prepare_join, semi_by_key_set
             j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
@@ -2108,7 +2175,7 @@ class HashAggExec(ExecNode):
         parent FilterExec still applies the predicate to them (NULL groups).
         None when the shape does not apply (the general path runs)."""
         lg, pred = self.logical, self.having
-        if (pred is None or ctx.device.type != "cuda" or ctx.spmd or ctx.budget is not None or self.runtime_filters
+        if (pred is None or ctx.device.type != "cuda" or ctx.budget is not None or self.runtime_filters
                 or not SORTED_HAVING or len(lg.groups) != 1 or not 1 <= len(lg.aggs) <= 4
                 or not isinstance(lg.groups[0][1], ColRef) or not isinstance(pred, BinOp)):
             return None
@@ -2134,7 +2201,13 @@ class HashAggExec(ExecNode):
         if not isinstance(child, ScanExec) or child.predicate is not None:
             return None
         gci, gexpr = lg.groups[0]
-        raw = child.scan_raw(ctx)
+        if ctx.spmd and not self._group_local(child, gexpr, ctx):
+            return None
+        raw = child.peek_raw(ctx)
+        if ctx.spmd:
+            from ..parallel.exchange import REPLICATED, placed_on
+            if raw.dist != REPLICATED and not placed_on(raw.dist, gexpr.cid):
+                return None      # (alike on every rank: placements follow from plan and catalog)
         kc = raw.columns.get(gexpr.cid) if hasattr(raw, "columns") else None
         if kc is None or kc.valid is not None or kc.data.dtype not in (torch.int32, torch.int64) \
                 or kc.data.dim() != 1 or kc.dtype.is_string or raw.num_rows < SORTED_HAVING_MIN_ROWS \
@@ -2167,11 +2240,38 @@ class HashAggExec(ExecNode):
         for fin in finals:
             ci, col = fin(results)
             out[ci.cid] = col
-        return Batch(out, rep.numel())
+        return Batch(out, rep.numel(), self._local_dist(raw.dist, gci) if ctx.spmd else None)
+
+    @staticmethod
+    def _group_local(scan: "ScanExec", gexpr, ctx) -> bool:
+        """SPMD: every group of GROUP BY ``gexpr`` over ``scan`` lives on one
+        rank (the scan's table is placed by that column -- hash-partitioned,
+        or a replicated table this query splits by ranges of it -- or is
+        replicated whole), so an aggregate over the rank's rows is final.
+        Decided from the plan and catalog, alike on every rank."""
+        src = scan.logical.source
+        names = {c.cid: c.name for c in getattr(scan.logical, "table_cols", scan.logical.schema)}
+        names.update({c.cid: c.name for c in scan.logical.schema})
+        col = names.get(gexpr.cid) if isinstance(gexpr, ColRef) else None
+        if getattr(src, "replicated", False):
+            sk = ctx.slices.get(id(src))
+            return sk is None or (col is not None and col == sk)
+        pk = getattr(src, "partitioned_by", None)
+        return pk is not None and col == pk
+
+    @staticmethod
+    def _local_dist(d, gci):
+        from ..parallel.exchange import REPLICATED, keyed
+        if d == REPLICATED:
+            return REPLICATED
+        return (d[0], gci.cid) if keyed(d) else None
 
     def _finish_general(self, b, ctx) -> Batch:
         lg = self.logical
-        return aggregate(lg.groups, lg.aggs, b, ctx)
+        out = aggregate(lg.groups, lg.aggs, b, ctx)
+        if ctx.spmd:
+            out.dist = self._local_dist(b.dist, lg.groups[0][0])
+        return out
 
     def describe(self):
         a = self.logical
@@ -2206,8 +2306,8 @@ class HashAggExec(ExecNode):
             from .morsel import big_streamable
             if big_streamable(child.children[1], ctx):
                 return self._eager_count_streamed(lkey, rkey, ctx)
-        if ctx.device.type != "cuda":
-            return None
+        if ctx.device.type != "cuda" and not ctx.spmd:
+            return None     # (the CPU engine stays the plain join + aggregate: the GPU tests' reference)
         lb = child.children[0].execute(ctx)
         masked = self._eager_count_masked(lg, lb, lkey, rkey, ctx)
         if masked is not None:
@@ -2220,19 +2320,12 @@ class HashAggExec(ExecNode):
                 rk = gather_tensor(rk, keep)
                 rb = _take_batch(rb, keep)
             cnt_cols = {}
-            rng = H.key_range(rk) if rk.numel() else None
             if ctx.spmd:
-                # SPMD: the right side is spread over ranks; one global key
-                # range, per-rank histograms summed by one all-reduce (a dense
-                # 8-byte count per key, ~120 MB at SF100, instead of shuffling
-                # the 150M-row right side by key); every left row then reads
-                # its global count, so the output keeps the left side's placement
-                lo_hi = ctx.comm.allgather_ints([rng[0], rng[1]] if rng else [2**62, -2**62])
-                g0, g1 = min(r[0] for r in lo_hi), max(r[1] for r in lo_hi)
-                rng = (g0, g1) if g0 <= g1 else None
+                out = self._spmd_counts(lg, lb, lkey, lk, lvalid, rk,
+                                        [ev.column(a.arg, rb).valid for _, a in lg.aggs], ctx)
+                return out if out is not None else self._spmd_join_aggregate(lb, rb, ctx)
+            rng = H.key_range(rk) if rk.numel() else None
             span = rng[1] - rng[0] + 1 if rng else 0
-            if ctx.spmd and (not rng or span > EAGER_COUNT_DIRECT_SPAN):
-                return self._spmd_join_aggregate(lb, rb, ctx)
             if rng and span <= EAGER_COUNT_DIRECT_SPAN:
                 # dense key domain: one histogram pass over the right keys, then a
                 # direct lookup per left key (no hash table, no group ids)
@@ -2245,8 +2338,6 @@ class HashAggExec(ExecNode):
                 for k, (_, a) in enumerate(lg.aggs):
                     hist = A.key_histogram(rk, kmin, span, ev.column(a.arg, rb).valid) if rk.numel() else \
                         torch.zeros(span, dtype=torch.int64, device=ctx.device)
-                    if ctx.spmd:
-                        hist = ctx.comm.allreduce_tensor(hist, "sum")
                     cnt_cols[-(k + 1)] = torch.where(inr, hist.index_select(0, li), torch.zeros_like(li))
             elif rk.numel():
                 gid, ng, rep, srt = H.group_ids_ex(rk)
@@ -2260,18 +2351,91 @@ class HashAggExec(ExecNode):
             else:
                 for k in range(len(lg.aggs)):
                     cnt_cols[-(k + 1)] = torch.zeros(lb.num_rows, dtype=torch.int64, device=ctx.device)
+        return self._count_sums(lg, lb, [cnt_cols[-(k + 1)] for k in range(len(lg.aggs))], ctx)
+
+    def _count_sums(self, lg, lb: Batch, counts, ctx, dist=None) -> Batch:
+        """GROUP BY <left key> SUM(per-row partner count) -- the eager COUNT's
+        final step over the left rows and their looked-up counts."""
         cols = dict(lb.columns)
         aggs = []
         for k, (ci, _) in enumerate(lg.aggs):
             tmp = -(10**9) - k  # temporary column ids (binder ids are positive)
-            cols[tmp] = Column(T.INT64, cnt_cols[-(k + 1)].contiguous())
+            cols[tmp] = Column(T.INT64, counts[k].to(torch.int64).contiguous())
             aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
         if ctx.spmd:
-            # the left side's placement carries over (a replicated left side
-            # gives a replicated result; a partitioned one is merged by key)
             from ..parallel.exchange import distributed_aggregate
-            return distributed_aggregate(L.Aggregate(None, lg.groups, aggs), Batch(cols, lb.num_rows, lb.dist), ctx)
+            return distributed_aggregate(L.Aggregate(None, lg.groups, aggs),
+                                         Batch(cols, lb.num_rows, dist if dist is not None else lb.dist), ctx)
         return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
+
+    def _spmd_counts(self, lg, lb: Batch, lkey, lk, lvalid, rk, rmasks, ctx) -> Optional[Batch]:
+        """SPMD eager COUNT: each rank histograms its right rows' keys over the
+        GLOBAL key range (one tiny all-gather of the ranges), then
+
+        * replicated left side (TPC-H Q13: customer against orders placed by
+          order key): ONE reduce-scatter sums the histograms and leaves rank r
+          the counts of key chunk r only (1/world of the bytes of an
+          all-reduce, which would hand every rank all 15M counts at SF100);
+          each rank keeps the left rows of its chunk, so the result is
+          partitioned by key range and the GROUP BY that follows is rank-local;
+        * partitioned left side: an all-reduce (every rank's left keys may
+          fall anywhere in the range).
+
+        Counts travel as int32 (half the bytes) when the global right row
+        count fits. None when the global key span is too large for dense
+        histograms (decided alike on every rank)."""
+        from ..parallel.exchange import REPLICATED
+        from ..parallel.slicing import range_chunk, range_tag
+        comm = ctx.comm
+        W = comm.world_size
+        dev = ctx.device
+        masks = list(rmasks)
+        rng = H.key_range(rk, masks[0] if len(set(map(id, masks))) == 1 else None) if rk.numel() else None
+        g = comm.allgather_ints([rng[0], rng[1], rk.numel()] if rng else [2**62, -2**62, rk.numel()])
+        g0, g1 = min(r[0] for r in g), max(r[1] for r in g)
+        if g0 > g1:
+            return self._count_sums(lg, lb, [torch.zeros(lb.num_rows, dtype=torch.int64, device=dev)] * len(masks), ctx)
+        span = g1 - g0 + 1
+        if span > EAGER_COUNT_DIRECT_SPAN:
+            return None
+        wide = sum(r[2] for r in g) >= 2**31
+        rep = lb.dist == REPLICATED
+        chunk = range_chunk(g0, g1, W) if rep else span
+        width = W * chunk if rep else span
+        hdt = torch.int64 if wide else torch.int32
+        hists = torch.zeros((len(masks), width), dtype=hdt, device=dev)
+        for k, m in enumerate(masks):
+            if rk.numel():
+                hists[k, :span] = A.key_histogram(rk, g0, span, m).to(hdt)
+        lkey64 = lk.to(torch.int64)
+        if rep:
+            # [world, aggs, chunk]: rank r's share is one contiguous block
+            mine = comm.reduce_scatter_tensor(hists.view(len(masks), W, chunk).transpose(0, 1).contiguous(), "sum")
+            mine = mine.view(len(masks), chunk)
+            # the left rows of this rank's key chunk (keys outside the right
+            # side's range clamp to the first / last chunk; NULL keys: rank 0)
+            owner = torch.clamp(torch.div(lkey64 - g0, chunk, rounding_mode="floor"), 0, W - 1)
+            own = owner == comm.rank
+            if lvalid is not None:
+                own = torch.where(lvalid, own, torch.full_like(own, comm.rank == 0))
+            if W > 1:
+                sel = mask_to_indices(own)
+                lb = _take_batch(lb, sel)
+                lkey64 = gather_tensor(lkey64, sel)
+                lvalid = gather_tensor(lvalid, sel) if lvalid is not None else None
+            base, size, table = g0 + comm.rank * chunk, chunk, mine
+            dist = (range_tag(W, g0, chunk), lkey.cid) if isinstance(lkey, ColRef) else None
+        else:
+            table = comm.allreduce_tensor(hists, "sum")
+            base, size, dist = g0, span, None
+        li = lkey64 - base
+        inr = (li >= 0) & (li < size)
+        if lvalid is not None:
+            inr &= lvalid
+        li = torch.where(inr, li, torch.zeros_like(li))
+        counts = [torch.where(inr, table[k].index_select(0, li).to(torch.int64), torch.zeros_like(li))
+                  for k in range(len(masks))]
+        return self._count_sums(lg, lb, counts, ctx, dist)
 
     def _eager_count_masked(self, lg, lb, lkey, rkey, ctx) -> Optional[Batch]:
         """``_eager_count`` over a filtered right-side scan without
@@ -2281,17 +2445,24 @@ class HashAggExec(ExecNode):
         pure copies). Dense key domains, single rank, no budget; None when
         the shape differs."""
         rnode = self.children[0].children[1]
-        if ctx.spmd or ctx.budget is not None or not isinstance(rnode, ScanExec) or rnode.predicate is None \
+        if ctx.budget is not None or not isinstance(rnode, ScanExec) or rnode.predicate is None \
                 or not EAGER_COUNT_MASKED or any(getattr(a.arg, "nullable", True) for _, a in lg.aggs) \
                 or not isinstance(rkey, ColRef):
             return None
         ev = ctx.evaluator
-        raw = rnode.scan_raw(ctx)
+        raw = rnode.peek_raw(ctx)
         rcol = raw.columns.get(rkey.cid)
         lcol = ev.column(lkey, lb)
         if rcol is None or rcol.dtype.is_string or lcol.dtype.is_string or rcol.is_dict \
-                or rcol.data.dtype not in (torch.int32, torch.int64):
+                or rcol.data.dtype not in (torch.int32, torch.int64) or lcol.data.dtype not in (torch.int32, torch.int64):
             return None
+        if ctx.spmd:
+            # (the global key span decides, alike on every rank)
+            with ctx.span("agg.eager_count"):
+                m = predicate_mask(rnode.predicate, raw, ctx)
+                if rcol.valid is not None:
+                    m = m & rcol.valid
+                return self._spmd_counts(lg, lb, lkey, lcol.data, lcol.valid, rcol.data, [m] * len(lg.aggs), ctx)
         rng = H.key_range(rcol.data, rcol.valid)
         span = rng[1] - rng[0] + 1 if rng else 0
         if not rng or span > EAGER_COUNT_DIRECT_SPAN:
@@ -2362,7 +2533,7 @@ class HashAggExec(ExecNode):
     def _run(self, ctx):
         lg = self.logical
         child = self.children[0]
-        if self.having is not None and not ctx.spmd and ctx.budget is None and ctx.device.type == "cuda" \
+        if self.having is not None and ctx.budget is None and ctx.device.type == "cuda" \
                 and not self.runtime_filters:
             out = self._sorted_having(ctx)
             if out is not None:
@@ -2372,7 +2543,7 @@ class HashAggExec(ExecNode):
             out = streamed_aggregate(self, ctx)
             if out is not None:
                 return out
-        if (ctx.device.type == "cuda" or ctx.budget is not None) and not self.runtime_filters:
+        if (ctx.device.type == "cuda" or ctx.budget is not None or ctx.spmd) and not self.runtime_filters:
             out = self._eager_count(ctx)
             if out is not None:
                 return out
@@ -2390,7 +2561,7 @@ class HashAggExec(ExecNode):
                     return out
             b = LazyBatch(lambda: child.finish(raw, ctx), raw.dist)
         elif self.runtime_filters and isinstance(child, ScanExec) and child.predicate is not None \
-                and ctx.device.type == "cuda" and not ctx.spmd and ctx.budget is None and INDEX_THEN_FILTER:
+                and ctx.device.type == "cuda" and ctx.budget is None and INDEX_THEN_FILTER:
             # decided before the scan filter runs over the whole table
             raw = child.scan_raw(ctx)
             filters, self.runtime_filters = self.runtime_filters, []

@@ -332,6 +332,9 @@ PARTITIONED = ("orders", "lineitem")
 PARTITION_KEY = {"region": None, "nation": None, "supplier": "s_suppkey", "customer": "c_custkey",
                  "part": "p_partkey", "partsupp": "ps_partkey", "orders": "o_orderkey", "lineitem": "l_orderkey"}
 REPLICATED = ("region", "nation", "supplier", "customer", "part", "partsupp")
+#: the column every generated table is stored in ascending order of
+CLUSTER_KEY = {"region": "r_regionkey", "nation": "n_nationkey", "supplier": "s_suppkey", "customer": "c_custkey",
+               "part": "p_partkey", "partsupp": "ps_partkey", "orders": "o_orderkey", "lineitem": "l_orderkey"}
 
 
 def generate(sf: float, device="cpu", rank: int = 0, world: int = 1, lean: bool = False,
@@ -345,7 +348,7 @@ def generate(sf: float, device="cpu", rank: int = 0, world: int = 1, lean: bool 
     out: Dict[str, MemoryTable] = {}
     spmd = world > 1 if spmd is None else spmd
     if spmd and world == 1:
-        out = generate(sf, device, 0, 1, lean, tables, spmd=False)
+        out = generate(sf, device, 0, 1, lean, tables, spmd=False, replicate_dims=replicate_dims)
         for t, tab in out.items():
             if replicate_dims and t in REPLICATED:
                 tab.replicated, tab.partitioned_by = True, None
@@ -379,6 +382,8 @@ def generate(sf: float, device="cpu", rank: int = 0, world: int = 1, lean: bool 
             out["orders"] = o
         if "lineitem" in want:
             out["lineitem"] = l
+    for name, tab in out.items():
+        tab.cluster_key = CLUSTER_KEY[name]
     return out
 
 

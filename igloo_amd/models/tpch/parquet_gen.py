@@ -191,5 +191,5 @@ def register_dataset(engine, root: str, sf: float, rank: int = 0, world: int = 1
         key = PARTITION_KEY[name]
         srcs[name] = engine.register_parquet(
             name, _table_dir(root, sf, name, rank, world, lean), local=True, replicated=(key is None and spmd),
-            partitioned_by=key if spmd else None, **kw)
+            partitioned_by=key if spmd else None, cluster_key=datagen.CLUSTER_KEY[name], **kw)
     return srcs

@@ -173,6 +173,25 @@ class Communicator:
         self.bytes_sent += w.numel() * w.element_size()
         return w.to(t.device)
 
+    def reduce_scatter_tensor(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """``t`` is [world, ...]: every rank contributes all of it and receives
+        the element-wise SUM / MIN / MAX over ranks of block ``t[rank]`` only
+        (partitioned aggregates: each rank keeps the states of the keys it
+        owns; RCCL moves (world-1)/world of the bytes an all-reduce would
+        hand every rank)."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "reduce_scatter_tensor")
+        assert t.shape[0] == self.world_size, (t.shape, self.world_size)
+        if not self.spmd:
+            return t[0]
+        src = t.contiguous().to(self.wire).reshape(-1)        # [world * block], block-major
+        out = torch.empty(src.numel() // self.world_size, dtype=src.dtype, device=self.wire)
+        self.calls += 1
+        dist.reduce_scatter_tensor(out, src, op={"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN,
+                                                  "max": dist.ReduceOp.MAX}[op], group=self.group)
+        self.bytes_sent += src.numel() * src.element_size() * (self.world_size - 1) // max(self.world_size, 1)
+        return out.view(tuple(t.shape[1:])).to(t.device)
+
     def allgather_ints(self, xs: Sequence[int]) -> List[List[int]]:
         """Every rank contributes len(xs) ints; returns [rank][i]."""
         if faults.ACTIVE:

@@ -68,6 +68,24 @@ def hashed_on(d, cid) -> bool:
     return cid is not None and bool(d) and d[0] == "hash" and cid in d[1:]
 
 
+def keyed(d) -> bool:
+    """A placement by the value of its key columns ``d[1:]``: hash
+    (("hash", cid, ...)) or key range ((("range", world, kmin, chunk), cid,
+    ...), parallel/slicing.py)."""
+    return bool(d) and (d[0] == "hash" or (isinstance(d[0], tuple) and d[0][0] == "range"))
+
+
+def placed_on(d, cid) -> bool:
+    """All rows with one value of column ``cid`` live on one rank."""
+    return cid is not None and keyed(d) and cid in d[1:]
+
+
+def copartitioned(ld, lc, rd, rc) -> bool:
+    """Equal values of ``lc`` (left) and ``rc`` (right) live on the same rank:
+    both placed by those columns with the same mapping."""
+    return placed_on(ld, lc) and placed_on(rd, rc) and ld[0] == rd[0]
+
+
 def with_dist(b: Batch, d) -> Batch:
     b.dist = d
     return b
@@ -230,42 +248,82 @@ def _rebuild(cols: List[Column], spec, parts: List[torch.Tensor], chars: Dict[in
     return out
 
 
-def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
+def _split_bytes(buf: torch.Tensor, sizes: List[int]) -> List[torch.Tensor]:
+    """Consecutive pieces of a byte buffer (views)."""
+    out, pos = [], 0
+    for z in sizes:
+        out.append(buf[pos:pos + z])
+        pos += z
+    return out
+
+
+def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = False) -> Batch:
     """Hash-repartition rows of ``b`` by ``key`` across all ranks.
 
-    Collectives: one all-to-all of the [rank x (rows, string bytes...)] count
-    matrix, ONE all-to-all-v of every fixed-width column packed row-wise
-    (gathered into destination order by the pack kernel itself), and one
-    all-to-all-v of bytes per plain-string column."""
+    Collectives: the structure all-gather (skipped when the caller already
+    ``normalized`` the batch), one all-to-all of the [rank x (rows, string
+    bytes...)] count matrix, and ONE all-to-all-v of bytes: per destination
+    the packed fixed-width rows (gathered into destination order by the pack
+    kernel itself) followed by every plain-string column's bytes."""
     from ..ops.gather import take
     from ..ops.pack import pack_rows, unpack_rows
     comm = ctx.comm
     W = comm.world_size
-    b = normalize_structure(materialized(b), comm)
+    if not normalized:
+        b = normalize_structure(materialized(b), comm)
     perm, send = M.hash_partition(key, W)
     keys = list(b.columns)
     cols = [b.columns[k] for k in keys]
     tensors, spec = _fixed_parts(cols)
-    # string bytes per destination (strings gathered into destination order)
+    # string bytes per destination (strings gathered into destination order;
+    # every column's W + 1 byte bounds in one readback)
     bounds = np.cumsum([0] + list(send)).tolist()
-    sgath, sbytes = {}, []
-    for j, c in enumerate(cols):
-        if c.is_plain_string:
-            g = take(c, perm)
-            sgath[j] = g
-            offs = to_host_ints(g.offsets.index_select(0, device_ints(bounds, g.offsets.device)))
-            sbytes.append([offs[r + 1] - offs[r] for r in range(W)])
+    sgath = {j: take(c, perm) for j, c in enumerate(cols) if c.is_plain_string}
+    sbytes = []
+    if sgath:
+        bidx = device_ints(bounds, key.device)
+        offs = to_host_ints(torch.cat([g.offsets.index_select(0, bidx).to(torch.int64) for g in sgath.values()]))
+        for k in range(len(sgath)):
+            o = offs[k * (W + 1):(k + 1) * (W + 1)]
+            sbytes.append([o[r + 1] - o[r] for r in range(W)])
     mat = [[send[r]] + [sb[r] for sb in sbytes] for r in range(W)]
     rmat = comm.all_to_all_matrix(mat)
     recv = [r[0] for r in rmat]
-    parts: List[torch.Tensor] = []
+    packed, lay = pack_rows(tensors, perm, b.num_rows) if tensors else (None, (0, []))
+    rb = lay[0]
+    if not sgath:
+        parts: List[torch.Tensor] = []
+        if tensors:
+            rpacked, _ = comm.all_to_all_v(packed, send, recv)
+            parts = unpack_rows(rpacked, lay, tensors)
+        out = dict(zip(keys, _rebuild(cols, spec, parts, {})))
+        return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
+    # one byte stream per destination: [rows | string column 1 | string column 2 ...]
+    flat = packed.reshape(-1) if packed is not None else None
+    pieces, send_b = [], []
+    for r in range(W):
+        if flat is not None:
+            pieces.append(flat[bounds[r] * rb:bounds[r + 1] * rb])
+        for k, g in enumerate(sgath.values()):
+            lo = sum(sbytes[k][:r])
+            pieces.append(g.data[lo:lo + sbytes[k][r]])
+        send_b.append(send[r] * rb + sum(sb[r] for sb in sbytes))
+    recv_b = [rmat[r][0] * rb + sum(rmat[r][1:]) for r in range(W)]
+    buf, _ = comm.all_to_all_v(torch.cat(pieces) if pieces else torch.zeros(0, dtype=torch.uint8, device=key.device),
+                               send_b, recv_b)
+    row_parts, str_parts = [], [[] for _ in sgath]
+    for r, blk in enumerate(_split_bytes(buf, recv_b)):
+        sizes = [rmat[r][0] * rb] + list(rmat[r][1:])
+        sp = _split_bytes(blk, sizes)
+        row_parts.append(sp[0])
+        for k in range(len(sgath)):
+            str_parts[k].append(sp[1 + k])
+    parts = []
     if tensors:
-        packed, lay = pack_rows(tensors, perm, b.num_rows)
-        rpacked, _ = comm.all_to_all_v(packed, send, recv)
-        parts = unpack_rows(rpacked, lay, tensors)
-    chars = {}
-    for k, (j, g) in enumerate(sgath.items()):
-        chars[j], _ = comm.all_to_all_v(g.data, sbytes[k], [r[1 + k] for r in rmat])
+        rows = torch.cat(row_parts) if len(row_parts) > 1 else row_parts[0]
+        parts = unpack_rows(rows.view(-1, rb) if rb else rows.view(0, 0), lay, tensors)
+    chars = {j: (torch.cat(str_parts[k]) if len(str_parts[k]) > 1 else str_parts[k][0])
+             for k, j in enumerate(sgath)}
     out = dict(zip(keys, _rebuild(cols, spec, parts, chars)))
     return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
 
@@ -299,49 +357,70 @@ def _str_bytes(c: Column) -> int:
 
 def _gather_columns(cols: List[Column], counts: List[int], comm,
                     str_bytes: Optional[List[List[int]]] = None) -> List[Column]:
-    """All-gather of columns with agreeing structure: one packed all-gather-v
-    of the fixed-width parts and ONE all-gather-v of every plain-string
-    column's bytes concatenated (``str_bytes[rank][k]``: byte count of the
+    """All-gather of columns with agreeing structure: ONE all-gather-v of
+    bytes carrying every rank's packed fixed-width rows followed by its
+    plain-string columns' bytes (``str_bytes[rank][k]``: byte count of the
     k-th string column per rank, exchanged here when not given)."""
     from ..ops.pack import pack_rows, unpack_rows
     n = len(cols[0]) if cols else 0
     tensors, spec = _fixed_parts(cols)
-    parts: List[torch.Tensor] = []
-    if tensors:
-        packed, lay = pack_rows(tensors, None, n)
-        rpacked, _ = comm.all_gather_v(packed, counts)
-        parts = unpack_rows(rpacked, lay, tensors)
     sj = [j for j, c in enumerate(cols) if c.is_plain_string]
-    chars = {}
-    if sj:
-        if str_bytes is None:
-            str_bytes = comm.allgather_ints([_str_bytes(cols[j]) for j in sj])
-        local = cols[sj[0]].data if len(sj) == 1 else torch.cat([cols[j].data for j in sj])
-        allb, _ = comm.all_gather_v(local, [sum(r) for r in str_bytes])
-        pieces = {j: [] for j in sj}
-        pos = 0
-        for r in range(len(str_bytes)):
-            for k, j in enumerate(sj):
-                pieces[j].append(allb[pos:pos + str_bytes[r][k]])
-                pos += str_bytes[r][k]
-        for j in sj:
-            chars[j] = pieces[j][0] if len(pieces[j]) == 1 else torch.cat(pieces[j])
+    packed, lay = pack_rows(tensors, None, n) if tensors else (None, (0, []))
+    rb = lay[0]
+    if not sj:
+        parts: List[torch.Tensor] = []
+        if tensors:
+            rpacked, _ = comm.all_gather_v(packed, counts)
+            parts = unpack_rows(rpacked, lay, tensors)
+        return _rebuild(cols, spec, parts, {})
+    if str_bytes is None:
+        str_bytes = comm.allgather_ints([_str_bytes(cols[j]) for j in sj])
+    local = [packed.reshape(-1)] if packed is not None else []
+    local += [cols[j].data for j in sj]
+    sizes = [counts[r] * rb + sum(str_bytes[r]) for r in range(len(counts))]
+    allb, _ = comm.all_gather_v(torch.cat(local) if len(local) > 1 else local[0], sizes)
+    row_parts, pieces = [], {j: [] for j in sj}
+    for r, blk in enumerate(_split_bytes(allb, sizes)):
+        sp = _split_bytes(blk, [counts[r] * rb] + list(str_bytes[r]))
+        row_parts.append(sp[0])
+        for k, j in enumerate(sj):
+            pieces[j].append(sp[1 + k])
+    parts = []
+    if tensors:
+        rows = torch.cat(row_parts) if len(row_parts) > 1 else row_parts[0]
+        parts = unpack_rows(rows.view(-1, rb), lay, tensors)
+    chars = {j: (pieces[j][0] if len(pieces[j]) == 1 else torch.cat(pieces[j])) for j in sj}
     return _rebuild(cols, spec, parts, chars)
 
 
-def gather_all(b: Batch, ctx) -> Batch:
+def gather_all(b: Batch, ctx, max_rows: Optional[int] = None, normalized: bool = False) -> Optional[Batch]:
     """Every rank receives the concatenation of all ranks' rows (one packed
-    all-gather-v for the fixed-width columns)."""
+    all-gather-v for the fixed-width columns). ``max_rows``: return None
+    (on every rank alike) when the rows of all ranks exceed it -- decided
+    from the structure preamble, before any data moves."""
     comm = ctx.comm
     if comm is None or not comm.spmd or dist_of(b) == REPLICATED:
-        return b
+        return b if max_rows is None or b.num_rows <= max_rows else None
     b = materialized(b)
     keys = list(b.columns)
     # string byte counts ride along in the preamble (-1: not a plain string
     # here; same length on every rank)
+    if normalized:
+        # the caller's structure all-gather happened: only the counts (and
+        # string byte counts) travel, in one tiny all-gather
+        sj = [k for k in keys if b.columns[k].is_plain_string]
+        rows = comm.allgather_ints([b.num_rows] + [_str_bytes(b.columns[k]) for k in sj])
+        counts = [r[0] for r in rows]
+        if max_rows is not None and sum(counts) > max_rows:
+            return None
+        out = dict(zip(keys, _gather_columns([b.columns[k] for k in keys], counts, comm,
+                                             [r[1:] for r in rows] if sj else None))) if keys else {}
+        return with_dist(Batch(out, sum(counts)), REPLICATED)
     pre = [b.num_rows] + [_str_bytes(b.columns[k]) if b.columns[k].is_plain_string else -1 for k in keys]
     b = normalize_structure(b, comm, pre)
     counts = [p[0] for p in b.preamble]
+    if max_rows is not None and sum(counts) > max_rows:
+        return None
     cols = [b.columns[k] for k in keys]
     sj = [j for j, c in enumerate(cols) if c.is_plain_string]
     sb = [[p[1 + j] for j in sj] for p in b.preamble]
@@ -354,6 +433,29 @@ def gather_all(b: Batch, ctx) -> Batch:
 # ----------------------------------------------------------------------- joins
 def _cid(e: Expr):
     return e.cid if isinstance(e, ColRef) else None
+
+
+def join_out_dist(kind: str, ld, rd):
+    """Placement of a rank-local join's output given the placement keys of
+    its inputs (``ld``/``rd``: ("hash", cid, ...) or None). A key column
+    describes the output's placement only when it can never be NULL-padded:
+    an outer join pads the non-preserved side with NULLs on whatever rank
+    the preserved row lives, so GROUP BY that column would form one NULL
+    group per rank. Inner / semi / anti keep both sides' keys (semi and anti
+    output only left columns anyway), LEFT only the left side's, RIGHT only
+    the right side's, FULL none."""
+    scheme = ld[0] if keyed(ld) else (rd[0] if keyed(rd) else None)
+    lk = tuple(ld[1:]) if keyed(ld) and ld[0] == scheme else ()
+    rk = tuple(rd[1:]) if keyed(rd) and rd[0] == scheme else ()
+    if kind in ("inner", "cross", "semi", "anti"):
+        keys = lk + tuple(c for c in rk if c not in lk)
+    elif kind == "left":
+        keys = lk
+    elif kind == "right":
+        keys = rk
+    else:
+        keys = ()
+    return (scheme,) + keys if keys else None
 
 
 def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[int, int]] = None):
@@ -376,9 +478,10 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
     if on:
         for le, re_ in on:
             lc, rc = _cid(le), _cid(re_)
-            if hashed_on(ld, lc) and hashed_on(rd, rc):
-                # co-partitioned: rank-local; the output is placed by both keys
-                return done(lb, rb, ld + tuple(c for c in rd[1:] if c not in ld))
+            if copartitioned(ld, lc, rd, rc):
+                # co-partitioned: rank-local; the output is placed by the keys
+                # of the sides that are never NULL-padded
+                return done(lb, rb, join_out_dist(kind, ld, rd))
     if kind in ("inner", "cross") and (rep_l or rep_r):
         return done(lb, rb, rd if rep_l else ld)
     if kind in ("left", "semi", "anti") and rep_r:
@@ -434,7 +537,11 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
         rb = local_slice(rb, rk, ctx, rc)
     elif not (hashed_on(rd, rc) and lcol.dtype == rcol.dtype):
         rb = shuffle(rb, rk, ctx, rc)
-    return done(lb, rb, ("hash",) + tuple(c for c in (lc, rc) if c is not None) if lc is not None else None)
+    # a key converted to a common type (decimal scales) is no longer placed by
+    # the hash of its own column's values
+    same = lcol.dtype == rcol.dtype
+    return done(lb, rb, join_out_dist(kind, ("hash", lc) if lc is not None and same else None,
+                                      ("hash", rc) if rc is not None and same else None))
 
 
 #: largest global key span a semi / anti join filters through a dense
@@ -504,10 +611,11 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     d = dist_of(b)
     if d == REPLICATED:
         return with_dist(aggregate(groups, aggs, b, ctx), REPLICATED)
-    if d and d[0] == "hash":
+    if keyed(d):
         for ci, e in groups:
-            if isinstance(e, ColRef) and hashed_on(d, e.cid):
-                return with_dist(aggregate(groups, aggs, b, ctx), ("hash", ci.cid))
+            if isinstance(e, ColRef) and placed_on(d, e.cid):
+                # every group lives on one rank: the local aggregate is final
+                return with_dist(aggregate(groups, aggs, b, ctx), (d[0], ci.cid))
     ev = ctx.evaluator
     if not decomposable(aggs):
         if groups:
@@ -521,19 +629,78 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     pb = local(groups, partial) if local is not None else None
     if pb is None:
         pb = aggregate(groups, partial, b, ctx)
-    # ---- exchange partial states: all-reduce over a small dense key domain
-    # (global aggregates, dictionary-coded group keys) else hash shuffle
-    rb = _dense_allreduce(groups, partial, pb, ctx)
+    # ---- exchange partial states. ONE all-gather agrees on the structure of
+    # the partial batch (validity, dictionary vs plain, 64 vs 128-bit sums,
+    # shared dictionary codes) and carries the local ranges of the integer
+    # group keys; from that, alike on every rank: an all-reduce over a small
+    # dense key domain (global aggregates, dictionary / boolean / small-range
+    # integer keys: TPC-H Q1, Q4, Q9's year x nation, Q13's order counts) or
+    # a hash shuffle by the group key
+    dense_plan = _dense_candidate(groups, partial)
+    extra = _int_key_ranges(groups, pb) if dense_plan else []
+    pbn = normalize_structure(materialized(pb), ctx.comm, extra)
+    rb = _dense_allreduce(groups, partial, pbn, ctx) if dense_plan else None
     out_dist = REPLICATED if rb is not None else None
     if rb is None and groups:
         g0 = groups[0][0]
-        rb = shuffle(pb, partition_keys(pb.columns[g0.cid]), ctx, g0.cid)
+        key, cid = _shuffle_key(groups, pbn)
+        rb = shuffle(pbn, key, ctx, cid, normalized=True)
+        out_dist = rb.dist
     elif rb is None:
-        rb = gather_all(pb, ctx)
+        rb = gather_all(pbn, ctx, normalized=True)
         out_dist = REPLICATED
     # ---- phase 2: merge
     res = merge_partials(groups, plan, rb, ids, ctx)
-    return with_dist(res, out_dist if out_dist is not None else ("hash", groups[0][0].cid))
+    return with_dist(res, out_dist)
+
+
+def _shuffle_key(groups, b: Batch):
+    """Partition key of a shuffle by the group keys: the first key's, unless
+    it is a low-cardinality type (dictionary string, boolean) and more keys
+    follow -- then a mix of all of them (TPC-H Q16 groups by brand, type,
+    size: 25 brands would leave ranks idle). Returns (key, placement cid or
+    None for a mixed key)."""
+    cols = [b.columns[ci.cid] for ci, _ in groups]
+    c0 = cols[0]
+    if len(cols) == 1 or not (c0.is_dict or c0.dtype.kind == "bool"):
+        return partition_keys(c0), groups[0][0].cid
+    key = None
+    for c in cols:
+        k = partition_keys(c).to(torch.int64)
+        key = k if key is None else key * 1000003 + k
+    return key.contiguous(), None
+
+
+def _dense_candidate(groups, partial) -> bool:
+    """Plan-level part of the dense all-reduce test (alike on every rank)."""
+    for _, a in partial:
+        if a.func not in ("sum", "count", "min", "max", "bool_and", "bool_or") or a.dtype.is_string:
+            return False
+    for ci, _ in groups:
+        t = ci.dtype
+        if not (t.is_string or t.kind == "bool" or t.kind == "date32" or (t.is_integer and not t.is_decimal)):
+            return False
+    return True
+
+
+def _is_int_key(ci) -> bool:
+    t = ci.dtype
+    return not t.is_string and t.kind != "bool" and (t.kind == "date32" or t.is_integer)
+
+
+def _int_key_ranges(groups, pb: Batch) -> List[int]:
+    """[lo, hi] of every integer-typed group key over this rank's partial
+    groups (an empty rank reports an empty range)."""
+    from ..ops import hashing as H
+    out = []
+    for ci, _ in groups:
+        if not _is_int_key(ci):
+            continue
+        c = pb.columns[ci.cid]
+        rng = H.key_range(c.data.to(torch.int64) if c.data.dtype not in (torch.int32, torch.int64) else c.data,
+                          c.valid) if pb.num_rows and c.data.dim() == 1 else None
+        out += list(rng) if rng else [2**62, -2**62]
+    return out
 
 
 def decomposable(aggs) -> bool:
@@ -609,38 +776,48 @@ _I64_MAX, _I64_MIN = 2**63 - 1, -2**63
 
 def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
     """Two-phase aggregation over a small dense key domain (no GROUP BY, or
-    dictionary-coded / boolean group keys whose dictionary sizes multiply to
-    at most DENSE_ALLREDUCE_MAX, e.g. TPC-H Q1's returnflag x linestatus):
-    every rank scatters its partial states into dense per-key arrays and ONE
-    all-reduce per reduction op (SUM / MIN / MAX) merges them — no shuffle,
-    and the result is replicated on every rank (so a following ORDER BY needs
-    no gather). Returns the merged partial-state batch or None when the shape
-    does not apply (128-bit sums, strings, large domains)."""
+    group keys that are dictionary strings, booleans or integers whose
+    domains multiply to at most DENSE_ALLREDUCE_MAX, e.g. TPC-H Q1's
+    returnflag x linestatus, Q13's order counts): every rank scatters its
+    partial states into dense per-key arrays and ONE all-reduce per
+    reduction op (SUM / MIN / MAX) merges them -- no shuffle, and the result
+    is replicated on every rank (so a following ORDER BY needs no gather).
+    ``pb`` comes from ``normalize_structure`` (identical structure on every
+    rank; its preamble holds every rank's integer-key ranges), so every rank
+    takes the same decision. Integer SUMs travel as three int64 parts (high
+    word, low word's two 32-bit halves) that cannot overflow and recombine
+    into exact 128-bit sums. Returns the merged partial-state batch or None
+    when the shape does not apply."""
     comm = ctx.comm
     dev = ctx.device
     cols = [pb.columns[ci.cid] for ci, _ in partial]
-    for (ci, a), c in zip(partial, cols):
-        if a.func not in ("sum", "count", "min", "max", "bool_and", "bool_or") or c.is_wide or c.dtype.is_string \
-                or c.data.dim() != 1:
-            return None
-    # group keys -> dense index (structure agreement first: every rank decides alike)
     keys = [pb.columns[ci.cid] for ci, _ in groups]
-    if any(not (k.is_dict or k.dtype.kind == "bool") for k in keys):
+    if any(k.dtype.is_string and not k.is_dict for k in keys):
         return None
-    sig = comm.allgather_ints([int(k.valid is not None) for k in keys] + [int(pb.num_rows)])
-    nullable = [any(r[j] for r in sig) for j in range(len(keys))]
-    keys = unify_dictionaries(keys, comm) if keys else keys
-    sizes = [(len(k.dictionary) if k.is_dict else 2) + (1 if nullable[j] else 0) for j, k in enumerate(keys)]
+    ranges = [list(r) for r in pb.preamble]
+    sizes, offs, ri = [], [], 0
+    for (ci, _), k in zip(groups, keys):
+        nullable = k.valid is not None
+        if _is_int_key(ci):
+            lo = min(r[ri] for r in ranges)
+            hi = max(r[ri + 1] for r in ranges)
+            ri += 2
+            span = hi - lo + 1 if lo <= hi else 1
+            offs.append(lo if lo <= hi else 0)
+        else:
+            span = len(k.dictionary) if k.is_dict else 2
+            offs.append(0)
+        sizes.append(max(span, 1) + (1 if nullable else 0))
     domain = 1
     for z in sizes:
-        domain *= max(z, 1)
-    if domain > DENSE_ALLREDUCE_MAX:
-        return None
+        domain *= z
+        if domain > DENSE_ALLREDUCE_MAX:
+            return None
     n = pb.num_rows
     idx = torch.zeros(n, dtype=torch.int64, device=dev)
     for j, k in enumerate(keys):
-        code = k.data.to(torch.int64)
-        if nullable[j] and k.valid is not None:
+        code = k.data.to(torch.int64) - offs[j]
+        if k.valid is not None:
             code = torch.where(k.valid, code, torch.full_like(code, sizes[j] - 1))
         idx = idx * sizes[j] + code
     isum, fsum, imin, imax, fmin, fmax = [], [], [], [], [], []
@@ -657,12 +834,23 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
     for (ci, a), c in zip(partial, cols):
         isf = c.data.dtype in (torch.float32, torch.float64)
         valid = c.valid if c.valid is not None else torch.ones(n, dtype=torch.bool, device=dev)
-        vcount = dense(valid.to(torch.int64), 0, torch.int64)
-        isum.append(vcount)
-        if a.func in ("sum", "count"):
-            v = torch.where(valid, c.data, torch.zeros_like(c.data))
-            lst = fsum if isf else isum
-            lst.append(dense(v, 0, torch.float64 if isf else torch.int64))
+        isum.append(dense(valid.to(torch.int64), 0, torch.int64))
+        vi = len(isum) - 1
+        if a.func in ("sum", "count") and not isf:
+            # exact: hi word + the low word's 32-bit halves, each summed in int64
+            if c.is_wide:
+                lo_w, hi_w = c.data[:, 0], c.data[:, 1]
+            else:
+                lo_w = c.data.to(torch.int64)
+                hi_w = lo_w >> 63
+            z = torch.zeros_like(lo_w)
+            first = len(isum)
+            for part in (hi_w, (lo_w >> 32) & 0xFFFFFFFF, lo_w & 0xFFFFFFFF):
+                isum.append(dense(torch.where(valid, part, z), 0, torch.int64))
+            slots.append(("wide", first, vi))
+        elif a.func in ("sum", "count"):
+            fsum.append(dense(torch.where(valid, c.data, torch.zeros_like(c.data)), 0, torch.float64))
+            slots.append(("fsum", len(fsum) - 1, vi))
         else:
             is_min = a.func in ("min", "bool_and")
             fill = (float("inf") if is_min else float("-inf")) if isf else (_I64_MAX if is_min else _I64_MIN)
@@ -670,15 +858,15 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
                             torch.full((n,), fill, dtype=torch.float64 if isf else torch.int64, device=dev))
             lst = (fmin if is_min else fmax) if isf else (imin if is_min else imax)
             lst.append(dense(v, fill, torch.float64 if isf else torch.int64))
-        slots.append((lst, len(lst) - 1, len(isum) - 1))
+            slots.append(({id(fmin): "fmin", id(fmax): "fmax", id(imin): "imin", id(imax): "imax"}[id(lst)],
+                          len(lst) - 1, vi))
     red = {}
     for name, lst, op in (("isum", isum, "sum"), ("fsum", fsum, "sum"), ("imin", imin, "min"), ("imax", imax, "max"),
                           ("fmin", fmin, "min"), ("fmax", fmax, "max")):
         if lst:
-            red[id(lst)] = comm.allreduce_tensor(torch.stack(lst), op)
-    present = mask_idx = None
-    tot = red[id(isum)]
+            red[name] = comm.allreduce_tensor(torch.stack(lst), op)
     from ..ops.select import mask_to_indices
+    tot = red["isum"]
     mask_idx = mask_to_indices(tot[0] > 0)
     m = mask_idx.numel()
     out = {}
@@ -688,22 +876,33 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
         rest = rest // sizes[j]
         k = keys[j]
         valid = None
-        if nullable[j]:
+        if k.valid is not None:
             valid = code != sizes[j] - 1
             code = torch.where(valid, code, torch.zeros_like(code))
         ci = groups[j][0]
         if k.is_dict:
             out[ci.cid] = Column(k.dtype, code.to(torch.int32), valid, dictionary=k.dictionary)
-        else:
+        elif k.dtype.kind == "bool":
             out[ci.cid] = Column(k.dtype, code.to(torch.bool), valid)
-    for ((ci, a), c), (lst, li, vi) in zip(zip(partial, cols), slots):
-        vals = gather_tensor(red[id(lst)][li], mask_idx)
-        has = gather_tensor(tot[vi], mask_idx) > 0
-        if a.func == "count":
-            out[ci.cid] = Column(c.dtype, vals.to(torch.int64))
         else:
-            data = vals.to(c.data.dtype) if c.dtype.kind != "bool" else vals != 0
-            out[ci.cid] = Column(c.dtype, torch.where(has, data, torch.zeros_like(data)), has)
+            out[ci.cid] = Column(k.dtype, (code + offs[j]).to(k.data.dtype), valid)
+    sign = -(2**63)
+    for ((ci, a), c), (kind, li, vi) in zip(zip(partial, cols), slots):
+        has = gather_tensor(tot[vi], mask_idx) > 0
+        if kind == "wide":
+            hi, mid, low = (gather_tensor(tot[li + t], mask_idx) for t in range(3))
+            lo = low + ((mid & 0xFFFFFFFF) << 32)                     # wraps as uint64
+            carry = ((lo ^ sign) < (low ^ sign)).to(torch.int64)      # unsigned overflow of that add
+            hi = hi + (mid >> 32) + carry
+            if a.func == "count":
+                out[ci.cid] = Column(c.dtype, lo)
+                continue
+            from ..ops.agg import _wide_to_result
+            out[ci.cid] = Column(c.dtype, _wide_to_result(lo.contiguous(), hi.contiguous()), has)
+            continue
+        vals = gather_tensor(red[kind][li], mask_idx)
+        data = vals.to(c.data.dtype) if c.dtype.kind != "bool" else vals != 0
+        out[ci.cid] = Column(c.dtype, torch.where(has, data, torch.zeros_like(data)), has)
     return Batch(out, m)
 
 

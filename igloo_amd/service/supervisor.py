@@ -159,6 +159,31 @@ class NodeSupervisor:
                 p.kill()
 
 
+def count_gpus(env=None, topology: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """Visible GPUs, counted WITHOUT touching the HIP runtime (the supervisor
+    forks and execs worker generations, which a GPU-initialised process must
+    not do): an explicit ``*_VISIBLE_DEVICES`` list wins, else the KFD
+    topology's nodes with SIMDs (CPU nodes report ``simd_count 0``)."""
+    env = os.environ if env is None else env
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() and x.strip() != "-1"])
+    n = 0
+    try:
+        for node in sorted(os.listdir(topology)):
+            try:
+                with open(os.path.join(topology, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    return n
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="igloo-node", description=__doc__.split("\n\n")[0])
     ap.add_argument("--devices", default=None,
@@ -170,8 +195,7 @@ def main(argv=None) -> int:
     a, rest = ap.parse_known_args(argv)
     devs = a.devices.split(",") if a.devices else None
     if devs is None:
-        import torch   # counting devices does not initialise the GPU runtime
-        n = torch.cuda.device_count()
+        n = count_gpus()
         devs = [f"cuda:{i}" for i in range(n)] or ["cpu"]
     sup = NodeSupervisor(devs, a.coordinator, rest, min_world=a.min_world, max_generations=a.max_generations,
                          grace_s=a.grace_s)

@@ -30,9 +30,11 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
         # small data must still take the large-data paths (sorted joins, run ids, Bloom probes)
         from igloo_amd.exec import operators as O
         from igloo_amd.ops import hashing as H
+        from igloo_amd.parallel import slicing as SL
         O.SORTED_JOIN_MIN_ROWS = 1000
         H.SORTED_CHECK_ROWS = 1000
         H.BLOOM_MIN_RATIO = 2
+        SL.SLICE_MIN_ROWS = 1000
     comm = Communicator.init(backend="gloo", device=device, timeout_s=120)
     e = ig.QueryEngine(device=device, comm=comm)
     for name, t in datagen.generate(sf, device, rank, world, replicate_dims=replicate_dims).items():
@@ -66,13 +68,16 @@ def run_distributed(world, con, device="cpu", low_thresholds=False, replicate_di
     return check(res, qs, con)
 
 
-@pytest.mark.parametrize("world,replicate_dims", [(2, True), (3, True), (2, False), (3, False)])
-def test_tpch_distributed_gloo(world, replicate_dims, tpch_cpu):
+@pytest.mark.parametrize("world,replicate_dims,low", [(2, True, False), (3, True, True), (2, False, False),
+                                                      (3, False, False)])
+def test_tpch_distributed_gloo(world, replicate_dims, low, tpch_cpu):
     """Both multi-rank layouts: replicated dimension tables with fact tables
     co-partitioned by order key (the bench layout), and every table
-    hash-partitioned by its primary key (every shuffle / broadcast path)."""
+    hash-partitioned by its primary key (every shuffle / broadcast path).
+    ``low``: small data takes the large-data paths (sorted joins, key-range
+    slices of replicated tables for Q2 / Q11 / Q16)."""
     _, _, con = tpch_cpu
-    bad = run_distributed(world, con, replicate_dims=replicate_dims)
+    bad = run_distributed(world, con, replicate_dims=replicate_dims, low_thresholds=low)
     assert not bad, "\n".join(bad)
     calls = {int(q): r["collectives"] for q, r in run_distributed.last.items()}
     print("collectives per query:", calls)
@@ -109,6 +114,76 @@ def _num(x):
         except ValueError:
             return x
     return x
+
+
+_OUTER_SQL = {
+    "left": "SELECT t2.k AS rk, count(*) AS n, sum(t1.a) AS s FROM t1 LEFT JOIN t2 ON t1.k = t2.k "
+            "GROUP BY t2.k ORDER BY rk NULLS FIRST",
+    "right": "SELECT t1.k AS lk, count(*) AS n, sum(t2.b) AS s FROM t1 RIGHT JOIN t2 ON t1.k = t2.k "
+             "GROUP BY t1.k ORDER BY lk NULLS FIRST",
+    "full": "SELECT t1.k AS lk, count(*) AS n FROM t1 FULL JOIN t2 ON t1.k = t2.k "
+            "GROUP BY t1.k ORDER BY lk NULLS FIRST",
+    "full_r": "SELECT t2.k AS rk, count(*) AS n FROM t1 FULL JOIN t2 ON t1.k = t2.k "
+              "GROUP BY t2.k ORDER BY rk NULLS FIRST",
+}
+
+
+def _outer_tables(rank, world):
+    """t1 (k 0..99) and t2 (k 50..149, two rows per key), hash-partitioned by k
+    with the engine's partition function (a world of one holds everything)."""
+    import numpy as np
+    import pyarrow as pa
+    import torch
+    from igloo_amd.ops.misc import partition_ids
+    k1 = np.arange(100, dtype=np.int64)
+    k2 = np.repeat(np.arange(50, 150, dtype=np.int64), 2)
+
+    def mine(k):
+        if world == 1:
+            return np.ones(len(k), dtype=bool)
+        return partition_ids(torch.from_numpy(k), world).numpy() == rank
+    m1, m2 = mine(k1), mine(k2)
+    t1 = pa.table({"k": k1[m1], "a": (k1 * 3)[m1]})
+    t2 = pa.table({"k": k2[m2], "b": (k2 + 1)[m2]})
+    return t1, t2
+
+
+def _outer_worker(rank, world, port, out_path):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import igloo_amd as ig
+    from igloo_amd.catalog import MemoryTable
+    from igloo_amd.parallel.comm import Communicator
+    comm = Communicator.init(backend="gloo", device="cpu", timeout_s=120)
+    e = ig.QueryEngine(device="cpu", comm=comm)
+    t1, t2 = _outer_tables(rank, world)
+    e.register_table("t1", MemoryTable.from_arrow(t1, partitioned_by="k"))
+    e.register_table("t2", MemoryTable.from_arrow(t2, partitioned_by="k"))
+    res = {name: e.query(sql).to_pylist() for name, sql in _OUTER_SQL.items()}
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    comm.shutdown()
+
+
+def test_outer_join_null_group_placement():
+    """GROUP BY the NULL-padded side's key of a co-partitioned outer join:
+    NULL-padded rows live on every rank, so the key must not be taken as the
+    output's placement (one NULL group, not one per rank)."""
+    import igloo_amd as ig
+    from igloo_amd.catalog import MemoryTable
+    e = ig.QueryEngine(device="cpu")
+    t1, t2 = _outer_tables(0, 1)
+    e.register_table("t1", MemoryTable.from_arrow(t1))
+    e.register_table("t2", MemoryTable.from_arrow(t2))
+    want = {name: e.query(sql).to_pylist() for name, sql in _OUTER_SQL.items()}
+    assert sum(r["rk"] is None for r in want["left"]) == 1
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.json")
+        mp.start_processes(_outer_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+        got = json.load(open(out))
+    for name in _OUTER_SQL:
+        assert got[name] == want[name], name
 
 
 def _wide_worker(rank, world, port, out_path):

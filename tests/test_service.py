@@ -323,3 +323,17 @@ def test_rank_death_recovers_on_surviving_ranks_of_the_node():
     finally:
         sup.shutdown()
         co.shutdown()
+
+
+def test_supervisor_counts_gpus_without_hip(tmp_path):
+    """The node supervisor counts devices from the environment or the KFD
+    topology (never through the HIP runtime: it forks worker generations)."""
+    from igloo_amd.service.supervisor import count_gpus
+    assert count_gpus({"HIP_VISIBLE_DEVICES": "0,3,5"}) == 3
+    assert count_gpus({"ROCR_VISIBLE_DEVICES": ""}) == 0
+    topo = tmp_path / "nodes"
+    for i, simds in enumerate([0, 256, 256]):
+        (topo / str(i)).mkdir(parents=True)
+        (topo / str(i) / "properties").write_text(f"cpu_cores_count {4 if not simds else 0}\nsimd_count {simds}\n")
+    assert count_gpus({}, str(topo)) == 2
+    assert count_gpus({}, str(tmp_path / "missing")) == 0
