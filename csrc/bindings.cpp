@@ -127,6 +127,7 @@ kern::PqDecodeSpec decode_spec(const py::dict& d, bool need_output = true) {
 
 namespace igloo {
 void register_jit(py::module_& m);  // runtime/jit.cpp
+void register_arrow_device(py::module_& m);  // runtime/arrow_device.cpp
 }
 
 PYBIND11_MODULE(_native, m) {
@@ -136,6 +137,7 @@ PYBIND11_MODULE(_native, m) {
   m.attr("MAX_GATHER_COLS") = kern::kMaxGatherCols;
   m.attr("MAX_PARTS") = kern::kMaxParts;
   igloo::register_jit(m);
+  igloo::register_arrow_device(m);
 
   // ------------------------------------------------------------------ SQL
   m.def("parse_sql", &parse, "Parse SQL text into a list of statement ASTs (dicts)");

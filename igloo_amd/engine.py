@@ -237,6 +237,20 @@ class QueryEngine:
     def query(self, sql: str) -> pa.Table:
         return self.sql(sql).table
 
+    def sql_device(self, sql: str):
+        """Run a query and leave its result in device memory: a
+        ``interop.DeviceResult`` exported zero-copy through the Arrow C Device
+        Data Interface (``__arrow_c_device_array__``) and DLPack, instead of
+        the host Arrow table ``sql`` returns."""
+        from .interop import DeviceResult
+        plan, names = self.logical_plan(sql)
+        with self._lock:
+            batch = self._execute_plan(plan, self.make_context())
+        cols = {}
+        for ci, nm in zip(plan.schema, names):
+            cols[nm] = batch.columns[ci.cid]
+        return DeviceResult(cols, batch.num_rows, {nm: ci.nullable for ci, nm in zip(plan.schema, names)})
+
     def sql(self, sql: str) -> QueryResult:
         key = None
         if PLAN_CACHE:

@@ -75,6 +75,39 @@ class IglooClient:
     def tables(self) -> List[str]:
         return [f.descriptor.path[0].decode() for f in self.client.list_flights(options=self.options)]
 
+    # ------------------------------------------------------------ Flight SQL
+    def _fsql(self, cmd: bytes) -> pa.Table:
+        info = self.client.get_flight_info(fl.FlightDescriptor.for_command(cmd), self.options)
+        tables = [self.client.do_get(ep.ticket, self.options).read_all() for ep in info.endpoints]
+        return pa.concat_tables(tables) if len(tables) > 1 else (tables[0] if tables else info.schema.empty_table())
+
+    def sql_info(self, ids=()) -> dict:
+        """CommandGetSqlInfo: {info id: value}."""
+        body = b"".join(P.pb_field(1, int(i)) for i in ids)
+        t = self._fsql(P.pack_any("CommandGetSqlInfo", body))
+        return {r["info_name"]: r["value"] for r in t.to_pylist()}
+
+    def get_tables(self, table_pattern: Optional[str] = None, table_types=(), include_schema: bool = False
+                   ) -> pa.Table:
+        """CommandGetTables (LIKE pattern on the table name)."""
+        body = (P.pb_field(3, table_pattern) if table_pattern is not None else b"") + \
+            b"".join(P.pb_field(4, t) for t in table_types) + (P.pb_field(5, 1) if include_schema else b"")
+        return self._fsql(P.pack_any("CommandGetTables", body))
+
+    def get_catalogs(self) -> pa.Table:
+        return self._fsql(P.pack_any("CommandGetCatalogs", b""))
+
+    def get_db_schemas(self) -> pa.Table:
+        return self._fsql(P.pack_any("CommandGetDbSchemas", b""))
+
+    def prepare(self, sql: str) -> "PreparedStatement":
+        """ActionCreatePreparedStatement: a server-side prepared statement."""
+        res = self.action("CreatePreparedStatement", P.pack_any("ActionCreatePreparedStatementRequest",
+                                                                 P.pb_field(1, sql)))
+        body = P.pb_decode(P.pb_decode(res)[2][0])
+        schema = pa.ipc.read_schema(pa.py_buffer(body[2][0])) if body.get(2) and body[2][0] else None
+        return PreparedStatement(self, body[1][0], schema)
+
     # --------------------------------------------------------- control plane
     def action(self, kind: str, body: bytes = b"") -> bytes:
         res = list(self.client.do_action(fl.Action(kind, body), self.options))
@@ -113,6 +146,39 @@ class IglooClient:
 
     def explain(self, sql: str) -> str:
         return self.action("explain", sql.encode()).decode()
+
+
+class PreparedStatement:
+    """A Flight SQL prepared statement; ``execute(params)`` binds the ``?``
+    placeholders (DoPut) and runs it (GetFlightInfo + DoGet)."""
+
+    def __init__(self, client: IglooClient, handle: bytes, schema: Optional[pa.Schema]):
+        self.client, self.handle, self.schema = client, bytes(handle), schema
+
+    def _cmd(self) -> bytes:
+        return P.pack_any("CommandPreparedStatementQuery", P.pb_field(1, self.handle))
+
+    def execute(self, params=None) -> pa.Table:
+        if params is not None:
+            t = params if isinstance(params, pa.Table) else \
+                pa.table({f"p{i + 1}": [v] for i, v in enumerate(params)})
+            w, r = self.client.client.do_put(fl.FlightDescriptor.for_command(self._cmd()), t.schema,
+                                             self.client.options)
+            w.write_table(t)
+            w.done_writing()
+            r.read()
+            w.close()
+        return self.client._fsql(self._cmd())
+
+    def close(self) -> None:
+        self.client.action("ClosePreparedStatement", P.pack_any("ActionClosePreparedStatementRequest",
+                                                                P.pb_field(1, self.handle)))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def main(argv=None) -> int:

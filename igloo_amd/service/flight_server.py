@@ -14,8 +14,16 @@ Parity: reference crates/api/src/lib.rs:40-184 (IglooFlightSqlService):
   DoPut ingests a table into the HBM tier, and Handshake/middleware check an
   optional bearer token (reference auth.proto is an empty stub).
 
-Flight SQL: ``CommandStatementQuery`` / ``TicketStatementQuery`` (protobuf Any)
-are decoded by ``protocol.unpack_any`` (no Flight SQL library ships here).
+Flight SQL (protobuf ``Any`` commands decoded by ``protocol.unpack_any``; no
+Flight SQL library ships here; service/flight_sql.py): statements
+(``CommandStatementQuery`` / ``TicketStatementQuery``), metadata
+(``CommandGetSqlInfo``, ``GetCatalogs``, ``GetDbSchemas``, ``GetTables`` with
+or without schemas, ``GetTableTypes``, primary / exported / imported keys,
+cross reference), prepared statements (DoAction ``CreatePreparedStatement`` /
+``ClosePreparedStatement``, ``CommandPreparedStatementQuery`` with ``?``
+parameters bound by DoPut) and updates (DoPut ``CommandStatementUpdate`` /
+``CommandPreparedStatementUpdate``). GetFlightInfo and GetSchema answer every
+command from its plan or fixed schema without running it.
 """
 from __future__ import annotations
 
@@ -30,6 +38,7 @@ import pyarrow.flight as fl
 
 from ..utils.errors import CommError, DeviceError, IglooError, PlanError, SqlParseError, TableNotFound
 from ..utils.log import get_logger
+from . import flight_sql as FS
 from . import protocol as P
 
 log = get_logger("flight")
@@ -68,6 +77,8 @@ class IglooFlightServer(fl.FlightServerBase):
         self._session_lock = threading.Lock()   # per-request session settings (execute_query)
         self.metrics = {"queries": 0, "rows": 0, "errors": 0, "ms": 0.0}
         self._location = location
+        self.prepared = FS.PreparedStatements()
+        self.meta = FS.Metadata(engine) if engine is not None else None
 
     def start_background(self, timeout_s: float = 30.0, host: str = "127.0.0.1") -> "IglooFlightServer":
         """Serve on a daemon thread and return once the endpoint answers."""
@@ -104,6 +115,33 @@ class IglooFlightServer(fl.FlightServerBase):
             return b.decode("utf-8"), False, None
         except UnicodeDecodeError:
             raise ValueError("ticket/command is not valid UTF-8") from None
+
+    @staticmethod
+    def _flight_sql(b: bytes):
+        """(command name, fields) of a Flight SQL command other than a
+        statement query / ticket, else None."""
+        a = P.unpack_any(b) if b else None
+        if a is None or a[0] in ("CommandStatementQuery", "TicketStatementQuery"):
+            return None
+        return a
+
+    def _command_schema(self, name: str, f) -> pa.Schema:
+        sch = FS.metadata_schema(name, f)
+        if sch is not None:
+            return sch
+        if name == "CommandPreparedStatementQuery":
+            h = f.get(1, [b""])[0]
+            st = self.prepared.get(h)
+            if st["schema"] is None:
+                if not _is_query(st["sql"]):
+                    raise ValueError("prepared statement is an update: it has no result set (DoPut it)")
+                st["schema"] = self._schema_of(self.prepared.sql_of(h))
+            return st["schema"]
+        raise NotImplementedError(f"Flight SQL command {name} is not supported")
+
+    def _version(self) -> str:
+        from .. import __version__
+        return __version__
 
     def _run_with_session(self, sql: str, session_config) -> pa.Table:
         """Run with the request's session settings applied for this query only."""
@@ -155,6 +193,12 @@ class IglooFlightServer(fl.FlightServerBase):
         else:
             if not descriptor.command:
                 raise ValueError("empty SQL command")
+            cmd = self._flight_sql(descriptor.command)
+            if cmd is not None:
+                # metadata / prepared statements: the command itself is the ticket
+                schema = self._command_schema(*cmd)
+                return fl.FlightInfo(schema, descriptor,
+                                     [fl.FlightEndpoint(fl.Ticket(descriptor.command), [self._location])], -1, -1)
             sql, flight_sql, _ = self._sql_from_bytes(descriptor.command)
             if not sql.strip():
                 raise ValueError("empty SQL command")
@@ -169,10 +213,25 @@ class IglooFlightServer(fl.FlightServerBase):
         return fl.FlightInfo(schema, descriptor, [fl.FlightEndpoint(ticket, [self._location])], -1, -1)
 
     def get_schema(self, context, descriptor):
+        if descriptor.descriptor_type == fl.DescriptorType.PATH:
+            name = descriptor.path[0].decode() if isinstance(descriptor.path[0], bytes) else descriptor.path[0]
+            return fl.SchemaResult(self._schema_of(f"SELECT * FROM {name}"))
+        cmd = self._flight_sql(descriptor.command)
+        if cmd is not None:
+            return fl.SchemaResult(self._command_schema(*cmd))
         sql, _, _ = self._sql_from_bytes(descriptor.command)
         return fl.SchemaResult(self._schema_of(sql))
 
     def do_get(self, context, ticket):
+        cmd = self._flight_sql(ticket.ticket)
+        if cmd is not None:
+            name, f = cmd
+            if name == "CommandPreparedStatementQuery":
+                sql = self.prepared.sql_of(f.get(1, [b""])[0])
+                return fl.RecordBatchStream(self._run(sql))
+            if self.meta is None:
+                raise NotImplementedError("this endpoint has no catalog")
+            return fl.RecordBatchStream(FS.metadata_result(self.meta, name, f, self._version()))
         sql, flight_sql, handle = self._sql_from_bytes(ticket.ticket)
         if handle is not None:
             with self._lock:
@@ -188,6 +247,30 @@ class IglooFlightServer(fl.FlightServerBase):
         return fl.RecordBatchStream(t)
 
     def do_put(self, context, descriptor, reader, writer):
+        if descriptor.descriptor_type == fl.DescriptorType.CMD:
+            cmd = P.unpack_any(descriptor.command)
+            if cmd is None:
+                raise ValueError("DoPut command is not a Flight SQL command")
+            name, f = cmd
+            if name == "CommandPreparedStatementQuery":
+                # bind parameter values (first row) for the next execution
+                h = f.get(1, [b""])[0]
+                self.prepared.bind(h, reader.read_all())
+                writer.write(pa.py_buffer(P.pb_field(1, h)))     # DoPutPreparedStatementResult
+                return
+            if name == "CommandStatementUpdate":
+                sql = f.get(1, [b""])[0].decode()
+            elif name == "CommandPreparedStatementUpdate":
+                h = f.get(1, [b""])[0]
+                self.prepared.bind(h, reader.read_all())
+                sql = self.prepared.sql_of(h)
+            else:
+                raise NotImplementedError(f"Flight SQL DoPut command {name} is not supported")
+            res = self.engine.sql(sql)
+            t = res.table
+            n = int(t.column("count")[0].as_py()) if "count" in t.column_names and t.num_rows else -1
+            writer.write(pa.py_buffer(FS.encode_update_result(n)))
+            return
         name = descriptor.path[0].decode() if isinstance(descriptor.path[0], bytes) else descriptor.path[0]
         t = reader.read_all()
         self.engine.register_table(name, t)
@@ -208,7 +291,9 @@ class IglooFlightServer(fl.FlightServerBase):
                 ("execute_task", "TaskDefinition -> TaskStatus"), ("get_data_for_task", "DataForTaskRequest -> IPC"),
                 ("list_workers", "-> workers JSON"), ("metrics", "-> metrics JSON"), ("explain", "SQL -> plan text"),
                 ("execute_fragment", "serialized fragment + input IPC -> IPC batch stream + QueryComplete"),
-                ("execute_query", "QueryRequest JSON -> IPC batch stream + QueryComplete"), ("health", "-> ok")]
+                ("execute_query", "QueryRequest JSON -> IPC batch stream + QueryComplete"), ("health", "-> ok"),
+                ("CreatePreparedStatement", "Flight SQL ActionCreatePreparedStatementRequest -> Result"),
+                ("ClosePreparedStatement", "Flight SQL ActionClosePreparedStatementRequest")]
 
     def do_action(self, context, action):
         kind, body = action.type, action.body.to_pybytes() if action.body is not None else b""
@@ -274,8 +359,35 @@ class IglooFlightServer(fl.FlightServerBase):
                 yield fl.Result(chunk)
         elif kind == "health":
             yield fl.Result(b"ok")
+        elif kind == "CreatePreparedStatement":
+            a = P.unpack_any(body)
+            if a is None or a[0] != "ActionCreatePreparedStatementRequest":
+                raise ValueError("CreatePreparedStatement expects an ActionCreatePreparedStatementRequest")
+            sql = a[1].get(1, [b""])[0].decode()
+            n = FS.count_params(sql)
+            schema = None
+            if _is_query(sql):
+                try:
+                    # the result schema from the plan (placeholders planned as NULL literals)
+                    schema = self._schema_of(FS.bind_params(sql, [None] * n) if n else sql)
+                except ValueError:
+                    if not n:
+                        raise            # an invalid query fails at prepare time
+                    # (a placeholder NULL cannot be planned there, e.g. LIMIT ?: planned once bound)
+            h, _ = self.prepared.create(sql, schema)
+            yield fl.Result(FS.encode_prepared_result(h, schema, FS.parameter_schema(n) if n else None))
+        elif kind == "ClosePreparedStatement":
+            a = P.unpack_any(body)
+            if a is None or a[0] != "ActionClosePreparedStatementRequest":
+                raise ValueError("ClosePreparedStatement expects an ActionClosePreparedStatementRequest")
+            self.prepared.close(a[1].get(1, [b""])[0])
         else:
             raise NotImplementedError(f"unknown action {kind}")
 
     def do_exchange(self, context, descriptor, reader, writer):
         raise NotImplementedError("DoExchange: intra-node exchanges use RCCL; inter-node shuffle is not enabled")
+
+
+def _is_query(sql: str) -> bool:
+    head = sql.lstrip().split(None, 1)[0].upper() if sql.strip() else ""
+    return head in ("SELECT", "WITH", "VALUES", "EXPLAIN", "(")

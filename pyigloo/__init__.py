@@ -11,8 +11,18 @@ the user-facing Python API over the native engine (pybind11 extension
     eng.register_parquet("t", "data/t.parquet")
     print(eng.sql("SELECT count(*) FROM t"))
 
-    with pyigloo.connect("grpc://127.0.0.1:50051") as conn:   # remote coordinator
+    res = eng.sql_device("SELECT a, b FROM t")  # result stays in HBM:
+    batch = pyarrow.record_batch(res)           #   Arrow C Device Data Interface (zero copy)
+    a = torch.from_dlpack(res.to_dlpack("a"))   #   or DLPack, per column
+
+    with pyigloo.connect("grpc://127.0.0.1:50051") as conn:   # remote coordinator (Flight SQL)
         table = conn.sql("SELECT 42 AS answer")                # -> pyarrow.Table
+        conn.get_tables("line%")                               # catalog metadata
+        with conn.prepare("SELECT * FROM t WHERE a = ?") as st:
+            st.execute([7])
+
+``pyigloo.native`` is the compiled core itself (SQL parser, gfx950 kernel
+launchers, device runtime, Arrow C Device exporter).
 """
 from __future__ import annotations
 
@@ -22,8 +32,10 @@ import igloo_amd as _ig
 from igloo_amd import Catalog, MemoryCatalog, MemoryTable, QueryEngine, QueryResult, hello  # noqa: F401
 from igloo_amd.utils.errors import IglooError  # noqa: F401
 
-__all__ = ["connect", "local", "sql", "Connection", "QueryEngine", "QueryResult", "Catalog", "MemoryCatalog",
-           "MemoryTable", "IglooError", "hello", "__version__"]
+from igloo_amd.interop import DeviceResult  # noqa: F401
+
+__all__ = ["connect", "local", "sql", "sql_device", "Connection", "QueryEngine", "QueryResult", "DeviceResult",
+           "Catalog", "MemoryCatalog", "MemoryTable", "IglooError", "hello", "native", "__version__"]
 __version__ = getattr(_ig, "__version__", "0.1.0")
 
 _default: Optional[QueryEngine] = None
@@ -37,15 +49,31 @@ def local(device: Optional[str] = None, **kw) -> QueryEngine:
     return QueryEngine(device=device, **kw)
 
 
-def sql(query: str, engine: Optional[QueryEngine] = None):
-    """Run ``query`` on ``engine`` (or a lazily created default local engine);
-    returns a pyarrow.Table."""
+def _engine(engine: Optional[QueryEngine]) -> QueryEngine:
     global _default
     if engine is None:
         if _default is None:
             _default = local()
         engine = _default
-    return engine.query(query)
+    return engine
+
+
+def sql(query: str, engine: Optional[QueryEngine] = None):
+    """Run ``query`` on ``engine`` (or a lazily created default local engine);
+    returns a pyarrow.Table."""
+    return _engine(engine).query(query)
+
+
+def sql_device(query: str, engine: Optional[QueryEngine] = None) -> DeviceResult:
+    """Run ``query`` and keep the result on the device (zero-copy export)."""
+    return _engine(engine).sql_device(query)
+
+
+def __getattr__(name):
+    if name == "native":        # the compiled core, loaded on first use
+        from igloo_amd.ops._lib import native as _native
+        return _native()
+    raise AttributeError(name)
 
 
 class Connection:
@@ -63,6 +91,17 @@ class Connection:
 
     def tables(self):
         return self._client.tables()
+
+    def get_tables(self, pattern: Optional[str] = None, include_schema: bool = False):
+        """Flight SQL CommandGetTables -> pyarrow.Table."""
+        return self._client.get_tables(pattern, include_schema=include_schema)
+
+    def sql_info(self, ids=()) -> dict:
+        return self._client.sql_info(ids)
+
+    def prepare(self, query: str):
+        """A server-side prepared statement (``?`` placeholders)."""
+        return self._client.prepare(query)
 
     def upload(self, name: str, table) -> None:
         self._client.upload(name, table)
