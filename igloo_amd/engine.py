@@ -495,7 +495,10 @@ class QueryEngine:
             if comm is not None:
                 comm.calls += g.comm_calls
                 comm.bytes_sent += g.comm_bytes
-            if not agree(not ok, True)[0]:
+            # a checked graph's mismatch count is already summed over the ranks
+            # inside the graph: every rank read the same value
+            any_bad = (not ok) if (g.checked and g.global_check) else agree(not ok, True)[0]
+            if not any_bad:
                 g.checked = True
                 self._touch_graph(st)
                 return g.batch, "graph", st, table

@@ -88,7 +88,7 @@ class QueryGraph:
     mismatch counter of its replayed values."""
 
     __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp",
-                 "nbytes", "comm_calls", "comm_bytes", "keep")
+                 "nbytes", "comm_calls", "comm_bytes", "keep", "global_check")
 
     def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None, nbytes=0):
         self.sp = sp                   # the capture's speculation (sites + device values, for reports)
@@ -96,6 +96,7 @@ class QueryGraph:
         self.comm_calls = 0            # collectives inside the graph (SPMD)
         self.comm_bytes = 0
         self.keep = []
+        self.global_check = False      # ``bad`` is summed over SPMD ranks inside the graph
         self.graph = graph
         self.batch = batch
         self.bad = bad
@@ -118,7 +119,7 @@ class QueryGraph:
         STATS["replays"] += 1
         ctx.rows_scanned = self.rows_scanned
         ctx.spill = dict(self.spill)
-        ok = int(self.bad.item()) == 0
+        ok = int(self.bad.reshape(-1)[0].item()) == 0
         if not ok:
             STATS["mismatch"] += 1
             try:
@@ -166,6 +167,12 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
                 if not sp.complete:
                     raise _lib.CaptureAbort("call sequence left the recording")
                 bad = sp.device_mismatches(expected)
+                comm = engine.comm
+                if comm is not None and comm.spmd:
+                    # SPMD: the mismatch count is summed over ranks inside the
+                    # graph, so the one readback after a replay is already the
+                    # agreement of every rank (no extra host round trip)
+                    bad = comm.allreduce_tensor(bad.reshape(1).to(torch.int64), "sum")
             finally:
                 g.capture_end()
     except _lib.CaptureAbort as e:
@@ -209,5 +216,6 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     STATS["captured"] += 1
     nbytes = max(0, torch.cuda.memory_reserved(dev) - reserved0)
     qg = QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp, nbytes)
+    qg.global_check = engine.comm is not None and engine.comm.spmd
     qg.keep = _lib.capture_keepalive()     # pinned host buffers its copy nodes read
     return qg

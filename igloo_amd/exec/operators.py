@@ -239,10 +239,15 @@ class ExecNode:
         if ctx.analyze:
             _sync(ctx)
             t0 = time.perf_counter()
+        c0 = (ctx.comm.calls, ctx.comm.bytes_sent) if ctx.analyze and ctx.comm is not None else (0, 0)
         out = self._run(ctx)
         if ctx.analyze:
             _sync(ctx)
-            ctx.metrics[id(self)] = {"ms": (time.perf_counter() - t0) * 1e3, "rows": out.num_rows}
+            m = {"ms": (time.perf_counter() - t0) * 1e3, "rows": out.num_rows, "dist": getattr(out, "dist", None)}
+            if ctx.comm is not None:
+                m["collectives"] = ctx.comm.calls - c0[0]
+                m["bytes"] = ctx.comm.bytes_sent - c0[1]
+            ctx.metrics[id(self)] = m
         return out
 
     def _run(self, ctx: ExecContext) -> Batch:  # pragma: no cover
@@ -2582,12 +2587,19 @@ class HashAggExec(ExecNode):
         return aggregate(lg.groups, lg.aggs, b, ctx)
 
 
-def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
+def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None) -> Batch:
+    """GROUP BY ``groups`` computing ``aggs`` over ``b``. ``row_parts``
+    ({output cid: part index} of a LateBatch ``b``): when the grouping runs
+    on the join result's index form (``_late_group_keys``: every other key is
+    functionally dependent on the leading integer key), each group's row in
+    those parts is added as an int64 column -- the SPMD exchange ships that
+    row instead of the part's string columns (parallel/exchange.py). The
+    columns are absent when the dependency did not hold."""
     ev = ctx.evaluator
     n = b.num_rows
     dev = ctx.device
     late = None
-    if groups and n and isinstance(b, LateBatch) and dev.type == "cuda":
+    if groups and n and isinstance(b, LateBatch) and (dev.type == "cuda" or row_parts):
         with ctx.span("agg.late_keys"):
             late = _late_group_keys(groups, b, ctx)
     if late is not None:
@@ -2610,6 +2622,10 @@ def aggregate(groups, aggs, b: Batch, ctx) -> Batch:
     if groups:
         for (ci, _), c in zip(groups, taken):
             out[ci.cid] = c
+    if late is not None and row_parts:
+        for cid, k in row_parts.items():
+            idx = b.parts[k][1]
+            out[cid] = Column(T.INT64, gather_tensor(idx, rep).to(torch.int64))
     specs, finals = [], []
     with ctx.span("agg.eval_args"):
         for ci, a in aggs:
@@ -2660,7 +2676,7 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
         return None
     keys = {i: group_key_tensor(b.gather(cids[i]))[0] for i in others}
     spans = {i: H.key_range(keys[i]) for i in others}
-    lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
+    lead = _lead_key(others, spans, base)
     gid, ng, rep, srt = H.group_ids_ex(keys[lead])
     rr = gather_tensor(rep, gid)
     checks, parts = [], set()
@@ -2686,6 +2702,18 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
     return gid, ng, rep, taken
 
 
+def _lead_key(others, spans, cols) -> int:
+    """The grouping key the others are tested to depend on: the widest-range
+    plain integer key (a key column, e.g. c_custkey), before decimals and
+    dictionary codes (an account balance spans more values than 150K
+    customer keys at SF1, but identifies nothing)."""
+    def rank(i):
+        t = cols[i].dtype
+        intlike = (t.is_integer and not t.is_decimal) and not cols[i].is_dict
+        return (1 if intlike else 0, spans[i][1] - spans[i][0] if spans[i] else -1)
+    return max(others, key=rank)
+
+
 def _encode_groups(gcols: List[Column], ctx):
     """Dense group ids for GROUP BY over ``gcols`` -> (gid, ng, rep_row, rep_source_cols).
 
@@ -2706,7 +2734,7 @@ def _encode_groups(gcols: List[Column], ctx):
     needed = list(range(len(gcols)))
     if plain and others and ctx.device.type == "cuda":
         spans = {i: H.key_range(keys[i]) for i in others}
-        lead = max(others, key=lambda i: spans[i][1] - spans[i][0] if spans[i] else -1)
+        lead = _lead_key(others, spans, gcols)
         gid, ng, rep, srt = H.group_ids_ex(keys[lead])
         ctx.sorted_gids = srt
         rr = gather_tensor(rep, gid)

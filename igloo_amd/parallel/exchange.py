@@ -544,21 +544,18 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
                                       ("hash", rc) if rc is not None and same else None))
 
 
-#: largest global key span a semi / anti join filters through a dense
-#: key-presence table (bytes, all-reduced)
-KEYSET_MAX_SPAN = 1 << 27
-
-
 def semi_by_key_set(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
     """SEMI / ANTI join of a REPLICATED left side against a partitioned right
-    side (TPC-H Q22: customer NOT EXISTS orders) with no row movement: every
-    rank marks the keys of its right rows in a dense presence table over the
-    global key range, ONE all-reduce (max) makes it the global key set, and
-    each rank filters its replicated left rows locally — the result stays
-    replicated. Two collectives (key range, presence table) instead of
-    slicing the left side and shuffling the right side. None when the shape
-    does not apply."""
+    side (TPC-H Q22: customer NOT EXISTS orders) with no row movement: each
+    rank builds a hash table on the (small, replicated) left keys, streams
+    its own right rows through it marking the left rows that found a partner,
+    and ONE all-reduce (max) of those per-left-row marks -- the left side is
+    identical on every rank, so mark i means the same row everywhere -- gives
+    the global answer; each rank then filters its replicated left rows
+    locally and the result stays replicated. One collective of n_left bytes,
+    no key-range exchange, no shuffle. None when the shape does not apply."""
     from ..exec.operators import _pair_key
+    from ..ops import hashing as H
     from ..ops.select import mask_to_indices
     comm = ctx.comm
     if join.kind not in ("semi", "anti") or len(join.on or []) != 1 or join.residual is not None \
@@ -574,29 +571,16 @@ def semi_by_key_set(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
             or not (rcol.dtype.is_integer or rcol.dtype.kind == "date32"):
         return None
     lk, rk = _pair_key(lcol, rcol)
-    lk, rk = lk.to(torch.int64), rk.to(torch.int64)
-    if rcol.valid is not None:
-        rk = gather_tensor(rk, mask_to_indices(rcol.valid))
-    from ..ops import hashing as H
-    rng = H.key_range(rk) if rk.numel() else None
-    lo_hi = comm.allgather_ints([rng[0], rng[1]] if rng else [2**62, -2**62])
-    g0, g1 = min(r[0] for r in lo_hi), max(r[1] for r in lo_hi)
-    span = g1 - g0 + 1 if g0 <= g1 else 0
-    if span > KEYSET_MAX_SPAN:
-        return None     # every rank decides alike (global range)
-    present = torch.zeros(max(span, 1), dtype=torch.uint8, device=ctx.device)
-    if rk.numel():
-        present.index_fill_(0, rk - g0, 1)
-    present = comm.allreduce_tensor(present, "max")
-    li = lk - g0
-    inr = (li >= 0) & (li < span)
-    hit = inr & (present.index_select(0, torch.where(inr, li, torch.zeros_like(li))) > 0)
-    if lcol.valid is not None:
-        hit &= lcol.valid
+    n_l = lb.num_rows
+    matched = torch.zeros(n_l, dtype=torch.bool, device=ctx.device)
+    if n_l and rk.numel():
+        with ctx.span("join.semi_marks"):
+            H.JoinTable(lk.contiguous(), lcol.valid).probe_first(rk.contiguous(), rcol.valid, build_matched=matched)
+    marks = comm.allreduce_tensor(matched.to(torch.uint8), "max") if n_l else matched.to(torch.uint8)
+    hit = marks > 0
     keep = mask_to_indices(hit if join.kind == "semi" else ~hit)
     keys = list(lb.columns)
-    out = Batch(dict(zip(keys, take_many([lb.columns[k] for k in keys], keep))), int(keep.numel()), REPLICATED)
-    return out
+    return Batch(dict(zip(keys, take_many([lb.columns[k] for k in keys], keep))), int(keep.numel()), REPLICATED)
 
 
 # ------------------------------------------------------------------ aggregation
@@ -627,8 +611,9 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     ids = _TmpIds()
     partial, plan = partial_plan(aggs, ids)
     pb = local(groups, partial) if local is not None else None
+    restore = None
     if pb is None:
-        pb = aggregate(groups, partial, b, ctx)
+        pb, groups, restore = _partial_by_rows(groups, partial, b, ids, ctx)
     # ---- exchange partial states. ONE all-gather agrees on the structure of
     # the partial batch (validity, dictionary vs plain, 64 vs 128-bit sums,
     # shared dictionary codes) and carries the local ranges of the integer
@@ -641,6 +626,9 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     pbn = normalize_structure(materialized(pb), ctx.comm, extra)
     rb = _dense_allreduce(groups, partial, pbn, ctx) if dense_plan else None
     out_dist = REPLICATED if rb is not None else None
+    log.debug("aggregate exchange: %d partial groups, %s", pb.num_rows, "dense all-reduce" if rb is not None
+              else "shuffle" if groups else "gather")
+    unique = rb is not None
     if rb is None and groups:
         g0 = groups[0][0]
         key, cid = _shuffle_key(groups, pbn)
@@ -649,9 +637,68 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     elif rb is None:
         rb = gather_all(pbn, ctx, normalized=True)
         out_dist = REPLICATED
-    # ---- phase 2: merge
-    res = merge_partials(groups, plan, rb, ids, ctx)
+    # ---- phase 2: merge (the dense all-reduce leaves one row per group:
+    # its states only need finalising)
+    res = finalize_unique(groups, plan, rb) if unique else merge_partials(groups, plan, rb, ids, ctx)
+    if restore is not None:
+        res = restore(res)
     return with_dist(res, out_dist)
+
+
+def _partial_by_rows(groups, partial, b: Batch, ids, ctx):
+    """Phase-1 partial aggregate whose exchange ships ROW NUMBERS instead of
+    string group keys, where it can: GROUP BY keys that are plain strings of
+    a REPLICATED input of a join still in index form (TPC-H Q10: c_name,
+    c_address, c_phone, c_comment of the replicated customer table, grouped
+    with c_custkey over orders x lineitem partitioned by order key). The
+    local grouping runs by the leading integer key with the others checked
+    to be functionally dependent on it (exec/operators.py _late_group_keys);
+    each group then carries its row in the replicated input -- the same row
+    number on every rank -- and the strings are taken from that input after
+    the merge, on the owning rank only (~4M groups x ~130 string bytes at
+    SF100 no longer cross the fabric). Every rank must take the same shape,
+    so the dependency check's outcome is agreed by one tiny all-gather.
+    Returns (partial batch, exchange group keys, restore(merged) or None)."""
+    from ..exec.operators import LateBatch, aggregate
+    rows = {}
+    if isinstance(b, LateBatch) and len(groups) > 1 and b.num_rows >= 0:
+        for i, (ci, e) in enumerate(groups):
+            if not isinstance(e, ColRef) or e.cid not in b.owner:
+                continue
+            k = b.owner[e.cid]
+            bb, idx = b.parts[k]
+            src = bb.src if hasattr(bb, "take_rows") else bb      # (a lazy filtered scan: its source column)
+            if idx is not None and dist_of(bb) == REPLICATED and src.columns[e.cid].is_plain_string:
+                rows[i] = k
+    if not rows or len(rows) == len(groups):
+        return aggregate(groups, partial, b, ctx), groups, None
+    row_ci = {k: L.ColInfo(ids(), "__row", T.INT64, False) for k in sorted(set(rows.values()))}
+    pb = aggregate(groups, partial, b, ctx, row_parts={ci.cid: k for k, ci in row_ci.items()})
+    have = all(ci.cid in pb.columns for ci in row_ci.values())
+    ok = all(r[0] for r in ctx.comm.allgather_ints([int(have)]))
+    log.debug("partial aggregate ships row numbers for %d string key(s): local %s, agreed %s",
+              len(rows), have, ok)
+    if not ok:
+        if have:
+            pb = Batch({c: v for c, v in pb.columns.items() if c not in {ci.cid for ci in row_ci.values()}},
+                       pb.num_rows, pb.dist)
+        return pb, groups, None
+    replaced = {groups[i][0].cid for i in rows}
+    pb = Batch({c: v for c, v in pb.columns.items() if c not in replaced}, pb.num_rows, pb.dist)
+    ex_groups = [g for i, g in enumerate(groups) if i not in rows] + \
+        [(ci, ColRef(ci.cid, ci.name, ci.dtype, False)) for ci in row_ci.values()]
+    parts = {k: b.parts[k][0] for k in row_ci}
+
+    def restore(res: Batch) -> Batch:
+        from ..ops.gather import take
+        cols = {c: v for c, v in res.columns.items() if c not in {ci.cid for ci in row_ci.values()}}
+        for i, k in rows.items():
+            ci, e = groups[i]
+            r = res.columns[row_ci[k].cid].data
+            bb = parts[k]
+            cols[ci.cid] = bb.take_rows([e.cid], r)[0] if hasattr(bb, "take_rows") else take(bb.columns[e.cid], r)
+        return Batch(cols, res.num_rows, res.dist)
+    return pb, ex_groups, restore
 
 
 def _shuffle_key(groups, b: Batch):
@@ -769,6 +816,27 @@ def merge_partials(groups, plan, rb: Batch, ids, ctx) -> Batch:
     return Batch(out, fb.num_rows)
 
 
+def finalize_unique(groups, plan, rb: Batch) -> Batch:
+    """``merge_partials`` for partial states already merged to one row per
+    group (the dense all-reduce): the final columns come straight from the
+    states -- no second grouping pass."""
+    from ..exec.operators import _avg
+    out = {ci.cid: rb.columns[ci.cid] for ci, _ in groups}
+    for func, ci, a, p1, p2 in plan:
+        if func == "avg":
+            s, c = rb.columns[p1.cid], rb.columns[p2.cid]
+            cnt = c.data if c.valid is None else torch.where(c.valid, c.data, torch.zeros_like(c.data))
+            out[ci.cid] = Column(a.dtype, _avg(s.data, cnt, a.arg.dtype, a.dtype), cnt > 0)
+        elif func == "count":
+            c = rb.columns[p1.cid]
+            out[ci.cid] = Column(T.INT64, c.data if c.valid is None else
+                                 torch.where(c.valid, c.data, torch.zeros_like(c.data)))
+        else:
+            c = rb.columns[p1.cid]
+            out[ci.cid] = Column(a.dtype, c.data, c.valid)
+    return Batch(out, rb.num_rows)
+
+
 #: largest dense group-key domain whose partial states are all-reduced
 DENSE_ALLREDUCE_MAX = 4096
 _I64_MAX, _I64_MIN = 2**63 - 1, -2**63
@@ -779,15 +847,19 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
     group keys that are dictionary strings, booleans or integers whose
     domains multiply to at most DENSE_ALLREDUCE_MAX, e.g. TPC-H Q1's
     returnflag x linestatus, Q13's order counts): every rank scatters its
-    partial states into dense per-key arrays and ONE all-reduce per
-    reduction op (SUM / MIN / MAX) merges them -- no shuffle, and the result
-    is replicated on every rank (so a following ORDER BY needs no gather).
+    partial states into dense per-key tables and ONE all-reduce per reduction
+    op (SUM / MIN / MAX) merges them -- no shuffle, and the result is
+    replicated on every rank (so a following ORDER BY needs no gather).
     ``pb`` comes from ``normalize_structure`` (identical structure on every
     rank; its preamble holds every rank's integer-key ranges), so every rank
     takes the same decision. Integer SUMs travel as three int64 parts (high
     word, low word's two 32-bit halves) that cannot overflow and recombine
-    into exact 128-bit sums. Returns the merged partial-state batch or None
+    into exact 128-bit sums. The states are scattered as matrices (one
+    index_add / scatter_reduce per op), so the launch count does not grow with
+    the number of aggregates. Returns the merged partial-state batch or None
     when the shape does not apply."""
+    from ..ops.agg import _wide_flags
+    from ..ops.select import mask_to_indices
     comm = ctx.comm
     dev = ctx.device
     cols = [pb.columns[ci.cid] for ci, _ in partial]
@@ -814,63 +886,81 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
         if domain > DENSE_ALLREDUCE_MAX:
             return None
     n = pb.num_rows
-    idx = torch.zeros(n, dtype=torch.int64, device=dev)
+    idx = None
     for j, k in enumerate(keys):
-        code = k.data.to(torch.int64) - offs[j]
+        code = k.data.to(torch.int64) - offs[j] if offs[j] else k.data.to(torch.int64)
         if k.valid is not None:
             code = torch.where(k.valid, code, torch.full_like(code, sizes[j] - 1))
-        idx = idx * sizes[j] + code
-    isum, fsum, imin, imax, fmin, fmax = [], [], [], [], [], []
-
-    def dense(vals, fill, dtype):
-        d = torch.full((domain,), fill, dtype=dtype, device=dev)
-        if n:
-            d.index_put_((idx,), vals.to(dtype), accumulate=False)
-        return d
-
-    presence = dense(torch.ones(n, dtype=torch.int64, device=dev), 0, torch.int64)
-    isum.append(presence)
-    slots = []
-    for (ci, a), c in zip(partial, cols):
+        idx = code if idx is None else idx * sizes[j] + code
+    if idx is None:
+        idx = torch.zeros(n, dtype=torch.int64, device=dev)
+    i64 = torch.int64
+    # ---- per aggregate: which matrix columns hold its state
+    valid_cols = []        # (slot, valid mask) for columns that have a validity
+    isums, fsums, mins, maxs = [], [], [], []    # (partial index, tensor)
+    for j, ((ci, a), c) in enumerate(zip(partial, cols)):
         isf = c.data.dtype in (torch.float32, torch.float64)
-        valid = c.valid if c.valid is not None else torch.ones(n, dtype=torch.bool, device=dev)
-        isum.append(dense(valid.to(torch.int64), 0, torch.int64))
-        vi = len(isum) - 1
+        if c.valid is not None:
+            valid_cols.append((j, c.valid))
         if a.func in ("sum", "count") and not isf:
-            # exact: hi word + the low word's 32-bit halves, each summed in int64
-            if c.is_wide:
-                lo_w, hi_w = c.data[:, 0], c.data[:, 1]
-            else:
-                lo_w = c.data.to(torch.int64)
-                hi_w = lo_w >> 63
-            z = torch.zeros_like(lo_w)
-            first = len(isum)
-            for part in (hi_w, (lo_w >> 32) & 0xFFFFFFFF, lo_w & 0xFFFFFFFF):
-                isum.append(dense(torch.where(valid, part, z), 0, torch.int64))
-            slots.append(("wide", first, vi))
+            isums.append((j, c))
         elif a.func in ("sum", "count"):
-            fsum.append(dense(torch.where(valid, c.data, torch.zeros_like(c.data)), 0, torch.float64))
-            slots.append(("fsum", len(fsum) - 1, vi))
+            fsums.append((j, c.data.to(torch.float64)))
+        elif a.func in ("min", "bool_and"):
+            mins.append((j, c.data.to(torch.float64 if isf else i64)))
         else:
-            is_min = a.func in ("min", "bool_and")
-            fill = (float("inf") if is_min else float("-inf")) if isf else (_I64_MAX if is_min else _I64_MIN)
-            v = torch.where(valid, c.data.to(torch.float64 if isf else torch.int64),
-                            torch.full((n,), fill, dtype=torch.float64 if isf else torch.int64, device=dev))
-            lst = (fmin if is_min else fmax) if isf else (imin if is_min else imax)
-            lst.append(dense(v, fill, torch.float64 if isf else torch.int64))
-            slots.append(({id(fmin): "fmin", id(fmax): "fmax", id(imin): "imin", id(imax): "imax"}[id(lst)],
-                          len(lst) - 1, vi))
-    red = {}
-    for name, lst, op in (("isum", isum, "sum"), ("fsum", fsum, "sum"), ("imin", imin, "min"), ("imax", imax, "max"),
-                          ("fmin", fmin, "min"), ("fmax", fmax, "max")):
-        if lst:
-            red[name] = comm.allreduce_tensor(torch.stack(lst), op)
-    from ..ops.select import mask_to_indices
-    tot = red["isum"]
-    mask_idx = mask_to_indices(tot[0] > 0)
-    m = mask_idx.numel()
+            maxs.append((j, c.data.to(torch.float64 if isf else i64)))
+    # int64 matrix: [presence | valid counts | sum hi words | mid halves | low halves]
+    icols = [torch.ones(n, dtype=i64, device=dev)] + [v.to(i64) for _, v in valid_cols]
+    if isums:
+        lo_w = torch.stack([c.data[:, 0] if c.is_wide else c.data.to(i64) for _, c in isums], 1)
+        hi_w = lo_w >> 63
+        for t, (_, c) in enumerate(isums):
+            if c.is_wide:
+                hi_w[:, t] = c.data[:, 1]
+        parts = torch.cat([hi_w, (lo_w >> 32) & 0xFFFFFFFF, lo_w & 0xFFFFFFFF], 1)
+        vmask = [c.valid for _, c in isums]
+        if any(v is not None for v in vmask):
+            vm = torch.stack([v if v is not None else torch.ones(n, dtype=torch.bool, device=dev) for v in vmask], 1)
+            parts = parts * vm.repeat(1, 3).to(i64)
+        imat = torch.cat([torch.stack(icols, 1), parts], 1)
+    else:
+        imat = torch.stack(icols, 1)
+    reds = {}
+
+    def scatter(mat, op, fill):
+        out = torch.full((domain, mat.shape[1]), fill, dtype=mat.dtype, device=dev)
+        if n:
+            if op == "sum":
+                out.index_add_(0, idx, mat)
+            else:
+                out.scatter_reduce_(0, idx.view(-1, 1).expand(-1, mat.shape[1]), mat, op, include_self=True)
+        return comm.allreduce_tensor(out, {"amin": "min", "amax": "max"}.get(op, op))
+
+    def masked(lst, fill):
+        m = torch.stack([t for _, t in lst], 1)
+        vm = [cols[j].valid for j, _ in lst]
+        if any(v is not None for v in vm):
+            ok = torch.stack([v if v is not None else torch.ones(n, dtype=torch.bool, device=dev) for v in vm], 1)
+            m = torch.where(ok, m, torch.full_like(m, fill))
+        return m
+    reds["i"] = scatter(imat, "sum", 0)
+    if fsums:
+        reds["f"] = scatter(masked(fsums, 0.0), "sum", 0.0)
+    for name, lst, op in (("mn", mins, "amin"), ("mx", maxs, "amax")):
+        fl_ = [x for x in lst if x[1].dtype == torch.float64]
+        it_ = [x for x in lst if x[1].dtype != torch.float64]
+        if fl_:
+            fill = float("inf") if op == "amin" else float("-inf")
+            reds[name + "f"] = scatter(masked(fl_, fill), op, fill)
+        if it_:
+            fill = _I64_MAX if op == "amin" else _I64_MIN
+            reds[name + "i"] = scatter(masked(it_, fill), op, fill)
+    present = mask_to_indices(reds["i"][:, 0] > 0)
+    m = present.numel()
+    rows = {k: v.index_select(0, present) for k, v in reds.items()}
     out = {}
-    rest = mask_idx.to(torch.int64)
+    rest = present.to(i64)
     for j in range(len(keys) - 1, -1, -1):
         code = rest % sizes[j]
         rest = rest // sizes[j]
@@ -886,23 +976,48 @@ def _dense_allreduce(groups, partial, pb: Batch, ctx) -> Optional[Batch]:
             out[ci.cid] = Column(k.dtype, code.to(torch.bool), valid)
         else:
             out[ci.cid] = Column(k.dtype, (code + offs[j]).to(k.data.dtype), valid)
-    sign = -(2**63)
-    for ((ci, a), c), (kind, li, vi) in zip(zip(partial, cols), slots):
-        has = gather_tensor(tot[vi], mask_idx) > 0
-        if kind == "wide":
-            hi, mid, low = (gather_tensor(tot[li + t], mask_idx) for t in range(3))
-            lo = low + ((mid & 0xFFFFFFFF) << 32)                     # wraps as uint64
-            carry = ((lo ^ sign) < (low ^ sign)).to(torch.int64)      # unsigned overflow of that add
-            hi = hi + (mid >> 32) + carry
-            if a.func == "count":
-                out[ci.cid] = Column(c.dtype, lo)
+    iv = rows["i"]
+    vslot = {j: 1 + t for t, (j, _) in enumerate(valid_cols)}
+
+    def has(j):
+        return iv[:, vslot[j]] > 0 if j in vslot else None
+    if isums:
+        S = len(isums)
+        base = 1 + len(valid_cols)
+        hi, mid, low = iv[:, base:base + S], iv[:, base + S:base + 2 * S], iv[:, base + 2 * S:base + 3 * S]
+        sign = -(2**63)
+        lo = low + ((mid & 0xFFFFFFFF) << 32)                     # wraps as uint64
+        carry = ((lo ^ sign) < (low ^ sign)).to(i64)              # unsigned overflow of that add
+        hi = hi + (mid >> 32) + carry
+        # column-major once (every state column a contiguous view), and ONE
+        # device check (one readback) whether any merged sum needs 128 bits
+        lo_t, hi_t = lo.t().contiguous(), hi.t().contiguous()
+        wide = False
+        if m and any(partial[j][1].func != "count" for j, _ in isums):
+            if lo.is_cuda:
+                wide = bool(to_host_ints(_wide_flags([(lo_t.reshape(-1), hi_t.reshape(-1))]))[0])
+            else:
+                wide = not bool((hi_t == (lo_t >> 63)).all())
+        for t, (j, c) in enumerate(isums):
+            ci = partial[j][0]
+            if partial[j][1].func == "count":
+                out[ci.cid] = Column(c.dtype, lo_t[t])
                 continue
-            from ..ops.agg import _wide_to_result
-            out[ci.cid] = Column(c.dtype, _wide_to_result(lo.contiguous(), hi.contiguous()), has)
-            continue
-        vals = gather_tensor(red[kind][li], mask_idx)
-        data = vals.to(c.data.dtype) if c.dtype.kind != "bool" else vals != 0
-        out[ci.cid] = Column(c.dtype, torch.where(has, data, torch.zeros_like(data)), has)
+            data = torch.stack([lo_t[t], hi_t[t]], 1) if wide else lo_t[t]
+            out[ci.cid] = Column(c.dtype, data, has(j))
+    for key, lst in (("f", fsums), ("mnf", [x for x in mins if x[1].dtype == torch.float64]),
+                     ("mxf", [x for x in maxs if x[1].dtype == torch.float64]),
+                     ("mni", [x for x in mins if x[1].dtype != torch.float64]),
+                     ("mxi", [x for x in maxs if x[1].dtype != torch.float64])):
+        mat = rows[key].t().contiguous() if lst else None
+        for t, (j, _) in enumerate(lst):
+            c = cols[j]
+            v = mat[t]
+            data = v.to(c.data.dtype) if c.dtype.kind != "bool" else v != 0
+            hv = has(j)
+            if hv is not None:
+                data = torch.where(hv, data, torch.zeros_like(data))
+            out[partial[j][0].cid] = Column(c.dtype, data.contiguous(), hv)
     return Batch(out, m)
 
 
