@@ -210,48 +210,6 @@ __device__ inline void store_exclusive(const AggDesc& a, int64_t g, unsigned lon
   if (a.op == AGG_SUM_INT && a.dst2) ((long long*)a.dst2)[g] = hi;
 }
 
-__global__ __launch_bounds__(kBlock) void agg_sorted_kernel(const int32_t* __restrict__ gid, int64_t n, AggParams p) {
-  const int lane = lane_id();
-  const int64_t wave_id = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
-  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
-  for (int64_t base = wave_id * kWave; base < n; base += nwaves * kWave) {
-    const int64_t i = base + lane;
-    const bool live = i < n;
-    const int g = live ? gid[i] : -1;
-    int og[6];
-#pragma unroll
-    for (int s = 0; s < 6; ++s) og[s] = __shfl_up(g, 1 << s, kWave);
-    const int gnext = __shfl_down(g, 1, kWave);
-    const bool tail = live && (lane == kWave - 1 || gnext != g || i + 1 >= n);
-    const bool head_in_tile = __shfl_up(g, 1, kWave) != g && lane > 0;
-    // lane index where this lane's segment starts inside the tile
-    int start = lane;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int o = __shfl_up(start, 1 << s, kWave);
-      if (lane >= (1 << s) && og[s] == g && o < start) start = o;
-    }
-    (void)head_in_tile;
-    const bool edge = start == 0 || lane == kWave - 1;
-    for (int k = 0; k < p.nagg; ++k) {
-      const AggDesc& a = p.d[k];
-      unsigned long long lo;
-      long long hi;
-      row_state(a, i, live, &lo, &hi);
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        const unsigned long long olo = __shfl_up(lo, 1 << s, kWave);
-        const long long ohi = __shfl_up(hi, 1 << s, kWave);
-        if (lane >= (1 << s) && og[s] == g) seg_combine(a.op, &lo, &hi, olo, ohi);
-      }
-      if (tail) {
-        if (edge) merge_global(a, g, lo, hi);
-        else store_exclusive(a, g, lo, hi);
-      }
-    }
-  }
-}
-
 // Non-decreasing group ids, chunked: each lane folds kSortedRows consecutive
 // rows in registers first (segments closed inside the chunk are stored
 // directly), so the cross-lane segmented scan runs once per kSortedRows rows
@@ -724,15 +682,6 @@ __global__ __launch_bounds__(kBlock) void sorted_having_kernel(const K* __restri
 }
 }  // namespace
 
-// IGLOO_AGG_SORTED_ROWS=1 selects the one-row-per-lane sorted kernel (A/B)
-static bool sorted_per_row() {
-  static const bool v = [] {
-    const char* e = std::getenv("IGLOO_AGG_SORTED_ROWS");
-    return e && e[0] == '1' && e[1] == 0;
-  }();
-  return v;
-}
-
 int agg_lds_max_groups(int nagg) {
   // keep the LDS state at <= 64 KiB so several workgroups stay resident per CU
   const int bytes = 64 * 1024;
@@ -777,13 +726,10 @@ void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs
     int64_t maxg = ngroups <= 64 ? 8192 : 2048;
     hipLaunchKernelGGL(agg_lds_kernel, dim3(grid_for(n, kBlock * 8, maxg)), dim3(kBlock), lds, stream, gid, n, ngroups, p);
     check_launch("agg_lds", stream);
-  } else if (sorted_gids && !sorted_per_row()) {
+  } else if (sorted_gids) {
     hipLaunchKernelGGL(agg_sorted_chunk_kernel, dim3(grid_for(n, kBlock * kSortedRows, 32768)), dim3(kBlock), 0, stream,
                        gid, n, p);
     check_launch("agg_sorted_chunk", stream);
-  } else if (sorted_gids) {
-    hipLaunchKernelGGL(agg_sorted_kernel, dim3(grid_for(n, kBlock, 32768)), dim3(kBlock), 0, stream, gid, n, p);
-    check_launch("agg_sorted", stream);
   } else {
     hipLaunchKernelGGL(agg_global_kernel, dim3(grid_for(n, kBlock, 32768)), dim3(kBlock), 0, stream, gid, n, p);
     check_launch("agg_global", stream);

@@ -41,68 +41,12 @@ __device__ inline void gather_col(const void* src_, void* dst_, const int64_t (&
     if (i[r] < n) dst[i[r]] = v[r];
 }
 
-// Grouped variant (IGLOO_GATHER=grouped; within 1% of the per-column kernel over
-// the SF100 suite, profiles/r3_ab_gather_grouped.txt, where 3 of 4 gathers
-// move one column): one launch per element type T and
-// column count NC (<= 4, the launcher splits a request), rows base + r *
-// blockDim (r < kGatherRows) per lane. Every load is unconditional — the
-// index load clamps the row to n - 1, a source load clamps a NULL row's
-// negative index to 0, values are selected afterwards — so a lane issues its
-// NC x kGatherRows random reads back to back and waits once before the
-// stores (a load under a per-lane condition compiles to a branch whose merge
-// waits for it).
-template <typename I, typename T, int NC>
-__global__ __launch_bounds__(kBlock) void gather_grouped_kernel(const I* __restrict__ idx, int64_t n, GatherParams p) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherRows;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x * kGatherRows + threadIdx.x; base < n; base += step) {
-    int64_t i[kGatherRows], s[kGatherRows], sc[kGatherRows];
-#pragma unroll
-    for (int r = 0; r < kGatherRows; ++r) {
-      i[r] = base + (int64_t)r * blockDim.x;
-      s[r] = (int64_t)idx[i[r] < n ? i[r] : n - 1];
-      sc[r] = s[r] < 0 ? 0 : s[r];
-    }
-    T v[NC][kGatherRows];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const T* __restrict__ src = p.d[c].src ? static_cast<const T*>(p.d[c].src)
-                                             : reinterpret_cast<const T*>(g_gather_zero);
-#pragma unroll
-      for (int r = 0; r < kGatherRows; ++r) v[c][r] = src[sc[r]];
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      T* __restrict__ dst = static_cast<T*>(p.d[c].dst);
-#pragma unroll
-      for (int r = 0; r < kGatherRows; ++r)
-        if (i[r] < n) dst[i[r]] = s[r] < 0 ? T{} : v[c][r];
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      uint8_t* __restrict__ dv = p.d[c].dst_valid;
-      if (!dv) continue;
-      const uint8_t* __restrict__ sv = p.d[c].src_valid;
-      uint8_t vv[kGatherRows];
-      if (sv) {
-#pragma unroll
-        for (int r = 0; r < kGatherRows; ++r) vv[r] = sv[sc[r]];
-#pragma unroll
-        for (int r = 0; r < kGatherRows; ++r) vv[r] = s[r] >= 0 && vv[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < kGatherRows; ++r) vv[r] = s[r] >= 0;
-      }
-#pragma unroll
-      for (int r = 0; r < kGatherRows; ++r)
-        if (i[r] < n) dv[i[r]] = vv[r];
-    }
-  }
-}
-
-// Per-column variant (IGLOO_GATHER=percol): rows base + r * blockDim (r <
-// kGatherRows) per lane, every column in one launch: every store of a column
-// follows all of that column's loads, so a lane keeps kGatherRows random
-// reads in flight instead of one load->store round trip per value.
+// Rows base + r * blockDim (r < kGatherRows) per lane, every column in one
+// launch: every store of a column follows all of that column's loads, so a
+// lane keeps kGatherRows random reads in flight instead of one load->store
+// round trip per value. (A variant grouping up to 4 columns of one element
+// type per launch, every load unconditional, measured within 1% over the
+// SF100 suite -- profiles/r3_ab_gather_grouped.txt -- and was removed.)
 template <typename I, int kGatherRows>
 __global__ __launch_bounds__(kBlock) void gather_percol_kernel(const I* __restrict__ idx, int64_t n, GatherParams p) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherRows;
@@ -162,36 +106,6 @@ __global__ __launch_bounds__(kBlock) void str_copy_kernel(const int64_t* __restr
 
 }  // namespace
 
-namespace {
-template <typename T, int NC>
-void launch_grouped(const void* idx, bool idx64, int64_t n, const GatherParams& p, hipStream_t stream) {
-  const dim3 g(grid_for(n, kBlock * kGatherRows, 65536)), b(kBlock);
-  if (idx64)
-    hipLaunchKernelGGL((gather_grouped_kernel<int64_t, T, NC>), g, b, 0, stream, (const int64_t*)idx, n, p);
-  else
-    hipLaunchKernelGGL((gather_grouped_kernel<int32_t, T, NC>), g, b, 0, stream, (const int32_t*)idx, n, p);
-  check_launch("gather_multi", stream);
-}
-
-template <typename T>
-void launch_grouped_n(const void* idx, bool idx64, int64_t n, const GatherParams& p, hipStream_t stream) {
-  switch (p.ncols) {
-    case 1: launch_grouped<T, 1>(idx, idx64, n, p, stream); break;
-    case 2: launch_grouped<T, 2>(idx, idx64, n, p, stream); break;
-    case 3: launch_grouped<T, 3>(idx, idx64, n, p, stream); break;
-    default: launch_grouped<T, 4>(idx, idx64, n, p, stream); break;
-  }
-}
-
-bool grouped_gather() {
-  static const bool g = [] {
-    const char* e = getenv("IGLOO_GATHER");
-    return e && std::string(e) == "grouped";
-  }();
-  return g;
-}
-}  // namespace
-
 void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* descs, int ncols, hipStream_t stream) {
   if (n == 0 || ncols == 0) return;
   for (int c = 0; c < ncols; ++c) {
@@ -199,40 +113,17 @@ void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* desc
     if (eb != 1 && eb != 2 && eb != 4 && eb != 8 && eb != 16)
       throw std::runtime_error("gather_multi: unsupported element size " + std::to_string(eb));
   }
-  if (!grouped_gather()) {
-    // per-column kernel: every column of the request in one launch
-    for (int base = 0; base < ncols; base += kMaxGatherCols) {
-      GatherParams p;
-      p.ncols = ncols - base < kMaxGatherCols ? ncols - base : kMaxGatherCols;
-      for (int c = 0; c < p.ncols; ++c) p.d[c] = descs[base + c];
-      const dim3 g(grid_for(n, kBlock * kGatherRows, 65536)), b(kBlock);
-      if (idx64)
-        hipLaunchKernelGGL((gather_percol_kernel<int64_t, kGatherRows>), g, b, 0, stream, (const int64_t*)idx, n, p);
-      else
-        hipLaunchKernelGGL((gather_percol_kernel<int32_t, kGatherRows>), g, b, 0, stream, (const int32_t*)idx, n, p);
-      check_launch("gather_multi", stream);
-    }
-    return;
-  }
-  // grouped kernel: one launch per element size and group of <= 4 columns
-  static const int sizes[5] = {1, 2, 4, 8, 16};
-  for (int eb : sizes) {
+  // every column of the request in one launch (kMaxGatherCols per launch)
+  for (int base = 0; base < ncols; base += kMaxGatherCols) {
     GatherParams p;
-    p.ncols = 0;
-    for (int c = 0; c <= ncols; ++c) {
-      const bool flush = c == ncols ? p.ncols > 0 : p.ncols == 4;
-      if (flush) {
-        switch (eb) {
-          case 1: launch_grouped_n<uint8_t>(idx, idx64, n, p, stream); break;
-          case 2: launch_grouped_n<uint16_t>(idx, idx64, n, p, stream); break;
-          case 4: launch_grouped_n<uint32_t>(idx, idx64, n, p, stream); break;
-          case 8: launch_grouped_n<uint64_t>(idx, idx64, n, p, stream); break;
-          default: launch_grouped_n<uint4>(idx, idx64, n, p, stream); break;
-        }
-        p.ncols = 0;
-      }
-      if (c < ncols && descs[c].elem_bytes == eb) p.d[p.ncols++] = descs[c];
-    }
+    p.ncols = ncols - base < kMaxGatherCols ? ncols - base : kMaxGatherCols;
+    for (int c = 0; c < p.ncols; ++c) p.d[c] = descs[base + c];
+    const dim3 g(grid_for(n, kBlock * kGatherRows, 65536)), b(kBlock);
+    if (idx64)
+      hipLaunchKernelGGL((gather_percol_kernel<int64_t, kGatherRows>), g, b, 0, stream, (const int64_t*)idx, n, p);
+    else
+      hipLaunchKernelGGL((gather_percol_kernel<int32_t, kGatherRows>), g, b, 0, stream, (const int32_t*)idx, n, p);
+    check_launch("gather_multi", stream);
   }
 }
 

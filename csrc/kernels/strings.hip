@@ -430,25 +430,10 @@ void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, cons
                        hipStream_t stream) {
   if (n == 0) return;
   if (nseg > kSegMax) throw std::runtime_error("str_like_segments: too many segments");
-  // IGLOO_LIKE_WAVE=1: one-wave workgroups (A/B; measured slower for Q13 at
-  // SF100, 14.6 vs 11.7 ms per query, profiles/r3_ab_like_wave.txt)
-  static const bool wave = [] {
-    const char* e = getenv("IGLOO_LIKE_WAVE");
-    return e && e[0] == '1';
-  }();
-  // one wave per workgroup; tiles of 64 strings sized from the mean length
-  // (4 KB fits 64 TPC-H o_comment values, ~49 B, with room; longer strings
-  // take the 8 KB tile) so that nearly every tile is staged in LDS
-  const int64_t mean = nbytes / n;
-  if (wave && mean <= 48)
-    hipLaunchKernelGGL((like_seg_kernel<64, 4096>), dim3(grid_for(n, 64, 256 * 24 * 4)), dim3(64), 0, stream, off,
-                       chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
-  else if (wave && mean <= 100)
-    hipLaunchKernelGGL((like_seg_kernel<64, 8192>), dim3(grid_for(n, 64, 256 * 12 * 4)), dim3(64), 0, stream, off,
-                       chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
-  else
-    hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes>), dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock),
-                       0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  // (a one-wave-per-workgroup variant with 4 / 8 KB tiles measured slower for
+  // Q13 at SF100, 14.6 vs 11.7 ms per query: profiles/r3_ab_like_wave.txt)
+  hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes>), dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock),
+                     0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
   check_launch("str_like_segments", stream);
 }
 

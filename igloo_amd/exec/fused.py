@@ -35,7 +35,7 @@ MAX_COLS, MAX_TERMS, MAX_AGGS, MAX_GROUPS, MAX_FACTORS = 8, 16, 8, 16, 3
 MAX_OR_GROUPS = 31  # disjuncts of the one OR conjunct a launch can hold
 # column-vs-column range terms (l_commitdate < l_receiptdate): with generated
 # scan kernels the extra compare is free; SF100 A/B: Q12 6.1 -> 3.7 ms
-COL_COL = os.environ.get("IGLOO_FF_COLCOL", "1") == "1"
+COL_COL = True
 I64_MIN, I64_MAX = -(2**63), 2**63 - 1
 FLIP = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
 
@@ -291,7 +291,7 @@ class Spec:
                 self.mask.data_ptr() if self.mask is not None else 0)
 
 
-NARROW = os.environ.get("IGLOO_NARROW", "1") == "1"
+NARROW = True
 NARROW_MIN_ROWS = 1 << 20
 _NARROW_TYPES = (torch.int8, torch.int16, torch.int32)
 

@@ -1,0 +1,1518 @@
+"""Join operators: binary hash / sorted / index joins and the multi-way join.
+
+Split out of exec/operators.py, which re-exports every name."""
+from __future__ import annotations
+
+import math
+import os
+import re
+import time
+from fractions import Fraction
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+import torch
+
+from .. import types as T
+from ..columnar import Batch, Column, batch_device
+from ..ops import agg as A
+from ..ops import hashing as H
+from ..ops import misc as M
+from ..ops import strings as S
+from ..ops._lib import (check_not_capturing, device_ints, launch, ptr, stream, to_host_f64s, to_host_int,
+                       to_host_ints, unlogged)
+from ..utils import trace as _trace
+from ..ops.gather import gather_tensor, take, take_many
+from ..ops.select import exclusive_scan, mask_to_indices
+from ..sql import logical as L
+from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
+from ..utils.errors import ExecutionError, NotSupported
+from . import fused
+from .expr_eval import Evaluator, Scalar, _convert_tensor
+from .context import ExecContext, ExecNode
+from .scan import (FilterExec, ProjectExec, ScanExec, _LazyScanBatch, _tag_base, filter_batch,
+                   predicate_mask, LATE_SCAN)
+
+
+# ====================================================================== join keys
+def key_tensors(lcols: Sequence[Column], rcols: Sequence[Column]):
+    """Encode join keys of both sides into comparable int tensors (+ validity)."""
+    lk, rk = [], []
+    lvalid, rvalid = None, None
+    for a, b in zip(lcols, rcols):
+        ka, kb = _pair_key(a, b)
+        lk.append(ka)
+        rk.append(kb)
+        if a.valid is not None:
+            lvalid = a.valid if lvalid is None else lvalid & a.valid
+        if b.valid is not None:
+            rvalid = b.valid if rvalid is None else rvalid & b.valid
+    pl, pr = H.pack_keys_pair(lk, rk)
+    return pl, pr, lvalid, rvalid
+
+
+def _pair_key(a: Column, b: Column) -> Tuple[torch.Tensor, torch.Tensor]:
+    if a.dtype.is_string or b.dtype.is_string:
+        if a.is_dict and b.is_dict and a.dictionary is b.dictionary:
+            return a.data, b.data
+        from .expr_eval import _concat_strings
+        both = S.dict_encode(_concat_strings(S.decode(a), S.decode(b)))
+        n = len(a)
+        return both.data[:n], both.data[n:]
+    ta, tb = _num_key(a), _num_key(b)
+    if a.dtype != b.dtype and (a.dtype.is_decimal or b.dtype.is_decimal):
+        t = T.common_numeric(a.dtype, b.dtype)
+        ta, tb = _convert_tensor(a, t), _convert_tensor(b, t)
+    return ta, tb
+
+
+def _num_key(c: Column) -> torch.Tensor:
+    x = c.data
+    if x.dtype == torch.float64:
+        x = torch.where(x == 0, torch.zeros_like(x), x)  # -0.0 == 0.0
+        return x.view(torch.int64)
+    if x.dtype == torch.float32:
+        return x.to(torch.float64).view(torch.int64)
+    if x.dtype in (torch.bool, torch.int8, torch.int16, torch.uint8):
+        return x.to(torch.int32)
+    if c.is_wide:
+        raise NotSupported("128-bit decimal join / group keys")
+    return x
+
+
+def group_key_tensor(c: Column) -> Tuple[torch.Tensor, Column]:
+    """Int key per row for GROUP BY (NULL is its own group); returns (key, column to take reps from)."""
+    if c.dtype.is_string:
+        d = c if c.is_dict else S.dict_encode(c)
+        k = d.data.to(torch.int64)
+        if d.valid is not None:
+            k = torch.where(d.valid, k, torch.full_like(k, -1))
+        return k, d
+    k = _num_key(c)
+    if c.valid is not None:
+        if k.numel():
+            mx = to_host_int(k.max().to(torch.int64))
+            k = torch.where(c.valid, k.to(torch.int64), torch.full((k.numel(),), mx + 1, dtype=torch.int64, device=k.device))
+    return k, c
+
+
+# ============================================================================ join
+class HashJoinExec(ExecNode):
+    """Binary hash join (inner / left / right / full / semi / anti), build = right."""
+
+    def __init__(self, logical: L.Join, left: ExecNode, right: ExecNode):
+        self.logical = logical
+        self.children = [left, right]
+
+    def describe(self):
+        j = self.logical
+        on = ", ".join(f"{a.sql()} = {b.sql()}" for a, b in j.on)
+        r = f", filter={j.residual.sql()}" if j.residual is not None else ""
+        return f"{j.kind} on=[{on}]{r}"
+
+    def _run(self, ctx):
+        j = self.logical
+        if ctx.budget is not None and j.kind in ("semi", "anti"):
+            from .morsel import aggregated_semi_join
+            out = aggregated_semi_join(self, ctx)
+            if out is not None:
+                return out
+        lb = self.children[0].execute(ctx)
+        found = _semi_index_scan(self.children[1], j, ctx)
+        if found is not None:
+            out = _semi_index_then_filter(found, j, lb, ctx)
+            if out is not None:
+                return out
+        if j.kind in ("inner", "left", "semi") and j.on and ctx.memo is None:
+            # (not inside a morsel pipeline: the build side is computed once
+            # for all morsels, so it must not be narrowed to one morsel's keys)
+            push_key_filter(self.children[1], j.on, lb, ctx)
+        rb = self.children[1].execute(ctx)
+        if ctx.spmd:
+            from ..parallel.exchange import prepare_join, semi_by_key_set
+            out = semi_by_key_set(lb, rb, j, ctx)
+            if out is not None:
+                return out
+            lb, rb = prepare_join(lb, rb, j, ctx)
+            out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
+            out.dist = lb.out_dist
+            return out
+        return hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
+
+
+
+#: largest (global) probe side whose keys are pushed into the build side's aggregate
+RUNTIME_FILTER_MAX_ROWS = 16_000_000
+
+
+def _agg_group_source(node: ExecNode, cid: int):
+    """Follow output column ``cid`` down through projections / filters to the
+    aggregate that produces it as a GROUP BY key: (HashAggExec, group expr)."""
+    from .aggregate import HashAggExec
+    while True:
+        if isinstance(node, ProjectExec):
+            src = [e for ci, e in node.logical.exprs if ci.cid == cid]
+            if not src or not isinstance(src[0], ColRef):
+                return None
+            cid = src[0].cid
+            node = node.children[0]
+        elif isinstance(node, FilterExec):
+            node = node.children[0]
+        elif isinstance(node, HashAggExec):
+            for ci, e in node.logical.groups:
+                if ci.cid == cid:
+                    return node, e
+            return None
+        else:
+            return None
+
+
+def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
+    """Sideways information passing: when the build side of an inner / left /
+    semi join is an aggregate grouped by the join key, only groups whose key
+    occurs on the (already materialised, small) probe side can ever match, so
+    the aggregate's INPUT is semi-joined with those keys before grouping.
+    TPC-H Q17/Q20/Q2: a correlated aggregate over all of lineitem/partsupp
+    shrinks to the handful of parts the outer query selected."""
+    # (the candidate is found from the plan first: a build side that is no
+    # aggregate costs no collective, so SPMD ranks that reach this point by
+    # different rank-local fast-path decisions stay aligned)
+    for a, b in on:
+        if not isinstance(b, ColRef):
+            continue
+        found = _agg_group_source(build, b.cid)
+        if found is None:
+            continue
+        agg, gexpr = found
+        if a.dtype.is_string or gexpr.dtype.is_string:
+            continue
+        lcol = ctx.evaluator.column(a, lb)
+        if ctx.spmd and lb.dist != ("replicated",):
+            # the global key set; the size check rides on the gather's own
+            # preamble (one collective fewer than counting first)
+            from ..parallel.exchange import gather_all
+            g = gather_all(Batch({0: lcol}, lb.num_rows, lb.dist), ctx, max_rows=RUNTIME_FILTER_MAX_ROWS)
+            if g is None:
+                return
+            lcol = g.columns[0]
+        elif lb.num_rows > RUNTIME_FILTER_MAX_ROWS:
+            return
+        agg.runtime_filters.append((gexpr, lcol))
+        return
+
+
+def _index_key_filter(pk: torch.Tensor, bk: torch.Tensor, bvalid, ctx) -> Optional[torch.Tensor]:
+    """Rows of the resident unsorted key column ``pk`` whose key is in the
+    small set ``bk``, ascending, through the column's secondary index (the
+    same rule as inner_pairs): only the matching ranges are read instead of
+    probing every row (TPC-H Q17: 20K parts against 600M l_partkey, where the
+    probe fetches an L2 line per row for its bitmap bit). None when it does
+    not apply."""
+    n = pk.numel()
+    if not (ctx.device.type == "cuda" and PERM_INDEX and getattr(pk, "_igloo_resident", False)
+            and n >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * bk.numel() <= n
+            and bk.numel() * (n / _resident_ndv(pk)) * PERM_INDEX_SORT_FRAC <= n):
+        return None
+    keys = (bk if bvalid is None else gather_tensor(bk, mask_to_indices(bvalid))).to(pk.dtype)
+    _, _, rep = H.group_ids(keys)                       # a key set: each matching row once
+    keys = gather_tensor(keys, rep)
+    srt = H.is_sorted(pk)                              # sorted column: its own index (no permutation)
+    skeys, perm = (pk, None) if srt else H.perm_index(pk)
+    with ctx.span("agg.runtime_filter_index"):
+        lo, cnt = H.sorted_ranges(skeys, keys)
+        scanned = exclusive_scan(cnt)
+        if scanned[1] * PERM_INDEX_SORT_FRAC > n:
+            return None
+        _, pos = H.expand_ranges(lo, cnt, n, scanned)
+        rows = pos if perm is None else gather_tensor(perm, pos)
+        from ..ops.sort import sort_pairs
+        rows, _ = sort_pairs(rows, rows, max(1, (n - 1).bit_length()))
+    ctx.note_partial_read(pk, scanned[1])
+    return rows
+
+
+def _index_then_filter(scan: "ScanExec", raw: Batch, filters, ctx):
+    """A runtime key filter over a FILTERED scan of a resident table, index
+    first: the rows whose key is in the (small) key set come from the key
+    column's index ranges (``_index_key_filter``), and the scan's own filter
+    runs only on them — instead of evaluating it over the whole table and
+    gathering every surviving row (TPC-H Q20: lineitem's one-year shipdate
+    filter keeps 91M of 600M rows before the 6M rows of the forest parts are
+    picked). Returns (batch, remaining filters) or None."""
+    ev = ctx.evaluator
+    for i, (gexpr, lcol) in enumerate(filters):
+        if not isinstance(gexpr, ColRef) or gexpr.cid not in raw.columns:
+            continue
+        kcol = raw.columns[gexpr.cid]
+        pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
+        if pvalid is not None or raw.num_rows == 0:
+            continue
+        rows = _index_key_filter(pk, bk, bvalid, ctx)
+        if rows is None:
+            continue
+        with ctx.span("agg.index_then_filter"):
+            keys = list(raw.columns)
+            sub = Batch(dict(zip(keys, take_many([raw.columns[k] for k in keys], rows))), rows.numel(), raw.dist)
+            m = predicate_mask(scan.predicate, sub, ctx)
+            keep = mask_to_indices(m)
+            out_cids = [c.cid for c in scan.logical.schema]
+            cols = take_many([sub.columns[c] for c in out_cids], keep)
+        return Batch(dict(zip(out_cids, cols)), keep.numel(), raw.dist), filters[:i] + filters[i + 1:]
+    return None
+
+
+def _semi_index_scan(rnode, j, ctx):
+    """The filtered resident scan under a [NOT] EXISTS build side, for
+    ``_semi_index_then_filter``: (scan, raw batch, key column, output cid ->
+    scan cid) or None. Cheap: resident columns are not filtered here."""
+    if not (SEMI_INDEX and ctx.device.type == "cuda" and ctx.budget is None and ctx.memo is None) \
+            or j.kind not in ("semi", "anti") or j.null_aware or len(j.on) != 1:
+        return None
+    le, re_ = j.on[0]
+    if not isinstance(le, ColRef) or not isinstance(re_, ColRef):
+        return None
+    chain = []
+    while isinstance(rnode, ProjectExec):               # column renames above the scan
+        chain.append(rnode)
+        rnode = rnode.children[0]
+    if not isinstance(rnode, ScanExec) or rnode.predicate is None:
+        return None
+
+    def resolve(cid):
+        for p in chain:
+            src = [e for ci, e in p.logical.exprs if ci.cid == cid]
+            if not src or not isinstance(src[0], ColRef):
+                return None
+            cid = src[0].cid
+        return cid
+    names = {c.cid: resolve(c.cid) for c in (chain[0].logical.schema if chain else rnode.logical.schema)}
+    raw = rnode.peek_raw(ctx)
+    rcol = raw.columns.get(names.get(re_.cid))
+    if rcol is None or rcol.valid is not None or rcol.dtype.is_string or raw.num_rows < SORTED_JOIN_MIN_ROWS \
+            or not getattr(rcol.data, "_igloo_resident", False) or not H.is_sorted(rcol.data):
+        return None
+    if j.residual is not None and any(c not in names or names[c] not in raw.columns
+                                      for c in col_refs(j.residual) if c in names):
+        return None
+    return rnode, raw, rcol, names
+
+
+def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
+    """[NOT] EXISTS against a FILTERED scan of a resident table sorted on
+    the join key, as an index nested loop: each left row's range of the
+    sorted key column (dense lower-bound table or binary search), the scan's
+    filter (and the join's residual) evaluated only on those candidate rows,
+    and a left row kept when some candidate passes (semi) or none does
+    (anti). TPC-H Q4: 5.7M orders against lineitem's commit < receipt filter
+    — 23M candidate rows checked instead of the filter over 600M rows, the
+    compaction and the gather of 385M keys; Q21's NOT EXISTS the same way
+    with its l_suppkey <> residual. None when the size does not apply."""
+    scan, raw, rcol, names = found
+    le, re_ = j.on[0]
+    n_r, n_l = raw.num_rows, lb.num_rows
+    if ctx.spmd and not _rank_local_semi(lb, le, raw, names.get(re_.cid)):
+        return None
+    if le.cid not in lb.columns or n_l == 0 or n_l * 2 > n_r:
+        return None
+    lcol = ctx.evaluator.column(le, lb)
+    if lcol.dtype.is_string:
+        return None
+    pl, pr, lvalid, _ = key_tensors([lcol], [rcol])
+    if pr is not rcol.data:
+        return None
+    with ctx.span("join.index_then_filter"):
+        _dense_lookup_ok(pr, n_l)           # the column's dense table, built once
+        lo, cnt = H.sorted_ranges(pr, pl, lvalid)
+        scanned = exclusive_scan(cnt)
+        if scanned[1] * PERM_INDEX_SORT_FRAC > n_r:
+            return None
+        lidx, pos = H.expand_ranges(lo, cnt, n_r, scanned)
+        # only the filter's inputs at every candidate; residual inputs at the survivors
+        keys = sorted(col_refs(scan.predicate))
+        sub = Batch(dict(zip(keys, take_many([raw.columns[k] for k in keys], pos))), pos.numel(), raw.dist)
+        ok = mask_to_indices(predicate_mask(scan.predicate, sub, ctx))
+        li = gather_tensor(lidx, ok)
+        if j.residual is not None and ok.numel():
+            refs = sorted(col_refs(j.residual))
+            lref = [c for c in refs if c in lb.columns]
+            rref = [c for c in refs if c not in lb.columns]
+            pair = dict(zip(lref, take_many([lb.columns[c] for c in lref], li)))
+            pair.update(zip(rref, take_many([raw.columns[names[c]] for c in rref], gather_tensor(pos, ok))))
+            li = gather_tensor(li, mask_to_indices(predicate_mask(j.residual, Batch(pair, ok.numel()), ctx)))
+        mark = torch.zeros(n_l, dtype=torch.bool, device=ctx.device)
+        if li.numel():
+            mark.index_fill_(0, li.long(), True)
+        keep = mask_to_indices(mark if j.kind == "semi" else ~mark)
+    ctx.note_partial_read(rcol.data, scanned[1])
+    out = _take_batch(lb, keep)
+    out.dist = lb.dist
+    return out
+
+
+def _rank_local_semi(lb: Batch, lkey, rb: Batch, rcid) -> bool:
+    """SPMD: a SEMI / ANTI join of ``lb`` against ``rb`` on ``lkey`` = column
+    ``rcid`` can run on each rank's rows alone: the build side is replicated,
+    or both sides are placed by the join key with the same mapping (lineitem
+    and orders by order key). The rank-local fast paths check this from the
+    placements (plan + catalog, alike on every rank); whatever size check
+    they make on their own rows may differ between ranks, which is safe
+    because the general path they fall back to issues no collective for
+    such inputs either (parallel/exchange.py prepare_join, semi_by_key_set)."""
+    from ..parallel.exchange import REPLICATED, copartitioned
+    if rb.dist == REPLICATED:
+        return True
+    return isinstance(lkey, ColRef) and copartitioned(lb.dist, lkey.cid, rb.dist, rcid)
+
+
+def apply_key_filters(b: Batch, filters, ctx) -> Batch:
+    for gexpr, lcol in filters:
+        with ctx.span("agg.runtime_filter"):
+            kcol = ctx.evaluator.column(gexpr, b)
+            pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
+            if b.num_rows == 0:
+                continue
+            sel = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
+            if sel is None:
+                sel, _ = H.JoinTable(bk, bvalid).probe_select(pk, pvalid, want_build=False)
+            if sel.numel() < b.num_rows:
+                keys = list(b.columns)
+                b = Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], sel))), sel.numel(), b.dist)
+    return b
+
+
+def _batch_bytes(b: Batch) -> int:
+    try:
+        return sum(c.nbytes for c in b.columns.values())
+    except Exception:  # noqa: BLE001 - lazy batches
+        return 0
+
+
+#: a join's working memory is taken as this multiple of its input bytes
+#: (hash table, pair lists, gathered output)
+JOIN_MEM_FACTOR = 3
+
+
+def _to_host(b: Batch) -> Batch:
+    """Spill a batch to (pinned) host memory."""
+    check_not_capturing("spill to host memory")
+    out = {}
+    for k, c in b.columns.items():
+        def mv(t):
+            if t is None or not t.is_cuda:
+                return t
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            return h
+        d = c.dictionary
+        out[k] = Column(c.dtype, mv(c.data), mv(c.valid), mv(c.offsets), d)
+    if b.num_rows and any(c.data.is_cuda for c in b.columns.values()):
+        torch.cuda.synchronize()
+    return Batch(out, b.num_rows, b.dist)
+
+
+def _to_device(b: Batch, dev) -> Batch:
+    return Batch({k: Column(c.dtype, c.data.to(dev, non_blocking=True),
+                            None if c.valid is None else c.valid.to(dev, non_blocking=True),
+                            None if c.offsets is None else c.offsets.to(dev, non_blocking=True), c.dictionary)
+                  for k, c in b.columns.items()}, b.num_rows, b.dist)
+
+
+def grace_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Optional[Batch]:
+    """Partitioned (grace) hash join for inputs whose working memory exceeds
+    ``ctx.budget``: both sides are hash-partitioned on the join keys into P
+    partitions, every partition is moved to pinned host memory, then each
+    partition pair is brought back and joined on the device on its own and
+    its output spilled; the outputs are concatenated at the end. Rows with
+    equal keys share a partition, so inner / left / semi / anti joins
+    decompose exactly (NULL keys go to partition 0 on both sides; NOT IN's
+    "any NULL on the build side" rule is decided before partitioning).
+    Returns None when the inputs fit the budget."""
+    if ctx.budget is None or not on or kind not in ("inner", "left", "semi", "anti"):
+        return None
+    need = JOIN_MEM_FACTOR * (_batch_bytes(lb) + _batch_bytes(rb))
+    if need <= ctx.budget or lb.num_rows == 0 or rb.num_rows == 0:
+        return None
+    from ..parallel.exchange import partition_keys
+    ev = ctx.evaluator
+    if kind == "anti" and null_aware:
+        rcols = [ev.column(b, rb) for _, b in on]
+        if any(c.valid is not None and to_host_int((~c.valid).any().to(torch.int64)) for c in rcols):
+            return _empty_like(lb)
+    P = 2
+    while need / P > ctx.budget / 2 and P < 1024:
+        P *= 2
+    dev = ctx.device
+
+    def parts(b: Batch, exprs) -> List[Batch]:
+        key = None
+        for e in exprs:
+            k = partition_keys(ev.column(e, b)).to(torch.int64)
+            key = k if key is None else (key * 1000003) ^ k
+        perm, counts = M.hash_partition(key.contiguous(), P)
+        out, start = [], 0
+        keys = list(b.columns)
+        for c in counts:
+            idx = perm[start:start + c]
+            start += c
+            cols = take_many([b.columns[k] for k in keys], idx) if keys else []
+            piece = Batch(dict(zip(keys, cols)), c)
+            ctx.spill["bytes"] += _batch_bytes(piece)
+            out.append(_to_host(piece) if dev.type == "cuda" else piece)
+        return out
+
+    with ctx.span("join.spill_partition"):
+        lparts = parts(lb, [a for a, _ in on])
+        rparts = parts(rb, [b for _, b in on])
+    ctx.spill["joins"] += 1
+    ctx.spill["partitions"] += P
+    outs = []
+    with ctx.span("join.spill_probe"):
+        saved, ctx.budget = ctx.budget, None      # each partition pair runs in memory
+        try:
+            for lp, rp in zip(lparts, rparts):
+                l_d, r_d = _to_device(lp, dev), _to_device(rp, dev)
+                o = hash_join(l_d, r_d, kind, on, residual, ctx, null_aware=null_aware)
+                outs.append(_to_host(o) if dev.type == "cuda" else o)
+        finally:
+            ctx.budget = saved
+    return concat_batches([_to_device(o, dev) for o in outs])
+
+
+def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Batch:
+    if ctx.budget is not None:
+        g = grace_join(lb, rb, kind, on, residual, ctx, null_aware)
+        if g is not None:
+            return g
+    ev = ctx.evaluator
+    if kind == "right":
+        # mirror into a left join
+        out = hash_join(rb, lb, "left", [(b, a) for a, b in on], residual, ctx)
+        return out
+    if kind == "cross" or not on:
+        return _nested_loop(lb, rb, kind, residual, ctx)
+    with ctx.span("join.keys"):
+        lcols = [ev.column(a, lb) for a, _ in on]
+        rcols = [ev.column(b, rb) for _, b in on]
+        lk, rk, lvalid, rvalid = key_tensors(lcols, rcols)
+    n_l, n_r = lb.num_rows, rb.num_rows
+    dev = ctx.device
+    # null-aware anti join (NOT IN): a NULL on the build side empties the result
+    if kind == "anti" and null_aware:
+        if rvalid is not None and n_r and to_host_int((~rvalid).any().to(torch.int64)):
+            return _empty_like(lb)
+        if n_r and lvalid is not None:
+            keep = mask_to_indices(lvalid)
+            lb = _take_batch(lb, keep)
+            lk = gather_tensor(lk, keep)
+            lvalid = None
+            n_l = lb.num_rows
+    if dev.type == "cuda" and len(on) == 1 and kind in ("inner", "semi", "anti", "left") and not null_aware:
+        out = _sorted_join(lb, rb, lk, rk, lvalid, rvalid, kind, residual, ctx)
+        if out is not None:
+            return out
+    if kind in ("semi", "anti") and not null_aware and n_l and n_r > 4 * n_l:
+        # EXISTS against a much larger relation (TPC-H Q21/Q4 shapes): build on
+        # the small probe side, stream the big side through it and flag the
+        # probe rows that found a (residual-qualified) partner
+        with ctx.span("join.build"):
+            table = H.JoinTable(lk, lvalid)
+        matched = torch.zeros(n_l, dtype=torch.bool, device=dev)
+        with ctx.span("join.probe"):
+            if residual is None:
+                table.probe_first(rk, rvalid, build_matched=matched)
+            else:
+                ridx, lidx, _ = table.probe_pairs(rk, rvalid)
+                pair = _combine(lb, rb, lidx, ridx, False)
+                keep = mask_to_indices(predicate_mask(residual, pair, ctx))
+                matched.index_fill_(0, gather_tensor(lidx, keep).long(), True)
+            sel = mask_to_indices(matched if kind == "semi" else ~matched)
+        with ctx.span("join.gather"):
+            return _take_batch(lb, sel)
+    if kind == "left" and residual is None and n_l and n_r > 4 * n_l:
+        # LEFT JOIN against a much larger relation (TPC-H Q13: customer ⟕ orders):
+        # build on the preserved side, stream the big side through it, then
+        # append the preserved rows nothing matched
+        with ctx.span("join.build"):
+            table = H.JoinTable(lk, lvalid)
+        matched = torch.zeros(n_l, dtype=torch.bool, device=dev)
+        with ctx.span("join.probe"):
+            if table.unique:
+                first = table.probe_first(rk, rvalid, build_matched=matched)
+                ridx = mask_to_indices(first >= 0)
+                lidx = gather_tensor(first, ridx)
+            else:
+                ridx, lidx, _ = table.probe_pairs(rk, rvalid, build_matched=matched)
+            miss = mask_to_indices(~matched)
+        with ctx.span("join.gather"):
+            all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
+            all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
+            return _combine(lb, rb, all_l, all_r, True)
+    if kind == "inner" and residual is None and n_l < n_r:
+        # build on the smaller side
+        out = hash_join(rb, lb, "inner", [(b, a) for a, b in on], None, ctx)
+        return out
+    with ctx.span("join.build"):
+        table = H.JoinTable(rk, rvalid)
+    if kind in ("semi", "anti") and residual is None:
+        with ctx.span("join.probe"):
+            sel, _ = table.probe_select(lk, lvalid, negate=kind != "semi", want_build=False)
+        with ctx.span("join.gather"):
+            return _take_batch(lb, sel)
+    if residual is None and table.unique and kind in ("inner", "left"):
+        with ctx.span("join.probe"):
+            if kind == "inner":
+                pidx, bidx = table.probe_select(lk, lvalid)
+            else:
+                first = table.probe_first(lk, lvalid)
+        with ctx.span("join.gather"):
+            if kind == "inner":
+                return _combine(lb, rb, pidx, bidx, False)
+            lidx = torch.arange(n_l, dtype=torch.int32, device=dev)
+            return _combine(lb, rb, lidx, first, True)
+    matched = torch.zeros(n_r, dtype=torch.bool, device=dev) if (kind == "full" and residual is None) else None
+    with ctx.span("join.probe_pairs"):
+        pidx, bidx, counts = table.probe_pairs(lk, lvalid, matched)
+    if residual is not None:
+        with ctx.span("join.residual"):
+            pair = _combine(lb, rb, pidx, bidx, False)
+            keep = predicate_mask(residual, pair, ctx)
+        sel = mask_to_indices(keep)
+        pidx = gather_tensor(pidx, sel)
+        bidx = gather_tensor(bidx, sel)
+        if kind in ("semi", "anti", "left", "full"):
+            hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
+            hit.index_fill_(0, pidx.long(), True)
+            if kind == "semi":
+                return _take_batch(lb, mask_to_indices(hit))
+            if kind == "anti":
+                return _take_batch(lb, mask_to_indices(~hit))
+            if kind == "full":
+                matched = torch.zeros(n_r, dtype=torch.bool, device=dev)
+                matched.index_fill_(0, bidx.long(), True)
+            counts = hit.to(torch.int32)
+        else:
+            return _combine(lb, rb, pidx, bidx, False)
+    if kind == "inner":
+        with ctx.span("join.gather"):
+            return _combine(lb, rb, pidx, bidx, False)
+    if kind in ("left", "full"):
+        # unmatched probe rows get a NULL build side
+        miss = mask_to_indices(counts == 0)
+        all_l = torch.cat([pidx.to(torch.int64), miss.to(torch.int64)])
+        all_r = torch.cat([bidx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
+        out = _combine(lb, rb, all_l, all_r, True)
+        if kind == "full":
+            um = mask_to_indices(~matched)
+            extra = _combine(lb, rb, torch.full((um.numel(),), -1, dtype=torch.int64, device=dev), um.to(torch.int64),
+                             True, left_null=True)
+            out = concat_batches([out, extra])
+        return out
+    if kind == "semi":
+        return _take_batch(lb, mask_to_indices(counts > 0))
+    if kind == "anti":
+        return _take_batch(lb, mask_to_indices(counts == 0))
+    raise NotSupported(f"join kind {kind}")
+
+
+#: big side of a join at least this large is checked for a sorted key column
+SORTED_JOIN_MIN_ROWS = 1 << 22
+
+
+def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residual, ctx) -> Optional[Batch]:
+    """Join against a big side whose key column is sorted (clustered tables:
+    lineitem by l_orderkey, orders by o_orderkey, and every filtered / joined
+    batch that preserved that order). The small side binary-searches its key
+    range in the big side instead of hashing and streaming the big side
+    (TPC-H Q21: 1.5M probes into 600M lineitem rows instead of 980M probes),
+    and the output stays in key order, which the GROUP BY then exploits.
+    Returns None when the shape does not apply."""
+    n_l, n_r = lb.num_rows, rb.num_rows
+    if n_l == 0 or n_r == 0:
+        return None
+    big_right = n_r >= n_l if kind == "inner" else True
+    big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
+    nb, ns = big.numel(), small.numel()
+    if nb < SORTED_JOIN_MIN_ROWS or 4 * ns > nb or bvalid is not None:
+        return None
+    with ctx.span("join.sorted_check"):
+        if not H.is_sorted(big):
+            return None
+    dev = ctx.device
+    with ctx.span("join.sorted_search"):
+        lo, cnt = H.sorted_ranges(big, small, svalid)
+    if kind in ("semi", "anti") and residual is None:
+        with ctx.span("join.gather"):
+            m = cnt > 0
+            return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
+    if kind in ("semi", "anti") and dev.type == "cuda":
+        cmp = _col_compare(residual, lb, rb)
+        if cmp is not None:
+            with ctx.span("join.sorted_exists"):
+                lcol, rcol, op = cmp   # residual: lcol OP rcol; the big side is the right
+                m = H.sorted_exists(rcol, lcol, lo, cnt, FLIP_OP[op])
+                return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
+    with ctx.span("join.sorted_expand"):
+        sidx, bidx = H.expand_ranges(lo, cnt, nb)
+        lidx, ridx = (sidx, bidx) if big_right else (bidx, sidx)
+    if residual is not None:
+        with ctx.span("join.residual"):
+            pair = _combine(lb, rb, lidx, ridx, False)
+            keep = mask_to_indices(predicate_mask(residual, pair, ctx))
+            lidx = gather_tensor(lidx, keep)
+            ridx = gather_tensor(ridx, keep)
+            if kind == "inner":
+                return _take_batch(pair, keep)
+    if kind == "inner":
+        with ctx.span("join.gather"):
+            return _combine(lb, rb, lidx, ridx, False)
+    hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
+    hit.index_fill_(0, lidx.long(), True)
+    if kind == "semi":
+        return _take_batch(lb, mask_to_indices(hit))
+    if kind == "anti":
+        return _take_batch(lb, mask_to_indices(~hit))
+    # left join, big right side
+    miss = mask_to_indices(~hit)
+    all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
+    all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
+    return _combine(lb, rb, all_l, all_r, True)
+
+
+FLIP_OP = {"=": "=", "<>": "<>", "<": ">", "<=": ">=", ">": "<", ">=": "<="}
+_CMP_KINDS = ("int8", "int16", "int32", "int64", "date32")
+
+
+def _col_compare(residual, lb: Batch, rb: Batch):
+    """(left data, right data, op) when the residual is ``left_col OP right_col``
+    over non-null integer-like columns of one type; else None."""
+    if not (isinstance(residual, BinOp) and residual.op in FLIP_OP and isinstance(residual.left, ColRef)
+            and isinstance(residual.right, ColRef)):
+        return None
+    l, r, op = residual.left, residual.right, residual.op
+    if l.cid in rb.columns and r.cid in lb.columns:
+        l, r, op = r, l, FLIP_OP[op]
+    if l.cid not in lb.columns or r.cid not in rb.columns:
+        return None
+    a, b = lb.columns[l.cid], rb.columns[r.cid]
+    if a.valid is not None or b.valid is not None or a.dtype != b.dtype or a.dtype.kind not in _CMP_KINDS \
+            or a.is_dict or b.is_dict:
+        return None
+    return a.data, b.data, op
+
+
+def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:
+    n_l, n_r = lb.num_rows, rb.num_rows
+    if n_l * n_r > 2**31:
+        raise ExecutionError(f"cross join of {n_l} x {n_r} rows is too large")
+    dev = ctx.device
+    li = torch.arange(n_l, device=dev, dtype=torch.int64).repeat_interleave(n_r)
+    ri = torch.arange(n_r, device=dev, dtype=torch.int64).repeat(n_l)
+    pair = _combine(lb, rb, li, ri, False)
+    if residual is not None:
+        keep = mask_to_indices(predicate_mask(residual, pair, ctx))
+        li, ri = gather_tensor(li, keep), gather_tensor(ri, keep)
+        pair = _take_batch(pair, keep) if kind in ("inner", "cross") else pair
+    if kind in ("inner", "cross"):
+        return pair
+    hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
+    hit.index_fill_(0, li.long(), True)
+    if kind == "semi":
+        return _take_batch(lb, mask_to_indices(hit))
+    if kind == "anti":
+        return _take_batch(lb, mask_to_indices(~hit))
+    if kind in ("left", "full"):
+        miss = mask_to_indices(~hit).to(torch.int64)
+        out = _combine(lb, rb, torch.cat([li, miss]), torch.cat([ri, torch.full_like(miss, -1)]), True)
+        if kind == "full":
+            rh = torch.zeros(n_r, dtype=torch.bool, device=dev)
+            rh.index_fill_(0, ri.long(), True)
+            um = mask_to_indices(~rh).to(torch.int64)
+            out = concat_batches([out, _combine(lb, rb, torch.full_like(um, -1), um, True, left_null=True)])
+        return out
+    raise NotSupported(f"nested loop join kind {kind}")
+
+
+def _take_batch(b: Batch, idx: torch.Tensor, neg: bool = False) -> Batch:
+    keys = list(b.columns)
+    cols = take_many([b.columns[k] for k in keys], idx, neg)
+    return Batch(dict(zip(keys, cols)), idx.numel())
+
+
+def _combine(lb: Batch, rb: Batch, lidx, ridx, right_nullable: bool, left_null: bool = False) -> Batch:
+    out = {}
+    n = lidx.numel()
+    lkeys, rkeys = list(lb.columns), list(rb.columns)
+    lcols = take_many([lb.columns[k] for k in lkeys], lidx, neg=left_null) if lkeys else []
+    rcols = take_many([rb.columns[k] for k in rkeys], ridx, neg=right_nullable) if rkeys else []
+    out.update(zip(lkeys, lcols))
+    out.update(zip(rkeys, rcols))
+    return Batch(out, n)
+
+
+def _empty_like(b: Batch) -> Batch:
+    idx = torch.zeros(0, dtype=torch.int32, device=next(iter(b.columns.values())).device) if b.columns else torch.zeros(0, dtype=torch.int32)
+    return _take_batch(b, idx)
+
+
+def concat_batches(bs: List[Batch]) -> Batch:
+    bs = [b for b in bs if b is not None]
+    if not bs:
+        return Batch({}, 0)
+    if len(bs) == 1:
+        return bs[0]
+    keys = list(bs[0].columns)
+    out = {}
+    for k in keys:
+        out[k] = concat_columns([b.columns[k] for b in bs])
+    return Batch(out, sum(b.num_rows for b in bs))
+
+
+def concat_columns(cols: List[Column]) -> Column:
+    c0 = cols[0]
+    dev = c0.device
+    valid = None
+    if any(c.valid is not None for c in cols):
+        valid = torch.cat([c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool, device=dev)
+                           for c in cols])
+    if c0.dtype.is_string:
+        if all(c.is_dict and c.dictionary is c0.dictionary for c in cols):
+            return Column(c0.dtype, torch.cat([c.data for c in cols]), valid, dictionary=c0.dictionary)
+        plains = [S.decode(c) for c in cols]
+        offs, base = [], 0
+        for i, p in enumerate(plains):
+            o = p.offsets if i == 0 else p.offsets[1:]
+            offs.append(o + base)
+            base += to_host_int(p.offsets[-1:])
+        return Column(T.UTF8, torch.cat([p.data for p in plains]), valid, offsets=torch.cat(offs))
+    if any(c.is_wide for c in cols) and not all(c.is_wide for c in cols):
+        cols = [c if c.is_wide else Column(c.dtype, torch.stack([c.data, c.data >> 63], 1), c.valid) for c in cols]
+    return Column(c0.dtype, torch.cat([c.data for c in cols]), valid)
+
+
+# ====================================================================== multi join
+def _resident_ndv(t: torch.Tensor) -> int:
+    """NDV of a resident key column (HyperLogLog, remembered on the tensor)."""
+    d = getattr(t, "_igloo_ndv", None)
+    if d is None:
+        with unlogged():      # remembered on the resident tensor: a one-time build
+            d = max(1, int(round(H.hll_estimate(H.hll_sketch(t)))))
+        try:
+            t._igloo_ndv = d
+        except (AttributeError, RuntimeError):
+            pass
+    return d
+
+
+def _dense_lookup_ok(big: torch.Tensor, nq: int) -> bool:
+    """A sorted resident key column whose dense lower-bound table exists (or
+    is built now, once): a lookup is two reads whatever the probe count, so
+    the join needs no hash table even when the other side is not much
+    smaller (TPC-H customer.c_custkey against 5.7M-22.7M filtered orders)."""
+    if not (DENSE_JOIN and getattr(big, "_igloo_resident", False) and nq >= H.DENSE_RESIDENT_MIN_QUERIES):
+        return False
+    if not H.is_sorted(big):
+        return False
+    return bool(H.dense_index(big, build=True, queries=nq))
+
+
+#: inner_pairs: sorted resident key columns with a dense index take the range path at any size ratio
+DENSE_JOIN = os.environ.get("IGLOO_DENSE_JOIN", "1") == "1"
+#: HashJoinExec: [NOT] EXISTS against a filtered scan sorted on the key runs as an index nested loop
+SEMI_INDEX = os.environ.get("IGLOO_SEMI_INDEX", "1") == "1"
+#: ... and the smaller side's sorted resident key column serves the bigger side's lookups
+DENSE_JOIN_SMALL = True
+
+
+def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(left row, right row) index pairs of an inner equi-join on packed keys:
+    binary search into a sorted big side, else hash build on the smaller side
+    (first-match probe when the build keys are unique)."""
+    n_l, n_r = lk.numel(), rk.numel()
+    dev = lk.device
+    if n_l == 0 or n_r == 0:
+        z = torch.zeros(0, dtype=torch.int32, device=dev)
+        return z, z
+    big_right = n_r >= n_l
+    big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
+    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS and bvalid is None \
+            and (4 * small.numel() <= big.numel() or _dense_lookup_ok(big, small.numel())) and H.is_sorted(big):
+        with ctx.span("join.sorted_search"):
+            lo, cnt = H.sorted_ranges(big, small, svalid)
+        with ctx.span("join.sorted_expand"):
+            sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
+        ctx.note_partial_read(big, sidx.numel())
+        return (sidx, bidx) if big_right else (bidx, sidx)
+    if dev.type == "cuda" and DENSE_JOIN_SMALL and svalid is None and small.numel() >= SORTED_JOIN_MIN_ROWS \
+            and _dense_lookup_ok(small, big.numel()):
+        # the smaller side is a sorted resident key column with a dense index
+        # (customer.c_custkey against 22.7M filtered orders in Q5): every row of
+        # the bigger side looks its key up (two reads) — no hash table is built
+        with ctx.span("join.dense_lookup"):
+            lo, cnt = H.sorted_ranges(small, big, bvalid)
+            bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
+        return (sidx, bidx) if big_right else (bidx, sidx)
+    if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
+            and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
+            and small.numel() * (big.numel() / _resident_ndv(big)) * PERM_INDEX_SORT_FRAC <= big.numel():
+        # unsorted resident column, much smaller other side: search its
+        # secondary index and touch only the matching rows
+        skeys, perm = H.perm_index(big)
+        with ctx.span("join.index_search"):
+            lo, cnt = H.sorted_ranges(skeys, small, svalid)
+            scanned = exclusive_scan(cnt)     # one sync: size check + expansion offsets
+            total = scanned[1]
+        # the index hands out rows grouped by key, i.e. in random row order:
+        # for a large result the ordered hash probe output gathers (and
+        # probes later sorted joins) far more cheaply, so the index only
+        # serves results below 1/PERM_INDEX_MAX_FRAC of the column
+        if total * PERM_INDEX_SORT_FRAC <= big.numel():
+            ctx.note_partial_read(big, total)
+            with ctx.span("join.index_expand"):
+                sidx, pos = H.expand_ranges(lo, cnt, big.numel(), scanned)
+                bidx = gather_tensor(perm, pos)
+                if bidx.dtype != sidx.dtype:
+                    bidx = bidx.to(sidx.dtype)
+            if total * PERM_INDEX_MAX_FRAC > big.numel():
+                # a larger result (Q9: 32.6M of 600M lineitem rows for the
+                # green parts): back into row order with one radix sort of the
+                # pairs, so later gathers and sorted joins read ascending rows
+                # — cheaper than probing all 600M keys (an L2-line fetch per
+                # bitmap lookup)
+                from ..ops.sort import sort_pairs
+                with ctx.span("join.index_sort"):
+                    bidx, sidx = sort_pairs(bidx, sidx, max(1, (big.numel() - 1).bit_length()))
+            return (sidx, bidx) if big_right else (bidx, sidx)
+    # hash: build on the smaller side, probe with the bigger
+    with ctx.span("join.build"):
+        table = H.JoinTable(small, svalid)
+    with ctx.span("join.probe"):
+        if table.unique:
+            bsel, ssel = table.probe_select(big, bvalid)
+        else:
+            bsel, ssel, _ = table.probe_pairs(big, bvalid)
+    return (ssel, bsel) if big_right else (bsel, ssel)
+
+
+#: join a resident unsorted key column through its secondary index when the
+#: other side has at most 1/PERM_INDEX_RATIO of its rows
+PERM_INDEX = os.environ.get("IGLOO_PERM_INDEX", "1") == "1"
+PERM_INDEX_RATIO = int(os.environ.get("IGLOO_PERM_INDEX_RATIO", "32"))
+PERM_INDEX_MAX_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_MAX_FRAC", "20"))
+#: results up to 1/PERM_INDEX_SORT_FRAC of the column still take the index,
+#: sorted back into row order (above 1/PERM_INDEX_MAX_FRAC)
+PERM_INDEX_SORT_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_SORT_FRAC", "8"))
+
+_INT_KEYS = ("int32", "int64")
+TWO_KEY_SORTED = True
+
+
+def _two_key_sorted_pairs(A, B, on, ctx) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """Two-column inner equi-join whose bigger side is sorted on one of the two
+    key columns (partsupp on ps_partkey in Q9's (partkey, suppkey) join): a
+    binary search finds each probe row's range of the sorted key and the other
+    key is compared inside that range on the device (ops.hashing
+    .sorted_match_pairs) — no key packing, no hash table. None when the shape
+    does not apply (nulls, non-integer keys, unsorted big side)."""
+    if A.num_rows == 0 or B.num_rows == 0:
+        return None
+    ev = ctx.evaluator
+    big_right = B.num_rows >= A.num_rows
+    big_rel, small_rel = (B, A) if big_right else (A, B)
+    pair_cols = []
+    for x, y in on:
+        bx, sx = (y, x) if big_right else (x, y)
+        bc, sc = ev.column(bx, big_rel), ev.column(sx, small_rel)
+        if bc.dtype.kind not in _INT_KEYS or sc.dtype.kind not in _INT_KEYS or bc.valid is not None \
+                or sc.valid is not None:
+            return None
+        pair_cols.append((bc.data, sc.data))
+    for first in (0, 1):
+        b1, s1 = pair_cols[first]
+        b2, s2 = pair_cols[1 - first]
+        if b1.numel() < SORTED_JOIN_MIN_ROWS or not H.is_sorted(b1):
+            continue
+        dt = torch.int64 if torch.int64 in (b1.dtype, s1.dtype) else torch.int32
+        k2 = torch.int64 if torch.int64 in (b2.dtype, s2.dtype) else torch.int32
+        with ctx.span("join.sorted_match"):
+            sidx, bidx = H.sorted_match_pairs(b1.to(dt), b2.to(k2), s1.to(dt), s2.to(k2))
+        return (sidx, bidx) if big_right else (bidx, sidx)
+    return None
+
+
+class _LazyColumns:
+    """Mapping view of a LateBatch: gathers a column the first time it is read."""
+
+    def __init__(self, lb: "LateBatch"):
+        self._lb = lb
+
+    def __getitem__(self, cid):
+        return self._lb.gather(cid)
+
+    def get(self, cid, default=None):
+        return self._lb.gather(cid) if cid in self._lb.owner else default
+
+    def __contains__(self, cid):
+        return cid in self._lb.owner
+
+    def __iter__(self):
+        return iter(self._lb.owner)
+
+    def __len__(self):
+        return len(self._lb.owner)
+
+    def keys(self):
+        return list(self._lb.owner)
+
+    def values(self):
+        # lazy: a caller that only looks at the first column gathers one
+        return (self._lb.gather(c) for c in list(self._lb.owner))
+
+    def items(self):
+        return ((c, self._lb.gather(c)) for c in list(self._lb.owner))
+
+
+class LateBatch(Batch):
+    """Intermediate join result as row indices into the joined inputs (late
+    materialization): only key / residual columns are gathered while the join
+    order unfolds, payload columns once at the end — instead of re-gathering
+    every column of every intermediate (TPC-H Q9: six inputs, 33M rows)."""
+
+    def __init__(self, parts, n: int, dist=None):  # noqa: D401 - Batch attributes are lazy here
+        self.parts = parts          # [(base Batch, row index tensor | None for identity)]
+        self._n = n
+        self.dist = dist
+        self._cache: Dict[int, Column] = {}
+        self.owner = {cid: k for k, (bb, _) in enumerate(parts) for cid in bb.columns}
+
+    @property
+    def num_rows(self):  # type: ignore[override]
+        return self._n
+
+    @property
+    def columns(self):  # type: ignore[override]
+        return _LazyColumns(self)
+
+    @property
+    def device(self):
+        """Device of the join result, from its index tensors (gathers nothing)."""
+        for bb, idx in self.parts:
+            d = idx.device if idx is not None else batch_device(bb)
+            if d is not None:
+                return d
+        return None
+
+    def gather(self, cid) -> Column:
+        c = self._cache.get(cid)
+        if c is None:
+            bb, idx = self.parts[self.owner[cid]]
+            if idx is None:
+                c = bb.columns[cid]
+            elif isinstance(bb, _LazyScanBatch):
+                c = bb.take_rows([cid], idx)[0]
+            else:
+                c = take(bb.columns[cid], idx)
+            self._cache[cid] = c
+        return c
+
+    def compose(self, sel: torch.Tensor):
+        return [(bb, sel if idx is None else gather_tensor(idx, sel).to(sel.dtype if sel.dtype == torch.int64
+                                                                               else idx.dtype))
+                for bb, idx in self.parts]
+
+    def materialize(self) -> Batch:
+        out: Dict[int, Column] = {}
+        for bb, idx in self.parts:
+            keys = list(bb.columns)
+            if idx is None:
+                out.update({k: bb.columns[k] for k in keys})
+            else:
+                pending = [k for k in keys if k not in self._cache]
+                out.update({k: self._cache[k] for k in keys if k in self._cache})
+                if isinstance(bb, _LazyScanBatch):
+                    out.update(zip(pending, bb.take_rows(pending, idx)))
+                else:
+                    out.update(zip(pending, take_many([bb.columns[k] for k in pending], idx)))
+        return Batch(out, self._n, self.dist)
+
+
+PRUNE_PARTS = True
+
+
+#: a multi-way join returns its LateBatch (row indices into the inputs) to the
+#: parent instead of materialising every input column
+LAZY_JOIN_OUTPUT = True
+
+
+class MultiJoinExec(ExecNode):
+    """N-ary inner join. Inputs are materialised first, then joined greedily:
+    each step joins the connected pair with the smallest estimated result
+    (|A|*|B| / max(ndv_A(key), ndv_B(key)), exact NDVs from the GPU hash
+    table), building on the smaller side."""
+
+    def __init__(self, logical: L.MultiJoin, children: List[ExecNode]):
+        self.logical = logical
+        self.children = children
+        self.required = None   # column ids the parent reads (set by the planner when known)
+        for ch in children[:len(logical.children)]:
+            if isinstance(ch, ScanExec):
+                ch.late_ok = True
+        self.order_log: List[str] = []
+
+    #: a semi join is applied to its input before the join when the subquery
+    #: side has at most this fraction of the input's rows
+    EAGER_SEMI_RATIO = 0.125
+
+    def describe(self):
+        lg = self.logical
+        extra = f", semi=[{'; '.join(s.sql() for s in lg.semis)}]" if lg.semis else ""
+        return f"{len(lg.children)} inputs, conds=[{', '.join(c.sql() for c in lg.conds)}]{extra}"
+
+    def _semi(self, lb: Batch, rb: Batch, sp, ctx) -> Batch:
+        if isinstance(lb, LateBatch):
+            lb = lb.materialize()
+        elif isinstance(lb, _LazyScanBatch):
+            lb = Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
+        agg = ctx.semi_builds.get(("multi", id(sp)))
+        if agg is not None and agg[0] is rb:
+            from .morsel import apply_semi_aggregate
+            return apply_semi_aggregate(lb, rb, agg[1], ctx)
+        if sp.kind == "semi" and sp.residual is None and not sp.null_aware and len(sp.on) == 1 \
+                and lb.num_rows and rb.num_rows:
+            # a small key set against a big resident column (Q18's 6.5K qualifying
+            # orders against 150M o_orderkey): its index ranges, not a full probe
+            le, re_ = sp.on[0]
+            if isinstance(le, ColRef) and isinstance(re_, ColRef) and le.cid in lb.columns and re_.cid in rb.columns \
+                    and (not ctx.spmd or _rank_local_semi(lb, le, rb, re_.cid)):
+                pk, bk, pvalid, bvalid = key_tensors([ctx.evaluator.column(le, lb)], [ctx.evaluator.column(re_, rb)])
+                rows = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
+                if rows is not None:
+                    out = _take_batch(lb, rows)
+                    out.dist = lb.dist
+                    return out
+        if ctx.spmd:
+            from ..parallel.exchange import prepare_join, semi_by_key_set
+            j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
+            out = semi_by_key_set(lb, rb, j, ctx)
+            if out is not None:
+                return out
+            lb, rb = prepare_join(lb, rb, j, ctx)
+            out = hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
+            out.dist = lb.out_dist
+            return out
+        return hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
+
+    def _run(self, ctx):
+        lg = self.logical
+        nch = len(lg.children)
+        rels = []
+        for ch in self.children[:nch]:
+            b = ch.execute(ctx)
+            rels.append({"batch": b, "cids": set(b.columns), "ndv": {}, "name": ch.describe()[:40],
+                         "scan": _scan_info(ch)})
+        self.order_log = []
+        deferred = []
+        semis = []
+        for sp, rex in zip(lg.semis, self.children[nch:]):
+            agg = None
+            if ctx.budget is not None:
+                # a build side over the budget: its aggregate instead (exec/morsel.py)
+                from .morsel import semi_aggregate
+                lc = set().union(*[{c.cid for c in ch.schema} for ch in lg.children])
+                agg = semi_aggregate(sp.kind, sp.on, sp.residual, sp.null_aware, lc, sp.right, rex, ctx,
+                                     ("multi", id(sp)))
+            semis.append((sp, agg[0] if agg is not None else rex.execute(ctx)))
+        conds = list(lg.conds)
+        # global row counts of every input (SPMD: every rank must derive the
+        # same join order) — together with the merged NDV sketches of every
+        # join key the ordering will ask for, in ONE collective
+        if ctx.spmd:
+            g = self._spmd_stats([r["batch"] for r in rels] + [rb for _, rb in semis],
+                                 self._ndv_needs(rels, conds), ctx, rels)
+        else:
+            g = _global_rows_many([r["batch"] for r in rels] + [rb for _, rb in semis], ctx)
+        for r, n in zip(rels, g):
+            r["grows"] = n
+        for (sp, rb), nrb in zip(semis, g[len(rels):]):
+            tgt = rels[sp.child]
+            if sp.kind == "semi" and nrb <= self.EAGER_SEMI_RATIO * tgt["grows"]:
+                tgt["batch"] = self._semi(tgt["batch"], rb, sp, ctx)
+                if ctx.spmd:
+                    # estimated (no collective): a semi join keeps at most the
+                    # subquery side's rows; key NDVs are capped alike
+                    tgt["grows"] = max(1, min(tgt["grows"], nrb))
+                    tgt["ndv"] = {k: max(1, min(v, tgt["grows"])) for k, v in tgt["ndv"].items()}
+                else:
+                    tgt["grows"] = _global_rows(tgt["batch"], ctx)
+                self.order_log.append(f"{sp.kind} pre-filter on {tgt['name']} -> {tgt['batch'].num_rows}")
+            else:
+                deferred.append((sp, rb))
+        while len(rels) > 1:
+            if ctx.spmd:
+                self._prefetch_ndv(rels, conds, ctx)
+            best = None
+            for i in range(len(rels)):
+                for k in range(i + 1, len(rels)):
+                    keys = _edges(conds, rels[i]["cids"], rels[k]["cids"])
+                    if not keys:
+                        continue
+                    est = self._estimate(rels[i], rels[k], keys, ctx)
+                    if best is None or est < best[0]:
+                        best = (est, i, k, keys)
+            if best is None:
+                # no join edge: cross join the two smallest inputs
+                order = sorted(range(len(rels)), key=lambda x: rels[x]["grows"])
+                i, k = sorted(order[:2])
+                keys = []
+            else:
+                _, i, k, keys = best
+            a, b = rels[i], rels[k]
+            cids = a["cids"] | b["cids"]
+            used = [c for c in conds if (col_refs(c) <= cids) and (not keys or c not in [kk[2] for kk in keys])]
+            resid = [c for c in used]
+            conds = [c for c in conds if c not in resid and (not keys or c not in [kk[2] for kk in keys])]
+            on = [(kk[0], kk[1]) for kk in keys]
+            la, lb_ = a["batch"], b["batch"]
+            out_dist = None
+            if ctx.spmd:
+                from ..parallel.exchange import prepare_join
+                fake = L.Join(None, None, "inner", on)  # type: ignore[arg-type]
+                la, lb_ = prepare_join(la, lb_, fake, ctx, rows=(a["grows"], b["grows"]))
+                out_dist = la.out_dist
+            over = ctx.budget is not None and \
+                JOIN_MEM_FACTOR * (_batch_bytes(la) + _batch_bytes(lb_)) > ctx.budget
+            # rank-local after prepare_join in SPMD too: index pairs over the
+            # (possibly exchanged) inputs, payload gathered once at the end
+            if on and not over:
+                out = self._late_join(la, lb_, on, and_all(resid), ctx)
+            else:
+                if isinstance(la, LateBatch):
+                    la = la.materialize()
+                if isinstance(lb_, LateBatch):
+                    lb_ = lb_.materialize()
+                if on:
+                    out = hash_join(la, lb_, "inner", on, and_all(resid), ctx)
+                else:
+                    out = _nested_loop(la, lb_, "inner", and_all(resid), ctx)
+            out.dist = out_dist
+            if self.required is not None and isinstance(out, LateBatch) and PRUNE_PARTS:
+                out = self._prune(out, conds, deferred)
+            self.order_log.append(f"{a['name']} ⋈ {b['name']} -> {out.num_rows}")
+            # key NDVs carry over (capped by the output size) instead of re-sketching intermediates.
+            # SPMD ranks take the estimate as the output's global size (every rank
+            # derives the same value with no collective; the estimate is from
+            # global counts and merged sketches) instead of counting it
+            if ctx.spmd:
+                cap = max(1, int(min(best[0], 2**62))) if best is not None else max(1, a["grows"] * b["grows"])
+            else:
+                cap = _global_rows(out, ctx)
+            ndv = {k: max(1, min(v, cap)) for d in (a["ndv"], b["ndv"]) for k, v in d.items()}
+            merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})", "grows": cap}
+            rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
+        b = rels[0]["batch"]
+        if isinstance(b, LateBatch) and not conds and not deferred and LAZY_JOIN_OUTPUT:
+            # hand the index form up: the parent gathers only the columns it
+            # reads (join keys and unused payload are never materialised)
+            return b
+        if isinstance(b, LateBatch):
+            with ctx.span("join.gather"):
+                b = b.materialize()
+        if conds:
+            b = filter_batch(b, and_all(conds), ctx)
+        for sp, rb in deferred:
+            b = self._semi(b, rb, sp, ctx)
+        return b
+
+    def _prune(self, out: "LateBatch", conds, deferred) -> "LateBatch":
+        """Drop index parts none of whose columns is read any more (by the
+        parent, a remaining join condition or a deferred semi join): later
+        steps then compose fewer row-index vectors."""
+        need = set(self.required)
+        for c in conds:
+            need |= col_refs(c)
+        for sp, _ in deferred:
+            for x, _y in sp.on:
+                need |= col_refs(x)
+            if sp.residual is not None:
+                need |= col_refs(sp.residual)
+        keep = [(bb, idx) for bb, idx in out.parts if any(c in need for c in bb.columns)] or out.parts[:1]
+        if len(keep) == len(out.parts):
+            return out
+        pruned = LateBatch(keep, out.num_rows, out.dist)
+        pruned._cache = {k: v for k, v in out._cache.items() if k in pruned.owner}
+        return pruned
+
+    def _late_join(self, la: Batch, lb: Batch, on, residual, ctx) -> "LateBatch":
+        """Inner join producing index pairs over the inputs' rows (no payload gather)."""
+        A = la if isinstance(la, LateBatch) else LateBatch([(la, None)], la.num_rows)
+        B = lb if isinstance(lb, LateBatch) else LateBatch([(lb, None)], lb.num_rows)
+        ev = ctx.evaluator
+        pairs = _two_key_sorted_pairs(A, B, on, ctx) \
+            if TWO_KEY_SORTED and len(on) == 2 and ctx.device.type == "cuda" else None
+        if pairs is not None:
+            lidx, ridx = pairs
+        else:
+            with ctx.span("join.keys"):
+                lk, rk, lvalid, rvalid = key_tensors([ev.column(x, A) for x, _ in on],
+                                                     [ev.column(y, B) for _, y in on])
+            lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx)
+        if residual is not None:
+            with ctx.span("join.residual"):
+                P = LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
+                keep = mask_to_indices(predicate_mask(residual, P, ctx))
+                lidx = gather_tensor(lidx, keep)
+                ridx = gather_tensor(ridx, keep)
+        with ctx.span("join.compose"):
+            return LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
+
+    @staticmethod
+    def _ndv_needs(rels, conds, only=None) -> list:
+        """(relation, key expression) of every join key the next ordering step
+        asks an NDV for and that is not known yet."""
+        need = []
+        for i in range(len(rels)):
+            for k in range(i + 1, len(rels)):
+                keys = _edges(conds, rels[i]["cids"], rels[k]["cids"])
+                if keys:
+                    for rel, e in ((rels[i], keys[0][0]), (rels[k], keys[0][1])):
+                        if only is not None and rel is not only:
+                            continue
+                        if e.sql() not in rel["ndv"] and all(e.sql() != x.sql() or rel is not r for r, x in need):
+                            need.append((rel, e))
+        return need
+
+    def _spmd_stats(self, batches, need, ctx, rels=()) -> List[int]:
+        """SPMD: global row counts of ``batches`` (a replicated batch counts
+        once) and the global NDV of every ``need`` key, in ONE collective: an
+        all-gather of [counts | HLL registers] (counts summed, registers
+        max-merged locally) on the GPU, one all-reduce of [counts | exact local
+        distinct counts] on the CPU. Sets ``rel["ndv"]``; returns the counts.
+
+        Base-table key columns are sketched once: their global NDV (and the
+        table's global rows) is kept per engine, keyed by (table, column,
+        catalog version, cache generation); a later query reads it, and a
+        filtered scan of that column derives its NDV from it (Cardenas) with
+        its global row count — no sketch pass. Which keys are sketched follows
+        from the plan and that cache alone, so every rank sketches the same
+        ones (the all-gather's shape matches on every rank)."""
+        comm = ctx.comm
+        local = [0 if _replicated(b) else b.num_rows for b in batches]
+        eng = ctx.engine
+        cache = getattr(eng, "_gndv", None) if eng is not None else None
+        ver = (eng.catalog.version, eng.cache.generation) if cache is not None else None
+        plan = []      # per need: (kind, cache key, rel index)
+        for rel, e in need:
+            ri = next((i for i, r in enumerate(rels) if r is rel), None)
+            info = rel.get("scan")
+            kind, key = "sketch", None
+            if cache is not None and info is not None and isinstance(e, ColRef) and e.cid in info[1]:
+                key = (ver, info[0], info[1][e.cid])
+                if key in cache:
+                    kind = "derived" if info[2] else "cached"
+                elif not info[2]:
+                    kind = "sketch_base"
+            plan.append((kind, key, ri))
+        sk = [j for j, (kind, _, _) in enumerate(plan) if kind.startswith("sketch")]
+        if ctx.device.type != "cuda":
+            nd = []
+            for j in sk:
+                rel, e = need[j]
+                b = rel["batch"]
+                mine = b.num_rows and (not _replicated(b) or comm.rank == 0)   # a replicated input counts once
+                nd.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
+            g = comm.allreduce_ints(local + nd)
+            est = dict(zip(sk, g[len(local):]))
+            g = g[:len(local)]
+        else:
+            regs = []
+            for j in sk:
+                rel, e = need[j]
+                b = rel["batch"]
+                if b.num_rows:
+                    k, _ = group_key_tensor(ctx.evaluator.column(e, b))
+                    regs.append(H.hll_sketch(k))
+                else:
+                    regs.append(torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
+            parts = [device_ints(local, ctx.device)]
+            if regs:
+                parts.append(torch.stack(regs).view(torch.int64).reshape(-1))
+            allg = comm.allgather_tensor(torch.cat(parts)).view(comm.world_size, -1)
+            nb = len(local)
+            # counts and NDV estimates reach the host in one readback
+            vals = [allg[:, :nb].sum(0)]
+            if regs:
+                merged = allg[:, nb:].contiguous().view(torch.uint8).view(comm.world_size, len(regs), H.HLL_M) \
+                    .amax(0)
+                vals.append(H.hll_terms(merged).view(torch.int64).reshape(-1))
+            host = to_host_ints(torch.cat(vals))
+            g = host[:nb]
+            est = {}
+            for t, j in enumerate(sk):
+                z, zeros = np.array(host[nb + 2 * t:nb + 2 * t + 2], dtype=np.int64).view(np.float64)
+                est[j] = int(round(H.hll_from_terms(float(z), int(zeros))))
+        counts = [b.num_rows if _replicated(b) else n for b, n in zip(batches, g)]
+        for j, ((rel, e), (kind, key, ri)) in enumerate(zip(need, plan)):
+            if kind == "cached":
+                v = cache[key][0]
+            elif kind == "derived":
+                D, N = cache[key]
+                n = counts[ri] if ri is not None else rel["batch"].num_rows
+                sel = min(n / max(N, 1), 1.0)
+                v = max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / max(D, 1)))))))
+            else:
+                v = est[j]
+                if kind == "sketch_base" and ri is not None:
+                    if len(cache) > 4096:
+                        cache.clear()
+                    cache[key] = (max(v, 1), counts[ri])
+            rel["ndv"][e.sql()] = max(v, 1)
+        return counts
+
+    def _prefetch_ndv(self, rels, conds, ctx) -> None:
+        """SPMD: sketch every join key the next ordering step will ask for and
+        merge all rank sketches with ONE all-reduce (instead of one per key)."""
+        need = self._ndv_needs(rels, conds)
+        if not need:
+            return
+        if ctx.device.type != "cuda":
+            # CPU ranks: exact local distinct counts, summed (an upper bound) in one all-reduce
+            local = []
+            for rel, e in need:
+                b = rel["batch"]
+                mine = b.num_rows and (not _replicated(b) or ctx.comm.rank == 0)   # a replicated input counts once
+                local.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
+            for (rel, e), g in zip(need, ctx.comm.allreduce_ints(local)):
+                rel["ndv"][e.sql()] = max(g, 1)
+            return
+        regs = []
+        for rel, e in need:
+            b = rel["batch"]
+            if b.num_rows:
+                k, _ = group_key_tensor(ctx.evaluator.column(e, b))
+                regs.append(H.hll_sketch(k))
+            else:
+                regs.append(torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
+        merged = ctx.comm.allreduce_max_tensor(torch.stack(regs))
+        for (rel, e), r in zip(need, merged):
+            rel["ndv"][e.sql()] = max(int(round(H.hll_estimate(r))), 1)
+
+    def _estimate(self, a, b, keys, ctx) -> float:
+        na, nb = a["grows"], b["grows"]
+        ka, kb = keys[0][0], keys[0][1]
+        da = self._ndv(a, ka, ctx)
+        db = self._ndv(b, kb, ctx)
+        return na * nb / max(da, db, 1)
+
+    def _ndv(self, rel, e: Expr, ctx) -> int:
+        """NDV of a join key: HyperLogLog sketch on the GPU (one streaming read;
+        rank sketches merge by max, so the distributed estimate is global),
+        exact distinct count on the CPU."""
+        key = e.sql()
+        if key not in rel["ndv"]:
+            b = rel["batch"]
+            with ctx.span("multijoin.ndv"):
+                cached = None
+                if not ctx.spmd and b.num_rows:
+                    c = ctx.evaluator.column(e, b)
+                    # resident table columns: the sketch of the same tensor is reused across queries
+                    cached = getattr(c.data, "_igloo_ndv", None) if c.valid is None else None
+                base = getattr(c.data, "_igloo_base", None) if cached is None and not ctx.spmd and \
+                    b.num_rows and c.valid is None else None
+                if cached is not None:
+                    g = cached
+                elif base is not None:
+                    g = _derived_ndv(base, b.num_rows)
+                elif ctx.device.type == "cuda":
+                    if b.num_rows:
+                        c = ctx.evaluator.column(e, b)
+                        k, _ = group_key_tensor(c)
+                        regs = H.hll_sketch(k)
+                    else:
+                        regs = torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device)
+                    if ctx.spmd:
+                        # every rank takes part, even with an empty slice (collective order must match)
+                        regs = ctx.comm.allreduce_max_tensor(regs)
+                    if b.num_rows and c.valid is None and getattr(c.data, "_igloo_resident", False):
+                        with unlogged():     # remembered on the resident column below
+                            g = int(round(H.hll_estimate(regs)))
+                    else:
+                        g = int(round(H.hll_estimate(regs)))
+                else:
+                    g = 0
+                    if b.num_rows:
+                        c = ctx.evaluator.column(e, b)
+                        k, _ = group_key_tensor(c)
+                        g = H.ndv(k)
+                    if ctx.spmd:
+                        g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
+                if cached is None and not ctx.spmd and b.num_rows and c.valid is None and not c.is_dict:
+                    try:
+                        c.data._igloo_ndv = g
+                    except (AttributeError, RuntimeError):
+                        pass
+            rel["ndv"][key] = max(g, 1)
+        return rel["ndv"][key]
+
+
+
+
+def _derived_ndv(base, n: int) -> int:
+    """NDV of an n-row filtered subset of a source column with N rows and D
+    distinct values, by Cardenas' formula D * (1 - (1 - n/N)^(N/D)) (rows
+    selected independently of the key) — no pass over the subset. D comes
+    from one sketch of the source column, remembered on its tensor."""
+    col, N = base
+    D = getattr(col.data, "_igloo_ndv", None)
+    if D is None:
+        k, _ = group_key_tensor(col)
+        with unlogged():
+            D = max(int(round(H.hll_estimate(H.hll_sketch(k)))) if k.is_cuda else H.ndv(k), 1)
+        try:
+            col.data._igloo_ndv = D
+        except (AttributeError, RuntimeError):
+            pass
+    sel = min(n / max(N, 1), 1.0)
+    return max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / D))))))
+
+
+def _scan_info(node):
+    """(table, {cid: column name}, filtered) of a plain table-scan input of a
+    multi-way join, else None (SPMD NDV cache, MultiJoinExec._spmd_stats)."""
+    if not isinstance(node, ScanExec):
+        return None
+    s = node.logical
+    names = {c.cid: c.name for c in getattr(s, "table_cols", s.schema)}
+    names.update({c.cid: c.name for c in s.schema})
+    return (s.table, names, bool(s.filters))
+
+
+def _replicated(b) -> bool:
+    return getattr(b, "dist", None) == ("replicated",)
+
+
+def _global_rows(b: Batch, ctx) -> int:
+    if ctx.spmd and not _replicated(b):
+        return ctx.comm.allreduce_int(b.num_rows)
+    return b.num_rows
+
+
+def _global_rows_many(bs: Sequence[Batch], ctx) -> List[int]:
+    """Global row counts (a replicated batch's rows count once) in at most
+    one all-reduce."""
+    if ctx.spmd and any(not _replicated(b) for b in bs):
+        g = ctx.comm.allreduce_ints([0 if _replicated(b) else b.num_rows for b in bs])
+        return [b.num_rows if _replicated(b) else n for b, n in zip(bs, g)]
+    return [b.num_rows for b in bs]
+
+
+def _edges(conds, ca: set, cb: set):
+    """Equi-join edges between two inputs: list of (expr_a, expr_b, cond)."""
+    out = []
+    for c in conds:
+        if isinstance(c, BinOp) and c.op == "=":
+            l, r = col_refs(c.left), col_refs(c.right)
+            if l and r and l <= ca and r <= cb:
+                out.append((c.left, c.right, c))
+            elif l and r and l <= cb and r <= ca:
+                out.append((c.right, c.left, c))
+    return out

@@ -323,7 +323,8 @@ class _PartialStates:
     def _distribute(self, b: Batch) -> None:
         from ..ops import misc as M
         from ..parallel.exchange import partition_keys
-        from .operators import _batch_bytes, _to_host, take_many
+        from ..ops.gather import take_many
+        from .operators import _batch_bytes, _to_host
         P = len(self.spill)
         key = None
         for ci, _ in self.groups:

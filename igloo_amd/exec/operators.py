@@ -16,3039 +16,38 @@ reference's ExecutionPlan implementations and DataFusion's inherited ones
   SortExec        SortExec / top-k
   LimitExec       GlobalLimitExec
   UnionExec, ValuesExec
+
+The operators live in five modules -- ``context`` (ExecContext, ExecNode),
+``scan`` (scan / values / filter / projection), ``joins`` (binary and
+multi-way joins), ``aggregate`` (hash aggregation) and ``sorting`` (sort /
+limit / union); this module re-exports all of their names. Tunables are
+module constants of the module that reads them (e.g.
+``joins.SORTED_JOIN_MIN_ROWS``): patch them there.
 """
 from __future__ import annotations
 
-import math
-import os
-import re
-import time
-from fractions import Fraction
-from typing import Dict, List, Optional, Sequence, Tuple
-
-import numpy as np
-import pyarrow as pa
-import torch
-
-from .. import types as T
-from ..columnar import Batch, Column, batch_device
-from ..ops import agg as A
-from ..ops import hashing as H
-from ..ops import misc as M
-from ..ops import strings as S
-from ..ops._lib import (check_not_capturing, device_ints, launch, ptr, stream, to_host_f64s, to_host_int,
-                       to_host_ints, unlogged)
-from ..utils import trace as _trace
-from ..ops.gather import gather_tensor, take, take_many
-from ..ops.select import exclusive_scan, mask_to_indices
-from ..sql import logical as L
-from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
-from ..utils.errors import ExecutionError, NotSupported
-from . import fused
-from .expr_eval import Evaluator, Scalar, _convert_tensor
-
-
-class ExecContext:
-    """Per-query execution state: device, communicator, metrics, subquery cache."""
-
-    def __init__(self, engine=None, device="cpu", comm=None, analyze: bool = False):
-        self.engine = engine
-        self.device = torch.device(device)
-        self.comm = comm
-        self.analyze = analyze
-        self.metrics: Dict[int, dict] = {}
-        self._subq: Dict[int, object] = {}
-        self.evaluator = Evaluator(self)
-        self.spans: Dict[str, list] = {}  # phase -> [total ms, calls] (EXPLAIN ANALYZE only)
-        self.scan_cache: Dict[tuple, tuple] = {}  # (source, filters) -> (row ids, gathered columns by name)
-        # device working-memory budget of the join operators (bytes, None =
-        # unbounded): a join whose inputs exceed it runs partitioned, spilling
-        # partitions to pinned host memory (``grace_join``)
-        sess = getattr(engine, "session", None) or {}
-        gb = sess.get("device_budget_gb", os.environ.get("IGLOO_DEVICE_BUDGET_GB"))
-        self.budget = int(float(gb) * 2**30) if gb not in (None, "", 0, "0") else None
-        self.spill = {"joins": 0, "partitions": 0, "bytes": 0}
-        # rows of base tables this query read (each table once; index / range
-        # searches into a resident column subtract the rows they skipped)
-        self.rows_scanned = 0
-        self._scanned_sources: set = set()
-        # table sources this query read (engine.py polls their CDC probes before
-        # replaying the query's graph) and the cache-tier keys it was served
-        # from (a graph replay refreshes their LRU position)
-        self.sources: list = []
-        self.cache_keys: list = []
-        # morsel pipelines (exec/morsel.py): the streamed scan's current morsel
-        # (scan node id, raw batch, tag), results of the operators a pipeline
-        # computes once (node id -> Batch, for the node ids in memo_ids)
-        self.morsel = None
-        self.memo: Optional[dict] = None
-        self.memo_ids: set = set()
-        self.morsel_depth = 0
-        self.morsels = {"pipelines": 0, "morsels": 0, "rows": 0, "bytes": 0}
-        self.semi_builds: dict = {}   # aggregated SEMI / ANTI build sides (exec/morsel.py)
-        # raw scans a fast-path check already read (ScanExec.peek_raw): the
-        # general path that runs when the check fails reuses them
-        self.raw_peeks: Dict[int, Batch] = {}
-        # SPMD: {id(source): key column} of the replicated table this query
-        # splits by key range (parallel/slicing.py plan_slices)
-        self.slices: Dict[int, str] = {}
-
-    def note_scan(self, source, rows: int) -> None:
-        if id(source) not in self._scanned_sources:
-            self._scanned_sources.add(id(source))
-            self.sources.append(source)
-            self.rows_scanned += rows
-
-    def note_partial_read(self, t: torch.Tensor, rows_read: int) -> None:
-        """A join searched resident column ``t`` and touched only ``rows_read`` rows."""
-        if getattr(t, "_igloo_resident", False):
-            self.rows_scanned -= max(0, t.numel() - rows_read)
-
-    def span(self, name: str):
-        """Time a phase inside an operator (device-synchronised; no-op unless
-        analyzing); a roctx range when IGLOO_ROCTX=1 (utils/trace.py)."""
-        if self.analyze:
-            return _Span(self, name)
-        return _trace.Range(name) if _trace.ENABLED else _NOSPAN
-
-    def span_report(self) -> str:
-        rows = sorted(self.spans.items(), key=lambda kv: -kv[1][0])
-        return "\n".join(f"  {k:<28} {v[0]:10.3f} ms  x{v[1]}" for k, v in rows)
-
-    @property
-    def world(self) -> int:
-        return self.comm.world_size if self.comm is not None else 1
-
-    @property
-    def spmd(self) -> bool:
-        """Rows are spread over ranks: exchanges run (also a forced world of
-        one, parallel/comm.py ``force_spmd``, which runs every collective)."""
-        return self.comm is not None and self.comm.spmd
-
-    def scalar_subquery(self, e) -> object:
-        key = id(e.plan)
-        if key not in self._subq:
-            from .planner import execute_plan
-            b = execute_plan(e.plan, self)
-            if self.spmd:
-                from ..parallel.exchange import gather_all
-                b = gather_all(b, self)
-            if b.num_rows > 1:
-                raise ExecutionError("scalar subquery returned more than one row")
-            if b.num_rows == 0:
-                self._subq[key] = None
-            else:
-                col = b.columns[e.plan.schema[0].cid]
-                t = e.plan.schema[0].dtype
-                dv = _device_scalar(col, t)
-                if dv is not _NO_SCALAR:
-                    self._subq[key] = dv
-                    return dv
-                v = col.to_arrow()[0].as_py()
-                if t.is_decimal and v is not None:
-                    from decimal import Decimal
-                    v = int(Decimal(v).scaleb(t.scale))
-                elif t.kind == "date32" and v is not None:
-                    import datetime
-                    v = (v - datetime.date(1970, 1, 1)).days
-                self._subq[key] = v
-        return self._subq[key]
-
-
-_NO_SCALAR = object()
-
-
-def _device_scalar(col: Column, t):
-    """First value of a device column through the replayable readback path
-    (ops/_lib.py to_host_ints): integers, dates (days) and decimals (scaled
-    integers) as int, floats bit-exact, NULL as None. Other types return
-    ``_NO_SCALAR`` (host conversion)."""
-    d = col.data
-    if not d.is_cuda or col.offsets is not None or col.dictionary is not None or t.kind in ("null", "timestamp") \
-            or t.is_string:
-        return _NO_SCALAR
-    if col.valid is not None and not to_host_int(col.valid[:1]):
-        return None
-    if d.dim() == 2:
-        lo, hi = to_host_ints(d[:1].reshape(-1))
-        return (hi << 64) | (lo & 0xFFFFFFFFFFFFFFFF)
-    if d.dtype.is_floating_point:
-        return to_host_f64s(d[:1])[0]
-    if d.dtype == torch.bool:
-        return bool(to_host_int(d[:1]))
-    return to_host_int(d[:1])
-
-
-class _Span:
-    __slots__ = ("ctx", "name", "t0")
-
-    def __init__(self, ctx, name):
-        self.ctx, self.name = ctx, name
-
-    def __enter__(self):
-        _sync(self.ctx)
-        self.t0 = time.perf_counter()
-
-    def __exit__(self, *exc):
-        _sync(self.ctx)
-        v = self.ctx.spans.setdefault(self.name, [0.0, 0])
-        v[0] += (time.perf_counter() - self.t0) * 1e3
-        v[1] += 1
-        return False
-
-
-class _NoSpan:
-    def __enter__(self):
-        return None
-
-    def __exit__(self, *exc):
-        return False
-
-
-_NOSPAN = _NoSpan()
-
-
-def _sync(ctx):
-    if ctx.device.type == "cuda":
-        torch.cuda.synchronize(ctx.device)
-
-
-class ExecNode:
-    children: List["ExecNode"]
-    logical: L.Plan
-
-    def execute(self, ctx: ExecContext) -> Batch:
-        if ctx.memo is not None and id(self) in ctx.memo_ids:
-            # computed once per morsel pipeline (exec/morsel.py)
-            hit = ctx.memo.get(id(self))
-            if hit is None:
-                hit = ctx.memo[id(self)] = self._execute_traced(ctx)
-            return hit
-        return self._execute_traced(ctx)
-
-    def _execute_traced(self, ctx: ExecContext) -> Batch:
-        if _trace.ENABLED:
-            _trace.push(type(self).__name__)
-            try:
-                return self._execute(ctx)
-            finally:
-                _trace.pop()
-        return self._execute(ctx)
-
-    def _execute(self, ctx: ExecContext) -> Batch:
-        if ctx.analyze:
-            _sync(ctx)
-            t0 = time.perf_counter()
-        c0 = (ctx.comm.calls, ctx.comm.bytes_sent) if ctx.analyze and ctx.comm is not None else (0, 0)
-        out = self._run(ctx)
-        if ctx.analyze:
-            _sync(ctx)
-            m = {"ms": (time.perf_counter() - t0) * 1e3, "rows": out.num_rows, "dist": getattr(out, "dist", None)}
-            if ctx.comm is not None:
-                m["collectives"] = ctx.comm.calls - c0[0]
-                m["bytes"] = ctx.comm.bytes_sent - c0[1]
-            ctx.metrics[id(self)] = m
-        return out
-
-    def _run(self, ctx: ExecContext) -> Batch:  # pragma: no cover
-        raise NotImplementedError
-
-    def name(self) -> str:
-        return type(self).__name__
-
-    def describe(self) -> str:
-        return self.logical.label()
-
-    def explain(self, ctx: Optional[ExecContext] = None, indent: int = 0) -> str:
-        m = ""
-        if ctx is not None and id(self) in ctx.metrics:
-            mm = ctx.metrics[id(self)]
-            m = f"  [rows={mm['rows']}, time={mm['ms']:.3f}ms]"
-        lines = ["  " * indent + f"{self.name()}: {self.describe()}{m}"]
-        for c in self.children:
-            lines.append(c.explain(ctx, indent + 1))
-        return "\n".join(lines)
-
-
-# ============================================================================ scan
-_CID = re.compile(r"#\d+")
-
-
-def _tag_base(col: Column, src: Column, n_src: int):
-    if NDV_DERIVED and col.valid is None and not col.is_dict:
-        try:   # filtered subset of a source column: its NDV derives from the source's
-            col.data._igloo_base = (src, n_src)
-        except (AttributeError, RuntimeError):
-            pass
-
-
-class ScanExec(ExecNode):
-    #: set by a parent multi-way join: a filtered scan may hand over its rows
-    #: as indices into the source (LateBatch) instead of gathered columns
-    late_ok = False
-
-    def __init__(self, logical: L.Scan):
-        self.logical = logical
-        self.children = []
-
-    def describe(self):
-        s = self.logical
-        f = f", filters=[{', '.join(x.sql() for x in s.filters)}]" if s.filters else ""
-        return f"{s.table} projection=[{', '.join(c.name for c in s.schema)}]{f}"
-
-    def column_names(self):
-        """(source column names to read, their cids, cid -> ColInfo): the
-        projection plus every filter input."""
-        s = self.logical
-        table_cols = getattr(s, "table_cols", s.schema)
-        by_cid = {c.cid: c for c in table_cols}
-        for c in s.schema:
-            by_cid[c.cid] = c
-        need = {c.cid for c in s.schema}
-        for f in s.filters:
-            need |= col_refs(f)
-        return [by_cid[cid].name for cid in sorted(need)], need, by_cid
-
-    def pushable(self):
-        """Filters the source can test against row-group statistics (or None)."""
-        s = self.logical
-        if not (s.filters and getattr(s.source, "prunes", False)):
-            return None
-        from ..connectors.parquet import pushable_filters
-        _, need, by_cid = self.column_names()
-        return pushable_filters(s.filters, {cid: by_cid[cid].name for cid in need})
-
-    def scan_raw(self, ctx) -> Batch:
-        """Scanned columns (projection + filter inputs) before filtering, keyed by cid."""
-        if ctx.morsel is None and id(self) in ctx.raw_peeks:
-            return ctx.raw_peeks.pop(id(self))
-        s = self.logical
-        table_cols = getattr(s, "table_cols", s.schema)
-        names, need, by_cid = self.column_names()
-        slice_key = ctx.slices.get(id(s.source)) if ctx.morsel is None else None
-        if ctx.morsel is not None and ctx.morsel[0] == id(self):
-            raw = ctx.morsel[1]          # the current morsel of a pipeline (exec/morsel.py)
-        elif slice_key is not None:
-            # a query over replicated tables only: this rank's key-range
-            # slice of the largest one (parallel/slicing.py); read whole
-            # (no row-group pruning), so every scan of the table slices alike
-            from ..parallel.slicing import slice_columns
-            with ctx.span("scan.source"):
-                full = s.source.scan(names + ([slice_key] if slice_key not in names else []), ctx)
-                ctx.note_scan(s.source, full.num_rows)
-                scols, n, tag = slice_columns(full.columns, full.num_rows, slice_key, ctx.world, ctx.comm.rank)
-            cols = {cid: scols[by_cid[cid].name] for cid in sorted(need)}
-            kc = [cid for cid in sorted(need) if by_cid[cid].name == slice_key]
-            # (an unsorted key column splits by rows: partitioned, placed by no key)
-            return Batch(cols, n, (tag,) + tuple(kc) if tag is not None and kc else None)
-        else:
-            with ctx.span("scan.source"):
-                pf = self.pushable()
-                # row-group statistics pruning (the filter is still applied below)
-                raw = s.source.scan(names, ctx, filters=pf) if pf is not None else s.source.scan(names, ctx)
-            ctx.note_scan(s.source, raw.num_rows)
-        cols = {cid: raw.columns[by_cid[cid].name] for cid in sorted(need)}
-        dist = None
-        if ctx.spmd:
-            if getattr(s.source, "replicated", False):
-                dist = ("replicated",)
-            elif getattr(s.source, "partitioned_by", None):
-                pc = [c.cid for c in table_cols if c.name == s.source.partitioned_by]
-                dist = ("hash", pc[0]) if pc else None
-        return Batch(cols, raw.num_rows, dist)
-
-    def peek_raw(self, ctx) -> Batch:
-        """``scan_raw`` for a fast-path check that may still fall back to the
-        general path: the batch is kept so the scan is not read (decoded,
-        copied to the device) a second time when the check fails."""
-        raw = self.scan_raw(ctx)
-        if ctx.morsel is None:
-            ctx.raw_peeks[id(self)] = raw
-        return raw
-
-    @property
-    def predicate(self) -> Optional[Expr]:
-        return and_all(self.logical.filters) if self.logical.filters else None
-
-    def finish(self, b: Batch, ctx) -> Batch:
-        """Apply the fused scan filter and the projection to a ``scan_raw`` batch."""
-        s = self.logical
-        out_cids = [c.cid for c in s.schema]
-        if s.filters:
-            # one query scanning a table twice under the same filter (Q21's l1 and
-            # l3, Q11/Q15 view repeats) evaluates it and gathers each column once
-            name = {c.cid: c.name for c in getattr(s, "table_cols", s.schema)}
-            name.update({c.cid: c.name for c in s.schema})
-            fsql = tuple(sorted(_CID.sub("", f.sql()) for f in s.filters))
-            key = (id(s.source), b.num_rows, fsql, ctx.morsel[2] if ctx.morsel is not None else None)
-            hit = None if any("random" in x.lower() for x in fsql) else ctx.scan_cache.get(key)
-            if hit is None:
-                with ctx.span("scan.filter_eval"):
-                    m = predicate_mask(self.predicate, b, ctx)
-                    idx = mask_to_indices(m)
-                hit = ctx.scan_cache[key] = (idx, {})
-            idx, taken_by_name = hit
-            if self.late_ok and LATE_SCAN and ctx.device.type == "cuda":
-                # index form: the join gathers its key columns now and payload
-                # columns only for the rows that survive it
-                src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
-                return _LazyScanBatch(src, idx, name, taken_by_name, ctx)
-            todo = [c for c in out_cids if name[c] not in taken_by_name]
-            if todo:
-                with ctx.span("scan.filter_gather"):
-                    for c, col in zip(todo, take_many([b.columns[c] for c in todo], idx)):
-                        _tag_base(col, b.columns[c], b.num_rows)
-                        taken_by_name[name[c]] = col
-            return Batch({c: taken_by_name[name[c]] for c in out_cids}, idx.numel(), b.dist)
-        return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
-
-    def _run(self, ctx):
-        if ctx.budget is not None and self.logical.filters and not ctx.spmd \
-                and not (ctx.morsel is not None and ctx.morsel[0] == id(self)):
-            from .morsel import streamed_scan
-            out = streamed_scan(self, ctx)
-            if out is not None:
-                return out
-        return self.finish(self.scan_raw(ctx), ctx)
-
-
-def predicate_mask(pred: Expr, b: Batch, ctx) -> torch.Tensor:
-    """Filter mask: one fused VM kernel on the GPU when the predicate fits, else
-    node-by-node evaluation."""
-    if ctx.device.type == "cuda":
-        m = fused.predicate_mask(pred, b, ctx.evaluator)
-        if m is not None:
-            return m
-    return ctx.evaluator.mask(pred, b)
-
-
-class LazyBatch(Batch):
-    """A Batch materialised on first access (lets the aggregate fuse the scan
-    filter and skip building the filtered batch altogether)."""
-
-    def __init__(self, thunk, dist):  # noqa: D401 - no Batch.__init__: attributes are lazy
-        self._thunk = thunk
-        self._b = None
-        self.dist = dist
-
-    def _get(self) -> Batch:
-        if self._b is None:
-            self._b = self._thunk()
-        return self._b
-
-    @property
-    def columns(self):  # type: ignore[override]
-        return self._get().columns
-
-    @property
-    def num_rows(self):  # type: ignore[override]
-        return self._get().num_rows
-
-
-class FragmentInputExec(ExecNode):
-    """Output of another query fragment, materialized by the fragment scheduler."""
-
-    def __init__(self, logical: L.FragmentRef):
-        self.logical = logical
-        self.children = []
-
-    def _run(self, ctx):
-        inputs = getattr(ctx, "fragment_inputs", None) or {}
-        if self.logical.fragment_id not in inputs:
-            raise ExecutionError(f"input of fragment {self.logical.fragment_id} is not available")
-        return inputs[self.logical.fragment_id]
-
-
-class ValuesExec(ExecNode):
-    def __init__(self, logical: L.Values):
-        self.logical = logical
-        self.children = []
-
-    def _run(self, ctx):
-        v = self.logical
-        n = len(v.rows)
-        cols = {}
-        for j, ci in enumerate(v.schema):
-            vals = []
-            for r in v.rows:
-                e = ctx.evaluator.eval(r[j], Batch({}, 1))
-                vals.append(e.value if isinstance(e, Scalar) else e.to_pylist()[0])
-            cols[ci.cid] = _column_from_values(vals, ci.dtype, ctx.device)
-        return Batch(cols, n, ("replicated",) if ctx.spmd else None)
-
-
-def _column_from_values(vals, dtype, device) -> Column:
-    if dtype.is_decimal:
-        t = torch.tensor([0 if v is None else int(v) for v in vals], dtype=torch.int64)
-        valid = None if all(v is not None for v in vals) else torch.tensor([v is not None for v in vals])
-        return Column(dtype, t, valid).to(device)
-    if dtype.kind == "date32":
-        t = torch.tensor([0 if v is None else int(v) for v in vals], dtype=torch.int32)
-        valid = None if all(v is not None for v in vals) else torch.tensor([v is not None for v in vals])
-        return Column(dtype, t, valid).to(device)
-    if dtype.kind == "null":
-        return Column.full(None, T.NULL, len(vals), device)
-    return Column.from_arrow(pa.array(vals, dtype.to_arrow()), device=device, dtype=dtype,
-                             dict_encode=False if dtype.is_string else None)
-
-
-# ================================================================ filter / project
-class FilterExec(ExecNode):
-    def __init__(self, logical: L.Filter, child: ExecNode):
-        self.logical = logical
-        self.children = [child]
-        if isinstance(child, HashAggExec):
-            child.having = logical.pred     # HAVING: the aggregate may apply it while grouping
-
-    def describe(self):
-        return self.logical.pred.sql()
-
-    def _run(self, ctx):
-        b = self.children[0].execute(ctx)
-        return filter_batch(b, self.logical.pred, ctx)
-
-
-def filter_batch(b: Batch, pred: Expr, ctx) -> Batch:
-    with ctx.span("filter.eval"):
-        m = predicate_mask(pred, b, ctx)
-        idx = mask_to_indices(m)
-    if idx.numel() == b.num_rows:
-        return b
-    keys = list(b.columns)
-    with ctx.span("filter.gather"):
-        taken = take_many([b.columns[k] for k in keys], idx)
-    return Batch(dict(zip(keys, taken)), idx.numel(), b.dist)
-
-
-class ProjectExec(ExecNode):
-    def __init__(self, logical: L.Project, child: ExecNode):
-        self.logical = logical
-        self.children = [child]
-
-    def describe(self):
-        return ", ".join(e.sql() if isinstance(e, ColRef) and e.cid == c.cid else f"{e.sql()} AS {c.name}"
-                         for c, e in self.logical.exprs)
-
-    def _run(self, ctx):
-        b = self.children[0].execute(ctx)
-        from ..parallel.exchange import keyed
-        cols = {}
-        d = b.dist
-        # replicated / arbitrary carry over; a key placement keeps the
-        # output columns that are its key columns (renamed or not)
-        dist = d if d == ("replicated",) else None
-        placed = []
-        for ci, e in self.logical.exprs:
-            cols[ci.cid] = ctx.evaluator.column(e, b)
-            if keyed(d) and isinstance(e, ColRef) and e.cid in d[1:]:
-                placed.append(ci.cid)
-        if placed:
-            dist = (d[0],) + tuple(placed)
-        elif keyed(d):
-            dist = None
-        return Batch(cols, b.num_rows, dist)
-
-
-# ====================================================================== join keys
-def key_tensors(lcols: Sequence[Column], rcols: Sequence[Column]):
-    """Encode join keys of both sides into comparable int tensors (+ validity)."""
-    lk, rk = [], []
-    lvalid, rvalid = None, None
-    for a, b in zip(lcols, rcols):
-        ka, kb = _pair_key(a, b)
-        lk.append(ka)
-        rk.append(kb)
-        if a.valid is not None:
-            lvalid = a.valid if lvalid is None else lvalid & a.valid
-        if b.valid is not None:
-            rvalid = b.valid if rvalid is None else rvalid & b.valid
-    pl, pr = H.pack_keys_pair(lk, rk)
-    return pl, pr, lvalid, rvalid
-
-
-def _pair_key(a: Column, b: Column) -> Tuple[torch.Tensor, torch.Tensor]:
-    if a.dtype.is_string or b.dtype.is_string:
-        if a.is_dict and b.is_dict and a.dictionary is b.dictionary:
-            return a.data, b.data
-        from .expr_eval import _concat_strings
-        both = S.dict_encode(_concat_strings(S.decode(a), S.decode(b)))
-        n = len(a)
-        return both.data[:n], both.data[n:]
-    ta, tb = _num_key(a), _num_key(b)
-    if a.dtype != b.dtype and (a.dtype.is_decimal or b.dtype.is_decimal):
-        t = T.common_numeric(a.dtype, b.dtype)
-        ta, tb = _convert_tensor(a, t), _convert_tensor(b, t)
-    return ta, tb
-
-
-def _num_key(c: Column) -> torch.Tensor:
-    x = c.data
-    if x.dtype == torch.float64:
-        x = torch.where(x == 0, torch.zeros_like(x), x)  # -0.0 == 0.0
-        return x.view(torch.int64)
-    if x.dtype == torch.float32:
-        return x.to(torch.float64).view(torch.int64)
-    if x.dtype in (torch.bool, torch.int8, torch.int16, torch.uint8):
-        return x.to(torch.int32)
-    if c.is_wide:
-        raise NotSupported("128-bit decimal join / group keys")
-    return x
-
-
-def group_key_tensor(c: Column) -> Tuple[torch.Tensor, Column]:
-    """Int key per row for GROUP BY (NULL is its own group); returns (key, column to take reps from)."""
-    if c.dtype.is_string:
-        d = c if c.is_dict else S.dict_encode(c)
-        k = d.data.to(torch.int64)
-        if d.valid is not None:
-            k = torch.where(d.valid, k, torch.full_like(k, -1))
-        return k, d
-    k = _num_key(c)
-    if c.valid is not None:
-        if k.numel():
-            mx = to_host_int(k.max().to(torch.int64))
-            k = torch.where(c.valid, k.to(torch.int64), torch.full((k.numel(),), mx + 1, dtype=torch.int64, device=k.device))
-    return k, c
-
-
-# ============================================================================ join
-class HashJoinExec(ExecNode):
-    """Binary hash join (inner / left / right / full / semi / anti), build = right."""
-
-    def __init__(self, logical: L.Join, left: ExecNode, right: ExecNode):
-        self.logical = logical
-        self.children = [left, right]
-
-    def describe(self):
-        j = self.logical
-        on = ", ".join(f"{a.sql()} = {b.sql()}" for a, b in j.on)
-        r = f", filter={j.residual.sql()}" if j.residual is not None else ""
-        return f"{j.kind} on=[{on}]{r}"
-
-    def _run(self, ctx):
-        j = self.logical
-        if ctx.budget is not None and j.kind in ("semi", "anti"):
-            from .morsel import aggregated_semi_join
-            out = aggregated_semi_join(self, ctx)
-            if out is not None:
-                return out
-        lb = self.children[0].execute(ctx)
-        found = _semi_index_scan(self.children[1], j, ctx)
-        if found is not None:
-            out = _semi_index_then_filter(found, j, lb, ctx)
-            if out is not None:
-                return out
-        if j.kind in ("inner", "left", "semi") and j.on and ctx.memo is None:
-            # (not inside a morsel pipeline: the build side is computed once
-            # for all morsels, so it must not be narrowed to one morsel's keys)
-            push_key_filter(self.children[1], j.on, lb, ctx)
-        rb = self.children[1].execute(ctx)
-        if ctx.spmd:
-            from ..parallel.exchange import prepare_join, semi_by_key_set
-            out = semi_by_key_set(lb, rb, j, ctx)
-            if out is not None:
-                return out
-            lb, rb = prepare_join(lb, rb, j, ctx)
-            out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
-            out.dist = lb.out_dist
-            return out
-        return hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
-
-
-#: eager COUNT under LEFT JOIN: right-key spans up to this count with one histogram
-EAGER_COUNT_DIRECT_SPAN = 1 << 27
-#: HashAggExec._eager_count_masked (IGLOO_EAGER_COUNT_MASKED=0 turns it off)
-EAGER_COUNT_MASKED = os.environ.get("IGLOO_EAGER_COUNT_MASKED", "1") != "0"
-
-#: largest (global) probe side whose keys are pushed into the build side's aggregate
-RUNTIME_FILTER_MAX_ROWS = 16_000_000
-
-
-def _agg_group_source(node: ExecNode, cid: int):
-    """Follow output column ``cid`` down through projections / filters to the
-    aggregate that produces it as a GROUP BY key: (HashAggExec, group expr)."""
-    while True:
-        if isinstance(node, ProjectExec):
-            src = [e for ci, e in node.logical.exprs if ci.cid == cid]
-            if not src or not isinstance(src[0], ColRef):
-                return None
-            cid = src[0].cid
-            node = node.children[0]
-        elif isinstance(node, FilterExec):
-            node = node.children[0]
-        elif isinstance(node, HashAggExec):
-            for ci, e in node.logical.groups:
-                if ci.cid == cid:
-                    return node, e
-            return None
-        else:
-            return None
-
-
-def push_key_filter(build: ExecNode, on, lb: Batch, ctx) -> None:
-    """Sideways information passing: when the build side of an inner / left /
-    semi join is an aggregate grouped by the join key, only groups whose key
-    occurs on the (already materialised, small) probe side can ever match, so
-    the aggregate's INPUT is semi-joined with those keys before grouping.
-    TPC-H Q17/Q20/Q2: a correlated aggregate over all of lineitem/partsupp
-    shrinks to the handful of parts the outer query selected."""
-    # (the candidate is found from the plan first: a build side that is no
-    # aggregate costs no collective, so SPMD ranks that reach this point by
-    # different rank-local fast-path decisions stay aligned)
-    for a, b in on:
-        if not isinstance(b, ColRef):
-            continue
-        found = _agg_group_source(build, b.cid)
-        if found is None:
-            continue
-        agg, gexpr = found
-        if a.dtype.is_string or gexpr.dtype.is_string:
-            continue
-        lcol = ctx.evaluator.column(a, lb)
-        if ctx.spmd and lb.dist != ("replicated",):
-            # the global key set; the size check rides on the gather's own
-            # preamble (one collective fewer than counting first)
-            from ..parallel.exchange import gather_all
-            g = gather_all(Batch({0: lcol}, lb.num_rows, lb.dist), ctx, max_rows=RUNTIME_FILTER_MAX_ROWS)
-            if g is None:
-                return
-            lcol = g.columns[0]
-        elif lb.num_rows > RUNTIME_FILTER_MAX_ROWS:
-            return
-        agg.runtime_filters.append((gexpr, lcol))
-        return
-
-
-def _index_key_filter(pk: torch.Tensor, bk: torch.Tensor, bvalid, ctx) -> Optional[torch.Tensor]:
-    """Rows of the resident unsorted key column ``pk`` whose key is in the
-    small set ``bk``, ascending, through the column's secondary index (the
-    same rule as inner_pairs): only the matching ranges are read instead of
-    probing every row (TPC-H Q17: 20K parts against 600M l_partkey, where the
-    probe fetches an L2 line per row for its bitmap bit). None when it does
-    not apply."""
-    n = pk.numel()
-    if not (ctx.device.type == "cuda" and PERM_INDEX and getattr(pk, "_igloo_resident", False)
-            and n >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * bk.numel() <= n
-            and bk.numel() * (n / _resident_ndv(pk)) * PERM_INDEX_SORT_FRAC <= n):
-        return None
-    keys = (bk if bvalid is None else gather_tensor(bk, mask_to_indices(bvalid))).to(pk.dtype)
-    _, _, rep = H.group_ids(keys)                       # a key set: each matching row once
-    keys = gather_tensor(keys, rep)
-    srt = H.is_sorted(pk)                              # sorted column: its own index (no permutation)
-    skeys, perm = (pk, None) if srt else H.perm_index(pk)
-    with ctx.span("agg.runtime_filter_index"):
-        lo, cnt = H.sorted_ranges(skeys, keys)
-        scanned = exclusive_scan(cnt)
-        if scanned[1] * PERM_INDEX_SORT_FRAC > n:
-            return None
-        _, pos = H.expand_ranges(lo, cnt, n, scanned)
-        rows = pos if perm is None else gather_tensor(perm, pos)
-        from ..ops.sort import sort_pairs
-        rows, _ = sort_pairs(rows, rows, max(1, (n - 1).bit_length()))
-    ctx.note_partial_read(pk, scanned[1])
-    return rows
-
-
-def _index_then_filter(scan: "ScanExec", raw: Batch, filters, ctx):
-    """A runtime key filter over a FILTERED scan of a resident table, index
-    first: the rows whose key is in the (small) key set come from the key
-    column's index ranges (``_index_key_filter``), and the scan's own filter
-    runs only on them — instead of evaluating it over the whole table and
-    gathering every surviving row (TPC-H Q20: lineitem's one-year shipdate
-    filter keeps 91M of 600M rows before the 6M rows of the forest parts are
-    picked). Returns (batch, remaining filters) or None."""
-    ev = ctx.evaluator
-    for i, (gexpr, lcol) in enumerate(filters):
-        if not isinstance(gexpr, ColRef) or gexpr.cid not in raw.columns:
-            continue
-        kcol = raw.columns[gexpr.cid]
-        pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
-        if pvalid is not None or raw.num_rows == 0:
-            continue
-        rows = _index_key_filter(pk, bk, bvalid, ctx)
-        if rows is None:
-            continue
-        with ctx.span("agg.index_then_filter"):
-            keys = list(raw.columns)
-            sub = Batch(dict(zip(keys, take_many([raw.columns[k] for k in keys], rows))), rows.numel(), raw.dist)
-            m = predicate_mask(scan.predicate, sub, ctx)
-            keep = mask_to_indices(m)
-            out_cids = [c.cid for c in scan.logical.schema]
-            cols = take_many([sub.columns[c] for c in out_cids], keep)
-        return Batch(dict(zip(out_cids, cols)), keep.numel(), raw.dist), filters[:i] + filters[i + 1:]
-    return None
-
-
-def _semi_index_scan(rnode, j, ctx):
-    """The filtered resident scan under a [NOT] EXISTS build side, for
-    ``_semi_index_then_filter``: (scan, raw batch, key column, output cid ->
-    scan cid) or None. Cheap: resident columns are not filtered here."""
-    if not (SEMI_INDEX and ctx.device.type == "cuda" and ctx.budget is None and ctx.memo is None) \
-            or j.kind not in ("semi", "anti") or j.null_aware or len(j.on) != 1:
-        return None
-    le, re_ = j.on[0]
-    if not isinstance(le, ColRef) or not isinstance(re_, ColRef):
-        return None
-    chain = []
-    while isinstance(rnode, ProjectExec):               # column renames above the scan
-        chain.append(rnode)
-        rnode = rnode.children[0]
-    if not isinstance(rnode, ScanExec) or rnode.predicate is None:
-        return None
-
-    def resolve(cid):
-        for p in chain:
-            src = [e for ci, e in p.logical.exprs if ci.cid == cid]
-            if not src or not isinstance(src[0], ColRef):
-                return None
-            cid = src[0].cid
-        return cid
-    names = {c.cid: resolve(c.cid) for c in (chain[0].logical.schema if chain else rnode.logical.schema)}
-    raw = rnode.peek_raw(ctx)
-    rcol = raw.columns.get(names.get(re_.cid))
-    if rcol is None or rcol.valid is not None or rcol.dtype.is_string or raw.num_rows < SORTED_JOIN_MIN_ROWS \
-            or not getattr(rcol.data, "_igloo_resident", False) or not H.is_sorted(rcol.data):
-        return None
-    if j.residual is not None and any(c not in names or names[c] not in raw.columns
-                                      for c in col_refs(j.residual) if c in names):
-        return None
-    return rnode, raw, rcol, names
-
-
-def _semi_index_then_filter(found, j, lb: Batch, ctx) -> Optional[Batch]:
-    """[NOT] EXISTS against a FILTERED scan of a resident table sorted on
-    the join key, as an index nested loop: each left row's range of the
-    sorted key column (dense lower-bound table or binary search), the scan's
-    filter (and the join's residual) evaluated only on those candidate rows,
-    and a left row kept when some candidate passes (semi) or none does
-    (anti). TPC-H Q4: 5.7M orders against lineitem's commit < receipt filter
-    — 23M candidate rows checked instead of the filter over 600M rows, the
-    compaction and the gather of 385M keys; Q21's NOT EXISTS the same way
-    with its l_suppkey <> residual. None when the size does not apply."""
-    scan, raw, rcol, names = found
-    le, re_ = j.on[0]
-    n_r, n_l = raw.num_rows, lb.num_rows
-    if ctx.spmd and not _rank_local_semi(lb, le, raw, names.get(re_.cid)):
-        return None
-    if le.cid not in lb.columns or n_l == 0 or n_l * 2 > n_r:
-        return None
-    lcol = ctx.evaluator.column(le, lb)
-    if lcol.dtype.is_string:
-        return None
-    pl, pr, lvalid, _ = key_tensors([lcol], [rcol])
-    if pr is not rcol.data:
-        return None
-    with ctx.span("join.index_then_filter"):
-        _dense_lookup_ok(pr, n_l)           # the column's dense table, built once
-        lo, cnt = H.sorted_ranges(pr, pl, lvalid)
-        scanned = exclusive_scan(cnt)
-        if scanned[1] * PERM_INDEX_SORT_FRAC > n_r:
-            return None
-        lidx, pos = H.expand_ranges(lo, cnt, n_r, scanned)
-        # only the filter's inputs at every candidate; residual inputs at the survivors
-        keys = sorted(col_refs(scan.predicate))
-        sub = Batch(dict(zip(keys, take_many([raw.columns[k] for k in keys], pos))), pos.numel(), raw.dist)
-        ok = mask_to_indices(predicate_mask(scan.predicate, sub, ctx))
-        li = gather_tensor(lidx, ok)
-        if j.residual is not None and ok.numel():
-            refs = sorted(col_refs(j.residual))
-            lref = [c for c in refs if c in lb.columns]
-            rref = [c for c in refs if c not in lb.columns]
-            pair = dict(zip(lref, take_many([lb.columns[c] for c in lref], li)))
-            pair.update(zip(rref, take_many([raw.columns[names[c]] for c in rref], gather_tensor(pos, ok))))
-            li = gather_tensor(li, mask_to_indices(predicate_mask(j.residual, Batch(pair, ok.numel()), ctx)))
-        mark = torch.zeros(n_l, dtype=torch.bool, device=ctx.device)
-        if li.numel():
-            mark.index_fill_(0, li.long(), True)
-        keep = mask_to_indices(mark if j.kind == "semi" else ~mark)
-    ctx.note_partial_read(rcol.data, scanned[1])
-    out = _take_batch(lb, keep)
-    out.dist = lb.dist
-    return out
-
-
-def _rank_local_semi(lb: Batch, lkey, rb: Batch, rcid) -> bool:
-    """SPMD: a SEMI / ANTI join of ``lb`` against ``rb`` on ``lkey`` = column
-    ``rcid`` can run on each rank's rows alone: the build side is replicated,
-    or both sides are placed by the join key with the same mapping (lineitem
-    and orders by order key). The rank-local fast paths check this from the
-    placements (plan + catalog, alike on every rank); whatever size check
-    they make on their own rows may differ between ranks, which is safe
-    because the general path they fall back to issues no collective for
-    such inputs either (parallel/exchange.py prepare_join, semi_by_key_set)."""
-    from ..parallel.exchange import REPLICATED, copartitioned
-    if rb.dist == REPLICATED:
-        return True
-    return isinstance(lkey, ColRef) and copartitioned(lb.dist, lkey.cid, rb.dist, rcid)
-
-
-def apply_key_filters(b: Batch, filters, ctx) -> Batch:
-    for gexpr, lcol in filters:
-        with ctx.span("agg.runtime_filter"):
-            kcol = ctx.evaluator.column(gexpr, b)
-            pk, bk, pvalid, bvalid = key_tensors([kcol], [lcol])
-            if b.num_rows == 0:
-                continue
-            sel = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
-            if sel is None:
-                sel, _ = H.JoinTable(bk, bvalid).probe_select(pk, pvalid, want_build=False)
-            if sel.numel() < b.num_rows:
-                keys = list(b.columns)
-                b = Batch(dict(zip(keys, take_many([b.columns[k] for k in keys], sel))), sel.numel(), b.dist)
-    return b
-
-
-def _batch_bytes(b: Batch) -> int:
-    try:
-        return sum(c.nbytes for c in b.columns.values())
-    except Exception:  # noqa: BLE001 - lazy batches
-        return 0
-
-
-#: a join's working memory is taken as this multiple of its input bytes
-#: (hash table, pair lists, gathered output)
-JOIN_MEM_FACTOR = 3
-
-
-def _to_host(b: Batch) -> Batch:
-    """Spill a batch to (pinned) host memory."""
-    check_not_capturing("spill to host memory")
-    out = {}
-    for k, c in b.columns.items():
-        def mv(t):
-            if t is None or not t.is_cuda:
-                return t
-            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            h.copy_(t, non_blocking=True)
-            return h
-        d = c.dictionary
-        out[k] = Column(c.dtype, mv(c.data), mv(c.valid), mv(c.offsets), d)
-    if b.num_rows and any(c.data.is_cuda for c in b.columns.values()):
-        torch.cuda.synchronize()
-    return Batch(out, b.num_rows, b.dist)
-
-
-def _to_device(b: Batch, dev) -> Batch:
-    return Batch({k: Column(c.dtype, c.data.to(dev, non_blocking=True),
-                            None if c.valid is None else c.valid.to(dev, non_blocking=True),
-                            None if c.offsets is None else c.offsets.to(dev, non_blocking=True), c.dictionary)
-                  for k, c in b.columns.items()}, b.num_rows, b.dist)
-
-
-def grace_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Optional[Batch]:
-    """Partitioned (grace) hash join for inputs whose working memory exceeds
-    ``ctx.budget``: both sides are hash-partitioned on the join keys into P
-    partitions, every partition is moved to pinned host memory, then each
-    partition pair is brought back and joined on the device on its own and
-    its output spilled; the outputs are concatenated at the end. Rows with
-    equal keys share a partition, so inner / left / semi / anti joins
-    decompose exactly (NULL keys go to partition 0 on both sides; NOT IN's
-    "any NULL on the build side" rule is decided before partitioning).
-    Returns None when the inputs fit the budget."""
-    if ctx.budget is None or not on or kind not in ("inner", "left", "semi", "anti"):
-        return None
-    need = JOIN_MEM_FACTOR * (_batch_bytes(lb) + _batch_bytes(rb))
-    if need <= ctx.budget or lb.num_rows == 0 or rb.num_rows == 0:
-        return None
-    from ..parallel.exchange import partition_keys
-    ev = ctx.evaluator
-    if kind == "anti" and null_aware:
-        rcols = [ev.column(b, rb) for _, b in on]
-        if any(c.valid is not None and to_host_int((~c.valid).any().to(torch.int64)) for c in rcols):
-            return _empty_like(lb)
-    P = 2
-    while need / P > ctx.budget / 2 and P < 1024:
-        P *= 2
-    dev = ctx.device
-
-    def parts(b: Batch, exprs) -> List[Batch]:
-        key = None
-        for e in exprs:
-            k = partition_keys(ev.column(e, b)).to(torch.int64)
-            key = k if key is None else (key * 1000003) ^ k
-        perm, counts = M.hash_partition(key.contiguous(), P)
-        out, start = [], 0
-        keys = list(b.columns)
-        for c in counts:
-            idx = perm[start:start + c]
-            start += c
-            cols = take_many([b.columns[k] for k in keys], idx) if keys else []
-            piece = Batch(dict(zip(keys, cols)), c)
-            ctx.spill["bytes"] += _batch_bytes(piece)
-            out.append(_to_host(piece) if dev.type == "cuda" else piece)
-        return out
-
-    with ctx.span("join.spill_partition"):
-        lparts = parts(lb, [a for a, _ in on])
-        rparts = parts(rb, [b for _, b in on])
-    ctx.spill["joins"] += 1
-    ctx.spill["partitions"] += P
-    outs = []
-    with ctx.span("join.spill_probe"):
-        saved, ctx.budget = ctx.budget, None      # each partition pair runs in memory
-        try:
-            for lp, rp in zip(lparts, rparts):
-                l_d, r_d = _to_device(lp, dev), _to_device(rp, dev)
-                o = hash_join(l_d, r_d, kind, on, residual, ctx, null_aware=null_aware)
-                outs.append(_to_host(o) if dev.type == "cuda" else o)
-        finally:
-            ctx.budget = saved
-    return concat_batches([_to_device(o, dev) for o in outs])
-
-
-def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Batch:
-    if ctx.budget is not None:
-        g = grace_join(lb, rb, kind, on, residual, ctx, null_aware)
-        if g is not None:
-            return g
-    ev = ctx.evaluator
-    if kind == "right":
-        # mirror into a left join
-        out = hash_join(rb, lb, "left", [(b, a) for a, b in on], residual, ctx)
-        return out
-    if kind == "cross" or not on:
-        return _nested_loop(lb, rb, kind, residual, ctx)
-    with ctx.span("join.keys"):
-        lcols = [ev.column(a, lb) for a, _ in on]
-        rcols = [ev.column(b, rb) for _, b in on]
-        lk, rk, lvalid, rvalid = key_tensors(lcols, rcols)
-    n_l, n_r = lb.num_rows, rb.num_rows
-    dev = ctx.device
-    # null-aware anti join (NOT IN): a NULL on the build side empties the result
-    if kind == "anti" and null_aware:
-        if rvalid is not None and n_r and to_host_int((~rvalid).any().to(torch.int64)):
-            return _empty_like(lb)
-        if n_r and lvalid is not None:
-            keep = mask_to_indices(lvalid)
-            lb = _take_batch(lb, keep)
-            lk = gather_tensor(lk, keep)
-            lvalid = None
-            n_l = lb.num_rows
-    if dev.type == "cuda" and len(on) == 1 and kind in ("inner", "semi", "anti", "left") and not null_aware:
-        out = _sorted_join(lb, rb, lk, rk, lvalid, rvalid, kind, residual, ctx)
-        if out is not None:
-            return out
-    if kind in ("semi", "anti") and not null_aware and n_l and n_r > 4 * n_l:
-        # EXISTS against a much larger relation (TPC-H Q21/Q4 shapes): build on
-        # the small probe side, stream the big side through it and flag the
-        # probe rows that found a (residual-qualified) partner
-        with ctx.span("join.build"):
-            table = H.JoinTable(lk, lvalid)
-        matched = torch.zeros(n_l, dtype=torch.bool, device=dev)
-        with ctx.span("join.probe"):
-            if residual is None:
-                table.probe_first(rk, rvalid, build_matched=matched)
-            else:
-                ridx, lidx, _ = table.probe_pairs(rk, rvalid)
-                pair = _combine(lb, rb, lidx, ridx, False)
-                keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-                matched.index_fill_(0, gather_tensor(lidx, keep).long(), True)
-            sel = mask_to_indices(matched if kind == "semi" else ~matched)
-        with ctx.span("join.gather"):
-            return _take_batch(lb, sel)
-    if kind == "left" and residual is None and n_l and n_r > 4 * n_l:
-        # LEFT JOIN against a much larger relation (TPC-H Q13: customer ⟕ orders):
-        # build on the preserved side, stream the big side through it, then
-        # append the preserved rows nothing matched
-        with ctx.span("join.build"):
-            table = H.JoinTable(lk, lvalid)
-        matched = torch.zeros(n_l, dtype=torch.bool, device=dev)
-        with ctx.span("join.probe"):
-            if table.unique:
-                first = table.probe_first(rk, rvalid, build_matched=matched)
-                ridx = mask_to_indices(first >= 0)
-                lidx = gather_tensor(first, ridx)
-            else:
-                ridx, lidx, _ = table.probe_pairs(rk, rvalid, build_matched=matched)
-            miss = mask_to_indices(~matched)
-        with ctx.span("join.gather"):
-            all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
-            all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
-            return _combine(lb, rb, all_l, all_r, True)
-    if kind == "inner" and residual is None and n_l < n_r:
-        # build on the smaller side
-        out = hash_join(rb, lb, "inner", [(b, a) for a, b in on], None, ctx)
-        return out
-    with ctx.span("join.build"):
-        table = H.JoinTable(rk, rvalid)
-    if kind in ("semi", "anti") and residual is None:
-        with ctx.span("join.probe"):
-            sel, _ = table.probe_select(lk, lvalid, negate=kind != "semi", want_build=False)
-        with ctx.span("join.gather"):
-            return _take_batch(lb, sel)
-    if residual is None and table.unique and kind in ("inner", "left"):
-        with ctx.span("join.probe"):
-            if kind == "inner":
-                pidx, bidx = table.probe_select(lk, lvalid)
-            else:
-                first = table.probe_first(lk, lvalid)
-        with ctx.span("join.gather"):
-            if kind == "inner":
-                return _combine(lb, rb, pidx, bidx, False)
-            lidx = torch.arange(n_l, dtype=torch.int32, device=dev)
-            return _combine(lb, rb, lidx, first, True)
-    matched = torch.zeros(n_r, dtype=torch.bool, device=dev) if (kind == "full" and residual is None) else None
-    with ctx.span("join.probe_pairs"):
-        pidx, bidx, counts = table.probe_pairs(lk, lvalid, matched)
-    if residual is not None:
-        with ctx.span("join.residual"):
-            pair = _combine(lb, rb, pidx, bidx, False)
-            keep = predicate_mask(residual, pair, ctx)
-        sel = mask_to_indices(keep)
-        pidx = gather_tensor(pidx, sel)
-        bidx = gather_tensor(bidx, sel)
-        if kind in ("semi", "anti", "left", "full"):
-            hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
-            hit.index_fill_(0, pidx.long(), True)
-            if kind == "semi":
-                return _take_batch(lb, mask_to_indices(hit))
-            if kind == "anti":
-                return _take_batch(lb, mask_to_indices(~hit))
-            if kind == "full":
-                matched = torch.zeros(n_r, dtype=torch.bool, device=dev)
-                matched.index_fill_(0, bidx.long(), True)
-            counts = hit.to(torch.int32)
-        else:
-            return _combine(lb, rb, pidx, bidx, False)
-    if kind == "inner":
-        with ctx.span("join.gather"):
-            return _combine(lb, rb, pidx, bidx, False)
-    if kind in ("left", "full"):
-        # unmatched probe rows get a NULL build side
-        miss = mask_to_indices(counts == 0)
-        all_l = torch.cat([pidx.to(torch.int64), miss.to(torch.int64)])
-        all_r = torch.cat([bidx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
-        out = _combine(lb, rb, all_l, all_r, True)
-        if kind == "full":
-            um = mask_to_indices(~matched)
-            extra = _combine(lb, rb, torch.full((um.numel(),), -1, dtype=torch.int64, device=dev), um.to(torch.int64),
-                             True, left_null=True)
-            out = concat_batches([out, extra])
-        return out
-    if kind == "semi":
-        return _take_batch(lb, mask_to_indices(counts > 0))
-    if kind == "anti":
-        return _take_batch(lb, mask_to_indices(counts == 0))
-    raise NotSupported(f"join kind {kind}")
-
-
-#: big side of a join at least this large is checked for a sorted key column
-SORTED_JOIN_MIN_ROWS = 1 << 22
-#: HashAggExec._sorted_having: fused sorted GROUP BY + HAVING (IGLOO_SORTED_HAVING=0 turns it off)
-SORTED_HAVING = os.environ.get("IGLOO_SORTED_HAVING", "1") != "0"
-SORTED_HAVING_MIN_ROWS = 1 << 16
-
-
-def _sorted_join(lb: Batch, rb: Batch, lk, rk, lvalid, rvalid, kind: str, residual, ctx) -> Optional[Batch]:
-    """Join against a big side whose key column is sorted (clustered tables:
-    lineitem by l_orderkey, orders by o_orderkey, and every filtered / joined
-    batch that preserved that order). The small side binary-searches its key
-    range in the big side instead of hashing and streaming the big side
-    (TPC-H Q21: 1.5M probes into 600M lineitem rows instead of 980M probes),
-    and the output stays in key order, which the GROUP BY then exploits.
-    Returns None when the shape does not apply."""
-    n_l, n_r = lb.num_rows, rb.num_rows
-    if n_l == 0 or n_r == 0:
-        return None
-    big_right = n_r >= n_l if kind == "inner" else True
-    big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
-    nb, ns = big.numel(), small.numel()
-    if nb < SORTED_JOIN_MIN_ROWS or 4 * ns > nb or bvalid is not None:
-        return None
-    with ctx.span("join.sorted_check"):
-        if not H.is_sorted(big):
-            return None
-    dev = ctx.device
-    with ctx.span("join.sorted_search"):
-        lo, cnt = H.sorted_ranges(big, small, svalid)
-    if kind in ("semi", "anti") and residual is None:
-        with ctx.span("join.gather"):
-            m = cnt > 0
-            return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
-    if kind in ("semi", "anti") and dev.type == "cuda":
-        cmp = _col_compare(residual, lb, rb)
-        if cmp is not None:
-            with ctx.span("join.sorted_exists"):
-                lcol, rcol, op = cmp   # residual: lcol OP rcol; the big side is the right
-                m = H.sorted_exists(rcol, lcol, lo, cnt, FLIP_OP[op])
-                return _take_batch(lb, mask_to_indices(m if kind == "semi" else ~m))
-    with ctx.span("join.sorted_expand"):
-        sidx, bidx = H.expand_ranges(lo, cnt, nb)
-        lidx, ridx = (sidx, bidx) if big_right else (bidx, sidx)
-    if residual is not None:
-        with ctx.span("join.residual"):
-            pair = _combine(lb, rb, lidx, ridx, False)
-            keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-            lidx = gather_tensor(lidx, keep)
-            ridx = gather_tensor(ridx, keep)
-            if kind == "inner":
-                return _take_batch(pair, keep)
-    if kind == "inner":
-        with ctx.span("join.gather"):
-            return _combine(lb, rb, lidx, ridx, False)
-    hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
-    hit.index_fill_(0, lidx.long(), True)
-    if kind == "semi":
-        return _take_batch(lb, mask_to_indices(hit))
-    if kind == "anti":
-        return _take_batch(lb, mask_to_indices(~hit))
-    # left join, big right side
-    miss = mask_to_indices(~hit)
-    all_l = torch.cat([lidx.to(torch.int64), miss.to(torch.int64)])
-    all_r = torch.cat([ridx.to(torch.int64), torch.full((miss.numel(),), -1, dtype=torch.int64, device=dev)])
-    return _combine(lb, rb, all_l, all_r, True)
-
-
-FLIP_OP = {"=": "=", "<>": "<>", "<": ">", "<=": ">=", ">": "<", ">=": "<="}
-_CMP_KINDS = ("int8", "int16", "int32", "int64", "date32")
-
-
-def _col_compare(residual, lb: Batch, rb: Batch):
-    """(left data, right data, op) when the residual is ``left_col OP right_col``
-    over non-null integer-like columns of one type; else None."""
-    if not (isinstance(residual, BinOp) and residual.op in FLIP_OP and isinstance(residual.left, ColRef)
-            and isinstance(residual.right, ColRef)):
-        return None
-    l, r, op = residual.left, residual.right, residual.op
-    if l.cid in rb.columns and r.cid in lb.columns:
-        l, r, op = r, l, FLIP_OP[op]
-    if l.cid not in lb.columns or r.cid not in rb.columns:
-        return None
-    a, b = lb.columns[l.cid], rb.columns[r.cid]
-    if a.valid is not None or b.valid is not None or a.dtype != b.dtype or a.dtype.kind not in _CMP_KINDS \
-            or a.is_dict or b.is_dict:
-        return None
-    return a.data, b.data, op
-
-
-def _nested_loop(lb: Batch, rb: Batch, kind: str, residual, ctx) -> Batch:
-    n_l, n_r = lb.num_rows, rb.num_rows
-    if n_l * n_r > 2**31:
-        raise ExecutionError(f"cross join of {n_l} x {n_r} rows is too large")
-    dev = ctx.device
-    li = torch.arange(n_l, device=dev, dtype=torch.int64).repeat_interleave(n_r)
-    ri = torch.arange(n_r, device=dev, dtype=torch.int64).repeat(n_l)
-    pair = _combine(lb, rb, li, ri, False)
-    if residual is not None:
-        keep = mask_to_indices(predicate_mask(residual, pair, ctx))
-        li, ri = gather_tensor(li, keep), gather_tensor(ri, keep)
-        pair = _take_batch(pair, keep) if kind in ("inner", "cross") else pair
-    if kind in ("inner", "cross"):
-        return pair
-    hit = torch.zeros(n_l, dtype=torch.bool, device=dev)
-    hit.index_fill_(0, li.long(), True)
-    if kind == "semi":
-        return _take_batch(lb, mask_to_indices(hit))
-    if kind == "anti":
-        return _take_batch(lb, mask_to_indices(~hit))
-    if kind in ("left", "full"):
-        miss = mask_to_indices(~hit).to(torch.int64)
-        out = _combine(lb, rb, torch.cat([li, miss]), torch.cat([ri, torch.full_like(miss, -1)]), True)
-        if kind == "full":
-            rh = torch.zeros(n_r, dtype=torch.bool, device=dev)
-            rh.index_fill_(0, ri.long(), True)
-            um = mask_to_indices(~rh).to(torch.int64)
-            out = concat_batches([out, _combine(lb, rb, torch.full_like(um, -1), um, True, left_null=True)])
-        return out
-    raise NotSupported(f"nested loop join kind {kind}")
-
-
-def _take_batch(b: Batch, idx: torch.Tensor, neg: bool = False) -> Batch:
-    keys = list(b.columns)
-    cols = take_many([b.columns[k] for k in keys], idx, neg)
-    return Batch(dict(zip(keys, cols)), idx.numel())
-
-
-def _combine(lb: Batch, rb: Batch, lidx, ridx, right_nullable: bool, left_null: bool = False) -> Batch:
-    out = {}
-    n = lidx.numel()
-    lkeys, rkeys = list(lb.columns), list(rb.columns)
-    lcols = take_many([lb.columns[k] for k in lkeys], lidx, neg=left_null) if lkeys else []
-    rcols = take_many([rb.columns[k] for k in rkeys], ridx, neg=right_nullable) if rkeys else []
-    out.update(zip(lkeys, lcols))
-    out.update(zip(rkeys, rcols))
-    return Batch(out, n)
-
-
-def _empty_like(b: Batch) -> Batch:
-    idx = torch.zeros(0, dtype=torch.int32, device=next(iter(b.columns.values())).device) if b.columns else torch.zeros(0, dtype=torch.int32)
-    return _take_batch(b, idx)
-
-
-def concat_batches(bs: List[Batch]) -> Batch:
-    bs = [b for b in bs if b is not None]
-    if not bs:
-        return Batch({}, 0)
-    if len(bs) == 1:
-        return bs[0]
-    keys = list(bs[0].columns)
-    out = {}
-    for k in keys:
-        out[k] = concat_columns([b.columns[k] for b in bs])
-    return Batch(out, sum(b.num_rows for b in bs))
-
-
-def concat_columns(cols: List[Column]) -> Column:
-    c0 = cols[0]
-    dev = c0.device
-    valid = None
-    if any(c.valid is not None for c in cols):
-        valid = torch.cat([c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool, device=dev)
-                           for c in cols])
-    if c0.dtype.is_string:
-        if all(c.is_dict and c.dictionary is c0.dictionary for c in cols):
-            return Column(c0.dtype, torch.cat([c.data for c in cols]), valid, dictionary=c0.dictionary)
-        plains = [S.decode(c) for c in cols]
-        offs, base = [], 0
-        for i, p in enumerate(plains):
-            o = p.offsets if i == 0 else p.offsets[1:]
-            offs.append(o + base)
-            base += to_host_int(p.offsets[-1:])
-        return Column(T.UTF8, torch.cat([p.data for p in plains]), valid, offsets=torch.cat(offs))
-    if any(c.is_wide for c in cols) and not all(c.is_wide for c in cols):
-        cols = [c if c.is_wide else Column(c.dtype, torch.stack([c.data, c.data >> 63], 1), c.valid) for c in cols]
-    return Column(c0.dtype, torch.cat([c.data for c in cols]), valid)
-
-
-# ====================================================================== multi join
-def _resident_ndv(t: torch.Tensor) -> int:
-    """NDV of a resident key column (HyperLogLog, remembered on the tensor)."""
-    d = getattr(t, "_igloo_ndv", None)
-    if d is None:
-        with unlogged():      # remembered on the resident tensor: a one-time build
-            d = max(1, int(round(H.hll_estimate(H.hll_sketch(t)))))
-        try:
-            t._igloo_ndv = d
-        except (AttributeError, RuntimeError):
-            pass
-    return d
-
-
-def _dense_lookup_ok(big: torch.Tensor, nq: int) -> bool:
-    """A sorted resident key column whose dense lower-bound table exists (or
-    is built now, once): a lookup is two reads whatever the probe count, so
-    the join needs no hash table even when the other side is not much
-    smaller (TPC-H customer.c_custkey against 5.7M-22.7M filtered orders)."""
-    if not (DENSE_JOIN and getattr(big, "_igloo_resident", False) and nq >= H.DENSE_RESIDENT_MIN_QUERIES):
-        return False
-    if not H.is_sorted(big):
-        return False
-    return bool(H.dense_index(big, build=True, queries=nq))
-
-
-#: inner_pairs: sorted resident key columns with a dense index take the range path at any size ratio
-DENSE_JOIN = os.environ.get("IGLOO_DENSE_JOIN", "1") == "1"
-#: HashAggExec: a runtime key filter over a filtered resident scan takes the key index first
-INDEX_THEN_FILTER = os.environ.get("IGLOO_INDEX_THEN_FILTER", "1") == "1"
-#: HashJoinExec: [NOT] EXISTS against a filtered scan sorted on the key runs as an index nested loop
-SEMI_INDEX = os.environ.get("IGLOO_SEMI_INDEX", "1") == "1"
-#: ... also for the semi joins deferred past a multi-way join (off: Q21 10.0 -> 10.8 ms, the residual's pair
-#: gathers cost more than the build-side filter they save; profiles/r3_ab_semi_index.txt)
-SEMI_INDEX_MULTI = os.environ.get("IGLOO_SEMI_INDEX_MULTI", "0") == "1"
-#: ... and the smaller side's sorted resident key column serves the bigger side's lookups
-DENSE_JOIN_SMALL = os.environ.get("IGLOO_DENSE_JOIN_SMALL", "1") == "1"
-
-
-def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(left row, right row) index pairs of an inner equi-join on packed keys:
-    binary search into a sorted big side, else hash build on the smaller side
-    (first-match probe when the build keys are unique)."""
-    n_l, n_r = lk.numel(), rk.numel()
-    dev = lk.device
-    if n_l == 0 or n_r == 0:
-        z = torch.zeros(0, dtype=torch.int32, device=dev)
-        return z, z
-    big_right = n_r >= n_l
-    big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
-    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS and bvalid is None \
-            and (4 * small.numel() <= big.numel() or _dense_lookup_ok(big, small.numel())) and H.is_sorted(big):
-        with ctx.span("join.sorted_search"):
-            lo, cnt = H.sorted_ranges(big, small, svalid)
-        with ctx.span("join.sorted_expand"):
-            sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
-        ctx.note_partial_read(big, sidx.numel())
-        return (sidx, bidx) if big_right else (bidx, sidx)
-    if dev.type == "cuda" and DENSE_JOIN_SMALL and svalid is None and small.numel() >= SORTED_JOIN_MIN_ROWS \
-            and _dense_lookup_ok(small, big.numel()):
-        # the smaller side is a sorted resident key column with a dense index
-        # (customer.c_custkey against 22.7M filtered orders in Q5): every row of
-        # the bigger side looks its key up (two reads) — no hash table is built
-        with ctx.span("join.dense_lookup"):
-            lo, cnt = H.sorted_ranges(small, big, bvalid)
-            bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
-        return (sidx, bidx) if big_right else (bidx, sidx)
-    if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
-            and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
-            and small.numel() * (big.numel() / _resident_ndv(big)) * PERM_INDEX_SORT_FRAC <= big.numel():
-        # unsorted resident column, much smaller other side: search its
-        # secondary index and touch only the matching rows
-        skeys, perm = H.perm_index(big)
-        with ctx.span("join.index_search"):
-            lo, cnt = H.sorted_ranges(skeys, small, svalid)
-            scanned = exclusive_scan(cnt)     # one sync: size check + expansion offsets
-            total = scanned[1]
-        # the index hands out rows grouped by key, i.e. in random row order:
-        # for a large result the ordered hash probe output gathers (and
-        # probes later sorted joins) far more cheaply, so the index only
-        # serves results below 1/PERM_INDEX_MAX_FRAC of the column
-        if total * PERM_INDEX_SORT_FRAC <= big.numel():
-            ctx.note_partial_read(big, total)
-            with ctx.span("join.index_expand"):
-                sidx, pos = H.expand_ranges(lo, cnt, big.numel(), scanned)
-                bidx = gather_tensor(perm, pos)
-                if bidx.dtype != sidx.dtype:
-                    bidx = bidx.to(sidx.dtype)
-            if total * PERM_INDEX_MAX_FRAC > big.numel():
-                # a larger result (Q9: 32.6M of 600M lineitem rows for the
-                # green parts): back into row order with one radix sort of the
-                # pairs, so later gathers and sorted joins read ascending rows
-                # — cheaper than probing all 600M keys (an L2-line fetch per
-                # bitmap lookup)
-                from ..ops.sort import sort_pairs
-                with ctx.span("join.index_sort"):
-                    bidx, sidx = sort_pairs(bidx, sidx, max(1, (big.numel() - 1).bit_length()))
-            return (sidx, bidx) if big_right else (bidx, sidx)
-    # hash: build on the smaller side, probe with the bigger
-    with ctx.span("join.build"):
-        table = H.JoinTable(small, svalid)
-    with ctx.span("join.probe"):
-        if table.unique:
-            bsel, ssel = table.probe_select(big, bvalid)
-        else:
-            bsel, ssel, _ = table.probe_pairs(big, bvalid)
-    return (ssel, bsel) if big_right else (bsel, ssel)
-
-
-#: join a resident unsorted key column through its secondary index when the
-#: other side has at most 1/PERM_INDEX_RATIO of its rows
-PERM_INDEX = os.environ.get("IGLOO_PERM_INDEX", "1") == "1"
-PERM_INDEX_RATIO = int(os.environ.get("IGLOO_PERM_INDEX_RATIO", "32"))
-PERM_INDEX_MAX_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_MAX_FRAC", "20"))
-#: results up to 1/PERM_INDEX_SORT_FRAC of the column still take the index,
-#: sorted back into row order (above 1/PERM_INDEX_MAX_FRAC)
-PERM_INDEX_SORT_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_SORT_FRAC", "8"))
-
-_INT_KEYS = ("int32", "int64")
-TWO_KEY_SORTED = os.environ.get("IGLOO_TWO_KEY_SORTED", "1") == "1"
-
-
-def _two_key_sorted_pairs(A, B, on, ctx) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
-    """Two-column inner equi-join whose bigger side is sorted on one of the two
-    key columns (partsupp on ps_partkey in Q9's (partkey, suppkey) join): a
-    binary search finds each probe row's range of the sorted key and the other
-    key is compared inside that range on the device (ops.hashing
-    .sorted_match_pairs) — no key packing, no hash table. None when the shape
-    does not apply (nulls, non-integer keys, unsorted big side)."""
-    if A.num_rows == 0 or B.num_rows == 0:
-        return None
-    ev = ctx.evaluator
-    big_right = B.num_rows >= A.num_rows
-    big_rel, small_rel = (B, A) if big_right else (A, B)
-    pair_cols = []
-    for x, y in on:
-        bx, sx = (y, x) if big_right else (x, y)
-        bc, sc = ev.column(bx, big_rel), ev.column(sx, small_rel)
-        if bc.dtype.kind not in _INT_KEYS or sc.dtype.kind not in _INT_KEYS or bc.valid is not None \
-                or sc.valid is not None:
-            return None
-        pair_cols.append((bc.data, sc.data))
-    for first in (0, 1):
-        b1, s1 = pair_cols[first]
-        b2, s2 = pair_cols[1 - first]
-        if b1.numel() < SORTED_JOIN_MIN_ROWS or not H.is_sorted(b1):
-            continue
-        dt = torch.int64 if torch.int64 in (b1.dtype, s1.dtype) else torch.int32
-        k2 = torch.int64 if torch.int64 in (b2.dtype, s2.dtype) else torch.int32
-        with ctx.span("join.sorted_match"):
-            sidx, bidx = H.sorted_match_pairs(b1.to(dt), b2.to(k2), s1.to(dt), s2.to(k2))
-        return (sidx, bidx) if big_right else (bidx, sidx)
-    return None
-
-
-class _LazyColumns:
-    """Mapping view of a LateBatch: gathers a column the first time it is read."""
-
-    def __init__(self, lb: "LateBatch"):
-        self._lb = lb
-
-    def __getitem__(self, cid):
-        return self._lb.gather(cid)
-
-    def get(self, cid, default=None):
-        return self._lb.gather(cid) if cid in self._lb.owner else default
-
-    def __contains__(self, cid):
-        return cid in self._lb.owner
-
-    def __iter__(self):
-        return iter(self._lb.owner)
-
-    def __len__(self):
-        return len(self._lb.owner)
-
-    def keys(self):
-        return list(self._lb.owner)
-
-    def values(self):
-        # lazy: a caller that only looks at the first column gathers one
-        return (self._lb.gather(c) for c in list(self._lb.owner))
-
-    def items(self):
-        return ((c, self._lb.gather(c)) for c in list(self._lb.owner))
-
-
-class LateBatch(Batch):
-    """Intermediate join result as row indices into the joined inputs (late
-    materialization): only key / residual columns are gathered while the join
-    order unfolds, payload columns once at the end — instead of re-gathering
-    every column of every intermediate (TPC-H Q9: six inputs, 33M rows)."""
-
-    def __init__(self, parts, n: int, dist=None):  # noqa: D401 - Batch attributes are lazy here
-        self.parts = parts          # [(base Batch, row index tensor | None for identity)]
-        self._n = n
-        self.dist = dist
-        self._cache: Dict[int, Column] = {}
-        self.owner = {cid: k for k, (bb, _) in enumerate(parts) for cid in bb.columns}
-
-    @property
-    def num_rows(self):  # type: ignore[override]
-        return self._n
-
-    @property
-    def columns(self):  # type: ignore[override]
-        return _LazyColumns(self)
-
-    @property
-    def device(self):
-        """Device of the join result, from its index tensors (gathers nothing)."""
-        for bb, idx in self.parts:
-            d = idx.device if idx is not None else batch_device(bb)
-            if d is not None:
-                return d
-        return None
-
-    def gather(self, cid) -> Column:
-        c = self._cache.get(cid)
-        if c is None:
-            bb, idx = self.parts[self.owner[cid]]
-            if idx is None:
-                c = bb.columns[cid]
-            elif isinstance(bb, _LazyScanBatch):
-                c = bb.take_rows([cid], idx)[0]
-            else:
-                c = take(bb.columns[cid], idx)
-            self._cache[cid] = c
-        return c
-
-    def compose(self, sel: torch.Tensor):
-        return [(bb, sel if idx is None else gather_tensor(idx, sel).to(sel.dtype if sel.dtype == torch.int64
-                                                                               else idx.dtype))
-                for bb, idx in self.parts]
-
-    def materialize(self) -> Batch:
-        out: Dict[int, Column] = {}
-        for bb, idx in self.parts:
-            keys = list(bb.columns)
-            if idx is None:
-                out.update({k: bb.columns[k] for k in keys})
-            else:
-                pending = [k for k in keys if k not in self._cache]
-                out.update({k: self._cache[k] for k in keys if k in self._cache})
-                if isinstance(bb, _LazyScanBatch):
-                    out.update(zip(pending, bb.take_rows(pending, idx)))
-                else:
-                    out.update(zip(pending, take_many([bb.columns[k] for k in pending], idx)))
-        return Batch(out, self._n, self.dist)
-
-
-LATE_SCAN = os.environ.get("IGLOO_LATE_SCAN", "1") == "1"
-PRUNE_PARTS = os.environ.get("IGLOO_PRUNE_PARTS", "1") == "1"
-
-
-class _ScanColumns:
-    """Mapping view of a _LazyScanBatch: gathers a column on first read."""
-
-    def __init__(self, b: "_LazyScanBatch"):
-        self._b = b
-
-    def __getitem__(self, cid):
-        return self._b.gather(cid)
-
-    def get(self, cid, default=None):
-        return self._b.gather(cid) if cid in self._b.src.columns else default
-
-    def __contains__(self, cid):
-        return cid in self._b.src.columns
-
-    def __iter__(self):
-        return iter(self._b.src.columns)
-
-    def __len__(self):
-        return len(self._b.src.columns)
-
-    def keys(self):
-        return list(self._b.src.columns)
-
-    def values(self):
-        return (self._b.gather(c) for c in list(self._b.src.columns))
-
-    def items(self):
-        return ((c, self._b.gather(c)) for c in list(self._b.src.columns))
-
-
-class _LazyScanBatch(Batch):
-    """A filtered scan whose columns are gathered on first read (shared with
-    other scans of the same table under the same filter in the query). A
-    LateBatch over it gathers never-read payload columns straight from the
-    source through the composed row index — only for rows that survive the
-    join — while its own row indices stay those of the filtered scan."""
-
-    def __init__(self, src: Batch, idx: torch.Tensor, names: dict, shared: dict, ctx):  # noqa: D401
-        self.src, self.idx, self._names, self._shared, self._ctx = src, idx, names, shared, ctx
-        self.num_rows = idx.numel()
-        self.dist = src.dist
-        self.out_dist = None
-        self.columns = _ScanColumns(self)
-
-    @property
-    def device(self):
-        return self.idx.device
-
-    def has(self, cid) -> bool:
-        return self._names[cid] in self._shared
-
-    def gather(self, cid) -> Column:
-        c = self._shared.get(self._names[cid])
-        if c is None:
-            with self._ctx.span("scan.filter_gather"):
-                c = take(self.src.columns[cid], self.idx)
-            _tag_base(c, self.src.columns[cid], self.src.num_rows)
-            self._shared[self._names[cid]] = c
-        return c
-
-    def take_rows(self, cids, rows: torch.Tensor) -> List[Column]:
-        """Columns at filtered-scan rows ``rows``; unread ones via the source."""
-        out, pend = {}, []
-        for c in cids:
-            if self.has(c):
-                out[c] = take(self._shared[self._names[c]], rows)
-            else:
-                pend.append(c)
-        if pend:
-            comp = gather_tensor(self.idx, rows)
-            out.update(zip(pend, take_many([self.src.columns[c] for c in pend], comp)))
-        return [out[c] for c in cids]
-
-
-#: a multi-way join returns its LateBatch (row indices into the inputs) to the
-#: parent instead of materialising every input column
-LAZY_JOIN_OUTPUT = os.environ.get("IGLOO_LAZY_JOIN", "1") != "0"
-
-
-class _IndexSemi:
-    """A deferred semi / anti join build side taken by ``_semi_index_then_filter``."""
-
-    def __init__(self, node):
-        self.node = node
-
-
-def _plain(lb: Batch) -> Batch:
-    if isinstance(lb, LateBatch):
-        return lb.materialize()
-    if isinstance(lb, _LazyScanBatch):
-        return Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
-    return lb
-
-
-class MultiJoinExec(ExecNode):
-    """N-ary inner join. Inputs are materialised first, then joined greedily:
-    each step joins the connected pair with the smallest estimated result
-    (|A|*|B| / max(ndv_A(key), ndv_B(key)), exact NDVs from the GPU hash
-    table), building on the smaller side."""
-
-    def __init__(self, logical: L.MultiJoin, children: List[ExecNode]):
-        self.logical = logical
-        self.children = children
-        self.required = None   # column ids the parent reads (set by the planner when known)
-        for ch in children[:len(logical.children)]:
-            if isinstance(ch, ScanExec):
-                ch.late_ok = True
-        self.order_log: List[str] = []
-
-    #: a semi join is applied to its input before the join when the subquery
-    #: side has at most this fraction of the input's rows
-    EAGER_SEMI_RATIO = 0.125
-
-    def describe(self):
-        lg = self.logical
-        extra = f", semi=[{'; '.join(s.sql() for s in lg.semis)}]" if lg.semis else ""
-        return f"{len(lg.children)} inputs, conds=[{', '.join(c.sql() for c in lg.conds)}]{extra}"
-
-    def _semi(self, lb: Batch, rb: Batch, sp, ctx) -> Batch:
-        if isinstance(lb, LateBatch):
-            lb = lb.materialize()
-        elif isinstance(lb, _LazyScanBatch):
-            lb = Batch(dict(lb.columns.items()), lb.num_rows, lb.dist)
-        agg = ctx.semi_builds.get(("multi", id(sp)))
-        if agg is not None and agg[0] is rb:
-            from .morsel import apply_semi_aggregate
-            return apply_semi_aggregate(lb, rb, agg[1], ctx)
-        if sp.kind == "semi" and sp.residual is None and not sp.null_aware and len(sp.on) == 1 \
-                and lb.num_rows and rb.num_rows:
-            # a small key set against a big resident column (Q18's 6.5K qualifying
-            # orders against 150M o_orderkey): its index ranges, not a full probe
-            le, re_ = sp.on[0]
-            if isinstance(le, ColRef) and isinstance(re_, ColRef) and le.cid in lb.columns and re_.cid in rb.columns \
-                    and (not ctx.spmd or _rank_local_semi(lb, le, rb, re_.cid)):
-                pk, bk, pvalid, bvalid = key_tensors([ctx.evaluator.column(le, lb)], [ctx.evaluator.column(re_, rb)])
-                rows = _index_key_filter(pk, bk, bvalid, ctx) if pvalid is None else None
-                if rows is not None:
-                    out = _take_batch(lb, rows)
-                    out.dist = lb.dist
-                    return out
-        if ctx.spmd:
-            from ..parallel.exchange import prepare_join, semi_by_key_set
-            j = L.Join(None, None, sp.kind, sp.on, sp.residual, sp.null_aware)  # type: ignore[arg-type]
-            out = semi_by_key_set(lb, rb, j, ctx)
-            if out is not None:
-                return out
-            lb, rb = prepare_join(lb, rb, j, ctx)
-            out = hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
-            out.dist = lb.out_dist
-            return out
-        return hash_join(lb, rb, sp.kind, sp.on, sp.residual, ctx, null_aware=sp.null_aware)
-
-    def _run(self, ctx):
-        lg = self.logical
-        nch = len(lg.children)
-        rels = []
-        for ch in self.children[:nch]:
-            b = ch.execute(ctx)
-            rels.append({"batch": b, "cids": set(b.columns), "ndv": {}, "name": ch.describe()[:40],
-                         "scan": _scan_info(ch)})
-        self.order_log = []
-        deferred = []
-        semis = []
-        for sp, rex in zip(lg.semis, self.children[nch:]):
-            agg = None
-            if ctx.budget is not None:
-                # a build side over the budget: its aggregate instead (exec/morsel.py)
-                from .morsel import semi_aggregate
-                lc = set().union(*[{c.cid for c in ch.schema} for ch in lg.children])
-                agg = semi_aggregate(sp.kind, sp.on, sp.residual, sp.null_aware, lc, sp.right, rex, ctx,
-                                     ("multi", id(sp)))
-            elif SEMI_INDEX_MULTI and (found := _semi_index_scan(rex, sp, ctx)) is not None \
-                    and found[1].num_rows > self.EAGER_SEMI_RATIO * rels[sp.child]["batch"].num_rows:
-                # applied after the joins as an index nested loop (the filtered
-                # build side is never materialised): deferred unconditionally
-                deferred.append((sp, _IndexSemi(rex)))
-                continue
-            semis.append((sp, agg[0] if agg is not None else rex.execute(ctx)))
-        conds = list(lg.conds)
-        # global row counts of every input (SPMD: every rank must derive the
-        # same join order) — together with the merged NDV sketches of every
-        # join key the ordering will ask for, in ONE collective
-        if ctx.spmd:
-            g = self._spmd_stats([r["batch"] for r in rels] + [rb for _, rb in semis],
-                                 self._ndv_needs(rels, conds), ctx, rels)
-        else:
-            g = _global_rows_many([r["batch"] for r in rels] + [rb for _, rb in semis], ctx)
-        for r, n in zip(rels, g):
-            r["grows"] = n
-        for (sp, rb), nrb in zip(semis, g[len(rels):]):
-            tgt = rels[sp.child]
-            if sp.kind == "semi" and nrb <= self.EAGER_SEMI_RATIO * tgt["grows"]:
-                tgt["batch"] = self._semi(tgt["batch"], rb, sp, ctx)
-                if ctx.spmd:
-                    # estimated (no collective): a semi join keeps at most the
-                    # subquery side's rows; key NDVs are capped alike
-                    tgt["grows"] = max(1, min(tgt["grows"], nrb))
-                    tgt["ndv"] = {k: max(1, min(v, tgt["grows"])) for k, v in tgt["ndv"].items()}
-                else:
-                    tgt["grows"] = _global_rows(tgt["batch"], ctx)
-                self.order_log.append(f"{sp.kind} pre-filter on {tgt['name']} -> {tgt['batch'].num_rows}")
-            else:
-                deferred.append((sp, rb))
-        while len(rels) > 1:
-            if ctx.spmd:
-                self._prefetch_ndv(rels, conds, ctx)
-            best = None
-            for i in range(len(rels)):
-                for k in range(i + 1, len(rels)):
-                    keys = _edges(conds, rels[i]["cids"], rels[k]["cids"])
-                    if not keys:
-                        continue
-                    est = self._estimate(rels[i], rels[k], keys, ctx)
-                    if best is None or est < best[0]:
-                        best = (est, i, k, keys)
-            if best is None:
-                # no join edge: cross join the two smallest inputs
-                order = sorted(range(len(rels)), key=lambda x: rels[x]["grows"])
-                i, k = sorted(order[:2])
-                keys = []
-            else:
-                _, i, k, keys = best
-            a, b = rels[i], rels[k]
-            cids = a["cids"] | b["cids"]
-            used = [c for c in conds if (col_refs(c) <= cids) and (not keys or c not in [kk[2] for kk in keys])]
-            resid = [c for c in used]
-            conds = [c for c in conds if c not in resid and (not keys or c not in [kk[2] for kk in keys])]
-            on = [(kk[0], kk[1]) for kk in keys]
-            la, lb_ = a["batch"], b["batch"]
-            out_dist = None
-            if ctx.spmd:
-                from ..parallel.exchange import prepare_join
-                fake = L.Join(None, None, "inner", on)  # type: ignore[arg-type]
-                la, lb_ = prepare_join(la, lb_, fake, ctx, rows=(a["grows"], b["grows"]))
-                out_dist = la.out_dist
-            over = ctx.budget is not None and \
-                JOIN_MEM_FACTOR * (_batch_bytes(la) + _batch_bytes(lb_)) > ctx.budget
-            # rank-local after prepare_join in SPMD too: index pairs over the
-            # (possibly exchanged) inputs, payload gathered once at the end
-            if on and not over:
-                out = self._late_join(la, lb_, on, and_all(resid), ctx)
-            else:
-                if isinstance(la, LateBatch):
-                    la = la.materialize()
-                if isinstance(lb_, LateBatch):
-                    lb_ = lb_.materialize()
-                if on:
-                    out = hash_join(la, lb_, "inner", on, and_all(resid), ctx)
-                else:
-                    out = _nested_loop(la, lb_, "inner", and_all(resid), ctx)
-            out.dist = out_dist
-            if self.required is not None and isinstance(out, LateBatch) and PRUNE_PARTS:
-                out = self._prune(out, conds, deferred)
-            self.order_log.append(f"{a['name']} ⋈ {b['name']} -> {out.num_rows}")
-            # key NDVs carry over (capped by the output size) instead of re-sketching intermediates.
-            # SPMD ranks take the estimate as the output's global size (every rank
-            # derives the same value with no collective; the estimate is from
-            # global counts and merged sketches) instead of counting it
-            if ctx.spmd:
-                cap = max(1, int(min(best[0], 2**62))) if best is not None else max(1, a["grows"] * b["grows"])
-            else:
-                cap = _global_rows(out, ctx)
-            ndv = {k: max(1, min(v, cap)) for d in (a["ndv"], b["ndv"]) for k, v in d.items()}
-            merged = {"batch": out, "cids": cids, "ndv": ndv, "name": f"({a['name']}⋈{b['name']})", "grows": cap}
-            rels = [r for x, r in enumerate(rels) if x not in (i, k)] + [merged]
-        b = rels[0]["batch"]
-        if isinstance(b, LateBatch) and not conds and not deferred and LAZY_JOIN_OUTPUT:
-            # hand the index form up: the parent gathers only the columns it
-            # reads (join keys and unused payload are never materialised)
-            return b
-        if isinstance(b, LateBatch):
-            with ctx.span("join.gather"):
-                b = b.materialize()
-        if conds:
-            b = filter_batch(b, and_all(conds), ctx)
-        for sp, rb in deferred:
-            if isinstance(rb, _IndexSemi):
-                found = _semi_index_scan(rb.node, sp, ctx)
-                out = _semi_index_then_filter(found, sp, _plain(b), ctx) if found is not None else None
-                if out is not None:
-                    b = out
-                    continue
-                rb = rb.node.execute(ctx)
-            b = self._semi(b, rb, sp, ctx)
-        return b
-
-    def _prune(self, out: "LateBatch", conds, deferred) -> "LateBatch":
-        """Drop index parts none of whose columns is read any more (by the
-        parent, a remaining join condition or a deferred semi join): later
-        steps then compose fewer row-index vectors."""
-        need = set(self.required)
-        for c in conds:
-            need |= col_refs(c)
-        for sp, _ in deferred:
-            for x, _y in sp.on:
-                need |= col_refs(x)
-            if sp.residual is not None:
-                need |= col_refs(sp.residual)
-        keep = [(bb, idx) for bb, idx in out.parts if any(c in need for c in bb.columns)] or out.parts[:1]
-        if len(keep) == len(out.parts):
-            return out
-        pruned = LateBatch(keep, out.num_rows, out.dist)
-        pruned._cache = {k: v for k, v in out._cache.items() if k in pruned.owner}
-        return pruned
-
-    def _late_join(self, la: Batch, lb: Batch, on, residual, ctx) -> "LateBatch":
-        """Inner join producing index pairs over the inputs' rows (no payload gather)."""
-        A = la if isinstance(la, LateBatch) else LateBatch([(la, None)], la.num_rows)
-        B = lb if isinstance(lb, LateBatch) else LateBatch([(lb, None)], lb.num_rows)
-        ev = ctx.evaluator
-        pairs = _two_key_sorted_pairs(A, B, on, ctx) \
-            if TWO_KEY_SORTED and len(on) == 2 and ctx.device.type == "cuda" else None
-        if pairs is not None:
-            lidx, ridx = pairs
-        else:
-            with ctx.span("join.keys"):
-                lk, rk, lvalid, rvalid = key_tensors([ev.column(x, A) for x, _ in on],
-                                                     [ev.column(y, B) for _, y in on])
-            lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx)
-        if residual is not None:
-            with ctx.span("join.residual"):
-                P = LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
-                keep = mask_to_indices(predicate_mask(residual, P, ctx))
-                lidx = gather_tensor(lidx, keep)
-                ridx = gather_tensor(ridx, keep)
-        with ctx.span("join.compose"):
-            return LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
-
-    @staticmethod
-    def _ndv_needs(rels, conds, only=None) -> list:
-        """(relation, key expression) of every join key the next ordering step
-        asks an NDV for and that is not known yet."""
-        need = []
-        for i in range(len(rels)):
-            for k in range(i + 1, len(rels)):
-                keys = _edges(conds, rels[i]["cids"], rels[k]["cids"])
-                if keys:
-                    for rel, e in ((rels[i], keys[0][0]), (rels[k], keys[0][1])):
-                        if only is not None and rel is not only:
-                            continue
-                        if e.sql() not in rel["ndv"] and all(e.sql() != x.sql() or rel is not r for r, x in need):
-                            need.append((rel, e))
-        return need
-
-    def _spmd_stats(self, batches, need, ctx, rels=()) -> List[int]:
-        """SPMD: global row counts of ``batches`` (a replicated batch counts
-        once) and the global NDV of every ``need`` key, in ONE collective: an
-        all-gather of [counts | HLL registers] (counts summed, registers
-        max-merged locally) on the GPU, one all-reduce of [counts | exact local
-        distinct counts] on the CPU. Sets ``rel["ndv"]``; returns the counts.
-
-        Base-table key columns are sketched once: their global NDV (and the
-        table's global rows) is kept per engine, keyed by (table, column,
-        catalog version, cache generation); a later query reads it, and a
-        filtered scan of that column derives its NDV from it (Cardenas) with
-        its global row count — no sketch pass. Which keys are sketched follows
-        from the plan and that cache alone, so every rank sketches the same
-        ones (the all-gather's shape matches on every rank)."""
-        comm = ctx.comm
-        local = [0 if _replicated(b) else b.num_rows for b in batches]
-        eng = ctx.engine
-        cache = getattr(eng, "_gndv", None) if eng is not None else None
-        ver = (eng.catalog.version, eng.cache.generation) if cache is not None else None
-        plan = []      # per need: (kind, cache key, rel index)
-        for rel, e in need:
-            ri = next((i for i, r in enumerate(rels) if r is rel), None)
-            info = rel.get("scan")
-            kind, key = "sketch", None
-            if cache is not None and info is not None and isinstance(e, ColRef) and e.cid in info[1]:
-                key = (ver, info[0], info[1][e.cid])
-                if key in cache:
-                    kind = "derived" if info[2] else "cached"
-                elif not info[2]:
-                    kind = "sketch_base"
-            plan.append((kind, key, ri))
-        sk = [j for j, (kind, _, _) in enumerate(plan) if kind.startswith("sketch")]
-        if ctx.device.type != "cuda":
-            nd = []
-            for j in sk:
-                rel, e = need[j]
-                b = rel["batch"]
-                mine = b.num_rows and (not _replicated(b) or comm.rank == 0)   # a replicated input counts once
-                nd.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
-            g = comm.allreduce_ints(local + nd)
-            est = dict(zip(sk, g[len(local):]))
-            g = g[:len(local)]
-        else:
-            regs = []
-            for j in sk:
-                rel, e = need[j]
-                b = rel["batch"]
-                if b.num_rows:
-                    k, _ = group_key_tensor(ctx.evaluator.column(e, b))
-                    regs.append(H.hll_sketch(k))
-                else:
-                    regs.append(torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
-            parts = [device_ints(local, ctx.device)]
-            if regs:
-                parts.append(torch.stack(regs).view(torch.int64).reshape(-1))
-            allg = comm.allgather_tensor(torch.cat(parts)).view(comm.world_size, -1)
-            nb = len(local)
-            # counts and NDV estimates reach the host in one readback
-            vals = [allg[:, :nb].sum(0)]
-            if regs:
-                merged = allg[:, nb:].contiguous().view(torch.uint8).view(comm.world_size, len(regs), H.HLL_M) \
-                    .amax(0)
-                vals.append(H.hll_terms(merged).view(torch.int64).reshape(-1))
-            host = to_host_ints(torch.cat(vals))
-            g = host[:nb]
-            est = {}
-            for t, j in enumerate(sk):
-                z, zeros = np.array(host[nb + 2 * t:nb + 2 * t + 2], dtype=np.int64).view(np.float64)
-                est[j] = int(round(H.hll_from_terms(float(z), int(zeros))))
-        counts = [b.num_rows if _replicated(b) else n for b, n in zip(batches, g)]
-        for j, ((rel, e), (kind, key, ri)) in enumerate(zip(need, plan)):
-            if kind == "cached":
-                v = cache[key][0]
-            elif kind == "derived":
-                D, N = cache[key]
-                n = counts[ri] if ri is not None else rel["batch"].num_rows
-                sel = min(n / max(N, 1), 1.0)
-                v = max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / max(D, 1)))))))
-            else:
-                v = est[j]
-                if kind == "sketch_base" and ri is not None:
-                    if len(cache) > 4096:
-                        cache.clear()
-                    cache[key] = (max(v, 1), counts[ri])
-            rel["ndv"][e.sql()] = max(v, 1)
-        return counts
-
-    def _prefetch_ndv(self, rels, conds, ctx) -> None:
-        """SPMD: sketch every join key the next ordering step will ask for and
-        merge all rank sketches with ONE all-reduce (instead of one per key)."""
-        need = self._ndv_needs(rels, conds)
-        if not need:
-            return
-        if ctx.device.type != "cuda":
-            # CPU ranks: exact local distinct counts, summed (an upper bound) in one all-reduce
-            local = []
-            for rel, e in need:
-                b = rel["batch"]
-                mine = b.num_rows and (not _replicated(b) or ctx.comm.rank == 0)   # a replicated input counts once
-                local.append(H.ndv(group_key_tensor(ctx.evaluator.column(e, b))[0]) if mine else 0)
-            for (rel, e), g in zip(need, ctx.comm.allreduce_ints(local)):
-                rel["ndv"][e.sql()] = max(g, 1)
-            return
-        regs = []
-        for rel, e in need:
-            b = rel["batch"]
-            if b.num_rows:
-                k, _ = group_key_tensor(ctx.evaluator.column(e, b))
-                regs.append(H.hll_sketch(k))
-            else:
-                regs.append(torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
-        merged = ctx.comm.allreduce_max_tensor(torch.stack(regs))
-        for (rel, e), r in zip(need, merged):
-            rel["ndv"][e.sql()] = max(int(round(H.hll_estimate(r))), 1)
-
-    def _estimate(self, a, b, keys, ctx) -> float:
-        na, nb = a["grows"], b["grows"]
-        ka, kb = keys[0][0], keys[0][1]
-        da = self._ndv(a, ka, ctx)
-        db = self._ndv(b, kb, ctx)
-        return na * nb / max(da, db, 1)
-
-    def _ndv(self, rel, e: Expr, ctx) -> int:
-        """NDV of a join key: HyperLogLog sketch on the GPU (one streaming read;
-        rank sketches merge by max, so the distributed estimate is global),
-        exact distinct count on the CPU."""
-        key = e.sql()
-        if key not in rel["ndv"]:
-            b = rel["batch"]
-            with ctx.span("multijoin.ndv"):
-                cached = None
-                if not ctx.spmd and b.num_rows:
-                    c = ctx.evaluator.column(e, b)
-                    # resident table columns: the sketch of the same tensor is reused across queries
-                    cached = getattr(c.data, "_igloo_ndv", None) if c.valid is None else None
-                base = getattr(c.data, "_igloo_base", None) if cached is None and not ctx.spmd and \
-                    b.num_rows and c.valid is None else None
-                if cached is not None:
-                    g = cached
-                elif base is not None:
-                    g = _derived_ndv(base, b.num_rows)
-                elif ctx.device.type == "cuda":
-                    if b.num_rows:
-                        c = ctx.evaluator.column(e, b)
-                        k, _ = group_key_tensor(c)
-                        regs = H.hll_sketch(k)
-                    else:
-                        regs = torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device)
-                    if ctx.spmd:
-                        # every rank takes part, even with an empty slice (collective order must match)
-                        regs = ctx.comm.allreduce_max_tensor(regs)
-                    if b.num_rows and c.valid is None and getattr(c.data, "_igloo_resident", False):
-                        with unlogged():     # remembered on the resident column below
-                            g = int(round(H.hll_estimate(regs)))
-                    else:
-                        g = int(round(H.hll_estimate(regs)))
-                else:
-                    g = 0
-                    if b.num_rows:
-                        c = ctx.evaluator.column(e, b)
-                        k, _ = group_key_tensor(c)
-                        g = H.ndv(k)
-                    if ctx.spmd:
-                        g = ctx.comm.allreduce_int(g)  # upper bound of the global NDV
-                if cached is None and not ctx.spmd and b.num_rows and c.valid is None and not c.is_dict:
-                    try:
-                        c.data._igloo_ndv = g
-                    except (AttributeError, RuntimeError):
-                        pass
-            rel["ndv"][key] = max(g, 1)
-        return rel["ndv"][key]
-
-
-NDV_DERIVED = os.environ.get("IGLOO_NDV_DERIVED", "1") == "1"
-
-
-def _derived_ndv(base, n: int) -> int:
-    """NDV of an n-row filtered subset of a source column with N rows and D
-    distinct values, by Cardenas' formula D * (1 - (1 - n/N)^(N/D)) (rows
-    selected independently of the key) — no pass over the subset. D comes
-    from one sketch of the source column, remembered on its tensor."""
-    col, N = base
-    D = getattr(col.data, "_igloo_ndv", None)
-    if D is None:
-        k, _ = group_key_tensor(col)
-        with unlogged():
-            D = max(int(round(H.hll_estimate(H.hll_sketch(k)))) if k.is_cuda else H.ndv(k), 1)
-        try:
-            col.data._igloo_ndv = D
-        except (AttributeError, RuntimeError):
-            pass
-    sel = min(n / max(N, 1), 1.0)
-    return max(1, min(n, int(round(D * (1.0 - (1.0 - sel) ** (N / D))))))
-
-
-def _scan_info(node):
-    """(table, {cid: column name}, filtered) of a plain table-scan input of a
-    multi-way join, else None (SPMD NDV cache, MultiJoinExec._spmd_stats)."""
-    if not isinstance(node, ScanExec):
-        return None
-    s = node.logical
-    names = {c.cid: c.name for c in getattr(s, "table_cols", s.schema)}
-    names.update({c.cid: c.name for c in s.schema})
-    return (s.table, names, bool(s.filters))
-
-
-def _replicated(b) -> bool:
-    return getattr(b, "dist", None) == ("replicated",)
-
-
-def _global_rows(b: Batch, ctx) -> int:
-    if ctx.spmd and not _replicated(b):
-        return ctx.comm.allreduce_int(b.num_rows)
-    return b.num_rows
-
-
-def _global_rows_many(bs: Sequence[Batch], ctx) -> List[int]:
-    """Global row counts (a replicated batch's rows count once) in at most
-    one all-reduce."""
-    if ctx.spmd and any(not _replicated(b) for b in bs):
-        g = ctx.comm.allreduce_ints([0 if _replicated(b) else b.num_rows for b in bs])
-        return [b.num_rows if _replicated(b) else n for b, n in zip(bs, g)]
-    return [b.num_rows for b in bs]
-
-
-def _edges(conds, ca: set, cb: set):
-    """Equi-join edges between two inputs: list of (expr_a, expr_b, cond)."""
-    out = []
-    for c in conds:
-        if isinstance(c, BinOp) and c.op == "=":
-            l, r = col_refs(c.left), col_refs(c.right)
-            if l and r and l <= ca and r <= cb:
-                out.append((c.left, c.right, c))
-            elif l and r and l <= cb and r <= ca:
-                out.append((c.right, c.left, c))
-    return out
-
-
-# ======================================================================= aggregate
-def having_constant(op: str, lit: Lit, src: T.DataType, func: str, float_state: bool):
-    """The HAVING literal in the units of the aggregate's raw state (fused
-    sorted GROUP BY + HAVING): a float for f64 states; else an int, where a
-    fractional threshold is rounded so that the integer comparison keeps its
-    meaning (x > 2.5 <=> x > 2, x >= 2.5 <=> x >= 3, x < 2.5 <=> x < 3,
-    x <= 2.5 <=> x <= 2). None for = / <> against a fractional value."""
-    lv = Fraction(lit.value, 10 ** lit.dtype.scale) if lit.dtype.is_decimal else Fraction(lit.value)
-    if float_state:
-        return float(lv)
-    thr = lv * 10 ** (src.scale if (src.is_decimal and func != "count") else 0)
-    if thr.denominator != 1:
-        if op in ("=", "<>"):
-            return None
-        thr = math.floor(thr) if op in (">", "<=") else math.ceil(thr)
-    return int(thr)
-
-
-class HashAggExec(ExecNode):
-    def __init__(self, logical: L.Aggregate, child: ExecNode):
-        self.logical = logical
-        self.children = [child]
-        self.runtime_filters: list = []  # (group expr, key column) set by a parent join
-        self.having = None               # predicate of a parent FilterExec (HAVING)
-
-    def _sorted_having(self, ctx) -> Optional[Batch]:
-        """GROUP BY a sorted key column HAVING <aggregate> <cmp> <constant> as
-        one fused pass (ops/agg.py sorted_having): only the passing groups are
-        materialised (TPC-H Q18: 6.5K of 150M l_orderkey groups at SF100). The
-        parent FilterExec still applies the predicate to them (NULL groups).
-        None when the shape does not apply (the general path runs)."""
-        lg, pred = self.logical, self.having
-        if (pred is None or ctx.device.type != "cuda" or ctx.budget is not None or self.runtime_filters
-                or not SORTED_HAVING or len(lg.groups) != 1 or not 1 <= len(lg.aggs) <= 4
-                or not isinstance(lg.groups[0][1], ColRef) or not isinstance(pred, BinOp)):
-            return None
-        if any(a.func not in ("sum", "count", "min", "max") or a.distinct or a.filter is not None for _, a in lg.aggs):
-            return None
-        flip = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
-        if pred.op not in flip:
-            return None
-        agg_cids = {ci.cid: i for i, (ci, _) in enumerate(lg.aggs)}
-        if isinstance(pred.left, ColRef) and pred.left.cid in agg_cids and isinstance(pred.right, Lit):
-            ref, lit, op = pred.left, pred.right, pred.op
-        elif isinstance(pred.right, ColRef) and pred.right.cid in agg_cids and isinstance(pred.left, Lit):
-            ref, lit, op = pred.right, pred.left, flip[pred.op]
-        else:
-            return None
-        if lit.value is None or not (lit.dtype.is_integer or lit.dtype.is_decimal or lit.dtype.is_float):
-            return None
-        if any(a.func in ("min", "max") and a.arg is not None and a.arg.dtype.is_string for _, a in lg.aggs):
-            return None
-        # an unfiltered scan whose group key column is sorted (decided before
-        # running anything, so every other aggregate path stays available)
-        child = self.children[0]
-        if not isinstance(child, ScanExec) or child.predicate is not None:
-            return None
-        gci, gexpr = lg.groups[0]
-        if ctx.spmd and not self._group_local(child, gexpr, ctx):
-            return None
-        raw = child.peek_raw(ctx)
-        if ctx.spmd:
-            from ..parallel.exchange import REPLICATED, placed_on
-            if raw.dist != REPLICATED and not placed_on(raw.dist, gexpr.cid):
-                return None      # (alike on every rank: placements follow from plan and catalog)
-        kc = raw.columns.get(gexpr.cid) if hasattr(raw, "columns") else None
-        if kc is None or kc.valid is not None or kc.data.dtype not in (torch.int32, torch.int64) \
-                or kc.data.dim() != 1 or kc.dtype.is_string or raw.num_rows < SORTED_HAVING_MIN_ROWS \
-                or not H.is_sorted(kc.data):
-            return None
-        b = child.finish(raw, ctx)
-        n = b.num_rows
-        kcol = ctx.evaluator.column(gexpr, b)
-        if kcol.data.data_ptr() != kc.data.data_ptr() or n != raw.num_rows:
-            return self._finish_general(b, ctx)
-        specs, finals, vidx = [], [], {}
-        for i, (ci, a) in enumerate(lg.aggs):
-            _plan_agg(ci, a, b, None, 1, n, ctx, specs, finals)
-            vidx[i] = len(specs) - 1          # the aggregate's value spec (sum/min/max/count)
-        if len(specs) > 4:
-            return self._finish_general(b, ctx)
-        hidx = vidx[agg_cids[ref.cid]]
-        hop_spec = specs[hidx][0]
-        a = lg.aggs[agg_cids[ref.cid]][1]
-        src = a.arg.dtype if a.arg is not None else T.INT64
-        const = having_constant(op, lit, src, a.func, hop_spec in ("sum_f64", "min_f64", "max_f64"))
-        if const is None:
-            return self._finish_general(b, ctx)
-        with ctx.span("agg.sorted_having"):
-            got = A.sorted_having(kcol.data, [sp[:3] for sp in specs], hidx, op, const)
-        if got is None:
-            return self._finish_general(b, ctx)
-        rep, results = got
-        out = {gci.cid: take(kcol, rep)}
-        for fin in finals:
-            ci, col = fin(results)
-            out[ci.cid] = col
-        return Batch(out, rep.numel(), self._local_dist(raw.dist, gci) if ctx.spmd else None)
-
-    @staticmethod
-    def _group_local(scan: "ScanExec", gexpr, ctx) -> bool:
-        """SPMD: every group of GROUP BY ``gexpr`` over ``scan`` lives on one
-        rank (the scan's table is placed by that column -- hash-partitioned,
-        or a replicated table this query splits by ranges of it -- or is
-        replicated whole), so an aggregate over the rank's rows is final.
-        Decided from the plan and catalog, alike on every rank."""
-        src = scan.logical.source
-        names = {c.cid: c.name for c in getattr(scan.logical, "table_cols", scan.logical.schema)}
-        names.update({c.cid: c.name for c in scan.logical.schema})
-        col = names.get(gexpr.cid) if isinstance(gexpr, ColRef) else None
-        if getattr(src, "replicated", False):
-            sk = ctx.slices.get(id(src))
-            return sk is None or (col is not None and col == sk)
-        pk = getattr(src, "partitioned_by", None)
-        return pk is not None and col == pk
-
-    @staticmethod
-    def _local_dist(d, gci):
-        from ..parallel.exchange import REPLICATED, keyed
-        if d == REPLICATED:
-            return REPLICATED
-        return (d[0], gci.cid) if keyed(d) else None
-
-    def _finish_general(self, b, ctx) -> Batch:
-        lg = self.logical
-        out = aggregate(lg.groups, lg.aggs, b, ctx)
-        if ctx.spmd:
-            out.dist = self._local_dist(b.dist, lg.groups[0][0])
-        return out
-
-    def describe(self):
-        a = self.logical
-        return (f"gby=[{', '.join(e.sql() for _, e in a.groups)}], "
-                f"aggr=[{', '.join(x.sql() for _, x in a.aggs)}]")
-
-    def _eager_count(self, ctx) -> Optional[Batch]:
-        """GROUP BY <left join key>, COUNT(<right column>)... over a LEFT JOIN on
-        that key (TPC-H Q13: customer LEFT JOIN orders, count per customer):
-        count the right side per key first, then look the counts up per left row
-        and sum them per group — a group-by over the right input plus a probe of
-        the left keys, instead of materialising and re-grouping the join
-        (150M-row join output at SF100). Exact: a left row with k partners
-        contributes k to COUNT(x) exactly when x is non-NULL on each partner."""
-        lg, child = self.logical, self.children[0]
-        if not isinstance(child, HashJoinExec) or len(lg.groups) != 1 or not lg.aggs:
-            return None
-        j = child.logical
-        if j.kind != "left" or j.residual is not None or len(j.on) != 1:
-            return None
-        lkey, rkey = j.on[0]
-        gci, gexpr = lg.groups[0]
-        if not (isinstance(gexpr, ColRef) and isinstance(lkey, ColRef) and gexpr.cid == lkey.cid):
-            return None
-        right_cids = {c.cid for c in j.right.schema}
-        for _, a in lg.aggs:
-            if not (a.func == "count" and not a.distinct and a.filter is None and isinstance(a.arg, ColRef)
-                    and a.arg.cid in right_cids):
-                return None
-        ev = ctx.evaluator
-        if ctx.budget is not None and not ctx.spmd:
-            from .morsel import big_streamable
-            if big_streamable(child.children[1], ctx):
-                return self._eager_count_streamed(lkey, rkey, ctx)
-        if ctx.device.type != "cuda" and not ctx.spmd:
-            return None     # (the CPU engine stays the plain join + aggregate: the GPU tests' reference)
-        lb = child.children[0].execute(ctx)
-        masked = self._eager_count_masked(lg, lb, lkey, rkey, ctx)
-        if masked is not None:
-            return masked
-        rb = child.children[1].execute(ctx)
-        with ctx.span("agg.eager_count"):
-            lk, rk, lvalid, rvalid = key_tensors([ev.column(lkey, lb)], [ev.column(rkey, rb)])
-            if rvalid is not None:  # NULL keys never match
-                keep = mask_to_indices(rvalid)
-                rk = gather_tensor(rk, keep)
-                rb = _take_batch(rb, keep)
-            cnt_cols = {}
-            if ctx.spmd:
-                out = self._spmd_counts(lg, lb, lkey, lk, lvalid, rk,
-                                        [ev.column(a.arg, rb).valid for _, a in lg.aggs], ctx)
-                return out if out is not None else self._spmd_join_aggregate(lb, rb, ctx)
-            rng = H.key_range(rk) if rk.numel() else None
-            span = rng[1] - rng[0] + 1 if rng else 0
-            if rng and span <= EAGER_COUNT_DIRECT_SPAN:
-                # dense key domain: one histogram pass over the right keys, then a
-                # direct lookup per left key (no hash table, no group ids)
-                kmin = rng[0]
-                li = lk.to(torch.int64) - kmin
-                inr = (li >= 0) & (li < span)
-                if lvalid is not None:
-                    inr &= lvalid
-                li = torch.where(inr, li, torch.zeros_like(li))
-                for k, (_, a) in enumerate(lg.aggs):
-                    hist = A.key_histogram(rk, kmin, span, ev.column(a.arg, rb).valid) if rk.numel() else \
-                        torch.zeros(span, dtype=torch.int64, device=ctx.device)
-                    cnt_cols[-(k + 1)] = torch.where(inr, hist.index_select(0, li), torch.zeros_like(li))
-            elif rk.numel():
-                gid, ng, rep, srt = H.group_ids_ex(rk)
-                specs = [("count", None, ev.column(a.arg, rb).valid) for _, a in lg.aggs]
-                counts = A.grouped_aggregate(gid, ng, specs, rk.numel(), ctx.device, sorted_gids=srt)
-                first = H.JoinTable(gather_tensor(rk, rep)).probe_first(lk, lvalid)
-                hit = first >= 0
-                safe = torch.where(hit, first, torch.zeros_like(first)).long()
-                for k, c in enumerate(counts):
-                    cnt_cols[-(k + 1)] = torch.where(hit, c.index_select(0, safe), torch.zeros_like(safe))
-            else:
-                for k in range(len(lg.aggs)):
-                    cnt_cols[-(k + 1)] = torch.zeros(lb.num_rows, dtype=torch.int64, device=ctx.device)
-        return self._count_sums(lg, lb, [cnt_cols[-(k + 1)] for k in range(len(lg.aggs))], ctx)
-
-    def _count_sums(self, lg, lb: Batch, counts, ctx, dist=None) -> Batch:
-        """GROUP BY <left key> SUM(per-row partner count) -- the eager COUNT's
-        final step over the left rows and their looked-up counts."""
-        cols = dict(lb.columns)
-        aggs = []
-        for k, (ci, _) in enumerate(lg.aggs):
-            tmp = -(10**9) - k  # temporary column ids (binder ids are positive)
-            cols[tmp] = Column(T.INT64, counts[k].to(torch.int64).contiguous())
-            aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
-        if ctx.spmd:
-            from ..parallel.exchange import distributed_aggregate
-            return distributed_aggregate(L.Aggregate(None, lg.groups, aggs),
-                                         Batch(cols, lb.num_rows, dist if dist is not None else lb.dist), ctx)
-        return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
-
-    def _spmd_counts(self, lg, lb: Batch, lkey, lk, lvalid, rk, rmasks, ctx) -> Optional[Batch]:
-        """SPMD eager COUNT: each rank histograms its right rows' keys over the
-        GLOBAL key range (one tiny all-gather of the ranges), then
-
-        * replicated left side (TPC-H Q13: customer against orders placed by
-          order key): ONE reduce-scatter sums the histograms and leaves rank r
-          the counts of key chunk r only (1/world of the bytes of an
-          all-reduce, which would hand every rank all 15M counts at SF100);
-          each rank keeps the left rows of its chunk, so the result is
-          partitioned by key range and the GROUP BY that follows is rank-local;
-        * partitioned left side: an all-reduce (every rank's left keys may
-          fall anywhere in the range).
-
-        Counts travel as int32 (half the bytes) when the global right row
-        count fits. None when the global key span is too large for dense
-        histograms (decided alike on every rank)."""
-        from ..parallel.exchange import REPLICATED
-        from ..parallel.slicing import range_chunk, range_tag
-        comm = ctx.comm
-        W = comm.world_size
-        dev = ctx.device
-        masks = list(rmasks)
-        rng = H.key_range(rk, masks[0] if len(set(map(id, masks))) == 1 else None) if rk.numel() else None
-        g = comm.allgather_ints([rng[0], rng[1], rk.numel()] if rng else [2**62, -2**62, rk.numel()])
-        g0, g1 = min(r[0] for r in g), max(r[1] for r in g)
-        if g0 > g1:
-            return self._count_sums(lg, lb, [torch.zeros(lb.num_rows, dtype=torch.int64, device=dev)] * len(masks), ctx)
-        span = g1 - g0 + 1
-        if span > EAGER_COUNT_DIRECT_SPAN:
-            return None
-        wide = sum(r[2] for r in g) >= 2**31
-        rep = lb.dist == REPLICATED
-        chunk = range_chunk(g0, g1, W) if rep else span
-        width = W * chunk if rep else span
-        hdt = torch.int64 if wide else torch.int32
-        hists = torch.zeros((len(masks), width), dtype=hdt, device=dev)
-        for k, m in enumerate(masks):
-            if rk.numel():
-                hists[k, :span] = A.key_histogram(rk, g0, span, m).to(hdt)
-        lkey64 = lk.to(torch.int64)
-        if rep:
-            # [world, aggs, chunk]: rank r's share is one contiguous block
-            mine = comm.reduce_scatter_tensor(hists.view(len(masks), W, chunk).transpose(0, 1).contiguous(), "sum")
-            mine = mine.view(len(masks), chunk)
-            # the left rows of this rank's key chunk (keys outside the right
-            # side's range clamp to the first / last chunk; NULL keys: rank 0)
-            owner = torch.clamp(torch.div(lkey64 - g0, chunk, rounding_mode="floor"), 0, W - 1)
-            own = owner == comm.rank
-            if lvalid is not None:
-                own = torch.where(lvalid, own, torch.full_like(own, comm.rank == 0))
-            if W > 1:
-                sel = mask_to_indices(own)
-                lb = _take_batch(lb, sel)
-                lkey64 = gather_tensor(lkey64, sel)
-                lvalid = gather_tensor(lvalid, sel) if lvalid is not None else None
-            base, size, table = g0 + comm.rank * chunk, chunk, mine
-            dist = (range_tag(W, g0, chunk), lkey.cid) if isinstance(lkey, ColRef) else None
-        else:
-            table = comm.allreduce_tensor(hists, "sum")
-            base, size, dist = g0, span, None
-        li = lkey64 - base
-        inr = (li >= 0) & (li < size)
-        if lvalid is not None:
-            inr &= lvalid
-        li = torch.where(inr, li, torch.zeros_like(li))
-        counts = [torch.where(inr, table[k].index_select(0, li).to(torch.int64), torch.zeros_like(li))
-                  for k in range(len(masks))]
-        return self._count_sums(lg, lb, counts, ctx, dist)
-
-    def _eager_count_masked(self, lg, lb, lkey, rkey, ctx) -> Optional[Batch]:
-        """``_eager_count`` over a filtered right-side scan without
-        compacting it: the per-key histogram reads the resident key column
-        with the filter mask as its validity (Q13: 148M of 150M orders pass
-        o_comment NOT LIKE, so the compaction and the o_custkey gather were
-        pure copies). Dense key domains, single rank, no budget; None when
-        the shape differs."""
-        rnode = self.children[0].children[1]
-        if ctx.budget is not None or not isinstance(rnode, ScanExec) or rnode.predicate is None \
-                or not EAGER_COUNT_MASKED or any(getattr(a.arg, "nullable", True) for _, a in lg.aggs) \
-                or not isinstance(rkey, ColRef):
-            return None
-        ev = ctx.evaluator
-        raw = rnode.peek_raw(ctx)
-        rcol = raw.columns.get(rkey.cid)
-        lcol = ev.column(lkey, lb)
-        if rcol is None or rcol.dtype.is_string or lcol.dtype.is_string or rcol.is_dict \
-                or rcol.data.dtype not in (torch.int32, torch.int64) or lcol.data.dtype not in (torch.int32, torch.int64):
-            return None
-        if ctx.spmd:
-            # (the global key span decides, alike on every rank)
-            with ctx.span("agg.eager_count"):
-                m = predicate_mask(rnode.predicate, raw, ctx)
-                if rcol.valid is not None:
-                    m = m & rcol.valid
-                return self._spmd_counts(lg, lb, lkey, lcol.data, lcol.valid, rcol.data, [m] * len(lg.aggs), ctx)
-        rng = H.key_range(rcol.data, rcol.valid)
-        span = rng[1] - rng[0] + 1 if rng else 0
-        if not rng or span > EAGER_COUNT_DIRECT_SPAN:
-            return None
-        with ctx.span("agg.eager_count"):
-            m = predicate_mask(rnode.predicate, raw, ctx)
-            if rcol.valid is not None:
-                m = m & rcol.valid
-            kmin = rng[0]
-            li = lcol.data.to(torch.int64) - kmin
-            inr = (li >= 0) & (li < span)
-            if lcol.valid is not None:
-                inr &= lcol.valid
-            li = torch.where(inr, li, torch.zeros_like(li))
-            hist = A.key_histogram(rcol.data, kmin, span, m)
-            cnt = torch.where(inr, hist.index_select(0, li), torch.zeros_like(li))
-        cols = dict(lb.columns)
-        aggs = []
-        for k, (ci, _) in enumerate(lg.aggs):
-            tmp = -(10**9) - k  # temporary column ids (binder ids are positive)
-            cols[tmp] = Column(T.INT64, cnt.contiguous())
-            aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
-        return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
-
-    def _eager_count_streamed(self, lkey, rkey, ctx) -> Batch:
-        """``_eager_count`` with a right side over the device budget: the
-        per-key counts come from an aggregate of the right side (GROUP BY the
-        join key, one COUNT per aggregate), which streams in morsels
-        (exec/morsel.py), instead of the materialised right side."""
-        from ..parallel.exchange import _TmpIds
-        lg, child = self.logical, self.children[0]
-        j = child.logical
-        ids = _TmpIds()
-        kci = L.ColInfo(ids(), "__k", rkey.dtype, rkey.nullable)
-        cnt = [(L.ColInfo(ids(), "__c", T.INT64, False), AggCall("count", a.arg, False, T.INT64)) for _, a in lg.aggs]
-        ab = HashAggExec(L.Aggregate(j.right, [(kci, rkey)], cnt), child.children[1]).execute(ctx)
-        lb = child.children[0].execute(ctx)
-        ev = ctx.evaluator
-        with ctx.span("agg.eager_count"):
-            lk, rk, lvalid, rvalid = key_tensors([ev.column(lkey, lb)], [ab.columns[kci.cid]])
-            cols = dict(lb.columns)
-            aggs = []
-            if ab.num_rows and lb.num_rows:
-                first = H.JoinTable(rk, rvalid).probe_first(lk, lvalid)
-                hit = first >= 0
-                safe = torch.where(hit, first, torch.zeros_like(first)).long()
-            for k, (ci, _) in enumerate(lg.aggs):
-                if ab.num_rows and lb.num_rows:
-                    c = ab.columns[cnt[k][0].cid].data
-                    v = torch.where(hit, c.index_select(0, safe), torch.zeros_like(safe))
-                else:
-                    v = torch.zeros(lb.num_rows, dtype=torch.int64, device=ctx.device)
-                tmp = -(10**9) - k
-                cols[tmp] = Column(T.INT64, v.contiguous())
-                aggs.append((ci, AggCall("sum", ColRef(tmp, "__cnt", T.INT64, False), False, T.INT64)))
-        return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
-
-    def _spmd_join_aggregate(self, lb: Batch, rb: Batch, ctx) -> Batch:
-        """SPMD fallback after the inputs were computed: the plain exchange +
-        join + distributed aggregation."""
-        from ..parallel.exchange import distributed_aggregate, prepare_join
-        j = self.children[0].logical
-        lb, rb = prepare_join(lb, rb, j, ctx)
-        out = hash_join(lb, rb, j.kind, j.on, j.residual, ctx, null_aware=j.null_aware)
-        out.dist = lb.out_dist
-        return distributed_aggregate(self.logical, out, ctx)
-
-    def _run(self, ctx):
-        lg = self.logical
-        child = self.children[0]
-        if self.having is not None and ctx.budget is None and ctx.device.type == "cuda" \
-                and not self.runtime_filters:
-            out = self._sorted_having(ctx)
-            if out is not None:
-                return out
-        if ctx.budget is not None:
-            from .morsel import streamed_aggregate
-            out = streamed_aggregate(self, ctx)
-            if out is not None:
-                return out
-        if (ctx.device.type == "cuda" or ctx.budget is not None or ctx.spmd) and not self.runtime_filters:
-            out = self._eager_count(ctx)
-            if out is not None:
-                return out
-        local = None
-        if isinstance(child, ScanExec) and ctx.device.type == "cuda" and not self.runtime_filters:
-            # scan -> filter -> aggregate in one fused kernel when the shape allows
-            raw = child.scan_raw(ctx)
-            pred = child.predicate
-
-            def local(groups, aggs, raw=raw, pred=pred):
-                return fused.fused_scan_aggregate(groups, aggs, raw, pred, ctx)
-            if not ctx.spmd:
-                out = local(lg.groups, lg.aggs)
-                if out is not None:
-                    return out
-            b = LazyBatch(lambda: child.finish(raw, ctx), raw.dist)
-        elif self.runtime_filters and isinstance(child, ScanExec) and child.predicate is not None \
-                and ctx.device.type == "cuda" and ctx.budget is None and INDEX_THEN_FILTER:
-            # decided before the scan filter runs over the whole table
-            raw = child.scan_raw(ctx)
-            filters, self.runtime_filters = self.runtime_filters, []
-            pre = _index_then_filter(child, raw, filters, ctx)
-            if pre is not None:
-                b, filters = pre
-            else:
-                b = child.finish(raw, ctx)
-            self.runtime_filters = filters
-        else:
-            b = child.execute(ctx)
-        if self.runtime_filters:
-            filters, self.runtime_filters = self.runtime_filters, []
-            b = apply_key_filters(b, filters, ctx)
-        if ctx.spmd:
-            from ..parallel.exchange import distributed_aggregate
-            return distributed_aggregate(lg, b, ctx, local=local)
-        return aggregate(lg.groups, lg.aggs, b, ctx)
-
-
-def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None) -> Batch:
-    """GROUP BY ``groups`` computing ``aggs`` over ``b``. ``row_parts``
-    ({output cid: part index} of a LateBatch ``b``): when the grouping runs
-    on the join result's index form (``_late_group_keys``: every other key is
-    functionally dependent on the leading integer key), each group's row in
-    those parts is added as an int64 column -- the SPMD exchange ships that
-    row instead of the part's string columns (parallel/exchange.py). The
-    columns are absent when the dependency did not hold."""
-    ev = ctx.evaluator
-    n = b.num_rows
-    dev = ctx.device
-    late = None
-    if groups and n and isinstance(b, LateBatch) and (dev.type == "cuda" or row_parts):
-        with ctx.span("agg.late_keys"):
-            late = _late_group_keys(groups, b, ctx)
-    if late is not None:
-        gid, ng, rep, taken = late
-    else:
-        with ctx.span("agg.eval_keys"):
-            gcols = [ev.column(e, b) for _, e in groups]
-        if groups:
-            if n == 0:
-                return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
-            with ctx.span("agg.group_ids"):
-                ctx.sorted_gids = False
-                gid, ng, rep, reps_src = _encode_groups(gcols, ctx)
-        else:
-            gid, ng, rep = None, 1, None
-        if groups:
-            with ctx.span("agg.take_keys"):
-                taken = take_many(reps_src, rep)
-    out: Dict[int, Column] = {}
-    if groups:
-        for (ci, _), c in zip(groups, taken):
-            out[ci.cid] = c
-    if late is not None and row_parts:
-        for cid, k in row_parts.items():
-            idx = b.parts[k][1]
-            out[cid] = Column(T.INT64, gather_tensor(idx, rep).to(torch.int64))
-    specs, finals = [], []
-    with ctx.span("agg.eval_args"):
-        for ci, a in aggs:
-            _plan_agg(ci, a, b, gid, ng, n, ctx, specs, finals)
-    with ctx.span("agg.kernel"):
-        results = A.grouped_aggregate(gid, ng, [s[:3] for s in specs], n, dev,
-                                      sorted_gids=gid is not None and getattr(ctx, "sorted_gids", False)) \
-            if specs else []
-        for fin in finals:
-            ci, col = fin(results)
-            out[ci.cid] = col
-    return Batch(out, ng)
-
-
-def _diff_bounds(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """Device int64 [min, max] of a - b (both 0 <=> a == b everywhere) from
-    the two-stage column_stats kernel: an ATen ``(a != b).sum()`` is a
-    multi-block reduction whose semaphore memset does not replay inside a HIP
-    graph (the query would never graph)."""
-    d = (a.to(torch.int64) - b.to(torch.int64)).contiguous()
-    if not d.is_cuda:
-        return torch.stack([d.min(), d.max()]) if d.numel() else torch.zeros(2, dtype=torch.int64)
-    N = launch("column_stats")
-    buf = torch.empty(N.STATS_SLOTS, dtype=torch.int64, device=d.device)
-    if d.numel() == 0:
-        return torch.zeros(2, dtype=torch.int64, device=d.device)
-    N.column_stats(ptr(d), True, 0, d.numel(), ptr(buf), stream(d))
-    return buf[:2]
-
-
-def _late_group_keys(groups, b: "LateBatch", ctx):
-    """GROUP BY over a join result still in index form, with plain string keys
-    (TPC-H Q10: c_custkey plus six customer/nation attributes over 11M joined
-    rows). Group by the widest integer key, then check per join input that its
-    row index is constant within every group: a key whose source row is fixed
-    by the group is functionally dependent on it, so it is dropped from the
-    grouping and gathered only for the ng representative rows — the strings
-    are never materialised for all joined rows. Returns (gid, ng, rep, taken)
-    or None (shape does not apply or a dependency fails: the caller groups
-    normally)."""
-    cids = [e.cid if isinstance(e, ColRef) else None for _, e in groups]
-    if any(c is None or c not in b.owner for c in cids):
-        return None
-    base = [b.parts[b.owner[c]][0].columns[c] for c in cids]
-    plain = [i for i, c in enumerate(base) if c.dtype.is_string and not c.is_dict]
-    others = [i for i in range(len(cids)) if i not in plain]
-    if not plain or not others:
-        return None
-    keys = {i: group_key_tensor(b.gather(cids[i]))[0] for i in others}
-    spans = {i: H.key_range(keys[i]) for i in others}
-    lead = _lead_key(others, spans, base)
-    gid, ng, rep, srt = H.group_ids_ex(keys[lead])
-    rr = gather_tensor(rep, gid)
-    checks, parts = [], set()
-    for i in range(len(cids)):
-        k = b.owner[cids[i]]
-        if i == lead or k in parts:
-            continue
-        idx = b.parts[k][1]
-        if idx is None:
-            return None
-        parts.add(k)
-        checks.append(_diff_bounds(idx, gather_tensor(idx, rr)))
-    if checks and any(to_host_ints(torch.cat(checks))):
-        return None
-    ctx.sorted_gids = srt
-    taken = []
-    for i, c in enumerate(cids):
-        if i == lead:
-            taken.append(take(b.gather(c), rep))
-        else:
-            bb, idx = b.parts[b.owner[c]]
-            taken.append(take(bb.columns[c], gather_tensor(idx, rep)))
-    return gid, ng, rep, taken
-
-
-def _lead_key(others, spans, cols) -> int:
-    """The grouping key the others are tested to depend on: the widest-range
-    plain integer key (a key column, e.g. c_custkey), before decimals and
-    dictionary codes (an account balance spans more values than 150K
-    customer keys at SF1, but identifies nothing)."""
-    def rank(i):
-        t = cols[i].dtype
-        intlike = (t.is_integer and not t.is_decimal) and not cols[i].is_dict
-        return (1 if intlike else 0, spans[i][1] - spans[i][0] if spans[i] else -1)
-    return max(others, key=rank)
-
-
-def _encode_groups(gcols: List[Column], ctx):
-    """Dense group ids for GROUP BY over ``gcols`` -> (gid, ng, rep_row, rep_source_cols).
-
-    Functional-dependency shortcut (GPU): when plain (non-dictionary) string
-    keys are present, group by the integer key with the widest domain first and
-    verify on the device that every other key is constant within those groups
-    (a row-vs-representative comparison, far cheaper than hashing and
-    dictionary-encoding strings). Keys that pass are dropped from the grouping
-    — the result is identical to grouping by all of them. TPC-H Q10 groups by
-    c_custkey plus six customer attributes: one direct-mapped integer group-by
-    replaces seven encodings."""
-    plain = [i for i, c in enumerate(gcols) if c.dtype.is_string and not c.is_dict]
-    others = [i for i in range(len(gcols)) if i not in plain]
-    keys: Dict[int, torch.Tensor] = {}
-    reps_src: List[Column] = list(gcols)
-    for i in others:
-        keys[i], reps_src[i] = group_key_tensor(gcols[i])
-    needed = list(range(len(gcols)))
-    if plain and others and ctx.device.type == "cuda":
-        spans = {i: H.key_range(keys[i]) for i in others}
-        lead = _lead_key(others, spans, gcols)
-        gid, ng, rep, srt = H.group_ids_ex(keys[lead])
-        ctx.sorted_gids = srt
-        rr = gather_tensor(rep, gid)
-        bad = []
-        for i in range(len(gcols)):
-            if i == lead:
-                continue
-            c = gcols[i]
-            if i in plain:
-                m = torch.zeros(1, dtype=torch.int32, device=ctx.device)
-                launch("str_eq_rows").str_eq_rows(ptr(c.offsets), ptr(c.data), 0, ptr(c.offsets), ptr(c.data),
-                                                  ptr(rr), False, len(c), ptr(m), stream(m))
-                m = m.to(torch.int64)[0]
-            else:
-                m = (keys[i] != keys[i].index_select(0, rr)).sum()
-            if c.valid is not None:
-                m = m + (c.valid != c.valid.index_select(0, rr)).sum()
-            bad.append((i, m))
-        counts = to_host_ints(torch.stack([m for _, m in bad]).to(torch.int64))
-        needed = [lead] + [i for (i, _), cnt in zip(bad, counts) if cnt]
-        if len(needed) == 1:
-            return gid, ng, rep, reps_src
-    for i in plain:
-        if i in needed:
-            keys[i], _ = group_key_tensor(gcols[i])
-    packed = H.pack_keys([keys[i] for i in needed])
-    gid, ng, rep, srt = H.group_ids_ex(packed)
-    ctx.sorted_gids = srt
-    return gid, ng, rep, reps_src
-
-
-def _empty_col(t, dev) -> Column:
-    if t.is_string:
-        return Column(t, torch.zeros(0, dtype=torch.uint8, device=dev), None, offsets=torch.zeros(1, dtype=torch.int64, device=dev))
-    return Column(t, torch.zeros(0, dtype=t.torch_dtype if t.kind != "null" else torch.bool, device=dev))
-
-
-def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
-    """Append kernel specs for one aggregate and a finaliser producing its column."""
-    ev = ctx.evaluator
-    dev = ctx.device
-    func = a.func
-    col = ev.column(a.arg, b) if a.arg is not None else None
-    valid = col.valid if col is not None else None
-    if a.filter is not None:
-        fm = ev.mask(a.filter, b)
-        valid = fm if valid is None else (valid & fm)
-    if a.distinct and func in ("count", "sum", "avg"):
-        # de-duplicate (group, value) pairs first, then aggregate the survivors
-        k, _ = group_key_tensor(col)
-        pair = H.pack_keys([gid.to(torch.int64) if gid is not None else torch.zeros(n, dtype=torch.int64, device=dev), k])
-        keep_rows = torch.ones(n, dtype=torch.bool, device=dev) if valid is None else valid
-        if n:
-            _, _, rep = H.group_ids(pair)
-            first = torch.zeros(n, dtype=torch.bool, device=dev)
-            first.index_fill_(0, rep.long(), True)
-            keep_rows = keep_rows & first
-        valid = keep_rows
-    base = len(specs)
-
-    def add(op, vals, vv):
-        specs.append((op, vals, vv))
-        return len(specs) - 1
-
-    t = a.dtype
-    if func == "count":
-        i = add("count", None, valid)
-        finals.append(lambda r, i=i: (ci, Column(T.INT64, r[i])))
-        return
-    if col is None:
-        raise ExecutionError(f"{func} needs an argument")
-    src = col.dtype
-    cnt_i = add("count", None, valid) if (valid is not None or func in ("avg",) or n == 0 or gid is None) else None
-
-    def null_if_empty(r, data, cnt_i=cnt_i):
-        if cnt_i is None:
-            return None
-        return r[cnt_i] > 0
-
-    if func in ("sum", "avg"):
-        if src.is_float:
-            si = add("sum_f64", col.data.to(torch.float64).contiguous(), valid)
-        else:
-            vals = col.data
-            if vals.dtype not in (torch.int32, torch.int64):
-                vals = vals.to(torch.int64)
-            si = add("sum_int", vals.contiguous(), valid)
-        if func == "sum":
-            def fin(r, si=si):
-                v = r[si]
-                vv = null_if_empty(r, v)
-                return ci, Column(t, v if not t.is_float else v.to(torch.float64), vv)
-            finals.append(fin)
-        else:
-            def fin(r, si=si):
-                s, c = r[si], r[cnt_i]
-                vv = c > 0
-                return ci, Column(t, _avg(s, c, src, t), vv)
-            finals.append(fin)
-        return
-    if func in ("min", "max"):
-        if src.is_string:
-            d = col if col.is_dict else S.dict_encode(col)
-            ranks = S.sort_ranks(d)
-            vals = d.dictionary
-            i = add("min_int" if func == "min" else "max_int", ranks.contiguous(), valid)
-            # map winning rank back to a dictionary code
-            from ..ops.sort import argsort as _argsort
-            dranks = S.sort_ranks(Column(T.UTF8, torch.arange(len(vals), dtype=torch.int32, device=dev), None,
-                                         dictionary=vals))
-            order = _argsort([(dranks, False, False, None)], dranks.numel(), dev)
-
-            def fin(r, i=i, order=order, d=d):
-                rk = r[i]
-                vv = null_if_empty(r, rk)
-                safe = rk.clamp(0, max(len(order) - 1, 0))
-                codes = gather_tensor(order, safe).to(torch.int32) if len(order) else safe.to(torch.int32)
-                return ci, Column(T.UTF8, codes, vv, dictionary=d.dictionary)
-            finals.append(fin)
-            return
-        if src.is_float:
-            i = add("min_f64" if func == "min" else "max_f64", col.data.to(torch.float64).contiguous(), valid)
-            finals.append(lambda r, i=i: (ci, Column(t, r[i].to(t.torch_dtype), null_if_empty(r, r[i]))))
-            return
-        vals = col.data
-        if vals.dtype not in (torch.int32, torch.int64):
-            vals = vals.to(torch.int64)
-        i = add("min_int" if func == "min" else "max_int", vals.contiguous(), valid)
-        finals.append(lambda r, i=i: (ci, Column(t, r[i].to(t.torch_dtype) if t.kind != "bool" else r[i] != 0,
-                                                 null_if_empty(r, r[i]))))
-        return
-    if func in ("bool_and", "bool_or"):
-        vals = col.data.to(torch.int64)
-        i = add("min_int" if func == "bool_and" else "max_int", vals.contiguous(), valid)
-        finals.append(lambda r, i=i: (ci, Column(T.BOOL, r[i] != 0, null_if_empty(r, r[i]))))
-        return
-    if func in ("stddev", "stddev_samp", "stddev_pop", "var", "var_samp", "var_pop"):
-        x = _convert_tensor(col, T.FLOAT64).contiguous()
-        s1 = add("sum_f64", x, valid)
-        s2 = add("sum_f64", (x * x).contiguous(), valid)
-        ci_ = add("count", None, valid)
-
-        def fin(r, s1=s1, s2=s2, ci_=ci_):
-            c = r[ci_].to(torch.float64)
-            mean = r[s1] / c.clamp(min=1)
-            pop = func.endswith("_pop")
-            denom = c if pop else (c - 1)
-            var = (r[s2] - c * mean * mean) / denom.clamp(min=1)
-            var = var.clamp(min=0)
-            out = var.sqrt() if func.startswith("stddev") else var
-            return ci, Column(T.FLOAT64, out, c > (0 if pop else 1))
-        finals.append(fin)
-        return
-    raise NotSupported(f"aggregate {func}")
-
-
-def _avg(s: torch.Tensor, c: torch.Tensor, src, t) -> torch.Tensor:
-    cc = c.clamp(min=1)
-    if t.is_decimal:
-        up = 10 ** (t.scale - (src.scale if src.is_decimal else 0))
-        if s.is_cuda:
-            # exact rounded division of the (int64 or 128-bit) sums on the device
-            out = torch.empty(s.shape[0], dtype=torch.int64, device=s.device)
-            launch("avg_wide").avg_wide(ptr(s.contiguous()), s.dim() == 2, ptr(c.to(torch.int64).contiguous()),
-                                        s.shape[0], up, ptr(out), stream(s))
-            return out
-        if s.dim() == 1:
-            lim = (2**63 - 1) // up
-            if to_host_int((s.abs() < lim).all().to(torch.int64)):
-                num = s * up
-                q = torch.div(num.abs() + cc // 2, cc, rounding_mode="floor") * torch.sign(num)
-                return q
-        # exact host path for huge sums (few groups)
-        vals = A.wide_to_python(s)
-        cs = c.cpu().tolist()
-        res = []
-        for v, k in zip(vals, cs):
-            k = max(k, 1)
-            num = v * up
-            q = (abs(num) + k // 2) // k
-            res.append(q if num >= 0 else -q)
-        return torch.tensor(res, dtype=torch.int64, device=s.device)
-    if s.dim() == 2:
-        lo = s[:, 0].to(torch.float64)
-        lo = torch.where(lo < 0, lo + 18446744073709551616.0, lo)
-        sf = s[:, 1].to(torch.float64) * 18446744073709551616.0 + lo
-    else:
-        sf = s.to(torch.float64)
-    if src.is_decimal:
-        sf = sf / 10**src.scale
-    return sf / cc.to(torch.float64)
-
-
-# ============================================================ sort / limit / union
-class SortExec(ExecNode):
-    def __init__(self, logical: L.Sort, child: ExecNode):
-        self.logical = logical
-        self.children = [child]
-
-    def describe(self):
-        s = self.logical
-        k = ", ".join(f"{e.sql()} {'ASC' if a else 'DESC'} NULLS {'FIRST' if nf else 'LAST'}" for e, a, nf in s.keys)
-        return k + (f", fetch={s.fetch}" if s.fetch is not None else "")
-
-    def _run(self, ctx):
-        b = self.children[0].execute(ctx)
-        fetch = self.logical.fetch
-        if ctx.spmd and b.dist != ("replicated",):
-            from ..parallel.exchange import gather_all
-            if fetch is not None:
-                # distributed ORDER BY ... LIMIT k: local top-k first, then only
-                # k rows per rank cross the fabric
-                dist = b.dist
-                b = sort_batch(b, self.logical.keys, fetch, ctx)
-                b.dist = dist
-            b = gather_all(b, ctx)
-        out = None
-        if ctx.budget is not None:
-            from .morsel import external_sort
-            out = external_sort(b, self.logical.keys, fetch, ctx)
-        if out is None:
-            out = sort_batch(b, self.logical.keys, fetch, ctx)
-        out.dist = b.dist
-        return out
-
-
-def sort_batch(b: Batch, keys, fetch, ctx) -> Batch:
-    """ORDER BY [LIMIT fetch]: packed keys + radix sort, or radix select +
-    candidate sort for a LIMIT (ops/sort.py)."""
-    from ..ops import sort as SO
-    n = b.num_rows
-    if n <= 1:
-        return b
-    ev = ctx.evaluator
-    if fetch is not None and len(keys) > 1 and ctx.device.type == "cuda":
-        # keep the rows the leading numeric keys can still admit to the top
-        # `fetch` before ranking string tie-breakers (TPC-H Q2, Q21)
-        lead = []
-        for e, asc, nf in keys:
-            c = ev.column(e, b)
-            if c.dtype.is_string or c.is_wide or c.data.dim() != 1:
-                break
-            lead.append((c.data, not asc, nf, c.valid))
-        if lead and len(lead) < len(keys):
-            cand = SO.topk_candidates(lead, n, fetch)
-            if cand is not None and cand.numel() < n:
-                b = _take_batch(b, cand)
-                n = b.num_rows
-    ks = []
-    for e, asc, nf in keys:
-        c = ev.column(e, b)
-        if c.dtype.is_string:
-            v = S.sort_ranks(c)
-        elif c.is_wide:
-            v = _convert_tensor(c, T.FLOAT64)
-        else:
-            v = c.data
-        ks.append((v, not asc, nf, c.valid))
-    if fetch is not None and fetch < n:
-        perm = SO.topk(ks, n, fetch, ctx.device)
-    else:
-        perm = SO.argsort(ks, n, ctx.device)
-    return _take_batch(b, perm)
-
-
-class LimitExec(ExecNode):
-    def __init__(self, logical: L.Limit, child: ExecNode):
-        self.logical = logical
-        self.children = [child]
-
-    def describe(self):
-        return f"skip={self.logical.offset}, fetch={self.logical.limit}"
-
-    def _run(self, ctx):
-        b = self.children[0].execute(ctx)
-        if ctx.spmd and b.dist != ("replicated",):
-            from ..parallel.exchange import gather_all
-            if self.logical.limit is not None:
-                # any offset+limit rows of each rank can make the answer
-                keep = min(b.num_rows, self.logical.offset + self.logical.limit)
-                if keep < b.num_rows:
-                    dist = b.dist
-                    b = _take_batch(b, torch.arange(keep, dtype=torch.int64, device=ctx.device))
-                    b.dist = dist
-            b = gather_all(b, ctx)
-        lo = min(self.logical.offset, b.num_rows)
-        hi = b.num_rows if self.logical.limit is None else min(b.num_rows, lo + self.logical.limit)
-        if lo == 0 and hi == b.num_rows:
-            return b
-        idx = torch.arange(lo, hi, dtype=torch.int64, device=ctx.device)
-        out = _take_batch(b, idx)
-        out.dist = b.dist
-        return out
-
-
-class UnionExec(ExecNode):
-    def __init__(self, logical: L.Union, children: List[ExecNode]):
-        self.logical = logical
-        self.children = children
-
-    def _run(self, ctx):
-        outs = []
-        for ch, p in zip(self.children, self.logical.children):
-            b = ch.execute(ctx)
-            outs.append(Batch({s.cid: b.columns[c.cid] for s, c in zip(self.logical.schema, p.schema)}, b.num_rows,
-                              b.dist))
-        if ctx.spmd:
-            reps = [o.dist == ("replicated",) for o in outs]
-            if all(reps):
-                out = concat_batches(outs)
-                out.dist = ("replicated",)
-                return out
-            if any(reps) and ctx.comm.rank != 0:
-                # a replicated input contributes its rows once (from rank 0)
-                outs = [_take_batch(o, torch.zeros(0, dtype=torch.int32, device=ctx.device)) if r else o
-                        for o, r in zip(outs, reps)]
-        return concat_batches(outs)
+from .context import (  # noqa: F401
+    ExecContext, _NO_SCALAR, _device_scalar, _Span, _NoSpan, _NOSPAN, _sync, ExecNode,
+)
+from .scan import (  # noqa: F401
+    _CID, LATE_SCAN, NDV_DERIVED, _tag_base, ScanExec, predicate_mask, LazyBatch, FragmentInputExec, ValuesExec,
+    _column_from_values, FilterExec, filter_batch, ProjectExec, _ScanColumns, _LazyScanBatch,
+)
+from .joins import (  # noqa: F401
+    key_tensors, _pair_key, _num_key, group_key_tensor, HashJoinExec, RUNTIME_FILTER_MAX_ROWS, _agg_group_source,
+    push_key_filter, _index_key_filter, _index_then_filter, _semi_index_scan, _semi_index_then_filter,
+    _rank_local_semi, apply_key_filters, _batch_bytes, JOIN_MEM_FACTOR, _to_host, _to_device, grace_join, hash_join,
+    SORTED_JOIN_MIN_ROWS, _sorted_join, FLIP_OP, _CMP_KINDS, _col_compare, _nested_loop, _take_batch, _combine,
+    _empty_like, concat_batches, concat_columns, _resident_ndv, _dense_lookup_ok, DENSE_JOIN, SEMI_INDEX,
+    DENSE_JOIN_SMALL, inner_pairs, PERM_INDEX, PERM_INDEX_RATIO, PERM_INDEX_MAX_FRAC, PERM_INDEX_SORT_FRAC,
+    _INT_KEYS, TWO_KEY_SORTED, _two_key_sorted_pairs, _LazyColumns, LateBatch, PRUNE_PARTS, LAZY_JOIN_OUTPUT,
+    MultiJoinExec, _derived_ndv, _scan_info, _replicated, _global_rows, _global_rows_many, _edges,
+)
+from .aggregate import (  # noqa: F401
+    EAGER_COUNT_DIRECT_SPAN, EAGER_COUNT_MASKED, SORTED_HAVING, SORTED_HAVING_MIN_ROWS, INDEX_THEN_FILTER,
+    having_constant, HashAggExec, aggregate, _diff_bounds, _late_group_keys, _lead_key, _encode_groups, _empty_col,
+    _plan_agg, _avg,
+)
+from .sorting import (  # noqa: F401
+    SortExec, sort_batch, LimitExec, UnionExec,
+)

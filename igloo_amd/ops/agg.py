@@ -57,35 +57,16 @@ def grouped_aggregate(gid: Optional[torch.Tensor], ngroups: int, specs: Sequence
     return _cpu(gid, ngroups, specs, n)
 
 
-#: IGLOO_NARROW_SUMS=1: integer SUMs whose exact total provably fits int64
-#: (max|v| * rows < 2^62) accumulate in one 64-bit word (no carry word, half
-#: the atomics, no "fits" pass afterwards). Off by default: the bounds pass
-#: and its host sync cost what the narrow state saves (same-box A/B, SF100
-#: suite 0.1118 s off vs 0.1128 s on, profiles/r3_ab_narrow_sums.txt).
-NARROW_SUMS = os.environ.get("IGLOO_NARROW_SUMS", "0") == "1"
-
-
 def _narrow_sums(specs, n) -> set:
-    """Indices of the integer SUM specs that can accumulate in int64: int32
-    values always (n < 2^31), int64 values when max|v| * n < 2^62 (one device
-    bounds pass per column, one host sync for all)."""
-    if not NARROW_SUMS or n == 0:
+    """Indices of the integer SUM specs that accumulate in one int64 word (no
+    carry word, half the atomics, no "fits" pass afterwards): int32 values,
+    whose exact total over fewer than 2^31 rows provably fits. (int64 values
+    would need a bounds pass and a host sync to decide: measured no gain,
+    profiles/r3_ab_narrow_sums.txt, so they keep the 128-bit state.)"""
+    if n == 0 or n >= 2**31:
         return set()
-    out, wide = set(), []
-    for i, (op, vals, _valid) in enumerate(specs):
-        if op != "sum_int" or vals is None:
-            continue
-        if vals.dtype == torch.int32 and n < 2**31:
-            out.add(i)
-        elif vals.dtype == torch.int64:
-            wide.append((i, vals))
-    if wide:
-        from .sort import _int_bounds
-        b = to_host_ints(torch.cat([_int_bounds(v) for _, v in wide]))
-        for j, (i, _) in enumerate(wide):
-            if max(abs(b[2 * j]), abs(b[2 * j + 1])) * n < 2**62:
-                out.add(i)
-    return out
+    return {i for i, (op, vals, _valid) in enumerate(specs)
+            if op == "sum_int" and vals is not None and vals.dtype == torch.int32}
 
 
 def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor]:
@@ -214,7 +195,7 @@ def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torc
     return counts.to(torch.int64)
 
 
-HIST_PARTITIONED = os.environ.get("IGLOO_HIST_PARTITIONED", "1") == "1"
+HIST_PARTITIONED = True
 
 
 def _key_histogram_partitioned(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torch.Tensor]):

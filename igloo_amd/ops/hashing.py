@@ -22,7 +22,7 @@ EMPTY_KEY = -(2**63)
 INT32_MAX = 2**31 - 1
 BLOOM_MAX_KEYS = 4 << 20   # build sides up to this size get a Bloom filter
 BLOOM_MIN_RATIO = 4        # ... used when probe rows >= ratio x build rows
-EXACT_BITMAP = os.environ.get("IGLOO_EXACT_BITMAP", "1") == "1"
+EXACT_BITMAP = True
 EXACT_BITMAP_MAX_SPAN = 1 << 25   # direct tables up to this key span use an exact bitmap instead
 #: join build keys whose [min, max] span is at most this use the direct-mapped
 #: table (one random read per probe) whatever the build size: 2^26 slots is a
@@ -35,7 +35,7 @@ DIRECT_JOIN_MAX_SPAN = 1 << 26
 #: semi-join build side keeps the whole span of its keys
 TABLE_BYTES_LIMIT: "contextvars.ContextVar[Optional[int]]" = contextvars.ContextVar("igloo_table_bytes", default=None)
 #: first-match probes that only select rows use the two-pass hit-bit kernels
-PROBE_SELECT = os.environ.get("IGLOO_PROBE_SELECT", "1") == "1"
+PROBE_SELECT = True
 
 
 def _next_pow2(x: int) -> int:
@@ -417,7 +417,7 @@ def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Ten
     return lo, cnt
 
 
-SEARCH_FENCE = os.environ.get("IGLOO_SEARCH_FENCE", "1") == "1"
+SEARCH_FENCE = True
 SEARCH_FENCE_MIN_ROWS = 1 << 22
 
 

@@ -72,10 +72,13 @@ def main():
 
     G.take_many, G.gather_tensor, G._take_plain_strings = take_many, gather_tensor, take_str
     # modules that imported the names directly
-    import igloo_amd.exec.operators as OP
+    import igloo_amd.exec.aggregate as AG
+    import igloo_amd.exec.joins as JN
+    import igloo_amd.exec.scan as SC
+    import igloo_amd.exec.sorting as SR
     import igloo_amd.ops.strings as ST
     import igloo_amd.parallel.exchange as EX
-    for mod in (OP, ST, EX):
+    for mod in (SC, JN, AG, SR, ST, EX):
         for name, fn in (("take_many", take_many), ("gather_tensor", gather_tensor)):
             if hasattr(mod, name):
                 setattr(mod, name, fn)

@@ -28,7 +28,7 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
     from igloo_amd.parallel.comm import Communicator
     if low_thresholds:
         # small data must still take the large-data paths (sorted joins, run ids, Bloom probes)
-        from igloo_amd.exec import operators as O
+        from igloo_amd.exec import joins as O
         from igloo_amd.ops import hashing as H
         from igloo_amd.parallel import slicing as SL
         O.SORTED_JOIN_MIN_ROWS = 1000

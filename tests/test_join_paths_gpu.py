@@ -10,7 +10,7 @@ import pyarrow as pa
 import pytest
 
 import igloo_amd as ig
-from igloo_amd.exec import operators as O
+from igloo_amd.exec import joins as J
 from igloo_amd.ops import hashing as H
 
 pytestmark = pytest.mark.gpu
@@ -52,9 +52,9 @@ def _norm(t):
 def test_join_paths_match_cpu(gpu_device, monkeypatch, sorted_big, perm, qi):
     """perm: the unsorted resident big side is joined through its secondary
     (sorted permutation) index instead of a hash probe."""
-    monkeypatch.setattr(O, "PERM_INDEX", perm)
-    monkeypatch.setattr(O, "PERM_INDEX_MAX_FRAC", 1)
-    monkeypatch.setattr(O, "SORTED_JOIN_MIN_ROWS", 1000)
+    monkeypatch.setattr(J, "PERM_INDEX", perm)
+    monkeypatch.setattr(J, "PERM_INDEX_MAX_FRAC", 1)
+    monkeypatch.setattr(J, "SORTED_JOIN_MIN_ROWS", 1000)
     monkeypatch.setattr(H, "SORTED_CHECK_ROWS", 1000)
     monkeypatch.setattr(H, "BLOOM_MIN_RATIO", 2)
     big, small = _tables(sorted_big=sorted_big)
@@ -136,7 +136,7 @@ INDEX_QUERIES = [
     ("SELECT count(*) AS c, sum(b1.bv) AS s FROM big b1, small WHERE b1.ok = sk AND sk < 50000 "
      "AND EXISTS (SELECT * FROM big b2 WHERE b2.ok = b1.ok AND b2.bv <> b1.bv AND b2.bv < 500) "
      "AND NOT EXISTS (SELECT * FROM big b3 WHERE b3.ok = b1.ok AND b3.bk <> b1.bk AND b3.bv < 30)",
-     "join.index_then_filter"),
+     None),
 ]
 
 
@@ -145,7 +145,6 @@ def test_index_paths_default_thresholds(gpu_device, qi, monkeypatch):
     """Mid-size secondary-index joins, index-range runtime key filters and
     semi joins (exec/operators.py inner_pairs, _index_key_filter) with the
     default thresholds, against the CPU engine."""
-    monkeypatch.setattr(O, "SEMI_INDEX_MULTI", True)      # opt-in path (Q21 shape) checked too
     big, small = _index_tables()
     sql, phase = INDEX_QUERIES[qi]
     res = {}

@@ -557,8 +557,7 @@ def test_like_many_tiles_per_workgroup(gpu_device):
 @pytest.mark.parametrize("words", [(1, 4), (4, 9), (8, 20)])
 def test_like_tile_shapes(gpu_device, words):
     """like_seg over short, medium and long strings against the CPU matcher
-    (the one-wave variant, IGLOO_LIKE_WAVE=1, picks its 4 KB / 8 KB tile from
-    the mean length; the default takes 16 KB four-wave tiles)."""
+    (LDS-staged tiles of strings; long strings fall back to direct reads)."""
     r = _rng(21)
     lo, hi = words
     vals = [" ".join(r.choice(WORDS, r.integers(lo, hi))) for _ in range(60_000)]
