@@ -113,8 +113,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--no-aot", action="store_true", help="skip the generated-kernel code objects")
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.jobs, verbose=True)
+    if not a.no_aot:
+        sys.path.insert(0, str(ROOT))
+        from igloo_amd.ops import jit
+        print("jit aot:", jit.aot_compile(jobs=a.jobs or 8))
     return 0
 
 

@@ -485,14 +485,17 @@ class HashAggExec(ExecNode):
         return aggregate(lg.groups, lg.aggs, b, ctx)
 
 
-def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None) -> Batch:
+def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None, fd: bool = False) -> Batch:
     """GROUP BY ``groups`` computing ``aggs`` over ``b``. ``row_parts``
     ({output cid: part index} of a LateBatch ``b``): when the grouping runs
     on the join result's index form (``_late_group_keys``: every other key is
     functionally dependent on the leading integer key), each group's row in
     those parts is added as an int64 column -- the SPMD exchange ships that
     row instead of the part's string columns (parallel/exchange.py). The
-    columns are absent when the dependency did not hold."""
+    columns are absent when the dependency did not hold. ``fd``: the keys are
+    expected to depend on one integer key (the exchange's merge of such
+    partial groups): ``_encode_groups`` tries that shortcut even without
+    plain string keys."""
     ev = ctx.evaluator
     n = b.num_rows
     dev = ctx.device
@@ -510,7 +513,7 @@ def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] =
                 return Batch({ci.cid: _empty_col(ci.dtype, dev) for ci, _ in list(groups) + list(aggs)}, 0)
             with ctx.span("agg.group_ids"):
                 ctx.sorted_gids = False
-                gid, ng, rep, reps_src = _encode_groups(gcols, ctx)
+                gid, ng, rep, reps_src = _encode_groups(gcols, ctx, fd)
         else:
             gid, ng, rep = None, 1, None
         if groups:
@@ -612,17 +615,20 @@ def _lead_key(others, spans, cols) -> int:
     return max(others, key=rank)
 
 
-def _encode_groups(gcols: List[Column], ctx):
+def _encode_groups(gcols: List[Column], ctx, fd: bool = False):
     """Dense group ids for GROUP BY over ``gcols`` -> (gid, ng, rep_row, rep_source_cols).
 
     Functional-dependency shortcut (GPU): when plain (non-dictionary) string
-    keys are present, group by the integer key with the widest domain first and
-    verify on the device that every other key is constant within those groups
-    (a row-vs-representative comparison, far cheaper than hashing and
-    dictionary-encoding strings). Keys that pass are dropped from the grouping
-    — the result is identical to grouping by all of them. TPC-H Q10 groups by
-    c_custkey plus six customer attributes: one direct-mapped integer group-by
-    replaces seven encodings."""
+    keys are present -- or ``fd`` says the keys should depend on one integer
+    key -- group by the integer key with the widest domain first and verify
+    on the device that every other key is constant within those groups (a
+    row-vs-representative comparison, far cheaper than hashing and
+    dictionary-encoding strings or packing several keys). Keys that pass are
+    dropped from the grouping -- the result is identical to grouping by all
+    of them. TPC-H Q10 groups by c_custkey plus six customer attributes: one
+    direct-mapped integer group-by replaces seven encodings; its SPMD merge
+    groups custkey, balance, nation and the customer row shipped instead of
+    the strings (parallel/exchange.py _partial_by_rows) the same way."""
     plain = [i for i, c in enumerate(gcols) if c.dtype.is_string and not c.is_dict]
     others = [i for i in range(len(gcols)) if i not in plain]
     keys: Dict[int, torch.Tensor] = {}
@@ -630,13 +636,13 @@ def _encode_groups(gcols: List[Column], ctx):
     for i in others:
         keys[i], reps_src[i] = group_key_tensor(gcols[i])
     needed = list(range(len(gcols)))
-    if plain and others and ctx.device.type == "cuda":
+    if (plain or (fd and len(gcols) > 1)) and others and ctx.device.type == "cuda":
         spans = {i: H.key_range(keys[i]) for i in others}
         lead = _lead_key(others, spans, gcols)
         gid, ng, rep, srt = H.group_ids_ex(keys[lead])
         ctx.sorted_gids = srt
         rr = gather_tensor(rep, gid)
-        bad = []
+        checks, owner = [], []
         for i in range(len(gcols)):
             if i == lead:
                 continue
@@ -645,14 +651,17 @@ def _encode_groups(gcols: List[Column], ctx):
                 m = torch.zeros(1, dtype=torch.int32, device=ctx.device)
                 launch("str_eq_rows").str_eq_rows(ptr(c.offsets), ptr(c.data), 0, ptr(c.offsets), ptr(c.data),
                                                   ptr(rr), False, len(c), ptr(m), stream(m))
-                m = m.to(torch.int64)[0]
+                checks.append(m.to(torch.int64))
+                owner.append(i)
             else:
-                m = (keys[i] != keys[i].index_select(0, rr)).sum()
+                # device [min, max] of key - representative's key (graph-safe)
+                checks.append(_diff_bounds(keys[i], keys[i].index_select(0, rr)))
+                owner += [i, i]
             if c.valid is not None:
-                m = m + (c.valid != c.valid.index_select(0, rr)).sum()
-            bad.append((i, m))
-        counts = to_host_ints(torch.stack([m for _, m in bad]).to(torch.int64))
-        needed = [lead] + [i for (i, _), cnt in zip(bad, counts) if cnt]
+                checks.append(_diff_bounds(c.valid, c.valid.index_select(0, rr)))
+                owner += [i, i]
+        bad = {i for i, v in zip(owner, to_host_ints(torch.cat(checks))) if v}
+        needed = [lead] + [i for i in range(len(gcols)) if i != lead and i in bad]
         if len(needed) == 1:
             return gid, ng, rep, reps_src
     for i in plain:

@@ -49,14 +49,15 @@ class SortExec(ExecNode):
         b = self.children[0].execute(ctx)
         fetch = self.logical.fetch
         if ctx.spmd and b.dist != ("replicated",):
-            from ..parallel.exchange import gather_all
+            from ..parallel.exchange import SMALL_GATHER_ROWS, gather_all, gather_small
             if fetch is not None:
                 # distributed ORDER BY ... LIMIT k: local top-k first, then only
-                # k rows per rank cross the fabric
+                # k rows per rank cross the fabric, in one fixed-size all-gather
                 dist = b.dist
                 b = sort_batch(b, self.logical.keys, fetch, ctx)
                 b.dist = dist
-            b = gather_all(b, ctx)
+            b = gather_small(b, ctx, fetch) if fetch is not None and fetch <= SMALL_GATHER_ROWS \
+                else gather_all(b, ctx)
         out = None
         if ctx.budget is not None:
             from .morsel import external_sort

@@ -41,6 +41,14 @@ CACHE_DIR = Path(os.environ.get("IGLOO_JIT_CACHE", os.path.join(os.environ.get("
 #: in CACHE_DIR compiles on demand as usual.
 AOT_DIR = Path(os.environ.get("IGLOO_JIT_AOT", os.path.join(os.path.dirname(os.path.dirname(
     os.path.abspath(__file__))), "_jit_cache")))
+#: generated-kernel SOURCES recorded from the benchmark suite (committed text):
+#: ``build()`` (igloo_amd/_build.py ``build_aot``) compiles each into AOT_DIR
+#: with hiprtc on the build host -- no GPU needed -- so the code objects are
+#: our own build output, not checked-in binaries
+AOT_SOURCES = Path(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "jit_sources"))
+#: IGLOO_JIT_DUMP=<dir>: write every generated kernel's source there (how
+#: AOT_SOURCES is recorded: scripts/gpu_run.sh jitsources)
+DUMP_DIR = os.environ.get("IGLOO_JIT_DUMP")
 
 _lock = threading.Lock()
 _kernels: Dict[str, "JitKernel"] = {}
@@ -109,6 +117,8 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
     k = _kernels.get(key)
     if k is not None:
         return k
+    if DUMP_DIR:
+        _dump(src, name, key)
     with _lock:
         k = _kernels.get(key)
         if k is not None:
@@ -156,6 +166,58 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
                 print(f"[jit] {name}: compile failed:\n{e}\n{src}", flush=True)
             return None
         return _load(code, name, key)
+
+
+def _dump(src: str, name: str, key: str) -> None:
+    try:
+        d = Path(DUMP_DIR)
+        d.mkdir(parents=True, exist_ok=True)
+        p = d / f"{key}.hip"
+        if not p.exists():
+            p.write_text(f"// igloo-jit-kernel: {name}\n{src}")
+    except OSError:
+        pass
+
+
+def aot_compile(sources: Path = AOT_SOURCES, out: Path = AOT_DIR, jobs: int = 8) -> dict:
+    """Compile every recorded generated-kernel source (``<key>.hip`` with a
+    ``// igloo-jit-kernel: <entry>`` first line) into ``out/<key>.co`` with
+    hiprtc for gfx950. Incremental: a code object newer than its source is
+    kept. Returns counts."""
+    stats = {"sources": 0, "compiled": 0, "kept": 0, "failed": 0}
+    if not sources.is_dir():
+        return stats
+    out.mkdir(parents=True, exist_ok=True)
+    todo = []
+    for p in sorted(sources.glob("*.hip")):
+        stats["sources"] += 1
+        text = p.read_text()
+        first, _, src = text.partition("\n")
+        if not first.startswith("// igloo-jit-kernel: "):
+            stats["failed"] += 1
+            continue
+        name = first.split(": ", 1)[1].strip()
+        key = _key(src, name)
+        co = out / f"{key}.co"
+        if co.exists() and co.stat().st_mtime >= p.stat().st_mtime:
+            stats["kept"] += 1
+            continue
+        todo.append((src, name, co))
+
+    def one(job):
+        src, name, co = job
+        code = native().jit_compile(src, name, ARCH)
+        tmp = co.with_suffix(f".{os.getpid()}.tmp")
+        tmp.write_bytes(code)
+        os.replace(tmp, co)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(one, j) for j in todo]:
+            try:
+                f.result()
+                stats["compiled"] += 1
+            except Exception:   # noqa: BLE001 - that shape compiles on demand at run time
+                stats["failed"] += 1
+    return stats
 
 
 def wait_all(timeout: Optional[float] = None) -> None:

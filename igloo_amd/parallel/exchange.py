@@ -257,37 +257,96 @@ def _split_bytes(buf: torch.Tensor, sizes: List[int]) -> List[torch.Tensor]:
     return out
 
 
-def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = False) -> Batch:
+class ShufflePlan:
+    """Where this rank's rows go: the stable permutation grouping them by
+    destination, rows per destination, the plain-string columns gathered into
+    that order and their byte counts per destination. Built before the
+    structure all-gather when the caller can ship it in that all-gather's
+    preamble (``preamble``/``receive``): the shuffle then needs no count
+    exchange of its own."""
+
+    def __init__(self, b: Batch, key: torch.Tensor, W: int):
+        from ..ops.gather import take
+        self.W = W
+        n = key.numel()
+        self.perm, self.send = M.hash_partition(key, W) if n else \
+            (torch.zeros(0, dtype=torch.int32, device=key.device), [0] * W)
+        cols = [b.columns[k] for k in b.columns]
+        self.bounds = np.cumsum([0] + list(self.send)).tolist()
+        self.sgath = {j: take(c, self.perm) for j, c in enumerate(cols) if c.is_plain_string}
+        self.sbytes: List[List[int]] = []
+        if self.sgath and not n:
+            self.sbytes = [[0] * W for _ in self.sgath]
+        elif self.sgath:
+            bidx = device_ints(self.bounds, key.device)
+            offs = to_host_ints(torch.cat([g.offsets.index_select(0, bidx).to(torch.int64)
+                                           for g in self.sgath.values()]))
+            for k in range(len(self.sgath)):
+                o = offs[k * (W + 1):(k + 1) * (W + 1)]
+                self.sbytes.append([o[r + 1] - o[r] for r in range(W)])
+        self.str_cols = [j for j, c in enumerate(cols) if c.dtype.is_string]
+        self.rmat: Optional[List[List[int]]] = None
+
+    def matrix(self) -> List[List[int]]:
+        return [[self.send[r]] + [sb[r] for sb in self.sbytes] for r in range(self.W)]
+
+    def preamble(self) -> List[int]:
+        """Fixed-length ints (same on every rank): per destination the row
+        count and every string column's bytes (-1: dictionary here)."""
+        by = {j: sb for j, sb in zip(self.sgath, self.sbytes)}
+        out = []
+        for r in range(self.W):
+            out.append(self.send[r])
+            out += [by[j][r] if j in by else -1 for j in self.str_cols]
+        return out
+
+    @staticmethod
+    def width(b: Batch, W: int) -> int:
+        return W * (1 + sum(1 for c in b.columns.values() if c.dtype.is_string))
+
+    def receive(self, pre: List[List[int]], rank: int, nb: Batch) -> bool:
+        """The count matrix from every rank's ``preamble`` (``pre[r]``);
+        False when a string column is plain on some ranks and dictionary-
+        coded on others (normalisation decoded it: byte counts unknown)."""
+        ns = len(self.str_cols)
+        cols = [nb.columns[k] for k in nb.columns]
+        plain_now = [j for j in self.str_cols if cols[j].is_plain_string]
+        if plain_now != list(self.sgath):
+            return False
+        rmat = []
+        for r in range(self.W):
+            blk = pre[r][rank * (1 + ns):(rank + 1) * (1 + ns)]
+            bys = [blk[1 + t] for t, j in enumerate(self.str_cols) if j in self.sgath]
+            if any(x < 0 for x in bys):
+                return False
+            rmat.append([blk[0]] + bys)
+        self.rmat = rmat
+        return True
+
+
+def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = False,
+            plan: Optional[ShufflePlan] = None) -> Batch:
     """Hash-repartition rows of ``b`` by ``key`` across all ranks.
 
     Collectives: the structure all-gather (skipped when the caller already
     ``normalized`` the batch), one all-to-all of the [rank x (rows, string
-    bytes...)] count matrix, and ONE all-to-all-v of bytes: per destination
-    the packed fixed-width rows (gathered into destination order by the pack
-    kernel itself) followed by every plain-string column's bytes."""
-    from ..ops.gather import take
+    bytes...)] count matrix (skipped when ``plan`` carries it: the caller
+    shipped it in its structure all-gather), and ONE all-to-all-v of bytes:
+    per destination the packed fixed-width rows (gathered into destination
+    order by the pack kernel itself) followed by every plain-string column's
+    bytes."""
     from ..ops.pack import pack_rows, unpack_rows
     comm = ctx.comm
     W = comm.world_size
     if not normalized:
         b = normalize_structure(materialized(b), comm)
-    perm, send = M.hash_partition(key, W)
+    if plan is None or plan.rmat is None:
+        plan = ShufflePlan(b, key, W)
+        plan.rmat = comm.all_to_all_matrix(plan.matrix())
+    perm, send, bounds, sgath, sbytes, rmat = plan.perm, plan.send, plan.bounds, plan.sgath, plan.sbytes, plan.rmat
     keys = list(b.columns)
     cols = [b.columns[k] for k in keys]
     tensors, spec = _fixed_parts(cols)
-    # string bytes per destination (strings gathered into destination order;
-    # every column's W + 1 byte bounds in one readback)
-    bounds = np.cumsum([0] + list(send)).tolist()
-    sgath = {j: take(c, perm) for j, c in enumerate(cols) if c.is_plain_string}
-    sbytes = []
-    if sgath:
-        bidx = device_ints(bounds, key.device)
-        offs = to_host_ints(torch.cat([g.offsets.index_select(0, bidx).to(torch.int64) for g in sgath.values()]))
-        for k in range(len(sgath)):
-            o = offs[k * (W + 1):(k + 1) * (W + 1)]
-            sbytes.append([o[r + 1] - o[r] for r in range(W)])
-    mat = [[send[r]] + [sb[r] for sb in sbytes] for r in range(W)]
-    rmat = comm.all_to_all_matrix(mat)
     recv = [r[0] for r in rmat]
     packed, lay = pack_rows(tensors, perm, b.num_rows) if tensors else (None, (0, []))
     rb = lay[0]
@@ -428,6 +487,100 @@ def gather_all(b: Batch, ctx, max_rows: Optional[int] = None, normalized: bool =
         sb = None   # a dictionary column was decoded by normalisation: exchange its byte counts
     out = dict(zip(keys, _gather_columns(cols, counts, comm, sb))) if keys else {}
     return with_dist(Batch(out, sum(counts)), REPLICATED)
+
+
+#: string bytes per row and string column a small gather reserves per rank
+SMALL_GATHER_STR_BYTES = 160
+#: largest per-rank row count ``gather_small`` serves (ORDER BY ... LIMIT k)
+SMALL_GATHER_ROWS = 4096
+
+
+def gather_small(b: Batch, ctx, cap_rows: int) -> Batch:
+    """``gather_all`` for a batch of at most ``cap_rows`` rows per rank (the
+    local top-k of a distributed ORDER BY ... LIMIT k) in ONE collective: a
+    fixed-size all-gather of per-rank slots whose layout follows from the
+    schema and ``cap_rows`` alone -- [header | packed rows | string bytes per
+    column] with validity always present, strings plain and decimals 128-bit
+    -- so no structure or count exchange precedes it. The header carries the
+    row count, the string byte counts and the local structure bits (validity
+    and 128-bit sums are dropped again when no rank had them). A rank whose
+    rows or string bytes exceed the slot flags it there; every rank then sees
+    the flag and falls back to ``gather_all`` alike."""
+    from ..ops.pack import pack_rows, unpack_rows
+    from ..ops.select import offsets_from_lengths
+    comm = ctx.comm
+    if comm is None or not comm.spmd or dist_of(b) == REPLICATED:
+        return b
+    b = materialized(b)
+    W = comm.world_size
+    keys = list(b.columns)
+    n = b.num_rows
+    dev = ctx.device
+    cap_s = cap_rows * SMALL_GATHER_STR_BYTES
+    flags, tensors, chars = [], [], []
+    over = n > cap_rows
+    for k in keys:
+        c = b.columns[k]
+        flags.append((1 if c.valid is not None else 0) | (2 if c.is_wide else 0))
+        if c.is_dict:
+            c = S.decode(c)
+        tensors.append(c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool, device=dev))
+        if c.is_plain_string:
+            tensors.append((c.offsets[1:] - c.offsets[:-1]).to(torch.int64))
+            chars.append(c.data)
+            over = over or c.data.numel() > cap_s
+        elif c.dtype.is_decimal and not c.is_wide:
+            x = c.data.to(torch.int64)
+            tensors.append(torch.stack([x, x >> 63], 1))
+        else:
+            tensors.append(c.data)
+    sbytes = [int(x.numel()) for x in chars]
+    hdr = [n, int(over)] + flags + sbytes
+    H = 8 * len(hdr)
+    packed, lay = pack_rows(tensors, None, n)
+    rb = lay[0]
+    slot = H + cap_rows * rb + len(chars) * cap_s
+    pieces = [device_ints(hdr, dev).view(torch.uint8)]
+    if not over:
+        pieces.append(packed.reshape(-1))
+        pieces.append(torch.zeros((cap_rows - n) * rb, dtype=torch.uint8, device=dev))
+        for x in chars:
+            pieces += [x.view(torch.uint8), torch.zeros(cap_s - x.numel(), dtype=torch.uint8, device=dev)]
+    else:
+        pieces.append(torch.zeros(slot - H, dtype=torch.uint8, device=dev))
+    allb = comm.allgather_tensor(torch.cat(pieces)).view(W, slot)
+    hv = to_host_ints(allb[:, :H].contiguous().view(torch.int64).reshape(-1))
+    hd = [hv[r * len(hdr):(r + 1) * len(hdr)] for r in range(W)]
+    if any(h[1] for h in hd):
+        log.debug("small gather overflowed its slot: falling back to the counted gather")
+        return gather_all(b, ctx)
+    counts = [h[0] for h in hd]
+    total = sum(counts)
+    rows = torch.cat([allb[r, H:H + counts[r] * rb] for r in range(W)]).view(total, rb)
+    parts = unpack_rows(rows, lay, tensors)
+    out, t, sc = {}, 0, 0
+    for j, k in enumerate(keys):
+        c0 = b.columns[k]
+        anyf = 0
+        for h in hd:
+            anyf |= h[2 + j]
+        valid = parts[t] if anyf & 1 else None
+        t += 1
+        if c0.dtype.is_string:
+            lens = parts[t]
+            t += 1
+            base = H + cap_rows * rb + sc * cap_s
+            data = torch.cat([allb[r, base:base + hd[r][2 + len(keys) + sc]] for r in range(W)])
+            sc += 1
+            off = offsets_from_lengths(lens)[0] if total else torch.zeros(1, dtype=torch.int64, device=dev)
+            out[k] = Column(c0.dtype, data, valid, offsets=off)
+            continue
+        data = parts[t]
+        t += 1
+        if c0.dtype.is_decimal and not anyf & 2:
+            data = data[:, 0].contiguous().to(c0.data.dtype)
+        out[k] = Column(c0.dtype, data, valid, dictionary=None)
+    return with_dist(Batch(out, total), REPLICATED)
 
 
 # ----------------------------------------------------------------------- joins
@@ -614,32 +767,81 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     restore = None
     if pb is None:
         pb, groups, restore = _partial_by_rows(groups, partial, b, ids, ctx)
-    # ---- exchange partial states. ONE all-gather agrees on the structure of
-    # the partial batch (validity, dictionary vs plain, 64 vs 128-bit sums,
-    # shared dictionary codes) and carries the local ranges of the integer
-    # group keys; from that, alike on every rank: an all-reduce over a small
-    # dense key domain (global aggregates, dictionary / boolean / small-range
-    # integer keys: TPC-H Q1, Q4, Q9's year x nation, Q13's order counts) or
-    # a hash shuffle by the group key
+    # ---- exchange partial states. A global aggregate (no GROUP BY) is ONE
+    # all-reduce of dense state matrices (every partial column carries a
+    # validity count, so no structure agreement is needed). Otherwise ONE
+    # all-gather agrees on the structure of the partial batch (validity,
+    # dictionary vs plain, 64 vs 128-bit sums, shared dictionary codes) and
+    # carries in its preamble: the local ranges of the integer group keys,
+    # the partial row count and string bytes, and -- where a hash shuffle is
+    # certain to follow -- the shuffle's count matrix row. From that, alike on
+    # every rank, one of:
+    #   * an all-reduce over a small dense key domain (dictionary / boolean /
+    #     small-range integer keys: TPC-H Q1, Q4, Q9's year x nation, Q13);
+    #   * few partial groups in all (<= SMALL_AGG_GATHER): ONE all-gather-v
+    #     and a replicated merge (a following join or ORDER BY needs no
+    #     exchange: Q17's per-part averages, Q20's per-(part, supplier) sums);
+    #   * a hash shuffle by the group key: ONE all-to-all-v.
+    comm = ctx.comm
+    W = comm.world_size
     dense_plan = _dense_candidate(groups, partial)
-    extra = _int_key_ranges(groups, pb) if dense_plan else []
-    pbn = normalize_structure(materialized(pb), ctx.comm, extra)
-    rb = _dense_allreduce(groups, partial, pbn, ctx) if dense_plan else None
-    out_dist = REPLICATED if rb is not None else None
-    log.debug("aggregate exchange: %d partial groups, %s", pb.num_rows, "dense all-reduce" if rb is not None
-              else "shuffle" if groups else "gather")
-    unique = rb is not None
-    if rb is None and groups:
-        g0 = groups[0][0]
-        key, cid = _shuffle_key(groups, pbn)
-        rb = shuffle(pbn, key, ctx, cid, normalized=True)
-        out_dist = rb.dist
-    elif rb is None:
-        rb = gather_all(pbn, ctx, normalized=True)
-        out_dist = REPLICATED
+    unique = False
+    if dense_plan and not groups:
+        pbn = _with_validity(materialized(pb))
+        pbn.preamble = [[] for _ in range(W)]
+        rb = _dense_allreduce(groups, partial, pbn, ctx)
+        log.debug("aggregate exchange: global, dense all-reduce")
+        unique, out_dist = True, REPLICATED
+    else:
+        pm = materialized(pb)
+        extra = _int_key_ranges(groups, pm) if dense_plan else []
+        nr = len(extra)
+        strs = [k for k, c in pm.columns.items() if c.dtype.is_string]
+        extra += [pm.num_rows] + [_str_bytes(pm.columns[k]) if pm.columns[k].is_plain_string else -1 for k in strs]
+        # a shuffle plan travels with the preamble when this rank already
+        # knows the dense domain is too large (its local ranges exceed it)
+        splan, key, kcid = None, None, None
+        if groups and (not dense_plan or pm.num_rows == 0 or
+                       _local_domain(groups, pm, extra[:nr]) > DENSE_ALLREDUCE_MAX):
+            key, kcid = _shuffle_key(groups, pm)
+            splan = ShufflePlan(pm, key, W)
+        pw = ShufflePlan.width(pm, W) if groups else 0
+        extra += ([1] + splan.preamble()) if splan is not None else [0] * (1 + pw)
+        pbn = normalize_structure(pm, comm, extra)
+        pre = pbn.preamble
+        pbn.preamble = [r[:nr] for r in pre]
+        rb = _dense_allreduce(groups, partial, pbn, ctx) if dense_plan and groups else None
+        counts = [r[nr] for r in pre]
+        if rb is not None:
+            unique, out_dist = True, REPLICATED
+            how = "dense all-reduce"
+        elif not groups or sum(counts) <= SMALL_AGG_GATHER:
+            sj = [j for j, k in enumerate(strs) if pbn.columns[k].is_plain_string]
+            sb = [[r[nr + 1 + j] for j in sj] for r in pre]
+            keys = list(pbn.columns)
+            cols = _gather_columns([pbn.columns[k] for k in keys], counts, comm,
+                                   None if any(x < 0 for x in sum(sb, [])) else sb)
+            rb, out_dist = Batch(dict(zip(keys, cols)), sum(counts)), REPLICATED
+            how = "gather"
+        else:
+            base = nr + 1 + len(strs)
+            if splan is not None and all(r[base] for r in pre):
+                if not splan.receive([r[base + 1:] for r in pre], comm.rank, pbn):
+                    splan = None
+            else:
+                splan = None
+            if key is None:
+                key, kcid = _shuffle_key(groups, pbn)
+            rb = shuffle(pbn, key, ctx, kcid, normalized=True, plan=splan)
+            out_dist = rb.dist
+            how = "shuffle" + (" (counts in preamble)" if splan is not None else "")
+        log.debug("aggregate exchange: %d partial groups here, %d in all, %s", pb.num_rows, sum(counts), how)
     # ---- phase 2: merge (the dense all-reduce leaves one row per group:
     # its states only need finalising)
-    res = finalize_unique(groups, plan, rb) if unique else merge_partials(groups, plan, rb, ids, ctx)
+    # (groups that shipped row numbers all depend on the leading integer key:
+    # the merge groups by it and checks the rest)
+    res = finalize_unique(groups, plan, rb) if unique else \
+        merge_partials(groups, plan, rb, ids, ctx, fd=restore is not None)
     if restore is not None:
         res = restore(res)
     return with_dist(res, out_dist)
@@ -750,6 +952,41 @@ def _int_key_ranges(groups, pb: Batch) -> List[int]:
     return out
 
 
+#: partial groups (all ranks) up to which the exchange all-gathers them and
+#: merges on every rank (replicated result) instead of shuffling
+SMALL_AGG_GATHER = 1 << 15
+
+
+def _local_domain(groups, pb: Batch, ranges: List[int]) -> int:
+    """Dense key domain over this rank's partial groups alone (a lower bound
+    of the global one: shared dictionaries and merged ranges only grow)."""
+    dom, ri = 1, 0
+    for ci, _ in groups:
+        c = pb.columns[ci.cid]
+        if _is_int_key(ci):
+            lo, hi = ranges[ri], ranges[ri + 1]
+            ri += 2
+            span = hi - lo + 1 if lo <= hi else 1
+        elif c.dtype.is_string and not c.is_dict:
+            return DENSE_ALLREDUCE_MAX + 1
+        else:
+            span = len(c.dictionary) if c.is_dict else 2
+        dom *= max(span, 1) + (1 if c.valid is not None else 0)
+    return dom
+
+
+def _with_validity(b: Batch) -> Batch:
+    """Every column with a validity mask (all-true where absent): the dense
+    all-reduce's state matrix then has the same columns on every rank."""
+    out = {}
+    for k, c in b.columns.items():
+        if c.valid is None:
+            c = Column(c.dtype, c.data, torch.ones(len(c), dtype=torch.bool, device=c.data.device), c.offsets,
+                       c.dictionary)
+        out[k] = c
+    return Batch(out, b.num_rows, b.dist)
+
+
 def decomposable(aggs) -> bool:
     """Every aggregate merges from partial states (two-phase aggregation)."""
     return all(a.func in DECOMPOSABLE and not a.distinct for _, a in aggs)
@@ -775,7 +1012,7 @@ def partial_plan(aggs, ids):
     return partial, plan
 
 
-def merge_partials(groups, plan, rb: Batch, ids, ctx) -> Batch:
+def merge_partials(groups, plan, rb: Batch, ids, ctx, fd: bool = False) -> Batch:
     """Phase 2: merge the partial states in ``rb`` (rows = partial groups) into
     the final aggregates of ``plan`` (see ``partial_plan``)."""
     from ..exec.operators import _avg, aggregate
@@ -799,7 +1036,7 @@ def merge_partials(groups, plan, rb: Batch, ids, ctx) -> Batch:
             final.append((ci, AggCall(merge, p1.ref(), False, a.dtype)))
             post.append((func, ci, a, None, None))
     final, recombine = _wide_finals(final, wide_parts, ids)
-    fb = aggregate(fgroups, final, rb, ctx)
+    fb = aggregate(fgroups, final, rb, ctx, fd=fd)
     fb = _join_wide_finals(fb, recombine)
     out = {ci.cid: fb.columns[ci.cid] for ci, _ in groups}
     for func, ci, a, fs, fc in post:

@@ -84,6 +84,14 @@ SETS
       IGLOO_JIT_CACHE="$R/gpurun_out/jit_cache" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
         --steps 1 --warmup 1 --eager-steps 0 --vary-params 0 > gpurun_out/jitcache.log 2>&1
       rc=$?; echo "jitcache rc=$rc"; ls gpurun_out/jit_cache | wc -l ;;
+    jitsources)
+      # record the source of every query-specialised kernel the suite generates
+      # at SF100 (validation parameters + two ad-hoc parameter streams) into
+      # gpurun_out/jit_sources; committed as igloo_amd/jit_sources, compiled
+      # ahead of time by build() (igloo_amd/ops/jit.py aot_compile)
+      IGLOO_JIT_DUMP="$R/gpurun_out/jit_sources" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
+        --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 > gpurun_out/jitsources.log 2>&1
+      rc=$?; echo "jitsources rc=$rc"; ls gpurun_out/jit_sources | wc -l ;;
     budget)
       # all 22 queries at SF${SF:-10} with the device capped at 1 GB (morsels, spill, external sort)
       timeout -k 10 900 python -u scripts/budget_check.py --sf ${SF:-10} --cap-gb 1 --budget-gb 0.25 --ref gpu \
