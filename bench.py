@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="run on CPU (debug)")
     ap.add_argument("--eager-steps", type=int, default=2,
                     help="suites timed with query graphs off (warm_eager_s), after the headline steps")
+    ap.add_argument("--param-seed", type=int, default=1000,
+                    help="seed of the first ad-hoc parameter stream (stream k uses seed + k)")
     ap.add_argument("--vary-params", type=int, default=2, metavar="STREAMS",
                     help="suites with fresh TPC-H substitution parameters per query (adhoc_s; 0 = skip)")
     a = ap.parse_args()
@@ -231,6 +233,7 @@ def main():
     from igloo_amd.exec import graphs as _graphs_mod
     from igloo_amd.models.tpch import params as _params
     eager_s = adhoc_s = None
+    adhoc_streams, adhoc_readbacks, adhoc_modes = [], [], {}
     if a.eager_steps > 0:
         saved = _graphs_mod.GRAPHS
         _graphs_mod.GRAPHS = False
@@ -248,17 +251,27 @@ def main():
             eager_s = comm.allreduce_max_float(eager_s)
         log(f"[bench] warm eager (graphs off): {eager_s:.4f}s per suite")
     if a.vary_params > 0:
-        streams = [_params.stream(qs, 1000 + k, a.sf) for k in range(a.vary_params)]
+        streams = [_params.stream(qs, a.param_seed + k, a.sf) for k in range(a.vary_params)]
         barrier()
         ta = time.perf_counter()
         for st_sql in streams:
+            ts = time.perf_counter()
+            nrb = 0
             for q in qs:
                 eng.sql(st_sql[q])
+                nrb += eng.last_metrics.get("readbacks", 0)
+                m = eng.last_metrics.get("speculation")
+                adhoc_modes[m] = adhoc_modes.get(m, 0) + 1
+            barrier()
+            adhoc_streams.append(time.perf_counter() - ts)
+            adhoc_readbacks.append(nrb)
         barrier()
         adhoc_s = (time.perf_counter() - ta) / a.vary_params
         if comm is not None:
             adhoc_s = comm.allreduce_max_float(adhoc_s)
-        log(f"[bench] ad-hoc (fresh substitution parameters): {adhoc_s:.4f}s per suite")
+            adhoc_streams = [comm.allreduce_max_float(x) for x in adhoc_streams]
+        log(f"[bench] ad-hoc (fresh substitution parameters): {adhoc_s:.4f}s per suite; per stream "
+            f"{[round(x, 4) for x in adhoc_streams]} s, blocking readbacks {adhoc_readbacks}, modes {adhoc_modes}")
 
     # ---- verification (outside the timed region)
     mismatches = [(i, q) for i, res in enumerate(step_results) for q, t in res.items() if digest(t) != ref[q]]
@@ -320,6 +333,10 @@ def main():
             "warm_graph_s": round(step_s, 4),
             "warm_eager_s": round(eager_s, 4) if eager_s is not None else None,
             "adhoc_s": round(adhoc_s, 4) if adhoc_s is not None else None,
+            # per ad-hoc stream: wall seconds and blocking host readbacks (the
+            # first stream's templates have seen only the validation statements)
+            "adhoc_streams_s": [round(x, 4) for x in adhoc_streams],
+            "adhoc_readbacks": adhoc_readbacks,
             "cold_s": round(cold_s, 4),
             # timed-step queries whose host readbacks were replayed and validated
             # on the device (engine.QueryEngine._execute_speculative)

@@ -222,6 +222,21 @@ class Speculation:
             pos += len(vals)
         return out
 
+    def mismatched_entries(self) -> list:
+        """Indices into ``log`` of the replayed entries whose values differed
+        from the device (after a failed ``validate``; one more readback)."""
+        if not self.actual:
+            return []
+        act = torch.cat(self.actual).tolist()
+        out, pos = [], 0
+        for i, (_site, vals) in enumerate(self.log[:self.pos]):
+            if vals is None:
+                continue
+            if act[pos:pos + len(vals)] != list(vals):
+                out.append(i)
+            pos += len(vals)
+        return out
+
     def validate(self) -> bool:
         """True when every replayed value equals the device value (one sync).
         Values handed out before a divergence were replayed at matching call
@@ -315,6 +330,10 @@ def to_host_ints(t: torch.Tensor) -> list:
     return v
 
 
+#: blocking device -> host readbacks so far (engine.py reports them per query)
+READBACKS = [0]
+
+
 def _to_host_ints(t: torch.Tensor) -> list:
     """Small int device tensor -> Python ints with one stream-ordered copy into
     pinned memory that the host polls, instead of ``.item()`` / ``.tolist()``
@@ -323,6 +342,7 @@ def _to_host_ints(t: torch.Tensor) -> list:
     the poll ends on a changed sentinel or an idle stream, whichever first."""
     if t.is_cuda:
         check_not_capturing("host readback")
+        READBACKS[0] += 1
     # single-process only: a 2-rank run sharing one GPU hung in its first query
     # with polled readbacks (cause not isolated), so SPMD ranks keep .tolist()
     if not t.is_cuda or not FAST_READBACK or _distributed():

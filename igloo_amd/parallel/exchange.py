@@ -118,15 +118,41 @@ def partition_keys(c: Column) -> torch.Tensor:
 
 
 # -------------------------------------------------------------- dictionary sync
+_GOLDEN = -0x61C8864680B583EB          # 0x9E3779B97F4A7C15 as int64
+_MIX1, _MIX2 = -0x40A7B892E31B1A47, -0x6B2FB644ECCEEE15
+
+
+def _mix64(x: torch.Tensor) -> torch.Tensor:
+    """splitmix64 finaliser on int64 (wrapping arithmetic, logical shifts)."""
+    m = (1 << 64) - 1
+    def srl(v, k):
+        return (v >> k) & ((m >> k) if k else m)
+    x = (x ^ srl(x, 30)) * _MIX1
+    x = (x ^ srl(x, 27)) * _MIX2
+    return x ^ srl(x, 31)
+
+
 def _dict_digest(d: Column) -> int:
-    """Order-sensitive 63-bit digest of a dictionary's values (cached on it)."""
+    """Order-sensitive 63-bit digest of a dictionary's values (cached on it):
+    the per-entry string hashes (ops/strings.py hash64: the str_hash64 kernel
+    on the GPU) mixed with their positions and summed on the device -- one
+    8-byte readback, no host copy of the dictionary."""
     h = d._unified
     if h is None:
-        import hashlib
-        hh = hashlib.blake2b(digest_size=8)
-        for v in d.to_arrow().to_pylist():
-            hh.update(b"\x00" if v is None else (v.encode() + b"\x01"))
-        h = int.from_bytes(hh.digest(), "little") >> 1
+        from ..ops._lib import unlogged
+        n = len(d)
+        if n == 0:
+            h = 0
+        else:
+            if d.is_dict:
+                d = S.decode(d)
+            hv = S.hash64(d)
+            if d.valid is not None:
+                hv = torch.where(d.valid, hv, torch.full_like(hv, 0x5bd1e995))
+            pos = torch.arange(n, dtype=torch.int64, device=hv.device) * _GOLDEN
+            tot = _mix64(hv ^ pos).sum().reshape(1) + n
+            with unlogged():
+                h = to_host_ints(tot)[0] & ((1 << 63) - 1)
         d._unified = h
     return h
 

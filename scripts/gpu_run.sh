@@ -13,6 +13,8 @@
 #   jitcache  compile the suite's generated kernels at SF100 (validation
 #           parameters only: ad-hoc runs must not find theirs precompiled) into
 #           gpurun_out/jit_cache
+#   jitsources  record generated-kernel sources (igloo_amd/jit_sources)
+#   rbsites blocking readbacks per query, parameter-dependent or not
 #   pmc     rocprofv3 counter passes (FETCH_SIZE / WRITE_SIZE / instruction
 #           mix; one pass per counter set, --kernel-trace only) over the warm
 #           graphed suite; per-kernel bandwidth table (scripts/pmc_summary.py)
@@ -86,11 +88,12 @@ SETS
       rc=$?; echo "jitcache rc=$rc"; ls gpurun_out/jit_cache | wc -l ;;
     jitsources)
       # record the source of every query-specialised kernel the suite generates
-      # at SF100 (validation parameters + two ad-hoc parameter streams) into
-      # gpurun_out/jit_sources; committed as igloo_amd/jit_sources, compiled
-      # ahead of time by build() (igloo_amd/ops/jit.py aot_compile)
+      # at SF100 (validation parameters + two ad-hoc parameter streams whose
+      # seeds differ from the ones bench.py times) into gpurun_out/jit_sources;
+      # committed as igloo_amd/jit_sources, compiled ahead of time by build()
+      # (igloo_amd/ops/jit.py aot_compile)
       IGLOO_JIT_DUMP="$R/gpurun_out/jit_sources" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
-        --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 > gpurun_out/jitsources.log 2>&1
+        --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 --param-seed 7000 > gpurun_out/jitsources.log 2>&1
       rc=$?; echo "jitsources rc=$rc"; ls gpurun_out/jit_sources | wc -l ;;
     budget)
       # all 22 queries at SF${SF:-10} with the device capped at 1 GB (morsels, spill, external sort)
@@ -107,6 +110,11 @@ SETS
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --sf 1 \
         --steps 10 --warmup 3 --per-query > gpurun_out/bench_sf1_2rank_shared.log 2>&1
       rc=$?; echo "sf1 2-rank shared rc=$rc"; tail -1 gpurun_out/bench_sf1_2rank_shared.log | cut -c1-200 ;;
+    rbsites)
+      # blocking readbacks per query and how many are parameter-independent
+      timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 \
+        --out gpurun_out/readback_sites.txt > gpurun_out/readback_sites.log 2>&1
+      rc=$?; echo "rbsites rc=$rc"; head -24 gpurun_out/readback_sites.txt ;;
     gsites)
       timeout -k 10 600 python -u scripts/gather_sites.py --sf ${SF:-100} --queries ${QS:-1-22} \
         --out gpurun_out/gather_sites.txt > gpurun_out/gather_sites.log 2>&1

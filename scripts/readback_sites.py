@@ -1,0 +1,93 @@
+"""Blocking host readbacks per TPC-H query, and how many of them a plan-shape
+keyed replay could serve: each query runs with the validation parameters and
+with ``--streams`` fresh substitution-parameter sets (twice each, so every
+recording is confirmed); the readback logs (ops/_lib.py Speculation) are
+compared site by site.
+
+    python scripts/readback_sites.py --sf 10 [--streams 2] [--out gpurun_out/readback_sites.txt]
+
+Per query: readbacks (call sites in order), whether every parameter set took
+the same call sequence, and how many values were equal across all of them
+(replayable without a device wait) vs parameter-dependent. Tables in HBM."""
+from __future__ import annotations
+
+import argparse
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf", type=float, default=10.0)
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--queries", default="1-22")
+    ap.add_argument("--out", default="gpurun_out/readback_sites.txt")
+    a = ap.parse_args()
+    import igloo_amd as ig
+    from igloo_amd.models.tpch import datagen, params, queries
+    from igloo_amd.ops import jit
+    qs = []
+    for part in a.queries.split(","):
+        lo, _, hi = part.partition("-")
+        qs += list(range(int(lo), int(hi or lo) + 1))
+    e = ig.QueryEngine(device="cuda:0")
+    for name, t in datagen.generate(a.sf, "cuda:0").items():
+        e.register_table(name, t)
+    for q in qs:
+        e.sql(queries.QUERIES[q])
+    jit.wait_all(timeout=300)
+    texts = [{q: queries.QUERIES[q] for q in qs}] + [params.stream(qs, 4000 + k, a.sf) for k in range(a.streams)]
+
+    def log_of(sql):
+        before = set(map(id, e._spec.values()))
+        for _ in range(3):
+            e.sql(sql)
+        new = [st for st in e._spec.values() if id(st) not in before] or list(e._spec.values())
+        st = new[-1]
+        return st["log"] or st["candidate"] or []
+
+    lines = []
+    tot = collections.Counter()
+    sites_all = collections.Counter()
+    vol_sites = collections.Counter()
+    for q in qs:
+        logs = [log_of(t[q]) for t in texts]
+        seqs = [[s for s, _ in lg] for lg in logs]
+        same = all(s == seqs[0] for s in seqs)
+        n = len(logs[0])
+        stable = vol = 0
+        if same:
+            for i in range(n):
+                vals = [lg[i][1] for lg in logs]
+                if all(v is not None and v == vals[0] for v in vals):
+                    stable += 1
+                else:
+                    vol += 1
+                    (code, line), _ = logs[0][i][0]
+                    vol_sites[f"{code.co_filename.split('igloo_amd/')[-1]}:{line} {code.co_name}"] += 1
+        for (site, _vals) in logs[0]:
+            (code, line), _ = site
+            sites_all[f"{code.co_filename.split('igloo_amd/')[-1]}:{line} {code.co_name}"] += 1
+        tot["readbacks"] += n
+        tot["stable"] += stable
+        tot["volatile"] += vol if same else n
+        lines.append(f"Q{q:02d}: {n:3d} readbacks  sequences {'same' if same else 'DIFFER ' + str([len(s) for s in seqs])}"
+                     f"  stable {stable:3d}  parameter-dependent {vol if same else n:3d}")
+    lines.append(f"suite: {dict(tot)}")
+    lines.append("\nreadback sites (validation parameters), most frequent:")
+    lines += [f"  {v:4d}  {k}" for k, v in sites_all.most_common(60)]
+    lines.append("\nparameter-dependent sites:")
+    lines += [f"  {v:4d}  {k}" for k, v in vol_sites.most_common(60)]
+    text = "\n".join(lines)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        f.write(text + "\n")
+    print(text[:6000])
+
+
+if __name__ == "__main__":
+    main()
