@@ -10,7 +10,6 @@ from __future__ import annotations
 
 import collections
 import os
-import re
 import threading
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence, Union
@@ -47,19 +46,6 @@ SPMD_SPECULATE = os.environ.get("IGLOO_SPMD_SPECULATE", "1") == "1"
 SPMD_GRAPHS = os.environ.get("IGLOO_SPMD_GRAPHS", "1") == "1"
 #: SPMD: a query over replicated tables only splits its largest table by key range
 SLICE_REPLICATED = os.environ.get("IGLOO_SLICE_REPLICATED", "1") == "1"
-#: fresh SQL text of a known TEMPLATE (the text with its literals masked, e.g.
-#: TPC-H with new substitution parameters) replays the readbacks that were
-#: equal across the template's earlier statements; the parameter-dependent
-#: ones are read for real (QueryEngine._execute_speculative)
-TEMPLATE_SPECULATE = os.environ.get("IGLOO_TEMPLATE_SPECULATE", "1") == "1"
-#: distinct statements of a template seen before its readbacks are replayed
-TEMPLATE_MIN_STATEMENTS = 2
-_LITERAL_RE = re.compile(r"'(?:[^']|'')*'|(?<![\w.])\d+(?:\.\d+)?(?![\w.])")
-
-
-def sql_template(sql: str) -> str:
-    """``sql`` with every string / numeric literal replaced by ``?``."""
-    return _LITERAL_RE.sub("?", sql)
 
 log = get_logger("engine")
 
@@ -179,9 +165,6 @@ class QueryEngine:
         self.graph_bytes = 0
         self.graph_stats = {"evicted": 0, "dropped_stale": 0}
         self._spec_current: Dict[Any, Any] = {}     # plan key -> its live speculation key
-        # per query template: readback log merged over its statements (None =
-        # parameter-dependent value), the statements seen, failed replays
-        self._tspec: "collections.OrderedDict" = collections.OrderedDict()
         self._query_sources: Dict[Any, list] = {}   # plan key -> cached table sources it reads
         #: SPMD: global NDV and global rows of base-table join keys
         #: ((catalog version, cache generation), table, column) -> (ndv, rows)
@@ -275,17 +258,15 @@ class QueryEngine:
             hit = self._plans.get(key)
             if hit is not None:
                 self._plans.move_to_end(key)
-                return self._exec_query(hit[0], hit[1], time.perf_counter(), cached=True, key=key,
-                                        tkey=hit[2] if len(hit) > 2 else None)
+                return self._exec_query(hit[0], hit[1], time.perf_counter(), cached=True, key=key)
         stmts = parse(sql)
         if key is not None and len(stmts) == 1 and stmts[0]["k"] == "query":
             t0 = time.perf_counter()
             plan, names = self._plan_query(stmts[0])
-            tkey = (sql_template(sql),) + key[1:] if TEMPLATE_SPECULATE else None
-            self._plans[key] = (plan, names, tkey)
+            self._plans[key] = (plan, names)
             while len(self._plans) > PLAN_CACHE_SIZE:
                 self._plans.popitem(last=False)
-            return self._exec_query(plan, names, t0, key=key, tkey=tkey)
+            return self._exec_query(plan, names, t0, key=key)
         if not stmts:
             raise PlanError("empty SQL statement")
         res = None
@@ -357,7 +338,7 @@ class QueryEngine:
         plan, names = self._plan_query(st)
         return self._exec_query(plan, names, t0)
 
-    def _exec_query(self, plan, names, t0: float, cached: bool = False, key=None, tkey=None) -> QueryResult:
+    def _exec_query(self, plan, names, t0: float, cached: bool = False, key=None) -> QueryResult:
         """Execute an optimized logical plan. A cached plan is only the
         parse / bind / optimize output for the same SQL text, catalog version
         and session settings: every execution builds fresh physical operators
@@ -378,7 +359,7 @@ class QueryEngine:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
         with _trace.Range("query"):
-            batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names, tkey)
+            batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
         if table is None:
             table = self._to_arrow(batch, plan.schema, bq_names)
         dev_metrics = {}
@@ -390,7 +371,7 @@ class QueryEngine:
             dev_metrics = {"device_span_ms": round(ev0.elapsed_time(ev1), 3), "hbm_peak_bytes": int(peak),
                            "hbm_query_bytes": int(max(0, peak - mem0))}
         hits, misses = self.cache.stats["hits"] - cs0[0], self.cache.stats["misses"] - cs0[1]
-        if st is not None and spec in ("replayed", "recorded") and st.get("capture_next"):
+        if st is not None and spec in ("replayed", "recorded") and st["capture_next"]:
             st["digest"] = digest(table)      # the next execution's graph must reproduce it
         if spec != "graph":
             self.cache.enforce()   # derived structures built by this query count against the budget
@@ -423,7 +404,7 @@ class QueryEngine:
     def make_context(self, analyze: bool = False) -> ExecContext:
         return ExecContext(self, self.device, self.comm, analyze)
 
-    def _execute_speculative(self, plan: Plan, ctx: ExecContext, key, names=None, tkey=None):
+    def _execute_speculative(self, plan: Plan, ctx: ExecContext, key, names=None):
         """Run the plan; for a repeated query over unchanged data, replay the
         host readbacks (sizes, ranges, strategy choices) of the previous
         executions instead of waiting on the device for each (ops/_lib.py
@@ -434,6 +415,13 @@ class QueryEngine:
         every time); a replay that leaves the recorded sequence continues with
         real readbacks and needs re-confirming; a value mismatch re-executes the query with
         real readbacks (after two, the query is no longer replayed).
+
+        Only byte-identical SQL over unchanged data replays: a replayed value
+        sizes device buffers before the device confirms it, so handing a new
+        statement of the same template (literals masked) the readbacks of an
+        earlier one is unsafe -- a value that matched across earlier statements
+        but follows the parameters undersizes a buffer and the kernels writing
+        it fault (tried: a GPU memory fault on TPC-H with fresh parameters).
 
         SPMD ranks (one per GPU) speculate too: replaying a readback changes
         only when the host waits, never which collectives a rank issues, so
@@ -533,23 +521,8 @@ class QueryEngine:
             replay = False
             ctx = self.make_context()
             log.warning("query graph: replayed values did not match the device; re-executing")
-        tst = None
-        if not replay and st["fails"] == 0 and st["candidate"] is None and tkey is not None:
-            tskey = (tkey,) + skey[1:]
-            tst = self._tspec.get(tskey)
-            if tst is None:
-                tst = self._tspec[tskey] = {"log": None, "keys": set(), "fails": 0}
-                while len(self._tspec) > PLAN_CACHE_SIZE:
-                    self._tspec.popitem(last=False)
-            else:
-                self._tspec.move_to_end(tskey)
-        use_t = tst is not None and tst["log"] is not None and len(tst["keys"]) >= TEMPLATE_MIN_STATEMENTS \
-            and tst["fails"] < 4 and key not in tst["keys"]
         for attempt in range(3):
-            if use_t and attempt == 0:
-                sp = _lib.Speculation("replay", tst["log"])
-            else:
-                sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
+            sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
             _lib.set_speculation(sp)
             try:
                 batch = self._execute_plan(plan, ctx)
@@ -560,21 +533,11 @@ class QueryEngine:
             # recording confirmed by this run)? Agreed with the validation:
             # ranks capture only together
             ready = graphs_on and ok and st["fails"] == 0 and st["graph"] is None and st["graph_aborts"] < 2 \
-                and not self.graphs_disabled and _jit.generation() is not None and not (use_t and attempt == 0) \
-                and (sp.complete if sp.mode == "replay" else _confirm(st["candidate"], sp.log) is not None)
+                and not self.graphs_disabled and _jit.generation() is not None and (
+                    sp.complete if sp.mode == "replay" else _confirm(st["candidate"], sp.log) is not None)
             bad, not_ready = agree(not ok, not ready)
             if not bad:
                 break
-            if use_t and attempt == 0:
-                # a template value that follows the parameters after all: mark
-                # the entries that differed (on this rank) and re-execute
-                tst["fails"] += 1
-                if not ok:
-                    for i in sp.mismatched_entries():
-                        tst["log"][i] = (tst["log"][i][0], None)
-                ctx = self.make_context()
-                log.info("template readbacks did not match the device; re-executing")
-                continue
             # some rank's replayed value did not match its device: every rank
             # re-executes with real readbacks (the same collectives on all)
             if replay:
@@ -587,35 +550,15 @@ class QueryEngine:
         st["cache_keys"] = tuple(dict.fromkeys(ctx.cache_keys))
         if not bad and not not_ready:
             st["capture_next"] = True       # _exec_query keeps this result's digest
-        if use_t and attempt == 0:
-            # this statement's own first recording: the template replay's
-            # sequence (every value validated or read for real)
-            st["candidate"] = sp.fresh
-            self._template_learn(tst, key, sp.fresh)
-            return batch, "template" if sp.complete else "template-partial", st, None
         if sp.mode == "replay":
             if not sp.complete:
                 # the call sequence changed: this run's own sequence must be
                 # confirmed by the next execution before it is replayed
                 st["log"], st["candidate"] = None, sp.fresh
             return batch, "replayed" if sp.complete else "partial", st, None
-        if tst is not None:
-            self._template_learn(tst, key, sp.log)
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
         return batch, "recorded", st, None
-
-    @staticmethod
-    def _template_learn(tst: dict, key, seq: list) -> None:
-        """Merge one statement's readback sequence into its template's log:
-        entries whose values differ become parameter-dependent (None). A
-        different call sequence restarts the template from this statement."""
-        merged = _confirm(tst["log"], seq) if tst["log"] is not None else None
-        if merged is None:
-            tst["log"], tst["keys"] = list(seq), {key}
-        else:
-            tst["log"] = merged
-            tst["keys"].add(key)
 
     def _capture(self, st: dict, plan: Plan) -> bool:
         """Capture ``plan`` under a replay of ``st``'s recording into a query graph."""

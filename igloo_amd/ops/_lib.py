@@ -222,21 +222,6 @@ class Speculation:
             pos += len(vals)
         return out
 
-    def mismatched_entries(self) -> list:
-        """Indices into ``log`` of the replayed entries whose values differed
-        from the device (after a failed ``validate``; one more readback)."""
-        if not self.actual:
-            return []
-        act = torch.cat(self.actual).tolist()
-        out, pos = [], 0
-        for i, (_site, vals) in enumerate(self.log[:self.pos]):
-            if vals is None:
-                continue
-            if act[pos:pos + len(vals)] != list(vals):
-                out.append(i)
-            pos += len(vals)
-        return out
-
     def validate(self) -> bool:
         """True when every replayed value equals the device value (one sync).
         Values handed out before a divergence were replayed at matching call

@@ -14,6 +14,7 @@
 #           parameters only: ad-hoc runs must not find theirs precompiled) into
 #           gpurun_out/jit_cache
 #   jitsources  record generated-kernel sources (igloo_amd/jit_sources)
+#   proj    per-query 8-GPU projection (scripts/spmd_projection.py) at SF100
 #   rbsites blocking readbacks per query, parameter-dependent or not
 #   pmc     rocprofv3 counter passes (FETCH_SIZE / WRITE_SIZE / instruction
 #           mix; one pass per counter set, --kernel-trace only) over the warm
@@ -110,6 +111,13 @@ SETS
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --sf 1 \
         --steps 10 --warmup 3 --per-query > gpurun_out/bench_sf1_2rank_shared.log 2>&1
       rc=$?; echo "sf1 2-rank shared rc=$rc"; tail -1 gpurun_out/bench_sf1_2rank_shared.log | cut -c1-200 ;;
+    proj)
+      # per-query 8-GPU projection from a world-of-one SPMD EXPLAIN ANALYZE at
+      # SF100, scaled by the committed SPMD graph-mode per-query times
+      timeout -k 10 900 python -u scripts/spmd_projection.py --sf ${SF:-100} \
+        --graph-log ${GLOG:-profiles/r4_bench_sf100_spmd_world1_c.log} --json gpurun_out/spmd_projection.json \
+        > gpurun_out/spmd_projection.txt 2>&1
+      rc=$?; echo "proj rc=$rc"; tail -30 gpurun_out/spmd_projection.txt ;;
     rbsites)
       # blocking readbacks per query and how many are parameter-independent
       timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 \

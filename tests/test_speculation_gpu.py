@@ -82,30 +82,16 @@ def test_diverging_site_fails_validation():
     assert not changed.validate()
 
 
-@pytest.mark.parametrize("q", [1, 3, 5, 10, 13, 18, 21, 22])
-def test_template_replay_fresh_parameters(gpu_engine, q):
-    """Fresh SQL text of a known template (new TPC-H substitution parameters)
-    replays the template's parameter-independent readbacks: fewer blocking
-    readbacks than a recording, and the same rows as an engine that reads
-    every value for real."""
-    import igloo_amd as ig
-    from igloo_amd.engine import TEMPLATE_MIN_STATEMENTS
+def test_readbacks_metric(gpu_engine):
+    """``last_metrics["readbacks"]`` counts blocking host readbacks: a fresh
+    statement waits on the device for its sizes, a replayed one does not."""
     from igloo_amd.models.tpch import params
-    from igloo_amd.utils.digest import digest
     e = gpu_engine
-    streams = [params.stream([q], 9100 + k, 0.1)[q] for k in range(TEMPLATE_MIN_STATEMENTS + 3)]
-    modes, reads = [], []
-    for sql in streams:
-        got = e.sql(sql).table
-        modes.append(e.last_metrics["speculation"])
-        reads.append(e.last_metrics["readbacks"])
-        prev = ig.engine.TEMPLATE_SPECULATE
-        ig.engine.TEMPLATE_SPECULATE = False
-        try:
-            ref = ig.QueryEngine(device="cuda:0", catalog=e.catalog)
-            assert digest(ref.sql(sql).table) == digest(got), (q, sql)
-        finally:
-            ig.engine.TEMPLATE_SPECULATE = prev
-    late = modes[TEMPLATE_MIN_STATEMENTS:]
-    assert any(m and m.startswith("template") for m in late), modes
-    assert min(reads[TEMPLATE_MIN_STATEMENTS:]) < max(reads[:TEMPLATE_MIN_STATEMENTS]), (modes, reads)
+    sql = params.stream([3], 9100, 0.1)[3]
+    e.sql(sql)
+    fresh = e.last_metrics["readbacks"]
+    assert fresh > 0
+    for _ in range(4):
+        e.sql(sql)
+    assert e.last_metrics["speculation"] in ("replayed", "graph")
+    assert e.last_metrics["readbacks"] < fresh, e.last_metrics
