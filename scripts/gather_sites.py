@@ -2,9 +2,12 @@
 
 Wraps ops/gather.py (take_many, gather_tensor, the plain-string gather) and
 attributes every gather to its three innermost igloo_amd frames, with rows and
-bytes written; the summary lists per query the sites by bytes.
+bytes written; the summary lists per query the sites by bytes. With
+``--timed`` every fixed-width gather is also bracketed by HIP events and
+classified by index pattern (ascending or not) and source size (fits the 4 MB
+L2, the 256 MB MALL, or neither): kernel milliseconds per class.
 
-usage: python scripts/gather_sites.py [--sf 10] [--queries 9,10] [--out gpurun_out/gather_sites.txt]
+usage: python scripts/gather_sites.py [--sf 10] [--queries 9,10] [--timed] [--out gpurun_out/gather_sites.txt]
 """
 import argparse
 import collections
@@ -28,6 +31,7 @@ def main():
     ap.add_argument("--queries", default="1-22")
     ap.add_argument("--out", default="gpurun_out/gather_sites.txt")
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--timed", action="store_true")
     a = ap.parse_args()
     import torch
     import igloo_amd as ig
@@ -45,21 +49,45 @@ def main():
 
     rec = collections.defaultdict(lambda: [0, 0, 0])     # site -> [calls, rows, bytes]
     o_many, o_tensor, o_str = G.take_many, G.gather_tensor, G._take_plain_strings
+    events = []        # (start, end, class, rows, bytes, site)
+
+    def klass(srcs, idx):
+        n = idx.numel()
+        asc = n < 2 or bool((idx[1:] >= idx[:-1]).all().item())
+        sb = max((t.numel() * t.element_size() for t in srcs), default=0)
+        size = "L2" if sb <= 4 << 20 else "MALL" if sb <= 256 << 20 else "HBM"
+        rows = max((t.shape[0] for t in srcs), default=1)
+        dens = n / max(rows, 1)
+        return f"{'ascending' if asc else 'random':9s} src {size:4s} density {'>=0.1' if dens >= 0.1 else '<0.1':5s}"
+
+    def timed(fn, srcs, idx, kind):
+        if not a.timed or not idx.is_cuda or idx.numel() == 0:
+            return fn(), None
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        out = fn()
+        ev1.record()
+        return out, (ev0, ev1, klass(srcs, idx))
 
     def take_many(cols, idx, neg=False):
-        out = o_many(cols, idx, neg)
+        out, ev = timed(lambda: o_many(cols, idx, neg), [c.data for c in cols if not c.is_plain_string], idx, "m")
         r = rec[("take_many", site())]
         r[0] += 1
         r[1] += idx.numel()
-        r[2] += sum(c.data.numel() * c.data.element_size() for c in out if not c.is_plain_string)
+        b = sum(c.data.numel() * c.data.element_size() for c in out if not c.is_plain_string)
+        r[2] += b
+        if ev:
+            events.append(ev + (idx.numel(), b))
         return out
 
     def gather_tensor(t, idx):
-        out = o_tensor(t, idx)
+        out, ev = timed(lambda: o_tensor(t, idx), [t], idx, "t")
         r = rec[("gather_tensor", site())]
         r[0] += 1
         r[1] += idx.numel()
         r[2] += out.numel() * out.element_size()
+        if ev:
+            events.append(ev + (idx.numel(), out.numel() * out.element_size()))
         return out
 
     def take_str(col, idx, neg):
@@ -83,14 +111,30 @@ def main():
             if hasattr(mod, name):
                 setattr(mod, name, fn)
     lines = []
+    by_class = collections.defaultdict(lambda: [0, 0.0, 0, 0])    # class -> calls, ms, rows, bytes
     for q in qs:
         rec.clear()
+        del events[:]
         e.sql(queries.QUERIES[q])
         sync()
+        qms = 0.0
+        for ev0, ev1, k, rows, b in events:
+            ms = ev0.elapsed_time(ev1)
+            qms += ms
+            c = by_class[k]
+            c[0] += 1
+            c[1] += ms
+            c[2] += rows
+            c[3] += b
         tot = sum(v[2] for v in rec.values())
-        lines.append(f"== Q{q}: {tot / 1e9:.3f} GB gathered")
+        lines.append(f"== Q{q}: {tot / 1e9:.3f} GB gathered" + (f", {qms:.3f} ms in gather launches" if a.timed else ""))
         for (kind, s), (c, rows, b) in sorted(rec.items(), key=lambda kv: -kv[1][2])[:8]:
             lines.append(f"  {b / 1e9:8.3f} GB {rows / 1e6:9.2f} Mrows {c:4d} calls  {kind:13s} {s}")
+    if a.timed:
+        lines.append("\n== by index pattern / source size (fixed-width gathers, event-timed)")
+        for k, (c, ms, rows, b) in sorted(by_class.items(), key=lambda kv: -kv[1][1]):
+            lines.append(f"  {k}  {c:4d} calls {ms:8.3f} ms {rows / 1e6:9.1f} Mrows {b / 1e9:7.3f} GB written "
+                         f"{b / max(ms, 1e-9) / 1e6:7.0f} GB/s")
     txt = "\n".join(lines)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:

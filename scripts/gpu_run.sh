@@ -96,6 +96,12 @@ SETS
       IGLOO_JIT_DUMP="$R/gpurun_out/jit_sources" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
         --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 --param-seed 7000 > gpurun_out/jitsources.log 2>&1
       rc=$?; echo "jitsources rc=$rc"; ls gpurun_out/jit_sources | wc -l ;;
+    jitdiff)
+      # generated kernels the timed ad-hoc streams request (to compare with
+      # igloo_amd/jit_sources: parameter-dependent kernel sources)
+      IGLOO_JIT_DUMP="$R/gpurun_out/jit_b" timeout -k 10 900 python -u bench.py \
+        --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 > gpurun_out/jitdiff.log 2>&1
+      rc=$?; echo "jitdiff rc=$rc"; ls gpurun_out/jit_b | wc -l ;;
     budget)
       # all 22 queries at SF${SF:-10} with the device capped at 1 GB (morsels, spill, external sort)
       timeout -k 10 900 python -u scripts/budget_check.py --sf ${SF:-10} --cap-gb 1 --budget-gb 0.25 --ref gpu \
@@ -118,13 +124,17 @@ SETS
         --graph-log ${GLOG:-profiles/r4_bench_sf100_spmd_world1_c.log} --json gpurun_out/spmd_projection.json \
         > gpurun_out/spmd_projection.txt 2>&1
       rc=$?; echo "proj rc=$rc"; tail -30 gpurun_out/spmd_projection.txt ;;
+    gbench)
+      timeout -k 10 300 python -u scripts/gather_bench.py --out gpurun_out/gather_bench.txt \
+        > gpurun_out/gather_bench.log 2>&1
+      rc=$?; echo "gbench rc=$rc"; tail -20 gpurun_out/gather_bench.txt ;;
     rbsites)
       # blocking readbacks per query and how many are parameter-independent
       timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 \
         --out gpurun_out/readback_sites.txt > gpurun_out/readback_sites.log 2>&1
       rc=$?; echo "rbsites rc=$rc"; head -24 gpurun_out/readback_sites.txt ;;
     gsites)
-      timeout -k 10 600 python -u scripts/gather_sites.py --sf ${SF:-100} --queries ${QS:-1-22} \
+      timeout -k 10 600 python -u scripts/gather_sites.py --sf ${SF:-100} --queries ${QS:-1-22} --timed \
         --out gpurun_out/gather_sites.txt > gpurun_out/gather_sites.log 2>&1
       rc=$?; echo "gsites rc=$rc"; head -30 gpurun_out/gather_sites.txt ;;
     *) echo "unknown mode $mode"; exit 2 ;;

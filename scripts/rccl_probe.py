@@ -1,6 +1,9 @@
 """RCCL probe for a world of one rank (tests/test_rccl_gpu.py): every
-collective parallel/comm.py uses, then the same collectives captured in a HIP
-graph. Prints a progress line after each step so a hang names its step.
+collective parallel/comm.py uses (all-to-all-v, all-gather(-v), all-reduce,
+reduce-scatter, broadcast; no point-to-point: the uneven all-gather pads to
+equal blocks), then all-to-all / all-reduce / all-gather / reduce-scatter
+captured in a HIP graph and replayed with new inputs. Prints a progress line
+after each step so a hang names its step.
 
     MASTER_PORT=29555 python scripts/rccl_probe.py
 """
@@ -34,12 +37,12 @@ print("step 8", flush=True)
 b = c.broadcast_tensor(torch.full((4,), 9, dtype=torch.int32, device=dev))   # broadcast
 assert b.tolist() == [9] * 4
 print("step 9", flush=True)
-# point-to-point (the uneven all-gather-v path): send to / receive from self
-r = torch.empty(200, dtype=torch.int64, device=dev)
-for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, x[:200], 0), dist.P2POp(dist.irecv, r, 0)]):
-    q.wait()
-    print("step 10", flush=True)
-assert torch.equal(r, x[:200])
+# reduce-scatter (partitioned dense aggregates: each rank keeps its key range)
+rs = c.reduce_scatter_tensor(torch.arange(12, dtype=torch.int64, device=dev).view(1, 12), "sum")
+assert rs.tolist() == list(range(12)), rs
+print("step 10", flush=True)
+g2 = c.allgather_tensor(x[:100])                         # all_gather_into_tensor, equal blocks
+assert torch.equal(g2, x[:100])
 print("step 11", flush=True)
 # collectives inside a captured HIP graph, replayed with new inputs
 if os.environ.get("PROBE_GRAPH", "1") == "1":
@@ -61,6 +64,8 @@ if os.environ.get("PROBE_GRAPH", "1") == "1":
         dist.all_reduce(red)
         ag = torch.empty(512, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(ag, dst)
+        rsd = torch.empty(512, dtype=torch.int64, device=dev)
+        dist.reduce_scatter_tensor(rsd, dst)
     for k in (1, 5):
         src.copy_(torch.arange(512, device=dev) + k)
         red.fill_(k)
@@ -68,6 +73,7 @@ if os.environ.get("PROBE_GRAPH", "1") == "1":
         torch.cuda.synchronize()
         assert torch.equal(dst, (torch.arange(512, device=dev) + k) * 2), k
         assert torch.equal(ag, dst) and red.tolist() == [k] * 8, k
+        assert torch.equal(rsd, dst), k
         print("step 14", flush=True)
 mode = os.environ.get("PROBE_SHUTDOWN", "comm")
 print("shutdown:", mode, flush=True)

@@ -43,11 +43,10 @@ def main():
     texts = [{q: queries.QUERIES[q] for q in qs}] + [params.stream(qs, 4000 + k, a.sf) for k in range(a.streams)]
 
     def log_of(sql):
-        before = set(map(id, e._spec.values()))
         for _ in range(3):
             e.sql(sql)
-        new = [st for st in e._spec.values() if id(st) not in before] or list(e._spec.values())
-        st = new[-1]
+        key = (sql, e.catalog.version, tuple(sorted((k, repr(v)) for k, v in e.session.items())))
+        st = e._spec[e._spec_current[key]]
         return st["log"] or st["candidate"] or []
 
     lines = []
