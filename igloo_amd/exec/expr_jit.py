@@ -49,6 +49,7 @@ _UNS = {"i32": "u32", "i64": "u64"}
 PRELUDE = r"""
 typedef signed char i8; typedef short i16; typedef int i32; typedef long long i64;
 typedef unsigned char u8; typedef unsigned int u32; typedef unsigned long long u64;
+__device__ __forceinline__ double i2d(i64 x) { union { i64 i; double d; } u; u.i = x; return u.d; }
 __device__ __forceinline__ void civil(i32 z0, i32* y, i32* m, i32* d) {
   i64 z = (i64)z0 + 719468;
   i64 era = (z >= 0 ? z : z - 146096) / 146097;
@@ -143,6 +144,10 @@ class _Gen:
         self.lines: List[str] = []
         self.n = 0
         self.guard = False
+        # literal / scalar-subquery values travel as 64-bit kernel arguments
+        # (p0, p1, ...): statements that differ only in their constants (TPC-H
+        # substitution parameters, a subquery's result) share one kernel
+        self.params: List[int] = []
 
     def tmp(self) -> str:
         self.n += 1
@@ -195,10 +200,30 @@ class _Gen:
             self.lines.append(f"const {_ct(t)} {name} = ({_ct(t)})c{k}[i];")
         return name, (f"(v{k}[i] != 0)" if c.valid is not None else None), t
 
+    def param(self, x, t: DataType) -> str:
+        """C expression of constant ``x`` of type ``t`` read from a kernel
+        argument (booleans stay inline: they only select code)."""
+        import struct
+        c = _ct(t)
+        if c == "bool":
+            return _lit(x, t)
+        j = len(self.params)
+        if c in ("double", "float"):
+            _flit(float(x))                   # non-finite constants are not generated
+            self.params.append(struct.unpack("<q", struct.pack("<d", float(x)))[0])
+            return f"(({c})i2d(p{j}))"
+        x = int(x)
+        if c == "i32":
+            x = (x + 2**31) % 2**32 - 2**31
+        elif not -(2**63) <= x < 2**63:
+            raise Bail("literal beyond int64")
+        self.params.append(x)
+        return f"(({c})p{j})"
+
     def _lit_value(self, x, t: DataType):
         if x is None:
             return ("0" if _ct(t) != "bool" else "false"), "false", t
-        return _lit(x, t), None, t
+        return self.param(x, t), None, t
 
     def _ColRef(self, e: ColRef):
         c = self.b.columns.get(e.cid)
@@ -424,7 +449,7 @@ class _Gen:
         lits = [_convert_scalar(x.value, x.dtype, t) for x in e.values if x.value is not None]
         ct = _ct(t)
         x = self.bind(ct, v)
-        hit = " || ".join(f"{x} == {_lit(c, t)}" for c in lits) or "false"
+        hit = " || ".join(f"{x} == {self.param(c, t)}" for c in lits) or "false"
         return self.bind("bool", f"!({hit})" if e.negated else f"({hit})"), va, T.BOOL
 
     def _Func(self, e: Func):
@@ -504,7 +529,7 @@ def _source(g: _Gen, out_t: DataType, val: str, valid: Optional[str]) -> str:
     ps.append(f"{_STORE[out_t.kind]}* __restrict__ out")
     if valid is not None:
         ps.append("u8* __restrict__ outv")
-    ps += ["int* __restrict__ errp", "i64 n"]
+    ps += ["int* __restrict__ errp", "i64 n"] + [f"i64 p{j}" for j in range(len(g.params))]
     L = [PRELUDE, f"extern \"C\" __global__ __launch_bounds__({BLOCK}) void igloo_jit_expr(" + ", ".join(ps) + ") {",
          "  int err = 0;",
          f"  for (i64 i = (i64)blockIdx.x * {BLOCK} + threadIdx.x; i < n; i += (i64)gridDim.x * {BLOCK}) {{"]
@@ -566,7 +591,7 @@ def evaluate(e: Expr, b: Batch, ev) -> object:
     args.append(out.data_ptr())
     if outv is not None:
         args.append(outv.data_ptr())
-    args += [err.data_ptr(), n]
+    args += [err.data_ptr(), n] + g.params
     from ..ops._lib import stream, to_host_ints
     grid = max(1, min(-(-n // BLOCK), 256 * 16))
     k.launch(grid, BLOCK, 0, stream(out), args)

@@ -740,8 +740,10 @@ def semi_by_key_set(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
     if join.kind not in ("semi", "anti") or len(join.on or []) != 1 or join.residual is not None \
             or getattr(join, "null_aware", False):
         return None
-    if dist_of(lb) != REPLICATED or dist_of(rb) == REPLICATED:
+    if dist_of(rb) == REPLICATED:
         return None
+    if dist_of(lb) != REPLICATED:
+        return _semi_by_range_marks(lb, rb, join, ctx)
     ev = ctx.evaluator
     le, re_ = join.on[0]
     lcol, rcol = ev.column(le, lb), ev.column(re_, rb)
@@ -760,6 +762,61 @@ def semi_by_key_set(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
     keep = mask_to_indices(hit if join.kind == "semi" else ~hit)
     keys = list(lb.columns)
     return Batch(dict(zip(keys, take_many([lb.columns[k] for k in keys], keep))), int(keep.numel()), REPLICATED)
+
+
+#: largest key domain (bytes of marks per rank) of the range-sliced semi join
+RANGE_MARKS_MAX = 1 << 28
+
+
+def _semi_by_range_marks(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
+    """SEMI / ANTI join of a left side sliced by key range ON THE JOIN KEY
+    (parallel/slicing.py: TPC-H Q22's customer, every rank a contiguous
+    c_custkey chunk) against a partitioned right side: every rank marks the
+    right keys it holds in a dense byte array over the whole key domain
+    [kmin, kmin + world * chunk), and ONE reduce-scatter (max) hands rank r
+    the marks of its own chunk -- the keys of its left rows. (world - 1) /
+    world of the domain's bytes move per rank; no row moves. None when the
+    shape does not apply (the caller exchanges rows instead)."""
+    from ..ops.gather import take_many as _take_many
+    from ..ops.select import mask_to_indices
+    comm = ctx.comm
+    d = dist_of(lb)
+    le, re_ = join.on[0]
+    if not (keyed(d) and isinstance(d[0], tuple) and d[0][0] == "range" and isinstance(le, ColRef)
+            and placed_on(d, le.cid)):
+        return None
+    _tag, W, kmin, chunk = d[0]
+    if W != comm.world_size or W * chunk > RANGE_MARKS_MAX:
+        return None
+    ev = ctx.evaluator
+    lcol, rcol = ev.column(le, lb), ev.column(re_, rb)
+    for c in (lcol, rcol):
+        if c.dtype.is_string or c.data.dim() != 1 or not (c.dtype.is_integer or c.dtype.kind == "date32") \
+                or c.dtype.is_decimal:
+            return None
+    dev = ctx.device
+    dom = W * chunk
+    marks = torch.zeros(dom + 1, dtype=torch.uint8, device=dev)       # [dom]: out-of-domain / NULL keys
+    if rb.num_rows:
+        rk = rcol.data.to(torch.int64) - kmin
+        ok = (rk >= 0) & (rk < dom)
+        if rcol.valid is not None:
+            ok = ok & rcol.valid
+        pos = torch.where(ok, rk, torch.full_like(rk, dom))
+        marks.index_fill_(0, pos, 1)
+    mine = comm.reduce_scatter_tensor(marks[:dom].view(W, chunk), "max")
+    n_l = lb.num_rows
+    if n_l:
+        lk = lcol.data.to(torch.int64) - (kmin + comm.rank * chunk)
+        inr = (lk >= 0) & (lk < chunk)
+        if lcol.valid is not None:
+            inr = inr & lcol.valid
+        hit = (mine.index_select(0, lk.clamp(0, chunk - 1)) > 0) & inr
+    else:
+        hit = torch.zeros(0, dtype=torch.bool, device=dev)
+    keep = mask_to_indices(hit if join.kind == "semi" else ~hit)
+    keys = list(lb.columns)
+    return Batch(dict(zip(keys, _take_many([lb.columns[k] for k in keys], keep))), int(keep.numel()), d)
 
 
 # ------------------------------------------------------------------ aggregation

@@ -13,6 +13,16 @@ The slice is placed ``(("range", world, kmin, chunk), key cid)``: GROUP BY the
 key is rank-local, joins with the other (replicated) inputs are rank-local,
 and two scans sliced with the same mapping are co-partitioned on the key.
 
+A query mixing replicated and partitioned tables slices its largest replicated
+table too when every partitioned input is REDUCED before it meets that table's
+rows in a join:
+under an aggregate, inside a subquery expression, or on the subquery side of
+a semi / anti join (TPC-H Q22: customer anti-joined with orders -- the
+anti-join marks come from a dense reduce-scatter over the customer key range,
+parallel/exchange.py semi_by_key_set; Q20: partsupp against per-(part,
+supplier) lineitem sums). Inner joins with a partitioned table keep the
+replicated side whole (they are rank-local that way).
+
 The same range mapping places the output of the partitioned dense aggregates
 reduced with RCCL reduce-scatter (exec/operators.py eager COUNT, Q13): each
 rank receives the counts of one contiguous key chunk.
@@ -102,18 +112,68 @@ def all_scans(plan: L.Plan):
                     stack.extend(_subplans(e))
 
 
+def _unsliceable(plan: L.Plan) -> set:
+    """ids of the replicated sources whose rows meet UNREDUCED rows of a
+    partitioned table in a join (an inner / outer join input holds the
+    replicated table while another holds a partitioned scan with no aggregate
+    in between): slicing them would turn a rank-local join into an exchange.
+    Rows under an aggregate, on the subquery side of a semi / anti join, or
+    inside a subquery expression count as reduced."""
+    bad = set()
+
+    def visit(p):
+        """(partitioned rows flow out unreduced, replicated sources whose rows flow out)"""
+        for e in _exprs_of(p):
+            for sp in _subplans(e):
+                visit(sp)
+        if isinstance(p, L.Scan):
+            return (False, {id(p.source)}) if getattr(p.source, "replicated", False) else (True, set())
+        if isinstance(p, L.Aggregate):
+            for c in p.inputs:
+                visit(c)
+            return False, set()
+        if isinstance(p, L.Join) and p.kind in ("semi", "anti"):
+            visit(p.right)
+            return visit(p.left)
+        if isinstance(p, (L.Join, L.MultiJoin)):
+            kids = [p.left, p.right] if isinstance(p, L.Join) else list(p.children)
+            if isinstance(p, L.MultiJoin):
+                for sp in p.semis:
+                    visit(sp.right)
+            infos = [visit(c) for c in kids]
+            for i, (part, _) in enumerate(infos):
+                if part:
+                    for k, (_, reps) in enumerate(infos):
+                        if k != i:
+                            bad.update(reps)
+            return any(x[0] for x in infos), set().union(*[x[1] for x in infos])
+        part, reps = False, set()
+        for c in p.inputs:
+            a, r = visit(c)
+            part, reps = part or a, reps | r
+        return part, reps
+
+    visit(plan)
+    return bad
+
+
 def plan_slices(plan: L.Plan, comm) -> Dict[int, str]:
-    """{id(source): key column name} of the table a query over replicated
-    tables only splits by key range (empty when the query reads any
-    partitioned table, or outside SPMD). Decided from the plan and the
-    catalog alone, so every rank decides alike."""
+    """{id(source): key column name} of the replicated table a query splits
+    by key range: a query over replicated tables only, or one whose
+    table's rows meet partitioned rows only after those are reduced
+    (``_unsliceable``; then it must hold SLICE_MIXED_MIN_ROWS). Empty outside SPMD. Decided
+    from the plan and the catalog alone, so every rank decides alike."""
     if comm is None or not comm.spmd:
         return {}
     scans = list(all_scans(plan))
-    if not scans or any(not getattr(s.source, "replicated", False) for s in scans):
+    if not scans:
         return {}
+    mixed = any(not getattr(s.source, "replicated", False) for s in scans)
+    bad = _unsliceable(plan) if mixed else set()
     best = None
     for s in scans:
+        if not getattr(s.source, "replicated", False) or id(s.source) in bad:
+            continue
         key = getattr(s.source, "cluster_key", None)
         if key is None:
             continue
@@ -123,7 +183,7 @@ def plan_slices(plan: L.Plan, comm) -> Dict[int, str]:
             continue
         if best is None or n > best[0]:
             best = (n, s.source, key)
-    if best is None or best[0] < SLICE_MIN_ROWS:
+    if best is None or best[0] < (SLICE_MIXED_MIN_ROWS if mixed else SLICE_MIN_ROWS):
         return {}
     return {id(best[1]): best[2]}
 
@@ -131,6 +191,9 @@ def plan_slices(plan: L.Plan, comm) -> Dict[int, str]:
 #: tables smaller than this are not worth splitting (the exchange of the
 #: partial results costs more than the repeated work)
 SLICE_MIN_ROWS = 1 << 16
+#: ... in a query that also reads partitioned tables (its joins with the
+#: reduced partitioned side may need an exchange the whole table avoids)
+SLICE_MIXED_MIN_ROWS = 1 << 22
 
 
 def _cut(c: Column, a: int, b: int) -> Column:

@@ -36,6 +36,7 @@ def main():
         O.SORTED_JOIN_MIN_ROWS = 1000
         H.SORTED_CHECK_ROWS = 1000
         SL.SLICE_MIN_ROWS = 1000
+        SL.SLICE_MIXED_MIN_ROWS = 1000
     qs = []
     for part in a.queries.split(","):
         lo, _, hi = part.partition("-")

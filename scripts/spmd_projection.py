@@ -34,6 +34,41 @@ def walk(n):
         yield from walk(c)
 
 
+def _graph_ms(path):
+    out = {}
+    if path and os.path.exists(path):
+        for line in open(path):
+            m = re.match(r"\[bench\] Q(\d+)\s+([\d.]+) ms", line)
+            if m:
+                out[int(m.group(1))] = float(m.group(2))
+    return out
+
+
+def rescore(a):
+    """Graph-scaled projection from a saved run (the EXPLAIN ANALYZE split into
+    replicated / partitioned work and collectives) and a bench.py log."""
+    d = json.load(open(a.rescore))
+    g = _graph_ms(a.graph_log)
+    tot = {"g1": 0.0, "t8_scaled": 0.0}
+    for r in d["queries"]:
+        g1 = g.get(r["q"])
+        r["graph_world1_ms"] = g1
+        r["t8_scaled_to_graph_ms"] = round(r["t8_ms"] * g1 / r["t1_analyze_ms"], 3) if g1 else None
+        if g1:
+            tot["g1"] += g1
+            tot["t8_scaled"] += r["t8_scaled_to_graph_ms"]
+        print(f"Q{r['q']:02d}  world-1 graph {g1 or 0:7.2f} ms  replicated share "
+              f"{r['replicated_ms'] / max(r['t1_analyze_ms'], 1e-9):5.1%}  collectives {r['collectives']:2d}  "
+              f"-> T8 {r['t8_scaled_to_graph_ms'] or 0:6.2f} ms")
+    print(f"suite: world-1 graph {tot['g1']:.2f} ms -> projected {d['world']} GPUs {tot['t8_scaled']:.2f} ms "
+          f"({tot['g1'] / max(tot['t8_scaled'], 1e-9):.2f}x)")
+    d["suite_graph_world1_ms"] = round(tot["g1"], 3)
+    d["suite_t8_scaled_ms"] = round(tot["t8_scaled"], 3)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(d, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sf", type=float, default=100)
@@ -43,7 +78,10 @@ def main():
     ap.add_argument("--gbps", type=float, default=500.0, help="per-rank aggregate xGMI egress used by exchanges")
     ap.add_argument("--graph-log", default=None, help="bench.py --per-query log of the SPMD world-1 graph run")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--rescore", default=None, help="a --json output: recompute the graph-scaled column only")
     a = ap.parse_args()
+    if a.rescore:
+        return rescore(a)
     os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29800 + os.getpid() % 100))
     import torch
     import igloo_amd as ig

@@ -38,6 +38,7 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
         H.SORTED_CHECK_ROWS = 1000
         H.BLOOM_MIN_RATIO = 2
         SL.SLICE_MIN_ROWS = 1000
+        SL.SLICE_MIXED_MIN_ROWS = 1000      # Q20 / Q22 slice partsupp / customer
     comm = Communicator.init(backend="gloo", device=device, timeout_s=120)
     e = ig.QueryEngine(device=device, comm=comm)
     for name, t in datagen.generate(sf, device, rank, world, replicate_dims=replicate_dims).items():
