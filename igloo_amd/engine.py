@@ -653,6 +653,7 @@ class QueryEngine:
         if self.comm is not None and self.comm.spmd:
             from .parallel.exchange import gather_all
             out = gather_all(out, ctx)
+        ctx.check_deferred()
         return out
 
     def _slices_for(self, plan: Plan) -> Dict[int, str]:
@@ -693,6 +694,7 @@ class QueryEngine:
             h0 = dict(HOST_STEPS)
             t0 = time.perf_counter()
             node.execute(ctx)
+            ctx.check_deferred()
             ms = (time.perf_counter() - t0) * 1e3
             rows_t = ["physical_plan_with_metrics"]
             txt = node.explain(ctx) + f"\ntotal: {ms:.3f} ms"

@@ -36,6 +36,20 @@ from .expr_eval import Evaluator, Scalar, _convert_tensor
 class ExecContext:
     """Per-query execution state: device, communicator, metrics, subquery cache."""
 
+    def check_deferred(self) -> None:
+        """Raise the first deferred device error whose flag is set (ONE
+        readback for all of them, at the end of the query)."""
+        if not self.deferred_checks:
+            return
+        import torch
+        from ..ops._lib import to_host_ints
+        from ..utils.errors import ExecutionError
+        flags = to_host_ints(torch.cat([f.reshape(-1).to(torch.int64) for f, _ in self.deferred_checks]))
+        checks, self.deferred_checks = self.deferred_checks, []
+        for v, (_, msg) in zip(flags, checks):
+            if v:
+                raise ExecutionError(msg)
+
     def __init__(self, engine=None, device="cpu", comm=None, analyze: bool = False):
         self.engine = engine
         self.device = torch.device(device)
@@ -74,6 +88,9 @@ class ExecContext:
         # raw scans a fast-path check already read (ScanExec.peek_raw): the
         # general path that runs when the check fails reuses them
         self.raw_peeks: Dict[int, Batch] = {}
+        # device error flags checked once when the query's result is ready
+        # (generated kernels' decimal-overflow flags: no mid-query sync)
+        self.deferred_checks: list = []
         # SPMD: {id(source): key column} of the replicated table this query
         # splits by key range (parallel/slicing.py plan_slices)
         self.slices: Dict[int, str] = {}

@@ -595,6 +595,11 @@ def evaluate(e: Expr, b: Batch, ev) -> object:
     from ..ops._lib import stream, to_host_ints
     grid = max(1, min(-(-n // BLOCK), 256 * 16))
     k.launch(grid, BLOCK, 0, stream(out), args)
-    if g.guard and to_host_ints(err)[0]:
-        raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
+    if g.guard:
+        msg = "decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE"
+        qctx = getattr(ev, "ctx", None)
+        if qctx is not None and hasattr(qctx, "deferred_checks"):
+            qctx.deferred_checks.append((err, msg))     # checked once at the end of the query
+        elif to_host_ints(err)[0]:
+            raise ExecutionError(msg)
     return Column(out_t, out, outv)

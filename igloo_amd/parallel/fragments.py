@@ -279,7 +279,9 @@ def local_runner(engine):
     def run(frag: QueryFragment, inputs: Dict[str, object]):
         ctx = engine.make_context()
         ctx.fragment_inputs = inputs
-        return create_physical_plan(frag.plan).execute(ctx)
+        out = create_physical_plan(frag.plan).execute(ctx)
+        ctx.check_deferred()
+        return out
     return run
 
 
@@ -352,6 +354,7 @@ def run_encoded_fragment(engine, payload: bytes):
         ctx = engine.make_context()
         ctx.fragment_inputs = inputs
         out = create_physical_plan(plan).execute(ctx)
+        ctx.check_deferred()
         if spmd:
             from .exchange import gather_all
             out = gather_all(out, ctx)

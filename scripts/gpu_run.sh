@@ -130,7 +130,7 @@ SETS
       rc=$?; echo "gbench rc=$rc"; tail -20 gpurun_out/gather_bench.txt ;;
     rbsites)
       # blocking readbacks per query and how many are parameter-independent
-      timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 \
+      timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 --stacks \
         --out gpurun_out/readback_sites.txt > gpurun_out/readback_sites.log 2>&1
       rc=$?; echo "rbsites rc=$rc"; head -24 gpurun_out/readback_sites.txt ;;
     gsites)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--queries", default="1-22")
     ap.add_argument("--out", default="gpurun_out/readback_sites.txt")
+    ap.add_argument("--stacks", action="store_true",
+                    help="also count real readbacks of a fresh stream by their 3 innermost engine frames")
     a = ap.parse_args()
     import igloo_amd as ig
     from igloo_amd.models.tpch import datagen, params, queries
@@ -77,6 +79,26 @@ def main():
         lines.append(f"Q{q:02d}: {n:3d} readbacks  sequences {'same' if same else 'DIFFER ' + str([len(s) for s in seqs])}"
                      f"  stable {stable:3d}  parameter-dependent {vol if same else n:3d}")
     lines.append(f"suite: {dict(tot)}")
+    if a.stacks:
+        import traceback
+        from igloo_amd.ops import _lib
+        stacks = collections.Counter()
+        orig = _lib._to_host_ints
+
+        def counted(t):
+            if t.is_cuda:
+                fr = [f for f in traceback.extract_stack()[:-1] if "igloo_amd" in f.filename
+                      and "ops/_lib.py" not in f.filename]
+                stacks[" <- ".join(f"{f.filename.split('igloo_amd/')[-1]}:{f.lineno}({f.name})"
+                                   for f in fr[-3:][::-1])] += 1
+            return orig(t)
+        _lib._to_host_ints = counted
+        fresh = params.stream(qs, 5000, a.sf)
+        for q in qs:
+            e.sql(fresh[q])
+        _lib._to_host_ints = orig
+        lines.append(f"\nreal readbacks of one fresh stream by call stack ({sum(stacks.values())}):")
+        lines += [f"  {v:4d}  {k}" for k, v in stacks.most_common(70)]
     lines.append("\nreadback sites (validation parameters), most frequent:")
     lines += [f"  {v:4d}  {k}" for k, v in sites_all.most_common(60)]
     lines.append("\nparameter-dependent sites:")
