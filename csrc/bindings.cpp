@@ -478,6 +478,15 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("mark_keys", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, int64_t kmin, int64_t dom,
+                        uintptr_t marks, uintptr_t s) {
+    kern::mark_keys(P<const void>(keys), key64, P<const uint8_t>(valid), n, kmin, dom, P<uint8_t>(marks), S(s));
+  });
+  m.def("probe_marks", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, int64_t base, int64_t dom,
+                          uintptr_t marks, bool negate, uintptr_t out, uintptr_t s) {
+    kern::probe_marks(P<const void>(keys), key64, P<const uint8_t>(valid), n, base, dom, P<const uint8_t>(marks),
+                      negate, P<uint8_t>(out), S(s));
+  });
   m.def("const_ints", [](uintptr_t out, std::vector<int64_t> vals, uintptr_t s) {
     kern::const_ints(P<int64_t>(out), vals.data(), (int64_t)vals.size(), S(s));
   });

@@ -296,6 +296,57 @@ void const_ints(int64_t* out, const int64_t* vals, int64_t n, hipStream_t stream
   check_launch("const_ints", stream);
 }
 
+// Dense key marks (range-sliced SEMI / ANTI joins, parallel/exchange.py):
+// marks[k - kmin] = 1 for every valid key k in [kmin, kmin + dom) -- one
+// pass over the keys, plain byte stores (racing stores all write 1).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void mark_keys_kernel(const T* __restrict__ k, const uint8_t* __restrict__ valid,
+                                                          int64_t n, int64_t kmin, int64_t dom,
+                                                          uint8_t* __restrict__ marks) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t d = (int64_t)k[i] - kmin;
+    if (d >= 0 && d < dom && (!valid || valid[i])) marks[d] = 1;
+  }
+}
+
+// out[i] = (key i has a mark in [base, base + dom)) != negate; a NULL or
+// out-of-domain key has none.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void probe_marks_kernel(const T* __restrict__ k, const uint8_t* __restrict__ valid,
+                                                            int64_t n, int64_t base, int64_t dom,
+                                                            const uint8_t* __restrict__ marks, bool negate,
+                                                            uint8_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t d = (int64_t)k[i] - base;
+    const bool hit = d >= 0 && d < dom && (!valid || valid[i]) && marks[d] != 0;
+    out[i] = hit != negate;
+  }
+}
+
+void mark_keys(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t dom,
+               uint8_t* marks, hipStream_t stream) {
+  if (n == 0) return;
+  const dim3 g(grid_for(n, kBlock, 65536)), b(kBlock);
+  if (key64)
+    hipLaunchKernelGGL(mark_keys_kernel<int64_t>, g, b, 0, stream, (const int64_t*)keys, valid, n, kmin, dom, marks);
+  else
+    hipLaunchKernelGGL(mark_keys_kernel<int32_t>, g, b, 0, stream, (const int32_t*)keys, valid, n, kmin, dom, marks);
+  check_launch("mark_keys", stream);
+}
+
+void probe_marks(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t base, int64_t dom,
+                 const uint8_t* marks, bool negate, uint8_t* out, hipStream_t stream) {
+  if (n == 0) return;
+  const dim3 g(grid_for(n, kBlock, 65536)), b(kBlock);
+  if (key64)
+    hipLaunchKernelGGL(probe_marks_kernel<int64_t>, g, b, 0, stream, (const int64_t*)keys, valid, n, base, dom, marks,
+                       negate, out);
+  else
+    hipLaunchKernelGGL(probe_marks_kernel<int32_t>, g, b, 0, stream, (const int32_t*)keys, valid, n, base, dom, marks,
+                       negate, out);
+  check_launch("probe_marks", stream);
+}
+
 // End a stream capture the runtime invalidated (the failed capture's graph
 // is discarded), so the thread can launch again.
 void end_capture(hipStream_t stream) {

@@ -796,25 +796,42 @@ def _semi_by_range_marks(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Ba
             return None
     dev = ctx.device
     dom = W * chunk
-    marks = torch.zeros(dom + 1, dtype=torch.uint8, device=dev)       # [dom]: out-of-domain / NULL keys
+    gpu = dev.type == "cuda"
+    marks = torch.zeros(dom + (0 if gpu else 1), dtype=torch.uint8, device=dev)
     if rb.num_rows:
-        rk = rcol.data.to(torch.int64) - kmin
-        ok = (rk >= 0) & (rk < dom)
-        if rcol.valid is not None:
-            ok = ok & rcol.valid
-        pos = torch.where(ok, rk, torch.full_like(rk, dom))
-        marks.index_fill_(0, pos, 1)
+        if gpu:
+            # one pass over the keys (ops/_lib: the mark_keys kernel), no temporaries
+            from ..ops._lib import launch, ptr, stream
+            rk = rcol.data if rcol.data.dtype in (torch.int32, torch.int64) else rcol.data.to(torch.int64)
+            rk = rk.contiguous()
+            launch("mark_keys").mark_keys(ptr(rk), rk.dtype == torch.int64, ptr(rcol.valid), rk.numel(), kmin, dom,
+                                          ptr(marks), stream(marks))
+        else:
+            rk = rcol.data.to(torch.int64) - kmin
+            ok = (rk >= 0) & (rk < dom)
+            if rcol.valid is not None:
+                ok = ok & rcol.valid
+            marks.index_fill_(0, torch.where(ok, rk, torch.full_like(rk, dom)), 1)   # [dom]: no mark
     mine = comm.reduce_scatter_tensor(marks[:dom].view(W, chunk), "max")
     n_l = lb.num_rows
-    if n_l:
-        lk = lcol.data.to(torch.int64) - (kmin + comm.rank * chunk)
+    base = kmin + comm.rank * chunk
+    if n_l and gpu:
+        from ..ops._lib import launch, ptr, stream
+        lk = lcol.data if lcol.data.dtype in (torch.int32, torch.int64) else lcol.data.to(torch.int64)
+        lk = lk.contiguous()
+        keepm = torch.empty(n_l, dtype=torch.bool, device=dev)
+        launch("probe_marks").probe_marks(ptr(lk), lk.dtype == torch.int64, ptr(lcol.valid), n_l, base, chunk,
+                                          ptr(mine.contiguous()), join.kind == "anti", ptr(keepm), stream(keepm))
+    elif n_l:
+        lk = lcol.data.to(torch.int64) - base
         inr = (lk >= 0) & (lk < chunk)
         if lcol.valid is not None:
             inr = inr & lcol.valid
         hit = (mine.index_select(0, lk.clamp(0, chunk - 1)) > 0) & inr
+        keepm = hit if join.kind == "semi" else ~hit
     else:
-        hit = torch.zeros(0, dtype=torch.bool, device=dev)
-    keep = mask_to_indices(hit if join.kind == "semi" else ~hit)
+        keepm = torch.zeros(0, dtype=torch.bool, device=dev)
+    keep = mask_to_indices(keepm)
     keys = list(lb.columns)
     return Batch(dict(zip(keys, _take_many([lb.columns[k] for k in keys], keep))), int(keep.numel()), d)
 
