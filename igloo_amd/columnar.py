@@ -275,6 +275,79 @@ def _decimal_to_int64(arr: pa.Array) -> np.ndarray:
     return out
 
 
+class LazyColumn(Column):
+    """Column ``cid`` of batch ``src`` taken at rows ``idx``, gathered only when
+    its values are first read. ``take`` composes a further row selection into
+    the index instead of gathering (ops/gather.py ``take_many``): TPC-H Q10's
+    ORDER BY revenue LIMIT 20 over 3.9M customer groups gathers the names,
+    addresses and comments of its 20 rows, not of 3.9M. Length and structure
+    (dictionary / plain string / 128-bit) come from the source column without
+    gathering. ``src`` may be a filtered lazy scan (``take_rows``)."""
+
+    __slots__ = ("_src", "_cid", "_idx", "_mat", "_proto")
+
+    def __init__(self, dtype: DataType, src, cid, idx: torch.Tensor):  # noqa: D401 - no Column.__init__
+        self.dtype = dtype
+        self._src, self._cid, self._idx, self._mat = src, cid, idx, None
+        base = getattr(src, "src", None) if hasattr(src, "take_rows") else None
+        self._proto = (base if base is not None else src).columns[cid]
+        self._host_dict = None
+        self._cache = None
+        self._sorted_dict = None
+        self._unified = None
+
+    def materialize(self) -> Column:
+        if self._mat is None:
+            if hasattr(self._src, "take_rows"):
+                self._mat = self._src.take_rows([self._cid], self._idx)[0]
+            else:
+                from .ops.gather import take
+                self._mat = take(self._src.columns[self._cid], self._idx)
+        return self._mat
+
+    def taken(self, idx: torch.Tensor) -> "LazyColumn":
+        """Still lazy: this column at its rows ``idx`` (no negatives)."""
+        from .ops.gather import gather_tensor
+        return LazyColumn(self.dtype, self._src, self._cid, gather_tensor(self._idx, idx))
+
+    @property
+    def pending(self) -> bool:
+        return self._mat is None
+
+    def __len__(self) -> int:
+        return self._idx.numel()
+
+    @property
+    def device(self) -> torch.device:
+        return self._idx.device
+
+    @property
+    def is_dict(self) -> bool:
+        return self._proto.is_dict
+
+    @property
+    def is_plain_string(self) -> bool:
+        return self._proto.is_plain_string
+
+    @property
+    def is_wide(self) -> bool:
+        return self._proto.is_wide
+
+    def _get(name):
+        def get(self):
+            return getattr(self.materialize(), name)
+
+        def put(self, v):
+            setattr(self.materialize(), name, v)
+        return property(get, put)
+
+    data = _get("data")
+    valid = _get("valid")
+    offsets = _get("offsets")
+    dictionary = _get("dictionary")
+    del _get
+
+
 def batch_device(b) -> Optional[torch.device]:
     """Device of a batch's columns without materialising any: lazy batches
     (join results in index form, filtered scans) report theirs from their

@@ -15,7 +15,7 @@ import pyarrow as pa
 import torch
 
 from .. import types as T
-from ..columnar import Batch, Column, batch_device
+from ..columnar import LazyColumn, Batch, Column, batch_device
 from ..ops import agg as A
 from ..ops import hashing as H
 from ..ops import misc as M
@@ -485,14 +485,17 @@ class HashAggExec(ExecNode):
         return aggregate(lg.groups, lg.aggs, b, ctx)
 
 
-def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None, fd: bool = False) -> Batch:
+def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None, fd: bool = False,
+              skip: Optional[set] = None) -> Batch:
     """GROUP BY ``groups`` computing ``aggs`` over ``b``. ``row_parts``
     ({output cid: part index} of a LateBatch ``b``): when the grouping runs
     on the join result's index form (``_late_group_keys``: every other key is
     functionally dependent on the leading integer key), each group's row in
     those parts is added as an int64 column -- the SPMD exchange ships that
     row instead of the part's string columns (parallel/exchange.py). The
-    columns are absent when the dependency did not hold. ``fd``: the keys are
+    columns are absent when the dependency did not hold; group keys in
+    ``skip`` (output cids the caller replaces by those rows) are then not
+    materialised at all. ``fd``: the keys are
     expected to depend on one integer key (the exchange's merge of such
     partial groups): ``_encode_groups`` tries that shortcut even without
     plain string keys."""
@@ -502,7 +505,7 @@ def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] =
     late = None
     if groups and n and isinstance(b, LateBatch) and (dev.type == "cuda" or row_parts):
         with ctx.span("agg.late_keys"):
-            late = _late_group_keys(groups, b, ctx)
+            late = _late_group_keys(groups, b, ctx, skip if row_parts else None)
     if late is not None:
         gid, ng, rep, taken = late
     else:
@@ -522,7 +525,8 @@ def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] =
     out: Dict[int, Column] = {}
     if groups:
         for (ci, _), c in zip(groups, taken):
-            out[ci.cid] = c
+            if c is not None:
+                out[ci.cid] = c
     if late is not None and row_parts:
         for cid, k in row_parts.items():
             idx = b.parts[k][1]
@@ -557,7 +561,7 @@ def _diff_bounds(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return buf[:2]
 
 
-def _late_group_keys(groups, b: "LateBatch", ctx):
+def _late_group_keys(groups, b: "LateBatch", ctx, skip: Optional[set] = None):
     """GROUP BY over a join result still in index form, with plain string keys
     (TPC-H Q10: c_custkey plus six customer/nation attributes over 11M joined
     rows). Group by the widest integer key, then check per join input that its
@@ -595,11 +599,18 @@ def _late_group_keys(groups, b: "LateBatch", ctx):
     ctx.sorted_gids = srt
     taken = []
     for i, c in enumerate(cids):
-        if i == lead:
+        if skip and groups[i][0].cid in skip:
+            taken.append(None)          # the caller ships this part's row instead
+        elif i == lead:
             taken.append(take(b.gather(c), rep))
         else:
             bb, idx = b.parts[b.owner[c]]
-            taken.append(take(bb.columns[c], gather_tensor(idx, rep)))
+            if i in plain:
+                # strings are gathered when read: an ORDER BY ... LIMIT above
+                # takes only its rows (columnar.py LazyColumn)
+                taken.append(LazyColumn(base[i].dtype, bb, c, gather_tensor(idx, rep)))
+            else:
+                taken.append(take(bb.columns[c], gather_tensor(idx, rep)))
     return gid, ng, rep, taken
 
 

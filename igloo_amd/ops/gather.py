@@ -66,6 +66,13 @@ def _src_ptr(t) -> int:
 def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> List[Column]:
     """Gather rows ``idx`` of every column. ``neg=True``: idx may hold -1 (NULL row)."""
     assert idx.dim() == 1 and idx.dtype in (torch.int32, torch.int64)
+    from ..columnar import LazyColumn
+    if not neg and any(isinstance(c, LazyColumn) and c.pending for c in cols):
+        # deferred columns stay deferred: only their row index is composed
+        lazy = {i: c.taken(idx) for i, c in enumerate(cols) if isinstance(c, LazyColumn) and c.pending}
+        rest = [c for i, c in enumerate(cols) if i not in lazy]
+        done = iter(take_many(rest, idx, neg) if rest else [])
+        return [lazy[i] if i in lazy else next(done) for i in range(len(cols))]
     n = idx.numel()
     gpu = is_gpu(idx)
     out: List[Column] = []

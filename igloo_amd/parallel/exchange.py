@@ -975,30 +975,32 @@ def _partial_by_rows(groups, partial, b: Batch, ids, ctx):
     if not rows or len(rows) == len(groups):
         return aggregate(groups, partial, b, ctx), groups, None
     row_ci = {k: L.ColInfo(ids(), "__row", T.INT64, False) for k in sorted(set(rows.values()))}
-    pb = aggregate(groups, partial, b, ctx, row_parts={ci.cid: k for k, ci in row_ci.items()})
+    replaced = {groups[i][0].cid for i in rows}
+    pb = aggregate(groups, partial, b, ctx, row_parts={ci.cid: k for k, ci in row_ci.items()}, skip=replaced)
     have = all(ci.cid in pb.columns for ci in row_ci.values())
     ok = all(r[0] for r in ctx.comm.allgather_ints([int(have)]))
     log.debug("partial aggregate ships row numbers for %d string key(s): local %s, agreed %s",
               len(rows), have, ok)
     if not ok:
         if have:
-            pb = Batch({c: v for c, v in pb.columns.items() if c not in {ci.cid for ci in row_ci.values()}},
-                       pb.num_rows, pb.dist)
+            # another rank's grouping did not take the row-number shape: this
+            # rank groups again with every key materialised
+            pb = aggregate(groups, partial, b, ctx)
         return pb, groups, None
-    replaced = {groups[i][0].cid for i in rows}
     pb = Batch({c: v for c, v in pb.columns.items() if c not in replaced}, pb.num_rows, pb.dist)
     ex_groups = [g for i, g in enumerate(groups) if i not in rows] + \
         [(ci, ColRef(ci.cid, ci.name, ci.dtype, False)) for ci in row_ci.values()]
     parts = {k: b.parts[k][0] for k in row_ci}
 
     def restore(res: Batch) -> Batch:
-        from ..ops.gather import take
+        # the strings stay in the replicated input until read (columnar.py
+        # LazyColumn): a top-k above takes only its rows
+        from ..columnar import LazyColumn
         cols = {c: v for c, v in res.columns.items() if c not in {ci.cid for ci in row_ci.values()}}
         for i, k in rows.items():
             ci, e = groups[i]
             r = res.columns[row_ci[k].cid].data
-            bb = parts[k]
-            cols[ci.cid] = bb.take_rows([e.cid], r)[0] if hasattr(bb, "take_rows") else take(bb.columns[e.cid], r)
+            cols[ci.cid] = LazyColumn(ci.dtype, parts[k], e.cid, r)
         return Batch(cols, res.num_rows, res.dist)
     return pb, ex_groups, restore
 
