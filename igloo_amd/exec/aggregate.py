@@ -441,6 +441,21 @@ class HashAggExec(ExecNode):
             out = self._sorted_having(ctx)
             if out is not None:
                 return out
+        # the same aggregate subtree twice in one query (TPC-H Q15's revenue
+        # view, read by the outer query and by its max() subquery) runs once
+        key = _subtree_key(lg) if not self.runtime_filters and ctx.morsel is None and ctx.memo is None \
+            and ctx.budget is None else None
+        if key is not None:
+            hit = ctx.subplans.get(key)
+            if hit is not None:
+                return _rekeyed(hit, lg)
+        out = self._run_agg(ctx, child)
+        if key is not None:
+            ctx.subplans[key] = (out, [c.cid for c in lg.schema])
+        return out
+
+    def _run_agg(self, ctx, child):
+        lg = self.logical
         if ctx.budget is not None:
             from .morsel import streamed_aggregate
             out = streamed_aggregate(self, ctx)
@@ -483,6 +498,35 @@ class HashAggExec(ExecNode):
             from ..parallel.exchange import distributed_aggregate
             return distributed_aggregate(lg, b, ctx, local=local)
         return aggregate(lg.groups, lg.aggs, b, ctx)
+
+
+_CIDNUM = re.compile(r"#(\d+)")
+
+
+def _subtree_key(plan) -> Optional[str]:
+    """Text of a logical subtree with its column ids renumbered in order of
+    appearance: two subtrees with equal keys compute the same rows (same
+    tables, filters, expressions). None for subtrees holding a subquery
+    (its plan is not part of the text)."""
+    txt = plan.explain()
+    if "subquery" in txt:
+        return None
+    seen: Dict[str, int] = {}
+
+    def ren(m):
+        return "#" + str(seen.setdefault(m.group(1), len(seen)))
+    return _CIDNUM.sub(ren, txt)
+
+
+def _rekeyed(hit, lg) -> Batch:
+    """A cached aggregate result under this subtree's output column ids."""
+    out, cids = hit
+    mine = [c.cid for c in lg.schema]
+    m = dict(zip(cids, mine))
+    d = out.dist
+    if isinstance(d, tuple) and len(d) > 1:          # key placements name output columns
+        d = (d[0],) + tuple(m.get(c, c) for c in d[1:])
+    return Batch({m[c]: out.columns[c] for c in cids}, out.num_rows, d)
 
 
 def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] = None, fd: bool = False,

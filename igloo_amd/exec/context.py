@@ -91,6 +91,8 @@ class ExecContext:
         # device error flags checked once when the query's result is ready
         # (generated kernels' decimal-overflow flags: no mid-query sync)
         self.deferred_checks: list = []
+        # aggregate subtrees computed once per query (exec/aggregate.py _subtree_key)
+        self.subplans: Dict[str, tuple] = {}
         # SPMD: {id(source): key column} of the replicated table this query
         # splits by key range (parallel/slicing.py plan_slices)
         self.slices: Dict[int, str] = {}

@@ -128,6 +128,10 @@ SETS
       timeout -k 10 300 python -u scripts/gather_bench.py --out gpurun_out/gather_bench.txt \
         > gpurun_out/gather_bench.log 2>&1
       rc=$?; echo "gbench rc=$rc"; tail -20 gpurun_out/gather_bench.txt ;;
+    atsites)
+      # ATen kernels of the warm suite by igloo call site (torch.profiler)
+      timeout -k 10 600 python -u scripts/aten_sites.py --sf ${SF:-100} --top 45 > gpurun_out/aten_sites.txt 2>&1
+      rc=$?; echo "atsites rc=$rc"; head -30 gpurun_out/aten_sites.txt ;;
     rbsites)
       # blocking readbacks per query and how many are parameter-independent
       timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 --stacks \
