@@ -4,6 +4,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_R
 rc=$?; echo "run rc=$rc"; tail -25 gpurun_out/spmd_overhead_run.log
 [ $rc -eq 0 ] || exit $rc
 T=$(find gpurun_out/spo -name "*kernel_trace.csv" | head -1)
-python3 scripts/spmd_overhead.py --parse "$T" --queries ${QS:-1-22} --sf ${SF:-10} --top ${TOP:-12} > gpurun_out/spmd_overhead.txt 2>&1
+python3 scripts/spmd_overhead.py --parse "$T" --queries ${QS:-1-22} --sf ${SF:-10} --top ${TOP:-12} --seq ${SEQ:-0} > gpurun_out/spmd_overhead.txt 2>&1
 rm -rf gpurun_out/spo
 head -60 gpurun_out/spmd_overhead.txt

@@ -157,6 +157,15 @@ def _report(a, table):
         extra = sorted(((cp[n] - cs.get(n, 0), n) for n in cp if cp[n] > cs.get(n, 0)), reverse=True)[:a.top]
         for d, n in extra:
             print(f"      +{d:3d} x {n:70s} ({tp[n]:.3f} ms in spmd)")
+        if a.seq:
+            # the long kernels of both executions in launch order, side by side
+            ls = [(short(n), (e - b) / 1e3) for b, e, n in s if e - b >= a.seq * 1e3]
+            lp = [(short(n), (e - b) / 1e3) for b, e, n in p if e - b >= a.seq * 1e3]
+            print(f"      kernels >= {a.seq:.0f} us (single | spmd):")
+            for i in range(max(len(ls), len(lp))):
+                x = f"{ls[i][0][:44]:44s} {ls[i][1]:7.1f}" if i < len(ls) else " " * 52
+                y = f"{lp[i][0][:44]:44s} {lp[i][1]:7.1f}" if i < len(lp) else ""
+                print(f"        {x} | {y}")
         tot["single_busy"] += bs
         tot["spmd_busy"] += bp
         tot["single_span"] += span_s
@@ -171,6 +180,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--parse", default=None)
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--seq", type=float, default=0.0, help="also list kernels longer than this many us, in order")
     ap.add_argument("--windows", default="gpurun_out/spmd_overhead_windows.json",
                     help="host monotonic-clock window of every timed execution (written by the run)")
     a = ap.parse_args()
