@@ -355,9 +355,10 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = F
     """Hash-repartition rows of ``b`` by ``key`` across all ranks.
 
     Collectives: the structure all-gather (skipped when the caller already
-    ``normalized`` the batch), one all-to-all of the [rank x (rows, string
-    bytes...)] count matrix (skipped when ``plan`` carries it: the caller
-    shipped it in its structure all-gather), and ONE all-to-all-v of bytes:
+    ``normalized`` the batch; otherwise it also carries every rank's count
+    matrix row), one all-to-all of the [rank x (rows, string bytes...)] count
+    matrix only when neither did (or a string column changed representation
+    in the normalisation), and ONE all-to-all-v of bytes:
     per destination the packed fixed-width rows (gathered into destination
     order by the pack kernel itself) followed by every plain-string column's
     bytes."""
@@ -365,7 +366,12 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = F
     comm = ctx.comm
     W = comm.world_size
     if not normalized:
-        b = normalize_structure(materialized(b), comm)
+        # the count matrix rides in the structure all-gather's preamble
+        b = materialized(b)
+        plan = ShufflePlan(b, key, W)
+        b = normalize_structure(b, comm, plan.preamble())
+        if not plan.receive(b.preamble, comm.rank, b):
+            plan = None
     if plan is None or plan.rmat is None:
         plan = ShufflePlan(b, key, W)
         plan.rmat = comm.all_to_all_matrix(plan.matrix())

@@ -36,6 +36,7 @@ def main():
             e.sql(queries.QUERIES[q])
     jit.wait_all(timeout=120)
     rows = {q: [0.0, 0.0, 0, 0.0] for q in qs}    # wall ms, dev span ms, host steps, plan ms
+    per_stream = {q: [] for q in qs}                # (wall ms, readbacks) per stream
     t_streams = []
     for k in range(a.streams):
         st = params.stream(qs, 2000 + k, a.sf)
@@ -48,6 +49,7 @@ def main():
             r[0] += m["elapsed_ms"]
             r[1] += m.get("device_span_ms", 0.0)
             r[2] += m.get("host_steps", 0)
+            per_stream[q].append((m["elapsed_ms"], m.get("readbacks", 0)))
         torch.cuda.synchronize()
         t_streams.append(time.perf_counter() - t0)
     # planning alone (parse + bind + optimize) of a fresh stream
@@ -69,6 +71,10 @@ def main():
         tot[2] += p
         s.write(f"{'Q%d' % q:>6} {w:9.2f} {d:10.2f} {w - d:9.2f} {p:8.2f} {h:10.1f}\n")
     s.write(f"{'total':>6} {tot[0]:9.2f} {tot[1]:10.2f} {tot[0] - tot[1]:9.2f} {tot[2]:8.2f}\n\n")
+    s.write("per stream (wall ms / blocking readbacks):\n")
+    for q in qs:
+        s.write(f"{'Q%d' % q:>6} " + "  ".join(f"{w:8.2f}/{rb:3d}" for w, rb in per_stream[q]) + "\n")
+    s.write("\n")
     pr = cProfile.Profile()
     st = params.stream(qs, 3000, a.sf)
     pr.enable()

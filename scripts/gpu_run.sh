@@ -132,6 +132,12 @@ SETS
       # ATen kernels of the warm suite by igloo call site (torch.profiler)
       timeout -k 10 600 python -u scripts/aten_sites.py --sf ${SF:-100} --top 45 > gpurun_out/aten_sites.txt 2>&1
       rc=$?; echo "atsites rc=$rc"; head -30 gpurun_out/aten_sites.txt ;;
+    adhoc)
+      # ad-hoc statements (fresh TPC-H parameters): per query wall vs device
+      # span per stream, then one stream under cProfile
+      timeout -k 10 600 python -u scripts/adhoc_profile.py --sf ${SF:-100} --streams 3 \
+        --out gpurun_out/adhoc_profile.txt > gpurun_out/adhoc_profile.log 2>&1
+      rc=$?; echo "adhoc rc=$rc"; head -60 gpurun_out/adhoc_profile.txt ;;
     rbsites)
       # blocking readbacks per query and how many are parameter-independent
       timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 --stacks \
