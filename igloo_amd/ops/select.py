@@ -28,28 +28,33 @@ def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def exclusive_scan(counts: torch.Tensor) -> Tuple[torch.Tensor, int]:
-    """int32/int64 counts -> (int64 exclusive offsets, total)."""
+def exclusive_scan(counts: torch.Tensor, host_total: bool = True):
+    """int32/int64 counts -> (int64 exclusive offsets, total). ``host_total``
+    False: the total stays a 1-element device tensor (no readback)."""
     assert counts.dim() == 1 and counts.dtype in (torch.int32, torch.int64)
     n = counts.numel()
     if not is_gpu(counts):
         c = counts.to(torch.int64)
         inc = torch.cumsum(c, 0)
         total = int(inc[-1].item()) if n else 0
-        return inc - c, total
+        return inc - c, (total if host_total else torch.tensor([total], dtype=torch.int64))
     counts = counts.contiguous()
     N = launch("exclusive_scan")
     tiles = N.scan_workspace_tiles(n)
     ws = torch.empty(tiles + 1, dtype=torch.int64, device=counts.device)
     out = torch.empty(n, dtype=torch.int64, device=counts.device)
     N.exclusive_scan(ptr(counts), counts.dtype == torch.int64, n, ptr(out), ptr(ws), ptr(ws) + 8 * tiles, stream(counts))
-    return out, to_host_int(ws[tiles:])
+    return out, (to_host_int(ws[tiles:]) if host_total else ws[tiles:])
 
 
-def offsets_from_lengths(lengths: torch.Tensor) -> Tuple[torch.Tensor, int]:
-    """Arrow offsets [n+1] from per-row lengths."""
-    ex, total = exclusive_scan(lengths)
+def offsets_from_lengths(lengths: torch.Tensor, host_total: bool = True):
+    """Arrow offsets [n+1] from per-row lengths (``host_total`` False: no
+    readback; the total comes back as a device tensor)."""
+    ex, total = exclusive_scan(lengths, host_total)
     off = torch.empty(lengths.numel() + 1, dtype=torch.int64, device=lengths.device)
     off[:-1] = ex
-    off[-1:].fill_(total)     # a device fill (item assignment would upload a host scalar)
+    if host_total:
+        off[-1:].fill_(total)     # a device fill (item assignment would upload a host scalar)
+    else:
+        off[-1:].copy_(total.reshape(1))
     return off, total

@@ -265,7 +265,7 @@ def _rebuild(cols: List[Column], spec, parts: List[torch.Tensor], chars: Dict[in
             lens = parts[di]
             if lens.numel():
                 from ..ops.select import offsets_from_lengths
-                off, _ = offsets_from_lengths(lens)
+                off, _ = offsets_from_lengths(lens, host_total=False)
             else:
                 off = torch.zeros(1, dtype=torch.int64, device=lens.device)
             out.append(Column(c.dtype, chars[j], valid, offsets=off))
@@ -604,7 +604,8 @@ def gather_small(b: Batch, ctx, cap_rows: int) -> Batch:
             base = H + cap_rows * rb + sc * cap_s
             data = torch.cat([allb[r, base:base + hd[r][2 + len(keys) + sc]] for r in range(W)])
             sc += 1
-            off = offsets_from_lengths(lens)[0] if total else torch.zeros(1, dtype=torch.int64, device=dev)
+            off = offsets_from_lengths(lens, host_total=False)[0] if total else \
+                torch.zeros(1, dtype=torch.int64, device=dev)
             out[k] = Column(c0.dtype, data, valid, offsets=off)
             continue
         data = parts[t]
