@@ -58,12 +58,42 @@ __global__ __launch_bounds__(kBlock) void tile_scan_kernel(const T* __restrict__
   }
 }
 
+// Inputs of at most kSmall values (the common case: per-group counts, the
+// string lengths of a top-k, small joins): the whole scan in ONE workgroup,
+// one launch instead of three. Each lane owns kSmallItems consecutive values.
+constexpr int kSmallItems = 32;
+constexpr int64_t kSmall = (int64_t)kBlock * kSmallItems;
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void small_scan_kernel(const T* __restrict__ in, int64_t n,
+                                                           int64_t* __restrict__ out, int64_t* __restrict__ total) {
+  __shared__ int64_t scratch[kWavesPerBlock + 1];
+  const int64_t base = (int64_t)threadIdx.x * kSmallItems;
+  int64_t s = 0;
+  for (int j = 0; j < kSmallItems; ++j)
+    if (base + j < n) s += (int64_t)in[base + j];
+  int64_t tot;
+  int64_t run = block_exclusive_scan(s, scratch, &tot);
+  for (int j = 0; j < kSmallItems; ++j)
+    if (base + j < n) {
+      const int64_t v = (int64_t)in[base + j];
+      out[base + j] = run;
+      run += v;
+    }
+  if (threadIdx.x == 0 && total) *total = tot;
+}
+
 template <typename T>
 void exclusive_scan_impl(const T* in, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
                          hipStream_t stream) {
   int64_t tiles = (n + kTile - 1) / kTile;
   if (tiles == 0) {
     IGLOO_HIP_CHECK(hipMemsetAsync(total, 0, sizeof(int64_t), stream));
+    return;
+  }
+  if (n <= kSmall) {
+    hipLaunchKernelGGL(small_scan_kernel<T>, dim3(1), dim3(kBlock), 0, stream, in, n, out, total);
+    check_launch("scan.small", stream);
     return;
   }
   hipLaunchKernelGGL(tile_sum_kernel<T>, dim3((unsigned)tiles), dim3(kBlock), 0, stream, in, n, tile_ws);

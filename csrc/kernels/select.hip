@@ -70,6 +70,29 @@ __global__ __launch_bounds__(kBlock) void tile_count_kernel(const uint8_t* __res
   }
 }
 
+// Masks of at most kSmallTiles tiles: ONE workgroup counts every tile in turn
+// and writes the tiles' exclusive offsets and the total directly (one launch
+// instead of tile counts + a scan of them).
+constexpr int kSmallTiles = 8;
+
+__global__ __launch_bounds__(kBlock) void small_count_kernel(const uint8_t* __restrict__ mask, int64_t n, int tiles,
+                                                            int64_t* __restrict__ offsets, int64_t* __restrict__ total) {
+  __shared__ int64_t red[kWavesPerBlock];
+  int64_t run = 0;
+  for (int t = 0; t < tiles; ++t) {
+    const int64_t base = (int64_t)t * kTile + (int64_t)threadIdx.x * kItems;
+    int64_t c = wave_reduce_sum((int64_t)count_flags(mask, base, n));
+    if (lane_id() == 0) red[threadIdx.x / kWave] = c;
+    __syncthreads();
+    int64_t tile_total = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) tile_total += red[w];
+    if (threadIdx.x == 0) offsets[t] = run;
+    run += tile_total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = run;
+}
+
 }  // namespace
 
 // Exclusive scan of `n` int64 counts in place with one workgroup of 1024
@@ -148,6 +171,11 @@ void select_count(const uint8_t* mask, int64_t n, int64_t* tile_counts, int64_t*
   int64_t tiles = select_num_tiles(n);
   if (tiles == 0) {
     IGLOO_HIP_CHECK(hipMemsetAsync(total, 0, sizeof(int64_t), stream));
+    return;
+  }
+  if (tiles <= kSmallTiles) {
+    hipLaunchKernelGGL(small_count_kernel, dim3(1), dim3(kBlock), 0, stream, mask, n, (int)tiles, tile_counts, total);
+    check_launch("select.small_count", stream);
     return;
   }
   hipLaunchKernelGGL(tile_count_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, stream, mask, n,

@@ -23,7 +23,7 @@ def _rng(seed=0):
     return np.random.default_rng(seed)
 
 
-@pytest.mark.parametrize("n", [0, 1, 17, 4096, 4097, 1_000_003])
+@pytest.mark.parametrize("n", [0, 1, 17, 4096, 4097, 8192, 8193, 65536, 65537, 1_000_003])
 def test_select(gpu_device, n):
     m = torch.from_numpy(_rng(n).random(n) < 0.3)
     ref = mask_to_indices(m)
@@ -31,12 +31,16 @@ def test_select(gpu_device, n):
     assert got.dtype == ref.dtype and torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("n,dt", [(0, torch.int32), (5, torch.int32), (100_001, torch.int64), (3_000_000, torch.int32)])
+@pytest.mark.parametrize("n,dt", [(0, torch.int32), (5, torch.int32), (8191, torch.int64), (8192, torch.int32),
+                                  (8193, torch.int32), (100_001, torch.int64), (3_000_000, torch.int32)])
 def test_exclusive_scan(gpu_device, n, dt):
     c = torch.from_numpy(_rng(1).integers(0, 9, n)).to(dt)
     ref, rt = exclusive_scan(c)
     got, gt = exclusive_scan(c.to(DEV))
     assert rt == gt and torch.equal(got.cpu(), ref)
+    if n:
+        got2, dt_ = exclusive_scan(c.to(DEV), host_total=False)     # the total left on the device
+        assert int(dt_.item()) == rt and torch.equal(got2.cpu(), ref)
 
 
 def test_take_many_fixed_strings_nulls(gpu_device):
