@@ -1311,8 +1311,20 @@ class MultiJoinExec(ExecNode):
                     kind = "derived" if info[2] else "cached"
                 elif not info[2]:
                     kind = "sketch_base"
+                elif ctx.device.type == "cuda" and isinstance(rel["batch"], _LazyScanBatch) \
+                        and e.cid in rel["batch"].src.columns:
+                    # a filtered scan: sketch the table's column once (kept
+                    # like an unfiltered one) and derive the filtered NDV from
+                    # it -- later executions sketch nothing (Q21's 379M-row
+                    # lineitem keys were re-sketched every replay)
+                    kind = "sketch_base_filtered"
             plan.append((kind, key, ri))
         sk = [j for j, (kind, _, _) in enumerate(plan) if kind.startswith("sketch")]
+        base_rows = {}      # need index -> position of its base table's local rows in ``local``
+        for j, (kind, _, _) in enumerate(plan):
+            if kind == "sketch_base_filtered":
+                base_rows[j] = len(local)
+                local.append(need[j][0]["batch"].src.num_rows)
         if ctx.device.type != "cuda":
             nd = []
             for j in sk:
@@ -1328,7 +1340,11 @@ class MultiJoinExec(ExecNode):
             for j in sk:
                 rel, e = need[j]
                 b = rel["batch"]
-                if b.num_rows:
+                if plan[j][0] == "sketch_base_filtered":
+                    c = b.src.columns[e.cid]
+                    regs.append(H.hll_sketch(group_key_tensor(c)[0]) if len(c) else
+                                torch.zeros(H.HLL_M, dtype=torch.uint8, device=ctx.device))
+                elif b.num_rows:
                     k, _ = group_key_tensor(ctx.evaluator.column(e, b))
                     regs.append(H.hll_sketch(k))
                 else:
@@ -1352,6 +1368,11 @@ class MultiJoinExec(ExecNode):
                 est[j] = int(round(H.hll_from_terms(float(z), int(zeros))))
         counts = [b.num_rows if _replicated(b) else n for b, n in zip(batches, g)]
         for j, ((rel, e), (kind, key, ri)) in enumerate(zip(need, plan)):
+            if kind == "sketch_base_filtered":
+                if len(cache) > 4096:
+                    cache.clear()
+                cache[key] = (max(est[j], 1), g[base_rows[j]])
+                kind = "derived"
             if kind == "cached":
                 v = cache[key][0]
             elif kind == "derived":
