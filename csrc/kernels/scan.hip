@@ -69,17 +69,20 @@ __global__ __launch_bounds__(kBlock) void small_scan_kernel(const T* __restrict_
                                                            int64_t* __restrict__ out, int64_t* __restrict__ total) {
   __shared__ int64_t scratch[kWavesPerBlock + 1];
   const int64_t base = (int64_t)threadIdx.x * kSmallItems;
+  // every load issued before any is used: one memory latency, not 32
+  int64_t v[kSmallItems];
+#pragma unroll
+  for (int j = 0; j < kSmallItems; ++j) v[j] = base + j < n ? (int64_t)in[base + j] : 0;
   int64_t s = 0;
-  for (int j = 0; j < kSmallItems; ++j)
-    if (base + j < n) s += (int64_t)in[base + j];
+#pragma unroll
+  for (int j = 0; j < kSmallItems; ++j) s += v[j];
   int64_t tot;
   int64_t run = block_exclusive_scan(s, scratch, &tot);
-  for (int j = 0; j < kSmallItems; ++j)
-    if (base + j < n) {
-      const int64_t v = (int64_t)in[base + j];
-      out[base + j] = run;
-      run += v;
-    }
+#pragma unroll
+  for (int j = 0; j < kSmallItems; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += v[j];
+  }
   if (threadIdx.x == 0 && total) *total = tot;
 }
 
