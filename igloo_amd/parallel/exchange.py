@@ -810,6 +810,13 @@ def _semi_by_range_marks(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Ba
             # one pass over the keys (ops/_lib: the mark_keys kernel), no temporaries
             from ..ops._lib import launch, ptr, stream
             rk = rcol.data if rcol.data.dtype in (torch.int32, torch.int64) else rcol.data.to(torch.int64)
+            if rcol.valid is None and getattr(rk, "_igloo_resident", False) and rk.numel() >= (1 << 20):
+                # a resident key column: its sorted secondary index (built once,
+                # kept with the column) makes the mark stores ascending --
+                # coalesced, instead of one random byte store per row (Q22:
+                # 150M o_custkey into a 15 MB mark array, 2.6 -> ~0.2 ms)
+                from ..ops import hashing as H
+                rk = H.perm_index(rk)[0]
             rk = rk.contiguous()
             launch("mark_keys").mark_keys(ptr(rk), rk.dtype == torch.int64, ptr(rcol.valid), rk.numel(), kmin, dom,
                                           ptr(marks), stream(marks))

@@ -81,6 +81,18 @@ SETS
         python3 scripts/kernel_summary.py "$T" --steps 3 --top 25 ${KD:+--dispatches "$KD"} > gpurun_out/profq_${q}_summary.txt
         rm -rf gpurun_out/profq_$q; head -8 gpurun_out/profq_${q}_summary.txt
       done ;;
+    profspmd)
+      # per-query kernel summaries of the SPMD path on one GPU (bench.py with
+      # IGLOO_FORCE_SPMD=1: every collective real), one rocprofv3 run per set
+      for q in ${QS:-20 22}; do
+        IGLOO_FORCE_SPMD=1 IGLOO_PROF_GAP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$R/gpurun_out/profspmd_$q" -o run -- python3 "$R/bench.py" --source hbm --queries $q --steps 3 \
+          --warmup 5 --eager-steps 0 --vary-params 0 > gpurun_out/profspmd_$q.log 2>&1
+        rc=$?; echo "profspmd $q rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        T=$(find gpurun_out/profspmd_$q -name "*kernel_trace.csv" | head -1)
+        python3 scripts/kernel_summary.py "$T" --steps 3 --top 25 > gpurun_out/profspmd_${q}_summary.txt
+        rm -rf gpurun_out/profspmd_$q; head -8 gpurun_out/profspmd_${q}_summary.txt
+      done ;;
     jitcache)
       # compile the suite's query-specialised kernels at the benchmark scale
       # into gpurun_out/jit_cache (copied into igloo_amd/_jit_cache/ afterwards)
