@@ -257,18 +257,18 @@ def main():
         for k, st_sql in enumerate(streams):
             ts = time.perf_counter()
             nrb = 0
-            per_q = []
+            qtimes = []
             for q in qs:
                 tq = time.perf_counter()
                 eng.sql(st_sql[q])
-                per_q.append(f"Q{q}={(time.perf_counter() - tq) * 1e3:.1f}")
+                qtimes.append(f"Q{q}={(time.perf_counter() - tq) * 1e3:.1f}")
                 nrb += eng.last_metrics.get("readbacks", 0)
                 m = eng.last_metrics.get("speculation")
                 adhoc_modes[m] = adhoc_modes.get(m, 0) + 1
             barrier()
             adhoc_streams.append(time.perf_counter() - ts)
             adhoc_readbacks.append(nrb)
-            log(f"[bench] ad-hoc stream {k} per query (ms): {' '.join(per_q)}")
+            log(f"[bench] ad-hoc stream {k} per query (ms): {' '.join(qtimes)}")
         barrier()
         adhoc_s = (time.perf_counter() - ta) / a.vary_params
         if comm is not None:
