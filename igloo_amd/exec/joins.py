@@ -479,6 +479,49 @@ def grace_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fa
     return concat_batches([_to_device(o, dev) for o in outs])
 
 
+#: [NOT] EXISTS against a resident key column of at least this many rows,
+#: with a probe side at most 1/SEMI_MARKS_RATIO of it, runs as key marks
+SEMI_MARKS_MIN_ROWS = 1 << 22
+SEMI_MARKS_RATIO = 8
+SEMI_MARKS_MAX_DOMAIN = 1 << 28
+
+
+def _semi_by_index_marks(lb: Batch, lk, lvalid, rk, rvalid, kind: str, ctx) -> Optional[Batch]:
+    """SEMI / ANTI join against a big RESIDENT key column (TPC-H Q22: ~2M
+    customers NOT EXISTS among 150M o_custkey) as dense key marks: the
+    column's sorted secondary index (built once, kept with the column) marks
+    the keys present in a byte array over the column's key range with
+    ascending, coalesced stores, and each probe row reads its mark -- instead
+    of probing a hash table of the small side with every one of the big
+    side's rows (1.4 ms -> ~0.2 ms at SF100). None when it does not apply."""
+    if rvalid is not None or not getattr(rk, "_igloo_resident", False) or rk.numel() < SEMI_MARKS_MIN_ROWS \
+            or rk.dtype not in (torch.int32, torch.int64) or lk.dtype not in (torch.int32, torch.int64) \
+            or SEMI_MARKS_RATIO * lk.numel() > rk.numel():
+        return None
+    rng = H.key_range(rk)              # remembered on the resident column
+    if rng is None:
+        return None
+    lo, hi = rng
+    dom = hi - lo + 1
+    if dom > SEMI_MARKS_MAX_DOMAIN:
+        return None
+    srt = rk if H.is_sorted(rk) else H.perm_index(rk)[0]
+    with ctx.span("join.semi_marks"):
+        marks = torch.zeros(dom, dtype=torch.uint8, device=rk.device)
+        st = stream(marks)
+        launch("mark_keys").mark_keys(ptr(srt.contiguous()), srt.dtype == torch.int64, 0, srt.numel(), lo, dom,
+                                      ptr(marks), st)
+        n_l = lk.numel()
+        keepm = torch.empty(n_l, dtype=torch.bool, device=rk.device)
+        lkc = lk.contiguous()
+        launch("probe_marks").probe_marks(ptr(lkc), lkc.dtype == torch.int64, ptr(lvalid), n_l, lo, dom, ptr(marks),
+                                          kind == "anti", ptr(keepm), st)
+        keep = mask_to_indices(keepm)
+    out = _take_batch(lb, keep)
+    out.dist = lb.dist
+    return out
+
+
 def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=False) -> Batch:
     if ctx.budget is not None:
         g = grace_join(lb, rb, kind, on, residual, ctx, null_aware)
@@ -507,6 +550,11 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             lk = gather_tensor(lk, keep)
             lvalid = None
             n_l = lb.num_rows
+    if dev.type == "cuda" and len(on) == 1 and kind in ("semi", "anti") and residual is None and not null_aware \
+            and not ctx.spmd:
+        out = _semi_by_index_marks(lb, lk, lvalid, rk, rvalid, kind, ctx)
+        if out is not None:
+            return out
     if dev.type == "cuda" and len(on) == 1 and kind in ("inner", "semi", "anti", "left") and not null_aware:
         out = _sorted_join(lb, rb, lk, rk, lvalid, rvalid, kind, residual, ctx)
         if out is not None:

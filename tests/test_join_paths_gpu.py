@@ -39,6 +39,8 @@ QUERIES = [
     "SELECT sk FROM small WHERE EXISTS (SELECT 1 FROM big WHERE bk = sk AND bs < ss)",
     "SELECT sk FROM small WHERE NOT EXISTS (SELECT 1 FROM big WHERE bk = sk AND ss >= bs)",
     "SELECT sn, count(bv) AS c FROM small LEFT JOIN big ON sn = bk GROUP BY sn",
+    "SELECT sn FROM small WHERE EXISTS (SELECT 1 FROM big WHERE bk = sn)",
+    "SELECT sn FROM small WHERE NOT EXISTS (SELECT 1 FROM big WHERE bk = sn)",
     "SELECT sk, count(*) AS c FROM small JOIN big ON sk = bk GROUP BY sk",
 ]
 
@@ -54,6 +56,7 @@ def test_join_paths_match_cpu(gpu_device, monkeypatch, sorted_big, perm, qi):
     (sorted permutation) index instead of a hash probe."""
     monkeypatch.setattr(J, "PERM_INDEX", perm)
     monkeypatch.setattr(J, "PERM_INDEX_MAX_FRAC", 1)
+    monkeypatch.setattr(J, "SEMI_MARKS_MIN_ROWS", 1000 if perm else 1 << 22)   # [NOT] EXISTS as index key marks
     monkeypatch.setattr(J, "SORTED_JOIN_MIN_ROWS", 1000)
     monkeypatch.setattr(H, "SORTED_CHECK_ROWS", 1000)
     monkeypatch.setattr(H, "BLOOM_MIN_RATIO", 2)
