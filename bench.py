@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="run on CPU (debug)")
     ap.add_argument("--eager-steps", type=int, default=2,
                     help="suites timed with query graphs off (warm_eager_s), after the headline steps")
+    ap.add_argument("--profile-adhoc", type=float, default=0.0, metavar="MS",
+                    help="diagnostics: cProfile every ad-hoc statement, print those slower than MS")
     ap.add_argument("--param-seed", type=int, default=1000,
                     help="seed of the first ad-hoc parameter stream (stream k uses seed + k)")
     ap.add_argument("--vary-params", type=int, default=2, metavar="STREAMS",
@@ -260,7 +262,22 @@ def main():
             qtimes = []
             for q in qs:
                 tq = time.perf_counter()
-                eng.sql(st_sql[q])
+                if a.profile_adhoc:
+                    # diagnostics: where does a slow fresh statement spend its time
+                    import cProfile
+                    import io
+                    import pstats
+                    pr = cProfile.Profile()
+                    pr.enable()
+                    eng.sql(st_sql[q])
+                    pr.disable()
+                    if time.perf_counter() - tq > a.profile_adhoc / 1e3:
+                        buf = io.StringIO()
+                        pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(25)
+                        log(f"[bench] ad-hoc stream {k} Q{q} took {(time.perf_counter() - tq) * 1e3:.1f} ms:\n"
+                            + buf.getvalue())
+                else:
+                    eng.sql(st_sql[q])
                 qtimes.append(f"Q{q}={(time.perf_counter() - tq) * 1e3:.1f}")
                 nrb += eng.last_metrics.get("readbacks", 0)
                 m = eng.last_metrics.get("speculation")
