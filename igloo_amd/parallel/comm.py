@@ -254,6 +254,21 @@ class Communicator:
             out = out.view(torch.bool)
         return out.to(t.device), list(recv_counts)
 
+    def all_to_all_v_async(self, t: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]):
+        """``all_to_all_v`` issued asynchronously (a pipelined exchange keeps
+        packing the next chunk while this one moves): returns (output on the
+        wire device, work handle); ``wait()`` the handle before reading."""
+        if faults.ACTIVE:
+            faults.check("comm_timeout", "all_to_all_v")
+        tail = tuple(t.shape[1:])
+        out = torch.empty((sum(recv_counts),) + tail, dtype=t.dtype, device=self.wire)
+        src = t.contiguous().to(self.wire)
+        self.calls += 1
+        work = dist.all_to_all_single(out, src, list(map(int, recv_counts)), list(map(int, send_counts)),
+                                      group=self.group, async_op=True)
+        self.bytes_sent += src.numel() * src.element_size()
+        return out, work
+
     def all_to_all_counts(self, send_counts: Sequence[int]) -> List[int]:
         if faults.ACTIVE:
             faults.check("comm_timeout", "all_to_all_counts")

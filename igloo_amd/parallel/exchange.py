@@ -312,6 +312,7 @@ class ShufflePlan:
                 self.sbytes.append([o[r + 1] - o[r] for r in range(W)])
         self.str_cols = [j for j, c in enumerate(cols) if c.dtype.is_string]
         self.rmat: Optional[List[List[int]]] = None
+        self.full_max: Optional[int] = None
 
     def matrix(self) -> List[List[int]]:
         return [[self.send[r]] + [sb[r] for sb in self.sbytes] for r in range(self.W)]
@@ -340,6 +341,9 @@ class ShufflePlan:
         if plain_now != list(self.sgath):
             return False
         rmat = []
+        # every rank's rows per destination (the whole count matrix, known
+        # alike on every rank: a pipelined exchange sizes its chunks from it)
+        self.full_max = max((pre[r][d * (1 + ns)] for r in range(self.W) for d in range(self.W)), default=0)
         for r in range(self.W):
             blk = pre[r][rank * (1 + ns):(rank + 1) * (1 + ns)]
             bys = [blk[1 + t] for t, j in enumerate(self.str_cols) if j in self.sgath]
@@ -380,6 +384,14 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = F
     cols = [b.columns[k] for k in keys]
     tensors, spec = _fixed_parts(cols)
     recv = [r[0] for r in rmat]
+    if not sgath and tensors and plan.full_max is not None and W > 1 and \
+            plan.full_max * sum(t.element_size() * (t.shape[1] if t.dim() == 2 else 1) for t in tensors) \
+            > PIPELINE_MIN_BYTES:
+        from ..ops._lib import capturing
+        if not capturing():
+            parts = _pipelined_exchange(tensors, plan, comm)
+            out = dict(zip(keys, _rebuild(cols, spec, parts, {})))
+            return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
     packed, lay = pack_rows(tensors, perm, b.num_rows) if tensors else (None, (0, []))
     rb = lay[0]
     if not sgath:
@@ -417,6 +429,60 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = F
              for k, j in enumerate(sgath)}
     out = dict(zip(keys, _rebuild(cols, spec, parts, chars)))
     return with_dist(Batch(out, sum(recv)), ("hash", key_cid) if key_cid is not None else None)
+
+
+#: a fixed-width shuffle whose largest (sender, destination) block exceeds this
+#: many bytes is pipelined in chunks of PIPELINE_CHUNK_BYTES per rank
+PIPELINE_MIN_BYTES = 256 << 20
+PIPELINE_CHUNK_BYTES = 64 << 20
+
+
+def _pipelined_exchange(tensors: List[torch.Tensor], plan: ShufflePlan, comm) -> List[torch.Tensor]:
+    """The rows of a large fixed-width shuffle in chunks: chunk j carries rows
+    [j*C, (j+1)*C) of every (sender, destination) block. While chunk j moves
+    (an asynchronous all-to-all-v), chunk j+1 is packed and chunk j-1 is
+    placed into the assembled receive buffer -- pack, transfer and unpack of
+    consecutive chunks overlap instead of running as three full-size
+    barriers. The chunk count follows from the whole count matrix (the
+    structure all-gather carried it), so every rank issues the same
+    collectives. Rows come out in the unchunked order (by sender, then send
+    order). Returns the unpacked tensors."""
+    from ..ops.pack import layout, pack_rows, unpack_rows
+    W = plan.W
+    lay = layout(tensors)
+    rb = lay[0]
+    send, recv = plan.send, [r[0] for r in plan.rmat]
+    C = max(1, PIPELINE_CHUNK_BYTES // max(rb * W, 1))
+    nchunks = -(-plan.full_max // C)
+    dev = tensors[0].device
+    total = sum(recv)
+    assembled = torch.empty((total, rb), dtype=torch.uint8, device=dev)
+    roff = np.cumsum([0] + recv).tolist()
+    perm = plan.perm
+    pending = []
+
+    def land(j, out, work, r_j):
+        work.wait()
+        out = out.to(dev)
+        pos = 0
+        for r in range(W):
+            if r_j[r]:
+                assembled[roff[r] + j * C:roff[r] + j * C + r_j[r]].copy_(out[pos:pos + r_j[r]])
+            pos += r_j[r]
+
+    for j in range(nchunks):
+        s_j = [max(0, min(C, send[r] - j * C)) for r in range(W)]
+        r_j = [max(0, min(C, recv[r] - j * C)) for r in range(W)]
+        sl = [perm[plan.bounds[r] + j * C:plan.bounds[r] + j * C + s_j[r]] for r in range(W) if s_j[r]]
+        idx = torch.cat(sl) if sl else perm[:0]
+        packed, _ = pack_rows(tensors, idx, idx.numel(), lay)
+        out, work = comm.all_to_all_v_async(packed, s_j, r_j)
+        pending.append((j, out, work, r_j))
+        if len(pending) > 1:
+            land(*pending.pop(0))
+    for item in pending:
+        land(*item)
+    return unpack_rows(assembled, lay, tensors)
 
 
 def local_slice(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:

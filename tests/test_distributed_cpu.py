@@ -34,6 +34,8 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
         from igloo_amd.parallel import slicing as SL
         X.SMALL_AGG_GATHER = 0              # aggregates shuffle their partial groups
         X.SMALL_GATHER_STR_BYTES = 16       # long strings overflow the one-collective top-k gather
+        X.PIPELINE_MIN_BYTES = 0            # fixed-width shuffles run as pipelined chunks
+        X.PIPELINE_CHUNK_BYTES = 2048
         O.SORTED_JOIN_MIN_ROWS = 1000
         H.SORTED_CHECK_ROWS = 1000
         H.BLOOM_MIN_RATIO = 2
