@@ -268,6 +268,11 @@ class WorkerGroup:
 
     def serve(self):
         """Blocking: rank 0 serves + heartbeats; other ranks follow."""
+        # the startup heap (catalog, loaded tables, caches) moves to the
+        # permanent GC generation: full collections during queries stay short
+        import gc
+        gc.collect()
+        gc.freeze()
         devs = self.devices()  # collective: every rank
         if self.rank != 0:
             self.follower_loop()
