@@ -8,6 +8,7 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["IGLOO_GRAPHS"] = "0"     # eager execution: a graph replay issues no ATen op to attribute
 
 
 def main():
@@ -42,10 +43,9 @@ def main():
         if any(ch.name.startswith("aten::") for ch in ev.cpu_children):
             continue     # count the innermost aten op only
         site = "?"
-        for fr in ev.stack or []:
-            if "igloo_amd" in fr and "ops/_lib.py" not in fr:
-                site = fr.split("igloo_amd/")[-1]
-                break
+        frames = [fr for fr in (ev.stack or []) if "igloo_amd" in fr and "ops/_lib.py" not in fr]
+        if frames:
+            site = " <- ".join(fr.split("igloo_amd/")[-1] for fr in frames[:2])
         k = (ev.name, site)
         agg[k][0] += dev_us / 1e3
         agg[k][1] += 1
