@@ -478,6 +478,10 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("differs_from_rep", [](uintptr_t a, int elem_bytes, uintptr_t rep, bool rep64, int64_t n, uintptr_t flag,
+                               uintptr_t s) {
+    kern::differs_from_rep(P<const void>(a), elem_bytes, P<const void>(rep), rep64, n, P<int>(flag), S(s));
+  });
   m.def("mark_keys", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, int64_t kmin, int64_t dom,
                         uintptr_t marks, uintptr_t s) {
     kern::mark_keys(P<const void>(keys), key64, P<const uint8_t>(valid), n, kmin, dom, P<uint8_t>(marks), S(s));

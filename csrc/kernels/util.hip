@@ -251,7 +251,41 @@ __global__ __launch_bounds__(kBlock) void wide_fits_kernel(const int64_t* __rest
   if (__any(bad) && lane_id() == 0) atomicOr(flag, 1);
 }
 
+// flag = 1 when some row's value differs from its group representative's
+// (a[i] != a[rep[i]]): the functional-dependency check of a GROUP BY key,
+// one pass with no gathered copy or difference temporary.
+template <typename T, typename R>
+__global__ __launch_bounds__(kBlock) void differs_from_rep_kernel(const T* __restrict__ a, const R* __restrict__ rep,
+                                                                 int64_t n, int* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= a[i] != a[rep[i]];
+  if (__any(bad) && lane_id() == 0) atomicOr(flag, 1);
+}
+
 }  // namespace
+
+void differs_from_rep(const void* a, int elem_bytes, const void* rep, bool rep64, int64_t n, int* flag,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(zero_flag_kernel, dim3(1), dim3(1), 0, stream, flag);
+  if (n > 0) {
+    const dim3 g(grid_for(n, kBlock * 4, 8192)), b(kBlock);
+#define IGLOO_DIFF(T)                                                                                      \
+  if (rep64)                                                                                               \
+    hipLaunchKernelGGL((differs_from_rep_kernel<T, int64_t>), g, b, 0, stream, (const T*)a, (const int64_t*)rep, n, \
+                       flag);                                                                              \
+  else                                                                                                     \
+    hipLaunchKernelGGL((differs_from_rep_kernel<T, int32_t>), g, b, 0, stream, (const T*)a, (const int32_t*)rep, n, flag);
+    switch (elem_bytes) {
+      case 1: IGLOO_DIFF(uint8_t) break;
+      case 2: IGLOO_DIFF(uint16_t) break;
+      case 4: IGLOO_DIFF(uint32_t) break;
+      default: IGLOO_DIFF(uint64_t) break;
+    }
+#undef IGLOO_DIFF
+  }
+  check_launch("util.differs_from_rep", stream);
+}
 
 // flag = 1 when some 128-bit (lo, hi) sum does not fit int64 (hi is not the
 // sign extension of lo). Replaces a torch `.all()` over the groups: a torch

@@ -605,6 +605,20 @@ def _diff_bounds(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return buf[:2]
 
 
+def _differs_from_rep(a: torch.Tensor, rr: torch.Tensor) -> torch.Tensor:
+    """Device int32 flag: some a[i] != a[rr[i]] (csrc/kernels/util.hip
+    differs_from_rep: one pass, no gathered copy)."""
+    a = a.contiguous()
+    flag = torch.empty(1, dtype=torch.int32, device=a.device)
+    esz = a.element_size() * (a.shape[1] if a.dim() == 2 else 1)
+    if esz not in (1, 2, 4, 8):
+        d = _diff_bounds(a.reshape(a.shape[0], -1)[:, 0], a.reshape(a.shape[0], -1)[:, 0].index_select(0, rr))
+        return (d != 0).any().to(torch.int32).reshape(1)
+    launch("differs_from_rep").differs_from_rep(ptr(a), esz, ptr(rr), rr.dtype == torch.int64, a.shape[0],
+                                                ptr(flag), stream(flag))
+    return flag
+
+
 def _late_group_keys(groups, b: "LateBatch", ctx, skip: Optional[set] = None):
     """GROUP BY over a join result still in index form, with plain string keys
     (TPC-H Q10: c_custkey plus six customer/nation attributes over 11M joined
@@ -637,8 +651,8 @@ def _late_group_keys(groups, b: "LateBatch", ctx, skip: Optional[set] = None):
         if idx is None:
             return None
         parts.add(k)
-        checks.append(_diff_bounds(idx, gather_tensor(idx, rr)))
-    if checks and any(to_host_ints(torch.cat(checks))):
+        checks.append(_differs_from_rep(idx, rr) if idx.is_cuda else _diff_bounds(idx, gather_tensor(idx, rr)))
+    if checks and any(to_host_ints(torch.cat([c.to(torch.int64) for c in checks]))):
         return None
     ctx.sorted_gids = srt
     taken = []
@@ -709,12 +723,12 @@ def _encode_groups(gcols: List[Column], ctx, fd: bool = False):
                 checks.append(m.to(torch.int64))
                 owner.append(i)
             else:
-                # device [min, max] of key - representative's key (graph-safe)
-                checks.append(_diff_bounds(keys[i], keys[i].index_select(0, rr)))
-                owner += [i, i]
+                # any key unlike its representative's (one pass, graph-safe)
+                checks.append(_differs_from_rep(keys[i], rr).to(torch.int64))
+                owner.append(i)
             if c.valid is not None:
-                checks.append(_diff_bounds(c.valid, c.valid.index_select(0, rr)))
-                owner += [i, i]
+                checks.append(_differs_from_rep(c.valid, rr).to(torch.int64))
+                owner.append(i)
         bad = {i for i, v in zip(owner, to_host_ints(torch.cat(checks))) if v}
         needed = [lead] + [i for i in range(len(gcols)) if i != lead and i in bad]
         if len(needed) == 1:
