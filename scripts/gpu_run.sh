@@ -150,6 +150,10 @@ SETS
       timeout -k 10 600 python -u scripts/adhoc_profile.py --sf ${SF:-100} --streams 3 \
         --out gpurun_out/adhoc_profile.txt > gpurun_out/adhoc_profile.log 2>&1
       rc=$?; echo "adhoc rc=$rc"; head -60 gpurun_out/adhoc_profile.txt ;;
+    atbytes)
+      # ATen ops by engine call site, bytes written (TorchDispatchMode)
+      timeout -k 10 600 python -u scripts/aten_bytes.py --sf ${SF:-10} --top 50 > gpurun_out/aten_bytes.txt 2>&1
+      rc=$?; echo "atbytes rc=$rc"; head -40 gpurun_out/aten_bytes.txt ;;
     rbsites)
       # blocking readbacks per query and how many are parameter-independent
       timeout -k 10 600 python -u scripts/readback_sites.py --sf ${SF:-10} --streams 2 --stacks \
