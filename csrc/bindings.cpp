@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include <tuple>
+#include <memory>
 #include <vector>
 
 #include "io/parquet_meta.h"
@@ -477,6 +478,16 @@ PYBIND11_MODULE(_native, m) {
                               uintptr_t new_off, uintptr_t out, uintptr_t s) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
+  });
+  m.def("pack_bits", [](std::vector<uintptr_t> cols, std::vector<bool> is64, std::vector<int64_t> lo,
+                        std::vector<int> shift, int64_t n, uintptr_t out, uintptr_t s) {
+    std::vector<const void*> c(cols.size());
+    std::unique_ptr<bool[]> w(new bool[cols.size()]);
+    for (size_t i = 0; i < cols.size(); ++i) {
+      c[i] = reinterpret_cast<const void*>(cols[i]);
+      w[i] = is64[i];
+    }
+    kern::pack_bits(c.data(), w.get(), lo.data(), shift.data(), (int)cols.size(), n, P<int64_t>(out), S(s));
   });
   m.def("differs_from_rep", [](uintptr_t a, int elem_bytes, uintptr_t rep, bool rep64, int64_t n, uintptr_t flag,
                                uintptr_t s) {

@@ -68,6 +68,9 @@ void unpack_rows(const PackSpec& spec, const uint8_t* in, int64_t n, hipStream_t
 
 // ---- util.hip -------------------------------------------------------------------
 void const_ints(int64_t* out, const int64_t* vals, int64_t n, hipStream_t stream);
+constexpr int kMaxPackBits = 8;
+void pack_bits(const void* const* cols, const bool* is64, const int64_t* lo, const int* shift, int ncols, int64_t n,
+               int64_t* out, hipStream_t stream);
 void differs_from_rep(const void* a, int elem_bytes, const void* rep, bool rep64, int64_t n, int* flag,
                       hipStream_t stream);
 void mark_keys(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t dom,

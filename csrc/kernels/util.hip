@@ -13,6 +13,8 @@
 //                    over clustered keys.
 #include <limits>
 
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -330,6 +332,28 @@ void const_ints(int64_t* out, const int64_t* vals, int64_t n, hipStream_t stream
   check_launch("const_ints", stream);
 }
 
+// Composite integer keys bit-packed into one int64 per row (GROUP BY / join
+// on several columns whose ranges fit in 62 bits): one pass over all key
+// columns instead of a subtract, shift and OR per column in ATen.
+struct PackBitsParams {
+  int ncols;
+  const void* col[kMaxPackBits];
+  int is64[kMaxPackBits];
+  long long lo[kMaxPackBits];
+  int shift[kMaxPackBits];
+};
+
+__global__ __launch_bounds__(kBlock) void pack_bits_kernel(PackBitsParams p, int64_t n, int64_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    uint64_t acc = 0;
+    for (int c = 0; c < p.ncols; ++c) {
+      const int64_t v = p.is64[c] ? ((const int64_t*)p.col[c])[i] : (int64_t)((const int32_t*)p.col[c])[i];
+      acc = (acc << p.shift[c]) | (uint64_t)(v - p.lo[c]);
+    }
+    out[i] = (int64_t)acc;
+  }
+}
+
 // Dense key marks (range-sliced SEMI / ANTI joins, parallel/exchange.py):
 // marks[k - kmin] = 1 for every valid key k in [kmin, kmin + dom) -- one
 // pass over the keys, plain byte stores (racing stores all write 1).
@@ -355,6 +379,22 @@ __global__ __launch_bounds__(kBlock) void probe_marks_kernel(const T* __restrict
     const bool hit = d >= 0 && d < dom && (!valid || valid[i]) && marks[d] != 0;
     out[i] = hit != negate;
   }
+}
+
+void pack_bits(const void* const* cols, const bool* is64, const int64_t* lo, const int* shift, int ncols, int64_t n,
+               int64_t* out, hipStream_t stream) {
+  if (n == 0) return;
+  if (ncols < 1 || ncols > kMaxPackBits) throw std::runtime_error("pack_bits: column count");
+  PackBitsParams p{};
+  p.ncols = ncols;
+  for (int c = 0; c < ncols; ++c) {
+    p.col[c] = cols[c];
+    p.is64[c] = is64[c] ? 1 : 0;
+    p.lo[c] = lo[c];
+    p.shift[c] = shift[c];
+  }
+  hipLaunchKernelGGL(pack_bits_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, p, n, out);
+  check_launch("util.pack_bits", stream);
 }
 
 void mark_keys(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t dom,

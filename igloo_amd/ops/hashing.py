@@ -678,17 +678,10 @@ def pack_keys(cols: Sequence[torch.Tensor]) -> torch.Tensor:
     if len(cols) == 1:
         c = cols[0]
         return c if c.dtype in (torch.int32, torch.int64) else c.to(torch.int64)
-    ranges = []
-    for c in cols:
-        r = key_range(c) if c.numel() else (0, 0)
-        ranges.append(r)
+    ranges = key_ranges(cols)
     bits = [max(1, int(hi - lo).bit_length()) for lo, hi in ranges]
     if sum(bits) <= 62:
-        out = None
-        for c, (lo, _), b in zip(cols, ranges, bits):
-            v = c.to(torch.int64) - lo
-            out = v if out is None else (out << b) | v
-        return out
+        return _pack_bits(cols, ranges, bits)
     # pairwise dense re-encoding keeps every intermediate code < n
     acc = cols[0].to(torch.int64)
     for c in cols[1:]:
@@ -703,6 +696,68 @@ def pack_keys_pair(left: Sequence[torch.Tensor], right: Sequence[torch.Tensor]) 
     if len(left) == 1:
         return left[0], right[0]
     nl = left[0].numel()
+    if is_gpu(left[0]) and len(left) <= MAX_PACK_BITS:
+        # one shared bit layout from both sides' ranges: each side packed in
+        # place, no concatenated copies
+        rl, rr = key_ranges(list(left)), key_ranges(list(right))
+        ranges = [(min(a[0], b[0]), max(a[1], b[1])) for a, b in zip(rl, rr)]
+        bits = [max(1, int(hi - lo).bit_length()) for lo, hi in ranges]
+        if sum(bits) <= 62:
+            return _pack_bits(list(left), ranges, bits), _pack_bits(list(right), ranges, bits)
     both = [torch.cat([a.to(torch.int64), b.to(torch.int64)]) for a, b in zip(left, right)]
     packed = pack_keys(both)
     return packed[:nl], packed[nl:]
+
+
+#: columns one pack_bits launch combines (csrc/kernels/kernels.h kMaxPackBits)
+MAX_PACK_BITS = 8
+
+
+def key_ranges(cols: Sequence[torch.Tensor]) -> List[Tuple[int, int]]:
+    """(min, max) of each integer key column ((0, 0) for an empty one; an
+    all-NULL-free column assumed), with ONE readback for all of them on the
+    GPU (resident columns answer from their remembered stats)."""
+    out: List[Optional[Tuple[int, int]]] = [None] * len(cols)
+    todo = []
+    for i, c in enumerate(cols):
+        if c.numel() == 0:
+            out[i] = (0, 0)
+            continue
+        hit = getattr(c, "_igloo_stats", None)
+        if hit is not None and hit[0] is not None:
+            out[i] = hit[0]
+        elif is_gpu(c) and c.dtype in (torch.int32, torch.int64) and c.dim() == 1:
+            todo.append(i)
+        else:
+            r = key_range(c)
+            out[i] = r if r is not None else (0, 0)
+    if todo:
+        N = launch("column_stats")
+        bufs = []
+        for i in todo:
+            c = cols[i].contiguous()
+            buf = torch.empty(N.STATS_SLOTS, dtype=torch.int64, device=c.device)
+            N.column_stats(ptr(c), c.dtype == torch.int64, 0, c.numel(), ptr(buf), stream(c))
+            bufs.append(buf[:2])
+        vals = to_host_ints(torch.cat(bufs))
+        for j, i in enumerate(todo):
+            lo, hi = vals[2 * j], vals[2 * j + 1]
+            out[i] = (lo, hi) if lo <= hi else (0, 0)
+    return out  # type: ignore[return-value]
+
+
+def _pack_bits(cols: Sequence[torch.Tensor], ranges, bits) -> torch.Tensor:
+    n = cols[0].numel()
+    if not is_gpu(cols[0]) or len(cols) > MAX_PACK_BITS or any(c.dtype not in (torch.int32, torch.int64)
+                                                                for c in cols):
+        out = None
+        for c, (lo, _), b in zip(cols, ranges, bits):
+            v = c.to(torch.int64) - lo
+            out = v if out is None else (out << b) | v
+        return out
+    cs = [c.contiguous() for c in cols]
+    out = torch.empty(n, dtype=torch.int64, device=cs[0].device)
+    shifts = [0] + list(bits[1:])      # acc = (acc << bits[c]) | (v - lo) for every column after the first
+    launch("pack_bits").pack_bits([ptr(c) for c in cs], [c.dtype == torch.int64 for c in cs],
+                                  [int(lo) for lo, _ in ranges], shifts, n, ptr(out), stream(out))
+    return out

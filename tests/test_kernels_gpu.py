@@ -570,3 +570,29 @@ def test_like_tile_shapes(gpu_device, words):
     for pat in ("%special%requests%", "%Customer%Complaints%", "forest%", "%BRASS", "%e%e%e%"):
         assert torch.equal(S.like(c, pat), S.like(g, pat).cpu()), pat
         assert torch.equal(S.like(c, pat, negate=True), S.like(g, pat, negate=True).cpu()), pat
+
+
+@pytest.mark.parametrize("ncols", [1, 3, 8])
+def test_pack_keys_native(gpu_device, ncols):
+    """csrc/kernels/util.hip pack_bits vs the plain int64 shift/OR formula."""
+    g = torch.Generator().manual_seed(ncols)
+    n = 100_003
+    cols = []
+    for c in range(ncols):
+        lo = int(torch.randint(-1000, 1000, (1,), generator=g))
+        hi = lo + int(torch.randint(1, 200, (1,), generator=g))
+        dt = torch.int32 if c % 2 == 0 else torch.int64
+        cols.append(torch.randint(lo, hi, (n,), generator=g).to(dt))
+    ref_ranges = [(int(c.min()), int(c.max())) for c in cols]
+    bits = [max(1, (hi - lo).bit_length()) for lo, hi in ref_ranges]
+    ref = None
+    for c, (lo, _), b in zip(cols, ref_ranges, bits):
+        v = c.to(torch.int64) - lo
+        ref = v if ref is None else (ref << b) | v
+    got = H.pack_keys([c.to(DEV) for c in cols]).cpu()
+    assert torch.equal(got, ref)
+    # pair packing: one shared layout, both sides packed separately
+    left = [c[: n // 3].to(DEV) for c in cols]
+    right = [c[n // 3:].to(DEV) for c in cols]
+    pl, pr = H.pack_keys_pair(left, right)
+    assert torch.equal(torch.cat([pl, pr]).cpu(), ref)
