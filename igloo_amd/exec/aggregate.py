@@ -703,7 +703,7 @@ def _encode_groups(gcols: List[Column], ctx, fd: bool = False):
     keys: Dict[int, torch.Tensor] = {}
     reps_src: List[Column] = list(gcols)
     for i in others:
-        keys[i], reps_src[i] = group_key_tensor(gcols[i])
+        keys[i], reps_src[i] = group_key_tensor(gcols[i], narrow=True)
     needed = list(range(len(gcols)))
     if (plain or (fd and len(gcols) > 1)) and others and ctx.device.type == "cuda":
         spans = {i: H.key_range(keys[i]) for i in others}
@@ -735,7 +735,7 @@ def _encode_groups(gcols: List[Column], ctx, fd: bool = False):
             return gid, ng, rep, reps_src
     for i in plain:
         if i in needed:
-            keys[i], _ = group_key_tensor(gcols[i])
+            keys[i], _ = group_key_tensor(gcols[i], narrow=True)
     packed = H.pack_keys([keys[i] for i in needed])
     gid, ng, rep, srt = H.group_ids_ex(packed)
     ctx.sorted_gids = srt

@@ -81,10 +81,15 @@ def _num_key(c: Column) -> torch.Tensor:
     return x
 
 
-def group_key_tensor(c: Column) -> Tuple[torch.Tensor, Column]:
-    """Int key per row for GROUP BY (NULL is its own group); returns (key, column to take reps from)."""
+def group_key_tensor(c: Column, narrow: bool = False) -> Tuple[torch.Tensor, Column]:
+    """Int key per row for GROUP BY (NULL is its own group); returns (key, column to take reps from).
+    ``narrow``: a NULL-free dictionary column keeps its int32 codes (local
+    grouping, whose packing and group-id kernels read either width) instead
+    of a widened copy; sketches and exchanged keys stay int64."""
     if c.dtype.is_string:
         d = c if c.is_dict else S.dict_encode(c)
+        if narrow and d.valid is None and d.data.dtype == torch.int32:
+            return d.data, d
         k = d.data.to(torch.int64)
         if d.valid is not None:
             k = torch.where(d.valid, k, torch.full_like(k, -1))

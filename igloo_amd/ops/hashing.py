@@ -699,8 +699,14 @@ def pack_keys_pair(left: Sequence[torch.Tensor], right: Sequence[torch.Tensor]) 
     if is_gpu(left[0]) and len(left) <= MAX_PACK_BITS:
         # one shared bit layout from both sides' ranges: each side packed in
         # place, no concatenated copies
-        rl, rr = key_ranges(list(left)), key_ranges(list(right))
-        ranges = [(min(a[0], b[0]), max(a[1], b[1])) for a, b in zip(rl, rr)]
+        both = key_ranges(list(left) + list(right))      # one readback for both sides
+        rl, rr = both[:len(left)], both[len(left):]
+        if right[0].numel() == 0:
+            ranges = rl
+        elif nl == 0:
+            ranges = rr
+        else:
+            ranges = [(min(a[0], b[0]), max(a[1], b[1])) for a, b in zip(rl, rr)]
         bits = [max(1, int(hi - lo).bit_length()) for lo, hi in ranges]
         if sum(bits) <= 62:
             return _pack_bits(list(left), ranges, bits), _pack_bits(list(right), ranges, bits)
