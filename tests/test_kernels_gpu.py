@@ -572,7 +572,7 @@ def test_like_tile_shapes(gpu_device, words):
         assert torch.equal(S.like(c, pat, negate=True), S.like(g, pat, negate=True).cpu()), pat
 
 
-@pytest.mark.parametrize("ncols", [1, 3, 8])
+@pytest.mark.parametrize("ncols", [2, 3, 8])
 def test_pack_keys_native(gpu_device, ncols):
     """csrc/kernels/util.hip pack_bits vs the plain int64 shift/OR formula."""
     g = torch.Generator().manual_seed(ncols)
