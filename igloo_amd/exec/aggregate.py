@@ -638,7 +638,7 @@ def _late_group_keys(groups, b: "LateBatch", ctx, skip: Optional[set] = None):
     if not plain or not others:
         return None
     keys = {i: group_key_tensor(b.gather(cids[i]))[0] for i in others}
-    spans = {i: H.key_range(keys[i]) for i in others}
+    spans = _span_hints(keys, others)
     lead = _lead_key(others, spans, base)
     gid, ng, rep, srt = H.group_ids_ex(keys[lead])
     rr = gather_tensor(rep, gid)
@@ -670,6 +670,17 @@ def _late_group_keys(groups, b: "LateBatch", ctx, skip: Optional[set] = None):
             else:
                 taken.append(take(bb.columns[c], gather_tensor(idx, rep)))
     return gid, ng, rep, taken
+
+
+def _span_hints(keys, others):
+    """Key ranges for ranking the lead key: resident-derived bounds where
+    known (ops/hashing.py key_bound), the rest read back together."""
+    spans = {i: H.key_bound(keys[i]) for i in others}
+    todo = [i for i in others if spans[i] is None]
+    if todo:
+        for i, r in zip(todo, H.key_ranges([keys[i] for i in todo])):
+            spans[i] = r
+    return spans
 
 
 def _lead_key(others, spans, cols) -> int:
@@ -706,7 +717,7 @@ def _encode_groups(gcols: List[Column], ctx, fd: bool = False):
         keys[i], reps_src[i] = group_key_tensor(gcols[i], narrow=True)
     needed = list(range(len(gcols)))
     if (plain or (fd and len(gcols) > 1)) and others and ctx.device.type == "cuda":
-        spans = {i: H.key_range(keys[i]) for i in others}
+        spans = _span_hints(keys, others)
         lead = _lead_key(others, spans, gcols)
         gid, ng, rep, srt = H.group_ids_ex(keys[lead])
         ctx.sorted_gids = srt

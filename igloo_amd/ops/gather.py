@@ -11,8 +11,30 @@ from typing import List, Optional, Sequence
 import torch
 
 from ..columnar import Column
-from ._lib import is_gpu, launch, ptr, stream
+from ._lib import is_gpu, launch, ptr, stream, to_host_ints
 from .select import offsets_from_lengths
+
+
+def origin(t: torch.Tensor) -> Optional[torch.Tensor]:
+    """The resident table column every value of ``t`` was gathered from (no
+    negative rows), or None: ``t`` itself, a filtered scan's source
+    (exec/scan.py _tag_base) or the origin a gather inherited (take_many).
+    ops/hashing.py key_bound derives key ranges from it without a readback."""
+    if getattr(t, "_igloo_resident", False):
+        return t
+    o = getattr(t, "_igloo_origin", None)
+    if o is not None:
+        return o
+    base = getattr(t, "_igloo_base", None)
+    if base is not None and base[0].data.dtype == t.dtype:
+        return origin(base[0].data)
+    return None
+
+
+def _inherit(dst: torch.Tensor, src: torch.Tensor) -> None:
+    o = origin(src)
+    if o is not None:
+        dst._igloo_origin = o
 
 
 def _cpu_take_tensor(t: torch.Tensor, idx: torch.Tensor, neg: bool) -> torch.Tensor:
@@ -44,16 +66,30 @@ def _take_plain_strings(col: Column, idx: torch.Tensor, neg: bool) -> Column:
         else:
             chars = torch.zeros(0, dtype=torch.uint8)
         return Column(col.dtype, chars, None, offsets=new_off)
+    return _take_strings_gpu([col], idx)[0]
+
+
+def _take_strings_gpu(cols: Sequence[Column], idx: torch.Tensor) -> List[Column]:
+    """Plain string gathers of several columns by one index: the lengths and
+    offsets of every column first, then ONE readback of all their byte totals
+    (to size the character buffers), then the copies."""
+    n = idx.numel()
     N = launch("str_gather")
     s = stream(idx)
     idx64 = idx.dtype == torch.int64
-    lens = torch.empty(n, dtype=torch.int64, device=idx.device)
-    N.str_gather_lengths(ptr(col.offsets), ptr(idx), idx64, n, ptr(lens), s)
-    new_off, total = offsets_from_lengths(lens)
-    chars = torch.empty(max(total, 0), dtype=torch.uint8, device=idx.device)
-    if total:
-        N.str_gather_copy(ptr(col.offsets), ptr(col.data), ptr(idx), idx64, n, ptr(new_off), ptr(chars), s)
-    return Column(col.dtype, chars, None, offsets=new_off)
+    offs = []
+    for col in cols:
+        lens = torch.empty(n, dtype=torch.int64, device=idx.device)
+        N.str_gather_lengths(ptr(col.offsets), ptr(idx), idx64, n, ptr(lens), s)
+        offs.append(offsets_from_lengths(lens, host_total=False)[0])
+    totals = to_host_ints(torch.cat([o[-1:] for o in offs]) if len(offs) > 1 else offs[0][-1:])
+    out = []
+    for col, new_off, total in zip(cols, offs, totals):
+        chars = torch.empty(max(total, 0), dtype=torch.uint8, device=idx.device)
+        if total:
+            N.str_gather_copy(ptr(col.offsets), ptr(col.data), ptr(idx), idx64, n, ptr(new_off), ptr(chars), s)
+        out.append(Column(col.dtype, chars, None, offsets=new_off))
+    return out
 
 
 def _src_ptr(t) -> int:
@@ -78,10 +114,12 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
     out: List[Column] = []
     descs = []      # GPU: (src, dst, elem_bytes, src_valid, dst_valid) -> one gather_multi launch
     keepalive = []  # temporaries that must outlive the (stream-ordered) launch
+    strs = [c for c in cols if c.is_plain_string]
+    pre = iter(_take_strings_gpu(strs, idx) if gpu and strs else [])
     for c in cols:
         need_valid = neg or c.valid is not None
         if c.is_plain_string:
-            nc = _take_plain_strings(c, idx, neg)
+            nc = next(pre) if gpu else _take_plain_strings(c, idx, neg)
             if need_valid:
                 if gpu:
                     src = c.valid
@@ -109,6 +147,8 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
         esz = c.data.element_size() * (c.data.shape[1] if c.data.dim() == 2 else 1)
         valid = torch.empty(n, dtype=torch.bool, device=idx.device) if need_valid else None
         descs.append((_src_ptr(c.data), ptr(data), esz, _src_ptr(c.valid), ptr(valid)))
+        if not neg:
+            _inherit(data, c.data)
         out.append(Column(c.dtype, data, valid, dictionary=c.dictionary))
     if gpu and descs and n:
         N = launch("gather_multi")
@@ -129,6 +169,7 @@ def gather_tensor(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         esz = t.element_size() * (t.shape[1] if t.dim() == 2 else 1)
         launch("gather_multi").gather_multi(ptr(idx), idx.dtype == torch.int64, n, [(ptr(t), ptr(out), esz, 0, 0)],
                                             stream(idx))
+    _inherit(out, t)
     return out
 
 

@@ -15,7 +15,8 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import check_not_capturing, is_gpu, launch, native, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
+from .gather import origin as _origin
+from ._lib import capturing, check_not_capturing, is_gpu, launch, native, ptr, stream, to_host_f64s, to_host_int, to_host_ints, unlogged
 from .select import exclusive_scan, mask_to_indices
 
 EMPTY_KEY = -(2**63)
@@ -85,6 +86,53 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
     return column_stats(keys, valid)[0]
 
 
+def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
+    """An interval holding every key, known without a readback in steady
+    state: the (remembered) range of the resident column the keys were
+    gathered from. Looser than ``key_range`` for a filtered subset; callers
+    use it where a bound suffices (direct-mapped table spans, bit widths)."""
+    o = _origin(keys)
+    if o is None or o.dtype != keys.dtype or o.dim() != 1:
+        return None
+    st = getattr(o, "_igloo_stats", None)
+    if st is None:
+        if capturing():
+            return None
+        st = column_stats(o)
+    return st[0]
+
+
+def key_unique(keys: torch.Tensor) -> bool:
+    """True only when the keys are known distinct with no readback in steady
+    state: distinct rows (a resident column, or a filtered scan's rows of one,
+    in row order) of a resident column whose values are unique (checked once
+    and remembered on it)."""
+    if getattr(keys, "_igloo_resident", False):
+        o = keys
+    else:
+        base = getattr(keys, "_igloo_base", None)
+        if base is None or base[0].data.dtype != keys.dtype or not getattr(base[0].data, "_igloo_resident", False):
+            return False
+        o = base[0].data
+    u = getattr(o, "_igloo_unique", None)
+    if u is None:
+        if capturing() or not is_gpu(o) or o.dim() != 1:
+            return False
+        with unlogged():     # one-time check of a resident column (ops/_lib.py unlogged)
+            n = o.numel()
+            if n < 2:
+                u = True
+            elif column_stats(o)[1]:
+                u = to_host_int((o[1:] == o[:-1]).any().to(torch.int64)) == 0
+            else:
+                u = group_ids(o)[1] == n
+        try:
+            o._igloo_unique = u
+        except (AttributeError, RuntimeError):
+            return False
+    return u
+
+
 def _keys_ok(k: torch.Tensor) -> torch.Tensor:
     assert k.dim() == 1 and k.dtype in (torch.int32, torch.int64), f"join keys must be int32/int64, got {k.dtype}"
     return k.contiguous()
@@ -99,17 +147,22 @@ class JoinTable:
         self.device = keys.device
         self.gpu = is_gpu(keys)
         self.valid = valid
-        rng = key_range(keys, valid)
+        rng = None
+        if valid is None and self.gpu:
+            # a resident-derived bound that already selects the direct table
+            # (the exact range could only narrow it): no range readback
+            bnd = key_bound(keys)
+            if bnd is not None and self._direct_for(bnd[1] - bnd[0] + 1, n):
+                rng = bnd
+        if rng is None:
+            rng = key_range(keys, valid)
         self.empty = rng is None
         if self.empty:
             self.unique = True
             return
         self.kmin, kmax = rng
         span = kmax - self.kmin + 1
-        lim = TABLE_BYTES_LIMIT.get()
-        # (head + CSR start/count arrays: up to 3 int32 words per slot)
-        wide_ok = span <= DIRECT_JOIN_MAX_SPAN and (lim is None or 12 * span <= lim)
-        self.direct = span < 2**31 - 1 and (span <= 4 * n + 4096 or wide_ok)
+        self.direct = self._direct_for(span, n)
         if not self.gpu:
             k = keys if valid is None else torch.where(valid, keys, torch.full_like(keys, kmax + 1) if kmax < 2**62 else keys)
             sk, order = torch.sort(k.to(torch.int64), stable=True)
@@ -119,6 +172,7 @@ class JoinTable:
             self.sorted_keys, self.order = sk, order
             self.unique = bool((sk[1:] != sk[:-1]).all().item()) if sk.numel() > 1 else True
             return
+        known_unique = valid is None and key_unique(keys)
         N = launch("join_build")
         self.cap = span if self.direct else _next_pow2(2 * n)
         # Bloom filter for selective probes: ~8 bits per key, at most 4 MB (L2-resident)
@@ -143,7 +197,7 @@ class JoinTable:
         st = stream(keys)
         N.join_build(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
                      self.kmin, self.direct, ptr(dups), ptr(self.bits), self.bmask, st)
-        self.unique = to_host_int(dups) == 0
+        self.unique = known_unique or to_host_int(dups) == 0
         # duplicate keys: CSR runs (count -> exclusive scan -> scatter), so a
         # multi-match probe reads one contiguous run of build rows
         self.cstart = self.crows = None
@@ -157,6 +211,13 @@ class JoinTable:
             launch("join_csr_scatter").join_csr_scatter(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(cnt),
                                                         ptr(self.cstart), ptr(self.crows), self.rid64, self.cap,
                                                         self.kmin, self.direct, st)
+
+    @staticmethod
+    def _direct_for(span: int, n: int) -> bool:
+        lim = TABLE_BYTES_LIMIT.get()
+        # (head + CSR start/count arrays: up to 3 int32 words per slot)
+        wide_ok = span <= DIRECT_JOIN_MAX_SPAN and (lim is None or 12 * span <= lim)
+        return span < 2**31 - 1 and (span <= 4 * n + 4096 or wide_ok)
 
     # ----------------------------------------------------------------- probes
     def probe_first(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
@@ -564,7 +625,11 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
         g = uniq.numel()
         rep = torch.full((g,), n, dtype=torch.int64).scatter_reduce(0, inv, torch.arange(n), reduce="amin")
         return inv.to(torch.int32), g, rep.to(torch.int32)
-    kmin, kmax = key_range(keys)
+    bnd = key_bound(keys)
+    if bnd is not None and bnd[1] - bnd[0] + 1 <= 2 * n + 65536:
+        kmin, kmax = bnd         # resident-derived bound already direct: no range readback
+    else:
+        kmin, kmax = key_range(keys)
     span = kmax - kmin + 1
     direct = span <= 2 * n + 65536 and span < 2**31 - 1
     cap = span if direct else _next_pow2(2 * n)

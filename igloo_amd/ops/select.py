@@ -49,12 +49,20 @@ def exclusive_scan(counts: torch.Tensor, host_total: bool = True):
 
 def offsets_from_lengths(lengths: torch.Tensor, host_total: bool = True):
     """Arrow offsets [n+1] from per-row lengths (``host_total`` False: no
-    readback; the total comes back as a device tensor)."""
-    ex, total = exclusive_scan(lengths, host_total)
-    off = torch.empty(lengths.numel() + 1, dtype=torch.int64, device=lengths.device)
-    off[:-1] = ex
-    if host_total:
-        off[-1:].fill_(total)     # a device fill (item assignment would upload a host scalar)
-    else:
-        off[-1:].copy_(total.reshape(1))
-    return off, total
+    readback; the total comes back as a device tensor, the offsets' last
+    element). GPU: the scan writes the offsets and the total in place."""
+    n = lengths.numel()
+    if not is_gpu(lengths):
+        ex, total = exclusive_scan(lengths, host_total)
+        off = torch.empty(n + 1, dtype=torch.int64)
+        off[:-1] = ex
+        off[-1] = int(total) if host_total else int(total[0])
+        return off, (total if host_total else off[-1:])
+    lengths = lengths.contiguous()
+    N = launch("exclusive_scan")
+    tiles = N.scan_workspace_tiles(n)
+    ws = torch.empty(tiles, dtype=torch.int64, device=lengths.device)
+    off = torch.empty(n + 1, dtype=torch.int64, device=lengths.device)
+    N.exclusive_scan(ptr(lengths), lengths.dtype == torch.int64, n, ptr(off), ptr(ws), ptr(off) + 8 * n,
+                     stream(lengths))
+    return off, (to_host_int(off[n:]) if host_total else off[n:])
