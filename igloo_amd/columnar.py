@@ -363,9 +363,10 @@ def batch_device(b) -> Optional[torch.device]:
 class Batch:
     """An ordered set of equally long columns keyed by column id (or name)."""
 
-    __slots__ = ("columns", "num_rows", "dist", "out_dist", "preamble")
+    __slots__ = ("columns", "num_rows", "dist", "out_dist", "preamble", "deferred")
 
     def __init__(self, columns: Dict[Any, Column], num_rows: Optional[int] = None, dist=None):
+        self.deferred = None      # query result: (device error flags, messages) checked with its host copy
         self.dist = dist          # ("hash", cid) | ("replicated",) | None  (SPMD row placement)
         self.out_dist = None
         self.preamble = None      # per-rank ints of the last exchange preamble (parallel/exchange.py)

@@ -26,7 +26,7 @@ from .sql import parse
 from .sql.binder import Binder, IdGen
 from .sql.logical import ColInfo, Plan
 from .sql.optimizer import optimize
-from .utils.errors import IglooError, NotSupported, PlanError
+from .utils.errors import ExecutionError, IglooError, NotSupported, PlanError
 from .exec import graphs as _graphs
 from .ops import jit as _jit
 from .utils import trace as _trace
@@ -87,7 +87,13 @@ class QueryResult:
         return pretty_format(self.table)
 
 
-def _host_columns(cols: List[Column]) -> List[Column]:
+def _raise_deferred(deferred, flags) -> None:
+    for v, msg in zip(flags, deferred[1]):
+        if v:
+            raise ExecutionError(msg)
+
+
+def _host_columns(cols: List[Column], deferred=None) -> List[Column]:
     """Result columns moved to the host with ONE synchronisation: every device
     buffer (values, validity, offsets, small dictionaries) is copied with a
     non-blocking D2H copy, then the stream is synchronised once (instead of a
@@ -95,6 +101,8 @@ def _host_columns(cols: List[Column]) -> List[Column]:
     references a large device dictionary keeps its device path (it decodes
     only the referenced strings on the GPU)."""
     if not any(c.data.is_cuda for c in cols):
+        if deferred is not None:
+            _raise_deferred(deferred, deferred[0].tolist())
         return cols
 
     def cpu(t):
@@ -109,7 +117,11 @@ def _host_columns(cols: List[Column]) -> List[Column]:
         return Column(c.dtype, cpu(c.data), cpu(c.valid), offsets=cpu(c.offsets),
                       dictionary=move(d) if d is not None else None)
     out = [move(c) for c in cols]
+    flags = cpu(deferred[0]) if deferred is not None else None
     torch.cuda.current_stream(next(c.data.device for c in cols if c.data.is_cuda)).synchronize()
+    if deferred is not None:
+        # the query's deferred device error flags ride on the result copy
+        _raise_deferred(deferred, flags.tolist())
     return out
 
 
@@ -525,7 +537,7 @@ class QueryEngine:
             sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
             _lib.set_speculation(sp)
             try:
-                batch = self._execute_plan(plan, ctx)
+                batch = self._execute_plan(plan, ctx, fold_checks=True)
             finally:
                 _lib.set_speculation(None)
             ok = sp.validate()
@@ -640,7 +652,11 @@ class QueryEngine:
             self._graph_pool = torch.cuda.graph_pool_handle()
         return self._graph_pool
 
-    def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None) -> Batch:
+    def _execute_plan(self, plan: Plan, ctx: Optional[ExecContext] = None, fold_checks: bool = False) -> Batch:
+        """Run ``plan``. ``fold_checks``: the deferred device error flags are
+        attached to the result (``Batch.deferred``) and checked by its host
+        copy (``_to_arrow``), saving the query a readback; every caller passing
+        it converts the result with ``_to_arrow``."""
         ctx = ctx or self.make_context()
         ctx.slices = self._slices_for(plan)
         node = create_physical_plan(plan)
@@ -653,7 +669,10 @@ class QueryEngine:
         if self.comm is not None and self.comm.spmd:
             from .parallel.exchange import gather_all
             out = gather_all(out, ctx)
-        ctx.check_deferred()
+        if fold_checks and ctx.deferred_checks:
+            out.deferred = ctx.take_deferred()
+        else:
+            ctx.check_deferred()
         return out
 
     def _slices_for(self, plan: Plan) -> Dict[int, str]:
@@ -666,7 +685,7 @@ class QueryEngine:
 
     def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str]) -> pa.Table:
         arrays, fields = [], []
-        host = _host_columns([batch.columns[ci.cid] for ci in schema])
+        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None))
         for ci, nm, col in zip(schema, names, host):
             arr = col.to_arrow()
             want = ci.dtype.to_arrow() if ci.dtype.kind != "null" else pa.null()

@@ -36,6 +36,16 @@ from .expr_eval import Evaluator, Scalar, _convert_tensor
 class ExecContext:
     """Per-query execution state: device, communicator, metrics, subquery cache."""
 
+    def take_deferred(self):
+        """The deferred device error flags as ONE device tensor plus their
+        messages (None when there are none), handed to the result's host copy
+        (engine.py _host_columns) instead of a readback of their own."""
+        if not self.deferred_checks:
+            return None
+        import torch
+        checks, self.deferred_checks = self.deferred_checks, []
+        return torch.cat([f.reshape(-1).to(torch.int64) for f, _ in checks]), [m for _, m in checks]
+
     def check_deferred(self) -> None:
         """Raise the first deferred device error whose flag is set (ONE
         readback for all of them, at the end of the query)."""

@@ -163,7 +163,7 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         with torch.cuda.stream(s):
             g.capture_begin(pool=engine.graph_pool() if SHARED_POOL else None, capture_error_mode="thread_local")
             try:
-                batch = engine._execute_plan(plan, ctx)
+                batch = engine._execute_plan(plan, ctx, fold_checks=True)
                 if not sp.complete:
                     raise _lib.CaptureAbort("call sequence left the recording")
                 bad = sp.device_mismatches(expected)

@@ -88,11 +88,16 @@ def group_key_tensor(c: Column, narrow: bool = False) -> Tuple[torch.Tensor, Col
     of a widened copy; sketches and exchanged keys stay int64."""
     if c.dtype.is_string:
         d = c if c.is_dict else S.dict_encode(c)
+        nd = len(d.dictionary) if d.dictionary is not None else None
         if narrow and d.valid is None and d.data.dtype == torch.int32:
-            return d.data, d
-        k = d.data.to(torch.int64)
-        if d.valid is not None:
-            k = torch.where(d.valid, k, torch.full_like(k, -1))
+            k = d.data
+        else:
+            k = d.data.to(torch.int64)
+            if d.valid is not None:
+                k = torch.where(d.valid, k, torch.full_like(k, -1))
+        if nd is not None and k is not d.data:
+            # codes index the dictionary: a readback-free key bound (ops/hashing.py key_bound)
+            k._igloo_bound = (-1 if d.valid is not None else 0, max(nd - 1, 0))
         return k, d
     k = _num_key(c)
     if c.valid is not None:

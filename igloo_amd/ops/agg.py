@@ -57,6 +57,17 @@ def grouped_aggregate(gid: Optional[torch.Tensor], ngroups: int, specs: Sequence
     return _cpu(gid, ngroups, specs, n)
 
 
+def _sum_fits(vals: Optional[torch.Tensor], n: int) -> bool:
+    """Every partial and total SUM of these ``n`` values fits in int64, by a
+    bound known without a readback (ops/hashing.py key_bound: the range of
+    the resident column they were gathered from)."""
+    if vals is None or vals.dim() != 1:
+        return False
+    from .hashing import key_bound
+    b = key_bound(vals)
+    return b is not None and n * max(abs(b[0]), abs(b[1])) < 2**62
+
+
 def _narrow_sums(specs, n) -> set:
     """Indices of the integer SUM specs that accumulate in one int64 word (no
     carry word, half the atomics, no "fits" pass afterwards): int32 values,
@@ -101,12 +112,17 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
             launch("agg_update")
             N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s, bool(sorted_gids))
     # one host sync for every 128-bit integer SUM's "fits in int64" check
-    wide = [(dst, dst2) for op, dst, dst2 in posts if op == "sum_int" and dst2 is not None]
+    # (none for a SUM whose input has a readback-free bound proving it fits)
+    known = {si for si, (op, vals, _v) in enumerate(specs) if op == "sum_int" and posts[si][2] is not None
+             and _sum_fits(vals, n)}
+    wide = [(dst, dst2) for si, (op, dst, dst2) in enumerate(posts)
+            if op == "sum_int" and dst2 is not None and si not in known]
     fits = [1 - f for f in to_host_ints(_wide_flags(wide))] if wide else []
     fit_iter = iter(fits)
-    for op, dst, dst2 in posts:
+    for si, (op, dst, dst2) in enumerate(posts):
         if op == "sum_int":
-            outs.append(dst if dst2 is None or next(fit_iter) else torch.stack([dst, dst2], dim=1))
+            ok = dst2 is None or si in known or next(fit_iter)
+            outs.append(dst if ok else torch.stack([dst, dst2], dim=1))
         elif op in ("min_f64", "max_f64"):
             # empty groups keep the int64 sentinel: report +/-inf like the CPU path
             sentinel = I64_MAX if op == "min_f64" else I64_MIN

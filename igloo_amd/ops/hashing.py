@@ -89,8 +89,13 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
 def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
     """An interval holding every key, known without a readback in steady
     state: the (remembered) range of the resident column the keys were
-    gathered from. Looser than ``key_range`` for a filtered subset; callers
-    use it where a bound suffices (direct-mapped table spans, bit widths)."""
+    gathered from, or a bound its producer attached (``_igloo_bound``:
+    dictionary codes lie in [0, dictionary size)). Looser than ``key_range``
+    for a filtered subset; callers use it where a bound suffices
+    (direct-mapped table spans, bit widths, overflow-free sums)."""
+    b = getattr(keys, "_igloo_bound", None)
+    if b is not None:
+        return b
     o = _origin(keys)
     if o is None or o.dtype != keys.dtype or o.dim() != 1:
         return None
@@ -605,6 +610,7 @@ def group_ids_ex(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor, b
             g = starts.numel()
             gid = torch.empty(n, dtype=torch.int32, device=keys.device)
             launch("fill_runs").fill_runs(ptr(starts), starts.dtype == torch.int64, g, n, ptr(gid), stream(keys))
+            gid._igloo_bound = (0, max(g - 1, 0))
             return gid, g, starts.to(torch.int32), True
     gid, g, rep = group_ids(keys)
     return gid, g, rep, False
@@ -628,6 +634,8 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
     bnd = key_bound(keys)
     if bnd is not None and bnd[1] - bnd[0] + 1 <= 2 * n + 65536:
         kmin, kmax = bnd         # resident-derived bound already direct: no range readback
+    elif getattr(keys, "_igloo_hashed", False) and n > 1:
+        kmin, kmax = 0, 2**62    # 64-bit hashes: the hash table, no range readback
     else:
         kmin, kmax = key_range(keys)
     span = kmax - kmin + 1
@@ -660,12 +668,13 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
         first = rep.clamp(max=n - 1).long()        # in bounds even under a mismatched replay
         mark = torch.zeros(n, dtype=torch.bool, device=dev)
         mark.index_fill_(0, first, True)
-        order = mask_to_indices(mark)
+        order = mask_to_indices(mark, total=g)     # g marks: no count readback
         newpos = torch.zeros(n, dtype=torch.int32, device=dev)
         newpos.index_copy_(0, order.long(), torch.arange(order.numel(), dtype=torch.int32, device=dev))
         remap = newpos.index_select(0, first)
         gid = gather_tensor(remap, gid)
         rep = order.to(torch.int32)
+    gid._igloo_bound = (0, max(g - 1, 0))     # readback-free bound for packing / regrouping
     return gid, g, rep
 
 
@@ -743,7 +752,7 @@ def pack_keys(cols: Sequence[torch.Tensor]) -> torch.Tensor:
     if len(cols) == 1:
         c = cols[0]
         return c if c.dtype in (torch.int32, torch.int64) else c.to(torch.int64)
-    ranges = key_ranges(cols)
+    ranges = _bounded_ranges(cols)
     bits = [max(1, int(hi - lo).bit_length()) for lo, hi in ranges]
     if sum(bits) <= 62:
         return _pack_bits(cols, ranges, bits)
@@ -764,7 +773,7 @@ def pack_keys_pair(left: Sequence[torch.Tensor], right: Sequence[torch.Tensor]) 
     if is_gpu(left[0]) and len(left) <= MAX_PACK_BITS:
         # one shared bit layout from both sides' ranges: each side packed in
         # place, no concatenated copies
-        both = key_ranges(list(left) + list(right))      # one readback for both sides
+        both = _bounded_ranges(list(left) + list(right))      # at most one readback for both sides
         rl, rr = both[:len(left)], both[len(left):]
         if right[0].numel() == 0:
             ranges = rl
@@ -814,6 +823,24 @@ def key_ranges(cols: Sequence[torch.Tensor]) -> List[Tuple[int, int]]:
         for j, i in enumerate(todo):
             lo, hi = vals[2 * j], vals[2 * j + 1]
             out[i] = (lo, hi) if lo <= hi else (0, 0)
+    return out  # type: ignore[return-value]
+
+
+def _bounded_ranges(cols: Sequence[torch.Tensor]) -> List[Tuple[int, int]]:
+    """Per column an interval holding all its values: the readback-free
+    bound where one is known (``key_bound``), else the exact range (read
+    back together for all such columns). Packing needs no more than that."""
+    out: List[Optional[Tuple[int, int]]] = [None] * len(cols)
+    todo = []
+    for i, c in enumerate(cols):
+        b = key_bound(c) if is_gpu(c) and c.numel() else None
+        if b is not None:
+            out[i] = b
+        else:
+            todo.append(i)
+    if todo:
+        for i, r in zip(todo, key_ranges([cols[i] for i in todo])):
+            out[i] = r
     return out  # type: ignore[return-value]
 
 

@@ -1,15 +1,16 @@
 """Stream compaction and prefix sums (csrc/kernels/select.hip, scan.hip)."""
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
 from ._lib import idx_dtype, is_gpu, launch, ptr, stream, to_host_int
 
 
-def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
-    """Ordered indices of the True entries of a bool mask (int32 when they fit)."""
+def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Tensor:
+    """Ordered indices of the True entries of a bool mask (int32 when they fit).
+    ``total``: the caller knows how many are set (no count readback)."""
     assert mask.dtype == torch.bool and mask.dim() == 1
     n = mask.numel()
     it = idx_dtype(n)
@@ -21,7 +22,8 @@ def mask_to_indices(mask: torch.Tensor) -> torch.Tensor:
     ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
     s = stream(mask)
     N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
-    total = to_host_int(ws[tiles:])
+    if total is None:
+        total = to_host_int(ws[tiles:])
     out = torch.empty(total, dtype=it, device=mask.device)
     if total:
         N.select_write(ptr(mask), n, ptr(ws), ptr(out), it == torch.int64, total, s)

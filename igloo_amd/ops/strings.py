@@ -489,6 +489,7 @@ def hash64(col: Column) -> torch.Tensor:
                             dtype=torch.int64)
     out = torch.empty(n, dtype=torch.int64, device=col.device)
     launch("str_hash64").str_hash64(ptr(col.offsets), ptr(col.data), n, ptr(col.valid), ptr(out), stream(out))
+    out._igloo_hashed = True     # spread over 64 bits: group_ids goes straight to its hash table
     return out
 
 

@@ -128,5 +128,11 @@ def test_overflow_checked_product_raises(monkeypatch):
                     "b": pa.array([Decimal("9999999999999.99")] * 10, pa.decimal128(15, 2))})
     g = ig.QueryEngine(device="cuda:0")
     g.register_table("t", big)
-    with pytest.raises(Exception, match="overflow"):
-        g.sql("SELECT a * b AS x FROM t")
+    # every execution mode raises: recorded, replayed readbacks and (had the
+    # query reached it) a graph -- the flag rides on the result's host copy
+    for _ in range(4):
+        with pytest.raises(Exception, match="overflow"):
+            g.sql("SELECT a * b AS x FROM t")
+    # and a query whose guard stays clear returns its rows in every mode
+    for _ in range(4):
+        assert g.sql("SELECT a * 2 AS x FROM t").table.num_rows == 10
