@@ -86,6 +86,12 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
     return column_stats(keys, valid)[0]
 
 
+#: below this many keys a readback-free bound that rules out the direct table
+#: is trusted (hash table, no range readback); above it the exact range is read,
+#: since a filtered subset may still fit a direct table (far cheaper at size)
+BOUND_TRUST_ROWS = 1 << 20
+
+
 def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
     """An interval holding every key, known without a readback in steady
     state: the (remembered) range of the resident column the keys were
@@ -157,7 +163,7 @@ class JoinTable:
             # a resident-derived bound that already selects the direct table
             # (the exact range could only narrow it): no range readback
             bnd = key_bound(keys)
-            if bnd is not None and self._direct_for(bnd[1] - bnd[0] + 1, n):
+            if bnd is not None and (self._direct_for(bnd[1] - bnd[0] + 1, n) or n < BOUND_TRUST_ROWS):
                 rng = bnd
         if rng is None:
             rng = key_range(keys, valid)
@@ -632,8 +638,8 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
         rep = torch.full((g,), n, dtype=torch.int64).scatter_reduce(0, inv, torch.arange(n), reduce="amin")
         return inv.to(torch.int32), g, rep.to(torch.int32)
     bnd = key_bound(keys)
-    if bnd is not None and bnd[1] - bnd[0] + 1 <= 2 * n + 65536:
-        kmin, kmax = bnd         # resident-derived bound already direct: no range readback
+    if bnd is not None and (bnd[1] - bnd[0] + 1 <= 2 * n + 65536 or n < BOUND_TRUST_ROWS):
+        kmin, kmax = bnd         # a readback-free bound decides: no range readback
     elif getattr(keys, "_igloo_hashed", False) and n > 1:
         kmin, kmax = 0, 2**62    # 64-bit hashes: the hash table, no range readback
     else:

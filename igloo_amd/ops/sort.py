@@ -52,6 +52,18 @@ def _ordered_f32(x: float) -> int:
 
 def _fields(keys: Sequence[SortKey]) -> List[tuple]:
     """Per column: (tensor, valid, lo, span, kind, width, bits, desc, nulls_first). One host sync for all bounds."""
+    from .hashing import key_bound
+    known = []
+    for v, _desc, _nf, valid in keys:
+        b = key_bound(v) if valid is None and v.numel() and is_gpu(v) and v.dtype in (torch.int32, torch.int64) \
+            else None
+        if b is None and v.numel():
+            break
+        known.extend(b if b is not None else (0, 0))
+    else:
+        # every key has a readback-free bound (resident origin, dictionary
+        # codes, group ids): a wider field than the exact range, same order
+        return _fields_from(keys, known)
     stats = []
     for v, _desc, _nf, _valid in keys:
         if v.numel() == 0:
@@ -70,6 +82,10 @@ def _fields(keys: Sequence[SortKey]) -> List[tuple]:
         else:
             stats.append(torch.stack([mn.to(torch.int64), mx.to(torch.int64)]))
     vals = to_host_ints(torch.cat(stats)) if stats else []
+    return _fields_from(keys, vals)
+
+
+def _fields_from(keys: Sequence[SortKey], vals: Sequence[int]) -> List[tuple]:
     out = []
     for i, (v, desc, nf, valid) in enumerate(keys):
         if v.dtype not in _KIND:
