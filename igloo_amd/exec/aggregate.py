@@ -571,6 +571,14 @@ def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] =
         for (ci, _), c in zip(groups, taken):
             if c is not None:
                 out[ci.cid] = c
+        if len(groups) == 1 and taken[0] is not None and not getattr(taken[0], "pending", False) \
+                and taken[0].valid is None and not taken[0].is_plain_string:
+            # one row per group: a single key's values are distinct (a join
+            # building on them skips its duplicate check, ops/hashing.py key_unique)
+            try:
+                taken[0].data._igloo_distinct = True
+            except (AttributeError, RuntimeError):
+                pass
     if late is not None and row_parts:
         for cid, k in row_parts.items():
             idx = b.parts[k][1]

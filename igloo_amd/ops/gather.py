@@ -149,6 +149,8 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
         descs.append((_src_ptr(c.data), ptr(data), esz, _src_ptr(c.valid), ptr(valid)))
         if not neg:
             _inherit(data, c.data)
+            if getattr(idx, "_igloo_incr", False) and getattr(c.data, "_igloo_distinct", False):
+                data._igloo_distinct = True
         out.append(Column(c.dtype, data, valid, dictionary=c.dictionary))
     if gpu and descs and n:
         N = launch("gather_multi")

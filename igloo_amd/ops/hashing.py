@@ -115,9 +115,12 @@ def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
 
 def key_unique(keys: torch.Tensor) -> bool:
     """True only when the keys are known distinct with no readback in steady
-    state: distinct rows (a resident column, or a filtered scan's rows of one,
+    state: a single GROUP BY key (``_igloo_distinct``, kept through filters
+    that select rows in order, ops/gather.py take_many), distinct rows (a resident column, or a filtered scan's rows of one,
     in row order) of a resident column whose values are unique (checked once
     and remembered on it)."""
+    if getattr(keys, "_igloo_distinct", False):
+        return True
     if getattr(keys, "_igloo_resident", False):
         o = keys
     else:

@@ -15,7 +15,9 @@ def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Te
     n = mask.numel()
     it = idx_dtype(n)
     if not is_gpu(mask):
-        return torch.nonzero(mask).flatten().to(it)
+        out = torch.nonzero(mask).flatten().to(it)
+        out._igloo_incr = True
+        return out
     mask = mask.contiguous()
     N = launch("select")
     tiles = N.select_num_tiles(n)
@@ -27,6 +29,7 @@ def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Te
     out = torch.empty(total, dtype=it, device=mask.device)
     if total:
         N.select_write(ptr(mask), n, ptr(ws), ptr(out), it == torch.int64, total, s)
+    out._igloo_incr = True       # strictly increasing: gathers by it keep distinct rows distinct
     return out
 
 
