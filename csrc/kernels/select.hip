@@ -4,11 +4,18 @@
 // (reference crates/engine/src/operators/filter.rs:57). Three launches:
 //   1. per-tile popcount of the mask (32 bytes per lane, two uint4 loads),
 //   2. exclusive scan of the tile counts (one workgroup),
-//   3. per-tile rewrite: ballot-ranked rows staged in LDS (conflict-free:
-//      one row per lane, consecutive words), then streamed out with
-//      contiguous (coalesced) stores; output order equals input order
-//      (stable). (Writing the ballot-ranked runs straight to global memory
-//      without the LDS stage measured 56 us/call against 35 us.)
+//   3. per-tile rewrite: each lane expands its 32 flags at its block-scan
+//      offset into an LDS staging buffer, then the workgroup streams the
+//      tile's indices out with contiguous (coalesced) stores; output order
+//      equals input order (stable). (A variant without the LDS stage — one
+//      ballot-ranked output run per 256 rows, no bank conflicts — measured
+//      56 us/call against 35 us: its per-lane scattered stores cost more than
+//      the staging conflicts, profiles/r3_sf100_pmc_roofline.txt. A
+//      conflict-free LDS stage -- one row per lane per step, ballot-ranked
+//      into consecutive words -- took the conflicts from 150M to 0 but needs
+//      byte loads of the mask and ran 12-28 % slower: 0.445 vs 0.357 ms for
+//      a 600M-row mask at 1 %, profiles/r4_select_like_ab.txt. The staging
+//      conflicts are not on this kernel's critical path; the mask stream is.)
 // A tile is kBlock*32 = 8192 rows, so SF100 lineitem (600M rows) launches
 // ~73k workgroups: far more than 256 CUs x occupancy, as the HBM stream wants.
 #include "common.h"
@@ -128,51 +135,34 @@ __global__ __launch_bounds__(1024) void scan_counts_kernel(int64_t* __restrict__
 
 namespace {
 
-// Each wave owns a contiguous 2048-row quarter of the tile and walks it 64
-// rows at a time, one row per lane: a ballot ranks the set rows (mbcnt), so
-// the lanes of one step stage their rows in CONSECUTIVE LDS words -- no bank
-// conflicts (the per-lane 32-row expansion this replaces staged at a stride of
-// 32 rows: 150M conflict cycles per SF100 suite, profiles/r3_sf100_pmc_roofline.txt).
-// The quarters are in row order, so the block writes them out back to back.
 template <typename IdxT>
 __global__ __launch_bounds__(kBlock) void tile_write_kernel(const uint8_t* __restrict__ mask, int64_t n,
                                                            const int64_t* __restrict__ offsets,
                                                            IdxT* __restrict__ out, int64_t cap) {
-  constexpr int kWaveRows = kTile / kWavesPerBlock;
-  constexpr int kSteps = kWaveRows / kWave;
-  __shared__ int32_t stage[kTile];          // tile-relative rows in output order, one segment per wave
-  __shared__ int32_t wtot[kWavesPerBlock];
+  __shared__ int64_t scratch[kWavesPerBlock + 1];
+  __shared__ uint16_t stage[kTile];  // row offsets inside the tile, in output order
   const int64_t tile_base = (int64_t)blockIdx.x * kTile;
-  const int w = threadIdx.x / kWave, l = lane_id();
-  const int seg = w * kWaveRows;
-  const int64_t row0 = tile_base + seg + l;
-  uint8_t f[kSteps];
-  if (tile_base + kTile <= n) {
+  const int first = threadIdx.x * kItems;
+  uint32_t w[kItems / 4];
+  load_flags(mask, tile_base + first, n, w);
+  int64_t c = 0;
 #pragma unroll
-    for (int k = 0; k < kSteps; ++k) f[k] = mask[row0 + k * kWave];
-  } else {
+  for (int q = 0; q < kItems / 4; ++q) c += __popc(w[q]);
+  int64_t total;
+  int pos = (int)block_exclusive_scan(c, scratch, &total);
 #pragma unroll
-    for (int k = 0; k < kSteps; ++k) f[k] = row0 + k * kWave < n ? mask[row0 + k * kWave] : 0;
-  }
-  int run = 0;
+  for (int q = 0; q < kItems / 4; ++q)
 #pragma unroll
-  for (int k = 0; k < kSteps; ++k) {
-    const uint64_t bal = __ballot(f[k] != 0);
-    if (f[k]) stage[seg + run + lane_prefix(bal)] = seg + k * kWave + l;
-    run += __popcll(bal);
-  }
-  if (l == 0) wtot[w] = run;
+    for (int b = 0; b < 4; ++b)
+      if ((w[q] >> (8 * b)) & 1u) stage[pos++] = (uint16_t)(first + 4 * q + b);
   __syncthreads();
-  int woff = 0;
-#pragma unroll
-  for (int v = 0; v < kWavesPerBlock; ++v) woff += v < w ? wtot[v] : 0;
   // writes stay inside the caller's buffer of ``cap`` entries, and the last
   // tile zero-fills [total, cap): a size the host replayed instead of reading
   // (ops/_lib.py Speculation) can then never make this kernel or a consumer of
   // the indices touch memory out of bounds before the replay is validated
-  const int64_t o = offsets[blockIdx.x] + woff;
-  for (int k = l; k < run; k += kWave)
-    if (o + k < cap) out[o + k] = (IdxT)(tile_base + stage[seg + k]);
+  const int64_t o = offsets[blockIdx.x];
+  for (int k = threadIdx.x; k < (int)total; k += kBlock)
+    if (o + k < cap) out[o + k] = (IdxT)(tile_base + stage[k]);
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t p = offsets[gridDim.x] + threadIdx.x; p < cap; p += kBlock) out[p] = (IdxT)0;
 }

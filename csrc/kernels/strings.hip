@@ -120,7 +120,10 @@ __global__ __launch_bounds__(kBlock) void like_tile_kernel(const int64_t* __rest
 // (A variant that prefetches the next tile into registers while matching the
 // current one, with the chunk tail taken by a lane shuffle, measured 6.2 ms
 // against this kernel's 5.0 ms for Q13 at SF100: the extra registers cost
-// more occupancy than the overlap gained.)
+// more occupancy than the overlap gained. Removing the LDS bank conflicts --
+// the window's fifth dword from the neighbouring lane, mask pairs stored as
+// one dword -- took them from 54M to 0.2M per suite but ran 3 % slower:
+// profiles/r4_select_like_ab.txt.)
 constexpr int kSegMax = 4;
 
 __device__ inline int next_hit(const uint64_t* bits, int from, int last) {
@@ -180,14 +183,7 @@ __global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restri
       const int nchunks = ((len + 63) >> 6) * 4;
       for (int j = threadIdx.x; j < nchunks; j += BLOCK) {
         const uint4 v = *(const uint4*)(buf + j * 16);
-        // the window's fifth dword is the next chunk's first: taken from the
-        // neighbouring lane (a strided LDS dword read here was an 8-way bank
-        // conflict per wave); the wave's last active lane reads it from LDS.
-        // nchunks is a multiple of 4, so lane pairs below are always complete.
-        const int l = threadIdx.x & (kWave - 1);
-        const uint32_t nx = __shfl_down(v.x, 1);
-        const uint32_t d[5] = {v.x, v.y, v.z, v.w,
-                               (l < kWave - 1 && j + 1 < nchunks) ? nx : *(const uint32_t*)(buf + j * 16 + 16)};
+        const uint32_t d[5] = {v.x, v.y, v.z, v.w, *(const uint32_t*)(buf + j * 16 + 16)};
         for (int sg = 0; sg < nseg; ++sg) {
           const int s0 = soff[sg], sl = soff[sg + 1] - s0;
           const int pl = sl < 4 ? sl : 4;
@@ -213,10 +209,7 @@ __global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restri
                 }
             }
           }
-          // pairs of 16-bit masks leave as one dword from the even lane:
-          // consecutive lanes' halfword stores shared a bank word
-          const uint32_t mo = __shfl_down(m, 1);
-          if ((l & 1) == 0) ((uint32_t*)bits[sg])[j >> 1] = (m & 0xffffu) | (mo << 16);
+          ((uint16_t*)bits[sg])[j] = (uint16_t)m;
         }
       }
     }
