@@ -40,21 +40,53 @@ __global__ __launch_bounds__(kBlock) void tile_scan_kernel(const T* __restrict__
                                                           const int64_t* __restrict__ tile_off,
                                                           int64_t* __restrict__ out) {
   __shared__ int64_t scratch[kWavesPerBlock + 1];
-  // each lane owns kItems consecutive rows
-  int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+  // each lane owns kItems consecutive rows, moved with 16-byte loads and
+  // stores when whole and aligned (8 scalar accesses at a 32/64-byte lane
+  // stride otherwise)
+  static_assert(kItems == 8, "vector path assumes 8 items per lane");
+  const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+  const bool whole = base + kItems <= n && (((uintptr_t)(in + base)) & 15) == 0 &&
+                     (((uintptr_t)(out + base)) & 15) == 0;
   int64_t v[kItems];
+  if (whole) {
+    if (sizeof(T) == 4) {
+      const uint4 a = reinterpret_cast<const uint4*>(in + base)[0], b = reinterpret_cast<const uint4*>(in + base)[1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int j = 0; j < kItems; ++j) v[j] = (int64_t)(int32_t)w[j];
+    } else {
+#pragma unroll
+      for (int q = 0; q < kItems / 2; ++q) {
+        const longlong2 x = reinterpret_cast<const longlong2*>(in + base)[q];
+        v[2 * q] = x.x;
+        v[2 * q + 1] = x.y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) v[j] = base + j < n ? (int64_t)in[base + j] : 0;
+  }
   int64_t s = 0;
 #pragma unroll
-  for (int j = 0; j < kItems; ++j) {
-    v[j] = base + j < n ? (int64_t)in[base + j] : 0;
-    s += v[j];
-  }
+  for (int j = 0; j < kItems; ++j) s += v[j];
   int64_t total;
   int64_t run = tile_off[blockIdx.x] + block_exclusive_scan(s, scratch, &total);
+  if (whole) {
 #pragma unroll
-  for (int j = 0; j < kItems; ++j) {
-    if (base + j < n) out[base + j] = run;
-    run += v[j];
+    for (int q = 0; q < kItems / 2; ++q) {
+      longlong2 x;
+      x.x = run;
+      run += v[2 * q];
+      x.y = run;
+      run += v[2 * q + 1];
+      reinterpret_cast<longlong2*>(out + base)[q] = x;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      if (base + j < n) out[base + j] = run;
+      run += v[j];
+    }
   }
 }
 

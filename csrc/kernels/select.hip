@@ -108,8 +108,19 @@ __global__ __launch_bounds__(1024) void scan_counts_kernel(int64_t* __restrict__
   const int t = threadIdx.x;
   int64_t per = (n + 1023) / 1024;
   int64_t lo = t * per, hi = lo + per < n ? lo + per : n;
+  // eight independent loads in flight per step (a 600M-row mask has 73K
+  // tiles: 72 counts per lane, which one load at a time left latency-bound)
+  constexpr int kU = 8;
   int64_t s = 0;
-  for (int64_t i = lo; i < hi; ++i) s += counts[i];
+  int64_t i = lo;
+  for (; i + kU <= hi; i += kU) {
+    int64_t v[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) v[k] = counts[i + k];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) s += v[k];
+  }
+  for (; i < hi; ++i) s += counts[i];
   // block scan over 1024 threads (16 waves)
   int64_t inc = wave_inclusive_scan(s);
   if (lane_id() == kWave - 1) part[t / kWave] = inc;
@@ -125,7 +136,17 @@ __global__ __launch_bounds__(1024) void scan_counts_kernel(int64_t* __restrict__
   }
   __syncthreads();
   int64_t run = inc - s + part[t / kWave];
-  for (int64_t i = lo; i < hi; ++i) {
+  for (i = lo; i + kU <= hi; i += kU) {
+    int64_t v[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) v[k] = counts[i + k];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      counts[i + k] = run;
+      run += v[k];
+    }
+  }
+  for (; i < hi; ++i) {
     int64_t c = counts[i];
     counts[i] = run;
     run += c;

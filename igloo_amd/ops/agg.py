@@ -189,9 +189,12 @@ def wide_to_python(t: torch.Tensor) -> List[int]:
     return out
 
 
-def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torch.Tensor] = None) -> torch.Tensor:
+def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torch.Tensor] = None,
+                  sparse: bool = False) -> torch.Tensor:
     """int64 counts[span]: rows per key value kmin + i (NULL / out-of-domain keys skipped).
-    GPU: 32-bit atomics straight from the key column (csrc/kernels/agg.hip)."""
+    GPU: 32-bit atomics straight from the key column (csrc/kernels/agg.hip).
+    ``sparse``: few rows are valid -- always the direct atomic kernel (the
+    radix-partitioned one pays its fixed passes for the many)."""
     if keys.device.type == "cpu" or keys.numel() >= 2**31:   # (int32 counters)
         k = keys.to(torch.int64) - kmin
         ok = (k >= 0) & (k < span)
@@ -202,7 +205,7 @@ def key_histogram(keys: torch.Tensor, kmin: int, span: int, valid: Optional[torc
     keys = keys.contiguous()
     n = keys.numel()
     # (int32 scatter positions: n < 2^31 is guaranteed by the bincount branch above)
-    if HIST_PARTITIONED and (1 << 22) <= n < 2**31 - 1 and (1 << 16) <= span <= (1 << 27):
+    if HIST_PARTITIONED and not sparse and (1 << 22) <= n < 2**31 - 1 and (1 << 16) <= span <= (1 << 27):
         return _key_histogram_partitioned(keys, kmin, span, valid)
     counts = torch.zeros(span, dtype=torch.int32, device=keys.device)
     launch("key_histogram").key_histogram(ptr(keys), keys.dtype == torch.int64,

@@ -33,6 +33,20 @@ def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Te
     return out
 
 
+def count_true(mask: torch.Tensor) -> int:
+    """Number of True entries of a bool mask (one count pass, one readback)."""
+    assert mask.dtype == torch.bool and mask.dim() == 1
+    n = mask.numel()
+    if not is_gpu(mask):
+        return int(mask.sum().item())
+    mask = mask.contiguous()
+    N = launch("select")
+    tiles = N.select_num_tiles(n)
+    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
+    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, stream(mask))
+    return to_host_int(ws[tiles:])
+
+
 def exclusive_scan(counts: torch.Tensor, host_total: bool = True):
     """int32/int64 counts -> (int64 exclusive offsets, total). ``host_total``
     False: the total stays a 1-element device tensor (no readback)."""

@@ -57,6 +57,13 @@ def main():
             ms = timed(lambda: mask_to_indices(mask, total=ref.numel()))
             print(f"[{a.tag}] select n={n} sel={sel}: {ms:.3f} ms", flush=True)
         del u
+    from igloo_amd.ops.select import exclusive_scan
+    for n in (100_000_000, 10_000_000):
+        c = torch.randint(0, 4, (n,), device=dev, dtype=torch.int32, generator=g)
+        ex, tot = exclusive_scan(c)
+        assert tot == int(c.sum()) and int(ex[-1]) == tot - int(c[-1]), "scan mismatch"
+        ms = timed(lambda: exclusive_scan(c, host_total=False))
+        print(f"[{a.tag}] scan n={n}: {ms:.3f} ms", flush=True)
     torch.cuda.empty_cache()
     from igloo_amd.models.tpch import datagen
     e = ig.QueryEngine(device=dev)
