@@ -349,11 +349,18 @@ class HashAggExec(ExecNode):
         the shape differs."""
         rnode = self.children[0].children[1]
         if ctx.budget is not None or not isinstance(rnode, ScanExec) or rnode.predicate is None \
-                or not EAGER_COUNT_MASKED or any(getattr(a.arg, "nullable", True) for _, a in lg.aggs) \
-                or not isinstance(rkey, ColRef):
+                or not EAGER_COUNT_MASKED or not isinstance(rkey, ColRef) \
+                or any(not isinstance(a.arg, ColRef) for _, a in lg.aggs):
             return None
         ev = ctx.evaluator
         raw = rnode.peek_raw(ctx)
+        for _, a in lg.aggs:
+            # COUNT(x) counts the same rows as the key histogram when x holds
+            # no NULLs: a NOT NULL column, or one declared nullable that has no
+            # validity (Parquet fields are nullable by default)
+            c = raw.columns.get(a.arg.cid)
+            if getattr(a.arg, "nullable", True) and (c is None or c.valid is not None):
+                return None
         rcol = raw.columns.get(rkey.cid)
         lcol = ev.column(lkey, lb)
         if rcol is None or rcol.dtype.is_string or lcol.dtype.is_string or rcol.is_dict \

@@ -560,6 +560,10 @@ def hash_join(lb: Batch, rb: Batch, kind: str, on, residual, ctx, null_aware=Fal
             lk = gather_tensor(lk, keep)
             lvalid = None
             n_l = lb.num_rows
+        # no NULL is left on either side (or the build side is empty): NOT IN
+        # is a plain anti join from here, and the faster anti-join paths apply
+        # (Parquet columns are declared nullable even when they hold no NULL)
+        null_aware = False
     if dev.type == "cuda" and len(on) == 1 and kind in ("semi", "anti") and residual is None and not null_aware \
             and not ctx.spmd:
         out = _semi_by_index_marks(lb, lk, lvalid, rk, rvalid, kind, ctx)

@@ -162,13 +162,15 @@ def test_index_paths_default_thresholds(gpu_device, qi, monkeypatch):
     assert res["cpu"] == res[gpu_device]
 
 
+@pytest.mark.parametrize("nullable", [False, True])
 @pytest.mark.parametrize("pred", ["bv <> 5", "bv = 5", "bv > -90"])
-def test_eager_count_masked_complement(gpu_device, monkeypatch, pred):
+def test_eager_count_masked_complement(gpu_device, monkeypatch, pred, nullable):
     """Q13 shape (LEFT JOIN ... COUNT per left key over a filtered resident
     right scan): a filter most rows pass subtracts the failing rows' per-key
     counts from the column's remembered histogram (exec/aggregate.py
     _full_key_hist); a selective one histograms the passing rows. Both equal
-    the CPU engine's plain join + aggregate."""
+    the CPU engine's plain join + aggregate. ``nullable``: columns declared
+    nullable without any NULL (as Parquet files declare them) take the path too."""
     from igloo_amd.exec import aggregate as AG
     calls = []
     real = AG._full_key_hist
@@ -177,7 +179,7 @@ def test_eager_count_masked_complement(gpu_device, monkeypatch, pred):
     n_big, n_small = 300_000, 40_000
     big = pa.table({"bk": pa.array(r.integers(1, n_small, n_big), pa.int64()),
                     "bv": pa.array(r.integers(-100, 100, n_big), pa.int64())},
-                   schema=pa.schema([pa.field("bk", pa.int64(), False), pa.field("bv", pa.int64(), False)]))
+                   schema=pa.schema([pa.field("bk", pa.int64(), nullable), pa.field("bv", pa.int64(), nullable)]))
     small = pa.table({"sk": pa.array(np.arange(n_small), pa.int64())},
                      schema=pa.schema([pa.field("sk", pa.int64(), False)]))
     sql = (f"SELECT c, count(*) AS n FROM (SELECT sk, count(bv) AS c FROM small LEFT JOIN big "
