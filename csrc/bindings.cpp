@@ -479,6 +479,9 @@ PYBIND11_MODULE(_native, m) {
     kern::str_substr_copy(P<const int64_t>(off), P<const uint8_t>(chars), n, start, len, has_len,
                           P<const int64_t>(new_off), P<uint8_t>(out), S(s));
   });
+  m.def("mark_slot_rows", [](uintptr_t trow, int64_t cap, int64_t n, uintptr_t mark, uintptr_t s) {
+    kern::mark_slot_rows(P<const int32_t>(trow), cap, n, P<uint8_t>(mark), S(s));
+  });
   m.def("pack_bits", [](std::vector<uintptr_t> cols, std::vector<bool> is64, std::vector<int64_t> lo,
                         std::vector<int> shift, int64_t n, uintptr_t out, uintptr_t s) {
     std::vector<const void*> c(cols.size());

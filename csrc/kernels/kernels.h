@@ -73,6 +73,7 @@ void pack_bits(const void* const* cols, const bool* is64, const int64_t* lo, con
                int64_t* out, hipStream_t stream);
 void differs_from_rep(const void* a, int elem_bytes, const void* rep, bool rep64, int64_t n, int* flag,
                       hipStream_t stream);
+void mark_slot_rows(const int32_t* trow, int64_t cap, int64_t n, uint8_t* mark, hipStream_t stream);
 void mark_keys(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t dom,
                uint8_t* marks, hipStream_t stream);
 void probe_marks(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t base, int64_t dom,

@@ -397,6 +397,24 @@ void pack_bits(const void* const* cols, const bool* is64, const int64_t* lo, con
   check_launch("util.pack_bits", stream);
 }
 
+// mark[trow[s]] = 1 for every occupied slot of a group-by table: the first
+// row of every group (COUNT/SUM(DISTINCT) keep exactly those rows) without
+// assigning group ids or counting the groups.
+__global__ __launch_bounds__(kBlock) void mark_slot_rows_kernel(const int32_t* __restrict__ trow, int64_t cap,
+                                                               int64_t n, uint8_t* __restrict__ mark) {
+  for (int64_t s = blockIdx.x * (int64_t)kBlock + threadIdx.x; s < cap; s += (int64_t)gridDim.x * kBlock) {
+    const int32_t r = trow[s];
+    if (r >= 0 && (int64_t)r < n) mark[r] = 1;
+  }
+}
+
+void mark_slot_rows(const int32_t* trow, int64_t cap, int64_t n, uint8_t* mark, hipStream_t stream) {
+  if (cap == 0) return;
+  hipLaunchKernelGGL(mark_slot_rows_kernel, dim3(grid_for(cap, kBlock, 65536)), dim3(kBlock), 0, stream, trow, cap, n,
+                     mark);
+  check_launch("util.mark_slot_rows", stream);
+}
+
 void mark_keys(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t dom,
                uint8_t* marks, hipStream_t stream) {
   if (n == 0) return;

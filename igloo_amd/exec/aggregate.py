@@ -817,10 +817,7 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
         pair = H.pack_keys([gid.to(torch.int64) if gid is not None else torch.zeros(n, dtype=torch.int64, device=dev), k])
         keep_rows = torch.ones(n, dtype=torch.bool, device=dev) if valid is None else valid
         if n:
-            _, _, rep = H.group_ids(pair)
-            first = torch.zeros(n, dtype=torch.bool, device=dev)
-            first.index_fill_(0, rep.long(), True)
-            keep_rows = keep_rows & first
+            keep_rows = keep_rows & H.first_rows_mask(pair)
         valid = keep_rows
     base = len(specs)
 

@@ -687,6 +687,41 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
     return gid, g, rep
 
 
+def first_rows_mask(keys: torch.Tensor) -> torch.Tensor:
+    """bool[n]: True on the first row of every distinct key (the rows
+    COUNT/SUM(DISTINCT) keep). GPU: the group-by table's build pass (which
+    keeps each group's smallest row) and one pass over its slots -- no group
+    ids, no group count readback, no renumbering."""
+    keys = _keys_ok(keys)
+    n = keys.numel()
+    dev = keys.device
+    if n == 0 or not is_gpu(keys):
+        mark = torch.zeros(n, dtype=torch.bool, device=dev)
+        if n:
+            _, _, rep = group_ids(keys)
+            mark[rep.long()] = True
+        return mark
+    bnd = key_bound(keys)
+    if bnd is not None and (bnd[1] - bnd[0] + 1 <= 2 * n + 65536 or n < BOUND_TRUST_ROWS):
+        kmin, kmax = bnd
+    elif getattr(keys, "_igloo_hashed", False) and n > 1:
+        kmin, kmax = 0, 2**62
+    else:
+        kmin, kmax = key_range(keys)
+    span = kmax - kmin + 1
+    direct = span <= 2 * n + 65536 and span < 2**31 - 1
+    cap = span if direct else _next_pow2(2 * n)
+    s = stream(keys)
+    trow = torch.full((cap,), INT32_MAX, dtype=torch.int32, device=dev)
+    tkeys = (torch.empty(1, dtype=torch.int64, device=dev) if direct
+             else torch.full((cap,), EMPTY_KEY, dtype=torch.int64, device=dev))
+    launch("groupby").groupby_build(ptr(keys), keys.dtype == torch.int64, n, ptr(tkeys), ptr(trow), cap, kmin,
+                                    direct, s)
+    mark = torch.zeros(n, dtype=torch.bool, device=dev)
+    launch("mark_slot_rows").mark_slot_rows(ptr(trow), cap, n, ptr(mark), s)
+    return mark
+
+
 HLL_BITS = 12
 HLL_M = 1 << HLL_BITS
 

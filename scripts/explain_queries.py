@@ -21,10 +21,17 @@ def main():
     ap.add_argument("--queries", default="10,18")
     ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--lean", action="store_true")
+    ap.add_argument("--parquet", default=None, help="write + register the bench's Parquet dataset here")
     a = ap.parse_args()
     e = ig.QueryEngine(device=a.device)
     t0 = time.time()
-    datagen.register(e, a.sf, lean=a.lean)
+    if a.parquet:
+        from igloo_amd.models.tpch import parquet_gen
+        parquet_gen.write_dataset(a.sf, a.parquet, device=a.device, rank=0, world=1, lean=a.lean)
+        torch.cuda.empty_cache()
+        parquet_gen.register_dataset(e, a.parquet, a.sf, 0, 1, lean=a.lean)
+    else:
+        datagen.register(e, a.sf, lean=a.lean)
     print(f"datagen sf={a.sf} {time.time() - t0:.1f}s", flush=True)
     for q in [int(x) for x in a.queries.split(",")]:
         e.query(queries.QUERIES[q])  # warm
