@@ -50,7 +50,16 @@ def is_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream(t: torch.Tensor) -> int:
+    """Handle of the current HIP stream of ``t``'s device (inside a capture:
+    the capture stream). The raw-handle query skips building a Stream
+    object per launch (~5 us each, ~1000 launches per fresh query suite)."""
+    d = t.device.index
+    if _raw_stream is not None and d is not None:
+        return _raw_stream(d)
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
