@@ -102,7 +102,11 @@ def _raise_deferred(deferred, flags) -> None:
             raise ExecutionError(msg)
 
 
-def _host_columns(cols: List[Column], deferred=None) -> List[Column]:
+class _ReplayMismatch(Exception):
+    """A graph replay's values did not match the device (seen with its result copy)."""
+
+
+def _host_columns(cols: List[Column], deferred=None, guard=None) -> List[Column]:
     """Result columns moved to the host with ONE synchronisation: every device
     buffer (values, validity, offsets, small dictionaries) is copied with a
     non-blocking D2H copy, then the stream is synchronised once (instead of a
@@ -110,6 +114,8 @@ def _host_columns(cols: List[Column], deferred=None) -> List[Column]:
     references a large device dictionary keeps its device path (it decodes
     only the referenced strings on the GPU)."""
     if not any(c.data.is_cuda for c in cols):
+        if guard is not None and int(guard.reshape(-1)[0].item()):
+            raise _ReplayMismatch()
         if deferred is not None:
             _raise_deferred(deferred, deferred[0].tolist())
         return cols
@@ -127,7 +133,10 @@ def _host_columns(cols: List[Column], deferred=None) -> List[Column]:
                       dictionary=move(d) if d is not None else None)
     out = [move(c) for c in cols]
     flags = cpu(deferred[0]) if deferred is not None else None
+    bad = cpu(guard.reshape(-1)[:1]) if guard is not None else None
     torch.cuda.current_stream(next(c.data.device for c in cols if c.data.is_cuda)).synchronize()
+    if bad is not None and int(bad[0]):
+        raise _ReplayMismatch()      # the copied rows are not the query's: the caller re-executes
     if deferred is not None:
         # the query's deferred device error flags ride on the result copy
         _raise_deferred(deferred, flags.tolist())
@@ -382,7 +391,18 @@ class QueryEngine:
         with _trace.Range("query"):
             batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
         if table is None:
-            table = self._to_arrow(batch, plan.schema, bq_names)
+            guard = st.pop("pending_guard", None) if st is not None else None
+            try:
+                table = self._to_arrow(batch, plan.schema, bq_names, guard=guard)
+            except _ReplayMismatch:
+                # a checked graph's replayed values did not match this time:
+                # drop it and run the query again with real readbacks
+                self._graph_mismatch(st)
+                ctx = self.make_context()
+                with _trace.Range("query"):
+                    batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
+                if table is None:
+                    table = self._to_arrow(batch, plan.schema, bq_names)
         dev_metrics = {}
         if gpu:
             ev1.record()
@@ -512,6 +532,13 @@ class QueryEngine:
             if self.graphs_disabled or not self._capture(st, plan):
                 st["graph_aborts"] += 1
             g = st["graph"]
+        if g is not None and g.checked and comm is None:
+            # a verified single-rank graph: launch it and let the result's host
+            # copy carry its mismatch count (one sync per query, not two)
+            g.launch(ctx)
+            self._touch_graph(st)
+            st["pending_guard"] = g.bad
+            return g.batch, "graph", st, None
         if g is not None:
             ok = g.replay(ctx)
             table = None
@@ -580,6 +607,15 @@ class QueryEngine:
         st["log"] = _confirm(st["candidate"], sp.log)
         st["candidate"] = sp.log if st["log"] is None else None
         return batch, "recorded", st, None
+
+    def _graph_mismatch(self, st: dict) -> None:
+        """Drop ``st``'s graph after a replay whose values the device did not
+        confirm; the query re-executes eagerly with real readbacks."""
+        _graphs.STATS["mismatch"] += 1
+        log.warning("query graph: replayed values did not match the device; re-executing")
+        self._set_graph(st, None)
+        st["fails"] += 1
+        st["log"] = st["candidate"] = None
 
     def _capture(self, st: dict, plan: Plan) -> bool:
         """Capture ``plan`` under a replay of ``st``'s recording into a query graph."""
@@ -692,9 +728,9 @@ class QueryEngine:
         from .parallel.slicing import plan_slices
         return plan_slices(plan, self.comm)
 
-    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str]) -> pa.Table:
+    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str], guard=None) -> pa.Table:
         arrays, fields = [], []
-        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None))
+        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None), guard)
         for ci, nm, col in zip(schema, names, host):
             arr = col.to_arrow()
             want = ci.dtype.to_arrow() if ci.dtype.kind != "null" else pa.null()

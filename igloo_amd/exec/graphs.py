@@ -111,6 +111,15 @@ class QueryGraph:
         """Still built from the generated kernels that are loaded now."""
         return self.jit_gen == _jit.generation()
 
+    def launch(self, ctx) -> None:
+        """Launch the graph without waiting for it: the caller checks ``bad``
+        with the result's host copy (engine.py _host_columns), one sync."""
+        self.graph.replay()
+        self.replays += 1
+        STATS["replays"] += 1
+        ctx.rows_scanned = self.rows_scanned
+        ctx.spill = dict(self.spill)
+
     def replay(self, ctx) -> bool:
         """Launch the graph on the current stream; True when every replayed
         value matched the device (one sync)."""
