@@ -532,10 +532,15 @@ class QueryEngine:
             if self.graphs_disabled or not self._capture(st, plan):
                 st["graph_aborts"] += 1
             g = st["graph"]
-        if g is not None and g.checked and comm is None:
-            # a verified single-rank graph: launch it and let the result's host
-            # copy carry its mismatch count (one sync per query, not two)
+        if g is not None and g.checked and (comm is None or g.global_check):
+            # a verified graph: launch it and let the result's host copy carry
+            # its mismatch count (one sync per query, not two). Under SPMD the
+            # count was summed over the ranks inside the graph, so every rank
+            # reads the same value and all re-execute together on a mismatch.
             g.launch(ctx)
+            if comm is not None:
+                comm.calls += g.comm_calls
+                comm.bytes_sent += g.comm_bytes
             self._touch_graph(st)
             st["pending_guard"] = g.bad
             return g.batch, "graph", st, None
