@@ -113,6 +113,11 @@ def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
     return st[0]
 
 
+#: unsorted resident key columns up to this many rows get a one-time
+#: uniqueness check (sorted ones: one adjacent-difference pass at any size)
+UNIQUE_CHECK_MAX_ROWS = 1 << 27
+
+
 def key_unique(keys: torch.Tensor) -> bool:
     """True only when the keys are known distinct with no readback in steady
     state: a single GROUP BY key (``_igloo_distinct``, kept through filters
@@ -131,6 +136,11 @@ def key_unique(keys: torch.Tensor) -> bool:
     u = getattr(o, "_igloo_unique", None)
     if u is None:
         if capturing() or not is_gpu(o) or o.dim() != 1:
+            return False
+        if TABLE_BYTES_LIMIT.get() is not None or (o.numel() > UNIQUE_CHECK_MAX_ROWS and not is_sorted(o)):
+            # under a device budget, or an unsorted column too large for a
+            # one-time group-by pass: not known unique (the build's own
+            # duplicate check decides)
             return False
         with unlogged():     # one-time check of a resident column (ops/_lib.py unlogged)
             n = o.numel()
