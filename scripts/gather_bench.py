@@ -23,8 +23,17 @@ def main():
     ap.add_argument("--src-rows", type=int, default=600_000_000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="gpurun_out/gather_bench.txt")
+    ap.add_argument("--so", default=None, help="load this build of the native extension instead (A/B)")
     a = ap.parse_args()
     import torch
+    if a.so:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("igloo_amd._native", a.so)
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        sys.modules["igloo_amd._native"] = m
+        from igloo_amd.ops import _lib
+        _lib._native = m
     from igloo_amd.columnar import Column
     from igloo_amd import types as T
     from igloo_amd.ops.gather import take_many

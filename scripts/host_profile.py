@@ -31,7 +31,7 @@ def main():
     e = ig.QueryEngine(device="cuda:0")
     datagen.register(e, a.sf)
     from igloo_amd.ops import jit
-    for _ in range(3):      # JIT compiles settle, speculation recordings confirmed
+    for _ in range(5):      # JIT compiles settle, recordings confirmed, graphs captured
         for q in qs:
             e.sql(queries.QUERIES[q])
         jit.wait_all(120)
