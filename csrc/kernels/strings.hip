@@ -146,7 +146,7 @@ __device__ inline int next_hit(const uint64_t* bits, int from, int last) {
 // BLOCK = 64 makes every wave its own workgroup: the three tile barriers are
 // single-wave barriers, and a wave waiting on its tile's loads never holds up
 // the three others' matching (the 256-thread shape syncs all four per tile).
-template <int BLOCK, int TILE>
+template <int BLOCK, int TILE, int SEGS = kSegMax>
 __global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restrict__ off,
                                                          const uint8_t* __restrict__ chars, int64_t n,
                                                          const uint8_t* __restrict__ seg, const int32_t* seg_off,
@@ -154,9 +154,9 @@ __global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restri
                                                          uint8_t* __restrict__ out) {
   constexpr int kSegBits = TILE / 64;  // 64-bit words per segment bitmap
   __shared__ __attribute__((aligned(16))) uint8_t buf[TILE + 64];
-  __shared__ uint64_t bits[kSegMax][kSegBits];
+  __shared__ uint64_t bits[SEGS][kSegBits];
   __shared__ uint8_t sseg[kLikeMaxPattern];
-  __shared__ int32_t soff[kSegMax + 1];
+  __shared__ int32_t soff[SEGS + 1];
   const int total = seg_off[nseg];
   for (int i = threadIdx.x; i < total; i += BLOCK) sseg[i] = seg[i];
   if (threadIdx.x <= nseg) soff[threadIdx.x] = seg_off[threadIdx.x];
@@ -435,8 +435,19 @@ void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, cons
   if (nseg > kSegMax) throw std::runtime_error("str_like_segments: too many segments");
   // (a one-wave-per-workgroup variant with 4 / 8 KB tiles measured slower for
   // Q13 at SF100, 14.6 vs 11.7 ms per query: profiles/r3_ab_like_wave.txt)
-  hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes>), dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock),
-                     0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  // one or two segments (nearly every analytic LIKE): a bitmap sized for
+  // them frees 4-6 KB of LDS per workgroup, one or two more resident
+  // workgroups per CU (-9 % / -10 % for two / one segment,
+  // profiles/r4_select_like_ab.txt)
+  if (nseg <= 1)
+    hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes, 1>), dim3(grid_for(n, kBlock, 256 * 8 * 4)),
+                       dim3(kBlock), 0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  else if (nseg <= 2)
+    hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes, 2>), dim3(grid_for(n, kBlock, 256 * 8 * 4)),
+                       dim3(kBlock), 0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
+  else
+    hipLaunchKernelGGL((like_seg_kernel<kBlock, kLikeTileBytes>), dim3(grid_for(n, kBlock, 256 * 8 * 4)), dim3(kBlock),
+                       0, stream, off, chars, n, seg, seg_off, nseg, anchor_start, anchor_end, negate, out);
   check_launch("str_like_segments", stream);
 }
 
