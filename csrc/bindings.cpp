@@ -672,6 +672,41 @@ PYBIND11_MODULE(_native, m) {
   m.def("partition_ids", [](uintptr_t keys, bool key64, int64_t n, int nparts, uintptr_t out, uintptr_t s) {
     kern::partition_ids(P<const void>(keys), key64, n, nparts, P<int32_t>(out), S(s));
   });
+  m.def("win_scan_tiles", &kern::win_scan_tiles);
+  m.def("win_seg_scan", [](uintptr_t ids, bool ids64, uintptr_t ids2, bool ids2_64, uintptr_t vals, int vkind,
+                           uintptr_t valid, int64_t n, int op, bool reverse, uintptr_t tflag, uintptr_t tval,
+                           uintptr_t out, uintptr_t err, uintptr_t s) {
+    kern::win_seg_scan(P<void>(ids), ids64, P<void>(ids2), ids2_64, P<void>(vals), vkind, P<uint8_t>(valid), n, op,
+                       reverse, P<int>(tflag), P<int64_t>(tval), P<int64_t>(out), P<int>(err), S(s));
+  });
+  m.def("win_bounds", [](int64_t n, uintptr_t ss, uintptr_t se, uintptr_t ps, uintptr_t pe, int unit, int skind,
+                         int64_t soff_i, double soff_f, int ekind, int64_t eoff_i, double eoff_f, uintptr_t key,
+                         bool key_f64, uintptr_t key_valid, bool desc, uintptr_t gnum, uintptr_t gpos,
+                         int64_t ngroups, uintptr_t lo, uintptr_t hi, uintptr_t s) {
+    kern::win_bounds(n, P<int64_t>(ss), P<int64_t>(se), P<int64_t>(ps), P<int64_t>(pe), unit, skind, soff_i, soff_f,
+                     ekind, eoff_i, eoff_f, P<void>(key), key_f64, P<uint8_t>(key_valid), desc, P<int64_t>(gnum),
+                     P<int64_t>(gpos), ngroups, P<int64_t>(lo), P<int64_t>(hi), S(s));
+  });
+  m.def("win_frame_sum", [](uintptr_t psum, bool f64, uintptr_t pcnt, uintptr_t lo, uintptr_t hi, int64_t n,
+                            uintptr_t sum_out, uintptr_t cnt_out, uintptr_t s) {
+    kern::win_frame_sum(P<int64_t>(psum), f64, P<int64_t>(pcnt), P<int64_t>(lo), P<int64_t>(hi), n,
+                        P<int64_t>(sum_out), P<int64_t>(cnt_out), S(s));
+  });
+  m.def("win_frame_minmax", [](uintptr_t vals, bool f64, bool is_max, uintptr_t valid, uintptr_t lo, uintptr_t hi,
+                               int64_t n, uintptr_t out, uintptr_t out_valid, uintptr_t s) {
+    kern::win_frame_minmax(P<int64_t>(vals), f64, is_max, P<uint8_t>(valid), P<int64_t>(lo), P<int64_t>(hi), n,
+                           P<int64_t>(out), P<uint8_t>(out_valid), S(s));
+  });
+  m.def("win_rank", [](int fn, int64_t arg, int64_t n, uintptr_t ss, uintptr_t se, uintptr_t ps, uintptr_t pe,
+                       uintptr_t dense, uintptr_t out, uintptr_t s) {
+    kern::win_rank(fn, arg, n, P<int64_t>(ss), P<int64_t>(se), P<int64_t>(ps), P<int64_t>(pe), P<int64_t>(dense),
+                   P<int64_t>(out), S(s));
+  });
+  m.def("win_index", [](int fn, int64_t arg, int64_t n, uintptr_t ss, uintptr_t se, uintptr_t lo, uintptr_t hi,
+                        uintptr_t out, uintptr_t s) {
+    kern::win_index(fn, arg, n, P<int64_t>(ss), P<int64_t>(se), P<int64_t>(lo), P<int64_t>(hi), P<int64_t>(out),
+                    S(s));
+  });
   m.def("date_part", [](uintptr_t days, int64_t n, int field, uintptr_t out, uintptr_t s) {
     kern::date_part(P<const int32_t>(days), n, field, P<int32_t>(out), S(s));
   });

@@ -419,5 +419,31 @@ void pq_decode(const PqPage* pages, int64_t npages, const int32_t* page_col, con
                hipStream_t stream);
 void pq_str_copy(const int64_t* pos, const int64_t* off, int64_t n, uint8_t* out, hipStream_t stream);
 
+// ---- window.hip (window functions over rows sorted by partition / order keys)
+enum WinVal { kWinI64 = 0, kWinI32 = 1, kWinF64 = 2, kWinOne = 3, kWinHeadIdx = 4, kWinHead2 = 5 };
+enum WinFn {
+  kWinRowNumber = 0, kWinRank = 1, kWinDenseRank = 2, kWinPercentRank = 3, kWinCumeDist = 4, kWinNtile = 5,
+  kWinLag = 10, kWinFirst = 11, kWinLast = 12, kWinNth = 13
+};
+int64_t win_scan_tiles(int64_t n);
+// op: 0 sum i64, 1 sum f64, 2 min i64, 3 max i64, 4 min f64, 5 max f64; tflag/tval: win_scan_tiles(n) slots
+void win_seg_scan(const void* ids, bool ids64, const void* ids2, bool ids2_64, const void* vals, int vkind,
+                  const uint8_t* valid, int64_t n, int op, bool reverse, int* tflag, int64_t* tval, int64_t* out,
+                  int* err, hipStream_t s);
+void win_bounds(int64_t n, const int64_t* seg_start, const int64_t* seg_end, const int64_t* peer_start,
+                const int64_t* peer_end, int unit, int skind, int64_t soff_i, double soff_f, int ekind,
+                int64_t eoff_i, double eoff_f, const void* key, bool key_f64, const uint8_t* key_valid, bool desc,
+                const int64_t* gnum, const int64_t* gpos, int64_t ngroups, int64_t* lo, int64_t* hi,
+                hipStream_t s);
+void win_frame_sum(const int64_t* psum, bool f64, const int64_t* pcnt, const int64_t* lo, const int64_t* hi,
+                   int64_t n, int64_t* sum_out, int64_t* cnt_out, hipStream_t s);
+void win_frame_minmax(const int64_t* vals, bool f64, bool is_max, const uint8_t* valid, const int64_t* lo,
+                      const int64_t* hi, int64_t n, int64_t* out, uint8_t* out_valid, hipStream_t s);
+void win_rank(int fn, int64_t arg, int64_t n, const int64_t* seg_start, const int64_t* seg_end,
+              const int64_t* peer_start, const int64_t* peer_end, const int64_t* dense, int64_t* out,
+              hipStream_t s);
+void win_index(int fn, int64_t arg, int64_t n, const int64_t* seg_start, const int64_t* seg_end, const int64_t* lo,
+               const int64_t* hi, int64_t* out, hipStream_t s);
+
 }  // namespace kern
 }  // namespace igloo

@@ -232,12 +232,49 @@ class Parser {
       n->kids.push_back(expr());
     } else if (acceptKw("SHOW")) {
       n = make("show");
-      n->str = ident();
+      if (acceptWord("all")) {
+        n->str = "all";
+      } else {
+        n->str = ident();
+        if (n->str == "columns" || n->str == "fields") {
+          if (!acceptKw("FROM")) expectKw("IN");
+          std::string t = ident();
+          while (acceptOp(".")) t += "." + ident();
+          n->flags["table"] = t;
+          n->str = "columns";
+        } else {
+          while (acceptOp(".")) n->str += "." + ident();
+        }
+      }
+    } else if (isWord("describe") || (isKw("DESC") && peek(1).kind != Token::End)) {
+      ++p_;
+      n = make("describe");
+      std::string t = ident();
+      while (acceptOp(".")) t += "." + ident();
+      n->str = t;
+    } else if (acceptWord("insert")) {
+      acceptWord("into");
+      n = make("insert");
+      std::string t = ident();
+      while (acceptOp(".")) t += "." + ident();
+      n->str = t;
+      if (isOp("(") && (peek(1).kind == Token::Ident || peek(1).kind == Token::QuotedIdent)) {
+        ++p_;
+        std::vector<NodeP> cols;
+        do cols.push_back(make("name", ident()));
+        while (acceptOp(","));
+        expectOp(")");
+        n->attrs["columns"] = list(cols);
+      }
+      n->attrs["query"] = query();
+    } else if (acceptWord("truncate")) {
+      acceptWord("table");
+      n = make("truncate", ident());
     } else if (acceptKw("CREATE")) {
       n = createStmt();
     } else if (acceptKw("DROP")) {
-      expectWord("table");
-      n = make("drop_table");
+      if (acceptWord("view")) n = make("drop_view");
+      else { expectWord("table"); n = make("drop_table"); }
       if (acceptWord("if")) { expectKw("EXISTS"); n->flags["if_exists"] = "1"; }
       n->str = ident();
     } else {
@@ -248,10 +285,22 @@ class Parser {
   }
 
   NodeP createStmt() {
+    bool replace = false;
+    if (acceptKw("OR")) { expectWord("replace"); replace = true; }
     bool external = acceptWord("external");
     if (acceptWord("view")) {
       auto n = make("create_view");
+      if (replace) n->flags["replace"] = "1";
+      if (acceptWord("if")) { expectKw("NOT"); expectKw("EXISTS"); n->flags["if_not_exists"] = "1"; }
       n->str = ident();
+      if (isOp("(")) {
+        ++p_;
+        std::vector<NodeP> cols;
+        do cols.push_back(make("name", ident()));
+        while (acceptOp(","));
+        expectOp(")");
+        n->attrs["columns"] = list(cols);
+      }
       expectKw("AS");
       n->attrs["query"] = query();
       return n;
@@ -325,7 +374,7 @@ class Parser {
     auto q = make("query");
     q->pos = peek().pos;
     if (acceptKw("WITH")) {
-      acceptWord("recursive");
+      if (acceptWord("recursive")) q->flags["recursive"] = "1";
       std::vector<NodeP> ctes;
       do {
         auto c = make("cte", ident());
@@ -460,12 +509,71 @@ class Parser {
     if (acceptKw("GROUP")) {
       expectKw("BY");
       std::vector<NodeP> g;
-      do g.push_back(expr());
+      do g.push_back(groupItem());
       while (acceptOp(","));
       s->attrs["group"] = list(g);
     }
     if (acceptKw("HAVING")) s->attrs["having"] = expr();
+    if (acceptKw("WINDOW")) {
+      std::vector<NodeP> ws;
+      do {
+        std::string name = ident();
+        expectKw("AS");
+        expectOp("(");
+        auto w = windowSpec();
+        expectOp(")");
+        auto d = make("window_def", name);
+        d->attrs["spec"] = w;
+        ws.push_back(d);
+      } while (acceptOp(","));
+      s->attrs["windows"] = list(ws);
+    }
+    if (acceptKw("QUALIFY")) s->attrs["qualify"] = expr();
     return s;
+  }
+
+  // GROUP BY item: expr | ROLLUP (...) | CUBE (...) | GROUPING SETS ((...), ...)
+  NodeP groupItem() {
+    if ((isWord("rollup") || isWord("cube")) && isOp("(", 1)) {
+      auto n = make(next().text);
+      expectOp("(");
+      do n->kids.push_back(groupingElem());
+      while (acceptOp(","));
+      expectOp(")");
+      return n;
+    }
+    if (isWord("grouping") && isWord("sets", 1)) {
+      p_ += 2;
+      auto n = make("grouping_sets");
+      expectOp("(");
+      do {
+        if (isWord("rollup") || isWord("cube")) n->kids.push_back(groupItem());
+        else n->kids.push_back(groupingElem());
+      } while (acceptOp(","));
+      expectOp(")");
+      return n;
+    }
+    return expr();
+  }
+
+  // one grouping element: expr or a parenthesised (possibly empty) list
+  NodeP groupingElem() {
+    if (isOp("(")) {
+      size_t save = p_;
+      ++p_;
+      if (acceptOp(")")) return list({});
+      std::vector<NodeP> v;
+      v.push_back(expr());
+      if (acceptOp(",")) {
+        do v.push_back(expr());
+        while (acceptOp(","));
+        expectOp(")");
+        return list(v);
+      }
+      if (acceptOp(")")) return list(v);
+      p_ = save;
+    }
+    return list({expr()});
   }
 
   NodeP selectItem() {
@@ -890,7 +998,20 @@ class Parser {
       case Token::Ident:
       case Token::QuotedIdent: {
         std::string name = next().text;
-        if (isOp("(") && t.kind == Token::Ident) return funcCall(name);
+        if (isOp("(") && t.kind == Token::Ident) {
+          if (name == "trim") return trimCall();
+          if (name == "position") {  // POSITION(needle IN haystack) -> strpos(haystack, needle)
+            ++p_;
+            NodeP needle = additive();
+            expectKw("IN");
+            NodeP hay = expr();
+            expectOp(")");
+            auto f = make("func", "strpos");
+            f->kids = {hay, needle};
+            return f;
+          }
+          return funcCall(name);
+        }
         return colRef(name);
       }
       default:
@@ -931,7 +1052,101 @@ class Parser {
       f->attrs["filter"] = expr();
       expectOp(")");
     }
-    if (acceptWord("over")) fail("window functions are not supported yet");
+    if (acceptWord("over")) {
+      if (isOp("(")) {
+        ++p_;
+        f->attrs["over"] = windowSpec();
+        expectOp(")");
+      } else {
+        auto w = make("window", ident());  // named window (WINDOW clause)
+        f->attrs["over"] = w;
+      }
+    }
+    return f;
+  }
+
+  // ( [base] [PARTITION BY ...] [ORDER BY ...] [frame] ) -- body without parens
+  NodeP windowSpec() {
+    auto w = make("window");
+    if ((peek().kind == Token::Ident || peek().kind == Token::QuotedIdent) && !isWord("partition") &&
+        !isWord("rows") && !isWord("range") && !isWord("groups"))
+      w->str = ident();  // OVER (w ORDER BY ...) refines a named window
+    if (acceptWord("partition")) {
+      expectKw("BY");
+      std::vector<NodeP> ps;
+      do ps.push_back(expr());
+      while (acceptOp(","));
+      w->attrs["partition"] = list(ps);
+    }
+    if (acceptKw("ORDER")) {
+      expectKw("BY");
+      std::vector<NodeP> os;
+      do os.push_back(orderItem());
+      while (acceptOp(","));
+      w->attrs["order"] = list(os);
+    }
+    std::string unit;
+    if (acceptWord("rows")) unit = "rows";
+    else if (acceptWord("range")) unit = "range";
+    else if (acceptWord("groups")) unit = "groups";
+    if (!unit.empty()) {
+      auto fr = make("frame", unit);
+      if (acceptKw("BETWEEN")) {
+        fr->kids.push_back(frameBound());
+        expectKw("AND");
+        fr->kids.push_back(frameBound());
+      } else {
+        fr->kids.push_back(frameBound());
+        fr->kids.push_back(make("bound", "current"));
+      }
+      if (acceptWord("exclude")) {
+        if (acceptWord("no")) expectWord("others");
+        else fail("only EXCLUDE NO OTHERS is supported");
+      }
+      w->attrs["frame"] = fr;
+    }
+    return w;
+  }
+
+  NodeP frameBound() {
+    if (acceptWord("unbounded")) {
+      if (acceptWord("preceding")) return make("bound", "unbounded_preceding");
+      expectWord("following");
+      return make("bound", "unbounded_following");
+    }
+    if (acceptWord("current")) {
+      expectWord("row");
+      return make("bound", "current");
+    }
+    NodeP off = additive();
+    NodeP b;
+    if (acceptWord("preceding")) b = make("bound", "preceding");
+    else { expectWord("following"); b = make("bound", "following"); }
+    b->kids.push_back(off);
+    return b;
+  }
+
+  // TRIM([LEADING|TRAILING|BOTH] [chars] FROM s) / trim(s [, chars])
+  NodeP trimCall() {
+    expectOp("(");
+    std::string fn = "btrim";
+    if (acceptWord("leading")) fn = "ltrim";
+    else if (acceptWord("trailing")) fn = "rtrim";
+    else acceptWord("both");
+    auto f = make("func", fn);
+    if (acceptKw("FROM")) {
+      f->kids.push_back(expr());
+    } else {
+      NodeP first = expr();
+      if (acceptKw("FROM")) {
+        f->kids = {expr(), first};
+      } else if (acceptOp(",")) {
+        f->kids = {first, expr()};
+      } else {
+        f->kids = {first};
+      }
+    }
+    expectOp(")");
     return f;
   }
 

@@ -523,7 +523,7 @@ def _subtree_key(plan) -> Optional[str]:
     tables, filters, expressions). None for subtrees holding a subquery
     (its plan is not part of the text)."""
     txt = plan.explain()
-    if "subquery" in txt:
+    if "subquery" in txt or "WorkTable" in txt:
         return None
     seen: Dict[str, int] = {}
 

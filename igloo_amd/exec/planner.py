@@ -49,6 +49,17 @@ def create_physical_plan(p: L.Plan) -> ExecNode:
         return UnionExec(p, [create_physical_plan(c) for c in p.children])
     if isinstance(p, L.FragmentRef):
         return FragmentInputExec(p)
+    if isinstance(p, L.Window):
+        from .window import WindowExec
+        node = WindowExec(p, create_physical_plan(p.input))
+        _require(node.children[0], [w for _, w in p.wexprs] + [c.ref() for c in p.input.schema])
+        return node
+    if isinstance(p, L.RecursiveCTE):
+        from .window import RecursiveCTEExec
+        return RecursiveCTEExec(p, create_physical_plan(p.anchor), create_physical_plan(p.recursive))
+    if isinstance(p, L.WorkTableScan):
+        from .window import WorkTableExec
+        return WorkTableExec(p)
     raise NotSupported(f"no physical operator for {type(p).__name__}")
 
 

@@ -17,9 +17,11 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 from .. import types as T
 from ..types import BOOL, DATE32, FLOAT64, INT32, INT64, UTF8, DataType
 from ..utils.errors import NotSupported, PlanError, TableNotFound
-from .expr import (AGG_FUNCS, AggCall, BinOp, Case, Cast, ColRef, Expr, Func, InList, IsNull, Like, Lit, Neg,
-                   Not, SubqueryExpr, and_all, col_refs, transform, walk)
-from .logical import (Aggregate, ColInfo, Filter, Join, Limit, Plan, Project, Scan, Sort, Union, Values)
+from .expr import (AGG_FUNCS, FRAME_KINDS, RANKING_FUNCS, VALUE_FUNCS, AggCall, BinOp, Case, Cast, ColRef, Expr,
+                   Func, InList, IsNull, Like, Lit, Neg, Not, SubqueryExpr, WindowCall, WindowFrame, and_all, col_refs,
+                   transform, walk)
+from .logical import (Aggregate, ColInfo, Filter, Join, Limit, Plan, Project, RecursiveCTE, Scan, Sort, Union, Values,
+                      Window, WorkTableScan)
 
 EPOCH = datetime.date(1970, 1, 1)
 INTERVAL = DataType("interval")
@@ -117,7 +119,8 @@ class Binder:
     def bind_query(self, q: dict, outer: Optional[Scope] = None, ctes: Optional[dict] = None) -> BoundQuery:
         ctes = dict(ctes or {})
         for c in _lst(q.get("with")):
-            ctes[c["s"]] = (c, dict(ctes))
+            rec = bool(q.get("recursive")) and _is_recursive_cte(c)
+            ctes[c["s"]] = (c, dict(ctes), rec)
         prev = getattr(self, "_ctes", None)
         self._ctes = ctes
         try:
@@ -183,11 +186,45 @@ class Binder:
                 plan = self._distinct(plan)
             return BoundQuery(plan, a.names)
         if op.startswith("intersect") or op.startswith("except"):
-            on = [(ca.ref(), cb.ref()) for ca, cb in zip(a.plan.schema, b.plan.schema)]
             kind = "semi" if op.startswith("intersect") else "anti"
-            plan = Join(self._distinct(a.plan), b.plan, kind, on)
-            return BoundQuery(plan, a.names)
+            if op.endswith("_all"):
+                # bag semantics: the k-th copy of a row matches the k-th copy
+                # on the other side (row_number over all columns)
+                la, lrn = self._numbered(a.plan)
+                rb, rrn = self._numbered(b.plan)
+                on = self._null_safe_keys(la.schema[:-1], rb.schema[:-1]) + [(lrn.ref(), rrn.ref())]
+                j = Join(la, rb, kind, on)
+                keep = [(ColInfo(self.ids(), c.name, c.dtype, c.nullable), c.ref()) for c in la.schema[:-1]]
+                return BoundQuery(Project(j, keep), a.names)
+            left = self._distinct(a.plan)
+            on = self._null_safe_keys(left.schema, b.plan.schema)
+            return BoundQuery(Join(left, b.plan, kind, on), a.names)
         raise NotSupported(op)
+
+    def _numbered(self, plan: Plan) -> Tuple[Plan, ColInfo]:
+        """``plan`` plus row_number() over (partition by every column)."""
+        part = [c.ref() for c in plan.schema]
+        w = WindowCall("row_number", [], part, [], WindowFrame("rows", "unbounded_preceding", "unbounded_following"),
+                       INT64)
+        ci = ColInfo(self.ids(), "__rn", INT64, False)
+        return Window(plan, [(ci, w)]), ci
+
+    def _null_safe_keys(self, ls: List[ColInfo], rs: List[ColInfo]) -> List[Tuple[Expr, Expr]]:
+        """Equi-join keys under which NULL equals NULL (set operations): a
+        nullable column contributes (is-null flag, value-or-default)."""
+        on = []
+        for ca, cb in zip(ls, rs):
+            a, b = ca.ref(), cb.ref()
+            if a.dtype != b.dtype:
+                t = T.common_numeric(a.dtype, b.dtype) if (a.dtype.is_numeric and b.dtype.is_numeric) else a.dtype
+                a, b = self._coerce(a, t), self._coerce(b, t)
+            if not (ca.nullable or cb.nullable):
+                on.append((a, b))
+                continue
+            d = _default_lit(a.dtype)
+            on.append((Cast(IsNull(a), INT32), Cast(IsNull(b), INT32)))
+            on.append((Func("coalesce", [a, d], a.dtype), Func("coalesce", [b, d], b.dtype)))
+        return on
 
     def _distinct(self, plan: Plan) -> Plan:
         groups = [(ColInfo(self.ids(), c.name, c.dtype, c.nullable), c.ref()) for c in plan.schema]
@@ -223,6 +260,14 @@ class Binder:
 
     # ================================================================== select
     def _bind_select(self, s: dict, outer: Optional[Scope], ctes: dict, order: list) -> BoundQuery:
+        prev_w = getattr(self, "_win_defs", None)
+        self._win_defs = {d["s"]: d["spec"] for d in _lst(s.get("windows"))}
+        try:
+            return self._bind_select_inner(s, outer, ctes, order)
+        finally:
+            self._win_defs = prev_w
+
+    def _bind_select_inner(self, s: dict, outer: Optional[Scope], ctes: dict, order: list) -> BoundQuery:
         # ---- FROM
         if s.get("from"):
             plan, rels = None, []
@@ -252,27 +297,26 @@ class Binder:
                 continue
             e = self.bind_expr(it["c"][0], scope, allow_agg=True)
             items.append((e, it.get("alias") or self._display_name(it["c"][0], e)))
-        # ---- GROUP BY
+        # ---- GROUP BY (plain keys, or ROLLUP / CUBE / GROUPING SETS)
+        group_nodes, set_nodes = _expand_group_by(_lst(s.get("group")))
         group_exprs: List[Expr] = []
-        for g in _lst(s.get("group")):
-            if g["k"] == "lit" and g.get("type") == "int":
-                idx = int(g["s"]) - 1
-                if not 0 <= idx < len(items):
-                    raise PlanError(f"GROUP BY position {idx + 1} out of range")
-                group_exprs.append(items[idx][0])
-                continue
-            if g["k"] == "col" and len(g["c"]) == 1:
-                # a select alias may be used in GROUP BY (when it is not also an input column)
-                nm = g["s"]
-                try:
-                    scope.resolve([nm])
-                except PlanError:
-                    hit = [e for e, a in items if a == nm]
-                    if hit:
-                        group_exprs.append(hit[0])
-                        continue
-            group_exprs.append(self.bind_expr(g, scope))
+        for g in group_nodes:
+            group_exprs.append(self._bind_group_key(g, scope, items))
+        sets = None
+        if set_nodes is not None:
+            keyidx: Dict[str, int] = {}
+            uniq: List[Expr] = []
+            for g in group_exprs:
+                if g.sql() not in keyidx:
+                    keyidx[g.sql()] = len(uniq)
+                    uniq.append(g)
+            sets = []
+            for gs in set_nodes:
+                ids = sorted({keyidx[group_exprs[k].sql()] for k in gs})
+                sets.append(ids)
+            group_exprs = uniq
         having = self.bind_expr(s["having"], scope, allow_agg=True) if s.get("having") else None
+        qualify = self.bind_expr(s["qualify"], scope, allow_agg=True) if s.get("qualify") else None
         # ORDER BY expressions bound against input scope + aliases (resolved later)
         aliases = {a: e for e, a in items}
         order_bound = []
@@ -298,18 +342,47 @@ class Binder:
             else:
                 order_bound.append(("expr", bound, asc, nf))
         # ---- aggregation
-        has_aggs = any(_contains_agg(e) for e, _ in items) or (having is not None and _contains_agg(having)) or \
-            any(k == "expr" and _contains_agg(x) for k, x, _, _ in order_bound)
-        if group_exprs or has_aggs:
-            plan, rewrite = self._aggregate(plan, group_exprs, [e for e, _ in items] + ([having] if having is not None else [])
-                                            + [x for k, x, _, _ in order_bound if k == "expr"])
+        extra = ([having] if having is not None else []) + ([qualify] if qualify is not None else [])
+        has_aggs = any(_contains_agg(e) for e, _ in items) or any(_contains_agg(x) for x in extra) or \
+            any(k == "expr" and _contains_agg(x) for k, x, _, _ in order_bound) or \
+            any(_contains_grouping(e) for e, _ in items)
+        if group_exprs or has_aggs or sets is not None:
+            plan, rewrite = self._aggregate(plan, group_exprs, [e for e, _ in items] + extra
+                                            + [x for k, x, _, _ in order_bound if k == "expr"], sets)
             items = [(rewrite(e), a) for e, a in items]
             if having is not None:
                 having = rewrite(having)
+            if qualify is not None:
+                qualify = rewrite(qualify)
             order_bound = [(k, rewrite(x) if k == "expr" else x, a, nf) for k, x, a, nf in order_bound]
         if having is not None:
             self._require_bool(having, "HAVING")
             plan = Filter(plan, having)
+        # ---- window functions (after GROUP BY / HAVING, before DISTINCT / ORDER BY)
+        wsrc = [e for e, _ in items] + ([qualify] if qualify is not None else []) + \
+            [x for k, x, _, _ in order_bound if k == "expr"]
+        wmap: Dict[str, ColRef] = {}
+        wexprs: List[Tuple[ColInfo, WindowCall]] = []
+        for e in wsrc:
+            for x in walk(e):
+                if isinstance(x, WindowCall) and x.sql() not in wmap:
+                    if any(isinstance(y, WindowCall) for k in x.children() for y in walk(k)):
+                        raise PlanError("window function calls cannot be nested")
+                    ci = ColInfo(self.ids(), x.func, x.dtype, x.nullable)
+                    wexprs.append((ci, x))
+                    wmap[x.sql()] = ci.ref()
+        if wexprs:
+            plan = Window(plan, wexprs)
+
+            def wrw(e: Expr) -> Expr:
+                return _transform_top_down(e, lambda x: wmap.get(x.sql()) if isinstance(x, WindowCall) else None)
+            items = [(wrw(e), a) for e, a in items]
+            if qualify is not None:
+                qualify = wrw(qualify)
+            order_bound = [(k, wrw(x) if k == "expr" else x, a, nf) for k, x, a, nf in order_bound]
+        if qualify is not None:
+            self._require_bool(qualify, "QUALIFY")
+            plan = Filter(plan, qualify)
         # ---- projection (+ hidden ORDER BY columns)
         proj = [(ColInfo(self.ids(), a, e.dtype, e.nullable), e) for e, a in items]
         hidden = []
@@ -334,12 +407,34 @@ class Binder:
         names = [c.name for c, _ in proj]
         return BoundQuery(plan, names)
 
+    def _bind_group_key(self, g: dict, scope: Scope, items) -> Expr:
+        if g["k"] == "lit" and g.get("type") == "int":
+            idx = int(g["s"]) - 1
+            if not 0 <= idx < len(items):
+                raise PlanError(f"GROUP BY position {idx + 1} out of range")
+            return items[idx][0]
+        if g["k"] == "col" and len(g["c"]) == 1:
+            # a select alias may be used in GROUP BY (when it is not also an input column)
+            nm = g["s"]
+            try:
+                scope.resolve([nm])
+            except PlanError:
+                hit = [e for e, a in items if a == nm]
+                if hit:
+                    return hit[0]
+        return self.bind_expr(g, scope)
+
     def _distinct_keep(self, plan: Project) -> Plan:
         # DISTINCT keeps the projected cids so ORDER BY references stay valid
         groups = [(c, c.ref()) for c in plan.schema]
         return Aggregate(plan, [(ColInfo(c.cid, c.name, c.dtype, c.nullable), _Passthrough(c)) for c, _ in groups], [])
 
-    def _aggregate(self, plan: Plan, group_exprs: List[Expr], exprs: List[Expr]):
+    def _aggregate(self, plan: Plan, group_exprs: List[Expr], exprs: List[Expr], sets=None):
+        """One Aggregate over ``plan`` (``sets`` None), or for GROUPING SETS /
+        ROLLUP / CUBE a UNION ALL of one Aggregate per grouping set, each
+        padded with NULL for the keys it does not group by and tagged with a
+        grouping-id column (bit k-1-i set when key i is aggregated away) that
+        ``grouping(...)`` reads."""
         groups: List[Tuple[ColInfo, Expr]] = []
         gmap: Dict[str, ColRef] = {}
         for g in group_exprs:
@@ -347,7 +442,7 @@ class Binder:
             if key in gmap:
                 continue
             name = g.name if isinstance(g, ColRef) else key
-            ci = ColInfo(self.ids(), name, g.dtype, g.nullable)
+            ci = ColInfo(self.ids(), name, g.dtype, g.nullable or sets is not None)
             groups.append((ci, g))
             gmap[key] = ci.ref()
         aggs: List[Tuple[ColInfo, AggCall]] = []
@@ -359,23 +454,66 @@ class Binder:
                     if key not in amap:
                         if x.arg is not None and _contains_agg(x.arg):
                             raise PlanError("aggregate function calls cannot be nested")
-                        ci = ColInfo(self.ids(), x.sql(), x.dtype, x.func not in ("count",))
+                        ci = ColInfo(self.ids(), x.sql(), x.dtype, x.func not in ("count", "approx_distinct"))
                         aggs.append((ci, x))
                         amap[key] = ci.ref()
-        agg = Aggregate(plan, groups, aggs)
+        gid_ref: Optional[ColRef] = None
+        if sets is None:
+            agg: Plan = Aggregate(plan, groups, aggs)
+        else:
+            k = len(groups)
+            gid_ci = ColInfo(self.ids(), "__grouping_id", INT64, False)
+            gid_ref = gid_ci.ref()
+            schema = [c for c, _ in groups] + [gid_ci] + [c for c, _ in aggs]
+            branches = []
+            for st in sets:
+                gi = [(ColInfo(self.ids(), groups[i][0].name, groups[i][1].dtype, groups[i][1].nullable), groups[i][1])
+                      for i in st]
+                ai = [(ColInfo(self.ids(), c.name, c.dtype, c.nullable), a) for c, a in aggs]
+                a_plan = Aggregate(plan, gi, ai)
+                pos = {i: gi[n][0] for n, i in enumerate(st)}
+                bits = sum(1 << (k - 1 - i) for i in range(k) if i not in pos)
+                pe: List[Tuple[ColInfo, Expr]] = []
+                for i, (c, _) in enumerate(groups):
+                    e = pos[i].ref() if i in pos else Lit(None, c.dtype)
+                    pe.append((ColInfo(self.ids(), c.name, c.dtype, True), e))
+                pe.append((ColInfo(self.ids(), "__grouping_id", INT64, False), Lit(bits, INT64)))
+                for (c, _), (cc, _) in zip(aggs, ai):
+                    pe.append((ColInfo(self.ids(), c.name, c.dtype, c.nullable), cc.ref()))
+                branches.append(Project(a_plan, pe))
+            agg = Union(branches, schema)
         group_cids = {ci.cid for ci, _ in groups}
+        ginfo = [g for _, g in groups]
+
+        def grouping_expr(f: Func) -> Expr:
+            out: Expr = Lit(0, INT64)
+            m = len(f.args)
+            for j, a in enumerate(f.args):
+                idx = next((i for i, g in enumerate(ginfo) if g.sql() == a.sql()), None)
+                if idx is None:
+                    raise PlanError(f"grouping() argument {a.sql()} is not a GROUP BY expression")
+                if gid_ref is None:
+                    continue
+                bit = BinOp("%", BinOp("/", gid_ref, Lit(1 << (len(ginfo) - 1 - idx), INT64), INT64),
+                            Lit(2, INT64), INT64)
+                term = BinOp("*", bit, Lit(1 << (m - 1 - j), INT64), INT64)
+                out = term if isinstance(out, Lit) and out.value == 0 else BinOp("+", out, term, INT64)
+            return Cast(out, INT32) if not isinstance(out, Lit) else Lit(0, INT32)
 
         def rewrite(e: Expr) -> Expr:
             def fn(x):
-                k = x.sql()
+                k_ = x.sql()
                 if isinstance(x, AggCall):
-                    return amap[k + (f" FILTER {x.filter.sql()}" if x.filter is not None else "")]
-                if k in gmap:
-                    return gmap[k]
+                    return amap[k_ + (f" FILTER {x.filter.sql()}" if x.filter is not None else "")]
+                if isinstance(x, Func) and x.name == "grouping":
+                    return grouping_expr(x)
+                if k_ in gmap:
+                    return gmap[k_]
                 return None
             out = _transform_top_down(e, fn)
             for x in walk(out):
-                if isinstance(x, ColRef) and x.cid not in group_cids and x.cid not in {c.cid for c, _ in aggs}:
+                if isinstance(x, ColRef) and x.cid not in group_cids and x.cid not in {c.cid for c, _ in aggs} \
+                        and (gid_ref is None or x.cid != gid_ref.cid):
                     if isinstance(x, ColRef) and not getattr(x, "_outer", False):
                         raise PlanError(f"column '{x.name}' must appear in the GROUP BY clause or be used in an aggregate function")
             return out
@@ -388,8 +526,17 @@ class Binder:
             name = item["s"]
             alias = item.get("alias")
             if name in ctes:
-                cnode, cenv = ctes[name]
-                bq = self.bind_query(cnode["query"], outer, cenv)
+                ent = ctes[name]
+                if ent[0] == "__work":
+                    # the recursive term's reference to its own CTE: last iteration's rows
+                    _, tid, wschema = ent
+                    sch = [ColInfo(self.ids(), c.name, c.dtype, c.nullable, alias or name) for c in wschema]
+                    return WorkTableScan(tid, sch), [Relation(alias or name, sch)]
+                cnode, cenv = ent[0], ent[1]
+                if len(ent) > 2 and ent[2]:
+                    bq = self._bind_recursive_cte(cnode, outer, cenv)
+                else:
+                    bq = self.bind_query(cnode["query"], outer, cenv)
                 cols = [c["s"] for c in _lst(cnode.get("columns"))] or bq.names
                 return self._derived(bq, alias or name, cols, item)
             view = self.catalog.get_view(name) if hasattr(self.catalog, "get_view") else None
@@ -442,6 +589,36 @@ class Binder:
                 return Join(lp, rp, "cross"), lr + rr
             return Join(lp, rp, kind, [], residual), (lr + rr if kind not in ("semi", "anti") else lr)
         raise NotSupported(f"FROM item {k}")
+
+    def _bind_recursive_cte(self, cnode: dict, outer, cenv: dict) -> BoundQuery:
+        """WITH RECURSIVE name AS (anchor UNION [ALL] recursive-term)."""
+        q = cnode["query"]
+        body = q["body"]
+        if body["k"] != "setop" or not body["s"].startswith("union"):
+            raise PlanError(f"recursive CTE '{cnode['s']}' must be <anchor> UNION [ALL] <recursive term>")
+        if q.get("order") or q.get("limit"):
+            raise NotSupported("ORDER BY / LIMIT on a recursive CTE body")
+        env = dict(cenv)
+        env.update(getattr(self, "_ctes", None) or {})
+        env.pop(cnode["s"], None)
+        anchor = self._bind_setop(body["c"][0], outer, env)
+        names = [c["s"] for c in _lst(cnode.get("columns"))] or anchor.names
+        if len(names) != len(anchor.plan.schema):
+            raise PlanError(f"recursive CTE '{cnode['s']}' has {len(names)} column names for "
+                            f"{len(anchor.plan.schema)} columns")
+        tid = self.ids()
+        wschema = [ColInfo(self.ids(), n, c.dtype, True) for n, c in zip(names, anchor.plan.schema)]
+        env[cnode["s"]] = ("__work", tid, wschema)
+        rec = self._bind_setop(body["c"][1], outer, env)
+        if len(rec.plan.schema) != len(wschema):
+            raise PlanError("recursive term returns a different number of columns than the anchor")
+        out = [ColInfo(self.ids(), w.name, w.dtype, True) for w in wschema]
+        ap = Project(anchor.plan, [(ColInfo(self.ids(), o.name, o.dtype, True), self._coerce(c.ref(), o.dtype))
+                                   for o, c in zip(out, anchor.plan.schema)])
+        rp = Project(rec.plan, [(ColInfo(self.ids(), o.name, o.dtype, True), self._coerce(c.ref(), o.dtype))
+                                for o, c in zip(out, rec.plan.schema)])
+        limit = int(self.session.get("max_recursion", 1000) or 1000)
+        return BoundQuery(RecursiveCTE(ap, rp, tid, out, body["s"] == "union", limit), names)
 
     def _derived(self, bq: BoundQuery, alias, names, item) -> Tuple[Plan, List[Relation]]:
         cols = [ColInfo(c.cid, n, c.dtype, c.nullable, alias) for c, n in zip(bq.plan.schema, names)]
@@ -643,6 +820,8 @@ class Binder:
         if lt != rt:
             ct = T.common_numeric(lt, rt)
             l, r = self._coerce(l, ct), self._coerce(r, ct)
+        if op in ("is_distinct_from", "is_not_distinct_from"):
+            return _distinct_from(op == "is_distinct_from", l, r)
         return _fold(BinOp(op, l, r, BOOL))
 
     def _arith(self, op: str, l: Expr, r: Expr) -> Expr:
@@ -725,6 +904,12 @@ class Binder:
 
     def _func(self, node, scope, allow_agg) -> Expr:
         name = node["s"].lower()
+        if node.get("over") is not None:
+            return self._window_call(name, node, scope, allow_agg)
+        if name == "grouping":
+            if not allow_agg:
+                raise PlanError("grouping() is only allowed with GROUP BY")
+            return Func("grouping", [self.bind_expr(a, scope) for a in node["c"]], INT32)
         if name in AGG_FUNCS or name in ("stddev_samp", "stddev_pop", "var_samp", "var_pop"):
             if not allow_agg:
                 raise PlanError(f"aggregate function {name} not allowed here")
@@ -800,6 +985,129 @@ class Binder:
             return self._coerce(args[0], DATE32)
         raise NotSupported(f"function {name}()")
 
+    # ------------------------------------------------------------ windows
+    def _window_call(self, name: str, node, scope, allow_agg) -> Expr:
+        if not allow_agg:
+            raise PlanError(f"window function {name}() is only allowed in SELECT, QUALIFY and ORDER BY")
+        if node.get("distinct"):
+            raise NotSupported("DISTINCT in a window aggregate")
+        spec = self._window_spec(node["over"])
+        part = [self.bind_expr(e, scope, allow_agg=True) for e in _lst(spec.get("partition"))]
+        order = []
+        for o in _lst(spec.get("order")):
+            e = self.bind_expr(o["c"][0], scope, allow_agg=True)
+            asc = not o.get("desc")
+            order.append((e, asc, o.get("nulls", "last" if asc else "first") == "first"))
+        args = [self.bind_expr(a, scope, allow_agg=True) for a in node["c"]]
+        flt = self.bind_expr(node["filter"], scope, allow_agg=True) if node.get("filter") else None
+        frame = self._frame(spec.get("frame"), order)
+        if name in RANKING_FUNCS:
+            opts: tuple = ()
+            if name == "ntile":
+                if len(args) != 1 or not isinstance(args[0], Lit) or not isinstance(args[0].value, int) \
+                        or args[0].value <= 0:
+                    raise PlanError("ntile() takes one positive integer literal")
+                opts = (int(args[0].value),)
+            elif args:
+                raise PlanError(f"{name}() takes no arguments")
+            dt = FLOAT64 if name in ("percent_rank", "cume_dist") else INT64
+            return WindowCall(name, [], part, order, frame, dt, None, opts)
+        if name in VALUE_FUNCS:
+            if not args:
+                raise PlanError(f"{name}() needs an argument")
+            x = args[0]
+            if name in ("lag", "lead"):
+                if len(args) > 3:
+                    raise PlanError(f"{name}() takes at most 3 arguments")
+                k = 1
+                if len(args) > 1:
+                    if not isinstance(args[1], Lit) or not isinstance(args[1].value, int):
+                        raise NotSupported(f"{name}() offset must be an integer literal")
+                    k = int(args[1].value)
+                wargs = [x]
+                t = x.dtype
+                if len(args) > 2 and not (isinstance(args[2], Lit) and args[2].value is None):
+                    if not isinstance(args[2], Lit):
+                        raise NotSupported(f"{name}() default must be a literal")
+                    if t.kind == "null":
+                        t = args[2].dtype
+                    wargs.append(self._coerce(args[2], t))
+                return WindowCall("lag", wargs, part, order, frame, t, None, (k if name == "lag" else -k,))
+            if name == "nth_value":
+                if len(args) != 2 or not isinstance(args[1], Lit) or not isinstance(args[1].value, int) \
+                        or args[1].value < 1:
+                    raise PlanError("nth_value(x, n) needs a positive integer literal n")
+                return WindowCall(name, [x], part, order, frame, x.dtype, None, (int(args[1].value),))
+            if len(args) != 1:
+                raise PlanError(f"{name}() takes one argument")
+            return WindowCall(name, [x], part, order, frame, x.dtype)
+        if name in AGG_FUNCS or name in _EXTRA_AGGS:
+            if node.get("star") or not args:
+                arg = None
+            elif len(args) == 1:
+                arg = args[0]
+            else:
+                raise NotSupported(f"window aggregate {name} with {len(args)} arguments")
+            a = _make_agg(name, arg, False, None)
+            if a.func not in _WINDOW_AGGS:
+                raise NotSupported(f"{name}() as a window function")
+            return WindowCall(a.func, [arg] if arg is not None else [], part, order, frame, a.dtype, flt)
+        raise NotSupported(f"window function {name}()")
+
+    def _window_spec(self, w: dict) -> dict:
+        """Named-window references merged with the inline spec."""
+        out: dict = {}
+        if w.get("s"):
+            named = (getattr(self, "_win_defs", None) or {}).get(w["s"])
+            if named is None:
+                raise PlanError(f"window '{w['s']}' is not defined")
+            out = dict(self._window_spec(named))
+        for k in ("partition", "order", "frame"):
+            if w.get(k):
+                out[k] = w[k]
+        return out
+
+    def _frame(self, fr: Optional[dict], order) -> WindowFrame:
+        if fr is None:
+            if order:
+                return WindowFrame("range", "unbounded_preceding", "current")
+            return WindowFrame("rows", "unbounded_preceding", "unbounded_following")
+        unit = fr["s"]
+        (sb, eb) = fr["c"]
+        sk, ek = sb["s"], eb["s"]
+        if sk == "unbounded_following" or ek == "unbounded_preceding" or FRAME_KINDS.index(sk) > FRAME_KINDS.index(ek):
+            raise PlanError("window frame start cannot be after its end")
+
+        def off(b):
+            if b["s"] not in ("preceding", "following"):
+                return None
+            v = self.bind_expr(b["c"][0], Scope([]))
+            if not isinstance(v, Lit) or v.value is None:
+                raise PlanError("window frame offset must be a constant")
+            if unit in ("rows", "groups"):
+                if not isinstance(v.value, int) or v.value < 0:
+                    raise PlanError(f"{unit.upper()} frame offset must be a non-negative integer")
+                return int(v.value)
+            if len(order) != 1:
+                raise PlanError("RANGE with an offset needs exactly one ORDER BY key")
+            kt = order[0][0].dtype
+            if v.dtype == INTERVAL:
+                months, days = v.value
+                if months or kt.kind != "date32":
+                    raise NotSupported("RANGE offsets in months")
+                return Lit(days, INT64)
+            if kt.kind == "date32":
+                return Lit(int(v.value), INT64)
+            if not kt.is_numeric:
+                raise PlanError(f"RANGE offset over a {kt} key")
+            lv = self._coerce_lit(v, kt) if v.dtype != kt else v
+            if kt.is_decimal and lv.dtype.is_decimal and lv.dtype.scale != kt.scale:
+                lv = _fold_cast(lv, kt)
+            if (lv.value or 0) < 0:
+                raise PlanError("RANGE offset must not be negative")
+            return lv
+        return WindowFrame(unit, sk, ek, off(sb), off(eb))
+
     def _display_name(self, ast: dict, e: Expr) -> str:
         if isinstance(e, ColRef) and ast["k"] == "col":
             return e.name
@@ -814,6 +1122,106 @@ class _Passthrough(ColRef):
 
 
 # ---------------------------------------------------------------------- helpers
+#: aggregates computed by the window operator (exec/window.py)
+_WINDOW_AGGS = ("sum", "count", "avg", "min", "max", "stddev", "stddev_samp", "stddev_pop", "var", "var_samp",
+                "var_pop", "bool_and", "bool_or")
+_EXTRA_AGGS = ("stddev_samp", "stddev_pop", "var_samp", "var_pop", "variance", "var_population", "stddev_population",
+               "median", "approx_distinct", "approx_median", "string_agg", "array_agg", "bit_and", "bit_or",
+               "bit_xor", "covar", "covar_samp", "covar_pop", "corr", "approx_percentile_cont", "first_value",
+               "last_value", "every", "any", "some")
+
+
+def _distinct_from(distinct: bool, l: Expr, r: Expr) -> Expr:
+    """a IS [NOT] DISTINCT FROM b: NULL-safe (in)equality, never NULL."""
+    eq = "<>" if distinct else "="
+    if isinstance(l, Lit) and l.value is None:
+        l, r = r, l
+    if isinstance(r, Lit) and r.value is None:
+        if isinstance(l, Lit):
+            return Lit((l.value is not None) == distinct, BOOL)
+        return IsNull(l, negated=distinct)
+    if not l.nullable and not r.nullable:
+        return _fold(BinOp(eq, l, r, BOOL))
+    both = BinOp("and", IsNull(l), IsNull(r), BOOL)
+    one = BinOp("or", IsNull(l), IsNull(r), BOOL)
+    return Case([(both, Lit(not distinct, BOOL)), (one, Lit(distinct, BOOL))], BinOp(eq, l, r, BOOL), BOOL)
+
+
+def _default_lit(t: DataType) -> Lit:
+    if t.is_string:
+        return Lit("", t)
+    if t.kind == "bool":
+        return Lit(False, t)
+    if t.is_float:
+        return Lit(0.0, t)
+    return Lit(0, t)
+
+
+def _is_recursive_cte(c: dict) -> bool:
+    """A CTE body of the form anchor UNION [ALL] term, the term reading the CTE itself."""
+    body = c["query"]["body"]
+    if body["k"] != "setop" or not body["s"].startswith("union"):
+        return False
+    return _mentions_table(body["c"][1], c["s"])
+
+
+def _mentions_table(n, name: str) -> bool:
+    if isinstance(n, dict):
+        if n.get("k") == "table" and n.get("s") == name:
+            return True
+        return any(_mentions_table(v, name) for k, v in n.items() if k not in ("k", "s", "pos"))
+    if isinstance(n, list):
+        return any(_mentions_table(v, name) for v in n)
+    return False
+
+
+def _expand_group_by(items: list):
+    """GROUP BY items -> (key expression nodes, grouping sets as lists of
+    positions into them, or None when no ROLLUP / CUBE / GROUPING SETS)."""
+    if not any(it["k"] in ("rollup", "cube", "grouping_sets") for it in items):
+        return items, None
+    keys: list = []
+
+    def pos(e):
+        keys.append(e)
+        return len(keys) - 1
+
+    def elem(lst):  # a grouping element: list node of expressions
+        return [pos(e) for e in lst["c"]]
+
+    def item_sets(it):
+        k = it["k"]
+        if k == "rollup":
+            els = [elem(x) for x in it["c"]]
+            return [sum(els[:i], []) for i in range(len(els), -1, -1)]
+        if k == "cube":
+            els = [elem(x) for x in it["c"]]
+            out = []
+            for mask in range((1 << len(els)) - 1, -1, -1):
+                out.append(sum((els[i] for i in range(len(els)) if mask >> (len(els) - 1 - i) & 1), []))
+            return out
+        if k == "grouping_sets":
+            out = []
+            for x in it["c"]:
+                if x["k"] in ("rollup", "cube"):
+                    out += item_sets(x)
+                else:
+                    out.append(elem(x))
+            return out
+        return [[pos(it)]]
+
+    sets = [[]]
+    for it in items:
+        sets = [a + b for a in sets for b in item_sets(it)]
+    if len(sets) > 4096:
+        raise PlanError("too many grouping sets")
+    return keys, sets
+
+
+def _contains_grouping(e: Expr) -> bool:
+    return any(isinstance(x, Func) and x.name == "grouping" for x in walk(e))
+
+
 def _rename(p: Project, schema: List[ColInfo]) -> Project:
     return Project(p.input, [(s, e) for s, (_, e) in zip(schema, p.exprs)])
 

@@ -280,6 +280,77 @@ class AggCall(Expr):
         return f"{self.func.upper()}({a})"
 
 
+#: window-function frame bound kinds (sql order: a frame's start never comes after its end)
+FRAME_KINDS = ("unbounded_preceding", "preceding", "current", "following", "unbounded_following")
+RANKING_FUNCS = ("row_number", "rank", "dense_rank", "percent_rank", "cume_dist", "ntile")
+VALUE_FUNCS = ("lag", "lead", "first_value", "last_value", "nth_value")
+
+
+@dataclass(eq=False)
+class WindowFrame:
+    """ROWS / RANGE / GROUPS frame: bound kinds (FRAME_KINDS) and offsets
+    (``Lit`` in the ORDER BY key's representation for RANGE, int otherwise)."""
+    unit: str
+    start: str
+    end: str
+    start_off: Any = None
+    end_off: Any = None
+
+    def sql(self) -> str:
+        def b(kind, off):
+            if kind in ("preceding", "following"):
+                v = off.sql() if isinstance(off, Lit) else str(off)
+                return f"{v} {kind.upper()}"
+            return kind.replace("_", " ").upper().replace("CURRENT", "CURRENT ROW")
+        return f"{self.unit.upper()} BETWEEN {b(self.start, self.start_off)} AND {b(self.end, self.end_off)}"
+
+
+@dataclass(eq=False)
+class WindowCall(Expr):
+    """``func(args) [FILTER (WHERE f)] OVER (PARTITION BY .. ORDER BY .. frame)``.
+    Aggregates (sum/count/avg/min/max/stddev/var/bool_*), ranking functions
+    and value functions; ``options`` holds constant arguments (ntile buckets,
+    lag/lead offset, nth_value position)."""
+    func: str
+    args: List[Expr]
+    partition: List[Expr]
+    order: List[Tuple[Expr, bool, bool]]   # (expr, ascending, nulls_first)
+    frame: WindowFrame
+    dtype: DataType
+    filter: Optional[Expr] = None
+    options: Tuple = ()
+
+    @property
+    def nullable(self) -> bool:  # type: ignore[override]
+        return self.func not in ("row_number", "rank", "dense_rank", "percent_rank", "cume_dist", "ntile", "count")
+
+    def children(self):
+        out = list(self.args) + list(self.partition) + [e for e, _, _ in self.order]
+        if self.filter is not None:
+            out.append(self.filter)
+        return out
+
+    def with_children(self, kids):
+        na, np_ = len(self.args), len(self.partition)
+        no = len(self.order)
+        args = kids[:na]
+        part = kids[na:na + np_]
+        order = [(k, a, nf) for k, (_, a, nf) in zip(kids[na + np_:na + np_ + no], self.order)]
+        flt = kids[na + np_ + no] if self.filter is not None else None
+        return WindowCall(self.func, list(args), list(part), order, self.frame, self.dtype, flt, self.options)
+
+    def spec_sql(self) -> str:
+        p = ", ".join(e.sql() for e in self.partition)
+        o = ", ".join(f"{e.sql()} {'ASC' if a else 'DESC'} NULLS {'FIRST' if nf else 'LAST'}" for e, a, nf in self.order)
+        return (f"PARTITION BY {p} " if p else "") + (f"ORDER BY {o}" if o else "")
+
+    def sql(self):
+        opt = f"[{','.join(map(str, self.options))}]" if self.options else ""
+        f = f" FILTER (WHERE {self.filter.sql()})" if self.filter is not None else ""
+        return (f"{self.func}{opt}({', '.join(a.sql() for a in self.args)}){f} OVER "
+                f"({self.spec_sql()} {self.frame.sql()})")
+
+
 @dataclass(eq=False)
 class SubqueryExpr(Expr):
     """Unresolved subquery in an expression: kind in {scalar, exists, in}."""
@@ -335,6 +406,10 @@ def has_subquery(e: Expr) -> bool:
 
 def has_agg(e: Expr) -> bool:
     return any(isinstance(x, AggCall) for x in walk(e))
+
+
+def has_window(e: Expr) -> bool:
+    return any(isinstance(x, WindowCall) for x in walk(e))
 
 
 def conjuncts(e: Optional[Expr]) -> List[Expr]:

@@ -14,7 +14,7 @@ from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from ..types import DataType
-from .expr import AggCall, ColRef, Expr
+from .expr import AggCall, ColRef, Expr, WindowCall
 
 
 @dataclass
@@ -76,7 +76,9 @@ class Values(Plan):
     schema: List[ColInfo]
 
     def label(self):
-        return f"Values: {len(self.rows)} rows"
+        body = "; ".join(", ".join(e.sql() for e in r) for r in self.rows[:4])
+        more = f" +{len(self.rows) - 4}" if len(self.rows) > 4 else ""
+        return f"Values: {len(self.rows)} rows [{body}{more}]"
 
 
 @dataclass(eq=False)
@@ -296,6 +298,61 @@ class Union(Plan):
 
     def label(self):
         return "Union"
+
+
+@dataclass(eq=False)
+class Window(Plan):
+    """Window functions over ``input``: the input's columns plus one column per
+    window call (SURVEY E4 "Window"; DataFusion WindowAggExec)."""
+    input: Plan
+    wexprs: List[Tuple[ColInfo, WindowCall]]
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return self.input.schema + [c for c, _ in self.wexprs]
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Window(inputs[0], self.wexprs)
+
+    def label(self):
+        return "Window: " + ", ".join(f"{w.sql()} AS {c.name}#{c.cid}" for c, w in self.wexprs)
+
+
+@dataclass(eq=False)
+class WorkTableScan(Plan):
+    """The rows of the previous iteration of a recursive CTE (``table_id``)."""
+    table_id: int
+    schema: List[ColInfo]
+
+    def label(self):
+        return f"WorkTable: #{self.table_id} subquery"
+
+
+@dataclass(eq=False)
+class RecursiveCTE(Plan):
+    """WITH RECURSIVE: ``anchor`` once, then ``recursive`` over the previous
+    iteration's rows (``WorkTableScan(table_id)``) until it yields none;
+    ``distinct`` (UNION) drops rows already produced."""
+    anchor: Plan
+    recursive: Plan
+    table_id: int
+    schema: List[ColInfo]
+    distinct: bool = False
+    max_iterations: int = 1000
+
+    @property
+    def inputs(self):
+        return [self.anchor, self.recursive]
+
+    def with_inputs(self, inputs):
+        return RecursiveCTE(inputs[0], inputs[1], self.table_id, self.schema, self.distinct, self.max_iterations)
+
+    def label(self):
+        return f"RecursiveCTE: #{self.table_id}{' distinct' if self.distinct else ''} subquery"
 
 
 def transform_plan(p: Plan, fn) -> Plan:

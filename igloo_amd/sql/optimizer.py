@@ -23,8 +23,8 @@ from ..types import BOOL
 from ..utils.errors import NotSupported, PlanError
 from .expr import (AggCall, BinOp, ColRef, Expr, Not, SubqueryExpr, and_all, col_refs, conjuncts, has_subquery,
                    replace_cols, transform, walk)
-from .logical import (Aggregate, ColInfo, Filter, Join, Limit, MultiJoin, Plan, Project, Scan, SemiSpec, Sort,
-                      Union, Values, produced_cids, transform_plan, walk_plan)
+from .logical import (Aggregate, ColInfo, Filter, Join, Limit, MultiJoin, Plan, Project, RecursiveCTE, Scan, SemiSpec,
+                      Sort, Union, Values, Window, WorkTableScan, produced_cids, transform_plan, walk_plan)
 
 
 def optimize(plan: Plan) -> Plan:
@@ -80,6 +80,8 @@ def _plan_exprs(p: Plan) -> List[Expr]:
         return [e for e, _, _ in p.keys]
     if isinstance(p, Scan):
         return list(p.filters)
+    if isinstance(p, Window):
+        return [w for _, w in p.wexprs]
     return []
 
 
@@ -371,6 +373,21 @@ def push_filters(p: Plan, preds: List[Expr]) -> Plan:
         return _wrap(Limit(push_filters(p.input, []), p.limit, p.offset), preds)
     if isinstance(p, Union):
         return _wrap(Union([push_filters(ch, []) for ch in p.children], p.schema), preds)
+    if isinstance(p, Window):
+        # a predicate on keys every window call partitions by keeps whole
+        # partitions: it may run before the window functions
+        common = None
+        for _, w in p.wexprs:
+            ks = {e.cid for e in w.partition if isinstance(e, ColRef)}
+            common = ks if common is None else common & ks
+        down, above = [], []
+        for c in preds:
+            refs = col_refs(c)
+            (down if refs and common and refs <= common and not has_subquery(c) else above).append(c)
+        return _wrap(Window(push_filters(p.input, down), p.wexprs), above)
+    if isinstance(p, RecursiveCTE):
+        return _wrap(RecursiveCTE(push_filters(p.anchor, []), push_filters(p.recursive, []), p.table_id, p.schema,
+                                  p.distinct, p.max_iterations), preds)
     return _wrap(p, preds)
 
 
@@ -467,4 +484,14 @@ def prune(p: Plan, required: Set[int]) -> Plan:
         return Limit(prune(p.input, required), p.limit, p.offset)
     if isinstance(p, Union):
         return Union([prune(ch, set(ch.cids())) for ch in p.children], p.schema)
+    if isinstance(p, Window):
+        wexprs = [(c, w) for c, w in p.wexprs if c.cid in required]
+        in_cids = set(p.input.cids())
+        need = (required & in_cids) | _refs(w for _, w in wexprs)
+        if not wexprs:
+            return prune(p.input, need)
+        return Window(prune(p.input, need), wexprs)
+    if isinstance(p, RecursiveCTE):
+        return RecursiveCTE(prune(p.anchor, set(p.anchor.cids())), prune(p.recursive, set(p.recursive.cids())),
+                            p.table_id, p.schema, p.distinct, p.max_iterations)
     return p
