@@ -672,6 +672,20 @@ PYBIND11_MODULE(_native, m) {
   m.def("partition_ids", [](uintptr_t keys, bool key64, int64_t n, int nparts, uintptr_t out, uintptr_t s) {
     kern::partition_ids(P<const void>(keys), key64, n, nparts, P<int32_t>(out), S(s));
   });
+  m.def("str_fn_lengths", [](int fn, int64_t n1, uintptr_t a, int64_t alen, uintptr_t b, int64_t blen, uintptr_t off,
+                             uintptr_t chars, int64_t n, uintptr_t len, uintptr_t s) {
+    kern::StrFnArgs args{fn, n1, P<uint8_t>(a), alen, P<uint8_t>(b), blen};
+    kern::str_fn_lengths(args, P<int64_t>(off), P<uint8_t>(chars), n, P<int64_t>(len), S(s));
+  });
+  m.def("str_fn_copy", [](int fn, int64_t n1, uintptr_t a, int64_t alen, uintptr_t b, int64_t blen, uintptr_t off,
+                          uintptr_t chars, int64_t n, uintptr_t new_off, uintptr_t out, uintptr_t s) {
+    kern::StrFnArgs args{fn, n1, P<uint8_t>(a), alen, P<uint8_t>(b), blen};
+    kern::str_fn_copy(args, P<int64_t>(off), P<uint8_t>(chars), n, P<int64_t>(new_off), P<uint8_t>(out), S(s));
+  });
+  m.def("str_fn_int", [](int fn, uintptr_t pat, int64_t plen, uintptr_t off, uintptr_t chars, int64_t n, uintptr_t out,
+                         uintptr_t s) {
+    kern::str_fn_int(fn, P<uint8_t>(pat), plen, P<int64_t>(off), P<uint8_t>(chars), n, P<int32_t>(out), S(s));
+  });
   m.def("win_scan_tiles", &kern::win_scan_tiles);
   m.def("win_seg_scan", [](uintptr_t ids, bool ids64, uintptr_t ids2, bool ids2_64, uintptr_t vals, int vkind,
                            uintptr_t valid, int64_t n, int op, bool reverse, uintptr_t tflag, uintptr_t tval,

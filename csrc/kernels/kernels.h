@@ -445,5 +445,26 @@ void win_rank(int fn, int64_t arg, int64_t n, const int64_t* seg_start, const in
 void win_index(int fn, int64_t arg, int64_t n, const int64_t* seg_start, const int64_t* seg_end, const int64_t* lo,
                const int64_t* hi, int64_t* out, hipStream_t s);
 
+// ---- strfunc.hip (scalar string functions over plain UTF-8 columns)
+enum StrFnCode {
+  kSfTrim = 0, kSfReplace = 1, kSfLpad = 2, kSfRpad = 3, kSfReverse = 4, kSfRepeat = 5, kSfLeft = 6, kSfRight = 7,
+  kSfInitcap = 8, kSfTranslate = 9, kSfSplitPart = 10,
+  kSfStrpos = 20, kSfAscii = 21, kSfOctetLength = 22
+};
+struct StrFnArgs {
+  int fn;
+  int64_t n1;              // trim mode bits (1 left, 2 right) / pad length / repeat count / left-right n / part
+  const uint8_t* a;        // device bytes: trim set / search / fill / from-chars / delimiter
+  int64_t alen;
+  const uint8_t* b;        // device bytes: replacement / to-chars
+  int64_t blen;
+};
+void str_fn_lengths(const StrFnArgs& a, const int64_t* off, const uint8_t* chars, int64_t n, int64_t* len,
+                    hipStream_t s);
+void str_fn_copy(const StrFnArgs& a, const int64_t* off, const uint8_t* chars, int64_t n, const int64_t* new_off,
+                 uint8_t* out, hipStream_t s);
+void str_fn_int(int fn, const uint8_t* pat, int64_t plen, const int64_t* off, const uint8_t* chars, int64_t n,
+                int32_t* out, hipStream_t s);
+
 }  // namespace kern
 }  // namespace igloo

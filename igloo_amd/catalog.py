@@ -165,6 +165,15 @@ class Catalog:
             self.version += 1
             self.views[name] = sql
 
+    def drop_view(self, name: str):
+        with self._lock:
+            self.version += 1
+            return self.views.pop(name, None)
+
+    def view_names(self) -> List[str]:
+        with self._lock:
+            return sorted(self.views)
+
     def get_view(self, name: str) -> Optional[str]:
         with self._lock:
             return self.views.get(name)

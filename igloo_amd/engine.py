@@ -24,9 +24,9 @@ from .exec.operators import ExecContext
 from .exec.planner import create_physical_plan
 from .sql import parse
 from .sql.binder import Binder, IdGen
-from .sql.logical import ColInfo, Plan
+from .sql.logical import ColInfo, Plan, Project
 from .sql.optimizer import optimize
-from .utils.errors import ExecutionError, IglooError, NotSupported, PlanError
+from .utils.errors import ExecutionError, IglooError, NotSupported, PlanError, TableNotFound
 from .exec import graphs as _graphs
 from .ops import jit as _jit
 from .utils import trace as _trace
@@ -317,7 +317,16 @@ class QueryEngine:
             self.session[st["s"]] = getattr(v, "value", None)
             return QueryResult(pa.table({}), 0.0)
         if k == "show":
+            if st["s"] == "columns":
+                return self._describe(st["table"], full=True)
+            if st["s"] == "all":
+                keys = sorted(self.session)
+                return QueryResult(pa.table({"name": pa.array(keys, pa.string()),
+                                             "value": pa.array([str(self.session[k]) for k in keys], pa.string())}),
+                                   0.0)
             if st["s"] != "tables":
+                if st["s"] in self.session:
+                    return QueryResult(pa.table({"name": [st["s"]], "value": [str(self.session[st["s"]])]}), 0.0)
                 raise NotSupported(f"SHOW {st['s']}")
             names = self.catalog.table_names()
             return QueryResult(pa.table({"table_name": pa.array(names, pa.string())}), 0.0)
@@ -326,7 +335,43 @@ class QueryEngine:
                 raise PlanError(f"table '{st['s']}' does not exist")
             return QueryResult(pa.table({}), 0.0)
         if k == "create_view":
-            raise NotSupported("CREATE VIEW (use the Python API register_view)")
+            name = st["s"]
+            if self.catalog.get_view(name) is not None or self.catalog.get_table(name) is not None:
+                if st.get("if_not_exists"):
+                    return QueryResult(pa.table({}), 0.0)
+                if not st.get("replace") or self.catalog.get_table(name) is not None:
+                    raise PlanError(f"'{name}' already exists")
+            view = dict(st["query"])
+            cols = [c["s"] for c in (st.get("columns") or {}).get("c", [])]
+            # bind once now: an invalid view fails at CREATE, like DataFusion
+            bq = Binder(self.catalog, self._ids, self.session).bind_query(view)
+            if cols:
+                if len(cols) != len(bq.names):
+                    raise PlanError(f"view '{name}' lists {len(cols)} columns for {len(bq.names)}")
+                view["__columns"] = cols
+            self.catalog.register_view(name, view)
+            return QueryResult(pa.table({}), 0.0)
+        if k == "drop_view":
+            if self.catalog.get_view(st["s"]) is None:
+                if not st.get("if_exists"):
+                    raise PlanError(f"view '{st['s']}' does not exist")
+                return QueryResult(pa.table({}), 0.0)
+            self.catalog.drop_view(st["s"])
+            return QueryResult(pa.table({}), 0.0)
+        if k == "describe":
+            return self._describe(st["s"])
+        if k == "insert":
+            return self._insert(st)
+        if k == "truncate":
+            src = self.catalog.get_table(st["s"])
+            if not isinstance(src, MemoryTable):
+                raise NotSupported("TRUNCATE of a table that is not in memory")
+            empty = {f.name: src.columns[f.name] for f in src.schema()}
+            from .ops.gather import take_many
+            idx = torch.zeros(0, dtype=torch.int64, device=next(iter(empty.values())).device) if empty else None
+            cols = dict(zip(empty, take_many(list(empty.values()), idx))) if empty else {}
+            self.register_table(st["s"], MemoryTable(cols, 0, fields=list(src.schema())))
+            return QueryResult(pa.table({"count": pa.array([src.num_rows()], pa.int64())}), 0.0)
         if k == "create_external_table":
             return self._create_external(st)
         if k == "create_table":
@@ -339,6 +384,84 @@ class QueryEngine:
                 return QueryResult(pa.table({"count": [batch.num_rows]}), 0.0)
             raise NotSupported("CREATE TABLE without AS SELECT")
         raise NotSupported(f"statement {k}")
+
+    def _describe(self, name: str, full: bool = False) -> QueryResult:
+        """DESCRIBE t / SHOW COLUMNS FROM t (DataFusion's column layout)."""
+        src = self.catalog.get_table(name)
+        if src is not None:
+            fields = [(f.name, f.dtype, f.nullable) for f in src.schema()]
+        else:
+            view = self.catalog.get_view(name)
+            if view is None:
+                raise TableNotFound(f"table '{name}' not found")
+            plan, names = self._plan_query({"k": "query", "s": "", "c": [], "pos": 0,
+                                            "body": {"k": "select", "s": "", "c": [], "pos": 0,
+                                                     "items": {"k": "list", "s": "", "c": [{"k": "star", "s": "",
+                                                                                            "c": [], "pos": 0}],
+                                                               "pos": 0},
+                                                     "from": {"k": "list", "s": "", "pos": 0,
+                                                              "c": [{"k": "table", "s": name, "c": [], "pos": 0}]}}})
+            fields = [(n, c.dtype, c.nullable) for n, c in zip(names, plan.schema)]
+        cols = {"column_name": pa.array([f[0] for f in fields], pa.string()),
+                "data_type": pa.array([str(f[1]) for f in fields], pa.string()),
+                "is_nullable": pa.array(["YES" if f[2] else "NO" for f in fields], pa.string())}
+        if full:
+            cols = {"table_catalog": pa.array(["datafusion"] * len(fields), pa.string()),
+                    "table_schema": pa.array(["public"] * len(fields), pa.string()),
+                    "table_name": pa.array([name] * len(fields), pa.string()), **cols}
+        return QueryResult(pa.table(cols), 0.0)
+
+    def _insert(self, st) -> QueryResult:
+        """INSERT INTO t [(cols)] VALUES ... | SELECT ...: appends to an
+        in-memory table (the new rows are cast to the table's column types;
+        unlisted columns are NULL)."""
+        from .exec.joins import concat_columns
+        from .sql.expr import Cast, Lit
+        name = st["s"]
+        src = self.catalog.get_table(name)
+        if src is None:
+            raise TableNotFound(f"table '{name}' not found")
+        if not isinstance(src, MemoryTable):
+            raise NotSupported(f"INSERT INTO '{name}': only in-memory tables accept inserts")
+        fields = list(src.schema())
+        target = [c["s"] for c in (st.get("columns") or {}).get("c", [])] or [f.name for f in fields]
+        known = {f.name: f for f in fields}
+        for c in target:
+            if c not in known:
+                raise PlanError(f"column '{c}' not found in '{name}'")
+        b = Binder(self.catalog, self._ids, self.session)
+        bq = b.bind_query(st["query"])
+        if len(bq.plan.schema) != len(target):
+            raise PlanError(f"INSERT has {len(bq.plan.schema)} columns but {len(target)} target columns")
+        plan = bq.plan
+        exprs = []
+        by_name = dict(zip(target, plan.schema))
+        for f in fields:
+            ci = ColInfo(b.ids(), f.name, f.dtype, True)
+            if f.name in by_name:
+                e = by_name[f.name].ref()
+                exprs.append((ci, e if e.dtype == f.dtype else Cast(e, f.dtype)))
+            else:
+                if not f.nullable:
+                    raise PlanError(f"column '{f.name}' of '{name}' is NOT NULL and has no value")
+                exprs.append((ci, Lit(None, f.dtype)))
+        plan = Project(plan, exprs)
+        batch = self._execute_plan(optimize(plan))
+        dev = next(iter(src.columns.values())).device if src.columns else self.device
+        new = {}
+        for (ci, _), f in zip(exprs, fields):
+            col = batch.columns[ci.cid].to(dev)
+            if col.dtype.is_string and col.is_dict:
+                from .ops import strings as S
+                col = S.decode(col)
+            old = src.columns[f.name]
+            if old.is_dict:
+                from .ops import strings as S
+                old = S.decode(old)
+            new[f.name] = concat_columns([old, col]) if src.num_rows() else col
+        fl = [Field(f.name, f.dtype, f.nullable or new[f.name].valid is not None) for f in fields]
+        self.register_table(name, MemoryTable(new, src.num_rows() + batch.num_rows, fields=fl))
+        return QueryResult(pa.table({"count": pa.array([batch.num_rows], pa.int64())}), 0.0)
 
     def _create_external(self, st) -> QueryResult:
         name = st["s"]

@@ -812,11 +812,15 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
         fm = ev.mask(a.filter, b)
         valid = fm if valid is None else (valid & fm)
     if a.distinct and func in ("count", "sum", "avg"):
-        # de-duplicate (group, value) pairs first, then aggregate the survivors
+        # de-duplicate (group, value) pairs first, then aggregate the survivors;
+        # rows a FILTER (or NULL) drops share one sentinel pair, so each kept
+        # pair's first row is a row that passes
         k, _ = group_key_tensor(col)
         pair = H.pack_keys([gid.to(torch.int64) if gid is not None else torch.zeros(n, dtype=torch.int64, device=dev), k])
         keep_rows = torch.ones(n, dtype=torch.bool, device=dev) if valid is None else valid
         if n:
+            if valid is not None:
+                pair = torch.where(valid, pair.to(torch.int64), torch.full((n,), -1, dtype=torch.int64, device=dev))
             keep_rows = keep_rows & H.first_rows_mask(pair)
         valid = keep_rows
     base = len(specs)
@@ -829,6 +833,34 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
     if func == "count":
         i = add("count", None, valid)
         finals.append(lambda r, i=i: (ci, Column(T.INT64, r[i])))
+        return
+    if func in ("median", "percentile"):
+        out = _order_stat(a, col, valid, gid, ng, n, ctx)
+        finals.append(lambda r, out=out: (ci, out))
+        return
+    if func == "string_agg":
+        out = _string_agg(a, col, valid, gid, ng, n, ctx)
+        finals.append(lambda r, out=out: (ci, out))
+        return
+    if func in ("covar_samp", "covar_pop", "corr"):
+        c2 = ev.column(a.arg2, b)
+        both = valid if c2.valid is None else (c2.valid if valid is None else valid & c2.valid)
+        x = _convert_tensor(col, T.FLOAT64).contiguous()
+        y = _convert_tensor(c2, T.FLOAT64).contiguous()
+        ids = [add("sum_f64", v.contiguous(), both) for v in (x, y, x * y, x * x, y * y)]
+        ic = add("count", None, both)
+
+        def fin(r, ids=ids, ic=ic):
+            sx, sy, sxy, sxx, syy = (r[i] for i in ids)
+            c = r[ic].to(torch.float64)
+            if func == "corr":
+                num = c * sxy - sx * sy
+                den = ((c * sxx - sx * sx) * (c * syy - sy * sy)).clamp(min=0).sqrt()
+                return ci, Column(T.FLOAT64, num / den.clamp(min=1e-300), (c > 1) & (den > 0))
+            pop = func == "covar_pop"
+            cov = (sxy - sx * sy / c.clamp(min=1)) / (c if pop else c - 1).clamp(min=1)
+            return ci, Column(T.FLOAT64, cov, c > (0 if pop else 1))
+        finals.append(fin)
         return
     if col is None:
         raise ExecutionError(f"{func} needs an argument")
@@ -915,6 +947,84 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
         finals.append(fin)
         return
     raise NotSupported(f"aggregate {func}")
+
+
+def _group_sorted(x: torch.Tensor, valid, gid, ng: int, n: int, ctx, by_value: bool):
+    """Valid rows ordered by (group[, value]) -> (row ids, per-group counts,
+    per-group first position)."""
+    from ..ops import sort as SO
+    from ..ops.select import mask_to_indices
+    dev = ctx.device
+    rows = mask_to_indices(valid).to(torch.int64) if valid is not None else \
+        torch.arange(n, dtype=torch.int64, device=dev)
+    m = rows.numel()
+    g = gather_tensor(gid, rows).to(torch.int64) if gid is not None else torch.zeros(m, dtype=torch.int64, device=dev)
+    keys = [] if gid is None else [(g, False, False, None)]
+    if by_value:
+        keys.append((gather_tensor(x, rows), False, False, None))
+    if keys and m > 1:
+        perm = SO.argsort(keys, m, dev).to(torch.int64)
+        rows, g = gather_tensor(rows, perm), gather_tensor(g, perm)
+    counts = torch.bincount(g, minlength=ng)[:ng] if m else torch.zeros(ng, dtype=torch.int64, device=dev)
+    starts = torch.cumsum(counts, 0) - counts
+    return rows, counts, starts
+
+
+def _order_stat(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Column:
+    """median (middle value; the mean of the two middle values, truncated in
+    the input type) and approx_percentile_cont (linear interpolation) per group."""
+    t = a.dtype
+    fl = col.dtype.is_float or col.is_wide or a.func == "percentile"
+    x = _convert_tensor(col, T.FLOAT64) if (fl or col.is_wide) else col.data.to(torch.int64)
+    rows, counts, starts = _group_sorted(x, valid, gid, ng, n, ctx, True)
+    xs = gather_tensor(x, rows) if rows.numel() else x[:0]
+    last = max(rows.numel() - 1, 0)
+    ok = counts > 0
+    if not rows.numel():
+        return Column(t, torch.zeros(ng, dtype=t.torch_dtype if t.kind != "decimal" else torch.int64,
+                                     device=ctx.device), ok)
+    if a.func == "percentile":
+        pos = (counts - 1).clamp(min=0).to(torch.float64) * float(a.param)
+        lo = pos.floor().to(torch.int64)
+        frac = pos - lo.to(torch.float64)
+        hi_ = torch.minimum(lo + 1, (counts - 1).clamp(min=0))
+        v0 = gather_tensor(xs, (starts + lo).clamp(0, last))
+        v1 = gather_tensor(xs, (starts + hi_).clamp(0, last))
+        return Column(T.FLOAT64, v0 + (v1 - v0) * frac, ok)
+    lo = (starts + torch.div(counts - 1, 2, rounding_mode="floor")).clamp(0, last)
+    hi_ = (starts + torch.div(counts, 2, rounding_mode="floor")).clamp(0, last)
+    v0, v1 = gather_tensor(xs, lo), gather_tensor(xs, hi_)
+    if x.dtype == torch.float64:
+        med = (v0 + v1) / 2
+        return Column(t, med if t.is_float else med.to(torch.int64), ok)
+    med = torch.div(v0 + v1, 2, rounding_mode="trunc")
+    return Column(t, med.to(t.torch_dtype) if not t.is_decimal else med, ok)
+
+
+def _string_agg(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Column:
+    """string_agg(s, sep): each group's strings in input order joined by sep.
+    Rows are ordered by group (stable), a separator is prefixed to every row
+    that does not start its group, and each group's string is then one
+    contiguous byte range of the concatenated pieces: the output offsets are
+    the pieces' offsets at the group starts (no per-group copy)."""
+    from ..ops.gather import take
+    dev = ctx.device
+    rows, counts, starts = _group_sorted(None, valid, gid, ng, n, ctx, False)
+    m = rows.numel()
+    if m == 0:
+        z = torch.zeros(ng + 1, dtype=torch.int64, device=dev)
+        return Column(T.UTF8, torch.zeros(0, dtype=torch.uint8, device=dev), counts > 0, offsets=z)
+    sv = S.decode(take(col, rows))
+    sv = Column(T.UTF8, sv.data, None, offsets=sv.offsets)
+    head = torch.zeros(m, dtype=torch.bool, device=dev)
+    head.index_fill_(0, starts[counts > 0], True)
+    sep = S.const_column(str(a.param), dev)
+    empty = S.const_column("", dev)
+    prefix = S.select_rows([empty, sep], (~head).to(torch.int64), m)
+    pieces = S.concat(prefix, sv, m)
+    off = pieces.offsets
+    out_off = torch.cat([gather_tensor(off, starts.clamp(max=m)), off[m:m + 1]])
+    return Column(T.UTF8, pieces.data, counts > 0, offsets=out_off)
 
 
 def _avg(s: torch.Tensor, c: torch.Tensor, src, t) -> torch.Tensor:

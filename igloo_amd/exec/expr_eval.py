@@ -347,6 +347,12 @@ class Evaluator:
                 return v
             if src.is_decimal or src.kind in ("date32",) or src.is_numeric or src.kind == "bool":
                 return S.to_string(v)       # GPU text formatting (strexpr.hip)
+        if t.kind == "timestamp" and src.kind == "date32":
+            return Column(t, v.data.to(torch.int64) * _US_DAY, v.valid)
+        if t.kind == "date32" and src.kind == "timestamp":
+            return Column(t, torch.div(v.data, _US_DAY, rounding_mode="floor").to(torch.int32), v.valid)
+        if src.is_string and t.kind == "timestamp":
+            return _parse_ts_host(v)
         if src.is_string:
             return S.parse(v, t)            # GPU parse (strexpr.hip); malformed -> error
         if t.kind == "bool":
@@ -441,7 +447,7 @@ class Evaluator:
     def _Func(self, e: Func, b: Batch) -> Value:
         name = e.name
         args = [self.eval(a, b) for a in e.args]
-        if all(isinstance(a, Scalar) for a in args) and name not in ("coalesce",):
+        if args and all(isinstance(a, Scalar) for a in args) and name not in ("coalesce",):
             return self._func_scalar(e, args)
         if name == "upper":
             return S.upper(args[0])
@@ -455,7 +461,74 @@ class Evaluator:
             return Column(T.INT32, S.char_length(c), c.valid)
         if name == "date_part":
             c = args[0]
+            if e.options[0] == "week":
+                return Column(T.INT32, iso_week(c.data.to(torch.int64)).to(torch.int32), c.valid)
             return Column(T.INT32, M.date_part(c.data, e.options[0]), c.valid)
+        if name in _STRFN:
+            from ..ops import strfuncs as SF
+            c = args[0]
+            return SF.apply(c, name, e.options)
+        if name in ("strpos", "ascii", "octet_length"):
+            from ..ops import strfuncs as SF
+            c = args[0]
+            return Column(T.INT32, SF.apply_int(c, name, e.options), c.valid)
+        if name in ("regexp_like", "regexp_count", "regexp_replace"):
+            from ..ops import strfuncs as SF
+            c = args[0]
+            if name == "regexp_replace":
+                pat, rep, flags = e.options
+                return SF.regexp(c, name, pat, rep, flags)
+            pat, flags = e.options
+            return Column(e.dtype, SF.regexp(c, name, pat, None, flags), c.valid)
+        if name in _MATH1:
+            c = args[0]
+            x = _convert_tensor(c, T.FLOAT64) if name != "factorial" else c.data.to(torch.int64)
+            return Column(e.dtype, _math1(name, x, e.options), c.valid)
+        if name in ("logb", "atan2", "nanvl"):
+            a, va = self._num(args[0], T.FLOAT64)
+            c, vc = self._num(args[1], T.FLOAT64)
+            a = a if isinstance(a, torch.Tensor) else torch.tensor(a, dtype=torch.float64, device=self.device(b))
+            if name == "logb":
+                out = torch.log(c) / torch.log(a)
+            elif name == "atan2":
+                out = torch.atan2(a, c)
+            else:
+                out = torch.where(torch.isnan(a), c if isinstance(c, torch.Tensor) else torch.full_like(a, c), a)
+            return self._mk(out, T.FLOAT64, _and_valid(va, vc), b)
+        if name == "random":
+            return Column(T.FLOAT64, torch.rand(b.num_rows, dtype=torch.float64, device=self.device(b)))
+        if name in ("greatest", "least"):
+            return self._extreme(e, args, b)
+        if name in ("gcd", "lcm"):
+            a, va = self._num(args[0], T.INT64)
+            c, vc = self._num(args[1], T.INT64)
+            a = a if isinstance(a, torch.Tensor) else torch.full((b.num_rows,), a, dtype=torch.int64,
+                                                                  device=self.device(b))
+            g = torch.gcd(a, c if isinstance(c, torch.Tensor) else torch.full_like(a, c))
+            out = g if name == "gcd" else torch.where(g == 0, torch.zeros_like(g), (a * c).abs() // g.clamp(min=1))
+            return self._mk(out, T.INT64, _and_valid(va, vc), b)
+        if name == "date_trunc":
+            c = args[0]
+            return Column(T.TIMESTAMP, trunc_ts(c.data.to(torch.int64), e.options[0]), c.valid)
+        if name == "ts_add":
+            c = args[0]
+            return Column(T.TIMESTAMP, ts_add(c.data.to(torch.int64), *e.options), c.valid)
+        if name == "ts_part":
+            c = args[0]
+            out = ts_part(c.data.to(torch.int64), e.options[0])
+            return Column(e.dtype, out.to(e.dtype.torch_dtype), c.valid)
+        if name == "to_unixtime":
+            c = args[0]
+            return Column(T.INT64, torch.div(c.data.to(torch.int64), 1_000_000, rounding_mode="floor"), c.valid)
+        if name == "ts_from_float":
+            c = args[0]
+            return Column(T.TIMESTAMP, (c.data.to(torch.float64) * 1e6).round().to(torch.int64), c.valid)
+        if name == "make_date":
+            ys, ms, ds = [self._num(a, T.INT64) for a in args]
+            vals = [x if isinstance(x, torch.Tensor) else torch.full((b.num_rows,), x, dtype=torch.int64,
+                                                                    device=self.device(b)) for x, _ in (ys, ms, ds)]
+            valid = _and_valid(_and_valid(ys[1], ms[1]), ds[1])
+            return Column(T.DATE32, days_from_civil(*vals).to(torch.int32), valid)
         if name == "add_months":
             months, days = e.options
             c = args[0]
@@ -477,7 +550,9 @@ class Evaluator:
             if c.dtype.is_integer:
                 return c
             f = 10.0**d
-            return Column(T.FLOAT64, torch.round(c.data.double() * f) / f, c.valid)
+            x = c.data.double() * f
+            # half away from zero (Rust f64::round, what DataFusion's round uses)
+            return Column(T.FLOAT64, torch.sign(x) * torch.floor(x.abs() + 0.5) / f, c.valid)
         if name == "coalesce":
             return self._coalesce(e, args, b)
         if name == "concat":
@@ -528,7 +603,33 @@ class Evaluator:
             f = {"sqrt": math.sqrt, "ln": math.log, "log10": math.log10, "exp": math.exp, "floor": math.floor,
                  "ceil": math.ceil, "power": math.pow}[name]
             return Scalar(float(f(*[float(v) for v in vals])), T.FLOAT64)
-        raise NotSupported(f"function {name}")
+        # everything else: the column path over a one-row batch
+        dev = torch.device(self.ctx.device if self.ctx is not None else "cpu")
+        cols = {i: Column.full(v, a.dtype, 1, dev) for i, (v, a) in enumerate(zip(vals, args))}
+        from ..sql.expr import ColRef as _CR
+        e1 = Func(e.name, [_CR(i, f"a{i}", a.dtype) for i, a in enumerate(args)], e.dtype, e.options)
+        r = self._Func(e1, Batch(cols, 1))
+        if isinstance(r, Scalar):
+            return r
+        return Scalar(_host_value(r, e.dtype), e.dtype)
+
+    def _extreme(self, e: Func, args, b: Batch) -> Value:
+        """greatest / least: the largest / smallest non-NULL argument."""
+        n = b.num_rows
+        dev = self.device(b)
+        t = e.dtype
+        out, valid = None, None
+        for a in args:
+            x, xv = _full_of(a, t, n, dev)
+            ok = xv if xv is not None else torch.ones(n, dtype=torch.bool, device=dev)
+            if out is None:
+                out, valid = x, ok
+                continue
+            better = (x > out) if e.name == "greatest" else (x < out)
+            take_x = ok & (~valid | better)
+            out = torch.where(take_x, x, out)
+            valid = valid | ok
+        return Column(t, out, None if bool(valid.all()) and not valid.is_cuda else valid)
 
     def _coalesce(self, e: Func, args, b: Batch) -> Value:
         n = b.num_rows
@@ -555,6 +656,147 @@ class Evaluator:
             out = torch.where(xv, x, out)
             valid = xv | valid if valid is not None else None
         return Column(t, out, valid)
+
+
+_STRFN = ("trim", "replace", "lpad", "rpad", "reverse", "repeat", "left", "right", "initcap", "translate",
+          "split_part")
+_MATH1 = ("sign", "trunc", "log2", "cbrt", "degrees", "radians", "sin", "cos", "tan", "asin", "acos", "atan", "sinh",
+          "cosh", "tanh", "isnan", "iszero", "factorial")
+_US_DAY = 86_400_000_000
+
+
+def _math1(name: str, x: torch.Tensor, options) -> torch.Tensor:
+    if name == "sign":
+        return torch.sign(x)
+    if name == "trunc":
+        d = options[0] if options else 0
+        f = 10.0 ** d
+        return torch.trunc(x * f) / f
+    if name == "log2":
+        return torch.log2(x)
+    if name == "cbrt":
+        return torch.sign(x) * x.abs().pow(1.0 / 3.0)
+    if name == "degrees":
+        return torch.rad2deg(x)
+    if name == "radians":
+        return torch.deg2rad(x)
+    if name == "isnan":
+        return torch.isnan(x)
+    if name == "iszero":
+        return x == 0
+    if name == "factorial":
+        lut = torch.tensor([math.factorial(i) for i in range(21)], dtype=torch.int64, device=x.device)
+        return lut.index_select(0, x.clamp(0, 20))
+    return getattr(torch, name)(x)
+
+
+def civil_from_days(days: torch.Tensor):
+    """(year, month, day) int64 tensors from days since 1970-01-01 (Hinnant)."""
+    z = days.to(torch.int64) + 719468
+    era = torch.div(z, 146097, rounding_mode="floor")
+    doe = z - era * 146097
+    yoe = torch.div(doe - torch.div(doe, 1460, rounding_mode="floor") + torch.div(doe, 36524, rounding_mode="floor")
+                    - torch.div(doe, 146096, rounding_mode="floor"), 365, rounding_mode="floor")
+    doy = doe - (365 * yoe + torch.div(yoe, 4, rounding_mode="floor") - torch.div(yoe, 100, rounding_mode="floor"))
+    mp = torch.div(5 * doy + 2, 153, rounding_mode="floor")
+    d = doy - torch.div(153 * mp + 2, 5, rounding_mode="floor") + 1
+    m = torch.where(mp < 10, mp + 3, mp - 9)
+    y = yoe + era * 400 + (m <= 2).to(torch.int64)
+    return y, m, d
+
+
+def days_from_civil(y: torch.Tensor, m: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+    yy = y - (m <= 2).to(torch.int64)
+    era = torch.div(yy, 400, rounding_mode="floor")
+    yoe = yy - era * 400
+    doy = torch.div(153 * torch.where(m > 2, m - 3, m + 9) + 2, 5, rounding_mode="floor") + d - 1
+    doe = yoe * 365 + torch.div(yoe, 4, rounding_mode="floor") - torch.div(yoe, 100, rounding_mode="floor") + doy
+    return era * 146097 + doe - 719468
+
+
+def iso_week(days: torch.Tensor) -> torch.Tensor:
+    wd = torch.remainder(days + 3, 7)            # Monday = 0 (1970-01-01 was a Thursday)
+    thu = days - wd + 3
+    y, _, _ = civil_from_days(thu)
+    jan1 = days_from_civil(y, torch.ones_like(y), torch.ones_like(y))
+    return torch.div(thu - jan1, 7, rounding_mode="floor") + 1
+
+
+def trunc_ts(us: torch.Tensor, unit: str) -> torch.Tensor:
+    """date_trunc over timestamps (microseconds since the epoch)."""
+    step = {"microsecond": 1, "millisecond": 1000, "second": 1_000_000, "minute": 60_000_000,
+            "hour": 3_600_000_000, "day": _US_DAY}.get(unit)
+    if step is not None:
+        return torch.div(us, step, rounding_mode="floor") * step
+    days = torch.div(us, _US_DAY, rounding_mode="floor")
+    if unit == "week":
+        return (days - torch.remainder(days + 3, 7)) * _US_DAY
+    y, m, _ = civil_from_days(days)
+    if unit == "quarter":
+        m = torch.div(m - 1, 3, rounding_mode="floor") * 3 + 1
+    elif unit == "year":
+        m = torch.ones_like(m)
+    return days_from_civil(y, m, torch.ones_like(m)) * _US_DAY
+
+
+def ts_add(us: torch.Tensor, months: int, days: int, micros: int) -> torch.Tensor:
+    d = torch.div(us, _US_DAY, rounding_mode="floor")
+    rem = us - d * _US_DAY
+    if months:
+        d = add_months(d, months).to(torch.int64)
+    return (d + days) * _US_DAY + rem + micros
+
+
+def ts_part(us: torch.Tensor, field: str) -> torch.Tensor:
+    if field == "epoch":
+        return us.to(torch.float64) / 1e6
+    days = torch.div(us, _US_DAY, rounding_mode="floor")
+    rem = us - days * _US_DAY
+    if field == "hour":
+        return torch.div(rem, 3_600_000_000, rounding_mode="floor")
+    if field == "minute":
+        return torch.remainder(torch.div(rem, 60_000_000, rounding_mode="floor"), 60)
+    if field == "second":
+        return torch.remainder(torch.div(rem, 1_000_000, rounding_mode="floor"), 60)
+    if field == "millisecond":
+        return torch.remainder(torch.div(rem, 1000, rounding_mode="floor"), 60_000)
+    if field == "microsecond":
+        return torch.remainder(rem, 60_000_000)
+    if field == "week":
+        return iso_week(days)
+    if field in ("dow", "doy", "quarter"):
+        y, m, d = civil_from_days(days)
+        if field == "dow":
+            return torch.remainder(days + 4, 7)
+        if field == "quarter":
+            return torch.div(m - 1, 3, rounding_mode="floor") + 1
+        return days - days_from_civil(y, torch.ones_like(y), torch.ones_like(y)) + 1
+    y, m, d = civil_from_days(days)
+    return {"year": y, "month": m, "day": d}[field]
+
+
+def trunc_ts_py(us: int, unit: str) -> int:
+    return int(trunc_ts(torch.tensor([us], dtype=torch.int64), unit)[0])
+
+
+def ts_part_py(us: int, field: str):
+    v = ts_part(torch.tensor([us], dtype=torch.int64), field)[0]
+    return float(v) if field == "epoch" else int(v)
+
+
+def _host_value(c: Column, t: DataType):
+    """Engine representation of a one-row column's value (dates in days,
+    timestamps in microseconds, decimals unscaled)."""
+    if c.valid is not None and not bool(c.valid.cpu()[0]):
+        return None
+    if t.is_string:
+        return c.to_arrow()[0].as_py()
+    v = c.data.cpu()[0]
+    if t.kind == "bool":
+        return bool(v)
+    if t.is_float:
+        return float(v)
+    return int(v)
 
 
 def add_months(days: torch.Tensor, months: int, extra_days: int = 0) -> torch.Tensor:
@@ -589,6 +831,21 @@ def add_months(days: torch.Tensor, months: int, extra_days: int = 0) -> torch.Te
 
 
 # =============================================================== conversions
+def _parse_ts_host(v: Column) -> Column:
+    from ..ops.strings import note_host_step
+    note_host_step("string -> timestamp")
+    arr = v.to_arrow()
+    try:
+        ts = pc.cast(pc.strptime(arr, "%Y-%m-%dT%H:%M:%S", "us", error_is_null=True), pa.timestamp("us"))
+        miss = pc.and_(pc.is_null(ts), pc.is_valid(arr))
+        if pc.any(miss).as_py():
+            ts = pc.cast(arr, pa.timestamp("us"))
+    except (pa.ArrowInvalid, pa.ArrowNotImplementedError) as e:
+        raise ExecutionError(f"cannot parse timestamp: {e}") from None
+    out = Column.from_arrow(ts, device=v.device)
+    return Column(T.TIMESTAMP, out.data.to(torch.int64), out.valid)
+
+
 def _convert_scalar(x, src: DataType, t: DataType):
     if t.is_decimal:
         if src.is_decimal:

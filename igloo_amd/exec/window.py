@@ -216,9 +216,11 @@ def _apply_spec(b: Batch, calls, ctx) -> Batch:
             if pid is not None:
                 h[1:] |= pid[1:] != pid[:-1]
             for v, _, _, vv in okeys:
-                h[1:] |= v[1:] != v[:-1]
-                if vv is not None:
-                    h[1:] |= vv[1:] != vv[:-1]
+                if vv is None:
+                    h[1:] |= v[1:] != v[:-1]
+                else:
+                    # NULL keys are peers whatever value sits under them
+                    h[1:] |= ((v[1:] != v[:-1]) & vv[1:] & vv[:-1]) | (vv[1:] != vv[:-1])
         peer = torch.cumsum(h.to(torch.int64), 0)
     st = _Sorted(n, pid, peer, dev)
     out = dict(b.columns)
@@ -425,9 +427,12 @@ def _string_minmax(w, col: Column, valid, st: _Sorted, lo, hi, read, ctx) -> Col
         vv = _at(cnt, read) > 0
     else:
         r, vv = W.frame_minmax(ranks, valid, lo, hi, n, is_max)
-    # a row per rank value (any row holding that rank carries the same string)
-    row_of = torch.zeros(int(to_host_int(ranks.max())) + 1 if n else 1, dtype=torch.int64, device=dev)
-    row_of.scatter_(0, ranks, torch.arange(n, dtype=torch.int64, device=dev))
+    # a row per rank value (any non-NULL row holding that rank carries the
+    # same string; NULL rows scatter into a spare slot)
+    top = int(to_host_int(ranks.max())) + 1 if n else 0
+    row_of = torch.zeros(top + 1, dtype=torch.int64, device=dev)
+    slot = ranks if col.valid is None else torch.where(col.valid, ranks, torch.full_like(ranks, top))
+    row_of.scatter_(0, slot, torch.arange(n, dtype=torch.int64, device=dev))
     src = torch.where(vv, gather_tensor(row_of, r.clamp(min=0, max=row_of.numel() - 1)),
                       torch.full((n,), -1, dtype=torch.int64, device=dev))
     return take_many([col], src, neg=True)[0]

@@ -37,6 +37,7 @@ SERVER_BULK_INGESTION, SERVER_STATEMENT_TIMEOUT = 10, 100
 SQL_DDL_CATALOG, SQL_DDL_SCHEMA, SQL_DDL_TABLE, SQL_IDENTIFIER_CASE = 500, 501, 502, 503
 SQL_IDENTIFIER_QUOTE_CHAR, SQL_QUOTED_IDENTIFIER_CASE, SQL_ALL_TABLES_ARE_SELECTABLE = 504, 505, 506
 SQL_NULL_ORDERING, SQL_KEYWORDS, SQL_NUMERIC_FUNCTIONS, SQL_STRING_FUNCTIONS = 507, 508, 509, 510
+SQL_SYSTEM_FUNCTIONS, SQL_DATETIME_FUNCTIONS = 511, 512
 SQL_SUPPORTS_COLUMN_ALIASING, SQL_NULL_PLUS_NULL_IS_NULL = 515, 516
 
 #: dense union of an SqlInfo value (FlightSql.proto CommandGetSqlInfo)
@@ -69,8 +70,13 @@ KEYS_SCHEMA = pa.schema([pa.field("pk_catalog_name", pa.utf8()), pa.field("pk_db
 
 KEYWORDS = ["ANALYZE", "EXPLAIN", "EXTERNAL", "ILIKE", "INTERVAL", "LIMIT", "LOCATION", "NULLS", "OFFSET", "SHOW",
             "STORED"]
-NUMERIC_FUNCTIONS = ["ABS", "AVG", "CEIL", "COUNT", "FLOOR", "MAX", "MIN", "ROUND", "STDDEV", "SUM", "VARIANCE"]
-STRING_FUNCTIONS = ["CAPITALIZE", "CHAR_LENGTH", "CONCAT", "LENGTH", "LOWER", "SUBSTRING", "TRIM", "UPPER"]
+# generated from the binder's function registry (sql/functions.py), whose every
+# entry tests/test_functions.py runs on the CPU and the GPU
+from ..sql import functions as _F  # noqa: E402
+NUMERIC_FUNCTIONS = sorted(n.upper() for n in list(_F.NUMERIC) + list(_F.AGGREGATE) + list(_F.WINDOW))
+STRING_FUNCTIONS = sorted(n.upper() for n in _F.STRING)
+SYSTEM_FUNCTIONS = sorted(n.upper() for n in _F.SYSTEM)
+DATETIME_FUNCTIONS = sorted(n.upper() for n in _F.DATETIME)
 
 
 def _sql_info_values(version: str) -> Dict[int, object]:
@@ -85,6 +91,7 @@ def _sql_info_values(version: str) -> Dict[int, object]:
         SQL_ALL_TABLES_ARE_SELECTABLE: True,
         SQL_NULL_ORDERING: 0,             # SQL_NULLS_SORTED_HIGH: ASC puts NULLs last (DataFusion's default)
         SQL_KEYWORDS: KEYWORDS, SQL_NUMERIC_FUNCTIONS: NUMERIC_FUNCTIONS, SQL_STRING_FUNCTIONS: STRING_FUNCTIONS,
+        SQL_SYSTEM_FUNCTIONS: SYSTEM_FUNCTIONS, SQL_DATETIME_FUNCTIONS: DATETIME_FUNCTIONS,
         SQL_SUPPORTS_COLUMN_ALIASING: True, SQL_NULL_PLUS_NULL_IS_NULL: True,
     }
 
@@ -141,29 +148,50 @@ def _opt_str(f: Dict[int, list], fno: int) -> Optional[str]:
 
 
 # ------------------------------------------------------- prepared statements
+def _placeholders(sql: str):
+    """Offsets of the ``?`` placeholders: outside string literals, quoted
+    identifiers, ``--`` line comments and ``/* */`` block comments."""
+    i, n = 0, len(sql)
+    while i < n:
+        ch = sql[i]
+        if ch in ("'", '"'):
+            j = sql.find(ch, i + 1)
+            while j != -1 and j + 1 < n and sql[j + 1] == ch:      # doubled quote inside the literal
+                j = sql.find(ch, j + 2)
+            i = n if j == -1 else j + 1
+        elif ch == "-" and sql.startswith("--", i):
+            j = sql.find("\n", i)
+            i = n if j == -1 else j + 1
+        elif ch == "/" and sql.startswith("/*", i):
+            j = sql.find("*/", i + 2)
+            i = n if j == -1 else j + 2
+        else:
+            if ch == "?":
+                yield i
+            i += 1
+
+
 def count_params(sql: str) -> int:
-    """``?`` placeholders outside string literals and quoted identifiers."""
-    n, q = 0, None
-    for ch in sql:
-        if q:
-            if ch == q:
-                q = None
-        elif ch in ("'", '"'):
-            q = ch
-        elif ch == "?":
-            n += 1
-    return n
+    return sum(1 for _ in _placeholders(sql))
 
 
 def _literal(v) -> str:
+    """A bound value as a self-delimiting SQL literal: numbers are
+    parenthesised (``a-?`` with -5 must not become the comment ``a--5``),
+    non-finite floats are spelled as casts."""
     import datetime
     import decimal
+    import math
     if v is None:
         return "NULL"
     if isinstance(v, bool):
         return "TRUE" if v else "FALSE"
+    if isinstance(v, float) and not math.isfinite(v):
+        return "CAST('" + ("NaN" if math.isnan(v) else ("inf" if v > 0 else "-inf")) + "' AS DOUBLE)"
+    if isinstance(v, decimal.Decimal) and not v.is_finite():
+        raise ValueError(f"cannot bind decimal {v}")
     if isinstance(v, (int, float, decimal.Decimal)):
-        return str(v)
+        return f"({v!r})" if isinstance(v, float) else f"({v})"
     if isinstance(v, datetime.datetime):
         return f"TIMESTAMP '{v.isoformat(sep=' ')}'"
     if isinstance(v, datetime.date):
@@ -173,22 +201,15 @@ def _literal(v) -> str:
 
 def bind_params(sql: str, values: Sequence) -> str:
     """Substitute ``?`` placeholders with SQL literals of ``values``."""
-    out, q, k = [], None, 0
-    for ch in sql:
-        if q:
-            if ch == q:
-                q = None
-            out.append(ch)
-        elif ch in ("'", '"'):
-            q = ch
-            out.append(ch)
-        elif ch == "?":
-            if k >= len(values):
-                raise ValueError(f"prepared statement has more parameters than the {len(values)} bound")
-            out.append(_literal(values[k]))
-            k += 1
-        else:
-            out.append(ch)
+    pos = list(_placeholders(sql))
+    if len(pos) > len(values):
+        raise ValueError(f"prepared statement has more parameters than the {len(values)} bound")
+    out, last = [], 0
+    for k, p in enumerate(pos):
+        out.append(sql[last:p])
+        out.append(_literal(values[k]))
+        last = p + 1
+    out.append(sql[last:])
     return "".join(out)
 
 

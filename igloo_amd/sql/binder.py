@@ -542,8 +542,9 @@ class Binder:
             view = self.catalog.get_view(name) if hasattr(self.catalog, "get_view") else None
             if view is not None:
                 from ..sql import parse
-                bq = self.bind_query(parse(view)[0], outer, {})
-                return self._derived(bq, alias or name, bq.names, item)
+                q = view if isinstance(view, dict) else parse(view)[0]
+                bq = self.bind_query(q, outer, {})
+                return self._derived(bq, alias or name, q.get("__columns") or bq.names, item)
             src = self.catalog.get_table(name)
             if src is None:
                 raise TableNotFound(f"table '{name}' not found")
@@ -633,7 +634,12 @@ class Binder:
             parts = [p["s"] for p in node["c"]]
             if len(parts) == 1 and parts[0] in scope.aliases:
                 return scope.aliases[parts[0]]
-            ci, depth = scope.resolve(parts)
+            try:
+                ci, depth = scope.resolve(parts)
+            except PlanError:
+                if len(parts) == 1 and parts[0] in ("current_date", "current_timestamp", "localtimestamp"):
+                    return self._func_library(parts[0].replace("localtimestamp", "current_timestamp"), [])
+                raise
             r = ci.ref()
             if depth > 0:
                 r._outer = True  # type: ignore[attr-defined]
@@ -710,14 +716,7 @@ class Binder:
             return self._case(node, scope, allow_agg)
         if k == "extract":
             x = self.bind_expr(node["c"][0], scope, allow_agg)
-            field = node["s"].lower()
-            field = {"years": "year", "months": "month", "days": "day", "dayofweek": "dow", "dayofyear": "doy"}.get(field, field)
-            if field not in ("year", "month", "day", "quarter", "dow", "doy"):
-                raise NotSupported(f"EXTRACT({field})")
-            x = self._coerce(x, DATE32)
-            if isinstance(x, Lit):
-                return Lit(_date_part_py(x.value, field), INT32)
-            return Func("date_part", [x], INT32, (field,))
+            return self._date_part(node["s"].lower(), x)
         if k == "func":
             return self._func(node, scope, allow_agg)
         if k in ("subq", "exists", "insub"):
@@ -807,12 +806,18 @@ class Binder:
         # literal coercion towards the column type
         if lt != rt:
             if isinstance(r, Lit) and not isinstance(l, Lit):
-                if lt.kind == "date32" and rt.is_string:
+                if lt.kind == "timestamp" and (rt.is_string or rt.kind == "date32"):
+                    r = _fold_cast(r, T.TIMESTAMP)
+                elif rt.kind == "timestamp" and lt.kind == "date32":
+                    l = self._to_ts(l)
+                elif lt.kind == "date32" and rt.is_string:
                     r = Lit(date_to_days(r.value), DATE32)
                 elif lt.is_string and not rt.is_string and r.value is not None:
                     r = _fold_cast(r, UTF8)
             elif isinstance(l, Lit) and not isinstance(r, Lit):
-                if rt.kind == "date32" and lt.is_string:
+                if rt.kind == "timestamp" and (lt.is_string or lt.kind == "date32"):
+                    l = _fold_cast(l, T.TIMESTAMP)
+                elif rt.kind == "date32" and lt.is_string:
                     l = Lit(date_to_days(l.value), DATE32)
                 elif rt.is_string and not lt.is_string and l.value is not None:
                     l = _fold_cast(l, UTF8)
@@ -828,18 +833,33 @@ class Binder:
         lt, rt = l.dtype, r.dtype
         # ---- DATE / INTERVAL arithmetic
         if lt == INTERVAL or rt == INTERVAL:
-            if rt == INTERVAL and op in ("+", "-") and lt.kind == "date32":
-                months, days = r.value
+            if rt == INTERVAL and op in ("+", "-") and lt.kind in ("date32", "timestamp"):
+                months, days, us = r.value
                 if op == "-":
-                    months, days = -months, -days
-                if isinstance(l, Lit):
-                    return Lit(add_months(l.value, months) + days if l.value is not None else None, DATE32)
-                if months:
-                    return Func("add_months", [l], DATE32, (months, days))
-                return BinOp("+", l, Lit(days, INT32), DATE32)
-            if lt == INTERVAL and op == "+" and rt.kind == "date32":
+                    months, days, us = -months, -days, -us
+                if lt.kind == "date32" and not us:
+                    if isinstance(l, Lit):
+                        return Lit(add_months(l.value, months) + days if l.value is not None else None, DATE32)
+                    if months:
+                        return Func("add_months", [l], DATE32, (months, days))
+                    return BinOp("+", l, Lit(days, INT32), DATE32)
+                x = self._to_ts(l)
+                if isinstance(x, Lit):
+                    if x.value is None:
+                        return Lit(None, T.TIMESTAMP)
+                    dd, rem = divmod(x.value, 86_400_000_000)
+                    return Lit((add_months(dd, months) + days) * 86_400_000_000 + rem + us, T.TIMESTAMP)
+                return Func("ts_add", [x], T.TIMESTAMP, (months, days, us))
+            if lt == INTERVAL and op == "+" and rt.kind in ("date32", "timestamp"):
                 return self._arith("+", r, l)
+            if lt == INTERVAL and rt == INTERVAL and op in ("+", "-"):
+                sg = 1 if op == "+" else -1
+                return Lit(tuple(a + sg * b for a, b in zip(l.value, r.value)), INTERVAL)
             raise NotSupported(f"interval arithmetic {lt} {op} {rt}")
+        if lt.kind == "timestamp" or rt.kind == "timestamp":
+            if op == "-" and lt.kind == "timestamp" and rt.kind in ("timestamp", "date32"):
+                return BinOp("-", l, self._to_ts(r), INT64)
+            raise PlanError(f"cannot apply {op} to {lt} and {rt}")
         if lt.kind == "date32" or rt.kind == "date32":
             if op == "-" and lt.kind == "date32" and rt.kind == "date32":
                 return _fold(BinOp("-", l, r, INT64))
@@ -910,19 +930,36 @@ class Binder:
             if not allow_agg:
                 raise PlanError("grouping() is only allowed with GROUP BY")
             return Func("grouping", [self.bind_expr(a, scope) for a in node["c"]], INT32)
-        if name in AGG_FUNCS or name in ("stddev_samp", "stddev_pop", "var_samp", "var_pop"):
+        if name in AGG_FUNCS or name in _EXTRA_AGGS:
             if not allow_agg:
                 raise PlanError(f"aggregate function {name} not allowed here")
             distinct = bool(node.get("distinct"))
+            arg2, param = None, None
             if node.get("star"):
                 arg = None
             else:
                 args = [self.bind_expr(a, scope) for a in node["c"]]
-                if len(args) != 1:
-                    raise NotSupported(f"{name} with {len(args)} arguments")
+                if not args:
+                    raise PlanError(f"{name}() needs an argument")
                 arg = args[0]
+                if name in ("covar", "covar_samp", "covar_pop", "corr"):
+                    if len(args) != 2:
+                        raise PlanError(f"{name}() takes two arguments")
+                    arg2 = args[1]
+                elif name in ("string_agg", "approx_percentile_cont"):
+                    if len(args) != 2 or not isinstance(args[1], Lit) or args[1].value is None:
+                        raise PlanError(f"{name}() takes a constant second argument")
+                    param = args[1].value
+                    if name == "approx_percentile_cont":
+                        param = float(args[1].value) / (10 ** args[1].dtype.scale if args[1].dtype.is_decimal else 1)
+                        if not 0.0 <= param <= 1.0:
+                            raise PlanError("percentile must be between 0 and 1")
+                    else:
+                        param = str(param)
+                elif len(args) != 1:
+                    raise NotSupported(f"{name} with {len(args)} arguments")
             flt = self.bind_expr(node["filter"], scope) if node.get("filter") else None
-            return _make_agg(name, arg, distinct, flt)
+            return _make_agg(name, arg, distinct, flt, arg2, param)
         args = [self.bind_expr(a, scope, allow_agg) for a in node["c"]]
         if name in ("upper", "lower", "capitalize"):
             _nargs(name, args, 1)
@@ -967,14 +1004,19 @@ class Binder:
             _nargs(name, args, 2)
             return Case([(self._cmp("=", args[0], args[1]), Lit(None, args[0].dtype))], args[0], args[0].dtype)
         if name in ("date_part", "datepart"):
-            field = args[0].value.lower()
-            return Func("date_part", [self._coerce(args[1], DATE32)], INT32, (field,))
-        if name == "year":
-            return Func("date_part", [self._coerce(args[0], DATE32)], INT32, ("year",))
+            if not isinstance(args[0], Lit) or not isinstance(args[0].value, str):
+                raise PlanError("date_part() field must be a string literal")
+            return self._date_part(args[0].value.lower(), args[1])
+        if name in ("year", "month", "day", "hour", "minute", "second", "quarter", "week"):
+            return self._date_part(name, args[0])
         if name in ("concat",):
-            out = args[0]
-            for a in args[1:]:
-                out = Func("concat", [self._coerce(out, UTF8), self._coerce(a, UTF8)], UTF8)
+            # the concat() function reads NULL arguments as '' (the || operator propagates NULL)
+            parts = [a for a in args if not (isinstance(a, Lit) and a.value is None)]
+            parts = [Func("coalesce", [self._coerce(a, UTF8), Lit("", UTF8)], UTF8) if a.nullable
+                     else self._coerce(a, UTF8) for a in parts] or [Lit("", UTF8)]
+            out = parts[0]
+            for a in parts[1:]:
+                out = Func("concat", [out, a], UTF8)
             return out
         if name in ("sqrt", "ln", "log10", "exp", "floor", "ceil", "ceiling"):
             _nargs(name, args, 1)
@@ -983,7 +1025,208 @@ class Binder:
             return Func("power", [self._coerce(a, FLOAT64) for a in args], FLOAT64)
         if name in ("to_date",):
             return self._coerce(args[0], DATE32)
+        return self._func_library(name, args)
+
+    def _date_part(self, field: str, x: Expr) -> Expr:
+        field = {"years": "year", "months": "month", "days": "day", "dayofweek": "dow", "dayofyear": "doy",
+                 "hours": "hour", "minutes": "minute", "seconds": "second", "weeks": "week"}.get(field, field)
+        date_fields = ("year", "month", "day", "quarter", "dow", "doy", "week")
+        time_fields = ("hour", "minute", "second", "millisecond", "microsecond", "epoch")
+        if field not in date_fields + time_fields:
+            raise NotSupported(f"EXTRACT({field})")
+        if x.dtype.is_string:
+            x = self._coerce(x, T.TIMESTAMP if field in time_fields else DATE32)
+        if x.dtype.kind == "timestamp" or field in time_fields:
+            x = self._to_ts(x)
+            rt = FLOAT64 if field == "epoch" else INT32
+            if isinstance(x, Lit):
+                from ..exec.expr_eval import ts_part_py
+                return Lit(None if x.value is None else ts_part_py(x.value, field), rt)
+            return Func("ts_part", [x], rt, (field,))
+        x = self._coerce(x, DATE32)
+        if isinstance(x, Lit):
+            return Lit(None if x.value is None else _date_part_py(x.value, field), INT32)
+        return Func("date_part", [x], INT32, (field,))
+
+    # ------------------------------------------------------ function library
+    def _func_library(self, name: str, args: List[Expr]) -> Expr:
+        """DataFusion built-ins beyond the TPC-H set (strings, math, dates)."""
+        from ..ops import strfuncs as SF
+
+        def lit_str(i, what):
+            if len(args) <= i or not isinstance(args[i], Lit) or not isinstance(args[i].value, str):
+                raise NotSupported(f"{name}(): {what} must be a string literal")
+            return args[i].value
+
+        def lit_int(i, what):
+            if len(args) <= i or not isinstance(args[i], Lit) or not isinstance(args[i].value, int):
+                raise NotSupported(f"{name}(): {what} must be an integer literal")
+            return int(args[i].value)
+
+        def strfn(fname, opts, rt=UTF8):
+            a = self._coerce(args[0], UTF8)
+            if isinstance(a, Lit):
+                return Lit(None if a.value is None else SF.py_fn(fname, opts)(a.value), rt)
+            return Func(fname, [a], rt, opts)
+        if not args and name not in ("pi", "random", "now", "current_timestamp", "current_date", "today",
+                                     "uuid", "current_time"):
+            raise PlanError(f"{name}() needs arguments")
+        # ---- strings
+        if name in ("btrim", "trim", "ltrim", "rtrim"):
+            chars = lit_str(1, "trim characters") if len(args) > 1 else " "
+            return strfn("trim", ({"ltrim": 1, "rtrim": 2}.get(name, 3), chars))
+        if name == "replace":
+            return strfn("replace", (lit_str(1, "search string"), lit_str(2, "replacement")))
+        if name in ("lpad", "rpad"):
+            return strfn(name, (lit_int(1, "length"), lit_str(2, "fill") if len(args) > 2 else " "))
+        if name in ("reverse", "initcap"):
+            return strfn(name, ())
+        if name == "repeat":
+            return strfn("repeat", (lit_int(1, "count"),))
+        if name in ("left", "right"):
+            return strfn(name, (lit_int(1, "length"),))
+        if name == "translate":
+            return strfn("translate", (lit_str(1, "from"), lit_str(2, "to")))
+        if name == "split_part":
+            return strfn("split_part", (lit_str(1, "delimiter"), lit_int(2, "part")))
+        if name in ("strpos", "instr"):
+            return strfn("strpos", (lit_str(1, "substring"),), INT32)
+        if name == "ascii":
+            return strfn("ascii", (), INT32)
+        if name in ("octet_length",):
+            return strfn("octet_length", (), INT32)
+        if name == "bit_length":
+            return BinOp("*", Cast(strfn("octet_length", (), INT32), INT64), Lit(8, INT64), INT64)
+        if name in ("starts_with", "ends_with"):
+            p = _like_escape(lit_str(1, "prefix"))
+            return Like(self._coerce(args[0], UTF8), p + "%" if name == "starts_with" else "%" + p)
+        if name == "concat_ws":
+            sep = lit_str(0, "separator")
+            return self._concat_ws(sep, args[1:])
+        if name in ("regexp_like", "regexp_replace", "regexp_count"):
+            a = self._coerce(args[0], UTF8)
+            pat = lit_str(1, "pattern")
+            if name == "regexp_replace":
+                rep = lit_str(2, "replacement")
+                flags = lit_str(3, "flags") if len(args) > 3 else ""
+                return Func(name, [a], UTF8, (pat, rep, flags))
+            flags = lit_str(2, "flags") if len(args) > 2 else ""
+            return Func(name, [a], BOOL if name == "regexp_like" else INT64, (pat, flags))
+        if name == "chr":
+            if isinstance(args[0], Lit):
+                return Lit(None if args[0].value is None else chr(int(args[0].value)), UTF8)
+            raise NotSupported("chr() of a column")
+        if name == "to_hex":
+            if isinstance(args[0], Lit):
+                return Lit(None if args[0].value is None else format(int(args[0].value) & (2**64 - 1), "x"), UTF8)
+            raise NotSupported("to_hex() of a column")
+        # ---- math
+        if name == "mod":
+            return self._arith("%", args[0], args[1])
+        if name in ("sign", "signum", "trunc", "log2", "cbrt", "degrees", "radians", "sin", "cos", "tan", "asin",
+                    "acos", "atan", "sinh", "cosh", "tanh", "isnan", "iszero", "factorial"):
+            x = self._coerce(args[0], FLOAT64) if name != "factorial" else self._coerce(args[0], INT64)
+            if name == "trunc" and len(args) > 1:
+                return Func("trunc", [x], FLOAT64, (lit_int(1, "precision"),))
+            rt = BOOL if name in ("isnan", "iszero") else (INT64 if name == "factorial" else FLOAT64)
+            return Func(name.replace("signum", "sign"), [x], rt)
+        if name == "log":
+            if len(args) == 1:
+                return Func("log10", [self._coerce(args[0], FLOAT64)], FLOAT64)
+            return Func("logb", [self._coerce(args[0], FLOAT64), self._coerce(args[1], FLOAT64)], FLOAT64)
+        if name in ("atan2", "nanvl"):
+            return Func(name, [self._coerce(a, FLOAT64) for a in args[:2]], FLOAT64)
+        if name == "pi":
+            return Lit(3.141592653589793, FLOAT64)
+        if name == "random":
+            return Func("random", [], FLOAT64)
+        if name in ("greatest", "least"):
+            t = None
+            for a in args:
+                if a.dtype.kind != "null":
+                    t = a.dtype if t is None else (t if t == a.dtype else T.common_numeric(t, a.dtype))
+            t = t or T.NULL
+            if t.is_string:
+                raise NotSupported(f"{name}() over strings")
+            return Func(name, [self._coerce(a, t) for a in args], t)
+        if name in ("gcd", "lcm"):
+            return Func(name, [self._coerce(a, INT64) for a in args[:2]], INT64)
+        if name == "nvl2":
+            t = _common(args[1].dtype, args[2].dtype)
+            return Case([(IsNull(args[0], True), self._coerce(args[1], t))], self._coerce(args[2], t), t)
+        # ---- dates and timestamps
+        if name in ("now", "current_timestamp"):
+            return Lit(self._now_us(), T.TIMESTAMP)
+        if name in ("current_date", "today"):
+            return Lit(self._now_us() // 86_400_000_000, DATE32)
+        if name == "date_trunc":
+            unit = lit_str(0, "unit").lower()
+            if unit not in _TRUNC_UNITS:
+                raise PlanError(f"date_trunc unit '{unit}' is not supported")
+            x = args[1]
+            if x.dtype.is_string:
+                x = self._coerce(x, T.TIMESTAMP)
+            x = self._to_ts(x)
+            if isinstance(x, Lit):
+                from ..exec.expr_eval import trunc_ts_py
+                return Lit(None if x.value is None else trunc_ts_py(x.value, unit), T.TIMESTAMP)
+            return Func("date_trunc", [x], T.TIMESTAMP, (unit,))
+        if name in ("to_timestamp", "to_timestamp_micros", "to_timestamp_millis", "to_timestamp_seconds",
+                    "from_unixtime"):
+            x = args[0]
+            if x.dtype.is_string:
+                if isinstance(x, Lit):
+                    return _fold_cast(x, T.TIMESTAMP)
+                return Cast(x, T.TIMESTAMP)
+            scale = {"to_timestamp_micros": 1, "to_timestamp_millis": 1000}.get(name, 1_000_000)
+            if name == "to_timestamp" and x.dtype.is_float:
+                return Func("ts_from_float", [x], T.TIMESTAMP)
+            return self._arith_ts_scale(self._coerce(x, INT64), scale)
+        if name == "to_unixtime":
+            return Func("to_unixtime", [self._to_ts(args[0])], INT64)
+        if name == "make_date":
+            return Func("make_date", [self._coerce(a, INT64) for a in args[:3]], DATE32)
         raise NotSupported(f"function {name}()")
+
+    def _now_us(self) -> int:
+        now = getattr(self, "_now", None)
+        if now is None:
+            import time as _t
+            now = self._now = int(_t.time() * 1_000_000)
+        return now
+
+    def _to_ts(self, x: Expr) -> Expr:
+        if x.dtype.kind == "timestamp":
+            return x
+        if x.dtype.kind == "date32":
+            if isinstance(x, Lit):
+                return Lit(None if x.value is None else x.value * 86_400_000_000, T.TIMESTAMP)
+            return Cast(x, T.TIMESTAMP)
+        return self._coerce(x, T.TIMESTAMP)
+
+    def _arith_ts_scale(self, x: Expr, scale: int) -> Expr:
+        if isinstance(x, Lit):
+            return Lit(None if x.value is None else int(x.value) * scale, T.TIMESTAMP)
+        return Cast(BinOp("*", x, Lit(scale, INT64), INT64), T.TIMESTAMP)
+
+    def _concat_ws(self, sep: str, parts: List[Expr]) -> Expr:
+        """concat_ws(sep, a, b, ...): the non-NULL arguments joined by sep."""
+        out: Optional[Expr] = None
+        seen: Optional[Expr] = None   # some earlier argument is not NULL
+        for p in parts:
+            p = self._coerce(p, UTF8)
+            if isinstance(p, Lit) and p.value is None:
+                continue
+            if out is None:
+                out = Func("coalesce", [p, Lit("", UTF8)], UTF8) if p.nullable else p
+                seen = IsNull(p, True) if p.nullable else Lit(True, BOOL)
+                continue
+            piece: Expr = Func("concat", [Lit(sep, UTF8), p], UTF8)
+            if p.nullable or not (isinstance(seen, Lit) and seen.value):
+                piece = Case([(IsNull(p), Lit("", UTF8)), (seen, piece)], p, UTF8)
+            out = Func("concat", [out, piece], UTF8)
+            seen = Lit(True, BOOL) if not p.nullable else BinOp("or", seen, IsNull(p, True), BOOL)
+        return out if out is not None else Lit("", UTF8)
 
     # ------------------------------------------------------------ windows
     def _window_call(self, name: str, node, scope, allow_agg) -> Expr:
@@ -1092,9 +1335,13 @@ class Binder:
                 raise PlanError("RANGE with an offset needs exactly one ORDER BY key")
             kt = order[0][0].dtype
             if v.dtype == INTERVAL:
-                months, days = v.value
-                if months or kt.kind != "date32":
+                months, days, us = v.value
+                if months:
                     raise NotSupported("RANGE offsets in months")
+                if kt.kind == "timestamp":
+                    return Lit(days * 86_400_000_000 + us, INT64)
+                if us or kt.kind != "date32":
+                    raise PlanError("RANGE interval offset over a non-temporal key")
                 return Lit(days, INT64)
             if kt.kind == "date32":
                 return Lit(int(v.value), INT64)
@@ -1129,6 +1376,21 @@ _EXTRA_AGGS = ("stddev_samp", "stddev_pop", "var_samp", "var_pop", "variance", "
                "median", "approx_distinct", "approx_median", "string_agg", "array_agg", "bit_and", "bit_or",
                "bit_xor", "covar", "covar_samp", "covar_pop", "corr", "approx_percentile_cont", "first_value",
                "last_value", "every", "any", "some")
+
+
+_TRUNC_UNITS = ("microsecond", "millisecond", "second", "minute", "hour", "day", "week", "month", "quarter", "year")
+
+
+def _like_escape(s: str) -> str:
+    return s.replace("\\", "\\\\").replace("%", "\\%").replace("_", "\\_")
+
+
+def _common(a: DataType, b: DataType) -> DataType:
+    if a.kind == "null":
+        return b
+    if b.kind == "null" or a == b:
+        return a
+    return T.common_numeric(a, b)
 
 
 def _distinct_from(distinct: bool, l: Expr, r: Expr) -> Expr:
@@ -1258,11 +1520,21 @@ def _int_as_decimal(e: Expr) -> DataType:
     return T.DECIMAL(19 if e.dtype.kind == "int64" else 10, 0)
 
 
-def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt) -> AggCall:
-    if name == "mean":
-        name = "avg"
+_AGG_ALIASES = {"mean": "avg", "variance": "var_samp", "var": "var_samp", "var_population": "var_pop",
+                "stddev": "stddev_samp", "stddev_population": "stddev_pop", "approx_median": "median",
+                "covar": "covar_samp", "every": "bool_and", "any": "bool_or", "some": "bool_or"}
+
+
+def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt, arg2: Optional[Expr] = None,
+              param=None) -> AggCall:
+    name = _AGG_ALIASES.get(name, name)
     if name == "count":
         return AggCall("count", arg, distinct, INT64, flt)
+    if name == "approx_distinct":
+        # exact distinct count (a valid answer for the approximate function)
+        if arg is None:
+            raise PlanError("approx_distinct(*) is not valid")
+        return AggCall("count", arg, True, INT64, flt)
     if arg is None:
         raise PlanError(f"{name}(*) is not valid")
     t = arg.dtype
@@ -1284,12 +1556,33 @@ def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt) -> AggCall:
         else:
             raise PlanError(f"avg({t}) is not supported")
         return AggCall("avg", arg, distinct, rt, flt)
-    if name in ("min", "max", "first_value"):
-        return AggCall(name if name != "first_value" else "min", arg, distinct, t, flt)
-    if name in ("stddev", "stddev_samp", "stddev_pop", "var", "var_samp", "var_pop"):
+    if name in ("min", "max", "first_value", "last_value"):
+        return AggCall(name if name not in ("first_value", "last_value") else
+                       ("min" if name == "first_value" else "max"), arg, distinct, t, flt)
+    if name in ("stddev_samp", "stddev_pop", "var_samp", "var_pop"):
+        if not t.is_numeric:
+            raise PlanError(f"{name}({t}) is not supported")
         return AggCall(name, arg, distinct, FLOAT64, flt)
     if name in ("bool_and", "bool_or"):
         return AggCall(name, arg, distinct, BOOL, flt)
+    if name == "median":
+        if not t.is_numeric:
+            raise PlanError(f"median({t}) is not supported")
+        return AggCall("median", arg, distinct, t, flt)
+    if name == "approx_percentile_cont":
+        if not t.is_numeric:
+            raise PlanError(f"approx_percentile_cont({t}) is not supported")
+        return AggCall("percentile", arg, False, FLOAT64, flt, None, param)
+    if name == "string_agg":
+        if not t.is_string:
+            raise PlanError("string_agg() needs a string argument")
+        return AggCall("string_agg", arg, distinct, UTF8, flt, None, param)
+    if name in ("covar_samp", "covar_pop", "corr"):
+        if not (t.is_numeric and arg2 is not None and arg2.dtype.is_numeric):
+            raise PlanError(f"{name}() needs two numeric arguments")
+        return AggCall(name, arg, False, FLOAT64, flt, arg2)
+    if name == "array_agg":
+        raise NotSupported("array_agg(): list-typed results are not supported (use string_agg)")
     raise NotSupported(f"aggregate {name}")
 
 
@@ -1302,23 +1595,34 @@ def _parse_interval(s: str, unit: Optional[str]) -> Tuple[int, int]:
             txt, unit = parts
         else:
             unit = "day"
-    n = int(Decimal(txt.split()[0]))
+    d = Decimal(txt.split()[0])
+    n = int(d)
     unit = unit.rstrip("s")
     if unit == "year":
-        return (12 * n, 0)
+        return (12 * n, 0, 0)
     if unit == "month":
-        return (n, 0)
+        return (n, 0, 0)
     if unit == "week":
-        return (0, 7 * n)
+        return (0, 7 * n, 0)
     if unit == "day":
-        return (0, n)
+        return (0, n, 0)
+    if unit == "hour":
+        return (0, 0, int(d * 3_600_000_000))
+    if unit == "minute":
+        return (0, 0, int(d * 60_000_000))
+    if unit == "second":
+        return (0, 0, int(d * 1_000_000))
+    if unit in ("millisecond", "milli"):
+        return (0, 0, int(d * 1000))
+    if unit in ("microsecond", "micro"):
+        return (0, 0, n)
     raise NotSupported(f"interval unit {unit}")
 
 
 def _date_part_py(days: int, field: str) -> int:
     d = days_to_date(days)
     return {"year": d.year, "month": d.month, "day": d.day, "quarter": (d.month - 1) // 3 + 1,
-            "dow": (d.weekday() + 1) % 7, "doy": d.timetuple().tm_yday}[field]
+            "dow": (d.weekday() + 1) % 7, "doy": d.timetuple().tm_yday, "week": d.isocalendar()[1]}[field]
 
 
 def _fold_cast(v: Lit, t: DataType) -> Lit:
@@ -1354,6 +1658,17 @@ def _fold_cast(v: Lit, t: DataType) -> Lit:
         if t.kind == "date32":
             if src.is_string:
                 return Lit(date_to_days(x), t)
+            if src.kind == "timestamp":
+                return Lit(int(x) // 86_400_000_000, t)
+            return Lit(int(x), t)
+        if t.kind == "timestamp":
+            if src.is_string:
+                dt = datetime.datetime.fromisoformat(x.strip().replace("T", " ").rstrip("Z"))
+                if dt.tzinfo is not None:
+                    dt = dt.astimezone(datetime.timezone.utc).replace(tzinfo=None)
+                return Lit((dt - datetime.datetime(1970, 1, 1)) // datetime.timedelta(microseconds=1), t)
+            if src.kind == "date32":
+                return Lit(int(x) * 86_400_000_000, t)
             return Lit(int(x), t)
         if t.kind == "bool":
             if src.is_string:

@@ -258,25 +258,34 @@ AGG_FUNCS = {"sum", "count", "avg", "min", "max", "mean", "stddev", "var", "bool
 
 @dataclass(eq=False)
 class AggCall(Expr):
-    func: str           # sum count avg min max
+    func: str           # sum count avg min max median percentile string_agg covar_* corr ...
     arg: Optional[Expr]  # None for COUNT(*)
     distinct: bool
     dtype: DataType
     filter: Optional[Expr] = None
+    arg2: Optional[Expr] = None   # second argument (covar / corr)
+    param: Any = None             # constant parameter (percentile fraction, string_agg separator)
 
     def children(self):
         out = [] if self.arg is None else [self.arg]
+        if self.arg2 is not None:
+            out.append(self.arg2)
         if self.filter is not None:
             out.append(self.filter)
         return out
 
     def with_children(self, kids):
         arg = kids[0] if self.arg is not None else None
+        arg2 = kids[1] if self.arg2 is not None else None
         flt = kids[-1] if self.filter is not None else None
-        return AggCall(self.func, arg, self.distinct, self.dtype, flt)
+        return AggCall(self.func, arg, self.distinct, self.dtype, flt, arg2, self.param)
 
     def sql(self):
         a = "*" if self.arg is None else (("DISTINCT " if self.distinct else "") + self.arg.sql())
+        if self.arg2 is not None:
+            a += ", " + self.arg2.sql()
+        if self.param is not None:
+            a += f", {self.param!r}"
         return f"{self.func.upper()}({a})"
 
 

@@ -75,7 +75,8 @@ def run_distributed(world, con, device="cpu", low_thresholds=False, replicate_di
 
 
 @pytest.mark.parametrize("world,replicate_dims,low", [(2, True, False), (3, True, True), (2, False, False),
-                                                      (3, False, False)])
+                                                      (3, False, False), (4, True, True), (4, False, True),
+                                                      (8, True, False), (8, True, True), (8, False, False)])
 def test_tpch_distributed_gloo(world, replicate_dims, low, tpch_cpu):
     """Both multi-rank layouts: replicated dimension tables with fact tables
     co-partitioned by order key (the bench layout), and every table
@@ -100,6 +101,10 @@ def test_tpch_distributed_gloo(world, replicate_dims, low, tpch_cpu):
         # aggregates one all-reduce, grouped ones a structure all-gather plus
         # one data collective, a top-k result one fixed-size all-gather)
         assert max(calls.values()) <= 5 and sum(calls.values()) <= 60, calls
+    if replicate_dims and low:
+        # the SF100 code paths (range slices, sorted joins, shuffled partial
+        # groups, pipelined exchanges in tiny chunks): bounded too
+        assert max(calls.values()) <= 12 and sum(calls.values()) <= 120, calls
 
 
 def check(res, qs, con):
@@ -239,3 +244,60 @@ def test_distributed_aggregate_merges_128bit_partial_sums():
     for r in got:
         s, c = want[int(r["g"])]
         assert Decimal(r["s"]) == s and int(r["n"]) == c, r
+
+
+def _surface_worker(rank, world, port, out_path):
+    """The SQL-surface suite (tests/test_sql_surface.py: windows, set
+    operations, recursive CTEs, grouping sets) over tables whose rows are
+    spread round-robin over the ranks."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import pyarrow as pa
+    import igloo_amd as ig
+    import test_sql_surface as TS
+    from igloo_amd.catalog import MemoryTable
+    from igloo_amd.parallel.comm import Communicator
+    comm = Communicator.init(backend="gloo", device="cpu", timeout_s=120)
+    e = ig.QueryEngine(device="cpu", comm=comm)
+    full = TS._engine("cpu")
+    for name in ("t", "a", "b", "e"):
+        tab = full.catalog.get_table(name)
+        arrow = pa.table({f.name: tab.columns[f.name].to_arrow() for f in tab.schema()})
+        mine = arrow.take(pa.array(list(range(rank, arrow.num_rows, world)), pa.int64()))
+        e.register_table(name, MemoryTable.from_arrow(mine))
+    res = {}
+    for i, (q, _) in enumerate(TS.CASES):
+        try:
+            res[i] = [list(r.values()) for r in e.query(q).to_pylist()]
+        except Exception as ex:  # noqa: BLE001
+            res[i] = {"error": f"{type(ex).__name__}: {ex}"}
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f, default=str)
+    comm.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sql_surface_distributed(world):
+    """Window functions (shuffled by a shared PARTITION BY key, else
+    gathered), INTERSECT / EXCEPT [ALL], recursive CTEs and GROUPING SETS on
+    several gloo ranks match sqlite."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import test_sql_surface as TS
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.json")
+        mp.start_processes(_surface_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                           start_method="spawn")
+        got = json.load(open(out))
+    bad = []
+    for i, (q, oracle) in enumerate(TS.CASES):
+        r = got[str(i)]
+        if isinstance(r, dict):
+            bad.append(f"{q}: {r['error']}")
+            continue
+        if TS._rows(tuple(x) for x in r) != TS._expected(q, oracle):
+            bad.append(q)
+    assert not bad, "\n".join(bad)

@@ -1,0 +1,176 @@
+"""Every function of the binder's registry (igloo_amd/sql/functions.py, the
+source of Flight SQL's SqlInfo function lists) runs on the CPU engine and
+(gpu marker) on the device. The CPU result is checked against sqlite 3.37
+where sqlite has the function (``SQLITE``: the same call spelled for sqlite,
+its math functions included); the rest are parity-unpinned against
+DataFusion and pinned to the Python definitions of ops/strfuncs.py through
+the CPU run. The GPU result must equal the CPU result, and the string
+kernels (csrc/kernels/strfunc.hip) must have run."""
+import datetime
+import math
+import sqlite3
+
+import pyarrow as pa
+import pytest
+
+import igloo_amd as ig
+from igloo_amd.sql import functions as F
+
+S = ["abc", "xabcx", "hello world", "a b c", None, "zz top", "  pad me ", "caba", "Mixed CASE word", "a,b,,c"]
+NV = [1, 2, 3, None, 5, 2, 4, 1, 3, 5]
+FV = [1.25, -2.5, 0.0, 3.75, None, -0.125, 7.5, 2.0, -9.875, 4.5]
+DV = [datetime.date(2024, 3, 15), datetime.date(1999, 12, 31), None, datetime.date(2020, 2, 29),
+      datetime.date(2021, 1, 3), datetime.date(1995, 6, 17), datetime.date(2000, 1, 1), datetime.date(2010, 10, 10),
+      datetime.date(1970, 1, 2), datetime.date(2038, 1, 19)]
+TSV = [datetime.datetime(2024, 3, 15, 13, 45, 30), datetime.datetime(1999, 12, 31, 23, 59, 59), None,
+       datetime.datetime(2020, 2, 29, 0, 0, 1), datetime.datetime(2021, 1, 3, 7, 8, 9),
+       datetime.datetime(1995, 6, 17, 12, 0, 0), datetime.datetime(2000, 1, 1, 0, 0, 0),
+       datetime.datetime(2010, 10, 10, 10, 10, 10), datetime.datetime(1970, 1, 2, 3, 4, 5),
+       datetime.datetime(2038, 1, 19, 3, 14, 7)]
+
+# sqlite spellings of the registry examples (None: parity unpinned)
+SQLITE = {
+    "upper": "upper(s)", "lower": "lower(s)", "capitalize": "upper(s)", "length": "length(s)",
+    "char_length": "length(s)", "character_length": "length(s)", "substr": "substr(s, 2, 3)",
+    "substring": "substr(s, 2, 2)", "concat": "coalesce(s, '') || '-' || coalesce(n, '')",
+    "trim": "trim(s)", "btrim": "trim(s, 'x')", "ltrim": "ltrim(s)", "rtrim": "rtrim(s)",
+    "replace": "replace(s, 'a', 'AA')", "left": "substr(s, 1, 2)", "strpos": "instr(s, 'a')",
+    "instr": "instr(s, 'b')", "position": "instr(s, 'a')", "ascii": "unicode(s)",
+    "octet_length": "length(cast(s as blob))", "bit_length": "8 * length(cast(s as blob))",
+    "starts_with": "substr(s, 1, 2) = 'ab'", "ends_with": "substr(s, -1) = 'c'", "chr": "char(65)",
+    "to_hex": "printf('%x', 255)",
+    "abs": "abs(n - 3)", "round": "round(f, 1)", "ceil": "ceil(f)", "ceiling": "ceiling(f)", "floor": "floor(f)",
+    "sqrt": "sqrt(abs(f))", "ln": "ln(abs(f) + 1)", "log": "log(abs(f) + 1)", "log10": "log10(abs(f) + 1)",
+    "log2": "log2(abs(f) + 1)", "exp": "exp(f / 10)", "power": "power(f, 2)", "pow": "pow(n, 2)",
+    "mod": "n % 3", "sign": "sign(f)", "signum": "sign(n - 2)", "trunc": "trunc(f * 10) / 10",
+    "degrees": "degrees(f)", "radians": "radians(f)", "sin": "sin(f)", "cos": "cos(f)", "tan": "tan(f)",
+    "asin": "asin(f / 100)", "acos": "acos(f / 100)", "atan": "atan(f)", "atan2": "atan2(f, n + 1)",
+    "sinh": "sinh(f / 10)", "cosh": "cosh(f / 10)", "tanh": "tanh(f)", "pi": "pi()", "iszero": "f = 0",
+    "random": "1",
+    "date_part": "cast(strftime('%m', d) as int)", "extract": "cast(strftime('%Y', d) as int)",
+    "year": "cast(strftime('%Y', d) as int)", "month": "cast(strftime('%m', d) as int)",
+    "day": "cast(strftime('%d', d) as int)", "hour": "cast(strftime('%H', ts) as int)",
+    "minute": "cast(strftime('%M', ts) as int)", "second": "cast(strftime('%S', ts) as int)",
+    "to_unixtime": "cast(strftime('%s', ts) as int)", "to_timestamp": "datetime(n, 'unixepoch')",
+    "to_timestamp_seconds": "datetime(n, 'unixepoch')", "from_unixtime": "datetime(n, 'unixepoch')",
+    "make_date": "date(printf('2020-%02d-01', n))", "to_date": "'2024-01-02'",
+    "date_trunc": "strftime('%Y-%m-01 00:00:00', ts)",
+    "coalesce": "coalesce(s, 'none')", "ifnull": "ifnull(n, 0)", "nvl": "ifnull(n, -1)", "nullif": "nullif(n, 2)",
+    "nvl2": "case when s is not null then 1 else 0 end",
+    "count": "count(n)", "sum": "sum(n)", "avg": "avg(f)", "mean": "avg(f)", "min": "min(s)", "max": "max(d)",
+    "approx_distinct": "count(distinct s)", "string_agg": "group_concat(s, ',')", "bool_and": "min(n > 0)",
+    "bool_or": "max(n > 2)", "every": "min(n > 0)",
+}
+SQLITE.update({k: v for k, v in F.WINDOW.items()})     # window functions are native in sqlite
+
+
+def _table():
+    return pa.table({"s": pa.array(S, pa.string()), "n": pa.array(NV, pa.int64()), "f": pa.array(FV, pa.float64()),
+                     "d": pa.array(DV, pa.date32()), "ts": pa.array(TSV, pa.timestamp("us"))})
+
+
+def _sql(name, expr):
+    if name == "grouping":
+        return f"select s, {expr} as v from t group by rollup(s)"
+    return f"select {expr} as v from t"
+
+
+CASES = sorted((cat, name) for cat, d in F.CATEGORIES.items() for name in d)
+_ENG = {}
+
+
+def _engine(dev):
+    if dev not in _ENG:
+        e = ig.QueryEngine(device=dev)
+        e.register_table("t", _table())
+        _ENG[dev] = e
+    return _ENG[dev]
+
+
+def _norm(v):
+    if isinstance(v, bool):
+        return float(v)
+    if isinstance(v, (int, float)):
+        return round(float(v), 6) if math.isfinite(float(v)) else repr(float(v))
+    if isinstance(v, datetime.datetime):
+        return v.strftime("%Y-%m-%d %H:%M:%S")
+    if isinstance(v, datetime.date):
+        return v.isoformat()
+    return v
+
+
+def _rows(rs):
+    return sorted((tuple(_norm(x) for x in r) for r in rs), key=repr)
+
+
+def _sqlite_rows(name, expr):
+    con = sqlite3.connect(":memory:")
+    con.execute("create table t(s text, n int, f real, d text, ts text)")
+    con.executemany("insert into t values (?,?,?,?,?)",
+                    [(s, n, f, None if d is None else d.isoformat(), None if t is None else t.strftime("%Y-%m-%d %H:%M:%S"))
+                     for s, n, f, d, t in zip(S, NV, FV, DV, TSV)])
+    return _rows(con.execute(_sql(name, expr)).fetchall())
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c}-{n}" for c, n in CASES])
+def test_function_cpu(case):
+    cat, name = case
+    expr = F.CATEGORIES[cat][name]
+    got = _rows(tuple(r.values()) for r in _engine("cpu").query(_sql(name, expr)).to_pylist())
+    assert got, name
+    if name in SQLITE:
+        assert got == _sqlite_rows(name, SQLITE[name]), (name, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[f"{c}-{n}" for c, n in CASES])
+def test_function_gpu(gpu_device, case):
+    from igloo_amd.ops._lib import KERNEL_CALLS
+    cat, name = case
+    expr = F.CATEGORIES[cat][name]
+    before = KERNEL_CALLS["str_fn"] + KERNEL_CALLS["str_fn_int"]
+    got = _rows(tuple(r.values()) for r in _engine(gpu_device).query(_sql(name, expr)).to_pylist())
+    want = _rows(tuple(r.values()) for r in _engine("cpu").query(_sql(name, expr)).to_pylist())
+    assert got == want, (name, got, want)
+    if name in ("btrim", "trim", "ltrim", "rtrim", "replace", "lpad", "rpad", "reverse", "repeat", "left", "right",
+                "translate", "split_part", "strpos", "instr", "position", "octet_length", "initcap"):
+        assert KERNEL_CALLS["str_fn"] + KERNEL_CALLS["str_fn_int"] > before, f"{name}: string kernel did not run"
+
+
+def test_sqlinfo_lists_registry():
+    from igloo_amd.service import flight_sql as FS
+    assert "TRIM" in FS.STRING_FUNCTIONS and "VARIANCE" in FS.NUMERIC_FUNCTIONS
+    assert set(FS.STRING_FUNCTIONS) == {n.upper() for n in F.STRING}
+    assert "DATE_TRUNC" in FS.DATETIME_FUNCTIONS
+
+
+def test_bind_params_negative_and_comments():
+    from igloo_amd.service import flight_sql as FS
+    q = "select 10-? as a /* ? */ -- ?\n, '?' as b"
+    assert FS.count_params(q) == 1
+    e = _engine("cpu")
+    r = e.query(FS.bind_params(q, [-5])).to_pylist()
+    assert r == [{"a": 15, "b": "?"}]
+    assert "NaN" in FS.bind_params("select ?", [float("nan")])
+
+
+def test_statements():
+    e = ig.QueryEngine(device="cpu")
+    e.register_table("u", pa.table({"a": pa.array([1, 2], pa.int64()), "b": pa.array(["x", None], pa.string())}))
+    assert e.sql("describe u").table.to_pylist() == [
+        {"column_name": "a", "data_type": "Int64", "is_nullable": "YES"},
+        {"column_name": "b", "data_type": "Utf8", "is_nullable": "YES"}]
+    assert e.sql("show columns from u").table.num_rows == 2
+    assert e.sql("insert into u values (3, 'y'), (4, null)").table.to_pylist() == [{"count": 2}]
+    assert e.sql("insert into u (a) select a + 10 from u where a < 3").table.to_pylist() == [{"count": 2}]
+    assert e.query("select a, b from u order by a").to_pylist() == [
+        {"a": 1, "b": "x"}, {"a": 2, "b": None}, {"a": 3, "b": "y"}, {"a": 4, "b": None}, {"a": 11, "b": None},
+        {"a": 12, "b": None}]
+    e.sql("create view v (k, m) as select a, b from u where a > 2")
+    assert e.query("select k from v order by k").column("k").to_pylist() == [3, 4, 11, 12]
+    assert [r["column_name"] for r in e.sql("describe v").table.to_pylist()] == ["k", "m"]
+    e.sql("create or replace view v as select a from u where a = 1")
+    assert e.query("select count(*) c from v").to_pylist() == [{"c": 1}]
+    e.sql("drop view v")
+    e.sql("truncate table u")
+    assert e.query("select count(*) c from u").to_pylist() == [{"c": 0}]
