@@ -482,6 +482,8 @@ class _Gen:
             if t.kind != "date32":
                 raise Bail("date_part of non-date")
             from ..ops.misc import DATE_FIELDS
+            if e.options[0] not in DATE_FIELDS:
+                raise Bail(f"date_part {e.options[0]}")
             return self.bind("i32", f"date_part((i32)({v}), {DATE_FIELDS[e.options[0]]})"), va, T.INT32
         if name == "add_months":
             v, va, t = args[0]
@@ -506,17 +508,18 @@ class _Gen:
             if not t.is_float:
                 raise Bail("round type")
             f = _flit(10.0**d)
-            return self.bind("double", f"__builtin_rint((double)({v}) * {f}) / {f}"), va, T.FLOAT64
+            # half away from zero, like the CPU path (Rust f64::round)
+            return self.bind("double", f"__builtin_round((double)({v}) * {f}) / {f}"), va, T.FLOAT64
         if name in ("sqrt", "ln", "log10", "exp", "floor", "ceil"):
             v, va, t = args[0]
             x = self.conv((v, va, t), T.FLOAT64)
-            fn = {"sqrt": "__builtin_sqrt", "ln": "__builtin_log", "log10": "__builtin_log10",
-                  "exp": "__builtin_exp", "floor": "__builtin_floor", "ceil": "__builtin_ceil"}[name]
+            fn = {"sqrt": "__builtin_sqrt", "ln": "__ocml_log_f64", "log10": "__ocml_log10_f64",
+                  "exp": "__ocml_exp_f64", "floor": "__builtin_floor", "ceil": "__builtin_ceil"}[name]
             return self.bind("double", f"{fn}({x})"), va, T.FLOAT64
         if name == "power":
             a = self.conv(args[0], T.FLOAT64)
             c = self.conv(args[1], T.FLOAT64)
-            return self.bind("double", f"__builtin_pow({a}, {c})"), self.vand(args[0][1], args[1][1]), T.FLOAT64
+            return self.bind("double", f"__ocml_pow_f64({a}, {c})"), self.vand(args[0][1], args[1][1]), T.FLOAT64
         raise Bail(f"function {name}")
 
 
@@ -530,7 +533,12 @@ def _source(g: _Gen, out_t: DataType, val: str, valid: Optional[str]) -> str:
     if valid is not None:
         ps.append("u8* __restrict__ outv")
     ps += ["int* __restrict__ errp", "i64 n"] + [f"i64 p{j}" for j in range(len(g.params))]
-    L = [PRELUDE, f"extern \"C\" __global__ __launch_bounds__({BLOCK}) void igloo_jit_expr(" + ", ".join(ps) + ") {",
+    body = "\n".join(g.lines)
+    # device math library entry points, declared only where used (hiprtc links
+    # ocml; a bare __builtin_exp / log / pow has no gfx950 lowering), so the
+    # recorded sources of other kernels (igloo_amd/jit_sources) stay valid
+    ocml = "".join(f'extern "C" __device__ double {fn}({args});\n' for fn, args in _OCML if fn in body)
+    L = [PRELUDE + ocml, f"extern \"C\" __global__ __launch_bounds__({BLOCK}) void igloo_jit_expr(" + ", ".join(ps) + ") {",
          "  int err = 0;",
          f"  for (i64 i = (i64)blockIdx.x * {BLOCK} + threadIdx.x; i < n; i += (i64)gridDim.x * {BLOCK}) {{"]
     L += ["    " + s for s in g.lines]
@@ -544,6 +552,8 @@ def _source(g: _Gen, out_t: DataType, val: str, valid: Optional[str]) -> str:
     return "\n".join(L)
 
 
+_OCML = (("__ocml_exp_f64", "double"), ("__ocml_log_f64", "double"), ("__ocml_log10_f64", "double"),
+         ("__ocml_pow_f64", "double, double"))
 _SIMPLE = (ColRef, Lit)
 _ROOTS = (BinOp, Case, Cast, Func, Not, Neg, IsNull, InList)
 

@@ -92,6 +92,20 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
 BOUND_TRUST_ROWS = 1 << 20
 
 
+#: IGLOO_CHECK_KEY_TAGS=1 (the GPU test suite sets it): verify every
+#: readback-free key fact (key_unique tags, key_bound intervals) against the
+#: data it describes, one readback each
+CHECK_KEY_TAGS = os.environ.get("IGLOO_CHECK_KEY_TAGS", "0") not in ("", "0")
+
+
+def _check_bound(keys: torch.Tensor, b: Tuple[int, int]) -> Tuple[int, int]:
+    if CHECK_KEY_TAGS and keys.numel() and not capturing():
+        lo, hi = to_host_ints(torch.stack([keys.min().to(torch.int64), keys.max().to(torch.int64)]))
+        if lo < b[0] or hi > b[1]:
+            raise AssertionError(f"key_bound {b} does not hold the keys' range [{lo}, {hi}]")
+    return b
+
+
 def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
     """An interval holding every key, known without a readback in steady
     state: the (remembered) range of the resident column the keys were
@@ -101,7 +115,7 @@ def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
     (direct-mapped table spans, bit widths, overflow-free sums)."""
     b = getattr(keys, "_igloo_bound", None)
     if b is not None:
-        return b
+        return _check_bound(keys, b)
     o = _origin(keys)
     if o is None or o.dtype != keys.dtype or o.dim() != 1:
         return None
@@ -110,7 +124,7 @@ def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
         if capturing():
             return None
         st = column_stats(o)
-    return st[0]
+    return _check_bound(keys, st[0]) if st[0] is not None else None
 
 
 #: unsorted resident key columns up to this many rows get a one-time
@@ -221,6 +235,10 @@ class JoinTable:
         st = stream(keys)
         N.join_build(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
                      self.kmin, self.direct, ptr(dups), ptr(self.bits), self.bmask, st)
+        if known_unique and CHECK_KEY_TAGS and not capturing():
+            # debug / test mode: the tag-derived uniqueness must match the build's own duplicate count
+            if to_host_int(dups) != 0:
+                raise AssertionError("key_unique() trusted a key tag on keys that hold duplicates")
         self.unique = known_unique or to_host_int(dups) == 0
         # duplicate keys: CSR runs (count -> exclusive scan -> scatter), so a
         # multi-match probe reads one contiguous run of build rows

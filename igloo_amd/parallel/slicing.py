@@ -229,9 +229,19 @@ def slice_columns(cols: Dict[str, Column], n: int, key: str, world: int, rank: i
                     and kt.dtype in (torch.int32, torch.int64) and n and H.is_sorted(kt):
                 kmin, kmax = to_host_ints(kt[[0, -1]].to(torch.int64))
                 chunk = range_chunk(kmin, kmax, world)
-                cuts = device_ints([kmin + r * chunk for r in (rank, rank + 1)], kt.device, kt.dtype) \
-                    if kt.is_cuda else torch.tensor([kmin + r * chunk for r in (rank, rank + 1)], dtype=kt.dtype)
+                # cut points in int64, clamped to kmax + 1: kmin + world * chunk
+                # can pass the key type's range (an int32 key near INT32_MAX)
+                cut_vals = [min(kmin + r * chunk, kmax + 1) for r in (rank, rank + 1)]
+                if kt.dtype == torch.int32:
+                    cut_vals = [min(v, 2**31 - 1) for v in cut_vals]
+                    hi_full = cut_vals[1] == 2**31 - 1 and kmax == 2**31 - 1
+                else:
+                    hi_full = False
+                cuts = device_ints(cut_vals, kt.device, kt.dtype) if kt.is_cuda \
+                    else torch.tensor(cut_vals, dtype=kt.dtype)
                 a, b = to_host_ints(torch.searchsorted(kt, cuts).to(torch.int64))
+                if hi_full or (rank == world - 1):
+                    b = n                 # the last slice ends at the last row
                 tag = range_tag(world, kmin, chunk)
             else:
                 a, b = n * rank // world, n * (rank + 1) // world

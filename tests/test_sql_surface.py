@@ -193,7 +193,7 @@ def test_surface_gpu(gpu_device, qi):
     before = KERNEL_CALLS["win_seg_scan"] + KERNEL_CALLS["win_rank"] + KERNEL_CALLS["win_index"] + \
         KERNEL_CALLS["win_bounds"]
     assert _run(gpu_device, q) == _expected(q, oracle), q
-    if "over" in q or "qualify" in q or "all" in q.split():
+    if "over" in q or "qualify" in q or "intersect all" in q or "except all" in q:
         after = KERNEL_CALLS["win_seg_scan"] + KERNEL_CALLS["win_rank"] + KERNEL_CALLS["win_index"] + \
             KERNEL_CALLS["win_bounds"]
         assert after > before, "window kernels did not run"
