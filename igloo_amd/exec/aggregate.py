@@ -485,7 +485,7 @@ class HashAggExec(ExecNode):
             raw = child.scan_raw(ctx)
             pred = child.predicate
 
-            def local(groups, aggs, raw=raw, pred=pred):
+            def local(groups, aggs, plan=None, raw=raw, pred=pred):
                 return fused.fused_scan_aggregate(groups, aggs, raw, pred, ctx)
             if not ctx.spmd:
                 out = local(lg.groups, lg.aggs)

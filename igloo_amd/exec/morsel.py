@@ -201,11 +201,15 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
     from ..parallel.exchange import _TmpIds, decomposable, partial_plan
     from .operators import ScanExec, aggregate, apply_key_filters
     lg = agg.logical
-    if ctx.budget is None or ctx.spmd or not decomposable(lg.aggs):
+    if ctx.budget is None or not decomposable(lg.aggs):
         return None
     if any(getattr(a, "filter", None) is not None and _has_subquery(a.filter) for _, a in lg.aggs):
         return None
     scan = pick_stream_scan(agg, ctx)
+    if ctx.spmd:
+        # every rank takes the same path with the same morsel count: the
+        # subtree below the aggregate may exchange rows once per morsel
+        return _spmd_streamed_aggregate(agg, scan, ctx)
     if scan is None:
         return None
     child = agg.children[0]
@@ -254,6 +258,122 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
         agg.runtime_filters = []
     with ctx.span("morsel.merge"):
         return acc.finish()
+
+
+def _morsel_rows(scan, ctx) -> int:
+    src = scan.logical.source
+    row_bytes = max(1, scan_bytes(scan) // max(1, src.num_rows() or 1))
+    return max(MORSEL_MIN_ROWS, ctx.budget // MORSEL_FRACTION // row_bytes)
+
+
+def _agreed_morsels(gen_fn, scan, count: int, ctx):
+    """This rank's morsels, padded with empty ones to ``count`` (every rank
+    runs the same number of pipeline iterations: each may hold collectives)."""
+    n = 0
+    first = None
+    for raw in gen_fn():
+        if first is None:
+            first = raw
+        n += 1
+        yield raw
+    if n >= count:
+        return
+    empty = _empty_morsel(scan, first, ctx)
+    for _ in range(count - n):
+        yield empty
+
+
+def _empty_morsel(scan, like, ctx) -> Batch:
+    from ..ops.gather import take_many
+    if like is None:
+        names, _, _ = scan.column_names()
+        like = scan.logical.source.scan(names, ctx)
+    keys = list(like.columns)
+    dev = next(iter(like.columns.values())).device if keys else ctx.device
+    idx = torch.zeros(0, dtype=torch.int64, device=dev)
+    return Batch(dict(zip(keys, take_many([like.columns[k] for k in keys], idx))) if keys else {}, 0, like.dist)
+
+
+def _spmd_streamed_aggregate(agg, scan, ctx) -> Optional[Batch]:
+    """Bounded-memory aggregation under SPMD: ranks agree (one all-reduce) on
+    whether to stream and on the morsel count; each rank folds its morsels
+    into partial states (compacted under the budget like the single-rank
+    pipeline), and ``distributed_aggregate`` exchanges and merges them."""
+    from ..parallel.exchange import distributed_aggregate
+    from .operators import ScanExec, aggregate, apply_key_filters
+    lg = agg.logical
+    from .joins import MultiJoinExec
+    if any(isinstance(n, MultiJoinExec) for n in _walk(agg.children[0])):
+        # a multi-way join re-planned per morsel under SPMD carries
+        # rank-dependent column sets into its exchanges: not streamed (a
+        # plan-only test, alike on every rank)
+        return None
+    want = 0
+    if scan is not None:
+        src = scan.logical.source
+        want = max(1, -(-(src.num_rows() or 0) // _morsel_rows(scan, ctx)))
+    count = max(x[0] for x in ctx.comm.allgather_ints([want]))
+    if count == 0:
+        return None                   # no rank streams: the plain path on every rank
+    if scan is None:
+        # this rank's data fits but another's does not: stream anyway (one
+        # morsel per pipeline step) so the collective sequences match
+        scan = _any_stream_scan(agg)
+        if scan is None:
+            raise RuntimeError("SPMD morsel pipeline: no streamable scan on this rank")
+    child = agg.children[0]
+    names, _, _ = scan.column_names()
+    src = scan.logical.source
+    max_rows = _morsel_rows(scan, ctx)
+
+    def local(groups, partial, plan):
+        from ..parallel.exchange import _TmpIds
+        on_path = {id(n) for n in _walk(child) if _contains(n, scan)}
+        saved = (ctx.memo, ctx.memo_ids, ctx.morsel)
+        ctx.memo, ctx.memo_ids = {}, {id(n) for n in _walk(child) if id(n) not in on_path}
+        ctx.morsel_depth += 1
+        acc = _PartialStates(groups, partial, plan, _TmpIds(), ctx, count)
+        stats = ctx.morsels
+        stats["pipelines"] += 1
+        try:
+            gen = _agreed_morsels(lambda: src.scan_morsels(names, ctx, scan.pushable(), max_rows), scan, count, ctx)
+            for k, raw in enumerate(prefetched(gen, ctx)):
+                ctx.morsel = (id(scan), raw, ("morsel", stats["pipelines"], k))
+                stats["morsels"] += 1
+                stats["rows"] += raw.num_rows
+                ctx.rows_scanned += raw.num_rows
+                b = child.execute(ctx)
+                if agg.runtime_filters:
+                    b = apply_key_filters(b, list(agg.runtime_filters), ctx)
+                acc.add(aggregate(groups, partial, b, ctx))
+                ctx.scan_cache = {k2: v for k2, v in ctx.scan_cache.items() if k2[-1] != ctx.morsel[2]}
+                ctx.morsel = None
+        finally:
+            ctx.memo, ctx.memo_ids, ctx.morsel = saved
+            ctx.morsel_depth -= 1
+        out = acc.partials()
+        return out if out is not None else _empty_partials(groups, partial, ctx)
+    try:
+        return distributed_aggregate(lg, Batch({}, 0, None), ctx, local=local)
+    finally:
+        agg.runtime_filters = []
+
+
+def _empty_partials(groups, partial, ctx) -> Batch:
+    from .aggregate import _empty_col
+    return Batch({ci.cid: _empty_col(ci.dtype, ctx.device) for ci, _ in list(groups) + list(partial)}, 0)
+
+
+def _any_stream_scan(agg):
+    from .operators import ScanExec
+    best, best_bytes = None, -1
+    for n in _walk(agg.children[0]):
+        if isinstance(n, ScanExec) and getattr(n.logical.source, "can_stream", False) \
+                and stream_path_ok(agg.children[0], n):
+            b = scan_bytes(n)
+            if b > best_bytes:
+                best, best_bytes = n, b
+    return best
 
 
 class _PartialStates:
@@ -342,6 +462,26 @@ class _PartialStates:
             self.ctx.spill["bytes"] += _batch_bytes(piece)
             self.spill[p].append(_to_host(piece) if self.ctx.device.type == "cuda" else piece)
         self.ctx.spill["aggregate_partitions"] = P
+
+    def partials(self) -> Optional[Batch]:
+        """The partial states compacted to one row per group (not finalised:
+        an SPMD exchange merges them across ranks)."""
+        from .operators import _to_device, _to_host, concat_batches
+        if self.spill is None:
+            if not self.parts:
+                return None
+            return self._compact(concat_batches(self.parts)) if self.groups and len(self.parts) > 1 \
+                else concat_batches(self.parts)
+        dev = self.ctx.device
+        outs = []
+        for plist in self.spill:
+            if plist:
+                d = concat_batches([_to_device(b, dev) if dev.type == "cuda" else b for b in plist])
+                o = self._compact(d)
+                outs.append(_to_host(o) if dev.type == "cuda" else o)
+        if not outs:
+            return None
+        return concat_batches([_to_device(o, dev) if dev.type == "cuda" else o for o in outs])
 
     def finish(self) -> Optional[Batch]:
         from ..parallel.exchange import merge_partials

@@ -170,7 +170,9 @@ class ScanExec(ExecNode):
         return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
 
     def _run(self, ctx):
-        if ctx.budget is not None and self.logical.filters and not ctx.spmd \
+        # (under SPMD too: a filtered scan is rank-local, so each rank may stream
+        # its own rows or not without changing any collective)
+        if ctx.budget is not None and self.logical.filters \
                 and not (ctx.morsel is not None and ctx.morsel[0] == id(self)):
             from .morsel import streamed_scan
             out = streamed_scan(self, ctx)

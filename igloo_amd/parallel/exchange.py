@@ -943,7 +943,7 @@ def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     # ---- phase 1: partial states
     ids = _TmpIds()
     partial, plan = partial_plan(aggs, ids)
-    pb = local(groups, partial) if local is not None else None
+    pb = local(groups, partial, plan) if local is not None else None
     restore = None
     if pb is None:
         pb, groups, restore = _partial_by_rows(groups, partial, b, ids, ctx)

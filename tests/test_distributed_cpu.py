@@ -19,9 +19,12 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_thresholds=False, replicate_dims=True):
+def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_thresholds=False, replicate_dims=True,
+            budget_gb=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
+    if budget_gb is not None:
+        os.environ["IGLOO_DEVICE_BUDGET_GB"] = str(budget_gb)
     import igloo_amd as ig
     from igloo_amd.models.tpch import datagen
     from igloo_amd.models.tpch import queries as Q
@@ -51,7 +54,8 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
             from igloo_amd.models.tpch.oracle import normalize
             rows = [[normalize(v) for v in r.values()] for r in e.sql(Q.QUERIES[q]).table.to_pylist()]
             res[q] = {"rows": rows, "collectives": e.last_metrics.get("collectives"),
-                      "bytes": e.last_metrics.get("exchange_bytes")}
+                      "bytes": e.last_metrics.get("exchange_bytes"),
+                      "morsels": (e.last_metrics.get("morsels") or {}).get("morsels", 0)}
         except Exception as ex:  # noqa: BLE001
             res[q] = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0:
@@ -60,13 +64,14 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
     comm.shutdown()
 
 
-def run_distributed(world, con, device="cpu", low_thresholds=False, replicate_dims=True):
+def run_distributed(world, con, device="cpu", low_thresholds=False, replicate_dims=True, budget_gb=None):
     """Run TPC-H 1-22 on ``world`` ranks (gloo) and compare rank 0 with sqlite."""
     from igloo_amd.models.tpch import oracle
     qs = list(range(1, 23))
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.json")
-        mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs, device, low_thresholds, replicate_dims),
+        mp.start_processes(_worker, args=(world, _free_port(), out, 0.01, qs, device, low_thresholds, replicate_dims,
+                                          budget_gb),
                            nprocs=world,
                            join=True, start_method="spawn")
         res = json.load(open(out))
@@ -301,3 +306,16 @@ def test_sql_surface_distributed(world):
         if TS._rows(tuple(x) for x in r) != TS._expected(q, oracle):
             bad.append(q)
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tpch_distributed_bounded_memory(world, tpch_cpu):
+    """Bounded-memory execution under SPMD: a per-rank device
+    budget far below the data makes filtered scans stream and aggregates run
+    as morsel pipelines whose rank-agreed morsel counts keep every rank's
+    collectives in step; all 22 queries still match sqlite."""
+    _, _, con = tpch_cpu
+    bad = run_distributed(world, con, replicate_dims=False, budget_gb=0.0004)
+    assert not bad, "\n".join(bad)
+    streamed = [int(q) for q, r in run_distributed.last.items() if r.get("morsels")]
+    assert len(streamed) >= 10, streamed
