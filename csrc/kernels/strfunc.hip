@@ -285,7 +285,10 @@ __global__ __launch_bounds__(kBlock) void strfn_copy_kernel(StrFnArgs a, const i
   }
 }
 
-__global__ __launch_bounds__(kBlock) void strfn_int_kernel(int fn, const uint8_t* __restrict__ pat, int64_t plen,
+// one instantiation per function: a runtime switch over the three bodies in
+// one kernel was mis-compiled (the octet-length branch stored stale data)
+template <int FN>
+__global__ __launch_bounds__(kBlock) void strfn_int_kernel(const uint8_t* __restrict__ pat, int64_t plen,
                                                            const int64_t* __restrict__ off,
                                                            const uint8_t* __restrict__ chars, int64_t n,
                                                            int32_t* __restrict__ out) {
@@ -293,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void strfn_int_kernel(int fn, const uint8_t
     const uint8_t* s = chars + off[i];
     const int64_t m = off[i + 1] - off[i];
     int32_t v = 0;
-    if (fn == kSfStrpos) {
+    if constexpr (FN == kSfStrpos) {
       // 1-based character position of the first occurrence, 0 when absent
       int64_t c = 0;
       v = plen == 0 ? 1 : 0;
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void strfn_int_kernel(int fn, const uint8_t
           break;
         }
       }
-    } else if (fn == kSfAscii) {
+    } else if constexpr (FN == kSfAscii) {
       if (m > 0) {
         const uint8_t c0 = s[0];
         const int l = utf8_len(c0);
@@ -341,8 +344,15 @@ void str_fn_copy(const StrFnArgs& a, const int64_t* off, const uint8_t* chars, i
 void str_fn_int(int fn, const uint8_t* pat, int64_t plen, const int64_t* off, const uint8_t* chars, int64_t n,
                 int32_t* out, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(strfn_int_kernel, dim3(grid_for(n, kBlock, 1 << 16)), dim3(kBlock), 0, s, fn, pat, plen, off,
-                     chars, n, out);
+  dim3 g(grid_for(n, kBlock, 1 << 16)), b(kBlock);
+  if (fn == kSfStrpos)
+    hipLaunchKernelGGL(strfn_int_kernel<kSfStrpos>, g, b, 0, s, pat, plen, off, chars, n, out);
+  else if (fn == kSfAscii)
+    hipLaunchKernelGGL(strfn_int_kernel<kSfAscii>, g, b, 0, s, pat, plen, off, chars, n, out);
+  else if (fn == kSfOctetLength)
+    hipLaunchKernelGGL(strfn_int_kernel<kSfOctetLength>, g, b, 0, s, pat, plen, off, chars, n, out);
+  else
+    throw std::runtime_error("str_fn_int: bad function");
   check_launch("strfn.int", s);
 }
 
