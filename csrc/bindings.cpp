@@ -249,6 +249,21 @@ PYBIND11_MODULE(_native, m) {
                            uintptr_t s) {
     kern::select_write(P<const uint8_t>(mask), n, P<const int64_t>(tiles), P<void>(out), idx64, cap, S(s));
   });
+  m.def("select_compact", [](uintptr_t mask, int64_t n, uintptr_t tiles,
+                             const std::vector<std::tuple<uintptr_t, uintptr_t, int, uintptr_t, uintptr_t>>& cols,
+                             uintptr_t idx, bool idx64, int64_t cap, uintptr_t s) {
+    kern::CompactArgs a{};
+    if ((int)cols.size() > kern::kMaxCompactCols) throw std::runtime_error("select_compact: too many columns");
+    for (size_t j = 0; j < cols.size(); ++j) {
+      auto& c = cols[j];
+      a.cols[j] = {P<void>(std::get<0>(c)), P<void>(std::get<1>(c)), std::get<2>(c), P<uint8_t>(std::get<3>(c)),
+                   P<uint8_t>(std::get<4>(c))};
+    }
+    a.ncols = (int)cols.size();
+    a.idx = P<void>(idx);
+    a.idx64 = idx64;
+    kern::select_compact(P<uint8_t>(mask), n, P<int64_t>(tiles), a, cap, S(s));
+  });
   m.def("scan_workspace_tiles", &kern::scan_workspace_tiles);
   m.def("exclusive_scan", [](uintptr_t in, bool in64, int64_t n, uintptr_t out, uintptr_t ws, uintptr_t total, uintptr_t s) {
     kern::exclusive_scan(P<const void>(in), in64, n, P<int64_t>(out), P<int64_t>(ws), P<int64_t>(total), S(s));

@@ -21,6 +21,23 @@ void select_count(const uint8_t* mask, int64_t n, int64_t* tile_counts, int64_t*
 void select_write(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, void* out, bool idx64, int64_t cap,
                   hipStream_t stream);
 void scan_counts(int64_t* counts, int64_t n, int64_t* total, hipStream_t stream);
+constexpr int kMaxCompactCols = 12;
+struct CompactCol {
+  const void* src;
+  void* dst;
+  int esz;              // 1, 2, 4, 8 or 16 bytes per row
+  const uint8_t* sv;    // source validity (bytes) or null
+  uint8_t* dv;          // destination validity
+};
+struct CompactArgs {
+  CompactCol cols[kMaxCompactCols];
+  int ncols;
+  void* idx;            // optional: the surviving row indices too
+  bool idx64;
+};
+// columns compacted by a mask whose tile offsets select_count produced (cap: rows the outputs hold)
+void select_compact(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, const CompactArgs& a, int64_t cap,
+                    hipStream_t stream);
 int64_t scan_workspace_tiles(int64_t n);
 void exclusive_scan(const void* in, bool in64, int64_t n, int64_t* out, int64_t* tile_ws, int64_t* total,
                     hipStream_t stream);

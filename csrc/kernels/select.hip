@@ -188,7 +188,96 @@ __global__ __launch_bounds__(kBlock) void tile_write_kernel(const uint8_t* __res
     for (int64_t p = offsets[gridDim.x] + threadIdx.x; p < cap; p += kBlock) out[p] = (IdxT)0;
 }
 
+template <typename IdxT>
+__device__ __forceinline__ void compact_idx(IdxT* __restrict__ out, const uint16_t* stage, int total,
+                                            int64_t tile_base, int64_t o, int64_t cap) {
+  for (int k = threadIdx.x; k < total; k += kBlock)
+    if (o + k < cap) out[o + k] = (IdxT)(tile_base + stage[k]);
+}
+
+// Fused stream compaction of whole columns: the tile's surviving row
+// offsets are staged in LDS once (as in tile_write) and every column of the
+// batch is copied through them -- one pass over each column with the writes
+// coalesced, and no index vector written to and read back from HBM per
+// column (mask -> indices -> gather). Reads stay inside the tile's 8192-row
+// window of each column, so the lines a sparse tile touches are fetched once.
+template <typename T>
+__device__ __forceinline__ void compact_copy(const T* __restrict__ src, T* __restrict__ dst, const uint16_t* stage,
+                                             int total, int64_t tile_base, int64_t o, int64_t cap) {
+  for (int k = threadIdx.x; k < total; k += kBlock)
+    if (o + k < cap) dst[o + k] = src[tile_base + stage[k]];
+}
+
+struct U128 {
+  uint64_t lo, hi;
+};
+
+__global__ __launch_bounds__(kBlock) void tile_compact_kernel(const uint8_t* __restrict__ mask, int64_t n,
+                                                             const int64_t* __restrict__ offsets, CompactArgs a,
+                                                             int64_t cap) {
+  __shared__ int64_t scratch[kWavesPerBlock + 1];
+  __shared__ uint16_t stage[kTile];
+  const int64_t tile_base = (int64_t)blockIdx.x * kTile;
+  const int first = threadIdx.x * kItems;
+  uint32_t w[kItems / 4];
+  load_flags(mask, tile_base + first, n, w);
+  int64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < kItems / 4; ++q) c += __popc(w[q]);
+  int64_t total64;
+  int pos = (int)block_exclusive_scan(c, scratch, &total64);
+#pragma unroll
+  for (int q = 0; q < kItems / 4; ++q)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((w[q] >> (8 * b)) & 1u) stage[pos++] = (uint16_t)(first + 4 * q + b);
+  __syncthreads();
+  const int total = (int)total64;
+  const int64_t o = offsets[blockIdx.x];
+  if (a.idx != nullptr) {
+    if (a.idx64) compact_idx<int64_t>((int64_t*)a.idx, stage, total, tile_base, o, cap);
+    else compact_idx<int32_t>((int32_t*)a.idx, stage, total, tile_base, o, cap);
+  }
+  for (int j = 0; j < a.ncols; ++j) {
+    const CompactCol& cc = a.cols[j];
+    switch (cc.esz) {
+      case 1: compact_copy((const uint8_t*)cc.src, (uint8_t*)cc.dst, stage, total, tile_base, o, cap); break;
+      case 2: compact_copy((const uint16_t*)cc.src, (uint16_t*)cc.dst, stage, total, tile_base, o, cap); break;
+      case 4: compact_copy((const uint32_t*)cc.src, (uint32_t*)cc.dst, stage, total, tile_base, o, cap); break;
+      case 8: compact_copy((const uint64_t*)cc.src, (uint64_t*)cc.dst, stage, total, tile_base, o, cap); break;
+      default: compact_copy((const U128*)cc.src, (U128*)cc.dst, stage, total, tile_base, o, cap); break;
+    }
+    if (cc.sv != nullptr) compact_copy(cc.sv, cc.dv, stage, total, tile_base, o, cap);
+  }
+  // as in tile_write: a row count the host replayed instead of reading back
+  // may exceed the real one; the tail [real total, cap) is zeroed so no
+  // consumer of these outputs (row indices, join keys) sees garbage
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int64_t p = offsets[gridDim.x] + threadIdx.x; p < cap; p += kBlock) {
+      if (a.idx != nullptr) {
+        if (a.idx64) ((int64_t*)a.idx)[p] = 0;
+        else ((int32_t*)a.idx)[p] = 0;
+      }
+      for (int j = 0; j < a.ncols; ++j) {
+        const CompactCol& cc = a.cols[j];
+        uint8_t* d = (uint8_t*)cc.dst + p * cc.esz;
+        for (int q = 0; q < cc.esz; ++q) d[q] = 0;
+        if (cc.dv != nullptr) cc.dv[p] = 0;
+      }
+    }
+  }
+}
+
 }  // namespace
+
+void select_compact(const uint8_t* mask, int64_t n, const int64_t* tile_offsets, const CompactArgs& a, int64_t cap,
+                    hipStream_t stream) {
+  int64_t tiles = select_num_tiles(n);
+  if (tiles == 0) return;
+  hipLaunchKernelGGL(tile_compact_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, stream, mask, n, tile_offsets, a,
+                     cap);
+  check_launch("select.compact", stream);
+}
 
 int64_t select_num_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 

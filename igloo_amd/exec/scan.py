@@ -24,7 +24,7 @@ from ..ops._lib import (check_not_capturing, device_ints, launch, ptr, stream, t
                        to_host_ints, unlogged)
 from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
-from ..ops.select import exclusive_scan, mask_to_indices
+from ..ops.select import compact_columns, exclusive_scan, mask_to_indices
 from ..sql import logical as L
 from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
 from ..utils.errors import ExecutionError, NotSupported
@@ -39,6 +39,11 @@ _CID = re.compile(r"#\d+")
 LATE_SCAN = True
 NDV_DERIVED = True
 
+
+
+#: fused mask compaction of a filtered scan's columns (IGLOO_COMPACT=0: mask ->
+#: indices -> gather, the A/B baseline)
+COMPACT = os.environ.get("IGLOO_COMPACT", "1") != "0"
 
 
 def _tag_base(col: Column, src: Column, n_src: int):
@@ -149,13 +154,27 @@ class ScanExec(ExecNode):
             fsql = tuple(sorted(_CID.sub("", f.sql()) for f in s.filters))
             key = (id(s.source), b.num_rows, fsql, ctx.morsel[2] if ctx.morsel is not None else None)
             hit = None if any("random" in x.lower() for x in fsql) else ctx.scan_cache.get(key)
+            late = self.late_ok and LATE_SCAN and ctx.device.type == "cuda"
             if hit is None:
                 with ctx.span("scan.filter_eval"):
                     m = predicate_mask(self.predicate, b, ctx)
-                    idx = mask_to_indices(m)
-                hit = ctx.scan_cache[key] = (idx, {})
+                if COMPACT and not late and ctx.device.type == "cuda":
+                    # every projected column in the same pass as the mask's
+                    # compaction (select.hip tile_compact): no index vector
+                    # between the mask and the column copies
+                    with ctx.span("scan.filter_compact"):
+                        idx, cols = compact_columns(m, [b.columns[c] for c in out_cids])
+                    taken = {}
+                    for c, col in zip(out_cids, cols):
+                        _tag_base(col, b.columns[c], b.num_rows)
+                        taken[name[c]] = col
+                    hit = ctx.scan_cache[key] = (idx, taken)
+                else:
+                    with ctx.span("scan.filter_eval"):
+                        idx = mask_to_indices(m)
+                    hit = ctx.scan_cache[key] = (idx, {})
             idx, taken_by_name = hit
-            if self.late_ok and LATE_SCAN and ctx.device.type == "cuda":
+            if late:
                 # index form: the join gathers its key columns now and payload
                 # columns only for the rows that survive it
                 src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)

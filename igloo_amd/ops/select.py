@@ -85,3 +85,61 @@ def offsets_from_lengths(lengths: torch.Tensor, host_total: bool = True):
     N.exclusive_scan(ptr(lengths), lengths.dtype == torch.int64, n, ptr(off), ptr(ws), ptr(off) + 8 * n,
                      stream(lengths))
     return off, (to_host_int(off[n:]) if host_total else off[n:])
+
+
+#: columns per fused compaction launch (csrc/kernels/kernels.h kMaxCompactCols)
+COMPACT_MAX_COLS = 12
+
+
+def compact_columns(mask: torch.Tensor, cols, total: Optional[int] = None, want_idx: bool = True):
+    """Rows where ``mask`` is True of every column in ``cols`` -> (row indices
+    or None, compacted columns). On the GPU the fixed-width columns (numbers,
+    dates, dictionary codes, 128-bit decimals, with their validity) are
+    compacted in ONE fused pass per 12 columns (select.hip tile_compact): the
+    mask's surviving offsets are staged per tile in LDS and every column is
+    copied through them, with no index vector between the mask and the
+    gathers. Plain string columns go through the indices."""
+    from ..columnar import Column
+    from .gather import _inherit, take_many
+    assert mask.dtype == torch.bool and mask.dim() == 1
+    n = mask.numel()
+    if not is_gpu(mask):
+        idx = mask_to_indices(mask, total)
+        return idx, take_many(list(cols), idx)
+    mask = mask.contiguous()
+    N = launch("select_compact")
+    tiles = N.select_num_tiles(n)
+    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
+    s = stream(mask)
+    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
+    if total is None:
+        total = to_host_int(ws[tiles:])
+    it = idx_dtype(n)
+    plain = [c for c in cols if c.is_plain_string]
+    idx = torch.empty(total, dtype=it, device=mask.device) if (want_idx or plain) else None
+    outs = {}
+    descs = []
+    for k, c in enumerate(cols):
+        if c.is_plain_string:
+            continue
+        d = c.data.contiguous()
+        out = torch.empty((total,) + tuple(d.shape[1:]), dtype=d.dtype, device=mask.device)
+        esz = d.element_size() * (d.shape[1] if d.dim() == 2 else 1)
+        dv = torch.empty(total, dtype=torch.bool, device=mask.device) if c.valid is not None else None
+        descs.append((ptr(d), ptr(out), esz, ptr(c.valid.contiguous() if c.valid is not None else None), ptr(dv)))
+        _inherit(out, c.data)
+        if getattr(c.data, "_igloo_distinct", False):
+            out._igloo_distinct = True        # rows kept in order: still distinct
+        outs[k] = Column(c.dtype, out, dv, dictionary=c.dictionary)
+    if n and (descs or idx is not None):
+        first = True
+        for a in range(0, max(len(descs), 1), COMPACT_MAX_COLS):
+            N.select_compact(ptr(mask), n, ptr(ws), descs[a:a + COMPACT_MAX_COLS],
+                             ptr(idx) if first and idx is not None else 0, it == torch.int64, total, s)
+            first = False
+    if idx is not None:
+        idx._igloo_incr = True
+    if plain:
+        for k, c in zip([k for k, c in enumerate(cols) if c.is_plain_string], take_many(plain, idx)):
+            outs[k] = c
+    return idx, [outs[k] for k in range(len(cols))]
