@@ -680,6 +680,216 @@ __global__ __launch_bounds__(kBlock) void sorted_having_kernel(const K* __restri
   }
   if (__any(overflow) && lane == 0) atomicOr(&counter[1], 1ULL);
 }
+
+// Streaming variant for the common shape (TPC-H Q18: HAVING sum(int32) with
+// COUNT(*) alongside): every aggregate is either THE valued one -- a SUM over
+// an int32 column without NULLs, summed in int64 (2^32 rows of int32 cannot
+// overflow it) -- or a COUNT without a validity mask, which is the run's
+// length. Each wave owns a contiguous span of rows and walks it in 512-row
+// tiles (8 rows per lane, 16 B loads, the next tile prefetched into
+// registers), so a run crossing lanes or tiles costs no extra memory round
+// trip: the open run's value is carried from tile to tile, and across lanes
+// it comes from one plain wave prefix sum of the lanes' totals -- the value
+// of a run closing in lane l is (prefix at its end) - (prefix at its start),
+// its start lane found from a ballot of the lanes holding run starts. A run
+// is owned by the wave holding its first row; the one still open at the span
+// end is followed past it 64 rows per step. No run-length limit.
+constexpr int kScanTile = kWave * kSortedRows;
+
+template <typename K>
+__device__ inline void load_keys8(const K* __restrict__ keys, int64_t r0, int live, K k[kSortedRows]) {
+  if (live == kSortedRows && ((uintptr_t)(keys + r0) & 15) == 0) {
+    if (sizeof(K) == 4) {
+      const int4 a = *(const int4*)(keys + r0), b = *(const int4*)(keys + r0 + 4);
+      k[0] = (K)a.x; k[1] = (K)a.y; k[2] = (K)a.z; k[3] = (K)a.w;
+      k[4] = (K)b.x; k[5] = (K)b.y; k[6] = (K)b.z; k[7] = (K)b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSortedRows; j += 2) {
+        const longlong2 x = *(const longlong2*)(keys + r0 + j);
+        k[j] = (K)x.x;
+        k[j + 1] = (K)x.y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) k[j] = j < live ? keys[r0 + j] : (K)0;
+  }
+}
+
+__device__ inline void load_i32x8(const int32_t* __restrict__ v, int64_t r0, int live, int x[kSortedRows]) {
+  if (live == kSortedRows && ((uintptr_t)(v + r0) & 15) == 0) {
+    const int4 a = *(const int4*)(v + r0), b = *(const int4*)(v + r0 + 4);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) x[j] = j < live ? v[r0 + j] : 0;
+  }
+}
+
+// the value of the compared aggregate for a run of `cnt` rows summing to `sum`
+__device__ inline bool scan_run_passes(const HavingParams& p, int vagg, long long sum, long long cnt) {
+  const long long x = p.hagg == vagg ? sum : cnt;
+  return having_ok(p, (unsigned long long)x, x < 0 ? -1LL : 0LL);
+}
+
+__device__ inline void scan_run_write(const HavingParams& p, int vagg, int64_t o, long long sum, long long cnt) {
+  for (int a = 0; a < p.nagg; ++a) {
+    const long long x = a == vagg ? sum : cnt;
+    ((long long*)p.d[a].dst)[o] = x;
+    if (p.d[a].dst2) ((long long*)p.d[a].dst2)[o] = x < 0 ? -1LL : 0LL;
+  }
+}
+
+template <typename K, bool HAS_V>
+__global__ __launch_bounds__(kBlock) void sorted_having_scan_kernel(const K* __restrict__ keys, int64_t n, int64_t span,
+                                                                   HavingParams p, int vagg, int64_t* __restrict__ rep,
+                                                                   int64_t cap,
+                                                                   unsigned long long* __restrict__ counter) {
+  const int lane = lane_id();
+  const int64_t wave_id = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t s = wave_id * span;
+  if (s >= n) return;
+  const int64_t e = s + span < n ? s + span : n;
+  const int32_t* __restrict__ vals = HAS_V ? (const int32_t*)p.d[vagg].src : nullptr;
+  const uint64_t below = lane ? (~0ULL >> (kWave - lane)) : 0ULL;   // lanes < this one
+  // the open run entering the tile: start row (-1: it began in an earlier
+  // wave's span, which owns it) and its value up to the tile
+  int64_t c_row = -1;
+  long long c_v = 0;
+  K last = s > 0 ? keys[s - 1] : (K)0;
+  K k[kSortedRows], nk[kSortedRows];
+  int v[kSortedRows] = {}, nvl[kSortedRows] = {};
+  {
+    const int64_t r0 = s + (int64_t)lane * kSortedRows;
+    const int live = (int)(e - r0 < 0 ? 0 : (e - r0 < kSortedRows ? e - r0 : kSortedRows));
+    load_keys8(keys, r0, live, nk);
+    if (HAS_V) load_i32x8(vals, r0, live, nvl);
+  }
+  for (int64_t base = s; base < e; base += kScanTile) {
+    const int64_t r0 = base + (int64_t)lane * kSortedRows;
+    const int live = (int)(e - r0 < 0 ? 0 : (e - r0 < kSortedRows ? e - r0 : kSortedRows));
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) {
+      k[j] = nk[j];
+      if (HAS_V) v[j] = nvl[j];
+    }
+    if (base + kScanTile < e) {     // prefetch the next tile while this one is folded
+      const int64_t q0 = r0 + kScanTile;
+      const int ql = (int)(e - q0 < 0 ? 0 : (e - q0 < kSortedRows ? e - q0 : kSortedRows));
+      load_keys8(keys, q0, ql, nk);
+      if (HAS_V) load_i32x8(vals, q0, ql, nvl);
+    }
+    K kp = __shfl_up(k[kSortedRows - 1], 1, kWave);
+    if (lane == 0) kp = last;
+    unsigned starts = 0;
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) {
+      const bool st = j < live && ((r0 + j == 0) || k[j] != (j ? k[j - 1] : kp));
+      starts |= st ? (1u << j) : 0u;
+    }
+    // lane totals, the sum before the first start (head) and before the last one
+    long long tot = 0, head = 0, pre_last = 0;
+    const int fs = starts ? __builtin_ctz(starts) : kSortedRows;
+    const int ls = starts ? 31 - __builtin_clz(starts) : -1;
+#pragma unroll
+    for (int j = 0; j < kSortedRows; ++j) {
+      const long long x = HAS_V ? (long long)v[j] : 0LL;
+      if (j == fs) head = tot;
+      if (j == ls) pre_last = tot;
+      tot += x;
+    }
+    if (!starts) head = tot;
+    const long long incl = wave_inclusive_scan(tot);
+    const long long excl = incl - tot;
+    const uint64_t smask = __ballot(starts != 0);
+    // prefix value at (and row of) this lane's last start
+    const long long q_last = excl + pre_last;
+    const int row_last = ls;   // within the lane
+    // run closing at this lane's first start: its start is the last start of
+    // the nearest lane below holding one, else the carried run
+    const uint64_t lower = smask & below;
+    const int m = lower ? 63 - __builtin_clzll(lower) : lane;
+    const long long q_m = __shfl(q_last, m, kWave);
+    const int rl_m = __shfl(row_last, m, kWave);
+    long long close_v;
+    int64_t close_row;
+    if (lower) {
+      close_v = excl + head - q_m;
+      close_row = base + (int64_t)m * kSortedRows + rl_m;
+    } else {
+      close_v = c_v + excl + head;
+      close_row = c_row;
+    }
+    // count passing runs: the closing one, then those between this lane's starts
+    auto runs = [&](auto&& emit) {
+      if (!starts) return;
+      if (close_row >= 0) emit(close_row, close_v, r0 + fs - close_row);
+      long long acc = 0;
+      int open = fs;
+#pragma unroll
+      for (int j = 0; j < kSortedRows; ++j) {
+        if (j > fs && ((starts >> j) & 1u)) {
+          emit(r0 + open, acc, (long long)(j - open));
+          acc = 0;
+          open = j;
+        }
+        if (j >= fs && HAS_V) acc += (long long)v[j];
+      }
+    };
+    int npass = 0;
+    runs([&](int64_t, long long sum, long long cnt) { npass += scan_run_passes(p, vagg, sum, cnt) ? 1 : 0; });
+    const int64_t pinc = wave_inclusive_scan((int64_t)npass);
+    const int64_t ptotal = __shfl(pinc, kWave - 1, kWave);
+    if (ptotal) {
+      unsigned long long wbase = 0;
+      if (lane == kWave - 1) wbase = atomicAdd(&counter[0], (unsigned long long)ptotal);
+      wbase = __shfl(wbase, kWave - 1, kWave);
+      int64_t o = (int64_t)wbase + pinc - npass;
+      runs([&](int64_t row, long long sum, long long cnt) {
+        if (!scan_run_passes(p, vagg, sum, cnt)) return;
+        if (o < cap) {
+          rep[o] = row;
+          scan_run_write(p, vagg, o, sum, cnt);
+        }
+        ++o;
+      });
+    }
+    // carry the run open at the tile's end
+    const long long tile_tot = __shfl(incl, kWave - 1, kWave);
+    if (smask) {
+      const int mt = 63 - __builtin_clzll(smask);
+      c_v = tile_tot - __shfl(q_last, mt, kWave);
+      c_row = base + (int64_t)mt * kSortedRows + __shfl(row_last, mt, kWave);
+    } else {
+      c_v += tile_tot;
+    }
+    last = __shfl(k[kSortedRows - 1], kWave - 1, kWave);
+  }
+  if (c_row < 0) return;
+  // follow the open run past the span, 64 rows per step
+  const K rk = keys[e - 1];
+  int64_t r = e;
+  while (r < n) {
+    const int64_t row = r + lane;
+    const bool in = row < n;
+    const bool same = in && keys[row] == rk;
+    const uint64_t ms = __ballot(same);
+    const int stop = ~ms ? __builtin_ctzll(~ms) : kWave;   // first lane off the run
+    long long x = (HAS_V && lane < stop) ? (long long)vals[row] : 0LL;
+    c_v += wave_reduce_sum(x);
+    r += stop;
+    if (stop < kWave) break;
+  }
+  if (lane == 0 && scan_run_passes(p, vagg, c_v, r - c_row)) {
+    const unsigned long long o = atomicAdd(&counter[0], 1ULL);
+    if ((int64_t)o < cap) {
+      rep[o] = c_row;
+      scan_run_write(p, vagg, (int64_t)o, c_v, r - c_row);
+    }
+  }
+}
 }  // namespace
 
 int agg_lds_max_groups(int nagg) {
@@ -702,6 +912,46 @@ void sorted_having(const void* keys, bool key64, int64_t n, const AggDesc* descs
   p.hlo = hlo;
   p.hhi = hhi;
   p.hf = hf;
+  // streaming shape: COUNTs without NULLs plus at most one NULL-free int32 SUM
+  int vagg = -1;
+  bool streaming = getenv("IGLOO_HAVING_SCAN") == nullptr || getenv("IGLOO_HAVING_SCAN")[0] != '0';
+  for (int k = 0; k < nagg && streaming; ++k) {
+    const AggDesc& d = descs[k];
+    if (d.valid) streaming = false;
+    else if (d.op == AGG_SUM_INT && !d.src64 && d.src && vagg < 0) vagg = k;
+    else if (d.op != AGG_COUNT) streaming = false;
+  }
+  if (streaming) {
+    // one resident round of waves (each owns one span): a second, partial
+    // round would double the kernel's time
+    static int resident[4] = {0, 0, 0, 0};
+    const void* fns[4] = {(const void*)sorted_having_scan_kernel<int32_t, false>,
+                          (const void*)sorted_having_scan_kernel<int32_t, true>,
+                          (const void*)sorted_having_scan_kernel<int64_t, false>,
+                          (const void*)sorted_having_scan_kernel<int64_t, true>};
+    const int which = (key64 ? 2 : 0) + (vagg >= 0 ? 1 : 0);
+    if (!resident[which]) {
+      int dev = 0, cus = 0, per_cu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[which], kBlock, 0);
+      resident[which] = std::max(1, cus * std::max(1, per_cu));
+    }
+    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    const int64_t blocks = std::min<int64_t>((tiles + kWavesPerBlock - 1) / kWavesPerBlock, resident[which]);
+    const int64_t waves = blocks * kWavesPerBlock;
+    const int64_t span = (tiles + waves - 1) / waves * kScanTile;
+    const dim3 g((unsigned)((((n + span - 1) / span) + kWavesPerBlock - 1) / kWavesPerBlock)), b(kBlock);
+#define IGLOO_HAVING_SCAN(K, V) \
+  hipLaunchKernelGGL((sorted_having_scan_kernel<K, V>), g, b, 0, stream, (const K*)keys, n, span, p, vagg, rep, cap, counter)
+    if (key64 && vagg >= 0) IGLOO_HAVING_SCAN(int64_t, true);
+    else if (key64) IGLOO_HAVING_SCAN(int64_t, false);
+    else if (vagg >= 0) IGLOO_HAVING_SCAN(int32_t, true);
+    else IGLOO_HAVING_SCAN(int32_t, false);
+#undef IGLOO_HAVING_SCAN
+    check_launch("sorted_having_scan", stream);
+    return;
+  }
   const dim3 g(grid_for(n, kBlock * kSortedRows, 32768)), b(kBlock);
   if (key64)
     hipLaunchKernelGGL(sorted_having_kernel<int64_t>, g, b, 0, stream, (const int64_t*)keys, n, p, rep, cap, counter);
