@@ -562,10 +562,10 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("str_like_segments", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t seg, uintptr_t seg_off, int nseg,
                                  bool anchor_start, bool anchor_end, bool negate, uintptr_t out, int64_t nbytes,
-                                 uintptr_t s) {
+                                 int min_seg, uintptr_t s) {
     kern::str_like_segments(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(seg),
                             P<const int32_t>(seg_off), nseg, anchor_start, anchor_end, negate, P<uint8_t>(out), nbytes,
-                            S(s));
+                            min_seg, S(s));
   });
   m.def("str_eq_rows", [](uintptr_t aoff, uintptr_t achars, uintptr_t ai, uintptr_t boff, uintptr_t bchars, uintptr_t bi,
                           bool idx64, int64_t n, uintptr_t mism, uintptr_t s) {

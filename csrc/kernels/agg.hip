@@ -717,15 +717,50 @@ __device__ inline void load_keys8(const K* __restrict__ keys, int64_t r0, int li
   }
 }
 
-__device__ inline void load_i32x8(const int32_t* __restrict__ v, int64_t r0, int live, int x[kSortedRows]) {
-  if (live == kSortedRows && ((uintptr_t)(v + r0) & 15) == 0) {
-    const int4 a = *(const int4*)(v + r0), b = *(const int4*)(v + r0 + 4);
-    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-  } else {
+// 8 values of VB bytes (4, 2, 1: int32 / int16 / int8, sign-extended) in one
+// or two vector loads
+template <int VB>
+__device__ inline void load_v8(const void* __restrict__ src, int64_t r0, int live, int x[kSortedRows]) {
+  if (VB == 4) {
+    const int32_t* v = (const int32_t*)src;
+    if (live == kSortedRows && ((uintptr_t)(v + r0) & 15) == 0) {
+      const int4 a = *(const int4*)(v + r0), b = *(const int4*)(v + r0 + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      return;
+    }
+  } else if (VB == 2) {
+    const int16_t* v = (const int16_t*)src;
+    if (live == kSortedRows && ((uintptr_t)(v + r0) & 15) == 0) {
+      const uint4 a = *(const uint4*)(v + r0);
+      const uint32_t w[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-    for (int j = 0; j < kSortedRows; ++j) x[j] = j < live ? v[r0 + j] : 0;
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = (int)(int16_t)(w[j] & 0xffff);
+        x[2 * j + 1] = (int)(int16_t)(w[j] >> 16);
+      }
+      return;
+    }
+  } else {
+    const int8_t* v = (const int8_t*)src;
+    if (live == kSortedRows && ((uintptr_t)(v + r0) & 7) == 0) {
+      const uint2 a = *(const uint2*)(v + r0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = (int)(int8_t)((a.x >> (8 * j)) & 0xff);
+        x[4 + j] = (int)(int8_t)((a.y >> (8 * j)) & 0xff);
+      }
+      return;
+    }
   }
+#pragma unroll
+  for (int j = 0; j < kSortedRows; ++j)
+    x[j] = j >= live ? 0 : VB == 4 ? ((const int32_t*)src)[r0 + j] : VB == 2 ? (int)((const int16_t*)src)[r0 + j]
+                                                                          : (int)((const int8_t*)src)[r0 + j];
+}
+
+__device__ inline int load_v1(const void* src, int vb, int64_t i) {
+  return vb == 4 ? ((const int32_t*)src)[i] : vb == 2 ? (int)((const int16_t*)src)[i] : (int)((const int8_t*)src)[i];
 }
 
 // the value of the compared aggregate for a run of `cnt` rows summing to `sum`
@@ -742,7 +777,7 @@ __device__ inline void scan_run_write(const HavingParams& p, int vagg, int64_t o
   }
 }
 
-template <typename K, bool HAS_V>
+template <typename K, int VB>
 __global__ __launch_bounds__(kBlock) void sorted_having_scan_kernel(const K* __restrict__ keys, int64_t n, int64_t span,
                                                                    HavingParams p, int vagg, int64_t* __restrict__ rep,
                                                                    int64_t cap,
@@ -752,7 +787,8 @@ __global__ __launch_bounds__(kBlock) void sorted_having_scan_kernel(const K* __r
   const int64_t s = wave_id * span;
   if (s >= n) return;
   const int64_t e = s + span < n ? s + span : n;
-  const int32_t* __restrict__ vals = HAS_V ? (const int32_t*)p.d[vagg].src : nullptr;
+  constexpr bool HAS_V = VB > 0;
+  const void* __restrict__ vals = HAS_V ? p.d[vagg].src : nullptr;
   const uint64_t below = lane ? (~0ULL >> (kWave - lane)) : 0ULL;   // lanes < this one
   // the open run entering the tile: start row (-1: it began in an earlier
   // wave's span, which owns it) and its value up to the tile
@@ -765,7 +801,7 @@ __global__ __launch_bounds__(kBlock) void sorted_having_scan_kernel(const K* __r
     const int64_t r0 = s + (int64_t)lane * kSortedRows;
     const int live = (int)(e - r0 < 0 ? 0 : (e - r0 < kSortedRows ? e - r0 : kSortedRows));
     load_keys8(keys, r0, live, nk);
-    if (HAS_V) load_i32x8(vals, r0, live, nvl);
+    if (HAS_V) load_v8<VB>(vals, r0, live, nvl);
   }
   for (int64_t base = s; base < e; base += kScanTile) {
     const int64_t r0 = base + (int64_t)lane * kSortedRows;
@@ -779,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void sorted_having_scan_kernel(const K* __r
       const int64_t q0 = r0 + kScanTile;
       const int ql = (int)(e - q0 < 0 ? 0 : (e - q0 < kSortedRows ? e - q0 : kSortedRows));
       load_keys8(keys, q0, ql, nk);
-      if (HAS_V) load_i32x8(vals, q0, ql, nvl);
+      if (HAS_V) load_v8<VB>(vals, q0, ql, nvl);
     }
     K kp = __shfl_up(k[kSortedRows - 1], 1, kWave);
     if (lane == 0) kp = last;
@@ -877,7 +913,7 @@ __global__ __launch_bounds__(kBlock) void sorted_having_scan_kernel(const K* __r
     const bool same = in && keys[row] == rk;
     const uint64_t ms = __ballot(same);
     const int stop = ~ms ? __builtin_ctzll(~ms) : kWave;   // first lane off the run
-    long long x = (HAS_V && lane < stop) ? (long long)vals[row] : 0LL;
+    long long x = (HAS_V && lane < stop) ? (long long)load_v1(vals, VB, row) : 0LL;
     c_v += wave_reduce_sum(x);
     r += stop;
     if (stop < kWave) break;
@@ -912,43 +948,51 @@ void sorted_having(const void* keys, bool key64, int64_t n, const AggDesc* descs
   p.hlo = hlo;
   p.hhi = hhi;
   p.hf = hf;
-  // streaming shape: COUNTs without NULLs plus at most one NULL-free int32 SUM
+  // streaming shape: COUNTs without NULLs plus at most one NULL-free SUM over
+  // int32 / int16 / int8 values (src64 codes 0 / 2 / 3; 2 and 3 only here)
   int vagg = -1;
   bool streaming = getenv("IGLOO_HAVING_SCAN") == nullptr || getenv("IGLOO_HAVING_SCAN")[0] != '0';
   for (int k = 0; k < nagg && streaming; ++k) {
     const AggDesc& d = descs[k];
     if (d.valid) streaming = false;
-    else if (d.op == AGG_SUM_INT && !d.src64 && d.src && vagg < 0) vagg = k;
+    else if (d.op == AGG_SUM_INT && d.src64 != 1 && d.src && vagg < 0) vagg = k;
     else if (d.op != AGG_COUNT) streaming = false;
   }
+  for (int k = 0; k < nagg; ++k)
+    if (descs[k].src64 > 1 && !(streaming && k == vagg))
+      throw std::runtime_error("sorted_having: int16 / int8 values need the streaming kernel");
   if (streaming) {
+    const int vb = vagg < 0 ? 0 : descs[vagg].src64 == 0 ? 4 : descs[vagg].src64 == 2 ? 2 : 1;
+    const void* fns[2][4] = {{(const void*)sorted_having_scan_kernel<int32_t, 0>,
+                              (const void*)sorted_having_scan_kernel<int32_t, 1>,
+                              (const void*)sorted_having_scan_kernel<int32_t, 2>,
+                              (const void*)sorted_having_scan_kernel<int32_t, 4>},
+                             {(const void*)sorted_having_scan_kernel<int64_t, 0>,
+                              (const void*)sorted_having_scan_kernel<int64_t, 1>,
+                              (const void*)sorted_having_scan_kernel<int64_t, 2>,
+                              (const void*)sorted_having_scan_kernel<int64_t, 4>}};
+    const int vi = vb == 0 ? 0 : vb == 1 ? 1 : vb == 2 ? 2 : 3;
+    const void* fn = fns[key64 ? 1 : 0][vi];
     // one resident round of waves (each owns one span): a second, partial
     // round would double the kernel's time
-    static int resident[4] = {0, 0, 0, 0};
-    const void* fns[4] = {(const void*)sorted_having_scan_kernel<int32_t, false>,
-                          (const void*)sorted_having_scan_kernel<int32_t, true>,
-                          (const void*)sorted_having_scan_kernel<int64_t, false>,
-                          (const void*)sorted_having_scan_kernel<int64_t, true>};
-    const int which = (key64 ? 2 : 0) + (vagg >= 0 ? 1 : 0);
-    if (!resident[which]) {
+    static int resident[2][4] = {};
+    int& res = resident[key64 ? 1 : 0][vi];
+    if (!res) {
       int dev = 0, cus = 0, per_cu = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[which], kBlock, 0);
-      resident[which] = std::max(1, cus * std::max(1, per_cu));
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0);
+      res = std::max(1, cus * std::max(1, per_cu));
     }
     const int64_t tiles = (n + kScanTile - 1) / kScanTile;
-    const int64_t blocks = std::min<int64_t>((tiles + kWavesPerBlock - 1) / kWavesPerBlock, resident[which]);
+    const int64_t blocks = std::min<int64_t>((tiles + kWavesPerBlock - 1) / kWavesPerBlock, res);
     const int64_t waves = blocks * kWavesPerBlock;
     const int64_t span = (tiles + waves - 1) / waves * kScanTile;
     const dim3 g((unsigned)((((n + span - 1) / span) + kWavesPerBlock - 1) / kWavesPerBlock)), b(kBlock);
-#define IGLOO_HAVING_SCAN(K, V) \
-  hipLaunchKernelGGL((sorted_having_scan_kernel<K, V>), g, b, 0, stream, (const K*)keys, n, span, p, vagg, rep, cap, counter)
-    if (key64 && vagg >= 0) IGLOO_HAVING_SCAN(int64_t, true);
-    else if (key64) IGLOO_HAVING_SCAN(int64_t, false);
-    else if (vagg >= 0) IGLOO_HAVING_SCAN(int32_t, true);
-    else IGLOO_HAVING_SCAN(int32_t, false);
-#undef IGLOO_HAVING_SCAN
+    int64_t nn = n, sp = span, cp = cap;
+    int va = vagg;
+    void* args[] = {(void*)&keys, &nn, &sp, &p, &va, &rep, &cp, &counter};
+    (void)hipLaunchKernel(fn, g, b, args, 0, stream);
     check_launch("sorted_having_scan", stream);
     return;
   }

@@ -280,9 +280,11 @@ void fmt_write(const void* vals, int kind, int64_t n, int scale, const uint8_t* 
 void str_parse(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* valid, int kind, int scale,
                void* out, int* err, hipStream_t stream);
 // LIKE made of '%'-separated literals (no '_'): segments concatenated in `seg`
-// with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%'
+// with offsets seg_off[nseg+1]; anchor_start/end = pattern does not begin/end with '%';
+// min_seg = the shortest segment's length (host-known: picks the kernel)
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
-                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, int64_t nbytes, hipStream_t stream);
+                       int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, int64_t nbytes,
+                       int min_seg, hipStream_t stream);
 void wide_fits(const int64_t* lo, const int64_t* hi, int64_t n, int* flag, hipStream_t stream);
 void avg_wide(const int64_t* sums, bool wide, const int64_t* cnt, int64_t n, int64_t up, int64_t* out,
               hipStream_t stream);

@@ -142,6 +142,63 @@ __device__ inline int next_hit(const uint64_t* bits, int from, int last) {
   }
 }
 
+// Greedy walk of one row [b0, b1) of a tile over the per-segment hit bitmaps:
+// the earliest hit of segment 0 at/after the cursor, then segment 1 after it, ...
+template <int SEGS, int WORDS>
+__device__ inline bool seg_walk(const uint64_t (&bits)[SEGS][WORDS], const int32_t* soff, int nseg, bool anchor_start,
+                                bool anchor_end, int b0, int b1) {
+  int cur = b0;
+  bool r = true;
+  for (int sg = 0; sg < nseg && r; ++sg) {
+    const int sl = soff[sg + 1] - soff[sg];
+    const bool last = sg == nseg - 1;
+    if (sg == 0 && anchor_start) {
+      r = cur + sl <= b1 && ((bits[0][cur >> 6] >> (cur & 63)) & 1ULL);
+      cur += sl;
+    } else if (last && anchor_end) {
+      const int p = b1 - sl;
+      r = p >= cur && ((bits[sg][p >> 6] >> (p & 63)) & 1ULL);
+      cur = b1;
+    } else {
+      const int p = next_hit(bits[sg], cur, b1 - sl);
+      r = p >= 0;
+      cur = p + sl;
+    }
+  }
+  if (r && anchor_end && (nseg == 0 || (nseg == 1 && anchor_start))) r = cur == b1;
+  return r;
+}
+
+// oversized tile: literal-by-literal search of one string in global memory
+__device__ inline bool seg_search(const uint8_t* s, int64_t L, const uint8_t* sseg, const int32_t* soff, int nseg,
+                                  bool anchor_start, bool anchor_end) {
+  int64_t cur = 0;
+  bool r = true;
+  for (int sg = 0; sg < nseg && r; ++sg) {
+    const int s0 = soff[sg], sl = soff[sg + 1] - s0;
+    const bool last = sg == nseg - 1;
+    auto eq = [&](int64_t p) {
+      for (int k = 0; k < sl; ++k)
+        if (s[p + k] != sseg[s0 + k]) return false;
+      return true;
+    };
+    if (sg == 0 && anchor_start) {
+      r = cur + sl <= L && eq(cur);
+      cur += sl;
+    } else if (last && anchor_end) {
+      r = L - sl >= cur && eq(L - sl);
+      cur = L;
+    } else {
+      int64_t p = cur;
+      while (p + sl <= L && !eq(p)) ++p;
+      r = p + sl <= L;
+      cur = p + sl;
+    }
+  }
+  if (r && anchor_end && (nseg == 0 || (nseg == 1 && anchor_start))) r = cur == L;
+  return r;
+}
+
 // BLOCK threads take BLOCK consecutive strings per tile of at most TILE bytes.
 // BLOCK = 64 makes every wave its own workgroup: the three tile barriers are
 // single-wave barriers, and a wave waiting on its tile's loads never holds up
@@ -217,57 +274,160 @@ __global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restri
     const int64_t i = i0 + threadIdx.x;
     if (i < i1) {
       const int64_t a = off[i], e = off[i + 1];
-      bool r;
-      if (staged) {
-        const int b0 = (int)((uintptr_t)(chars + a) - start), b1 = (int)((uintptr_t)(chars + e) - start);
-        int cur = b0;
-        r = true;
-        for (int sg = 0; sg < nseg && r; ++sg) {
-          const int sl = soff[sg + 1] - soff[sg];
-          const bool last = sg == nseg - 1;
-          if (sg == 0 && anchor_start) {
-            r = cur + sl <= b1 && ((bits[0][cur >> 6] >> (cur & 63)) & 1ULL);
-            cur += sl;
-          } else if (last && anchor_end) {
-            const int p = b1 - sl;
-            r = p >= cur && ((bits[sg][p >> 6] >> (p & 63)) & 1ULL);
-            cur = b1;
-          } else {
-            const int p = next_hit(bits[sg], cur, b1 - sl);
-            r = p >= 0;
-            cur = p + sl;
-          }
-        }
-        if (r && anchor_end && (nseg == 0 || (nseg == 1 && anchor_start))) r = cur == b1;
+      const bool r = staged ? seg_walk(bits, soff, nseg, anchor_start, anchor_end,
+                                       (int)((uintptr_t)(chars + a) - start), (int)((uintptr_t)(chars + e) - start))
+                            : seg_search(chars + a, e - a, sseg, soff, nseg, anchor_start, anchor_end);
+      out[i] = r != negate;
+    }
+  }
+}
+
+// Segments of >= 7 bytes ('%special%requests%', '%Customer%Complaints%'):
+// every occurrence at position p contains the aligned dword at a = p rounded
+// up to 4, and that dword equals the segment's bytes a-p .. a-p+3 (a-p < 4,
+// a-p+3 <= 6 < length). So the positions p of a 16-byte chunk can only hold a
+// hit if one of the chunk's 5 aligned dwords equals one of the segment's 4
+// leading dword windows: 16 plain compares per chunk and segment, no byte
+// windows -- the byte-exact test (v_alignbyte windows + verification) runs
+// only for the chunks that pass, gathered into a per-wave LDS list so the
+// wave runs them densely instead of idling lanes on a divergent branch.
+// Chunks come straight from global memory (16-byte loads, the fifth dword
+// from the same lines); LDS holds only the hit bitmaps and the lists.
+constexpr int kLikeDwordTile = 32768;
+
+template <int SEGS, int TILE, int kU>
+__global__ __launch_bounds__(kBlock) void like_dword_kernel(const int64_t* __restrict__ off,
+                                                           const uint8_t* __restrict__ chars, int64_t n,
+                                                           const uint8_t* __restrict__ seg, const int32_t* seg_off,
+                                                           int nseg, bool anchor_start, bool anchor_end, bool negate,
+                                                           uint8_t* __restrict__ out, int64_t nbytes) {
+  constexpr int kWords = TILE / 64;
+  constexpr int kChunks = TILE / 16;
+  constexpr int kListLen = kChunks / kWavesPerBlock + kWave;
+  __shared__ uint64_t bits[SEGS][kWords];
+  __shared__ uint16_t cand[kWavesPerBlock][kListLen];
+  __shared__ uint8_t sseg[kLikeMaxPattern];
+  __shared__ int32_t soff[SEGS + 1];
+  const int total = seg_off[nseg];
+  for (int i = threadIdx.x; i < total; i += kBlock) sseg[i] = seg[i];
+  if (threadIdx.x <= nseg) soff[threadIdx.x] = seg_off[threadIdx.x];
+  __syncthreads();
+  uint32_t P[SEGS][4];
+#pragma unroll
+  for (int sg = 0; sg < SEGS; ++sg)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int s0 = soff[sg < nseg ? sg : 0] + o;
+      // wave-uniform: kept in scalar registers (compares take an SGPR operand)
+      P[sg][o] = __builtin_amdgcn_readfirstlane((uint32_t)sseg[s0] | ((uint32_t)sseg[s0 + 1] << 8) |
+                                                ((uint32_t)sseg[s0 + 2] << 16) | ((uint32_t)sseg[s0 + 3] << 24));
+    }
+  const int wave = threadIdx.x / kWave, lane = lane_id();
+  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  const uint8_t* const chars_end = chars + nbytes;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t i0 = t * kBlock;
+    const int64_t i1 = i0 + kBlock < n ? i0 + kBlock : n;
+    const int64_t i = i0 + threadIdx.x;
+    // this row's bounds now: their loads overlap the tile's matching
+    const int64_t ra = i < i1 ? off[i] : 0, re = i < i1 ? off[i + 1] : 0;
+    const uintptr_t lo = (uintptr_t)(chars + off[i0]);
+    const uintptr_t hi = (uintptr_t)(chars + off[i1]);
+    const uintptr_t start = lo & ~(uintptr_t)15;   // never below the allocation (>= 256 B aligned)
+    const int len = (int)(hi - start);
+    const bool fits = hi - start <= (uintptr_t)TILE;
+    const uint8_t* base = (const uint8_t*)start;
+    // 20 bytes from chunk j (16 B and the next dword). Bytes past the tile
+    // are the next rows' (positions that would need them are masked by
+    // `room`); only the buffer's last bytes are read one by one.
+    const int64_t avail = chars_end - base;
+    auto load = [&](int j, uint32_t d[5]) {
+      const int b = j * 16;
+      if (b + 20 <= avail) {
+        const uint4 v = *(const uint4*)(base + b);
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        d[4] = *(const uint32_t*)(base + b + 16);
       } else {
-        // oversized tile: literal-by-literal search in global memory
-        const uint8_t* s = chars + a;
-        const int64_t L = e - a;
-        int64_t cur = 0;
-        r = true;
-        for (int sg = 0; sg < nseg && r; ++sg) {
-          const int s0 = soff[sg], sl = soff[sg + 1] - s0;
-          const bool last = sg == nseg - 1;
-          auto eq = [&](int64_t p) {
-            for (int k = 0; k < sl; ++k)
-              if (s[p + k] != sseg[s0 + k]) return false;
-            return true;
-          };
-          if (sg == 0 && anchor_start) {
-            r = cur + sl <= L && eq(cur);
-            cur += sl;
-          } else if (last && anchor_end) {
-            r = L - sl >= cur && eq(L - sl);
-            cur = L;
-          } else {
-            int64_t p = cur;
-            while (p + sl <= L && !eq(p)) ++p;
-            r = p + sl <= L;
-            cur = p + sl;
-          }
+#pragma unroll
+        for (int w = 0; w < 5; ++w) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (b + 4 * w + k < avail) x |= (uint32_t)base[b + 4 * w + k] << (8 * k);
+          d[w] = x;
         }
-        if (r && anchor_end && (nseg == 0 || (nseg == 1 && anchor_start))) r = cur == L;
       }
+    };
+    __syncthreads();   // the previous tile's walk is done with the bitmaps
+    if (fits) {
+      const int nchunks = (len + 15) >> 4;
+      int ncand = 0;
+      // kU chunks per lane in flight: all loads issued before any compare
+      for (int j0 = wave * kWave; j0 < nchunks; j0 += kU * kBlock) {
+        uint32_t d[kU][5];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int j = j0 + u * kBlock + lane;
+          if (j < nchunks) load(j, d[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int j = j0 + u * kBlock + lane;
+          if (j0 + u * kBlock >= nchunks) break;   // wave-uniform
+          bool any = false;
+          if (j < nchunks) {
+#pragma unroll
+            for (int sg = 0; sg < SEGS; ++sg) {
+              if (sg >= nseg) break;
+              bool f = d[u][0] == P[sg][0];
+#pragma unroll
+              for (int w = 1; w < 4; ++w)
+                f |= (d[u][w] == P[sg][0]) | (d[u][w] == P[sg][1]) | (d[u][w] == P[sg][2]) | (d[u][w] == P[sg][3]);
+              f |= (d[u][4] == P[sg][1]) | (d[u][4] == P[sg][2]) | (d[u][4] == P[sg][3]);
+              any |= f;
+              ((uint16_t*)bits[sg])[j] = 0;
+            }
+          }
+          const uint64_t bal = __ballot(any);
+          if (any) cand[wave][ncand + lane_prefix(bal)] = (uint16_t)j;
+          ncand += __popcll(bal);
+        }
+      }
+      // byte-exact masks for the listed chunks (same wave: ordered after the zeroing)
+      for (int c = lane; c < ncand; c += kWave) {
+        const int j = cand[wave][c];
+        uint32_t d[5];
+        load(j, d);
+        const int b = j * 16;
+#pragma unroll
+        for (int sg = 0; sg < SEGS; ++sg) {
+          if (sg >= nseg) break;
+          const int s0 = soff[sg], sl = soff[sg + 1] - s0;
+          uint32_t m = 0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3);
+            m |= (uint32_t)(w == P[sg][0]) << q;
+          }
+          const int room = len - sl - b + 1;
+          m &= room >= 16 ? 0xffffu : room <= 0 ? 0u : ((1u << room) - 1);
+          for (uint32_t c2 = m; c2; c2 &= c2 - 1) {
+            const int q = __builtin_ctz(c2);
+            for (int k = 4; k < sl; ++k)
+              if (base[b + q + k] != sseg[s0 + k]) {
+                m &= ~(1u << q);
+                break;
+              }
+          }
+          ((uint16_t*)bits[sg])[j] = (uint16_t)m;
+        }
+      }
+    }
+    __syncthreads();
+    if (i < i1) {
+      const bool r = fits ? seg_walk(bits, soff, nseg, anchor_start, anchor_end,
+                                     (int)((uintptr_t)(chars + ra) - start), (int)((uintptr_t)(chars + re) - start))
+                          : seg_search(chars + ra, re - ra, sseg, soff, nseg, anchor_start, anchor_end);
       out[i] = r != negate;
     }
   }
@@ -430,9 +590,30 @@ void str_like(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t
 
 void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* seg, const int32_t* seg_off,
                        int nseg, bool anchor_start, bool anchor_end, bool negate, uint8_t* out, int64_t nbytes,
-                       hipStream_t stream) {
+                       int min_seg, hipStream_t stream) {
   if (n == 0) return;
   if (nseg > kSegMax) throw std::runtime_error("str_like_segments: too many segments");
+  const bool dword_filter = getenv("IGLOO_LIKE_DWORD") == nullptr || getenv("IGLOO_LIKE_DWORD")[0] != '0';
+  if (dword_filter && nseg >= 1 && nseg <= 2 && min_seg >= 7) {
+    const dim3 g(grid_for(n, kBlock, 256 * 8 * 4)), b(kBlock);
+    const char* ue = getenv("IGLOO_LIKE_UNROLL");
+    const int u = ue ? atoi(ue) : 1;
+#define IGLOO_LIKE_DWORD(S, U)                                                                                  \
+  hipLaunchKernelGGL((like_dword_kernel<S, kLikeDwordTile, U>), g, b, 0, stream, off, chars, n, seg, seg_off, nseg, \
+                     anchor_start, anchor_end, negate, out, nbytes)
+    if (nseg == 1) {
+      if (u >= 4) IGLOO_LIKE_DWORD(1, 4);
+      else if (u == 2) IGLOO_LIKE_DWORD(1, 2);
+      else IGLOO_LIKE_DWORD(1, 1);
+    } else {
+      if (u >= 4) IGLOO_LIKE_DWORD(2, 4);
+      else if (u == 2) IGLOO_LIKE_DWORD(2, 2);
+      else IGLOO_LIKE_DWORD(2, 1);
+    }
+#undef IGLOO_LIKE_DWORD
+    check_launch("str_like_segments", stream);
+    return;
+  }
   // (a one-wave-per-workgroup variant with 4 / 8 KB tiles measured slower for
   // Q13 at SF100, 14.6 vs 11.7 ms per query: profiles/r3_ab_like_wave.txt)
   // one or two segments (nearly every analytic LIKE): a bitmap sized for

@@ -44,6 +44,8 @@ EAGER_COUNT_MASKED = os.environ.get("IGLOO_EAGER_COUNT_MASKED", "1") != "0"
 #: HashAggExec._sorted_having: fused sorted GROUP BY + HAVING (IGLOO_SORTED_HAVING=0 turns it off)
 SORTED_HAVING = os.environ.get("IGLOO_SORTED_HAVING", "1") != "0"
 SORTED_HAVING_MIN_ROWS = 1 << 16
+#: the streaming sorted-HAVING kernel (csrc/kernels/agg.hip sorted_having_scan_kernel; the C++ side reads it too)
+HAVING_SCAN = os.environ.get("IGLOO_HAVING_SCAN", "1") != "0"
 #: HashAggExec: a runtime key filter over a filtered resident scan takes the key index first
 INDEX_THEN_FILTER = os.environ.get("IGLOO_INDEX_THEN_FILTER", "1") == "1"
 
@@ -134,8 +136,15 @@ class HashAggExec(ExecNode):
         const = having_constant(op, lit, src, a.func, hop_spec in ("sum_f64", "min_f64", "max_f64"))
         if const is None:
             return self._finish_general(b, ctx)
+        specs = [sp[:3] for sp in specs]
+        if HAVING_SCAN and all(sp[2] is None and sp[0] in ("count", "sum_int") for sp in specs) \
+                and sum(sp[0] == "sum_int" for sp in specs) <= 1:
+            # the streaming kernel reads the summed column at its narrow width
+            # (Q18's l_quantity as int16: 1.2 GB instead of 4.8 GB at SF100)
+            from .fused import narrow
+            specs = [(o, narrow(v) if o == "sum_int" else v, vv) for o, v, vv in specs]
         with ctx.span("agg.sorted_having"):
-            got = A.sorted_having(kcol.data, [sp[:3] for sp in specs], hidx, op, const)
+            got = A.sorted_having(kcol.data, specs, hidx, op, const)
         if got is None:
             return self._finish_general(b, ctx)
         rep, results = got

@@ -261,7 +261,9 @@ def sorted_having(keys: torch.Tensor, specs: Sequence[Spec], hidx: int, hop: str
         if vals is not None:
             assert vals.numel() == n and vals.is_contiguous()
             if op in ("sum_int", "min_int", "max_int"):
-                src64 = 1 if vals.dtype == torch.int64 else 0
+                # int16 / int8 (codes 2 / 3): a NULL-free SUM for the streaming kernel only
+                src64 = {torch.int64: 1, torch.int32: 0, torch.int16: 2, torch.int8: 3}[vals.dtype]
+                assert src64 < 2 or (op == "sum_int" and valid is None), "narrow values: NULL-free SUM only"
         descs.append((OPS[op], src64, ptr(vals), ptr(valid), ptr(dst), ptr(dst2)))
         posts.append((op, dst, dst2))
     c = int(hconst) if not isinstance(hconst, float) else 0

@@ -184,6 +184,7 @@ def like(col: Column, pattern: str, ci: bool = False, negate: bool = False, esca
         out = torch.empty(n, dtype=torch.bool, device=dev)
         launch("str_like_segments").str_like_segments(ptr(col.offsets), ptr(col.data), n, ptr(sb), ptr(so),
                                                       len(seg_off) - 1, a0, a1, negate, ptr(out), col.data.numel(),
+                                                      min((b - a for a, b in zip(seg_off, seg_off[1:])), default=0),
                                                       stream(out))
         return out
     pt, kt = _consts(("pat", pattern, escape, dev), lambda: (

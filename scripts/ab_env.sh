@@ -1,17 +1,16 @@
 #!/bin/bash
-# Same-box A/B of one or more switches (off = the OFF environment, on = the
-# defaults). Box-to-box spread is several percent, so only same-box pairs are
-# compared. Default command: the HBM SF100 suite with graphs.
-#   OFF="IGLOO_DENSE_JOIN=0" bash scripts/ab_env.sh
-#   OFF="IGLOO_MORSEL_PREFETCH=0" CMD="python -u scripts/budget_check.py --sf 10 --cap-gb 1 --budget-gb 0.25 --ref gpu" \
-#     bash scripts/ab_env.sh
+# A/B of an on/off environment switch on the warm graphed SF100 suite, tables
+# in HBM, same box back to back (VALS, default 1 0 1 0):
+#   VAR=IGLOO_LIKE_DWORD QS=13 bash scripts/ab_env.sh -> gpurun_out/ab_$VAR.txt
+# (IGLOO_COMPACT, IGLOO_LIKE_DWORD, IGLOO_HAVING_SCAN, ... default on).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out
-CMD="${CMD:-python -u bench.py --source hbm --steps 10 --warmup 3 --eager-steps 0 --vary-params 0 --per-query}"
-for mode in off on; do
-  if [ $mode = off ]; then e="$OFF"; else e=""; fi
-  env $e timeout -k 10 500 $CMD > gpurun_out/ab_env_$mode.log 2>&1
-  rc=$?; echo "$mode ($e) rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  tail -1 gpurun_out/ab_env_$mode.log | cut -c1-120
-  grep "\] Q[0-9]\|^Q[0-9]*:" gpurun_out/ab_env_$mode.log | awk '{printf "%s=%s ", $1 == "[bench]" ? $2 : $1, $1 == "[bench]" ? $3 : $3}'; echo
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
+VAR=${VAR:?set VAR}
+OUT=gpurun_out/ab_$VAR.txt
+: > $OUT
+for v in ${VALS:-1 0 1 0}; do
+  env $VAR=$v timeout -k 10 400 python3 bench.py --source hbm --sf ${SF:-100} --queries ${QS:-1-22} --steps ${STEPS:-10} \
+    --warmup 3 --eager-steps 0 --vary-params 0 > gpurun_out/ab_${VAR}_$v.log 2>&1 || exit $?
+  echo "$VAR=$v $(tail -1 gpurun_out/ab_${VAR}_$v.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> $OUT
 done
+cat $OUT

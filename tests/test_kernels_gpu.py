@@ -572,6 +572,37 @@ def test_like_tile_shapes(gpu_device, words):
         assert torch.equal(S.like(c, pat, negate=True), S.like(g, pat, negate=True).cpu()), pat
 
 
+def test_like_dword_filter_every_alignment(gpu_device, monkeypatch):
+    """strings.hip like_dword_kernel (segments of >= 7 bytes: the aligned-dword
+    prefilter) against the CPU matcher and the byte-window kernel it replaces:
+    planted segments at every offset mod 16, near-misses sharing 4-byte
+    windows, overlapping repeats, hits at string ends and in oversized tiles."""
+    from igloo_amd.ops._lib import KERNEL_CALLS
+    r = _rng(33)
+    pieces = ["special", "requests", "specia", "pecial", "requestsrequests", "spespecial", "reques", "quests",
+              "Customer", "Complaints", "x", "yy", "zzz", "ünï"]
+    vals = []
+    for i in range(40_000):
+        pad = "." * int(r.integers(0, 16))
+        body = "".join(r.choice(pieces, int(r.integers(0, 6))))
+        vals.append(pad + body + ("." * int(r.integers(0, 3))))
+    vals += ["special requests " * 200]          # one oversized tile
+    c = _str_col(vals)
+    g = c.to(DEV)
+    for pat in ("%special%requests%", "%Customer%Complaints%", "%requests", "special%", "%pecial%", "special",
+                "%requestsrequests%", "%special%special%"):
+        ref = S.like(c, pat)
+        before = KERNEL_CALLS["str_like_segments"]
+        monkeypatch.setenv("IGLOO_LIKE_DWORD", "1")
+        got = S.like(g, pat).cpu()
+        monkeypatch.setenv("IGLOO_LIKE_DWORD", "0")
+        old = S.like(g, pat).cpu()
+        assert KERNEL_CALLS["str_like_segments"] == before + 2
+        assert torch.equal(ref, got), pat
+        assert torch.equal(ref, old), pat
+        assert int(ref.sum()) > 0, pat
+
+
 @pytest.mark.parametrize("ncols", [2, 3, 8])
 def test_pack_keys_native(gpu_device, ncols):
     """csrc/kernels/util.hip pack_bits vs the plain int64 shift/OR formula."""
