@@ -296,7 +296,7 @@ __global__ __launch_bounds__(BLOCK) void like_seg_kernel(const int64_t* __restri
 constexpr int kLikeDwordTile = 32768;
 
 template <int SEGS, int TILE, int kU>
-__global__ __launch_bounds__(kBlock) void like_dword_kernel(const int64_t* __restrict__ off,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void like_dword_kernel(const int64_t* __restrict__ off,
                                                            const uint8_t* __restrict__ chars, int64_t n,
                                                            const uint8_t* __restrict__ seg, const int32_t* seg_off,
                                                            int nseg, bool anchor_start, bool anchor_end, bool negate,
@@ -306,6 +306,8 @@ __global__ __launch_bounds__(kBlock) void like_dword_kernel(const int64_t* __res
   constexpr int kListLen = kChunks / kWavesPerBlock + kWave;
   __shared__ uint64_t bits[SEGS][kWords];
   __shared__ uint16_t cand[kWavesPerBlock][kListLen];
+  constexpr int kDataCap = 64;   // listed chunks whose bytes are kept in LDS (later ones are reloaded)
+  __shared__ uint32_t cdat[kWavesPerBlock][5][kDataCap];
   __shared__ uint8_t sseg[kLikeMaxPattern];
   __shared__ int32_t soff[SEGS + 1];
   const int total = seg_off[nseg];
@@ -325,14 +327,29 @@ __global__ __launch_bounds__(kBlock) void like_dword_kernel(const int64_t* __res
   const int wave = threadIdx.x / kWave, lane = lane_id();
   const int64_t tiles = (n + kBlock - 1) / kBlock;
   const uint8_t* const chars_end = chars + nbytes;
+  // the tile's byte range is known one tile ahead (no offsets -> chars load chain)
+  int64_t t_lo = 0, t_hi = 0;
+  if ((int64_t)blockIdx.x < tiles) {
+    const int64_t f0 = (int64_t)blockIdx.x * kBlock;
+    t_lo = off[f0];
+    t_hi = off[f0 + kBlock < n ? f0 + kBlock : n];
+  }
   for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
     const int64_t i0 = t * kBlock;
     const int64_t i1 = i0 + kBlock < n ? i0 + kBlock : n;
     const int64_t i = i0 + threadIdx.x;
     // this row's bounds now: their loads overlap the tile's matching
     const int64_t ra = i < i1 ? off[i] : 0, re = i < i1 ? off[i + 1] : 0;
-    const uintptr_t lo = (uintptr_t)(chars + off[i0]);
-    const uintptr_t hi = (uintptr_t)(chars + off[i1]);
+    const uintptr_t lo = (uintptr_t)(chars + t_lo);
+    const uintptr_t hi = (uintptr_t)(chars + t_hi);
+    {
+      const int64_t tn = t + gridDim.x;
+      if (tn < tiles) {
+        const int64_t f0 = tn * kBlock;
+        t_lo = off[f0];
+        t_hi = off[f0 + kBlock < n ? f0 + kBlock : n];
+      }
+    }
     const uintptr_t start = lo & ~(uintptr_t)15;   // never below the allocation (>= 256 B aligned)
     const int len = (int)(hi - start);
     const bool fits = hi - start <= (uintptr_t)TILE;
@@ -389,7 +406,13 @@ __global__ __launch_bounds__(kBlock) void like_dword_kernel(const int64_t* __res
             }
           }
           const uint64_t bal = __ballot(any);
-          if (any) cand[wave][ncand + lane_prefix(bal)] = (uint16_t)j;
+          if (any) {
+            const int c = ncand + lane_prefix(bal);
+            cand[wave][c] = (uint16_t)j;
+            if (c < kDataCap)
+#pragma unroll
+              for (int w = 0; w < 5; ++w) cdat[wave][w][c] = d[u][w];
+          }
           ncand += __popcll(bal);
         }
       }
@@ -397,7 +420,12 @@ __global__ __launch_bounds__(kBlock) void like_dword_kernel(const int64_t* __res
       for (int c = lane; c < ncand; c += kWave) {
         const int j = cand[wave][c];
         uint32_t d[5];
-        load(j, d);
+        if (c < kDataCap) {
+#pragma unroll
+          for (int w = 0; w < 5; ++w) d[w] = cdat[wave][w][c];
+        } else {
+          load(j, d);
+        }
         const int b = j * 16;
 #pragma unroll
         for (int sg = 0; sg < SEGS; ++sg) {
