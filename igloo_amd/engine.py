@@ -20,7 +20,7 @@ import torch
 from . import types as T
 from .catalog import Catalog, Field, MemoryTable, TableSource
 from .columnar import Batch, Column
-from .exec.operators import ExecContext
+from .exec.context import ExecContext
 from .exec.planner import create_physical_plan
 from .sql import parse
 from .sql.binder import Binder, IdGen

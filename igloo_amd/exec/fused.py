@@ -444,7 +444,7 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
     """GROUP BY (domain <= 16) over a scanned batch with the scan filter and the
     argument arithmetic fused into one kernel, or None if the shape does not fit."""
     from ..ops._lib import launch, stream
-    from .operators import _avg
+    from .aggregate import _avg
     dev = ctx.device
     if dev.type != "cuda" or b.num_rows == 0:
         return None

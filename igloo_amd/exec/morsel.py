@@ -25,7 +25,7 @@ distributes over a union of row sets: filters, projections, inner joins (either
 side), the preserved side of left joins, the probe side of semi / anti joins,
 and inner multi-way joins. Anything else (a scan under another aggregate, a
 sort, a limit, the build side of an outer / semi join) runs whole, where the
-grace join (operators.py ``grace_join``) bounds its joins.
+grace join (joins.py ``grace_join``) bounds its joins.
 
 ``external_sort`` is the ORDER BY counterpart: an input over the budget is
 range-partitioned on its leading sort key by sampled splitters, the partitions
@@ -66,7 +66,8 @@ def _contains(node, target) -> bool:
 def stream_path_ok(node, target) -> bool:
     """Every operator on the path from ``node`` down to scan ``target``
     distributes over a union of the scan's rows (see the module docstring)."""
-    from .operators import FilterExec, HashJoinExec, MultiJoinExec, ProjectExec
+    from .scan import FilterExec, ProjectExec
+    from .joins import HashJoinExec, MultiJoinExec
     if node is target:
         return True
     if isinstance(node, (FilterExec, ProjectExec)):
@@ -113,7 +114,7 @@ def scan_bytes(scan) -> int:
 def pick_stream_scan(agg, ctx):
     """The largest streamable scan below aggregate ``agg`` whose columns exceed
     budget / STREAM_FRACTION, or None."""
-    from .operators import ScanExec
+    from .scan import ScanExec
     best, best_bytes = None, ctx.budget // STREAM_FRACTION
     for n in _walk(agg.children[0]):
         if not isinstance(n, ScanExec) or not getattr(n.logical.source, "can_stream", False):
@@ -199,7 +200,9 @@ def streamed_aggregate(agg, ctx) -> Optional[Batch]:
     """Run aggregate node ``agg`` as a morsel pipeline when the budget calls
     for it; None when it does not (or the aggregates do not decompose)."""
     from ..parallel.exchange import _TmpIds, decomposable, partial_plan
-    from .operators import ScanExec, aggregate, apply_key_filters
+    from .scan import ScanExec
+    from .aggregate import aggregate
+    from .joins import apply_key_filters
     lg = agg.logical
     if ctx.budget is None or not decomposable(lg.aggs):
         return None
@@ -300,7 +303,9 @@ def _spmd_streamed_aggregate(agg, scan, ctx) -> Optional[Batch]:
     into partial states (compacted under the budget like the single-rank
     pipeline), and ``distributed_aggregate`` exchanges and merges them."""
     from ..parallel.exchange import distributed_aggregate
-    from .operators import ScanExec, aggregate, apply_key_filters
+    from .scan import ScanExec
+    from .aggregate import aggregate
+    from .joins import apply_key_filters
     lg = agg.logical
     from .joins import MultiJoinExec
     if any(isinstance(n, MultiJoinExec) for n in _walk(agg.children[0])):
@@ -365,7 +370,7 @@ def _empty_partials(groups, partial, ctx) -> Batch:
 
 
 def _any_stream_scan(agg):
-    from .operators import ScanExec
+    from .scan import ScanExec
     best, best_bytes = None, -1
     for n in _walk(agg.children[0]):
         if isinstance(n, ScanExec) and getattr(n.logical.source, "can_stream", False) \
@@ -399,7 +404,7 @@ class _PartialStates:
         self.seen = 0
 
     def add(self, pb: Batch) -> None:
-        from .operators import _batch_bytes, concat_batches
+        from .joins import _batch_bytes, concat_batches
         self.seen += 1
         if self.spill is not None:
             self._distribute(pb)
@@ -431,7 +436,7 @@ class _PartialStates:
         """Re-aggregate partial states into one partial row per group (same column ids)."""
         from ..parallel.exchange import _join_wide_finals, _split_wide_partials, _wide_finals
         from ..sql.expr import AggCall
-        from .operators import aggregate
+        from .aggregate import aggregate
         fgroups = [(ci, ci.ref()) for ci, _ in self.groups]
         rb, wide = _split_wide_partials(rb, self.plan, self.ids)
         merge = {"sum": "sum", "count": "sum", "min": "min", "max": "max", "bool_and": "bool_and",
@@ -444,7 +449,7 @@ class _PartialStates:
         from ..ops import misc as M
         from ..parallel.exchange import partition_keys
         from ..ops.gather import take_many
-        from .operators import _batch_bytes, _to_host
+        from .joins import _batch_bytes, _to_host
         P = len(self.spill)
         key = None
         for ci, _ in self.groups:
@@ -466,7 +471,7 @@ class _PartialStates:
     def partials(self) -> Optional[Batch]:
         """The partial states compacted to one row per group (not finalised:
         an SPMD exchange merges them across ranks)."""
-        from .operators import _to_device, _to_host, concat_batches
+        from .joins import _to_device, _to_host, concat_batches
         if self.spill is None:
             if not self.parts:
                 return None
@@ -485,7 +490,7 @@ class _PartialStates:
 
     def finish(self) -> Optional[Batch]:
         from ..parallel.exchange import merge_partials
-        from .operators import _to_device, _to_host, concat_batches
+        from .joins import _to_device, _to_host, concat_batches
         if self.spill is None:
             if not self.parts:
                 return None
@@ -509,7 +514,7 @@ def streamed_scan(scan, ctx) -> Optional[Batch]:
     morsel is filtered and projected on its own and only the surviving rows
     are kept (concatenated at the end), so the device never holds the
     unfiltered columns. None when the scan fits (or cannot stream)."""
-    from .operators import concat_batches
+    from .joins import concat_batches
     src = scan.logical.source
     if not getattr(src, "can_stream", False):
         return None
@@ -546,7 +551,7 @@ def streamed_scan(scan, ctx) -> Optional[Batch]:
 def big_streamable(node, ctx) -> bool:
     """``node``'s output derives from a scan too big for the budget that
     could stream (an aggregate over ``node`` would run as a morsel pipeline)."""
-    from .operators import ScanExec
+    from .scan import ScanExec
     lim = ctx.budget // STREAM_FRACTION
     return any(isinstance(n, ScanExec) and getattr(n.logical.source, "can_stream", False) and scan_bytes(n) > lim
                and stream_path_ok(node, n) for n in _walk(node))
@@ -569,7 +574,7 @@ def semi_aggregate(kind, on, residual, null_aware, left_cids, right_plan, right_
     from ..parallel.exchange import _TmpIds
     from ..sql import logical as L
     from ..sql.expr import AggCall, BinOp, ColRef
-    from .operators import HashAggExec
+    from .aggregate import HashAggExec
     if ctx.budget is None or ctx.spmd or kind not in ("semi", "anti") or not on or null_aware:
         return None
     hit = ctx.semi_builds.get(key)
@@ -612,7 +617,7 @@ def apply_semi_aggregate(lb: Batch, ab: Batch, spec, ctx) -> Batch:
     build side of ``semi_aggregate``."""
     from ..ops import hashing as H
     from ..ops.select import mask_to_indices
-    from .operators import _take_batch, key_tensors
+    from .joins import _take_batch, key_tensors
     ev = ctx.evaluator
     with ctx.span("join.aggregated_semi"):
         if ab.num_rows == 0 or lb.num_rows == 0:
@@ -698,7 +703,8 @@ def external_sort(b: Batch, keys, fetch, ctx) -> Optional[Batch]:
     partitions on the leading key (sampled splitters), staged in host memory,
     each sorted on the device; None when the input fits (or the leading key
     is not a plain fixed-width column)."""
-    from .operators import _batch_bytes, _take_batch, _to_device, _to_host, concat_batches, sort_batch
+    from .joins import _batch_bytes, _take_batch, _to_device, _to_host, concat_batches
+    from .sorting import sort_batch
     if ctx.budget is None or fetch is not None or b.num_rows < 2:
         return None
     need = SORT_MEM_FACTOR * _batch_bytes(b)

@@ -11,8 +11,11 @@ from ..columnar import Batch
 from ..sql import logical as L
 from ..sql.expr import col_refs, has_subquery
 from ..utils.errors import NotSupported
-from .operators import (ExecContext, ExecNode, FilterExec, FragmentInputExec, HashAggExec, HashJoinExec, LimitExec,
-                        MultiJoinExec, ProjectExec, ScanExec, SortExec, UnionExec, ValuesExec)
+from .context import ExecContext, ExecNode
+from .scan import FilterExec, FragmentInputExec, ProjectExec, ScanExec, ValuesExec
+from .aggregate import HashAggExec
+from .joins import HashJoinExec, MultiJoinExec
+from .sorting import LimitExec, SortExec, UnionExec
 
 
 def _require(child: ExecNode, exprs) -> None:

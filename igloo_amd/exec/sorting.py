@@ -1,6 +1,6 @@
 """Sort / top-k, limit and union operators.
 
-Split out of exec/operators.py, which re-exports every name."""
+One of the five operator modules (context, scan, joins, aggregate, sorting)."""
 from __future__ import annotations
 
 import math

@@ -396,7 +396,7 @@ def is_sorted(keys: torch.Tensor) -> bool:
     base = getattr(keys, "_igloo_base", None)
     if base is not None and base[0].data.dtype == keys.dtype and is_sorted(base[0].data):
         # a filtered scan's rows of a sorted source column, in row order
-        # (exec/operators.py _tag_base): sorted without another pass (the
+        # (exec/scan.py _tag_base): sorted without another pass (the
         # source's flag is computed once and remembered on it)
         return True
     n = keys.numel()

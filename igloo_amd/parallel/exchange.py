@@ -54,7 +54,7 @@ def dist_of(b: Batch):
 
 def materialized(b: Batch) -> Batch:
     """A plain Batch for an exchange: late-materialised join results and lazy
-    filtered scans (exec/operators.py LateBatch / _LazyScanBatch) gather their
+    filtered scans (exec/joins.py LateBatch, exec/scan.py _LazyScanBatch) gather their
     columns first."""
     if hasattr(b, "materialize"):
         return b.materialize()
@@ -714,7 +714,7 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
     """Move rows so the join can run rank-locally; returns (lb, rb) with the
     output distribution stored in ``lb.out_dist``. ``rows``: the inputs'
     global row counts when the caller already reduced them."""
-    from ..exec.operators import _pair_key
+    from ..exec.joins import _pair_key
     comm = ctx.comm
     kind, on = join.kind, join.on
     ld, rd = dist_of(lb), dist_of(rb)
@@ -806,7 +806,7 @@ def semi_by_key_set(lb: Batch, rb: Batch, join: L.Join, ctx) -> Optional[Batch]:
     the global answer; each rank then filters its replicated left rows
     locally and the result stays replicated. One collective of n_left bytes,
     no key-range exchange, no shuffle. None when the shape does not apply."""
-    from ..exec.operators import _pair_key
+    from ..exec.joins import _pair_key
     from ..ops import hashing as H
     from ..ops.select import mask_to_indices
     comm = ctx.comm
@@ -923,7 +923,7 @@ DECOMPOSABLE = {"sum", "count", "min", "max", "avg", "bool_and", "bool_or"}
 def distributed_aggregate(lg: L.Aggregate, b: Batch, ctx, local=None) -> Batch:
     """``local(groups, partial_aggs) -> Batch | None`` may compute the phase-1
     partial states directly from the scan (fused VM kernel)."""
-    from ..exec.operators import aggregate
+    from ..exec.aggregate import aggregate
     groups, aggs = lg.groups, lg.aggs
     d = dist_of(b)
     if d == REPLICATED:
@@ -1034,14 +1034,15 @@ def _partial_by_rows(groups, partial, b: Batch, ids, ctx):
     c_address, c_phone, c_comment of the replicated customer table, grouped
     with c_custkey over orders x lineitem partitioned by order key). The
     local grouping runs by the leading integer key with the others checked
-    to be functionally dependent on it (exec/operators.py _late_group_keys);
+    to be functionally dependent on it (exec/aggregate.py _late_group_keys);
     each group then carries its row in the replicated input -- the same row
     number on every rank -- and the strings are taken from that input after
     the merge, on the owning rank only (~4M groups x ~130 string bytes at
     SF100 no longer cross the fabric). Every rank must take the same shape,
     so the dependency check's outcome is agreed by one tiny all-gather.
     Returns (partial batch, exchange group keys, restore(merged) or None)."""
-    from ..exec.operators import LateBatch, aggregate
+    from ..exec.joins import LateBatch
+    from ..exec.aggregate import aggregate
     rows = {}
     if isinstance(b, LateBatch) and len(groups) > 1 and b.num_rows >= 0:
         for i, (ci, e) in enumerate(groups):
@@ -1197,7 +1198,7 @@ def partial_plan(aggs, ids):
 def merge_partials(groups, plan, rb: Batch, ids, ctx, fd: bool = False) -> Batch:
     """Phase 2: merge the partial states in ``rb`` (rows = partial groups) into
     the final aggregates of ``plan`` (see ``partial_plan``)."""
-    from ..exec.operators import _avg, aggregate
+    from ..exec.aggregate import _avg, aggregate
     fgroups = [(ci, ColRef(ci.cid, ci.name, ci.dtype, ci.nullable)) for ci, _ in groups]
     # 128-bit partial sums (wide decimals: SF100 charges) merge as three
     # int64 sums — high word, and the low word's two 32-bit halves — that
@@ -1239,7 +1240,7 @@ def finalize_unique(groups, plan, rb: Batch) -> Batch:
     """``merge_partials`` for partial states already merged to one row per
     group (the dense all-reduce): the final columns come straight from the
     states -- no second grouping pass."""
-    from ..exec.operators import _avg
+    from ..exec.aggregate import _avg
     out = {ci.cid: rb.columns[ci.cid] for ci, _ in groups}
     for func, ci, a, p1, p2 in plan:
         if func == "avg":

@@ -24,7 +24,7 @@ supplier) lineitem sums). Inner joins with a partitioned table keep the
 replicated side whole (they are rank-local that way).
 
 The same range mapping places the output of the partitioned dense aggregates
-reduced with RCCL reduce-scatter (exec/operators.py eager COUNT, Q13): each
+reduced with RCCL reduce-scatter (exec/aggregate.py eager COUNT, Q13): each
 rank receives the counts of one contiguous key chunk.
 
 Reference parity: the reference places one whole table per worker

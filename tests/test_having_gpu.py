@@ -1,5 +1,5 @@
 """Fused sorted GROUP BY + HAVING (csrc/kernels/agg.hip sorted_having,
-exec/operators.py HashAggExec._sorted_having) against the CPU engine: sums,
+exec/aggregate.py HashAggExec._sorted_having) against the CPU engine: sums,
 counts, min/max over int, decimal and float columns, every comparison, the
 literal on either side, NULL values, and runs longer than the kernel follows
 (the overflow flag sends the query to the general path). The streaming

@@ -146,7 +146,7 @@ INDEX_QUERIES = [
 @pytest.mark.parametrize("qi", range(len(INDEX_QUERIES)))
 def test_index_paths_default_thresholds(gpu_device, qi, monkeypatch):
     """Mid-size secondary-index joins, index-range runtime key filters and
-    semi joins (exec/operators.py inner_pairs, _index_key_filter) with the
+    semi joins (exec/joins.py inner_pairs, _index_key_filter) with the
     default thresholds, against the CPU engine."""
     big, small = _index_tables()
     sql, phase = INDEX_QUERIES[qi]

@@ -449,7 +449,7 @@ def test_avg_wide_exact_rounding():
     rounded half away from zero, vs Python integers."""
     import random
     import torch
-    from igloo_amd.exec.operators import _avg
+    from igloo_amd.exec.aggregate import _avg
     from igloo_amd import types as T
     rnd = random.Random(7)
     vals = [0, 1, -1, 5, -5, 2**63 - 1, -(2**63), 2**90 + 12345, -(2**95) - 7, 10**30 + 3]

@@ -33,10 +33,10 @@ def test_device_metrics_gpu(gpu_device):
 
 
 def test_having_constant_units():
-    """exec/operators.py having_constant: the HAVING literal in the raw units
+    """exec/aggregate.py having_constant: the HAVING literal in the raw units
     of the aggregate state, fractional thresholds rounded per comparison."""
     from igloo_amd import types as T
-    from igloo_amd.exec.operators import having_constant
+    from igloo_amd.exec.aggregate import having_constant
     from igloo_amd.sql.expr import Lit
     dec2 = T.DataType("decimal", 15, 2)
     lit = Lit(30000, T.DataType("decimal", 5, 2))          # 300.00
