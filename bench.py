@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--cpu-check", choices=["auto", "on", "off"], default="auto",
                     help="check result digests against the CPU engine (auto: sf <= 1)")
     ap.add_argument("--per-query", action="store_true", help="print per-query times to stderr")
+    ap.add_argument("--digests-out", default="", help="write the cold run's result digests (JSON) here")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (debug)")
     ap.add_argument("--eager-steps", type=int, default=2,
                     help="suites timed with query graphs off (warm_eager_s), after the headline steps")
@@ -193,6 +194,9 @@ def main():
         log("[bench] cold per query (ms): " + " ".join(f"Q{q}={cold_per_q[q] * 1e3:.1f}" for q in qs))
     ref = {q: digest(t) for q, t in cold_res.items()}
     del cold_res
+    if a.digests_out and rank == 0:
+        with open(a.digests_out, "w") as f:
+            json.dump({str(q): repr(d) for q, d in ref.items()}, f, indent=1, sort_keys=True)
     # generated scan kernels (ops/jit.py) compile on host threads while the
     # cold suite runs on the interpreted ones; whatever is still compiling is
     # waited for here and reported (not hidden in the warm steps)
