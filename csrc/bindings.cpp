@@ -781,19 +781,20 @@ PYBIND11_MODULE(_native, m) {
     io::pread_ranges(path, rs, threads);
   });
   m.def("pq_plan", [](uintptr_t host, const std::vector<std::tuple<int64_t, int64_t, int, int64_t, int64_t>>& chunks,
-                      int phys, int max_def, int max_rep, int64_t dec_base) {
+                      int phys, int max_def, int max_rep, int64_t dec_base, int type_len) {
     std::vector<io::PqChunkIn> cs;
     for (auto& [off, len, codec, first, rows] : chunks) cs.push_back({off, len, codec, first, rows});
     io::PqPlan plan;
     {
       py::gil_scoped_release rel;
-      plan = io::plan_column(P<const uint8_t>(host), cs, phys, max_def, max_rep, dec_base);
+      plan = io::plan_column(P<const uint8_t>(host), cs, phys, max_def, max_rep, dec_base, type_len);
     }
     py::dict d;
     d["pages"] = py::bytes((const char*)plan.pages.data(), plan.pages.size());
     d["jobs"] = py::bytes((const char*)plan.jobs.data(), plan.jobs.size());
     d["num_pages"] = plan.num_pages;
     d["num_jobs"] = plan.num_jobs;
+    d["num_zstd_jobs"] = plan.num_zstd_jobs;
     d["num_dict_pages"] = plan.num_dict_pages;
     d["dec_bytes"] = plan.dec_bytes;
     d["dict_entries"] = plan.dict_entries;
@@ -803,12 +804,30 @@ PYBIND11_MODULE(_native, m) {
     return d;
   }, "Plan GPU decode descriptors for one column's chunks staged at `host`",
      py::arg("host"), py::arg("chunks"), py::arg("phys"), py::arg("max_def"), py::arg("max_rep"),
-     py::arg("dec_base") = 0);
+     py::arg("dec_base") = 0, py::arg("type_len") = 0);
   m.def("pq_pack_spec", [](const py::dict& spec, bool need_output) {
     kern::PqDecodeSpec sp = decode_spec(spec, need_output);
     return py::bytes(reinterpret_cast<const char*>(&sp), sizeof(sp));
   }, "Validated binary PqDecodeSpec (concatenate one per column and upload)");
   m.attr("PQ_SPEC_BYTES") = (int)sizeof(kern::PqDecodeSpec);
+  m.def("pq_zstd_slots", &kern::pq_zstd_slots);
+  m.def("pq_zstd", [](uintptr_t jobs, int64_t njobs, uintptr_t raw, uintptr_t dec, uintptr_t lit, int64_t slots,
+                      uintptr_t err, uintptr_t s) {
+    if (njobs > 0 && (!jobs || !raw || !dec || !lit || !err)) throw std::runtime_error("pq_zstd: null buffer");
+    kern::pq_zstd(P<const kern::PqSnappyJob>(jobs), njobs, P<const uint8_t>(raw), P<uint8_t>(dec), P<uint8_t>(lit),
+                  slots, P<int>(err), S(s));
+  });
+  // host reference: decompress `src` (bytes) into exactly `size` bytes; (error code, output)
+  m.def("zstd_decompress_host", [](py::bytes src, int64_t size) {
+    std::string in = src;
+    std::string out((size_t)size, '\0');
+    int e;
+    {
+      py::gil_scoped_release nogil;
+      e = kern::zstd_decompress_host((const uint8_t*)in.data(), (int64_t)in.size(), (uint8_t*)out.data(), size);
+    }
+    return py::make_tuple(e, py::bytes(out));
+  });
   m.def("pq_snappy", [](uintptr_t jobs, int64_t njobs, uintptr_t raw, uintptr_t dec, uintptr_t err, uintptr_t s) {
     if (njobs > 0 && (!jobs || !raw || !dec || !err)) throw std::runtime_error("pq_snappy: null buffer");
     kern::pq_snappy(P<const kern::PqSnappyJob>(jobs), njobs, P<const uint8_t>(raw), P<uint8_t>(dec), P<int>(err), S(s));

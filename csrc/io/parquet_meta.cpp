@@ -528,7 +528,7 @@ void pread_ranges(const std::string& path, const std::vector<ReadRange>& ranges,
 }
 
 PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, int phys, int max_def, int max_rep,
-                   int64_t dec_base) {
+                   int64_t dec_base, int type_len) {
   PqPlan plan;
   plan.dec_bytes = align_up(dec_base, 16);
   if (max_rep > 0) {
@@ -546,18 +546,21 @@ PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, in
   std::vector<kern::PqPage> pages;
   std::vector<kern::PqSnappyJob> jobs;
   int64_t dict_base = 0;
+  int codec = PQ_UNCOMPRESSED;
   auto add_job = [&](int64_t src, int64_t src_len, int64_t dst_len) -> int64_t {
     const int64_t dst = plan.dec_bytes;
-    jobs.push_back(kern::PqSnappyJob{src, dst, (int32_t)src_len, (int32_t)dst_len});
+    jobs.push_back(kern::PqSnappyJob{src, dst, (int32_t)src_len, (int32_t)dst_len, codec, 0});
+    if (codec == PQ_ZSTD) ++plan.num_zstd_jobs;
     plan.dec_bytes = align_up(plan.dec_bytes + dst_len, 16);
     return dst;
   };
   for (const auto& ch : chunks) {
-    if (ch.codec != PQ_UNCOMPRESSED && ch.codec != PQ_SNAPPY) {
+    if (ch.codec != PQ_UNCOMPRESSED && ch.codec != PQ_SNAPPY && ch.codec != PQ_ZSTD) {
       plan.unsupported = "codec " + std::to_string(ch.codec);
       return plan;
     }
-    const bool snappy = ch.codec == PQ_SNAPPY;
+    codec = ch.codec;
+    const bool snappy = ch.codec != PQ_UNCOMPRESSED;   // a decompression job per page (snappy or zstd)
     int64_t pos = ch.buf_off;
     const int64_t end = ch.buf_off + ch.length;
     int64_t rows = 0;
@@ -572,6 +575,7 @@ PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, in
       kern::PqPage pg{};
       pg.levels_off = -1;
       pg.dict_off = -1;
+      pg.aux_off = -1;
       if (h.type == PQ_DICTIONARY_PAGE) {
         if (h.encoding != PQ_PLAIN && h.encoding != PQ_PLAIN_DICTIONARY) {
           plan.unsupported = "dictionary page encoding " + std::to_string(h.encoding);
@@ -601,7 +605,14 @@ PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, in
       if (h.type != PQ_DATA_PAGE && h.type != PQ_DATA_PAGE_V2) throw ParquetError("unknown page type");
       const int enc = h.encoding;
       const bool dict_enc = enc == PQ_PLAIN_DICTIONARY || enc == PQ_RLE_DICTIONARY;
-      if (!(enc == PQ_PLAIN || dict_enc || (enc == PQ_RLE && phys == PQ_BOOLEAN))) {
+      // DELTA_BINARY_PACKED ints, DELTA_LENGTH_BYTE_ARRAY strings and
+      // BYTE_STREAM_SPLIT values decode on the device into an aux slot of the
+      // decompression buffer (values, or string lengths), then read as PLAIN
+      const bool fixed = phys == PQ_INT32 || phys == PQ_INT64 || phys == PQ_FLOAT || phys == PQ_DOUBLE || phys == PQ_FLBA;
+      const bool delta = (enc == PQ_DELTA_BINARY_PACKED && (phys == PQ_INT32 || phys == PQ_INT64)) ||
+                         (enc == PQ_DELTA_LENGTH_BYTE_ARRAY && phys == PQ_BYTE_ARRAY) ||
+                         (enc == PQ_BYTE_STREAM_SPLIT && fixed);
+      if (!(enc == PQ_PLAIN || dict_enc || (enc == PQ_RLE && phys == PQ_BOOLEAN) || delta)) {
         plan.unsupported = "data page encoding " + std::to_string(enc);
         return plan;
       }
@@ -643,6 +654,14 @@ PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, in
       }
       pg.num_values = (int32_t)nrows;
       pg.encoding = enc;
+      if (delta) {
+        const int64_t w = enc == PQ_DELTA_LENGTH_BYTE_ARRAY ? 4
+                          : phys == PQ_INT32 || phys == PQ_FLOAT ? 4
+                          : phys == PQ_FLBA ? (int64_t)type_len
+                          : 8;
+        pg.aux_off = plan.dec_bytes;
+        plan.dec_bytes = align_up(plan.dec_bytes + std::max<int64_t>(nrows, 1) * w, 16);
+      }
       pg.out_row = ch.first_row + rows;
       pg.dict_off = dict_count ? dict_off : -1;
       pg.flags |= dict_flags;

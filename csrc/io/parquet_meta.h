@@ -30,7 +30,8 @@ enum PqCodec : int { PQ_UNCOMPRESSED = 0, PQ_SNAPPY = 1, PQ_GZIP = 2, PQ_LZO = 3
                      PQ_ZSTD = 6, PQ_LZ4_RAW = 7 };
 enum PqPageType : int { PQ_DATA_PAGE = 0, PQ_INDEX_PAGE = 1, PQ_DICTIONARY_PAGE = 2, PQ_DATA_PAGE_V2 = 3 };
 enum PqEncoding : int { PQ_PLAIN = 0, PQ_PLAIN_DICTIONARY = 2, PQ_RLE = 3, PQ_BIT_PACKED = 4,
-                        PQ_RLE_DICTIONARY = 8 };
+                        PQ_DELTA_BINARY_PACKED = 5, PQ_DELTA_LENGTH_BYTE_ARRAY = 6, PQ_DELTA_BYTE_ARRAY = 7,
+                        PQ_RLE_DICTIONARY = 8, PQ_BYTE_STREAM_SPLIT = 9 };
 
 struct PqStats {
   bool has_min = false, has_max = false, has_nulls = false;
@@ -122,6 +123,7 @@ struct PqPlan {
   std::vector<uint8_t> pages;  // packed kern::PqPage
   std::vector<uint8_t> jobs;   // packed kern::PqSnappyJob
   int64_t num_pages = 0, num_jobs = 0, num_dict_pages = 0;
+  int64_t num_zstd_jobs = 0;   // of num_jobs
   int64_t dec_bytes = 0;     // device bytes needed for decompressed payloads
   int64_t dict_entries = 0;  // sum of dictionary sizes over chunks
   int64_t plain_pages = 0;   // data pages not dictionary-encoded
@@ -132,7 +134,7 @@ struct PqPlan {
 // dec_base: first free byte of the (shared) decompression buffer; plan.dec_bytes
 // is returned as the end of this column's slots (dec_base included).
 PqPlan plan_column(const uint8_t* host, const std::vector<PqChunkIn>& chunks, int phys_type, int max_def,
-                   int max_rep, int64_t dec_base = 0);
+                   int max_rep, int64_t dec_base = 0, int type_len = 0);
 
 }  // namespace io
 }  // namespace igloo

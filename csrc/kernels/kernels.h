@@ -395,6 +395,7 @@ struct PqPage {
   int64_t levels_off;  // v2: definition levels (raw buffer); -1 otherwise
   int64_t dict_off;    // the chunk's dictionary payload; -1 if none
   int64_t out_row;     // first output row
+  int64_t aux_off;     // DELTA_* / BYTE_STREAM_SPLIT pages: decoded values (decompression buffer); -1 otherwise
   int32_t size;        // payload bytes at data_off
   int32_t num_values;  // rows of the page (flat columns)
   int32_t levels_len;  // v2 definition-level bytes
@@ -404,13 +405,18 @@ struct PqPage {
   int32_t dict_base;   // first global dictionary slot of the chunk
   int32_t dict_count;  // dictionary entries of the chunk
 };
-static_assert(sizeof(PqPage) == 64, "PqPage layout is shared with the host planner");
+static_assert(sizeof(PqPage) == 72, "PqPage layout is shared with the host planner");
 
+// A compressed page payload: raw -> decompression buffer, by codec
+enum PqJobCodec : int { PQ_CODEC_SNAPPY = 1, PQ_CODEC_ZSTD = 6 };
 struct PqSnappyJob {
   int64_t src_off;  // raw buffer
   int64_t dst_off;  // decompression buffer
   int32_t src_len, dst_len;
+  int32_t codec;    // PqJobCodec (parquet CompressionCodec numbering)
+  int32_t pad;
 };
+static_assert(sizeof(PqSnappyJob) == 32, "PqSnappyJob layout is shared with the host planner");
 
 struct PqDecodeSpec {
   int32_t phys, type_len, out_width, conv;
@@ -431,6 +437,14 @@ struct PqDecodeSpec {
 
 void pq_snappy(const PqSnappyJob* jobs, int64_t njobs, const uint8_t* raw, uint8_t* dec, int* error,
                hipStream_t stream);
+// zstd.hip: ZSTD pages, one 64-lane workgroup each; `lit` holds `slots` literal
+// buffers of 128 KiB (slots = pq_zstd_slots(njobs) workgroups run at a time)
+constexpr int64_t kZstdMaxSlots = 1024;
+int64_t pq_zstd_slots(int64_t njobs);
+void pq_zstd(const PqSnappyJob* jobs, int64_t njobs, const uint8_t* raw, uint8_t* dec, uint8_t* lit, int64_t slots,
+             int* error, hipStream_t stream);
+// host reference decoder (same code, one lane): 0 or a zstd error code (20..24)
+int zstd_decompress_host(const uint8_t* src, int64_t slen, uint8_t* dst, int64_t dcap);
 // pages of several columns in one launch: page_col[i] indexes specs[] (device arrays)
 void pq_dict_strings(const PqPage* pages, int64_t npages, const int32_t* page_col, const PqDecodeSpec* specs,
                      hipStream_t stream);

@@ -227,6 +227,138 @@ __device__ bool walk_byte_array(const uint8_t* p, const uint8_t* end, int count,
   return ok;
 }
 
+// DELTA_BINARY_PACKED (parquet Encodings.md): a header <block size> <miniblocks
+// per block> <value count> <first value>, then per block a zigzag min delta,
+// one bit width per miniblock and the bit-packed miniblocks. Thread 0 walks
+// the block headers (up to kDbpCap miniblocks per round) into LDS; then every
+// lane unpacks one delta (binary search for its miniblock) and a block-wide
+// scan turns deltas into values, carried from round to round.
+constexpr int kDbpCap = 256;
+struct DbpTable {
+  int64_t mb_ptr[kDbpCap];
+  uint64_t mb_min[kDbpCap];
+  int32_t mb_first[kDbpCap + 1];
+  uint8_t mb_bw[kDbpCap];
+  int64_t cur, bw_ptr, end;
+  uint64_t first, blk_min;
+  int32_t mpb, vpm, total, in_block, done, nmb, err;
+};
+
+__device__ inline bool uleb(const uint8_t*& q, const uint8_t* end, uint64_t* v) {
+  uint64_t x = 0;
+  for (int sh = 0; sh < 64 && q < end; sh += 7) {
+    const uint8_t b = *q++;
+    x |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) {
+      *v = x;
+      return true;
+    }
+  }
+  return false;
+}
+
+__device__ inline uint64_t unpack_bits(const uint8_t* p, int64_t bit, int bw) {
+  if (bw == 0) return 0;
+  const uint8_t* q = p + (bit >> 3);
+  const int sh = (int)(bit & 7);
+  const int nb = (sh + bw + 7) >> 3;
+  uint64_t lo = 0;
+  for (int k = 0; k < nb && k < 8; ++k) lo |= (uint64_t)q[k] << (8 * k);
+  uint64_t v = lo >> sh;
+  if (nb > 8) v |= (uint64_t)q[8] << (64 - sh);
+  return bw >= 64 ? v : v & ((1ull << bw) - 1ull);
+}
+
+// Decodes `count` values of a DELTA_BINARY_PACKED stream at [p, end):
+// out(i, value) once per value (some lane); returns the end of the stream (or
+// nullptr when malformed). Call with every thread of the block.
+template <typename Out>
+__device__ const uint8_t* dbp_decode(const uint8_t* p, const uint8_t* end, int count, DbpTable& d, int64_t* scan_ws,
+                                     Out out) {
+  if (threadIdx.x == 0) {
+    const uint8_t* q = p;
+    uint64_t bs = 0, mpb = 0, total = 0, first = 0;
+    d.err = !(uleb(q, end, &bs) && uleb(q, end, &mpb) && uleb(q, end, &total) && uleb(q, end, &first));
+    if (!d.err && (mpb == 0 || bs == 0 || bs % 128 != 0 || (bs / mpb) % 32 != 0 || (int64_t)total != count))
+      d.err = 1;
+    d.mpb = (int32_t)mpb;
+    d.vpm = mpb ? (int32_t)(bs / mpb) : 0;
+    d.total = (int32_t)total;
+    d.first = (first >> 1) ^ (0 - (first & 1));   // zigzag
+    d.cur = (int64_t)q;
+    d.end = (int64_t)end;
+    d.in_block = d.mpb;
+    d.done = 0;
+  }
+  __syncthreads();
+  if (d.err) return nullptr;
+  if (count > 0 && threadIdx.x == 0) out(0, d.first);
+  const int nd = count > 0 ? count - 1 : 0;
+  uint64_t carry = d.first;
+  while (d.done < nd) {
+    if (threadIdx.x == 0) {
+      const uint8_t* q = (const uint8_t*)d.cur;
+      int done = d.done, nmb = 0;
+      while (nmb < kDbpCap && done < nd && !d.err) {
+        if (d.in_block == d.mpb) {
+          uint64_t z;
+          if (!uleb(q, end, &z) || q + d.mpb > end) {
+            d.err = 1;
+            break;
+          }
+          d.blk_min = (z >> 1) ^ (0 - (z & 1));
+          d.bw_ptr = (int64_t)q;
+          q += d.mpb;
+          d.in_block = 0;
+        }
+        const int bw = ((const uint8_t*)d.bw_ptr)[d.in_block];
+        const int n = nd - done < d.vpm ? nd - done : d.vpm;
+        if (bw > 64 || q + (((int64_t)n * bw + 7) >> 3) > end) {
+          d.err = 1;
+          break;
+        }
+        d.mb_ptr[nmb] = (int64_t)q;
+        d.mb_min[nmb] = d.blk_min;
+        d.mb_bw[nmb] = (uint8_t)bw;
+        d.mb_first[nmb] = done;
+        const int64_t full = ((int64_t)d.vpm * bw) >> 3;
+        q = q + full <= end ? q + full : end;   // the last miniblock may stop at the stream end
+        ++d.in_block;
+        done += n;
+        ++nmb;
+      }
+      d.mb_first[nmb] = done;
+      d.nmb = nmb;
+      d.cur = (int64_t)q;
+    }
+    __syncthreads();
+    if (d.err) return nullptr;
+    const int nmb = d.nmb, lo = d.mb_first[0], hi = d.mb_first[nmb];
+    for (int base = lo; base < hi; base += kBlock) {
+      const int i = base + (int)threadIdx.x;
+      uint64_t dl = 0;
+      if (i < hi) {
+        int a = 0, b = nmb - 1;
+        while (a < b) {
+          const int m = (a + b + 1) >> 1;
+          if (d.mb_first[m] <= i) a = m;
+          else b = m - 1;
+        }
+        const int bw = d.mb_bw[a];
+        dl = d.mb_min[a] + unpack_bits((const uint8_t*)d.mb_ptr[a], (int64_t)(i - d.mb_first[a]) * bw, bw);
+      }
+      int64_t tot;
+      const uint64_t ex = (uint64_t)block_exclusive_scan((int64_t)dl, scan_ws, &tot);
+      if (i < hi) out(i + 1, carry + ex + dl);
+      carry += (uint64_t)tot;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) d.done = hi;
+    __syncthreads();
+  }
+  return (const uint8_t*)d.cur;
+}
+
 __device__ inline int block_sum_int(int v, int* red) {
   v = (int)wave_reduce_sum((int64_t)v);
   if (lane_id() == 0) red[threadIdx.x / kWave] = v;
@@ -331,6 +463,7 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
   __shared__ uint8_t win[kWalkWin];
   __shared__ int64_t scan_ws[kWavesPerBlock + 1];
   __shared__ int red[kWavesPerBlock];
+  __shared__ DbpTable dbp;
 
   const PqPage pg = pages[blockIdx.x];
   if (pg.kind == PQ_PAGE_DICT) return;
@@ -388,10 +521,59 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
   const bool dict = enc == 2 || enc == 8;
   const bool bool_rle = s.phys == PQ_PHYS_BOOLEAN && enc == 3;
   const bool str_plain = s.phys == PQ_PHYS_BYTE_ARRAY && !dict;
+  const bool dlba = enc == 6;
   uint32_t* idx = s.scratch + row0;
+  const int w_in = (s.phys == PQ_PHYS_INT32 || s.phys == PQ_PHYS_FLOAT) ? 4
+                   : s.phys == PQ_PHYS_FLBA                             ? s.type_len
+                                                                        : 8;
+  uint8_t* aux = pg.aux_off >= 0 ? const_cast<uint8_t*>(s.dec) + pg.aux_off : nullptr;   // this page's own slot
   if (nnz > 0) {
     bool ok = true;
-    if (dict) {
+    if ((enc == 5 || enc == 6 || enc == 9) && !aux) {
+      ok = false;
+    } else if (enc == 5) {
+      // DELTA_BINARY_PACKED ints -> plain little-endian values in the aux slot
+      const bool w4 = w_in == 4;
+      ok = dbp_decode(p, end, nnz, dbp, scan_ws, [&](int i, uint64_t v) {
+             if (w4) reinterpret_cast<uint32_t*>(aux)[i] = (uint32_t)v;
+             else reinterpret_cast<uint64_t*>(aux)[i] = v;
+           }) != nullptr;
+      __syncthreads();
+      p = aux;
+      end = aux + (int64_t)nnz * w_in;
+    } else if (enc == 6) {
+      // DELTA_LENGTH_BYTE_ARRAY: lengths (DELTA_BINARY_PACKED) -> aux, then the
+      // concatenated bytes; idx[j] = offset of value j's bytes from p
+      const uint8_t* bytes = dbp_decode(p, end, nnz, dbp, scan_ws, [&](int i, uint64_t v) {
+        reinterpret_cast<uint32_t*>(aux)[i] = (uint32_t)v;
+      });
+      __syncthreads();
+      ok = bytes != nullptr;
+      if (ok) {
+        int64_t carry = bytes - p;
+        for (int b0 = 0; b0 < nnz; b0 += kBlock) {
+          const int j = b0 + (int)threadIdx.x;
+          const int64_t len = j < nnz ? (int64_t)reinterpret_cast<const int32_t*>(aux)[j] : 0;
+          int64_t tot;
+          const int64_t ex = block_exclusive_scan(len < 0 ? 0 : len, scan_ws, &tot);
+          if (j < nnz) idx[j] = (uint32_t)(carry + ex);
+          carry += tot;
+          if (len < 0) ok = false;
+        }
+        ok = __syncthreads_and(ok) && carry <= end - p;
+      }
+    } else if (enc == 9) {
+      // BYTE_STREAM_SPLIT: byte k of value j at p[k * nnz + j] -> plain values in aux
+      ok = p + (int64_t)w_in * nnz <= end;
+      if (ok)
+        for (int64_t t = threadIdx.x; t < (int64_t)w_in * nnz; t += kBlock) {
+          const int64_t j = t / w_in, k = t - j * w_in;
+          aux[t] = p[k * nnz + j];
+        }
+      __syncthreads();
+      p = aux;
+      end = aux + (int64_t)nnz * w_in;
+    } else if (dict) {
       if (p >= end) {
         ok = false;
       } else {
@@ -409,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
     } else if (enc != 0) {
       if (threadIdx.x == 0) set_error(s.error, PQ_ERR_ENCODING);
       return;
-    } else if (str_plain) {
+    } else if (str_plain && !dlba) {
       if (!walk_byte_array(p, end, nnz, win, ws, [&](int j, uint32_t off, uint32_t) { idx[j] = off; })) {
         if (threadIdx.x == 0) set_error(s.error, PQ_ERR_BYTE_ARRAY);
         return;
@@ -423,9 +605,6 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
   __syncthreads();
 
   // ---- rows: compact value index j = number of valid rows before row i
-  const int w_in = (s.phys == PQ_PHYS_INT32 || s.phys == PQ_PHYS_FLOAT) ? 4
-                   : s.phys == PQ_PHYS_FLBA                             ? s.type_len
-                                                                        : 8;
   const uint8_t* dp = dict ? dict_ptr(pg, s) : nullptr;
   const uint32_t dcount = (uint32_t)pg.dict_count;
   int64_t carry = 0;
@@ -470,7 +649,7 @@ __global__ __launch_bounds__(kBlock) void pq_decode_kernel(const PqPage* __restr
           }
         } else {
           const uint32_t off = idx[j];
-          s.str_len[row] = (int64_t)ld_u32(p + off - 4);
+          s.str_len[row] = dlba ? (int64_t)reinterpret_cast<const int32_t*>(aux)[j] : (int64_t)ld_u32(p + off - 4);
           s.str_pos[row] = (int64_t)(p + off);
         }
       } else if (s.phys == PQ_PHYS_BOOLEAN) {
@@ -549,6 +728,7 @@ __global__ __launch_bounds__(64) void pq_snappy_kernel(const PqSnappyJob* __rest
   __shared__ uint8_t ring[kSnapRingS];
   __shared__ uint8_t inw[kSnapInS + 8];
   const PqSnappyJob jb = jobs[blockIdx.x];
+  if (jb.codec != PQ_CODEC_SNAPPY) return;   // (ZSTD pages: pq_zstd)
   const uint8_t* src = raw + jb.src_off;
   const int slen = uni(jb.src_len);
   uint8_t* dst = dec + jb.dst_off;

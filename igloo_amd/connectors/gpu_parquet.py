@@ -16,7 +16,8 @@ Pipeline per scan:
      emits device page descriptors + snappy jobs; the pages of every column
      of a batch go to ONE launch of each kernel (page -> column spec table),
      so small columns do not leave the GPU idle;
-  4. device: ``pq_snappy`` (one wave per compressed page, LDS history ring),
+  4. device: ``pq_snappy`` / ``pq_zstd`` (one wave per compressed page, LDS
+     history ring; csrc/kernels/zstd.hip decodes ZSTD frames on the GPU),
      ``pq_dict_strings`` (dictionary entry positions), ``pq_decode`` (levels ->
      validity, PLAIN / RLE_DICTIONARY values -> typed columns with the type
      conversion fused), ``pq_str_copy`` (string bytes after an offset scan).
@@ -25,8 +26,8 @@ Pipeline per scan:
      the device).
 
 The host only reads bytes and parses metadata; pages are decoded on the GPU.
-Columns this decoder does not handle (nested, INT96, GZIP/ZSTD/LZ4 codecs,
-DELTA encodings) are reported back, and the caller reads them with the host
+Columns this decoder does not handle (nested, INT96, GZIP/LZ4/BROTLI codecs,
+DELTA_BYTE_ARRAY) are reported back, and the caller reads them with the host
 decoder.
 """
 from __future__ import annotations
@@ -48,7 +49,8 @@ CONV = {"copy": 0, "narrow": 1, "sext": 2, "zext": 3, "f2d": 4, "flba": 5, "mul"
 ERRORS = {1: "malformed RLE/bit-packed stream", 2: "dictionary index out of range", 3: "malformed BYTE_ARRAY values",
           4: "malformed snappy stream", 5: "snappy size mismatch", 6: "decimal value exceeds 64-bit fixed point",
           7: "unsupported page encoding", 8: "NULL in a column whose statistics say it has none",
-          9: "truncated page"}
+          9: "truncated page", 20: "not a zstd frame", 21: "zstd frame needs a dictionary",
+          22: "malformed zstd stream", 23: "zstd size mismatch", 24: "malformed zstd entropy table"}
 READ_THREADS = int(os.environ.get("IGLOO_PARQUET_READ_THREADS", str(min(16, os.cpu_count() or 8))))
 #: staged bytes per decode batch (pinned host buffer + one set of launches):
 #: small enough that the host reads batch i+1 while the GPU copies and
@@ -139,7 +141,7 @@ class GpuParquetReader:
                 return f"type {dt} from physical type {leaf['type']} ({leaf['logical'] or 'plain'})"
             for g in m.row_groups:
                 c = g["chunks"][li]
-                if c["codec"] not in (0, 1):
+                if c["codec"] not in (0, 1, 6):   # uncompressed, snappy, zstd
                     return f"codec {c['codec']}"
                 if c["external"]:
                     return "column chunk in an external file"
@@ -245,7 +247,8 @@ class GpuParquetReader:
                       for _fi, _s, length, off, codec, first, rows in lay["ranges"]]
             leaf = lay["leaf"]
             try:
-                plan = N.pq_plan(hp, chunks, leaf["type"], leaf["max_def"], leaf["max_rep"], dec_end)
+                plan = N.pq_plan(hp, chunks, leaf["type"], leaf["max_def"], leaf["max_rep"], dec_end,
+                                 leaf["type_length"])
             except RuntimeError as e:
                 raise IoError(f"corrupt parquet column {lay['name']}: {e}") from e
             if plan["unsupported"]:
@@ -260,9 +263,16 @@ class GpuParquetReader:
         dec = torch.empty(dec_end + 64, dtype=torch.uint8, device=device) if dec_end else None
         jobs = b"".join(p["jobs"] for _, p in plans)
         njobs = sum(p["num_jobs"] for _, p in plans)
+        nzstd = sum(p["num_zstd_jobs"] for _, p in plans)
         if njobs:
             jt = _upload(jobs, device)
-            launch("pq_snappy").pq_snappy(ptr(jt), njobs, ptr(raw), ptr(dec), ptr(err), s)
+            if njobs > nzstd:
+                launch("pq_snappy").pq_snappy(ptr(jt), njobs, ptr(raw), ptr(dec), ptr(err), s)
+            if nzstd:
+                slots = N.pq_zstd_slots(nzstd)
+                lit = torch.empty(slots << 17, dtype=torch.uint8, device=device)   # 128 KiB literals per workgroup
+                launch("pq_zstd").pq_zstd(ptr(jt), njobs, ptr(raw), ptr(dec), ptr(lit), slots, ptr(err), s)
+                st["zstd_pages"] = st.get("zstd_pages", 0) + nzstd
         # ---- outputs + one spec per column
         specs, page_col, pages, posts = [], [], [], []
         scratch = torch.empty(max(n, 1) * len(plans), dtype=torch.int32, device=device)

@@ -163,9 +163,12 @@ _MANIFEST_SCHEMA = {
             {"name": "record_count", "type": "long"}, {"name": "file_size_in_bytes", "type": "long"}]}}]}
 
 
-def write_table(path: str, table, snapshot_id: int = 1, append: bool = False, rows_per_file: int = 1 << 20):
+def write_table(path: str, table, snapshot_id: int = 1, append: bool = False, rows_per_file: int = 1 << 20,
+                compression: str = "zstd", **parquet_options):
     """Write an Arrow table as a (v2-style) Iceberg table: parquet data files +
-    Avro manifest/manifest list + vN.metadata.json + version-hint.text."""
+    Avro manifest/manifest list + vN.metadata.json + version-hint.text. Data
+    files are ZSTD-compressed by default, like Iceberg's own writer
+    (write.parquet.compression-codec)."""
     import pyarrow.parquet as pq
     import uuid
     os.makedirs(os.path.join(path, "data"), exist_ok=True)
@@ -178,7 +181,7 @@ def write_table(path: str, table, snapshot_id: int = 1, append: bool = False, ro
     for i in range(0, max(table.num_rows, 1), rows_per_file):
         f = os.path.join(path, "data", f"{uuid.uuid4().hex}.parquet")
         part = table.slice(i, rows_per_file)
-        pq.write_table(part, f)
+        pq.write_table(part, f, compression=compression, **parquet_options)
         entries.append({"status": 1, "snapshot_id": snapshot_id,
                         "data_file": {"file_path": f, "file_format": "PARQUET", "record_count": part.num_rows,
                                       "file_size_in_bytes": os.path.getsize(f)}})

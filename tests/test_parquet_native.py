@@ -77,7 +77,7 @@ def test_statistics_min_max(tmp_path):
 
 
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
-@pytest.mark.parametrize("compression", ["none", "snappy"])
+@pytest.mark.parametrize("compression", ["none", "snappy", "zstd"])
 def test_page_headers_and_plan(tmp_path, version, compression):
     t = _table(20000)
     path = str(tmp_path / "t.parquet")
@@ -105,9 +105,10 @@ def test_page_headers_and_plan(tmp_path, version, compression):
             row += g["num_rows"]
         plan = N.pq_plan(hp, chunks, leaf["type"], leaf["max_def"], leaf["max_rep"])
         assert plan["unsupported"] == ""
-        assert plan["num_pages"] * 64 == len(plan["pages"])
-        if compression == "snappy":
+        assert plan["num_pages"] * 72 == len(plan["pages"])   # sizeof(kern::PqPage)
+        if compression != "none":
             assert plan["num_jobs"] > 0 and plan["dec_bytes"] > 0
+            assert plan["num_zstd_jobs"] == (plan["num_jobs"] if compression == "zstd" else 0)
         else:
             assert plan["num_jobs"] == 0
         if name == "s":   # 50 distinct strings: dictionary-encoded in every row group
@@ -138,7 +139,10 @@ def test_unsupported_columns_are_reported(tmp_path):
     t = _table(1000)
     p1 = str(tmp_path / "z.parquet")
     pq.write_table(t, p1, compression="zstd")
-    assert "codec" in GpuParquetReader([p1]).supports("i32", T.INT32)
+    assert GpuParquetReader([p1]).supports("i32", T.INT32) is None          # ZSTD decodes on the GPU
+    p0 = str(tmp_path / "g.parquet")
+    pq.write_table(t, p0, compression="gzip")
+    assert "codec" in GpuParquetReader([p0]).supports("i32", T.INT32)
     p2 = str(tmp_path / "n.parquet")
     pq.write_table(pa.table({"l": pa.array([[1, 2], [3]], pa.list_(pa.int64()))}), p2)
     assert FileMeta(p2).leaves[0]["max_rep"] == 1
