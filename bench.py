@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--source", choices=["parquet", "hbm"], default="parquet")
     ap.add_argument("--data-dir", default=os.environ.get("IGLOO_BENCH_DIR", "/tmp/igloo_tpch"))
     ap.add_argument("--lean", action="store_true", help="skip comment columns no query reads")
+    ap.add_argument("--parquet-codec", choices=["snappy", "zstd", "none"], default="snappy",
+                    help="codec of the generated Parquet files (--source parquet)")
     ap.add_argument("--cpu-check", choices=["auto", "on", "off"], default="auto",
                     help="check result digests against the CPU engine (auto: sf <= 1)")
     ap.add_argument("--per-query", action="store_true", help="print per-query times to stderr")
@@ -134,7 +136,7 @@ def main():
     t0 = time.perf_counter()
     if a.source == "parquet":
         man = parquet_gen.write_dataset(a.sf, a.data_dir, device=device, rank=rank, world=world, lean=a.lean,
-                                        log=log)
+                                        log=log, compression=a.parquet_codec)
         if not a.cpu:
             torch.cuda.empty_cache()
         barrier()
@@ -180,6 +182,9 @@ def main():
             log("[bench] modes " + " ".join(modes))
 
     # ---- cold: first touch of every column (Parquet read + GPU decode) and structure
+    from igloo_amd.connectors import gpu_parquet as _gpq
+    for k in _gpq.TOTALS:
+        _gpq.TOTALS[k] = 0
     barrier()
     tc = time.perf_counter()
     cold_res, cold_scanned = {}, {}
@@ -336,7 +341,7 @@ def main():
         if per_q:
             for q in qs:
                 print(f"[bench] Q{q:02d} {per_q[q] / a.steps * 1e3:9.2f} ms", file=sys.stderr)
-        src_txt = ("synthetic TPC-H-shaped Parquet (spec distributions, snappy, dictionary pages) generated on "
+        src_txt = (f"synthetic TPC-H-shaped Parquet (spec distributions, {a.parquet_codec}, dictionary pages) generated on "
                    "the device; GPU-decoded into the HBM cache tier; value = warm suite over the cached columns, "
                    "cold_s = first suite incl. file read + GPU decode + index builds"
                    if a.source == "parquet" else
@@ -379,6 +384,11 @@ def main():
             "cpu_check": cpu_check,
             "scan_rows_per_s": round(scanned / step_s, 1),
             "rows_read_per_suite": int(scanned),
+            # cold-run Parquet decode alone (file bytes through read + H2D + GPU
+            # decode, index builds excluded): rank 0's reader
+            "parquet_decode_gbps": (round(_gpq.TOTALS["file_bytes"] / _gpq.TOTALS["seconds"] / 1e9, 2)
+                                    if _gpq.TOTALS["seconds"] else None),
+            "parquet_decode": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in _gpq.TOTALS.items()},
         }
         print(json.dumps(out), flush=True)
     eng.close()              # query graphs hold RCCL resources (Communicator.shutdown)

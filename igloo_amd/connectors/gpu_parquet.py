@@ -56,6 +56,10 @@ READ_THREADS = int(os.environ.get("IGLOO_PARQUET_READ_THREADS", str(min(16, os.c
 #: small enough that the host reads batch i+1 while the GPU copies and
 #: decodes batch i, large enough that every launch fills the chip
 BATCH_BYTES = int(os.environ.get("IGLOO_PARQUET_BATCH_BYTES", str(256 << 20)))
+#: process-wide decode totals (bench.py reports parquet_decode_gbps from them):
+#: file bytes staged, decoded column bytes, seconds inside GpuParquetReader.read
+#: (positional reads + H2D + planning + device decode, up to the error-flag sync)
+TOTALS = {"file_bytes": 0, "out_bytes": 0, "seconds": 0.0, "pages": 0, "zstd_pages": 0, "columns": 0}
 
 
 class FileMeta:
@@ -195,6 +199,14 @@ class GpuParquetReader:
                 raise ExecutionError(f"parquet decode failed: {ERRORS.get(code, code)}")
         st["total_s"] = time.perf_counter() - t0
         self.last_stats = st
+        TOTALS["file_bytes"] += st["bytes"]
+        TOTALS["seconds"] += st["total_s"]
+        TOTALS["pages"] += st["pages"]
+        TOTALS["zstd_pages"] += st.get("zstd_pages", 0)
+        TOTALS["columns"] += len(out)
+        for c in out.values():
+            TOTALS["out_bytes"] += c.data.numel() * c.data.element_size() + (
+                c.offsets.numel() * 8 if c.offsets is not None else 0)
         return out, rejected
 
     # --------------------------------------------------------------- internals

@@ -131,11 +131,11 @@ def test_zstd_iceberg_table_on_gpu(tmp_path, gpu_device):
     e = ig.QueryEngine(device=gpu_device)
     src = e.register_iceberg("ice", root)
     before = KERNEL_CALLS["pq_zstd"]
-    got = e.query("select count(*) c, sum(i64) s, count(high) h, max(low) l, sum(f64) f from ice").to_pylist()[0]
+    got = e.query("select count(*) c, sum(i32) s, count(high) h, max(low) l, sum(f64) f from ice").to_pylist()[0]
     assert KERNEL_CALLS["pq_zstd"] > before
     assert src._inner.last_gpu_stats and not src._inner.last_gpu_stats["host_columns"]
     assert got["c"] == t.num_rows
-    assert got["s"] == sum(v for v in t.column("i64").to_pylist() if v is not None)
+    assert got["s"] == sum(v for v in t.column("i32").to_pylist() if v is not None)
     assert got["h"] == t.column("high").null_count * -1 + t.num_rows
     assert got["l"] == max(v for v in t.column("low").to_pylist() if v is not None)
     assert abs(got["f"] - sum(v for v in t.column("f64").to_pylist() if v is not None)) < 1e-6
