@@ -313,23 +313,23 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("probe_write", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
                           bool rid64, int64_t cap, int64_t kmin, bool direct, uintptr_t words, uintptr_t tile_off,
-                          uintptr_t out_probe, bool out64, uintptr_t out_build, uintptr_t s) {
+                          uintptr_t out_probe, bool out64, uintptr_t out_build, int64_t out_cap, uintptr_t s) {
     if (m_ > 0 && (!keys || !thead || !words || !tile_off || !out_probe || (!direct && !tkeys)))
       throw std::runtime_error("probe_write: null buffer");
     kern::probe_write(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
                       P<const void>(thead), rid64, cap, kmin, direct, P<const unsigned long long>(words),
-                      P<const int64_t>(tile_off), P<void>(out_probe), out64, P<void>(out_build), S(s));
+                      P<const int64_t>(tile_off), P<void>(out_probe), out64, P<void>(out_build), out_cap, S(s));
   });
   m.def("join_expand", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
                           uintptr_t cstart, uintptr_t crows, bool rid64, int64_t cap, int64_t kmin, bool direct,
                           uintptr_t offsets, uintptr_t out_probe, uintptr_t out_build, uintptr_t bits, uint64_t bmask,
-                          uintptr_t s) {
+                          int64_t out_cap, uintptr_t s) {
     if (m_ > 0 && (!keys || !thead || !offsets || !out_probe || !out_build || (!direct && !tkeys)))
       throw std::runtime_error("join_expand: null buffer");
     kern::join_expand(P<const void>(keys), key64, P<const uint8_t>(valid), m_, P<const int64_t>(tkeys),
                       P<const void>(thead), P<const void>(cstart), P<const void>(crows), rid64, cap, kmin, direct,
                       P<const int64_t>(offsets), P<int32_t>(out_probe), P<void>(out_build), P<const uint32_t>(bits),
-                      bmask, S(s));
+                      bmask, out_cap, S(s));
   });
   // fused scan kernels. cols: [(ptr, width)], terms: [(col, kind, lo, hi, set)],
   // keys: [(col, lo, mul)], aggs: [(op, checked, [(col, a, b)], dst, dst2, shared)]
@@ -422,9 +422,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("groupby_occupied", [](uintptr_t trow, int64_t cap, uintptr_t occ, uintptr_t gid_of_slot, uintptr_t s) {
     kern::groupby_occupied(P<const int32_t>(trow), cap, P<uint8_t>(occ), P<int32_t>(gid_of_slot), S(s));
   });
-  m.def("groupby_assign", [](uintptr_t slots, bool slots64, int64_t g, uintptr_t trow, uintptr_t gid_of_slot,
-                             uintptr_t rep_row, uintptr_t s) {
-    kern::groupby_assign(P<const void>(slots), slots64, g, P<const int32_t>(trow), P<int32_t>(gid_of_slot),
+  m.def("groupby_assign", [](uintptr_t slots, bool slots64, int64_t g, int64_t cap, uintptr_t trow,
+                             uintptr_t gid_of_slot, uintptr_t rep_row, uintptr_t s) {
+    kern::groupby_assign(P<const void>(slots), slots64, g, cap, P<const int32_t>(trow), P<int32_t>(gid_of_slot),
                          P<int32_t>(rep_row), S(s));
   });
   m.def("groupby_lookup", [](uintptr_t keys, bool key64, int64_t n, uintptr_t tkeys, uintptr_t gid_of_slot,
@@ -459,21 +459,22 @@ PYBIND11_MODULE(_native, m) {
   });
 
   // ----------------------------------------------------------------- gather
-  // descs: list of (src, dst, elem_bytes, src_valid, dst_valid)
-  m.def("gather_multi", [](uintptr_t idx, bool idx64, int64_t n, const std::vector<std::tuple<uintptr_t, uintptr_t, int, uintptr_t, uintptr_t>>& descs, uintptr_t s) {
+  // descs: list of (src, dst, elem_bytes, src_valid, dst_valid, src_rows)
+  m.def("gather_multi", [](uintptr_t idx, bool idx64, int64_t n, const std::vector<std::tuple<uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, int64_t>>& descs, uintptr_t s) {
     std::vector<kern::GatherDesc> d;
     for (auto& t : descs)
       d.push_back({P<const void>(std::get<0>(t)), P<void>(std::get<1>(t)), std::get<2>(t),
-                   P<const uint8_t>(std::get<3>(t)), P<uint8_t>(std::get<4>(t))});
+                   P<const uint8_t>(std::get<3>(t)), P<uint8_t>(std::get<4>(t)), std::get<5>(t)});
     kern::gather_multi(P<const void>(idx), idx64, n, d.data(), (int)d.size(), S(s));
   });
-  m.def("str_gather_lengths", [](uintptr_t off, uintptr_t idx, bool idx64, int64_t n, uintptr_t len, uintptr_t s) {
-    kern::str_gather_lengths(P<const int64_t>(off), P<const void>(idx), idx64, n, P<int64_t>(len), S(s));
+  m.def("str_gather_lengths", [](uintptr_t off, int64_t rows, uintptr_t idx, bool idx64, int64_t n, uintptr_t len,
+                                 uintptr_t s) {
+    kern::str_gather_lengths(P<const int64_t>(off), rows, P<const void>(idx), idx64, n, P<int64_t>(len), S(s));
   });
-  m.def("str_gather_copy", [](uintptr_t off, uintptr_t chars, uintptr_t idx, bool idx64, int64_t n, uintptr_t new_off,
-                              uintptr_t out, uintptr_t s) {
-    kern::str_gather_copy(P<const int64_t>(off), P<const uint8_t>(chars), P<const void>(idx), idx64, n,
-                          P<const int64_t>(new_off), P<uint8_t>(out), S(s));
+  m.def("str_gather_copy", [](uintptr_t off, int64_t rows, uintptr_t chars, uintptr_t idx, bool idx64, int64_t n,
+                              uintptr_t new_off, uintptr_t out, int64_t out_cap, uintptr_t s) {
+    kern::str_gather_copy(P<const int64_t>(off), rows, P<const uint8_t>(chars), P<const void>(idx), idx64, n,
+                          P<const int64_t>(new_off), P<uint8_t>(out), out_cap, S(s));
   });
 
   // ---------------------------------------------------------------- strings

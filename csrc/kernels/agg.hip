@@ -80,8 +80,11 @@ __device__ inline void init_state(int op, unsigned long long* lo, long long* hi)
   *hi = 0;
 }
 
-// merge an LDS/register state into the global output
+// merge an LDS/register state into the global output (a group id past the
+// state arrays -- a replayed group count below the real one -- is dropped;
+// the end-of-query check re-executes the query)
 __device__ inline void merge_global(const AggDesc& a, int64_t g, unsigned long long lo, long long hi) {
+  if (a.groups && (uint64_t)g >= (uint64_t)a.groups) return;
   unsigned long long* dlo = (unsigned long long*)a.dst + g;
   switch (a.op) {
     case AGG_SUM_INT:
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void agg_global_kernel(const int32_t* __res
     int64_t g = gid[i];
     for (int k = 0; k < p.nagg; ++k) {
       const AggDesc& a = p.d[k];
-      if (!row_valid(a, i)) continue;
+      if (!row_valid(a, i) || (uint64_t)g >= (uint64_t)a.groups) continue;
       upd(a, i, (unsigned long long*)a.dst + g, a.dst2 ? (long long*)a.dst2 + g : nullptr);
     }
   }
@@ -129,6 +132,7 @@ __global__ __launch_bounds__(kBlock) void agg_lds_kernel(const int32_t* __restri
   __syncthreads();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int g = gid ? gid[i] : 0;
+    if ((unsigned)g >= (unsigned)ngroups) continue;
     for (int k = 0; k < p.nagg; ++k) {
       const AggDesc& a = p.d[k];
       if (!row_valid(a, i)) continue;
@@ -206,6 +210,7 @@ __device__ inline void row_state(const AggDesc& a, int64_t i, bool live, unsigne
 }
 
 __device__ inline void store_exclusive(const AggDesc& a, int64_t g, unsigned long long lo, long long hi) {
+  if (a.groups && (uint64_t)g >= (uint64_t)a.groups) return;   // see merge_global
   ((unsigned long long*)a.dst)[g] = lo;
   if (a.op == AGG_SUM_INT && a.dst2) ((long long*)a.dst2)[g] = hi;
 }
@@ -1010,7 +1015,10 @@ void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs
   if (nagg > kMaxAggs) throw std::runtime_error("agg_update: too many aggregates in one launch");
   AggParams p;
   p.nagg = nagg;
-  for (int k = 0; k < nagg; ++k) p.d[k] = descs[k];
+  for (int k = 0; k < nagg; ++k) {
+    p.d[k] = descs[k];
+    p.d[k].groups = ngroups > 1 ? ngroups : 1;
+  }
   if (ngroups <= 1 || gid == nullptr) {
     hipLaunchKernelGGL(agg_single_kernel, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, stream, n, p);
     check_launch("agg_single", stream);

@@ -358,6 +358,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     ff_pass4<ff_vw<NC>()>(S, r0, r1, r2, r3, it, pass);
     int gid[kFfRows];
     ff_gid4<ff_vw<NC>()>(S, r0, r1, r2, r3, gid);
+    // a key outside the (possibly replayed) domain never indexes past the cells
+#pragma unroll
+    for (int j = 0; j < kFfRows; ++j) pass[j] = pass[j] && (unsigned)gid[j] < (unsigned)G;
     // per-row slot base (group g, this lane); aggregate a adds a * G cells
     int64_t* rowslot[kFfRows];
 #pragma unroll

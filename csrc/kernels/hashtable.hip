@@ -260,20 +260,23 @@ __global__ __launch_bounds__(kBlock) void join_expand_kernel(const K* __restrict
                                                             const R* __restrict__ crows, int64_t cap, int64_t kmin,
                                                             const int64_t* __restrict__ offsets,
                                                             int32_t* __restrict__ out_probe, R* __restrict__ out_build,
-                                                            const uint32_t* __restrict__ bits, uint64_t bmask) {
+                                                            const uint32_t* __restrict__ bits, uint64_t bmask,
+                                                            int64_t out_cap) {
+  // out_cap: pairs the outputs hold (sized by a possibly replayed total):
+  // writes past it are dropped; the end-of-query check rejects the run
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = probe_slot<K, DIRECT>(keys, valid, j, tkeys, cap, kmin, bits, bmask);
     if (s < 0) continue;
     int64_t o = offsets[j];
     if (cstart) {
       const int64_t e = cstart[s + 1];
-      for (int64_t r = cstart[s]; r < e; ++r, ++o) {
+      for (int64_t r = cstart[s]; r < e && o < out_cap; ++r, ++o) {
         out_probe[o] = (int32_t)j;
         out_build[o] = crows[r];
       }
     } else {
       const R h = thead[s];
-      if (h >= 0) {
+      if (h >= 0 && o < out_cap) {
         out_probe[o] = (int32_t)j;
         out_build[o] = h;
       }
@@ -341,12 +344,16 @@ __global__ __launch_bounds__(kBlock) void occupied_kernel(const int32_t* __restr
 
 // gid_of_slot[slots[g]] = g ; rep_row[g] = trow[slots[g]]
 template <typename S>
-__global__ __launch_bounds__(kBlock) void assign_gid_kernel(const S* __restrict__ slots, int64_t g,
+__global__ __launch_bounds__(kBlock) void assign_gid_kernel(const S* __restrict__ slots, int64_t g, int64_t cap,
                                                            const int32_t* __restrict__ trow,
                                                            int32_t* __restrict__ gid_of_slot,
                                                            int32_t* __restrict__ rep_row) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < g; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t s = (int64_t)slots[i];
+    if ((uint64_t)s >= (uint64_t)cap) {   // a replayed group count past the real one: unwritten slot ids
+      rep_row[i] = 0;
+      continue;
+    }
     gid_of_slot[s] = (int32_t)i;
     rep_row[i] = trow[s];
   }
@@ -371,7 +378,10 @@ template <typename I>
 __global__ __launch_bounds__(kBlock) void fill_runs_kernel(const I* __restrict__ starts, int64_t nruns, int64_t n,
                                                           int32_t* __restrict__ gid) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nruns; r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = starts[r], e = r + 1 < nruns ? (int64_t)starts[r + 1] : n;
+    int64_t b = starts[r], e = r + 1 < nruns ? (int64_t)starts[r + 1] : n;
+    // a replayed run count can leave the starts' tail unwritten: stay in [0, n)
+    b = b < 0 ? 0 : (b > n ? n : b);
+    e = e < b ? b : (e > n ? n : e);
     for (int64_t i = b; i < e; ++i) gid[i] = (int32_t)r;
   }
 }
@@ -480,17 +490,17 @@ void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, c
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const void* thead, const void* cstart, const void* crows, bool rid64, int64_t cap, int64_t kmin,
                  bool direct, const int64_t* offsets, int32_t* out_probe, void* out_build, const uint32_t* bits,
-                 uint64_t bmask, hipStream_t stream) {
+                 uint64_t bmask, int64_t out_cap, hipStream_t stream) {
   if (m == 0) return;
   dim3 g(grid_for(m, kBlock, kMaxGrid)), b(kBlock);
   if (rid64)
     DISPATCH_KEY3(key64, direct, int64_t, join_expand_kernel, g, b, 0, stream, keys, valid, m, tkeys,
                   (const int64_t*)thead, (const int64_t*)cstart, (const int64_t*)crows, cap, kmin, offsets, out_probe,
-                  (int64_t*)out_build, bits, bmask);
+                  (int64_t*)out_build, bits, bmask, out_cap);
   else
     DISPATCH_KEY3(key64, direct, int32_t, join_expand_kernel, g, b, 0, stream, keys, valid, m, tkeys,
                   (const int32_t*)thead, (const int32_t*)cstart, (const int32_t*)crows, cap, kmin, offsets, out_probe,
-                  (int32_t*)out_build, bits, bmask);
+                  (int32_t*)out_build, bits, bmask, out_cap);
   check_launch("join_expand", stream);
 }
 
@@ -523,14 +533,16 @@ void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, int32_t* g
   check_launch("groupby_occupied", stream);
 }
 
-void groupby_assign(const void* slots, bool slots64, int64_t g, const int32_t* trow, int32_t* gid_of_slot,
-                    int32_t* rep_row, hipStream_t stream) {
+void groupby_assign(const void* slots, bool slots64, int64_t g, int64_t cap, const int32_t* trow,
+                    int32_t* gid_of_slot, int32_t* rep_row, hipStream_t stream) {
   if (g == 0) return;
   dim3 gr(grid_for(g, kBlock, kMaxGrid)), b(kBlock);
   if (slots64)
-    hipLaunchKernelGGL(assign_gid_kernel<int64_t>, gr, b, 0, stream, (const int64_t*)slots, g, trow, gid_of_slot, rep_row);
+    hipLaunchKernelGGL(assign_gid_kernel<int64_t>, gr, b, 0, stream, (const int64_t*)slots, g, cap, trow, gid_of_slot,
+                       rep_row);
   else
-    hipLaunchKernelGGL(assign_gid_kernel<int32_t>, gr, b, 0, stream, (const int32_t*)slots, g, trow, gid_of_slot, rep_row);
+    hipLaunchKernelGGL(assign_gid_kernel<int32_t>, gr, b, 0, stream, (const int32_t*)slots, g, cap, trow, gid_of_slot,
+                       rep_row);
   check_launch("groupby_assign", stream);
 }
 
@@ -695,7 +707,8 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
                                                             const R* __restrict__ thead, int64_t cap,
                                                             int64_t kmin, const unsigned long long* __restrict__ words,
                                                             const int64_t* __restrict__ tile_off,
-                                                            O* __restrict__ out_probe, R* __restrict__ out_build) {
+                                                            O* __restrict__ out_probe, R* __restrict__ out_build,
+                                                            int64_t out_cap) {
   __shared__ int64_t woff[kHitWords];
   __shared__ int64_t scratch[kWavesPerBlock + 1];
   const int lane = lane_id(), wave = threadIdx.x / kWave;
@@ -728,6 +741,7 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
           if (row[r] >= m) continue;
           const int w = w0 + r * kWavesPerBlock;
           const int64_t pos = base + woff[w] + __popcll(b[r] & ((1ULL << lane) - 1ULL));
+          if (pos >= out_cap) continue;   // a replayed (undersized) total: see join_expand_kernel
           out_probe[pos] = (O)row[r];
           if (out_build) out_build[pos] = (R)h[r];
         }
@@ -757,44 +771,45 @@ void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, c
 template <typename R, typename O>
 static void probe_write_t(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                           const R* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
-                          const int64_t* tile_off, O* out_probe, R* out_build, hipStream_t stream) {
+                          const int64_t* tile_off, O* out_probe, R* out_build, int64_t out_cap, hipStream_t stream) {
   const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
   if (key64) {
     if (direct)
       hipLaunchKernelGGL((probe_write_kernel<int64_t, true, R, O>), g, b, 0, stream, (const int64_t*)keys, valid, m,
-                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build, out_cap);
     else
       hipLaunchKernelGGL((probe_write_kernel<int64_t, false, R, O>), g, b, 0, stream, (const int64_t*)keys, valid, m,
-                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build, out_cap);
   } else {
     if (direct)
       hipLaunchKernelGGL((probe_write_kernel<int32_t, true, R, O>), g, b, 0, stream, (const int32_t*)keys, valid, m,
-                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build, out_cap);
     else
       hipLaunchKernelGGL((probe_write_kernel<int32_t, false, R, O>), g, b, 0, stream, (const int32_t*)keys, valid, m,
-                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build);
+                         tkeys, thead, cap, kmin, words, tile_off, out_probe, out_build, out_cap);
   }
   check_launch("probe_write", stream);
 }
 
 void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
-                 const int64_t* tile_off, void* out_probe, bool out64, void* out_build, hipStream_t stream) {
+                 const int64_t* tile_off, void* out_probe, bool out64, void* out_build, int64_t out_cap,
+                 hipStream_t stream) {
   if (m == 0) return;
   if (rid64) {
     if (out64)
       probe_write_t<int64_t, int64_t>(keys, key64, valid, m, tkeys, (const int64_t*)thead, cap, kmin, direct, words,
-                                      tile_off, (int64_t*)out_probe, (int64_t*)out_build, stream);
+                                      tile_off, (int64_t*)out_probe, (int64_t*)out_build, out_cap, stream);
     else
       probe_write_t<int64_t, int32_t>(keys, key64, valid, m, tkeys, (const int64_t*)thead, cap, kmin, direct, words,
-                                      tile_off, (int32_t*)out_probe, (int64_t*)out_build, stream);
+                                      tile_off, (int32_t*)out_probe, (int64_t*)out_build, out_cap, stream);
   } else {
     if (out64)
       probe_write_t<int32_t, int64_t>(keys, key64, valid, m, tkeys, (const int32_t*)thead, cap, kmin, direct, words,
-                                      tile_off, (int64_t*)out_probe, (int32_t*)out_build, stream);
+                                      tile_off, (int64_t*)out_probe, (int32_t*)out_build, out_cap, stream);
     else
       probe_write_t<int32_t, int32_t>(keys, key64, valid, m, tkeys, (const int32_t*)thead, cap, kmin, direct, words,
-                                      tile_off, (int32_t*)out_probe, (int32_t*)out_build, stream);
+                                      tile_off, (int32_t*)out_probe, (int32_t*)out_build, out_cap, stream);
   }
 }
 }  // namespace kern

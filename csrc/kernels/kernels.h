@@ -189,18 +189,19 @@ void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, c
                 uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream);
 void probe_write(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
-                 const int64_t* tile_off, void* out_probe, bool out64, void* out_build, hipStream_t stream);
+                 const int64_t* tile_off, void* out_probe, bool out64, void* out_build, int64_t out_cap,
+                 hipStream_t stream);
 void join_expand(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                  const void* thead, const void* cstart, const void* crows, bool rid64, int64_t cap, int64_t kmin,
                  bool direct, const int64_t* offsets, int32_t* out_probe, void* out_build, const uint32_t* bits,
-                 uint64_t bmask, hipStream_t stream);
+                 uint64_t bmask, int64_t out_cap, hipStream_t stream);
 // run ids of a non-decreasing key column: gid[i] = r for rows in [starts[r], starts[r+1])
 void fill_runs(const void* starts, bool starts64, int64_t nruns, int64_t n, int32_t* gid, hipStream_t stream);
 void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int32_t* trow, int64_t cap, int64_t kmin,
                    bool direct, hipStream_t stream);
 void groupby_occupied(const int32_t* trow, int64_t cap, uint8_t* occ, int32_t* gid_of_slot, hipStream_t stream);
-void groupby_assign(const void* slots, bool slots64, int64_t g, const int32_t* trow, int32_t* gid_of_slot,
-                    int32_t* rep_row, hipStream_t stream);
+void groupby_assign(const void* slots, bool slots64, int64_t g, int64_t cap, const int32_t* trow,
+                    int32_t* gid_of_slot, int32_t* rep_row, hipStream_t stream);
 void groupby_lookup(const void* keys, bool key64, int64_t n, const int64_t* tkeys, const int32_t* gid_of_slot,
                     int64_t cap, int64_t kmin, bool direct, int32_t* gid, hipStream_t stream);
 
@@ -222,6 +223,7 @@ struct AggDesc {
   const uint8_t* valid;  // null = all rows valid
   void* dst;             // [ngroups] 8-byte states
   void* dst2;            // [ngroups] high words for AGG_SUM_INT
+  int64_t groups = 0;    // set by agg_update: states past it are never written (0: unchecked)
 };
 
 int agg_lds_max_groups(int nagg);
@@ -253,11 +255,14 @@ struct GatherDesc {
   int elem_bytes;  // 1, 2, 4, 8, 16
   const uint8_t* src_valid;
   uint8_t* dst_valid;  // null = do not produce validity
+  int64_t src_rows;    // indices outside [0, src_rows) gather NULL / zero (a replayed size can
+                       // leave an index buffer's tail unwritten: never read past the source)
 };
 void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* descs, int ncols, hipStream_t stream);
-void str_gather_lengths(const int64_t* off, const void* idx, bool idx64, int64_t n, int64_t* len, hipStream_t stream);
-void str_gather_copy(const int64_t* off, const uint8_t* chars, const void* idx, bool idx64, int64_t n,
-                     const int64_t* new_off, uint8_t* out, hipStream_t stream);
+void str_gather_lengths(const int64_t* off, int64_t src_rows, const void* idx, bool idx64, int64_t n, int64_t* len,
+                        hipStream_t stream);
+void str_gather_copy(const int64_t* off, int64_t src_rows, const uint8_t* chars, const void* idx, bool idx64,
+                     int64_t n, const int64_t* new_off, uint8_t* out, int64_t out_cap, hipStream_t stream);
 
 // ---- strings.hip ---------------------------------------------------------------
 void str_like(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* pat, const uint8_t* kind, int m,

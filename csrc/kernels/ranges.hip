@@ -259,7 +259,10 @@ __global__ __launch_bounds__(kBlock) void dense_index_kernel(const K* __restrict
     if (cur == prev) continue;
     int64_t k = cur - prev > kGapFill ? cur : prev + 1;
     if (k != prev + 1) *long_gap = 1;
-    for (; k <= cur; ++k) first[k - kmin] = (I)i;
+    // keys outside [kmin, kmax] (a replayed range narrower than the data)
+    // never index past the table's kmax - kmin + 2 entries
+    const int64_t hi = cur < kmax + 1 ? cur : kmax + 1;
+    for (k = k < kmin ? kmin : k; k <= hi; ++k) first[k - kmin] = (I)i;
   }
 }
 

@@ -34,6 +34,11 @@ struct DevWave {
   __device__ int64_t scan(int64_t v) const { return wave_inclusive_scan(v); }
   __device__ int64_t bcast(int64_t v, int k) const { return __shfl(v, k, kWave); }
   __device__ uint8_t ld(const uint8_t* p) const { return __builtin_nontemporal_load(p); }
+  // wave-uniform values: scalar registers, so the entropy decode runs on the scalar ALU
+  __device__ uint32_t uni(uint32_t v) const { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+  __device__ uint64_t uni64(uint64_t v) const {
+    return (uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32);
+  }
 };
 
 struct HostWave {
@@ -46,6 +51,8 @@ struct HostWave {
   int64_t scan(int64_t v) const { return v; }
   int64_t bcast(int64_t v, int) const { return v; }
   uint8_t ld(const uint8_t* p) const { return *p; }
+  uint32_t uni(uint32_t v) const { return v; }
+  uint64_t uni64(uint64_t v) const { return v; }
 };
 
 __global__ __launch_bounds__(kWave) void pq_zstd_kernel(const PqSnappyJob* __restrict__ jobs, int64_t njobs,

@@ -59,35 +59,70 @@ struct Scratch {
   int16_t norm[64];
   uint16_t next[64];
   uint8_t weights[256];
+  int32_t hcnt[16], hstart[16];    // Huffman weight counts / table starts
 };
 
-__host__ __device__ inline int hibit(uint32_t v) { return 31 - __builtin_clz(v); }
+// every decoder function is inlined into the kernel, so the decoder state and
+// bit readers live in registers (a call boundary would put them in scratch)
+#define ZINL __host__ __device__ __attribute__((always_inline)) inline
+
+ZINL int hibit(uint32_t v) { return 31 - __builtin_clz(v); }
 
 // baselines and extra bits of the literal-length / match-length codes
-__host__ __device__ inline void ll_code(int c, uint32_t* base, int* xb) {
+// (arithmetic + switch: no local arrays, which would live in scratch)
+ZINL void ll_code(int c, uint32_t* base, int* xb) {
   if (c < 16) {
     *base = c;
     *xb = 0;
-    return;
+  } else if (c >= 25) {
+    *xb = c - 19;
+    *base = 1u << (c - 19);
+  } else {
+    switch (c) {
+      case 16: *base = 16; *xb = 1; break;
+      case 17: *base = 18; *xb = 1; break;
+      case 18: *base = 20; *xb = 1; break;
+      case 19: *base = 22; *xb = 1; break;
+      case 20: *base = 24; *xb = 2; break;
+      case 21: *base = 28; *xb = 2; break;
+      case 22: *base = 32; *xb = 3; break;
+      case 23: *base = 40; *xb = 3; break;
+      default: *base = 48; *xb = 4; break;
+    }
   }
-  constexpr uint32_t B[20] = {16, 18, 20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384,
-                              32768, 65536};
-  constexpr uint8_t X[20] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-  *base = B[c - 16];
-  *xb = X[c - 16];
 }
-__host__ __device__ inline void ml_code(int c, uint32_t* base, int* xb) {
+ZINL void ml_code(int c, uint32_t* base, int* xb) {
   if (c < 32) {
     *base = c + 3;
     *xb = 0;
-    return;
+  } else if (c >= 43) {
+    *xb = c - 36;
+    *base = (1u << (c - 36)) + 3;
+  } else {
+    switch (c) {
+      case 32: *base = 35; *xb = 1; break;
+      case 33: *base = 37; *xb = 1; break;
+      case 34: *base = 39; *xb = 1; break;
+      case 35: *base = 41; *xb = 1; break;
+      case 36: *base = 43; *xb = 2; break;
+      case 37: *base = 47; *xb = 2; break;
+      case 38: *base = 51; *xb = 3; break;
+      case 39: *base = 59; *xb = 3; break;
+      case 40: *base = 67; *xb = 4; break;
+      case 41: *base = 83; *xb = 4; break;
+      default: *base = 99; *xb = 5; break;
+    }
   }
-  constexpr uint32_t B[21] = {35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195,
-                              16387, 32771, 65539};
-  constexpr uint8_t X[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-  *base = B[c - 32];
-  *xb = X[c - 32];
 }
+
+// predefined distributions (RFC 8878 3.1.1.3.2.2), at namespace scope so the
+// device reads them from constant memory
+constexpr int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
 // Wv: W (lanes), lane(), sync() (barrier), fence() (prior global stores
 // visible to the wave's later loads), any(bool), ballot(bool), scan(int64)
@@ -110,17 +145,17 @@ struct Decoder {
   int ll_log, of_log, ml_log;
   bool ll_ok, of_ok, ml_ok;
 
-  __host__ __device__ Decoder(Wv& w, Scratch& sc, const uint8_t* s_, int64_t sl, uint8_t* d, int64_t dc, uint8_t* l)
+  ZINL Decoder(Wv& w, Scratch& sc, const uint8_t* s_, int64_t sl, uint8_t* d, int64_t dc, uint8_t* l)
       : wv(w), s(sc), src(s_), slen(sl), dst(d), dcap(dc), lit(l), wlo(0), whi(0), op(0), frame0(0), err(ZE_OK),
         rep0(1), rep1(4), rep2(8), huf_log(0), ll_log(0), of_log(0), ml_log(0), ll_ok(false), of_ok(false),
         ml_ok(false) {}
 
-  __host__ __device__ void fail(int code) {
+  ZINL void fail(int code) {
     if (err == ZE_OK) err = code;
   }
 
   // ---- compressed bytes through the LDS window ------------------------------
-  __host__ __device__ void refill(int64_t lo) {
+  ZINL void refill(int64_t lo) {
     if (lo < 0) lo = 0;
     lo -= (int64_t)(((uintptr_t)(src + lo)) & 15);   // 16-byte aligned window start (never before src)
     if (lo < 0) lo = 0;
@@ -145,23 +180,32 @@ struct Decoder {
     whi = hi;
   }
   // forward / backward reads: the window is refilled ahead of / behind i
-  __host__ __device__ uint32_t fb(int64_t i) {
+  ZINL uint32_t fb(int64_t i) {
     if (i < 0 || i >= slen) {
       fail(ZE_CORRUPT);
       return 0;
     }
     if (i < wlo || i >= whi) refill(i);
-    return s.win[i - wlo];
+    return wv.uni(s.win[i - wlo]);
   }
-  __host__ __device__ uint32_t bb(int64_t i) {
+  ZINL uint32_t bb(int64_t i) {
     if (i < 0 || i >= slen) {
       fail(ZE_CORRUPT);
       return 0;
     }
     if (i < wlo || i >= whi) refill(i - kWin + 64);
-    return s.win[i - wlo];
+    return wv.uni(s.win[i - wlo]);
   }
-  __host__ __device__ uint64_t le(int64_t i, int n) {
+  // a table entry, made wave-uniform (scalar registers and scalar ALU on the GPU)
+  ZINL SeqEntry ent(const SeqEntry* t, uint32_t st) {
+    uint64_t raw;
+    __builtin_memcpy(&raw, &t[st], 8);
+    raw = wv.uni64(raw);
+    SeqEntry e;
+    __builtin_memcpy(&e, &raw, 8);
+    return e;
+  }
+  ZINL uint64_t le(int64_t i, int n) {
     uint64_t v = 0;
     for (int k = 0; k < n; ++k) v |= (uint64_t)fb(i + k) << (8 * k);
     return v;
@@ -174,7 +218,7 @@ struct Decoder {
     uint64_t c;
     int k;
   };
-  __host__ __device__ bool back_init(Back& b, int64_t base, int64_t len) {
+  ZINL bool back_init(Back& b, int64_t base, int64_t len) {
     if (len <= 0) {
       fail(ZE_CORRUPT);
       return false;
@@ -192,25 +236,25 @@ struct Decoder {
     b.k = h;
     return true;
   }
-  __host__ __device__ void back_fill(Back& b) {
+  ZINL void back_fill(Back& b) {
     while (b.k <= 56 && b.low > 0) {
       b.low -= 8;
       b.c = (b.c << 8) | bb(b.base + (b.low >> 3));
       b.k += 8;
     }
   }
-  __host__ __device__ uint32_t peek(Back& b, int n) {  // n in [1, 32]
+  ZINL uint32_t peek(Back& b, int n) {  // n in [1, 32]
     if (b.k < n) back_fill(b);
     const uint64_t m = (1ull << n) - 1ull;
     if (b.k >= n) return (uint32_t)((b.c >> (b.k - n)) & m);
     return (uint32_t)((b.c << (n - b.k)) & m);   // past the stream start: zeros
   }
-  __host__ __device__ void skip(Back& b, int n) {
+  ZINL void skip(Back& b, int n) {
     b.k -= n;
     b.pos -= n;
     if (b.k < 0) b.k = 0;
   }
-  __host__ __device__ uint32_t read(Back& b, int n) {
+  ZINL uint32_t read(Back& b, int n) {
     if (n <= 0) return 0;
     const uint32_t v = peek(b, n);
     skip(b, n);
@@ -219,7 +263,7 @@ struct Decoder {
 
   // ---- FSE tables -------------------------------------------------------------
   // Normalized counts at [p, limit): accuracy log (or -1), symbols, bytes used.
-  __host__ __device__ int read_ncount(int64_t p, int64_t limit, int max_sym, int max_log, int* nsym, int* used) {
+  ZINL int read_ncount(int64_t p, int64_t limit, int max_sym, int max_log, int* nsym, int* used) {
     int64_t bit = 0;
     auto get = [&](int n) -> uint32_t {
       const int64_t q = p + (bit >> 3);
@@ -268,7 +312,7 @@ struct Decoder {
   }
 
   // Decoding table from s.norm[0, nsym) (kind 0: plain symbols, 1: LL, 2: ML, 3: OF).
-  __host__ __device__ bool build(int nsym, int al, SeqEntry* t, int kind) {
+  ZINL bool build(int nsym, int al, SeqEntry* t, int kind) {
     const int size = 1 << al;
     int high = size - 1;
     for (int x = 0; x < nsym; ++x) {
@@ -317,7 +361,7 @@ struct Decoder {
     return true;
   }
 
-  __host__ __device__ void rle_table(SeqEntry* t, int x, int kind) {
+  ZINL void rle_table(SeqEntry* t, int x, int kind) {
     SeqEntry e;
     e.nb = 0;
     e.base = 0;
@@ -333,13 +377,8 @@ struct Decoder {
     wv.sync();
   }
 
-  __host__ __device__ bool predefined(int kind) {
-    constexpr int16_t LL[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
-                                2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
-    constexpr int16_t ML[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
-    constexpr int16_t OF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
-    const int16_t* d = kind == 1 ? LL : kind == 2 ? ML : OF;
+  ZINL bool predefined(int kind) {
+    const int16_t* d = kind == 1 ? kLLNorm : kind == 2 ? kMLNorm : kOFNorm;
     const int n = kind == 1 ? 36 : kind == 2 ? 53 : 29;
     for (int i = 0; i < n; ++i) s.norm[i] = d[i];
     return build(n, kind == 3 ? 5 : 6, kind == 1 ? s.ll : kind == 2 ? s.ml : s.of, kind);
@@ -347,7 +386,7 @@ struct Decoder {
 
   // ---- Huffman --------------------------------------------------------------
   // Tree description at p: bytes used, or -1.
-  __host__ __device__ int64_t read_huffman(int64_t p, int64_t limit) {
+  ZINL int64_t read_huffman(int64_t p, int64_t limit) {
     const uint32_t hb = fb(p);
     int nw = 0;
     int64_t used;
@@ -362,16 +401,18 @@ struct Decoder {
       uint32_t s1 = read(b, al), s2 = read(b, al);
       for (;;) {
         if (nw > 253) return -1;
-        s.weights[nw++] = (uint8_t)s.wt[s1].val;
-        s1 = s.wt[s1].base + read(b, s.wt[s1].nb);
+        const SeqEntry e1 = ent(s.wt, s1);
+        s.weights[nw++] = (uint8_t)e1.val;
+        s1 = e1.base + read(b, e1.nb);
         if (b.pos < 0) {
-          s.weights[nw++] = (uint8_t)s.wt[s2].val;
+          s.weights[nw++] = (uint8_t)ent(s.wt, s2).val;
           break;
         }
-        s.weights[nw++] = (uint8_t)s.wt[s2].val;
-        s2 = s.wt[s2].base + read(b, s.wt[s2].nb);
+        const SeqEntry e2 = ent(s.wt, s2);
+        s.weights[nw++] = (uint8_t)e2.val;
+        s2 = e2.base + read(b, e2.nb);
         if (b.pos < 0) {
-          s.weights[nw++] = (uint8_t)s.wt[s1].val;
+          s.weights[nw++] = (uint8_t)ent(s.wt, s1).val;
           break;
         }
       }
@@ -398,9 +439,9 @@ struct Decoder {
     if (left == 0 || (left & (left - 1)) || maxb > kMaxHufLog) return -1;
     s.weights[nw++] = (uint8_t)(hibit(left) + 1);
     // canonical table: lower weights (longer codes) first, by symbol within a weight
-    int start[kMaxHufLog + 2];
-    int cnt[kMaxHufLog + 2];
-    for (int w = 0; w <= kMaxHufLog + 1; ++w) cnt[w] = 0;
+    int32_t* cnt = s.hcnt;
+    int32_t* start = s.hstart;
+    for (int w = 0; w < 16; ++w) cnt[w] = 0;
     for (int i = 0; i < nw; ++i) cnt[s.weights[i]]++;
     int nxt = 0;
     for (int w = 1; w <= maxb; ++w) {
@@ -413,9 +454,11 @@ struct Decoder {
       const int w = s.weights[x];
       if (!w) continue;
       const int len = 1 << (w - 1);
+      const int st = start[w];
       const uint16_t e = (uint16_t)((x << 8) | (maxb + 1 - w));
-      for (int k = wv.lane(); k < len; k += Wv::W) s.huf[start[w] + k] = e;
-      start[w] += len;
+      for (int k = wv.lane(); k < len; k += Wv::W) s.huf[st + k] = e;
+      wv.sync();
+      start[w] = st + len;
     }
     wv.sync();
     huf_log = maxb;
@@ -423,14 +466,14 @@ struct Decoder {
   }
 
   // One Huffman stream [q, q + len) -> `count` literals at out.
-  __host__ __device__ bool huf_stream(int64_t q, int64_t len, int64_t count, uint8_t* out) {
+  ZINL bool huf_stream(int64_t q, int64_t len, int64_t count, uint8_t* out) {
     Back b;
     if (!back_init(b, q, len)) return false;
     const int lane = wv.lane();
     uint32_t mine = 0;
     const int hl = huf_log;
     for (int64_t i = 0; i < count; ++i) {
-      const uint16_t e = s.huf[peek(b, hl)];
+      const uint32_t e = wv.uni(s.huf[peek(b, hl)]);
       skip(b, e & 0xff);
       if (lane == (int)(i & (Wv::W - 1))) mine = e >> 8;
       if ((i & (Wv::W - 1)) == Wv::W - 1) out[i - (Wv::W - 1) + lane] = (uint8_t)mine;
@@ -441,27 +484,27 @@ struct Decoder {
   }
 
   // ---- output -----------------------------------------------------------------
-  __host__ __device__ void put(int64_t o, uint8_t v) {
+  ZINL void put(int64_t o, uint8_t v) {
     dst[o] = v;
     s.ring[o & (kRing - 1)] = v;
   }
   // output byte p while executing a batch ending at `end`
-  __host__ __device__ uint8_t got(int64_t p, int64_t end) {
+  ZINL uint8_t got(int64_t p, int64_t end) {
     return p >= end - kRing ? s.ring[p & (kRing - 1)] : wv.ld(dst + p);
   }
 
   // whole-wave copies (raw blocks, long literals, RLE)
-  __host__ __device__ void copy_in(const uint8_t* from, int64_t n, bool written) {
+  ZINL void copy_in(const uint8_t* from, int64_t n, bool written) {
     for (int64_t k = wv.lane(); k < n; k += Wv::W) put(op + k, written ? wv.ld(from + k) : from[k]);
     op += n;
   }
-  __host__ __device__ void fill(uint8_t v, int64_t n) {
+  ZINL void fill(uint8_t v, int64_t n) {
     for (int64_t k = wv.lane(); k < n; k += Wv::W) put(op + k, v);
     op += n;
   }
 
   // A batch of n <= W sequences (lane k holds sequence k).
-  __host__ __device__ bool exec_batch(int n, int64_t ll, int64_t ml, int64_t off, const uint8_t* lsrc, bool lwritten,
+  ZINL bool exec_batch(int n, int64_t ll, int64_t ml, int64_t off, const uint8_t* lsrc, bool lwritten,
                                       int64_t* lused, int64_t lsize) {
     const int lane = wv.lane();
     const bool act = lane < n;
@@ -486,18 +529,19 @@ struct Decoder {
       for (int64_t b = 0; b < ll; ++b) put(opos + b, lwritten ? wv.ld(lsrc + lpos + b) : lsrc[lpos + b]);
     if (act && !dep && !mlong)
       for (int64_t b = 0; b < ml; ++b) put(opos + ll + b, got(ms + b, bend));
-    // 2. in order, whole wave: long literals, dependent or long matches
-    const uint64_t lits2 = wv.ballot(llong), mats2 = wv.ballot(dep || mlong);
-    for (uint64_t todo = lits2 | mats2; todo; todo &= todo - 1) {
+    // 2. in order: long literals and long matches by the whole wave, short
+    //    dependent matches by their own lane (its ring reads see the earlier
+    //    elements' writes: one wave's LDS operations complete in order)
+    const uint64_t wl = wv.ballot(llong), wm = wv.ballot(mlong), sd = wv.ballot(dep && !mlong);
+    for (uint64_t todo = wl | wm | sd; todo; todo &= todo - 1) {
       const int k = __builtin_ctzll(todo);
-      const bool a = (lits2 >> k) & 1, m = (mats2 >> k) & 1;
-      const int64_t kl = wv.bcast(ll, k), km = wv.bcast(ml, k), ko = wv.bcast(opos, k);
-      if (a) {
-        wv.sync();
-        const int64_t kp = wv.bcast(lpos, k);
+      if ((wl >> k) & 1) {
+        const int64_t kl = wv.bcast(ll, k), ko = wv.bcast(opos, k), kp = wv.bcast(lpos, k);
         for (int64_t b = lane; b < kl; b += Wv::W) put(ko + b, lwritten ? wv.ld(lsrc + kp + b) : lsrc[kp + b]);
+        wv.sync();
       }
-      if (m) {
+      if ((wm >> k) & 1) {
+        const int64_t kl = wv.bcast(ll, k), km = wv.bcast(ml, k), ko = wv.bcast(opos, k);
         const int64_t kof = wv.bcast(off, k), kms = ko + kl - kof;
         if (kms < bend - kRing) wv.fence();
         wv.sync();
@@ -506,6 +550,8 @@ struct Decoder {
           put(ko + kl + b, got(kms + j, bend));
         }
         wv.sync();
+      } else if (((sd >> k) & 1) && lane == k) {
+        for (int64_t b = 0; b < ml; ++b) put(opos + ll + b, got(ms + (off >= ml ? b : b % off), bend));
       }
     }
     wv.sync();
@@ -515,7 +561,7 @@ struct Decoder {
   }
 
   // ---- blocks -----------------------------------------------------------------
-  __host__ __device__ bool table(int mode, int kind, int64_t* p, int64_t end) {
+  ZINL bool table(int mode, int kind, int64_t* p, int64_t end) {
     SeqEntry* t = kind == 1 ? s.ll : kind == 2 ? s.ml : s.of;
     int* lg = kind == 1 ? &ll_log : kind == 2 ? &ml_log : &of_log;
     bool* ok = kind == 1 ? &ll_ok : kind == 2 ? &ml_ok : &of_ok;
@@ -542,7 +588,7 @@ struct Decoder {
     return true;
   }
 
-  __host__ __device__ bool block(int64_t p, int64_t end) {
+  ZINL bool block(int64_t p, int64_t end) {
     // -- literals section
     const uint32_t b0 = fb(p);
     const int ltype = b0 & 3, sf = (b0 >> 2) & 3;
@@ -647,7 +693,7 @@ struct Decoder {
         int n = 0;
         int64_t bout = 0, my_ll = 0, my_ml = 0, my_off = 0;
         while (i < nseq && n < Wv::W) {
-          const SeqEntry eo = s.of[so], em = s.ml[sm], el = s.ll[sl];
+          const SeqEntry eo = ent(s.of, so), em = ent(s.ml, sm), el = ent(s.ll, sl);
           const int64_t ofv = (int64_t)eo.val + read(b, eo.xb);
           const int64_t mlv = (int64_t)em.val + read(b, em.xb);
           const int64_t llv = (int64_t)el.val + read(b, el.xb);
@@ -706,7 +752,7 @@ struct Decoder {
   }
 
   // Whole input: frames (skippable ones skipped). Returns an error code.
-  __host__ __device__ int run() {
+  ZINL int run() {
     int64_t ip = 0;
     while (ip < slen && !err) {
       const uint32_t magic = (uint32_t)le(ip, 4);

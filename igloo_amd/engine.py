@@ -700,11 +700,23 @@ class QueryEngine:
         for attempt in range(3):
             sp = _lib.Speculation("replay" if replay else "record", st["log"] if replay else None)
             _lib.set_speculation(sp)
+            failed = None
             try:
                 batch = self._execute_plan(plan, ctx, fold_checks=True)
+            except Exception as e:  # noqa: BLE001 - re-raised unless a replayed value caused it
+                # a replayed value that does not match the data can also stop
+                # the host side of a query (a shape or range it cannot hold):
+                # on one rank that is a mismatch like any other -- re-execute
+                # with real readbacks. (SPMD ranks re-raise: the others may be
+                # inside a collective this rank will not reach.)
+                if sp.mode != "replay" or comm is not None:
+                    raise
+                failed = e
             finally:
                 _lib.set_speculation(None)
-            ok = sp.validate()
+            ok = failed is None and sp.validate()
+            if failed is not None:
+                log.warning("replayed readbacks stopped the query (%s); re-executing", failed)
             # would this rank capture next time (a complete replay, or a
             # recording confirmed by this run)? Agreed with the validation:
             # ranks capture only together

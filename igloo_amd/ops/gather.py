@@ -80,14 +80,15 @@ def _take_strings_gpu(cols: Sequence[Column], idx: torch.Tensor) -> List[Column]
     offs = []
     for col in cols:
         lens = torch.empty(n, dtype=torch.int64, device=idx.device)
-        N.str_gather_lengths(ptr(col.offsets), ptr(idx), idx64, n, ptr(lens), s)
+        N.str_gather_lengths(ptr(col.offsets), len(col), ptr(idx), idx64, n, ptr(lens), s)
         offs.append(offsets_from_lengths(lens, host_total=False)[0])
     totals = to_host_ints(torch.cat([o[-1:] for o in offs]) if len(offs) > 1 else offs[0][-1:])
     out = []
     for col, new_off, total in zip(cols, offs, totals):
         chars = torch.empty(max(total, 0), dtype=torch.uint8, device=idx.device)
         if total:
-            N.str_gather_copy(ptr(col.offsets), ptr(col.data), ptr(idx), idx64, n, ptr(new_off), ptr(chars), s)
+            N.str_gather_copy(ptr(col.offsets), len(col), ptr(col.data), ptr(idx), idx64, n, ptr(new_off),
+                              ptr(chars), chars.numel(), s)
         out.append(Column(col.dtype, chars, None, offsets=new_off))
     return out
 
@@ -112,7 +113,9 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
     n = idx.numel()
     gpu = is_gpu(idx)
     out: List[Column] = []
-    descs = []      # GPU: (src, dst, elem_bytes, src_valid, dst_valid) -> one gather_multi launch
+    # GPU: (src, dst, elem_bytes, src_valid, dst_valid, src_rows) -> one gather_multi launch; indices
+    # outside the source (a replayed size can leave an index tail unwritten) gather NULL / zero
+    descs = []
     keepalive = []  # temporaries that must outlive the (stream-ordered) launch
     strs = [c for c in cols if c.is_plain_string]
     pre = iter(_take_strings_gpu(strs, idx) if gpu and strs else [])
@@ -128,7 +131,7 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
                         keepalive.append(src)
                     v = torch.empty(n, dtype=torch.bool, device=idx.device)
                     # validity gathered as a byte column; idx < 0 writes 0 = NULL
-                    descs.append((_src_ptr(src), ptr(v), 1, 0, 0))
+                    descs.append((_src_ptr(src), ptr(v), 1, 0, 0, src.numel()))
                 else:
                     base = c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool)
                     v = _cpu_take_tensor(base, idx, neg)
@@ -146,7 +149,7 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
         data = torch.empty((n,) + tuple(c.data.shape[1:]), dtype=c.data.dtype, device=idx.device)
         esz = c.data.element_size() * (c.data.shape[1] if c.data.dim() == 2 else 1)
         valid = torch.empty(n, dtype=torch.bool, device=idx.device) if need_valid else None
-        descs.append((_src_ptr(c.data), ptr(data), esz, _src_ptr(c.valid), ptr(valid)))
+        descs.append((_src_ptr(c.data), ptr(data), esz, _src_ptr(c.valid), ptr(valid), c.data.shape[0]))
         if not neg:
             _inherit(data, c.data)
             if getattr(idx, "_igloo_incr", False) and getattr(c.data, "_igloo_distinct", False):
@@ -169,8 +172,8 @@ def gather_tensor(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=idx.device)
     if n:
         esz = t.element_size() * (t.shape[1] if t.dim() == 2 else 1)
-        launch("gather_multi").gather_multi(ptr(idx), idx.dtype == torch.int64, n, [(ptr(t), ptr(out), esz, 0, 0)],
-                                            stream(idx))
+        launch("gather_multi").gather_multi(ptr(idx), idx.dtype == torch.int64, n,
+                                            [(ptr(t), ptr(out), esz, 0, 0, t.shape[0])], stream(idx))
     _inherit(out, t)
     return out
 

@@ -312,7 +312,8 @@ class JoinTable:
         bidx = torch.empty(total, dtype=self.rid, device=dev) if want_build and not negate else None
         if total:
             N.probe_write(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
-                          self.kmin, self.direct, ptr(words), ptr(toff), ptr(pidx), it == torch.int64, ptr(bidx), st)
+                          self.kmin, self.direct, ptr(words), ptr(toff), ptr(pidx), it == torch.int64, ptr(bidx),
+                          pidx.numel(), st)
         return pidx, bidx
 
     def probe_pairs(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
@@ -354,7 +355,7 @@ class JoinTable:
             launch("join_expand")
             N.join_expand(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), ptr(self.cstart),
                           ptr(self.crows), self.rid64, self.cap, self.kmin, self.direct, ptr(offsets), ptr(pidx),
-                          ptr(bidx), bits, bmask, s)
+                          ptr(bidx), bits, bmask, pidx.numel(), s)
         return pidx, bidx, counts
 
     def _bloom(self, m: int) -> Tuple[int, int]:
@@ -691,7 +692,7 @@ def group_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, int, torch.Tensor]:
     slots = mask_to_indices(occ)
     g = slots.numel()
     rep = torch.empty(g, dtype=torch.int32, device=dev)
-    N.groupby_assign(ptr(slots), slots.dtype == torch.int64, g, ptr(trow), ptr(gid_of_slot), ptr(rep), s)
+    N.groupby_assign(ptr(slots), slots.dtype == torch.int64, g, cap, ptr(trow), ptr(gid_of_slot), ptr(rep), s)
     gid = torch.empty(n, dtype=torch.int32, device=dev)
     N.groupby_lookup(ptr(keys), k64, n, ptr(tkeys), ptr(gid_of_slot), cap, kmin, direct, ptr(gid), s)
     if not direct and g > 1:
