@@ -532,7 +532,11 @@ struct Decoder {
     // 2. in order: long literals and long matches by the whole wave, short
     //    dependent matches by their own lane (its ring reads see the earlier
     //    elements' writes: one wave's LDS operations complete in order)
-    const uint64_t wl = wv.ballot(llong), wm = wv.ballot(mlong), sd = wv.ballot(dep && !mlong);
+    // (one lane copies a dependent match of at most kLane bytes; longer ones
+    // take the whole wave, 64 bytes per step)
+    constexpr int64_t kLane = 8;
+    const uint64_t wl = wv.ballot(llong), wm = wv.ballot(mlong || (dep && ml > kLane)),
+                   sd = wv.ballot(dep && ml <= kLane);
     for (uint64_t todo = wl | wm | sd; todo; todo &= todo - 1) {
       const int k = __builtin_ctzll(todo);
       if ((wl >> k) & 1) {
