@@ -67,8 +67,8 @@ _MODE_TAG = {"recorded": "R", "replayed": "P", "graph": "G", "partial": "x"}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--sf", type=float, default=100.0)
     ap.add_argument("--queries", default="1-22")
     ap.add_argument("--source", choices=["parquet", "hbm"], default="parquet")
