@@ -498,7 +498,7 @@ class QueryEngine:
         and recomputes everything from the tables (scalar subqueries included)."""
         bq_names = names
         ctx = self.make_context()
-        c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
+        c0 = (self.comm.calls, self.comm.bytes_sent, self.comm.chunk_calls) if self.comm is not None else (0, 0, 0)
         from .ops._lib import HOST_STEPS, READBACKS
         h0 = sum(HOST_STEPS.values())
         r0 = READBACKS[0]
@@ -550,7 +550,9 @@ class QueryEngine:
                                        "hit_ratio": round(hits / (hits + misses), 4) if hits + misses else None},
                              **dev_metrics}
         if self.comm is not None:
-            self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1])
+            # ``exchanges``: collectives with each pipelined exchange's chunks counted once
+            self.last_metrics.update(collectives=self.comm.calls - c0[0], exchange_bytes=self.comm.bytes_sent - c0[1],
+                                     exchanges=(self.comm.calls - c0[0]) - (self.comm.chunk_calls - c0[2]))
         return QueryResult(table, ms)
 
     def explain_fragments(self, sql: str, workers=("all-ranks",)) -> str:
@@ -663,6 +665,7 @@ class QueryEngine:
             g.launch(ctx)
             if comm is not None:
                 comm.calls += g.comm_calls
+                comm.chunk_calls += g.comm_chunks
                 comm.bytes_sent += g.comm_bytes
             self._touch_graph(st)
             st["pending_guard"] = g.bad
@@ -680,6 +683,7 @@ class QueryEngine:
                     st["graph_aborts"] = 2
             if comm is not None:
                 comm.calls += g.comm_calls
+                comm.chunk_calls += g.comm_chunks
                 comm.bytes_sent += g.comm_bytes
             # a checked graph's mismatch count is already summed over the ranks
             # inside the graph: every rank read the same value
@@ -761,7 +765,7 @@ class QueryEngine:
         """Capture ``plan`` under a replay of ``st``'s recording into a query graph."""
         if st["digest"] is None:
             return False
-        c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
+        c0 = (self.comm.calls, self.comm.bytes_sent, self.comm.chunk_calls) if self.comm is not None else (0, 0, 0)
         with _trace.Range("graph.capture"):
             g = _graphs.capture(self, plan, st["log"], self.make_context)
         if g is None:
@@ -769,6 +773,7 @@ class QueryEngine:
         if self.comm is not None:
             # collectives recorded into the graph (counted again on every replay)
             g.comm_calls, g.comm_bytes = self.comm.calls - c0[0], self.comm.bytes_sent - c0[1]
+            g.comm_chunks = self.comm.chunk_calls - c0[2]
             self.comm.calls, self.comm.bytes_sent = c0
         self._set_graph(st, g)
         return True
@@ -894,7 +899,7 @@ class QueryEngine:
             from .ops._lib import HOST_STEPS
             ctx = self.make_context(analyze=True)
             ctx.slices = self._slices_for(logical)
-            c0 = (self.comm.calls, self.comm.bytes_sent) if self.comm is not None else (0, 0)
+            c0 = (self.comm.calls, self.comm.bytes_sent, self.comm.chunk_calls) if self.comm is not None else (0, 0, 0)
             h0 = dict(HOST_STEPS)
             t0 = time.perf_counter()
             node.execute(ctx)

@@ -88,12 +88,13 @@ class QueryGraph:
     mismatch counter of its replayed values."""
 
     __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp",
-                 "nbytes", "comm_calls", "comm_bytes", "keep", "global_check")
+                 "nbytes", "comm_calls", "comm_bytes", "comm_chunks", "keep", "global_check")
 
     def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None, nbytes=0):
         self.sp = sp                   # the capture's speculation (sites + device values, for reports)
         self.nbytes = nbytes           # device bytes of the graph's private memory pool
         self.comm_calls = 0            # collectives inside the graph (SPMD)
+        self.comm_chunks = 0           # ... of which pipelined-exchange chunks past each exchange's first
         self.comm_bytes = 0
         self.keep = []
         self.global_check = False      # ``bad`` is summed over SPMD ranks inside the graph

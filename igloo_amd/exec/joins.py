@@ -1362,6 +1362,30 @@ class MultiJoinExec(ExecNode):
         eng = ctx.engine
         cache = getattr(eng, "_gndv", None) if eng is not None else None
         ver = (eng.catalog.version, eng.cache.generation) if cache is not None else None
+        # a repeated execution of this (cached) plan over unchanged data sees
+        # the same inputs: its global counts and NDVs are reused and the
+        # collective is skipped -- alike on every rank, since the key follows
+        # from the plan, the catalog and the cache generation only
+        memos = getattr(eng, "_join_stats_memo", None) if ver is not None else None
+        if eng is not None and ver is not None and memos is None:
+            memos = eng._join_stats_memo = {}
+        mkey = (id(self.logical), ver, len(batches), tuple(e.sql() for _, e in need))
+        memo = memos.get(mkey) if memos is not None else None
+        if memo is not None and memo[0] is self.logical:
+            for (rel, e), v in zip(need, memo[2]):
+                rel["ndv"][e.sql()] = v
+            return list(memo[1])
+        counts = self._spmd_stats_collect(batches, need, ctx, rels, comm, local, cache, ver)
+        if memos is not None:
+            if len(memos) > 1024:
+                memos.clear()
+            # (the logical node is kept with its entry: an id reused after it
+            # is freed never matches)
+            memos[mkey] = (self.logical, list(counts), [rel["ndv"][e.sql()] for rel, e in need])
+        return counts
+
+    def _spmd_stats_collect(self, batches, need, ctx, rels, comm, local, cache, ver) -> List[int]:
+        """The collective of ``_spmd_stats``."""
         plan = []      # per need: (kind, cache key, rel index)
         for rel, e in need:
             ri = next((i for i, r in enumerate(rels) if r is rel), None)

@@ -46,6 +46,8 @@ class Communicator:
         self.wire = torch.device("cpu") if backend == "gloo" else self.device
         self.bytes_sent = 0
         self.calls = 0
+        self.chunk_calls = 0     # of ``calls``: the 2nd.. chunks of pipelined exchanges (one logical exchange each)
+        self.trace = [] if os.environ.get("IGLOO_TRACE_COLLECTIVES") else None
 
     # ------------------------------------------------------------- lifecycle
     @staticmethod
@@ -94,7 +96,7 @@ class Communicator:
         lives, destroy_process_group does not return."""
         if dist.is_initialized():
             try:
-                self.calls += 1
+                self._count()
                 dist.barrier()
             except Exception:  # pragma: no cover
                 pass
@@ -110,11 +112,21 @@ class Communicator:
             return device_ints(x, self.wire, dtype)     # no sync; capture-safe
         return torch.as_tensor(x, dtype=dtype, device=self.wire)
 
+    def _count(self):
+        """One collective issued (``calls``); IGLOO_TRACE_COLLECTIVES=1 also
+        records the engine call site that issued it (``trace``)."""
+        self.calls += 1
+        if self.trace is not None:
+            import traceback
+            st = [f for f in traceback.extract_stack()[:-2] if "parallel/comm.py" not in f.filename]
+            site = " <- ".join(f"{f.filename.split('igloo_amd/')[-1]}:{f.lineno}({f.name})" for f in st[-3:][::-1])
+            self.trace.append(site)
+
     def barrier(self):
         if faults.ACTIVE:
             faults.check("comm_timeout", "barrier")
         if self.spmd:
-            self.calls += 1
+            self._count()
             dist.barrier(group=self.group)
 
     def allreduce_int(self, x: int) -> int:
@@ -123,7 +135,7 @@ class Communicator:
         if not self.spmd:
             return int(x)
         t = self._t([int(x)])
-        self.calls += 1
+        self._count()
         dist.all_reduce(t, group=self.group)
         return to_host_ints(t)[0]
 
@@ -133,7 +145,7 @@ class Communicator:
         if not self.spmd:
             return [int(x) for x in xs]
         t = self._t([int(x) for x in xs])
-        self.calls += 1
+        self._count()
         dist.all_reduce(t, group=self.group)
         return to_host_ints(t)
 
@@ -143,7 +155,7 @@ class Communicator:
         if not self.spmd:
             return float(x)
         t = self._t([float(x)], torch.float64)
-        self.calls += 1
+        self._count()
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return to_host_f64s(t)[0]
 
@@ -154,7 +166,7 @@ class Communicator:
         if not self.spmd:
             return t
         w = t.to(device=self.wire, dtype=torch.int32)
-        self.calls += 1
+        self._count()
         dist.all_reduce(w, op=dist.ReduceOp.MAX, group=self.group)
         return w.to(device=t.device, dtype=t.dtype)
 
@@ -167,7 +179,7 @@ class Communicator:
         w = t.contiguous().to(self.wire)
         if w is t:
             w = w.clone()
-        self.calls += 1
+        self._count()
         dist.all_reduce(w, op={"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op],
                         group=self.group)
         self.bytes_sent += w.numel() * w.element_size()
@@ -186,7 +198,7 @@ class Communicator:
             return t[0]
         src = t.contiguous().to(self.wire).reshape(-1)        # [world * block], block-major
         out = torch.empty(src.numel() // self.world_size, dtype=src.dtype, device=self.wire)
-        self.calls += 1
+        self._count()
         dist.reduce_scatter_tensor(out, src, op={"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN,
                                                   "max": dist.ReduceOp.MAX}[op], group=self.group)
         self.bytes_sent += src.numel() * src.element_size() * (self.world_size - 1) // max(self.world_size, 1)
@@ -201,7 +213,7 @@ class Communicator:
             return [list(map(int, xs))]
         t = self._t([int(x) for x in xs])
         out = torch.empty(self.world_size * k, dtype=torch.int64, device=self.wire)
-        self.calls += 1
+        self._count()
         dist.all_gather_into_tensor(out, t, group=self.group)
         v = to_host_ints(out)
         return [v[r * k:(r + 1) * k] for r in range(self.world_size)]
@@ -215,7 +227,7 @@ class Communicator:
             return t
         src = t.contiguous().to(self.wire)
         out = torch.empty((self.world_size * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=self.wire)
-        self.calls += 1
+        self._count()
         dist.all_gather_into_tensor(out, src, group=self.group)
         self.bytes_sent += src.numel() * src.element_size() * (self.world_size - 1)
         return out.to(t.device)
@@ -226,7 +238,7 @@ class Communicator:
         if not self.spmd:
             return [obj]
         out = [None] * self.world_size
-        self.calls += 1
+        self._count()
         dist.all_gather_object(out, obj, group=self.group)
         return out
 
@@ -247,7 +259,7 @@ class Communicator:
         if src.dtype == torch.bool:
             src = src.view(torch.uint8)
             out = out.view(torch.uint8)
-        self.calls += 1
+        self._count()
         dist.all_to_all_single(out, src, list(map(int, recv_counts)), list(map(int, send_counts)), group=self.group)
         self.bytes_sent += src.numel() * src.element_size()
         if t.dtype == torch.bool:
@@ -263,7 +275,7 @@ class Communicator:
         tail = tuple(t.shape[1:])
         out = torch.empty((sum(recv_counts),) + tail, dtype=t.dtype, device=self.wire)
         src = t.contiguous().to(self.wire)
-        self.calls += 1
+        self._count()
         work = dist.all_to_all_single(out, src, list(map(int, recv_counts)), list(map(int, send_counts)),
                                       group=self.group, async_op=True)
         self.bytes_sent += src.numel() * src.element_size()
@@ -275,7 +287,7 @@ class Communicator:
         W = self.world_size
         s = self._t(list(send_counts))
         r = torch.empty(W, dtype=torch.int64, device=self.wire)
-        self.calls += 1
+        self._count()
         dist.all_to_all_single(r, s, group=self.group)
         return to_host_ints(r)
 
@@ -290,7 +302,7 @@ class Communicator:
             return [list(map(int, r)) for r in rows]
         s = self._t([int(x) for r in rows for x in r])
         r = torch.empty(W * k, dtype=torch.int64, device=self.wire)
-        self.calls += 1
+        self._count()
         dist.all_to_all_single(r, s, group=self.group)
         v = to_host_ints(r)
         return [v[i * k:(i + 1) * k] for i in range(W)]
@@ -321,7 +333,7 @@ class Communicator:
                 pad = torch.zeros((mx - src.shape[0],) + tail, dtype=src.dtype, device=self.wire)
                 src = torch.cat([src, pad]) if src.shape[0] else pad
             blocks = torch.empty((W * mx,) + tail, dtype=src.dtype, device=self.wire)
-            self.calls += 1
+            self._count()
             dist.all_gather_into_tensor(blocks, src, group=self.group)
             self.bytes_sent += src.numel() * src.element_size() * (W - 1)
             if all(c == mx for c in counts):
@@ -351,7 +363,7 @@ class Communicator:
             faults.check("comm_timeout", "broadcast_tensor")
         if self.spmd:
             w = t.to(self.wire)
-            self.calls += 1
+            self._count()
             dist.broadcast(w, src, group=self.group)
             if w is not t:
                 t.copy_(w)

@@ -454,6 +454,7 @@ def _pipelined_exchange(tensors: List[torch.Tensor], plan: ShufflePlan, comm) ->
     send, recv = plan.send, [r[0] for r in plan.rmat]
     C = max(1, PIPELINE_CHUNK_BYTES // max(rb * W, 1))
     nchunks = -(-plan.full_max // C)
+    comm.chunk_calls += max(0, nchunks - 1)
     dev = tensors[0].device
     total = sum(recv)
     assembled = torch.empty((total, rb), dtype=torch.uint8, device=dev)
@@ -738,8 +739,18 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
         return done(lb, rb, rd if rep_l else ld)
     if kind in ("left", "semi", "anti") and rep_r:
         return done(lb, rb, ld)
+    null_aware = getattr(join, "null_aware", False)
+    if rows is None and kind in ("left", "semi", "anti") and on and not (rep_l or rep_r or null_aware):
+        # only the non-preserved side's global size matters here: the gather's
+        # own structure preamble decides it (None when it is too big to
+        # broadcast, on every rank alike), one collective fewer than counting
+        # first; a big side is shuffled below
+        g = gather_all(rb, ctx, max_rows=limit)
+        if g is not None:
+            return done(lb, g, ld)
+        nl, nr = lb.num_rows, limit + 1      # (not read again on this path)
     # global sizes decide broadcast vs shuffle (a replicated side counts once)
-    if rows is not None:
+    elif rows is not None:
         nl, nr = rows
     else:
         nl, nr = comm.allreduce_ints([lb.num_rows if not rep_l else 0, rb.num_rows if not rep_r else 0])
@@ -747,7 +758,6 @@ def prepare_join(lb: Batch, rb: Batch, join: L.Join, ctx, rows: Optional[Tuple[i
         nl = lb.num_rows
     if rep_r:
         nr = rb.num_rows
-    null_aware = getattr(join, "null_aware", False)
     if kind in ("inner", "cross"):
         if rep_r:
             return done(lb, rb, ld)

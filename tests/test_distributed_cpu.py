@@ -56,6 +56,11 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
             res[q] = {"rows": rows, "collectives": e.last_metrics.get("collectives"),
                       "bytes": e.last_metrics.get("exchange_bytes"),
                       "morsels": (e.last_metrics.get("morsels") or {}).get("morsels", 0)}
+            if low_thresholds:
+                # steady state (what a repeated query costs): join statistics
+                # memoised, pipelined-exchange chunks counted as one exchange
+                e.sql(Q.QUERIES[q])
+                res[q]["exchanges_warm"] = e.last_metrics.get("exchanges")
         except Exception as ex:  # noqa: BLE001
             res[q] = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0:
@@ -110,6 +115,12 @@ def test_tpch_distributed_gloo(world, replicate_dims, low, tpch_cpu):
         # the SF100 code paths (range slices, sorted joins, shuffled partial
         # groups, pipelined exchanges in tiny chunks): bounded too
         assert max(calls.values()) <= 12 and sum(calls.values()) <= 120, calls
+        # ... and in the steady state at most 6 exchanges a query, Q20 7 (its
+        # runtime key filter's gather, the grouped lineitem aggregate's
+        # shuffle, the part-key broadcast, the semi-join marks)
+        warm = {int(q): r["exchanges_warm"] for q, r in run_distributed.last.items()}
+        print("steady-state exchanges per query:", warm)
+        assert all(v <= (7 if q == 20 else 6) for q, v in warm.items()), warm
 
 
 def check(res, qs, con):
