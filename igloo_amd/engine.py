@@ -774,7 +774,7 @@ class QueryEngine:
             # collectives recorded into the graph (counted again on every replay)
             g.comm_calls, g.comm_bytes = self.comm.calls - c0[0], self.comm.bytes_sent - c0[1]
             g.comm_chunks = self.comm.chunk_calls - c0[2]
-            self.comm.calls, self.comm.bytes_sent = c0
+            self.comm.calls, self.comm.bytes_sent, self.comm.chunk_calls = c0
         self._set_graph(st, g)
         return True
 

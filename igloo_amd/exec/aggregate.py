@@ -280,7 +280,8 @@ class HashAggExec(ExecNode):
                                          Batch(cols, lb.num_rows, dist if dist is not None else lb.dist), ctx)
         return aggregate(lg.groups, aggs, Batch(cols, lb.num_rows), ctx)
 
-    def _spmd_counts(self, lg, lb: Batch, lkey, lk, lvalid, rk, rmasks, ctx) -> Optional[Batch]:
+    def _spmd_counts(self, lg, lb: Batch, lkey, lk, lvalid, rk, rmasks, ctx, rcol: Optional[Column] = None
+                     ) -> Optional[Batch]:
         """SPMD eager COUNT: each rank histograms its right rows' keys over the
         GLOBAL key range (one tiny all-gather of the ranges), then
 
@@ -316,9 +317,16 @@ class HashAggExec(ExecNode):
         width = W * chunk if rep else span
         hdt = torch.int64 if wide else torch.int32
         hists = torch.zeros((len(masks), width), dtype=hdt, device=dev)
+        full = _full_key_hist(rcol, g0, span) if rcol is not None and rk.numel() else None
         for k, m in enumerate(masks):
             if rk.numel():
-                hists[k, :span] = A.key_histogram(rk, g0, span, m).to(hdt)
+                if full is not None and m is not None and 2 * count_true(m) > m.numel():
+                    # most of this rank's rows pass (Q13): subtract the few
+                    # that fail from the resident column's remembered per-key
+                    # counts (as on one rank; a local choice, no collective)
+                    hists[k, :span] = (full - A.key_histogram(rk, g0, span, ~m, sparse=True)).to(hdt)
+                else:
+                    hists[k, :span] = A.key_histogram(rk, g0, span, m).to(hdt)
         lkey64 = lk.to(torch.int64)
         if rep:
             # [world, aggs, chunk]: rank r's share is one contiguous block
@@ -381,7 +389,8 @@ class HashAggExec(ExecNode):
                 m = predicate_mask(rnode.predicate, raw, ctx)
                 if rcol.valid is not None:
                     m = m & rcol.valid
-                return self._spmd_counts(lg, lb, lkey, lcol.data, lcol.valid, rcol.data, [m] * len(lg.aggs), ctx)
+                return self._spmd_counts(lg, lb, lkey, lcol.data, lcol.valid, rcol.data, [m] * len(lg.aggs), ctx,
+                                         rcol=rcol)
         rng = H.key_range(rcol.data, rcol.valid)
         span = rng[1] - rng[0] + 1 if rng else 0
         if not rng or span > EAGER_COUNT_DIRECT_SPAN:
