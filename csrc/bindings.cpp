@@ -467,6 +467,14 @@ PYBIND11_MODULE(_native, m) {
                    P<const uint8_t>(std::get<3>(t)), P<uint8_t>(std::get<4>(t)), std::get<5>(t)});
     kern::gather_multi(P<const void>(idx), idx64, n, d.data(), (int)d.size(), S(s));
   });
+  m.def("gather_packed", [](uintptr_t idx, bool idx64, int64_t n, uintptr_t src, int64_t rows, int row_bytes,
+                            const std::vector<std::tuple<uintptr_t, int, int, int, int>>& fields, uintptr_t s) {
+    std::vector<kern::PackedField> f;
+    for (auto& t : fields)
+      f.push_back({P<void>(std::get<0>(t)), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t)});
+    kern::gather_packed(P<const void>(idx), idx64, n, P<const uint8_t>(src), rows, row_bytes, f.data(), (int)f.size(),
+                        S(s));
+  });
   m.def("str_gather_lengths", [](uintptr_t off, int64_t rows, uintptr_t idx, bool idx64, int64_t n, uintptr_t len,
                                  uintptr_t s) {
     kern::str_gather_lengths(P<const int64_t>(off), rows, P<const void>(idx), idx64, n, P<int64_t>(len), S(s));

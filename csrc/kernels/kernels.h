@@ -259,6 +259,24 @@ struct GatherDesc {
                        // leave an index buffer's tail unwritten: never read past the source)
 };
 void gather_multi(const void* idx, bool idx64, int64_t n, const GatherDesc* descs, int ncols, hipStream_t stream);
+// one field of a row-packed source (gather_packed): bytes [off, off + width) of
+// each row, widened to out_bytes (sign-extended when flags & kPackedSigned);
+// flags & kPackedInRange writes 1 for an index inside the source instead
+constexpr int kMaxPackedFields = 16;
+constexpr int kPackedSigned = 1;
+constexpr int kPackedInRange = 2;
+struct PackedField {
+  void* dst;
+  int32_t off;
+  int32_t width;      // 1, 2, 4, 8 (naturally aligned inside the row)
+  int32_t out_bytes;  // 1, 2, 4, 8
+  int32_t flags;
+};
+// rows idx of a [src_rows, row_bytes] packed matrix (row_bytes 8/16/24/32)
+// split into up to kMaxPackedFields output columns: one row load per index
+// instead of one cache line per column (ops/packed_gather.py)
+void gather_packed(const void* idx, bool idx64, int64_t n, const uint8_t* src, int64_t src_rows, int row_bytes,
+                   const PackedField* fields, int nf, hipStream_t stream);
 void str_gather_lengths(const int64_t* off, int64_t src_rows, const void* idx, bool idx64, int64_t n, int64_t* len,
                         hipStream_t stream);
 void str_gather_copy(const int64_t* off, int64_t src_rows, const uint8_t* chars, const void* idx, bool idx64,

@@ -617,6 +617,7 @@ def aggregate(groups, aggs, b: Batch, ctx, row_parts: Optional[Dict[int, int]] =
             out[cid] = Column(T.INT64, gather_tensor(idx, rep).to(torch.int64))
     specs, finals = [], []
     with ctx.span("agg.eval_args"):
+        ev.prefetch([a.arg for _, a in aggs] + [getattr(a, "arg2", None) for _, a in aggs], b)
         for ci, a in aggs:
             _plan_agg(ci, a, b, gid, ng, n, ctx, specs, finals)
     with ctx.span("agg.kernel"):

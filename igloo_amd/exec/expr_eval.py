@@ -26,7 +26,7 @@ from ..ops import misc as M
 from ..ops._lib import to_host_ints
 from ..ops import strings as S
 from ..sql.expr import (AggCall, BinOp, Case, Cast, ColRef, Expr, Func, InList, IsNull, Like, Lit, Neg, Not,
-                        SubqueryExpr)
+                        SubqueryExpr, col_refs)
 from ..types import DataType
 from ..utils.errors import ExecutionError, NotSupported
 
@@ -91,8 +91,22 @@ class Evaluator:
             raise NotSupported(f"cannot evaluate {type(e).__name__}")
         return m(e, b)
 
+    @staticmethod
+    def prefetch(exprs, b: Batch) -> None:
+        """A join result's (LateBatch) columns read by ``exprs``: gathered
+        together, part by part, before they are read one by one."""
+        pf = getattr(b, "prefetch", None)
+        if pf is not None:
+            cids = set()
+            for e in exprs:
+                if e is not None:
+                    cids |= col_refs(e)
+            if len(cids) > 1:
+                pf(cids)
+
     def column(self, e: Expr, b: Batch) -> Column:
         """Evaluate and broadcast to a full column."""
+        self.prefetch((e,), b)
         v = self.eval(e, b)
         if isinstance(v, Scalar):
             return Column.full(v.value, e.dtype if v.dtype.kind == "null" else v.dtype, b.num_rows, self.device(b))
@@ -100,6 +114,7 @@ class Evaluator:
 
     def mask(self, e: Expr, b: Batch) -> torch.Tensor:
         """Predicate -> bool tensor (NULL counts as False)."""
+        self.prefetch((e,), b)
         v = self.eval(e, b)
         dev = self.device(b)
         if isinstance(v, Scalar):

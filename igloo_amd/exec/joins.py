@@ -1077,6 +1077,23 @@ class LateBatch(Batch):
             self._cache[cid] = c
         return c
 
+    def prefetch(self, cids) -> None:
+        """The not yet gathered columns among ``cids``, each part's in ONE take:
+        several columns of one resident table then go through one row-packed
+        gather (ops/packed_gather.py) instead of one sparse gather each."""
+        by_part: Dict[int, list] = {}
+        for cid in cids:
+            k = self.owner.get(cid)
+            if k is not None and cid not in self._cache and self.parts[k][1] is not None:
+                by_part.setdefault(k, []).append(cid)
+        for k, group in by_part.items():
+            if len(group) < 2:
+                continue
+            bb, idx = self.parts[k]
+            cols = bb.take_rows(group, idx) if isinstance(bb, _LazyScanBatch) else \
+                take_many([bb.columns[c] for c in group], idx)
+            self._cache.update(zip(group, cols))
+
     def compose(self, sel: torch.Tensor):
         return [(bb, sel if idx is None else gather_tensor(idx, sel).to(sel.dtype if sel.dtype == torch.int64
                                                                                else idx.dtype))

@@ -402,12 +402,9 @@ class _LazyScanBatch(Batch):
 
     def take_rows(self, cids, rows: torch.Tensor) -> List[Column]:
         """Columns at filtered-scan rows ``rows``; unread ones via the source."""
-        out, pend = {}, []
-        for c in cids:
-            if self.has(c):
-                out[c] = take(self._shared[self._names[c]], rows)
-            else:
-                pend.append(c)
+        have = [c for c in cids if self.has(c)]
+        pend = [c for c in cids if not self.has(c)]
+        out = dict(zip(have, take_many([self._shared[self._names[c]] for c in have], rows))) if have else {}
         if pend:
             comp = gather_tensor(self.idx, rows)
             out.update(zip(pend, take_many([self.src.columns[c] for c in pend], comp)))

@@ -12,6 +12,7 @@ import torch
 
 from ..columnar import Column
 from ._lib import is_gpu, launch, ptr, stream, to_host_ints
+from .packed_gather import packed_take
 from .select import offsets_from_lengths
 
 
@@ -119,7 +120,12 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
     keepalive = []  # temporaries that must outlive the (stream-ordered) launch
     strs = [c for c in cols if c.is_plain_string]
     pre = iter(_take_strings_gpu(strs, idx) if gpu and strs else [])
-    for c in cols:
+    # several resident columns at sparse / random rows: one row-packed gather
+    packed = packed_take(cols, idx, neg) if gpu and len(cols) > 1 else {}
+    for k, c in enumerate(cols):
+        if k in packed:
+            out.append(packed[k])
+            continue
         need_valid = neg or c.valid is not None
         if c.is_plain_string:
             nc = next(pre) if gpu else _take_plain_strings(c, idx, neg)

@@ -7,7 +7,9 @@ with the column tensor like an index (attributes set by the operators):
 * ``_igloo_perm``    secondary index: sorted keys + row permutation (ops/hashing.py);
 * ``_igloo_dense``   dense lower-bound range index of a sorted key column;
 * ``_igloo_hll``     HyperLogLog registers (4 KB);
-* ``_igloo_fence``   every 256th key of a sorted column (binary-search fence).
+* ``_igloo_fence``   every 256th key of a sorted column (binary-search fence);
+* ``_igloo_packed``  row-packed copies of column sets for sparse gathers
+  (ops/packed_gather.py), kept on the set's first column.
 
 The cache tier (cache/tiered.py) charges them to the column that owns them,
 so the HBM budget covers what the table really holds, and evicting a column
@@ -19,7 +21,7 @@ from typing import Iterable
 
 import torch
 
-DERIVED_ATTRS = ("_igloo_narrow", "_igloo_perm", "_igloo_dense", "_igloo_hll", "_igloo_fence")
+DERIVED_ATTRS = ("_igloo_narrow", "_igloo_perm", "_igloo_dense", "_igloo_hll", "_igloo_fence", "_igloo_packed")
 
 
 def _tensor_bytes(x) -> int:

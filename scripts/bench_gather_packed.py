@@ -60,6 +60,34 @@ def main():
     assert torch.equal(pout[:, 0], outs[0]) and torch.equal(pout[:, a.cols - 1], outs[-1])
     print(f"rows={n} density={a.density} gathered={m} cols={a.cols}: separate {t1:.3f} ms, "
           f"packed {wp} B rows {t2:.3f} ms ({t1 / t2:.2f}x)", flush=True)
+    del cols, outs, packed, pout
+
+    # the engine's case (ops/packed_gather.py): int64 columns whose values fit
+    # int32 / int8 / int16 / int32 (Q9's l_extendedprice, l_discount,
+    # l_quantity, l_suppkey), one 16-byte packed row widened back to int64
+    from igloo_amd.ops.pack import layout, pack_rows
+    lim = [(1 << 30), 100, 20000, (1 << 30)][:a.cols]
+    wide = [torch.randint(-v, v, (n,), device="cuda", dtype=torch.int64, generator=g) for v in lim]
+    narrowed = [w.to(torch.int32 if v > 30000 else torch.int16 if v > 120 else torch.int8) for w, v in zip(wide, lim)]
+    lay = layout(narrowed)
+    pk, _ = pack_rows(narrowed, None, n, lay)
+    del narrowed
+    wouts = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in wide]
+    pouts = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in wide]
+    fields = [(ptr(pouts[i]), off, w, 8, 1) for i, w, off in lay[1]]
+
+    def wide_separate():
+        N.gather_multi(ptr(idx), False, m, [(ptr(c), ptr(o), 8, 0, 0, n) for c, o in zip(wide, wouts)], s)
+
+    def wide_packed():
+        N.gather_packed(ptr(idx), False, m, ptr(pk), n, lay[0], fields, s)
+
+    t3 = timed(wide_separate)
+    t4 = timed(wide_packed)
+    for o, p in zip(wouts, pouts):
+        assert torch.equal(o, p)
+    print(f"int64 columns x{a.cols}: separate {t3:.3f} ms, gather_packed {lay[0]} B rows {t4:.3f} ms "
+          f"({t3 / t4:.2f}x)", flush=True)
 
 
 if __name__ == "__main__":
