@@ -55,6 +55,7 @@ def main():
     tot = collections.Counter()
     sites_all = collections.Counter()
     vol_sites = collections.Counter()
+    stable_sites = collections.Counter()
     for q in qs:
         logs = [log_of(t[q]) for t in texts]
         seqs = [[s for s, _ in lg] for lg in logs]
@@ -66,6 +67,8 @@ def main():
                 vals = [lg[i][1] for lg in logs]
                 if all(v is not None and v == vals[0] for v in vals):
                     stable += 1
+                    (code, line), _ = logs[0][i][0]
+                    stable_sites[f"{code.co_filename.split('igloo_amd/')[-1]}:{line} {code.co_name} Q{q}"] += 1
                 else:
                     vol += 1
                     (code, line), _ = logs[0][i][0]
@@ -103,6 +106,8 @@ def main():
     lines += [f"  {v:4d}  {k}" for k, v in sites_all.most_common(60)]
     lines.append("\nparameter-dependent sites:")
     lines += [f"  {v:4d}  {k}" for k, v in vol_sites.most_common(60)]
+    lines.append("\nstable sites (equal under every parameter set):")
+    lines += [f"  {v:4d}  {k}" for k, v in stable_sites.most_common(200)]
     text = "\n".join(lines)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
