@@ -171,24 +171,33 @@ namespace igloo {
 namespace kern {
 namespace {
 
-template <typename K2, typename O, bool WRITE>
+// MASKED: big2 is a byte mask over the big side (a filter the big column was
+// not compacted by: the join probes the table's own sorted key column) and a
+// range row matches where it is set; small2 is unused.
+template <typename K2, typename O, bool WRITE, bool MASKED = false>
 __global__ __launch_bounds__(kBlock) void sorted_match_kernel(const K2* __restrict__ big2,
                                                              const K2* __restrict__ small2,
                                                              const int64_t* __restrict__ lo,
                                                              const int64_t* __restrict__ cnt, int64_t ns,
                                                              int32_t* __restrict__ counts,
                                                              const int64_t* __restrict__ offsets,
-                                                             O* __restrict__ sidx, O* __restrict__ bidx) {
+                                                             O* __restrict__ sidx, O* __restrict__ bidx,
+                                                             int64_t out_cap) {
+  const uint8_t* __restrict__ mask = reinterpret_cast<const uint8_t*>(big2);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = lo[i], c = cnt[i];
-    const K2 key = small2[i];
+    const K2 key = MASKED ? K2{} : small2[i];
     int64_t o = WRITE ? offsets[i] : 0;
     int32_t m = 0;
     for (int64_t k = 0; k < c; ++k) {
-      if (big2[l + k] == key) {
+      if (MASKED ? mask[l + k] != 0 : big2[l + k] == key) {
         if (WRITE) {
-          sidx[o] = (O)i;
-          bidx[o] = (O)(l + k);
+          // (offsets from a device scan; the outputs sized by a possibly
+          // replayed total: never written past it)
+          if (o >= 0 && o < out_cap) {
+            sidx[o] = (O)i;
+            bidx[o] = (O)(l + k);
+          }
           ++o;
         }
         ++m;
@@ -198,34 +207,42 @@ __global__ __launch_bounds__(kBlock) void sorted_match_kernel(const K2* __restri
   }
 }
 
-template <typename K2>
+template <typename K2, bool MASKED>
 void launch_match(const void* big2, const void* small2, const int64_t* lo, const int64_t* cnt, int64_t ns,
-                  int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64, hipStream_t stream) {
+                  int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64, int64_t out_cap,
+                  hipStream_t stream) {
   const dim3 g(grid_for(ns, kBlock, 1 << 16)), b(kBlock);
   const K2* B = static_cast<const K2*>(big2);
   const K2* S = static_cast<const K2*>(small2);
   if (!offsets)
-    hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, false>), g, b, 0, stream, B, S, lo, cnt, ns, counts, nullptr,
-                       nullptr, nullptr);
+    hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, false, MASKED>), g, b, 0, stream, B, S, lo, cnt, ns, counts,
+                       nullptr, nullptr, nullptr, 0);
   else if (out64)
-    hipLaunchKernelGGL((sorted_match_kernel<K2, int64_t, true>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
-                       offsets, static_cast<int64_t*>(sidx), static_cast<int64_t*>(bidx));
+    hipLaunchKernelGGL((sorted_match_kernel<K2, int64_t, true, MASKED>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
+                       offsets, static_cast<int64_t*>(sidx), static_cast<int64_t*>(bidx), out_cap);
   else
-    hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, true>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
-                       offsets, static_cast<int32_t*>(sidx), static_cast<int32_t*>(bidx));
+    hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, true, MASKED>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
+                       offsets, static_cast<int32_t*>(sidx), static_cast<int32_t*>(bidx), out_cap);
 }
 
 }  // namespace
 
 void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
                   int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
-                  hipStream_t stream) {
+                  int64_t out_cap, hipStream_t stream) {
   if (ns <= 0) return;
   if (key64)
-    launch_match<int64_t>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, stream);
+    launch_match<int64_t, false>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, stream);
   else
-    launch_match<int32_t>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, stream);
+    launch_match<int32_t, false>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, stream);
   check_launch("sorted_match", stream);
+}
+
+void sorted_masked(const uint8_t* mask, const int64_t* lo, const int64_t* cnt, int64_t ns, int32_t* counts,
+                   const int64_t* offsets, void* sidx, void* bidx, bool out64, int64_t out_cap, hipStream_t stream) {
+  if (ns <= 0) return;
+  launch_match<int32_t, true>(mask, nullptr, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, stream);
+  check_launch("sorted_masked", stream);
 }
 
 }  // namespace kern

@@ -31,7 +31,7 @@ from ..utils.errors import ExecutionError, NotSupported
 from . import fused
 from .expr_eval import Evaluator, Scalar, _convert_tensor
 from .context import ExecContext, ExecNode
-from .scan import (FilterExec, ProjectExec, ScanExec, _LazyScanBatch, _tag_base, filter_batch,
+from .scan import (NDV_DERIVED, FilterExec, ProjectExec, ScanExec, _LazyScanBatch, _tag_base, filter_batch,
                    predicate_mask, LATE_SCAN)
 
 
@@ -897,12 +897,15 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         return z, z
     big_right = n_r >= n_l
     big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
-    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS and bvalid is None \
+    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS \
             and (4 * small.numel() <= big.numel() or _dense_lookup_ok(big, small.numel())) and H.is_sorted(big):
         with ctx.span("join.sorted_search"):
             lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
-            sidx, bidx = H.expand_ranges(lo, cnt, big.numel())
+            # a big side with NULLs or probed in place under its filter mask
+            # (MultiJoinExec._late_join): only its set rows pair up
+            sidx, bidx = H.expand_ranges(lo, cnt, big.numel()) if bvalid is None else \
+                H.masked_expand(lo, cnt, bvalid, big.numel())
         ctx.note_partial_read(big, sidx.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and DENSE_JOIN_SMALL and svalid is None and small.numel() >= SORTED_JOIN_MIN_ROWS \
@@ -1116,6 +1119,51 @@ class LateBatch(Batch):
 
 
 PRUNE_PARTS = True
+
+#: a filtered scan keeping at least this fraction of its table probes the
+#: table's key column under its filter mask instead of a gathered copy
+IN_PLACE_MIN_DENSITY = float(os.environ.get("IGLOO_IN_PLACE_DENSITY", "0.125"))
+#: ... and an unsorted key column (hash probe over every table row) when at
+#: least this fraction survives
+IN_PLACE_HASH_DENSITY = 0.4
+IN_PLACE_STATS = {"probes": 0}
+
+
+def _in_place_side(side: "LateBatch", keys, other_rows: int, ctx):
+    """(LateBatch over the whole table, filter mask) for the bigger side of a
+    join when it is one filtered scan in index form (_LazyScanBatch) with its
+    filter mask kept, at least IN_PLACE_MIN_DENSITY of the table surviving,
+    and one join key: a sorted resident column of the table not gathered yet,
+    at least 4x the other side's rows. Else None.
+
+    The other side's keys are then searched in the table's own sorted key
+    column and only the ranges' rows set in the mask pair up (inner_pairs ->
+    ops/hashing.py masked_expand): the compaction gather of the keys (mask ->
+    indices -> gather: ~1.2 ms for Q3's 324M lineitem keys) is skipped, and
+    the pairs name table rows, so later payload gathers need no index
+    composition either. Paths that iterate the bigger side (hash probe, dense
+    lookup) instead work over every table row -- Q5's 150M orders for 22.7M
+    surviving ones cost 1.7 ms more -- so an unsorted key column is probed in
+    place only when at least IN_PLACE_HASH_DENSITY of the table survives (Q3's
+    orders, 48 %: a hash probe with the mask as key validity)."""
+    if IN_PLACE_MIN_DENSITY <= 0 or ctx.device.type != "cuda" or len(side.parts) != 1 or len(keys) != 1:
+        return None
+    bb, idx = side.parts[0]
+    if idx is not None or not isinstance(bb, _LazyScanBatch) or bb.mask is None:
+        return None
+    n_src = bb.src.num_rows
+    if n_src < SORTED_JOIN_MIN_ROWS or bb.num_rows < IN_PLACE_MIN_DENSITY * n_src or bb.mask.numel() != n_src \
+            or 4 * other_rows > n_src:
+        return None
+    k = keys[0]
+    if not (isinstance(k, ColRef) and k.cid in bb.src.columns and not bb.has(k.cid)):
+        return None
+    col = bb.src.columns[k.cid]
+    if col.dtype.kind not in _INT_KEYS or col.valid is not None or not getattr(col.data, "_igloo_resident", False):
+        return None
+    if bb.num_rows < IN_PLACE_HASH_DENSITY * n_src and not H.is_sorted(col.data):
+        return None
+    return LateBatch([(bb.src, None)], n_src, side.dist), bb.mask
 
 
 #: a multi-way join returns its LateBatch (row indices into the inputs) to the
@@ -1331,9 +1379,27 @@ class MultiJoinExec(ExecNode):
         if pairs is not None:
             lidx, ridx = pairs
         else:
+            # the bigger side, a filtered scan whose key columns were not
+            # gathered yet: probe the table's own key columns under the filter
+            # mask (no key gather; its pairs name table rows)
+            big_left = A.num_rows >= B.num_rows
+            inplace = _in_place_side(A if big_left else B, [x if big_left else y for x, y in on],
+                                     B.num_rows if big_left else A.num_rows, ctx)
+            if inplace is not None:
+                IN_PLACE_STATS["probes"] += 1
+                if big_left:
+                    A = inplace[0]
+                else:
+                    B = inplace[0]
             with ctx.span("join.keys"):
                 lk, rk, lvalid, rvalid = key_tensors([ev.column(x, A) for x, _ in on],
                                                      [ev.column(y, B) for _, y in on])
+            if inplace is not None:
+                m = inplace[1]
+                if big_left:
+                    lvalid = m if lvalid is None else lvalid & m
+                else:
+                    rvalid = m if rvalid is None else rvalid & m
             lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx)
         if residual is not None:
             with ctx.span("join.residual"):
@@ -1536,6 +1602,15 @@ class MultiJoinExec(ExecNode):
             b = rel["batch"]
             with ctx.span("multijoin.ndv"):
                 cached = None
+                if not ctx.spmd and b.num_rows and isinstance(b, _LazyScanBatch) and isinstance(e, ColRef) \
+                        and e.cid in b.src.columns and not b.has(e.cid) and NDV_DERIVED:
+                    # a filtered scan's key not gathered yet: derived from the
+                    # table column's NDV without gathering it (the join may
+                    # probe that column in place, _in_place_side)
+                    src = b.src.columns[e.cid]
+                    if src.valid is None and not src.is_dict:
+                        rel["ndv"][key] = max(_derived_ndv((src, b.src.num_rows), b.num_rows), 1)
+                        return rel["ndv"][key]
                 if not ctx.spmd and b.num_rows:
                     c = ctx.evaluator.column(e, b)
                     # resident table columns: the sketch of the same tensor is reused across queries

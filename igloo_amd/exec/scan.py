@@ -172,13 +172,15 @@ class ScanExec(ExecNode):
                 else:
                     with ctx.span("scan.filter_eval"):
                         idx = mask_to_indices(m)
-                    hit = ctx.scan_cache[key] = (idx, {})
-            idx, taken_by_name = hit
+                    # (the mask stays with the index form: a join may probe the
+                    # table's own key column under it instead of gathering it)
+                    hit = ctx.scan_cache[key] = (idx, {}, m)
+            idx, taken_by_name = hit[0], hit[1]
             if late:
                 # index form: the join gathers its key columns now and payload
                 # columns only for the rows that survive it
                 src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
-                return _LazyScanBatch(src, idx, name, taken_by_name, ctx)
+                return _LazyScanBatch(src, idx, name, taken_by_name, ctx, hit[2] if len(hit) > 2 else None)
             todo = [c for c in out_cids if name[c] not in taken_by_name]
             if todo:
                 with ctx.span("scan.filter_gather"):
@@ -377,8 +379,10 @@ class _LazyScanBatch(Batch):
     source through the composed row index — only for rows that survive the
     join — while its own row indices stay those of the filtered scan."""
 
-    def __init__(self, src: Batch, idx: torch.Tensor, names: dict, shared: dict, ctx):  # noqa: D401
+    def __init__(self, src: Batch, idx: torch.Tensor, names: dict, shared: dict, ctx,
+                 mask: Optional[torch.Tensor] = None):  # noqa: D401
         self.src, self.idx, self._names, self._shared, self._ctx = src, idx, names, shared, ctx
+        self.mask = mask    # bool[src rows]: the filter idx was compacted from (None: not kept)
         self.num_rows = idx.numel()
         self.dist = src.dist
         self.out_dist = None

@@ -601,14 +601,40 @@ def sorted_match_pairs(big1: torch.Tensor, big2: torch.Tensor, small1: torch.Ten
     st = stream(big1)
     counts = torch.empty(max(ns, 1), dtype=torch.int32, device=big1.device)
     k64 = big2.dtype == torch.int64
-    N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, ptr(counts), 0, 0, 0, False, st)
+    N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, ptr(counts), 0, 0, 0, False, 0, st)
     off, total = exclusive_scan(counts[:ns])
     it = torch.int32 if max(total, big1.numel(), ns) < INT32_MAX else torch.int64
     sidx = torch.empty(total, dtype=it, device=big1.device)
     bidx = torch.empty(total, dtype=it, device=big1.device)
     if total:
         N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, 0, ptr(off), ptr(sidx), ptr(bidx),
-                       it == torch.int64, st)
+                       it == torch.int64, total, st)
+    return sidx, bidx
+
+
+def masked_expand(lo: torch.Tensor, cnt: torch.Tensor, mask: torch.Tensor, big_n: int
+                  ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``expand_ranges`` keeping only the big rows set in ``mask`` (bool[big_n]):
+    the pairs of a sorted join whose big side is a filtered table probed in
+    place -- its own sorted key column under the filter mask, not a compacted
+    copy (exec/joins.py inner_pairs). Grouped by small row."""
+    ns = lo.numel()
+    if not is_gpu(lo):
+        s, b = expand_ranges(lo, cnt, big_n)
+        keep = mask.index_select(0, b.long())
+        return s[keep], b[keep]
+    N = launch("sorted_masked")
+    st = stream(lo)
+    mk = mask.contiguous().view(torch.uint8)
+    counts = torch.empty(max(ns, 1), dtype=torch.int32, device=lo.device)
+    N.sorted_masked(ptr(mk), ptr(lo), ptr(cnt), ns, ptr(counts), 0, 0, 0, False, 0, st)
+    off, total = exclusive_scan(counts[:ns])
+    it = torch.int32 if max(total, big_n, ns) < INT32_MAX else torch.int64
+    sidx = torch.empty(total, dtype=it, device=lo.device)
+    bidx = torch.empty(total, dtype=it, device=lo.device)
+    if total:
+        N.sorted_masked(ptr(mk), ptr(lo), ptr(cnt), ns, 0, ptr(off), ptr(sidx), ptr(bidx), it == torch.int64, total,
+                        st)
     return sidx, bidx
 
 

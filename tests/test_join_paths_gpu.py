@@ -194,3 +194,23 @@ def test_eager_count_masked_complement(gpu_device, monkeypatch, pred, nullable):
             assert _norm(e.query(sql)) == res[dev]        # again with the remembered histogram
     assert res["cpu"] == res[gpu_device]
     assert calls, "the masked eager COUNT path did not run"
+
+
+@pytest.mark.parametrize("sorted_min", [1000, 1 << 40])
+def test_in_place_filtered_probe_side(gpu_device, monkeypatch, sorted_min):
+    """A filtered big scan in index form searches its table's own sorted key
+    column under the filter mask (joins.py _in_place_side, masked_expand);
+    TPC-H joins vs the gathered-key run, with the sorted path on and off."""
+    from igloo_amd.models.tpch import datagen, queries
+    from igloo_amd.ops._lib import KERNEL_CALLS
+    from igloo_amd.utils.digest import digest
+    monkeypatch.setattr(J, "SORTED_JOIN_MIN_ROWS", sorted_min)
+    e = ig.QueryEngine(device=gpu_device)
+    datagen.register(e, 0.05)
+    for q in (3, 5, 7, 10, 12, 21):
+        monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.0)
+        want = digest(e.query(queries.QUERIES[q]))
+        monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.125)
+        assert digest(e.query(queries.QUERIES[q] + " ")) == want, q
+    if sorted_min == 1000:
+        assert J.IN_PLACE_STATS["probes"] > 0 and KERNEL_CALLS["sorted_masked"] > 0
