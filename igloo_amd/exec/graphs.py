@@ -50,6 +50,7 @@ crates/engine/src/lib.rs:112-140). This is the HIP-graph half of SURVEY §5.7's
 """
 from __future__ import annotations
 
+import gc
 import logging
 import os
 import traceback
@@ -169,6 +170,12 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     dump = os.environ.get("IGLOO_GRAPH_DUMP")     # debugging: DOT dump of every captured graph
     if dump:
         g.enable_debug_mode()
+    # no cyclic garbage collection inside the capture: a collected object's
+    # tensors would be freed (and any synchronizing call in their teardown
+    # raised, under the sync-debug mode above, inside a destructor: abort)
+    # while the stream records
+    gc_on = gc.isenabled()
+    gc.disable()
     try:
         with torch.cuda.stream(s):
             g.capture_begin(pool=engine.graph_pool() if SHARED_POOL else None, capture_error_mode="thread_local")
@@ -214,6 +221,8 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
         torch.cuda.synchronize(dev)
         return None
     finally:
+        if gc_on:
+            gc.enable()
         torch.cuda.set_sync_debug_mode(sync_mode)
         if batch is None or bad is None:
             _lib.capture_keepalive()       # a failed capture keeps nothing

@@ -24,7 +24,7 @@ from ..ops._lib import (check_not_capturing, device_ints, launch, ptr, stream, t
                        to_host_ints, unlogged)
 from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
-from ..ops.select import compact_columns, exclusive_scan, mask_to_indices
+from ..ops.select import MaskRows, compact_columns, exclusive_scan, mask_to_indices
 from ..sql import logical as L
 from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
 from ..utils.errors import ExecutionError, NotSupported
@@ -171,23 +171,33 @@ class ScanExec(ExecNode):
                     hit = ctx.scan_cache[key] = (idx, taken)
                 else:
                     with ctx.span("scan.filter_eval"):
-                        idx = mask_to_indices(m)
+                        rows = MaskRows(m)
                     # (the mask stays with the index form: a join may probe the
-                    # table's own key column under it instead of gathering it)
-                    hit = ctx.scan_cache[key] = (idx, {}, m)
-            idx, taken_by_name = hit[0], hit[1]
+                    # table's own key column under it instead of gathering it,
+                    # and then the index vector is never written)
+                    hit = ctx.scan_cache[key] = (rows, {})
+            rows, taken_by_name = hit
             if late:
                 # index form: the join gathers its key columns now and payload
                 # columns only for the rows that survive it
                 src = Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
-                return _LazyScanBatch(src, idx, name, taken_by_name, ctx, hit[2] if len(hit) > 2 else None)
+                return _LazyScanBatch(src, rows, name, taken_by_name, ctx)
             todo = [c for c in out_cids if name[c] not in taken_by_name]
             if todo:
                 with ctx.span("scan.filter_gather"):
-                    for c, col in zip(todo, take_many([b.columns[c] for c in todo], idx)):
+                    if isinstance(rows, MaskRows) and COMPACT and rows.mask.is_cuda:
+                        # the index form of an earlier scan (Q21's l1 for l3):
+                        # the columns compacted straight from its mask
+                        taken = compact_columns(rows.mask, [b.columns[c] for c in todo], total=rows.total,
+                                                want_idx=False)[1]
+                    else:
+                        taken = take_many([b.columns[c] for c in todo],
+                                          rows.idx if isinstance(rows, MaskRows) else rows)
+                    for c, col in zip(todo, taken):
                         _tag_base(col, b.columns[c], b.num_rows)
                         taken_by_name[name[c]] = col
-            return Batch({c: taken_by_name[name[c]] for c in out_cids}, idx.numel(), b.dist)
+            n_rows = rows.total if isinstance(rows, MaskRows) else rows.numel()
+            return Batch({c: taken_by_name[name[c]] for c in out_cids}, n_rows, b.dist)
         return Batch({c: b.columns[c] for c in out_cids}, b.num_rows, b.dist)
 
     def _run(self, ctx):
@@ -379,18 +389,24 @@ class _LazyScanBatch(Batch):
     source through the composed row index — only for rows that survive the
     join — while its own row indices stay those of the filtered scan."""
 
-    def __init__(self, src: Batch, idx: torch.Tensor, names: dict, shared: dict, ctx,
-                 mask: Optional[torch.Tensor] = None):  # noqa: D401
-        self.src, self.idx, self._names, self._shared, self._ctx = src, idx, names, shared, ctx
-        self.mask = mask    # bool[src rows]: the filter idx was compacted from (None: not kept)
-        self.num_rows = idx.numel()
+    def __init__(self, src: Batch, rows, names: dict, shared: dict, ctx):  # noqa: D401
+        """rows: the surviving row ids (tensor) or ops/select.py MaskRows."""
+        self.src, self._rows, self._names, self._shared, self._ctx = src, rows, names, shared, ctx
+        # bool[src rows]: the filter the rows came from (None: not kept)
+        self.mask = rows.mask if isinstance(rows, MaskRows) else None
+        self.num_rows = rows.total if isinstance(rows, MaskRows) else rows.numel()
         self.dist = src.dist
         self.out_dist = None
         self.columns = _ScanColumns(self)
 
     @property
+    def idx(self) -> torch.Tensor:
+        """Row ids into ``src`` (written on first use)."""
+        return self._rows.idx if isinstance(self._rows, MaskRows) else self._rows
+
+    @property
     def device(self):
-        return self.idx.device
+        return self._rows.mask.device if isinstance(self._rows, MaskRows) else self._rows.device
 
     def has(self, cid) -> bool:
         return self._names[cid] in self._shared

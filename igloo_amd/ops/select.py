@@ -33,6 +33,44 @@ def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Te
     return out
 
 
+class MaskRows:
+    """The set rows of a bool mask as a count now and an index vector on
+    first use: the count pass and its readback run at once, the index write
+    (select_write: 4 bytes per surviving row) only when something reads
+    ``idx`` -- a join probing the masked table in place never does
+    (exec/joins.py _in_place_side)."""
+
+    __slots__ = ("mask", "total", "_ws", "_idx")
+
+    def __init__(self, mask: torch.Tensor):
+        assert mask.dtype == torch.bool and mask.dim() == 1
+        self.mask = mask.contiguous()
+        self._idx = None
+        self._ws = None
+        if not is_gpu(mask):
+            self._idx = mask_to_indices(self.mask)
+            self.total = self._idx.numel()
+            return
+        n = mask.numel()
+        N = launch("select")
+        tiles = N.select_num_tiles(n)
+        self._ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
+        N.select_count(ptr(self.mask), n, ptr(self._ws), ptr(self._ws) + 8 * tiles, stream(mask))
+        self.total = to_host_int(self._ws[tiles:])
+
+    @property
+    def idx(self) -> torch.Tensor:
+        if self._idx is None:
+            n = self.mask.numel()
+            out = torch.empty(self.total, dtype=idx_dtype(n), device=self.mask.device)
+            if self.total:
+                launch("select").select_write(ptr(self.mask), n, ptr(self._ws), ptr(out), out.dtype == torch.int64,
+                                              self.total, stream(self.mask))
+            out._igloo_incr = True
+            self._idx, self._ws = out, None
+        return self._idx
+
+
 def count_true(mask: torch.Tensor) -> int:
     """Number of True entries of a bool mask (one count pass, one readback)."""
     assert mask.dtype == torch.bool and mask.dim() == 1
