@@ -671,11 +671,12 @@ PYBIND11_MODULE(_native, m) {
                                     P<int32_t>(counts), S(s));
   });
   m.def("sorted_exists", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
-                            int op, uintptr_t hit, uintptr_t s) {
-    if (op < 0 || op > 5 || (ns > 0 && (!big2 || !small2 || !lo || !cnt || !hit)))
+                            int op, uintptr_t mask, uintptr_t hit, uintptr_t s) {
+    // op 6 (any row of the range set in mask) reads neither value column
+    if (op < 0 || op > 6 || (op == 6 && !mask) || (ns > 0 && (!lo || !cnt || !hit || (op < 6 && (!big2 || !small2)))))
       throw std::runtime_error("sorted_exists: bad arguments");
     kern::sorted_exists(P<const void>(big2), P<const void>(small2), key64, P<const int64_t>(lo), P<const int64_t>(cnt),
-                        ns, op, P<uint8_t>(hit), S(s));
+                        ns, op, P<const uint8_t>(mask), P<uint8_t>(hit), S(s));
   });
   m.def("sorted_match", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
                            uintptr_t counts, uintptr_t offsets, uintptr_t sidx, uintptr_t bidx, bool out64,

@@ -397,7 +397,7 @@ void dense_ranges(const void* first, bool first64, int64_t kmin, int64_t kmax, c
                   const uint8_t* qvalid, int64_t nq, int64_t* lo, int64_t* cnt, hipStream_t stream);
 // hit[i] = exists k in [lo[i], lo[i]+cnt[i]) with big2[k] OP small2[i] (op: 0 =, 1 <>, 2 <, 3 <=, 4 >, 5 >=)
 void sorted_exists(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
-                   int64_t ns, int op, uint8_t* hit, hipStream_t stream);
+                   int64_t ns, int op, const uint8_t* mask, uint8_t* hit, hipStream_t stream);
 void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
                   int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
                   int64_t out_cap, hipStream_t stream);

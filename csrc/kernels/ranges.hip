@@ -387,25 +387,30 @@ void dense_ranges(const void* first, bool first64, int64_t kmin, int64_t kmax, c
 namespace igloo {
 namespace kern {
 namespace {
+// mask (optional): only the big rows set in it exist (a filtered big side
+// searched in place, exec/joins.py _in_place_semi); op 6: any such row
 template <typename K2>
 __global__ __launch_bounds__(kBlock) void sorted_exists_kernel(const K2* __restrict__ big2,
                                                               const K2* __restrict__ small2,
                                                               const int64_t* __restrict__ lo,
                                                               const int64_t* __restrict__ cnt, int64_t ns, int op,
+                                                              const uint8_t* __restrict__ mask,
                                                               uint8_t* __restrict__ hit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = lo[i], c = cnt[i];
-    const K2 v = small2[i];
+    const K2 v = op == 6 ? K2{} : small2[i];
     bool any = false;
     for (int64_t k = 0; k < c && !any; ++k) {
-      const K2 b = big2[l + k];
+      if (mask && !mask[l + k]) continue;
+      const K2 b = op == 6 ? K2{} : big2[l + k];
       switch (op) {
         case 0: any = b == v; break;
         case 1: any = b != v; break;
         case 2: any = b < v; break;
         case 3: any = b <= v; break;
         case 4: any = b > v; break;
-        default: any = b >= v; break;
+        case 5: any = b >= v; break;
+        default: any = true; break;
       }
     }
     hit[i] = any;
@@ -414,15 +419,15 @@ __global__ __launch_bounds__(kBlock) void sorted_exists_kernel(const K2* __restr
 }  // namespace
 
 void sorted_exists(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
-                   int64_t ns, int op, uint8_t* hit, hipStream_t stream) {
+                   int64_t ns, int op, const uint8_t* mask, uint8_t* hit, hipStream_t stream) {
   if (ns <= 0) return;
   const dim3 g(grid_for(ns, kBlock, 1 << 16)), b(kBlock);
   if (key64)
     hipLaunchKernelGGL(sorted_exists_kernel<int64_t>, g, b, 0, stream, (const int64_t*)big2, (const int64_t*)small2,
-                       lo, cnt, ns, op, hit);
+                       lo, cnt, ns, op, mask, hit);
   else
     hipLaunchKernelGGL(sorted_exists_kernel<int32_t>, g, b, 0, stream, (const int32_t*)big2, (const int32_t*)small2,
-                       lo, cnt, ns, op, hit);
+                       lo, cnt, ns, op, mask, hit);
   check_launch("sorted_exists", stream);
 }
 }  // namespace kern

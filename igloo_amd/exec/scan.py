@@ -58,6 +58,10 @@ class ScanExec(ExecNode):
     #: set by a parent multi-way join: a filtered scan may hand over its rows
     #: as indices into the source (LateBatch) instead of gathered columns
     late_ok = False
+    #: set by a parent semi / anti join: the subquery side of EXISTS may stay
+    #: in index form too (its filter mask then decides which rows exist,
+    #: exec/joins.py _in_place_semi); single-process, unbudgeted runs only
+    late_semi = False
 
     def __init__(self, logical: L.Scan):
         self.logical = logical
@@ -154,7 +158,8 @@ class ScanExec(ExecNode):
             fsql = tuple(sorted(_CID.sub("", f.sql()) for f in s.filters))
             key = (id(s.source), b.num_rows, fsql, ctx.morsel[2] if ctx.morsel is not None else None)
             hit = None if any("random" in x.lower() for x in fsql) else ctx.scan_cache.get(key)
-            late = self.late_ok and LATE_SCAN and ctx.device.type == "cuda"
+            late = (self.late_ok or (self.late_semi and not ctx.spmd and ctx.budget is None)) and LATE_SCAN \
+                and ctx.device.type == "cuda"
             if hit is None:
                 with ctx.span("scan.filter_eval"):
                     m = predicate_mask(self.predicate, b, ctx)
@@ -330,8 +335,14 @@ class ProjectExec(ExecNode):
         return ", ".join(e.sql() if isinstance(e, ColRef) and e.cid == c.cid else f"{e.sql()} AS {c.name}"
                          for c, e in self.logical.exprs)
 
+    def identity(self) -> bool:
+        """Every output column is an input column under its own id."""
+        return all(isinstance(e, ColRef) and e.cid == ci.cid for ci, e in self.logical.exprs)
+
     def _run(self, ctx):
         b = self.children[0].execute(ctx)
+        if isinstance(b, _LazyScanBatch) and self.identity():
+            return b        # a filtered scan in index form stays so (its extra columns go unread)
         from ..parallel.exchange import keyed
         cols = {}
         d = b.dist

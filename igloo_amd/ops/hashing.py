@@ -638,25 +638,38 @@ def masked_expand(lo: torch.Tensor, cnt: torch.Tensor, mask: torch.Tensor, big_n
     return sidx, bidx
 
 
-EXISTS_OPS = {"=": 0, "<>": 1, "<": 2, "<=": 3, ">": 4, ">=": 5}
+EXISTS_OPS = {"=": 0, "<>": 1, "<": 2, "<=": 3, ">": 4, ">=": 5, "any": 6}
 
 
-def sorted_exists(big2: torch.Tensor, small2: torch.Tensor, lo: torch.Tensor, cnt: torch.Tensor, op: str
-                  ) -> torch.Tensor:
-    """bool[ns]: some row k of small row i's range (lo, cnt) has big2[k] OP small2[i]."""
-    dt = torch.int64 if torch.int64 in (big2.dtype, small2.dtype) else torch.int32
-    big2, small2 = big2.to(dt).contiguous(), small2.to(dt).contiguous()
-    ns = small2.numel()
-    if not is_gpu(big2):
-        s, b = expand_ranges(lo, cnt, big2.numel())
-        bv, sv = big2.index_select(0, b.long()), small2.index_select(0, s.long())
-        ok = {"=": bv == sv, "<>": bv != sv, "<": bv < sv, "<=": bv <= sv, ">": bv > sv, ">=": bv >= sv}[op]
+def sorted_exists(big2: Optional[torch.Tensor], small2: Optional[torch.Tensor], lo: torch.Tensor, cnt: torch.Tensor,
+                  op: str, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bool[ns]: some row k of small row i's range (lo, cnt) has big2[k] OP
+    small2[i] (op "any": any row; big2 / small2 unused). ``mask``: only the
+    big rows set in it count (a filtered big side searched in place)."""
+    ns = lo.numel()
+    if op == "any":
+        big2 = small2 = None
+        dt = torch.int32
+    else:
+        dt = torch.int64 if torch.int64 in (big2.dtype, small2.dtype) else torch.int32
+        big2, small2 = big2.to(dt).contiguous(), small2.to(dt).contiguous()
+    if not is_gpu(lo):
+        nb = mask.numel() if mask is not None else big2.numel()
+        s, b = expand_ranges(lo, cnt, nb)
+        if op == "any":
+            ok = torch.ones(s.numel(), dtype=torch.bool)
+        else:
+            bv, sv = big2.index_select(0, b.long()), small2.index_select(0, s.long())
+            ok = {"=": bv == sv, "<>": bv != sv, "<": bv < sv, "<=": bv <= sv, ">": bv > sv, ">=": bv >= sv}[op]
+        if mask is not None:
+            ok = ok & mask.index_select(0, b.long())
         hit = torch.zeros(ns, dtype=torch.bool)
         hit.index_fill_(0, s.long()[ok], True)
         return hit
-    hit = torch.empty(ns, dtype=torch.bool, device=big2.device)
+    hit = torch.empty(ns, dtype=torch.bool, device=lo.device)
+    mk = mask.contiguous().view(torch.uint8) if mask is not None else None
     launch("sorted_exists").sorted_exists(ptr(big2), ptr(small2), dt == torch.int64, ptr(lo), ptr(cnt), ns,
-                                          EXISTS_OPS[op], ptr(hit), stream(big2))
+                                          EXISTS_OPS[op], ptr(mk), ptr(hit), stream(lo))
     return hit
 
 

@@ -214,3 +214,21 @@ def test_in_place_filtered_probe_side(gpu_device, monkeypatch, sorted_min):
         assert digest(e.query(queries.QUERIES[q] + " ")) == want, q
     if sorted_min == 1000:
         assert J.IN_PLACE_STATS["probes"] > 0 and KERNEL_CALLS["sorted_masked"] > 0
+
+
+def test_in_place_exists_side(gpu_device, monkeypatch):
+    """[NOT] EXISTS against a filtered scan in index form searches the
+    table's own sorted key column under the filter mask (joins.py
+    _in_place_semi; Q21's l3, Q4's lineitem) vs the compacted run."""
+    from igloo_amd.models.tpch import datagen, queries
+    from igloo_amd.utils.digest import digest
+    monkeypatch.setattr(J, "SORTED_JOIN_MIN_ROWS", 1000)
+    e = ig.QueryEngine(device=gpu_device)
+    datagen.register(e, 0.05)
+    s0 = J.IN_PLACE_STATS["semis"]
+    for q in (4, 16, 20, 21, 22):
+        monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.0)
+        want = digest(e.query(queries.QUERIES[q]))
+        monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.125)
+        assert digest(e.query(queries.QUERIES[q] + " ")) == want, q
+    assert J.IN_PLACE_STATS["semis"] > s0
