@@ -680,12 +680,12 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("sorted_match", [](uintptr_t big2, uintptr_t small2, bool key64, uintptr_t lo, uintptr_t cnt, int64_t ns,
                            uintptr_t counts, uintptr_t offsets, uintptr_t sidx, uintptr_t bidx, bool out64,
-                           int64_t out_cap, uintptr_t s) {
+                           int64_t out_cap, uintptr_t first, uintptr_t s) {
     if (ns > 0 && (!big2 || !small2 || !lo || !cnt || (!offsets && !counts) || (offsets && (!sidx || !bidx))))
       throw std::runtime_error("sorted_match: null buffer");
     kern::sorted_match(P<const void>(big2), P<const void>(small2), key64, P<const int64_t>(lo), P<const int64_t>(cnt),
                        ns, P<int32_t>(counts), P<const int64_t>(offsets), P<void>(sidx), P<void>(bidx), out64,
-                       out_cap, S(s));
+                       out_cap, P<int32_t>(first), S(s));
   });
   m.def("sorted_masked", [](uintptr_t mask, uintptr_t lo, uintptr_t cnt, int64_t ns, uintptr_t counts,
                             uintptr_t offsets, uintptr_t sidx, uintptr_t bidx, bool out64, int64_t out_cap,

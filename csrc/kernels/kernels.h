@@ -400,7 +400,7 @@ void sorted_exists(const void* big2, const void* small2, bool key64, const int64
                    int64_t ns, int op, const uint8_t* mask, uint8_t* hit, hipStream_t stream);
 void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
                   int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
-                  int64_t out_cap, hipStream_t stream);
+                  int64_t out_cap, int32_t* first, hipStream_t stream);
 // the (small row, big row) pairs of sorted ranges whose big row is set in
 // ``mask`` (the big side's filter): pass 1 counts (offsets null), pass 2 writes
 void sorted_masked(const uint8_t* mask, const int64_t* lo, const int64_t* cnt, int64_t ns, int32_t* counts,

@@ -182,13 +182,14 @@ __global__ __launch_bounds__(kBlock) void sorted_match_kernel(const K2* __restri
                                                              int32_t* __restrict__ counts,
                                                              const int64_t* __restrict__ offsets,
                                                              O* __restrict__ sidx, O* __restrict__ bidx,
-                                                             int64_t out_cap) {
+                                                             int64_t out_cap, O* __restrict__ first) {
   const uint8_t* __restrict__ mask = reinterpret_cast<const uint8_t*>(big2);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = lo[i], c = cnt[i];
     const K2 key = MASKED ? K2{} : small2[i];
     int64_t o = WRITE ? offsets[i] : 0;
     int32_t m = 0;
+    int64_t f = -1;
     for (int64_t k = 0; k < c; ++k) {
       if (MASKED ? mask[l + k] != 0 : big2[l + k] == key) {
         if (WRITE) {
@@ -200,48 +201,57 @@ __global__ __launch_bounds__(kBlock) void sorted_match_kernel(const K2* __restri
           }
           ++o;
         }
+        if (m == 0) f = l + k;
         ++m;
       }
     }
-    if (!WRITE) counts[i] = m;
+    if (!WRITE) {
+      counts[i] = m;
+      // count pass: the first match too (a row with exactly one match -- every
+      // row, for a foreign key into a primary key -- needs no write pass)
+      if (first) first[i] = (O)f;
+    }
   }
 }
 
 template <typename K2, bool MASKED>
 void launch_match(const void* big2, const void* small2, const int64_t* lo, const int64_t* cnt, int64_t ns,
                   int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64, int64_t out_cap,
-                  hipStream_t stream) {
+                  int32_t* first, hipStream_t stream) {
   const dim3 g(grid_for(ns, kBlock, 1 << 16)), b(kBlock);
   const K2* B = static_cast<const K2*>(big2);
   const K2* S = static_cast<const K2*>(small2);
   if (!offsets)
     hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, false, MASKED>), g, b, 0, stream, B, S, lo, cnt, ns, counts,
-                       nullptr, nullptr, nullptr, 0);
+                       nullptr, nullptr, nullptr, 0, first);
   else if (out64)
     hipLaunchKernelGGL((sorted_match_kernel<K2, int64_t, true, MASKED>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
-                       offsets, static_cast<int64_t*>(sidx), static_cast<int64_t*>(bidx), out_cap);
+                       offsets, static_cast<int64_t*>(sidx), static_cast<int64_t*>(bidx), out_cap, nullptr);
   else
     hipLaunchKernelGGL((sorted_match_kernel<K2, int32_t, true, MASKED>), g, b, 0, stream, B, S, lo, cnt, ns, nullptr,
-                       offsets, static_cast<int32_t*>(sidx), static_cast<int32_t*>(bidx), out_cap);
+                       offsets, static_cast<int32_t*>(sidx), static_cast<int32_t*>(bidx), out_cap, nullptr);
 }
 
 }  // namespace
 
 void sorted_match(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
                   int64_t ns, int32_t* counts, const int64_t* offsets, void* sidx, void* bidx, bool out64,
-                  int64_t out_cap, hipStream_t stream) {
+                  int64_t out_cap, int32_t* first, hipStream_t stream) {
   if (ns <= 0) return;
   if (key64)
-    launch_match<int64_t, false>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, stream);
+    launch_match<int64_t, false>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, first,
+                                 stream);
   else
-    launch_match<int32_t, false>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, stream);
+    launch_match<int32_t, false>(big2, small2, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, first,
+                                 stream);
   check_launch("sorted_match", stream);
 }
 
 void sorted_masked(const uint8_t* mask, const int64_t* lo, const int64_t* cnt, int64_t ns, int32_t* counts,
                    const int64_t* offsets, void* sidx, void* bidx, bool out64, int64_t out_cap, hipStream_t stream) {
   if (ns <= 0) return;
-  launch_match<int32_t, true>(mask, nullptr, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, stream);
+  launch_match<int32_t, true>(mask, nullptr, lo, cnt, ns, counts, offsets, sidx, bidx, out64, out_cap, nullptr,
+                              stream);
   check_launch("sorted_masked", stream);
 }
 

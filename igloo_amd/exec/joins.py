@@ -24,7 +24,7 @@ from ..ops._lib import (check_not_capturing, device_ints, launch, ptr, stream, t
                        to_host_ints, unlogged)
 from ..utils import trace as _trace
 from ..ops.gather import gather_tensor, take, take_many
-from ..ops.select import exclusive_scan, mask_to_indices
+from ..ops.select import count_true, exclusive_scan, mask_to_indices
 from ..sql import logical as L
 from ..sql.expr import AggCall, BinOp, ColRef, Expr, Lit, and_all, col_refs, conjuncts
 from ..utils.errors import ExecutionError, NotSupported
@@ -942,10 +942,28 @@ SEMI_INDEX = os.environ.get("IGLOO_SEMI_INDEX", "1") == "1"
 DENSE_JOIN_SMALL = True
 
 
-def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor]:
+def _unique_pairs(lo: torch.Tensor, cnt: torch.Tensor, n: int, other_n: int, identity_ok: bool):
+    """Pairs of a range search whose searched column holds unique keys (every
+    range has 0 or 1 rows): (query rows with a match, their row in the
+    searched column). All n queries matching -- a foreign key into its
+    primary key, TPC-H's usual case -- gives the identity on the query side:
+    returned as None when ``identity_ok`` (the caller's index vectors then
+    stay as they are: no composition gather)."""
+    hit = cnt > 0
+    total = count_true(hit)
+    it = torch.int32 if max(n, other_n) < 2**31 - 1 else torch.int64
+    if total == n:
+        rows = None if identity_ok else torch.arange(n, dtype=it, device=lo.device)
+        return rows, lo.to(it)
+    rows = mask_to_indices(hit, total)
+    return rows, gather_tensor(lo, rows).to(it)
+
+
+def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
     """(left row, right row) index pairs of an inner equi-join on packed keys:
     binary search into a sorted big side, else hash build on the smaller side
-    (first-match probe when the build keys are unique)."""
+    (first-match probe when the build keys are unique). ``identity_ok``: a
+    side whose rows all pair up once, in order, is returned as None."""
     n_l, n_r = lk.numel(), rk.numel()
     dev = lk.device
     if n_l == 0 or n_r == 0:
@@ -958,11 +976,15 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         with ctx.span("join.sorted_search"):
             lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
-            # a big side with NULLs or probed in place under its filter mask
-            # (MultiJoinExec._late_join): only its set rows pair up
-            sidx, bidx = H.expand_ranges(lo, cnt, big.numel()) if bvalid is None else \
-                H.masked_expand(lo, cnt, bvalid, big.numel())
-        ctx.note_partial_read(big, sidx.numel())
+            if bvalid is None and UNIQUE_PAIRS and H.key_unique(big):
+                # (orders.o_orderkey searched by lineitem keys: one row each)
+                sidx, bidx = _unique_pairs(lo, cnt, small.numel(), big.numel(), identity_ok)
+            else:
+                # a big side with NULLs or probed in place under its filter
+                # mask (MultiJoinExec._late_join): only its set rows pair up
+                sidx, bidx = H.expand_ranges(lo, cnt, big.numel()) if bvalid is None else \
+                    H.masked_expand(lo, cnt, bvalid, big.numel())
+        ctx.note_partial_read(big, bidx.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and DENSE_JOIN_SMALL and svalid is None and small.numel() >= SORTED_JOIN_MIN_ROWS \
             and _dense_lookup_ok(small, big.numel()):
@@ -971,7 +993,10 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
         # the bigger side looks its key up (two reads) — no hash table is built
         with ctx.span("join.dense_lookup"):
             lo, cnt = H.sorted_ranges(small, big, bvalid)
-            bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
+            if UNIQUE_PAIRS and H.key_unique(small):
+                bidx, sidx = _unique_pairs(lo, cnt, big.numel(), small.numel(), identity_ok)
+            else:
+                bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \
             and big.numel() >= SORTED_JOIN_MIN_ROWS and PERM_INDEX_RATIO * small.numel() <= big.numel() \
@@ -1010,6 +1035,8 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx) -> Tuple[torch.Tensor, torch.Tensor
     with ctx.span("join.probe"):
         if table.unique:
             bsel, ssel = table.probe_select(big, bvalid)
+            if identity_ok and bsel.numel() == big.numel():
+                bsel = None      # every probe row found its one partner, in order
         else:
             bsel, ssel, _ = table.probe_pairs(big, bvalid)
     return (ssel, bsel) if big_right else (bsel, ssel)
@@ -1056,7 +1083,8 @@ def _two_key_sorted_pairs(A, B, on, ctx) -> Optional[Tuple[torch.Tensor, torch.T
         dt = torch.int64 if torch.int64 in (b1.dtype, s1.dtype) else torch.int32
         k2 = torch.int64 if torch.int64 in (b2.dtype, s2.dtype) else torch.int32
         with ctx.span("join.sorted_match"):
-            sidx, bidx = H.sorted_match_pairs(b1.to(dt), b2.to(k2), s1.to(dt), s2.to(k2))
+            sidx, bidx = H.sorted_match_pairs(b1.to(dt), b2.to(k2), s1.to(dt), s2.to(k2),
+                                              identity_ok=UNIQUE_PAIRS)
         return (sidx, bidx) if big_right else (bidx, sidx)
     return None
 
@@ -1175,6 +1203,9 @@ class LateBatch(Batch):
 
 
 PRUNE_PARTS = True
+#: a search into unique keys pairs each query row with at most one row: no
+#: range expansion, and the identity when every row matches (inner_pairs)
+UNIQUE_PAIRS = os.environ.get("IGLOO_UNIQUE_PAIRS", "1") == "1"
 
 #: a filtered scan keeping at least this fraction of its table probes the
 #: table's key column under its filter mask instead of a gathered copy
@@ -1459,15 +1490,21 @@ class MultiJoinExec(ExecNode):
                     lvalid = m if lvalid is None else lvalid & m
                 else:
                     rvalid = m if rvalid is None else rvalid & m
-            lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx)
+            lidx, ridx = inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok=True)
+
+        def comp(X: "LateBatch", idx):
+            # (None: every row of X pairs up once, in order -- its index vectors stay)
+            return list(X.parts) if idx is None else X.compose(idx)
+        n = lidx.numel() if lidx is not None else ridx.numel() if ridx is not None else A.num_rows
         if residual is not None:
             with ctx.span("join.residual"):
-                P = LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
+                P = LateBatch(comp(A, lidx) + comp(B, ridx), n)
                 keep = mask_to_indices(predicate_mask(residual, P, ctx))
-                lidx = gather_tensor(lidx, keep)
-                ridx = gather_tensor(ridx, keep)
+                lidx = keep if lidx is None else gather_tensor(lidx, keep)
+                ridx = keep if ridx is None else gather_tensor(ridx, keep)
+                n = keep.numel()
         with ctx.span("join.compose"):
-            return LateBatch(A.compose(lidx) + B.compose(ridx), lidx.numel())
+            return LateBatch(comp(A, lidx) + comp(B, ridx), n)
 
     @staticmethod
     def _ndv_needs(rels, conds, only=None) -> list:

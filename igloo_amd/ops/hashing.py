@@ -584,11 +584,14 @@ def expand_ranges(lo: torch.Tensor, cnt: torch.Tensor, big_n: int, scanned=None)
     return sidx, bidx
 
 
-def sorted_match_pairs(big1: torch.Tensor, big2: torch.Tensor, small1: torch.Tensor, small2: torch.Tensor
-                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+def sorted_match_pairs(big1: torch.Tensor, big2: torch.Tensor, small1: torch.Tensor, small2: torch.Tensor,
+                       identity_ok: bool = False) -> Tuple[Optional[torch.Tensor], torch.Tensor]:
     """(small row, big row) pairs with big1 == small1 and big2 == small2, big1
     non-decreasing (ranges on the first key, then the second key checked inside
-    each range on the device). Grouped by small row."""
+    each range on the device). Grouped by small row. ``identity_ok``: when
+    every small row has exactly one match (Q9's lineitem into partsupp's
+    (partkey, suppkey) key) the small side comes back as None and the count
+    pass's first matches are the big rows: no scan, no write pass."""
     lo, cnt = sorted_ranges(big1, small1)
     ns = small1.numel()
     big2 = _keys_ok(big2)
@@ -601,14 +604,23 @@ def sorted_match_pairs(big1: torch.Tensor, big2: torch.Tensor, small1: torch.Ten
     st = stream(big1)
     counts = torch.empty(max(ns, 1), dtype=torch.int32, device=big1.device)
     k64 = big2.dtype == torch.int64
-    N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, ptr(counts), 0, 0, 0, False, 0, st)
-    off, total = exclusive_scan(counts[:ns])
+    first = torch.empty(ns, dtype=torch.int32, device=big1.device) \
+        if identity_ok and ns and max(big1.numel(), ns) < INT32_MAX else None
+    N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, ptr(counts), 0, 0, 0, False, 0, ptr(first), st)
+    if first is not None:
+        c = counts[:ns]
+        total, odd = to_host_ints(torch.stack([c.sum(), (c != 1).sum()]))
+        if odd == 0:
+            return None, first
+        off, _ = exclusive_scan(c, host_total=False)
+    else:
+        off, total = exclusive_scan(counts[:ns])
     it = torch.int32 if max(total, big1.numel(), ns) < INT32_MAX else torch.int64
     sidx = torch.empty(total, dtype=it, device=big1.device)
     bidx = torch.empty(total, dtype=it, device=big1.device)
     if total:
         N.sorted_match(ptr(big2), ptr(small2), k64, ptr(lo), ptr(cnt), ns, 0, ptr(off), ptr(sidx), ptr(bidx),
-                       it == torch.int64, total, st)
+                       it == torch.int64, total, 0, st)
     return sidx, bidx
 
 

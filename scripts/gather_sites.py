@@ -71,23 +71,25 @@ def main():
 
     def take_many(cols, idx, neg=False):
         out, ev = timed(lambda: o_many(cols, idx, neg), [c.data for c in cols if not c.is_plain_string], idx, "m")
-        r = rec[("take_many", site())]
+        key = ("take_many", site())
+        r = rec[key]
         r[0] += 1
         r[1] += idx.numel()
         b = sum(c.data.numel() * c.data.element_size() for c in out if not c.is_plain_string)
         r[2] += b
         if ev:
-            events.append(ev + (idx.numel(), b))
+            events.append(ev + (idx.numel(), b, key))
         return out
 
     def gather_tensor(t, idx):
         out, ev = timed(lambda: o_tensor(t, idx), [t], idx, "t")
-        r = rec[("gather_tensor", site())]
+        key = ("gather_tensor", site())
+        r = rec[key]
         r[0] += 1
         r[1] += idx.numel()
         r[2] += out.numel() * out.element_size()
         if ev:
-            events.append(ev + (idx.numel(), out.numel() * out.element_size()))
+            events.append(ev + (idx.numel(), out.numel() * out.element_size(), key))
         return out
 
     def take_str(col, idx, neg):
@@ -118,9 +120,11 @@ def main():
         e.sql(queries.QUERIES[q])
         sync()
         qms = 0.0
-        for ev0, ev1, k, rows, b in events:
+        site_ms = collections.Counter()
+        for ev0, ev1, k, rows, b, key in events:
             ms = ev0.elapsed_time(ev1)
             qms += ms
+            site_ms[key] += ms
             c = by_class[k]
             c[0] += 1
             c[1] += ms
@@ -129,7 +133,8 @@ def main():
         tot = sum(v[2] for v in rec.values())
         lines.append(f"== Q{q}: {tot / 1e9:.3f} GB gathered" + (f", {qms:.3f} ms in gather launches" if a.timed else ""))
         for (kind, s), (c, rows, b) in sorted(rec.items(), key=lambda kv: -kv[1][2])[:8]:
-            lines.append(f"  {b / 1e9:8.3f} GB {rows / 1e6:9.2f} Mrows {c:4d} calls  {kind:13s} {s}")
+            ms = f"{site_ms[(kind, s)]:7.3f} ms " if a.timed else ""
+            lines.append(f"  {ms}{b / 1e9:8.3f} GB {rows / 1e6:9.2f} Mrows {c:4d} calls  {kind:13s} {s}")
     if a.timed:
         lines.append("\n== by index pattern / source size (fixed-width gathers, event-timed)")
         for k, (c, ms, rows, b) in sorted(by_class.items(), key=lambda kv: -kv[1][1]):
