@@ -581,6 +581,13 @@ PYBIND11_MODULE(_native, m) {
     kern::str_eq_rows(P<const int64_t>(aoff), P<const uint8_t>(achars), P<const void>(ai), P<const int64_t>(boff),
                       P<const uint8_t>(bchars), P<const void>(bi), idx64, n, P<int>(mism), S(s));
   });
+  m.def("str_in_set", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t vb, uintptr_t voff, uintptr_t vmode,
+                         int nv, uintptr_t out, uintptr_t s) {
+    if (n > 0 && (!off || !out || nv < 0 || (nv > 0 && (!vb || !voff || !vmode))))
+      throw std::runtime_error("str_in_set: bad arguments");
+    kern::str_in_set(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(vb), P<const int32_t>(voff),
+                     P<const uint8_t>(vmode), nv, P<uint8_t>(out), S(s));
+  });
   m.def("str_cmp_const", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t c, int64_t cn, int op, uintptr_t out,
                             uintptr_t s) {
     kern::str_cmp_const(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint8_t>(c), cn, op,

@@ -319,6 +319,9 @@ void str_eq_rows(const int64_t* aoff, const uint8_t* achars, const void* ai, con
                  const void* bi, bool idx64, int64_t n, int* mismatches, hipStream_t stream);
 void str_cmp_const(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* c, int64_t cn, int op,
                    uint8_t* out, hipStream_t stream);
+// rows equal to (vmode 1: starting with) one of nv constants (bytes vb, offsets voff[nv + 1])
+void str_in_set(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* vb, const int32_t* voff,
+                const uint8_t* vmode, int nv, uint8_t* out, hipStream_t stream);
 void str_prefix_key(const int64_t* off, const uint8_t* chars, int64_t n, int64_t skip, int64_t* out,
                     hipStream_t stream);
 

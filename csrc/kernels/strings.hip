@@ -590,6 +590,31 @@ __global__ __launch_bounds__(kBlock) void cmp_const_kernel(const int64_t* __rest
   }
 }
 
+// String IN (constants) in one pass: row i is set when its bytes equal one of
+// the nv constants vb[voff[v] .. voff[v+1]) -- or, with vmode[v] = 1, start
+// with them (substr(x, 1, L) IN (...) for a constant of exactly L code points;
+// UTF-8 is self-synchronising, so a byte prefix of L code points is the
+// substring). Replaces one compare pass per constant plus the substring copy
+// (TPC-H Q22's country codes: 7 passes over 15M phone numbers).
+__global__ __launch_bounds__(kBlock) void in_set_kernel(const int64_t* __restrict__ off,
+                                                       const uint8_t* __restrict__ chars, int64_t n,
+                                                       const uint8_t* __restrict__ vb, const int32_t* __restrict__ voff,
+                                                       const uint8_t* __restrict__ vmode, int nv,
+                                                       uint8_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = off[i], len = off[i + 1] - a;
+    bool hit = false;
+    for (int v = 0; v < nv && !hit; ++v) {
+      const int32_t c0 = voff[v], vl = voff[v + 1] - c0;
+      if (vmode[v] ? len < vl : len != vl) continue;
+      bool eq = true;
+      for (int32_t j = 0; j < vl && eq; ++j) eq = chars[a + j] == vb[c0 + j];
+      hit = eq;
+    }
+    out[i] = hit;
+  }
+}
+
 // 8-byte big-endian prefix as an order-preserving uint64 (minus sign flip):
 // first sort key for ORDER BY on strings.
 __global__ __launch_bounds__(kBlock) void prefix_key_kernel(const int64_t* __restrict__ off, const uint8_t* __restrict__ chars,
@@ -739,6 +764,14 @@ void str_cmp_const(const int64_t* off, const uint8_t* chars, int64_t n, const ui
   hipLaunchKernelGGL(cmp_const_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, off, chars, n, c, cn,
                      op, out);
   check_launch("str_cmp_const", stream);
+}
+
+void str_in_set(const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* vb, const int32_t* voff,
+                const uint8_t* vmode, int nv, uint8_t* out, hipStream_t stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(in_set_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, off, chars, n, vb, voff,
+                     vmode, nv, out);
+  check_launch("str_in_set", stream);
 }
 
 void str_prefix_key(const int64_t* off, const uint8_t* chars, int64_t n, int64_t skip, int64_t* out,

@@ -434,6 +434,14 @@ class Evaluator:
         return v
 
     def _InList(self, e: InList, b: Batch) -> Value:
+        x = e.x
+        if isinstance(x, Func) and x.name == "substr" and x.options[0] == 1 and x.options[1] \
+                and x.options[1] >= 1 and all(isinstance(y, Lit) for y in e.values):
+            # substr(s, 1, L) IN (...): the prefixes compared in place (ops/strings.py in_set)
+            c = self.eval(x.args[0], b)
+            if isinstance(c, Column) and c.is_plain_string and c.data.is_cuda:
+                m = S.in_set(c, [str(y.value) for y in e.values if y.value is not None], prefix_chars=x.options[1])
+                return Column(T.BOOL, ~m if e.negated else m, c.valid)
         v = self.eval(e.x, b)
         if isinstance(v, Scalar):
             hit = any(x.value == v.value for x in e.values)

@@ -151,6 +151,16 @@ def device_ints(values, device, dtype=torch.int64) -> torch.Tensor:
     return h.to(device, non_blocking=True)
 
 
+def capture_hold(obj) -> None:
+    """Keep ``obj`` (a device buffer a captured kernel reads, e.g. a cached
+    pattern constant) alive as long as the graph being captured."""
+    if getattr(_capture, "on", False):
+        keep = getattr(_capture, "keep", None)
+        if keep is None:
+            keep = _capture.keep = []
+        keep.append(obj)
+
+
 def capture_keepalive() -> list:
     """Host buffers the current capture's graph reads (cleared per capture)."""
     keep = getattr(_capture, "keep", None) or []

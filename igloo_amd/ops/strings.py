@@ -21,7 +21,7 @@ import torch
 from .. import types as T
 from ..columnar import Column
 from .gather import gather_tensor
-from ._lib import capturing, check_not_capturing, device_ints, is_gpu, launch, note_host_step, ptr, stream, to_host_int
+from ._lib import capture_hold, capturing, check_not_capturing, device_ints, is_gpu, launch, note_host_step, ptr, stream, to_host_int
 from .gather import take
 from .hashing import group_ids
 from .select import offsets_from_lengths
@@ -148,6 +148,8 @@ def _consts(key, build):
         if len(_CONSTS) > 4096:
             _CONSTS.clear()
         v = _CONSTS[key] = build()
+    # a captured graph reads it by address: it must outlive a later clear()
+    capture_hold(v)
     return v
 
 
@@ -221,7 +223,36 @@ def compare_const(col: Column, op: str, value: str) -> torch.Tensor:
     return out
 
 
+def in_set(col: Column, values: Sequence[str], prefix_chars: Optional[int] = None) -> torch.Tensor:
+    """bool per row of a plain string column: the row is one of ``values``;
+    with ``prefix_chars`` L: ``substr(row, 1, L)`` is (a constant of L code
+    points is a byte prefix of the row, a shorter one the whole row). One
+    pass on the GPU (strings.hip in_set_kernel), no substring copy."""
+    vals, modes = [], []
+    for v in dict.fromkeys(values):
+        nch = len(v)
+        if prefix_chars is not None and nch > prefix_chars:
+            continue                     # longer than the substring: never equal
+        vals.append(v.encode("utf-8"))
+        modes.append(1 if prefix_chars is not None and nch == prefix_chars else 0)
+    n = len(col)
+    if not is_gpu(col.data):
+        base = substr(col, 1, prefix_chars) if prefix_chars is not None else col
+        return in_list(base, [v.decode("utf-8") for v in vals]) if vals else torch.zeros(n, dtype=torch.bool)
+    out = torch.empty(n, dtype=torch.bool, device=col.device)
+    key = ("in_set", tuple(vals), tuple(modes), col.device)
+    vb = _consts(key + ("b",), lambda: torch.tensor(list(b"".join(vals)) or [0], dtype=torch.uint8).to(col.device))
+    voff = _consts(key + ("o",), lambda: torch.tensor(np.cumsum([0] + [len(v) for v in vals]).tolist(),
+                                                      dtype=torch.int32).to(col.device))
+    vm = _consts(key + ("m",), lambda: torch.tensor(modes or [0], dtype=torch.uint8).to(col.device))
+    launch("str_in_set").str_in_set(ptr(col.offsets), ptr(col.data), n, ptr(vb), ptr(voff), ptr(vm), len(vals),
+                                    ptr(out), stream(out))
+    return out
+
+
 def in_list(col: Column, values: Sequence[str]) -> torch.Tensor:
+    if not col.is_dict and is_gpu(col.data) and len(values) > 1:
+        return in_set(col, values)
     if col.is_dict:
         if is_gpu(col.data):
             return _dict_lut_dev(col, ("in", tuple(values)), lambda d: in_list(d, values))

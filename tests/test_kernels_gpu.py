@@ -656,3 +656,21 @@ def test_compact_columns_matches_gather(gpu_device, density):
     assert torch.equal(idx.cpu().long(), ref_idx.cpu().long())
     for a, b in zip(got, take_many(cols, ref_idx)):
         assert a.to_arrow().equals(b.to_arrow())
+
+
+@pytest.mark.parametrize("prefix", [None, 2, 3])
+def test_str_in_set(gpu_device, prefix):
+    """One-pass string IN list (strings.hip in_set_kernel), plain and as
+    substr(s, 1, L) IN (...), against the host evaluation."""
+    g = _rng(11)
+    words = ["13", "31", "1", "", "133", "ab", "aé", "ééx", "zz", "13x"]
+    vals = [words[i] for i in g.integers(0, len(words), 5000)] + ["13-555", "31", "aéb"]
+    arr = pa.array(vals, pa.large_string())
+    col = Column.from_arrow(arr, device=DEV, dict_encode=False)
+    consts = ["13", "31", "aé", "éé", "x"]
+    got = S.in_set(col, consts, prefix_chars=prefix).cpu().tolist()
+    if prefix is None:
+        want = [v in consts for v in vals]
+    else:
+        want = [v[:prefix] in consts for v in vals]
+    assert got == want
