@@ -1134,6 +1134,7 @@ class LateBatch(Batch):
         self._cache: Dict[int, Column] = {}
         self.owner = {cid: k for k, (bb, _) in enumerate(parts) for cid in bb.columns}
 
+
     @property
     def num_rows(self):  # type: ignore[override]
         return self._n
@@ -1440,10 +1441,9 @@ class MultiJoinExec(ExecNode):
             b = self._semi(b, rb, sp, ctx)
         return b
 
-    def _prune(self, out: "LateBatch", conds, deferred) -> "LateBatch":
-        """Drop index parts none of whose columns is read any more (by the
-        parent, a remaining join condition or a deferred semi join): later
-        steps then compose fewer row-index vectors."""
+    def _need(self, conds, deferred) -> set:
+        """Columns still read: by the parent, a remaining join condition or a
+        deferred semi join."""
         need = set(self.required)
         for c in conds:
             need |= col_refs(c)
@@ -1452,6 +1452,13 @@ class MultiJoinExec(ExecNode):
                 need |= col_refs(x)
             if sp.residual is not None:
                 need |= col_refs(sp.residual)
+        return need
+
+    def _prune(self, out: "LateBatch", conds, deferred) -> "LateBatch":
+        """Drop index parts none of whose columns is read any more (by the
+        parent, a remaining join condition or a deferred semi join): later
+        steps then compose fewer row-index vectors."""
+        need = self._need(conds, deferred)
         keep = [(bb, idx) for bb, idx in out.parts if any(c in need for c in bb.columns)] or out.parts[:1]
         if len(keep) == len(out.parts):
             return out
@@ -1504,7 +1511,12 @@ class MultiJoinExec(ExecNode):
                 ridx = keep if ridx is None else gather_tensor(ridx, keep)
                 n = keep.numel()
         with ctx.span("join.compose"):
-            return LateBatch(comp(A, lidx) + comp(B, ridx), n)
+            out = LateBatch(comp(A, lidx) + comp(B, ridx), n)
+        # an identity side keeps its rows: its gathered columns stay valid
+        for X, idx in ((A, lidx), (B, ridx)):
+            if idx is None:
+                out._cache.update(X._cache)
+        return out
 
     @staticmethod
     def _ndv_needs(rels, conds, only=None) -> list:
