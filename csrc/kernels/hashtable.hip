@@ -49,14 +49,16 @@ __device__ inline int64_t find_slot(const int64_t* __restrict__ tkeys, int64_t m
 // Insert-or-find `k` (hashed mode); returns the slot and whether the key
 // already existed.
 // A slot's key is read before it is claimed: a key already in the table (every
-// row of a low-cardinality GROUP BY -- Q22's 7 country codes over 636K rows,
+// row of a low-cardinality GROUP BY -- Q22's 7 country codes over 4M rows,
 // which serialised on 7 words as one CAS per row) costs one load, and only an
 // empty slot takes the CAS. Keys are never removed or changed once set, so a
-// stale read can only show EMPTY, which the CAS then settles.
+// stale read can only show EMPTY, which the CAS then settles -- the read may
+// therefore be a plain (L1-cached) load: hot slots are served per CU instead
+// of queueing on one L2 line.
 __device__ inline int64_t insert_slot(int64_t* __restrict__ tkeys, int64_t mask, int64_t k, bool* existed) {
   int64_t slot = (int64_t)(mix64((uint64_t)k) & (uint64_t)mask);
   for (;;) {
-    const int64_t cur = __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t cur = tkeys[slot];
     if (cur == k) { *existed = true; return slot; }
     if (cur == kEmptyKey) {
       unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[slot], (unsigned long long)kEmptyKey,
@@ -293,10 +295,28 @@ __global__ __launch_bounds__(kBlock) void join_expand_kernel(const K* __restrict
   }
 }
 
+// First-row table of a GROUP BY. Hashed keys (!DIRECT) go through a small
+// per-workgroup LDS cache of (slot -> smallest row): rows of a hot group take
+// an LDS atomic, and each workgroup sends one global atomicMin per cached slot
+// at the end. Without it a low-cardinality GROUP BY (Q22's 7 country codes
+// over 636K rows) had every wave's atomics -- and reads -- queue on the same
+// few L2 lines: 262 us for 636K rows. Slots the cache cannot hold (a
+// high-cardinality GROUP BY) take the global path directly.
+constexpr int kRowCache = 256;
+
 template <typename K, bool DIRECT>
 __global__ __launch_bounds__(kBlock) void groupby_build_kernel(const K* __restrict__ keys, int64_t n,
                                                               int64_t* __restrict__ tkeys, int32_t* __restrict__ trow,
                                                               int64_t cap, int64_t kmin) {
+  __shared__ int32_t cslot[DIRECT ? 1 : kRowCache];
+  __shared__ int32_t crow[DIRECT ? 1 : kRowCache];
+  if (!DIRECT) {
+    for (int h = threadIdx.x; h < kRowCache; h += blockDim.x) {
+      cslot[h] = -1;
+      crow[h] = INT32_MAX;
+    }
+    __syncthreads();
+  }
   const int64_t mask = cap - 1;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t k = (int64_t)keys[i];
@@ -309,9 +329,24 @@ __global__ __launch_bounds__(kBlock) void groupby_build_kernel(const K* __restri
     } else {
       bool existed;
       slot = insert_slot(tkeys, mask, k, &existed);
+      const int h = (int)(slot & (kRowCache - 1));
+      int cur = cap <= ((int64_t)1 << 31) ? cslot[h] : -2;    // (slots must fit the int32 cache)
+      if (cur == -1) {
+        cur = atomicCAS(&cslot[h], -1, (int32_t)slot);
+        if (cur == -1) cur = (int32_t)slot;
+      }
+      if (cur == (int32_t)slot) {
+        atomicMin(&crow[h], (int32_t)i);
+        continue;
+      }
     }
     // first occurrence row: plain read first avoids most atomics on hot groups
     if (trow[slot] > (int32_t)i) atomicMin(&trow[slot], (int32_t)i);
+  }
+  if (!DIRECT) {
+    __syncthreads();
+    for (int h = threadIdx.x; h < kRowCache; h += blockDim.x)
+      if (cslot[h] >= 0 && trow[cslot[h]] > crow[h]) atomicMin(&trow[cslot[h]], crow[h]);
   }
 }
 
@@ -526,7 +561,8 @@ void groupby_build(const void* keys, bool key64, int64_t n, int64_t* tkeys, int3
     check_launch("groupby_build_lds", stream);
     return;
   }
-  dim3 g(grid_for(n, kBlock, kMaxGrid)), b(kBlock);
+  // (hashed: several rows per lane, so each workgroup's row cache covers many rows)
+  dim3 g(grid_for(n, direct ? kBlock : kBlock * 8, kMaxGrid)), b(kBlock);
   if (key64) {
     if (direct) hipLaunchKernelGGL((groupby_build_kernel<int64_t, true>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, trow, cap, kmin);
     else hipLaunchKernelGGL((groupby_build_kernel<int64_t, false>), g, b, 0, stream, (const int64_t*)keys, n, tkeys, trow, cap, kmin);

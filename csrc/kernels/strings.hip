@@ -601,15 +601,34 @@ __global__ __launch_bounds__(kBlock) void in_set_kernel(const int64_t* __restric
                                                        const uint8_t* __restrict__ vb, const int32_t* __restrict__ voff,
                                                        const uint8_t* __restrict__ vmode, int nv,
                                                        uint8_t* __restrict__ out) {
+  // constants of at most 8 bytes (the usual case: codes, flags, short names)
+  // compare as masked words against the row's first bytes, loaded once
+  int maxb = 0;
+  for (int v = 0; v < nv; ++v) maxb = max(maxb, voff[v + 1] - voff[v]);
+  const bool words = maxb <= 8;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = off[i], len = off[i + 1] - a;
     bool hit = false;
-    for (int v = 0; v < nv && !hit; ++v) {
-      const int32_t c0 = voff[v], vl = voff[v + 1] - c0;
-      if (vmode[v] ? len < vl : len != vl) continue;
-      bool eq = true;
-      for (int32_t j = 0; j < vl && eq; ++j) eq = chars[a + j] == vb[c0 + j];
-      hit = eq;
+    if (words) {
+      const int nb = len < maxb ? (int)len : maxb;
+      uint64_t w = 0;
+      for (int j = 0; j < nb; ++j) w |= (uint64_t)chars[a + j] << (8 * j);
+      for (int v = 0; v < nv && !hit; ++v) {
+        const int32_t c0 = voff[v], vl = voff[v + 1] - c0;
+        if (vmode[v] ? len < vl : len != vl) continue;
+        uint64_t cw = 0;
+        for (int32_t j = 0; j < vl; ++j) cw |= (uint64_t)vb[c0 + j] << (8 * j);
+        const uint64_t m = vl >= 8 ? ~0ull : ((1ull << (8 * vl)) - 1);
+        hit = (w & m) == cw;
+      }
+    } else {
+      for (int v = 0; v < nv && !hit; ++v) {
+        const int32_t c0 = voff[v], vl = voff[v + 1] - c0;
+        if (vmode[v] ? len < vl : len != vl) continue;
+        bool eq = true;
+        for (int32_t j = 0; j < vl && eq; ++j) eq = chars[a + j] == vb[c0 + j];
+        hit = eq;
+      }
     }
     out[i] = hit;
   }
