@@ -538,14 +538,31 @@ def fused_scan_aggregate(groups, aggs, b: Batch, pred: Optional[Expr], ctx) -> O
             if not jit_aggregate(spec, keys, G, kaggs, counts, ovf, n, stream(counts)):
                 launch("ff_aggregate").ff_aggregate(cols, terms, mask, keys, G, kaggs, counts.data_ptr(),
                                                     ovf.data_ptr(), n, stream(counts))
-    if any(chk for _, chk, _ in descs) and to_host_ints(ovf)[0]:
-        raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
-    from ..ops.agg import _wide_to_result
-    res = [(_wide_to_result(d, d2) if d2 is not None else d) for d, d2 in bufs]
+    # ONE readback for the overflow flag, whether each 128-bit sum fits in 64
+    # bits and the number of non-empty groups (Q1: 7 readbacks -> 1)
+    from ..ops.agg import _wide_flags
+    checked = any(chk for _, chk, _ in descs)
+    wide = [(d, d2) for d, d2 in bufs if d2 is not None]
+    parts = []
+    if checked:
+        parts.append(ovf.reshape(-1)[:1].to(torch.int64))
+    if wide:
+        parts.append(_wide_flags(wide).to(torch.int64))
+    if groups:
+        parts.append((counts > 0).sum().reshape(1))
+    vals = to_host_ints(torch.cat(parts)) if parts else []
+    pos = 0
+    if checked:
+        if vals[0]:
+            raise ExecutionError("decimal multiplication overflows 64-bit fixed point; CAST to DOUBLE")
+        pos = 1
+    flags = iter(vals[pos:pos + len(wide)])
+    pos += len(wide)
+    res = [d if d2 is None else (d if not next(flags) else torch.stack([d, d2], dim=1)) for d, d2 in bufs]
     if groups:
         from ..ops.select import mask_to_indices
-        keep = mask_to_indices(counts > 0)     # replayable size readback (no hidden nonzero sync)
-        ng = keep.numel()
+        ng = vals[pos]
+        keep = mask_to_indices(counts > 0, total=ng)
     else:
         keep, ng = None, 1
 
