@@ -32,10 +32,14 @@ def origin(t: torch.Tensor) -> Optional[torch.Tensor]:
     return None
 
 
-def _inherit(dst: torch.Tensor, src: torch.Tensor) -> None:
+def _inherit(dst: torch.Tensor, src: torch.Tensor, idx: Optional[torch.Tensor] = None) -> None:
     o = origin(src)
     if o is not None:
         dst._igloo_origin = o
+    if idx is not None and getattr(idx, "_igloo_incr", False) and getattr(src, "_igloo_sorted", False) is True:
+        # rows of a sorted column taken in row order stay sorted: later
+        # sorted-join / run-grouping checks need no pass (ops/hashing.py is_sorted)
+        dst._igloo_sorted = True
 
 
 def _cpu_take_tensor(t: torch.Tensor, idx: torch.Tensor, neg: bool) -> torch.Tensor:
@@ -157,7 +161,7 @@ def take_many(cols: Sequence[Column], idx: torch.Tensor, neg: bool = False) -> L
         valid = torch.empty(n, dtype=torch.bool, device=idx.device) if need_valid else None
         descs.append((_src_ptr(c.data), ptr(data), esz, _src_ptr(c.valid), ptr(valid), c.data.shape[0]))
         if not neg:
-            _inherit(data, c.data)
+            _inherit(data, c.data, idx)
             if getattr(idx, "_igloo_incr", False) and getattr(c.data, "_igloo_distinct", False):
                 data._igloo_distinct = True
         out.append(Column(c.dtype, data, valid, dictionary=c.dictionary))

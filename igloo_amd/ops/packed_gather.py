@@ -170,7 +170,7 @@ def packed_take(cols: Sequence[Column], idx: torch.Tensor, neg: bool) -> Dict[in
             fields.append((ptr(valid), 0, 1, 1, 2))
         if not neg:
             from .gather import _inherit
-            _inherit(data, c.data)
+            _inherit(data, c.data, idx)
             if getattr(idx, "_igloo_incr", False) and getattr(c.data, "_igloo_distinct", False):
                 data._igloo_distinct = True
         out[i] = Column(c.dtype, data, valid, dictionary=c.dictionary)
