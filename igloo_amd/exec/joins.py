@@ -1027,7 +1027,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
                 # bitmap lookup)
                 from ..ops.sort import sort_pairs
                 with ctx.span("join.index_sort"):
-                    bidx, sidx = sort_pairs(bidx, sidx, max(1, (big.numel() - 1).bit_length()))
+                    bidx, sidx = sort_pairs(bidx, sidx, max(1, (big.numel() - 1).bit_length()), consume=True)
             return (sidx, bidx) if big_right else (bidx, sidx)
     # hash: build on the smaller side, probe with the bigger
     with ctx.span("join.build"):

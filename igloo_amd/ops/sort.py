@@ -145,10 +145,13 @@ def _pack(group: List[tuple], n: int, perm: Optional[torch.Tensor], device) -> T
     return keys, bits
 
 
-def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, end_bit: int, begin_bit: int = 0
-               ) -> Tuple[torch.Tensor, torch.Tensor]:
+def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, end_bit: int, begin_bit: int = 0,
+               consume: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """Stable sort of (key, value) pairs by key bits [begin_bit, end_bit);
-    keys are int32/int64 tensors holding unsigned values. Returns new tensors."""
+    keys are int32/int64 tensors holding unsigned values. Returns new tensors
+    (``consume``: the caller's contiguous, distinct inputs may serve as the
+    sort's first buffers -- their contents are then undefined -- instead of
+    being copied)."""
     n = keys.numel()
     if not is_gpu(keys):
         k = keys.to(torch.int64)
@@ -158,8 +161,9 @@ def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, end_bit: int, begin_bit: 
             k = k ^ torch.tensor(-(1 << 63), dtype=torch.int64)
         o = torch.sort(k, stable=True).indices
         return keys.index_select(0, o), vals.index_select(0, o)
-    k0 = keys.contiguous().clone()
-    v0 = vals.contiguous().clone()
+    own = consume and keys.is_contiguous() and vals.is_contiguous() and keys.data_ptr() != vals.data_ptr()
+    k0 = keys if own else keys.contiguous().clone()
+    v0 = vals if own else vals.contiguous().clone()
     if n <= 1 or end_bit <= begin_bit:
         return k0, v0
     N = launch("radix_sort")
