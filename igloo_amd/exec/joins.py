@@ -1340,6 +1340,10 @@ class MultiJoinExec(ExecNode):
                 agg = semi_aggregate(sp.kind, sp.on, sp.residual, sp.null_aware, lc, sp.right, rex, ctx,
                                      ("multi", id(sp)))
             semis.append((sp, agg[0] if agg is not None else rex.execute(ctx)))
+        # the filtered inputs' row counts: one readback for all of them
+        from ..ops.select import MaskRows
+        MaskRows.resolve([p for p in (getattr(b, "pending_rows", None) for b in
+                                      [r["batch"] for r in rels] + [rb for _, rb in semis]) if p is not None])
         conds = list(lg.conds)
         # global row counts of every input (SPMD: every rank must derive the
         # same join order) — together with the merged NDV sketches of every

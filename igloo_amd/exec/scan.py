@@ -176,7 +176,9 @@ class ScanExec(ExecNode):
                     hit = ctx.scan_cache[key] = (idx, taken)
                 else:
                     with ctx.span("scan.filter_eval"):
-                        rows = MaskRows(m)
+                        # (index form: the count's readback may wait for the
+                        # parent join's, MaskRows.resolve)
+                        rows = MaskRows(m, defer=late)
                     # (the mask stays with the index form: a join may probe the
                     # table's own key column under it instead of gathering it,
                     # and then the index vector is never written)
@@ -405,10 +407,20 @@ class _LazyScanBatch(Batch):
         self.src, self._rows, self._names, self._shared, self._ctx = src, rows, names, shared, ctx
         # bool[src rows]: the filter the rows came from (None: not kept)
         self.mask = rows.mask if isinstance(rows, MaskRows) else None
-        self.num_rows = rows.total if isinstance(rows, MaskRows) else rows.numel()
         self.dist = src.dist
         self.out_dist = None
         self.columns = _ScanColumns(self)
+
+    @property
+    def num_rows(self) -> int:  # type: ignore[override]
+        r = self._rows
+        return r.total if isinstance(r, MaskRows) else r.numel()
+
+    @property
+    def pending_rows(self):
+        """The MaskRows whose count is not read back yet (or None)."""
+        r = self._rows
+        return r if isinstance(r, MaskRows) and r._total is None else None
 
     @property
     def idx(self) -> torch.Tensor:

@@ -1,11 +1,11 @@
 """Stream compaction and prefix sums (csrc/kernels/select.hip, scan.hip)."""
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import idx_dtype, is_gpu, launch, ptr, stream, to_host_int
+from ._lib import idx_dtype, is_gpu, launch, ptr, stream, to_host_int, to_host_ints
 
 
 def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Tensor:
@@ -40,23 +40,42 @@ class MaskRows:
     ``idx`` -- a join probing the masked table in place never does
     (exec/joins.py _in_place_side)."""
 
-    __slots__ = ("mask", "total", "_ws", "_idx")
+    __slots__ = ("mask", "_total", "_ws", "_idx", "_tiles")
 
-    def __init__(self, mask: torch.Tensor):
+    def __init__(self, mask: torch.Tensor, defer: bool = False):
+        """``defer``: the count's readback waits until ``total`` is read (or
+        ``resolve`` reads several at once: a multi-way join's filtered inputs
+        are counted with one readback)."""
         assert mask.dtype == torch.bool and mask.dim() == 1
         self.mask = mask.contiguous()
         self._idx = None
         self._ws = None
+        self._total = None
         if not is_gpu(mask):
             self._idx = mask_to_indices(self.mask)
-            self.total = self._idx.numel()
+            self._total = self._idx.numel()
             return
         n = mask.numel()
         N = launch("select")
-        tiles = N.select_num_tiles(n)
+        self._tiles = tiles = N.select_num_tiles(n)
         self._ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
         N.select_count(ptr(self.mask), n, ptr(self._ws), ptr(self._ws) + 8 * tiles, stream(mask))
-        self.total = to_host_int(self._ws[tiles:])
+        if not defer:
+            self._total = to_host_int(self._ws[tiles:])
+
+    @property
+    def total(self) -> int:
+        if self._total is None:
+            self._total = to_host_int(self._ws[self._tiles:])
+        return self._total
+
+    @staticmethod
+    def resolve(rows: Sequence["MaskRows"]) -> None:
+        """Read the pending counts of ``rows`` back together (one sync)."""
+        pend = [r for r in rows if r._total is None]
+        if len(pend) > 1:
+            for r, v in zip(pend, to_host_ints(torch.cat([r._ws[r._tiles:] for r in pend]))):
+                r._total = v
 
     @property
     def idx(self) -> torch.Tensor:
