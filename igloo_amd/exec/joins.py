@@ -1031,10 +1031,12 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
             return (sidx, bidx) if big_right else (bidx, sidx)
     # hash: build on the smaller side, probe with the bigger
     with ctx.span("join.build"):
-        table = H.JoinTable(small, svalid)
+        # (uniqueness of the build keys is read back with the probe's hit total)
+        table = H.JoinTable(small, svalid, defer_unique=True)
     with ctx.span("join.probe"):
-        if table.unique:
-            bsel, ssel = table.probe_select(big, bvalid)
+        sel = table.probe_select(big, bvalid) if table._unique is not False else None
+        if sel is not None:
+            bsel, ssel = sel
             if identity_ok and bsel.numel() == big.numel():
                 bsel = None      # every probe row found its one partner, in order
         else:

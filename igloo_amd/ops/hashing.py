@@ -179,9 +179,13 @@ def _keys_ok(k: torch.Tensor) -> torch.Tensor:
 class JoinTable:
     """Hash table over build-side keys (int32/int64; NULL keys never match)."""
 
-    def __init__(self, keys: torch.Tensor, valid: Optional[torch.Tensor] = None):
+    def __init__(self, keys: torch.Tensor, valid: Optional[torch.Tensor] = None, defer_unique: bool = False):
+        """``defer_unique``: the build's duplicate count is read back only when
+        ``unique`` is first asked -- or together with the first
+        ``probe_select``'s hit total (one readback for both)."""
         keys = _keys_ok(keys)
         self.n = n = keys.numel()
+        self._dups = None
         self.device = keys.device
         self.gpu = is_gpu(keys)
         self.valid = valid
@@ -239,11 +243,35 @@ class JoinTable:
             # debug / test mode: the tag-derived uniqueness must match the build's own duplicate count
             if to_host_int(dups) != 0:
                 raise AssertionError("key_unique() trusted a key tag on keys that hold duplicates")
-        self.unique = known_unique or to_host_int(dups) == 0
-        # duplicate keys: CSR runs (count -> exclusive scan -> scatter), so a
-        # multi-match probe reads one contiguous run of build rows
         self.cstart = self.crows = None
-        if not self.unique:
+        self._csr_src = (keys, valid)
+        if known_unique:
+            self._unique = True
+        elif defer_unique:
+            self._unique, self._dups = None, dups
+        else:
+            self._set_unique(to_host_int(dups) == 0)
+
+    @property
+    def unique(self) -> bool:
+        if self._unique is None:
+            self._set_unique(to_host_int(self._dups) == 0)
+        return self._unique
+
+    @unique.setter
+    def unique(self, v: bool) -> None:
+        self._unique = v
+
+    def _set_unique(self, u: bool) -> None:
+        """Record the build's uniqueness; duplicate keys get CSR runs (count ->
+        exclusive scan -> scatter), so a multi-match probe reads one
+        contiguous run of build rows."""
+        self._unique, self._dups = u, None
+        if not u:
+            keys, valid = self._csr_src
+            k64 = keys.dtype == torch.int64
+            st = stream(keys)
+            n = self.n
             cnt = torch.zeros(self.cap + 1, dtype=self.rid, device=self.device)
             launch("join_csr_count").join_csr_count(ptr(keys), k64, ptr(valid), n, ptr(self.tkeys), ptr(cnt),
                                                     self.rid64, self.cap, self.kmin, self.direct, st)
@@ -266,6 +294,7 @@ class JoinTable:
                     build_matched: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One matching build row per probe row (-1 if none). Exact for unique builds;
         with duplicates it returns an arbitrary match (enough for semi/anti joins)."""
+        self.unique      # a deferred duplicate count is read now (CSR runs built if any)
         pkeys = _keys_ok(pkeys)
         m = pkeys.numel()
         if self.empty or m == 0:
@@ -306,7 +335,16 @@ class JoinTable:
         bits, bmask = self._bloom(m)
         N.probe_hits(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
                      self.kmin, self.direct, bits, bmask, negate, ptr(words), ptr(tcount), st)
-        toff, total = exclusive_scan(tcount)
+        if self._unique is None:
+            # deferred duplicate count: read back with the hit total (one sync);
+            # duplicate build keys leave the pairs to the multi-match probe
+            toff, tdev = exclusive_scan(tcount, host_total=False)
+            dups, total = to_host_ints(torch.cat([self._dups.reshape(-1)[:1], tdev.reshape(-1)[:1]]))
+            self._set_unique(dups == 0)
+            if dups and want_build and not negate:
+                return None
+        else:
+            toff, total = exclusive_scan(tcount)
         it = torch.int32 if m < INT32_MAX else torch.int64
         pidx = torch.empty(total, dtype=it, device=dev)
         bidx = torch.empty(total, dtype=self.rid, device=dev) if want_build and not negate else None
@@ -321,6 +359,7 @@ class JoinTable:
         """All (probe_row, build_row) matches, grouped by probe row.
         Returns (probe_idx int32, build_idx (int32 below 2^31 build rows, else int64),
         counts int32 per probe row)."""
+        self.unique      # a deferred duplicate count is read now (CSR runs built if any)
         pkeys = _keys_ok(pkeys)
         m = pkeys.numel()
         dev = pkeys.device
