@@ -184,7 +184,7 @@ def gather_tensor(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         esz = t.element_size() * (t.shape[1] if t.dim() == 2 else 1)
         launch("gather_multi").gather_multi(ptr(idx), idx.dtype == torch.int64, n,
                                             [(ptr(t), ptr(out), esz, 0, 0, t.shape[0])], stream(idx))
-    _inherit(out, t)
+    _inherit(out, t, idx)
     return out
 
 

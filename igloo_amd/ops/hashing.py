@@ -352,6 +352,7 @@ class JoinTable:
             N.probe_write(ptr(pkeys), k64, ptr(pvalid), m, ptr(self.tkeys), ptr(self.thead), self.rid64, self.cap,
                           self.kmin, self.direct, ptr(words), ptr(toff), ptr(pidx), it == torch.int64, ptr(bidx),
                           pidx.numel(), st)
+        pidx._igloo_incr = True      # hit rows in row order
         return pidx, bidx
 
     def probe_pairs(self, pkeys: torch.Tensor, pvalid: Optional[torch.Tensor] = None,
@@ -432,6 +433,11 @@ def is_sorted(keys: torch.Tensor) -> bool:
     resident key columns of a table are checked once)."""
     hit = getattr(keys, "_igloo_sorted", None)
     if hit is not None:
+        if hit and CHECK_KEY_TAGS and not capturing() and not getattr(keys, "_igloo_resident", False) \
+                and keys.numel() > 1 and keys.is_cuda:
+            # test mode: a sortedness tag inferred through gathers must hold
+            if to_host_int((keys[1:] < keys[:-1]).any().to(torch.int64)):
+                raise AssertionError("an inferred sorted tag does not hold")
         return hit
     base = getattr(keys, "_igloo_base", None)
     if base is not None and base[0].data.dtype == keys.dtype and is_sorted(base[0].data):

@@ -205,9 +205,10 @@ def test_in_place_filtered_probe_side(gpu_device, monkeypatch, sorted_min):
     from igloo_amd.ops._lib import KERNEL_CALLS
     from igloo_amd.utils.digest import digest
     monkeypatch.setattr(J, "SORTED_JOIN_MIN_ROWS", sorted_min)
+    monkeypatch.setattr(H, "CHECK_KEY_TAGS", True)     # inferred sorted / bound / unique tags must hold
     e = ig.QueryEngine(device=gpu_device)
     datagen.register(e, 0.05)
-    for q in (3, 5, 7, 10, 12, 21):
+    for q in (3, 5, 7, 9, 10, 12, 21):
         monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.0)
         want = digest(e.query(queries.QUERIES[q]))
         monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.125)
