@@ -73,10 +73,14 @@ def column_stats(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Tu
     else:
         mn, mx, bad = to_host_ints(out)
     res = ((mn, mx) if mn <= mx else None), (bad == 0 and valid is None)
-    if valid is None and getattr(keys, "_igloo_resident", False):
+    if valid is None:
+        # remembered on any key tensor (like is_sorted's flag): a sortedness
+        # check followed by a range lookup of the same keys (group_ids_ex ->
+        # group_ids, inner_pairs -> JoinTable) reads the stats back once
         try:
             keys._igloo_stats = res
-            keys._igloo_sorted = res[1]
+            if getattr(keys, "_igloo_resident", False):
+                keys._igloo_sorted = res[1]
         except (AttributeError, RuntimeError):
             pass
     return res
