@@ -605,6 +605,27 @@ def _bound_node(e: Expr, b: Batch) -> Optional[Tuple[float, float]]:
         return None if x is None else (-x[1], -x[0])
     if isinstance(e, Cast):
         return _bound(e.x, b)
+    if isinstance(e, Func) and e.name == "date_part" and e.options:
+        field = e.options[0]
+        fixed = {"month": (1, 12), "day": (1, 31), "quarter": (1, 4), "dow": (0, 6), "doy": (1, 366)}
+        if field in fixed:
+            return fixed[field]
+        x = e.args[0] if e.args else None
+        if field != "year" or not isinstance(x, ColRef) or x.dtype.kind != "date32":
+            return None
+        c = b.columns.get(x.cid)
+        if c is None or c.data.dim() != 1 or c.data.dtype not in (torch.int32, torch.int64):
+            return None
+        from ..ops.hashing import key_bound
+        kb = key_bound(c.data)
+        if kb is None:
+            return None
+        import datetime
+        try:
+            d0 = datetime.date(1970, 1, 1)
+            return (d0 + datetime.timedelta(days=kb[0])).year, (d0 + datetime.timedelta(days=kb[1])).year
+        except OverflowError:
+            return None
     if isinstance(e, Case):
         arms = [v for _, v in e.whens] + ([e.else_] if e.else_ is not None else [])
         bs = [_bound(v, b) for v in arms]

@@ -53,3 +53,23 @@ def test_expression_bounds():
     b32 = Batch({1: Column(T.INT32, price.to(torch.int32), None)}, 2)
     b32.columns[1].data._igloo_bound = (90000, 10494950)
     assert J._bound(big, b32) is None                       # would wrap in 32 bits
+
+
+def test_date_part_bounds():
+    """date_part bounds: fixed ranges for month / quarter / ..., the year
+    range of a date column with a readback-free bound."""
+    import torch
+    from igloo_amd import types as T
+    from igloo_amd.columnar import Batch, Column
+    from igloo_amd.exec import expr_jit as J
+    from igloo_amd.sql.expr import ColRef, Func
+
+    DATE = T.DataType("date32")
+    days = torch.tensor([8035, 10591], dtype=torch.int32)     # 1992-01-01 .. 1998-12-31
+    days._igloo_bound = (8035, 10591)
+    b = Batch({1: Column(DATE, days, None)}, 2)
+    year = Func("date_part", [ColRef(1, "d", DATE)], T.INT32, ("year",))
+    assert J._bound(year, b) == (1992, 1998)
+    assert J._bound(Func("date_part", [ColRef(1, "d", DATE)], T.INT32, ("month",)), b) == (1, 12)
+    del days._igloo_bound
+    assert J._bound(year, b) is None
