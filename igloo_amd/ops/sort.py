@@ -32,6 +32,10 @@ SortKey = Tuple[torch.Tensor, bool, bool, Optional[torch.Tensor]]
 _KIND = {torch.int8: (0, 1), torch.int16: (0, 2), torch.int32: (0, 4), torch.int64: (0, 8),
          torch.float64: (1, 8), torch.uint8: (2, 1), torch.bool: (2, 1), torch.float32: (3, 4)}
 U64 = (1 << 64) - 1
+#: integer key dtypes and their full value ranges (sort keys without a bound)
+_FULL = {torch.int8: (-(1 << 7), (1 << 7) - 1), torch.int16: (-(1 << 15), (1 << 15) - 1),
+         torch.int32: (-(1 << 31), (1 << 31) - 1), torch.int64: (-(1 << 63), (1 << 63) - 1),
+         torch.uint8: (0, 255), torch.bool: (0, 1)}
 #: inputs up to this many rows sort in one workgroup (sort.hip kRsTile)
 SMALL_SORT = 4096
 
@@ -64,6 +68,12 @@ def _fields(keys: Sequence[SortKey]) -> List[tuple]:
         # every key has a readback-free bound (resident origin, dictionary
         # codes, group ids): a wider field than the exact range, same order
         return _fields_from(keys, known)
+    if all(v.numel() <= SMALL_SORT and is_gpu(v) and v.dtype in _FULL and (valid is None or v.dtype != torch.int64)
+           for v, _desc, _nf, valid in keys):
+        # a small sort (one workgroup) over integer keys: full-width fields
+        # cost a few more digit passes inside one kernel, far less than the
+        # host sync that would read the exact ranges (ORDER BY of a result)
+        return _fields_from(keys, [x for v, _d, _n, _v in keys for x in _FULL[v.dtype]])
     stats = []
     for v, _desc, _nf, _valid in keys:
         if v.numel() == 0:
