@@ -33,8 +33,14 @@ table once per query; index / range searches count only the rows touched).
 ``--source hbm`` runs on tables generated straight into HBM (no Parquet).
 
 Single GPU:  python bench.py --gpus 1 --steps 3 --warmup 1
-N GPUs:      python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+N GPUs:      python bench.py --gpus N ...   (launches N rank processes itself), or
+             python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
                  --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+With ``--gpus N > 1`` and no launcher environment (no WORLD_SIZE), this
+process starts ``torch.distributed.run`` with N ranks as a CHILD process
+before anything touches the GPU (it only counts devices), and exits with the
+child's code; rank 0 prints the JSON line. A world that does not equal
+``--gpus``, or more ranks than visible GPUs, is an error (exit 2).
 """
 from __future__ import annotations
 
@@ -64,6 +70,38 @@ def parse_queries(s: str):
 _MODE_TAG = {"recorded": "R", "replayed": "P", "graph": "G", "partial": "x"}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a, argv) -> int:
+    """``--gpus N`` without a launcher: run N ranks under torch.distributed.run
+    as a child process (never exec: the GPU may not be touched by a process
+    that later replaces itself) and return its exit code. Only the device
+    COUNT is read here (torch.cuda.device_count does not initialise HIP)."""
+    shared = os.environ.get("IGLOO_BENCH_SHARE_GPU") == "1"
+    if not a.cpu and not shared:
+        import torch
+        ngpu = torch.cuda.device_count()
+        if ngpu < a.gpus:
+            print(f"[bench] error: --gpus {a.gpus} but only {ngpu} GPU(s) visible; one rank per GPU is required "
+                  f"(IGLOO_BENCH_SHARE_GPU=1 rehearses several ranks on one GPU over gloo)", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -91,20 +129,30 @@ def main():
                     help="suites with fresh TPC-H substitution parameters per query (adhoc_s; 0 = skip)")
     a = ap.parse_args()
 
+    if a.gpus < 1:
+        print(f"[bench] error: --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"[bench] error: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
+
     import torch
     import igloo_amd as ig
     from igloo_amd.models.tpch import datagen, parquet_gen, queries
     from igloo_amd.utils.digest import digest
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     # IGLOO_BENCH_SHARE_GPU=1: every rank on cuda:0 with host-staged gloo
     # collectives — a rehearsal of the multi-rank path on a one-GPU box
     shared = os.environ.get("IGLOO_BENCH_SHARE_GPU") == "1"
     device = "cpu" if a.cpu else ("cuda:0" if shared else f"cuda:{local}")
+    if not a.cpu and not shared and local >= torch.cuda.device_count():
+        print(f"[bench] error: rank {rank} (local {local}) has no GPU: {torch.cuda.device_count()} visible",
+              file=sys.stderr)
+        sys.exit(2)
     if not a.cpu:
         torch.cuda.set_device(torch.device(device))
     comm = None
@@ -119,6 +167,9 @@ def main():
         os.environ.setdefault("WORLD_SIZE", str(world))
         comm = Communicator.init(backend="gloo" if (a.cpu or shared) else "nccl", device=device,
                                  force_spmd=force_spmd)
+        if comm.world_size != world:
+            print(f"[bench] error: the process group has {comm.world_size} ranks, expected {world}", file=sys.stderr)
+            sys.exit(2)
     spmd = comm is not None
 
     def barrier():
@@ -238,7 +289,12 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t1
     timed_modes = dict(spec_modes)
+    rank_info = None
     if comm is not None:
+        # per-rank timed region and data-plane traffic (outside the timed region)
+        rank_info = comm.allgather_object({"rank": comm.rank, "world": comm.world_size, "device": device,
+                                           "backend": comm.backend, "timed_region_s": round(elapsed, 4),
+                                           "collectives": comm.calls, "bytes_sent": comm.bytes_sent})
         elapsed = comm.allreduce_max_float(elapsed)
     step_s = elapsed / max(a.steps, 1)
 
@@ -365,6 +421,10 @@ def main():
                        "layout": ("fact tables (lineitem, orders) hash-partitioned by order key, dimension tables "
                                   "replicated" if spmd else "single rank"),
                        "sf": a.sf, "queries": qs},
+            "world": world,
+            # one entry per rank: the process-group size it saw, its own timed
+            # region (``value`` uses the max), collectives issued over the run
+            "ranks": rank_info,
             "warm_s": round(step_s, 4),
             "warm_graph_s": round(step_s, 4),
             "warm_eager_s": round(eager_s, 4) if eager_s is not None else None,

@@ -719,9 +719,11 @@ PYBIND11_MODULE(_native, m) {
     kern::str_fn_lengths(args, P<int64_t>(off), P<uint8_t>(chars), n, P<int64_t>(len), S(s));
   });
   m.def("str_fn_copy", [](int fn, int64_t n1, uintptr_t a, int64_t alen, uintptr_t b, int64_t blen, uintptr_t off,
-                          uintptr_t chars, int64_t n, uintptr_t new_off, uintptr_t out, uintptr_t s) {
+                          uintptr_t chars, int64_t n, uintptr_t new_off, uintptr_t out, int64_t out_cap,
+                          uintptr_t s) {
     kern::StrFnArgs args{fn, n1, P<uint8_t>(a), alen, P<uint8_t>(b), blen};
-    kern::str_fn_copy(args, P<int64_t>(off), P<uint8_t>(chars), n, P<int64_t>(new_off), P<uint8_t>(out), S(s));
+    kern::str_fn_copy(args, P<int64_t>(off), P<uint8_t>(chars), n, P<int64_t>(new_off), P<uint8_t>(out), out_cap,
+                      S(s));
   });
   m.def("str_fn_int", [](int fn, uintptr_t pat, int64_t plen, uintptr_t off, uintptr_t chars, int64_t n, uintptr_t out,
                          uintptr_t s) {

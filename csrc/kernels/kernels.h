@@ -524,8 +524,10 @@ struct StrFnArgs {
 };
 void str_fn_lengths(const StrFnArgs& a, const int64_t* off, const uint8_t* chars, int64_t n, int64_t* len,
                     hipStream_t s);
+// out_cap: bytes of ``out``; a row whose new_off range passes it is skipped
+// (new_off may come from a replayed readback that does not match the data)
 void str_fn_copy(const StrFnArgs& a, const int64_t* off, const uint8_t* chars, int64_t n, const int64_t* new_off,
-                 uint8_t* out, hipStream_t s);
+                 uint8_t* out, int64_t out_cap, hipStream_t s);
 void str_fn_int(int fn, const uint8_t* pat, int64_t plen, const int64_t* off, const uint8_t* chars, int64_t n,
                 int32_t* out, hipStream_t s);
 

@@ -279,7 +279,10 @@ __device__ const uint8_t* dbp_decode(const uint8_t* p, const uint8_t* end, int c
     const uint8_t* q = p;
     uint64_t bs = 0, mpb = 0, total = 0, first = 0;
     d.err = !(uleb(q, end, &bs) && uleb(q, end, &mpb) && uleb(q, end, &total) && uleb(q, end, &first));
-    if (!d.err && (mpb == 0 || bs == 0 || bs % 128 != 0 || (bs / mpb) % 32 != 0 || (int64_t)total != count))
+    // mpb <= bs keeps values-per-miniblock >= 1 (0 % 32 == 0 would pass);
+    // the caps keep both in int32 (a negative mpb would move q backwards)
+    if (!d.err && (mpb == 0 || bs == 0 || mpb > bs || bs > (1u << 20) || mpb > kDbpCap || bs % 128 != 0 ||
+                   bs / mpb == 0 || (bs / mpb) % 32 != 0 || (int64_t)total != count))
       d.err = 1;
     d.mpb = (int32_t)mpb;
     d.vpm = mpb ? (int32_t)(bs / mpb) : 0;

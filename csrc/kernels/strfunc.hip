@@ -278,10 +278,15 @@ __global__ __launch_bounds__(kBlock) void strfn_len_kernel(StrFnArgs a, const in
 __global__ __launch_bounds__(kBlock) void strfn_copy_kernel(StrFnArgs a, const int64_t* __restrict__ off,
                                                             const uint8_t* __restrict__ chars, int64_t n,
                                                             const int64_t* __restrict__ new_off,
-                                                            uint8_t* __restrict__ out) {
+                                                            uint8_t* __restrict__ out, int64_t out_cap) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = off[i];
-    apply(a, chars + b, off[i + 1] - b, out + new_off[i]);
+    const int64_t o = new_off[i], e = new_off[i + 1];
+    // the row's output range must lie in the buffer and match what the
+    // length pass computes for it (a replayed total can disagree)
+    if (o < 0 || e < o || e > out_cap) continue;
+    if (apply(a, chars + b, off[i + 1] - b, nullptr) != e - o) continue;
+    apply(a, chars + b, off[i + 1] - b, out + o);
   }
 }
 
@@ -334,10 +339,10 @@ void str_fn_lengths(const StrFnArgs& a, const int64_t* off, const uint8_t* chars
 }
 
 void str_fn_copy(const StrFnArgs& a, const int64_t* off, const uint8_t* chars, int64_t n, const int64_t* new_off,
-                 uint8_t* out, hipStream_t s) {
+                 uint8_t* out, int64_t out_cap, hipStream_t s) {
   if (n == 0) return;
   hipLaunchKernelGGL(strfn_copy_kernel, dim3(grid_for(n, kBlock, 1 << 16)), dim3(kBlock), 0, s, a, off, chars, n,
-                     new_off, out);
+                     new_off, out, out_cap);
   check_launch("strfn.copy", s);
 }
 

@@ -327,7 +327,9 @@ class JoinTable:
         m = pkeys.numel()
         dev = pkeys.device
         if not self.gpu or self.empty or m == 0 or not PROBE_SELECT:
-            first = self.probe_first(pkeys, pvalid)
+            first = self.probe_first(pkeys, pvalid)      # resolves a deferred ``unique``
+            if not self.unique and want_build and not negate:
+                return None     # duplicate build keys: the caller takes the multi-match probe (as the GPU path)
             sel = mask_to_indices(first < 0 if negate else first >= 0)
             return sel, (first.index_select(0, sel.long()) if want_build and not negate else None)
         N = launch("probe_hits")

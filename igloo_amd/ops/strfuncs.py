@@ -149,7 +149,7 @@ def apply(col: Column, name: str, opts: tuple) -> Column:
     chars = torch.empty(max(total, 1), dtype=torch.uint8, device=col.device)[:total]
     if total:
         N.str_fn_copy(code, n1, ptr(ta), la, ptr(tb), lb, ptr(col.offsets), ptr(col.data), n, ptr(off),
-                      ptr(chars), s)
+                      ptr(chars), int(chars.numel()), s)
     return Column(T.UTF8, chars, col.valid, offsets=off)
 
 

@@ -204,6 +204,24 @@ def _cut(c: Column, a: int, b: int) -> Column:
     return out
 
 
+def _range_cut_rows(kt: torch.Tensor, n: int, kmin: int, kmax: int, chunk: int, rank: int) -> Tuple[int, int]:
+    """Rows [a, b) of sorted keys ``kt`` owned by ``rank``: keys in
+    [kmin + rank*chunk, kmin + (rank+1)*chunk). The cut values stay unclamped
+    Python ints (kmin + world*chunk can pass the key type's range, e.g. int32
+    keys near INT32_MAX); a cut past kmax means "end of the rows" and is never
+    searched, so every row lands on exactly one rank."""
+    from ..ops._lib import device_ints, to_host_ints
+    lo, hi = kmin + rank * chunk, kmin + (rank + 1) * chunk
+    search = [v for v in (lo, hi) if v <= kmax]
+    found = []
+    if search:
+        cuts = device_ints(search, kt.device, kt.dtype) if kt.is_cuda else torch.tensor(search, dtype=kt.dtype)
+        found = to_host_ints(torch.searchsorted(kt, cuts).to(torch.int64))
+    a = n if lo > kmax else found[0]
+    b = n if hi > kmax else found[-1]
+    return a, b
+
+
 def slice_columns(cols: Dict[str, Column], n: int, key: str, world: int, rank: int
                   ) -> Tuple[Dict[str, Column], int, Optional[tuple]]:
     """This rank's key-range slice of a replicated table's resident columns:
@@ -229,19 +247,7 @@ def slice_columns(cols: Dict[str, Column], n: int, key: str, world: int, rank: i
                     and kt.dtype in (torch.int32, torch.int64) and n and H.is_sorted(kt):
                 kmin, kmax = to_host_ints(kt[[0, -1]].to(torch.int64))
                 chunk = range_chunk(kmin, kmax, world)
-                # cut points in int64, clamped to kmax + 1: kmin + world * chunk
-                # can pass the key type's range (an int32 key near INT32_MAX)
-                cut_vals = [min(kmin + r * chunk, kmax + 1) for r in (rank, rank + 1)]
-                if kt.dtype == torch.int32:
-                    cut_vals = [min(v, 2**31 - 1) for v in cut_vals]
-                    hi_full = cut_vals[1] == 2**31 - 1 and kmax == 2**31 - 1
-                else:
-                    hi_full = False
-                cuts = device_ints(cut_vals, kt.device, kt.dtype) if kt.is_cuda \
-                    else torch.tensor(cut_vals, dtype=kt.dtype)
-                a, b = to_host_ints(torch.searchsorted(kt, cuts).to(torch.int64))
-                if hi_full or (rank == world - 1):
-                    b = n                 # the last slice ends at the last row
+                a, b = _range_cut_rows(kt, n, kmin, kmax, chunk, rank)
                 tag = range_tag(world, kmin, chunk)
             else:
                 a, b = n * rank // world, n * (rank + 1) // world

@@ -150,14 +150,20 @@ def _opt_str(f: Dict[int, list], fno: int) -> Optional[str]:
 # ------------------------------------------------------- prepared statements
 def _placeholders(sql: str):
     """Offsets of the ``?`` placeholders: outside string literals, quoted
-    identifiers, ``--`` line comments and ``/* */`` block comments."""
+    identifiers, ``--`` line comments and ``/* */`` block comments -- with
+    the SQL tokenizer's quoting rules (csrc/sql/parser.cpp tokenize): a
+    '...' literal escapes a quote by doubling it; "..." and `...`
+    identifiers end at their first closing quote."""
     i, n = 0, len(sql)
     while i < n:
         ch = sql[i]
-        if ch in ("'", '"'):
+        if ch == "'":
             j = sql.find(ch, i + 1)
             while j != -1 and j + 1 < n and sql[j + 1] == ch:      # doubled quote inside the literal
                 j = sql.find(ch, j + 2)
+            i = n if j == -1 else j + 1
+        elif ch in ('"', "`"):
+            j = sql.find(ch, i + 1)
             i = n if j == -1 else j + 1
         elif ch == "-" and sql.startswith("--", i):
             j = sql.find("\n", i)

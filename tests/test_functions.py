@@ -166,6 +166,10 @@ def test_bind_params_negative_and_comments():
     r = e.query(FS.bind_params(q, [-5])).to_pylist()
     assert r == [{"a": 15, "b": "?"}]
     assert "NaN" in FS.bind_params("select ?", [float("nan")])
+    # the tokenizer's quoting: backticks quote identifiers, "..." ends at its first quote
+    assert FS.count_params("select `it's` = ? from t") == 1
+    assert FS.count_params('select "a""b" = ?') == 1
+    assert FS.count_params("select 'it''s ?' , ?") == 1
 
 
 def test_statements():

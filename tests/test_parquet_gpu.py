@@ -212,3 +212,39 @@ def test_snappy_far_matches_beyond_lds_ring(tmp_path, gpu_device):
     path = str(tmp_path / "far.parquet")
     pq.write_table(t, path, compression="snappy", use_dictionary=False, data_page_size=1 << 20)
     _check(path, t, gpu_device)
+
+
+def _uleb(v):
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def test_corrupt_delta_header_is_rejected(tmp_path, gpu_device):
+    """A DELTA_BINARY_PACKED header with more miniblocks than values per block
+    (values per miniblock 0, which passed the old ``% 32`` check and spun or
+    read past the page) must fail the scan cleanly. The header is rewritten in
+    place: the first value's varint is shortened by one byte to make room for
+    a two-byte miniblock count, so the page keeps its length."""
+    from igloo_amd.utils.errors import ExecutionError
+    n = 5000
+    first = 2**40
+    t = pa.table({"a": pa.array([first] + list(range(n - 1)), pa.int64())})
+    path = str(tmp_path / "c.parquet")
+    pq.write_table(t, path, compression="none", use_dictionary=False, column_encoding={"a": "DELTA_BINARY_PACKED"},
+                   data_page_version="1.0")
+    raw = bytearray(open(path, "rb").read())
+    zz = first << 1
+    hdr = _uleb(256) + b"\x04" + _uleb(n) + _uleb(zz)          # pyarrow: 256-value blocks, 4 miniblocks
+    assert raw.count(hdr) == 1
+    bad = _uleb(256) + _uleb(257) + _uleb(n) + _uleb(zz >> 7)   # 257 miniblocks in a 256-value block
+    assert len(bad) == len(hdr)
+    raw[raw.index(hdr):raw.index(hdr) + len(hdr)] = bad
+    open(path, "wb").write(bytes(raw))
+    r = GpuParquetReader([path])
+    with pytest.raises(ExecutionError):
+        r.read([("a", T.INT64)], [(0, 0)], gpu_device)

@@ -60,3 +60,24 @@ def test_undersized_replay_reexecutes(gpu_device, graphs):
         assert digest(got) == want, q
         assert _fails(e) > before, q       # the mismatch was seen and the query re-executed
         assert digest(e.query(sql)) == want, q
+
+
+STR_SQL = ("SELECT c_custkey, replace(c_name, 'Customer', 'Cust#X') AS r, lpad(c_phone, 24, '*') AS p "
+           "FROM customer WHERE c_acctbal > 100 ORDER BY c_custkey")
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_undersized_replay_string_functions(gpu_device, graphs):
+    """replace / lpad output bytes are sized by a readback of the byte total:
+    a halved recording must not let strfn_copy write past the buffer."""
+    e = ig.QueryEngine(device=gpu_device)
+    datagen.register(e, 0.05)
+    e.graphs_disabled = not graphs
+    want = digest(e.query(STR_SQL))
+    e.query(STR_SQL)
+    assert _tamper(e) > 0
+    before = _fails(e)
+    got = e.query(STR_SQL)
+    assert digest(got) == want
+    assert _fails(e) > before
+    assert digest(e.query(STR_SQL)) == want

@@ -50,3 +50,19 @@ def test_tpch_distributed_gpu_ranks(tpch_cpu):
     _, _, con = tpch_cpu
     bad = D.run_distributed(2, con, device="cuda:0", low_thresholds=True)
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.parametrize("world,replicate_dims", [(4, True), (4, False), (8, True), (8, False)])
+def test_tpch_distributed_gpu_ranks_driver_worlds(world, replicate_dims, tpch_cpu):
+    """All 22 queries at the driver's scaling world sizes (4 and 8 ranks), every
+    rank's operators on the one GPU (collectives staged through gloo), both
+    layouts: replicated dimensions with co-partitioned facts (the bench layout)
+    and every table hash-partitioned (every shuffle / broadcast branch). Low
+    thresholds make SF0.01 take the SF100 code paths (sorted joins, range
+    slices, shuffled partial groups, pipelined chunked exchanges)."""
+    import test_distributed_cpu as D
+    _, _, con = tpch_cpu
+    bad = D.run_distributed(world, con, device="cuda:0", low_thresholds=True, replicate_dims=replicate_dims)
+    assert not bad, "\n".join(bad)
+    calls = {int(q): r["collectives"] for q, r in D.run_distributed.last.items()}
+    assert sum(calls.values()) > 0, calls
