@@ -634,6 +634,17 @@ PYBIND11_MODULE(_native, m) {
                        P<uint8_t>(out), S(s));
   });
 
+  m.def("json_parse", [](uintptr_t buf, int64_t start, uintptr_t rows_end, int64_t nrows, uintptr_t cols, int ncols,
+                         uintptr_t names, uintptr_t name_off, uintptr_t err, uintptr_t s) {
+    if (ncols > 64) throw std::runtime_error("json_parse: at most 64 fields");
+    kern::json_parse(P<const uint8_t>(buf), start, P<const int64_t>(rows_end), nrows, P<const kern::CsvColumn>(cols),
+                     ncols, P<const uint8_t>(names), P<const int32_t>(name_off), P<int>(err), S(s));
+  });
+  m.def("json_str_copy", [](uintptr_t pos, uintptr_t len_flag, uintptr_t off, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::json_str_copy(P<const int64_t>(pos), P<const int64_t>(len_flag), P<const int64_t>(off), n, P<uint8_t>(out),
+                        S(s));
+  });
+
   // ----------------------------------------------------------- sorted joins
   m.def("sorted_ranges", [](uintptr_t big, bool key64, int64_t nb, uintptr_t q, uintptr_t qvalid, int64_t nq,
                             uintptr_t lo, uintptr_t cnt, uintptr_t fence, int64_t nf, uintptr_t s) {

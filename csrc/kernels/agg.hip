@@ -61,6 +61,15 @@ __device__ inline void upd(const AggDesc& a, int64_t i, unsigned long long* lo, 
     case AGG_MAX_F64:
       atomicMax((long long*)lo, (long long)f64_to_ordered(((const double*)a.src)[i]));
       break;
+    case AGG_BIT_AND:
+      atomicAnd(lo, (unsigned long long)load_int(a, i));
+      break;
+    case AGG_BIT_OR:
+      atomicOr(lo, (unsigned long long)load_int(a, i));
+      break;
+    case AGG_BIT_XOR:
+      atomicXor(lo, (unsigned long long)load_int(a, i));
+      break;
   }
 }
 
@@ -73,6 +82,9 @@ __device__ inline void init_state(int op, unsigned long long* lo, long long* hi)
     case AGG_MAX_INT:
     case AGG_MAX_F64:
       *(long long*)lo = INT64_MIN;
+      break;
+    case AGG_BIT_AND:
+      *lo = ~0ULL;
       break;
     default:
       *lo = 0;
@@ -106,6 +118,15 @@ __device__ inline void merge_global(const AggDesc& a, int64_t g, unsigned long l
     case AGG_MAX_INT:
     case AGG_MAX_F64:
       if ((long long)lo != INT64_MIN) atomicMax((long long*)dlo, (long long)lo);
+      break;
+    case AGG_BIT_AND:
+      if (lo != ~0ULL) atomicAnd(dlo, lo);
+      break;
+    case AGG_BIT_OR:
+      if (lo) atomicOr(dlo, lo);
+      break;
+    case AGG_BIT_XOR:
+      if (lo) atomicXor(dlo, lo);
       break;
   }
 }
@@ -177,6 +198,15 @@ __device__ inline void seg_combine(int op, unsigned long long* lo, long long* hi
     case AGG_MIN_F64:
       if ((long long)olo < (long long)*lo) *lo = olo;
       break;
+    case AGG_BIT_AND:
+      *lo &= olo;
+      break;
+    case AGG_BIT_OR:
+      *lo |= olo;
+      break;
+    case AGG_BIT_XOR:
+      *lo ^= olo;
+      break;
     default:
       if ((long long)olo > (long long)*lo) *lo = olo;
       break;
@@ -201,6 +231,9 @@ __device__ inline void row_state(const AggDesc& a, int64_t i, bool live, unsigne
       break;
     case AGG_MIN_INT:
     case AGG_MAX_INT:
+    case AGG_BIT_AND:
+    case AGG_BIT_OR:
+    case AGG_BIT_XOR:
       *lo = (unsigned long long)load_int(a, i);
       break;
     default:
@@ -415,6 +448,15 @@ __device__ inline void wave_merge(const AggDesc& a, unsigned long long lo, long 
       case AGG_MAX_F64:
         lo = (long long)olo > (long long)lo ? olo : lo;
         break;
+      case AGG_BIT_AND:
+        lo &= olo;
+        break;
+      case AGG_BIT_OR:
+        lo |= olo;
+        break;
+      case AGG_BIT_XOR:
+        lo ^= olo;
+        break;
     }
   }
   if (lane_id() == 0) merge_global(a, 0, lo, hi);
@@ -470,6 +512,15 @@ __global__ __launch_bounds__(kBlock) void agg_single_kernel(int64_t n, AggParams
           if (v > (long long)lo[k]) lo[k] = (unsigned long long)v;
           break;
         }
+        case AGG_BIT_AND:
+          lo[k] &= (unsigned long long)load_int(a, i);
+          break;
+        case AGG_BIT_OR:
+          lo[k] |= (unsigned long long)load_int(a, i);
+          break;
+        case AGG_BIT_XOR:
+          lo[k] ^= (unsigned long long)load_int(a, i);
+          break;
       }
     }
   }

@@ -214,6 +214,9 @@ enum AggOp : int {
   AGG_MAX_INT = 4,
   AGG_MIN_F64 = 5,  // state is the order-preserving int64 image of the double
   AGG_MAX_F64 = 6,
+  AGG_BIT_AND = 7,  // integer bitwise folds (bit_and / bit_or / bit_xor)
+  AGG_BIT_OR = 8,
+  AGG_BIT_XOR = 9,
 };
 
 struct AggDesc {
@@ -381,6 +384,13 @@ void csv_parse(const uint8_t* buf, int64_t start, const int64_t* rows_end, int64
 void csv_str_lengths(const int64_t* len_flag, int64_t n, int64_t* len, hipStream_t stream);
 void csv_str_copy(const int64_t* pos, const int64_t* len_flag, const int64_t* off, int64_t n, uint8_t quote,
                   uint8_t* out, hipStream_t stream);
+
+// ---- json.hip (NDJSON records; rows split by csv_rows with no quote) ------------
+// names / name_off: the schema's field names, packed (ncols <= 64); cols as csv_parse
+void json_parse(const uint8_t* buf, int64_t start, const int64_t* rows_end, int64_t nrows, const CsvColumn* cols,
+                int ncols, const uint8_t* names, const int32_t* name_off, int* err, hipStream_t stream);
+void json_str_copy(const int64_t* pos, const int64_t* len_flag, const int64_t* off, int64_t n, uint8_t* out,
+                   hipStream_t stream);
 
 // ---- ranges.hip ----------------------------------------------------------------
 // big: non-decreasing int32/int64 keys; per probe key q[i]: big[lo[i] .. lo[i]+cnt[i]) == q[i]

@@ -117,7 +117,19 @@ std::vector<Token> tokenize(const std::string& t) {
       i = j + 1;
       continue;
     }
-    static const char* ops2[] = {"<>", "!=", "<=", ">=", "||", "::", "=="};
+    if (c == '$' && i + 1 < n && std::isdigit((unsigned char)t[i + 1])) {  // $n statement parameter
+      size_t j = i + 1;
+      while (j < n && std::isdigit((unsigned char)t[j])) ++j;
+      out.push_back({Token::Op, t.substr(i, j - i), start});
+      i = j;
+      continue;
+    }
+    if (t.compare(i, 3, "!~*") == 0) {
+      out.push_back({Token::Op, "!~*", start});
+      i += 3;
+      continue;
+    }
+    static const char* ops2[] = {"<>", "!=", "<=", ">=", "||", "::", "==", "~*", "!~"};
     bool matched = false;
     for (auto op : ops2) {
       if (t.compare(i, 2, op) == 0) {
@@ -128,7 +140,7 @@ std::vector<Token> tokenize(const std::string& t) {
       }
     }
     if (matched) continue;
-    if (std::string("+-*/%=<>(),.;").find(c) != std::string::npos) {
+    if (std::string("+-*/%=<>(),.;~[]").find(c) != std::string::npos) {
       out.push_back({Token::Op, std::string(1, c), start});
       ++i;
       continue;
@@ -272,6 +284,64 @@ class Parser {
       n = make("truncate", ident());
     } else if (acceptKw("CREATE")) {
       n = createStmt();
+    } else if (acceptWord("copy")) {
+      // COPY (query) | table TO 'path' [STORED AS fmt] [OPTIONS (k v, ...)]
+      n = make("copy");
+      if (acceptOp("(")) {
+        n->attrs["query"] = query();
+        expectOp(")");
+      } else {
+        std::string t = ident();
+        while (acceptOp(".")) t += "." + ident();
+        n->str = t;
+      }
+      expectWord("to");
+      if (peek().kind != Token::String) fail("expected target path string");
+      n->flags["path"] = next().text;
+      for (;;) {
+        if (acceptWord("stored")) {
+          expectKw("AS");
+          n->flags["stored_as"] = upper(ident());
+        } else if (acceptWord("options") || (isOp("(") && !n->flags.count("opts"))) {
+          n->flags["opts"] = "1";
+          expectOp("(");
+          do {
+            std::string k = peek().kind == Token::String ? next().text : ident();
+            while (acceptOp(".")) k += "." + ident();
+            std::string v = next().text;
+            n->flags["opt." + lower(k)] = v;
+          } while (acceptOp(","));
+          expectOp(")");
+        } else {
+          break;
+        }
+      }
+    } else if (acceptWord("prepare")) {
+      // PREPARE name [(type, ...)] AS statement
+      n = make("prepare", ident());
+      if (acceptOp("(")) {
+        std::vector<NodeP> ts;
+        do ts.push_back(make("name", typeName()));
+        while (acceptOp(","));
+        expectOp(")");
+        n->attrs["types"] = list(ts);
+      }
+      expectKw("AS");
+      n->kids.push_back(statement());
+    } else if (acceptWord("execute")) {
+      n = make("execute", ident());
+      std::vector<NodeP> args;
+      if (acceptOp("(")) {
+        if (!acceptOp(")")) {
+          do args.push_back(expr());
+          while (acceptOp(","));
+          expectOp(")");
+        }
+      }
+      n->attrs["args"] = list(args);
+    } else if (acceptWord("deallocate")) {
+      acceptWord("prepare");
+      n = make("deallocate", ident());
     } else if (acceptKw("DROP")) {
       if (acceptWord("view")) n = make("drop_view");
       else { expectWord("table"); n = make("drop_table"); }
@@ -493,8 +563,20 @@ class Parser {
     expectKw("SELECT");
     auto s = make("select");
     s->pos = pos;
-    if (acceptKw("DISTINCT")) s->flags["distinct"] = "1";
-    else acceptKw("ALL");
+    if (acceptKw("DISTINCT")) {
+      if (acceptKw("ON")) {  // DISTINCT ON (expr, ...): first row per key
+        expectOp("(");
+        std::vector<NodeP> on;
+        do on.push_back(expr());
+        while (acceptOp(","));
+        expectOp(")");
+        s->attrs["distinct_on"] = list(on);
+      } else {
+        s->flags["distinct"] = "1";
+      }
+    } else {
+      acceptKw("ALL");
+    }
     std::vector<NodeP> items;
     do items.push_back(selectItem());
     while (acceptOp(","));
@@ -650,6 +732,15 @@ class Parser {
     std::string name = ident();
     while (acceptOp(".")) name += "." + ident();
     n->str = name;
+    if (isOp("(")) {  // table function: generate_series(a, b [, step]), range(...), unnest(list)
+      ++p_;
+      n->kind = "table_func";
+      if (!acceptOp(")")) {
+        do n->kids.push_back(expr());
+        while (acceptOp(","));
+        expectOp(")");
+      }
+    }
     tableAlias(n);
     return n;
   }
@@ -760,6 +851,13 @@ class Parser {
           expectOp(")");
           l = n;
         }
+      } else if (isWord("similar") && isWord("to", 1)) {
+        p_ += 2;
+        auto n = make("similar");
+        if (neg) n->flags["neg"] = "1";
+        n->kids = {l, additive()};
+        if (acceptKw("ESCAPE")) n->attrs["escape"] = primary();
+        l = n;
       } else if (isKw("LIKE") || isKw("ILIKE")) {
         auto n = make("like");
         if (next().text == "ILIKE") n->flags["ilike"] = "1";
@@ -798,7 +896,7 @@ class Parser {
   NodeP comparison() {
     NodeP l = concat();
     for (;;) {
-      const char* ops[] = {"=", "<>", "!=", "<", "<=", ">", ">="};
+      const char* ops[] = {"=", "<>", "!=", "<", "<=", ">", ">=", "~", "~*", "!~", "!~*"};
       std::string op;
       for (auto o : ops)
         if (isOp(o)) { op = o; break; }
@@ -851,13 +949,33 @@ class Parser {
   }
   NodeP postfix() {
     NodeP x = primary();
-    while (acceptOp("::")) {
-      auto c = make("cast");
-      c->kids.push_back(x);
-      c->flags["type"] = typeName();
-      x = c;
+    for (;;) {
+      if (acceptOp("::")) {
+        auto c = make("cast");
+        c->kids.push_back(x);
+        c->flags["type"] = typeName();
+        x = c;
+      } else if (acceptOp("[")) {  // list element (1-based) or struct field by name
+        auto f = make("func", "array_element");
+        f->pos = x->pos;
+        f->kids = {x, expr()};
+        expectOp("]");
+        x = f;
+      } else {
+        return x;
+      }
     }
-    return x;
+  }
+
+  NodeP arrayLiteral() {  // [a, b, ...] -> make_array(a, b, ...)
+    expectOp("[");
+    auto f = make("func", "make_array");
+    if (!acceptOp("]")) {
+      do f->kids.push_back(expr());
+      while (acceptOp(","));
+      expectOp("]");
+    }
+    return f;
   }
 
   NodeP lit(const std::string& type, const std::string& s) {
@@ -887,6 +1005,11 @@ class Parser {
         ++p_;
         return lit("str", t.text);
       case Token::Op:
+        if (t.text == "[") return arrayLiteral();
+        if (t.text.size() > 1 && t.text[0] == '$') {  // $n parameter of a prepared statement
+          ++p_;
+          return make("param", t.text.substr(1));
+        }
         if (t.text == "(") {
           ++p_;
           if (isKw("SELECT") || isKw("WITH")) {
@@ -998,6 +1121,7 @@ class Parser {
       case Token::Ident:
       case Token::QuotedIdent: {
         std::string name = next().text;
+        if (name == "array" && t.kind == Token::Ident && isOp("[")) return arrayLiteral();
         if (isOp("(") && t.kind == Token::Ident) {
           if (name == "trim") return trimCall();
           if (name == "position") {  // POSITION(needle IN haystack) -> strpos(haystack, needle)
@@ -1044,7 +1168,25 @@ class Parser {
       else acceptKw("ALL");
       do f->kids.push_back(expr());
       while (acceptOp(","));
+      if (acceptKw("ORDER")) {  // ordered aggregate: array_agg(x ORDER BY y)
+        expectKw("BY");
+        std::vector<NodeP> os;
+        do os.push_back(orderItem());
+        while (acceptOp(","));
+        f->attrs["order"] = list(os);
+      }
       expectOp(")");
+    }
+    if (acceptWord("within")) {  // ordered-set aggregate: percentile_cont(q) WITHIN GROUP (ORDER BY x)
+      expectKw("GROUP");
+      expectOp("(");
+      expectKw("ORDER");
+      expectKw("BY");
+      std::vector<NodeP> os;
+      do os.push_back(orderItem());
+      while (acceptOp(","));
+      expectOp(")");
+      f->attrs["within_group"] = list(os);
     }
     if (acceptWord("filter")) {
       expectOp("(");

@@ -164,6 +164,7 @@ class QueryEngine:
         self.session: Dict[str, Any] = dict(config or {})
         # optimized logical plans by (SQL text, catalog version, session settings)
         self._plans: "collections.OrderedDict" = collections.OrderedDict()
+        self._prepared: Dict[str, tuple] = {}    # PREPARE name -> (statement AST, parameter types)
         self._graph_pool = None
         self.graphs_disabled = False    # set after a capture the runtime refused (exec/graphs.py)
         self._spec: Dict[Any, dict] = {}   # replayable host readbacks per (plan, catalog, cache generation)
@@ -232,6 +233,10 @@ class QueryEngine:
         from .connectors.csv import CsvTable
         return self.register_table(name, CsvTable(path, schema=schema, has_header=has_header, delimiter=delimiter,
                                                   **kw), cache=cache)
+
+    def register_json(self, name: str, path: str, schema=None, cache: Optional[bool] = None):
+        from .connectors.json import JsonTable
+        return self.register_table(name, JsonTable(path, schema=schema), cache=cache)
 
     def register_iceberg(self, name: str, path: str, cache: Optional[bool] = None, **kw):
         from .connectors.iceberg import IcebergTable
@@ -374,6 +379,18 @@ class QueryEngine:
             return QueryResult(pa.table({"count": pa.array([src.num_rows()], pa.int64())}), 0.0)
         if k == "create_external_table":
             return self._create_external(st)
+        if k == "prepare":
+            types = [T.parse_type_name(t["s"]) for t in (st.get("types") or {}).get("c", [])]
+            self._prepared[st["s"]] = (st["c"][0], types)
+            return QueryResult(pa.table({}), 0.0)
+        if k == "execute":
+            return self._execute_prepared(st)
+        if k == "deallocate":
+            if self._prepared.pop(st["s"], None) is None:
+                raise PlanError(f"prepared statement '{st['s']}' does not exist")
+            return QueryResult(pa.table({}), 0.0)
+        if k == "copy":
+            return self._copy(st)
         if k == "create_table":
             if st.get("query"):
                 b = Binder(self.catalog, self._ids, self.session)
@@ -384,6 +401,63 @@ class QueryEngine:
                 return QueryResult(pa.table({"count": [batch.num_rows]}), 0.0)
             raise NotSupported("CREATE TABLE without AS SELECT")
         raise NotSupported(f"statement {k}")
+
+    def _execute_prepared(self, st) -> QueryResult:
+        """EXECUTE name(args): the prepared statement bound with ``$n`` =
+        the n-th argument (constant expressions, cast to PREPARE's types)."""
+        from .sql import binder as _bd
+        name = st["s"]
+        if name not in self._prepared:
+            raise PlanError(f"prepared statement '{name}' does not exist")
+        stmt, types = self._prepared[name]
+        b = Binder(self.catalog, self._ids, self.session)
+        vals = []
+        for i, a in enumerate((st.get("args") or {}).get("c", [])):
+            v = _bd._fold(b.bind_expr(a, _bd.Scope([])))
+            if not isinstance(v, _bd.Lit):
+                raise PlanError(f"EXECUTE {name}: argument {i + 1} is not a constant")
+            if i < len(types) and v.dtype != types[i]:
+                v = b._coerce_lit(v, types[i]) if v.value is not None else _bd.Lit(None, types[i])
+            vals.append(v)
+        if types and len(vals) != len(types):
+            raise PlanError(f"EXECUTE {name}: expected {len(types)} arguments, got {len(vals)}")
+        tok = _bd.PARAMS.set(vals)
+        try:
+            return self._run_statement(stmt)
+        finally:
+            _bd.PARAMS.reset(tok)
+
+    def _copy(self, st) -> QueryResult:
+        """COPY (query) | table TO 'path' [STORED AS PARQUET|CSV|JSON|ARROW]
+        [OPTIONS (...)]: runs the query on the device and writes the result
+        (format from STORED AS, else the path's extension; a path ending in
+        '/' is a directory that gets one file). Returns the row count, like
+        DataFusion's COPY (reference Cargo.lock:1329 datafusion-sql)."""
+        import os as _os
+        if st.get("query"):
+            tab = self._run_statement(st["query"]).table
+        else:
+            src = self.catalog.get_table(st["s"])
+            if src is None and self.catalog.get_view(st["s"]) is None:
+                raise TableNotFound(f"table '{st['s']}' not found")
+            tab = self.sql(f'SELECT * FROM "{st["s"]}"').table
+        path = st["path"]
+        fmt = (st.get("stored_as") or st.get("opt.format") or "").upper()
+        if not fmt:
+            ext = _os.path.splitext(path.rstrip("/"))[1].lower().lstrip(".")
+            fmt = {"parquet": "PARQUET", "csv": "CSV", "json": "JSON", "ndjson": "JSON", "arrow": "ARROW"}.get(ext, "")
+        if not fmt:
+            raise PlanError(f"COPY: cannot infer the format of '{path}' (use STORED AS)")
+        if path.endswith("/"):
+            _os.makedirs(path, exist_ok=True)
+            path = _os.path.join(path, "part-0." + fmt.lower())
+        else:
+            d = _os.path.dirname(path)
+            if d:
+                _os.makedirs(d, exist_ok=True)
+        from .connectors import writers
+        writers.write_table(tab, path, fmt, {k[4:]: v for k, v in st.items() if k.startswith("opt.")})
+        return QueryResult(pa.table({"count": pa.array([tab.num_rows], pa.uint64())}), 0.0)
 
     def _describe(self, name: str, full: bool = False) -> QueryResult:
         """DESCRIBE t / SHOW COLUMNS FROM t (DataFusion's column layout)."""
@@ -478,6 +552,8 @@ class QueryEngine:
                               delimiter=st.get("delimiter", ","))
         elif fmt == "ICEBERG":
             self.register_iceberg(name, loc)
+        elif fmt in ("JSON", "NDJSON"):
+            self.register_json(name, loc, schema=schema)
         else:
             raise NotSupported(f"STORED AS {fmt}")
         return QueryResult(pa.table({}), 0.0)

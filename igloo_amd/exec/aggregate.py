@@ -853,12 +853,12 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
         i = add("count", None, valid)
         finals.append(lambda r, i=i: (ci, Column(T.INT64, r[i])))
         return
-    if func in ("median", "percentile"):
+    if func in ("median", "percentile", "percentile_disc"):
         out = _order_stat(a, col, valid, gid, ng, n, ctx)
         finals.append(lambda r, out=out: (ci, out))
         return
     if func == "string_agg":
-        out = _string_agg(a, col, valid, gid, ng, n, ctx)
+        out = _string_agg(a, col, valid, gid, ng, n, ctx, b)
         finals.append(lambda r, out=out: (ci, out))
         return
     if func in ("covar_samp", "covar_pop", "corr"):
@@ -943,6 +943,13 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
         finals.append(lambda r, i=i: (ci, Column(t, r[i].to(t.torch_dtype) if t.kind != "bool" else r[i] != 0,
                                                  null_if_empty(r, r[i]))))
         return
+    if func in ("bit_and", "bit_or", "bit_xor"):
+        vals = col.data
+        if vals.dtype not in (torch.int32, torch.int64):
+            vals = vals.to(torch.int64)
+        i = add({"bit_and": "and_int", "bit_or": "or_int", "bit_xor": "xor_int"}[func], vals.contiguous(), valid)
+        finals.append(lambda r, i=i: (ci, Column(t, r[i].to(t.torch_dtype), null_if_empty(r, r[i]))))
+        return
     if func in ("bool_and", "bool_or"):
         vals = col.data.to(torch.int64)
         i = add("min_int" if func == "bool_and" else "max_int", vals.contiguous(), valid)
@@ -968,14 +975,34 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
     raise NotSupported(f"aggregate {func}")
 
 
-def _group_sorted(x: torch.Tensor, valid, gid, ng: int, n: int, ctx, by_value: bool):
+def _order_perm(order, b: Batch, n: int, ctx) -> torch.Tensor:
+    """Row permutation of ``b`` by an ordered aggregate's ORDER BY keys."""
+    from ..ops import sort as SO
+    ks = []
+    for e, asc, nf in order:
+        c = ctx.evaluator.column(e, b)
+        if c.dtype.is_string:
+            v = S.sort_ranks(c)
+        elif c.is_wide:
+            v = _convert_tensor(c, T.FLOAT64)
+        else:
+            v = c.data
+        ks.append((v, not asc, nf, c.valid))
+    return SO.argsort(ks, n, ctx.device).to(torch.int64)
+
+
+def _group_sorted(x: torch.Tensor, valid, gid, ng: int, n: int, ctx, by_value: bool, perm0=None):
     """Valid rows ordered by (group[, value]) -> (row ids, per-group counts,
-    per-group first position)."""
+    per-group first position). ``perm0``: rows are taken in this order
+    (an ordered aggregate's ORDER BY) before the stable group sort."""
     from ..ops import sort as SO
     from ..ops.select import mask_to_indices
     dev = ctx.device
-    rows = mask_to_indices(valid).to(torch.int64) if valid is not None else \
-        torch.arange(n, dtype=torch.int64, device=dev)
+    if perm0 is not None:
+        rows = perm0 if valid is None else perm0[gather_tensor(valid, perm0)]
+    else:
+        rows = mask_to_indices(valid).to(torch.int64) if valid is not None else \
+            torch.arange(n, dtype=torch.int64, device=dev)
     m = rows.numel()
     g = gather_tensor(gid, rows).to(torch.int64) if gid is not None else torch.zeros(m, dtype=torch.int64, device=dev)
     keys = [] if gid is None else [(g, False, False, None)]
@@ -994,6 +1021,8 @@ def _order_stat(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Co
     the input type) and approx_percentile_cont (linear interpolation) per group."""
     t = a.dtype
     fl = col.dtype.is_float or col.is_wide or a.func == "percentile"
+    if a.func == "percentile_disc":
+        fl = col.dtype.is_float or col.is_wide
     x = _convert_tensor(col, T.FLOAT64) if (fl or col.is_wide) else col.data.to(torch.int64)
     rows, counts, starts = _group_sorted(x, valid, gid, ng, n, ctx, True)
     xs = gather_tensor(x, rows) if rows.numel() else x[:0]
@@ -1002,6 +1031,11 @@ def _order_stat(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Co
     if not rows.numel():
         return Column(t, torch.zeros(ng, dtype=t.torch_dtype if t.kind != "decimal" else torch.int64,
                                      device=ctx.device), ok)
+    if a.func == "percentile_disc":
+        # the first value whose cumulative distribution reaches the fraction
+        k = torch.ceil(counts.to(torch.float64) * float(a.param)).to(torch.int64) - 1
+        v = gather_tensor(xs, (starts + k.clamp(min=0)).clamp(0, last))
+        return Column(t, v if t.is_decimal else v.to(t.torch_dtype), ok)
     if a.func == "percentile":
         pos = (counts - 1).clamp(min=0).to(torch.float64) * float(a.param)
         lo = pos.floor().to(torch.int64)
@@ -1020,7 +1054,7 @@ def _order_stat(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Co
     return Column(t, med.to(t.torch_dtype) if not t.is_decimal else med, ok)
 
 
-def _string_agg(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Column:
+def _string_agg(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx, b=None) -> Column:
     """string_agg(s, sep): each group's strings in input order joined by sep.
     Rows are ordered by group (stable), a separator is prefixed to every row
     that does not start its group, and each group's string is then one
@@ -1028,7 +1062,8 @@ def _string_agg(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx) -> Co
     the pieces' offsets at the group starts (no per-group copy)."""
     from ..ops.gather import take
     dev = ctx.device
-    rows, counts, starts = _group_sorted(None, valid, gid, ng, n, ctx, False)
+    perm0 = _order_perm(a.order, b, n, ctx) if a.order and b is not None and n > 1 else None
+    rows, counts, starts = _group_sorted(None, valid, gid, ng, n, ctx, False, perm0)
     m = rows.numel()
     if m == 0:
         z = torch.zeros(ng + 1, dtype=torch.int64, device=dev)

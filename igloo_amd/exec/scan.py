@@ -284,6 +284,37 @@ class ValuesExec(ExecNode):
         return Batch(cols, n, ("replicated",) if ctx.spmd else None)
 
 
+class TableFunctionExec(ExecNode):
+    """generate_series / range rows made on the device (one arange), unnest
+    of a constant list: the list's child values."""
+
+    def __init__(self, logical: L.TableFunction):
+        self.logical = logical
+        self.children = []
+
+    def _run(self, ctx):
+        t = self.logical
+        ci = t.schema[0]
+        dist = ("replicated",) if ctx.spmd else None
+        if t.name in ("generate_series", "range"):
+            start, stop, step = t.args
+            if step == 0:
+                raise ExecutionError(f"{t.name}: step cannot be zero")
+            if t.name == "generate_series":
+                stop = stop + (1 if step > 0 else -1)
+            n = max(0, -(-(stop - start) // step)) if step > 0 else max(0, -(-(start - stop) // -step))
+            vals = torch.arange(n, dtype=torch.int64, device=ctx.device) * step + start if n else \
+                torch.zeros(0, dtype=torch.int64, device=ctx.device)
+            return Batch({ci.cid: Column(ci.dtype, vals)}, n, dist)
+        if t.name == "unnest":
+            from ..ops import nested as NS
+            v = ctx.evaluator.eval(t.args[0], Batch({}, 1))
+            lst = v if isinstance(v, Column) else NS.scalar_to_column(v, 1, ctx.device)
+            child = NS.unnest_values(lst, ctx.device)
+            return Batch({ci.cid: child}, len(child), dist)
+        raise NotSupported(f"table function {t.name}")
+
+
 def _column_from_values(vals, dtype, device) -> Column:
     if dtype.is_decimal:
         t = torch.tensor([0 if v is None else int(v) for v in vals], dtype=torch.int64)

@@ -13,7 +13,9 @@ import torch
 
 from ._lib import is_gpu, launch, native, ptr, stream, to_host_ints
 
-OPS = {"sum_int": 0, "sum_f64": 1, "count": 2, "min_int": 3, "max_int": 4, "min_f64": 5, "max_f64": 6}
+OPS = {"sum_int": 0, "sum_f64": 1, "count": 2, "min_int": 3, "max_int": 4, "min_f64": 5, "max_f64": 6,
+       "and_int": 7, "or_int": 8, "xor_int": 9}
+_INT_OPS = ("sum_int", "min_int", "max_int", "and_int", "or_int", "xor_int")
 I64_MAX = 2**63 - 1
 I64_MIN = -(2**63)
 
@@ -94,12 +96,14 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
                 dst2 = torch.zeros(g, dtype=torch.int64, device=device)
         elif op.startswith("min"):
             dst = torch.full((g,), I64_MAX, dtype=torch.int64, device=device)
+        elif op in ("and_int", "or_int", "xor_int"):
+            dst = torch.full((g,), -1 if op == "and_int" else 0, dtype=torch.int64, device=device)
         else:
             dst = torch.full((g,), I64_MIN, dtype=torch.int64, device=device)
         src64 = 1
         if vals is not None:
             assert vals.numel() == n and vals.is_contiguous()
-            if op in ("sum_int", "min_int", "max_int"):
+            if op in _INT_OPS:
                 assert vals.dtype in (torch.int32, torch.int64), vals.dtype
                 src64 = 1 if vals.dtype == torch.int64 else 0
             else:
@@ -173,6 +177,17 @@ def _cpu(gid, ngroups, specs, n) -> List[torch.Tensor]:
             init = float("inf") if op == "min_f64" else float("-inf")
             base = torch.full((g,), init, dtype=torch.float64)
             outs.append(base.scatter_reduce(0, idx, v.to(torch.float64), reduce="amin" if op == "min_f64" else "amax"))
+        elif op in ("and_int", "or_int", "xor_int"):
+            import numpy as np
+            ufn = {"and_int": np.bitwise_and, "or_int": np.bitwise_or, "xor_int": np.bitwise_xor}[op]
+            res = np.full(g, -1 if op == "and_int" else 0, dtype=np.int64)
+            if idx.numel():
+                order = torch.argsort(idx, stable=True)
+                gi_s = idx[order].numpy()
+                vs = v.to(torch.int64)[order].numpy()
+                starts = np.flatnonzero(np.r_[True, gi_s[1:] != gi_s[:-1]])
+                res[gi_s[starts]] = ufn.reduceat(vs, starts)
+            outs.append(torch.from_numpy(res))
         else:
             raise ValueError(op)
     return outs
@@ -260,7 +275,7 @@ def sorted_having(keys: torch.Tensor, specs: Sequence[Spec], hidx: int, hop: str
         src64 = 1
         if vals is not None:
             assert vals.numel() == n and vals.is_contiguous()
-            if op in ("sum_int", "min_int", "max_int"):
+            if op in _INT_OPS:
                 # int16 / int8 (codes 2 / 3): a NULL-free SUM for the streaming kernel only
                 src64 = {torch.int64: 1, torch.int32: 0, torch.int16: 2, torch.int8: 3}[vals.dtype]
                 assert src64 < 2 or (op == "sum_int" and valid is None), "narrow values: NULL-free SUM only"

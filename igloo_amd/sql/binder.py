@@ -21,9 +21,14 @@ from .expr import (AGG_FUNCS, FRAME_KINDS, RANKING_FUNCS, VALUE_FUNCS, AggCall, 
                    Func, InList, IsNull, Like, Lit, Neg, Not, SubqueryExpr, WindowCall, WindowFrame, and_all, col_refs,
                    transform, walk)
 from .logical import (Aggregate, ColInfo, Filter, Join, Limit, Plan, Project, RecursiveCTE, Scan, Sort, Union, Values,
-                      Window, WorkTableScan)
+                      TableFunction, Window, WorkTableScan)
 
 EPOCH = datetime.date(1970, 1, 1)
+
+import contextvars as _cv
+
+#: values of ``$n`` parameters while an EXECUTE binds its prepared statement
+PARAMS: "_cv.ContextVar[Optional[List[Lit]]]" = _cv.ContextVar("igloo_params", default=None)
 INTERVAL = DataType("interval")
 
 
@@ -317,6 +322,8 @@ class Binder:
             group_exprs = uniq
         having = self.bind_expr(s["having"], scope, allow_agg=True) if s.get("having") else None
         qualify = self.bind_expr(s["qualify"], scope, allow_agg=True) if s.get("qualify") else None
+        # DISTINCT ON (exprs): the first row of each key group in ORDER BY order
+        distinct_on = [self._bind_group_key(g, scope, items) for g in _lst(s.get("distinct_on"))]
         # ORDER BY expressions bound against input scope + aliases (resolved later)
         aliases = {a: e for e, a in items}
         order_bound = []
@@ -342,7 +349,7 @@ class Binder:
             else:
                 order_bound.append(("expr", bound, asc, nf))
         # ---- aggregation
-        extra = ([having] if having is not None else []) + ([qualify] if qualify is not None else [])
+        extra = ([having] if having is not None else []) + ([qualify] if qualify is not None else []) + distinct_on
         has_aggs = any(_contains_agg(e) for e, _ in items) or any(_contains_agg(x) for x in extra) or \
             any(k == "expr" and _contains_agg(x) for k, x, _, _ in order_bound) or \
             any(_contains_grouping(e) for e, _ in items)
@@ -354,6 +361,7 @@ class Binder:
                 having = rewrite(having)
             if qualify is not None:
                 qualify = rewrite(qualify)
+            distinct_on = [rewrite(x) for x in distinct_on]
             order_bound = [(k, rewrite(x) if k == "expr" else x, a, nf) for k, x, a, nf in order_bound]
         if having is not None:
             self._require_bool(having, "HAVING")
@@ -379,10 +387,16 @@ class Binder:
             items = [(wrw(e), a) for e, a in items]
             if qualify is not None:
                 qualify = wrw(qualify)
+            distinct_on = [wrw(x) for x in distinct_on]
             order_bound = [(k, wrw(x) if k == "expr" else x, a, nf) for k, x, a, nf in order_bound]
         if qualify is not None:
             self._require_bool(qualify, "QUALIFY")
             plan = Filter(plan, qualify)
+        if distinct_on:
+            okeys = [(items[x][0] if k == "item" else x, a, nf) for k, x, a, nf in order_bound]
+            rn = WindowCall("row_number", [], list(distinct_on), okeys, self._frame(None, okeys), INT64)
+            rci = ColInfo(self.ids(), "__distinct_on", INT64, False)
+            plan = Filter(Window(plan, [(rci, rn)]), BinOp("=", rci.ref(), Lit(1, INT64), BOOL))
         # ---- projection (+ hidden ORDER BY columns)
         proj = [(ColInfo(self.ids(), a, e.dtype, e.nullable), e) for e, a in items]
         hidden = []
@@ -559,6 +573,8 @@ class Binder:
             bq = self.bind_query(item["query"], outer, ctes)
             cols = [c["s"] for c in _lst(item.get("columns"))] or bq.names
             return self._derived(bq, item.get("alias"), cols, item)
+        if k == "table_func":
+            return self._table_func(item, outer)
         if k == "join":
             lp, lr = self._bind_from(item["c"][0], outer, ctes)
             rp, rr = self._bind_from(item["c"][1], outer, ctes)
@@ -590,6 +606,39 @@ class Binder:
                 return Join(lp, rp, "cross"), lr + rr
             return Join(lp, rp, kind, [], residual), (lr + rr if kind not in ("semi", "anti") else lr)
         raise NotSupported(f"FROM item {k}")
+
+    def _table_func(self, item: dict, outer) -> Tuple[Plan, List[Relation]]:
+        """generate_series / range / unnest in FROM (constant arguments)."""
+        name = item["s"].lower()
+        alias = item.get("alias") or name
+        names = [c["s"] for c in _lst(item.get("columns"))]
+        args = [self.bind_expr(a, Scope([], outer)) for a in item["c"]]
+        if name in ("generate_series", "range"):
+            if not 1 <= len(args) <= 3:
+                raise PlanError(f"{name}() takes 1 to 3 arguments")
+            vals = []
+            for a in args:
+                a = _fold(a)
+                if not isinstance(a, Lit) or a.value is None or not a.dtype.is_integer:
+                    raise NotSupported(f"{name}(): arguments must be integer constants")
+                vals.append(int(a.value))
+            if len(vals) == 1:
+                vals = [0, vals[0]]
+            if len(vals) == 2:
+                vals.append(1)
+            ci = ColInfo(self.ids(), names[0] if names else "value", INT64, False, alias)
+            return TableFunction(name, vals, [ci]), [Relation(alias, [ci])]
+        if name == "unnest":
+            _nargs(name, args, 1)
+            lt = args[0].dtype
+            if lt.kind != "list":
+                raise PlanError(f"unnest() needs a list argument, got {lt}")
+            if col_refs(args[0]):
+                raise NotSupported("unnest() in FROM of a column: use SELECT unnest(col) FROM t")
+            cname = names[0] if names else f"UNNEST({args[0].sql()})"
+            ci = ColInfo(self.ids(), cname, lt.child, True, alias)
+            return TableFunction("unnest", [args[0]], [ci]), [Relation(alias, [ci])]
+        raise NotSupported(f"table function {name}()")
 
     def _bind_recursive_cte(self, cnode: dict, outer, cenv: dict) -> BoundQuery:
         """WITH RECURSIVE name AS (anchor UNION [ALL] recursive-term)."""
@@ -662,6 +711,12 @@ class Binder:
                 return self._cmp(op, l, r)
             if op == "||":
                 return Func("concat", [self._coerce(l, UTF8), self._coerce(r, UTF8)], UTF8)
+            if op in ("~", "~*", "!~", "!~*"):
+                # POSIX regex match operators: regexp_like, '*' = case-insensitive
+                if not isinstance(r, Lit) or not isinstance(r.value, str):
+                    raise NotSupported(f"{op}: the pattern must be a string literal")
+                e = self._func_library("regexp_like", [l, r, Lit("i" if op.endswith("*") else "", UTF8)])
+                return Not(e) if op.startswith("!") else e
             return self._arith(op, l, r)
         if k == "un":
             x = self.bind_expr(node["c"][0], scope, allow_agg)
@@ -700,6 +755,20 @@ class Binder:
             if node.get("escape"):
                 esc = self.bind_expr(node["escape"], scope).value
             return Like(self._coerce(x, UTF8), p.value, bool(node.get("neg")), bool(node.get("ilike")), esc)
+        if k == "similar":
+            x = self.bind_expr(node["c"][0], scope, allow_agg)
+            p = self.bind_expr(node["c"][1], scope, allow_agg)
+            if not isinstance(p, Lit) or not isinstance(p.value, str):
+                raise NotSupported("SIMILAR TO pattern must be a string literal")
+            esc = self.bind_expr(node["escape"], scope).value if node.get("escape") else "\\"
+            e = self._func_library("regexp_like", [x, Lit(similar_to_regex(p.value, esc), UTF8), Lit("", UTF8)])
+            return Not(e) if node.get("neg") else e
+        if k == "param":
+            params = PARAMS.get() or []
+            i = int(node["s"]) - 1
+            if not 0 <= i < len(params):
+                raise PlanError(f"no value for parameter ${i + 1} ({len(params)} given)")
+            return params[i]
         if k == "isnull":
             x = self.bind_expr(node["c"][0], scope, allow_agg)
             return IsNull(x, bool(node.get("neg")))
@@ -935,6 +1004,29 @@ class Binder:
                 raise PlanError(f"aggregate function {name} not allowed here")
             distinct = bool(node.get("distinct"))
             arg2, param = None, None
+            order = tuple(self._agg_order(node.get("order"), scope))
+            if node.get("within_group") is not None:
+                # ordered-set aggregate: percentile_cont(q) WITHIN GROUP (ORDER BY x [DESC])
+                if name not in ("percentile_cont", "percentile_disc", "approx_percentile_cont", "median"):
+                    raise PlanError(f"WITHIN GROUP is not valid for {name}()")
+                wg = self._agg_order(node["within_group"], scope)
+                if len(wg) != 1:
+                    raise PlanError(f"{name}() WITHIN GROUP takes exactly one ORDER BY expression")
+                x, asc, _ = wg[0]
+                qs = [self.bind_expr(a, scope) for a in node["c"]]
+                if name == "median":
+                    q = 0.5
+                else:
+                    if len(qs) != 1 or not isinstance(qs[0], Lit) or qs[0].value is None:
+                        raise PlanError(f"{name}() takes a constant fraction")
+                    q = float(qs[0].value) / (10 ** qs[0].dtype.scale if qs[0].dtype.is_decimal else 1)
+                if not 0.0 <= q <= 1.0:
+                    raise PlanError("percentile must be between 0 and 1")
+                if not asc:
+                    q = 1.0 - q
+                flt = self.bind_expr(node["filter"], scope) if node.get("filter") else None
+                return _make_agg("percentile_disc" if name == "percentile_disc" else "percentile_cont", x, False,
+                                 flt, None, q)
             if node.get("star"):
                 arg = None
             else:
@@ -946,6 +1038,13 @@ class Binder:
                     if len(args) != 2:
                         raise PlanError(f"{name}() takes two arguments")
                     arg2 = args[1]
+                elif name in ("percentile_cont", "percentile_disc"):
+                    # percentile_cont(x, q): the DataFusion function-call spelling
+                    if len(args) != 2 or not isinstance(args[1], Lit) or args[1].value is None:
+                        raise PlanError(f"{name}() takes a constant fraction")
+                    param = float(args[1].value) / (10 ** args[1].dtype.scale if args[1].dtype.is_decimal else 1)
+                    if not 0.0 <= param <= 1.0:
+                        raise PlanError("percentile must be between 0 and 1")
                 elif name in ("string_agg", "approx_percentile_cont"):
                     if len(args) != 2 or not isinstance(args[1], Lit) or args[1].value is None:
                         raise PlanError(f"{name}() takes a constant second argument")
@@ -959,7 +1058,9 @@ class Binder:
                 elif len(args) != 1:
                     raise NotSupported(f"{name} with {len(args)} arguments")
             flt = self.bind_expr(node["filter"], scope) if node.get("filter") else None
-            return _make_agg(name, arg, distinct, flt, arg2, param)
+            if order and name not in ("array_agg", "string_agg", "first_value", "last_value"):
+                order = ()      # ORDER BY does not change an order-insensitive aggregate
+            return _make_agg(name, arg, distinct, flt, arg2, param, order)
         args = [self.bind_expr(a, scope, allow_agg) for a in node["c"]]
         if name in ("upper", "lower", "capitalize"):
             _nargs(name, args, 1)
@@ -1025,7 +1126,18 @@ class Binder:
             return Func("power", [self._coerce(a, FLOAT64) for a in args], FLOAT64)
         if name in ("to_date",):
             return self._coerce(args[0], DATE32)
+        if name == "arrow_typeof":
+            _nargs(name, args, 1)
+            return Lit(arrow_type_name(args[0].dtype), UTF8)
         return self._func_library(name, args)
+
+    def _agg_order(self, node, scope) -> List[Tuple[Expr, bool, bool]]:
+        out = []
+        for o in _lst(node):
+            asc = not o.get("desc")
+            nf = o.get("nulls", "last" if asc else "first") == "first"
+            out.append((self.bind_expr(o["c"][0], scope), asc, nf))
+        return out
 
     def _date_part(self, field: str, x: Expr) -> Expr:
         field = {"years": "year", "months": "month", "days": "day", "dayofweek": "dow", "dayofyear": "doy",
@@ -1374,11 +1486,57 @@ _WINDOW_AGGS = ("sum", "count", "avg", "min", "max", "stddev", "stddev_samp", "s
                 "var_pop", "bool_and", "bool_or")
 _EXTRA_AGGS = ("stddev_samp", "stddev_pop", "var_samp", "var_pop", "variance", "var_population", "stddev_population",
                "median", "approx_distinct", "approx_median", "string_agg", "array_agg", "bit_and", "bit_or",
-               "bit_xor", "covar", "covar_samp", "covar_pop", "corr", "approx_percentile_cont", "first_value",
+               "bit_xor", "percentile_cont", "percentile_disc", "covar", "covar_samp", "covar_pop", "corr", "approx_percentile_cont", "first_value",
                "last_value", "every", "any", "some")
 
 
 _TRUNC_UNITS = ("microsecond", "millisecond", "second", "minute", "hour", "day", "week", "month", "quarter", "year")
+
+
+def similar_to_regex(pat: str, esc: str = "\\") -> str:
+    """SQL ``SIMILAR TO`` pattern -> an anchored regular expression: ``%`` and
+    ``_`` are the LIKE wildcards, ``| * + ? {m,n} ( ) [...]`` keep their regex
+    meaning, everything else (``.`` included) is literal."""
+    import re as _re
+    out, i, n = [], 0, len(pat)
+    while i < n:
+        ch = pat[i]
+        if esc and ch == esc and i + 1 < n:
+            out.append(_re.escape(pat[i + 1]))
+            i += 2
+            continue
+        if ch == "%":
+            out.append(".*")
+        elif ch == "_":
+            out.append(".")
+        elif ch in "|*+?(){},":
+            out.append(ch)
+        elif ch == "[":
+            j = pat.find("]", i + 2 if i + 1 < n and pat[i + 1] in "^]" else i + 1)
+            if j < 0:
+                raise PlanError("SIMILAR TO: unterminated bracket expression")
+            out.append(pat[i:j + 1])
+            i = j + 1
+            continue
+        else:
+            out.append(_re.escape(ch))
+        i += 1
+    return "^(?:" + "".join(out) + ")$"
+
+
+def arrow_type_name(t: DataType) -> str:
+    """DataFusion's ``arrow_typeof`` spelling of a type (Arrow DataType Display)."""
+    k = t.kind
+    if k == "decimal":
+        return f"Decimal128({t.precision}, {t.scale})"
+    if k == "timestamp":
+        return "Timestamp(Microsecond, None)"
+    if k == "list":
+        return f"List(Field {{ name: \"item\", data_type: {arrow_type_name(t.child)}, nullable: true, dict_id: 0, " \
+               f"dict_is_ordered: false, metadata: {{}} }})"
+    if k == "struct":
+        return "Struct(" + ", ".join(f"{n} {arrow_type_name(ft)}" for n, ft in t.fields) + ")"
+    return str(t)
 
 
 def _like_escape(s: str) -> str:
@@ -1526,7 +1684,7 @@ _AGG_ALIASES = {"mean": "avg", "variance": "var_samp", "var": "var_samp", "var_p
 
 
 def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt, arg2: Optional[Expr] = None,
-              param=None) -> AggCall:
+              param=None, order: Tuple = ()) -> AggCall:
     name = _AGG_ALIASES.get(name, name)
     if name == "count":
         return AggCall("count", arg, distinct, INT64, flt)
@@ -1569,14 +1727,22 @@ def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt, arg2: Optiona
         if not t.is_numeric:
             raise PlanError(f"median({t}) is not supported")
         return AggCall("median", arg, distinct, t, flt)
-    if name == "approx_percentile_cont":
+    if name in ("approx_percentile_cont", "percentile_cont"):
         if not t.is_numeric:
-            raise PlanError(f"approx_percentile_cont({t}) is not supported")
+            raise PlanError(f"{name}({t}) is not supported")
         return AggCall("percentile", arg, False, FLOAT64, flt, None, param)
+    if name == "percentile_disc":
+        if not (t.is_numeric or t.is_temporal):
+            raise PlanError(f"percentile_disc({t}) is not supported")
+        return AggCall("percentile_disc", arg, False, t, flt, None, param)
+    if name in ("bit_and", "bit_or", "bit_xor"):
+        if not t.is_integer:
+            raise PlanError(f"{name}({t}) needs an integer argument")
+        return AggCall(name, arg, distinct, t, flt)
     if name == "string_agg":
         if not t.is_string:
             raise PlanError("string_agg() needs a string argument")
-        return AggCall("string_agg", arg, distinct, UTF8, flt, None, param)
+        return AggCall("string_agg", arg, distinct, UTF8, flt, None, param, order)
     if name in ("covar_samp", "covar_pop", "corr"):
         if not (t.is_numeric and arg2 is not None and arg2.dtype.is_numeric):
             raise PlanError(f"{name}() needs two numeric arguments")

@@ -265,20 +265,28 @@ class AggCall(Expr):
     filter: Optional[Expr] = None
     arg2: Optional[Expr] = None   # second argument (covar / corr)
     param: Any = None             # constant parameter (percentile fraction, string_agg separator)
+    #: ordered aggregates (array_agg / string_agg ... ORDER BY): (expr, ascending, nulls_first)
+    order: Tuple = ()
 
     def children(self):
         out = [] if self.arg is None else [self.arg]
         if self.arg2 is not None:
             out.append(self.arg2)
+        out += [e for e, _, _ in self.order]
         if self.filter is not None:
             out.append(self.filter)
         return out
 
     def with_children(self, kids):
-        arg = kids[0] if self.arg is not None else None
-        arg2 = kids[1] if self.arg2 is not None else None
+        k = 0
+        arg = arg2 = None
+        if self.arg is not None:
+            arg, k = kids[0], 1
+        if self.arg2 is not None:
+            arg2, k = kids[k], k + 1
+        order = tuple((kids[k + i], a, nf) for i, (_, a, nf) in enumerate(self.order))
         flt = kids[-1] if self.filter is not None else None
-        return AggCall(self.func, arg, self.distinct, self.dtype, flt, arg2, self.param)
+        return AggCall(self.func, arg, self.distinct, self.dtype, flt, arg2, self.param, order)
 
     def sql(self):
         a = "*" if self.arg is None else (("DISTINCT " if self.distinct else "") + self.arg.sql())
@@ -286,6 +294,9 @@ class AggCall(Expr):
             a += ", " + self.arg2.sql()
         if self.param is not None:
             a += f", {self.param!r}"
+        if self.order:
+            a += " ORDER BY " + ", ".join(f"{e.sql()} {'ASC' if asc else 'DESC'} NULLS {'FIRST' if nf else 'LAST'}"
+                                          for e, asc, nf in self.order)
         return f"{self.func.upper()}({a})"
 
 

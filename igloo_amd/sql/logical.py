@@ -82,6 +82,20 @@ class Values(Plan):
 
 
 @dataclass(eq=False)
+class TableFunction(Plan):
+    """A table-valued function in FROM: ``generate_series(a, b [, step])``
+    (inclusive), ``range(a, b [, step])`` (exclusive) with constant integer
+    arguments, or ``unnest(list)`` of a constant list expression (DataFusion's
+    datafusion-functions-table, reference Cargo.lock:1146)."""
+    name: str
+    args: List[Any]
+    schema: List[ColInfo]
+
+    def label(self):
+        return f"TableFunction: {self.name}({', '.join(a.sql() if hasattr(a, 'sql') else repr(a) for a in self.args)})"
+
+
+@dataclass(eq=False)
 class Filter(Plan):
     input: Plan
     pred: Expr
