@@ -634,6 +634,41 @@ PYBIND11_MODULE(_native, m) {
                        P<uint8_t>(out), S(s));
   });
 
+  m.def("strfmt_lengths", [](const std::string& fmt, bool is_date, uintptr_t v, int64_t n, uintptr_t len,
+                             uintptr_t s) {
+    kern::strfmt_lengths(reinterpret_cast<const uint8_t*>(fmt.data()), (int)fmt.size(), is_date, P<const void>(v), n,
+                         P<int64_t>(len), S(s));
+  });
+  m.def("strfmt_write", [](const std::string& fmt, bool is_date, uintptr_t v, int64_t n, uintptr_t off,
+                           int64_t out_cap, uintptr_t out, uintptr_t s) {
+    kern::strfmt_write(reinterpret_cast<const uint8_t*>(fmt.data()), (int)fmt.size(), is_date, P<const void>(v), n,
+                       P<const int64_t>(off), out_cap, P<uint8_t>(out), S(s));
+  });
+  m.def("regex_dfa_match", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t table, uintptr_t cls,
+                              uintptr_t flags, int nstates, int nclasses, int start, bool anchored_end, bool negate,
+                              uintptr_t out, uintptr_t s) {
+    kern::regex_dfa_match(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint16_t>(table),
+                          P<const uint8_t>(cls), P<const uint8_t>(flags), nstates, nclasses, start, anchored_end,
+                          negate, P<uint8_t>(out), S(s));
+  });
+  m.def("digest_width", &kern::digest_width);
+  m.def("digest_hex", [](int algo, uintptr_t off, uintptr_t chars, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::digest_hex(algo, P<const int64_t>(off), P<const uint8_t>(chars), n, P<uint8_t>(out), S(s));
+  });
+  m.def("uuid_v4", [](uint64_t seed, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::uuid_v4(seed, n, P<uint8_t>(out), S(s));
+  });
+  m.def("list_element_idx", [](uintptr_t se, uintptr_t valid, uintptr_t pos, uintptr_t pos_valid, int64_t pos_const,
+                               int64_t n, int64_t child_n, uintptr_t out, uintptr_t s) {
+    kern::list_element_idx(P<const int64_t>(se), P<const uint8_t>(valid), P<const int64_t>(pos),
+                           P<const uint8_t>(pos_valid), pos_const, n, child_n, P<int64_t>(out), S(s));
+  });
+  m.def("interleave_idx", [](int64_t n, int k, uintptr_t out, uintptr_t s) {
+    kern::interleave_idx(n, k, P<int64_t>(out), S(s));
+  });
+  m.def("list_slots", [](int64_t n, int64_t k, uintptr_t se, uintptr_t s) {
+    kern::list_slots(n, k, P<int64_t>(se), S(s));
+  });
   m.def("json_parse", [](uintptr_t buf, int64_t start, uintptr_t rows_end, int64_t nrows, uintptr_t cols, int ncols,
                          uintptr_t names, uintptr_t name_off, uintptr_t err, uintptr_t s) {
     if (ncols > 64) throw std::runtime_error("json_parse: at most 64 fields");

@@ -385,6 +385,32 @@ void csv_str_lengths(const int64_t* len_flag, int64_t n, int64_t* len, hipStream
 void csv_str_copy(const int64_t* pos, const int64_t* len_flag, const int64_t* off, int64_t n, uint8_t quote,
                   uint8_t* out, hipStream_t stream);
 
+// ---- digest.hip (md5 / sha2 hex digests of strings, uuid v4) --------------------
+enum DigestAlgo : int { kDigestMd5 = 0, kDigestSha224 = 1, kDigestSha256 = 2, kDigestSha384 = 3, kDigestSha512 = 4 };
+int digest_width(int algo);   // hex characters per digest
+// out: n * digest_width(algo) bytes (row r at r * width)
+void digest_hex(int algo, const int64_t* off, const uint8_t* chars, int64_t n, uint8_t* out, hipStream_t s);
+void uuid_v4(uint64_t seed, int64_t n, uint8_t* out, hipStream_t s);   // out: n * 36 bytes
+
+// ---- strfmt.hip (to_char / date_format with chrono-style patterns) --------------
+// v: int32 days (is_date) or int64 microseconds; lengths pass, then writes at off (bounded by out_cap)
+void strfmt_lengths(const uint8_t* fmt, int flen, bool is_date, const void* v, int64_t n, int64_t* len,
+                    hipStream_t s);
+void strfmt_write(const uint8_t* fmt, int flen, bool is_date, const void* v, int64_t n, const int64_t* off,
+                  int64_t out_cap, uint8_t* out, hipStream_t s);
+
+// ---- regex.hip (byte-class DFA match per string; table built by ops/regex_dfa.py) ---
+size_t regex_lds_bytes(int nstates, int nclasses);
+void regex_dfa_match(const int64_t* off, const uint8_t* chars, int64_t n, const uint16_t* table, const uint8_t* cls,
+                     const uint8_t* flags, int nstates, int nclasses, int start, bool anchored_end, bool negate,
+                     uint8_t* out, hipStream_t s);
+
+// ---- nested.hip (LIST rows: [n, 2] int64 (start, length) into a child column) ---
+void list_element_idx(const int64_t* se, const uint8_t* valid, const int64_t* pos, const uint8_t* pos_valid,
+                      int64_t pos_const, int64_t n, int64_t child_n, int64_t* out, hipStream_t s);
+void interleave_idx(int64_t n, int k, int64_t* out, hipStream_t s);
+void list_slots(int64_t n, int64_t k, int64_t* se, hipStream_t s);
+
 // ---- json.hip (NDJSON records; rows split by csv_rows with no quote) ------------
 // names / name_off: the schema's field names, packed (ncols <= 64); cols as csv_parse
 void json_parse(const uint8_t* buf, int64_t start, const int64_t* rows_end, int64_t nrows, const CsvColumn* cols,

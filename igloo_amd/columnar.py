@@ -57,7 +57,13 @@ class Column:
 
     @property
     def is_dict(self) -> bool:
-        return self.dictionary is not None
+        return self.dictionary is not None and not self.dtype.is_nested
+
+    @property
+    def nested(self) -> "Nested":
+        """LIST / STRUCT columns: the child column(s) the rows point into."""
+        assert self.dtype.is_nested and isinstance(self.dictionary, Nested), self
+        return self.dictionary
 
     @property
     def is_plain_string(self) -> bool:
@@ -119,6 +125,8 @@ class Column:
     @staticmethod
     def full(value: Any, dtype: DataType, n: int, device) -> "Column":
         device = torch.device(device)
+        if dtype.is_nested:
+            return Column.from_arrow(pa.array([value] * n, dtype.to_arrow()), device=device, dtype=dtype)
         if value is None:
             if dtype.is_string:
                 return Column(dtype, torch.zeros(0, dtype=torch.uint8, device=device),
@@ -144,6 +152,22 @@ class Column:
         valid = None
         if arr.null_count > 0:
             valid = torch.from_numpy(np.array(arr.is_valid().to_numpy(zero_copy_only=False), dtype=np.bool_)).to(device)
+        if dtype.kind == "list":
+            if pa.types.is_fixed_size_list(t):
+                arr = arr.cast(pa.list_(t.value_type))
+            flat = arr.flatten()         # the child values of the non-null rows, in row order
+            off = np.asarray(arr.value_lengths().fill_null(0).to_numpy(zero_copy_only=False), dtype=np.int64)
+            lens = off.copy()
+            starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n else np.zeros(0, np.int64)
+            child = Column.from_arrow(flat, device=device, dtype=dtype.child, dict_encode=False)
+            data = torch.from_numpy(np.stack([starts, lens], axis=1).astype(np.int64)).to(device)
+            return Column(dtype, data, valid, dictionary=Nested(child=child))
+        if dtype.kind == "struct":
+            kids = {}
+            for i, (fname, ft) in enumerate(dtype.fields):
+                kids[fname] = Column.from_arrow(arr.field(i), device=device, dtype=ft, dict_encode=False)
+            return Column(dtype, torch.arange(n, dtype=torch.int64, device=device), valid,
+                          dictionary=Nested(children=kids))
         if pa.types.is_dictionary(t):
             codes = np.array(arr.indices.cast(pa.int32()).fill_null(0).to_numpy(zero_copy_only=False))
             dic = Column.from_arrow(arr.dictionary.cast(pa.large_string()), device=device, dict_encode=False)
@@ -195,6 +219,8 @@ class Column:
             if not v.all():
                 validity = pa.array(v, pa.bool_()).buffers()[1]
         dt = self.dtype
+        if dt.is_nested:
+            return _nested_to_arrow(self, n, validity)
         if dt.is_string:
             if self.dictionary is not None and self.data.is_cuda and len(self.dictionary) > 2 * n + 1024:
                 # small slice of a big dictionary (e.g. top-k rows of a grouped
@@ -241,6 +267,58 @@ class Column:
     def __repr__(self) -> str:
         rep = "dict" if self.is_dict else ("plain" if self.is_plain_string else "fixed")
         return f"Column({self.dtype}, n={len(self)}, {rep}, device={self.device})"
+
+
+class Nested:
+    """Child column(s) of a LIST (``child``) or STRUCT (``children``) column,
+    carried in ``Column.dictionary`` so every operator that moves rows keeps
+    them (rows are views: (start, length) pairs or row ids into the child)."""
+
+    def __init__(self, child: Optional[Column] = None, children: Optional[Dict[str, Column]] = None):
+        self.child = child
+        self.children = children
+
+    def to(self, device) -> "Nested":
+        if self.child is not None:
+            return Nested(child=self.child.to(device))
+        return Nested(children={k: c.to(device) for k, c in self.children.items()})
+
+    @property
+    def nbytes(self) -> int:
+        if self.child is not None:
+            return self.child.nbytes
+        return sum(c.nbytes for c in self.children.values())
+
+    def __len__(self) -> int:
+        if self.child is not None:
+            return len(self.child)
+        return len(next(iter(self.children.values()))) if self.children else 0
+
+
+def _nested_to_arrow(col: "Column", n: int, validity) -> pa.Array:
+    dt = col.dtype
+    mask = None if col.valid is None else ~col.valid.cpu().numpy().astype(np.bool_)
+    if dt.kind == "struct":
+        rid = col.data.cpu().numpy().astype(np.int64)
+        arrs = []
+        for fname, ft in dt.fields:
+            ch = col.nested.children[fname].to_arrow()
+            arrs.append(pc.take(ch, pa.array(rid, pa.int64())) if n else pa.array([], ft.to_arrow()))
+        return pa.StructArray.from_arrays(arrs, names=[f for f, _ in dt.fields],
+                                          mask=pa.array(mask) if mask is not None else None)
+    se = col.data.cpu().numpy().astype(np.int64).reshape(n, 2) if n else np.zeros((0, 2), np.int64)
+    starts, lens = se[:, 0], se[:, 1]
+    if mask is not None:
+        lens = np.where(mask, 0, lens)
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    idx = (np.repeat(starts - off[:-1], lens) + np.arange(off[-1], dtype=np.int64)) if off[-1] else np.zeros(0, np.int64)
+    child = col.nested.child.to_arrow()
+    vals = pc.take(child, pa.array(idx, pa.int64())) if len(idx) else pa.array([], dt.child.to_arrow())
+    vals = vals.cast(dt.child.to_arrow())
+    out = pa.ListArray.from_arrays(pa.array(off.astype(np.int32)), vals,
+                                   mask=pa.array(mask) if mask is not None else None)
+    return out
 
 
 _NP = {

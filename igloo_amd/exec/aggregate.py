@@ -826,6 +826,22 @@ def _plan_agg(ci, a: AggCall, b: Batch, gid, ng, n, ctx, specs, finals):
     dev = ctx.device
     func = a.func
     col = ev.column(a.arg, b) if a.arg is not None else None
+    if func == "array_agg":
+        # NULL elements are kept (DataFusion's array_agg); FILTER drops rows
+        fv = ev.mask(a.filter, b) if a.filter is not None else None
+        if a.distinct:
+            k, _ = group_key_tensor(col)
+            pair = H.pack_keys([gid.to(torch.int64) if gid is not None else
+                                torch.zeros(n, dtype=torch.int64, device=dev), k])
+            if col.valid is not None:
+                pair = torch.where(col.valid, pair.to(torch.int64), torch.full((n,), -1, dtype=torch.int64, device=dev))
+            if fv is not None:
+                pair = torch.where(fv, pair.to(torch.int64), torch.full((n,), -2, dtype=torch.int64, device=dev))
+            first = H.first_rows_mask(pair) if n else torch.zeros(0, dtype=torch.bool, device=dev)
+            fv = first if fv is None else (fv & first)
+        out = _array_agg(a, col, fv, gid, ng, n, ctx, b)
+        finals.append(lambda r, out=out: (ci, out))
+        return
     valid = col.valid if col is not None else None
     if a.filter is not None:
         fm = ev.mask(a.filter, b)
@@ -1079,6 +1095,17 @@ def _string_agg(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx, b=Non
     off = pieces.offsets
     out_off = torch.cat([gather_tensor(off, starts.clamp(max=m)), off[m:m + 1]])
     return Column(T.UTF8, pieces.data, counts > 0, offsets=out_off)
+
+
+def _array_agg(a: AggCall, col: Column, valid, gid, ng: int, n: int, ctx, b) -> Column:
+    """array_agg(x [ORDER BY ...]): each group's values as one list, in input
+    (or the given) order. Rows are ordered by group (stable) and gathered
+    once; group g's list is the (start, count) slice of that child."""
+    from ..ops import nested as NS
+    perm0 = _order_perm(a.order, b, n, ctx) if a.order and n > 1 else None
+    rows, counts, starts = _group_sorted(None, valid, gid, ng, n, ctx, False, perm0)
+    child = take(col, rows)
+    return NS.from_groups(child, starts, counts, a.dtype, counts > 0)
 
 
 def _avg(s: torch.Tensor, c: torch.Tensor, src, t) -> torch.Tensor:

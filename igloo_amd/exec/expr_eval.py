@@ -16,6 +16,8 @@ import os
 from typing import Any, Optional, Tuple, Union
 
 import numpy as np
+import re
+
 import pyarrow as pa
 import pyarrow.compute as pc
 import torch
@@ -35,6 +37,10 @@ from ..utils.errors import ExecutionError, NotSupported
 JIT_MIN_ROWS = int(os.environ.get("IGLOO_EXPR_JIT_MIN_ROWS", "1"))
 _JIT_ROOTS = {BinOp, Case, Cast, Func, Not, Neg, IsNull, InList}
 _JIT_ON_CPU = False   # tests: run the generator (source collection only) on CPU batches
+
+
+_NESTED = ("make_array", "struct", "array_length", "array_element", "get_field", "array_has", "array_to_string",
+           "regexp_match", "unnest")
 
 
 class Scalar:
@@ -472,6 +478,14 @@ class Evaluator:
         args = [self.eval(a, b) for a in e.args]
         if args and all(isinstance(a, Scalar) for a in args) and name not in ("coalesce",):
             return self._func_scalar(e, args)
+        if name in _NESTED:
+            return self._nested(e, args, b)
+        if name in ("hex_digest", "to_char"):
+            from ..ops import digest as DG
+            c = args[0]
+            if isinstance(c, Scalar):
+                c = Column.full(c.value, e.args[0].dtype, b.num_rows, self.device(b))
+            return DG.hex_digest(c, e.options[0]) if name == "hex_digest" else DG.to_char(c, e.options[0])
         if name == "upper":
             return S.upper(args[0])
         if name == "lower":
@@ -520,6 +534,9 @@ class Evaluator:
             return self._mk(out, T.FLOAT64, _and_valid(va, vc), b)
         if name == "random":
             return Column(T.FLOAT64, torch.rand(b.num_rows, dtype=torch.float64, device=self.device(b)))
+        if name == "uuid":
+            from ..ops import digest as DG
+            return DG.uuid_column(b.num_rows, self.device(b))
         if name in ("greatest", "least"):
             return self._extreme(e, args, b)
         if name in ("gcd", "lcm"):
@@ -594,9 +611,60 @@ class Evaluator:
             return self._mk(torch.pow(a, c) if isinstance(a, torch.Tensor) else torch.pow(torch.as_tensor(a), c), T.FLOAT64, _and_valid(va, vc), b)
         raise NotSupported(f"function {name}")
 
+    def _nested(self, e: Func, args, b: Batch) -> Value:
+        from ..ops import nested as NS
+        name = e.name
+        n = b.num_rows
+        dev = self.device(b)
+
+        def col(i):
+            a = args[i]
+            if isinstance(a, Scalar):
+                return Column.full(a.value, e.args[i].dtype if a.dtype.kind == "null" else a.dtype, n, dev)
+            return a
+        if name == "make_array":
+            return NS.make_list([col(i) for i in range(len(args))], n, e.dtype, dev)
+        if name == "struct":
+            return NS.make_struct(list(e.options), [col(i) for i in range(len(args))], n, e.dtype, dev)
+        if name == "array_length":
+            c = col(0)
+            return Column(T.INT64, NS.lengths(c).clone(), c.valid)
+        if name == "array_element":
+            c = col(0)
+            if len(args) > 1:
+                p = col(1)
+                return NS.element(c, p.data, p.valid)
+            return NS.element(c, e.options[0])
+        if name == "get_field":
+            return NS.field(col(0), e.options[0])
+        if name == "array_has":
+            return NS.has(col(0), e.options[0])
+        if name == "array_to_string":
+            c = col(0)
+            return NS.to_string(c, *e.options)
+        if name == "regexp_match":
+            import pyarrow.compute as pc
+            c = col(0)
+            pat, flags = e.options
+            rx = re.compile(pat, re.I if "i" in flags else 0)
+            vals = []
+            for v in c.to_arrow().to_pylist():
+                m = rx.search(v) if v is not None else None
+                vals.append(None if m is None else (list(m.groups()) if rx.groups else [m.group(0)]))
+            from ..ops._lib import HOST_STEPS
+            HOST_STEPS["regexp_match"] += 1
+            return Column.from_arrow(pa.array(vals, pa.list_(pa.large_string())), device=dev, dtype=e.dtype)
+        if name == "unnest":
+            raise ExecutionError("unnest() is only valid as a SELECT list item or in FROM")
+        raise NotSupported(f"function {name}")
+
     def _func_scalar(self, e: Func, args) -> Scalar:
         vals = [a.value for a in args]
         name = e.name
+        if name == "make_array":
+            return Scalar(list(vals), e.dtype)
+        if name == "struct":
+            return Scalar(dict(zip(e.options, vals)), e.dtype)
         if any(v is None for v in vals):
             return Scalar(None, e.dtype)
         if name == "upper":

@@ -893,6 +893,9 @@ def concat_columns(cols: List[Column]) -> Column:
     if any(c.valid is not None for c in cols):
         valid = torch.cat([c.valid if c.valid is not None else torch.ones(len(c), dtype=torch.bool, device=dev)
                            for c in cols])
+    if c0.dtype.is_nested:
+        from ..ops import nested as NS
+        return NS.concat(cols, valid)
     if c0.dtype.is_string:
         if all(c.is_dict and c.dictionary is c0.dictionary for c in cols):
             return Column(c0.dtype, torch.cat([c.data for c in cols]), valid, dictionary=c0.dictionary)

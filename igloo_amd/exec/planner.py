@@ -30,6 +30,9 @@ def create_physical_plan(p: L.Plan) -> ExecNode:
         return ScanExec(p)
     if isinstance(p, L.Values):
         return ValuesExec(p)
+    if isinstance(p, L.Unnest):
+        from .scan import UnnestExec
+        return UnnestExec(p, create_physical_plan(p.input))
     if isinstance(p, L.TableFunction):
         from .scan import TableFunctionExec
         return TableFunctionExec(p)

@@ -284,6 +284,28 @@ class ValuesExec(ExecNode):
         return Batch(cols, n, ("replicated",) if ctx.spmd else None)
 
 
+class UnnestExec(ExecNode):
+    """Rows of the child repeated once per element of a list column
+    (ops/nested.py unnest_rows: the range-expansion kernel over the lists'
+    (start, length) pairs, then one gather per column)."""
+
+    def __init__(self, logical: L.Unnest, child: ExecNode):
+        self.logical = logical
+        self.children = [child]
+
+    def _run(self, ctx):
+        from ..ops import nested as NS
+        b = self.children[0].execute(ctx)
+        u = self.logical
+        lst = b.columns[u.list_col.cid]
+        parent, vals = NS.unnest_rows(lst)
+        keys = [k for k in b.columns if k != u.list_col.cid]
+        cols = dict(zip(keys, take_many([b.columns[k] for k in keys], parent))) if keys else {}
+        cols[u.list_col.cid] = take(lst, parent)
+        cols[u.out.cid] = vals
+        return Batch(cols, parent.numel(), b.dist)
+
+
 class TableFunctionExec(ExecNode):
     """generate_series / range rows made on the device (one arange), unnest
     of a constant list: the list's child values."""
@@ -309,7 +331,7 @@ class TableFunctionExec(ExecNode):
         if t.name == "unnest":
             from ..ops import nested as NS
             v = ctx.evaluator.eval(t.args[0], Batch({}, 1))
-            lst = v if isinstance(v, Column) else NS.scalar_to_column(v, 1, ctx.device)
+            lst = v if isinstance(v, Column) else NS.scalar_to_column(v.value, t.args[0].dtype, 1, ctx.device)
             child = NS.unnest_values(lst, ctx.device)
             return Batch({ci.cid: child}, len(child), dist)
         raise NotSupported(f"table function {t.name}")

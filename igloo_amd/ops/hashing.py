@@ -136,6 +136,16 @@ def key_bound(keys: torch.Tensor) -> Optional[Tuple[int, int]]:
 UNIQUE_CHECK_MAX_ROWS = 1 << 27
 
 
+def _check_unique(keys: torch.Tensor, why: str) -> bool:
+    """IGLOO_CHECK_KEY_TAGS: a tag-derived uniqueness must hold on the data."""
+    if CHECK_KEY_TAGS and keys.numel() > 1 and not capturing():
+        n = keys.numel()
+        u = torch.unique(keys.to(torch.int64)).numel()
+        if u != n:
+            raise AssertionError(f"key_unique() trusted {why} on {n} keys with {n - u} duplicates")
+    return True
+
+
 def key_unique(keys: torch.Tensor) -> bool:
     """True only when the keys are known distinct with no readback in steady
     state: a single GROUP BY key (``_igloo_distinct``, kept through filters
@@ -143,7 +153,7 @@ def key_unique(keys: torch.Tensor) -> bool:
     in row order) of a resident column whose values are unique (checked once
     and remembered on it)."""
     if getattr(keys, "_igloo_distinct", False):
-        return True
+        return _check_unique(keys, "a distinct tag")
     if getattr(keys, "_igloo_resident", False):
         o = keys
     else:
@@ -172,7 +182,8 @@ def key_unique(keys: torch.Tensor) -> bool:
             o._igloo_unique = u
         except (AttributeError, RuntimeError):
             return False
-    return u
+    return u and _check_unique(keys, "the resident base column's uniqueness" if o is not keys else
+                               "a resident column's uniqueness")
 
 
 def _keys_ok(k: torch.Tensor) -> torch.Tensor:

@@ -57,7 +57,8 @@ def _member(c: Column) -> Member:
 
 def _eligible(c: Column, rows: int) -> bool:
     d = c.data
-    return (not c.is_plain_string and d.dim() == 1 and d.dtype in _FIXED and d.is_cuda and len(d) == rows
+    return (not c.is_plain_string and not c.dtype.is_nested and d.dim() == 1 and d.dtype in _FIXED and d.is_cuda
+            and len(d) == rows
             and getattr(d, "_igloo_resident", False) and (c.valid is None or c.valid.numel() == rows))
 
 

@@ -21,7 +21,7 @@ import torch
 
 from .. import types as T
 from ..columnar import Column
-from ._lib import is_gpu, launch, ptr, stream
+from ._lib import is_gpu, launch, native, ptr, stream
 from .select import offsets_from_lengths
 
 CODES = {"trim": 0, "replace": 1, "lpad": 2, "rpad": 3, "reverse": 4, "repeat": 5, "left": 6, "right": 7,
@@ -189,6 +189,10 @@ def regexp(col: Column, name: str, pattern: str, repl: Optional[str] = None, fla
         re.compile(pattern)
     except re.error as e:
         raise PlanError(f"invalid regular expression {pattern!r}: {e}") from None
+    if name == "regexp_like" and set(flags) <= {"i", "c"} and col.data.is_cuda:
+        m = _regexp_like_gpu(col, pattern, "i" in flags and not flags.endswith("c"))
+        if m is not None:
+            return m
     note_host_step(name)
     fl = _re_flags(flags)
     pat = f"(?{fl}){pattern}" if fl else pattern
@@ -217,6 +221,36 @@ def regexp(col: Column, name: str, pattern: str, repl: Optional[str] = None, fla
         return c
     t = torch.tensor(res.cast(pa.int64()).fill_null(0).to_numpy(zero_copy_only=False), device=col.device)
     return t.to(torch.bool) if name == "regexp_like" else t
+
+
+def _regexp_like_gpu(col: Column, pattern: str, icase: bool) -> Optional[torch.Tensor]:
+    """regexp_like on the device: the pattern as a byte DFA (ops/regex_dfa.py)
+    walked by csrc/kernels/regex.hip, one lane per string (dictionary columns:
+    per dictionary entry, then the codes gather the flags). None when the
+    pattern needs the host engine."""
+    from . import regex_dfa as RD
+    from .gather import gather_tensor
+    from .strings import decode
+    try:
+        d = RD.compile_dfa(pattern, icase)
+    except (RD.Unsupported, RecursionError):
+        return None
+    if native().regex_lds_bytes(d.nstates, d.nclasses) > 64 * 1024:
+        return None
+    dev = col.device
+    src = col.dictionary if col.is_dict else (col if col.is_plain_string else decode(col))
+    n = len(src)
+    table = torch.tensor([x for row in d.table for x in row], dtype=torch.int32).to(torch.int16).to(dev)
+    cls = torch.tensor(d.cls, dtype=torch.uint8).to(dev)
+    flg = torch.tensor(d.accept, dtype=torch.uint8).to(dev)
+    out = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)[:n]
+    launch("regex_dfa").regex_dfa_match(ptr(src.offsets), ptr(src.data), n, ptr(table), ptr(cls), ptr(flg),
+                                        d.nstates, d.nclasses, d.start, d.anchored_end, False, ptr(out),
+                                        stream(out))
+    m = out.view(torch.bool)
+    if col.is_dict:
+        m = gather_tensor(m, col.data) if len(col) else m[:0]
+    return m
 
 
 def _regexp_arrow(arr, name, pat, repl, flags):

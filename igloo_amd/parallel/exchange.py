@@ -197,6 +197,14 @@ def _sig(c: Column) -> tuple:
     return (c.valid is not None, c.is_dict, c.is_plain_string, c.is_wide)
 
 
+def _no_nested(cols) -> None:
+    """LIST / STRUCT rows are views into per-rank child columns: they do not
+    travel in the packed collectives (single-rank engines evaluate them)."""
+    for c in cols:
+        if c.dtype.is_nested:
+            raise NotSupported(f"{c.dtype} columns cannot be exchanged between ranks")
+
+
 def normalize_structure(b: Batch, comm, extra: Sequence[int] = ()) -> Batch:
     """Make every rank's columns structurally identical (validity present,
     dictionary vs plain strings, 64- vs 128-bit decimals) so the packed
@@ -206,6 +214,7 @@ def normalize_structure(b: Batch, comm, extra: Sequence[int] = ()) -> Batch:
     (e.g. row counts); they come back as ``b.preamble[rank]``."""
     keys = list(b.columns)
     cols = [b.columns[k] for k in keys]
+    _no_nested(cols)
     bits = [sum(int(f) << i for i, f in enumerate(_sig(c))) for c in cols]
     digs = [_dict_digest(c.dictionary) if c.is_dict else 0 for c in cols]
     rows = comm.allgather_ints(list(extra) + bits + digs)
@@ -519,6 +528,7 @@ def _gather_columns(cols: List[Column], counts: List[int], comm,
     bytes carrying every rank's packed fixed-width rows followed by its
     plain-string columns' bytes (``str_bytes[rank][k]``: byte count of the
     k-th string column per rank, exchanged here when not given)."""
+    _no_nested(cols)
     from ..ops.pack import pack_rows, unpack_rows
     n = len(cols[0]) if cols else 0
     tensors, spec = _fixed_parts(cols)

@@ -21,7 +21,7 @@ from .expr import (AGG_FUNCS, FRAME_KINDS, RANKING_FUNCS, VALUE_FUNCS, AggCall, 
                    Func, InList, IsNull, Like, Lit, Neg, Not, SubqueryExpr, WindowCall, WindowFrame, and_all, col_refs,
                    transform, walk)
 from .logical import (Aggregate, ColInfo, Filter, Join, Limit, Plan, Project, RecursiveCTE, Scan, Sort, Union, Values,
-                      TableFunction, Window, WorkTableScan)
+                      TableFunction, Unnest, Window, WorkTableScan)
 
 EPOCH = datetime.date(1970, 1, 1)
 
@@ -397,6 +397,26 @@ class Binder:
             rn = WindowCall("row_number", [], list(distinct_on), okeys, self._frame(None, okeys), INT64)
             rci = ColInfo(self.ids(), "__distinct_on", INT64, False)
             plan = Filter(Window(plan, [(rci, rn)]), BinOp("=", rci.ref(), Lit(1, INT64), BOOL))
+        # ---- SELECT unnest(list): one row per element, the other items repeated
+        unn = {}
+        for e, _ in items:
+            for x in walk(e):
+                if isinstance(x, Func) and x.name == "unnest":
+                    unn.setdefault(x.args[0].sql(), x)
+        if len(unn) > 1:
+            raise NotSupported("more than one distinct unnest() in a SELECT list")
+        if unn:
+            u = next(iter(unn.values()))
+            lci = ColInfo(self.ids(), "__unnest_list", u.args[0].dtype, True)
+            plan = Project(plan, [(c, c.ref()) for c in plan.schema] + [(lci, u.args[0])])
+            oci = ColInfo(self.ids(), "__unnest", u.dtype, True)
+            plan = Unnest(plan, lci, oci)
+            key = u.sql()
+
+            def urw(e: Expr) -> Expr:
+                return _transform_top_down(e, lambda x: oci.ref() if x.sql() == key else None)
+            items = [(urw(e), a) for e, a in items]
+            order_bound = [(k, urw(x) if k == "expr" else x, a, nf) for k, x, a, nf in order_bound]
         # ---- projection (+ hidden ORDER BY columns)
         proj = [(ColInfo(self.ids(), a, e.dtype, e.nullable), e) for e, a in items]
         hidden = []
@@ -1129,7 +1149,111 @@ class Binder:
         if name == "arrow_typeof":
             _nargs(name, args, 1)
             return Lit(arrow_type_name(args[0].dtype), UTF8)
+        if name in _NESTED_FUNCS:
+            return self._nested_func(name, args)
+        if name in ("md5", "sha224", "sha256", "sha384", "sha512", "digest"):
+            if name == "digest":
+                if len(args) != 2 or not isinstance(args[1], Lit) or not isinstance(args[1].value, str):
+                    raise PlanError("digest(value, algorithm): the algorithm must be a string constant")
+                algo = args[1].value.lower()
+                if algo not in ("md5", "sha224", "sha256", "sha384", "sha512"):
+                    raise NotSupported(f"digest(): algorithm '{algo}'")
+            else:
+                _nargs(name, args, 1)
+                algo = name
+            a = self._coerce(args[0], UTF8)
+            if isinstance(a, Lit):
+                import hashlib
+                return Lit(None if a.value is None else hashlib.new(algo, a.value.encode()).hexdigest(), UTF8)
+            return Func("hex_digest", [a], UTF8, (algo,))
+        if name in ("uuid", "gen_random_uuid"):
+            return Func("uuid", [], UTF8)
+        if name in ("to_char", "date_format"):
+            _nargs(name, args, 2)
+            if not isinstance(args[1], Lit) or not isinstance(args[1].value, str):
+                raise NotSupported(f"{name}(): the format must be a string constant")
+            x = args[0]
+            if x.dtype.is_string:
+                x = self._coerce(x, T.TIMESTAMP)
+            if x.dtype.kind not in ("date32", "timestamp"):
+                raise PlanError(f"{name}() formats dates and timestamps, got {x.dtype}")
+            if isinstance(x, Lit):
+                from ..ops.digest import py_strftime
+                mult = 86_400_000_000 if x.dtype.kind == "date32" else 1
+                return Lit(None if x.value is None else py_strftime(x.value * mult, args[1].value), UTF8)
+            return Func("to_char", [x], UTF8, (args[1].value,))
         return self._func_library(name, args)
+
+    def _nested_func(self, name: str, args: List[Expr]) -> Expr:
+        """LIST / STRUCT functions (DataFusion's datafusion-functions-nested,
+        reference Cargo.lock:1125); evaluated by ops/nested.py."""
+        def lit(i, what, kind=None):
+            if len(args) <= i or not isinstance(args[i], Lit) or args[i].value is None or \
+                    (kind is not None and not isinstance(args[i].value, kind)):
+                raise NotSupported(f"{name}(): {what} must be a constant")
+            return args[i].value
+
+        def need_list(i=0):
+            if len(args) <= i or args[i].dtype.kind != "list":
+                raise PlanError(f"{name}() needs a list argument, got "
+                                f"{args[i].dtype if len(args) > i else 'nothing'}")
+            return args[i]
+        if name in ("make_array", "make_list", "array"):
+            t = None
+            for a in args:
+                if a.dtype.kind != "null":
+                    t = a.dtype if t is None else (t if t == a.dtype else T.common_numeric(t, a.dtype))
+            t = t or INT64
+            return Func("make_array", [self._coerce(a, t) for a in args], T.LIST(t))
+        if name in ("array_length", "cardinality", "list_length", "array_size"):
+            a = need_list()
+            return Func("array_length", [a], INT64)
+        if name in ("array_element", "list_element", "array_extract", "list_extract", "get_field"):
+            _nargs(name, args, 2)
+            a = args[0]
+            if a.dtype.kind == "struct":
+                f = lit(1, "field name", str)
+                ft = dict(a.dtype.fields).get(f)
+                if ft is None:
+                    raise PlanError(f"struct {a.dtype} has no field '{f}'")
+                return Func("get_field", [a], ft, (f,))
+            need_list()
+            i = args[1]
+            if isinstance(i, Lit):
+                if i.value is None:
+                    return Lit(None, a.dtype.child)
+                return Func("array_element", [a], a.dtype.child, (int(i.value),))
+            return Func("array_element", [a, self._coerce(i, INT64)], a.dtype.child)
+        if name == "struct":
+            names = [f"c{i}" for i in range(len(args))]
+            return Func("struct", args, T.STRUCT(list(zip(names, [a.dtype for a in args]))), tuple(names))
+        if name == "named_struct":
+            if len(args) % 2:
+                raise PlanError("named_struct() takes name, value pairs")
+            names = [lit(i, "field name", str) for i in range(0, len(args), 2)]
+            vals = args[1::2]
+            return Func("struct", list(vals), T.STRUCT(list(zip(names, [a.dtype for a in vals]))), tuple(names))
+        if name in ("array_has", "array_contains", "list_has", "list_contains"):
+            a = need_list()
+            v = args[1] if len(args) > 1 else None
+            if not isinstance(v, Lit):
+                raise NotSupported(f"{name}(): the value must be a constant")
+            v = self._coerce_lit(v, a.dtype.child) if v.value is not None else v
+            return Func("array_has", [a], BOOL, (v.value,))
+        if name in ("array_to_string", "list_to_string", "array_join", "list_join"):
+            a = need_list()
+            sep = lit(1, "separator", str)
+            null_str = lit(2, "null string", str) if len(args) > 2 else None
+            return Func("array_to_string", [a], UTF8, (sep, null_str))
+        if name == "unnest":
+            a = need_list()
+            return Func("unnest", [a], a.dtype.child)
+        if name == "regexp_match":
+            a = self._coerce(args[0], UTF8)
+            pat = lit(1, "pattern", str)
+            flags = lit(2, "flags", str) if len(args) > 2 else ""
+            return Func("regexp_match", [a], T.LIST(UTF8), (pat, flags))
+        raise NotSupported(f"function {name}()")
 
     def _agg_order(self, node, scope) -> List[Tuple[Expr, bool, bool]]:
         out = []
@@ -1493,6 +1617,12 @@ _EXTRA_AGGS = ("stddev_samp", "stddev_pop", "var_samp", "var_pop", "variance", "
 _TRUNC_UNITS = ("microsecond", "millisecond", "second", "minute", "hour", "day", "week", "month", "quarter", "year")
 
 
+_NESTED_FUNCS = ("make_array", "make_list", "array", "array_length", "cardinality", "list_length", "array_size",
+                 "array_element", "list_element", "array_extract", "list_extract", "get_field", "struct",
+                 "named_struct", "array_has", "array_contains", "list_has", "list_contains", "array_to_string",
+                 "list_to_string", "array_join", "list_join", "unnest", "regexp_match")
+
+
 def similar_to_regex(pat: str, esc: str = "\\") -> str:
     """SQL ``SIMILAR TO`` pattern -> an anchored regular expression: ``%`` and
     ``_`` are the LIKE wildcards, ``| * + ? {m,n} ( ) [...]`` keep their regex
@@ -1748,7 +1878,7 @@ def _make_agg(name: str, arg: Optional[Expr], distinct: bool, flt, arg2: Optiona
             raise PlanError(f"{name}() needs two numeric arguments")
         return AggCall(name, arg, False, FLOAT64, flt, arg2)
     if name == "array_agg":
-        raise NotSupported("array_agg(): list-typed results are not supported (use string_agg)")
+        return AggCall("array_agg", arg, distinct, T.LIST(t), flt, None, None, order)
     raise NotSupported(f"aggregate {name}")
 
 

@@ -96,6 +96,30 @@ class TableFunction(Plan):
 
 
 @dataclass(eq=False)
+class Unnest(Plan):
+    """``SELECT unnest(list_expr), ...``: one row per element of the list
+    column ``list_col`` (NULL / empty lists give none); every input column is
+    repeated, the element is ``out``."""
+    input: Plan
+    list_col: ColInfo
+    out: ColInfo
+
+    @property
+    def schema(self):  # type: ignore[override]
+        return self.input.schema + [self.out]
+
+    @property
+    def inputs(self):
+        return [self.input]
+
+    def with_inputs(self, inputs):
+        return Unnest(inputs[0], self.list_col, self.out)
+
+    def label(self):
+        return f"Unnest: {self.list_col.name}#{self.list_col.cid} -> {self.out.name}#{self.out.cid}"
+
+
+@dataclass(eq=False)
 class Filter(Plan):
     input: Plan
     pred: Expr

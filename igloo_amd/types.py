@@ -7,12 +7,18 @@ Device layout (Arrow-compatible in HBM):
 * DECIMAL(p, s): int64 scaled by 10**s (TPC-H decimals are (15, 2)); wide
   results (p > 18, e.g. SUM) may hold an [n, 2] int64 (lo, hi) int128 tensor;
 * UTF8: either plain (int64 offsets + uint8 bytes, Arrow large_string) or
-  dictionary-encoded (int32 codes + a plain-string dictionary column).
+  dictionary-encoded (int32 codes + a plain-string dictionary column);
+* LIST(t): an [n, 2] int64 (start, length) view per row into a child column
+  of type t (so a row gather is one 16-byte gather and the child values never
+  move until the result is built); STRUCT: an int64 row id per row into one
+  child column per field. The child columns ride in ``Column.dictionary``
+  (a ``columnar.Nested`` payload), which every operator already carries
+  along with the rows.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
+from typing import Optional, Tuple
 
 import pyarrow as pa
 import torch
@@ -28,6 +34,12 @@ class DataType:
     kind: str
     precision: int = 0
     scale: int = 0
+    child: Optional["DataType"] = None     # LIST element type
+    fields: Tuple = ()                     # STRUCT ((name, DataType), ...)
+
+    @property
+    def is_nested(self) -> bool:
+        return self.kind in ("list", "struct")
 
     # ---------------------------------------------------------------- predicates
     @property
@@ -61,6 +73,10 @@ class DataType:
 
     def to_arrow(self) -> pa.DataType:
         k = self.kind
+        if k == "list":
+            return pa.list_(self.child.to_arrow())
+        if k == "struct":
+            return pa.struct([pa.field(n, t.to_arrow()) for n, t in self.fields])
         if k == "decimal":
             return pa.decimal128(max(self.precision, 1), self.scale)
         if k == "utf8":
@@ -72,6 +88,10 @@ class DataType:
     def __str__(self) -> str:
         if self.kind == "decimal":
             return f"Decimal128({self.precision}, {self.scale})"
+        if self.kind == "list":
+            return f"List({self.child})"
+        if self.kind == "struct":
+            return "Struct(" + ", ".join(f"{n} {t}" for n, t in self.fields) + ")"
         return _NAMES.get(self.kind, self.kind)
 
     __repr__ = __str__
@@ -94,6 +114,14 @@ def DECIMAL(p: int, s: int) -> DataType:
     return DataType("decimal", min(p, 38), s)
 
 
+def LIST(child: DataType) -> DataType:
+    return DataType("list", child=child)
+
+
+def STRUCT(fields) -> DataType:
+    return DataType("struct", fields=tuple((str(n), t) for n, t in fields))
+
+
 _TORCH = {
     "bool": torch.bool,
     "int8": torch.int8,
@@ -107,6 +135,8 @@ _TORCH = {
     "decimal": torch.int64,
     "utf8": torch.uint8,
     "null": torch.bool,
+    "list": torch.int64,
+    "struct": torch.int64,
 }
 _ARROW = {
     "bool": pa.bool_(),
@@ -137,6 +167,10 @@ _NAMES = {
 def from_arrow_type(t: pa.DataType) -> DataType:
     if pa.types.is_dictionary(t):
         return from_arrow_type(t.value_type)
+    if pa.types.is_list(t) or pa.types.is_large_list(t) or pa.types.is_fixed_size_list(t):
+        return LIST(from_arrow_type(t.value_type))
+    if pa.types.is_struct(t):
+        return STRUCT([(t.field(i).name, from_arrow_type(t.field(i).type)) for i in range(t.num_fields)])
     if pa.types.is_boolean(t):
         return BOOL
     for k in ("int8", "int16", "int32", "int64"):
@@ -201,6 +235,8 @@ def common_numeric(a: DataType, b: DataType) -> DataType:
     """Type both operands are coerced to for comparison / CASE / UNION."""
     if a == b:
         return a
+    if a.kind == "list" and b.kind == "list":
+        return LIST(common_numeric(a.child, b.child))
     if a.kind == "null":
         return b
     if b.kind == "null":
