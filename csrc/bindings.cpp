@@ -644,12 +644,24 @@ PYBIND11_MODULE(_native, m) {
     kern::strfmt_write(reinterpret_cast<const uint8_t*>(fmt.data()), (int)fmt.size(), is_date, P<const void>(v), n,
                        P<const int64_t>(off), out_cap, P<uint8_t>(out), S(s));
   });
+  m.def("regex_lds_bytes", &kern::regex_lds_bytes);
   m.def("regex_dfa_match", [](uintptr_t off, uintptr_t chars, int64_t n, uintptr_t table, uintptr_t cls,
                               uintptr_t flags, int nstates, int nclasses, int start, bool anchored_end, bool negate,
                               uintptr_t out, uintptr_t s) {
     kern::regex_dfa_match(P<const int64_t>(off), P<const uint8_t>(chars), n, P<const uint16_t>(table),
                           P<const uint8_t>(cls), P<const uint8_t>(flags), nstates, nclasses, start, anchored_end,
                           negate, P<uint8_t>(out), S(s));
+  });
+  m.def("probe_hash16", [](bool mfma, uintptr_t k0, uintptr_t k1, uintptr_t k2, uintptr_t k3, int64_t n,
+                           uintptr_t proj, uintptr_t out, uintptr_t s) {
+    kern::probe_hash16(mfma, P<const int32_t>(k0), P<const int32_t>(k1), P<const int32_t>(k2), P<const int32_t>(k3),
+                       n, P<const int8_t>(proj), P<uint32_t>(out), S(s));
+  });
+  m.def("probe_inlist16", [](bool mfma, uintptr_t off, uintptr_t chars, int64_t n, const std::string& pats, int npat,
+                             int len, uintptr_t out, uintptr_t s) {
+    if ((int64_t)pats.size() < 16 * npat) throw std::runtime_error("probe_inlist16: 16 bytes per pattern");
+    kern::probe_inlist16(mfma, P<const int64_t>(off), P<const uint8_t>(chars), n,
+                         reinterpret_cast<const uint8_t*>(pats.data()), npat, len, P<uint8_t>(out), S(s));
   });
   m.def("digest_width", &kern::digest_width);
   m.def("digest_hex", [](int algo, uintptr_t off, uintptr_t chars, int64_t n, uintptr_t out, uintptr_t s) {
@@ -794,6 +806,15 @@ PYBIND11_MODULE(_native, m) {
                             uintptr_t sum_out, uintptr_t cnt_out, uintptr_t s) {
     kern::win_frame_sum(P<int64_t>(psum), f64, P<int64_t>(pcnt), P<int64_t>(lo), P<int64_t>(hi), n,
                         P<int64_t>(sum_out), P<int64_t>(cnt_out), S(s));
+  });
+  m.def("win_sparse_build", [](uintptr_t vals, bool f64, uintptr_t valid, int64_t n, bool is_max, int levels,
+                               uintptr_t table, uintptr_t s) {
+    kern::win_sparse_build(P<int64_t>(vals), f64, P<uint8_t>(valid), n, is_max, levels, P<int64_t>(table), S(s));
+  });
+  m.def("win_sparse_query", [](uintptr_t table, int levels, int64_t n, uintptr_t lo, uintptr_t hi, uintptr_t pcnt,
+                               bool is_max, bool f64, uintptr_t out, uintptr_t out_valid, uintptr_t s) {
+    kern::win_sparse_query(P<int64_t>(table), levels, n, P<int64_t>(lo), P<int64_t>(hi), P<int64_t>(pcnt), is_max,
+                           f64, P<int64_t>(out), P<uint8_t>(out_valid), S(s));
   });
   m.def("win_frame_minmax", [](uintptr_t vals, bool f64, bool is_max, uintptr_t valid, uintptr_t lo, uintptr_t hi,
                                int64_t n, uintptr_t out, uintptr_t out_valid, uintptr_t s) {

@@ -1007,7 +1007,7 @@ void sorted_having(const void* keys, bool key64, int64_t n, const AggDesc* descs
   // streaming shape: COUNTs without NULLs plus at most one NULL-free SUM over
   // int32 / int16 / int8 values (src64 codes 0 / 2 / 3; 2 and 3 only here)
   int vagg = -1;
-  bool streaming = getenv("IGLOO_HAVING_SCAN") == nullptr || getenv("IGLOO_HAVING_SCAN")[0] != '0';
+  bool streaming = !debug_flag("having_general");
   for (int k = 0; k < nagg && streaming; ++k) {
     const AggDesc& d = descs[k];
     if (d.valid) streaming = false;

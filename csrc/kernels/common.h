@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -27,10 +28,31 @@ constexpr int64_t kEmptyKey = INT64_MIN;  // hash-table empty-slot sentinel
                                " at " __FILE__ ":" + std::to_string(__LINE__));          \
   } while (0)
 
-// Launch-error check after every kernel launch. With IGLOO_SYNC_CHECK=1 the
+// Launch-error check after every kernel launch. With IGLOO_DEBUG=sync_check the
 // stream is also synchronised so an asynchronous fault is attributed to the
 // launch that caused it (SURVEY §5.2 debug mode).
 void check_launch(const char* what, hipStream_t stream);
+
+// IGLOO_DEBUG: comma list of debug / experimental tokens (``token`` or
+// ``token=value``), shared with the Python side (igloo_amd/utils/switches.py)
+inline bool debug_flag(const char* token) {
+  const char* e = std::getenv("IGLOO_DEBUG");
+  if (!e) return false;
+  const std::string s(e), t(token);
+  size_t p = 0;
+  while (p <= s.size()) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    std::string tok = s.substr(p, q - p);
+    const size_t eq = tok.find('=');
+    if (eq != std::string::npos) tok = tok.substr(0, eq);
+    while (!tok.empty() && tok.front() == ' ') tok.erase(tok.begin());
+    while (!tok.empty() && tok.back() == ' ') tok.pop_back();
+    if (tok == t) return true;
+    p = q + 1;
+  }
+  return false;
+}
 
 inline unsigned grid_for(int64_t n, int per_block, int64_t max_blocks = 1 << 20) {
   int64_t g = (n + per_block - 1) / per_block;

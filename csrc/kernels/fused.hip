@@ -620,11 +620,7 @@ void launch_agg(const FfSpec& spec, int64_t n, hipStream_t stream) {
   int lanes = kWave;
   while (lanes > 1 && cells * 2 * lanes * sizeof(int64_t) > (size_t)kFfLdsMax) lanes >>= 1;
   const size_t lds = cells * 2 * lanes * sizeof(int64_t);
-  static const int block = [] {
-    const char* e = std::getenv("IGLOO_FF_AGG_BLOCK");
-    const int v = e ? std::atoi(e) : kFfAggBlock;
-    return (v == 256 || v == 512) ? v : kFfAggBlock;
-  }();
+  constexpr int block = kFfAggBlock;
   // persistent-style grid: about as many blocks as stay resident (LDS-limited,
   // 160 KB per CU; at most 2048 threads), each streaming many rows, so the
   // per-block init/merge is amortised
@@ -655,10 +651,7 @@ void ff_mask(const FfSpec& spec, int64_t n, uint8_t* out, hipStream_t stream) {
 // for the LDS-atomic kernel (the per-row value/limb interpretation dominates
 // either way); the generated scan kernels (exec/fused_jit.py) replace both
 // on warm queries.
-static bool g_ff_mfma = [] {
-  const char* e = std::getenv("IGLOO_FF_MFMA");
-  return e ? std::atoi(e) != 0 : false;
-}();
+static bool g_ff_mfma = debug_flag("ff_mfma");
 
 bool ff_set_mfma(bool on) {
   const bool prev = g_ff_mfma;

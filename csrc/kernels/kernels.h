@@ -405,6 +405,13 @@ void regex_dfa_match(const int64_t* off, const uint8_t* chars, int64_t n, const 
                      const uint8_t* flags, int nstates, int nclasses, int start, bool anchored_end, bool negate,
                      uint8_t* out, hipStream_t s);
 
+// ---- mfma_probe.hip (MFMA vs VALU hash / compare experiment, scripts/mfma_hash_ab.py) ---
+void probe_hash16(bool mfma, const int32_t* k0, const int32_t* k1, const int32_t* k2, const int32_t* k3, int64_t n,
+                  const int8_t* proj, uint32_t* out, hipStream_t s);
+// pats: npat x 16 bytes (first len used); out[r] = string r equals one of them
+void probe_inlist16(bool mfma, const int64_t* off, const uint8_t* chars, int64_t n, const uint8_t* pats, int npat,
+                    int len, uint8_t* out, hipStream_t s);
+
 // ---- nested.hip (LIST rows: [n, 2] int64 (start, length) into a child column) ---
 void list_element_idx(const int64_t* se, const uint8_t* valid, const int64_t* pos, const uint8_t* pos_valid,
                       int64_t pos_const, int64_t n, int64_t child_n, int64_t* out, hipStream_t s);
@@ -536,6 +543,11 @@ void win_bounds(int64_t n, const int64_t* seg_start, const int64_t* seg_end, con
                 hipStream_t s);
 void win_frame_sum(const int64_t* psum, bool f64, const int64_t* pcnt, const int64_t* lo, const int64_t* hi,
                    int64_t n, int64_t* sum_out, int64_t* cnt_out, hipStream_t s);
+// sparse table [levels][n] of min / max (floats as ordered int64) and its O(1) frame queries
+void win_sparse_build(const int64_t* vals, bool f64, const uint8_t* valid, int64_t n, bool is_max, int levels,
+                      int64_t* table, hipStream_t s);
+void win_sparse_query(const int64_t* table, int levels, int64_t n, const int64_t* lo, const int64_t* hi,
+                      const int64_t* pcnt, bool is_max, bool f64, int64_t* out, uint8_t* out_valid, hipStream_t s);
 void win_frame_minmax(const int64_t* vals, bool f64, bool is_max, const uint8_t* valid, const int64_t* lo,
                       const int64_t* hi, int64_t n, int64_t* out, uint8_t* out_valid, hipStream_t s);
 void win_rank(int fn, int64_t arg, int64_t n, const int64_t* seg_start, const int64_t* seg_end,

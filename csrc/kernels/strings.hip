@@ -665,11 +665,10 @@ void str_like_segments(const int64_t* off, const uint8_t* chars, int64_t n, cons
                        int min_seg, hipStream_t stream) {
   if (n == 0) return;
   if (nseg > kSegMax) throw std::runtime_error("str_like_segments: too many segments");
-  const bool dword_filter = getenv("IGLOO_LIKE_DWORD") == nullptr || getenv("IGLOO_LIKE_DWORD")[0] != '0';
+  const bool dword_filter = !debug_flag("like_nodword");
   if (dword_filter && nseg >= 1 && nseg <= 2 && min_seg >= 7) {
     const dim3 g(grid_for(n, kBlock, 256 * 8 * 4)), b(kBlock);
-    const char* ue = getenv("IGLOO_LIKE_UNROLL");
-    const int u = ue ? atoi(ue) : 1;
+    constexpr int u = 1;   // (2 and 4 rows per lane measured no faster: profiles/r5_ab_like_*.txt)
 #define IGLOO_LIKE_DWORD(S, U)                                                                                  \
   hipLaunchKernelGGL((like_dword_kernel<S, kLikeDwordTile, U>), g, b, 0, stream, off, chars, n, seg, seg_off, nseg, \
                      anchor_start, anchor_end, negate, out, nbytes)

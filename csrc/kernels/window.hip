@@ -484,6 +484,64 @@ __global__ __launch_bounds__(kBlock) void win_frame_minmax_kernel(const int64_t*
   out_valid[r] = any;
 }
 
+// Sliding min / max of any width in O(1) per row: a sparse table
+// (level k holds the op over [i, i + 2^k)) built level by level, each level
+// one pass over the previous one; a frame [lo, hi] is covered by two
+// overlapping power-of-two blocks. NULLs enter as the op's identity; the
+// frame's NULL-free flag comes from the caller's prefix count (or hi >= lo).
+// Floats travel as order-preserving int64 images.
+__device__ inline int64_t f64_ord(int64_t bits) { return bits >= 0 ? bits : (bits ^ INT64_MAX); }
+
+__global__ __launch_bounds__(kBlock) void win_sparse_init_kernel(const int64_t* __restrict__ vals, bool f64,
+                                                                 const uint8_t* __restrict__ valid, int64_t n,
+                                                                 bool is_max, int64_t* __restrict__ t0) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool ok = !valid || valid[i];
+    const int64_t v = f64 ? f64_ord(vals[i]) : vals[i];
+    t0[i] = ok ? v : (is_max ? INT64_MIN : INT64_MAX);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void win_sparse_level_kernel(const int64_t* __restrict__ prev,
+                                                                  int64_t* __restrict__ next, int64_t n, int64_t half,
+                                                                  bool is_max) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = prev[i];
+    if (i + half < n) {
+      const int64_t b = prev[i + half];
+      next[i] = is_max ? (a > b ? a : b) : (a < b ? a : b);
+    } else {
+      next[i] = a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void win_sparse_query_kernel(const int64_t* __restrict__ table, int levels,
+                                                                  int64_t n, const int64_t* __restrict__ lo,
+                                                                  const int64_t* __restrict__ hi,
+                                                                  const int64_t* __restrict__ pcnt, bool is_max,
+                                                                  bool f64, int64_t* __restrict__ out,
+                                                                  uint8_t* __restrict__ out_valid) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = lo[r], h = hi[r];
+    if (h < l || l < 0 || h >= n) {
+      out[r] = 0;
+      out_valid[r] = 0;
+      continue;
+    }
+    const int64_t w = h - l + 1;
+    int k = 63 - __builtin_clzll((unsigned long long)w);
+    if (k >= levels) k = levels - 1;   // defensive: the host sized levels for the widest frame
+    const int64_t* t = table + (int64_t)k * n;
+    const int64_t a = t[l], b = t[h - ((int64_t)1 << k) + 1];
+    int64_t m = is_max ? (a > b ? a : b) : (a < b ? a : b);
+    const bool any = pcnt ? (pcnt[h] - (l > 0 ? pcnt[l - 1] : 0)) > 0 : true;
+    if (f64) m = f64_ord(m);           // the map is its own inverse
+    out[r] = any ? m : 0;
+    out_valid[r] = any;
+  }
+}
+
 // ------------------------------------------------------------------- ranking
 __global__ __launch_bounds__(kBlock) void win_rank_kernel(int fn, int64_t arg, int64_t n, const int64_t* seg_start,
                                                           const int64_t* seg_end, const int64_t* peer_start,
@@ -587,6 +645,25 @@ void win_frame_sum(const int64_t* psum, bool f64, const int64_t* pcnt, const int
   hipLaunchKernelGGL(win_frame_sum_kernel, dim3(grid_for(n, kBlock, INT32_MAX)), dim3(kBlock), 0, s, psum, f64, pcnt,
                      lo, hi, n, sum_out, cnt_out);
   check_launch("win.frame_sum", s);
+}
+
+void win_sparse_build(const int64_t* vals, bool f64, const uint8_t* valid, int64_t n, bool is_max, int levels,
+                      int64_t* table, hipStream_t s) {
+  if (n == 0) return;
+  dim3 g(grid_for(n, kBlock, 1 << 16)), b(kBlock);
+  hipLaunchKernelGGL(win_sparse_init_kernel, g, b, 0, s, vals, f64, valid, n, is_max, table);
+  for (int k = 1; k < levels; ++k)
+    hipLaunchKernelGGL(win_sparse_level_kernel, g, b, 0, s, table + (int64_t)(k - 1) * n, table + (int64_t)k * n, n,
+                       (int64_t)1 << (k - 1), is_max);
+  check_launch("win_sparse_build", s);
+}
+
+void win_sparse_query(const int64_t* table, int levels, int64_t n, const int64_t* lo, const int64_t* hi,
+                      const int64_t* pcnt, bool is_max, bool f64, int64_t* out, uint8_t* out_valid, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(win_sparse_query_kernel, dim3(grid_for(n, kBlock, 1 << 16)), dim3(kBlock), 0, s, table, levels,
+                     n, lo, hi, pcnt, is_max, f64, out, out_valid);
+  check_launch("win_sparse_query", s);
 }
 
 void win_frame_minmax(const int64_t* vals, bool f64, bool is_max, const uint8_t* valid, const int64_t* lo,

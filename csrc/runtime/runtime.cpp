@@ -19,10 +19,7 @@ namespace igloo {
 namespace kern {
 
 static int sync_check_mode() {
-  static int mode = [] {
-    const char* v = std::getenv("IGLOO_SYNC_CHECK");
-    return v && *v && std::strcmp(v, "0") != 0 ? 1 : 0;
-  }();
+  static int mode = debug_flag("sync_check") ? 1 : 0;
   return mode;
 }
 

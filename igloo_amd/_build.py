@@ -56,12 +56,22 @@ def _headers_digest() -> str:
     return h.hexdigest()
 
 
+def _sanitize() -> str:
+    """IGLOO_DEBUG=sanitize=address+undefined: host sanitizers for the build
+    (the value's '+' separates sanitizers; bare ``sanitize`` = address,undefined)."""
+    from .utils import switches
+    v = switches._parse(os.environ.get("IGLOO_DEBUG")).get("sanitize")
+    if not v:
+        return ""
+    return "address,undefined" if v == "1" else v.replace("+", ",")
+
+
 def _flags(src: Path) -> list[str]:
     base = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
             "-Wno-unused-result", "-fvisibility=hidden"]
-    if os.environ.get("IGLOO_SANITIZE"):
+    if _sanitize():
         # host-only sanitizers (GPU ASan is not available on the pool)
-        base += [f"-Xarch_host", f"-fsanitize={os.environ['IGLOO_SANITIZE']}"]
+        base += [f"-Xarch_host", f"-fsanitize={_sanitize()}"]
     # hipcc treats .cpp as HIP too; give every unit the real target so no
     # default-arch device pass is compiled
     return base + ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
@@ -83,7 +93,19 @@ def _compile(src: Path, hdr_digest: str, force: bool) -> Path:
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    """Compile what changed and link; one process at a time (a file lock:
+    parallel test workers and a manual build share build/obj)."""
+    import fcntl
     OBJ.mkdir(parents=True, exist_ok=True)
+    with open(OBJ / ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            return _build_locked(force, jobs, verbose)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(force: bool, jobs: int | None, verbose: bool) -> Path:
     srcs = _sources()
     hd = _headers_digest()
     jobs = jobs or min(8, os.cpu_count() or 4)
@@ -97,8 +119,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     tmp = out.with_suffix(".tmp.so")
     cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
            "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
-    if os.environ.get("IGLOO_SANITIZE"):
-        cmd += [f"-fsanitize={os.environ['IGLOO_SANITIZE']}"]
+    if _sanitize():
+        cmd += [f"-fsanitize={_sanitize()}"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

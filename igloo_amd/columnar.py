@@ -334,7 +334,8 @@ def _low_cardinality(arr: pa.Array) -> bool:
 
 
 def _decimal_to_int64(arr: pa.Array) -> np.ndarray:
-    """decimal128 array -> int64 unscaled values (raises if a value needs > 63 bits)."""
+    """decimal128 array -> int64 unscaled values, or [n, 2] (lo, hi) int64
+    pairs when some value needs more than 63 bits."""
     n = len(arr)
     if n == 0:
         return np.zeros(0, np.int64)
@@ -346,7 +347,11 @@ def _decimal_to_int64(arr: pa.Array) -> np.ndarray:
     if arr.null_count:
         ok |= ~arr.is_valid().to_numpy(zero_copy_only=False)
     if not ok.all():
-        raise ExecutionError("decimal value exceeds 64-bit fixed-point range")
+        # past 63 bits: the [n, 2] (lo, hi) 128-bit layout (NULL rows zeroed)
+        out = raw.copy()
+        if arr.null_count:
+            out[~arr.is_valid().to_numpy(zero_copy_only=False)] = 0
+        return out
     out = lo.copy()
     if arr.null_count:
         out[~arr.is_valid().to_numpy(zero_copy_only=False)] = 0

@@ -11,7 +11,7 @@ strings; ``scan()`` (TableSource) returns typed device columns. On a GPU the
 file is staged in HBM and parsed by gfx950 kernels (igloo_amd/connectors/
 gpu_csv.py: quote-aware row splitting + typed field parsing); on CPU, or when
 a value does not parse as the declared type, Arrow's multithreaded CSV reader
-is used. ``IGLOO_CSV_GPU=0`` forces the host reader.
+is used. ``GPU_PARSE = False`` forces the host reader.
 """
 from __future__ import annotations
 
@@ -29,7 +29,7 @@ from ..columnar import Batch, Column
 from ..utils.errors import IoError
 
 Row = List[str]
-GPU_PARSE = os.environ.get("IGLOO_CSV_GPU", "1") != "0"
+GPU_PARSE = True
 #: files up to this size infer their schema from the whole file, larger ones
 #: from the first block (the GPU parse then checks every value)
 FULL_INFER_BYTES = 64 << 20

@@ -18,7 +18,7 @@ chunks are staged with native preads + one H2D copy and their pages are
 decompressed and decoded by gfx950 kernels (connectors/gpu_parquet.py);
 columns that decoder does not handle (nested, INT96, non-snappy codecs, DELTA
 encodings) and CPU scans use the host decoder (pyarrow). IO errors raise.
-``IGLOO_PARQUET_GPU=0`` forces the host decoder.
+``GPU_DECODE = False`` forces the host decoder.
 
 The source itself keeps nothing resident: the engine wraps it in the cache
 tier (cache/cdc.py CachedTable) whose CDC probe is ``version`` — the listed
@@ -42,7 +42,7 @@ from ..catalog import Field, TableSource
 from ..columnar import Batch, Column
 from ..utils.errors import IoError
 
-GPU_DECODE = os.environ.get("IGLOO_PARQUET_GPU", "1") != "0"
+GPU_DECODE = True
 _FLIP = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<="}
 
 

@@ -36,16 +36,16 @@ from .utils.log import get_logger
 #: cache optimized logical plans per SQL text (parse + bind + optimize cost
 #: ~1 ms of Python per TPC-H query); keyed on the catalog version and the
 #: session settings, so any DDL or SET invalidates
-PLAN_CACHE = os.environ.get("IGLOO_PLAN_CACHE", "1") == "1"
+PLAN_CACHE = True
 PLAN_CACHE_SIZE = 256
 #: replay the host readbacks of repeated queries over unchanged data (see
 #: QueryEngine._execute_speculative)
-SPECULATE = os.environ.get("IGLOO_SPECULATE", "1") == "1"
-SPMD_SPECULATE = os.environ.get("IGLOO_SPMD_SPECULATE", "1") == "1"
+SPECULATE = True
+SPMD_SPECULATE = True
 #: SPMD query graphs (collectives captured with the kernels; RCCL only)
-SPMD_GRAPHS = os.environ.get("IGLOO_SPMD_GRAPHS", "1") == "1"
+SPMD_GRAPHS = True
 #: SPMD: a query over replicated tables only splits its largest table by key range
-SLICE_REPLICATED = os.environ.get("IGLOO_SLICE_REPLICATED", "1") == "1"
+SLICE_REPLICATED = True
 
 log = get_logger("engine")
 
@@ -124,8 +124,8 @@ def _host_columns(cols: List[Column], deferred=None, guard=None) -> List[Column]
         return None if t is None else t.to("cpu", non_blocking=True)
 
     def move(c: Column) -> Column:
-        if not c.data.is_cuda:
-            return c
+        if not c.data.is_cuda or c.dtype.is_nested:
+            return c          # (nested: rows are views into device children; to_arrow copies them)
         d = c.dictionary
         if d is not None and len(d) > 2 * len(c) + 1024:
             return c

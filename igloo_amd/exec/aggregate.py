@@ -3,6 +3,7 @@
 One of the five operator modules (context, scan, joins, aggregate, sorting)."""
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import math
 import os
 import re
@@ -39,15 +40,16 @@ from .joins import (HashJoinExec, LateBatch, _index_key_filter, _index_then_filt
 # ======================================================================= aggregate
 #: eager COUNT under LEFT JOIN: right-key spans up to this count with one histogram
 EAGER_COUNT_DIRECT_SPAN = 1 << 27
-#: HashAggExec._eager_count_masked (IGLOO_EAGER_COUNT_MASKED=0 turns it off)
-EAGER_COUNT_MASKED = os.environ.get("IGLOO_EAGER_COUNT_MASKED", "1") != "0"
-#: HashAggExec._sorted_having: fused sorted GROUP BY + HAVING (IGLOO_SORTED_HAVING=0 turns it off)
-SORTED_HAVING = os.environ.get("IGLOO_SORTED_HAVING", "1") != "0"
+#: HashAggExec._eager_count_masked
+EAGER_COUNT_MASKED = True
+#: HashAggExec._sorted_having: fused sorted GROUP BY + HAVING
+SORTED_HAVING = True
 SORTED_HAVING_MIN_ROWS = 1 << 16
-#: the streaming sorted-HAVING kernel (csrc/kernels/agg.hip sorted_having_scan_kernel; the C++ side reads it too)
-HAVING_SCAN = os.environ.get("IGLOO_HAVING_SCAN", "1") != "0"
+#: the streaming sorted-HAVING kernel (csrc/kernels/agg.hip sorted_having_scan_kernel; IGLOO_DEBUG=having_general
+#: takes the run-folding kernel, on the C++ side too)
+HAVING_SCAN = not _sw.debug("having_general")
 #: HashAggExec: a runtime key filter over a filtered resident scan takes the key index first
-INDEX_THEN_FILTER = os.environ.get("IGLOO_INDEX_THEN_FILTER", "1") == "1"
+INDEX_THEN_FILTER = True
 
 def having_constant(op: str, lit: Lit, src: T.DataType, func: str, float_state: bool):
     """The HAVING literal in the units of the aggregate's raw state (fused
@@ -1133,7 +1135,11 @@ def _avg(s: torch.Tensor, c: torch.Tensor, src, t) -> torch.Tensor:
             num = v * up
             q = (abs(num) + k // 2) // k
             res.append(q if num >= 0 else -q)
-        return torch.tensor(res, dtype=torch.int64, device=s.device)
+        if all(-(2**63) <= q < 2**63 for q in res):
+            return torch.tensor(res, dtype=torch.int64, device=s.device)
+        # a decimal(38, s) average past 63 bits: the (lo, hi) 128-bit layout
+        pairs = [[((q + 2**64) % 2**64) - (2**64 if ((q + 2**64) % 2**64) >= 2**63 else 0), q >> 64] for q in res]
+        return torch.tensor(pairs, dtype=torch.int64, device=s.device).reshape(len(res), 2)
     if s.dim() == 2:
         lo = s[:, 0].to(torch.float64)
         lo = torch.where(lo < 0, lo + 18446744073709551616.0, lo)

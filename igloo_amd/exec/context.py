@@ -120,7 +120,7 @@ class ExecContext:
 
     def span(self, name: str):
         """Time a phase inside an operator (device-synchronised; no-op unless
-        analyzing); a roctx range when IGLOO_ROCTX=1 (utils/trace.py)."""
+        analyzing); a roctx range under IGLOO_DEBUG=roctx (utils/trace.py)."""
         if self.analyze:
             return _Span(self, name)
         return _trace.Range(name) if _trace.ENABLED else _NOSPAN

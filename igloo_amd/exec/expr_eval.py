@@ -34,7 +34,7 @@ from ..utils.errors import ExecutionError, NotSupported
 
 #: generated expression kernels (exec/expr_jit.py) for composite expressions
 #: over GPU batches of at least this many rows
-JIT_MIN_ROWS = int(os.environ.get("IGLOO_EXPR_JIT_MIN_ROWS", "1"))
+JIT_MIN_ROWS = 1
 _JIT_ROOTS = {BinOp, Case, Cast, Func, Not, Neg, IsNull, InList}
 _JIT_ON_CPU = False   # tests: run the generator (source collection only) on CPU batches
 

@@ -23,6 +23,7 @@ projection.rs:60-64, filter.rs:47-57).
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import os
 from typing import Dict, List, Optional, Tuple
 
@@ -35,8 +36,8 @@ from ..sql.expr import BinOp, Case, Cast, ColRef, Expr, Func, InList, IsNull, Li
 from ..types import DataType
 from ..utils.errors import ExecutionError
 
-ENABLED = os.environ.get("IGLOO_EXPR_JIT", "1") == "1"
-_DEBUG = bool(os.environ.get("IGLOO_JIT_DEBUG"))
+ENABLED = os.environ.get("IGLOO_JIT", "async").lower() != "off"
+_DEBUG = _sw.debug("jit")
 BLOCK = 256
 PENDING = object()   # compile submitted, not ready: evaluate node by node this time
 

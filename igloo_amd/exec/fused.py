@@ -19,6 +19,7 @@ crates/engine/src/lib.rs:55-56; operators/filter.rs:47).
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import os
 from typing import Dict, List, Optional, Tuple
 
@@ -45,7 +46,7 @@ class Bail(Exception):
 
 
 def _debug(what, why):
-    if os.environ.get("IGLOO_FUSED_DEBUG"):
+    if _sw.debug("fused"):
         print(f"[fused] {what}: fallback ({why})", flush=True)
 
 

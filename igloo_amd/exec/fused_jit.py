@@ -30,6 +30,7 @@ identical; tests run both against the CPU engine.
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import math
 import os
 from typing import List, Optional, Sequence, Tuple
@@ -39,7 +40,7 @@ import torch
 from ..ops import jit
 
 I64_MIN, I64_MAX = -(2**63), 2**63 - 1
-ENABLED = os.environ.get("IGLOO_FF_JIT", "1") == "1"
+ENABLED = os.environ.get("IGLOO_JIT", "async").lower() != "off"
 
 _CT = {1: "i8", 2: "i16", 4: "i32", 8: "i64"}
 _VT = {1: "i8xR", 2: "i16xR", 4: "i32xR", 8: "i64xR"}
@@ -79,7 +80,7 @@ __device__ __forceinline__ i64 wmax(i64 v) {
 
 BLOCK = 256
 # consecutive rows per thread per iteration (one vector load per column)
-ROWS = int(os.environ.get("IGLOO_FF_JIT_ROWS", "4"))
+ROWS = 4
 LDS_MAX = 64 * 1024
 
 
@@ -446,7 +447,7 @@ def agg_source(sh: _Shape, terms, has_mask: bool, keys, G: int, aggs, split: Seq
 # the generated MFMA aggregation at 1.45 ms for Q1 against 1.23 ms for the
 # generated LDS-atomic kernel - the scan is bound by loads / filter / value
 # arithmetic, not by the per-row accumulation the matrix cores take over.
-MFMA = os.environ.get("IGLOO_FF_JIT_MFMA", "0") == "1"
+MFMA = _sw.debug("ff_jit_mfma")
 MFMA_COL = 272   # LDS bytes per limb column: 256 rows + 16 (spreads a ds_read_b128 over all banks)
 
 MFMA_PRELUDE = r"""

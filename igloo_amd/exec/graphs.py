@@ -35,7 +35,7 @@ Memory: each graph owns a private pool (its whole working set stays reserved
 between replays). The capture measures the pool's bytes and the engine charges
 them, together with the cache tier's resident columns, against its HBM budget
 (engine.py ``enforce_graph_budget``): past it, the least recently replayed
-graphs are dropped and their pools freed. ``IGLOO_GRAPH_SHARED_POOL=1`` shares
+graphs are dropped and their pools freed. ``SHARED_POOL = True`` shares
 one pool between all graphs of an engine instead.
 
 CDC: a replay never reaches ``CachedTable.scan``, so the engine polls the CDC
@@ -50,6 +50,7 @@ crates/engine/src/lib.rs:112-140). This is the HIP-graph half of SURVEY §5.7's
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import gc
 import logging
 import os
@@ -65,7 +66,7 @@ log = logging.getLogger("igloo.graphs")
 
 GRAPHS = os.environ.get("IGLOO_GRAPHS", "1") == "1"
 #: one memory pool for all graphs of an engine (0: a private pool per graph)
-SHARED_POOL = os.environ.get("IGLOO_GRAPH_SHARED_POOL", "0") == "1"
+SHARED_POOL = False
 
 _streams: dict = {}
 STATS = {"captured": 0, "replays": 0, "aborted": 0, "failed": 0, "mismatch": 0}
@@ -167,7 +168,7 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     # invalidating it inside the runtime
     sync_mode = torch.cuda.get_sync_debug_mode()
     torch.cuda.set_sync_debug_mode(2)
-    dump = os.environ.get("IGLOO_GRAPH_DUMP")     # debugging: DOT dump of every captured graph
+    dump = _sw.debug_value("graph_dump")     # debugging: DOT dump of every captured graph
     if dump:
         g.enable_debug_mode()
     # no cyclic garbage collection inside the capture: a collected object's

@@ -938,9 +938,9 @@ def _dense_lookup_ok(big: torch.Tensor, nq: int) -> bool:
 
 
 #: inner_pairs: sorted resident key columns with a dense index take the range path at any size ratio
-DENSE_JOIN = os.environ.get("IGLOO_DENSE_JOIN", "1") == "1"
+DENSE_JOIN = True
 #: HashJoinExec: [NOT] EXISTS against a filtered scan sorted on the key runs as an index nested loop
-SEMI_INDEX = os.environ.get("IGLOO_SEMI_INDEX", "1") == "1"
+SEMI_INDEX = True
 #: ... and the smaller side's sorted resident key column serves the bigger side's lookups
 DENSE_JOIN_SMALL = True
 
@@ -979,7 +979,8 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
         with ctx.span("join.sorted_search"):
             lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
-            if bvalid is None and UNIQUE_PAIRS and H.key_unique(big):
+            uniq = bvalid is None and UNIQUE_PAIRS and H.key_unique(big)
+            if uniq and UNIQUE_PAIRS_SORTED:
                 # (orders.o_orderkey searched by lineitem keys: one row each)
                 sidx, bidx = _unique_pairs(lo, cnt, small.numel(), big.numel(), identity_ok)
             else:
@@ -996,7 +997,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
         # the bigger side looks its key up (two reads) — no hash table is built
         with ctx.span("join.dense_lookup"):
             lo, cnt = H.sorted_ranges(small, big, bvalid)
-            if UNIQUE_PAIRS and H.key_unique(small):
+            if UNIQUE_PAIRS and UNIQUE_PAIRS_DENSE and H.key_unique(small):
                 bidx, sidx = _unique_pairs(lo, cnt, big.numel(), small.numel(), identity_ok)
             else:
                 bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
@@ -1049,12 +1050,12 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
 
 #: join a resident unsorted key column through its secondary index when the
 #: other side has at most 1/PERM_INDEX_RATIO of its rows
-PERM_INDEX = os.environ.get("IGLOO_PERM_INDEX", "1") == "1"
-PERM_INDEX_RATIO = int(os.environ.get("IGLOO_PERM_INDEX_RATIO", "32"))
-PERM_INDEX_MAX_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_MAX_FRAC", "20"))
+PERM_INDEX = True
+PERM_INDEX_RATIO = 32
+PERM_INDEX_MAX_FRAC = 20
 #: results up to 1/PERM_INDEX_SORT_FRAC of the column still take the index,
 #: sorted back into row order (above 1/PERM_INDEX_MAX_FRAC)
-PERM_INDEX_SORT_FRAC = int(os.environ.get("IGLOO_PERM_INDEX_SORT_FRAC", "8"))
+PERM_INDEX_SORT_FRAC = 8
 
 _INT_KEYS = ("int32", "int64")
 TWO_KEY_SORTED = True
@@ -1089,7 +1090,7 @@ def _two_key_sorted_pairs(A, B, on, ctx) -> Optional[Tuple[torch.Tensor, torch.T
         k2 = torch.int64 if torch.int64 in (b2.dtype, s2.dtype) else torch.int32
         with ctx.span("join.sorted_match"):
             sidx, bidx = H.sorted_match_pairs(b1.to(dt), b2.to(k2), s1.to(dt), s2.to(k2),
-                                              identity_ok=UNIQUE_PAIRS)
+                                              identity_ok=UNIQUE_PAIRS and UNIQUE_PAIRS_TWO_KEY)
         return (sidx, bidx) if big_right else (bidx, sidx)
     return None
 
@@ -1211,11 +1212,12 @@ class LateBatch(Batch):
 PRUNE_PARTS = True
 #: a search into unique keys pairs each query row with at most one row: no
 #: range expansion, and the identity when every row matches (inner_pairs)
-UNIQUE_PAIRS = os.environ.get("IGLOO_UNIQUE_PAIRS", "1") == "1"
+UNIQUE_PAIRS = True
+UNIQUE_PAIRS_SORTED = UNIQUE_PAIRS_DENSE = UNIQUE_PAIRS_TWO_KEY = True
 
 #: a filtered scan keeping at least this fraction of its table probes the
 #: table's key column under its filter mask instead of a gathered copy
-IN_PLACE_MIN_DENSITY = float(os.environ.get("IGLOO_IN_PLACE_DENSITY", "0.125"))
+IN_PLACE_MIN_DENSITY = 0.125
 #: ... and an unsorted key column (hash probe over every table row) when at
 #: least this fraction survives
 IN_PLACE_HASH_DENSITY = 0.4

@@ -44,9 +44,9 @@ import torch
 from ..columnar import Batch
 
 #: a morsel's scanned bytes are at most budget / MORSEL_FRACTION
-MORSEL_FRACTION = int(os.environ.get("IGLOO_MORSEL_FRACTION", "8"))
+MORSEL_FRACTION = 8
 #: stream a scan whose columns exceed budget / STREAM_FRACTION
-STREAM_FRACTION = int(os.environ.get("IGLOO_STREAM_FRACTION", "4"))
+STREAM_FRACTION = 4
 MORSEL_MIN_ROWS = 1 << 14
 #: bytes per row assumed for a string column without statistics
 STRING_ROW_BYTES = 40
@@ -125,8 +125,8 @@ def pick_stream_scan(agg, ctx):
     return best
 
 
-#: morsels prepared ahead of the one being processed (IGLOO_MORSEL_PREFETCH=0: serial)
-PREFETCH_DEPTH = int(os.environ.get("IGLOO_MORSEL_PREFETCH", "1"))
+#: morsels prepared ahead of the one being processed (0: serial)
+PREFETCH_DEPTH = 1
 
 
 def prefetched(gen, ctx):

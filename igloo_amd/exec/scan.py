@@ -41,9 +41,9 @@ NDV_DERIVED = True
 
 
 
-#: fused mask compaction of a filtered scan's columns (IGLOO_COMPACT=0: mask ->
+#: fused mask compaction of a filtered scan's columns (COMPACT = False: mask ->
 #: indices -> gather, the A/B baseline)
-COMPACT = os.environ.get("IGLOO_COMPACT", "1") != "0"
+COMPACT = True
 
 
 def _tag_base(col: Column, src: Column, n_src: int):

@@ -354,10 +354,30 @@ def _aggregate(w: WindowCall, b: Batch, st: _Sorted, lo, hi, ctx) -> Column:
     src = col.dtype
     if src.is_string and f in ("min", "max"):
         return _string_minmax(w, col, valid, st, lo, hi, read, ctx)
+    if f in ("sum", "avg") and (col.is_wide or (w.dtype.is_decimal and w.dtype.precision > 18)):
+        # exact 128-bit sums: three limb sums (32 + 32 + signed high word)
+        # with the int64 scans, recombined with carries
+        lo_w, hi_w = (col.data[:, 0], col.data[:, 1]) if col.is_wide else (col.data.to(torch.int64),
+                                                                            col.data.to(torch.int64) >> 63)
+        mask32 = 0xFFFFFFFF
+        limbs = [(lo_w & mask32).contiguous(), ((lo_w >> 32) & mask32).contiguous(), hi_w.contiguous()]
+        if read != "frame":
+            sums = [scan(x, W.V_I64, W.SUM_I) for x in limbs]
+        else:
+            sums = [W.frame_sum(prefix(x, W.V_I64, W.SUM_I), None, lo, hi, n)[0] for x in limbs]
+        s0, s1, s2 = sums
+        a0, a1 = s0 & mask32, s0 >> 32
+        mid = a1 + (s1 & mask32)
+        lo_r = a0 | ((mid & mask32) << 32)
+        hi_r = (mid >> 32) + (s1 >> 32) + s2
+        c = counts()
+        vv = c > 0
+        wide = torch.stack([lo_r, hi_r], 1).contiguous()
+        if f == "sum":
+            return Column(w.dtype, wide, vv)
+        return Column(w.dtype, _avg(wide, c, src, w.dtype), vv)
     if f in ("sum", "avg"):
         fl = src.is_float
-        if col.is_wide:
-            raise NotSupported("window sum over 128-bit decimals")
         vals = col.data.to(torch.float64) if fl else col.data
         if not fl and vals.dtype not in (torch.int32, torch.int64):
             vals = vals.to(torch.int64)
@@ -374,11 +394,27 @@ def _aggregate(w: WindowCall, b: Batch, st: _Sorted, lo, hi, ctx) -> Column:
             data = s if t.is_float else s.to(torch.int64)
             return Column(t, data, vv)
         return Column(w.dtype, _avg(s, c, src, w.dtype), vv)
+    if f in ("min", "max") and col.is_wide:
+        # 128-bit decimals: min / max of their ranks, mapped back to a value
+        from ..ops import sort as SO
+        hi_k = col.data[:, 1].contiguous()
+        lo_k = (col.data[:, 0] ^ (-(2**63))).contiguous()      # unsigned order of the low word
+        perm = SO.argsort([(hi_k, False, False, None), (lo_k, False, False, None)], n, dev).to(torch.int64)
+        ranks = torch.empty(n, dtype=torch.int64, device=dev)
+        ranks.scatter_(0, perm, torch.arange(n, dtype=torch.int64, device=dev))
+        is_max = f == "max"
+        op = W.MAX_I if is_max else W.MIN_I
+        if read != "frame":
+            r = scan(ranks, W.V_I64, op)
+            vv = counts() > 0
+        else:
+            r, vv = W.frame_minmax(ranks, valid, lo, hi, n, is_max)
+        src_rows = gather_tensor(perm, r.clamp(0, max(n - 1, 0)))
+        vals = gather_tensor(col.data, src_rows)
+        return Column(w.dtype, vals, vv)
     if f in ("min", "max", "bool_and", "bool_or"):
         is_max = f in ("max", "bool_or")
         fl = src.is_float
-        if col.is_wide:
-            raise NotSupported("window min/max over 128-bit decimals")
         vals = col.data.to(torch.float64) if fl else col.data.to(torch.int64)
         if read != "frame":
             op = (W.MAX_F if is_max else W.MIN_F) if fl else (W.MAX_I if is_max else W.MIN_I)
@@ -418,6 +454,8 @@ def _aggregate(w: WindowCall, b: Batch, st: _Sorted, lo, hi, ctx) -> Column:
 def _string_minmax(w, col: Column, valid, st: _Sorted, lo, hi, read, ctx) -> Column:  # noqa: C901
     """min / max over strings: on sort ranks, mapped back to a row holding the winner."""
     n, dev = st.n, st.dev
+    if not col.is_dict:
+        col = S.dict_encode(col)
     ranks = S.sort_ranks(col).to(torch.int64)
     is_max = w.func == "max"
     if read != "frame":
@@ -429,7 +467,7 @@ def _string_minmax(w, col: Column, valid, st: _Sorted, lo, hi, read, ctx) -> Col
         r, vv = W.frame_minmax(ranks, valid, lo, hi, n, is_max)
     # a row per rank value (any non-NULL row holding that rank carries the
     # same string; NULL rows scatter into a spare slot)
-    top = int(to_host_int(ranks.max())) + 1 if n else 0
+    top = len(col.dictionary)     # ranks lie in [0, dictionary size): no readback
     row_of = torch.zeros(top + 1, dtype=torch.int64, device=dev)
     slot = ranks if col.valid is None else torch.where(col.valid, ranks, torch.full_like(ranks, top))
     row_of.scatter_(0, slot, torch.arange(n, dtype=torch.int64, device=dev))

@@ -8,6 +8,7 @@ oracle for the GPU tests).
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import collections
 import os
 import sys
@@ -79,7 +80,7 @@ def idx_dtype(n: int) -> torch.dtype:
     return torch.int32 if n < 2**31 - 1 else torch.int64
 
 
-SYNC_CHECK = os.environ.get("IGLOO_SYNC_CHECK", "0") not in ("", "0")
+SYNC_CHECK = _sw.debug("sync_check")
 
 
 # ------------------------------------------------------------------ host readback
@@ -87,7 +88,7 @@ _SENTINEL = -0x5A5A5A5A5A5A5A5B
 _pinned = threading.local()
 # polled pinned readback: ~48 us less per sync in isolation (scripts/sync_bench.py) but no gain on the
 # SF100 suite (A/B 0.228 vs 0.226 s), so off by default
-FAST_READBACK = os.environ.get("IGLOO_FAST_READBACK", "0") == "1"
+FAST_READBACK = False
 
 
 def _pinned_buf(n: int) -> torch.Tensor:
@@ -255,7 +256,7 @@ class Speculation:
         exp = torch.tensor(self.expected, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
         self.checked = act.numel()
         ok = bool((act == exp).all().item())
-        if not ok and os.environ.get("IGLOO_SPEC_DEBUG"):
+        if not ok and _sw.debug("spec"):
             a, pos = act.tolist(), 0
             for (site, vals) in self.log[:self.pos]:
                 if vals is None:

@@ -9,6 +9,7 @@ CPU tensors use a sort + searchsorted reference implementation.
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import contextvars
 import os
 from typing import List, Optional, Sequence, Tuple
@@ -96,10 +97,10 @@ def key_range(keys: torch.Tensor, valid: Optional[torch.Tensor] = None) -> Optio
 BOUND_TRUST_ROWS = 1 << 20
 
 
-#: IGLOO_CHECK_KEY_TAGS=1 (the GPU test suite sets it): verify every
+#: IGLOO_DEBUG=key_tags (tests set CHECK_KEY_TAGS directly): verify every
 #: readback-free key fact (key_unique tags, key_bound intervals) against the
 #: data it describes, one readback each
-CHECK_KEY_TAGS = os.environ.get("IGLOO_CHECK_KEY_TAGS", "0") not in ("", "0")
+CHECK_KEY_TAGS = _sw.debug("key_tags")
 
 
 def _check_bound(keys: torch.Tensor, b: Tuple[int, int]) -> Tuple[int, int]:
@@ -137,7 +138,7 @@ UNIQUE_CHECK_MAX_ROWS = 1 << 27
 
 
 def _check_unique(keys: torch.Tensor, why: str) -> bool:
-    """IGLOO_CHECK_KEY_TAGS: a tag-derived uniqueness must hold on the data."""
+    """IGLOO_DEBUG=key_tags: a tag-derived uniqueness must hold on the data."""
     if CHECK_KEY_TAGS and keys.numel() > 1 and not capturing():
         n = keys.numel()
         u = torch.unique(keys.to(torch.int64)).numel()
@@ -471,7 +472,7 @@ def is_sorted(keys: torch.Tensor) -> bool:
     return r
 
 
-DENSE_INDEX = os.environ.get("IGLOO_DENSE_INDEX", "1") == "1"
+DENSE_INDEX = True
 DENSE_INDEX_MIN_QUERIES = 1 << 20   # below this a binary search per query is cheaper than building
 DENSE_INDEX_MAX_SPAN_RATIO = 4      # table entries per indexed row (orders: 1 of 4 key values used)
 

@@ -21,6 +21,7 @@ plan through Arrow compute kernels (reference crates/engine/src/lib.rs:55-56).
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import concurrent.futures as cf
 import hashlib
 import os
@@ -46,9 +47,9 @@ AOT_DIR = Path(os.environ.get("IGLOO_JIT_AOT", os.path.join(os.path.dirname(os.p
 #: with hiprtc on the build host -- no GPU needed -- so the code objects are
 #: our own build output, not checked-in binaries
 AOT_SOURCES = Path(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "jit_sources"))
-#: IGLOO_JIT_DUMP=<dir>: write every generated kernel's source there (how
+#: IGLOO_DEBUG=jit_dump=<dir>: write every generated kernel's source there (how
 #: AOT_SOURCES is recorded: scripts/gpu_run.sh jitsources)
-DUMP_DIR = os.environ.get("IGLOO_JIT_DUMP")
+DUMP_DIR = _sw.debug_value("jit_dump")
 
 _lock = threading.Lock()
 _kernels: Dict[str, "JitKernel"] = {}
@@ -147,7 +148,7 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
                     raise
             global _pool
             if _pool is None:
-                _pool = cf.ThreadPoolExecutor(max_workers=int(os.environ.get("IGLOO_JIT_THREADS", "2")),
+                _pool = cf.ThreadPoolExecutor(max_workers=2,
                                               thread_name_prefix="igloo-jit")
             _pending[key] = _pool.submit(_compile, src, name, key)
             _names[key] = name
@@ -162,7 +163,7 @@ def get(src: str, name: str, mode: Optional[str] = None) -> Optional[JitKernel]:
         except Exception as e:   # a generator bug must not take the query down: keep interpreting
             _failed[key] = str(e)
             STATS["failed"] += 1
-            if os.environ.get("IGLOO_JIT_DEBUG"):
+            if _sw.debug("jit"):
                 print(f"[jit] {name}: compile failed:\n{e}\n{src}", flush=True)
             return None
         return _load(code, name, key)

@@ -32,7 +32,7 @@ from ..columnar import Column
 from . import _lib
 from ._lib import launch, ptr, stream
 
-PACKED = os.environ.get("IGLOO_PACKED_GATHER", "1") == "1"
+PACKED = True
 #: fewer gathered rows than this: the per-column gather (launch-bound anyway)
 MIN_ROWS = 1 << 20
 #: an ascending index denser than this reads most lines of every column

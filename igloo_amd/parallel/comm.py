@@ -13,6 +13,7 @@ sizes, NDVs) are batched into one tiny all-reduce / all-gather.
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import datetime
 import os
 from typing import List, Optional, Sequence, Tuple
@@ -47,7 +48,7 @@ class Communicator:
         self.bytes_sent = 0
         self.calls = 0
         self.chunk_calls = 0     # of ``calls``: the 2nd.. chunks of pipelined exchanges (one logical exchange each)
-        self.trace = [] if os.environ.get("IGLOO_TRACE_COLLECTIVES") else None
+        self.trace = [] if _sw.debug("collectives") else None
 
     # ------------------------------------------------------------- lifecycle
     @staticmethod
@@ -113,7 +114,7 @@ class Communicator:
         return torch.as_tensor(x, dtype=dtype, device=self.wire)
 
     def _count(self):
-        """One collective issued (``calls``); IGLOO_TRACE_COLLECTIVES=1 also
+        """One collective issued (``calls``); IGLOO_DEBUG=collectives also
         records the engine call site that issued it (``trace``)."""
         self.calls += 1
         if self.trace is not None:

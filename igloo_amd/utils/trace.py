@@ -1,4 +1,4 @@
-"""roctx ranges for rocprofv3 timelines (``IGLOO_ROCTX=1``).
+"""roctx ranges for rocprofv3 timelines (``IGLOO_DEBUG=roctx``).
 
 Every physical operator's execution, every EXPLAIN-ANALYZE phase span and
 every query become named ranges in the marker trace
@@ -8,10 +8,11 @@ with the variable unset (the default) the hooks are a constant-False check.
 """
 from __future__ import annotations
 
+from ..utils import switches as _sw
 import ctypes
 import os
 
-ENABLED = os.environ.get("IGLOO_ROCTX", "0") == "1"
+ENABLED = _sw.debug("roctx")
 _lib = None
 
 

@@ -1,8 +1,9 @@
 #!/bin/bash
 # A/B of an on/off environment switch on the warm graphed SF100 suite, tables
 # in HBM, same box back to back (VALS, default 1 0 1 0):
-#   VAR=IGLOO_LIKE_DWORD QS=13 bash scripts/ab_env.sh -> gpurun_out/ab_$VAR.txt
-# (IGLOO_COMPACT, IGLOO_LIKE_DWORD, IGLOO_HAVING_SCAN, ... default on).
+#   VAR=IGLOO_DEBUG VALS="like_nodword none like_nodword none" QS=13 bash scripts/ab_env.sh
+#   -> gpurun_out/ab_$VAR.txt (IGLOO_DEBUG tokens: like_nodword, having_general, ff_mfma, ...;
+#   an unknown token such as "none" is the default path).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
 VAR=${VAR:?set VAR}

@@ -1,7 +1,7 @@
 """Time the fused sorted GROUP BY + HAVING kernels on a Q18-shaped input
 (SF100 lineitem: 600M sorted int32 l_orderkey, runs of 1..7 rows, int32
 quantities; HAVING sum(q) > 300 with COUNT(*) alongside): the streaming
-kernel (IGLOO_HAVING_SCAN=1) against the general one, in GB/s of keys +
+kernel against the general one (IGLOO_DEBUG=having_general), in GB/s of keys +
 values read.   python scripts/bench_having.py [--rows 600000000]"""
 import argparse
 import os
@@ -30,7 +30,8 @@ def main():
     specs = [("count", None, None), ("sum_int", vals, None)]
     gb = n * 8 / 1e9
     for env in ("1", "0"):
-        os.environ["IGLOO_HAVING_SCAN"] = env
+        # the C++ side reads IGLOO_DEBUG per call: having_general = the run-folding kernel
+        os.environ["IGLOO_DEBUG"] = "" if env == "1" else "having_general"
         got = A.sorted_having(keys, specs, 1, ">", 30000)
         m = got[0].numel() if got is not None else -1
         torch.cuda.synchronize()
@@ -39,7 +40,7 @@ def main():
             A.sorted_having(keys, specs, 1, ">", 30000)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) * 1e3 / a.reps
-        print(f"IGLOO_HAVING_SCAN={env}: rows={n} passing={m} {ms:.3f} ms/call (host sync included) "
+        print(f"streaming={env}: rows={n} passing={m} {ms:.3f} ms/call (host sync included) "
               f"{gb / ms * 1e3:.0f} GB/s", flush=True)
 
 

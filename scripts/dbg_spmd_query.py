@@ -36,6 +36,11 @@ def _worker(rank, world, port, out, q, env, thr, replicate):
             continue   # this low threshold left at its default
         m, name = k.split("_", 1)
         setattr(mods[m], name, v)
+    for item in filter(None, os.environ.get("DBG_SET", "").split(",")):
+        path, val = item.split("=")
+        mod, attr = path.rsplit(".", 1)
+        import importlib
+        setattr(importlib.import_module(mod), attr, type(getattr(importlib.import_module(mod), attr))(int(val)))
     comm = Communicator.init(backend="gloo", device=DEV, timeout_s=120)
     e = ig.QueryEngine(device=DEV, comm=comm)
     for name, t in datagen.generate(0.01, DEV, rank, world, replicate_dims=replicate).items():

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Kernel-level A/B of env-switchable scan paths (e.g. IGLOO_FF_JIT=0 vs 1,
-# IGLOO_FF_MFMA=0 vs 1) on the SF100 scan queries: rocprofv3 kernel trace of
+# Kernel-level A/B of env-switchable scan paths (e.g. IGLOO_JIT=off vs sync,
+# IGLOO_DEBUG=ff_mfma) on the SF100 scan queries: rocprofv3 kernel trace of
 # the timed steps per configuration, summarised by scripts/kernel_summary.py.
-# usage: bash scripts/ff_ab.sh "IGLOO_FF_JIT=0" "IGLOO_FF_JIT=1 IGLOO_JIT=sync"
+# usage: bash scripts/ff_ab.sh "IGLOO_JIT=off" "IGLOO_JIT=sync"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="$(pwd)"

@@ -50,6 +50,13 @@ def main():
     print(f"{'ms/step':>9} {'calls':>6} {'us/call':>9}  kernel")
     for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
         print(f"{t / 1e6 / a.steps:9.3f} {cnt[n] // a.steps:6d} {t / 1e3 / cnt[n]:9.1f}  {n}")
+    # idle time between consecutive kernels, by gap size: short gaps are the
+    # per-dispatch cost inside a graph / launch stream, long ones host work
+    gaps = [rows[i][0] - rows[i - 1][1] for i in range(1, len(rows))]
+    edges = [(0, 2e3), (2e3, 5e3), (5e3, 2e4), (2e4, 1e5), (1e5, 1e6), (1e6, 1e12)]
+    print("idle between kernels (ms/step by gap size):", "  ".join(
+        f"{lo / 1e3:g}-{hi / 1e3:g}us: {sum(g for g in gaps if lo <= g < hi) / 1e6 / a.steps:.2f} "
+        f"({sum(1 for g in gaps if lo <= g < hi) // a.steps})" for lo, hi in edges))
     if a.dispatches:
         print(f"\ndispatches matching {a.dispatches!r} (all timed steps, in order): us  grid  kernel")
         for r in rows:

@@ -14,10 +14,10 @@ export TMPDIR=/tmp
 R="$(pwd)"
 OUT="$R/gpurun_out/mfma_ab.txt"
 : > "$OUT"
-QS=${QS:-1,6} bash scripts/ff_ab.sh "IGLOO_FF_JIT=1" "IGLOO_FF_JIT=0 IGLOO_FF_MFMA=1" "IGLOO_FF_JIT=0 IGLOO_FF_MFMA=0" \
+QS=${QS:-1,6} bash scripts/ff_ab.sh "IGLOO_JIT=sync" "IGLOO_JIT=off IGLOO_DEBUG=ff_mfma" "IGLOO_JIT=off" \
   >> "$OUT" 2>&1 || exit 1
 i=0
-for cfg in "IGLOO_FF_JIT=1" "IGLOO_FF_JIT=0 IGLOO_FF_MFMA=1" "IGLOO_FF_JIT=0 IGLOO_FF_MFMA=0"; do
+for cfg in "IGLOO_JIT=sync" "IGLOO_JIT=off IGLOO_DEBUG=ff_mfma" "IGLOO_JIT=off"; do
   i=$((i+1))
   rm -rf "$R/gpurun_out/mfmapmc$i"
   env IGLOO_PROF_GAP=1 $cfg timeout -s KILL 300 rocprofv3 --kernel-trace \

@@ -1,11 +1,11 @@
 #!/bin/bash
 # rocprofv3 marker + kernel trace of a few warm SF10 queries with roctx ranges
-# per query / operator / phase (IGLOO_ROCTX=1); summarised per range name.
+# per query / operator / phase (IGLOO_DEBUG=roctx); summarised per range name.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="$(pwd)"
 rm -rf "$R/gpurun_out/roctx"
-IGLOO_ROCTX=1 IGLOO_PROF_GAP=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv \
+IGLOO_DEBUG=roctx IGLOO_PROF_GAP=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv \
   -d "$R/gpurun_out/roctx" -o run -- python3 "$R/bench.py" --sf ${SF:-10} --source hbm --queries ${QS:-3,5,9} \
   --steps 1 --warmup 2 > "$R/gpurun_out/roctx.log" 2>&1 || exit 1
 NQ=$(python3 -c "import sys; sys.path.insert(0, '$R'); from bench import parse_queries; print(len(parse_queries('${QS:-3,5,9}')))")

@@ -5,7 +5,7 @@
 # a pass each), merged per kernel by scripts/pmc_summary.py (bytes over the
 # summed kernel time, % of 8 TB/s; VALU / LDS / MFMA instructions per wave).
 #   SF=100 QS=1-22 [TAG=x] bash scripts/roofline.sh  -> gpurun_out/roofline[_x].txt
-# (environment switches pass through, e.g. IGLOO_FF_JIT=0 IGLOO_FF_MFMA=1 TAG=mfma)
+# (environment switches pass through, e.g. IGLOO_JIT=off IGLOO_DEBUG=ff_mfma TAG=mfma)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" && mkdir -p gpurun_out

@@ -7,7 +7,7 @@ bash scripts/build.sh
 python -m pytest tests -x -q -m "not gpu"
 if [ "${IGLOO_VALIDATE_SANITIZE:-0}" = "1" ]; then
   # host-side sanitizers only (no GPU ASan on this pool); builds a separate copy
-  IGLOO_SANITIZE=address,undefined python -m igloo_amd._build --force
+  IGLOO_DEBUG=sanitize=address+undefined python -m igloo_amd._build --force
   python -m igloo_amd._build --force
 fi
 echo "validate: ok"

@@ -95,7 +95,10 @@ def test_having_scan_kernel(monkeypatch, vdt, k64, shape, op, const):
     want = (starts[sel], [sums[sel] if s[0] == "sum_int" else cnt[sel] for s in specs])
     before = KERNEL_CALLS["sorted_having"]
     for env in ("1", "0") if vdt == "int32" else ("1",):     # int16 / int8: the streaming kernel only
-        monkeypatch.setenv("IGLOO_HAVING_SCAN", env)
+        if env == "1":
+            monkeypatch.delenv("IGLOO_DEBUG", raising=False)
+        else:
+            monkeypatch.setenv("IGLOO_DEBUG", "having_general")   # the run-folding kernel (C++ reads it per call)
         got = A.sorted_having(keys, specs, hidx, op, const)
         if got is None:
             assert env == "0"           # the general kernel gives up on the long runs

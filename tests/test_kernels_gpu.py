@@ -593,9 +593,9 @@ def test_like_dword_filter_every_alignment(gpu_device, monkeypatch):
                 "%requestsrequests%", "%special%special%"):
         ref = S.like(c, pat)
         before = KERNEL_CALLS["str_like_segments"]
-        monkeypatch.setenv("IGLOO_LIKE_DWORD", "1")
+        monkeypatch.delenv("IGLOO_DEBUG", raising=False)
         got = S.like(g, pat).cpu()
-        monkeypatch.setenv("IGLOO_LIKE_DWORD", "0")
+        monkeypatch.setenv("IGLOO_DEBUG", "like_nodword")
         old = S.like(g, pat).cpu()
         assert KERNEL_CALLS["str_like_segments"] == before + 2
         assert torch.equal(ref, got), pat

@@ -1,5 +1,5 @@
 """roctx ranges (utils/trace.py): operator / query ranges are pushed and popped
-in balance when IGLOO_ROCTX=1 (libroctx64 works without a GPU)."""
+in balance under IGLOO_DEBUG=roctx (libroctx64 works without a GPU)."""
 import pyarrow as pa
 
 
