@@ -51,6 +51,8 @@ ERRORS = {1: "malformed RLE/bit-packed stream", 2: "dictionary index out of rang
           7: "unsupported page encoding", 8: "NULL in a column whose statistics say it has none",
           9: "truncated page", 20: "not a zstd frame", 21: "zstd frame needs a dictionary",
           22: "malformed zstd stream", 23: "zstd size mismatch", 24: "malformed zstd entropy table"}
+#: batches whose positional reads run ahead of the batch being decoded
+READ_AHEAD = 2
 READ_THREADS = int(os.environ.get("IGLOO_PARQUET_READ_THREADS", str(min(16, os.cpu_count() or 8))))
 #: staged bytes per decode batch (pinned host buffer + one set of launches):
 #: small enough that the host reads batch i+1 while the GPU copies and
@@ -59,7 +61,11 @@ BATCH_BYTES = int(os.environ.get("IGLOO_PARQUET_BATCH_BYTES", str(256 << 20)))
 #: process-wide decode totals (bench.py reports parquet_decode_gbps from them):
 #: file bytes staged, decoded column bytes, seconds inside GpuParquetReader.read
 #: (positional reads + H2D + planning + device decode, up to the error-flag sync)
-TOTALS = {"file_bytes": 0, "out_bytes": 0, "seconds": 0.0, "pages": 0, "zstd_pages": 0, "columns": 0}
+#: cold-scan totals: file / output bytes, wall seconds of read(); read_s = positional-read
+#: time (read-ahead thread), read_wait_s = time the decode thread waited for a batch's
+#: reads, plan_s = host page planning
+TOTALS = {"file_bytes": 0, "out_bytes": 0, "seconds": 0.0, "pages": 0, "zstd_pages": 0, "columns": 0,
+          "read_s": 0.0, "read_wait_s": 0.0, "plan_s": 0.0}
 
 
 class FileMeta:
@@ -184,15 +190,30 @@ class GpuParquetReader:
                     rejected[name] = lay
                 else:
                     todo.append(lay)
-        batch, size = [], 0
+        batches, batch, size = [], [], 0
         for lay in todo:
             if batch and size + lay["bytes"] > BATCH_BYTES:
-                self._read_batch(N, batch, nrows, device, err, keep, st, out, rejected)
+                batches.append(batch)
                 batch, size = [], 0
             batch.append(lay)
             size += lay["bytes"]
         if batch:
-            self._read_batch(N, batch, nrows, device, err, keep, st, out, rejected)
+            batches.append(batch)
+        # pipeline: the positional reads of the next READ_AHEAD batches run on
+        # a host thread into their own pinned buffers while this thread plans,
+        # copies and launches the decode of the current one (the device work is
+        # asynchronous, so read k+1, H2D + decode k overlap)
+        if len(batches) > 1:
+            import concurrent.futures as cf
+            with cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="igloo-pq-read") as pool:
+                futs = [pool.submit(self._stage, N, b) for b in batches[:READ_AHEAD]]
+                for k, b in enumerate(batches):
+                    staged = futs[k].result()
+                    if k + READ_AHEAD < len(batches):
+                        futs.append(pool.submit(self._stage, N, batches[k + READ_AHEAD]))
+                    self._read_batch(N, b, nrows, device, err, keep, st, out, rejected, staged)
+        elif batches:
+            self._read_batch(N, batches[0], nrows, device, err, keep, st, out, rejected)
         if out:
             code = int(err.item())  # one sync for every column of the scan
             if code:
@@ -203,6 +224,9 @@ class GpuParquetReader:
         TOTALS["seconds"] += st["total_s"]
         TOTALS["pages"] += st["pages"]
         TOTALS["zstd_pages"] += st.get("zstd_pages", 0)
+        TOTALS["read_s"] += st["read_s"]
+        TOTALS["read_wait_s"] += st.get("read_wait_s", 0.0)
+        TOTALS["plan_s"] += st["plan_s"]
         TOTALS["columns"] += len(out)
         for c in out.values():
             TOTALS["out_bytes"] += c.data.numel() * c.data.element_size() + (
@@ -231,8 +255,9 @@ class GpuParquetReader:
         return {"name": name, "dt": dt, "leaf": leaf0, "conv": conv, "ranges": ranges, "bytes": total,
                 "may_null": may_null}
 
-    def _read_batch(self, N, batch, n, device, err, keep, st, out, rejected):
-        # ---- stage every column of the batch into one pinned buffer
+    def _stage(self, N, batch):
+        """Every column chunk of ``batch`` read into one pinned buffer
+        (thread-safe: called ahead of the batch on the read thread)."""
         base = 0
         for lay in batch:
             lay["base"] = base
@@ -246,7 +271,15 @@ class GpuParquetReader:
                 per_file.setdefault(fi, []).append((start, length, hp + lay["base"] + off))
         for fi, rs in per_file.items():
             N.pq_pread(self.files[fi], rs, READ_THREADS)
-        st["read_s"] += time.perf_counter() - t0
+        return host, base, time.perf_counter() - t0
+
+    def _read_batch(self, N, batch, n, device, err, keep, st, out, rejected, staged=None):
+        # ---- every column of the batch in one pinned buffer (read ahead on the pipeline thread)
+        tw = time.perf_counter()
+        host, base, read_s = staged if staged is not None else self._stage(N, batch)
+        hp = host.data_ptr()
+        st["read_s"] += read_s
+        st["read_wait_s"] = st.get("read_wait_s", 0.0) + (time.perf_counter() - tw)
         st["bytes"] += base
         st["batches"] += 1
         raw = torch.empty(base + 64, dtype=torch.uint8, device=device)

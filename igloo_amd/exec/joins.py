@@ -974,7 +974,7 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
         return z, z
     big_right = n_r >= n_l
     big, bvalid, small, svalid = (rk, rvalid, lk, lvalid) if big_right else (lk, lvalid, rk, rvalid)
-    if dev.type == "cuda" and big.numel() >= SORTED_JOIN_MIN_ROWS \
+    if (dev.type == "cuda" or SORTED_PATHS_ON_CPU) and big.numel() >= SORTED_JOIN_MIN_ROWS \
             and (4 * small.numel() <= big.numel() or _dense_lookup_ok(big, small.numel())) and H.is_sorted(big):
         with ctx.span("join.sorted_search"):
             lo, cnt = H.sorted_ranges(big, small, svalid)
@@ -1201,11 +1201,13 @@ class LateBatch(Batch):
                 out.update({k: bb.columns[k] for k in keys})
             else:
                 pending = [k for k in keys if k not in self._cache]
-                out.update({k: self._cache[k] for k in keys if k in self._cache})
-                if isinstance(bb, _LazyScanBatch):
-                    out.update(zip(pending, bb.take_rows(pending, idx)))
-                else:
-                    out.update(zip(pending, take_many([bb.columns[k] for k in pending], idx)))
+                got = dict(zip(pending, bb.take_rows(pending, idx) if isinstance(bb, _LazyScanBatch)
+                               else take_many([bb.columns[k] for k in pending], idx)))
+                # in the base batch's column order, whichever were gathered
+                # before: ranks whose caches differ (an identity join side on
+                # one rank, not on another) must still agree on the order an
+                # exchange packs the columns in
+                out.update({k: self._cache[k] if k in self._cache else got[k] for k in keys})
         return Batch(out, self._n, self.dist)
 
 
@@ -1214,6 +1216,8 @@ PRUNE_PARTS = True
 #: range expansion, and the identity when every row matches (inner_pairs)
 UNIQUE_PAIRS = True
 UNIQUE_PAIRS_SORTED = UNIQUE_PAIRS_DENSE = UNIQUE_PAIRS_TWO_KEY = True
+#: debugging: let CPU runs take inner_pairs' sorted-search path (GPU-only by cost)
+SORTED_PATHS_ON_CPU = False
 
 #: a filtered scan keeping at least this fraction of its table probes the
 #: table's key column under its filter mask instead of a gathered copy

@@ -212,7 +212,7 @@ def normalize_structure(b: Batch, comm, extra: Sequence[int] = ()) -> Batch:
     one shared code space. ONE all-gather carries every column's structure
     bits, every dictionary's content digest and the caller's ``extra`` ints
     (e.g. row counts); they come back as ``b.preamble[rank]``."""
-    keys = list(b.columns)
+    keys = wire_order(b)
     cols = [b.columns[k] for k in keys]
     _no_nested(cols)
     bits = [sum(int(f) << i for i, f in enumerate(_sig(c))) for c in cols]
@@ -389,7 +389,7 @@ def shuffle(b: Batch, key: torch.Tensor, ctx, key_cid=None, normalized: bool = F
         plan = ShufflePlan(b, key, W)
         plan.rmat = comm.all_to_all_matrix(plan.matrix())
     perm, send, bounds, sgath, sbytes, rmat = plan.perm, plan.send, plan.bounds, plan.sgath, plan.sbytes, plan.rmat
-    keys = list(b.columns)
+    keys = wire_order(b)
     cols = [b.columns[k] for k in keys]
     tensors, spec = _fixed_parts(cols)
     recv = [r[0] for r in rmat]
@@ -508,7 +508,7 @@ def local_slice(b: Batch, key: torch.Tensor, ctx, key_cid=None) -> Batch:
     if comm.world_size == 1:
         return Batch(dict(b.columns), b.num_rows, d)
     idx = mask_to_indices(M.partition_ids(key, comm.world_size) == comm.rank)
-    keys = list(b.columns)
+    keys = wire_order(b)
     cols = _take_many([b.columns[k] for k in keys], idx)
     return Batch(dict(zip(keys, cols)), idx.numel(), d)
 
@@ -570,7 +570,7 @@ def gather_all(b: Batch, ctx, max_rows: Optional[int] = None, normalized: bool =
     if comm is None or not comm.spmd or dist_of(b) == REPLICATED:
         return b if max_rows is None or b.num_rows <= max_rows else None
     b = materialized(b)
-    keys = list(b.columns)
+    keys = wire_order(b)
     # string byte counts ride along in the preamble (-1: not a plain string
     # here; same length on every rank)
     if normalized:
@@ -622,7 +622,7 @@ def gather_small(b: Batch, ctx, cap_rows: int) -> Batch:
         return b
     b = materialized(b)
     W = comm.world_size
-    keys = list(b.columns)
+    keys = wire_order(b)
     n = b.num_rows
     dev = ctx.device
     cap_s = cap_rows * SMALL_GATHER_STR_BYTES
@@ -1176,6 +1176,17 @@ def _local_domain(groups, pb: Batch, ranges: List[int]) -> int:
             span = len(c.dictionary) if c.is_dict else 2
         dom *= max(span, 1) + (1 if c.valid is not None else 0)
     return dom
+
+
+def wire_order(b: Batch) -> list:
+    """The order an exchange packs ``b``'s columns in: by column id, the same
+    on every rank -- a batch's dict order follows how its columns were built
+    (a join side taken as the identity on one rank keeps its gathered columns
+    first, exec/joins.py LateBatch), which ranks need not share."""
+    try:
+        return sorted(b.columns)
+    except TypeError:
+        return list(b.columns)
 
 
 def _with_validity(b: Batch) -> Batch:

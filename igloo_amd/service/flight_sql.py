@@ -149,12 +149,14 @@ def _opt_str(f: Dict[int, list], fno: int) -> Optional[str]:
 
 # ------------------------------------------------------- prepared statements
 def _placeholders(sql: str):
-    """Offsets of the ``?`` placeholders: outside string literals, quoted
+    """The placeholders as ``(offset, length, parameter index)``: ``?`` takes
+    the next index in order, ``$n`` (the DataFusion / PostgreSQL spelling)
+    names parameter n-1. Only outside string literals, quoted
     identifiers, ``--`` line comments and ``/* */`` block comments -- with
     the SQL tokenizer's quoting rules (csrc/sql/parser.cpp tokenize): a
     '...' literal escapes a quote by doubling it; "..." and `...`
     identifiers end at their first closing quote."""
-    i, n = 0, len(sql)
+    i, n, seq = 0, len(sql), 0
     while i < n:
         ch = sql[i]
         if ch == "'":
@@ -171,14 +173,22 @@ def _placeholders(sql: str):
         elif ch == "/" and sql.startswith("/*", i):
             j = sql.find("*/", i + 2)
             i = n if j == -1 else j + 2
+        elif ch == "?":
+            yield i, 1, seq
+            seq += 1
+            i += 1
+        elif ch == "$" and i + 1 < n and sql[i + 1].isdigit() and (i == 0 or not (sql[i - 1].isalnum() or sql[i - 1] == "_")):
+            j = i + 1
+            while j < n and sql[j].isdigit():
+                j += 1
+            yield i, j - i, int(sql[i + 1:j]) - 1
+            i = j
         else:
-            if ch == "?":
-                yield i
             i += 1
 
 
 def count_params(sql: str) -> int:
-    return sum(1 for _ in _placeholders(sql))
+    return max((k + 1 for _, _, k in _placeholders(sql)), default=0)
 
 
 def _literal(v) -> str:
@@ -206,15 +216,18 @@ def _literal(v) -> str:
 
 
 def bind_params(sql: str, values: Sequence) -> str:
-    """Substitute ``?`` placeholders with SQL literals of ``values``."""
+    """Substitute ``?`` / ``$n`` placeholders with SQL literals of ``values``."""
     pos = list(_placeholders(sql))
-    if len(pos) > len(values):
+    need = max((k + 1 for _, _, k in pos), default=0)
+    if need > len(values):
         raise ValueError(f"prepared statement has more parameters than the {len(values)} bound")
     out, last = [], 0
-    for k, p in enumerate(pos):
+    for p, ln, k in pos:
+        if k < 0:
+            raise ValueError("placeholder $0: parameters are numbered from $1")
         out.append(sql[last:p])
         out.append(_literal(values[k]))
-        last = p + 1
+        last = p + ln
     out.append(sql[last:])
     return "".join(out)
 

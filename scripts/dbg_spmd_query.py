@@ -41,6 +41,10 @@ def _worker(rank, world, port, out, q, env, thr, replicate):
         mod, attr = path.rsplit(".", 1)
         import importlib
         setattr(importlib.import_module(mod), attr, type(getattr(importlib.import_module(mod), attr))(int(val)))
+    if os.environ.get("DBG_TRUE_UNIQUE"):
+        # key_unique() from the data itself (lets the unique-pairs path run on CPU)
+        import torch
+        H.key_unique = lambda k: k.dim() == 1 and torch.unique(k).numel() == k.numel()
     comm = Communicator.init(backend="gloo", device=DEV, timeout_s=120)
     e = ig.QueryEngine(device=DEV, comm=comm)
     for name, t in datagen.generate(0.01, DEV, rank, world, replicate_dims=replicate).items():
@@ -75,6 +79,10 @@ def main():
             got = json.load(open(out))
         diff = oracle.rows_match([tuple(r) for r in got], exp)
         print(f"[{name}] rows={len(got)} diff={str(diff)[:600]}", flush=True)
+        if diff:
+            gs = {tuple(map(str, r)) for r in got}
+            es = {tuple(map(str, r)) for r in exp}
+            print(f"[{name}] missing {sorted(es - gs)[:5]} extra {sorted(gs - es)[:5]}", flush=True)
 
 
 if __name__ == "__main__":

@@ -44,6 +44,13 @@ def _worker(rank, world, port, out_path, sf, queries, device="cpu", low_threshol
         H.BLOOM_MIN_RATIO = 2
         SL.SLICE_MIN_ROWS = 1000
         SL.SLICE_MIXED_MIN_ROWS = 1000      # Q20 / Q22 slice partsupp / customer
+        if low_thresholds == "sorted" and device == "cpu":
+            # the GPU-only sorted-search join with its unique-key pairs (the
+            # identity side of a foreign-key join) on CPU ranks: key_unique()
+            # decided from the data, as resident-column tags do on the GPU
+            import torch
+            O.SORTED_PATHS_ON_CPU = True
+            H.key_unique = lambda k: k.dim() == 1 and torch.unique(k).numel() == k.numel()
     comm = Communicator.init(backend="gloo", device=device, timeout_s=120)
     e = ig.QueryEngine(device=device, comm=comm)
     for name, t in datagen.generate(sf, device, rank, world, replicate_dims=replicate_dims).items():
@@ -86,6 +93,7 @@ def run_distributed(world, con, device="cpu", low_thresholds=False, replicate_di
 
 @pytest.mark.parametrize("world,replicate_dims,low", [(2, True, False), (3, True, True), (2, False, False),
                                                       (3, False, False), (4, True, True), (4, False, True),
+                                                      (4, False, "sorted"),
                                                       (8, True, False), (8, True, True), (8, False, False)])
 def test_tpch_distributed_gloo(world, replicate_dims, low, tpch_cpu):
     """Both multi-rank layouts: replicated dimension tables with fact tables

@@ -170,6 +170,10 @@ def test_bind_params_negative_and_comments():
     assert FS.count_params("select `it's` = ? from t") == 1
     assert FS.count_params('select "a""b" = ?') == 1
     assert FS.count_params("select 'it''s ?' , ?") == 1
+    # $n placeholders (DataFusion's spelling) name their parameter; reuse is allowed
+    q = "select $2 - $1 as d, $2 as e, '$1' as s, a$1 from (select 1 as a$1) t"
+    assert FS.count_params(q) == 2
+    assert e.query(FS.bind_params(q, [3, 10])).to_pylist() == [{"d": 7, "e": 10, "s": "$1", "a$1": 1}]
 
 
 def test_statements():

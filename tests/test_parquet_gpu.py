@@ -248,3 +248,20 @@ def test_corrupt_delta_header_is_rejected(tmp_path, gpu_device):
     r = GpuParquetReader([path])
     with pytest.raises(ExecutionError):
         r.read([("a", T.INT64)], [(0, 0)], gpu_device)
+
+
+def test_pipelined_batches(tmp_path, gpu_device, monkeypatch):
+    """Many small batches: positional reads run ahead on the read thread
+    (READ_AHEAD batches) while earlier batches decode; results unchanged."""
+    from igloo_amd.connectors import gpu_parquet as G
+    monkeypatch.setattr(G, "BATCH_BYTES", 64 << 10)
+    t = _table(40000, seed=99)
+    path = str(tmp_path / "p.parquet")
+    pq.write_table(t, path, row_group_size=9000, compression="snappy", data_page_size=8192)
+    w0 = G.TOTALS["read_wait_s"]
+    _check(path, t, gpu_device)
+    r = GpuParquetReader([path])
+    r.read([(f.name, T.from_arrow_type(f.type)) for f in pq.read_schema(path)],
+           [(0, g) for g in range(len(r.metas[0].row_groups))], gpu_device)
+    assert r.last_stats["batches"] > 3, r.last_stats
+    assert G.TOTALS["read_wait_s"] >= w0
