@@ -183,6 +183,9 @@ def main():
             print(msg, file=sys.stderr, flush=True)
 
     qs = parse_queries(a.queries)
+    from igloo_amd.models.tpch import params as _params
+    # the spec's validation parameters, Q11's FRACTION scaled to the SF
+    SQL = {q: _params.validation(q, a.sf) for q in qs}
     load = {"source": a.source}
     t0 = time.perf_counter()
     if a.source == "parquet":
@@ -218,7 +221,7 @@ def main():
         modes = []
         for q in qs:
             tq = time.perf_counter()
-            r = eng.sql(queries.QUERIES[q])
+            r = eng.sql(SQL[q])
             m = eng.last_metrics.get("speculation")
             spec_modes[m] = spec_modes.get(m, 0) + 1
             modes.append(f"{q}:{_MODE_TAG.get(m, '-')}")
@@ -304,9 +307,8 @@ def main():
     # (TPC-H substitution parameters, models/tpch/params.py): nothing keyed
     # on the SQL text (plans, readbacks, graphs) applies
     from igloo_amd.exec import graphs as _graphs_mod
-    from igloo_amd.models.tpch import params as _params
     eager_s = adhoc_s = None
-    adhoc_streams, adhoc_readbacks, adhoc_modes = [], [], {}
+    adhoc_streams, adhoc_readbacks, adhoc_modes, adhoc_plans = [], [], {}, {}
     if a.eager_steps > 0:
         saved = _graphs_mod.GRAPHS
         _graphs_mod.GRAPHS = False
@@ -353,6 +355,8 @@ def main():
                 nrb += eng.last_metrics.get("readbacks", 0)
                 m = eng.last_metrics.get("speculation")
                 adhoc_modes[m] = adhoc_modes.get(m, 0) + 1
+                ps = eng.last_metrics.get("plan_source")
+                adhoc_plans[ps] = adhoc_plans.get(ps, 0) + 1
             barrier()
             adhoc_streams.append(time.perf_counter() - ts)
             adhoc_readbacks.append(nrb)
@@ -363,7 +367,8 @@ def main():
             adhoc_s = comm.allreduce_max_float(adhoc_s)
             adhoc_streams = [comm.allreduce_max_float(x) for x in adhoc_streams]
         log(f"[bench] ad-hoc (fresh substitution parameters): {adhoc_s:.4f}s per suite; per stream "
-            f"{[round(x, 4) for x in adhoc_streams]} s, blocking readbacks {adhoc_readbacks}, modes {adhoc_modes}")
+            f"{[round(x, 4) for x in adhoc_streams]} s, blocking readbacks {adhoc_readbacks}, modes {adhoc_modes}, "
+            f"plans {adhoc_plans}, templates {eng.template_stats}")
 
     # ---- verification (outside the timed region)
     mismatches = [(i, q) for i, res in enumerate(step_results) for q, t in res.items() if digest(t) != ref[q]]
@@ -375,7 +380,7 @@ def main():
             parquet_gen.register_dataset(ce, a.data_dir, a.sf, rank, world, lean=a.lean)
         else:
             datagen.register(ce, a.sf, lean=a.lean)
-        bad = [q for q in qs if digest(ce.sql(queries.QUERIES[q]).table) != ref[q]]
+        bad = [q for q in qs if digest(ce.sql(SQL[q]).table) != ref[q]]
         cpu_check = {"queries": len(qs), "mismatched": bad}
         if bad:
             log(f"[bench] CPU check mismatches: {bad}")
@@ -429,10 +434,13 @@ def main():
             "warm_graph_s": round(step_s, 4),
             "warm_eager_s": round(eager_s, 4) if eager_s is not None else None,
             "adhoc_s": round(adhoc_s, 4) if adhoc_s is not None else None,
-            # per ad-hoc stream: wall seconds and blocking host readbacks (the
-            # first stream's templates have seen only the validation statements)
+            # per ad-hoc stream: wall seconds and blocking host readbacks
             "adhoc_streams_s": [round(x, 4) for x in adhoc_streams],
             "adhoc_readbacks": adhoc_readbacks,
+            # how the fresh statements were planned: "template" = a verified
+            # statement template of the validation text (sql/template.py),
+            # "planned" = parse + bind + optimize
+            "adhoc_plans": adhoc_plans,
             "cold_s": round(cold_s, 4),
             # timed-step queries whose host readbacks were replayed and validated
             # on the device (engine.QueryEngine._execute_speculative)

@@ -23,6 +23,8 @@ from .columnar import Batch, Column
 from .exec.context import ExecContext
 from .exec.planner import create_physical_plan
 from .sql import parse
+from .utils import switches as _sw
+from .sql import template as TPL
 from .sql.binder import Binder, IdGen
 from .sql.logical import ColInfo, Plan, Project
 from .sql.optimizer import optimize
@@ -38,6 +40,10 @@ from .utils.log import get_logger
 #: session settings, so any DDL or SET invalidates
 PLAN_CACHE = True
 PLAN_CACHE_SIZE = 256
+#: statement templates (sql/template.py): fresh literal values reuse a
+#: verified bound + optimized plan of the same statement shape
+TEMPLATES = not _sw.debug("no_templates")
+TEMPLATE_CACHE_SIZE = 256
 #: replay the host readbacks of repeated queries over unchanged data (see
 #: QueryEngine._execute_speculative)
 SPECULATE = True
@@ -164,6 +170,9 @@ class QueryEngine:
         self.session: Dict[str, Any] = dict(config or {})
         # optimized logical plans by (SQL text, catalog version, session settings)
         self._plans: "collections.OrderedDict" = collections.OrderedDict()
+        # verified statement templates by (template text, catalog version, session settings)
+        self._templates: "collections.OrderedDict" = collections.OrderedDict()
+        self.template_stats = {"recorded": 0, "verified": 0, "rejected": 0, "instantiated": 0, "stale": 0}
         self._prepared: Dict[str, tuple] = {}    # PREPARE name -> (statement AST, parameter types)
         self._graph_pool = None
         self.graphs_disabled = False    # set after a capture the runtime refused (exec/graphs.py)
@@ -294,13 +303,27 @@ class QueryEngine:
             if hit is not None:
                 self._plans.move_to_end(key)
                 return self._exec_query(hit[0], hit[1], time.perf_counter(), cached=True, key=key)
+        lx = tkey = None
+        if key is not None and TEMPLATES:
+            t0 = time.perf_counter()
+            lx = TPL.lex(sql)
+            if lx is not None:
+                tkey = (lx.key,) + key[1:]
+                ent = self._templates.get(tkey)
+                if ent is not None and ent.verified and ent.matches(lx.texts):
+                    got = ent.instantiate(lx.texts, Binder.literal_of)
+                    if got is not None:
+                        self._templates.move_to_end(tkey)
+                        self.template_stats["instantiated"] += 1
+                        self._cache_plan(key, got)
+                        return self._exec_query(got[0], got[1], t0, key=key, planned="template")
+                    self.template_stats["stale"] += 1
         stmts = parse(sql)
         if key is not None and len(stmts) == 1 and stmts[0]["k"] == "query":
             t0 = time.perf_counter()
-            plan, names = self._plan_query(stmts[0])
-            self._plans[key] = (plan, names)
-            while len(self._plans) > PLAN_CACHE_SIZE:
-                self._plans.popitem(last=False)
+            got = self._record_template(sql, stmts[0], lx, tkey) if tkey is not None else None
+            plan, names = got if got is not None else self._plan_query(stmts[0])
+            self._cache_plan(key, (plan, names))
             return self._exec_query(plan, names, t0, key=key)
         if not stmts:
             raise PlanError("empty SQL statement")
@@ -558,6 +581,54 @@ class QueryEngine:
             raise NotSupported(f"STORED AS {fmt}")
         return QueryResult(pa.table({}), 0.0)
 
+    def _cache_plan(self, key, plan_names) -> None:
+        self._plans[key] = plan_names
+        while len(self._plans) > PLAN_CACHE_SIZE:
+            self._plans.popitem(last=False)
+
+    def _record_template(self, sql: str, st: dict, lx, tkey):
+        """Plan ``st`` while recording it as a statement template
+        (sql/template.py), verify the template against a plan of the same
+        statement with perturbed literals, and keep it when they agree.
+        Returns this statement's (plan, names) or None (plan it normally)."""
+        slots = TPL.annotate(st, lx)
+        if slots is None:
+            return None
+        try:
+            with TPL.recording() as rec:
+                bq = Binder(self.catalog, IdGen(), self.session).bind_query(st)
+                plan = optimize(bq.plan)
+        except IglooError:
+            raise
+        except Exception:       # noqa: BLE001 - recording failed: plan without a template
+            return None
+        ent = TPL.Template(plan, bq.names, lx, slots, rec)
+        own = ent.instantiate(lx.texts, Binder.literal_of)
+        if own is None:
+            return None
+        self.template_stats["recorded"] += 1
+        ptexts = TPL.perturb(lx.texts, lx.kinds, slots)
+        for s_ in ent.keyed:
+            ptexts[s_] = lx.texts[s_]
+        psql = TPL.render(sql, lx, ptexts)
+        ok = False
+        plx = TPL.lex(psql)
+        if ptexts != lx.texts and plx is not None and plx.key == lx.key:
+            try:
+                pst = parse(psql)
+                pbq = Binder(self.catalog, IdGen(), self.session).bind_query(pst[0])
+                pplan = optimize(pbq.plan)
+                inst = ent.instantiate(ptexts, Binder.literal_of)
+                ok = inst is not None and inst[1] == pbq.names and TPL.signature(inst[0]) == TPL.signature(pplan)
+            except Exception:   # noqa: BLE001 - the perturbed statement does not plan: unverified
+                ok = False
+        ent.verified = ok
+        self.template_stats["verified" if ok else "rejected"] += 1
+        self._templates[tkey] = ent
+        while len(self._templates) > TEMPLATE_CACHE_SIZE:
+            self._templates.popitem(last=False)
+        return own
+
     def _plan_query(self, st: dict):
         b = Binder(self.catalog, self._ids, self.session)
         bq = b.bind_query(st)
@@ -567,7 +638,7 @@ class QueryEngine:
         plan, names = self._plan_query(st)
         return self._exec_query(plan, names, t0)
 
-    def _exec_query(self, plan, names, t0: float, cached: bool = False, key=None) -> QueryResult:
+    def _exec_query(self, plan, names, t0: float, cached: bool = False, key=None, planned=None) -> QueryResult:
         """Execute an optimized logical plan. A cached plan is only the
         parse / bind / optimize output for the same SQL text, catalog version
         and session settings: every execution builds fresh physical operators
@@ -618,6 +689,7 @@ class QueryEngine:
         ms = (time.perf_counter() - t0) * 1e3
         self.last_metrics = {"elapsed_ms": ms, "rows": table.num_rows, "rows_scanned": ctx.rows_scanned,
                              "spill": dict(ctx.spill), "morsels": dict(ctx.morsels), "plan_cached": cached, "speculation": spec,
+                             "plan_source": "cache" if cached else (planned or "planned"),
                              # work that left the GPU (ops/_lib.py note_host_step)
                              "host_steps": sum(HOST_STEPS.values()) - h0,
                              # blocking device -> host readbacks (result copy excluded)

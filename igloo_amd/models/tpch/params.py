@@ -142,6 +142,18 @@ def query(q: int, rng: Optional[random.Random] = None, sf: float = 1.0) -> str:
     return sql
 
 
+def validation(q: int, sf: float = 1.0) -> str:
+    """Query ``q`` with the spec's validation parameters at scale factor
+    ``sf``: Q11's FRACTION is 0.0001 / SF (the validation text's 0.0001 is
+    the SF1 value; at SF100 it would select no rows)."""
+    from .queries import QUERIES
+    sql = QUERIES[q]
+    if q == 11 and sf != 1.0:
+        frac = f"{0.0001 / max(sf, 1e-9):.10f}".rstrip("0")
+        sql = sql.replace("* 0.0001", f"* {frac}")
+    return sql
+
+
 def stream(qs, seed: int, sf: float = 1.0) -> Dict[int, str]:
     """One query stream: every query of ``qs`` with its own parameters."""
     rng = random.Random(seed)

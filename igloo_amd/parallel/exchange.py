@@ -306,7 +306,7 @@ class ShufflePlan:
         n = key.numel()
         self.perm, self.send = M.hash_partition(key, W) if n else \
             (torch.zeros(0, dtype=torch.int32, device=key.device), [0] * W)
-        cols = [b.columns[k] for k in b.columns]
+        cols = [b.columns[k] for k in wire_order(b)]       # (positions j: the shuffle's column order)
         self.bounds = np.cumsum([0] + list(self.send)).tolist()
         self.sgath = {j: take(c, self.perm) for j, c in enumerate(cols) if c.is_plain_string}
         self.sbytes: List[List[int]] = []
@@ -345,7 +345,7 @@ class ShufflePlan:
         False when a string column is plain on some ranks and dictionary-
         coded on others (normalisation decoded it: byte counts unknown)."""
         ns = len(self.str_cols)
-        cols = [nb.columns[k] for k in nb.columns]
+        cols = [nb.columns[k] for k in wire_order(nb)]
         plain_now = [j for j in self.str_cols if cols[j].is_plain_string]
         if plain_now != list(self.sgath):
             return False

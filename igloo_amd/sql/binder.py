@@ -15,6 +15,7 @@ from decimal import Decimal
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from .. import types as T
+from . import template as TPL
 from ..types import BOOL, DATE32, FLOAT64, INT32, INT64, UTF8, DataType
 from ..utils.errors import NotSupported, PlanError, TableNotFound
 from .expr import (AGG_FUNCS, FRAME_KINDS, RANKING_FUNCS, VALUE_FUNCS, AggCall, BinOp, Case, Cast, ColRef, Expr,
@@ -472,7 +473,7 @@ class Binder:
         groups: List[Tuple[ColInfo, Expr]] = []
         gmap: Dict[str, ColRef] = {}
         for g in group_exprs:
-            key = g.sql()
+            key = TPL.eq_sql(g)
             if key in gmap:
                 continue
             name = g.name if isinstance(g, ColRef) else key
@@ -484,11 +485,11 @@ class Binder:
         for e in exprs:
             for x in walk(e):
                 if isinstance(x, AggCall):
-                    key = x.sql() + (f" FILTER {x.filter.sql()}" if x.filter is not None else "")
+                    key = TPL.eq_sql(x) + (f" FILTER {TPL.eq_sql(x.filter)}" if x.filter is not None else "")
                     if key not in amap:
                         if x.arg is not None and _contains_agg(x.arg):
                             raise PlanError("aggregate function calls cannot be nested")
-                        ci = ColInfo(self.ids(), x.sql(), x.dtype, x.func not in ("count", "approx_distinct"))
+                        ci = ColInfo(self.ids(), TPL.eq_sql(x), x.dtype, x.func not in ("count", "approx_distinct"))
                         aggs.append((ci, x))
                         amap[key] = ci.ref()
         gid_ref: Optional[ColRef] = None
@@ -536,9 +537,9 @@ class Binder:
 
         def rewrite(e: Expr) -> Expr:
             def fn(x):
-                k_ = x.sql()
+                k_ = TPL.eq_sql(x)
                 if isinstance(x, AggCall):
-                    return amap[k_ + (f" FILTER {x.filter.sql()}" if x.filter is not None else "")]
+                    return amap[k_ + (f" FILTER {TPL.eq_sql(x.filter)}" if x.filter is not None else "")]
                 if isinstance(x, Func) and x.name == "grouping":
                     return grouping_expr(x)
                 if k_ in gmap:
@@ -733,7 +734,7 @@ class Binder:
                 return Func("concat", [self._coerce(l, UTF8), self._coerce(r, UTF8)], UTF8)
             if op in ("~", "~*", "!~", "!~*"):
                 # POSIX regex match operators: regexp_like, '*' = case-insensitive
-                if not isinstance(r, Lit) or not isinstance(r.value, str):
+                if not isinstance(r, Lit) or not isinstance(TPL.peek(r), str):
                     raise NotSupported(f"{op}: the pattern must be a string literal")
                 e = self._func_library("regexp_like", [l, r, Lit("i" if op.endswith("*") else "", UTF8)])
                 return Not(e) if op.startswith("!") else e
@@ -743,10 +744,10 @@ class Binder:
             if node["s"] == "not":
                 self._require_bool(x, "NOT")
                 if isinstance(x, Lit):
-                    return Lit(None if x.value is None else (not x.value), BOOL)
+                    return TPL.derive(lambda a: Lit(None if a.value is None else (not a.value), BOOL), x)
                 return Not(x)
-            if isinstance(x, Lit) and x.value is not None:
-                return Lit(-x.value, x.dtype)
+            if isinstance(x, Lit) and TPL.peek(x) is not None:
+                return TPL.derive(lambda a: Lit(-a.value, a.dtype), x)
             return Neg(x, x.dtype)
         if k == "between":
             x = self.bind_expr(node["c"][0], scope, allow_agg)
@@ -769,12 +770,14 @@ class Binder:
         if k == "like":
             x = self.bind_expr(node["c"][0], scope, allow_agg)
             p = self.bind_expr(node["c"][1], scope, allow_agg)
-            if not isinstance(p, Lit) or not isinstance(p.value, str):
+            if not isinstance(p, Lit) or not isinstance(TPL.peek(p), str):
                 raise NotSupported("LIKE pattern must be a string literal")
             esc = "\\"
             if node.get("escape"):
                 esc = self.bind_expr(node["escape"], scope).value
-            return Like(self._coerce(x, UTF8), p.value, bool(node.get("neg")), bool(node.get("ilike")), esc)
+            e = Like(self._coerce(x, UTF8), TPL.peek(p), bool(node.get("neg")), bool(node.get("ilike")), esc)
+            TPL.raw(e, "pattern", lambda a: a.value, p)      # (a template re-reads the pattern)
+            return e
         if k == "similar":
             x = self.bind_expr(node["c"][0], scope, allow_agg)
             p = self.bind_expr(node["c"][1], scope, allow_agg)
@@ -829,6 +832,16 @@ class Binder:
 
     # ------------------------------------------------------------ literals
     def _literal(self, node) -> Lit:
+        x = self.literal_of(node)
+        slot = node.get("__slot")
+        if slot is not None and TPL.active():
+            # a literal token of a statement being recorded as a template (sql/template.py)
+            return TPL.SlotLit(x.value, x.dtype, slot)
+        return x
+
+    @staticmethod
+    def literal_of(node) -> Lit:
+        """The literal an AST literal node denotes."""
         t = node["type"]
         s = node["s"]
         if t == "int":
@@ -872,6 +885,8 @@ class Binder:
         return Cast(x, t)
 
     def _coerce_lit(self, v: Lit, t: DataType) -> Lit:
+        if TPL.tracking(v):
+            return TPL.derive(lambda a, t=t: self._coerce_lit(a, t), v)
         if v.dtype == t or v.value is None:
             return Lit(v.value, t) if v.value is None else v
         if t.is_string:
@@ -887,7 +902,7 @@ class Binder:
         if e.dtype == t:
             return e
         if isinstance(e, Lit):
-            return self._coerce_lit(e, t) if e.value is not None else Lit(None, t)
+            return self._coerce_lit(e, t) if TPL.peek(e) is not None else Lit(None, t)
         return Cast(e, t)
 
     def _cmp(self, op: str, l: Expr, r: Expr) -> Expr:
@@ -900,15 +915,15 @@ class Binder:
                 elif rt.kind == "timestamp" and lt.kind == "date32":
                     l = self._to_ts(l)
                 elif lt.kind == "date32" and rt.is_string:
-                    r = Lit(date_to_days(r.value), DATE32)
-                elif lt.is_string and not rt.is_string and r.value is not None:
+                    r = TPL.derive(lambda a: Lit(date_to_days(a.value), DATE32), r)
+                elif lt.is_string and not rt.is_string and TPL.peek(r) is not None:
                     r = _fold_cast(r, UTF8)
             elif isinstance(l, Lit) and not isinstance(r, Lit):
                 if rt.kind == "timestamp" and (lt.is_string or lt.kind == "date32"):
                     l = _fold_cast(l, T.TIMESTAMP)
                 elif rt.kind == "date32" and lt.is_string:
-                    l = Lit(date_to_days(l.value), DATE32)
-                elif rt.is_string and not lt.is_string and l.value is not None:
+                    l = TPL.derive(lambda a: Lit(date_to_days(a.value), DATE32), l)
+                elif rt.is_string and not lt.is_string and TPL.peek(l) is not None:
                     l = _fold_cast(l, UTF8)
             lt, rt = l.dtype, r.dtype
         if lt != rt:
@@ -919,6 +934,9 @@ class Binder:
         return _fold(BinOp(op, l, r, BOOL))
 
     def _arith(self, op: str, l: Expr, r: Expr) -> Expr:
+        if isinstance(l, Lit) and isinstance(r, Lit) and TPL.tracking(l, r):
+            # literal arithmetic (date +/- interval, folded numbers): re-derived per template instance
+            return TPL.derive(lambda a, b, op=op: self._arith(op, a, b), l, r)
         lt, rt = l.dtype, r.dtype
         # ---- DATE / INTERVAL arithmetic
         if lt == INTERVAL or rt == INTERVAL:
@@ -1922,6 +1940,8 @@ def _date_part_py(days: int, field: str) -> int:
 
 
 def _fold_cast(v: Lit, t: DataType) -> Lit:
+    if TPL.tracking(v):
+        return TPL.derive(lambda a, t=t: _fold_cast(a, t), v)
     x = v.value
     if x is None:
         return Lit(None, t)
@@ -1986,6 +2006,8 @@ def _fold(e: Expr) -> Expr:
     """Constant-fold binary operations on literals."""
     if not isinstance(e, BinOp) or not isinstance(e.left, Lit) or not isinstance(e.right, Lit):
         return e
+    if TPL.tracking(e.left, e.right):
+        return TPL.derive(lambda a, b, op=e.op, t=e.dtype: _fold(BinOp(op, a, b, t)), e.left, e.right)
     a, b = e.left.value, e.right.value
     op = e.op
     if op in ("and", "or"):

@@ -21,6 +21,7 @@ from typing import List, Optional, Set, Tuple
 
 from ..types import BOOL
 from ..utils.errors import NotSupported, PlanError
+from .template import eq_sql
 from .expr import (AggCall, BinOp, ColRef, Expr, Not, SubqueryExpr, and_all, col_refs, conjuncts, has_subquery,
                    replace_cols, transform, walk)
 from .logical import (Aggregate, ColInfo, Filter, Join, Limit, MultiJoin, Plan, Project, RecursiveCTE, Scan, SemiSpec,
@@ -258,11 +259,11 @@ def factor_or(e: Expr) -> List[Expr]:
         return [e]
     branches = _disjuncts(e)
     conj = [conjuncts(b) for b in branches]
-    common = [c for c in conj[0] if all(any(c.sql() == d.sql() for d in cs) for cs in conj[1:])]
+    common = [c for c in conj[0] if all(any(eq_sql(c) == eq_sql(d) for d in cs) for cs in conj[1:])]
     if not common:
         return [e]
-    keys = {c.sql() for c in common}
-    rest = [[c for c in cs if c.sql() not in keys] for cs in conj]
+    keys = {eq_sql(c) for c in common}
+    rest = [[c for c in cs if eq_sql(c) not in keys] for cs in conj]
     if any(not r for r in rest):
         return common  # one branch is exactly the common part: the OR is implied
     ors = and_all(rest[0])

@@ -45,7 +45,8 @@ def to_obj(x: Any) -> Any:
     if isinstance(x, bytes):
         return {"__bytes": x.hex()}
     if dataclasses.is_dataclass(x) and not isinstance(x, type):
-        name = type(x).__name__
+        # (a statement template's slot / derived literals serialize as literals)
+        name = "Lit" if isinstance(x, E.Lit) else type(x).__name__
         if name not in _CLASSES:
             raise TypeError(f"cannot serialize {name}")
         d = {"__c": name}

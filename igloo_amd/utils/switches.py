@@ -26,6 +26,8 @@ list of tokens (``token`` or ``token=value``), read by Python and C++ alike
 ``having_general``              sorted GROUP BY + HAVING on the run-folding kernel
                                 instead of the streaming scan (agg.hip)
 ``like_nodword``                LIKE without the aligned-dword prefilter (strings.hip)
+``no_templates``                plan every new statement text from scratch (no statement
+                                templates, sql/template.py)
 ==============================  =====================================================
 
 Other variables (each read in one place):

@@ -50,6 +50,14 @@ def _worker(rank, world, port, out, q, env, thr, replicate):
     for name, t in datagen.generate(0.01, DEV, rank, world, replicate_dims=replicate).items():
         e.register_table(name, t)
     rows = [[normalize(v) for v in r.values()] for r in e.sql(Q.QUERIES[q]).table.to_pylist()]
+    if os.environ.get("DBG_WARM"):
+        if comm.trace is not None:
+            comm.trace.clear()
+        e.sql(Q.QUERIES[q])
+        if rank == 0:
+            print("[warm] exchanges", e.last_metrics.get("exchanges"), "collectives", e.last_metrics.get("collectives"))
+            for t in (comm.trace or []):
+                print("   ", t)
     if rank == 0:
         json.dump(rows, open(out, "w"))
     comm.shutdown()

@@ -29,7 +29,7 @@ def main():
     import torch
     import igloo_amd as ig
     from igloo_amd.catalog import MemoryTable
-    from igloo_amd.models.tpch import datagen, queries
+    from igloo_amd.models.tpch import datagen, params
     from igloo_amd.utils.digest import digest
     qs = []
     for part in a.queries.split(","):
@@ -47,7 +47,7 @@ def main():
     print(f"[oracle] sf={a.sf} generated + copied in {time.perf_counter() - t0:.1f}s", flush=True)
     out = {"sf": a.sf, "queries": {}}
     for q in qs:
-        sql = queries.QUERIES[q]
+        sql = params.validation(q, a.sf)
         tg = time.perf_counter()
         rg = g.sql(sql).table
         tg = time.perf_counter() - tg

@@ -1,0 +1,118 @@
+"""Statement templates (sql/template.py): a statement that differs from an
+earlier one only in its literals reuses the earlier statement's verified plan
+with the new values -- and must return exactly what planning it from scratch
+returns. Every statement below runs on an engine with templates and on one
+planning every statement (``engine.TEMPLATES = False``); results must be
+identical, names included."""
+import pyarrow as pa
+import pytest
+
+import igloo_amd as ig
+from igloo_amd import engine as EN
+from igloo_amd.sql import template as TPL
+
+
+def _fresh(sql, eng):
+    saved = EN.TEMPLATES
+    EN.TEMPLATES = False
+    try:
+        return eng.sql(sql).table
+    finally:
+        EN.TEMPLATES = saved
+
+
+@pytest.fixture(scope="module")
+def engines():
+    t = pa.table({"a": pa.array([1, 2, 3, 4, 5, 6, 7, 8], pa.int64()),
+                  "b": pa.array([1, 1, 2, 2, 3, 3, None, 4], pa.int64()),
+                  "s": pa.array(["ab", "abc", "x'y", "b1", "zz", "a%", None, "AB"], pa.string()),
+                  "d": pa.array([8000, 8100, 8200, 8300, 8400, 8500, 8600, 8700], pa.date32()),
+                  "p": pa.array([1.25, 2.5, 10.75, 0.5, 3.0, 99.99, 7.5, 1.0], pa.float64())})
+    e = ig.QueryEngine(device="cpu")
+    e.register_table("t", t)
+    ref = ig.QueryEngine(device="cpu", catalog=e.catalog)
+    return e, ref
+
+
+def _check(e, ref, sql, source=None):
+    got = e.sql(sql).table
+    if source is not None:
+        assert e.last_metrics["plan_source"] == source, (sql, e.last_metrics["plan_source"])
+    want = _fresh(sql, ref)
+    assert got.column_names == want.column_names, sql
+    assert got.to_pylist() == want.to_pylist(), sql
+
+
+@pytest.mark.parametrize("first,then", [
+    ("select a, s from t where a > 2 and a < 7 order by a", ["select a, s from t where a > 4 and a < 6 order by a",
+                                                           "select a, s from t where a > 0 and a < 100 order by a"]),
+    # equal literals and then different ones (the plan may compare them)
+    ("select a from t where a >= 3 and b >= 3 order by a", ["select a from t where a >= 2 and b >= 3 order by a",
+                                                          "select a from t where a >= 1 and b >= 1 order by a"]),
+    ("select s from t where s like 'a%' order by s", ["select s from t where s like '%b%' order by s",
+                                                      "select s from t where s like 'x''%' order by s"]),
+    ("select a from t where d < date '1992-01-01' + interval '3' month order by a",
+     ["select a from t where d < date '1992-05-01' + interval '7' month order by a"]),
+    ("select a from t where p between 1.0 - 0.5 and 1.0 + 2.5 order by a",
+     ["select a from t where p between 2.0 - 0.5 and 9.0 + 2.5 order by a"]),
+    ("select b, count(*) c, sum(case when a > 4 then 1 else 0 end) k from t group by b order by b",
+     ["select b, count(*) c, sum(case when a > 6 then 1 else 2 end) k from t group by b order by b"]),
+    ("select a from t where s in ('ab', 'zz', 'b1') order by a", ["select a from t where s in ('abc', 'AB', 'x''y') order by a"]),
+    ("select a from t where a = -3 or a = 5 order by a", ["select a from t where a = -5 or a = 5 order by a"]),
+    # LIMIT counts are read while planning: a new count plans afresh
+    ("select a from t order by a limit 3", ["select a from t order by a limit 5"]),
+    # unaliased expressions name their columns after the literal
+    ("select a + 1, s from t where a < 3 order by a", ["select a + 2, s from t where a < 4 order by a"]),
+    # group key expressions matched by text
+    ("select a % 3, count(*) from t group by a % 3 order by 1", ["select a % 4, count(*) from t group by a % 4 order by 1"]),
+    ("select (a + 1) * 2 x from t where a = 1 + 1", ["select (a + 2) * 2 x from t where a = 2 + 1"]),
+])
+def test_template_instances_match_fresh_plans(engines, first, then):
+    e, ref = engines
+    _check(e, ref, first)
+    for sql in then:
+        _check(e, ref, sql)
+
+
+def test_templates_serve_fresh_literals(engines):
+    e, ref = engines
+    _check(e, ref, "select a, s from t where b = 2 and p > 1.5 order by a")
+    _check(e, ref, "select a, s from t where b = 3 and p > 0.5 order by a", source="template")
+    _check(e, ref, "/* 7 */ select a, s from t where b = 3 and p > 0.5 order by a")
+
+
+def test_lexer_token_classes():
+    lx = TPL.lex("select 'it''s', 3, 4.50, 1e3, \"c1\", x2 from t -- 9\nwhere y = 0.5 /* 6 */")
+    assert lx.texts == ["it's", "3", "4.50", "1e3", "0.5"]
+    assert lx.kinds == ["str", "int", "dec3,2", "float", "dec2,1"]
+    assert lx.key.count("?") == 5
+    # decimal shape is part of the template (it decides the literal's type)
+    assert TPL.lex("select 0.5").key != TPL.lex("select 10.55").key
+    assert TPL.lex("select 0.5").key == TPL.lex("select 0.7").key
+
+
+def test_perturbation_keeps_equality_pattern():
+    nodes = [{"type": "str"}] * 4 + [{"type": "int"}, {"type": "date"}]
+    texts = ["a9", "a8", "a9", "%x%", "41", "1994-12-31"]
+    out = TPL.perturb(texts, ["str", "str", "str", "str", "int", "str"], nodes)
+    assert out[0] == out[2] and out[0] != out[1] and out[3] == "%y%"
+    assert out[4] == "42" and out[5] == "1995-01-01"
+
+
+def test_tpch_streams_through_templates():
+    from igloo_amd.models.tpch import datagen, params
+    from igloo_amd.utils.digest import digest
+    e = ig.QueryEngine(device="cpu")
+    datagen.register(e, 0.01)
+    ref = ig.QueryEngine(device="cpu", catalog=e.catalog)
+    qs = list(range(1, 23))
+    for q in qs:
+        e.sql(params.validation(q, 0.01))
+    sources = {}
+    for seed in (3, 4):
+        for q, sql in params.stream(qs, seed, 0.01).items():
+            r = e.sql(sql).table
+            sources.setdefault(e.last_metrics["plan_source"], []).append(q)
+            assert digest(r) == digest(_fresh(sql, ref)), q
+    print(sources, e.template_stats)
+    assert len(sources.get("template", [])) >= 36, sources
