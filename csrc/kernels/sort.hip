@@ -172,7 +172,35 @@ __global__ __launch_bounds__(kBlock) void rs_scatter_kernel(const K* __restrict_
   }
 }
 
-// n <= kRsTile: every pass inside one workgroup, data stays in LDS/registers.
+// n <= kRsTile: one workgroup. The keys' OR and AND over the sorted bit
+// range show which 8-bit digits vary at all; passes over constant digits are
+// skipped (ORDER BY keys packed at full field width leave most high digits
+// constant). Up to kRankMax rows sort in one step instead: every item's
+// stable rank (keys below it + equal keys before it) from the keys in LDS.
+constexpr int kRankMax = 512;
+
+template <typename K>
+__device__ inline K bit_range_mask(int begin_bit, int end_bit) {
+  constexpr int kBits = 8 * (int)sizeof(K);
+  const K hi = end_bit >= kBits ? ~K(0) : ((K(1) << end_bit) - K(1));
+  const K lo = begin_bit <= 0 ? K(0) : ((K(1) << begin_bit) - K(1));
+  return hi & ~lo;
+}
+
+template <typename K>
+__device__ inline K wave_or(K v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v |= (K)__shfl_xor(v, off, kWave);
+  return v;
+}
+
+template <typename K>
+__device__ inline K wave_and(K v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v &= (K)__shfl_xor(v, off, kWave);
+  return v;
+}
+
 template <typename K, typename V>
 __global__ __launch_bounds__(kBlock) void rs_small_kernel(K* __restrict__ keys, V* __restrict__ vals, int64_t n,
                                                           int begin_bit, int end_bit) {
@@ -181,19 +209,82 @@ __global__ __launch_bounds__(kBlock) void rs_small_kernel(K* __restrict__ keys, 
   __shared__ int64_t scratch[kWavesPerBlock + 1];
   __shared__ K sk[kRsTile];
   __shared__ V sv[kRsTile];
+  __shared__ K red[2][kWavesPerBlock];
   const int w = threadIdx.x / kWave, lane = lane_id();
   const int wbase = w * kRsItems * kWave;
+  const K mask = bit_range_mask<K>(begin_bit, end_bit);
+  if (n <= kRankMax) {
+    // stable rank sort: stage the masked keys, rank every item against all of them
+    for (int i = threadIdx.x; i < n; i += kBlock) sk[i] = keys[i] & mask;
+    K mk[kRankMax / kBlock];
+    K fk[kRankMax / kBlock];
+    V fv[kRankMax / kBlock];
+    int64_t pos[kRankMax / kBlock];
+#pragma unroll
+    for (int j = 0; j < kRankMax / kBlock; ++j) {
+      const int i = threadIdx.x + j * kBlock;
+      if (i < n) {
+        fk[j] = keys[i];
+        fv[j] = vals[i];
+      }
+      pos[j] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRankMax / kBlock; ++j) mk[j] = sk[threadIdx.x + j * kBlock < n ? threadIdx.x + j * kBlock : 0];
+    for (int t = 0; t < n; ++t) {
+      const K o = sk[t];  // one address for the whole wave: an LDS broadcast
+#pragma unroll
+      for (int j = 0; j < kRankMax / kBlock; ++j) {
+        const int i = threadIdx.x + j * kBlock;
+        pos[j] += (o < mk[j]) || (o == mk[j] && t < i);
+      }
+    }
+    __syncthreads();  // every item was read before any is overwritten
+#pragma unroll
+    for (int j = 0; j < kRankMax / kBlock; ++j) {
+      const int i = threadIdx.x + j * kBlock;
+      if (i < n) {
+        keys[pos[j]] = fk[j];
+        vals[pos[j]] = fv[j];
+      }
+    }
+    return;
+  }
   K k[kRsItems];
   V v[kRsItems];
   bool ok[kRsItems];
+  K kor = K(0), kand = ~K(0);
 #pragma unroll
   for (int j = 0; j < kRsItems; ++j) {
     const int i = wbase + j * kWave + lane;
     ok[j] = i < n;
     k[j] = ok[j] ? keys[i] : K(0);
     v[j] = ok[j] ? vals[i] : V(0);
+    if (ok[j]) {
+      kor |= k[j];
+      kand &= k[j];
+    }
+  }
+  kor = wave_or(kor);
+  kand = wave_and(kand);
+  if (lane == 0) {
+    red[0][w] = kor;
+    red[1][w] = kand;
+  }
+  __syncthreads();
+  K diff = K(0);
+  {
+    K o = K(0), a = ~K(0);
+#pragma unroll
+    for (int x = 0; x < kWavesPerBlock; ++x) {
+      o |= red[0][x];
+      a &= red[1][x];
+    }
+    diff = (o ^ a) & mask;  // bits that differ between some two keys
   }
   for (int shift = begin_bit; shift < end_bit; shift += 8) {
+    if (((diff >> shift) & K(kRadix - 1)) == K(0)) continue;  // every key has the same digit here
     for (int i = threadIdx.x; i < kWavesPerBlock * kRadix; i += kBlock) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     int32_t r[kRsItems];

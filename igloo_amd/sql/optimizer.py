@@ -21,7 +21,7 @@ from typing import List, Optional, Set, Tuple
 
 from ..types import BOOL
 from ..utils.errors import NotSupported, PlanError
-from .template import eq_sql
+from .template import eq_sql, quiet_sql
 from .expr import (AggCall, BinOp, ColRef, Expr, Not, SubqueryExpr, and_all, col_refs, conjuncts, has_subquery,
                    replace_cols, transform, walk)
 from .logical import (Aggregate, ColInfo, Filter, Join, Limit, MultiJoin, Plan, Project, RecursiveCTE, Scan, SemiSpec,
@@ -259,11 +259,19 @@ def factor_or(e: Expr) -> List[Expr]:
         return [e]
     branches = _disjuncts(e)
     conj = [conjuncts(b) for b in branches]
-    common = [c for c in conj[0] if all(any(eq_sql(c) == eq_sql(d) for d in cs) for cs in conj[1:])]
+    texts = [[quiet_sql(c) for c in cs] for cs in conj]
+    common = [i for i, t in enumerate(texts[0]) if all(t in ts for ts in texts[1:])]
     if not common:
-        return [e]
-    keys = {eq_sql(c) for c in common}
-    rest = [[c for c in cs if eq_sql(c) not in keys] for cs in conj]
+        return [e]      # (for any literal values: leaving the OR as is stays correct)
+    keys = {texts[0][i] for i in common}
+    # what is factored out must stay equal in every instance of a statement
+    # template (sql/template.py eq_sql); other coincidences do not matter
+    for cs, ts in zip(conj, texts):
+        for c, t in zip(cs, ts):
+            if t in keys:
+                eq_sql(c)
+    rest = [[c for c, t in zip(cs, ts) if t not in keys] for cs, ts in zip(conj, texts)]
+    common = [conj[0][i] for i in common]
     if any(not r for r in rest):
         return common  # one branch is exactly the common part: the OR is implied
     ors = and_all(rest[0])

@@ -42,7 +42,16 @@ import threading
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
+from ..utils import switches as _sw
 from .expr import Lit
+
+#: IGLOO_DEBUG=templates: print why a template was not recorded, not verified or not instantiated
+DEBUG = _sw.debug("templates")
+
+
+def why(msg: str) -> None:
+    if DEBUG:
+        print(f"[template] {msg}", flush=True)
 
 # ------------------------------------------------------------------ lexing
 # one alternation, leftmost first: comments, quoted identifiers and string
@@ -160,12 +169,12 @@ class _Rec:
         self.raws: List[tuple] = []     # (obj, field name, fn, operand lits)
         self.quiet = 0
         self.eq = 0                     # inside eq_sql(): reads compare values for equality only
-        self.eq_objs: Dict[int, Any] = {}
+        self.mask: Optional[list] = None  # eq_sql's masked rendering: the tracked literals met, in order
+        # eq_sql calls: (text with tracked literals masked, those literals, full text)
+        self.eq_calls: List[Tuple[str, tuple, str]] = []
 
     def read(self, lit) -> None:
-        if self.eq:
-            self.eq_objs.setdefault(id(lit), lit)
-        else:
+        if not self.eq:
             self.reads.update(lit.leaves())
 
 
@@ -196,6 +205,13 @@ class SlotLit(Lit):
     def nullable(self) -> bool:  # a token is never NULL (NULL is a keyword)
         return False
 
+    def sql(self) -> str:
+        r = getattr(_TLS, "rec", None)
+        if r is not None and r.mask is not None:
+            r.mask.append(self)
+            return "\x00?"
+        return Lit.sql(self)
+
     def leaves(self):
         return (self.slot,)
 
@@ -225,6 +241,13 @@ class DerivedLit(Lit):
         finally:
             if r is not None:
                 r.quiet -= 1
+
+    def sql(self) -> str:
+        r = getattr(_TLS, "rec", None)
+        if r is not None and r.mask is not None:
+            r.mask.append(self)
+            return "\x00?"
+        return Lit.sql(self)
 
     def leaves(self):
         out = []
@@ -266,24 +289,49 @@ def derive(fn: Callable[..., Any], *args):
 
 
 def eq_sql(e) -> str:
-    """``e.sql()`` for a lookup or de-duplication by expression text: the
-    outcome depends only on which literals are equal, so the template
-    records that equality pattern (re-checked per instantiation) instead of
-    keying on the values. (Names built from the text keep the recorded
-    statement's literals: internal column names, not results.)"""
+    """``e.sql()`` for a lookup or de-duplication by expression text (equal
+    texts share one column, one aggregate, one factored-out predicate): the
+    template records which texts that differ only in literals were equal --
+    an instance must keep them equal -- instead of keying on the values.
+    (Names built from the text keep the recorded statement's literals:
+    internal column names, not results.)"""
     r = _rec()
     if r is None:
         return e.sql()
     r.eq += 1
     try:
-        return e.sql()
+        real = e.sql()
+        if r.mask is None:
+            r.mask = []
+            try:
+                masked = e.sql()
+                lits = tuple(r.mask)
+            finally:
+                r.mask = None
+            if lits:
+                r.eq_calls.append((masked, lits, real))
+        return real
     finally:
         r.eq -= 1
 
 
-def _eq_pattern(texts: List[str]) -> tuple:
-    first: Dict[str, int] = {}
-    return tuple(first.setdefault(t, i) for i, t in enumerate(texts))
+def quiet_sql(e) -> str:
+    """``e.sql()`` recording nothing: for decisions whose every outcome is
+    correct for any literal values (the caller records what must hold with
+    ``eq_sql``)."""
+    r = getattr(_TLS, "rec", None)
+    if r is None:
+        return e.sql()
+    r.quiet += 1
+    try:
+        return e.sql()
+    finally:
+        r.quiet -= 1
+
+
+def _partition(keys: list) -> tuple:
+    first: Dict[Any, int] = {}
+    return tuple(first.setdefault(k, i) for i, k in enumerate(keys))
 
 
 def peek(x):
@@ -375,8 +423,16 @@ class Template:
         self.keyed = {s: lx.texts[s] for s in sorted(set(rec.reads) | {i for i, n in enumerate(slot_nodes) if n is None})}
         self.raws = rec.raws
         raw_ids = {id(o) for o, _, _, _ in rec.raws}
-        self.eq_objs = list(rec.eq_objs.values())
-        self.eq_pattern = _eq_pattern([o.sql() for o in self.eq_objs])
+        # texts compared by eq_sql that differ only in literals: which of them
+        # were equal (every use shares, de-duplicates or factors equal texts)
+        groups: Dict[str, Dict[tuple, str]] = {}
+        for masked, lits, real in rec.eq_calls:
+            groups.setdefault(masked, {})[tuple(id(o) for o in lits)] = (lits, real)
+        self.eq_groups = []
+        for recs in groups.values():
+            if len(recs) > 1:
+                rs = list(recs.values())
+                self.eq_groups.append(([l for l, _ in rs], _partition([t for _, t in rs])))
         self.dirty, self._keep = _dirty_map((plan, names), raw_ids)
         self.verified = False
 
@@ -407,12 +463,12 @@ class Template:
                     base[s] = literal(node)
                 r = base[s]
                 if r.dtype != x.dtype:
-                    raise _Stale()
+                    raise _Stale(f"slot {s} type {r.dtype} != {x.dtype}")
             elif isinstance(x, DerivedLit):
                 r = x.fn(*[lit(a) if isinstance(a, _TRACKED) else a for a in x.args])
                 if not isinstance(r, Lit) or r.dtype != x.dtype or \
                         (r.value is None) != (object.__getattribute__(x, "value") is None):
-                    raise _Stale()
+                    raise _Stale(f"derived {getattr(r, 'dtype', r)} != {x.dtype}")
                 r = Lit(r.value, r.dtype) if type(r) is not Lit else r
             else:
                 r = x
@@ -443,12 +499,20 @@ class Template:
             return r
 
         try:
-            if self.eq_objs and _eq_pattern([lit(o).sql() for o in self.eq_objs]) != self.eq_pattern:
-                return None       # literals the plan compared for equality compare differently now
+            for lits_list, part in self.eq_groups:
+                # texts that were equal (shared, de-duplicated, factored out)
+                # must still be; texts that were distinct may coincide now --
+                # the plan then computes an equal thing twice
+                new = [tuple(lit(o).sql() for o in lits) for lits in lits_list]
+                if any(new[i] != new[p] for i, p in enumerate(part)):
+                    why(f"equal texts differ now: {new}")
+                    return None
             plan, names = sub((self.plan, self.names))
-        except _Stale:
+        except _Stale as ex:
+            why(f"stale derivation {ex}")
             return None
-        except Exception:       # noqa: BLE001 - a re-derivation failed: plan afresh
+        except Exception as ex:       # noqa: BLE001 - a re-derivation failed: plan afresh
+            why(f"re-derivation failed: {type(ex).__name__}: {ex}")
             return None
         return plan, names
 

@@ -204,3 +204,32 @@ def test_device_string_ranks_match_arrow_order():
     want = np.empty(len(vals), dtype=np.int64)
     want[order] = np.arange(len(vals))
     assert (got == want).all()
+
+
+@pytest.mark.parametrize("n", [2, 37, 256, 511, 512, 513, 1000, 4095, 4096])
+@pytest.mark.parametrize("kdt,bits", [(torch.int64, 64), (torch.int64, 40), (torch.int32, 32), (torch.int32, 12)])
+def test_small_sort_pairs_stable(gpu_device, n, kdt, bits):
+    """One-workgroup sorts (sort.hip rs_small_kernel): the rank sort up to
+    512 rows, radix passes over only the digits that vary above it; stable,
+    bits outside [begin_bit, end_bit) ignored. Oracle: numpy stable argsort."""
+    rng = np.random.default_rng(n * 7 + bits)
+    width = 64 if kdt == torch.int64 else 32
+    lo_bits = 4
+    # few distinct values in the sorted range (ties exercise stability), noise
+    # in the bits below begin_bit and constant high digits (skipped passes)
+    v = rng.integers(0, max(2, n // 3), n).astype(np.uint64) << np.uint64(lo_bits)
+    v |= rng.integers(0, 1 << lo_bits, n).astype(np.uint64)
+    if bits < width:
+        v &= np.uint64((1 << bits) - 1)
+    else:
+        v |= np.uint64(0x7000000000000000 if width == 64 else 0)
+    if width == 32:
+        v &= np.uint64(0xFFFFFFFF)
+    keys_np = v.astype(np.uint64).view(np.int64) if width == 64 else v.astype(np.uint32).view(np.int32)
+    vals_np = np.arange(n, dtype=np.int32)
+    k, vv = SO.sort_pairs(torch.from_numpy(keys_np.copy()).to(DEV), torch.from_numpy(vals_np).to(DEV), bits,
+                          begin_bit=lo_bits)
+    masked = (v >> np.uint64(lo_bits)).astype(np.uint64)
+    want = np.argsort(masked, kind="stable")
+    assert np.array_equal(vv.cpu().numpy(), vals_np[want])
+    assert np.array_equal(k.cpu().numpy(), keys_np[want])

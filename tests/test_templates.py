@@ -66,6 +66,12 @@ def _check(e, ref, sql, source=None):
     # group key expressions matched by text
     ("select a % 3, count(*) from t group by a % 3 order by 1", ["select a % 4, count(*) from t group by a % 4 order by 1"]),
     ("select (a + 1) * 2 x from t where a = 1 + 1", ["select (a + 2) * 2 x from t where a = 2 + 1"]),
+    # OR factoring (optimizer.factor_or): a factored-out conjunct must stay common
+    ("select a from t where (b = 1 and a > 1) or (b = 1 and a < 5) order by a",
+     ["select a from t where (b = 2 and a > 1) or (b = 3 and a < 5) order by a",
+      "select a from t where (b = 3 and a > 2) or (b = 3 and a < 6) order by a"]),
+    ("select a from t where (b = 1 and a > 1) or (b = 2 and a < 5) order by a",
+     ["select a from t where (b = 3 and a > 1) or (b = 3 and a < 5) order by a"]),
 ])
 def test_template_instances_match_fresh_plans(engines, first, then):
     e, ref = engines
