@@ -57,6 +57,20 @@ def main():
     print("idle between kernels (ms/step by gap size):", "  ".join(
         f"{lo / 1e3:g}-{hi / 1e3:g}us: {sum(g for g in gaps if lo <= g < hi) / 1e6 / a.steps:.2f} "
         f"({sum(1 for g in gaps if lo <= g < hi) // a.steps})" for lo, hi in edges))
+    # which kernel pairs the mid-size gaps (5-100 us: inside a query) sit
+    # between: a graph's non-kernel nodes (memset / memcpy) or a host
+    # readback between launches show up here
+    pairs = defaultdict(lambda: [0, 0])
+    for i in range(1, len(rows)):
+        g = rows[i][0] - rows[i - 1][1]
+        if 5e3 <= g < 1e5:
+            k = (short(rows[i - 1][2])[:48], short(rows[i][2])[:48])
+            pairs[k][0] += g
+            pairs[k][1] += 1
+    if pairs:
+        print("\nlargest 5-100 us gaps by kernel pair (ms/step, count/step): before -> after")
+        for (x, y), (g, c) in sorted(pairs.items(), key=lambda kv: -kv[1][0])[:25]:
+            print(f"{g / 1e6 / a.steps:7.3f} {c / a.steps:6.1f}  {x} -> {y}")
     if a.dispatches:
         print(f"\ndispatches matching {a.dispatches!r} (all timed steps, in order): us  grid  kernel")
         for r in rows:
