@@ -718,6 +718,15 @@ PYBIND11_MODULE(_native, m) {
     kern::dense_ranges(P<const void>(first), first64, kmin, kmax, P<const void>(q), key64, P<const uint8_t>(qvalid), nq,
                        P<int64_t>(lo), P<int64_t>(cnt), S(s));
   });
+  m.def("unique_lookup", [](uintptr_t big, bool key64, int64_t nb, uintptr_t first, bool first64, int64_t kmin,
+                            int64_t kmax, uintptr_t q, uintptr_t qvalid, int64_t nq, uintptr_t hit, uintptr_t pos,
+                            uintptr_t fence, int64_t nf, uintptr_t s) {
+    if (nq > 0 && (!q || !hit || !pos || (!first && !big))) throw std::runtime_error("unique_lookup: null buffer");
+    if (nb >= (int64_t{1} << 31)) throw std::runtime_error("unique_lookup: positions must fit int32");
+    kern::unique_lookup(P<const void>(big), key64, nb, P<const void>(first), first64, kmin, kmax, P<const void>(q),
+                        P<const uint8_t>(qvalid), nq, P<uint8_t>(hit), P<int32_t>(pos), P<const void>(fence), nf,
+                        S(s));
+  });
   m.def("key_histogram", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t n, int64_t kmin, int64_t span,
                             uintptr_t counts, uintptr_t s) {
     if (n > 0 && (!keys || !counts || span <= 0)) throw std::runtime_error("key_histogram: bad arguments");

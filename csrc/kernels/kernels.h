@@ -441,6 +441,11 @@ void dense_index_build(const void* big, bool key64, int64_t nb, int64_t kmin, in
                        int32_t* long_gap, hipStream_t stream);
 void dense_ranges(const void* first, bool first64, int64_t kmin, int64_t kmax, const void* q, bool key64,
                   const uint8_t* qvalid, int64_t nq, int64_t* lo, int64_t* cnt, hipStream_t stream);
+// probe keys into DISTINCT sorted keys (nb < 2^31): hit[i] 0/1 and pos[i] (int32 row, 0 on a miss);
+// first != null: through the dense lower-bound table, else a (fenced) binary search of big
+void unique_lookup(const void* big, bool key64, int64_t nb, const void* first, bool first64, int64_t kmin,
+                   int64_t kmax, const void* q, const uint8_t* qvalid, int64_t nq, uint8_t* hit, int32_t* pos,
+                   const void* fence, int64_t nf, hipStream_t stream);
 // hit[i] = exists k in [lo[i], lo[i]+cnt[i]) with big2[k] OP small2[i] (op: 0 =, 1 <>, 2 <, 3 <=, 4 >, 5 >=)
 void sorted_exists(const void* big2, const void* small2, bool key64, const int64_t* lo, const int64_t* cnt,
                    int64_t ns, int op, const uint8_t* mask, uint8_t* hit, hipStream_t stream);

@@ -124,8 +124,12 @@ def _d2h_packed(ts: List[torch.Tensor], dev) -> List[torch.Tensor]:
         return []
     pieces, spans, off = [], [], 0
     for t in ts:
-        b = t.contiguous().reshape(-1).view(torch.uint8) if t.dtype != torch.bool else \
-            t.contiguous().reshape(-1).view(torch.uint8)
+        b = t.reshape(-1)
+        if b.numel() <= 1:
+            b = b.as_strided((b.numel(),), (1,))     # (a one-element slice may carry any stride)
+        elif not b.is_contiguous():
+            b = b.contiguous()
+        b = b.view(torch.uint8)
         n = b.numel()
         pieces.append(b)
         spans.append((off, n, t.dtype, tuple(t.shape)))

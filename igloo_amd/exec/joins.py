@@ -945,21 +945,20 @@ SEMI_INDEX = True
 DENSE_JOIN_SMALL = True
 
 
-def _unique_pairs(lo: torch.Tensor, cnt: torch.Tensor, n: int, other_n: int, identity_ok: bool):
-    """Pairs of a range search whose searched column holds unique keys (every
-    range has 0 or 1 rows): (query rows with a match, their row in the
-    searched column). All n queries matching -- a foreign key into its
-    primary key, TPC-H's usual case -- gives the identity on the query side:
-    returned as None when ``identity_ok`` (the caller's index vectors then
-    stay as they are: no composition gather)."""
-    hit = cnt > 0
+def _unique_pairs(hit: torch.Tensor, pos: torch.Tensor, n: int, identity_ok: bool):
+    """Pairs of a search into unique keys (ops/hashing.py unique_lookup: a
+    hit flag and the int32 matching row per query): (query rows with a match,
+    their row in the searched column). All n queries matching -- a foreign
+    key into its primary key, TPC-H's usual case -- gives the identity on the
+    query side: returned as None when ``identity_ok`` (the caller's index
+    vectors then stay as they are: no composition gather)."""
     total = count_true(hit)
-    it = torch.int32 if max(n, other_n) < 2**31 - 1 else torch.int64
+    it = torch.int32 if n < 2**31 - 1 else torch.int64
     if total == n:
-        rows = None if identity_ok else torch.arange(n, dtype=it, device=lo.device)
-        return rows, lo.to(it)
+        rows = None if identity_ok else torch.arange(n, dtype=it, device=pos.device)
+        return rows, pos.to(it)
     rows = mask_to_indices(hit, total)
-    return rows, gather_tensor(lo, rows).to(it)
+    return rows, gather_tensor(pos, rows).to(it)
 
 
 def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
@@ -977,12 +976,14 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
     if (dev.type == "cuda" or SORTED_PATHS_ON_CPU) and big.numel() >= SORTED_JOIN_MIN_ROWS \
             and (4 * small.numel() <= big.numel() or _dense_lookup_ok(big, small.numel())) and H.is_sorted(big):
         with ctx.span("join.sorted_search"):
-            lo, cnt = H.sorted_ranges(big, small, svalid)
+            # (orders.o_orderkey searched by lineitem keys: one row each)
+            got = H.unique_lookup(big, small, svalid) \
+                if bvalid is None and UNIQUE_PAIRS and UNIQUE_PAIRS_SORTED and H.key_unique(big) else None
+            if got is None:
+                lo, cnt = H.sorted_ranges(big, small, svalid)
         with ctx.span("join.sorted_expand"):
-            uniq = bvalid is None and UNIQUE_PAIRS and H.key_unique(big)
-            if uniq and UNIQUE_PAIRS_SORTED:
-                # (orders.o_orderkey searched by lineitem keys: one row each)
-                sidx, bidx = _unique_pairs(lo, cnt, small.numel(), big.numel(), identity_ok)
+            if got is not None:
+                sidx, bidx = _unique_pairs(got[0], got[1], small.numel(), identity_ok)
             else:
                 # a big side with NULLs or probed in place under its filter
                 # mask (MultiJoinExec._late_join): only its set rows pair up
@@ -996,10 +997,12 @@ def inner_pairs(lk, rk, lvalid, rvalid, ctx, identity_ok: bool = False):
         # (customer.c_custkey against 22.7M filtered orders in Q5): every row of
         # the bigger side looks its key up (two reads) — no hash table is built
         with ctx.span("join.dense_lookup"):
-            lo, cnt = H.sorted_ranges(small, big, bvalid)
-            if UNIQUE_PAIRS and UNIQUE_PAIRS_DENSE and H.key_unique(small):
-                bidx, sidx = _unique_pairs(lo, cnt, big.numel(), small.numel(), identity_ok)
+            got = H.unique_lookup(small, big, bvalid) \
+                if UNIQUE_PAIRS and UNIQUE_PAIRS_DENSE and H.key_unique(small) else None
+            if got is not None:
+                bidx, sidx = _unique_pairs(got[0], got[1], big.numel(), identity_ok)
             else:
+                lo, cnt = H.sorted_ranges(small, big, bvalid)
                 bidx, sidx = H.expand_ranges(lo, cnt, small.numel())
         return (sidx, bidx) if big_right else (bidx, sidx)
     if dev.type == "cuda" and PERM_INDEX and bvalid is None and getattr(big, "_igloo_resident", False) \

@@ -584,6 +584,43 @@ def sorted_ranges(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Ten
     return lo, cnt
 
 
+def unique_lookup(big: torch.Tensor, q: torch.Tensor, qvalid: Optional[torch.Tensor] = None
+                  ) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """``sorted_ranges`` into DISTINCT sorted keys (``key_unique(big)``):
+    (hit bool mask, int32 row in ``big``; 0 on a miss) per probe key. None
+    when ``big`` has 2^31 rows or more (the caller takes ``sorted_ranges``).
+    GPU: one kernel writing 5 bytes per probe row (csrc/kernels/ranges.hip
+    unique_lookup) through the dense index when the column has one."""
+    big = _keys_ok(big)
+    nb = big.numel()
+    if nb >= 2**31 - 1:
+        return None
+    q = q.to(big.dtype).contiguous()
+    nq = q.numel()
+    if not is_gpu(big):
+        lo = torch.searchsorted(big, q)
+        hit = lo < nb
+        if nb:
+            hit &= big[lo.clamp(max=nb - 1)] == q
+        if qvalid is not None:
+            hit &= qvalid
+        return hit, torch.where(hit, lo, torch.zeros_like(lo)).to(torch.int32)
+    hit = torch.empty(nq, dtype=torch.bool, device=big.device)
+    pos = torch.empty(nq, dtype=torch.int32, device=big.device)
+    qv = ptr(qvalid.contiguous()) if qvalid is not None else 0
+    idx = dense_index(big, build=nq >= DENSE_INDEX_MIN_QUERIES, queries=nq) if DENSE_INDEX else None
+    N = launch("unique_lookup")
+    if idx:
+        kmin, kmax, first = idx
+        N.unique_lookup(0, big.dtype == torch.int64, nb, ptr(first), first.dtype == torch.int64, kmin, kmax, ptr(q),
+                        qv, nq, ptr(hit), ptr(pos), 0, 0, stream(big))
+    else:
+        fence = search_fence(big) if SEARCH_FENCE else None
+        N.unique_lookup(ptr(big), big.dtype == torch.int64, nb, 0, False, 0, 0, ptr(q), qv, nq, ptr(hit), ptr(pos),
+                        ptr(fence), 0 if fence is None else fence.numel(), stream(big))
+    return hit, pos
+
+
 SEARCH_FENCE = True
 SEARCH_FENCE_MIN_ROWS = 1 << 22
 

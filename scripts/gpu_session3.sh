@@ -1,7 +1,7 @@
 # full GPU suite, then the driver-config bench (SF100 Parquet) and a kernel trace with gap pairs
 cd /root/repo && export TMPDIR=/tmp
 out=gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $out/s3_pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $out/s3_pytest_gpu.log 2>&1 || exit $?
 timeout -k 10 900 python3 -u bench.py --steps 20 --warmup 5 --per-query > $out/s3_bench_sf100.log 2>&1 || exit $?
 IGLOO_PROF_GAP=1 timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $out/s3_trace -o run -- \
     python3 bench.py --source hbm --steps 3 --warmup 4 --eager-steps 0 --vary-params 0 > $out/s3_trace.log 2>&1 || exit $?

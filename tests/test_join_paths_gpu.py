@@ -8,6 +8,7 @@ reference exactly (order-insensitive)."""
 import numpy as np
 import pyarrow as pa
 import pytest
+import torch
 
 import igloo_amd as ig
 from igloo_amd.exec import joins as J
@@ -233,3 +234,32 @@ def test_in_place_exists_side(gpu_device, monkeypatch):
         monkeypatch.setattr(J, "IN_PLACE_MIN_DENSITY", 0.125)
         assert digest(e.query(queries.QUERIES[q] + " ")) == want, q
     assert J.IN_PLACE_STATS["semis"] > s0
+
+
+@pytest.mark.parametrize("kdt", [torch.int32, torch.int64])
+@pytest.mark.parametrize("nb,dense,nulls", [(1000, False, False), (300_000, True, True), (300_000, False, True),
+                                            (5_000_000, False, False), (5_000_000, True, False)])
+def test_unique_lookup_matches_searchsorted(gpu_device, kdt, nb, dense, nulls, monkeypatch):
+    """ops/hashing.py unique_lookup (ranges.hip unique_lookup: dense table or
+    fenced binary search) against numpy searchsorted over distinct sorted keys."""
+    rng = np.random.default_rng(nb + (7 if dense else 0))
+    step = 1 if dense else 5
+    keys = np.unique(rng.integers(0, nb * step * 2, nb)).astype(np.int64)
+    q = rng.integers(-5, nb * step * 2 + 5, 3 * nb).astype(np.int64)
+    qv = rng.random(q.size) > 0.1 if nulls else None
+    big = torch.from_numpy(keys).to(kdt).to(gpu_device)
+    if dense:
+        monkeypatch.setattr(H, "DENSE_INDEX_MIN_QUERIES", 1)
+    else:
+        monkeypatch.setattr(H, "DENSE_INDEX", False)
+    if nb >= 4_000_000:
+        big._igloo_resident = True          # (the fence serves resident columns)
+    hit, pos = H.unique_lookup(big, torch.from_numpy(q).to(kdt).to(gpu_device),
+                               None if qv is None else torch.from_numpy(qv).to(gpu_device))
+    lo = np.searchsorted(keys, q)
+    want = (lo < keys.size) & (keys[np.minimum(lo, keys.size - 1)] == q)
+    if qv is not None:
+        want &= qv
+    assert np.array_equal(hit.cpu().numpy(), want)
+    assert np.array_equal(pos.cpu().numpy(), np.where(want, lo, 0))
+    assert pos.dtype == torch.int32
