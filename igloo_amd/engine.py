@@ -115,13 +115,18 @@ class _ReplayMismatch(Exception):
 _PAD = {}
 
 
-def _d2h_packed(ts: List[torch.Tensor], dev) -> List[torch.Tensor]:
-    """Host copies of the device tensors ``ts`` through one byte
-    concatenation (one kernel; each piece padded to 16 bytes) and one
-    non-blocking copy into pinned memory. The caller synchronises before
-    reading them."""
-    if not ts:
-        return []
+def _pad(dev, n: int) -> torch.Tensor:
+    """n (< 16) zero bytes on ``dev`` (made outside any graph capture)."""
+    z = _PAD.get(dev)
+    if z is None:
+        z = _PAD[dev] = torch.zeros(16, dtype=torch.uint8, device=dev)
+    return z[:n]
+
+
+def _device_pack(ts: List[torch.Tensor], dev):
+    """The device tensors ``ts`` as ONE byte buffer (one concatenation
+    kernel; each piece padded to 16 bytes) and their (offset, bytes, dtype,
+    shape) spans in it."""
     pieces, spans, off = [], [], 0
     for t in ts:
         b = t.reshape(-1)
@@ -135,33 +140,36 @@ def _d2h_packed(ts: List[torch.Tensor], dev) -> List[torch.Tensor]:
         spans.append((off, n, t.dtype, tuple(t.shape)))
         pad = (-n) % 16
         if pad:
-            z = _PAD.get((dev, pad))
-            if z is None:
-                z = _PAD[(dev, pad)] = torch.zeros(pad, dtype=torch.uint8, device=dev)
-            pieces.append(z)
+            pieces.append(_pad(dev, pad))
         off += n + pad
-    buf = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+    return (torch.cat(pieces) if len(pieces) > 1 else pieces[0]), spans
+
+
+def _pinned_copy(buf: torch.Tensor, spans) -> List[torch.Tensor]:
+    """One non-blocking copy of ``buf`` into pinned memory, split into the
+    tensors of ``spans`` (the caller synchronises before reading them)."""
     host = torch.empty(buf.numel(), dtype=torch.uint8, pin_memory=True)
     host.copy_(buf, non_blocking=True)
     return [host[o:o + n].view(dt).reshape(shape) for o, n, dt, shape in spans]
 
 
-def _host_columns(cols: List[Column], deferred=None, guard=None) -> List[Column]:
-    """Result columns moved to the host with ONE synchronisation: every device
-    buffer (values, validity, offsets, small dictionaries) is copied with a
-    non-blocking D2H copy, then the stream is synchronised once (instead of a
-    blocking copy per buffer inside ``Column.to_arrow``). A string column that
-    references a large device dictionary keeps its device path (it decodes
-    only the referenced strings on the GPU)."""
-    if not any(c.data.is_cuda for c in cols):
-        if guard is not None and int(guard.reshape(-1)[0].item()):
-            raise _ReplayMismatch()
-        if deferred is not None:
-            _raise_deferred(deferred, deferred[0].tolist())
-        return cols
+class ResultPack:
+    """A query graph's result buffers concatenated INSIDE the graph (captured
+    with it, engine.py _result_layout order): a replay ends with the packed
+    buffer written, and only its one D2H copy follows."""
+    __slots__ = ("buf", "spans", "sig")
 
-    # every buffer travels in ONE device-side concatenation and ONE D2H copy
-    # (a copy per buffer costs ~18 us of host submission each, with the GPU idle)
+    def __init__(self, buf, spans, sig):
+        self.buf, self.spans, self.sig = buf, spans, sig
+
+
+def _sig(ts: List[torch.Tensor]) -> tuple:
+    return tuple((t.data_ptr(), t.numel(), t.dtype) for t in ts)
+
+
+def _result_layout(cols: List[Column], deferred=None, guard=None):
+    """How a result goes to the host: (per-column plan, device tensors to
+    copy in order, index of the deferred flags, index of the guard)."""
     pending: List[torch.Tensor] = []
 
     def cpu(t):
@@ -180,8 +188,43 @@ def _host_columns(cols: List[Column], deferred=None, guard=None) -> List[Column]
     plan = [move(c) for c in cols]
     fi = cpu(deferred[0]) if deferred is not None else None
     gi = cpu(guard.reshape(-1)[:1]) if guard is not None else None
+    return plan, pending, fi, gi
+
+
+def result_prepack(cols: List[Column], deferred, guard) -> Optional[ResultPack]:
+    """The packing of ``_host_columns`` for a result in a graph being
+    captured (called inside the capture: the concatenation is recorded)."""
+    if not any(c.data.is_cuda for c in cols):
+        return None
+    _, pending, _, _ = _result_layout(cols, deferred, guard)
+    if not pending:
+        return None
+    buf, spans = _device_pack(pending, pending[0].device)
+    return ResultPack(buf, spans, _sig(pending))
+
+
+def _host_columns(cols: List[Column], deferred=None, guard=None, prepack: Optional[ResultPack] = None) -> List[Column]:
+    """Result columns moved to the host with ONE synchronisation: every device
+    buffer (values, validity, offsets, small dictionaries) travels in one
+    device-side concatenation and one D2H copy (a copy per buffer costs ~18 us
+    of host submission each, with the GPU idle), then the stream is
+    synchronised once. ``prepack``: the concatenation already ran inside the
+    query graph. A string column that references a large device dictionary
+    keeps its device path (it decodes only the referenced strings on the GPU)."""
+    if not any(c.data.is_cuda for c in cols):
+        if guard is not None and int(guard.reshape(-1)[0].item()):
+            raise _ReplayMismatch()
+        if deferred is not None:
+            _raise_deferred(deferred, deferred[0].tolist())
+        return cols
+    plan, pending, fi, gi = _result_layout(cols, deferred, guard)
     dev = next(c.data.device for c in cols if c.data.is_cuda)
-    host = _d2h_packed(pending, dev)
+    if not pending:
+        host = []
+    elif prepack is not None and prepack.sig == _sig(pending):
+        host = _pinned_copy(prepack.buf, prepack.spans)
+    else:
+        host = _pinned_copy(*_device_pack(pending, dev))
     torch.cuda.current_stream(dev).synchronize()
 
     def build(x):
@@ -714,8 +757,9 @@ class QueryEngine:
             batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
         if table is None:
             guard = st.pop("pending_guard", None) if st is not None else None
+            pre = st.pop("pending_prepack", None) if st is not None else None
             try:
-                table = self._to_arrow(batch, plan.schema, bq_names, guard=guard)
+                table = self._to_arrow(batch, plan.schema, bq_names, guard=guard, prepack=pre)
             except _ReplayMismatch:
                 # a checked graph's replayed values did not match this time:
                 # drop it and run the query again with real readbacks
@@ -869,6 +913,7 @@ class QueryEngine:
                 comm.bytes_sent += g.comm_bytes
             self._touch_graph(st)
             st["pending_guard"] = g.bad
+            st["pending_prepack"] = g.prepack
             return g.batch, "graph", st, None
         if g is not None:
             ok = g.replay(ctx)
@@ -1073,9 +1118,10 @@ class QueryEngine:
         from .parallel.slicing import plan_slices
         return plan_slices(plan, self.comm)
 
-    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str], guard=None) -> pa.Table:
+    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str], guard=None, prepack=None) -> pa.Table:
         arrays, fields = [], []
-        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None), guard)
+        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None), guard,
+                             prepack)
         for ci, nm, col in zip(schema, names, host):
             arr = col.to_arrow()
             want = ci.dtype.to_arrow() if ci.dtype.kind != "null" else pa.null()
