@@ -153,20 +153,6 @@ def _pinned_copy(buf: torch.Tensor, spans) -> List[torch.Tensor]:
     return [host[o:o + n].view(dt).reshape(shape) for o, n, dt, shape in spans]
 
 
-class ResultPack:
-    """A query graph's result buffers concatenated INSIDE the graph (captured
-    with it, engine.py _result_layout order): a replay ends with the packed
-    buffer written, and only its one D2H copy follows."""
-    __slots__ = ("buf", "spans", "sig")
-
-    def __init__(self, buf, spans, sig):
-        self.buf, self.spans, self.sig = buf, spans, sig
-
-
-def _sig(ts: List[torch.Tensor]) -> tuple:
-    return tuple((t.data_ptr(), t.numel(), t.dtype) for t in ts)
-
-
 def _result_layout(cols: List[Column], deferred=None, guard=None):
     """How a result goes to the host: (per-column plan, device tensors to
     copy in order, index of the deferred flags, index of the guard)."""
@@ -191,26 +177,15 @@ def _result_layout(cols: List[Column], deferred=None, guard=None):
     return plan, pending, fi, gi
 
 
-def result_prepack(cols: List[Column], deferred, guard) -> Optional[ResultPack]:
-    """The packing of ``_host_columns`` for a result in a graph being
-    captured (called inside the capture: the concatenation is recorded)."""
-    if not any(c.data.is_cuda for c in cols):
-        return None
-    _, pending, _, _ = _result_layout(cols, deferred, guard)
-    if not pending:
-        return None
-    buf, spans = _device_pack(pending, pending[0].device)
-    return ResultPack(buf, spans, _sig(pending))
-
-
-def _host_columns(cols: List[Column], deferred=None, guard=None, prepack: Optional[ResultPack] = None) -> List[Column]:
+def _host_columns(cols: List[Column], deferred=None, guard=None) -> List[Column]:
     """Result columns moved to the host with ONE synchronisation: every device
     buffer (values, validity, offsets, small dictionaries) travels in one
     device-side concatenation and one D2H copy (a copy per buffer costs ~18 us
     of host submission each, with the GPU idle), then the stream is
-    synchronised once. ``prepack``: the concatenation already ran inside the
-    query graph. A string column that references a large device dictionary
-    keeps its device path (it decodes only the referenced strings on the GPU)."""
+    synchronised once. (Packing inside the query graph instead measured
+    slower: profiles/r6_ab_graph_result_pack_rejected.txt.) A string column
+    that references a large device dictionary keeps its device path (it
+    decodes only the referenced strings on the GPU)."""
     if not any(c.data.is_cuda for c in cols):
         if guard is not None and int(guard.reshape(-1)[0].item()):
             raise _ReplayMismatch()
@@ -219,12 +194,7 @@ def _host_columns(cols: List[Column], deferred=None, guard=None, prepack: Option
         return cols
     plan, pending, fi, gi = _result_layout(cols, deferred, guard)
     dev = next(c.data.device for c in cols if c.data.is_cuda)
-    if not pending:
-        host = []
-    elif prepack is not None and prepack.sig == _sig(pending):
-        host = _pinned_copy(prepack.buf, prepack.spans)
-    else:
-        host = _pinned_copy(*_device_pack(pending, dev))
+    host = _pinned_copy(*_device_pack(pending, dev)) if pending else []
     torch.cuda.current_stream(dev).synchronize()
 
     def build(x):
@@ -757,9 +727,8 @@ class QueryEngine:
             batch, spec, st, table = self._execute_speculative(plan, ctx, key, bq_names)
         if table is None:
             guard = st.pop("pending_guard", None) if st is not None else None
-            pre = st.pop("pending_prepack", None) if st is not None else None
             try:
-                table = self._to_arrow(batch, plan.schema, bq_names, guard=guard, prepack=pre)
+                table = self._to_arrow(batch, plan.schema, bq_names, guard=guard)
             except _ReplayMismatch:
                 # a checked graph's replayed values did not match this time:
                 # drop it and run the query again with real readbacks
@@ -913,7 +882,6 @@ class QueryEngine:
                 comm.bytes_sent += g.comm_bytes
             self._touch_graph(st)
             st["pending_guard"] = g.bad
-            st["pending_prepack"] = g.prepack
             return g.batch, "graph", st, None
         if g is not None:
             ok = g.replay(ctx)
@@ -1118,10 +1086,9 @@ class QueryEngine:
         from .parallel.slicing import plan_slices
         return plan_slices(plan, self.comm)
 
-    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str], guard=None, prepack=None) -> pa.Table:
+    def _to_arrow(self, batch: Batch, schema: List[ColInfo], names: List[str], guard=None) -> pa.Table:
         arrays, fields = [], []
-        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None), guard,
-                             prepack)
+        host = _host_columns([batch.columns[ci.cid] for ci in schema], getattr(batch, "deferred", None), guard)
         for ci, nm, col in zip(schema, names, host):
             arr = col.to_arrow()
             want = ci.dtype.to_arrow() if ci.dtype.kind != "null" else pa.null()

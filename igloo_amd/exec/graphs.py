@@ -69,8 +69,6 @@ GRAPHS = os.environ.get("IGLOO_GRAPHS", "1") == "1"
 SHARED_POOL = False
 
 _streams: dict = {}
-#: pack a query graph's result buffers inside the graph (IGLOO_DEBUG=no_result_pack: after it)
-RESULT_PACK = not _sw.debug("no_result_pack")
 STATS = {"captured": 0, "replays": 0, "aborted": 0, "failed": 0, "mismatch": 0}
 LAST_ERROR: list = []    # why the last captures did not produce a graph (debugging, tests)
 
@@ -92,7 +90,7 @@ class QueryGraph:
     mismatch counter of its replayed values."""
 
     __slots__ = ("graph", "batch", "bad", "expected", "jit_gen", "rows_scanned", "spill", "checked", "replays", "sp",
-                 "nbytes", "comm_calls", "comm_bytes", "comm_chunks", "keep", "global_check", "prepack")
+                 "nbytes", "comm_calls", "comm_bytes", "comm_chunks", "keep", "global_check")
 
     def __init__(self, graph, batch, bad, expected, jit_gen, rows_scanned, spill, sp=None, nbytes=0):
         self.sp = sp                   # the capture's speculation (sites + device values, for reports)
@@ -111,7 +109,6 @@ class QueryGraph:
         self.spill = spill
         self.checked = False           # first replay compared with the eager result
         self.replays = 0
-        self.prepack = None            # the result buffers packed inside the graph (engine.py ResultPack)
 
     def current(self) -> bool:
         """Still built from the generated kernels that are loaded now."""
@@ -160,9 +157,7 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     s = _capture_stream(dev)
     s.wait_stream(cur)
     g = torch.cuda.CUDAGraph()
-    batch = bad = pre = None
-    from ..engine import _pad, result_prepack
-    _pad(dev, 1)                       # (the packing's zero padding exists before the capture)
+    batch = bad = None
     # the graph's private pool is what capture adds to the reserved bytes
     # (engine.py charges it against the HBM budget)
     reserved0 = torch.cuda.memory_reserved(dev)
@@ -196,10 +191,6 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
                     # graph, so the one readback after a replay is already the
                     # agreement of every rank (no extra host round trip)
                     bad = comm.allreduce_tensor(bad.reshape(1).to(torch.int64), "sum")
-                # the result's host copy reads ONE buffer packed by the graph itself
-                if RESULT_PACK:
-                    pre = result_prepack([batch.columns[ci.cid] for ci in plan.schema],
-                                         getattr(batch, "deferred", None), bad)
             finally:
                 g.capture_end()
     except _lib.CaptureAbort as e:
@@ -246,6 +237,5 @@ def capture(engine, plan, log_: list, make_ctx) -> Optional[QueryGraph]:
     nbytes = max(0, torch.cuda.memory_reserved(dev) - reserved0)
     qg = QueryGraph(g, batch, bad, expected, gen, ctx.rows_scanned, ctx.spill, sp, nbytes)
     qg.global_check = engine.comm is not None and engine.comm.spmd
-    qg.prepack = pre
     qg.keep = _lib.capture_keepalive()     # pinned host buffers its copy nodes read
     return qg

@@ -28,8 +28,6 @@ list of tokens (``token`` or ``token=value``), read by Python and C++ alike
 ``like_nodword``                LIKE without the aligned-dword prefilter (strings.hip)
 ``no_templates``                plan every new statement text from scratch (no statement
                                 templates, sql/template.py)
-``no_result_pack``              pack a query graph's result buffers after the replay instead
-                                of inside the graph (exec/graphs.py)
 ==============================  =====================================================
 
 Other variables (each read in one place):
