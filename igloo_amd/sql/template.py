@@ -543,7 +543,8 @@ def perturb(texts: List[str], kinds: List[str], nodes: List[dict]) -> List[str]:
             out.append(t)
             continue
         typ = n.get("type")
-        if typ == "date":
+        if typ == "date" or (typ == "str" and re.fullmatch(r"\d{4}-\d{2}-\d{2}", t)):
+            # (a date, or a string that spells one: it may be coerced to a date)
             try:
                 d = datetime.date.fromisoformat(t.strip()) + datetime.timedelta(days=1)
                 out.append(d.isoformat())
