@@ -417,7 +417,18 @@ def transform(e: Expr, fn: Callable[[Expr], Optional[Expr]]) -> Expr:
 
 
 def col_refs(e: Expr) -> Set[int]:
-    return {x.cid for x in walk(e) if isinstance(x, ColRef)}
+    """Column ids ``e`` reads. Remembered on the expression object (bound
+    expressions are not mutated: rewrites build new nodes), since a cached
+    plan's operators ask again on every execution (join edges, prefetch
+    lists): a frozenset, callers do not modify it."""
+    r = e.__dict__.get("_igloo_refs") if hasattr(e, "__dict__") else None
+    if r is None:
+        r = frozenset(x.cid for x in walk(e) if isinstance(x, ColRef))
+        try:
+            e._igloo_refs = r
+        except AttributeError:
+            pass
+    return r
 
 
 def has_subquery(e: Expr) -> bool:
