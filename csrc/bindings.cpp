@@ -311,6 +311,8 @@ PYBIND11_MODULE(_native, m) {
                      P<const void>(thead), rid64, cap, kmin, direct, P<const uint32_t>(bits), bmask, negate,
                      P<unsigned long long>(words), P<int64_t>(tile_counts), S(s));
   });
+  m.def("set_probe_grid_cap", &kern::set_probe_grid_cap);
+  m.def("set_probe_bits", &kern::set_probe_bits);
   m.def("probe_write", [](uintptr_t keys, bool key64, uintptr_t valid, int64_t m_, uintptr_t tkeys, uintptr_t thead,
                           bool rid64, int64_t cap, int64_t kmin, bool direct, uintptr_t words, uintptr_t tile_off,
                           uintptr_t out_probe, bool out64, uintptr_t out_build, int64_t out_cap, uintptr_t s) {

@@ -629,6 +629,9 @@ constexpr int kHitWords = kHitTile / kWave;    // 64-bit hit words per tile (128
 // profiles/r3_sf100_pmc_roofline.txt). With an exact membership bitmap the bit
 // IS the answer and the table is not read at all (need_head false).
 constexpr int kHitBatch = 8;
+// probe_write: tiles with at most this many hits list them in LDS and give
+// every lane whole hits (denser tiles walk their hit words)
+constexpr int kSparseHits = 2048;
 //
 // All loads are unconditional (indices clamped into range, results selected
 // afterwards): a load under a per-lane condition compiles to a branch whose
@@ -756,9 +759,13 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
                                                             int64_t out_cap) {
   __shared__ int64_t woff[kHitWords];
   __shared__ int64_t scratch[kWavesPerBlock + 1];
+  __shared__ uint16_t hits[kSparseHits];
   const int lane = lane_id(), wave = threadIdx.x / kWave;
   const int64_t tiles = (m + kHitTile - 1) / kHitTile;
   for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    // a tile without hits (its offset equals the next one's): nothing to
+    // load, scan or write (selective probes: most tiles)
+    if ((t + 1 < tiles ? tile_off[t + 1] : out_cap) <= tile_off[t]) continue;
     const int64_t nrows = m - t * kHitTile < kHitTile ? m - t * kHitTile : kHitTile;
     const int nwords = (int)((nrows + kWave - 1) / kWave);
     const unsigned long long w0 = threadIdx.x < nwords ? words[t * kHitWords + threadIdx.x] : 0ULL;
@@ -766,7 +773,40 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
     const int64_t ex = block_exclusive_scan((int64_t)__popcll(w0), scratch, &total);
     if (threadIdx.x < kHitWords) woff[threadIdx.x] = ex;
     __syncthreads();
-    if (total) {
+    if (total && total <= kSparseHits) {
+      // a sparse tile: its hit rows listed in LDS first (in row order: the
+      // list index IS the output offset inside the tile), then every lane
+      // takes whole hits -- the work follows the hits, not the 8192 rows
+      const int64_t base = tile_off[t];
+      if (threadIdx.x < nwords) {
+        unsigned long long w = w0;
+        int o = (int)ex;
+        while (w) {
+          const int b = __ffsll((long long)w) - 1;
+          hits[o++] = (uint16_t)(threadIdx.x * kWave + b);
+          w &= w - 1ULL;
+        }
+      }
+      __syncthreads();
+      for (int64_t i0 = 0; i0 < total; i0 += (int64_t)kBlock * kHitBatch) {
+        int64_t row[kHitBatch];
+#pragma unroll
+        for (int r = 0; r < kHitBatch; ++r) {
+          const int64_t i = i0 + (int64_t)r * kBlock + threadIdx.x;
+          row[r] = i < total ? t * kHitTile + hits[i] : m;
+        }
+        int64_t h[kHitBatch];
+        if (out_build) probe_heads<K, DIRECT, R>(keys, valid, m, row, tkeys, thead, cap, kmin, nullptr, 0, true, h);
+#pragma unroll
+        for (int r = 0; r < kHitBatch; ++r) {
+          if (row[r] >= m) continue;
+          const int64_t pos = base + i0 + (int64_t)r * kBlock + threadIdx.x;
+          if (pos >= out_cap) continue;   // a replayed (undersized) total: see join_expand_kernel
+          out_probe[pos] = (O)row[r];
+          if (out_build) out_build[pos] = (R)h[r];
+        }
+      }
+    } else if (total) {
       const int64_t base = tile_off[t];
       // kHitBatch hit words per wave at a time (waves own words wave, wave+4, ...)
       for (int w0 = wave; w0 < nwords; w0 += kWavesPerBlock * kHitBatch) {
@@ -797,14 +837,104 @@ __global__ __launch_bounds__(kBlock) void probe_write_kernel(const K* __restrict
 }
 }  // namespace
 
+namespace {
+
+// probe_hits for int32 keys against a direct table with an exact membership
+// bitmap (no head read at all: the bit decides): every lane takes 4
+// consecutive rows per step -- one 16-byte key load and one 4-byte validity
+// load instead of 4 + 4 scalar loads -- and the 64-bit hit words are put
+// together from each 16-lane group's nibbles. Same tiles, words and counts
+// as probe_hits_kernel (probe_write reads them unchanged).
+constexpr int kBitsRows = 4;
+constexpr int kBitsSteps = kHitTile / (kBlock * kBitsRows);   // 8
+
+__global__ __launch_bounds__(kBlock) void probe_bits_kernel(const int32_t* __restrict__ keys,
+                                                           const uint8_t* __restrict__ valid, int64_t m,
+                                                           int64_t cap, int64_t kmin,
+                                                           const uint32_t* __restrict__ bits, bool negate,
+                                                           unsigned long long* __restrict__ words,
+                                                           int64_t* __restrict__ tile_counts) {
+  __shared__ int64_t red[kWavesPerBlock];
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  const int64_t tiles = (m + kHitTile - 1) / kHitTile;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    int64_t cnt = 0;
+#pragma unroll 2
+    for (int g = 0; g < kBitsSteps; ++g) {
+      const int64_t r0 = t * kHitTile + (int64_t)g * (kBlock * kBitsRows) + (int64_t)threadIdx.x * kBitsRows;
+      int32_t k[kBitsRows];
+      uint32_t vb = 0x01010101u;
+      if (r0 + kBitsRows <= m) {
+        const int4 kv = *reinterpret_cast<const int4*>(keys + r0);
+        k[0] = kv.x;
+        k[1] = kv.y;
+        k[2] = kv.z;
+        k[3] = kv.w;
+        if (valid) vb = *reinterpret_cast<const uint32_t*>(valid + r0);
+      } else {
+        vb = 0;
+#pragma unroll
+        for (int j = 0; j < kBitsRows; ++j) {
+          const bool in = r0 + j < m;
+          k[j] = in ? keys[r0 + j] : 0;
+          if (in && (!valid || valid[r0 + j])) vb |= 1u << (8 * j);
+        }
+      }
+      uint32_t nib = 0;
+#pragma unroll
+      for (int j = 0; j < kBitsRows; ++j) {
+        const int64_t d = (int64_t)k[j] - kmin;
+        bool ok = ((vb >> (8 * j)) & 0xffu) != 0 && d >= 0 && d < cap;
+        if (ok) ok = (bits[(uint64_t)d >> 5] >> (d & 31)) & 1u;
+        const bool hit = r0 + j < m && (ok != negate);
+        nib |= (hit ? 1u : 0u) << j;
+      }
+      cnt += __popc(nib);
+      // rows 4*lane .. 4*lane+3 of this wave's 256 are bits 4*(lane%16) .. +3
+      // of word lane/16: OR the 16 nibbles of each lane group together
+      unsigned long long w = (unsigned long long)nib << (4 * (lane & 15));
+      w |= __shfl_xor(w, 1, kWave);
+      w |= __shfl_xor(w, 2, kWave);
+      w |= __shfl_xor(w, 4, kWave);
+      w |= __shfl_xor(w, 8, kWave);
+      const int64_t wrow = t * kHitTile + (int64_t)g * (kBlock * kBitsRows) + (int64_t)wave * (kWave * kBitsRows) +
+                           (int64_t)(lane >> 4) * kWave;
+      if ((lane & 15) == 0 && wrow < m)
+        words[t * kHitWords + g * (kHitWords / kBitsSteps) + wave * kBitsRows + (lane >> 4)] = w;
+    }
+    cnt = wave_reduce_sum(cnt);
+    if (lane == 0) red[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t s = 0;
+      for (int w = 0; w < kWavesPerBlock; ++w) s += red[w];
+      tile_counts[t] = s;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
 int64_t probe_hit_tiles(int64_t m) { return (m + kHitTile - 1) / kHitTile; }
+
+// workgroups of a probe_hits / probe_write launch at most (both loop over
+// their tiles): tunable for the A/B in scripts/bench_probe.py
+static int g_probe_grid_cap = 1 << 16;
+void set_probe_grid_cap(int cap) { g_probe_grid_cap = cap > 0 ? cap : (1 << 16); }
+static bool g_probe_bits = true;   // the vector bitmap probe (scripts/bench_probe.py A/B)
+void set_probe_bits(bool on) { g_probe_bits = on; }
 
 void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                 const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits,
                 uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream) {
   if (m == 0) return;
-  const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
-  if (rid64)
+  const dim3 g(grid_for(probe_hit_tiles(m), 1, g_probe_grid_cap)), b(kBlock);
+  if (!key64 && direct && bits && (bmask & kExactBits) && ((uintptr_t)keys & 15) == 0 &&
+      ((uintptr_t)valid & 3) == 0 && g_probe_bits) {
+    hipLaunchKernelGGL(probe_bits_kernel, g, b, 0, stream, static_cast<const int32_t*>(keys), valid, m, cap, kmin,
+                       bits, negate, words, tile_counts);
+  } else if (rid64)
     DISPATCH_KEY3(key64, direct, int64_t, probe_hits_kernel, g, b, 0, stream, keys, valid, m, tkeys,
                   (const int64_t*)thead, cap, kmin, bits, bmask, negate, words, tile_counts);
   else
@@ -817,7 +947,7 @@ template <typename R, typename O>
 static void probe_write_t(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                           const R* thead, int64_t cap, int64_t kmin, bool direct, const unsigned long long* words,
                           const int64_t* tile_off, O* out_probe, R* out_build, int64_t out_cap, hipStream_t stream) {
-  const dim3 g(grid_for(probe_hit_tiles(m), 1, 1 << 16)), b(kBlock);
+  const dim3 g(grid_for(probe_hit_tiles(m), 1, g_probe_grid_cap)), b(kBlock);
   if (key64) {
     if (direct)
       hipLaunchKernelGGL((probe_write_kernel<int64_t, true, R, O>), g, b, 0, stream, (const int64_t*)keys, valid, m,

@@ -263,3 +263,41 @@ def test_unique_lookup_matches_searchsorted(gpu_device, kdt, nb, dense, nulls, m
     assert np.array_equal(hit.cpu().numpy(), want)
     assert np.array_equal(pos.cpu().numpy(), np.where(want, lo, 0))
     assert pos.dtype == torch.int32
+
+
+@pytest.mark.parametrize("m", [1, 3, 4, 1000, 8192, 8195, 100_003, 1_000_003])
+@pytest.mark.parametrize("masked,negate,offset", [(False, False, 0), (True, False, 0), (True, True, 0),
+                                                  (True, False, 1)])
+def test_probe_bits_kernel_matches_scalar(gpu_device, m, masked, negate, offset):
+    """hashtable.hip probe_bits_kernel (int32 keys, direct table with an
+    exact bitmap: 4 rows per lane, vector loads) writes the same hit words
+    and counts as probe_hits_kernel -- tails, NULL masks, NOT EXISTS, and an
+    unaligned probe view (the host falls back to the scalar kernel)."""
+    from igloo_amd.ops._lib import native
+    rng = np.random.default_rng(m)
+    span = 100_000
+    build = torch.from_numpy(rng.choice(np.arange(1, span + 1), 4000, replace=False).astype(np.int32)).to(gpu_device)
+    base = torch.from_numpy(rng.integers(-10, span + 10, m + offset).astype(np.int32)).to(gpu_device)
+    probe = base[offset:]
+    valid = torch.from_numpy(rng.random(m) > 0.3).to(gpu_device) if masked else None
+    table = H.JoinTable(build, None, defer_unique=False)
+    if m >= H.BLOOM_MIN_RATIO * build.numel():
+        # (the shape the vector kernel serves: direct table, exact bitmap in use)
+        bits, bmask = table._bloom(m)
+        assert table.direct and bits and bmask & (1 << 63), (table.direct, bits, bmask)
+    outs = []
+    for on in (True, False):
+        native().set_probe_bits(on)
+        try:
+            outs.append(table.probe_select(probe, valid, negate=negate, want_build=not negate))
+        finally:
+            native().set_probe_bits(True)
+    (p1, b1), (p0, b0) = outs
+    assert torch.equal(p1, p0)
+    assert (b1 is None and b0 is None) or torch.equal(b1, b0)
+    keys = probe.cpu().numpy()
+    hit = np.isin(keys, build.cpu().numpy())
+    if valid is not None:
+        hit &= valid.cpu().numpy()
+    want = np.nonzero(~hit if negate else hit)[0]
+    assert np.array_equal(p1.cpu().numpy(), want)
