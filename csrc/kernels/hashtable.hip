@@ -914,6 +914,92 @@ __global__ __launch_bounds__(kBlock) void probe_bits_kernel(const int32_t* __res
   }
 }
 
+// The same probe for large probe sides: the membership bitmap, folded
+// modulo 64 KiB (word i = OR of the bitmap's words i, i + 16K, ...), sits in
+// LDS, read by every workgroup once; a probe key whose folded bit is clear
+// is out without touching L2 (each global bitmap read moves a whole cache
+// line for 4 useful bytes), and only folded hits consult the exact bitmap
+// (none when the bitmap fits the fold: then the fold is exact). Workgroups of
+// 1024 lanes, two per CU, loop over the tiles.
+constexpr int kFoldWords = 16384;
+constexpr int kFoldBlock = 1024;
+constexpr int kFoldWaves = kFoldBlock / kWave;
+constexpr int kFoldSteps = kHitTile / (kFoldBlock * kBitsRows);   // 2
+
+__global__ __launch_bounds__(kFoldBlock) void probe_fold_kernel(const int32_t* __restrict__ keys,
+                                                               const uint8_t* __restrict__ valid, int64_t m,
+                                                               int64_t cap, int64_t kmin,
+                                                               const uint32_t* __restrict__ bits, bool negate,
+                                                               unsigned long long* __restrict__ words,
+                                                               int64_t* __restrict__ tile_counts) {
+  __shared__ uint32_t fold[kFoldWords];
+  __shared__ int64_t red[kFoldWaves];
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  const int64_t nbw = (cap + 31) >> 5;
+  for (int i = threadIdx.x; i < kFoldWords; i += kFoldBlock) {
+    uint32_t v = 0;
+    for (int64_t j = i; j < nbw; j += kFoldWords) v |= bits[j];
+    fold[i] = v;
+  }
+  __syncthreads();
+  const bool exact = nbw <= kFoldWords;
+  const int64_t tiles = (m + kHitTile - 1) / kHitTile;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    int64_t cnt = 0;
+#pragma unroll
+    for (int g = 0; g < kFoldSteps; ++g) {
+      const int64_t r0 = t * kHitTile + (int64_t)g * (kFoldBlock * kBitsRows) + (int64_t)threadIdx.x * kBitsRows;
+      int32_t k[kBitsRows];
+      uint32_t vb = 0x01010101u;
+      if (r0 + kBitsRows <= m) {
+        const int4 kv = *reinterpret_cast<const int4*>(keys + r0);
+        k[0] = kv.x;
+        k[1] = kv.y;
+        k[2] = kv.z;
+        k[3] = kv.w;
+        if (valid) vb = *reinterpret_cast<const uint32_t*>(valid + r0);
+      } else {
+        vb = 0;
+#pragma unroll
+        for (int j = 0; j < kBitsRows; ++j) {
+          const bool in = r0 + j < m;
+          k[j] = in ? keys[r0 + j] : 0;
+          if (in && (!valid || valid[r0 + j])) vb |= 1u << (8 * j);
+        }
+      }
+      uint32_t nib = 0;
+#pragma unroll
+      for (int j = 0; j < kBitsRows; ++j) {
+        const int64_t d = (int64_t)k[j] - kmin;
+        bool ok = ((vb >> (8 * j)) & 0xffu) != 0 && d >= 0 && d < cap;
+        if (ok) ok = (fold[(d >> 5) & (kFoldWords - 1)] >> (d & 31)) & 1u;
+        if (ok && !exact) ok = (bits[(uint64_t)d >> 5] >> (d & 31)) & 1u;
+        const bool hit = r0 + j < m && (ok != negate);
+        nib |= (hit ? 1u : 0u) << j;
+      }
+      cnt += __popc(nib);
+      unsigned long long w = (unsigned long long)nib << (4 * (lane & 15));
+      w |= __shfl_xor(w, 1, kWave);
+      w |= __shfl_xor(w, 2, kWave);
+      w |= __shfl_xor(w, 4, kWave);
+      w |= __shfl_xor(w, 8, kWave);
+      const int64_t wrow = t * kHitTile + (int64_t)g * (kFoldBlock * kBitsRows) +
+                           (int64_t)wave * (kWave * kBitsRows) + (int64_t)(lane >> 4) * kWave;
+      if ((lane & 15) == 0 && wrow < m)
+        words[t * kHitWords + g * (kHitWords / kFoldSteps) + wave * kBitsRows + (lane >> 4)] = w;
+    }
+    cnt = wave_reduce_sum(cnt);
+    if (lane == 0) red[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t s = 0;
+      for (int w = 0; w < kFoldWaves; ++w) s += red[w];
+      tile_counts[t] = s;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 int64_t probe_hit_tiles(int64_t m) { return (m + kHitTile - 1) / kHitTile; }
@@ -922,16 +1008,26 @@ int64_t probe_hit_tiles(int64_t m) { return (m + kHitTile - 1) / kHitTile; }
 // their tiles): tunable for the A/B in scripts/bench_probe.py
 static int g_probe_grid_cap = 1 << 16;
 void set_probe_grid_cap(int cap) { g_probe_grid_cap = cap > 0 ? cap : (1 << 16); }
-static bool g_probe_bits = true;   // the vector bitmap probe (scripts/bench_probe.py A/B)
-void set_probe_bits(bool on) { g_probe_bits = on; }
+// 0: scalar probe_hits_kernel only, 1: + the vector bitmap probe, 2: + the LDS-folded
+// bitmap for large probe sides (scripts/bench_probe.py A/B)
+static int g_probe_bits = 2;
+void set_probe_bits(int mode) { g_probe_bits = mode; }
+constexpr int64_t kFoldMinRows = 1 << 22;   // below: the fold's build per workgroup does not pay
+constexpr int64_t kFoldGrid = 512;          // two 1024-lane workgroups (64 KiB LDS each) per CU
 
 void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                 const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits,
                 uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream) {
   if (m == 0) return;
   const dim3 g(grid_for(probe_hit_tiles(m), 1, g_probe_grid_cap)), b(kBlock);
-  if (!key64 && direct && bits && (bmask & kExactBits) && ((uintptr_t)keys & 15) == 0 &&
-      ((uintptr_t)valid & 3) == 0 && g_probe_bits) {
+  const bool vec = !key64 && direct && bits && (bmask & kExactBits) && ((uintptr_t)keys & 15) == 0 &&
+                   ((uintptr_t)valid & 3) == 0;
+  if (vec && g_probe_bits >= 2 && m >= kFoldMinRows) {
+    const int64_t tiles = probe_hit_tiles(m);
+    const dim3 gf((unsigned)(tiles < kFoldGrid ? tiles : kFoldGrid)), bf(kFoldBlock);
+    hipLaunchKernelGGL(probe_fold_kernel, gf, bf, 0, stream, static_cast<const int32_t*>(keys), valid, m, cap, kmin,
+                       bits, negate, words, tile_counts);
+  } else if (vec && g_probe_bits >= 1) {
     hipLaunchKernelGGL(probe_bits_kernel, g, b, 0, stream, static_cast<const int32_t*>(keys), valid, m, cap, kmin,
                        bits, negate, words, tile_counts);
   } else if (rid64)

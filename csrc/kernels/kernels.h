@@ -185,7 +185,7 @@ void join_probe(const void* keys, bool key64, const uint8_t* valid, int64_t m, c
 // (tile_off = exclusive scan of the counts) writes hit rows (+ their build rows) in row order
 int64_t probe_hit_tiles(int64_t m);
 void set_probe_grid_cap(int cap);
-void set_probe_bits(bool on);
+void set_probe_bits(int mode);
 void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, const int64_t* tkeys,
                 const void* thead, bool rid64, int64_t cap, int64_t kmin, bool direct, const uint32_t* bits,
                 uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream);

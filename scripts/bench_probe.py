@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--build", type=int, default=40_000)
     ap.add_argument("--span", type=int, default=1_000_000)
     ap.add_argument("--caps", default="0,16384,8192,4096,2048,1024")
-    ap.add_argument("--bits", default="1,0", help="vector bitmap probe on / off (probe_bits_kernel)")
+    ap.add_argument("--bits", default="2,1,0",
+                    help="2: LDS-folded bitmap probe, 1: vector bitmap probe, 0: scalar probe (hashtable.hip)")
     ap.add_argument("--reps", type=int, default=7)
     a = ap.parse_args()
     import numpy as np
@@ -38,7 +39,7 @@ def main():
     out = {}
     for cap, bits in [(int(c), int(b)) for b in a.bits.split(",") for c in a.caps.split(",")]:
         native().set_probe_grid_cap(cap)
-        native().set_probe_bits(bool(bits))
+        native().set_probe_bits(bits)
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,7 +56,7 @@ def main():
         out[k] = {"ms": round(float(np.median(ts)), 3), "hits": int(pidx.numel()), "same": bool(same)}
         print(k, out[k], flush=True)
     native().set_probe_grid_cap(0)
-    native().set_probe_bits(True)
+    native().set_probe_bits(2)
     print(json.dumps(out))
 
 

@@ -265,13 +265,14 @@ def test_unique_lookup_matches_searchsorted(gpu_device, kdt, nb, dense, nulls, m
     assert pos.dtype == torch.int32
 
 
-@pytest.mark.parametrize("m", [1, 3, 4, 1000, 8192, 8195, 100_003, 1_000_003])
+@pytest.mark.parametrize("m", [1, 3, 4, 1000, 8192, 8195, 100_003, 1_000_003, 5_000_003])
 @pytest.mark.parametrize("masked,negate,offset", [(False, False, 0), (True, False, 0), (True, True, 0),
                                                   (True, False, 1)])
 def test_probe_bits_kernel_matches_scalar(gpu_device, m, masked, negate, offset):
     """hashtable.hip probe_bits_kernel (int32 keys, direct table with an
-    exact bitmap: 4 rows per lane, vector loads) writes the same hit words
-    and counts as probe_hits_kernel -- tails, NULL masks, NOT EXISTS, and an
+    exact bitmap: 4 rows per lane, vector loads) and probe_fold_kernel (the
+    bitmap folded into LDS, from 4M probe rows) write the same hit words and
+    counts as probe_hits_kernel -- tails, NULL masks, NOT EXISTS, and an
     unaligned probe view (the host falls back to the scalar kernel)."""
     from igloo_amd.ops._lib import native
     rng = np.random.default_rng(m)
@@ -286,18 +287,43 @@ def test_probe_bits_kernel_matches_scalar(gpu_device, m, masked, negate, offset)
         bits, bmask = table._bloom(m)
         assert table.direct and bits and bmask & (1 << 63), (table.direct, bits, bmask)
     outs = []
-    for on in (True, False):
-        native().set_probe_bits(on)
+    for mode in (2, 1, 0):
+        native().set_probe_bits(mode)
         try:
             outs.append(table.probe_select(probe, valid, negate=negate, want_build=not negate))
         finally:
-            native().set_probe_bits(True)
-    (p1, b1), (p0, b0) = outs
-    assert torch.equal(p1, p0)
-    assert (b1 is None and b0 is None) or torch.equal(b1, b0)
+            native().set_probe_bits(2)
+    (p1, b1), (p0, b0) = outs[0], outs[2]
+    for p, b in outs[1:]:
+        assert torch.equal(p1, p)
+        assert (b1 is None and b is None) or torch.equal(b1, b)
     keys = probe.cpu().numpy()
     hit = np.isin(keys, build.cpu().numpy())
     if valid is not None:
         hit &= valid.cpu().numpy()
     want = np.nonzero(~hit if negate else hit)[0]
     assert np.array_equal(p1.cpu().numpy(), want)
+
+
+def test_probe_fold_kernel_wide_bitmap(gpu_device):
+    """probe_fold_kernel with a bitmap wider than its 64 KiB LDS fold (2M-key
+    span): folded hits are confirmed against the exact bitmap."""
+    from igloo_amd.ops._lib import native
+    rng = np.random.default_rng(11)
+    span, m = 2_000_000, 5_000_001
+    build = torch.from_numpy(rng.choice(np.arange(1, span + 1), 50_000, replace=False).astype(np.int32)).to(gpu_device)
+    probe = torch.from_numpy(rng.integers(0, span + 2, m).astype(np.int32)).to(gpu_device)
+    valid = torch.from_numpy(rng.random(m) > 0.5).to(gpu_device)
+    table = H.JoinTable(build, None, defer_unique=False)
+    bits, bmask = table._bloom(m)
+    assert table.direct and bits and bmask & (1 << 63)
+    outs = []
+    for mode in (2, 0):
+        native().set_probe_bits(mode)
+        try:
+            outs.append(table.probe_select(probe, valid))
+        finally:
+            native().set_probe_bits(2)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    hit = np.isin(probe.cpu().numpy(), build.cpu().numpy()) & valid.cpu().numpy()
+    assert np.array_equal(outs[0][0].cpu().numpy(), np.nonzero(hit)[0])
