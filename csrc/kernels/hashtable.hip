@@ -848,7 +848,25 @@ namespace {
 constexpr int kBitsRows = 4;
 constexpr int kBitsSteps = kHitTile / (kBlock * kBitsRows);   // 8
 
-__global__ __launch_bounds__(kBlock) void probe_bits_kernel(const int32_t* __restrict__ keys,
+// 4 consecutive keys (16-byte aligned) in one or two 16-byte loads
+__device__ inline void load4(const int32_t* p, int32_t (&k)[4]) {
+  const int4 v = *reinterpret_cast<const int4*>(p);
+  k[0] = v.x;
+  k[1] = v.y;
+  k[2] = v.z;
+  k[3] = v.w;
+}
+__device__ inline void load4(const int64_t* p, int64_t (&k)[4]) {
+  const longlong2 a = *reinterpret_cast<const longlong2*>(p);
+  const longlong2 b = *reinterpret_cast<const longlong2*>(p + 2);
+  k[0] = a.x;
+  k[1] = a.y;
+  k[2] = b.x;
+  k[3] = b.y;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void probe_bits_kernel(const K* __restrict__ keys,
                                                            const uint8_t* __restrict__ valid, int64_t m,
                                                            int64_t cap, int64_t kmin,
                                                            const uint32_t* __restrict__ bits, bool negate,
@@ -862,21 +880,17 @@ __global__ __launch_bounds__(kBlock) void probe_bits_kernel(const int32_t* __res
 #pragma unroll 2
     for (int g = 0; g < kBitsSteps; ++g) {
       const int64_t r0 = t * kHitTile + (int64_t)g * (kBlock * kBitsRows) + (int64_t)threadIdx.x * kBitsRows;
-      int32_t k[kBitsRows];
+      K k[kBitsRows];
       uint32_t vb = 0x01010101u;
       if (r0 + kBitsRows <= m) {
-        const int4 kv = *reinterpret_cast<const int4*>(keys + r0);
-        k[0] = kv.x;
-        k[1] = kv.y;
-        k[2] = kv.z;
-        k[3] = kv.w;
+        load4(keys + r0, k);
         if (valid) vb = *reinterpret_cast<const uint32_t*>(valid + r0);
       } else {
         vb = 0;
 #pragma unroll
         for (int j = 0; j < kBitsRows; ++j) {
           const bool in = r0 + j < m;
-          k[j] = in ? keys[r0 + j] : 0;
+          k[j] = in ? keys[r0 + j] : K(0);
           if (in && (!valid || valid[r0 + j])) vb |= 1u << (8 * j);
         }
       }
@@ -926,7 +940,8 @@ constexpr int kFoldBlock = 1024;
 constexpr int kFoldWaves = kFoldBlock / kWave;
 constexpr int kFoldSteps = kHitTile / (kFoldBlock * kBitsRows);   // 2
 
-__global__ __launch_bounds__(kFoldBlock) void probe_fold_kernel(const int32_t* __restrict__ keys,
+template <typename K>
+__global__ __launch_bounds__(kFoldBlock) void probe_fold_kernel(const K* __restrict__ keys,
                                                                const uint8_t* __restrict__ valid, int64_t m,
                                                                int64_t cap, int64_t kmin,
                                                                const uint32_t* __restrict__ bits, bool negate,
@@ -949,21 +964,17 @@ __global__ __launch_bounds__(kFoldBlock) void probe_fold_kernel(const int32_t* _
 #pragma unroll
     for (int g = 0; g < kFoldSteps; ++g) {
       const int64_t r0 = t * kHitTile + (int64_t)g * (kFoldBlock * kBitsRows) + (int64_t)threadIdx.x * kBitsRows;
-      int32_t k[kBitsRows];
+      K k[kBitsRows];
       uint32_t vb = 0x01010101u;
       if (r0 + kBitsRows <= m) {
-        const int4 kv = *reinterpret_cast<const int4*>(keys + r0);
-        k[0] = kv.x;
-        k[1] = kv.y;
-        k[2] = kv.z;
-        k[3] = kv.w;
+        load4(keys + r0, k);
         if (valid) vb = *reinterpret_cast<const uint32_t*>(valid + r0);
       } else {
         vb = 0;
 #pragma unroll
         for (int j = 0; j < kBitsRows; ++j) {
           const bool in = r0 + j < m;
-          k[j] = in ? keys[r0 + j] : 0;
+          k[j] = in ? keys[r0 + j] : K(0);
           if (in && (!valid || valid[r0 + j])) vb |= 1u << (8 * j);
         }
       }
@@ -1020,16 +1031,24 @@ void probe_hits(const void* keys, bool key64, const uint8_t* valid, int64_t m, c
                 uint64_t bmask, bool negate, unsigned long long* words, int64_t* tile_counts, hipStream_t stream) {
   if (m == 0) return;
   const dim3 g(grid_for(probe_hit_tiles(m), 1, g_probe_grid_cap)), b(kBlock);
-  const bool vec = !key64 && direct && bits && (bmask & kExactBits) && ((uintptr_t)keys & 15) == 0 &&
+  const bool vec = direct && bits && (bmask & kExactBits) && ((uintptr_t)keys & 15) == 0 &&
                    ((uintptr_t)valid & 3) == 0;
   if (vec && g_probe_bits >= 2 && m >= kFoldMinRows) {
     const int64_t tiles = probe_hit_tiles(m);
     const dim3 gf((unsigned)(tiles < kFoldGrid ? tiles : kFoldGrid)), bf(kFoldBlock);
-    hipLaunchKernelGGL(probe_fold_kernel, gf, bf, 0, stream, static_cast<const int32_t*>(keys), valid, m, cap, kmin,
-                       bits, negate, words, tile_counts);
+    if (key64)
+      hipLaunchKernelGGL(probe_fold_kernel<int64_t>, gf, bf, 0, stream, static_cast<const int64_t*>(keys), valid, m,
+                         cap, kmin, bits, negate, words, tile_counts);
+    else
+      hipLaunchKernelGGL(probe_fold_kernel<int32_t>, gf, bf, 0, stream, static_cast<const int32_t*>(keys), valid, m,
+                         cap, kmin, bits, negate, words, tile_counts);
   } else if (vec && g_probe_bits >= 1) {
-    hipLaunchKernelGGL(probe_bits_kernel, g, b, 0, stream, static_cast<const int32_t*>(keys), valid, m, cap, kmin,
-                       bits, negate, words, tile_counts);
+    if (key64)
+      hipLaunchKernelGGL(probe_bits_kernel<int64_t>, g, b, 0, stream, static_cast<const int64_t*>(keys), valid, m, cap,
+                         kmin, bits, negate, words, tile_counts);
+    else
+      hipLaunchKernelGGL(probe_bits_kernel<int32_t>, g, b, 0, stream, static_cast<const int32_t*>(keys), valid, m, cap,
+                         kmin, bits, negate, words, tile_counts);
   } else if (rid64)
     DISPATCH_KEY3(key64, direct, int64_t, probe_hits_kernel, g, b, 0, stream, keys, valid, m, tkeys,
                   (const int64_t*)thead, cap, kmin, bits, bmask, negate, words, tile_counts);
