@@ -483,7 +483,10 @@ def dense_index(big: torch.Tensor, build: bool = True, queries: Optional[int] = 
     or None when the key span is too sparse. Remembered on the tensor object
     (resident table columns build it once)."""
     hit = getattr(big, "_igloo_dense", None)
-    resident = getattr(big, "_igloo_resident", False)
+    # (the sorted keys of a resident column's secondary index live as long as
+    # the column: their table is built once too -- Q9's 1.1M green parts
+    # searched 600M l_partkey keys by bisection, 0.93 ms per query)
+    resident = getattr(big, "_igloo_resident", False) or getattr(big, "_igloo_index_keys", False)
     if hit or (hit is False and (queries is None or resident)):
         return hit or None
     if resident:
@@ -658,6 +661,7 @@ def perm_index(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         out = perm_sort_int(keys)
     try:
         out[0]._igloo_sorted = True
+        out[0]._igloo_index_keys = True
         keys._igloo_perm = out
     except (AttributeError, RuntimeError):
         pass

@@ -40,6 +40,8 @@ def derived_nbytes(t: torch.Tensor) -> int:
         if v is None or v is t or v is False:
             continue
         n += _tensor_bytes(v)
+        if a == "_igloo_perm" and isinstance(v, tuple) and v and isinstance(v[0], torch.Tensor):
+            n += derived_nbytes(v[0])     # the index keys' own dense table
     return n
 
 

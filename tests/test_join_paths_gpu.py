@@ -351,3 +351,26 @@ def test_probe_bits_int64_keys(gpu_device, m):
         assert torch.equal(outs[0][0], p) and torch.equal(outs[0][1], b)
     hit = np.isin(probe.cpu().numpy(), build.cpu().numpy()) & valid.cpu().numpy()
     assert np.array_equal(outs[0][0].cpu().numpy(), np.nonzero(hit)[0])
+
+
+def test_perm_index_keys_get_dense_ranges(gpu_device):
+    """The sorted keys of a resident column's secondary index get the dense
+    lower-bound table like a sorted resident column (built once, charged to
+    the column): Q9's 1.1M green parts looked their l_partkey ranges up by
+    bisection of 600M keys. Ranges equal torch.searchsorted's, including keys
+    in long gaps and outside the key span."""
+    from igloo_amd.utils.memory import derived_nbytes
+    r = np.random.default_rng(3)
+    k = torch.from_numpy(r.integers(0, 50_000, 400_000)).to(torch.int32).to(gpu_device)
+    k[k % 7 == 3] += 200_000            # a sparse upper tail: long gaps in the key span
+    k._igloo_resident = True
+    skeys, perm = H.perm_index(k)
+    q = torch.from_numpy(r.integers(-5, 260_000, 8192)).to(torch.int32).to(gpu_device)
+    lo, cnt = H.sorted_ranges(skeys, q)
+    assert getattr(skeys, "_igloo_dense", None), "no dense table on the index keys"
+    ref_lo = torch.searchsorted(skeys, q)
+    ref_cnt = torch.searchsorted(skeys, q, right=True) - ref_lo
+    assert torch.equal(cnt, ref_cnt)
+    assert torch.equal(lo[cnt > 0], ref_lo[cnt > 0])
+    first = skeys._igloo_dense[2]
+    assert derived_nbytes(k) >= skeys.numel() * 4 + perm.numel() * perm.element_size() + first.numel() * first.element_size()
