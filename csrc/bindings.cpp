@@ -445,6 +445,26 @@ PYBIND11_MODULE(_native, m) {
                    P<void>(std::get<4>(t)), P<void>(std::get<5>(t))});
     kern::agg_update(P<const int32_t>(gid), n, ngroups, d.data(), (int)d.size(), S(s), sorted_gids);
   }, py::arg("gid"), py::arg("n"), py::arg("ngroups"), py::arg("descs"), py::arg("s"), py::arg("sorted_gids") = false);
+  m.def("agg_part_buckets", [](int64_t ngroups, int nagg) { return kern::agg_part_buckets(ngroups, nagg); });
+  m.def("agg_part_blocks", []() { return kern::agg_part_blocks(); });
+  // phase 0 / 1 / 2 of the radix-partitioned aggregate; vals: one pointer per desc (0: COUNT(*))
+  m.def("agg_partitioned", [](uintptr_t gid, int64_t n, int64_t ngroups,
+                              const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t>>& descs,
+                              int phase, uintptr_t cnt, uintptr_t off, uintptr_t total, uintptr_t pg,
+                              const std::vector<uintptr_t>& vals, uintptr_t s) {
+    if (!gid || n >= (int64_t(1) << 31) || ngroups <= 0 || ngroups >= (int64_t(1) << 31) || phase < 0 || phase > 2 ||
+        descs.empty() || descs.size() > 8 || vals.size() != descs.size() || (phase == 0 && !cnt) ||
+        (phase >= 1 && (!off || !pg)) || (phase == 2 && !total))
+      throw std::runtime_error("agg_partitioned: bad arguments");
+    std::vector<kern::AggDesc> d;
+    for (auto& t : descs)
+      d.push_back({std::get<0>(t), std::get<1>(t), P<const void>(std::get<2>(t)), P<const uint8_t>(std::get<3>(t)),
+                   P<void>(std::get<4>(t)), P<void>(std::get<5>(t))});
+    std::vector<int64_t*> v;
+    for (auto x : vals) v.push_back(P<int64_t>(x));
+    kern::agg_partitioned(P<const int32_t>(gid), n, ngroups, d.data(), (int)d.size(), phase, P<int32_t>(cnt),
+                          P<const int64_t>(off), P<const int64_t>(total), P<uint16_t>(pg), v.data(), S(s));
+  });
   m.def("sorted_having", [](uintptr_t keys, bool key64, int64_t n,
                             const std::vector<std::tuple<int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t>>& descs,
                             int hagg, int hop, long long hlo, long long hhi, double hf, uintptr_t rep, int64_t cap,

@@ -1209,6 +1209,252 @@ void key_histogram_partitioned(const void* keys, bool key64, const uint8_t* vali
 
 int key_histogram_blocks() { return kHistBlocks; }
 
+// ---- radix-partitioned aggregate ---------------------------------------------
+// High-cardinality GROUP BY over unclustered group ids (TPC-H Q15: 22.7M
+// lineitem rows over 1M suppliers). agg_global_kernel's direct atomics are one
+// memory-side request per row and aggregate (scattered 8-byte atomics run at a
+// fraction of the chip's store rate, and the 128-bit SUM's returning atomic
+// waits for each). Partitioned like the key histogram above: rows are bucketed
+// by the high group-id bits, their aggregate inputs scattered bucket by
+// bucket, then one workgroup per bucket aggregates it in LDS and adds the
+// result to the states with plain stores (a bucket owns its groups).
+//   phase 0: per (bucket, block) row counts         (caller: exclusive scan)
+//   phase 1: scatter of the low group-id bits and one 8-byte input per
+//            aggregate (COUNT(*) needs none)
+//   phase 2: one 1024-lane workgroup per bucket: LDS states, then the merge
+// Integer SUMs accumulate in LDS as two no-return 64-bit halves (low 32 bits
+// unsigned, the rest signed) and recombine exactly into the 128-bit state.
+namespace {
+constexpr int kPartBlocks = 512;
+constexpr int kPartLds = 64 * 1024;
+constexpr int kPartBlock2 = 1024;
+
+struct PartParams {
+  int nagg;
+  AggDesc d[kMaxAggs];
+  int64_t* vals[kMaxAggs];  // scattered inputs per aggregate (null: COUNT(*), 1 per row)
+};
+
+__device__ inline int64_t part_value(const AggDesc& a, int64_t i) {
+  const bool ok = row_valid(a, i);
+  switch (a.op) {
+    case AGG_SUM_INT:
+      return ok ? load_int(a, i) : 0;
+    case AGG_SUM_F64: {
+      const double d = ok ? ((const double*)a.src)[i] : 0.0;
+      int64_t r;
+      __builtin_memcpy(&r, &d, 8);
+      return r;
+    }
+    case AGG_COUNT:
+      return ok ? 1 : 0;
+    case AGG_MIN_INT:
+      return ok ? load_int(a, i) : INT64_MAX;
+    case AGG_MAX_INT:
+      return ok ? load_int(a, i) : INT64_MIN;
+    case AGG_MIN_F64:
+      return ok ? f64_to_ordered(((const double*)a.src)[i]) : INT64_MAX;
+    case AGG_MAX_F64:
+      return ok ? f64_to_ordered(((const double*)a.src)[i]) : INT64_MIN;
+    case AGG_BIT_AND:
+      return ok ? load_int(a, i) : -1;
+    default:  // OR, XOR
+      return ok ? load_int(a, i) : 0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void aggp_count_kernel(const int32_t* __restrict__ gid, int64_t n, int64_t groups,
+                                                           int bits, int nbk, int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t lc[];
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) lc[b] = 0;
+  __syncthreads();
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = blockIdx.x * chunk, r1 = r0 + chunk < n ? r0 + chunk : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+    const uint32_t g = (uint32_t)gid[i];
+    if (g < (uint64_t)groups) atomicAdd(&lc[g >> bits], 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) cnt[(int64_t)b * gridDim.x + blockIdx.x] = lc[b];
+}
+
+__global__ __launch_bounds__(kBlock) void aggp_scatter_kernel(const int32_t* __restrict__ gid, int64_t n,
+                                                             int64_t groups, int bits, int nbk,
+                                                             const int64_t* __restrict__ off,
+                                                             uint16_t* __restrict__ pg, PartParams p) {
+  extern __shared__ int32_t cur[];
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) cur[b] = (int32_t)off[(int64_t)b * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint32_t low = (1u << bits) - 1;
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = blockIdx.x * chunk, r1 = r0 + chunk < n ? r0 + chunk : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+    const uint32_t g = (uint32_t)gid[i];
+    if (g >= (uint64_t)groups) continue;
+    const int32_t pos = atomicAdd(&cur[g >> bits], 1);
+    pg[pos] = (uint16_t)(g & low);
+    for (int k = 0; k < p.nagg; ++k)
+      if (p.vals[k]) p.vals[k][pos] = part_value(p.d[k], i);
+  }
+}
+
+__device__ inline void part_init(int op, unsigned long long* lo, long long* hi) { init_state(op, lo, hi); }
+
+__global__ __launch_bounds__(kPartBlock2) void aggp_bucket_kernel(const uint16_t* __restrict__ pg,
+                                                                 const int64_t* __restrict__ off,
+                                                                 const int64_t* __restrict__ total, int nblk,
+                                                                 int64_t groups, int bits, PartParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long st[];
+  const int B = 1 << bits;
+  unsigned long long* slo = st;
+  long long* shi = (long long*)(st + (size_t)p.nagg * B);
+  for (int idx = threadIdx.x; idx < p.nagg * B; idx += blockDim.x) part_init(p.d[idx >> bits].op, &slo[idx], &shi[idx]);
+  __syncthreads();
+  const int b = blockIdx.x;
+  const int64_t lo = off[(int64_t)b * nblk];
+  const int64_t hi = b + 1 < (int)gridDim.x ? off[(int64_t)(b + 1) * nblk] : *total;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int g = pg[i];
+    for (int k = 0; k < p.nagg; ++k) {
+      const AggDesc& a = p.d[k];
+      const int idx = (k << bits) + g;
+      const int64_t v = p.vals[k] ? p.vals[k][i] : 1;
+      switch (a.op) {
+        case AGG_SUM_INT:
+          if (a.dst2) {
+            atomicAdd(&slo[idx], (unsigned long long)(uint32_t)v);
+            atomicAdd((unsigned long long*)&shi[idx], (unsigned long long)(v >> 32));
+          } else {
+            atomicAdd(&slo[idx], (unsigned long long)v);
+          }
+          break;
+        case AGG_SUM_F64: {
+          double d;
+          __builtin_memcpy(&d, &v, 8);
+          atomicAdd((double*)&slo[idx], d);
+          break;
+        }
+        case AGG_COUNT:
+          atomicAdd(&slo[idx], (unsigned long long)v);
+          break;
+        case AGG_MIN_INT:
+        case AGG_MIN_F64:
+          atomicMin((long long*)&slo[idx], (long long)v);
+          break;
+        case AGG_MAX_INT:
+        case AGG_MAX_F64:
+          atomicMax((long long*)&slo[idx], (long long)v);
+          break;
+        case AGG_BIT_AND:
+          atomicAnd(&slo[idx], (unsigned long long)v);
+          break;
+        case AGG_BIT_OR:
+          atomicOr(&slo[idx], (unsigned long long)v);
+          break;
+        case AGG_BIT_XOR:
+          atomicXor(&slo[idx], (unsigned long long)v);
+          break;
+      }
+    }
+  }
+  __syncthreads();
+  // merge: this bucket's groups belong to this workgroup alone (plain stores)
+  const int64_t g0 = (int64_t)b << bits;
+  for (int idx = threadIdx.x; idx < p.nagg * B; idx += blockDim.x) {
+    const int k = idx >> bits;
+    const int64_t g = g0 + (idx & (B - 1));
+    if (g >= groups) continue;
+    const AggDesc& a = p.d[k];
+    unsigned long long* d = (unsigned long long*)a.dst + g;
+    const unsigned long long x = slo[idx];
+    switch (a.op) {
+      case AGG_SUM_INT:
+        if (a.dst2) {
+          long long* d2 = (long long*)a.dst2 + g;
+          // total = shi * 2^32 + slo (slo < 2^63, |shi| < 2^62): exact in 128 bits
+          const __int128 t = ((__int128)shi[idx] << 32) + (__int128)x;
+          const __int128 c = (((__int128)*d2) << 64) + (__int128)*d;
+          const __int128 r = c + t;
+          *d = (unsigned long long)r;
+          *d2 = (long long)(r >> 64);
+        } else {
+          *d += x;
+        }
+        break;
+      case AGG_SUM_F64: {
+        double u, w;
+        __builtin_memcpy(&u, d, 8);
+        __builtin_memcpy(&w, &x, 8);
+        u += w;
+        __builtin_memcpy(d, &u, 8);
+        break;
+      }
+      case AGG_COUNT:
+        *d += x;
+        break;
+      case AGG_MIN_INT:
+      case AGG_MIN_F64:
+        if ((long long)x < (long long)*d) *d = x;
+        break;
+      case AGG_MAX_INT:
+      case AGG_MAX_F64:
+        if ((long long)x > (long long)*d) *d = x;
+        break;
+      case AGG_BIT_AND:
+        *d &= x;
+        break;
+      case AGG_BIT_OR:
+        *d |= x;
+        break;
+      case AGG_BIT_XOR:
+        *d ^= x;
+        break;
+    }
+  }
+}
+}  // namespace
+
+int agg_part_bits(int nagg) {
+  int b = 12;
+  while (b > 6 && (int64_t)nagg * (int64_t(1) << b) * 16 > kPartLds) --b;
+  return b;
+}
+
+int agg_part_buckets(int64_t ngroups, int nagg) {
+  const int64_t B = int64_t(1) << agg_part_bits(nagg);
+  return (int)((ngroups + B - 1) / B);
+}
+
+int agg_part_blocks() { return kPartBlocks; }
+
+void agg_partitioned(const int32_t* gid, int64_t n, int64_t ngroups, const AggDesc* descs, int nagg, int phase,
+                     int32_t* cnt, const int64_t* off, const int64_t* total, uint16_t* pg, int64_t* const* vals,
+                     hipStream_t stream) {
+  if (n <= 0) return;
+  if (nagg <= 0 || nagg > kMaxAggs) throw std::runtime_error("agg_partitioned: 1..8 aggregates per launch");
+  const int bits = agg_part_bits(nagg);
+  const int nbk = agg_part_buckets(ngroups, nagg);
+  PartParams p;
+  p.nagg = nagg;
+  for (int k = 0; k < nagg; ++k) {
+    p.d[k] = descs[k];
+    p.d[k].groups = ngroups;
+    p.vals[k] = vals ? vals[k] : nullptr;
+  }
+  const size_t lds = (size_t)nbk * sizeof(int32_t);
+  if (phase == 0) {
+    hipLaunchKernelGGL(aggp_count_kernel, dim3(kPartBlocks), dim3(kBlock), lds, stream, gid, n, ngroups, bits, nbk, cnt);
+  } else if (phase == 1) {
+    hipLaunchKernelGGL(aggp_scatter_kernel, dim3(kPartBlocks), dim3(kBlock), lds, stream, gid, n, ngroups, bits, nbk,
+                       off, pg, p);
+  } else {
+    const size_t st = (size_t)nagg * ((size_t)1 << bits) * 16;
+    hipLaunchKernelGGL(aggp_bucket_kernel, dim3(nbk), dim3(kPartBlock2), st, stream, pg, off, total, kPartBlocks,
+                       ngroups, bits, p);
+  }
+  check_launch("agg_partitioned", stream);
+}
+
 void key_histogram(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin, int64_t span,
                    int32_t* counts, hipStream_t stream) {
   if (n <= 0) return;

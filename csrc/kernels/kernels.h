@@ -250,6 +250,16 @@ int key_histogram_blocks();
 void key_histogram_partitioned(const void* keys, bool key64, const uint8_t* valid, int64_t n, int64_t kmin,
                                int64_t span, int phase, int32_t* cnt, const int64_t* off, int64_t total,
                                uint16_t* part, int32_t* counts, hipStream_t stream);
+// radix-partitioned GROUP BY aggregate for many groups (agg.hip): phase 0 per-(bucket, block) row
+// counts -> cnt[buckets * blocks] (caller scans them into off, total on the device); phase 1 scatters the
+// low group-id bits into pg[n] and one int64 input per aggregate into vals[k][n] (vals[k] null: COUNT(*));
+// phase 2 aggregates each bucket in LDS and adds it into the descs' zero / sentinel-initialised states.
+int agg_part_bits(int nagg);
+int agg_part_buckets(int64_t ngroups, int nagg);
+int agg_part_blocks();
+void agg_partitioned(const int32_t* gid, int64_t n, int64_t ngroups, const AggDesc* descs, int nagg, int phase,
+                     int32_t* cnt, const int64_t* off, const int64_t* total, uint16_t* pg, int64_t* const* vals,
+                     hipStream_t stream);
 void agg_update(const int32_t* gid, int64_t n, int ngroups, const AggDesc* descs, int nagg, hipStream_t stream,
                 bool sorted_gids = false);
 

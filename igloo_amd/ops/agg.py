@@ -11,6 +11,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
+from ..utils import switches as _sw
 from ._lib import is_gpu, launch, native, ptr, stream, to_host_ints
 
 OPS = {"sum_int": 0, "sum_f64": 1, "count": 2, "min_int": 3, "max_int": 4, "min_f64": 5, "max_f64": 6,
@@ -113,8 +114,12 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
     if n > 0:
         s = stream(gid if gid is not None else posts[0][1])
         for i in range(0, len(descs), 8):
+            chunk = descs[i:i + 8]
+            if gid is not None and not sorted_gids and _partitioned_ok(n, ngroups, len(chunk)):
+                _agg_partitioned(gid, n, ngroups, chunk, specs[i:i + 8], s)
+                continue
             launch("agg_update")
-            N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, descs[i:i + 8], s, bool(sorted_gids))
+            N.agg_update(ptr(gid), n, ngroups if gid is not None else 1, chunk, s, bool(sorted_gids))
     # one host sync for every 128-bit integer SUM's "fits in int64" check
     # (none for a SUM whose input has a readback-free bound proving it fits)
     known = {si for si, (op, vals, _v) in enumerate(specs) if op == "sum_int" and posts[si][2] is not None
@@ -135,6 +140,46 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
         else:
             outs.append(dst)
     return outs
+
+
+#: radix-partitioned aggregation (csrc/kernels/agg.hip agg_partitioned) for
+#: unclustered group ids past the LDS kernel's group count: from this many rows,
+#: at least AGG_PART_MIN_RATIO rows per group and AGG_PART_MIN_BUCKETS buckets
+#: (one LDS workgroup each: TPC-H Q16's 27,840 groups make 7 buckets, and 12M
+#: rows on 7 workgroups ran 0.5 ms slower than the atomics, which stay in L2 for
+#: so few groups; Q15's 1M suppliers make 244: -0.2 ms). IGLOO_DEBUG=no_agg_part: off
+AGG_PARTITIONED = not _sw.debug("no_agg_part")
+AGG_PART_MIN_ROWS = 1 << 21
+AGG_PART_MIN_RATIO = 2
+AGG_PART_MIN_BUCKETS = 128
+
+
+def _partitioned_ok(n: int, ngroups: int, nagg: int) -> bool:
+    if not (AGG_PARTITIONED and AGG_PART_MIN_ROWS <= n < 2**31 - 1 and ngroups < 2**31 - 1
+            and n >= AGG_PART_MIN_RATIO * ngroups):
+        return False
+    N = native()
+    return ngroups > N.agg_lds_max_groups(nagg) and N.agg_part_buckets(ngroups, nagg) >= AGG_PART_MIN_BUCKETS
+
+
+def _agg_partitioned(gid: torch.Tensor, n: int, ngroups: int, descs, specs, s) -> None:
+    """Rows bucketed by their high group-id bits, each bucket aggregated in
+    LDS by one workgroup: no global atomics (one memory-side request per row
+    and aggregate otherwise). No host synchronisation."""
+    from .select import exclusive_scan
+    N = launch("agg_partitioned")
+    dev = gid.device
+    gid = gid.contiguous()
+    nbk, nblk = N.agg_part_buckets(ngroups, len(descs)), N.agg_part_blocks()
+    cnt = torch.empty(nbk * nblk, dtype=torch.int32, device=dev)
+    N.agg_partitioned(ptr(gid), n, ngroups, descs, 0, ptr(cnt), 0, 0, 0, [0] * len(descs), s)
+    off, total = exclusive_scan(cnt, host_total=False)
+    pg = torch.empty(n, dtype=torch.int16, device=dev)
+    bufs = [None if (op == "count" and valid is None) else torch.empty(n, dtype=torch.int64, device=dev)
+            for op, _vals, valid in specs]
+    vp = [ptr(b) for b in bufs]
+    N.agg_partitioned(ptr(gid), n, ngroups, descs, 1, 0, ptr(off), 0, ptr(pg), vp, s)
+    N.agg_partitioned(ptr(gid), n, ngroups, descs, 2, 0, ptr(off), ptr(total), ptr(pg), vp, s)
 
 
 def _cpu(gid, ngroups, specs, n) -> List[torch.Tensor]:

@@ -28,6 +28,8 @@ list of tokens (``token`` or ``token=value``), read by Python and C++ alike
 ``like_nodword``                LIKE without the aligned-dword prefilter (strings.hip)
 ``no_templates``                plan every new statement text from scratch (no statement
                                 templates, sql/template.py)
+``no_agg_part``                 high-cardinality GROUP BY through global atomics instead
+                                of the radix-partitioned LDS aggregate (ops/agg.py)
 ==============================  =====================================================
 
 Other variables (each read in one place):
