@@ -245,6 +245,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("select_count", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t total, uintptr_t s) {
     kern::select_count(P<const uint8_t>(mask), n, P<int64_t>(tiles), P<int64_t>(total), S(s));
   });
+  // tile counts a fused scan wrote with its mask -> exclusive offsets in place + total
+  m.def("select_scan_counts", [](uintptr_t counts, int64_t tiles, uintptr_t total, uintptr_t s) {
+    if (!counts || !total || tiles <= 0) throw std::runtime_error("select_scan_counts: bad arguments");
+    kern::scan_counts(P<int64_t>(counts), tiles, P<int64_t>(total), S(s));
+  });
   m.def("select_write", [](uintptr_t mask, int64_t n, uintptr_t tiles, uintptr_t out, bool idx64, int64_t cap,
                            uintptr_t s) {
     kern::select_write(P<const uint8_t>(mask), n, P<const int64_t>(tiles), P<void>(out), idx64, cap, S(s));

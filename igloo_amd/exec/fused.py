@@ -353,8 +353,13 @@ def predicate_mask(pred: Expr, b: Batch, ev) -> Optional[torch.Tensor]:
     if not spec.terms:
         return spec.mask  # every conjunct needed the generic evaluator
     out = torch.empty(n, dtype=torch.bool, device=dev)
-    from .fused_jit import jit_mask
-    if jit_mask(spec, n, out, stream(out)):
+    from . import fused_jit as FJ
+    from ..ops.select import attach_tile_counts, fused_counts_ok
+    tc = torch.empty(-(-n // FJ.SELECT_TILE) + 1, dtype=torch.int64, device=dev) \
+        if FJ.TILE_COUNTS and fused_counts_ok(n) else None
+    if FJ.jit_mask(spec, n, out, stream(out), tc):
+        if tc is not None:
+            attach_tile_counts(out, tc)
         return out
     cols, terms, mask = spec.args()
     launch("ff_mask").ff_mask(cols, terms, mask, n, out.data_ptr(), stream(out))

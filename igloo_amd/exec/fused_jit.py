@@ -266,35 +266,71 @@ def _aligned(cols: Sequence[torch.Tensor]) -> bool:
 
 
 # ------------------------------------------------------------------ mask
-def mask_source(sh: _Shape, terms, has_mask: bool) -> str:
+#: rows per select tile (csrc/kernels/select.hip kTile): a tiled mask kernel
+#: writes each tile's set-row count with the mask, so the selection that
+#: follows skips its count pass over the mask (ops/select.py tile_counts)
+SELECT_TILE = 8192
+TILE_COUNTS = not _sw.debug("no_mask_counts")
+
+
+def mask_source(sh: _Shape, terms, has_mask: bool, tiled: bool = False) -> str:
     L = [f"#define ROWS {ROWS}", PRELUDE, f"extern \"C\" __global__ __launch_bounds__({BLOCK}) void igloo_jit_scan_mask("]
-    L.append("    " + ", ".join(_params(sh, has_mask) + ["u8* __restrict__ out", "i64 n"] + _term_params(terms))
-             + ") {")
-    L.append(f"  const i64 step = (i64)gridDim.x * {BLOCK * ROWS};")
-    L.append(f"  for (i64 r = ((i64)blockIdx.x * {BLOCK} + threadIdx.x) * {ROWS}; r < n; r += step) {{")
-    L += ["    " + s for s in _loads(sh, has_mask)]
+    L.append("    " + ", ".join(_params(sh, has_mask) + ["u8* __restrict__ out", "i64 n"]
+                            + (["i64* __restrict__ tc"] if tiled else []) + _term_params(terms)) + ") {")
+    body = ["    " + s for s in _loads(sh, has_mask)]
     for j in range(ROWS):
         p = f"lv{j} && " + _terms_expr(sh, terms, j) + (f" && mk{j}" if has_mask else "")
-        L.append(f"    const bool p{j} = {p};")
-    L.append(f"    if (r + {ROWS} <= n) *(u8xR*)(out + r) = u8xR{{" + ", ".join(f"(u8)p{j}" for j in range(ROWS)) + "};")
-    L.append("    else { " + " ".join(f"if (lv{j}) out[r + {j}] = p{j};" for j in range(ROWS)) + " }")
-    L.append("  }")
+        body.append(f"    const bool p{j} = {p};")
+    body.append(f"    if (r + {ROWS} <= n) *(u8xR*)(out + r) = u8xR{{" + ", ".join(f"(u8)p{j}" for j in range(ROWS)) + "};")
+    body.append("    else { " + " ".join(f"if (lv{j}) out[r + {j}] = p{j};" for j in range(ROWS)) + " }")
+    if not tiled:
+        L.append(f"  const i64 step = (i64)gridDim.x * {BLOCK * ROWS};")
+        L.append(f"  for (i64 r = ((i64)blockIdx.x * {BLOCK} + threadIdx.x) * {ROWS}; r < n; r += step) {{")
+        L += body
+        L.append("  }")
+    else:
+        # one workgroup per select tile at a time: the tile's rows in
+        # {SELECT_TILE // (BLOCK * ROWS)} block-wide steps, its set rows summed
+        # in registers, reduced over the block and stored (no atomics)
+        per = SELECT_TILE // (BLOCK * ROWS)
+        L.append(f"  __shared__ i32 red[{BLOCK // 64}];")
+        L.append(f"  const i64 ntiles = (n + {SELECT_TILE - 1}) / {SELECT_TILE};")
+        L.append("  for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {")
+        L.append("    i32 cnt = 0;")
+        L.append(f"    for (int it = 0; it < {per}; ++it) {{")
+        L.append(f"    const i64 r = t * {SELECT_TILE} + it * {BLOCK * ROWS} + threadIdx.x * {ROWS};")
+        L.append("    if (r >= n) break;")
+        L += body
+        L.append("    cnt += " + " + ".join(f"(i32)p{j}" for j in range(ROWS)) + ";")
+        L.append("    }")
+        L.append("    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);")
+        L.append("    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;")
+        L.append("    __syncthreads();")
+        L.append("    if (threadIdx.x == 0) tc[t] = " + " + ".join(f"(i64)red[{w}]" for w in range(BLOCK // 64)) + ";")
+        L.append("    __syncthreads();")
+        L.append("  }")
     L.append("}")
     return "\n".join(L)
 
 
-def jit_mask(spec, n: int, out: torch.Tensor, stream: int) -> bool:
+def jit_mask(spec, n: int, out: torch.Tensor, stream: int, tc: Optional[torch.Tensor] = None) -> bool:
+    """``tc``: int64 [tiles + 1] to receive the mask's per-select-tile counts
+    (the tiled kernel); None: the plain mask kernel."""
     if not (ENABLED and jit.enabled()) or n == 0 or not _aligned(spec.cols):
         return False
     has_mask = spec.mask is not None
     if has_mask and spec.mask.data_ptr() % 4:
         return False
     sh = _Shape(spec.cols)
-    k = jit.get(mask_source(sh, spec.terms, has_mask), "igloo_jit_scan_mask")
+    k = jit.get(mask_source(sh, spec.terms, has_mask, tc is not None), "igloo_jit_scan_mask")
     if k is None:
         return False
-    grid = max(1, min(-(-n // (BLOCK * ROWS)), 256 * 16))
     args = [t.data_ptr() for t in spec.cols] + ([spec.mask.data_ptr()] if has_mask else []) + [out.data_ptr(), n]
+    if tc is not None:
+        grid = max(1, min(-(-n // SELECT_TILE), 256 * 16))
+        args.append(tc.data_ptr())
+    else:
+        grid = max(1, min(-(-n // (BLOCK * ROWS)), 256 * 16))
     k.launch(grid, BLOCK, 0, stream, args + _term_args(spec.terms))
     return True
 

@@ -8,6 +8,39 @@ import torch
 from ._lib import idx_dtype, is_gpu, launch, ptr, stream, to_host_int, to_host_ints
 
 
+#: masks of more tiles than select.hip's one-workgroup count (kSmallTiles = 8)
+#: take per-tile counts from the kernel that wrote them
+_SMALL_TILES = 8
+
+
+def fused_counts_ok(n: int) -> bool:
+    return -(-n // 8192) > _SMALL_TILES
+
+
+def attach_tile_counts(mask: torch.Tensor, tc: torch.Tensor) -> None:
+    """``tc`` [tiles + 1] holds the per-tile set-row counts of ``mask`` as
+    written with it (exec/fused_jit.py tiled mask kernel): the next count of
+    this mask scans them instead of re-reading the mask. Tied to the mask's
+    version counter, so an in-place change of the mask drops them."""
+    mask._igloo_tc = (tc, mask._version)
+
+
+def _select_count(N, mask: torch.Tensor, n: int, tiles: int, s) -> torch.Tensor:
+    """ws [tiles + 1] int64: exclusive per-tile offsets of the set rows of
+    ``mask`` and their total (select.hip select_count) -- from the tile counts
+    the mask's kernel wrote when it has them (consumed: scanned in place)."""
+    pre = getattr(mask, "_igloo_tc", None)
+    if pre is not None:
+        mask._igloo_tc = None
+        ws, ver = pre
+        if ver == mask._version and ws.numel() == tiles + 1 and tiles > _SMALL_TILES:
+            N.select_scan_counts(ptr(ws), tiles, ptr(ws) + 8 * tiles, s)
+            return ws
+    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
+    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
+    return ws
+
+
 def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Tensor:
     """Ordered indices of the True entries of a bool mask (int32 when they fit).
     ``total``: the caller knows how many are set (no count readback)."""
@@ -21,9 +54,8 @@ def mask_to_indices(mask: torch.Tensor, total: Optional[int] = None) -> torch.Te
     mask = mask.contiguous()
     N = launch("select")
     tiles = N.select_num_tiles(n)
-    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
     s = stream(mask)
-    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
+    ws = _select_count(N, mask, n, tiles, s)
     if total is None:
         total = to_host_int(ws[tiles:])
     out = torch.empty(total, dtype=it, device=mask.device)
@@ -58,8 +90,7 @@ class MaskRows:
         n = mask.numel()
         N = launch("select")
         self._tiles = tiles = N.select_num_tiles(n)
-        self._ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
-        N.select_count(ptr(self.mask), n, ptr(self._ws), ptr(self._ws) + 8 * tiles, stream(mask))
+        self._ws = _select_count(N, self.mask, n, tiles, stream(mask))
         if not defer:
             self._total = to_host_int(self._ws[tiles:])
 
@@ -99,8 +130,7 @@ def count_true(mask: torch.Tensor) -> int:
     mask = mask.contiguous()
     N = launch("select")
     tiles = N.select_num_tiles(n)
-    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
-    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, stream(mask))
+    ws = _select_count(N, mask, n, tiles, stream(mask))
     return to_host_int(ws[tiles:])
 
 
@@ -166,9 +196,8 @@ def compact_columns(mask: torch.Tensor, cols, total: Optional[int] = None, want_
     mask = mask.contiguous()
     N = launch("select_compact")
     tiles = N.select_num_tiles(n)
-    ws = torch.empty(tiles + 1, dtype=torch.int64, device=mask.device)
     s = stream(mask)
-    N.select_count(ptr(mask), n, ptr(ws), ptr(ws) + 8 * tiles, s)
+    ws = _select_count(N, mask, n, tiles, s)
     if total is None:
         total = to_host_int(ws[tiles:])
     it = idx_dtype(n)

@@ -157,3 +157,45 @@ def test_fused_narrow_columns_match_cpu(gpu_device, monkeypatch):
     src = eg.catalog.get_table("t")
     widths = {getattr(c.data, "_igloo_narrow", c.data).dtype for c in src.columns.values()}
     assert torch.int8 in widths and torch.int16 in widths
+
+
+def test_mask_tile_counts_feed_selection(gpu_device, scan_mode, monkeypatch):
+    """The generated mask kernel writes each select tile's set-row count with
+    the mask (exec/fused_jit.py tiled variant); the selection scans those
+    instead of re-reading the mask. Results equal the CPU engine's; counts
+    attached to a mask are consumed by its first selection and dropped when
+    the mask changes in place."""
+    import torch
+    from igloo_amd.ops import select as S
+    if scan_mode != "jit":
+        pytest.skip("tiled counts come from the generated mask kernel")
+    n = 1_000_003                               # 123 tiles, the last one partial
+    r = np.random.default_rng(4)
+    t = pa.table({"a": pa.array(r.integers(0, 1000, n), pa.int32()),
+                  "b": pa.array(r.integers(0, 50, n), pa.int16())})
+    seen = []
+    real = S.attach_tile_counts
+
+    def spy(mask, tc):
+        ref = torch.nn.functional.pad(mask.to(torch.int64), (0, (-mask.numel()) % 8192)).view(-1, 8192).sum(1)
+        seen.append(bool(torch.equal(tc[:-1], ref)))
+        real(mask, tc)
+    monkeypatch.setattr(S, "attach_tile_counts", spy)
+    sql = "SELECT a, b FROM t WHERE a < 300 AND b >= 10"
+    res = {}
+    for dev in ("cpu", gpu_device):
+        e = ig.QueryEngine(device=dev)
+        e.register_table("t", t)
+        res[dev] = sorted(e.query(sql).to_pylist(), key=lambda x: (x["a"], x["b"]))
+    assert res["cpu"] == res[gpu_device]
+    assert seen and all(seen), seen
+    # consumed once; an in-place change drops them
+    m = torch.from_numpy(r.random(n) < 0.3).to(gpu_device)
+    ref = torch.nn.functional.pad(m.to(torch.int64), (0, (-n) % 8192)).view(-1, 8192).sum(1)
+    tc = torch.cat([ref, torch.zeros(1, dtype=torch.int64, device=gpu_device)])
+    real(m, tc)
+    assert torch.equal(S.mask_to_indices(m).long(), torch.nonzero(m).flatten())
+    assert m._igloo_tc is None
+    real(m, tc.clone())
+    m[:5] = True
+    assert torch.equal(S.mask_to_indices(m).long(), torch.nonzero(m).flatten())

@@ -28,6 +28,10 @@ def test_mask_kernel_compiles():
     src = FJ.mask_source(sh, terms, has_mask=True)
     assert "igloo_jit_scan_mask" in src
     _compile(src, "igloo_jit_scan_mask")
+    # the tiled variant: one select tile per workgroup step, its count stored with the mask
+    tiled = FJ.mask_source(sh, terms, has_mask=True, tiled=True)
+    assert "i64* __restrict__ tc" in tiled and f"{FJ.SELECT_TILE}" in tiled
+    _compile(tiled, "igloo_jit_scan_mask")
 
 
 def test_q6_shape_single_group():
