@@ -33,55 +33,54 @@ __device__ __forceinline__ i64 wmax(i64 v) {
 }
 
 extern "C" __global__ __launch_bounds__(256) void igloo_jit_scan_mask(
-    const i32* __restrict__ c0, const i32* __restrict__ c1, u8* __restrict__ out, i64 n, i64 f0lo, i64 f0hi) {
-  const i64 step = (i64)gridDim.x * 1024;
-  for (i64 r = ((i64)blockIdx.x * 256 + threadIdx.x) * 4; r < n; r += step) {
+    const i16* __restrict__ c0, u8* __restrict__ out, i64 n, i64* __restrict__ tc, i64 f0lo, i64 f0hi) {
+  __shared__ i32 red[4];
+  const i64 ntiles = (n + 8191) / 8192;
+  for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    i32 cnt = 0;
+    for (int it = 0; it < 8; ++it) {
+    const i64 r = t * 8192 + it * 1024 + threadIdx.x * 4;
+    if (r >= n) break;
     i32 x0_0;
     i32 x0_1;
     i32 x0_2;
     i32 x0_3;
-    i32 x1_0;
-    i32 x1_1;
-    i32 x1_2;
-    i32 x1_3;
     bool lv0;
     bool lv1;
     bool lv2;
     bool lv3;
     if (r + 4 <= n) {
-      const i32xR q0 = *(const i32xR*)(c0 + r);
-      const i32xR q1 = *(const i32xR*)(c1 + r);
+      const i16xR q0 = *(const i16xR*)(c0 + r);
       x0_0 = q0[0];
-      x1_0 = q1[0];
       lv0 = true;
       x0_1 = q0[1];
-      x1_1 = q1[1];
       lv1 = true;
       x0_2 = q0[2];
-      x1_2 = q1[2];
       lv2 = true;
       x0_3 = q0[3];
-      x1_3 = q1[3];
       lv3 = true;
     } else {
       lv0 = r + 0 < n;
       x0_0 = lv0 ? (i32)c0[r + 0] : 0;
-      x1_0 = lv0 ? (i32)c1[r + 0] : 0;
       lv1 = r + 1 < n;
       x0_1 = lv1 ? (i32)c0[r + 1] : 0;
-      x1_1 = lv1 ? (i32)c1[r + 1] : 0;
       lv2 = r + 2 < n;
       x0_2 = lv2 ? (i32)c0[r + 2] : 0;
-      x1_2 = lv2 ? (i32)c1[r + 2] : 0;
       lv3 = r + 3 < n;
       x0_3 = lv3 ? (i32)c0[r + 3] : 0;
-      x1_3 = lv3 ? (i32)c1[r + 3] : 0;
     }
-    const bool p0 = lv0 && (((i64)x0_0 - (i64)x1_0) >= f0lo && ((i64)x0_0 - (i64)x1_0) <= f0hi);
-    const bool p1 = lv1 && (((i64)x0_1 - (i64)x1_1) >= f0lo && ((i64)x0_1 - (i64)x1_1) <= f0hi);
-    const bool p2 = lv2 && (((i64)x0_2 - (i64)x1_2) >= f0lo && ((i64)x0_2 - (i64)x1_2) <= f0hi);
-    const bool p3 = lv3 && (((i64)x0_3 - (i64)x1_3) >= f0lo && ((i64)x0_3 - (i64)x1_3) <= f0hi);
+    const bool p0 = lv0 && (x0_0 >= f0lo && x0_0 <= f0hi);
+    const bool p1 = lv1 && (x0_1 >= f0lo && x0_1 <= f0hi);
+    const bool p2 = lv2 && (x0_2 >= f0lo && x0_2 <= f0hi);
+    const bool p3 = lv3 && (x0_3 >= f0lo && x0_3 <= f0hi);
     if (r + 4 <= n) *(u8xR*)(out + r) = u8xR{(u8)p0, (u8)p1, (u8)p2, (u8)p3};
     else { if (lv0) out[r + 0] = p0; if (lv1) out[r + 1] = p1; if (lv2) out[r + 2] = p2; if (lv3) out[r + 3] = p3; }
+    cnt += (i32)p0 + (i32)p1 + (i32)p2 + (i32)p3;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) tc[t] = (i64)red[0] + (i64)red[1] + (i64)red[2] + (i64)red[3];
+    __syncthreads();
   }
 }

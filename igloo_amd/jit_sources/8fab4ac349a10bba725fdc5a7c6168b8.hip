@@ -33,9 +33,14 @@ __device__ __forceinline__ i64 wmax(i64 v) {
 }
 
 extern "C" __global__ __launch_bounds__(256) void igloo_jit_scan_mask(
-    const i8* __restrict__ c0, const i8* __restrict__ c1, const i16* __restrict__ c2, u8* __restrict__ out, i64 n, u64 f0bits, i64 f1lo, i64 f1hi, i64 f2lo, i64 f2hi, i64 f3lo, i64 f3hi, i64 f4lo, i64 f4hi) {
-  const i64 step = (i64)gridDim.x * 1024;
-  for (i64 r = ((i64)blockIdx.x * 256 + threadIdx.x) * 4; r < n; r += step) {
+    const i8* __restrict__ c0, const i8* __restrict__ c1, const i16* __restrict__ c2, u8* __restrict__ out, i64 n, i64* __restrict__ tc, u64 f0bits, i64 f1lo, i64 f1hi, i64 f2lo, i64 f2hi, i64 f3lo, i64 f3hi, i64 f4lo, i64 f4hi) {
+  __shared__ i32 red[4];
+  const i64 ntiles = (n + 8191) / 8192;
+  for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    i32 cnt = 0;
+    for (int it = 0; it < 8; ++it) {
+    const i64 r = t * 8192 + it * 1024 + threadIdx.x * 4;
+    if (r >= n) break;
     i32 x0_0;
     i32 x0_1;
     i32 x0_2;
@@ -96,5 +101,12 @@ extern "C" __global__ __launch_bounds__(256) void igloo_jit_scan_mask(
     const bool p3 = lv3 && ((u64)x0_3 < 64ull && ((f0bits >> (u32)x0_3) & 1ull)) && (x1_3 >= f1lo && x1_3 <= f1hi) && (((x2_3 >= f2lo && x2_3 <= f2hi)) || ((x2_3 >= f3lo && x2_3 <= f3hi)) || ((x2_3 >= f4lo && x2_3 <= f4hi)));
     if (r + 4 <= n) *(u8xR*)(out + r) = u8xR{(u8)p0, (u8)p1, (u8)p2, (u8)p3};
     else { if (lv0) out[r + 0] = p0; if (lv1) out[r + 1] = p1; if (lv2) out[r + 2] = p2; if (lv3) out[r + 3] = p3; }
+    cnt += (i32)p0 + (i32)p1 + (i32)p2 + (i32)p3;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) tc[t] = (i64)red[0] + (i64)red[1] + (i64)red[2] + (i64)red[3];
+    __syncthreads();
   }
 }

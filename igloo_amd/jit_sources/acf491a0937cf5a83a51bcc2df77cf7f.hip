@@ -33,9 +33,14 @@ __device__ __forceinline__ i64 wmax(i64 v) {
 }
 
 extern "C" __global__ __launch_bounds__(256) void igloo_jit_scan_mask(
-    const i8* __restrict__ c0, const i16* __restrict__ c1, const i16* __restrict__ c2, const i16* __restrict__ c3, u8* __restrict__ out, i64 n, u64 f0bits, i64 f1lo, i64 f1hi, i64 f2lo, i64 f2hi, i64 f3lo, i64 f3hi) {
-  const i64 step = (i64)gridDim.x * 1024;
-  for (i64 r = ((i64)blockIdx.x * 256 + threadIdx.x) * 4; r < n; r += step) {
+    const i16* __restrict__ c0, const i16* __restrict__ c1, u8* __restrict__ out, i64 n, i64* __restrict__ tc, i64 f0lo, i64 f0hi) {
+  __shared__ i32 red[4];
+  const i64 ntiles = (n + 8191) / 8192;
+  for (i64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    i32 cnt = 0;
+    for (int it = 0; it < 8; ++it) {
+    const i64 r = t * 8192 + it * 1024 + threadIdx.x * 4;
+    if (r >= n) break;
     i32 x0_0;
     i32 x0_1;
     i32 x0_2;
@@ -44,70 +49,51 @@ extern "C" __global__ __launch_bounds__(256) void igloo_jit_scan_mask(
     i32 x1_1;
     i32 x1_2;
     i32 x1_3;
-    i32 x2_0;
-    i32 x2_1;
-    i32 x2_2;
-    i32 x2_3;
-    i32 x3_0;
-    i32 x3_1;
-    i32 x3_2;
-    i32 x3_3;
     bool lv0;
     bool lv1;
     bool lv2;
     bool lv3;
     if (r + 4 <= n) {
-      const i8xR q0 = *(const i8xR*)(c0 + r);
+      const i16xR q0 = *(const i16xR*)(c0 + r);
       const i16xR q1 = *(const i16xR*)(c1 + r);
-      const i16xR q2 = *(const i16xR*)(c2 + r);
-      const i16xR q3 = *(const i16xR*)(c3 + r);
       x0_0 = q0[0];
       x1_0 = q1[0];
-      x2_0 = q2[0];
-      x3_0 = q3[0];
       lv0 = true;
       x0_1 = q0[1];
       x1_1 = q1[1];
-      x2_1 = q2[1];
-      x3_1 = q3[1];
       lv1 = true;
       x0_2 = q0[2];
       x1_2 = q1[2];
-      x2_2 = q2[2];
-      x3_2 = q3[2];
       lv2 = true;
       x0_3 = q0[3];
       x1_3 = q1[3];
-      x2_3 = q2[3];
-      x3_3 = q3[3];
       lv3 = true;
     } else {
       lv0 = r + 0 < n;
       x0_0 = lv0 ? (i32)c0[r + 0] : 0;
       x1_0 = lv0 ? (i32)c1[r + 0] : 0;
-      x2_0 = lv0 ? (i32)c2[r + 0] : 0;
-      x3_0 = lv0 ? (i32)c3[r + 0] : 0;
       lv1 = r + 1 < n;
       x0_1 = lv1 ? (i32)c0[r + 1] : 0;
       x1_1 = lv1 ? (i32)c1[r + 1] : 0;
-      x2_1 = lv1 ? (i32)c2[r + 1] : 0;
-      x3_1 = lv1 ? (i32)c3[r + 1] : 0;
       lv2 = r + 2 < n;
       x0_2 = lv2 ? (i32)c0[r + 2] : 0;
       x1_2 = lv2 ? (i32)c1[r + 2] : 0;
-      x2_2 = lv2 ? (i32)c2[r + 2] : 0;
-      x3_2 = lv2 ? (i32)c3[r + 2] : 0;
       lv3 = r + 3 < n;
       x0_3 = lv3 ? (i32)c0[r + 3] : 0;
       x1_3 = lv3 ? (i32)c1[r + 3] : 0;
-      x2_3 = lv3 ? (i32)c2[r + 3] : 0;
-      x3_3 = lv3 ? (i32)c3[r + 3] : 0;
     }
-    const bool p0 = lv0 && ((u64)x0_0 < 64ull && ((f0bits >> (u32)x0_0) & 1ull)) && (((i64)x1_0 - (i64)x2_0) >= f1lo && ((i64)x1_0 - (i64)x2_0) <= f1hi) && (((i64)x3_0 - (i64)x1_0) >= f2lo && ((i64)x3_0 - (i64)x1_0) <= f2hi) && (x2_0 >= f3lo && x2_0 <= f3hi);
-    const bool p1 = lv1 && ((u64)x0_1 < 64ull && ((f0bits >> (u32)x0_1) & 1ull)) && (((i64)x1_1 - (i64)x2_1) >= f1lo && ((i64)x1_1 - (i64)x2_1) <= f1hi) && (((i64)x3_1 - (i64)x1_1) >= f2lo && ((i64)x3_1 - (i64)x1_1) <= f2hi) && (x2_1 >= f3lo && x2_1 <= f3hi);
-    const bool p2 = lv2 && ((u64)x0_2 < 64ull && ((f0bits >> (u32)x0_2) & 1ull)) && (((i64)x1_2 - (i64)x2_2) >= f1lo && ((i64)x1_2 - (i64)x2_2) <= f1hi) && (((i64)x3_2 - (i64)x1_2) >= f2lo && ((i64)x3_2 - (i64)x1_2) <= f2hi) && (x2_2 >= f3lo && x2_2 <= f3hi);
-    const bool p3 = lv3 && ((u64)x0_3 < 64ull && ((f0bits >> (u32)x0_3) & 1ull)) && (((i64)x1_3 - (i64)x2_3) >= f1lo && ((i64)x1_3 - (i64)x2_3) <= f1hi) && (((i64)x3_3 - (i64)x1_3) >= f2lo && ((i64)x3_3 - (i64)x1_3) <= f2hi) && (x2_3 >= f3lo && x2_3 <= f3hi);
+    const bool p0 = lv0 && (((i64)x0_0 - (i64)x1_0) >= f0lo && ((i64)x0_0 - (i64)x1_0) <= f0hi);
+    const bool p1 = lv1 && (((i64)x0_1 - (i64)x1_1) >= f0lo && ((i64)x0_1 - (i64)x1_1) <= f0hi);
+    const bool p2 = lv2 && (((i64)x0_2 - (i64)x1_2) >= f0lo && ((i64)x0_2 - (i64)x1_2) <= f0hi);
+    const bool p3 = lv3 && (((i64)x0_3 - (i64)x1_3) >= f0lo && ((i64)x0_3 - (i64)x1_3) <= f0hi);
     if (r + 4 <= n) *(u8xR*)(out + r) = u8xR{(u8)p0, (u8)p1, (u8)p2, (u8)p3};
     else { if (lv0) out[r + 0] = p0; if (lv1) out[r + 1] = p1; if (lv2) out[r + 2] = p2; if (lv3) out[r + 3] = p3; }
+    cnt += (i32)p0 + (i32)p1 + (i32)p2 + (i32)p3;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) tc[t] = (i64)red[0] + (i64)red[1] + (i64)red[2] + (i64)red[3];
+    __syncthreads();
   }
 }

@@ -105,13 +105,13 @@ SETS
       # seeds differ from the ones bench.py times) into gpurun_out/jit_sources;
       # committed as igloo_amd/jit_sources, compiled ahead of time by build()
       # (igloo_amd/ops/jit.py aot_compile)
-      IGLOO_JIT_DUMP="$R/gpurun_out/jit_sources" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
+      IGLOO_DEBUG="jit_dump=$R/gpurun_out/jit_sources" IGLOO_JIT_AOT=/nonexistent timeout -k 10 900 python -u bench.py \
         --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 --param-seed 7000 > gpurun_out/jitsources.log 2>&1
       rc=$?; echo "jitsources rc=$rc"; ls gpurun_out/jit_sources | wc -l ;;
     jitdiff)
       # generated kernels the timed ad-hoc streams request (to compare with
       # igloo_amd/jit_sources: parameter-dependent kernel sources)
-      IGLOO_JIT_DUMP="$R/gpurun_out/jit_b" timeout -k 10 900 python -u bench.py \
+      IGLOO_DEBUG="jit_dump=$R/gpurun_out/jit_b" timeout -k 10 900 python -u bench.py \
         --steps 1 --warmup 1 --eager-steps 0 --vary-params 2 > gpurun_out/jitdiff.log 2>&1
       rc=$?; echo "jitdiff rc=$rc"; ls gpurun_out/jit_b | wc -l ;;
     budget)
