@@ -108,14 +108,46 @@ __global__ __launch_bounds__(kBlock) void expand_ranges_kernel(const int64_t* __
   if (nr <= kExpTile) {
     for (int64_t k = threadIdx.x; k < nr; k += blockDim.x) soff[k] = off[r0 + k];
     __syncthreads();
+    // each lane expands kExpItems CONSECUTIVE outputs: one search for the
+    // first, then a forward walk over the (LDS) range starts, and the lane's
+    // outputs leave as whole vectors (a strided layout searched per output)
+    const int64_t ta = t0 + (int64_t)threadIdx.x * kExpItems;
+    if (ta < t1) {
+      int64_t j = row_of(soff, nr, ta);
+      int64_t base = lo[r0 + j] - soff[j];
+      O sv[kExpItems], bv[kExpItems];
 #pragma unroll
-    for (int k = 0; k < kExpItems; ++k) {
-      const int64_t t = t0 + threadIdx.x + (int64_t)k * kBlock;
-      if (t >= t1) break;
-      const int64_t j = row_of(soff, nr, t);
-      const int64_t r = r0 + j;
-      sidx[t] = (O)r;
-      bidx[t] = (O)(lo[r] + (t - soff[j]));
+      for (int k = 0; k < kExpItems; ++k) {
+        const int64_t t = ta + k;
+        while (j + 1 < nr && soff[j + 1] <= t) {
+          ++j;
+          base = lo[r0 + j] - soff[j];
+        }
+        sv[k] = (O)(r0 + j);
+        bv[k] = (O)(base + t);
+      }
+      if (ta + kExpItems <= t1 && (((uintptr_t)(sidx + ta) | (uintptr_t)(bidx + ta)) & 15) == 0) {
+        constexpr int kV = 16 / (int)sizeof(O);   // elements per 16-byte store
+        typedef O OV __attribute__((ext_vector_type(kV)));
+#pragma unroll
+        for (int k = 0; k < kExpItems; k += kV) {
+          OV a, b;
+#pragma unroll
+          for (int q = 0; q < kV; ++q) {
+            a[q] = sv[k + q];
+            b[q] = bv[k + q];
+          }
+          *(OV*)(sidx + ta + k) = a;
+          *(OV*)(bidx + ta + k) = b;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kExpItems; ++k)
+          if (ta + k < t1) {
+            sidx[ta + k] = sv[k];
+            bidx[ta + k] = bv[k];
+          }
+      }
     }
   } else {  // many empty ranges inside the tile: search the global offsets
     for (int k = 0; k < kExpItems; ++k) {

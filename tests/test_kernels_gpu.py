@@ -335,6 +335,16 @@ def test_sorted_ranges_and_expand_vs_torch(gpu_device):
         s_ref, b_ref = H.expand_ranges(lo_ref, cnt_ref, big.numel())
         assert torch.equal(s.cpu().long(), s_ref.long()) and torch.equal(b.cpu().long(), b_ref.long())
         assert torch.equal(big[b.cpu().long()], q[s.cpu().long()])
+    # consecutive-output walk: one range spanning many tiles, empty ranges
+    # between short ones, a partial last tile (ranges.hip expand_ranges)
+    cnt = torch.zeros(30000, dtype=torch.int64)
+    cnt[5] = 70001
+    cnt[100:20000:3] = torch.randint(1, 9, (len(range(100, 20000, 3)),), generator=g)
+    cnt[29999] = 3
+    lo = torch.randint(0, 10**6, (30000,), generator=g)
+    s, b = H.expand_ranges(lo.to(gpu_device), cnt.to(gpu_device), 2 * 10**6)
+    s_ref, b_ref = H.expand_ranges(lo, cnt, 2 * 10**6)
+    assert torch.equal(s.cpu().long(), s_ref.long()) and torch.equal(b.cpu().long(), b_ref.long())
 
 
 def test_sorted_match_pairs_vs_torch(gpu_device):
