@@ -354,6 +354,45 @@ __global__ __launch_bounds__(kBlock) void pack_bits_kernel(PackBitsParams p, int
   }
 }
 
+// 4 rows per lane: one 16-byte load per int32 column (two per int64 column)
+// and two 16-byte stores (all pointers 16-byte aligned; the host checks)
+__global__ __launch_bounds__(kBlock) void pack_bits4_kernel(PackBitsParams p, int64_t n, int64_t* __restrict__ out) {
+  const int64_t n4 = n >> 2;
+  for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < n4; q += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = q << 2;
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int c = 0; c < p.ncols; ++c) {
+      int64_t v0, v1, v2, v3;
+      if (p.is64[c]) {
+        const longlong2* src = (const longlong2*)((const int64_t*)p.col[c] + i);
+        const longlong2 x = src[0], y = src[1];
+        v0 = x.x; v1 = x.y; v2 = y.x; v3 = y.y;
+      } else {
+        const int4 x = *(const int4*)((const int32_t*)p.col[c] + i);
+        v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
+      }
+      const uint64_t lo = (uint64_t)p.lo[c];
+      const int sh = p.shift[c];
+      a0 = (a0 << sh) | ((uint64_t)v0 - lo);
+      a1 = (a1 << sh) | ((uint64_t)v1 - lo);
+      a2 = (a2 << sh) | ((uint64_t)v2 - lo);
+      a3 = (a3 << sh) | ((uint64_t)v3 - lo);
+    }
+    longlong2* o = (longlong2*)(out + i);
+    o[0] = longlong2{(long long)a0, (long long)a1};
+    o[1] = longlong2{(long long)a2, (long long)a3};
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    uint64_t acc = 0;
+    for (int c = 0; c < p.ncols; ++c) {
+      const int64_t v = p.is64[c] ? ((const int64_t*)p.col[c])[i] : (int64_t)((const int32_t*)p.col[c])[i];
+      acc = (acc << p.shift[c]) | (uint64_t)(v - p.lo[c]);
+    }
+    out[i] = (int64_t)acc;
+  }
+}
+
 // Dense key marks (range-sliced SEMI / ANTI joins, parallel/exchange.py):
 // marks[k - kmin] = 1 for every valid key k in [kmin, kmin + dom) -- one
 // pass over the keys, plain byte stores (racing stores all write 1).
@@ -393,7 +432,13 @@ void pack_bits(const void* const* cols, const bool* is64, const int64_t* lo, con
     p.lo[c] = lo[c];
     p.shift[c] = shift[c];
   }
-  hipLaunchKernelGGL(pack_bits_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, p, n, out);
+  static const bool scalar = debug_flag("pack_bits_scalar");
+  bool vec = ((uintptr_t)out & 15) == 0 && !scalar;
+  for (int c = 0; c < ncols; ++c) vec = vec && ((uintptr_t)cols[c] & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(pack_bits4_kernel, dim3(grid_for((n + 3) / 4, kBlock, 65536)), dim3(kBlock), 0, stream, p, n, out);
+  else
+    hipLaunchKernelGGL(pack_bits_kernel, dim3(grid_for(n, kBlock, 65536)), dim3(kBlock), 0, stream, p, n, out);
   check_launch("util.pack_bits", stream);
 }
 

@@ -32,6 +32,8 @@ list of tokens (``token`` or ``token=value``), read by Python and C++ alike
                                 of the radix-partitioned LDS aggregate (ops/agg.py)
 ``no_mask_counts``              generated scan masks without per-tile counts (the
                                 selection counts the mask again, ops/select.py)
+``pack_bits_scalar``            composite-key packing one row per lane instead of four
+                                with 16-byte loads (util.hip pack_bits)
 ==============================  =====================================================
 
 Other variables (each read in one place):
