@@ -88,13 +88,27 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
     g = max(ngroups, 1)
     outs, descs, posts = [], [], []
     narrow = _narrow_sums(specs, n)
+    # every zero-initialised state of the call (sums, their carry words,
+    # counts) in ONE zeroed buffer: one fill kernel instead of one per state
+    # (slots padded to 512 bytes, the alignment of a fresh allocation)
+    nz = sum((2 if op == "sum_int" and si not in narrow else 1) if op in ("sum_int", "sum_f64", "count") else 0
+             for si, (op, _v, _m) in enumerate(specs))
+    slot = -(-g // 64) * 64
+    zbuf = torch.zeros(nz * slot, dtype=torch.int64, device=device) if nz else None
+    zi = 0
+
+    def zeros(dt=torch.int64):
+        nonlocal zi
+        z = zbuf[zi * slot: zi * slot + g]
+        zi += 1
+        return z.view(dt) if dt != torch.int64 else z
     for si, (op, vals, valid) in enumerate(specs):
         code = OPS[op]
         dst2 = None
         if op in ("sum_int", "sum_f64", "count"):
-            dst = torch.zeros(g, dtype=torch.float64 if op == "sum_f64" else torch.int64, device=device)
+            dst = zeros(torch.float64 if op == "sum_f64" else torch.int64)
             if op == "sum_int" and si not in narrow:
-                dst2 = torch.zeros(g, dtype=torch.int64, device=device)
+                dst2 = zeros()
         elif op.startswith("min"):
             dst = torch.full((g,), I64_MAX, dtype=torch.int64, device=device)
         elif op in ("and_int", "or_int", "xor_int"):
