@@ -1323,16 +1323,21 @@ __device__ inline void part_init(int op, unsigned long long* lo, long long* hi) 
 __global__ __launch_bounds__(kPartBlock2) void aggp_bucket_kernel(const uint16_t* __restrict__ pg,
                                                                  const int64_t* __restrict__ off,
                                                                  const int64_t* __restrict__ total, int nblk,
-                                                                 int64_t groups, int bits, PartParams p) {
+                                                                 int64_t groups, int bits, int slices, PartParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long st[];
   const int B = 1 << bits;
   unsigned long long* slo = st;
   long long* shi = (long long*)(st + (size_t)p.nagg * B);
   for (int idx = threadIdx.x; idx < p.nagg * B; idx += blockDim.x) part_init(p.d[idx >> bits].op, &slo[idx], &shi[idx]);
   __syncthreads();
-  const int b = blockIdx.x;
-  const int64_t lo = off[(int64_t)b * nblk];
-  const int64_t hi = b + 1 < (int)gridDim.x ? off[(int64_t)(b + 1) * nblk] : *total;
+  // `slices` workgroups share a bucket when the buckets are few (each takes
+  // a contiguous slice of its rows and merges with atomics)
+  const int b = blockIdx.x / slices, sl = blockIdx.x % slices;
+  const int nbk = (int)gridDim.x / slices;
+  const int64_t blo = off[(int64_t)b * nblk];
+  const int64_t bhi = b + 1 < nbk ? off[(int64_t)(b + 1) * nblk] : *total;
+  const int64_t lo = blo + (bhi - blo) * sl / slices;
+  const int64_t hi = blo + (bhi - blo) * (sl + 1) / slices;
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const int g = pg[i];
     for (int k = 0; k < p.nagg; ++k) {
@@ -1380,6 +1385,23 @@ __global__ __launch_bounds__(kPartBlock2) void aggp_bucket_kernel(const uint16_t
   __syncthreads();
   // merge: this bucket's groups belong to this workgroup alone (plain stores)
   const int64_t g0 = (int64_t)b << bits;
+  if (slices > 1) {
+    for (int idx = threadIdx.x; idx < p.nagg * B; idx += blockDim.x) {
+      const int k = idx >> bits;
+      const int64_t g = g0 + (idx & (B - 1));
+      if (g >= groups) continue;
+      const AggDesc& a = p.d[k];
+      unsigned long long x = slo[idx];
+      long long h = 0;
+      if (a.op == AGG_SUM_INT && a.dst2) {
+        const __int128 t = ((__int128)shi[idx] << 32) + (__int128)x;
+        x = (unsigned long long)t;
+        h = (long long)(t >> 64);
+      }
+      merge_global(a, g, x, h);   // (identity states are skipped)
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < p.nagg * B; idx += blockDim.x) {
     const int k = idx >> bits;
     const int64_t g = g0 + (idx & (B - 1));
@@ -1469,8 +1491,10 @@ void agg_partitioned(const int32_t* gid, int64_t n, int64_t ngroups, const AggDe
                        off, pg, p);
   } else {
     const size_t st = (size_t)nagg * ((size_t)1 << bits) * 16;
-    hipLaunchKernelGGL(aggp_bucket_kernel, dim3(nbk), dim3(kPartBlock2), st, stream, pg, off, total, kPartBlocks,
-                       ngroups, bits, p);
+    // few buckets: enough workgroups to fill the chip (256 CUs), slices merged atomically
+    const int slices = nbk >= 128 ? 1 : std::min(64, (256 + nbk - 1) / nbk);
+    hipLaunchKernelGGL(aggp_bucket_kernel, dim3(nbk * slices), dim3(kPartBlock2), st, stream, pg, off, total,
+                       kPartBlocks, ngroups, bits, slices, p);
   }
   check_launch("agg_partitioned", stream);
 }

@@ -158,14 +158,14 @@ def _gpu(gid, ngroups, specs, n, device, sorted_gids=False) -> List[torch.Tensor
 
 #: radix-partitioned aggregation (csrc/kernels/agg.hip agg_partitioned) for
 #: unclustered group ids past the LDS kernel's group count: from this many rows,
-#: at least AGG_PART_MIN_RATIO rows per group and AGG_PART_MIN_BUCKETS buckets
-#: (one LDS workgroup each: TPC-H Q16's 27,840 groups make 7 buckets, and 12M
-#: rows on 7 workgroups ran 0.5 ms slower than the atomics, which stay in L2 for
-#: so few groups; Q15's 1M suppliers make 244: -0.2 ms). IGLOO_DEBUG=no_agg_part: off
+#: at least AGG_PART_MIN_RATIO rows per group and AGG_PART_MIN_BUCKETS buckets.
+#: Few buckets are shared by several LDS workgroups each (slices merged with
+#: atomics): TPC-H Q16's 27,840 groups make 7 buckets -- one workgroup per
+#: bucket ran 0.5 ms slower than the atomics. IGLOO_DEBUG=no_agg_part: off
 AGG_PARTITIONED = not _sw.debug("no_agg_part")
 AGG_PART_MIN_ROWS = 1 << 21
 AGG_PART_MIN_RATIO = 2
-AGG_PART_MIN_BUCKETS = 128
+AGG_PART_MIN_BUCKETS = 1 if not _sw.debug("agg_part_min128") else 128
 
 
 def _partitioned_ok(n: int, ngroups: int, nagg: int) -> bool:

@@ -30,6 +30,8 @@ list of tokens (``token`` or ``token=value``), read by Python and C++ alike
                                 templates, sql/template.py)
 ``no_agg_part``                 high-cardinality GROUP BY through global atomics instead
                                 of the radix-partitioned LDS aggregate (ops/agg.py)
+``agg_part_min128``             the partitioned aggregate only from 128 buckets (fewer
+                                buckets: global atomics instead of sliced buckets)
 ``no_mask_counts``              generated scan masks without per-tile counts (the
                                 selection counts the mask again, ops/select.py)
 ``pack_bits_scalar``            composite-key packing one row per lane instead of four

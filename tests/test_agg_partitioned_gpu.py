@@ -26,7 +26,7 @@ def _specs(rng, n, dev):
     return cpu, gpu
 
 
-@pytest.mark.parametrize("ngroups", [300_000, 70_001])
+@pytest.mark.parametrize("ngroups", [300_000, 70_001, 9_001])
 def test_partitioned_aggregate_matches_cpu(gpu_device, ngroups):
     rng = np.random.default_rng(ngroups)
     n = 3_000_000
