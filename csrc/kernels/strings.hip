@@ -596,20 +596,48 @@ __global__ __launch_bounds__(kBlock) void cmp_const_kernel(const int64_t* __rest
 // UTF-8 is self-synchronising, so a byte prefix of L code points is the
 // substring). Replaces one compare pass per constant plus the substring copy
 // (TPC-H Q22's country codes: 7 passes over 15M phone numbers).
+constexpr int kInSetWords = 256;   // constants staged in LDS as words
+
 __global__ __launch_bounds__(kBlock) void in_set_kernel(const int64_t* __restrict__ off,
                                                        const uint8_t* __restrict__ chars, int64_t n,
                                                        const uint8_t* __restrict__ vb, const int32_t* __restrict__ voff,
                                                        const uint8_t* __restrict__ vmode, int nv,
                                                        uint8_t* __restrict__ out) {
   // constants of at most 8 bytes (the usual case: codes, flags, short names)
-  // compare as masked words against the row's first bytes, loaded once
+  // compare as masked words against the row's first bytes, loaded once; the
+  // constants' words, lengths and modes are built once per workgroup in LDS
+  // (not re-read byte by byte from global memory for every row)
+  __shared__ uint64_t cword[kInSetWords];
+  __shared__ int32_t clen[kInSetWords];
   int maxb = 0;
   for (int v = 0; v < nv; ++v) maxb = max(maxb, voff[v + 1] - voff[v]);
   const bool words = maxb <= 8;
+  const bool staged = words && nv <= kInSetWords;
+  if (staged) {
+    for (int v = threadIdx.x; v < nv; v += blockDim.x) {
+      const int32_t c0 = voff[v], vl = voff[v + 1] - c0;
+      uint64_t cw = 0;
+      for (int32_t j = 0; j < vl; ++j) cw |= (uint64_t)vb[c0 + j] << (8 * j);
+      cword[v] = cw;
+      clen[v] = vmode[v] ? -vl - 1 : vl;   // negative: prefix match of length -clen-1
+    }
+    __syncthreads();
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = off[i], len = off[i + 1] - a;
     bool hit = false;
-    if (words) {
+    if (staged) {
+      const int nb = len < maxb ? (int)len : maxb;
+      uint64_t w = 0;
+      for (int j = 0; j < nb; ++j) w |= (uint64_t)chars[a + j] << (8 * j);
+      for (int v = 0; v < nv && !hit; ++v) {
+        const int32_t cl = clen[v];
+        const int32_t vl = cl < 0 ? -cl - 1 : cl;
+        if (cl < 0 ? len < vl : len != vl) continue;
+        const uint64_t m = vl >= 8 ? ~0ull : ((1ull << (8 * vl)) - 1);
+        hit = (w & m) == cword[v];
+      }
+    } else if (words) {
       const int nb = len < maxb ? (int)len : maxb;
       uint64_t w = 0;
       for (int j = 0; j < nb; ++j) w |= (uint64_t)chars[a + j] << (8 * j);

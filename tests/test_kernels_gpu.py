@@ -684,3 +684,8 @@ def test_str_in_set(gpu_device, prefix):
     else:
         want = [v[:prefix] in consts for v in vals]
     assert got == want
+    # an empty constant and one past 8 bytes (the byte-compare path)
+    for consts in (["", "13", "ab"], ["13", "aéb", "0123456789"]):
+        got = S.in_set(col, consts, prefix_chars=prefix).cpu().tolist()
+        want = [(v if prefix is None else v[:prefix]) in consts for v in vals]
+        assert got == want, consts
